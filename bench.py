@@ -1,0 +1,150 @@
+#!/usr/bin/env python
+"""Headline benchmark: env frames/sec (whole node) on 16x16 microRTS.
+
+Metric and config from BASELINE.json: "env frames/sec (whole node) on 16x16
+microRTS at 1/2/4/8 MI355X learners". One process per GPU (torchrun), each
+with its own native env workers + on-GPU batched inference (GpuActorRuntime)
+and a data-parallel learner (RCCL all-reduce). A timed step = one learner
+update (forward, V-trace, backward, bucketed all-reduce, Adam, weight
+publish) consuming ``batch_slots * envs_per_group * unroll`` fresh env frames
+per rank that the actors produced concurrently; value = frames consumed by all
+learners / wall time (weak scaling: per-GPU work fixed).
+
+Synthetic environment (native microRTS stand-in; gym-microrts/Java is not
+available offline) and random-init weights of the reference architecture
+(IMPALA-CNN 16/32/32 + 256 FC + flat 78*16*16 head, 5.27 M params).
+
+    python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_FPS = 38.9  # best reference run (5_ener), frames/s whole node
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--size", type=int, default=16)
+    p.add_argument("--groups", type=int, default=4)
+    p.add_argument("--envs_per_group", type=int, default=256)
+    p.add_argument("--unroll", type=int, default=64)
+    p.add_argument("--batch_slots", type=int, default=2)
+    p.add_argument("--threads", type=int, default=0, help="env worker threads per rank (0=auto)")
+    p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--profile_phases", action="store_true",
+                   help="also report per-phase learner timings (adds syncs; not for the headline)")
+    return p.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    import torch
+
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent, num_params
+    from microbeast_amd.parallel import dist as D
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime, available_cpus
+
+    if not torch.cuda.is_available():
+        print("bench.py needs a GPU", file=sys.stderr)
+        return 2
+    info = D.init_distributed(use_cuda=True)
+    dev = torch.device("cuda", info.local_rank)
+    torch.set_num_threads(2)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(info.world_size)))
+    threads = args.threads or max(2, min(24, available_cpus() // max(1, local_world) - 3))
+    s = args.size
+
+    def make_model():
+        return Agent((s, s, 27))
+
+    torch.manual_seed(args.seed)
+    model = make_model()
+    learner = Learner(model, LearnerHParams(), dev, info)
+    envs_total = args.groups * args.envs_per_group
+    rt = GpuActorRuntime(make_model, s, args.groups, args.envs_per_group, args.unroll,
+                         args.batch_slots, dev, n_threads=threads, seed=args.seed + 1000 * info.rank,
+                         env_index_base=info.rank * envs_total)
+    rt.start(learner.flat)
+    frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
+
+    def step():
+        batch, slots = rt.get_batch()
+        losses = learner.learn(batch)
+        rt.release(slots)
+        rt.publish(learner.flat)
+        return losses
+
+    for _ in range(args.warmup):
+        losses = step()
+    torch.cuda.synchronize()
+    D.barrier(info)
+    st0 = rt.stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        losses = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    D.barrier(info)
+    st1 = rt.stats()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if info.enabled:
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    el = float(elapsed.item())
+    total_frames = frames_per_step * args.steps * info.world_size
+    fps = total_frames / el
+    loss_vals = [float(x) for x in losses.tolist()]
+    phase = None
+    if args.profile_phases:
+        learner.learn(rt.get_batch()[0], sync_timing=True)
+        phase = learner.timing
+    rt.stop()
+    if info.is_main:
+        out = {
+            "metric": "env frames/sec (whole node) on 16x16 microRTS",
+            "value": round(fps, 1),
+            "unit": "frames/s",
+            "n_gpus": info.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * el / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(fps / BASELINE_FPS, 1),
+            "dtype": "bf16",
+            "data": "synthetic (native microRTS stand-in env, random-init weights)",
+            "config": {
+                "model": f"impala_flat IMPALA-CNN 16/32/32 + FC256 + flat 78x{s}x{s} head "
+                         f"({num_params(model) / 1e6:.2f}M params)",
+                "map": f"{s}x{s}",
+                "global_batch": frames_per_step * info.world_size,
+                "seq_len": args.unroll,
+                "parallelism": f"dp{info.world_size}",
+                "envs_per_gpu": envs_total,
+                "env_threads_per_gpu": threads,
+            },
+            "actor_stats": {
+                "env_frames_stepped_per_s_rank0": round((st1["frames"] - st0["frames"]) / el, 1),
+                "slot_wait_s": round(st1["slot_wait_s"] - st0["slot_wait_s"], 3),
+                "driver_idle_s": round(st1["driver_idle_s"] - st0["driver_idle_s"], 3),
+            },
+            "last_losses": {"pg": loss_vals[0], "value": loss_vals[1], "entropy": loss_vals[2],
+                            "total": loss_vals[3]},
+        }
+        if phase:
+            out["learner_phase_s"] = phase
+        print(json.dumps(out), flush=True)
+    D.destroy(info)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

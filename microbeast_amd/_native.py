@@ -1,0 +1,125 @@
+"""Loader for the in-tree native libraries (built by ``csrc/build.py``).
+
+* ``kernels()`` — ctypes handle to ``_lib/libmbk_kernels.so`` (HIP, gfx950).
+* ``runtime()`` — the pybind11 ``_mbrt`` module (env, rings, GPU engine).
+
+torch is imported first on purpose: the ROCm torch wheel ships its own
+``libamdhip64.so.7``; loading ours afterwards makes the dynamic loader reuse
+that already-loaded HIP runtime (same SONAME) instead of mapping a second one.
+
+GPU ops fail loudly when the kernel library is missing on a GPU box — there
+is no silent PyTorch fallback for device tensors.
+"""
+from __future__ import annotations
+
+import ctypes
+import importlib.util
+import os
+import sys
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the HIP libraries, see module doc)
+
+_LIB = Path(__file__).resolve().parent / "_lib"
+_lock = threading.Lock()
+_kern = None
+_rt = None
+
+c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+
+_SIGS = {
+    "mbk_multi_copy": [c_void_p, c_int, c_void_p],
+    "mbk_masked_cell_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64,
+                            c_void_p, c_void_p, c_void_p],
+    "mbk_masked_cell_bwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                            c_int64, c_void_p, c_int, c_void_p],
+    "mbk_row_sum": [c_void_p, c_int64, c_int, c_void_p, c_void_p],
+    "mbk_rng_advance": [c_void_p, c_void_p],
+    "mbk_vtrace": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                   c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
+                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mbk_grad_clip_scale": [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p],
+    "mbk_adam": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
+                 c_float, c_float, c_float, c_int64, c_void_p, c_void_p],
+    "mbk_to_bf16": [c_void_p, c_int64, c_void_p, c_void_p],
+}
+
+
+def _ensure_built() -> None:
+    kl = _LIB / "libmbk_kernels.so"
+    rts = list(_LIB.glob("_mbrt*.so"))
+    if kl.exists() and rts and os.environ.get("MBK_REBUILD", "0") != "1":
+        return
+    from .csrc import build as _b
+
+    _b.build()
+
+
+def kernels():
+    """ctypes handle to libmbk_kernels.so (builds it if missing)."""
+    global _kern
+    if _kern is not None:
+        return _kern
+    with _lock:
+        if _kern is None:
+            _ensure_built()
+            lib = ctypes.CDLL(str(_LIB / "libmbk_kernels.so"), mode=ctypes.RTLD_GLOBAL)
+            for name, args in _SIGS.items():
+                fn = getattr(lib, name, None)
+                if fn is None:
+                    continue
+                fn.argtypes = args
+                fn.restype = c_int
+            _kern = lib
+    return _kern
+
+
+def runtime():
+    """The _mbrt pybind11 module (builds it if missing)."""
+    global _rt
+    if _rt is not None:
+        return _rt
+    with _lock:
+        if _rt is None:
+            _ensure_built()
+            kernels_path = _LIB / "libmbk_kernels.so"
+            ctypes.CDLL(str(kernels_path), mode=ctypes.RTLD_GLOBAL)
+            cands = sorted(_LIB.glob("_mbrt*.so"))
+            if not cands:
+                raise ImportError("microbeast_amd native runtime (_mbrt) not built")
+            spec = importlib.util.spec_from_file_location("microbeast_amd._lib._mbrt", cands[0])
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            sys.modules["microbeast_amd._lib._mbrt"] = mod
+            _rt = mod
+    return _rt
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed with hipError {rc}")
+
+
+def stream_ptr(stream: torch.cuda.Stream | None = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def loaded_libraries() -> list[str]:
+    """In-tree native libraries mapped into this process (for smoke checks)."""
+    out = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if str(_LIB) in line:
+                    p = line.split()[-1]
+                    if p not in out:
+                        out.append(p)
+    except OSError:
+        pass
+    return out

@@ -1,0 +1,600 @@
+// Synthetic gym-microRTS simulator. See microrts_sim.h for the contract.
+#include "microrts_sim.h"
+#include <algorithm>
+#include <cstring>
+#include <cstdlib>
+
+namespace mb {
+
+//                       hp cost dmg rng move atk produce
+const UnitSpec kSpec[8] = {
+    {0, 0, 0, 0, 0, 0, 0},      // none
+    {1, 0, 0, 0, 0, 0, 0},      // resource
+    {16, 10, 0, 0, 0, 0, 60},   // base
+    {6, 5, 0, 0, 0, 0, 40},     // barracks
+    {1, 1, 1, 1, 4, 3, 14},     // worker
+    {4, 2, 2, 1, 3, 3, 22},     // light
+    {4, 3, 4, 1, 5, 3, 30},     // heavy
+    {1, 2, 1, 3, 4, 3, 26},     // ranged
+};
+static constexpr int kHarvestT = 5, kReturnT = 3;
+static constexpr int kDX[4] = {0, 1, 0, -1};
+static constexpr int kDY[4] = {-1, 0, 1, 0};
+
+// reward component indices (libs/utils.py:74 order)
+enum { R_WIN = 0, R_RES = 1, R_WORKER = 2, R_BUILD = 3, R_ATTACK = 4, R_COMBAT = 5 };
+
+static inline void setbit(uint32_t* w, int j) { w[j >> 5] |= 1u << (j & 31); }
+static inline bool getbit(const uint32_t* w, int j) { return (w[j >> 5] >> (j & 31)) & 1u; }
+
+MicroRTSSim::MicroRTSSim(int size, int max_steps, int bot, uint64_t seed, const float* rw)
+    : s_(size), max_steps_(max_steps), bot_(bot) {
+  static const float def[kNumRewards] = {10.f, 1.f, 1.f, 0.2f, 1.f, 4.f};
+  for (int i = 0; i < kNumRewards; ++i) rw_[i] = rw ? rw[i] : def[i];
+  // splitmix64 seeding so neighbouring seeds give unrelated streams
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  rng_ = (z ^ (z >> 31)) | 1ull;
+  grid_.assign(s_ * s_, -1);
+  mask_.assign(s_ * s_ * kMaskWords, 0u);
+  mask_p1_.assign(s_ * s_ * kMaskWords, 0u);
+  opp_actions_.assign(s_ * s_ * kActComps, 0);
+  reset();
+}
+
+uint32_t MicroRTSSim::rand_u32() {
+  rng_ ^= rng_ << 13; rng_ ^= rng_ >> 7; rng_ ^= rng_ << 17;
+  return (uint32_t)(rng_ >> 16);
+}
+float MicroRTSSim::rand_unit() { return (rand_u32() & 0xFFFFFF) * (1.f / 16777216.f); }
+
+int MicroRTSSim::add_unit(int type, int owner, int x, int y, int res) {
+  Unit u{};
+  u.x = x; u.y = y; u.type = type; u.owner = owner;
+  u.hp = kSpec[type].hp; u.res = res; u.busy = 0; u.act = A_NOOP; u.alive = 1;
+  // reuse a dead slot when possible
+  int uid = -1;
+  for (size_t i = 0; i < units_.size(); ++i)
+    if (!units_[i].alive) { uid = (int)i; break; }
+  if (uid < 0) { uid = (int)units_.size(); units_.push_back(u); }
+  else units_[uid] = u;
+  grid_[cell(x, y)] = (int16_t)uid;
+  return uid;
+}
+
+void MicroRTSSim::kill(int uid) {
+  Unit& u = units_[uid];
+  if (!u.alive) return;
+  grid_[cell(u.x, u.y)] = -1;
+  u.alive = 0;
+}
+
+// "maps/{s}x{s}/basesWorkers{s}x{s}.xml" stand-in (libs/utils.py:73): each
+// player owns a base and a worker next to a resource field in opposite corners.
+void MicroRTSSim::reset() {
+  units_.clear();
+  units_.reserve((size_t)s_ * s_ + 4);  // units never outnumber cells: no reallocation
+  std::fill(grid_.begin(), grid_.end(), (int16_t)-1);
+  tick_ = 0;
+  resources_[0] = resources_[1] = 5;
+  const int o = s_ >= 8 ? 1 : 0;
+  const int b = s_ >= 8 ? 2 : 1;
+  // player 0 top-left, player 1 bottom-right (180 degree rotation)
+  for (int p = 0; p < 2; ++p) {
+    auto X = [&](int x) { return p == 0 ? x : s_ - 1 - x; };
+    auto Y = [&](int y) { return p == 0 ? y : s_ - 1 - y; };
+    add_unit(RESOURCE, -1, X(0), Y(0), s_ >= 8 ? 20 : 10);
+    if (s_ >= 8) add_unit(RESOURCE, -1, X(0), Y(1), 20);
+    add_unit(BASE, p, X(b), Y(b));
+    add_unit(WORKER, p, X(o), Y(b == 1 ? 0 : o), 0);
+    if (s_ >= 12) add_unit(WORKER, p, X(b + 1), Y(b), 0);
+  }
+  compute_mask(0, mask_);
+  if (external_opp_) compute_mask(1, mask_p1_);
+}
+
+// ---------------------------------------------------------------- masks
+void MicroRTSSim::unit_mask(const Unit& u, int player, uint32_t* w) const {
+  // w: 3 words, real-frame bits; caller mirrors for player 1 perspective.
+  w[0] = w[1] = w[2] = 0;
+  if (!u.alive || u.owner != player || u.busy > 0 || u.type == RESOURCE) return;
+  const UnitSpec& sp = kSpec[u.type];
+  setbit(w, kNvecOff[0] + A_NOOP);
+  bool any_move = false, any_harv = false, any_ret = false, any_prod = false, any_att = false;
+  const bool mobile = u.type >= WORKER;
+  for (int d = 0; d < 4; ++d) {
+    int nx = u.x + kDX[d], ny = u.y + kDY[d];
+    if (!in_bounds(nx, ny)) continue;
+    int g = grid_[cell(nx, ny)];
+    if (g < 0) {
+      if (mobile) { setbit(w, kNvecOff[1] + d); any_move = true; }
+      // produce direction: any empty neighbour when something is affordable
+      bool can_prod = false;
+      if (u.type == BASE && resources_[player] >= kSpec[WORKER].cost) can_prod = true;
+      if (u.type == BARRACKS && resources_[player] >= kSpec[LIGHT].cost) can_prod = true;
+      if (u.type == WORKER && resources_[player] >= kSpec[BARRACKS].cost) can_prod = true;
+      if (can_prod) { setbit(w, kNvecOff[4] + d); any_prod = true; }
+    } else {
+      const Unit& t = units_[g];
+      if (u.type == WORKER && t.type == RESOURCE && u.res == 0 && t.res > 0) {
+        setbit(w, kNvecOff[2] + d); any_harv = true;
+      }
+      if (u.type == WORKER && t.type == BASE && t.owner == player && u.res > 0) {
+        setbit(w, kNvecOff[3] + d); any_ret = true;
+      }
+    }
+  }
+  if (any_prod) {
+    const int r = resources_[player];
+    if (u.type == BASE) setbit(w, kNvecOff[5] + (WORKER - 1));
+    if (u.type == BARRACKS) {
+      if (r >= kSpec[LIGHT].cost) setbit(w, kNvecOff[5] + (LIGHT - 1));
+      if (r >= kSpec[HEAVY].cost) setbit(w, kNvecOff[5] + (HEAVY - 1));
+      if (r >= kSpec[RANGED].cost) setbit(w, kNvecOff[5] + (RANGED - 1));
+    }
+    if (u.type == WORKER) {
+      if (r >= kSpec[BASE].cost) setbit(w, kNvecOff[5] + (BASE - 1));
+      if (r >= kSpec[BARRACKS].cost) setbit(w, kNvecOff[5] + (BARRACKS - 1));
+    }
+  }
+  if (sp.damage > 0) {
+    const int R = sp.range;
+    for (int ay = -3; ay <= 3; ++ay)
+      for (int ax = -3; ax <= 3; ++ax) {
+        if (ax * ax + ay * ay > R * R || (ax == 0 && ay == 0)) continue;
+        int tx = u.x + ax, ty = u.y + ay;
+        if (!in_bounds(tx, ty)) continue;
+        int g = grid_[cell(tx, ty)];
+        if (g >= 0 && units_[g].owner == 1 - player) {
+          setbit(w, kNvecOff[6] + (ay + 3) * 7 + (ax + 3)); any_att = true;
+        }
+      }
+  }
+  if (any_move) setbit(w, kNvecOff[0] + A_MOVE);
+  if (any_harv) setbit(w, kNvecOff[0] + A_HARVEST);
+  if (any_ret) setbit(w, kNvecOff[0] + A_RETURN);
+  if (any_prod) setbit(w, kNvecOff[0] + A_PRODUCE);
+  if (any_att) setbit(w, kNvecOff[0] + A_ATTACK);
+}
+
+static void mirror_mask_bits(const uint32_t* in, uint32_t* out) {
+  out[0] = out[1] = out[2] = 0;
+  for (int j = 0; j < kMaskBits; ++j) {
+    if (!getbit(in, j)) continue;
+    int k = j;
+    if (j >= kNvecOff[1] && j < kNvecOff[5]) {  // the four direction groups
+      int g = (j - kNvecOff[1]) / 4, d = (j - kNvecOff[1]) % 4;
+      k = kNvecOff[1] + g * 4 + (d + 2) % 4;
+    } else if (j >= kNvecOff[6]) {
+      int a = j - kNvecOff[6];
+      k = kNvecOff[6] + (6 - a / 7) * 7 + (6 - a % 7);
+    }
+    setbit(out, k);
+  }
+}
+
+void MicroRTSSim::map_xy(int player, int x, int y, int* ox, int* oy) const {
+  if (player == 0) { *ox = x; *oy = y; }
+  else { *ox = s_ - 1 - x; *oy = s_ - 1 - y; }
+}
+
+void MicroRTSSim::compute_mask(int player, std::vector<uint32_t>& out) const {
+  std::fill(out.begin(), out.end(), 0u);
+  for (const Unit& u : units_) {
+    if (!u.alive || u.owner != player || u.busy > 0) continue;
+    uint32_t w[3];
+    unit_mask(u, player, w);
+    int px, py;
+    map_xy(player, u.x, u.y, &px, &py);
+    uint32_t* dst = &out[(size_t)cell(px, py) * kMaskWords];
+    if (player == 0) { dst[0] = w[0]; dst[1] = w[1]; dst[2] = w[2]; }
+    else mirror_mask_bits(w, dst);
+  }
+}
+
+// ---------------------------------------------------------------- actions
+bool MicroRTSSim::exec(int uid, const uint8_t* a, float* rw) {
+  Unit& u = units_[uid];
+  if (!u.alive || u.busy > 0) return false;
+  const int player = u.owner;
+  const UnitSpec& sp = kSpec[u.type];
+  switch (a[0]) {
+    case A_NOOP: return true;
+    case A_MOVE: {
+      if (u.type < WORKER) return false;
+      int d = a[1] & 3, nx = u.x + kDX[d], ny = u.y + kDY[d];
+      if (!empty(nx, ny)) return false;
+      grid_[cell(u.x, u.y)] = -1;
+      u.x = nx; u.y = ny;
+      grid_[cell(nx, ny)] = (int16_t)uid;
+      u.busy = sp.move_t; u.act = A_MOVE;
+      return true;
+    }
+    case A_HARVEST: {
+      int d = a[2] & 3, nx = u.x + kDX[d], ny = u.y + kDY[d];
+      if (u.type != WORKER || u.res > 0 || !in_bounds(nx, ny)) return false;
+      int g = grid_[cell(nx, ny)];
+      if (g < 0 || units_[g].type != RESOURCE || units_[g].res <= 0) return false;
+      units_[g].res -= 1; u.res = 1;
+      if (units_[g].res <= 0) kill(g);
+      u.busy = kHarvestT; u.act = A_HARVEST;
+      if (rw) rw[R_RES] += 1.f;
+      return true;
+    }
+    case A_RETURN: {
+      int d = a[3] & 3, nx = u.x + kDX[d], ny = u.y + kDY[d];
+      if (u.type != WORKER || u.res <= 0 || !in_bounds(nx, ny)) return false;
+      int g = grid_[cell(nx, ny)];
+      if (g < 0 || units_[g].type != BASE || units_[g].owner != player) return false;
+      resources_[player] += u.res; u.res = 0;
+      u.busy = kReturnT; u.act = A_RETURN;
+      if (rw) rw[R_RES] += 1.f;
+      return true;
+    }
+    case A_PRODUCE: {
+      int d = a[4] & 3, nx = u.x + kDX[d], ny = u.y + kDY[d];
+      int t = (int)a[5] + 1;
+      if (t < 1 || t > 7 || !empty(nx, ny)) return false;
+      bool ok = (u.type == BASE && t == WORKER) ||
+                (u.type == BARRACKS && (t == LIGHT || t == HEAVY || t == RANGED)) ||
+                (u.type == WORKER && (t == BASE || t == BARRACKS));
+      if (!ok || resources_[player] < kSpec[t].cost) return false;
+      resources_[player] -= kSpec[t].cost;
+      int nu = add_unit(t, player, nx, ny);
+      Unit& uu = units_[uid];  // add_unit may reallocate
+      units_[nu].busy = kSpec[t].produce_t;  // "under construction"
+      units_[nu].act = A_NOOP;
+      uu.busy = kSpec[t].produce_t; uu.act = A_PRODUCE;
+      if (rw) {
+        if (t == WORKER) rw[R_WORKER] += 1.f;
+        else if (t == BASE || t == BARRACKS) rw[R_BUILD] += 1.f;
+        else rw[R_COMBAT] += 1.f;
+      }
+      return true;
+    }
+    case A_ATTACK: {
+      if (sp.damage <= 0) return false;
+      int ax = (int)(a[6] % 7) - 3, ay = (int)(a[6] / 7) - 3;
+      if (ax * ax + ay * ay > sp.range * sp.range) return false;
+      int tx = u.x + ax, ty = u.y + ay;
+      if (!in_bounds(tx, ty)) return false;
+      int g = grid_[cell(tx, ty)];
+      if (g < 0 || units_[g].owner != 1 - player) return false;
+      units_[g].hp -= sp.damage;
+      if (units_[g].hp <= 0) kill(g);
+      u.busy = sp.attack_t; u.act = A_ATTACK;
+      if (rw) rw[R_ATTACK] += 1.f;
+      return true;
+    }
+  }
+  return false;
+}
+
+int MicroRTSSim::nearest(int uid, int owner_filter, int type_filter, int* dist) const {
+  const Unit& u = units_[uid];
+  int best = -1, bd = 1 << 30;
+  for (size_t i = 0; i < units_.size(); ++i) {
+    const Unit& t = units_[i];
+    if (!t.alive || (int)i == uid) continue;
+    if (owner_filter != -2 && t.owner != owner_filter) continue;
+    if (type_filter > 0 && t.type != type_filter) continue;
+    int d = std::abs(t.x - u.x) + std::abs(t.y - u.y);
+    if (d < bd) { bd = d; best = (int)i; }
+  }
+  if (dist) *dist = bd;
+  return best;
+}
+
+int MicroRTSSim::dir_toward(const Unit& u, int tx, int ty) const {
+  int best = -1, bd = 1 << 30;
+  for (int d = 0; d < 4; ++d) {
+    int nx = u.x + kDX[d], ny = u.y + kDY[d];
+    if (!empty(nx, ny)) continue;
+    int dd = std::abs(tx - nx) + std::abs(ty - ny);
+    if (dd < bd) { bd = dd; best = d; }
+  }
+  return best;
+}
+
+// Scripted opponents (stand-ins for coacAI, randomBiasedAI, lightRushAI,
+// workerRushAI — libs/utils.py:69-72). They act through exec() with the same
+// validity rules as the learning agent.
+void MicroRTSSim::bot_unit(int uid, int player, float* rwo) {
+  Unit& u = units_[uid];
+  uint8_t a[7] = {0, 0, 0, 0, 0, 0, 0};
+  const int enemy = 1 - player;
+  auto try_attack = [&]() -> bool {
+    const UnitSpec& sp = kSpec[u.type];
+    if (sp.damage <= 0) return false;
+    for (int ay = -3; ay <= 3; ++ay)
+      for (int ax = -3; ax <= 3; ++ax) {
+        if (ax * ax + ay * ay > sp.range * sp.range || (ax == 0 && ay == 0)) continue;
+        int tx = u.x + ax, ty = u.y + ay;
+        if (!in_bounds(tx, ty)) continue;
+        int g = grid_[cell(tx, ty)];
+        if (g >= 0 && units_[g].owner == enemy) {
+          a[0] = A_ATTACK; a[6] = (uint8_t)((ay + 3) * 7 + (ax + 3));
+          return exec(uid, a, rwo);
+        }
+      }
+    return false;
+  };
+  auto move_to = [&](int tx, int ty) -> bool {
+    int d = dir_toward(u, tx, ty);
+    if (d < 0) return false;
+    a[0] = A_MOVE; a[1] = (uint8_t)d;
+    return exec(uid, a, rwo);
+  };
+  auto produce = [&](int type) -> bool {
+    for (int k = 0; k < 4; ++k) {
+      int d = (int)((rand_u32() + k) & 3);
+      if (!empty(u.x + kDX[d], u.y + kDY[d])) continue;
+      a[0] = A_PRODUCE; a[4] = (uint8_t)d; a[5] = (uint8_t)(type - 1);
+      return exec(uid, a, rwo);
+    }
+    return false;
+  };
+  auto harvest_cycle = [&]() -> bool {
+    if (u.res > 0) {
+      int dist, b = nearest(uid, player, BASE, &dist);
+      if (b < 0) return false;
+      if (dist == 1) {
+        for (int d = 0; d < 4; ++d)
+          if (u.x + kDX[d] == units_[b].x && u.y + kDY[d] == units_[b].y) {
+            a[0] = A_RETURN; a[3] = (uint8_t)d; return exec(uid, a, rwo);
+          }
+      }
+      return move_to(units_[b].x, units_[b].y);
+    }
+    int dist, r = nearest(uid, -1, RESOURCE, &dist);
+    if (r < 0) return false;
+    if (dist == 1) {
+      for (int d = 0; d < 4; ++d)
+        if (u.x + kDX[d] == units_[r].x && u.y + kDY[d] == units_[r].y) {
+          a[0] = A_HARVEST; a[2] = (uint8_t)d; return exec(uid, a, rwo);
+        }
+    }
+    return move_to(units_[r].x, units_[r].y);
+  };
+  auto chase = [&]() -> bool {
+    int dist, e = nearest(uid, enemy, -1, &dist);
+    if (e < 0) return false;
+    return move_to(units_[e].x, units_[e].y);
+  };
+
+  // count own workers / barracks for the build orders
+  int n_workers = 0, n_barracks = 0;
+  for (const Unit& t : units_)
+    if (t.alive && t.owner == player) {
+      n_workers += t.type == WORKER;
+      n_barracks += t.type == BARRACKS;
+    }
+  // index of this worker among own workers (first one harvests)
+  int widx = 0;
+  if (u.type == WORKER)
+    for (int i = 0; i < uid; ++i)
+      if (units_[i].alive && units_[i].owner == player && units_[i].type == WORKER) ++widx;
+
+  switch (bot_) {
+    case BOT_PASSIVE: return;
+    case BOT_RANDOM:
+    case BOT_RANDOM_BIASED: {
+      uint32_t w[3];
+      unit_mask(u, player, w);
+      // biased: prefer attack > harvest/return > produce > move (randomBiasedAI)
+      int order[6] = {A_ATTACK, A_RETURN, A_HARVEST, A_PRODUCE, A_MOVE, A_NOOP};
+      int at = A_NOOP;
+      if (bot_ == BOT_RANDOM_BIASED && rand_unit() < 0.8f) {
+        for (int k = 0; k < 6; ++k) if (getbit(w, order[k])) { at = order[k]; break; }
+      } else {
+        int c[6], n = 0;
+        for (int k = 0; k < 6; ++k) if (getbit(w, k)) c[n++] = k;
+        at = n ? c[rand_u32() % n] : A_NOOP;
+      }
+      a[0] = (uint8_t)at;
+      for (int comp = 1; comp < 7; ++comp) {
+        int cand[49], n = 0;
+        for (int j = 0; j < kNvec[comp]; ++j)
+          if (getbit(w, kNvecOff[comp] + j)) cand[n++] = j;
+        a[comp] = n ? (uint8_t)cand[rand_u32() % n] : 0;
+      }
+      exec(uid, a, rwo);
+      return;
+    }
+    case BOT_WORKER_RUSH: {
+      if (u.type == BASE) { produce(WORKER); return; }
+      if (u.type == WORKER) {
+        if (try_attack()) return;
+        if (widx == 0 && harvest_cycle()) return;
+        chase();
+      }
+      return;
+    }
+    case BOT_LIGHT_RUSH: {
+      if (u.type == BASE) { if (n_workers < 2) produce(WORKER); return; }
+      if (u.type == BARRACKS) { produce(LIGHT); return; }
+      if (u.type == WORKER) {
+        if (try_attack()) return;
+        if (n_barracks == 0 && resources_[player] >= kSpec[BARRACKS].cost && widx == 1) {
+          if (produce(BARRACKS)) return;
+        }
+        if (harvest_cycle()) return;
+        return;
+      }
+      if (try_attack()) return;
+      chase();
+      return;
+    }
+    case BOT_COAC:
+    default: {
+      // economy + mixed army (a small "coacAI"-like build order)
+      if (u.type == BASE) { if (n_workers < 3) produce(WORKER); return; }
+      if (u.type == BARRACKS) {
+        const int r = resources_[player];
+        int t = (r >= kSpec[HEAVY].cost && rand_unit() < 0.3f) ? HEAVY
+              : (rand_unit() < 0.5f ? RANGED : LIGHT);
+        produce(t);
+        return;
+      }
+      if (u.type == WORKER) {
+        if (try_attack()) return;
+        if (n_barracks == 0 && resources_[player] >= kSpec[BARRACKS].cost && widx == 1) {
+          if (produce(BARRACKS)) return;
+        }
+        if (widx <= 1 && harvest_cycle()) return;
+        chase();
+        return;
+      }
+      if (try_attack()) return;
+      chase();
+      return;
+    }
+  }
+}
+
+void MicroRTSSim::bot_act(int player, float* rwo) {
+  const size_t n = units_.size();
+  for (size_t i = 0; i < n; ++i) {
+    if (!units_[i].alive || units_[i].owner != player || units_[i].busy > 0) continue;
+    bot_unit((int)i, player, rwo);
+  }
+}
+
+void MicroRTSSim::set_opponent_actions(const uint8_t* a) {
+  std::memcpy(opp_actions_.data(), a, opp_actions_.size());
+}
+
+float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
+  float rw[kNumRewards] = {0, 0, 0, 0, 0, 0};
+  // 1) agent actions for idle units, validated against the mask it observed
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c) {
+    const int g = grid_[c];
+    if (g < 0) continue;
+    const Unit& u = units_[g];
+    if (u.owner != 0 || u.busy > 0) continue;
+    const uint8_t* a = actions + (size_t)c * kActComps;
+    const uint32_t* m = &mask_[(size_t)c * kMaskWords];
+    if (a[0] >= 6 || !getbit(m, a[0])) continue;
+    // the chosen type's parameter must be legal too
+    int comp = 0;
+    switch (a[0]) {
+      case A_MOVE: comp = 1; break; case A_HARVEST: comp = 2; break;
+      case A_RETURN: comp = 3; break; case A_PRODUCE: comp = 4; break;
+      case A_ATTACK: comp = 6; break; default: comp = 0;
+    }
+    if (comp && (a[comp] >= kNvec[comp] || !getbit(m, kNvecOff[comp] + a[comp]))) continue;
+    if (a[0] == A_PRODUCE && (a[5] >= 7 || !getbit(m, kNvecOff[5] + a[5]))) continue;
+    exec(g, a, rw);
+  }
+  // 2) opponent
+  if (external_opp_) {
+    for (int c = 0; c < nc; ++c) {
+      // opponent actions are given in its own (mirrored) frame
+      const uint8_t* ap = &opp_actions_[(size_t)c * kActComps];
+      int rx, ry;
+      map_xy(1, c % s_, c / s_, &rx, &ry);
+      const int g = grid_[cell(rx, ry)];
+      if (g < 0) continue;
+      const Unit& u = units_[g];
+      if (u.owner != 1 || u.busy > 0) continue;
+      const uint32_t* m = &mask_p1_[(size_t)c * kMaskWords];
+      if (ap[0] >= 6 || !getbit(m, ap[0])) continue;
+      uint8_t a[7];
+      for (int k = 0; k < 7; ++k) a[k] = ap[k];
+      for (int k = 1; k <= 4; ++k) a[k] = (uint8_t)((ap[k] + 2) & 3);
+      a[6] = (uint8_t)((6 - ap[6] / 7) * 7 + (6 - ap[6] % 7));
+      exec(g, a, nullptr);
+    }
+  } else {
+    bot_act(1, nullptr);
+  }
+  // 3) advance time
+  for (Unit& u : units_)
+    if (u.alive && u.busy > 0) {
+      if (--u.busy == 0) u.act = A_NOOP;
+    }
+  ++tick_;
+  // 4) terminal check
+  int alive[2] = {0, 0};
+  for (const Unit& u : units_)
+    if (u.alive && u.owner >= 0) alive[u.owner]++;
+  bool d = false;
+  if (alive[1] == 0 || alive[0] == 0) {
+    d = true;
+    last_winner_ = alive[1] == 0 ? (alive[0] == 0 ? -1 : 0) : 1;
+    rw[R_WIN] = last_winner_ == 0 ? 1.f : (last_winner_ == 1 ? -1.f : 0.f);
+  } else if (tick_ >= max_steps_) {
+    d = true;
+    last_winner_ = -1;
+  }
+  float r = 0.f;
+  for (int i = 0; i < kNumRewards; ++i) r += rw_[i] * rw[i];
+  if (raw) for (int i = 0; i < kNumRewards; ++i) raw[i] = rw[i];
+  *done = d;
+  if (d) {
+    reset();
+  } else {
+    compute_mask(0, mask_);
+    if (external_opp_) compute_mask(1, mask_p1_);
+  }
+  return r;
+}
+
+// ---------------------------------------------------------------- observations
+static inline uint32_t unit_bits(const Unit* u, int player) {
+  // empty cell: hp0, res0, owner none, type none, action noop
+  if (!u) return (1u << 0) | (1u << 5) | (1u << 10) | (1u << 13) | (1u << 21);
+  uint32_t b = 0;
+  b |= 1u << (0 + std::min<int>(std::max<int>(u->hp, 0), 4));
+  b |= 1u << (5 + std::min<int>(std::max<int>(u->res, 0), 4));
+  int own = u->owner < 0 ? 0 : (u->owner == player ? 1 : 2);
+  b |= 1u << (10 + own);
+  b |= 1u << (13 + u->type);
+  b |= 1u << (21 + u->act);
+  return b;
+}
+
+void MicroRTSSim::write_obs(uint32_t* out) const {
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c) {
+    int g = grid_[c];
+    out[c] = unit_bits(g >= 0 ? &units_[g] : nullptr, 0);
+  }
+}
+
+void MicroRTSSim::write_obs_p1(uint32_t* out) const {
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c) {
+    int rx, ry;
+    map_xy(1, c % s_, c / s_, &rx, &ry);
+    int g = grid_[cell(rx, ry)];
+    out[c] = unit_bits(g >= 0 ? &units_[g] : nullptr, 1);
+  }
+}
+
+void MicroRTSSim::write_mask(uint32_t* out) const {
+  std::memcpy(out, mask_.data(), mask_.size() * sizeof(uint32_t));
+}
+void MicroRTSSim::write_mask_p1(uint32_t* out) const {
+  std::memcpy(out, mask_p1_.data(), mask_p1_.size() * sizeof(uint32_t));
+}
+
+void MicroRTSSim::write_obs_dense(float* out) const {
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c) {
+    int g = grid_[c];
+    uint32_t b = unit_bits(g >= 0 ? &units_[g] : nullptr, 0);
+    for (int p = 0; p < kPlanes; ++p) out[(size_t)c * kPlanes + p] = (float)((b >> p) & 1u);
+  }
+}
+
+void MicroRTSSim::write_mask_dense(uint8_t* out) const {
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c)
+    for (int j = 0; j < kMaskBits; ++j)
+      out[(size_t)c * kMaskBits + j] = getbit(&mask_[(size_t)c * kMaskWords], j) ? 1 : 0;
+}
+
+}  // namespace mb

@@ -1,0 +1,154 @@
+// Device-side helpers shared by the microbeast_amd HIP kernels (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define MBK_WAVE 64
+
+namespace mbk {
+
+// microRTS GridMode per-cell action components (reference model.py:168,
+// libs/utils.py:40-44): nvec = [6,4,4,4,4,7,49], 78 logits per cell.
+constexpr int kComps = 7;
+constexpr int kCell = 78;
+__host__ __device__ constexpr int seg_off(int k) {
+  return k == 0 ? 0 : k == 1 ? 6 : k == 2 ? 10 : k == 3 ? 14 : k == 4 ? 18 : k == 5 ? 22
+       : k == 6 ? 29 : 78;
+}
+
+__device__ __forceinline__ bool mask_bit(const uint32_t m[3], int j) {
+  return (m[j >> 5] >> (j & 31)) & 1u;
+}
+
+// ------------------------------------------------------------------ Philox4x32-10
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    u32x4 n;
+    n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+    n.y = (uint32_t)p1;
+    n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+    n.w = (uint32_t)p0;
+    c = n;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) {  // (0,1]
+  return ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+}
+
+// ------------------------------------------------------------------ cell epilogue
+// One microRTS cell: 78 logits z (fp32, any stride-1 storage), 78 mask bits,
+// 7 categorical segments. Semantics match the reference CategoricalMasked
+// (model.py:33-52): masked logits are replaced by -1e8, so a masked entry has
+// probability 0 and contributes 0 to the entropy; a fully-masked segment has
+// log-prob 0 and entropy 0 in fp32 (as in the reference); we sample index 0
+// there (the env ignores it — no unit to command).
+//
+// mode 0 = score the given actions; mode 1 = sample (writes actions).
+template <typename ZPtr>
+__device__ __forceinline__ void cell_forward(const ZPtr z, const uint32_t m[3], uint8_t* act,
+                                             bool sample, const float u[kComps], float* logp_out,
+                                             float* ent_out) {
+  float lp = 0.f, ent = 0.f;
+#pragma unroll
+  for (int k = 0; k < kComps; ++k) {
+    const int off = seg_off(k), n = seg_off(k + 1) - off;
+    float mx = -INFINITY;
+    for (int j = 0; j < n; ++j)
+      if (mask_bit(m, off + j)) mx = fmaxf(mx, (float)z[off + j]);
+    if (mx == -INFINITY) {  // fully masked segment
+      if (sample) act[k] = 0;
+      continue;
+    }
+    float s = 0.f, sz = 0.f;
+    for (int j = 0; j < n; ++j)
+      if (mask_bit(m, off + j)) {
+        const float zj = (float)z[off + j];
+        const float e = __expf(zj - mx);
+        s += e;
+        sz += e * zj;
+      }
+    const float inv = 1.f / s;
+    const float lse = mx + __logf(s);
+    ent += lse - sz * inv;  // -sum p log p = lse - sum p z
+    int a;
+    if (sample) {
+      const float target = u[k] * s;
+      float c = 0.f;
+      a = -1;
+      int last = 0;
+      for (int j = 0; j < n; ++j)
+        if (mask_bit(m, off + j)) {
+          last = j;
+          c += __expf((float)z[off + j] - mx);
+          if (a < 0 && c >= target) a = j;
+        }
+      if (a < 0) a = last;
+      act[k] = (uint8_t)a;
+    } else {
+      a = act[k];
+    }
+    const bool valid = a < n && mask_bit(m, off + a);
+    lp += (valid ? (float)z[off + a] : -1e8f) - lse;
+  }
+  *logp_out = lp;
+  *ent_out = ent;
+}
+
+// dL/dz for one cell given dL/dlogp (gl) and dL/dentropy (ge) of its sample.
+//   valid j: gl*(1[j==a] - p_j) - ge*p_j*(log p_j + H_seg);  masked j: 0
+template <typename ZPtr, typename DPtr>
+__device__ __forceinline__ void cell_backward(const ZPtr z, const uint32_t m[3],
+                                              const uint8_t* act, float gl, float ge, DPtr dz) {
+#pragma unroll
+  for (int k = 0; k < kComps; ++k) {
+    const int off = seg_off(k), n = seg_off(k + 1) - off;
+    float mx = -INFINITY;
+    for (int j = 0; j < n; ++j)
+      if (mask_bit(m, off + j)) mx = fmaxf(mx, (float)z[off + j]);
+    if (mx == -INFINITY) {
+      for (int j = 0; j < n; ++j) dz[off + j] = 0.f;
+      continue;
+    }
+    float s = 0.f, sz = 0.f;
+    for (int j = 0; j < n; ++j)
+      if (mask_bit(m, off + j)) {
+        const float zj = (float)z[off + j];
+        const float e = __expf(zj - mx);
+        s += e;
+        sz += e * zj;
+      }
+    const float inv = 1.f / s;
+    const float lse = mx + __logf(s);
+    const float H = lse - sz * inv;
+    const int a = act[k];
+    for (int j = 0; j < n; ++j) {
+      float d = 0.f;
+      if (mask_bit(m, off + j)) {
+        const float zj = (float)z[off + j];
+        const float p = __expf(zj - mx) * inv;
+        const float logp = zj - lse;
+        d = gl * ((j == a ? 1.f : 0.f) - p) - ge * p * (logp + H);
+      }
+      dz[off + j] = d;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace mbk

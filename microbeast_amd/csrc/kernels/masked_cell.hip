@@ -1,0 +1,167 @@
+// Masked multi-discrete microRTS action head epilogue as standalone kernels
+// (materialised logits). Replaces the reference's Python loop over 7*s*s
+// CategoricalMasked objects per forward (model.py:168-200; 1,792 objects at
+// 16x16), each doing where(mask, l, -1e8) + logsumexp + sample/log_prob/entropy.
+//
+// One thread owns one cell (78 logits, 7 segments). A 64-cell tile of the
+// contiguous cell-major logits is staged through LDS with coalesced loads
+// into rows padded to 79 floats (odd stride => conflict-free per-lane reads).
+// Used by the GridNet arch (logits from a deconv decoder) and as the parity
+// oracle of the fused GEMM+epilogue head (head.hip).
+#include "../include/mbk_api.h"
+#include "common.h"
+
+using namespace mbk;
+
+namespace {
+
+constexpr int kTile = 64;        // cells per block (one wave)
+constexpr int kRow = kCell + 1;  // padded LDS row
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p) { return (float)*p; }
+template <>
+__device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p) {
+  return __bfloat162float(*p);
+}
+
+template <typename TZ>
+__device__ __forceinline__ void stage_tile(const TZ* __restrict__ logits, int64_t c0, int ncell,
+                                           float* zs) {
+  const int64_t base = c0 * kCell;
+  const int total = ncell * kCell;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int r = e / kCell, c = e - r * kCell;
+    zs[r * kRow + c] = ld(logits + base + e);
+  }
+}
+
+template <typename TZ>
+__global__ __launch_bounds__(kTile) void masked_cell_fwd_kernel(
+    const TZ* __restrict__ logits, const uint32_t* __restrict__ mask, uint8_t* __restrict__ action,
+    const uint64_t* __restrict__ rng, int sample, int64_t ncells, float* __restrict__ cell_logp,
+    float* __restrict__ cell_ent) {
+  __shared__ float zs[kTile * kRow];
+  const int64_t c0 = (int64_t)blockIdx.x * kTile;
+  const int nc = (int)min((int64_t)kTile, ncells - c0);
+  stage_tile(logits, c0, nc, zs);
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i >= nc) return;
+  const int64_t cell = c0 + i;
+  uint32_t m[3] = {mask[cell * 3 + 0], mask[cell * 3 + 1], mask[cell * 3 + 2]};
+  uint8_t a[kComps];
+  float u[kComps];
+  if (sample) {
+    const uint64_t seed = rng[0], step = rng[1];
+    u32x4 c = {(uint32_t)cell, (uint32_t)(cell >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
+    u32x4 r0 = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    c.y ^= 0x80000000u;
+    u32x4 r1 = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    u[0] = u01(r0.x); u[1] = u01(r0.y); u[2] = u01(r0.z); u[3] = u01(r0.w);
+    u[4] = u01(r1.x); u[5] = u01(r1.y); u[6] = u01(r1.z);
+  } else {
+#pragma unroll
+    for (int k = 0; k < kComps; ++k) a[k] = action[cell * kComps + k];
+  }
+  float lp, ent;
+  cell_forward(zs + i * kRow, m, a, sample != 0, u, &lp, &ent);
+  if (sample) {
+#pragma unroll
+    for (int k = 0; k < kComps; ++k) action[cell * kComps + k] = a[k];
+  }
+  cell_logp[cell] = lp;
+  if (cell_ent) cell_ent[cell] = ent;
+}
+
+template <typename TZ, typename TD>
+__global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
+    const TZ* __restrict__ logits, const uint32_t* __restrict__ mask,
+    const uint8_t* __restrict__ action, const float* __restrict__ g_logp,
+    const float* __restrict__ g_ent, int cells_per_sample, int64_t ncells,
+    TD* __restrict__ dlogits) {
+  __shared__ float zs[kTile * kRow];
+  const int64_t c0 = (int64_t)blockIdx.x * kTile;
+  const int nc = (int)min((int64_t)kTile, ncells - c0);
+  stage_tile(logits, c0, nc, zs);
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i < nc) {
+    const int64_t cell = c0 + i;
+    const int64_t smp = cell / cells_per_sample;
+    uint32_t m[3] = {mask[cell * 3 + 0], mask[cell * 3 + 1], mask[cell * 3 + 2]};
+    uint8_t a[kComps];
+#pragma unroll
+    for (int k = 0; k < kComps; ++k) a[k] = action[cell * kComps + k];
+    // in place: each segment's logits are read before its gradients overwrite them
+    float* row = zs + i * kRow;
+    cell_backward(row, m, a, g_logp[smp], g_ent ? g_ent[smp] : 0.f, row);
+  }
+  __syncthreads();
+  const int64_t base = c0 * kCell;
+  const int total = nc * kCell;
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int r = e / kCell, c = e - r * kCell;
+    dlogits[base + e] = (TD)zs[r * kRow + c];
+  }
+}
+
+// Per-sample sums of per-cell values: out[n] = sum_c in[n, c] (one wave per sample).
+__global__ __launch_bounds__(256) void row_sum_kernel(const float* __restrict__ in, int64_t rows,
+                                                       int cols, float* __restrict__ out) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += in[r * cols + c];
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s;
+}
+
+__global__ void rng_advance_kernel(uint64_t* rng) { rng[1] += 1; }
+
+}  // namespace
+
+extern "C" int mbk_masked_cell_fwd(const void* logits, int logits_bf16, const uint32_t* mask,
+                                   uint8_t* action, const uint64_t* rng, int sample,
+                                   int64_t ncells, float* cell_logp, float* cell_ent,
+                                   hipStream_t stream) {
+  dim3 grid((unsigned)((ncells + kTile - 1) / kTile));
+  if (logits_bf16)
+    hipLaunchKernelGGL(masked_cell_fwd_kernel<__hip_bfloat16>, grid, dim3(kTile), 0, stream,
+                       (const __hip_bfloat16*)logits, mask, action, rng, sample, ncells, cell_logp,
+                       cell_ent);
+  else
+    hipLaunchKernelGGL(masked_cell_fwd_kernel<float>, grid, dim3(kTile), 0, stream,
+                       (const float*)logits, mask, action, rng, sample, ncells, cell_logp, cell_ent);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_masked_cell_bwd(const void* logits, int logits_bf16, const uint32_t* mask,
+                                   const uint8_t* action, const float* g_logp, const float* g_ent,
+                                   int cells_per_sample, int64_t ncells, void* dlogits,
+                                   int dlogits_bf16, hipStream_t stream) {
+  dim3 grid((unsigned)((ncells + kTile - 1) / kTile));
+#define MBK_BWD(TZ, TD)                                                                        \
+  hipLaunchKernelGGL((masked_cell_bwd_kernel<TZ, TD>), grid, dim3(kTile), 0, stream,           \
+                     (const TZ*)logits, mask, action, g_logp, g_ent, cells_per_sample, ncells, \
+                     (TD*)dlogits)
+  if (logits_bf16 && dlogits_bf16) MBK_BWD(__hip_bfloat16, __hip_bfloat16);
+  else if (logits_bf16) MBK_BWD(__hip_bfloat16, float);
+  else if (dlogits_bf16) MBK_BWD(float, __hip_bfloat16);
+  else MBK_BWD(float, float);
+#undef MBK_BWD
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_row_sum(const float* in, int64_t rows, int cols, float* out,
+                           hipStream_t stream) {
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipLaunchKernelGGL(row_sum_kernel, grid, dim3(256), 0, stream, in, rows, cols, out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_rng_advance(uint64_t* rng, hipStream_t stream) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, stream, rng);
+  return (int)hipGetLastError();
+}

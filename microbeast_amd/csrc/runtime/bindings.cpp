@@ -1,0 +1,210 @@
+// pybind11 bindings of the native runtime (_mbrt). Buffers cross the boundary
+// as raw addresses (torch tensor .data_ptr()), so the same calls work on
+// pinned host tensors, shared-memory tensors and numpy arrays; every
+// potentially long call releases the GIL.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+
+#include "engine.h"
+#include "shm_ring.h"
+#include "vec_env.h"
+
+namespace py = pybind11;
+using namespace mb;
+
+namespace {
+
+template <typename T>
+T* P(uintptr_t a) { return reinterpret_cast<T*>(a); }
+
+struct PyVecEnv {
+  std::unique_ptr<VecEnv> env;
+  EpisodeLog log;
+  PyVecEnv(int size, int n, int max_steps, uint64_t seed, std::vector<int> bots,
+           std::vector<float> rw, int base)
+      : env(new VecEnv(size, n, max_steps, seed, bots, rw.empty() ? nullptr : rw.data(), base)) {}
+};
+
+py::list records_to_list(const std::vector<EpisodeRecord>& recs) {
+  py::list out;
+  for (const auto& r : recs) out.append(py::make_tuple(r.ep_return, r.ep_step, r.env_index, r.winner));
+  return out;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_mbrt, m) {
+  m.doc() = "microbeast_amd native runtime";
+  m.attr("PLANES") = kPlanes;
+  m.attr("MASK_BITS") = kMaskBits;
+  m.attr("MASK_WORDS") = kMaskWords;
+  m.attr("ACT_COMPS") = kActComps;
+  m.attr("NVEC") = std::vector<int>(kNvec, kNvec + kActComps);
+  py::dict bots;
+  bots["coac"] = (int)BOT_COAC;
+  bots["random_biased"] = (int)BOT_RANDOM_BIASED;
+  bots["light_rush"] = (int)BOT_LIGHT_RUSH;
+  bots["worker_rush"] = (int)BOT_WORKER_RUSH;
+  bots["passive"] = (int)BOT_PASSIVE;
+  bots["random"] = (int)BOT_RANDOM;
+  m.attr("BOTS") = bots;
+
+  py::class_<PyVecEnv>(m, "VecEnv")
+      .def(py::init<int, int, int, uint64_t, std::vector<int>, std::vector<float>, int>(),
+           py::arg("size"), py::arg("n_envs"), py::arg("max_steps"), py::arg("seed"),
+           py::arg("bots") = std::vector<int>{}, py::arg("reward_weight") = std::vector<float>{},
+           py::arg("env_index_base") = 0)
+      .def_property_readonly("num_envs", [](PyVecEnv& e) { return e.env->num_envs(); })
+      .def_property_readonly("size", [](PyVecEnv& e) { return e.env->size(); })
+      .def("reset",
+           [](PyVecEnv& e, uintptr_t obs, uintptr_t mask) {
+             py::gil_scoped_release g;
+             e.env->reset(P<uint32_t>(obs), P<uint32_t>(mask));
+           })
+      .def("step",
+           [](PyVecEnv& e, uintptr_t act, uintptr_t obs, uintptr_t mask, uintptr_t rew,
+              uintptr_t done, uintptr_t ep_ret, uintptr_t ep_step) {
+             py::gil_scoped_release g;
+             e.env->step_range(0, e.env->num_envs(), 0, P<uint8_t>(act), P<uint32_t>(obs),
+                               P<uint32_t>(mask), P<float>(rew), P<uint8_t>(done),
+                               P<float>(ep_ret), P<int32_t>(ep_step), &e.log);
+           },
+           py::arg("actions"), py::arg("obs"), py::arg("mask"), py::arg("reward"),
+           py::arg("done"), py::arg("ep_return") = 0, py::arg("ep_step") = 0)
+      .def("dense_obs", [](PyVecEnv& e, uintptr_t out) { e.env->dense_obs(P<float>(out)); })
+      .def("dense_mask", [](PyVecEnv& e, uintptr_t out) { e.env->dense_mask(P<uint8_t>(out)); })
+      .def("drain_episodes", [](PyVecEnv& e) { return records_to_list(e.log.drain()); })
+      .def("set_bot", [](PyVecEnv& e, int i, int bot) { e.env->sim(i).set_bot(bot); })
+      .def("bot", [](PyVecEnv& e, int i) { return e.env->sim(i).bot(); })
+      .def("set_external_opponent",
+           [](PyVecEnv& e, bool on) {
+             for (int i = 0; i < e.env->num_envs(); ++i) e.env->sim(i).set_external_opponent(on);
+           })
+      .def("obs_p1",
+           [](PyVecEnv& e, uintptr_t out) {
+             const size_t S = (size_t)e.env->size() * e.env->size();
+             for (int i = 0; i < e.env->num_envs(); ++i)
+               e.env->sim(i).write_obs_p1(P<uint32_t>(out) + i * S);
+           })
+      .def("mask_p1",
+           [](PyVecEnv& e, uintptr_t out) {
+             const size_t S = (size_t)e.env->size() * e.env->size();
+             for (int i = 0; i < e.env->num_envs(); ++i)
+               e.env->sim(i).write_mask_p1(P<uint32_t>(out) + i * S * kMaskWords);
+           })
+      .def("set_opponent_actions",
+           [](PyVecEnv& e, uintptr_t act) {
+             const size_t S = (size_t)e.env->size() * e.env->size();
+             for (int i = 0; i < e.env->num_envs(); ++i)
+               e.env->sim(i).set_opponent_actions(P<uint8_t>(act) + i * S * kActComps);
+           })
+      .def("ticks", [](PyVecEnv& e, int i) { return e.env->sim(i).ticks(); });
+
+  py::class_<IndexRing>(m, "IndexRing")
+      .def(py::init([](uintptr_t addr, size_t cap, bool init) {
+             return new IndexRing(P<void>(addr), cap, init);
+           }),
+           py::arg("addr"), py::arg("capacity"), py::arg("init"))
+      .def_static("bytes_needed", &IndexRing::bytes_needed)
+      .def("try_push", &IndexRing::try_push)
+      .def("try_pop",
+           [](IndexRing& r) -> py::object {
+             int64_t v;
+             if (r.try_pop(&v)) return py::int_(v);
+             return py::none();
+           })
+      .def("push",
+           [](IndexRing& r, int64_t v, double timeout) {
+             py::gil_scoped_release g;
+             return r.push(v, timeout);
+           },
+           py::arg("value"), py::arg("timeout") = -1.0)
+      .def("pop",
+           [](IndexRing& r, double timeout) -> py::object {
+             int64_t v;
+             bool ok;
+             {
+               py::gil_scoped_release g;
+               ok = r.pop(&v, timeout);
+             }
+             if (ok) return py::int_(v);
+             return py::none();
+           },
+           py::arg("timeout") = -1.0)
+      .def("size", &IndexRing::size)
+      .def("capacity", &IndexRing::capacity)
+      .def("close", &IndexRing::close)
+      .def("closed", &IndexRing::closed);
+
+  m.def("seqlock_write_begin",
+        [](uintptr_t ver) { return seqlock_write_begin(P<std::atomic<uint64_t>>(ver)); });
+  m.def("seqlock_write_end", [](uintptr_t ver) { seqlock_write_end(P<std::atomic<uint64_t>>(ver)); });
+  m.def("seqlock_read",
+        [](uintptr_t ver, uintptr_t src, uintptr_t dst, size_t n, int tries) {
+          py::gil_scoped_release g;
+          return seqlock_read(P<const std::atomic<uint64_t>>(ver), P<const void>(src), P<void>(dst),
+                              n, tries);
+        },
+        py::arg("ver"), py::arg("src"), py::arg("dst"), py::arg("nbytes"),
+        py::arg("max_tries") = 1000);
+
+  py::class_<GpuEngine>(m, "GpuEngine")
+      .def(py::init([](py::dict c, py::dict b) {
+        EngineConfig cfg;
+        cfg.size = c["size"].cast<int>();
+        cfg.n_groups = c["n_groups"].cast<int>();
+        cfg.envs_per_group = c["envs_per_group"].cast<int>();
+        cfg.unroll = c["unroll"].cast<int>();
+        cfg.n_slots = c["n_slots"].cast<int>();
+        cfg.n_threads = c["n_threads"].cast<int>();
+        cfg.max_steps = c["max_steps"].cast<int>();
+        cfg.seed = c["seed"].cast<uint64_t>();
+        cfg.bots = c["bots"].cast<std::vector<int>>();
+        cfg.reward_weight = c["reward_weight"].cast<std::vector<float>>();
+        cfg.env_index_base = c["env_index_base"].cast<int>();
+        cfg.device = c["device"].cast<int>();
+        EngineBuffers buf;
+        buf.obs = b["obs"].cast<uintptr_t>();
+        buf.mask = b["mask"].cast<uintptr_t>();
+        buf.action = b["action"].cast<uintptr_t>();
+        buf.logp = b["logp"].cast<uintptr_t>();
+        buf.value = b["value"].cast<uintptr_t>();
+        buf.reward = b["reward"].cast<uintptr_t>();
+        buf.done = b["done"].cast<uintptr_t>();
+        buf.in_obs = b["in_obs"].cast<uintptr_t>();
+        buf.in_mask = b["in_mask"].cast<uintptr_t>();
+        buf.out_action = b["out_action"].cast<uintptr_t>();
+        buf.out_logp = b["out_logp"].cast<uintptr_t>();
+        buf.out_value = b["out_value"].cast<uintptr_t>();
+        return new GpuEngine(cfg, buf);
+      }))
+      .def("start", &GpuEngine::start, py::arg("graph_exec"))
+      .def("stop", [](GpuEngine& e) { py::gil_scoped_release g; e.stop(); })
+      .def("get_full",
+           [](GpuEngine& e, int n, double timeout) {
+             py::gil_scoped_release g;
+             return e.get_full(n, timeout);
+           },
+           py::arg("n"), py::arg("timeout") = -1.0)
+      .def("stream_wait_full", &GpuEngine::stream_wait_full)
+      .def("release", &GpuEngine::release)
+      .def("publish", &GpuEngine::publish)
+      .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
+      .def("stream", &GpuEngine::stream)
+      .def("failed", &GpuEngine::failed)
+      .def("error", &GpuEngine::error)
+      .def("stats", [](GpuEngine& e) {
+        EngineStats s = e.stats();
+        py::dict d;
+        d["frames"] = s.frames;
+        d["gpu_steps"] = s.gpu_steps;
+        d["slots_full"] = s.slots_full;
+        d["driver_idle_s"] = s.driver_idle_s;
+        d["slot_wait_s"] = s.slot_wait_s;
+        d["env_s"] = s.env_s;
+        d["publishes"] = s.publishes;
+        return d;
+      });
+}

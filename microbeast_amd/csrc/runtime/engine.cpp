@@ -1,0 +1,383 @@
+#include "engine.h"
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "../include/mbk_api.h"
+
+namespace mb {
+
+#define ENG_CHECK(expr)                                                              \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      fail(std::string(#expr) + " failed: " + hipGetErrorString(_e));                \
+      return false;                                                                  \
+    }                                                                                \
+  } while (0)
+
+#define CTOR_CHECK(expr)                                                             \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess)                                                            \
+      throw std::runtime_error(std::string(#expr) + " failed: " + hipGetErrorString(_e)); \
+  } while (0)
+
+GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(cfg), buf_(buf) {
+  if (cfg_.n_groups < 1 || cfg_.envs_per_group < 1 || cfg_.unroll < 1)
+    throw std::runtime_error("GpuEngine: bad config");
+  if (cfg_.n_slots < cfg_.n_groups + 1)
+    throw std::runtime_error("GpuEngine: need n_slots >= n_groups + 1");
+  S_ = cfg_.size * cfg_.size;
+  const size_t E = cfg_.envs_per_group, T1 = cfg_.unroll + 1;
+  slot_stride_obs_ = T1 * E * S_ * 4;
+  slot_stride_mask_ = T1 * E * S_ * 4 * kMaskWords;
+  slot_stride_act_ = T1 * E * S_ * kActComps;
+  slot_stride_scalar_ = T1 * E;  // elements
+  const int total = cfg_.n_groups * cfg_.envs_per_group;
+  env_.reset(new VecEnv(cfg_.size, total, cfg_.max_steps, cfg_.seed, cfg_.bots,
+                        cfg_.reward_weight.empty() ? nullptr : cfg_.reward_weight.data(),
+                        cfg_.env_index_base));
+  CTOR_CHECK(hipSetDevice(cfg_.device));
+  CTOR_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  CTOR_CHECK(hipHostMalloc((void**)&h_obs_, (size_t)total * S_ * 4, hipHostMallocDefault));
+  CTOR_CHECK(hipHostMalloc((void**)&h_mask_, (size_t)total * S_ * 4 * kMaskWords,
+                           hipHostMallocDefault));
+  CTOR_CHECK(hipHostMalloc((void**)&h_action_, (size_t)total * S_ * kActComps,
+                           hipHostMallocDefault));
+  CTOR_CHECK(hipHostMalloc((void**)&h_reward_, (size_t)total * 4, hipHostMallocDefault));
+  CTOR_CHECK(hipHostMalloc((void**)&h_done_, (size_t)total, hipHostMallocDefault));
+  CTOR_CHECK(hipMalloc((void**)&d_rd_, E * 4 + E + 64));
+  std::memset(h_reward_, 0, (size_t)total * 4);
+  std::memset(h_done_, 0, (size_t)total);
+  env_->reset(h_obs_, h_mask_);
+  for (int g = 0; g < cfg_.n_groups; ++g) {
+    groups_.emplace_back(new Group());
+    CTOR_CHECK(hipEventCreateWithFlags(&groups_[g]->ev, hipEventDisableTiming));
+    groups_[g]->phase.store(READY);  // reset observations are ready
+  }
+  full_ev_.resize(cfg_.n_slots);
+  release_ev_.resize(cfg_.n_slots);
+  release_pending_.assign(cfg_.n_slots, false);
+  for (int s = 0; s < cfg_.n_slots; ++s) {
+    CTOR_CHECK(hipEventCreateWithFlags(&full_ev_[s], hipEventDisableTiming));
+    CTOR_CHECK(hipEventCreateWithFlags(&release_ev_[s], hipEventDisableTiming));
+    free_slots_.push_back(s);
+  }
+  CTOR_CHECK(hipEventCreateWithFlags(&pub_ready_, hipEventDisableTiming));
+  CTOR_CHECK(hipEventCreateWithFlags(&pub_consumed_, hipEventDisableTiming));
+  CTOR_CHECK(hipMalloc((void**)&pub_staging_, 16));
+  pub_staging_n_ = 0;
+  // work chunk: enough chunks for every worker, at least 2 envs each
+  chunk_ = std::max(1, std::min(16, cfg_.envs_per_group / std::max(1, 2 * cfg_.n_threads)));
+}
+
+GpuEngine::~GpuEngine() {
+  stop();
+  if (stream_) hipStreamSynchronize(stream_);
+  for (auto& g : groups_) if (g->ev) hipEventDestroy(g->ev);
+  for (auto e : full_ev_) hipEventDestroy(e);
+  for (auto e : release_ev_) hipEventDestroy(e);
+  if (pub_ready_) hipEventDestroy(pub_ready_);
+  if (pub_consumed_) hipEventDestroy(pub_consumed_);
+  if (pub_staging_) hipFree(pub_staging_);
+  if (h_obs_) hipHostFree(h_obs_);
+  if (h_mask_) hipHostFree(h_mask_);
+  if (h_action_) hipHostFree(h_action_);
+  if (h_reward_) hipHostFree(h_reward_);
+  if (h_done_) hipHostFree(h_done_);
+  if (d_rd_) hipFree(d_rd_);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+void GpuEngine::fail(const std::string& msg) {
+  {
+    std::lock_guard<std::mutex> g(err_m_);
+    if (err_.empty()) err_ = msg;
+  }
+  failed_.store(true);
+  running_.store(false);
+  work_cv_.notify_all();
+  full_cv_.notify_all();
+}
+
+std::string GpuEngine::error() const {
+  std::lock_guard<std::mutex> g(err_m_);
+  return err_;
+}
+
+void GpuEngine::start(uintptr_t graph_exec) {
+  if (running_.load()) return;
+  graph_ = (hipGraphExec_t)graph_exec;
+  running_.store(true);
+  for (int w = 0; w < cfg_.n_threads; ++w) workers_.emplace_back(&GpuEngine::worker_loop, this, w);
+  driver_ = std::thread(&GpuEngine::driver_loop, this);
+}
+
+void GpuEngine::stop() {
+  running_.store(false);
+  work_cv_.notify_all();
+  full_cv_.notify_all();
+  if (driver_.joinable()) driver_.join();
+  for (auto& t : workers_) if (t.joinable()) t.join();
+  workers_.clear();
+  if (stream_) hipStreamSynchronize(stream_);
+}
+
+void GpuEngine::dispatch_env(int g) {
+  Group& G = *groups_[g];
+  G.phase.store(ENV_BUSY, std::memory_order_release);
+  G.remaining.store(cfg_.envs_per_group, std::memory_order_release);
+  G.next_env.store(0, std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> l(work_m_);
+    work_epoch_.fetch_add(1);
+  }
+  work_cv_.notify_all();
+}
+
+void GpuEngine::worker_loop(int wid) {
+  const int E = cfg_.envs_per_group, NG = cfg_.n_groups;
+  while (running_.load(std::memory_order_relaxed)) {
+    const uint64_t epoch = work_epoch_.load();
+    bool did = false;
+    for (int k = 0; k < NG; ++k) {
+      const int g = (wid + k) % NG;
+      Group& G = *groups_[g];
+      if (G.phase.load(std::memory_order_acquire) != ENV_BUSY) continue;
+      for (;;) {
+        int e = G.next_env.fetch_add(chunk_);
+        if (e >= E) break;
+        int e1 = std::min(e + chunk_, E);
+        const int a0 = g * E;
+        auto t0 = std::chrono::steady_clock::now();
+        env_->step_range(a0 + e, a0 + e1, 0, h_action_, h_obs_, h_mask_, h_reward_, h_done_,
+                         nullptr, nullptr, &log_);
+        env_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                              std::chrono::steady_clock::now() - t0).count(),
+                          std::memory_order_relaxed);
+        frames_.fetch_add(e1 - e, std::memory_order_relaxed);
+        did = true;
+        if (G.remaining.fetch_sub(e1 - e) == e1 - e) G.phase.store(READY, std::memory_order_release);
+      }
+    }
+    if (!did) {
+      std::unique_lock<std::mutex> l(work_m_);
+      work_cv_.wait_for(l, std::chrono::milliseconds(2),
+                        [&] { return work_epoch_.load() != epoch || !running_.load(); });
+    }
+  }
+}
+
+bool GpuEngine::enqueue_gpu(int g) {
+  Group& G = *groups_[g];
+  const size_t E = cfg_.envs_per_group, T = cfg_.unroll;
+  if (G.t == 0) {
+    int slot = -1;
+    {
+      std::lock_guard<std::mutex> l(slot_m_);
+      if (!free_slots_.empty()) { slot = free_slots_.front(); free_slots_.pop_front(); }
+    }
+    if (slot < 0) return false;  // learner-bound: wait for a released slot
+    if (release_pending_[slot]) ENG_CHECK(hipStreamWaitEvent(stream_, release_ev_[slot], 0));
+    G.cur = slot;
+  }
+  {  // apply a pending weight publish between two inference steps
+    std::lock_guard<std::mutex> l(pub_m_);
+    if (pub_pending_) {
+      ENG_CHECK(hipStreamWaitEvent(stream_, pub_ready_, 0));
+      ENG_CHECK(hipMemcpyAsync((void*)pub_dst_, pub_staging_, pub_n_, hipMemcpyDeviceToDevice,
+                               stream_));
+      ENG_CHECK(hipEventRecord(pub_consumed_, stream_));
+      pub_pending_ = false;
+      publishes_.fetch_add(1);
+    }
+  }
+  const size_t e0 = (size_t)g * E;
+  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_obs, h_obs_ + e0 * S_, E * S_ * 4,
+                           hipMemcpyHostToDevice, stream_));
+  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_mask, h_mask_ + e0 * S_ * kMaskWords,
+                           E * S_ * 4 * kMaskWords, hipMemcpyHostToDevice, stream_));
+  if (!G.first) {
+    ENG_CHECK(hipMemcpyAsync(d_rd_, h_reward_ + e0, E * 4, hipMemcpyHostToDevice, stream_));
+    ENG_CHECK(hipMemcpyAsync(d_rd_ + E * 4, h_done_ + e0, E, hipMemcpyHostToDevice, stream_));
+  }
+  ENG_CHECK(hipGraphLaunch(graph_, stream_));
+
+  // scatter this step into the HBM rollout slot(s)
+  MbkCopySeg seg[MBK_MAX_COPY_SEGS];
+  int n = 0;
+  const size_t t = G.t;
+  auto obs_at = [&](int slot, size_t i) {
+    return (char*)buf_.obs + slot * slot_stride_obs_ + i * E * S_ * 4;
+  };
+  auto mask_at = [&](int slot, size_t i) {
+    return (char*)buf_.mask + slot * slot_stride_mask_ + i * E * S_ * 4 * kMaskWords;
+  };
+  auto act_at = [&](int slot, size_t i) {
+    return (char*)buf_.action + slot * slot_stride_act_ + i * E * S_ * kActComps;
+  };
+  auto f32_at = [&](uintptr_t base, int slot, size_t i) {
+    return (char*)base + (slot * slot_stride_scalar_ + i * E) * 4;
+  };
+  auto u8_at = [&](uintptr_t base, int slot, size_t i) {
+    return (char*)base + (slot * slot_stride_scalar_ + i * E);
+  };
+  seg[n++] = {(const void*)buf_.in_obs, obs_at(G.cur, t), E * S_ * 4};
+  seg[n++] = {(const void*)buf_.in_mask, mask_at(G.cur, t), E * S_ * 4 * kMaskWords};
+  seg[n++] = {(const void*)buf_.out_action, act_at(G.cur, t), E * S_ * kActComps};
+  seg[n++] = {(const void*)buf_.out_logp, f32_at(buf_.logp, G.cur, t), E * 4};
+  seg[n++] = {(const void*)buf_.out_value, f32_at(buf_.value, G.cur, t), E * 4};
+  if (!G.first) {
+    const int rs = t > 0 ? G.cur : G.prev;
+    const size_t ri = t > 0 ? t - 1 : T - 1;
+    seg[n++] = {(const void*)d_rd_, f32_at(buf_.reward, rs, ri), E * 4};
+    seg[n++] = {(const void*)(d_rd_ + E * 4), u8_at(buf_.done, rs, ri), E};
+  }
+  const bool close_prev = (t == 0 && G.prev >= 0);
+  if (close_prev) {
+    seg[n++] = {(const void*)buf_.in_obs, obs_at(G.prev, T), E * S_ * 4};
+    seg[n++] = {(const void*)buf_.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
+  }
+  ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, stream_));
+  if (close_prev) {
+    ENG_CHECK(hipEventRecord(full_ev_[G.prev], stream_));
+    {
+      std::lock_guard<std::mutex> l(slot_m_);
+      full_slots_.push_back(G.prev);
+    }
+    slots_full_.fetch_add(1);
+    full_cv_.notify_all();
+    G.prev = -1;
+  }
+  ENG_CHECK(hipMemcpyAsync(h_action_ + e0 * S_ * kActComps, (const void*)buf_.out_action,
+                           E * S_ * kActComps, hipMemcpyDeviceToHost, stream_));
+  ENG_CHECK(hipEventRecord(G.ev, stream_));
+  gpu_steps_.fetch_add(1);
+  G.t += 1;
+  if (G.t == (int)T) {
+    G.t = 0;
+    G.prev = G.cur;
+    G.cur = -1;
+  }
+  G.first = false;
+  G.phase.store(ON_GPU, std::memory_order_release);
+  return true;
+}
+
+void GpuEngine::driver_loop() {
+  hipSetDevice(cfg_.device);
+  const int NG = cfg_.n_groups;
+  int idle_spins = 0;
+  auto idle_t0 = std::chrono::steady_clock::now();
+  bool idle = false;
+  double stall_s = 0.0;
+  while (running_.load(std::memory_order_relaxed)) {
+    bool progressed = false, stalled = false;
+    for (int g = 0; g < NG && running_.load(std::memory_order_relaxed); ++g) {
+      Group& G = *groups_[g];
+      int ph = G.phase.load(std::memory_order_acquire);
+      if (ph == READY) {
+        if (enqueue_gpu(g)) progressed = true;
+        else if (failed_.load()) return;
+        else stalled = true;
+      } else if (ph == ON_GPU) {
+        hipError_t q = hipEventQuery(G.ev);
+        if (q == hipSuccess) {
+          dispatch_env(g);
+          progressed = true;
+        } else if (q != hipErrorNotReady) {
+          fail(std::string("hipEventQuery: ") + hipGetErrorString(q));
+          return;
+        }
+      }
+    }
+    if (progressed) {
+      if (idle) {
+        double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - idle_t0).count();
+        std::lock_guard<std::mutex> l(stats_m_);
+        driver_idle_s_ += dt;
+        if (stall_s > 0) slot_wait_s_ += dt;
+      }
+      idle = false;
+      idle_spins = 0;
+      stall_s = 0.0;
+    } else {
+      if (!idle) { idle = true; idle_t0 = std::chrono::steady_clock::now(); }
+      if (stalled) stall_s = 1.0;
+      if (++idle_spins < 256) {
+        __builtin_ia32_pause();
+      } else if (idle_spins < 2048) {
+        std::this_thread::yield();
+      } else {
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      }
+    }
+  }
+}
+
+std::vector<int> GpuEngine::get_full(int n, double timeout_s) {
+  std::unique_lock<std::mutex> l(slot_m_);
+  auto pred = [&] { return (int)full_slots_.size() >= n || !running_.load() || failed_.load(); };
+  if (timeout_s < 0) full_cv_.wait(l, pred);
+  else full_cv_.wait_for(l, std::chrono::duration<double>(timeout_s), pred);
+  std::vector<int> out;
+  if ((int)full_slots_.size() < n) return out;
+  for (int i = 0; i < n; ++i) { out.push_back(full_slots_.front()); full_slots_.pop_front(); }
+  return out;
+}
+
+void GpuEngine::stream_wait_full(uintptr_t stream, int slot) {
+  hipError_t e = hipStreamWaitEvent((hipStream_t)stream, full_ev_[slot], 0);
+  if (e != hipSuccess) throw std::runtime_error(std::string("stream_wait_full: ") + hipGetErrorString(e));
+}
+
+void GpuEngine::release(const std::vector<int>& slots, uintptr_t stream) {
+  for (int s : slots) {
+    hipError_t e = hipEventRecord(release_ev_[s], (hipStream_t)stream);
+    if (e != hipSuccess) throw std::runtime_error(std::string("release: ") + hipGetErrorString(e));
+  }
+  std::lock_guard<std::mutex> l(slot_m_);
+  for (int s : slots) {
+    release_pending_[s] = true;
+    free_slots_.push_back(s);
+  }
+}
+
+bool GpuEngine::publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream) {
+  std::lock_guard<std::mutex> l(pub_m_);
+  if (pub_pending_) return false;  // previous version not applied yet: skip this one
+  hipStream_t s = (hipStream_t)stream;
+  if (nbytes > pub_staging_n_) {
+    // first publish (or growth): synchronous realloc is fine outside the hot loop
+    if (pub_staging_) { hipStreamSynchronize(stream_); hipFree(pub_staging_); }
+    if (hipMalloc((void**)&pub_staging_, nbytes) != hipSuccess)
+      throw std::runtime_error("publish: hipMalloc staging failed");
+    pub_staging_n_ = nbytes;
+  }
+  // staging is reused only after the driver's previous copy-out has executed
+  hipStreamWaitEvent(s, pub_consumed_, 0);
+  hipMemcpyAsync(pub_staging_, (const void*)src, nbytes, hipMemcpyDeviceToDevice, s);
+  hipEventRecord(pub_ready_, s);
+  pub_dst_ = dst;
+  pub_n_ = nbytes;
+  pub_pending_ = true;
+  return true;
+}
+
+EngineStats GpuEngine::stats() const {
+  EngineStats s;
+  s.frames = frames_.load();
+  s.gpu_steps = gpu_steps_.load();
+  s.slots_full = slots_full_.load();
+  s.env_s = env_ns_.load() * 1e-9;
+  s.publishes = publishes_.load();
+  std::lock_guard<std::mutex> l(stats_m_);
+  s.driver_idle_s = driver_idle_s_;
+  s.slot_wait_s = slot_wait_s_;
+  return s;
+}
+
+}  // namespace mb

@@ -1,0 +1,168 @@
+// GPU actor engine: native replacement for the reference's actor processes
+// (reference microbeast.py:30-105 act(), :179-191 spawn loop) re-designed for
+// one MI355X per learner process:
+//
+//   * env worker threads (C++, no GIL) step the synthetic microRTS sims and
+//     write compact obs / mask / reward / done into PINNED host staging;
+//   * a driver thread pipelines env groups through the GPU on its own HIP
+//     stream: H2D staging -> hipGraphLaunch(policy inference graph) ->
+//     one multi-segment copy kernel that scatters the step into an
+//     HBM-resident rollout slot -> D2H actions -> event;
+//   * rollout slots live in HBM (288 GB/GPU: thousands of slots fit), so the
+//     learner reads them in place — no stack/reshape/copy (reference
+//     libs/utils.py:197-205 get_batch);
+//   * free/full slot hand-off with HIP events instead of pickled queue ints;
+//   * weight publish is a D2D copy applied between inference steps, ordered by
+//     events (no torn reads; reference libs/utils.py:337 had none).
+//
+// Slot layout (time-major [T+1, E]): index t holds obs_t, mask_t, the action
+// a_t sampled at obs_t with its behaviour log-prob and value, and r_t/done_t
+// produced by stepping a_t. Index T holds obs_T/mask_T for the bootstrap and is
+// also index 0 of the group's next slot (TorchBeast overlap), fixing the
+// reference's obs/action off-by-one.
+#pragma once
+#include <hip/hip_runtime_api.h>
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "vec_env.h"
+
+namespace mb {
+
+struct EngineConfig {
+  int size = 16;
+  int n_groups = 2;
+  int envs_per_group = 256;
+  int unroll = 64;  // T
+  int n_slots = 8;
+  int n_threads = 8;
+  int max_steps = 2000;
+  uint64_t seed = 1;
+  std::vector<int> bots;
+  std::vector<float> reward_weight;
+  int env_index_base = 0;
+  int device = 0;
+};
+
+// Device buffers owned by Python (torch tensors); raw addresses.
+struct EngineBuffers {
+  // rollout storage, all [n_slots, T+1, E, ...]
+  uintptr_t obs = 0;      // u32 [.., S]
+  uintptr_t mask = 0;     // u32 [.., S, 3]
+  uintptr_t action = 0;   // u8  [.., S, 7]
+  uintptr_t logp = 0;     // f32
+  uintptr_t value = 0;    // f32
+  uintptr_t reward = 0;   // f32
+  uintptr_t done = 0;     // u8
+  // inference graph I/O (fixed addresses)
+  uintptr_t in_obs = 0, in_mask = 0, out_action = 0, out_logp = 0, out_value = 0;
+};
+
+struct EngineStats {
+  int64_t frames = 0;          // env steps taken (all envs)
+  int64_t gpu_steps = 0;       // inference graph launches
+  int64_t slots_full = 0;
+  double driver_idle_s = 0.0;  // driver found nothing to do
+  double slot_wait_s = 0.0;    // groups stalled for a free slot (learner-bound)
+  double env_s = 0.0;          // summed worker time inside env step
+  int64_t publishes = 0;
+};
+
+class GpuEngine {
+ public:
+  GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf);
+  ~GpuEngine();
+  void start(uintptr_t graph_exec);
+  void stop();
+  // Blocks until n full slots are available (or timeout). Returns slot ids.
+  std::vector<int> get_full(int n, double timeout_s);
+  void stream_wait_full(uintptr_t stream, int slot);
+  void release(const std::vector<int>& slots, uintptr_t stream);
+  // Returns false if the previous publish has not been applied yet (skipped).
+  bool publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream);
+  std::vector<EpisodeRecord> drain_episodes() { return log_.drain(); }
+  EngineStats stats() const;
+  uintptr_t stream() const { return (uintptr_t)stream_; }
+  const EngineConfig& config() const { return cfg_; }
+  VecEnv& env() { return *env_; }
+  bool failed() const { return failed_.load(); }
+  std::string error() const;
+
+ private:
+  enum Phase : int { ENV_BUSY = 0, READY = 1, ON_GPU = 2 };
+  struct Group {
+    std::atomic<int> phase{ENV_BUSY};
+    std::atomic<int> next_env{0};
+    std::atomic<int> remaining{0};
+    int cur = -1, prev = -1, t = 0;
+    bool first = true;
+    hipEvent_t ev = nullptr;
+  };
+
+  EngineConfig cfg_;
+  EngineBuffers buf_;
+  int S_;
+  size_t slot_stride_obs_, slot_stride_mask_, slot_stride_act_, slot_stride_scalar_;
+  std::unique_ptr<VecEnv> env_;
+  EpisodeLog log_;
+  hipStream_t stream_ = nullptr;
+  hipGraphExec_t graph_ = nullptr;
+  std::vector<std::unique_ptr<Group>> groups_;
+  // pinned staging, all envs contiguous
+  uint32_t* h_obs_ = nullptr;
+  uint32_t* h_mask_ = nullptr;
+  float* h_reward_ = nullptr;
+  uint8_t* h_done_ = nullptr;
+  uint8_t* h_action_ = nullptr;
+  uint8_t* d_rd_ = nullptr;  // device staging for reward+done of one group
+
+  // slots
+  std::mutex slot_m_;
+  std::condition_variable full_cv_;
+  std::deque<int> free_slots_, full_slots_;
+  std::vector<hipEvent_t> full_ev_, release_ev_;
+  std::vector<bool> release_pending_;
+
+  // publish
+  std::mutex pub_m_;
+  bool pub_pending_ = false;
+  uintptr_t pub_dst_ = 0;
+  size_t pub_n_ = 0;
+  hipEvent_t pub_ready_ = nullptr;     // learner stream: staging filled
+  hipEvent_t pub_consumed_ = nullptr;  // engine stream: staging copied out
+  uint8_t* pub_staging_ = nullptr;
+  size_t pub_staging_n_ = 0;
+
+  // workers
+  std::vector<std::thread> workers_;
+  std::thread driver_;
+  std::mutex work_m_;
+  std::condition_variable work_cv_;
+  std::atomic<uint64_t> work_epoch_{0};
+  std::atomic<bool> running_{false};
+  std::atomic<bool> failed_{false};
+  mutable std::mutex err_m_;
+  std::string err_;
+
+  // stats
+  std::atomic<int64_t> frames_{0}, gpu_steps_{0}, slots_full_{0}, publishes_{0};
+  std::atomic<int64_t> env_ns_{0};
+  double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
+  mutable std::mutex stats_m_;
+
+  void worker_loop(int wid);
+  void driver_loop();
+  bool enqueue_gpu(int g);
+  void dispatch_env(int g);
+  void fail(const std::string& msg);
+  int chunk_;
+};
+
+}  // namespace mb

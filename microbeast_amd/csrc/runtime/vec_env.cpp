@@ -1,0 +1,62 @@
+#include "vec_env.h"
+
+namespace mb {
+
+VecEnv::VecEnv(int size, int n_envs, int max_steps, uint64_t seed, const std::vector<int>& bots,
+               const float* rw, int env_index_base)
+    : size_(size), base_(env_index_base) {
+  for (int i = 0; i < n_envs; ++i) {
+    int bot = bots.empty() ? (int)BOT_COAC : bots[i % bots.size()];
+    sims_.emplace_back(new MicroRTSSim(size, max_steps, bot,
+                                       seed * 1000003ull + (uint64_t)(env_index_base + i), rw));
+  }
+  ep_ret_.assign(n_envs, 0.f);
+  ep_len_.assign(n_envs, 0);
+}
+
+void VecEnv::reset(uint32_t* obs, uint32_t* mask) {
+  const size_t S = (size_t)size_ * size_;
+  for (size_t i = 0; i < sims_.size(); ++i) {
+    sims_[i]->reset();
+    ep_ret_[i] = 0.f;
+    ep_len_[i] = 0;
+    if (obs) sims_[i]->write_obs(obs + i * S);
+    if (mask) sims_[i]->write_mask(mask + i * S * kMaskWords);
+  }
+}
+
+void VecEnv::step_range(int e0, int e1, int base, const uint8_t* actions, uint32_t* obs,
+                        uint32_t* mask, float* reward, uint8_t* done, float* ep_return,
+                        int32_t* ep_step, EpisodeLog* log) {
+  const size_t S = (size_t)size_ * size_;
+  for (int i = e0; i < e1; ++i) {
+    const size_t j = (size_t)(i - base);
+    bool d = false;
+    float r = sims_[i]->step(actions + j * S * kActComps, &d, nullptr);
+    ep_ret_[i] += r;
+    ep_len_[i] += 1;
+    if (ep_return) ep_return[j] = ep_ret_[i];
+    if (ep_step) ep_step[j] = ep_len_[i];
+    if (d) {
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner()});
+      ep_ret_[i] = 0.f;
+      ep_len_[i] = 0;
+    }
+    if (reward) reward[j] = r;
+    if (done) done[j] = d ? 1 : 0;
+    if (obs) sims_[i]->write_obs(obs + j * S);
+    if (mask) sims_[i]->write_mask(mask + j * S * kMaskWords);
+  }
+}
+
+void VecEnv::dense_obs(float* out) const {
+  const size_t S = (size_t)size_ * size_;
+  for (size_t i = 0; i < sims_.size(); ++i) sims_[i]->write_obs_dense(out + i * S * kPlanes);
+}
+
+void VecEnv::dense_mask(uint8_t* out) const {
+  const size_t S = (size_t)size_ * size_;
+  for (size_t i = 0; i < sims_.size(); ++i) sims_[i]->write_mask_dense(out + i * S * kMaskBits);
+}
+
+}  // namespace mb

@@ -1,0 +1,72 @@
+// Vectorised synthetic microRTS env: n independent simulators stepped in one
+// call (the analogue of one MicroRTSGridModeVecEnv instance,
+// reference libs/utils.py:64-75), with episode accounting that the reference
+// did in Python (env_packer.py:55-100) done natively and with correct dtypes
+// (float return, int32 length — fixes the uint8 wrap of env_packer.py:35-37).
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <vector>
+#include "../env/microrts_sim.h"
+
+namespace mb {
+
+struct EpisodeRecord {
+  float ep_return;
+  int32_t ep_step;
+  int32_t env_index;
+  int32_t winner;
+};
+
+class EpisodeLog {
+ public:
+  void push(const EpisodeRecord& r) {
+    std::lock_guard<std::mutex> g(m_);
+    recs_.push_back(r);
+    ++total_;
+  }
+  std::vector<EpisodeRecord> drain() {
+    std::lock_guard<std::mutex> g(m_);
+    std::vector<EpisodeRecord> out;
+    out.swap(recs_);
+    return out;
+  }
+  int64_t total() const { return total_; }
+
+ private:
+  std::mutex m_;
+  std::vector<EpisodeRecord> recs_;
+  int64_t total_ = 0;
+};
+
+class VecEnv {
+ public:
+  VecEnv(int size, int n_envs, int max_steps, uint64_t seed, const std::vector<int>& bots,
+         const float* reward_weight, int env_index_base = 0);
+  int num_envs() const { return (int)sims_.size(); }
+  int size() const { return size_; }
+  // Compact I/O (see microrts_sim.h). Pointers cover all envs, env-major.
+  void reset(uint32_t* obs, uint32_t* mask);
+  // Steps envs [e0, e1). All I/O pointers address env `base` at offset 0, so
+  // callers can pass either whole-vector buffers (base = 0) or group-local
+  // staging (base = first env of the group).
+  void step_range(int e0, int e1, int base, const uint8_t* actions, uint32_t* obs,
+                  uint32_t* mask, float* reward, uint8_t* done, float* ep_return,
+                  int32_t* ep_step, EpisodeLog* log);
+  // Dense reference layout for parity tools: obs f32 (n,s,s,27), mask u8 (n,s*s*78)
+  void dense_obs(float* out) const;
+  void dense_mask(uint8_t* out) const;
+  MicroRTSSim& sim(int i) { return *sims_[i]; }
+  const std::vector<float>& ep_return() const { return ep_ret_; }
+  const std::vector<int32_t>& ep_step() const { return ep_len_; }
+
+ private:
+  int size_;
+  int base_;
+  std::vector<std::unique_ptr<MicroRTSSim>> sims_;
+  std::vector<float> ep_ret_;
+  std::vector<int32_t> ep_len_;
+};
+
+}  // namespace mb

@@ -1,0 +1,103 @@
+"""IMPALA learner step: forward -> V-trace -> backward -> all-reduce -> Adam.
+
+Reference: ``PPO_learn`` (libs/utils.py:223-342) + the learner loop
+(microbeast.py:211-248). Re-designed:
+
+* the batch is time-major ``[T+1, B, ...]`` and stays that way (no
+  reshape scrambling); row t holds obs_t/mask_t with the action
+  a_t sampled there (D3 fixed);
+* one model, one optimizer over a flat fp32 buffer (D1 fixed);
+* the V-trace kernel returns dL/dlogp, dL/dV, dL/dH directly and backward is
+  seeded with them (``autograd.backward`` on three outputs) — no scalar
+  loss graph, no extra reductions;
+* gradients are all-reduced in buckets overlapped with backward (DP);
+* nothing syncs the host inside ``learn`` except the optional loss readout.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass
+
+import torch
+
+from .ops.optim import FlatAdam, FlatParams
+from .ops.vtrace import VTraceWorkspace, vtrace
+from .parallel.dist import DistInfo, GradAllReducer, broadcast_flat
+
+
+@dataclass
+class LearnerHParams:
+    lr: float = 2.5e-4          # microbeast.py:200
+    adam_eps: float = 1e-5      # microbeast.py:200
+    gamma: float = 0.99         # microbeast.py:118 / libs/utils.py:277
+    baseline_cost: float = 0.5  # libs/utils.py:323 (0.5 * mean sq)
+    entropy_cost: float = 0.01  # libs/utils.py:329
+    rho_bar: float = 1.0        # libs/utils.py:293
+    c_bar: float = 1.0          # libs/utils.py:294
+    pg_rho_bar: float = 1.0     # libs/utils.py:316
+    reward_clip: float = 0.0    # reference: none
+    max_grad_norm: float = 0.0  # reference: none
+    bucket_mb: float = 8.0
+
+
+class Learner:
+    def __init__(self, model: torch.nn.Module, hp: LearnerHParams, device: torch.device,
+                 info: DistInfo | None = None):
+        self.model = model.to(device)
+        self.device = device
+        self.hp = hp
+        self.info = info or DistInfo()
+        self.flat = FlatParams(self.model, device)
+        broadcast_flat(self.flat, self.info)
+        self.opt = FlatAdam(self.flat, lr=hp.lr, eps=hp.adam_eps, max_grad_norm=hp.max_grad_norm)
+        self.reducer = GradAllReducer(self.flat, self.info, hp.bucket_mb)
+        self.ws = VTraceWorkspace()
+        self.n_updates = 0
+        self.timing = {}
+
+    def learn(self, batch: dict, sync_timing: bool = False) -> torch.Tensor:
+        """batch keys (time-major): obs [T+1,B,...], mask [T+1,B,S,3] int32,
+        action [T+1,B,S,7] uint8, logp [T+1,B], reward [T+1,B], done [T+1,B].
+        Returns the device tensor [5] = pg, value, entropy, total, mean rho."""
+        t0 = time.perf_counter()
+        obs, mask, action = batch["obs"], batch["mask"], batch["action"]
+        T1, B = batch["logp"].shape[:2]
+        T = T1 - 1
+        self.flat.zero_grad()
+        self.reducer.start_step()
+        flat_obs = obs.reshape(T1 * B, *obs.shape[2:])
+        S = mask.shape[2]
+        m = mask[:T].reshape(T * B, S, mask.shape[-1])
+        a = action[:T].reshape(T * B, S, action.shape[-1])
+        logp, ent, value = self.model.evaluate(flat_obs, m, a, n_score=T * B)
+        vt = vtrace(logp.view(T, B), batch["logp"][:T], value.view(T1, B), batch["reward"][:T],
+                    batch["done"][:T], ent.view(T, B), gamma=self.hp.gamma, rho_bar=self.hp.rho_bar,
+                    c_bar=self.hp.c_bar, pg_rho_bar=self.hp.pg_rho_bar,
+                    baseline_cost=self.hp.baseline_cost, entropy_cost=self.hp.entropy_cost,
+                    reward_clip=self.hp.reward_clip, ws=self.ws)
+        if sync_timing and logp.is_cuda:
+            torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        torch.autograd.backward(
+            [logp, value, ent],
+            [vt.g_logp.reshape(-1), vt.g_value.reshape(-1), torch.full_like(ent, vt.g_ent)])
+        self.reducer.finish()
+        if sync_timing and logp.is_cuda:
+            torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        self.opt.step()
+        if sync_timing and logp.is_cuda:
+            torch.cuda.synchronize()
+        t3 = time.perf_counter()
+        self.n_updates += 1
+        self.timing = {"fwd_s": t1 - t0, "bwd_allreduce_s": t2 - t1, "optim_s": t3 - t2}
+        return vt.losses
+
+    def state_dict(self):
+        return {"model": self.model.state_dict(), "optim": self.opt.state_dict(),
+                "n_updates": self.n_updates}
+
+    def load_state_dict(self, sd):
+        self.model.load_state_dict(sd["model"])
+        self.opt.load_state_dict(sd["optim"])
+        self.n_updates = int(sd.get("n_updates", 0))

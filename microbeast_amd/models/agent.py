@@ -1,0 +1,200 @@
+"""IMPALA-CNN agent with a flat per-cell masked multi-discrete head.
+
+Same architecture, parameter names and initialisation as the reference
+``Agent`` (reference model.py:112-220), so reference state_dicts load 1:1:
+
+* ``network.{0,1,2}``: ConvSequence(conv3x3 -> maxpool(3,2,1) -> 2 residual
+  blocks), channels 16/32/32 (model.py:77-107, 56-73);
+* ``network.5``: Linear(32*ceil(h/8)*ceil(w/8), 256) after Flatten+ReLU,
+  followed by ReLU (model.py:125-133);
+* ``actor``: Linear(256, 78*h*w), orthogonal gain 0 (uniform initial policy);
+  ``critic``: Linear(256, 1), orthogonal gain 1 (model.py:136-137).
+
+Differences that fix reference defects: the encoder runs once per
+call and feeds both heads (D7); device handling is real (D6); learning scores
+actions against the observation they were sampled at (the caller aligns, D3).
+
+Observations may be the compact uint32 bit planes (GPU engine / native env)
+or the reference dense float (N, h, w, 27) layout.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops import cell_head
+from ..ops.obs import bits_to_planes
+
+
+def layer_init(layer: nn.Module, std: float = math.sqrt(2), bias_const: float = 0.0) -> nn.Module:
+    """reference model.py:24-27"""
+    nn.init.orthogonal_(layer.weight, std)
+    nn.init.constant_(layer.bias, bias_const)
+    return layer
+
+
+class ResidualBlock(nn.Module):
+    """x + conv1(relu(conv0(relu(x)))) — reference model.py:56-73."""
+
+    def __init__(self, channels: int):
+        super().__init__()
+        self.conv0 = nn.Conv2d(channels, channels, 3, padding=1)
+        self.conv1 = nn.Conv2d(channels, channels, 3, padding=1)
+
+    def forward(self, x):
+        y = self.conv0(F.relu(x))
+        y = self.conv1(F.relu(y))
+        return x + y
+
+
+class ConvSequence(nn.Module):
+    """conv -> maxpool(3, 2, 1) -> res -> res — reference model.py:77-107."""
+
+    def __init__(self, input_shape, out_channels: int):
+        super().__init__()
+        self._input_shape = tuple(input_shape)
+        self._out_channels = out_channels
+        self.conv = nn.Conv2d(input_shape[0], out_channels, 3, padding=1)
+        self.res_block0 = ResidualBlock(out_channels)
+        self.res_block1 = ResidualBlock(out_channels)
+
+    def forward(self, x):
+        x = self.conv(x)
+        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
+        x = self.res_block0(x)
+        return self.res_block1(x)
+
+    def get_output_shape(self):
+        _c, h, w = self._input_shape
+        return (self._out_channels, (h + 1) // 2, (w + 1) // 2)
+
+
+class Agent(nn.Module):
+    """Reference-compatible constructor: ``Agent(obs_space_shape, nvec, mapsize, device)``.
+
+    ``obs_space_shape`` = (h, w, planes); ``nvec`` = the MultiDiscrete nvec list
+    ([6,4,4,4,4,7,49] * h*w) or None to derive it from the map size.
+    """
+
+    def __init__(self, obs_space_shape=(16, 16, 27), nvec=None, mapsize=None, device="cpu",
+                 channels=(16, 32, 32), hidden=256, compute_dtype=torch.bfloat16):
+        super().__init__()
+        h, w, c = obs_space_shape
+        self.h, self.w, self.planes = h, w, c
+        self.mapsize = mapsize if mapsize is not None else h * w
+        self.nvec = list(nvec) if nvec is not None else list(cell_head.NVEC) * (h * w)
+        assert sum(self.nvec) == cell_head.CELL * h * w, "flat head expects 78 logits per cell"
+        shape = (c, h, w)
+        seqs = []
+        for oc in channels:
+            cs = ConvSequence(shape, oc)
+            shape = cs.get_output_shape()
+            seqs.append(cs)
+        self.network = nn.Sequential(
+            *seqs, nn.Flatten(), nn.ReLU(),
+            nn.Linear(shape[0] * shape[1] * shape[2], hidden), nn.ReLU())
+        self.actor = layer_init(nn.Linear(hidden, sum(self.nvec)), std=0.0)
+        self.critic = layer_init(nn.Linear(hidden, 1), std=1)
+        self.compute_dtype = compute_dtype
+        self.to(device)
+
+    # ------------------------------------------------------------ encoder
+    def _planes(self, obs: torch.Tensor) -> torch.Tensor:
+        if obs.dtype in (torch.int32, torch.uint32):
+            return bits_to_planes(obs.reshape(-1, self.h * self.w), self.h, self.w, torch.float32,
+                                  self.planes)
+        return obs.reshape(-1, self.h, self.w, self.planes).permute(0, 3, 1, 2).float()
+
+    def _autocast(self, t: torch.Tensor):
+        enabled = t.is_cuda and self.compute_dtype in (torch.bfloat16, torch.float16)
+        # no weight-cast cache: each weight is used once per forward, and cached
+        # casts must not leak across hipGraph capture boundaries
+        return torch.autocast("cuda", dtype=self.compute_dtype, enabled=enabled,
+                              cache_enabled=False)
+
+    def features(self, obs: torch.Tensor) -> torch.Tensor:
+        x = self._planes(obs)
+        with self._autocast(x):
+            return self.network(x)
+
+    def policy_value(self, obs: torch.Tensor):
+        f = self.features(obs)
+        with self._autocast(f):
+            logits = self.actor(f)
+            value = self.critic(f)
+        return logits, value.float().view(-1)
+
+    def initial_state(self, batch_size: int = 1):
+        """No recurrent state (reference model.py:139-141)."""
+        return tuple()
+
+    # ------------------------------------------------------------ acting / learning
+    @torch.no_grad()
+    def act(self, obs, mask_bits, rng_state=None, generator=None):
+        """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N])."""
+        logits, value = self.policy_value(obs)
+        action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)
+        return action, logp, value
+
+    def evaluate(self, obs, mask_bits, action, n_score: int | None = None):
+        """Log-prob/entropy of ``action`` (first ``n_score`` rows) and values (all rows).
+
+        Used by the learner on a time-major (T+1)*B batch: values are needed on
+        all T+1 rows (bootstrap), the head only on the first T*B.
+        """
+        f = self.features(obs)
+        with self._autocast(f):
+            value = self.critic(f).float().view(-1)
+            fh = f if n_score is None else f[:n_score]
+            logits = self.actor(fh)
+        logp, ent = cell_head.score(logits, mask_bits, action)
+        return logp, ent, value
+
+    def get_action(self, input_dict: dict, learning: bool = False, inds=(), agent_state=()):
+        """Reference-compatible API (model.py:165-216) on reference-layout inputs.
+
+        input_dict["obs"]: (1,1,n,h,w,27) when acting, (N,h,w,27) when learning;
+        ["action_mask"]: (1,n,78hw) / (N,78hw); ["action"] (N,7hw) when learning.
+        Returns ({action, policy_logits, logprobs, baseline[, entropy]}, ()).
+        """
+        obs = input_dict["obs"]
+        mask = input_dict["action_mask"]
+        if not learning:
+            obs = obs.reshape(-1, self.h, self.w, self.planes)
+            mask = mask.reshape(obs.shape[0], -1)
+        n = obs.shape[0]
+        maskb = mask.reshape(n, self.h * self.w, cell_head.CELL).bool()
+        logits, value = self.policy_value(obs)
+        if learning:
+            a = input_dict["action"].reshape(n, self.h * self.w, cell_head.COMPS)
+            act, logp, ent = cell_head.cell_head_torch(logits.float(), maskb, a)
+            out = dict(action=act.view(n, -1).long(), policy_logits=logits.float(), logprobs=logp,
+                       baseline=value.view(1, -1), entropy=ent)
+        else:
+            with torch.no_grad():
+                act, logp, _ = cell_head.cell_head_torch(logits.float(), maskb, None)
+            out = dict(action=act.view(n, -1).long(), policy_logits=logits.float(),
+                       logprobs=logp, baseline=value.view(1, -1))
+        return out, ()
+
+    def get_value(self, input_dict: dict, agent_state=(), learning=False, inds=()):
+        obs = input_dict["obs"]
+        if not learning:
+            obs = obs.reshape(-1, self.h, self.w, self.planes)
+        return self.policy_value(obs)[1].view(-1, 1)
+
+
+def num_params(model: nn.Module) -> int:
+    return int(sum(p.numel() for p in model.parameters()))
+
+
+def reference_param_count(h: int, w: int) -> int:
+    """Closed form used by tests (matches SURVEY §7.6 counts)."""
+    m = Agent((h, w, 27))
+    return num_params(m)
+
+
+__all__ = ["Agent", "ConvSequence", "ResidualBlock", "layer_init", "num_params"]

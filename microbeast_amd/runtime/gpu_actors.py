@@ -1,0 +1,172 @@
+"""GPU actor runtime: native env workers + batched on-GPU policy inference.
+
+Python side of ``csrc/runtime/engine.cpp``. Replaces the reference's actor
+processes (microbeast.py:30-105, 179-191) and get_batch (libs/utils.py:166-218):
+
+* rollout slots are allocated once in HBM, time-major ``[n_slots, T+1, E, ...]``
+  with compact dtypes (obs uint32 bit planes, mask 3 x uint32 bits, actions
+  uint8) — ~6 KB per 16x16 frame instead of ~170 KB in the reference layout;
+* the policy step (encoder + head + masked sampling) for one env group is
+  captured once into a hipGraph; the C++ driver thread replays it, so acting
+  costs no Python and no GIL;
+* the inference model is a separate parameter copy refreshed by an
+  event-ordered D2D publish after each update (bounded policy lag).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+
+from .. import _native as N
+from ..ops import cell_head
+from ..ops.optim import FlatParams
+
+BOT_IDS = {"coac": 0, "random_biased": 1, "light_rush": 2, "worker_rush": 3, "passive": 4,
+           "random": 5}
+# reference libs/utils.py:69-72: 3x coacAI, randomBiasedAI, lightRushAI, workerRushAI
+DEFAULT_BOTS = ("coac", "coac", "coac", "random_biased", "light_rush", "worker_rush")
+
+
+def available_cpus() -> int:
+    """CPUs this process may use (affinity and cgroup quota aware)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+            if q != "max":
+                n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+class GpuActorRuntime:
+    def __init__(self, make_model, size: int, n_groups: int, envs_per_group: int, unroll: int,
+                 batch_slots: int, device: torch.device, n_threads: int | None = None,
+                 n_slots: int | None = None, max_steps: int = 2000, seed: int = 1,
+                 bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
+                 env_index_base: int = 0):
+        rt = N.runtime()
+        self.device = device
+        self.size, self.S = size, size * size
+        self.G, self.E, self.T = n_groups, envs_per_group, unroll
+        self.batch_slots = batch_slots
+        self.n_slots = n_slots or (2 * n_groups + batch_slots + 1)
+        S, E, T1, NS = self.S, self.E, self.T + 1, self.n_slots
+        dev = device
+        self.rb = {
+            "obs": torch.zeros(NS, T1, E, S, dtype=torch.int32, device=dev),
+            "mask": torch.zeros(NS, T1, E, S, 3, dtype=torch.int32, device=dev),
+            "action": torch.zeros(NS, T1, E, S, 7, dtype=torch.uint8, device=dev),
+            "logp": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
+            "value": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
+            "reward": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
+            "done": torch.zeros(NS, T1, E, dtype=torch.uint8, device=dev),
+        }
+        self.io = {
+            "in_obs": torch.zeros(E, S, dtype=torch.int32, device=dev),
+            "in_mask": torch.zeros(E, S, 3, dtype=torch.int32, device=dev),
+            "out_action": torch.zeros(E, S, 7, dtype=torch.uint8, device=dev),
+            "out_logp": torch.zeros(E, dtype=torch.float32, device=dev),
+            "out_value": torch.zeros(E, dtype=torch.float32, device=dev),
+        }
+        self.rng = torch.tensor([seed * 7919 + env_index_base, 0], dtype=torch.int64, device=dev)
+        self._cell_logp = torch.zeros(E * S, dtype=torch.float32, device=dev)
+        self.infer_model = make_model().to(dev)
+        self.infer_model.eval()
+        self.infer_flat = FlatParams(self.infer_model, dev)
+        self.graph = self._capture()
+        if n_threads is None:
+            n_threads = max(1, min(32, available_cpus() - 3))
+        self.n_threads = n_threads
+        cfg = dict(size=size, n_groups=n_groups, envs_per_group=E, unroll=self.T, n_slots=NS,
+                   n_threads=n_threads, max_steps=max_steps, seed=seed,
+                   bots=[BOT_IDS[b] if isinstance(b, str) else int(b) for b in bots],
+                   reward_weight=list(reward_weight), env_index_base=env_index_base,
+                   device=dev.index if dev.index is not None else torch.cuda.current_device())
+        bufs = {k: v.data_ptr() for k, v in self.rb.items()}
+        bufs.update({k: v.data_ptr() for k, v in self.io.items()})
+        torch.cuda.synchronize()
+        self.engine = rt.GpuEngine(cfg, bufs)
+        self.started = False
+        self.frames_per_slot = E * self.T
+
+    # ------------------------------------------------------------ inference graph
+    def _policy_step(self):
+        io = self.io
+        m = self.infer_model
+        logits, value = m.policy_value(io["in_obs"])
+        cell_head.sample_gpu(logits, io["in_mask"], self.rng, action_out=io["out_action"],
+                             cell_logp=self._cell_logp, logp_out=io["out_logp"])
+        io["out_value"].copy_(value)
+
+    def _capture(self):
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):  # warm up allocator / kernels outside capture
+                self._policy_step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._policy_step()
+        torch.cuda.synchronize()
+        self.rng[1] = 0
+        return g
+
+    # ------------------------------------------------------------ control
+    def start(self, learner_flat: FlatParams | None = None):
+        if learner_flat is not None:
+            self.infer_flat.data.copy_(learner_flat.data)
+            torch.cuda.synchronize()
+        self.engine.start(int(self.graph.raw_cuda_graph_exec()))
+        self.started = True
+
+    def stop(self):
+        if self.started:
+            self.engine.stop()
+            self.started = False
+
+    def check(self):
+        if self.engine.failed():
+            raise RuntimeError(f"GPU actor engine failed: {self.engine.error()}")
+
+    def get_batch(self, n_slots: int | None = None, timeout: float = 600.0):
+        """Block until n full rollout slots exist; return (batch dict, slot ids).
+
+        The learner's current stream is made to wait on the slots' completion
+        events; no host synchronisation with the GPU happens here.
+        """
+        n = n_slots or self.batch_slots
+        slots = self.engine.get_full(n, timeout)
+        self.check()
+        if len(slots) < n:
+            raise TimeoutError(f"no full rollout slot within {timeout}s (engine stats "
+                               f"{self.engine.stats()})")
+        sp = N.stream_ptr()
+        for s in slots:
+            self.engine.stream_wait_full(sp, s)
+        if n == 1:
+            s = slots[0]
+            batch = {k: v[s] for k, v in self.rb.items()}
+        else:
+            batch = {k: torch.cat([v[s] for s in slots], dim=1) for k, v in self.rb.items()}
+        return batch, slots
+
+    def release(self, slots):
+        self.engine.release(list(slots), N.stream_ptr())
+
+    def publish(self, learner_flat: FlatParams) -> bool:
+        return self.engine.publish(learner_flat.data.data_ptr(), self.infer_flat.data.data_ptr(),
+                                   learner_flat.numel * 4, N.stream_ptr())
+
+    def drain_episodes(self):
+        return self.engine.drain_episodes()
+
+    def stats(self):
+        return self.engine.stats()

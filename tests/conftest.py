@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: multi-process / long CPU tests")
+
+
+@pytest.fixture(scope="session")
+def rt():
+    from microbeast_amd import _native as N
+    return N.runtime()
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from microbeast_amd import _native as N
+    N.kernels()  # fail loudly if the HIP library is missing
+    return torch.device("cuda", 0)
