@@ -39,6 +39,7 @@ def parse(argv=None):
     p.add_argument("--batch_slots", type=int, default=2)
     p.add_argument("--threads", type=int, default=0, help="env worker threads per rank (0=auto)")
     p.add_argument("--seed", type=int, default=1)
+    p.add_argument("--verbose", action="store_true", help="per-step progress on stderr")
     p.add_argument("--profile_phases", action="store_true",
                    help="also report per-phase learner timings (adds syncs; not for the headline)")
     return p.parse_args(argv)
@@ -76,8 +77,14 @@ def main(argv=None):
     rt.start(learner.flat)
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
 
+    nstep = [0]
+
     def step():
-        batch, slots = rt.get_batch()
+        batch, slots = rt.get_batch(timeout=120.0)
+        nstep[0] += 1
+        if args.verbose:
+            print(f"[rank {info.rank}] step {nstep[0]} slots {slots} {rt.stats()}",
+                  file=sys.stderr, flush=True)
         losses = learner.learn(batch)
         rt.release(slots)
         rt.publish(learner.flat)
@@ -133,6 +140,9 @@ def main(argv=None):
             },
             "actor_stats": {
                 "env_frames_stepped_per_s_rank0": round((st1["frames"] - st0["frames"]) / el, 1),
+                "env_worker_busy_frac": round((st1["env_s"] - st0["env_s"]) / (el * threads), 3),
+                "gpu_policy_steps_per_s": round((st1["gpu_steps"] - st0["gpu_steps"]) / el, 1),
+                "publishes": st1["publishes"] - st0["publishes"],
                 "slot_wait_s": round(st1["slot_wait_s"] - st0["slot_wait_s"], 3),
                 "driver_idle_s": round(st1["driver_idle_s"] - st0["driver_idle_s"], 3),
             },

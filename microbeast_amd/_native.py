@@ -43,6 +43,14 @@ _SIGS = {
     "mbk_adam": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                  c_float, c_float, c_float, c_int64, c_void_p, c_void_p],
     "mbk_to_bf16": [c_void_p, c_int64, c_void_p, c_void_p],
+    "mbk_conv_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                       c_int, c_int, c_int, c_void_p],
+    "mbk_wgrad_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
+                         c_void_p],
+    "mbk_pool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_conv_pack": [c_void_p, c_int, c_void_p],
 }
 
 
@@ -66,13 +74,24 @@ def kernels():
             _ensure_built()
             lib = ctypes.CDLL(str(_LIB / "libmbk_kernels.so"), mode=ctypes.RTLD_GLOBAL)
             for name, args in _SIGS.items():
-                fn = getattr(lib, name, None)
-                if fn is None:
-                    continue
+                fn = getattr(lib, name)  # a missing symbol is a build error: fail loudly
                 fn.argtypes = args
                 fn.restype = c_int
-            _kern = lib
+            _kern = _Checked(lib)
     return _kern
+
+
+class _Checked:
+    """Only signature-declared launchers are reachable (ctypes' default int
+    conversion would silently truncate 64-bit device pointers)."""
+
+    def __init__(self, lib):
+        self._lib = lib
+
+    def __getattr__(self, name):
+        if name not in _SIGS:
+            raise AttributeError(f"{name}: no ctypes signature declared in _native._SIGS")
+        return getattr(self._lib, name)
 
 
 def runtime():

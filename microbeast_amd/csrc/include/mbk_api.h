@@ -20,6 +20,15 @@ typedef struct {
 // Many independent D2D copies in ONE launch (rollout scatter).
 int mbk_multi_copy(const MbkCopySeg* segs, int n, hipStream_t stream);
 
+typedef struct {
+  const float* w;  // fp32 [cout][cin_real][3][3]
+  void* fwd;       // bf16 packed fwd weights
+  void* bwd;       // bf16 packed dgrad weights (nullable)
+  int cin, cin_real, cout;
+} MbkPackJob;
+
+int mbk_conv_pack(const MbkPackJob* jobs, int n, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,611 @@
+// 3x3 / stride 1 / pad 1 convolutions of the IMPALA encoder on CDNA4 MFMA.
+//
+// Reference: every nn.Conv2d of ConvSequence / Residual_Block (reference
+// model.py:60-61, 83) plus the relu / residual add / max_pool2d around them
+// (model.py:69-73, 97) — 15 convs, 3 pools, 10 relus, 6 adds per forward, each a
+// separate ATen kernel in the reference (and ~170 launches per policy step with
+// MIOpen on ROCm, see profiles/). Here one launch per conv, with everything
+// around it fused:
+//
+//   conv_fwd   : y = [pool3x3s2]( conv(relu?(x)) + bias ) * [mask_src > 0] + [add]
+//                - input either NHWC bf16 (C = 16 | 32) or the env's uint32
+//                  bit-plane observation expanded on the fly (27 planes -> 32 ch)
+//                - implicit GEMM on v_mfma_f32_16x16x32_bf16: M = pixels (whole
+//                  images per workgroup, halo'd NHWC tile in LDS, one
+//                  ds_read_b128 A-fragment per lane), N = Cout, K = 9*Cin;
+//                  all B fragments (weights) live in VGPRs for the launch
+//                - the same kernel is the data-gradient (dgrad) with flipped /
+//                  transposed weights: dx = convT(dy) * (x_pre > 0) + dres
+//   conv_wgrad : dW[co][t][ci] = sum_p dy[p][co] * relu?(x)[p + t][ci]
+//                K = pixels; BOTH operands come from plain NHWC LDS tiles via
+//                ds_read_b64_tr_b16 (CDNA4 transposed LDS read: 4 pixels of one
+//                channel per lane), so no im2col is ever materialised; per-WG
+//                fp32 partials + a deterministic reduce (bias grad included)
+//   pool_bwd   : gather form of max_pool2d(3,2,1) backward (no atomics)
+//   conv_pack  : fp32 [Cout][Cin][3][3] params -> packed bf16 fwd / dgrad layouts
+//
+// Layouts: activations NHWC bf16. Packed fwd weights wf[co][chunk][32] with
+// chunk = tap (Cin 32) or tap pair (Cin 16: k = h*16 + ci for tap 2c+h).
+#include "../include/mbk_api.h"
+#include "common.h"
+
+using namespace mbk;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __hip_bfloat16 bf16;
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float bf2f(bf16 v) { return __bfloat162float(v); }
+__device__ __forceinline__ bf16 f2bf(float v) { return __float2bfloat16(v); }
+
+__device__ __forceinline__ uint32_t relu_bf16x2(uint32_t w) {
+  // bf16 pair: negative (sign bit set) -> +0; NaN propagates as is (never produced)
+  uint32_t lo = (w & 0x8000u) ? 0u : (w & 0xFFFFu);
+  uint32_t hi = (w & 0x80000000u) ? 0u : (w & 0xFFFF0000u);
+  return lo | hi;
+}
+
+union Frag8 {
+  bf16x8 v;
+  uint4 u;
+  s16x4 h[2];
+};
+
+template <int CIN>
+struct Geo {
+  static constexpr int NCH = CIN == 16 ? 5 : 9;  // K chunks of 32
+  static constexpr int PIXB = CIN * 2 + 16;       // padded NHWC pixel stride in LDS (bytes)
+};
+
+struct ConvFwdArgs {
+  const void* x;
+  const bf16* w;
+  const float* bias;
+  const bf16* add;
+  const bf16* mask_src;
+  bf16* y;
+  bf16* y_full;
+  int N, H, W, imgs, relu_in, pool;
+};
+
+// ------------------------------------------------------------------ forward / dgrad
+template <int CIN, int COUT, bool BITS>
+__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NCH = Geo<CIN>::NCH;
+  constexpr int PIXB = BITS ? 4 : Geo<CIN>::PIXB;
+  constexpr int NB = COUT / 16;
+  const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const int img0 = blockIdx.x * a.imgs;
+  const int nimg = min(a.imgs, a.N - img0);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  char* tile = smem;
+  const int tile_bytes = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
+
+  // ---- stage halo'd input tile
+  if (BITS) {
+    const uint32_t* xb = (const uint32_t*)a.x + (size_t)img0 * HW;
+    uint32_t* t32 = (uint32_t*)tile;
+    const int tot = nimg * Hp * Wp;
+    for (int e = tid; e < tot; e += kThreads) {
+      const int im = e / (Hp * Wp), r = e - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
+      const int y = py - 1, x = px - 1;
+      t32[e] = (y >= 0 && y < H && x >= 0 && x < W) ? xb[im * HW + y * W + x] : 0u;
+    }
+  } else {
+    constexpr int CH16 = CIN / 8;  // 16-byte chunks per pixel
+    const uint4* xg = (const uint4*)((const bf16*)a.x + (size_t)img0 * HW * CIN);
+    const int tot = nimg * Hp * Wp * CH16;
+    for (int e = tid; e < tot; e += kThreads) {
+      const int q = e % CH16, pos = e / CH16;
+      const int im = pos / (Hp * Wp), r = pos - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
+      const int y = py - 1, x = px - 1;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (y >= 0 && y < H && x >= 0 && x < W) {
+        v = xg[(im * HW + y * W + x) * CH16 + q];
+        if (a.relu_in) {
+          v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
+          v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
+        }
+      }
+      *(uint4*)(tile + pos * PIXB + q * 16) = v;
+    }
+  }
+
+  // ---- weights -> registers (B fragments): lane holds w[co = nb*16 + lane&15][c][8g..8g+7]
+  Frag8 bw[NCH][NB];
+  {
+    const int g = lane >> 4, col = lane & 15;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const uint4* wp = (const uint4*)(a.w + (size_t)(nb * 16 + col) * NCH * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
+    }
+  }
+  float bias_v[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) bias_v[nb] = a.bias ? a.bias[nb * 16 + (lane & 15)] : 0.f;
+  __syncthreads();
+
+  float* otile = (float*)(smem + tile_bytes);  // pool staging [nimg][H][W][COUT] fp32
+  const int M = nimg * HW;
+  const int nblk = (M + 15) >> 4;
+  const size_t gpix0 = (size_t)img0 * HW;
+  const int g = lane >> 4;
+  for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+    const int m = pb * 16 + (lane & 15);
+    const bool valid = m < M;
+    const int mm = valid ? m : 0;
+    const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
+    const int base_pos = (im * Hp + y) * Wp + x;  // padded position of tap (0,0)
+    f32x4 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      Frag8 av;
+      int tap, ch0;
+      if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
+      else { tap = c; ch0 = 8 * g; }
+      const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
+      const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
+      if (BITS) {
+        const uint32_t bits = ((const uint32_t*)tile)[pos] >> ch0;
+        uint32_t w4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
+                  (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
+        av.u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      } else {
+        av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
+      }
+      if (!valid || (CIN == 16 && tap >= 9)) av.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.v, bw[c][nb].v, acc[nb], 0, 0, 0);
+    }
+    // ---- epilogue: lane holds rows 4g+i (pixels), col lane&15 (channel)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co = nb * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pm = pb * 16 + 4 * g + i;
+        if (pm >= M) continue;
+        float v = acc[nb][i] + bias_v[nb];
+        const size_t gi = (gpix0 + pm) * COUT + co;
+        if (a.mask_src) v = bf2f(a.mask_src[gi]) > 0.f ? v : 0.f;
+        if (a.add) v += bf2f(a.add[gi]);
+        if (a.pool) {
+          // pool over the bf16-rounded values so a recomputed argmax (pool_bwd
+          // reads y_full) sees exactly what the forward compared
+          const bf16 vb = f2bf(v);
+          otile[pm * COUT + co] = bf2f(vb);
+          if (a.y_full) a.y_full[gi] = vb;
+        } else {
+          a.y[gi] = f2bf(v);
+        }
+      }
+    }
+  }
+  if (!a.pool) return;
+  __syncthreads();
+  // ---- max_pool2d(kernel 3, stride 2, pad 1)
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  const int tot = nimg * Ho * Wo * COUT;
+  bf16* yo = a.y + (size_t)img0 * Ho * Wo * COUT;
+  for (int e = tid; e < tot; e += kThreads) {
+    const int co = e % COUT, p = e / COUT;
+    const int im = p / (Ho * Wo), r = p - im * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
+    float mx = -INFINITY;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int yy = 2 * oy - 1 + ky;
+      if (yy < 0 || yy >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int xx = 2 * ox - 1 + kx;
+        if (xx < 0 || xx >= W) continue;
+        mx = fmaxf(mx, otile[((im * H + yy) * W + xx) * COUT + co]);
+      }
+    }
+    yo[e] = f2bf(mx);
+  }
+}
+
+// ------------------------------------------------------------------ weight gradient
+struct ConvWgradArgs {
+  const void* x;
+  const bf16* dy;
+  float* partial;  // [gridDim.x][COUT*9*CIN + COUT]
+  int N, H, W, imgs, relu_in;
+};
+
+__device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
+}
+
+template <int CIN, int COUT, bool BITS>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int XPB = CIN * 2;       // X tile pixel stride (bytes), NHWC bf16
+  constexpr int DPB = COUT * 2;      // dY tile pixel stride
+  constexpr int MB = COUT / 16;
+  constexpr int CB = CIN / 16;
+  constexpr int NBLK = 9 * CB;
+  constexpr int KTOT = 9 * CIN;
+  const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = (lane >> 4), li = lane & 15;
+  // LDS carve: [X tile | zero row (64B) | dY tile | zero row]
+  const int xbytes = ((a.imgs * Hp * Wp * XPB) + 15) & ~15;
+  char* xt = smem;
+  char* xzero = smem + xbytes;
+  char* dt = xzero + 64;
+  const int dbytes = ((a.imgs * HW * DPB) + 15) & ~15;
+  char* dzero = dt + dbytes;
+  float* red = (float*)(dzero + 64);  // [COUT][KTOT] reduction buffer
+
+  for (int e = tid; e < 16; e += kThreads) {
+    ((uint32_t*)xzero)[e] = 0u;
+    ((uint32_t*)dzero)[e] = 0u;
+  }
+  f32x4 acc[MB][NBLK];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < NBLK; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // bias grad: each thread always stages the same 8-channel group of dY
+  constexpr int DCH = COUT / 8;
+  float dbias[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+  const int nrounds = (a.N + a.imgs - 1) / a.imgs;
+  for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
+    const int img0 = rd * a.imgs;
+    const int nimg = min(a.imgs, a.N - img0);
+    __syncthreads();  // previous round's reads done
+    // stage X (relu'd if the forward applied relu to its input), halo'd, NHWC bf16
+    if (BITS) {
+      const uint32_t* xb = (const uint32_t*)a.x + (size_t)img0 * HW;
+      const int tot = nimg * Hp * Wp * 4;  // 4 chunks of 8 channels
+      for (int e = tid; e < tot; e += kThreads) {
+        const int q = e & 3, pos = e >> 2;
+        const int im = pos / (Hp * Wp), r = pos - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
+        const int y = py - 1, x = px - 1;
+        uint32_t bits = (y >= 0 && y < H && x >= 0 && x < W) ? xb[im * HW + y * W + x] : 0u;
+        bits >>= 8 * q;
+        uint32_t w4[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
+                  (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
+        *(uint4*)(xt + pos * XPB + q * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+      }
+    } else {
+      constexpr int CH16 = CIN / 8;
+      const uint4* xg = (const uint4*)((const bf16*)a.x + (size_t)img0 * HW * CIN);
+      const int tot = nimg * Hp * Wp * CH16;
+      for (int e = tid; e < tot; e += kThreads) {
+        const int q = e % CH16, pos = e / CH16;
+        const int im = pos / (Hp * Wp), r = pos - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
+        const int y = py - 1, x = px - 1;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (y >= 0 && y < H && x >= 0 && x < W) {
+          v = xg[(im * HW + y * W + x) * CH16 + q];
+          if (a.relu_in) {
+            v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
+            v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
+          }
+        }
+        *(uint4*)(xt + pos * XPB + q * 16) = v;
+      }
+    }
+    {  // stage dY (dense NHWC) + bias-grad partial sums
+      const uint4* dg = (const uint4*)(a.dy + (size_t)img0 * HW * COUT);
+      const int tot = nimg * HW * DCH;
+      for (int e = tid; e < tot; e += kThreads) {
+        const uint4 v = dg[e];
+        *(uint4*)(dt + e * 16) = v;
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dbias[2 * j] += __uint_as_float(w[j] << 16);
+          dbias[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
+        }
+      }
+    }
+    __syncthreads();
+    const int M = nimg * HW;
+    const int nk = (M + 31) >> 5;
+    for (int kb = wave; kb < nk; kb += kThreads / 64) {
+      // this lane's two pixels (rows q = li>>2 of halves h = 0, 1)
+      const char* dptr[2];
+      int xpos[2];
+      bool ok[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = kb * 32 + 8 * G + 4 * h + (li >> 2);
+        ok[h] = p < M;
+        const int pp = ok[h] ? p : 0;
+        const int im = pp / HW, r = pp - im * HW, y = r / W, x = r - y * W;
+        xpos[h] = (im * Hp + y) * Wp + x;
+        dptr[h] = ok[h] ? dt + pp * DPB : dzero;
+      }
+      Frag8 af[MB];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          af[mb].h[h] = tr_read(dptr[h] + (mb * 16 + 4 * (li & 3)) * 2);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = (t / 3) * Wp + (t % 3);
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          Frag8 bf;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const char* p = ok[h] ? xt + (xpos[h] + off) * XPB : xzero;
+            bf.h[h] = tr_read(p + (cb * 16 + 4 * (li & 3)) * 2);
+          }
+#pragma unroll
+          for (int mb = 0; mb < MB; ++mb)
+            acc[mb][t * CB + cb] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bf.v, acc[mb][t * CB + cb], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // ---- reduce the 4 waves through LDS (sequential adds, no atomics)
+  __syncthreads();
+  for (int w = 0; w < kThreads / 64; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < NBLK; ++nb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            // C layout: row (co) = 4G + i, col (n) = li
+            const int co = mb * 16 + 4 * G + i, n = nb * 16 + li;
+            float* p = red + co * KTOT + n;
+            *p = (w == 0 ? 0.f : *p) + acc[mb][nb][i];
+          }
+    }
+    __syncthreads();
+  }
+  float* out = a.partial + (size_t)blockIdx.x * (COUT * KTOT + COUT);
+  for (int e = tid; e < COUT * KTOT; e += kThreads) out[e] = red[e];
+  // bias grad: thread tid staged channel group (tid % DCH) in every pass
+  __syncthreads();
+  float* bred = red;  // reuse: [kThreads][8]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bred[tid * 8 + j] = dbias[j];
+  __syncthreads();
+  if (tid < COUT) {
+    const int grp = tid / 8, j = tid % 8;
+    float s = 0.f;
+    for (int t = grp; t < kThreads; t += DCH) s += bred[t * 8 + j];
+    out[COUT * KTOT + tid] = s;
+  }
+}
+
+// partial[nparts][COUT*9*CIN + COUT] -> dw[co][ci][ky][kx] (+)=, db[co] (+)=
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial,
+                                                           int nparts, int cin, int cin_real,
+                                                           int cout, float* __restrict__ dw,
+                                                           float* __restrict__ db, int accumulate) {
+  const int ktot = 9 * cin, row = cout * ktot + cout;
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= row) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += partial[(size_t)p * row + e];
+  if (e < cout * ktot) {
+    const int co = e / ktot, r = e - co * ktot, t = r / cin, ci = r - t * cin;
+    if (ci >= cin_real) return;
+    float* d = dw + ((size_t)co * cin_real + ci) * 9 + t;
+    *d = accumulate ? *d + s : s;
+  } else if (db) {
+    const int co = e - cout * ktot;
+    db[co] = accumulate ? db[co] + s : s;
+  }
+}
+
+// ------------------------------------------------------------------ maxpool backward
+// dc[n][y][x][c] = sum of dp over the (<= 4) windows whose first-in-scan-order
+// argmax is (y, x) — matches ATen's max_pool2d index semantics.
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ cfull,
+                                                       const bf16* __restrict__ dp, int N, int H,
+                                                       int W, int C, bf16* __restrict__ dc) {
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  const size_t tot = (size_t)N * H * W * C;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int c = e % C;
+    const size_t p = e / C;
+    const int x = p % W, y = (p / W) % H;
+    const size_t n = p / ((size_t)H * W);
+    float g = 0.f;
+    // windows (oy, ox) with 2*oy-1 <= y <= 2*oy+1
+    const int oy_lo = y / 2, oy_hi = min(Ho - 1, (y + 1) / 2);
+    const int ox_lo = x / 2, ox_hi = min(Wo - 1, (x + 1) / 2);
+    for (int oy = max(0, oy_lo - 1); oy <= oy_hi; ++oy) {
+      if (y < 2 * oy - 1 || y > 2 * oy + 1) continue;
+      for (int ox = max(0, ox_lo - 1); ox <= ox_hi; ++ox) {
+        if (x < 2 * ox - 1 || x > 2 * ox + 1) continue;
+        float mx = -INFINITY;
+        int ay = -1, ax = -1;
+        for (int ky = 0; ky < 3; ++ky) {
+          const int yy = 2 * oy - 1 + ky;
+          if (yy < 0 || yy >= H) continue;
+          for (int kx = 0; kx < 3; ++kx) {
+            const int xx = 2 * ox - 1 + kx;
+            if (xx < 0 || xx >= W) continue;
+            const float v = bf2f(cfull[((n * H + yy) * W + xx) * C + c]);
+            if (v > mx || ay < 0) { mx = v; ay = yy; ax = xx; }
+          }
+        }
+        if (ay == y && ax == x) g += bf2f(dp[((n * Ho + oy) * Wo + ox) * C + c]);
+      }
+    }
+    dc[e] = f2bf(g);
+  }
+}
+
+// ------------------------------------------------------------------ weight packing
+struct PackJob {
+  const float* w;   // [cout][cin_real][3][3]
+  bf16* fwd;        // [cout][nch(cin)][32]
+  bf16* bwd;        // dgrad weights: conv with cin'=cout, cout'=cin -> [cin][nch(cout)][32]
+  int cin, cin_real, cout;
+};
+struct PackJobs {
+  PackJob j[16];
+  int n;
+};
+
+__device__ __forceinline__ int nch_of(int c) { return c == 16 ? 5 : 9; }
+
+__global__ __launch_bounds__(256) void conv_pack_kernel(PackJobs jobs) {
+  const PackJob& J = jobs.j[blockIdx.y];
+  if (blockIdx.y >= jobs.n) return;
+  const int nf = J.cout * nch_of(J.cin) * 32;
+  const int nb = J.bwd ? J.cin * nch_of(J.cout) * 32 : 0;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < nf + nb; e += gridDim.x * blockDim.x) {
+    if (e < nf) {
+      const int co = e / (nch_of(J.cin) * 32), r = e % (nch_of(J.cin) * 32);
+      const int c = r / 32, k = r % 32;
+      int tap, ci;
+      if (J.cin == 16) { tap = 2 * c + k / 16; ci = k % 16; }
+      else { tap = c; ci = k; }
+      float v = 0.f;
+      if (tap < 9 && ci < J.cin_real) v = J.w[((size_t)co * J.cin_real + ci) * 9 + tap];
+      J.fwd[e] = f2bf(v);
+    } else {
+      // dgrad: out channel = original ci, input channel = original co, tap flipped
+      const int f = e - nf;
+      const int ci = f / (nch_of(J.cout) * 32), r = f % (nch_of(J.cout) * 32);
+      const int c = r / 32, k = r % 32;
+      int tap, co;
+      if (J.cout == 16) { tap = 2 * c + k / 16; co = k % 16; }
+      else { tap = c; co = k; }
+      float v = 0.f;
+      if (tap < 9 && ci < J.cin_real) v = J.w[((size_t)co * J.cin_real + ci) * 9 + (8 - tap)];
+      J.bwd[f] = f2bf(v);
+    }
+  }
+}
+
+inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool) {
+  const int pixb = bits ? 4 : cin * 2 + 16;
+  size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
+  if (pool) t += (size_t)imgs * H * W * cout * 4;
+  return t;
+}
+
+inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W) {
+  size_t x = (((size_t)imgs * (H + 2) * (W + 2) * cin * 2) + 15) & ~(size_t)15;
+  size_t d = (((size_t)imgs * H * W * cout * 2) + 15) & ~(size_t)15;
+  size_t red = (size_t)cout * 9 * cin * 4;
+  if (red < (size_t)kThreads * 8 * 4) red = (size_t)kThreads * 8 * 4;
+  return x + 64 + d + 64 + red;
+}
+
+}  // namespace
+
+extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const void* w,
+                            const float* bias, const void* add, const void* mask_src, void* y,
+                            void* y_full, int N, int H, int W, int imgs, int relu_in, int pool,
+                            hipStream_t stream) {
+  ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
+                (bf16*)y_full, N, H, W, imgs, relu_in, pool};
+  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  dim3 grid((N + imgs - 1) / imgs);
+#define LAUNCH(CI, CO, B)                                                                   \
+  do {                                                                                      \
+    auto kfn = conv_fwd_kernel<CI, CO, B>;                                                  \
+    if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
+    hipLaunchKernelGGL(kfn, grid, dim3(kThreads), sm, stream, a);                           \
+  } while (0)
+  if (in_bits) {
+    if (cout == 16) LAUNCH(32, 16, true);
+    else if (cout == 32) LAUNCH(32, 32, true);
+    else return (int)hipErrorInvalidValue;
+  } else if (cin == 16 && cout == 16) LAUNCH(16, 16, false);
+  else if (cin == 16 && cout == 32) LAUNCH(16, 32, false);
+  else if (cin == 32 && cout == 16) LAUNCH(32, 16, false);
+  else if (cin == 32 && cout == 32) LAUNCH(32, 32, false);
+  else return (int)hipErrorInvalidValue;
+#undef LAUNCH
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, const void* dy,
+                              float* partial, int nparts, int N, int H, int W, int imgs,
+                              int relu_in, hipStream_t stream) {
+  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in};
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  dim3 grid(nparts);
+#define LAUNCH(CI, CO, B)                                                                   \
+  do {                                                                                      \
+    auto kfn = conv_wgrad_kernel<CI, CO, B>;                                                \
+    if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
+    hipLaunchKernelGGL(kfn, grid, dim3(kThreads), sm, stream, a);                           \
+  } while (0)
+  if (in_bits) {
+    if (cout == 16) LAUNCH(32, 16, true);
+    else if (cout == 32) LAUNCH(32, 32, true);
+    else return (int)hipErrorInvalidValue;
+  } else if (cin == 16 && cout == 16) LAUNCH(16, 16, false);
+  else if (cin == 16 && cout == 32) LAUNCH(16, 32, false);
+  else if (cin == 32 && cout == 16) LAUNCH(32, 16, false);
+  else if (cin == 32 && cout == 32) LAUNCH(32, 32, false);
+  else return (int)hipErrorInvalidValue;
+#undef LAUNCH
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,
+                                float* dw, float* db, int accumulate, hipStream_t stream) {
+  const int row = cout * 9 * cin + cout;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row + 255) / 256), dim3(256), 0, stream, partial,
+                     nparts, cin, cin_real, cout, dw, db, accumulate);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_pool_bwd(const void* cfull, const void* dp, int N, int H, int W, int C,
+                            void* dc, hipStream_t stream) {
+  const size_t tot = (size_t)N * H * W * C;
+  size_t blocks = (tot + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     (const bf16*)cfull, (const bf16*)dp, N, H, W, C, (bf16*)dc);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_conv_pack(const MbkPackJob* jobs, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n > 16) return (int)hipErrorInvalidValue;
+  PackJobs p;
+  for (int i = 0; i < n; ++i) {
+    p.j[i].w = jobs[i].w;
+    p.j[i].fwd = (bf16*)jobs[i].fwd;
+    p.j[i].bwd = (bf16*)jobs[i].bwd;
+    p.j[i].cin = jobs[i].cin;
+    p.j[i].cin_real = jobs[i].cin_real;
+    p.j[i].cout = jobs[i].cout;
+  }
+  p.n = n;
+  hipLaunchKernelGGL(conv_pack_kernel, dim3(16, n), dim3(256), 0, stream, p);
+  return (int)hipGetLastError();
+}

@@ -26,6 +26,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import cell_head
+from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.obs import bits_to_planes
 
 
@@ -80,8 +81,12 @@ class Agent(nn.Module):
     """
 
     def __init__(self, obs_space_shape=(16, 16, 27), nvec=None, mapsize=None, device="cpu",
-                 channels=(16, 32, 32), hidden=256, compute_dtype=torch.bfloat16):
+                 channels=(16, 32, 32), hidden=256, compute_dtype=torch.bfloat16,
+                 hip_kernels: bool = True):
         super().__init__()
+        self.channels = tuple(channels)
+        self.hip_kernels = hip_kernels
+        self._hip_enc = None
         h, w, c = obs_space_shape
         self.h, self.w, self.planes = h, w, c
         self.mapsize = mapsize if mapsize is not None else h * w
@@ -115,7 +120,25 @@ class Agent(nn.Module):
         return torch.autocast("cuda", dtype=self.compute_dtype, enabled=enabled,
                               cache_enabled=False)
 
+    def _use_hip(self, obs: torch.Tensor) -> bool:
+        return (self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32
+                and all(c in (16, 32) for c in self.channels))
+
     def features(self, obs: torch.Tensor) -> torch.Tensor:
+        if self._use_hip(obs):
+            # conv trunk on the HIP MFMA kernels (NHWC bf16), then the reference's
+            # NCHW flatten order into network.5
+            if self._hip_enc is None or self._hip_enc.packed_fwd.device != obs.device:
+                self._hip_enc = HipEncoder(self.h, self.w, self.planes, self.channels, obs.device)
+            n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
+            y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
+                       encoder_params(self.network, len(self.channels)), torch.is_grad_enabled())
+            f = y.permute(0, 3, 1, 2).reshape(n, -1)
+            nseq = len(self.channels)
+            with self._autocast(f):
+                f = self.network[nseq + 1](f)           # ReLU
+                f = self.network[nseq + 2](f)           # Linear (network.5)
+                return self.network[nseq + 3](f)        # ReLU
         x = self._planes(obs)
         with self._autocast(x):
             return self.network(x)

@@ -1,0 +1,224 @@
+"""IMPALA-CNN conv trunk on the HIP MFMA conv kernels (``conv.hip``).
+
+Reference trunk: 3 x ConvSequence(conv -> maxpool -> res -> res)
+(model.py:77-107, 56-73, 119-123). On device this runs as 15 fused conv
+launches forward (relu / bias / residual / pool / bit-plane input folded in)
+and 12 dgrad + 15 wgrad launches backward, all NHWC bf16 with fp32
+accumulation, plus ONE weight-pack launch per call that converts the fp32
+master parameters into the kernels' packed bf16 layouts.
+
+Saved for backward per stage: the stage input, the full-resolution conv
+output (pool argmax), the pooled output and each residual block's input and
+inner conv output.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import torch
+
+from .. import _native as N
+
+
+@dataclass
+class ConvLayer:
+    cin: int        # kernel input channels (27 -> 32 for the bit-plane input)
+    cin_real: int   # parameter input channels
+    cout: int
+    H: int          # input spatial size
+    W: int
+    bits: bool      # input is the uint32 observation bit planes
+    relu_in: bool
+    pool: bool      # stage conv followed by maxpool(3,2,1)
+    w_off: int = 0  # offsets into the packed buffers (elements)
+    wb_off: int = -1
+
+
+class _Job(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("fwd", ctypes.c_void_p), ("bwd", ctypes.c_void_p),
+                ("cin", ctypes.c_int), ("cin_real", ctypes.c_int), ("cout", ctypes.c_int)]
+
+
+def _nch(c: int) -> int:
+    return 5 if c == 16 else 9
+
+
+def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool) -> int:
+    hw = layer.H * layer.W
+    imgs = max(1, 256 // hw)
+    while imgs > 1:
+        pixb = 4 if bits else cin * 2 + 16
+        sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * cout * 4 if pool else 0)
+        if sm <= 48 * 1024:
+            break
+        imgs //= 2
+    return imgs
+
+
+def _imgs_wgrad(layer: ConvLayer) -> int:
+    per = (layer.H + 2) * (layer.W + 2) * layer.cin * 2 + layer.H * layer.W * layer.cout * 2
+    return max(1, min(64, (56 * 1024) // per))
+
+
+class HipEncoder:
+    """Owns layer geometry, packed-weight buffers and backward workspace."""
+
+    def __init__(self, h: int, w: int, planes: int, channels=(16, 32, 32), device=None):
+        assert planes <= 32, "bit-plane observations carry at most 32 planes"
+        self.layers: list[ConvLayer] = []
+        H, W, cin, cin_real, bits = h, w, 32, planes, True
+        for co in channels:
+            self.layers.append(ConvLayer(cin, cin_real, co, H, W, bits, False, True))
+            H, W = (H + 1) // 2, (W + 1) // 2
+            for _ in range(4):
+                self.layers.append(ConvLayer(co, co, co, H, W, False, True, False))
+            cin, cin_real, bits = co, co, False
+        self.out_hw = (H, W)
+        self.out_c = channels[-1]
+        off = boff = 0
+        for i, L in enumerate(self.layers):
+            L.w_off = off
+            off += L.cout * _nch(L.cin) * 32
+            if i > 0:  # the observation layer needs no input gradient
+                L.wb_off = boff
+                boff += L.cin * _nch(L.cout) * 32
+        self.packed_fwd = torch.zeros(off, dtype=torch.bfloat16, device=device)
+        self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
+        self._partial = None
+
+    # ------------------------------------------------------------ helpers
+    def pack(self, weights: list[torch.Tensor], with_bwd: bool) -> None:
+        k = N.kernels()
+        jobs = (_Job * len(self.layers))()
+        for i, (L, wt) in enumerate(zip(self.layers, weights)):
+            assert wt.dtype == torch.float32 and wt.is_contiguous()
+            bwd = (self.packed_bwd.data_ptr() + 2 * L.wb_off) if (with_bwd and L.wb_off >= 0) else None
+            jobs[i] = _Job(wt.data_ptr(), self.packed_fwd.data_ptr() + 2 * L.w_off, bwd, L.cin,
+                           L.cin_real, L.cout)
+        N.check(k.mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), len(self.layers),
+                                N.stream_ptr()), "conv_pack")
+
+    def _fwd(self, L: ConvLayer, x, bias, add=None, mask_src=None, y_full=None, dgrad=False):
+        n = x.shape[0]
+        if dgrad:
+            # data gradient = conv with flipped/transposed weights at the layer's input size
+            cin, cout, w = L.cout, L.cin, self.packed_bwd.data_ptr() + 2 * L.wb_off
+            H, W = L.H, L.W
+            bits, relu, pool = False, False, False
+        else:
+            cin, cout, w = L.cin, L.cout, self.packed_fwd.data_ptr() + 2 * L.w_off
+            H, W, bits, relu, pool = L.H, L.W, L.bits, L.relu_in, L.pool
+        Ho, Wo = ((H + 1) // 2, (W + 1) // 2) if pool else (H, W)
+        y = torch.empty(n, Ho, Wo, cout, dtype=torch.bfloat16, device=x.device)
+        imgs = _imgs_fwd(L, cin, cout, bits, pool)
+        N.check(N.kernels().mbk_conv_fwd(
+            x.data_ptr(), int(bits), cin, cout, w, N.ptr(bias), N.ptr(add), N.ptr(mask_src),
+            y.data_ptr(), N.ptr(y_full), n, H, W, imgs, int(relu), int(pool), N.stream_ptr()),
+            "conv_fwd")
+        return y
+
+    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor):
+        n = x.shape[0]
+        imgs = _imgs_wgrad(L)
+        nparts = max(1, min(1024, (n + imgs - 1) // imgs))
+        row = L.cout * 9 * L.cin + L.cout
+        need = nparts * row
+        if self._partial is None or self._partial.numel() < need or self._partial.device != dy.device:
+            self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=dy.device)
+        k = N.kernels()
+        st = N.stream_ptr()
+        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, dy.data_ptr(),
+                                 self._partial.data_ptr(), nparts, n, L.H, L.W, imgs,
+                                 int(L.relu_in), st), "conv_wgrad")
+        N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
+                                   dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
+
+    # ------------------------------------------------------------ passes
+    def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool):
+        """params: [w0, b0, w1, b1, ...] fp32 in layer order. Returns (out NHWC bf16, saved)."""
+        ws, bs = params[0::2], params[1::2]
+        self.pack([w.detach() for w in ws], with_bwd=save)
+        x = obs_bits.contiguous()
+        saved = []
+        li = 0
+        n = x.shape[0]
+        for _stage in range(len(self.layers) // 5):
+            L = self.layers[li]
+            cfull = (torch.empty(n, L.H, L.W, L.cout, dtype=torch.bfloat16, device=x.device)
+                     if save else None)
+            p = self._fwd(L, x, bs[li].detach(), y_full=cfull)
+            u0 = self._fwd(self.layers[li + 1], p, bs[li + 1].detach())
+            y0 = self._fwd(self.layers[li + 2], u0, bs[li + 2].detach(), add=p)
+            u1 = self._fwd(self.layers[li + 3], y0, bs[li + 3].detach())
+            y1 = self._fwd(self.layers[li + 4], u1, bs[li + 4].detach(), add=y0)
+            if save:
+                saved += [x, cfull, p, u0, y0, u1]
+            x = y1
+            li += 5
+        return x, saved
+
+    def backward(self, g: torch.Tensor, saved: list[torch.Tensor], params: list[torch.Tensor]):
+        grads = [torch.empty_like(p) for p in params]
+        nst = len(self.layers) // 5
+        g = g.contiguous()
+        for s in range(nst - 1, -1, -1):
+            li = 5 * s
+            x, cfull, p, u0, y0, u1 = saved[6 * s:6 * s + 6]
+            L = self.layers
+            # res block 1: y1 = y0 + conv4(relu(u1)), u1 = conv3(relu(y0))
+            self._wgrad(L[li + 4], u1, g, grads[2 * (li + 4)], grads[2 * (li + 4) + 1])
+            du1 = self._fwd(L[li + 4], g, None, mask_src=u1, dgrad=True)
+            self._wgrad(L[li + 3], y0, du1, grads[2 * (li + 3)], grads[2 * (li + 3) + 1])
+            dy0 = self._fwd(L[li + 3], du1, None, mask_src=y0, add=g, dgrad=True)
+            # res block 0
+            self._wgrad(L[li + 2], u0, dy0, grads[2 * (li + 2)], grads[2 * (li + 2) + 1])
+            du0 = self._fwd(L[li + 2], dy0, None, mask_src=u0, dgrad=True)
+            self._wgrad(L[li + 1], p, du0, grads[2 * (li + 1)], grads[2 * (li + 1) + 1])
+            dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
+            # maxpool + stage conv
+            Ls = L[li]
+            dc = torch.empty_like(cfull)
+            N.check(N.kernels().mbk_pool_bwd(cfull.data_ptr(), dp.data_ptr(), cfull.shape[0],
+                                             Ls.H, Ls.W, Ls.cout, dc.data_ptr(), N.stream_ptr()),
+                    "pool_bwd")
+            self._wgrad(Ls, x, dc, grads[2 * li], grads[2 * li + 1])
+            g = self._fwd(Ls, dc, None, dgrad=True) if s > 0 else None
+        return grads
+
+
+class _EncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, obs_bits, enc: HipEncoder, *params):
+        out, saved = enc.forward(obs_bits, list(params), save=True)
+        ctx.enc = enc
+        ctx.nsaved = len(saved)
+        ctx.save_for_backward(*saved, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        t = ctx.saved_tensors
+        saved, params = list(t[:ctx.nsaved]), list(t[ctx.nsaved:])
+        grads = ctx.enc.backward(g.to(torch.bfloat16), saved, params)
+        return (None, None, *grads)
+
+
+def encoder_params(network: torch.nn.Sequential, n_stages: int) -> list[torch.nn.Parameter]:
+    """[w, b] per conv in HipEncoder layer order from a reference-named ``network``."""
+    out = []
+    for s in range(n_stages):
+        cs = network[s]
+        for conv in (cs.conv, cs.res_block0.conv0, cs.res_block0.conv1, cs.res_block1.conv0,
+                     cs.res_block1.conv1):
+            out += [conv.weight, conv.bias]
+    return out
+
+
+def encode(obs_bits: torch.Tensor, enc: HipEncoder, params: list[torch.Tensor],
+           need_grad: bool) -> torch.Tensor:
+    """NHWC bf16 trunk output [N, Ho, Wo, C]."""
+    if need_grad:
+        return _EncoderFn.apply(obs_bits, enc, *params)
+    with torch.no_grad():
+        return enc.forward(obs_bits, [p.detach() for p in params], save=False)[0]

@@ -1,0 +1,161 @@
+"""MFMA conv trunk (conv.hip) vs the plain PyTorch fp32 reference network."""
+import copy
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _random_obs_bits(n, S, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    groups = [(0, 5), (5, 5), (10, 3), (13, 8), (21, 6)]
+    bits = torch.zeros(n, S, dtype=torch.int64)
+    for off, k in groups:
+        idx = torch.randint(0, k, (n, S), generator=g)
+        bits |= (1 << (off + idx))
+    return bits.to(torch.int32)
+
+
+def _rel(a, b):
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def test_single_conv_layers_exact_structure(cuda):
+    """One residual conv with relu-in + residual add, and one stage conv + pool, vs torch on
+    bf16-rounded inputs (isolates indexing bugs from accumulated bf16 drift)."""
+    from microbeast_amd.ops.encoder import HipEncoder
+    torch.manual_seed(1)
+    enc = HipEncoder(16, 16, 27, (16, 32, 32), cuda)
+    L1 = enc.layers[1]  # 16->16 @ 8x8, relu_in
+    w = torch.randn(16, 16, 3, 3) * 0.2
+    b = torch.randn(16) * 0.1
+    ws = [torch.randn(L.cout, L.cin_real, 3, 3) * 0.1 for L in enc.layers]
+    ws[1] = w
+    enc.pack([t.to(cuda).contiguous() for t in ws], with_bwd=True)
+    x = torch.randn(5, 8, 8, 16).bfloat16()
+    add = torch.randn(5, 8, 8, 16).bfloat16()
+    y = enc._fwd(L1, x.to(cuda), b.to(cuda), add=add.to(cuda))
+    xr = F.relu(x.float()).permute(0, 3, 1, 2)
+    yr = F.conv2d(xr, w.bfloat16().float(), b, padding=1).permute(0, 2, 3, 1) + add.float()
+    torch.testing.assert_close(y.float().cpu(), yr, rtol=2e-2, atol=2e-2)
+    # dgrad of that conv: d = convT(dy) * (x > 0) + add
+    dy = torch.randn(5, 8, 8, 16).bfloat16()
+    d = enc._fwd(L1, dy.to(cuda), None, mask_src=x.to(cuda), add=add.to(cuda), dgrad=True)
+    xt = xr.clone().requires_grad_(True)
+    out = F.conv2d(xt, w.bfloat16().float(), None, padding=1)
+    out.backward(dy.float().permute(0, 3, 1, 2))
+    dr = xt.grad.permute(0, 2, 3, 1) * (x.float() > 0) + add.float()
+    torch.testing.assert_close(d.float().cpu(), dr, rtol=2e-2, atol=3e-2)
+    # wgrad of that conv
+    dw = torch.zeros(16, 16, 3, 3, device=cuda)
+    db = torch.zeros(16, device=cuda)
+    enc._wgrad(L1, x.to(cuda), dy.to(cuda), dw, db)
+    wt = w.bfloat16().float().clone().requires_grad_(True)
+    bt = torch.zeros(16, requires_grad=True)
+    F.conv2d(xr, wt, bt, padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dw.cpu(), wt.grad, rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(db.cpu(), bt.grad, rtol=1e-2, atol=2e-2)
+    # stage conv from bit planes + fused maxpool
+    L0 = enc.layers[0]
+    obs = _random_obs_bits(3, 256, seed=5)
+    cfull = torch.empty(3, 16, 16, 16, dtype=torch.bfloat16, device=cuda)
+    b0 = torch.randn(16) * 0.1
+    p = enc._fwd(L0, obs.to(cuda), b0.to(cuda), y_full=cfull)
+    from microbeast_amd.ops.obs import bits_to_planes
+    planes = bits_to_planes(obs, 16, 16)
+    cr = F.conv2d(planes, ws[0].bfloat16().float(), b0, padding=1)
+    torch.testing.assert_close(cfull.float().cpu().permute(0, 3, 1, 2), cr, rtol=2e-2, atol=2e-2)
+    pr = F.max_pool2d(cfull.float().cpu().permute(0, 3, 1, 2), 3, 2, 1)
+    torch.testing.assert_close(p.float().cpu().permute(0, 3, 1, 2), pr, rtol=0, atol=0)
+
+
+def test_pool_bwd_and_l0_wgrad(cuda):
+    from microbeast_amd import _native as N
+    from microbeast_amd.ops.encoder import HipEncoder
+    from microbeast_amd.ops.obs import bits_to_planes
+    torch.manual_seed(2)
+    # pool backward vs autograd of max_pool2d on the same bf16 values
+    c = torch.randn(3, 16, 16, 16).bfloat16()
+    dp = torch.randn(3, 8, 8, 16).bfloat16()
+    dc = torch.empty_like(c).to(cuda)
+    cg, dpg = c.to(cuda), dp.to(cuda)  # keep the device copies alive across the launch
+    N.check(N.kernels().mbk_pool_bwd(cg.data_ptr(), dpg.data_ptr(), 3, 16, 16, 16,
+                                     dc.data_ptr(), N.stream_ptr()), "pool_bwd")
+    torch.cuda.synchronize()
+    ct = c.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    F.max_pool2d(ct, 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
+    # wgrad of the bit-plane input layer
+    enc = HipEncoder(16, 16, 27, (16, 32, 32), cuda)
+    L0 = enc.layers[0]
+    obs = _random_obs_bits(4, 256, seed=7)
+    dy = torch.randn(4, 16, 16, 16).bfloat16()
+    dw = torch.zeros(16, 27, 3, 3, device=cuda)
+    db = torch.zeros(16, device=cuda)
+    enc._wgrad(L0, obs.to(cuda), dy.to(cuda), dw, db)
+    planes = bits_to_planes(obs, 16, 16)
+    wt = torch.zeros(16, 27, 3, 3, requires_grad=True)
+    bt = torch.zeros(16, requires_grad=True)
+    F.conv2d(planes, wt, bt, padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dw.cpu(), wt.grad, rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(db.cpu(), bt.grad, rtol=1e-2, atol=2e-2)
+
+
+def _bf(t):
+    return t.bfloat16().float()
+
+
+class _RoundBF16(torch.autograd.Function):
+    """Forward: round to bf16 (what the HIP trunk stores); backward: round the gradient too."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return _bf(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bf(g)
+
+
+def _ref_trunk(net, planes, nst):
+    """fp32 torch trunk that rounds activations / weights to bf16 where the kernels do."""
+    R = _RoundBF16.apply
+    x = planes
+    for s in range(nst):
+        cs = net[s]
+        c = R(F.conv2d(x, R(cs.conv.weight), cs.conv.bias, padding=1))
+        x = F.max_pool2d(c, 3, 2, 1)
+        for rb in (cs.res_block0, cs.res_block1):
+            u = R(F.conv2d(F.relu(x), R(rb.conv0.weight), rb.conv0.bias, padding=1))
+            x = R(x + F.conv2d(F.relu(u), R(rb.conv1.weight), rb.conv1.bias, padding=1))
+    return x
+
+
+@pytest.mark.parametrize("s", [16, 10, 8])
+def test_encoder_fwd_bwd_matches_torch(cuda, s):
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    from microbeast_amd.ops.obs import bits_to_planes
+    torch.manual_seed(0)
+    m = Agent((s, s, 27)).to(cuda)
+    ref = copy.deepcopy(m).cpu().float()
+    n = 12
+    obs = _random_obs_bits(n, s * s)
+    m.features(obs.to(cuda))  # builds the encoder
+    params = encoder_params(m.network, 3)
+    y = encode(obs.to(cuda), m._hip_enc, params, True).float()       # NHWC
+    yr = _ref_trunk(ref.network, bits_to_planes(obs, s, s), 3).permute(0, 2, 3, 1)
+    assert _rel(y.cpu(), yr) < 1e-2, _rel(y.cpu(), yr)
+    r = torch.randn_like(yr)
+    (y * r.to(cuda)).sum().backward()
+    (yr * r).sum().backward()
+    errs = {}
+    for (name, p), (_, q) in zip(m.named_parameters(), ref.named_parameters()):
+        if not name.startswith("network") or name.startswith("network.5"):
+            continue
+        assert p.grad is not None, name
+        errs[name] = _rel(p.grad.cpu(), q.grad)
+    print(s, max(errs.values()), errs)
+    assert max(errs.values()) < 4e-2, errs
