@@ -1,0 +1,137 @@
+"""Configuration + CLI.
+
+Reference CLI (parser.py:1-15): ``--test`` (flag, or ``--test true/false``)
+and ``--exp_name`` (default "No_name", interactive prompt when omitted,
+microbeast.py:123-124). Everything the reference hard-codes in ``train()``
+(microbeast.py:113-121), ``create_env`` (libs/utils.py:64-75) and
+``PPO_learn`` (libs/utils.py:277-329) is a flag here, defaulting to the
+reference value. ``strtobool`` is implemented (the reference used it without
+importing it, so ``--test true`` crashed there).
+"""
+from __future__ import annotations
+
+import argparse
+import dataclasses
+import sys
+from dataclasses import dataclass, field
+
+
+def strtobool(v: str) -> bool:
+    s = str(v).strip().lower()
+    if s in ("y", "yes", "t", "true", "on", "1"):
+        return True
+    if s in ("n", "no", "f", "false", "off", "0"):
+        return False
+    raise argparse.ArgumentTypeError(f"invalid truth value {v!r}")
+
+
+@dataclass
+class Flags:
+    # --- reference CLI
+    exp_name: str = "No_name"
+    test: bool = False
+    # --- run shape (reference microbeast.py:113-121)
+    n_actors: int = 10
+    n_envs: int = 6
+    env_size: int = 8
+    unroll_length: int = 64
+    batch_size: int = 2
+    n_buffers: int = 0            # 0 -> max(2 * n_actors, batch_size)
+    total_steps: int = 100_000_000
+    max_episode_steps: int = 2000
+    # --- algorithm (libs/utils.py:277-329, microbeast.py:200)
+    gamma: float = 0.99
+    lr: float = 2.5e-4
+    adam_eps: float = 1e-5
+    baseline_cost: float = 0.5
+    entropy_cost: float = 0.01
+    rho_bar: float = 1.0
+    c_bar: float = 1.0
+    pg_rho_bar: float = 1.0
+    reward_clip: float = 0.0
+    max_grad_norm: float = 0.0
+    # --- environment
+    env: str = "synthetic"        # synthetic | microrts (gym-microrts adapter, if installed)
+    opponents: str = "coac,coac,coac,random_biased,light_rush,worker_rush"
+    reward_weight: str = "10,1,1,0.2,1,4"
+    self_play: bool = False       # league of past checkpoints as opponents
+    league_size: int = 4
+    league_update_every: int = 50
+    # --- model
+    arch: str = "impala_flat"     # impala_flat | gridnet | impala_deep
+    channels: str = "16,32,32"
+    hidden: int = 256
+    dtype: str = "bf16"           # fp32 | bf16
+    # --- runtime
+    runtime: str = "auto"         # auto | gpu (native engine) | mono (CPU actor processes)
+    device: str = "auto"          # auto | cpu | cuda
+    groups: int = 2               # gpu runtime: env groups pipelined through the GPU
+    envs_per_group: int = 256
+    actor_threads: int = 0        # gpu runtime: native env worker threads (0 = auto)
+    seed: int = 1
+    nproc_per_node: int = 1       # informative; launch with torchrun for DP
+    bucket_mb: float = 8.0
+    # --- io / robustness
+    savedir: str = "."
+    checkpoint_every: int = 100   # updates
+    resume: bool = False
+    checkpoint: str = ""          # path for --test / --resume (default <savedir>/<exp>.ckpt)
+    eval_episodes: int = 10
+    batch_timeout: float = 600.0
+    actor_restarts: int = 3       # watchdog: respawn a dead actor at most this often
+    fault_inject_every: int = 0   # kill an actor every N updates (tests the watchdog)
+    log_every: int = 1
+    quiet: bool = False
+    max_updates: int = 0          # stop after N updates (0 = until total_steps)
+
+    def resolved_n_buffers(self) -> int:
+        return self.n_buffers or max(2 * self.n_actors, self.batch_size)
+
+    def opponent_list(self) -> list[str]:
+        return [s.strip() for s in self.opponents.split(",") if s.strip()]
+
+    def reward_weights(self) -> list[float]:
+        return [float(x) for x in self.reward_weight.split(",")]
+
+    def channel_list(self) -> tuple[int, ...]:
+        return tuple(int(x) for x in self.channels.split(","))
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(
+        prog="microbeast",
+        description="microbeast_amd: MI355X-native IMPALA for (synthetic) gym-microRTS")
+    p.add_argument("--test", type=strtobool, default=False, nargs="?", const=True,
+                   help="evaluate a saved model instead of training")
+    p.add_argument("--exp_name", type=str, default="No_name", nargs="?",
+                   help="name of the result tables of this experiment")
+    for f in dataclasses.fields(Flags):
+        if f.name in ("test", "exp_name"):
+            continue
+        flag = "--" + f.name
+        if f.type in ("bool", bool):
+            p.add_argument(flag, type=strtobool, default=f.default, nargs="?", const=True)
+        elif f.type in ("int", int):
+            p.add_argument(flag, type=int, default=f.default)
+        elif f.type in ("float", float):
+            p.add_argument(flag, type=float, default=f.default)
+        else:
+            p.add_argument(flag, type=str, default=f.default)
+    return p
+
+
+def parse_flags(argv=None, interactive: bool | None = None) -> Flags:
+    ns = build_parser().parse_args(argv)
+    flags = Flags(**vars(ns))
+    if interactive is None:
+        interactive = sys.stdin is not None and sys.stdin.isatty()
+    if flags.exp_name in (None, "No_name") and interactive and not flags.test:
+        name = input("Nombre del experimento:").strip()  # reference microbeast.py:124
+        if name:
+            flags.exp_name = name
+    if flags.exp_name is None:
+        flags.exp_name = "No_name"
+    return flags
+
+
+__all__ = ["Flags", "build_parser", "parse_flags", "strtobool", "field"]

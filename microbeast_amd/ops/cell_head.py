@@ -165,3 +165,13 @@ def sample(logits: torch.Tensor, mask_bits: torch.Tensor, rng_state: torch.Tenso
     with torch.no_grad():
         a, lp, _ = cell_head_torch(logits, mask_bits, None, generator)
     return a, lp
+
+
+def greedy(logits: torch.Tensor, mask_bits: torch.Tensor) -> torch.Tensor:
+    """Arg-max action per component under the mask (evaluation), uint8 [N,S,7]."""
+    n = logits.shape[0]
+    z = logits.float().view(n, -1, CELL)
+    mask = unpack_mask(mask_bits).view(n, -1, CELL)
+    zm = torch.where(mask, z, torch.full_like(z, MASK_FILL))
+    return torch.stack([zm[..., OFFS[k]:OFFS[k + 1]].argmax(-1) for k in range(COMPS)],
+                       -1).to(torch.uint8)

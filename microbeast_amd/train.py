@@ -1,0 +1,141 @@
+"""Training orchestration (reference ``train()`` + ``batch_and_learn``,
+microbeast.py:109-264), one process per GPU.
+
+Runtimes:
+* ``gpu``  — native env workers + on-GPU batched policy inference + HBM
+  rollout slots (runtime/gpu_actors.py); the flagship throughput path;
+* ``mono`` — CPU actor processes with shared-memory buffers
+  (runtime/mono.py); the reference shape, CPU-only capable (config 1).
+
+Data parallelism: launch with torchrun; each rank owns its actors, the
+learners all-reduce gradients (parallel/dist.py); rank 0 writes the CSVs and
+checkpoints. The reference's learner loop never terminated (while-True spin,
+microbeast.py:262-263); this one stops at ``total_steps`` / ``max_updates``,
+checkpoints and shuts its actors down.
+"""
+from __future__ import annotations
+
+import os
+import time
+
+import torch
+
+from .config import Flags
+from .learner import Learner, LearnerHParams
+from .models.factory import make_model
+from .parallel import dist as D
+from .utils.checkpoint import load_checkpoint, restore, save_checkpoint
+from .utils.metrics import CsvLogger
+
+
+def _hparams(flags: Flags) -> LearnerHParams:
+    return LearnerHParams(lr=flags.lr, adam_eps=flags.adam_eps, gamma=flags.gamma,
+                          baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost,
+                          rho_bar=flags.rho_bar, c_bar=flags.c_bar, pg_rho_bar=flags.pg_rho_bar,
+                          reward_clip=flags.reward_clip, max_grad_norm=flags.max_grad_norm,
+                          bucket_mb=flags.bucket_mb)
+
+
+def checkpoint_path(flags: Flags) -> str:
+    return flags.checkpoint or os.path.join(flags.savedir, f"{flags.exp_name}.ckpt")
+
+
+def _gather_episodes(recs, info):
+    if not info.enabled:
+        return recs
+    out = [None] * info.world_size
+    torch.distributed.all_gather_object(out, recs)
+    return [r for part in out for r in (part or [])] if info.is_main else []
+
+
+def train(flags: Flags) -> dict:
+    want_cuda = flags.device == "cuda" or (flags.device == "auto" and torch.cuda.is_available())
+    info = D.init_distributed(use_cuda=want_cuda)
+    dev = torch.device("cuda", info.local_rank) if want_cuda else torch.device("cpu")
+    runtime = flags.runtime if flags.runtime != "auto" else ("gpu" if want_cuda else "mono")
+    if runtime == "gpu" and not want_cuda:
+        raise RuntimeError("--runtime gpu needs a GPU")
+    torch.manual_seed(flags.seed + info.rank)
+    log = (lambda *a: None) if (flags.quiet or not info.is_main) else (lambda *a: print(*a, flush=True))
+    log(f"[microbeast_amd] exp={flags.exp_name} runtime={runtime} device={dev} "
+        f"world={info.world_size} map={flags.env_size}x{flags.env_size} arch={flags.arch}")
+
+    model = make_model(flags, dev)
+    learner = Learner(model, _hparams(flags), dev, info)
+    step = n_update = 0
+    ck_path = checkpoint_path(flags)
+    if flags.resume and os.path.exists(ck_path):
+        ck = load_checkpoint(ck_path)
+        step, n_update = restore(ck, learner.model, learner.opt)
+        learner.n_updates = n_update
+        log(f"[microbeast_amd] resumed {ck_path} at step={step} update={n_update}")
+    logger = CsvLogger(flags.savedir, flags.exp_name, enabled=info.is_main, append=flags.resume)
+
+    if runtime == "gpu":
+        from .runtime.gpu_actors import GpuActorRuntime
+
+        envs_total = flags.groups * flags.envs_per_group
+        rt = GpuActorRuntime(lambda: make_model(flags, "cpu"), flags.env_size, flags.groups,
+                             flags.envs_per_group, flags.unroll_length, flags.batch_size, dev,
+                             n_threads=flags.actor_threads or None,
+                             max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
+                             bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
+                             env_index_base=info.rank * envs_total)
+        rt.start(learner.flat)
+        frames_per_update = flags.batch_size * flags.envs_per_group * flags.unroll_length
+    else:
+        from .runtime.mono import MonoRuntime
+
+        rt = MonoRuntime(flags, learner.flat.numel)
+        rt.publish(learner.flat.data)
+        rt.start()
+        frames_per_update = flags.batch_size * flags.n_envs * flags.unroll_length
+    frames_per_update *= info.world_size
+
+    t_start = time.perf_counter()
+    last = {}
+    try:
+        while step < flags.total_steps and (flags.max_updates <= 0 or n_update < flags.max_updates):
+            t0 = time.perf_counter()
+            if runtime == "gpu":
+                batch, slots = rt.get_batch(timeout=flags.batch_timeout)
+            else:
+                batch, slots = rt.get_batch(flags.batch_timeout)
+                batch = {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
+            t1 = time.perf_counter()
+            losses = learner.learn(batch)
+            if runtime == "gpu":
+                rt.release(slots)
+                rt.publish(learner.flat)
+            else:
+                rt.publish(learner.flat.data)
+            step += frames_per_update
+            n_update += 1
+            if flags.fault_inject_every and runtime == "mono" and n_update % flags.fault_inject_every == 0:
+                rt.kill_random_actor()
+            if n_update % flags.log_every == 0:
+                lv = D.all_reduce_mean(losses.detach().clone(), info).tolist()
+                t2 = time.perf_counter()
+                fps = frames_per_update / max(t2 - t0, 1e-9)
+                logger.losses(n_update, lv[0], lv[1], lv[2], lv[3], t2 - t0, step, fps, t1 - t0,
+                              t2 - t1, lv[4])
+                logger.episodes(_gather_episodes(rt.drain_episodes(), info))
+                last = {"update": n_update, "step": step, "pg_loss": lv[0], "value_loss": lv[1],
+                        "entropy": lv[2], "total_loss": lv[3], "fps": fps}
+                log(f"update {n_update} step {step} total_loss {lv[3]:.4f} pg {lv[0]:.4f} "
+                    f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {fps:,.0f}")
+            if flags.checkpoint_every and n_update % flags.checkpoint_every == 0:
+                if info.is_main:
+                    save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags)
+                D.barrier(info)
+    finally:
+        rt.stop()
+        if info.is_main:
+            save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags)
+        logger.close()
+    wall = time.perf_counter() - t_start
+    out = dict(last, updates=n_update, steps=step, wall_s=wall, checkpoint=ck_path,
+               mean_fps=step / max(wall, 1e-9))
+    log(f"[microbeast_amd] done: {out}")
+    D.destroy(info)
+    return out
