@@ -30,13 +30,13 @@ BASELINE_FPS = 38.9  # best reference run (5_ener), frames/s whole 
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--size", type=int, default=16)
-    p.add_argument("--groups", type=int, default=4)
-    p.add_argument("--envs_per_group", type=int, default=256)
+    p.add_argument("--groups", type=int, default=2)
+    p.add_argument("--envs_per_group", type=int, default=4096)
     p.add_argument("--unroll", type=int, default=64)
-    p.add_argument("--batch_slots", type=int, default=2)
+    p.add_argument("--batch_slots", type=int, default=1)
     p.add_argument("--threads", type=int, default=0, help="env worker threads per rank (0=auto)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--verbose", action="store_true", help="per-step progress on stderr")
@@ -92,7 +92,14 @@ def main(argv=None):
 
     for _ in range(args.warmup):
         losses = step()
+    # drop rollouts that piled up during warm-up (graph capture, first-call setup) so the
+    # timed window measures the steady-state production rate, not a pre-filled backlog
     torch.cuda.synchronize()
+    while True:
+        slots = rt.engine.get_full(1, 0.0)
+        if not slots:
+            break
+        rt.engine.release(slots, torch.cuda.current_stream().cuda_stream)
     D.barrier(info)
     st0 = rt.stats()
     t0 = time.perf_counter()

@@ -44,13 +44,27 @@ _SIGS = {
                  c_float, c_float, c_float, c_int64, c_void_p, c_void_p],
     "mbk_to_bf16": [c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_conv_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+                     c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
+                     c_void_p],
+    "mbk_pool_bwd_idx": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_void_p],
     "mbk_wgrad_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                          c_void_p],
     "mbk_pool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_conv_pack": [c_void_p, c_int, c_void_p],
+    "mbk_head_compact": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mbk_head_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                     c_void_p, c_void_p, c_void_p],
+    "mbk_head_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                     c_void_p, c_void_p],
+    "mbk_head_dx_gather": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "mbk_head_pack": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
 }
 
 

@@ -70,6 +70,7 @@ struct ConvFwdArgs {
   const bf16* mask_src;
   bf16* y;
   bf16* y_full;
+  uint8_t* pool_idx;  // pooled argmax (0..8 in the 3x3 window) for the backward
   int N, H, W, imgs, relu_in, pool;
 };
 
@@ -205,16 +206,19 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     const int co = e % COUT, p = e / COUT;
     const int im = p / (Ho * Wo), r = p - im * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
     float mx = -INFINITY;
+    int am = -1;
     for (int ky = 0; ky < 3; ++ky) {
       const int yy = 2 * oy - 1 + ky;
       if (yy < 0 || yy >= H) continue;
       for (int kx = 0; kx < 3; ++kx) {
         const int xx = 2 * ox - 1 + kx;
         if (xx < 0 || xx >= W) continue;
-        mx = fmaxf(mx, otile[((im * H + yy) * W + xx) * COUT + co]);
+        const float v = otile[((im * H + yy) * W + xx) * COUT + co];
+        if (v > mx || am < 0) { mx = v; am = ky * 3 + kx; }  // first max in scan order (ATen)
       }
     }
     yo[e] = f2bf(mx);
+    if (a.pool_idx) a.pool_idx[(size_t)img0 * Ho * Wo * COUT + e] = (uint8_t)am;
   }
 }
 
@@ -397,15 +401,24 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // partial[nparts][COUT*9*CIN + COUT] -> dw[co][ci][ky][kx] (+)=, db[co] (+)=
+// block = 64 output columns x 4 part-lanes; fixed summation order (deterministic)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial,
                                                            int nparts, int cin, int cin_real,
                                                            int cout, float* __restrict__ dw,
                                                            float* __restrict__ db, int accumulate) {
+  __shared__ float red[4][64];
   const int ktot = 9 * cin, row = cout * ktot + cout;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= row) return;
+  const int col = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + col;
   float s = 0.f;
-  for (int p = 0; p < nparts; ++p) s += partial[(size_t)p * row + e];
+  if (e < row) {
+#pragma unroll 4
+    for (int p = pl; p < nparts; p += 4) s += partial[(size_t)p * row + e];
+  }
+  red[pl][col] = s;
+  __syncthreads();
+  if (pl != 0 || e >= row) return;
+  s = red[0][col] + red[1][col] + red[2][col] + red[3][col];
   if (e < cout * ktot) {
     const int co = e / ktot, r = e - co * ktot, t = r / cin, ci = r - t * cin;
     if (ci >= cin_real) return;
@@ -455,6 +468,52 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ 
       }
     }
     dc[e] = f2bf(g);
+  }
+}
+
+// dc[n][y][x][c..c+7] = sum of dp over the (<= 4) windows whose stored argmax is (y, x)
+__global__ __launch_bounds__(256) void pool_bwd_idx_kernel(const uint8_t* __restrict__ pidx,
+                                                           const bf16* __restrict__ dp, int N,
+                                                           int H, int W, int C,
+                                                           bf16* __restrict__ dc) {
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  const int C8 = C / 8;
+  const size_t tot = (size_t)N * H * W * C8;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    const size_t p = e / C8;
+    const int x = p % W, y = (p / W) % H;
+    const size_t n = p / ((size_t)H * W);
+    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int oy = max(0, y / 2 - 1); oy <= min(Ho - 1, (y + 1) / 2); ++oy) {
+      const int ky = y - (2 * oy - 1);
+      if (ky < 0 || ky > 2) continue;
+      for (int ox = max(0, x / 2 - 1); ox <= min(Wo - 1, (x + 1) / 2); ++ox) {
+        const int kx = x - (2 * ox - 1);
+        if (kx < 0 || kx > 2) continue;
+        const uint8_t me = (uint8_t)(ky * 3 + kx);
+        const size_t q = ((n * Ho + oy) * Wo + ox) * C + c8 * 8;
+        const uint2 ids = *(const uint2*)(pidx + q);
+        const uint4 dv = *(const uint4*)(dp + q);
+        const uint32_t iw[2] = {ids.x, ids.y};
+        const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint8_t id = (uint8_t)(iw[j >> 2] >> (8 * (j & 3)));
+          const uint32_t hb = (dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+          if (id == me) g[j] += __uint_as_float(hb << 16);
+        }
+      }
+    }
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = __bfloat16_as_ushort(f2bf(g[2 * j]));
+      const uint32_t hi = __bfloat16_as_ushort(f2bf(g[2 * j + 1]));
+      o[j] = lo | (hi << 16);
+    }
+    *(uint4*)(dc + p * C + c8 * 8) = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -521,10 +580,10 @@ inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W) {
 
 extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const void* w,
                             const float* bias, const void* add, const void* mask_src, void* y,
-                            void* y_full, int N, int H, int W, int imgs, int relu_in, int pool,
-                            hipStream_t stream) {
+                            void* y_full, void* pool_idx, int N, int H, int W, int imgs,
+                            int relu_in, int pool, hipStream_t stream) {
   ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
-                (bf16*)y_full, N, H, W, imgs, relu_in, pool};
+                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool};
   const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   dim3 grid((N + imgs - 1) / imgs);
@@ -578,7 +637,7 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
 extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,
                                 float* dw, float* db, int accumulate, hipStream_t stream) {
   const int row = cout * 9 * cin + cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row + 255) / 256), dim3(256), 0, stream, partial,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row + 63) / 64), dim3(256), 0, stream, partial,
                      nparts, cin, cin_real, cout, dw, db, accumulate);
   return (int)hipGetLastError();
 }
@@ -590,6 +649,17 @@ extern "C" int mbk_pool_bwd(const void* cfull, const void* dp, int N, int H, int
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(pool_bwd_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                      (const bf16*)cfull, (const bf16*)dp, N, H, W, C, (bf16*)dc);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, int W, int C,
+                                void* dc, hipStream_t stream) {
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const size_t tot = (size_t)N * H * W * (C / 8);
+  size_t blocks = (tot + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(pool_bwd_idx_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     (const uint8_t*)pidx, (const bf16*)dp, N, H, W, C, (bf16*)dc);
   return (int)hipGetLastError();
 }
 

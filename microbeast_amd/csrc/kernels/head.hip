@@ -1,0 +1,562 @@
+// Sparse per-cell action head: active-cell compaction + grouped MFMA GEMM with
+// the masked segmented softmax fused into the epilogue.
+//
+// Reference: actor Linear(256, 78*h*w) + 7*h*w CategoricalMasked objects
+// (model.py:136, 167-200) — a dense N x 256 x 19,968 GEMM (65 % of the model's
+// FLOPs at 16x16) followed by a masked softmax over every cell.
+//
+// Observation: a cell whose 78 mask bits are all zero (no own idle unit — the
+// vast majority of cells) contributes EXACTLY nothing under the reference's fp32
+// semantics: its logits are replaced by -1e8, so log-prob = -1e8 - (-1e8 +
+// log n) rounds to 0, the masked entropy is 0 and torch.where passes no
+// gradient. So only "active" (frame, cell) pairs need logits at all:
+//
+//   head_count / head_scan / head_scatter : deterministic, stable counting sort
+//       of active pairs by cell (frames ascending inside a cell group), a tile
+//       list of 16-pair units, and pidx[f][c] (pair slot or -1). Inactive cells
+//       get action 0 / log-prob 0 / entropy 0 written here.
+//   head_fwd   : one wave per 16-pair unit: Z[16x80] = X[f rows] . W_c^T + b_c on
+//                v_mfma_f32_16x16x32_bf16 (W_c = that cell's 78 rows, padded to 80),
+//                then sample (Philox, inverse CDF) or score per row.
+//   head_bwd   : one workgroup per cell: recompute Z, dZ in the epilogue, then
+//                dX_pair = dZ . W_c (MFMA) and dW_c += dZ^T . X accumulated in
+//                registers over all the cell's pairs (both operands via
+//                ds_read_b64_tr_b16 from LDS tiles) -> written straight into the
+//                actor.weight/bias gradient rows of that cell (deterministic).
+//   head_dx_gather : dX[f] = sum of dX_pair over f's active cells (no atomics).
+#include "../include/mbk_api.h"
+#include "common.h"
+
+using namespace mbk;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __hip_bfloat16 bf16;
+
+namespace {
+
+constexpr int KD = 256;      // feature width
+constexpr int NP = 80;       // 78 logits padded to 5 x 16
+constexpr int NPT = 96;      // 78 padded to 3 x 32 (K of dZ . W)
+
+union Frag8 {
+  bf16x8 v;
+  uint4 u;
+  s16x4 h[2];
+};
+
+__device__ __forceinline__ float bf2f(bf16 v) { return __bfloat162float(v); }
+__device__ __forceinline__ bf16 f2bf(float v) { return __float2bfloat16(v); }
+
+__device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
+}
+
+__device__ __forceinline__ bool active3(const uint32_t* m) { return (m[0] | m[1] | m[2]) != 0u; }
+
+// ------------------------------------------------------------------ compaction
+// cnt[c * nfb + b] = active pairs of cell c among frames [b*FB, (b+1)*FB)
+__global__ __launch_bounds__(256) void head_count_kernel(const uint32_t* __restrict__ mask,
+                                                         int F, int S, int FB,
+                                                         int* __restrict__ cnt) {
+  const int b = blockIdx.x, nfb = gridDim.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= S) return;
+  const int f0 = b * FB, f1 = min(F, f0 + FB);
+  int n = 0;
+#pragma unroll 8
+  for (int f = f0; f < f1; ++f) n += active3(mask + ((size_t)f * S + c) * 3);
+  cnt[c * nfb + b] = n;
+}
+
+// exclusive scan in (c, b) order + per-cell groups + 16-pair unit list
+constexpr int CHUNK = 512;  // pairs per backward work item (heavy cells are split)
+
+__global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__ cnt, int S, int nfb,
+                                                         int* __restrict__ off,
+                                                         int* __restrict__ grp_start,
+                                                         int* __restrict__ grp_count,
+                                                         int* __restrict__ unit_cell,
+                                                         int* __restrict__ unit_row,
+                                                         int* __restrict__ chunk_cell,
+                                                         int* __restrict__ chunk_row,
+                                                         int* __restrict__ chunk_start,
+                                                         int* __restrict__ totals /* [3] */) {
+  __shared__ int part[1024];
+  __shared__ int upart[1024];
+  __shared__ int cpart[1024];
+  const int tid = threadIdx.x;
+  // each thread owns a contiguous range of cells
+  const int per = (S + 1023) / 1024;
+  const int c0 = min(S, tid * per), c1 = min(S, c0 + per);
+  int s = 0, u = 0, q = 0;
+  for (int c = c0; c < c1; ++c) {
+    int n = 0;
+    for (int b = 0; b < nfb; ++b) n += cnt[c * nfb + b];
+    s += n;
+    u += (n + 15) / 16;
+    q += (n + CHUNK - 1) / CHUNK;
+  }
+  part[tid] = s;
+  upart[tid] = u;
+  cpart[tid] = q;
+  __syncthreads();
+  // Hillis-Steele inclusive scans (1024 entries)
+  for (int o = 1; o < 1024; o <<= 1) {
+    int a = tid >= o ? part[tid - o] : 0, bq = tid >= o ? upart[tid - o] : 0;
+    int cq = tid >= o ? cpart[tid - o] : 0;
+    __syncthreads();
+    part[tid] += a;
+    upart[tid] += bq;
+    cpart[tid] += cq;
+    __syncthreads();
+  }
+  int pos = part[tid] - s, upos = upart[tid] - u, cpos = cpart[tid] - q;
+  for (int c = c0; c < c1; ++c) {
+    grp_start[c] = pos;
+    int n = 0;
+    for (int b = 0; b < nfb; ++b) {
+      off[c * nfb + b] = pos + n;
+      n += cnt[c * nfb + b];
+    }
+    grp_count[c] = n;
+    for (int r = 0; r < n; r += 16) {
+      unit_cell[upos] = c;
+      unit_row[upos] = pos + r;
+      ++upos;
+    }
+    chunk_start[c] = cpos;
+    for (int r = 0; r < n; r += CHUNK) {
+      chunk_cell[cpos] = c;
+      chunk_row[cpos] = pos + r;
+      ++cpos;
+    }
+    pos += n;
+  }
+  if (tid == 1023) {
+    totals[0] = part[1023];
+    totals[1] = upart[1023];
+    totals[2] = cpart[1023];
+  }
+}
+
+// pairs[] (frame ids, grouped by cell), pidx[f][c]; zero outputs of inactive cells
+__global__ __launch_bounds__(256) void head_scatter_kernel(
+    const uint32_t* __restrict__ mask, int F, int S, int FB, const int* __restrict__ off,
+    int* __restrict__ pairs, int* __restrict__ pidx, uint8_t* __restrict__ action_zero,
+    float* __restrict__ cell_lp, float* __restrict__ cell_ent) {
+  const int b = blockIdx.x, nfb = gridDim.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= S) return;
+  const int f0 = b * FB, f1 = min(F, f0 + FB);
+  int pos = off[c * nfb + b];
+  for (int f = f0; f < f1; ++f) {
+    const size_t fc = (size_t)f * S + c;
+    if (active3(mask + fc * 3)) {
+      pairs[pos] = f;
+      pidx[fc] = pos;
+      ++pos;
+    } else {
+      pidx[fc] = -1;
+      if (action_zero) {
+#pragma unroll
+        for (int k = 0; k < kComps; ++k) action_zero[fc * kComps + k] = 0;
+      }
+      if (cell_lp) cell_lp[fc] = 0.f;
+      if (cell_ent) cell_ent[fc] = 0.f;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ forward
+// Persistent: each wave takes 16-pair units until none is left.
+__global__ __launch_bounds__(256) void head_fwd_kernel(
+    const bf16* __restrict__ X, const bf16* __restrict__ Wp, const float* __restrict__ bp,
+    const uint32_t* __restrict__ mask, uint8_t* __restrict__ action, const uint64_t* __restrict__ rng,
+    int sample, const int* __restrict__ pairs, const int* __restrict__ unit_cell,
+    const int* __restrict__ unit_row, const int* __restrict__ grp_start,
+    const int* __restrict__ grp_count, const int* __restrict__ totals, int S,
+    float* __restrict__ cell_lp, float* __restrict__ cell_ent) {
+  __shared__ float zs[4][16][NP + 1];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int nunits = totals[1];
+  float (*z)[NP + 1] = zs[wave];
+  for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
+    const int c = unit_cell[u], r0 = unit_row[u];
+    const int gend = grp_start[c] + grp_count[c];
+    const int r = r0 + li;
+    const bool valid = r < gend;
+    const int f = valid ? pairs[r] : pairs[r0];
+    f32x4 acc[5];
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint4* xrow = (const uint4*)(X + (size_t)f * KD) + G;  // 8 bf16 per uint4
+    const bf16* wc = Wp + (size_t)c * NP * KD;
+#pragma unroll
+    for (int ks = 0; ks < KD / 32; ++ks) {
+      Frag8 a;
+      a.u = valid ? xrow[ks * 4] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) {
+        Frag8 b;
+        b.u = *((const uint4*)(wc + (size_t)(nb * 16 + li) * KD + ks * 32) + G);
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+      }
+    }
+    // C layout: row (pair) 4G+i, col (logit) nb*16 + li
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      const int col = nb * 16 + li;
+      const float bias = bp[c * NP + col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) z[4 * G + i][col] = acc[nb][i] + bias;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of this wave visible
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 16 && valid) {
+      const size_t fc = (size_t)f * S + c;
+      uint32_t m[3] = {mask[fc * 3], mask[fc * 3 + 1], mask[fc * 3 + 2]};
+      uint8_t a[kComps];
+      float uu[kComps];
+      if (sample) {
+        const uint64_t seed = rng[0], step = rng[1];
+        u32x4 ctr = {(uint32_t)fc, (uint32_t)(fc >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
+        u32x4 q0 = philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        ctr.y ^= 0x80000000u;
+        u32x4 q1 = philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+        uu[0] = u01(q0.x); uu[1] = u01(q0.y); uu[2] = u01(q0.z); uu[3] = u01(q0.w);
+        uu[4] = u01(q1.x); uu[5] = u01(q1.y); uu[6] = u01(q1.z);
+      } else {
+#pragma unroll
+        for (int k = 0; k < kComps; ++k) a[k] = action[fc * kComps + k];
+      }
+      float lp, ent;
+      cell_forward(&z[lane][0], m, a, sample != 0, uu, &lp, &ent);
+      if (sample) {
+#pragma unroll
+        for (int k = 0; k < kComps; ++k) action[fc * kComps + k] = a[k];
+      }
+      cell_lp[fc] = lp;
+      if (cell_ent) cell_ent[fc] = ent;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------ backward
+// One workgroup (4 waves) per cell; 64-pair tiles.
+// LDS: Wc [80][256] bf16 | X tile [64][256] bf16 | dZ tile [64][96] bf16 | z [64][81] f32
+constexpr int BW_TM = 64;
+constexpr int LDS_WC = NP * KD * 2;
+constexpr int LDS_XT = BW_TM * KD * 2;
+constexpr int LDS_DZ = BW_TM * NPT * 2;
+constexpr int LDS_Z = BW_TM * (NP + 1) * 4;
+
+__global__ __launch_bounds__(256) void head_bwd_kernel(
+    const bf16* __restrict__ X, const bf16* __restrict__ Wp, const bf16* __restrict__ WpT,
+    const float* __restrict__ bp, const uint32_t* __restrict__ mask,
+    const uint8_t* __restrict__ action, const int* __restrict__ pairs,
+    const int* __restrict__ grp_start, const int* __restrict__ grp_count,
+    const int* __restrict__ chunk_cell, const int* __restrict__ chunk_row,
+    const int* __restrict__ totals, const float* __restrict__ g_logp,
+    const float* __restrict__ g_ent, int S, float* __restrict__ dXp,
+    float* __restrict__ dWp /* [nchunks][78][256] */, float* __restrict__ dbp /* [nchunks][78] */) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wc_l = smem;
+  char* xt = wc_l + LDS_WC;
+  char* dzt = xt + LDS_XT;
+  float* zb = (float*)(dzt + LDS_DZ);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int nchunks = totals[2];
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+  const int c = chunk_cell[ch];
+  const int g0 = chunk_row[ch];
+  const int gn = min(CHUNK, grp_start[c] + grp_count[c] - g0);
+  __syncthreads();  // previous chunk's LDS reads done
+
+  // stage W_c (80 x 256 bf16 = 40 KB)
+  {
+    const uint4* src = (const uint4*)(Wp + (size_t)c * NP * KD);
+    for (int e = tid; e < NP * KD / 8; e += 256) ((uint4*)wc_l)[e] = src[e];
+  }
+  f32x4 accw[5][4];  // dW_c rows 16mb.., cols 64*wave + 16nb..
+#pragma unroll
+  for (int mb = 0; mb < 5; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) accw[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbias = 0.f;  // thread tid < 78 owns logit column tid
+
+  for (int t0 = 0; t0 < gn; t0 += BW_TM) {
+    const int nr = min(BW_TM, gn - t0);
+    __syncthreads();  // previous tile fully consumed
+    // stage X rows of this tile (zero rows past the group end)
+    for (int e = tid; e < BW_TM * KD / 8; e += 256) {
+      const int row = e / (KD / 8), q = e % (KD / 8);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (row < nr) v = ((const uint4*)(X + (size_t)pairs[g0 + t0 + row] * KD))[q];
+      ((uint4*)xt)[e] = v;
+    }
+    __syncthreads();
+    // ---- Z = X . Wc^T + b (wave w: rows 16w..16w+15)
+    {
+      f32x4 acc[5];
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KD / 32; ++ks) {
+        Frag8 a;
+        a.u = *(const uint4*)(xt + ((16 * wave + li) * KD + ks * 32 + 8 * G) * 2);
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) {
+          Frag8 b;
+          b.u = *(const uint4*)(wc_l + ((nb * 16 + li) * KD + ks * 32 + 8 * G) * 2);
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) {
+        const int col = nb * 16 + li;
+        const float bias = bp[c * NP + col];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zb[(16 * wave + 4 * G + i) * (NP + 1) + col] = acc[nb][i] + bias;
+      }
+    }
+    __syncthreads();
+    // ---- dZ per row (threads 0..63 one row each), in place in zb
+    if (tid < BW_TM) {
+      float* zr = zb + tid * (NP + 1);
+      if (tid < nr) {
+        const int f = pairs[g0 + t0 + tid];
+        const size_t fc = (size_t)f * S + c;
+        uint32_t m[3] = {mask[fc * 3], mask[fc * 3 + 1], mask[fc * 3 + 2]};
+        uint8_t a[kComps];
+#pragma unroll
+        for (int k = 0; k < kComps; ++k) a[k] = action[fc * kComps + k];
+        cell_backward(zr, m, a, g_logp[f], g_ent ? g_ent[f] : 0.f, zr);
+      } else {
+        for (int j = 0; j < kCell; ++j) zr[j] = 0.f;
+      }
+      zr[78] = 0.f;
+      zr[79] = 0.f;
+    }
+    __syncthreads();
+    // ---- dZ -> bf16 tile [64][96] (cols >= 78 zero); bias grad column sums
+    for (int e = tid; e < BW_TM * NPT; e += 256) {
+      const int row = e / NPT, col = e % NPT;
+      const float v = col < kCell ? zb[row * (NP + 1) + col] : 0.f;
+      ((bf16*)dzt)[e] = f2bf(v);
+    }
+    if (tid < kCell) {
+      float s = 0.f;
+      for (int row = 0; row < nr; ++row) s += zb[row * (NP + 1) + tid];
+      dbias += s;
+    }
+    __syncthreads();
+    // ---- dX_pair = dZ . Wc (wave w: rows 16w..16w+15, 256 cols; K = 96)
+    {
+      f32x4 acc[16];
+#pragma unroll
+      for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const bf16* wt = WpT + (size_t)c * KD * NPT;
+#pragma unroll
+      for (int ks = 0; ks < NPT / 32; ++ks) {
+        Frag8 a;
+        a.u = *(const uint4*)(dzt + ((16 * wave + li) * NPT + ks * 32 + 8 * G) * 2);
+#pragma unroll
+        for (int nb = 0; nb < 16; ++nb) {
+          Frag8 b;
+          b.u = *((const uint4*)(wt + (size_t)(nb * 16 + li) * NPT + ks * 32) + G);
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * wave + 4 * G + i;
+        if (row < nr) {
+          float* dst = dXp + (size_t)(g0 + t0 + row) * KD;
+#pragma unroll
+          for (int nb = 0; nb < 16; ++nb) dst[nb * 16 + li] = acc[nb][i];
+        }
+      }
+    }
+    // ---- dW_c += dZ^T . X  (rows = logits, cols = features 64*wave.., K = 64 pairs)
+#pragma unroll
+    for (int ks = 0; ks < BW_TM / 32; ++ks) {
+      Frag8 a[5];
+#pragma unroll
+      for (int mb = 0; mb < 5; ++mb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int prow = ks * 32 + 8 * G + 4 * h + (li >> 2);
+          a[mb].h[h] = tr_read(dzt + (prow * NPT + mb * 16 + 4 * (li & 3)) * 2);
+        }
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) {
+        Frag8 b;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int prow = ks * 32 + 8 * G + 4 * h + (li >> 2);
+          b.h[h] = tr_read(xt + (prow * KD + 64 * wave + nb * 16 + 4 * (li & 3)) * 2);
+        }
+#pragma unroll
+        for (int mb = 0; mb < 5; ++mb)
+          accw[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb].v, b.v, accw[mb][nb], 0, 0, 0);
+      }
+    }
+  }
+  // ---- this chunk's partial dW / db (reduced per cell by head_dw_reduce)
+#pragma unroll
+  for (int mb = 0; mb < 5; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = mb * 16 + 4 * G + i;
+      if (n >= kCell) continue;
+      float* dst = dWp + ((size_t)ch * kCell + n) * KD + 64 * wave;
+#pragma unroll
+      for (int nb = 0; nb < 4; ++nb) dst[nb * 16 + li] = accw[mb][nb][i];
+    }
+  if (tid < kCell) dbp[(size_t)ch * kCell + tid] = dbias;
+  }  // chunks
+}
+
+// dW[c*78+n][d] = sum over the cell's chunks (fixed order); zero for idle cells
+__global__ __launch_bounds__(256) void head_dw_reduce_kernel(const float* __restrict__ dWp,
+                                                             const float* __restrict__ dbp,
+                                                             const int* __restrict__ chunk_start,
+                                                             const int* __restrict__ grp_count,
+                                                             int S, float* __restrict__ dW,
+                                                             float* __restrict__ db) {
+  const int c = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;  // within [78][256] (+78 bias entries)
+  const int nch = (grp_count[c] + CHUNK - 1) / CHUNK, c0 = chunk_start[c];
+  if (e < kCell * KD) {
+    float s = 0.f;
+    for (int q = 0; q < nch; ++q) s += dWp[(size_t)(c0 + q) * kCell * KD + e];
+    dW[(size_t)c * kCell * KD + e] = s;
+  } else if (e < kCell * KD + kCell) {
+    const int n = e - kCell * KD;
+    float s = 0.f;
+    for (int q = 0; q < nch; ++q) s += dbp[(size_t)(c0 + q) * kCell + n];
+    db[c * kCell + n] = s;
+  }
+}
+
+// dX[f][:] = sum over active cells c of dXp[pidx[f][c]][:]; one wave per frame
+__global__ __launch_bounds__(256) void head_dx_gather_kernel(const float* __restrict__ dXp,
+                                                             const int* __restrict__ pidx, int F,
+                                                             int S, float* __restrict__ dX) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= F) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int* pr = pidx + (size_t)f * S;
+  for (int c = 0; c < S; ++c) {
+    const int p = pr[c];
+    if (p < 0) continue;
+    const float4 v = ((const float4*)(dXp + (size_t)p * KD))[lane];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  ((float4*)(dX + (size_t)f * KD))[lane] = acc;
+}
+
+// W [S*78][256] fp32, b [S*78] -> Wp [S][80][256] bf16, bp [S][80], WpT [S][256][96] bf16
+__global__ __launch_bounds__(256) void head_pack_kernel(const float* __restrict__ W,
+                                                        const float* __restrict__ b, int S,
+                                                        bf16* __restrict__ Wp,
+                                                        float* __restrict__ bp,
+                                                        bf16* __restrict__ WpT) {
+  const size_t nWp = (size_t)S * NP * KD;
+  const size_t nWt = WpT ? (size_t)S * KD * NPT : 0;
+  const size_t nb = (size_t)S * NP;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < nWp + nWt + nb;
+       e += (size_t)gridDim.x * blockDim.x) {
+    if (e < nWp) {
+      const size_t c = e / (NP * KD), r = e % (NP * KD), n = r / KD, k = r % KD;
+      Wp[e] = f2bf(n < (size_t)kCell ? W[(c * kCell + n) * KD + k] : 0.f);
+    } else if (e < nWp + nWt) {
+      const size_t q = e - nWp, c = q / (KD * NPT), r = q % (KD * NPT), d = r / NPT, n = r % NPT;
+      WpT[q] = f2bf(n < (size_t)kCell ? W[(c * kCell + n) * KD + d] : 0.f);
+    } else {
+      const size_t q = e - nWp - nWt, c = q / NP, n = q % NP;
+      bp[q] = n < (size_t)kCell ? b[c * kCell + n] : 0.f;
+    }
+  }
+}
+
+}  // namespace
+
+// frames per counting block: small batches (policy steps) use short blocks so the
+// serial per-thread frame loop stays short; big learner batches cap the scan length.
+extern "C" int mbk_head_fb(int F) {
+  int fb = F / 64;
+  if (fb < 8) fb = 8;
+  if (fb > 256) fb = 256;
+  return fb;
+}
+
+extern "C" int mbk_head_compact(const uint32_t* mask, int F, int S, int* cnt, int* off,
+                                int* grp_start, int* grp_count, int* unit_cell, int* unit_row,
+                                int* chunk_cell, int* chunk_row, int* chunk_start,
+                                int* totals, int* pairs, int* pidx, uint8_t* action_zero,
+                                float* cell_lp, float* cell_ent, hipStream_t stream) {
+  const int FB = mbk_head_fb(F);
+  const int nfb = (F + FB - 1) / FB;
+  dim3 g1(nfb, (S + 255) / 256);
+  hipLaunchKernelGGL(head_count_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, cnt);
+  hipLaunchKernelGGL(head_scan_kernel, dim3(1), dim3(1024), 0, stream, cnt, S, nfb, off,
+                     grp_start, grp_count, unit_cell, unit_row, chunk_cell, chunk_row, chunk_start,
+                     totals);
+  hipLaunchKernelGGL(head_scatter_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, off, pairs,
+                     pidx, action_zero, cell_lp, cell_ent);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_head_fwd(const void* X, const void* Wp, const float* bp, const uint32_t* mask,
+                            uint8_t* action, const uint64_t* rng, int sample, const int* pairs,
+                            const int* unit_cell, const int* unit_row, const int* grp_start,
+                            const int* grp_count, const int* totals, int S, int grid,
+                            float* cell_lp, float* cell_ent, hipStream_t stream) {
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const bf16*)X,
+                     (const bf16*)Wp, bp, mask, action, rng, sample, pairs, unit_cell, unit_row,
+                     grp_start, grp_count, totals, S, cell_lp, cell_ent);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, const float* bp,
+                            const uint32_t* mask, const uint8_t* action, const int* pairs,
+                            const int* grp_start, const int* grp_count, const int* chunk_cell,
+                            const int* chunk_row, const int* chunk_start, const int* totals,
+                            const float* g_logp, const float* g_ent, int S, int grid, float* dXp,
+                            float* dWp, float* dbp, float* dW, float* db, hipStream_t stream) {
+  const size_t sm = LDS_WC + LDS_XT + LDS_DZ + LDS_Z;
+  hipFuncSetAttribute((const void*)head_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)sm);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(grid), dim3(256), sm, stream, (const bf16*)X,
+                     (const bf16*)Wp, (const bf16*)WpT, bp, mask, action, pairs, grp_start,
+                     grp_count, chunk_cell, chunk_row, totals, g_logp, g_ent, S, dXp, dWp, dbp);
+  dim3 g2((kCell * KD + kCell + 255) / 256, S);
+  hipLaunchKernelGGL(head_dw_reduce_kernel, g2, dim3(256), 0, stream, dWp, dbp, chunk_start,
+                     grp_count, S, dW, db);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_head_dx_gather(const float* dXp, const int* pidx, int F, int S, float* dX,
+                                  hipStream_t stream) {
+  hipLaunchKernelGGL(head_dx_gather_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, dXp, pidx, F,
+                     S, dX);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_head_pack(const float* W, const float* b, int S, void* Wp, float* bp, void* WpT,
+                             hipStream_t stream) {
+  size_t tot = (size_t)S * (NP * KD + (WpT ? KD * NPT : 0) + NP);
+  size_t blocks = (tot + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(head_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, W, b, S,
+                     (bf16*)Wp, bp, (bf16*)WpT);
+  return (int)hipGetLastError();
+}

@@ -41,7 +41,11 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
                         cfg_.reward_weight.empty() ? nullptr : cfg_.reward_weight.data(),
                         cfg_.env_index_base));
   CTOR_CHECK(hipSetDevice(cfg_.device));
-  CTOR_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  // highest priority: a policy step is latency-critical (env workers wait on it) and
+  // must not queue behind the learner's long kernels on the other stream
+  int prio_least = 0, prio_greatest = 0;
+  CTOR_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
+  CTOR_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_greatest));
   CTOR_CHECK(hipHostMalloc((void**)&h_obs_, (size_t)total * S_ * 4, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_mask_, (size_t)total * S_ * 4 * kMaskWords,
                            hipHostMallocDefault));

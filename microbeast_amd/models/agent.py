@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from ..ops import cell_head
 from ..ops.encoder import HipEncoder, encode, encoder_params
+from ..ops.head import SparseHead, sparse_sample, sparse_score
 from ..ops.obs import bits_to_planes
 
 
@@ -87,6 +88,7 @@ class Agent(nn.Module):
         self.channels = tuple(channels)
         self.hip_kernels = hip_kernels
         self._hip_enc = None
+        self._hip_head = None
         h, w, c = obs_space_shape
         self.h, self.w, self.planes = h, w, c
         self.mapsize = mapsize if mapsize is not None else h * w
@@ -155,9 +157,25 @@ class Agent(nn.Module):
         return tuple()
 
     # ------------------------------------------------------------ acting / learning
+    def _head(self, dev) -> SparseHead:
+        if self._hip_head is None or self._hip_head.device != dev:
+            self._hip_head = SparseHead(self.h * self.w, dev)
+        return self._hip_head
+
     @torch.no_grad()
-    def act(self, obs, mask_bits, rng_state=None, generator=None):
+    def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
+            logp_out=None):
         """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N])."""
+        if self._use_hip(obs):
+            # sparse head: only cells with a legal action are computed (ops/head.py)
+            f = self.features(obs)
+            with self._autocast(f):
+                value = self.critic(f).float().view(-1)
+            n = f.shape[0]
+            action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
+                                         mask_bits.reshape(n, -1, 3), rng_state,
+                                         self._head(f.device), action_out, logp_out)
+            return action, logp, value
         logits, value = self.policy_value(obs)
         action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)
         return action, logp, value
@@ -171,7 +189,13 @@ class Agent(nn.Module):
         f = self.features(obs)
         with self._autocast(f):
             value = self.critic(f).float().view(-1)
-            fh = f if n_score is None else f[:n_score]
+        fh = f if n_score is None else f[:n_score]
+        if self._use_hip(obs):
+            logp, ent = sparse_score(fh.to(torch.bfloat16), self.actor.weight, self.actor.bias,
+                                     mask_bits.reshape(fh.shape[0], -1, 3),
+                                     action.reshape(fh.shape[0], -1, 7), self._head(f.device))
+            return logp, ent, value
+        with self._autocast(fh):
             logits = self.actor(fh)
         logp, ent = cell_head.score(logits, mask_bits, action)
         return logp, ent, value

@@ -7,8 +7,8 @@ and 12 dgrad + 15 wgrad launches backward, all NHWC bf16 with fp32
 accumulation, plus ONE weight-pack launch per call that converts the fp32
 master parameters into the kernels' packed bf16 layouts.
 
-Saved for backward per stage: the stage input, the full-resolution conv
-output (pool argmax), the pooled output and each residual block's input and
+Saved for backward per stage: the stage input, the pooled argmax (one byte
+per pooled output), the pooled output and each residual block's input and
 inner conv output.
 """
 from __future__ import annotations
@@ -99,7 +99,8 @@ class HipEncoder:
         N.check(k.mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), len(self.layers),
                                 N.stream_ptr()), "conv_pack")
 
-    def _fwd(self, L: ConvLayer, x, bias, add=None, mask_src=None, y_full=None, dgrad=False):
+    def _fwd(self, L: ConvLayer, x, bias, add=None, mask_src=None, y_full=None, dgrad=False,
+             pool_idx=None):
         n = x.shape[0]
         if dgrad:
             # data gradient = conv with flipped/transposed weights at the layer's input size
@@ -114,14 +115,15 @@ class HipEncoder:
         imgs = _imgs_fwd(L, cin, cout, bits, pool)
         N.check(N.kernels().mbk_conv_fwd(
             x.data_ptr(), int(bits), cin, cout, w, N.ptr(bias), N.ptr(add), N.ptr(mask_src),
-            y.data_ptr(), N.ptr(y_full), n, H, W, imgs, int(relu), int(pool), N.stream_ptr()),
+            y.data_ptr(), N.ptr(y_full), N.ptr(pool_idx), n, H, W, imgs, int(relu), int(pool),
+            N.stream_ptr()),
             "conv_fwd")
         return y
 
     def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor):
         n = x.shape[0]
         imgs = _imgs_wgrad(L)
-        nparts = max(1, min(1024, (n + imgs - 1) // imgs))
+        nparts = max(1, min(256, (n + imgs - 1) // imgs))  # ~one workgroup per CU
         row = L.cout * 9 * L.cin + L.cout
         need = nparts * row
         if self._partial is None or self._partial.numel() < need or self._partial.device != dy.device:
@@ -145,15 +147,17 @@ class HipEncoder:
         n = x.shape[0]
         for _stage in range(len(self.layers) // 5):
             L = self.layers[li]
-            cfull = (torch.empty(n, L.H, L.W, L.cout, dtype=torch.bfloat16, device=x.device)
-                     if save else None)
-            p = self._fwd(L, x, bs[li].detach(), y_full=cfull)
+            Ho, Wo = (L.H + 1) // 2, (L.W + 1) // 2
+            # pooled argmax (1 byte) instead of the full-resolution conv output
+            pidx = (torch.empty(n, Ho, Wo, L.cout, dtype=torch.uint8, device=x.device)
+                    if save else None)
+            p = self._fwd(L, x, bs[li].detach(), pool_idx=pidx)
             u0 = self._fwd(self.layers[li + 1], p, bs[li + 1].detach())
             y0 = self._fwd(self.layers[li + 2], u0, bs[li + 2].detach(), add=p)
             u1 = self._fwd(self.layers[li + 3], y0, bs[li + 3].detach())
             y1 = self._fwd(self.layers[li + 4], u1, bs[li + 4].detach(), add=y0)
             if save:
-                saved += [x, cfull, p, u0, y0, u1]
+                saved += [x, pidx, p, u0, y0, u1]
             x = y1
             li += 5
         return x, saved
@@ -164,7 +168,7 @@ class HipEncoder:
         g = g.contiguous()
         for s in range(nst - 1, -1, -1):
             li = 5 * s
-            x, cfull, p, u0, y0, u1 = saved[6 * s:6 * s + 6]
+            x, pidx, p, u0, y0, u1 = saved[6 * s:6 * s + 6]
             L = self.layers
             # res block 1: y1 = y0 + conv4(relu(u1)), u1 = conv3(relu(y0))
             self._wgrad(L[li + 4], u1, g, grads[2 * (li + 4)], grads[2 * (li + 4) + 1])
@@ -178,10 +182,11 @@ class HipEncoder:
             dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
-            dc = torch.empty_like(cfull)
-            N.check(N.kernels().mbk_pool_bwd(cfull.data_ptr(), dp.data_ptr(), cfull.shape[0],
-                                             Ls.H, Ls.W, Ls.cout, dc.data_ptr(), N.stream_ptr()),
-                    "pool_bwd")
+            dc = torch.empty(pidx.shape[0], Ls.H, Ls.W, Ls.cout, dtype=torch.bfloat16,
+                             device=pidx.device)
+            N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dp.data_ptr(), pidx.shape[0],
+                                                 Ls.H, Ls.W, Ls.cout, dc.data_ptr(),
+                                                 N.stream_ptr()), "pool_bwd_idx")
             self._wgrad(Ls, x, dc, grads[2 * li], grads[2 * li + 1])
             g = self._fwd(Ls, dc, None, dgrad=True) if s > 0 else None
         return grads

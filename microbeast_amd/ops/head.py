@@ -1,0 +1,161 @@
+"""Sparse per-cell action head on the HIP kernels of ``head.hip``.
+
+Exact reformulation of the reference's dense head (actor Linear(256, 78*h*w)
++ CategoricalMasked per component, model.py:136-200): only (frame, cell)
+pairs with at least one legal action are computed — a fully-masked cell has
+log-prob 0, entropy 0 and zero gradient in the reference's fp32 semantics, so
+skipping it changes nothing but the cost (typically 1-5 % of cells are active).
+
+Pipeline per call: compaction (3 small launches) -> grouped MFMA GEMM with
+the masked-softmax epilogue (sample or score) -> per-frame sums; backward:
+per-cell recompute + dZ + dX_pair + dW_c (one workgroup per cell) -> dX gather.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _native as N
+
+KD, NP, NPT = 256, 80, 96
+
+
+class SparseHead:
+    def __init__(self, S: int, device: torch.device):
+        self.S = S
+        self.device = device
+        self.Wp = torch.zeros(S, NP, KD, dtype=torch.bfloat16, device=device)
+        self.WpT = torch.zeros(S, KD, NPT, dtype=torch.bfloat16, device=device)
+        self.bp = torch.zeros(S, NP, dtype=torch.float32, device=device)
+        self.totals = torch.zeros(3, dtype=torch.int32, device=device)
+        self.chunk_start = torch.zeros(S, dtype=torch.int32, device=device)
+        self.grp_start = torch.zeros(S, dtype=torch.int32, device=device)
+        self.grp_count = torch.zeros(S, dtype=torch.int32, device=device)
+        self._F = -1
+        n_cu = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 1
+        self.fwd_grid = 2 * n_cu
+
+    def _ensure(self, F: int):
+        if F <= self._F:
+            return
+        S, dev = self.S, self.device
+        fb = min(256, max(8, F // 64))  # mirrors mbk_head_fb
+        nfb = (F + fb - 1) // fb
+        self.cnt = torch.zeros(S * nfb, dtype=torch.int32, device=dev)
+        self.off = torch.zeros(S * nfb, dtype=torch.int32, device=dev)
+        self.unit_cell = torch.zeros(F * S // 16 + S + 1, dtype=torch.int32, device=dev)
+        self.unit_row = torch.zeros_like(self.unit_cell)
+        self.chunk_cell = torch.zeros(F * S // 512 + S + 1, dtype=torch.int32, device=dev)
+        self.chunk_row = torch.zeros_like(self.chunk_cell)
+        self.pairs = torch.zeros(F * S, dtype=torch.int32, device=dev)
+        self.pidx = torch.zeros(F * S, dtype=torch.int32, device=dev)
+        self.cell_lp = torch.zeros(F * S, dtype=torch.float32, device=dev)
+        self.cell_ent = torch.zeros(F * S, dtype=torch.float32, device=dev)
+        self._F = F
+
+    def pack(self, W: torch.Tensor, b: torch.Tensor, with_t: bool):
+        N.check(N.kernels().mbk_head_pack(W.data_ptr(), b.data_ptr(), self.S,
+                                          self.Wp.data_ptr(), self.bp.data_ptr(),
+                                          self.WpT.data_ptr() if with_t else None,
+                                          N.stream_ptr()), "head_pack")
+
+    def compact(self, mask_bits: torch.Tensor, F: int, action_zero: torch.Tensor | None):
+        self._ensure(F)
+        N.check(N.kernels().mbk_head_compact(
+            mask_bits.data_ptr(), F, self.S, self.cnt.data_ptr(), self.off.data_ptr(),
+            self.grp_start.data_ptr(), self.grp_count.data_ptr(), self.unit_cell.data_ptr(),
+            self.unit_row.data_ptr(), self.chunk_cell.data_ptr(), self.chunk_row.data_ptr(),
+            self.chunk_start.data_ptr(), self.totals.data_ptr(), self.pairs.data_ptr(),
+            self.pidx.data_ptr(), N.ptr(action_zero), self.cell_lp.data_ptr(),
+            self.cell_ent.data_ptr(), N.stream_ptr()), "head_compact")
+
+    def forward(self, X: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor,
+                sample: bool, rng: torch.Tensor | None, logp_out: torch.Tensor | None = None,
+                ent_out: torch.Tensor | None = None, want_ent: bool = True):
+        """X bf16 [F,256] contiguous. sample=True writes ``action`` (uint8 [F,S,7])."""
+        F = X.shape[0]
+        k = N.kernels()
+        st = N.stream_ptr()
+        self.compact(mask_bits, F, action if sample else None)
+        N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
+                               mask_bits.data_ptr(), action.data_ptr(), N.ptr(rng), int(sample),
+                               self.pairs.data_ptr(), self.unit_cell.data_ptr(),
+                               self.unit_row.data_ptr(), self.grp_start.data_ptr(),
+                               self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
+                               self.fwd_grid, self.cell_lp.data_ptr(),
+                               self.cell_ent.data_ptr() if want_ent else None, st), "head_fwd")
+        logp = logp_out if logp_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
+        N.check(k.mbk_row_sum(self.cell_lp.data_ptr(), F, self.S, logp.data_ptr(), st), "row_sum")
+        ent = None
+        if want_ent:
+            ent = ent_out if ent_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
+            N.check(k.mbk_row_sum(self.cell_ent.data_ptr(), F, self.S, ent.data_ptr(), st), "row_sum")
+        if sample:
+            N.check(k.mbk_rng_advance(rng.data_ptr(), st), "rng_advance")
+        return logp, ent
+
+    def backward(self, X, mask_bits, action, g_logp, g_ent):
+        """Returns (dX fp32 [F,256], dW fp32 [S*78,256], db fp32 [S*78]).
+
+        Relies on the compaction left by the matching forward (same batch)."""
+        F = X.shape[0]
+        k = N.kernels()
+        st = N.stream_ptr()
+        # one sync: sizes the pair-major dX and per-chunk dW buffers
+        P, _, nch = (int(v) for v in self.totals.tolist())
+        dXp = torch.empty(max(P, 1), KD, dtype=torch.float32, device=X.device)
+        dWp = torch.empty(max(nch, 1), 78, KD, dtype=torch.float32, device=X.device)
+        dbp = torch.empty(max(nch, 1), 78, dtype=torch.float32, device=X.device)
+        dW = torch.empty(self.S * 78, KD, dtype=torch.float32, device=X.device)
+        db = torch.empty(self.S * 78, dtype=torch.float32, device=X.device)
+        grid = max(1, min(nch, self.fwd_grid // 2))
+        N.check(k.mbk_head_bwd(X.data_ptr(), self.Wp.data_ptr(), self.WpT.data_ptr(),
+                               self.bp.data_ptr(), mask_bits.data_ptr(), action.data_ptr(),
+                               self.pairs.data_ptr(), self.grp_start.data_ptr(),
+                               self.grp_count.data_ptr(), self.chunk_cell.data_ptr(),
+                               self.chunk_row.data_ptr(), self.chunk_start.data_ptr(),
+                               self.totals.data_ptr(), g_logp.data_ptr(), N.ptr(g_ent), self.S,
+                               grid, dXp.data_ptr(), dWp.data_ptr(), dbp.data_ptr(),
+                               dW.data_ptr(), db.data_ptr(), st), "head_bwd")
+        dX = torch.empty(F, KD, dtype=torch.float32, device=X.device)
+        N.check(k.mbk_head_dx_gather(dXp.data_ptr(), self.pidx.data_ptr(), F, self.S,
+                                     dX.data_ptr(), st), "head_dx_gather")
+        return dX, dW, db
+
+
+class _SparseHeadScore(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, W, b, mask_bits, action, head: SparseHead):
+        Xc = X.contiguous()
+        head.pack(W.detach(), b.detach(), with_t=True)
+        logp, ent = head.forward(Xc, mask_bits, action, sample=False, rng=None)
+        ctx.head = head
+        ctx.save_for_backward(Xc, mask_bits, action)
+        ctx.x_dtype = X.dtype
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        Xc, mask_bits, action = ctx.saved_tensors
+        F = Xc.shape[0]
+        if g_logp is None:
+            g_logp = torch.zeros(F, device=Xc.device)
+        g_logp = g_logp.float().contiguous()
+        g_ent = g_ent.float().contiguous() if g_ent is not None else None
+        dX, dW, db = ctx.head.backward(Xc, mask_bits, action, g_logp, g_ent)
+        return dX.to(ctx.x_dtype), dW, db, None, None, None
+
+
+def sparse_score(X, W, b, mask_bits, action, head: SparseHead):
+    """(logp [F], entropy [F]); differentiable in X, W, b."""
+    return _SparseHeadScore.apply(X, W, b, mask_bits.contiguous(), action.contiguous(), head)
+
+
+@torch.no_grad()
+def sparse_sample(X, W, b, mask_bits, rng, head: SparseHead, action_out=None, logp_out=None):
+    F = X.shape[0]
+    if action_out is None:
+        action_out = torch.empty(F, head.S, 7, dtype=torch.uint8, device=X.device)
+    head.pack(W, b, with_t=False)
+    logp, _ = head.forward(X.contiguous(), mask_bits.contiguous(), action_out, sample=True,
+                           rng=rng, logp_out=logp_out, want_ent=False)
+    return action_out, logp

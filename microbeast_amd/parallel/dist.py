@@ -54,12 +54,14 @@ def init_distributed(use_cuda: bool, timeout_s: float = 600.0) -> DistInfo:
             torch.cuda.set_device(local)
         return DistInfo(rank, world, local, "none")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    backend = "nccl" if use_cuda else "gloo"
+    # nccl == RCCL on ROCm; MBK_DIST_BACKEND=gloo lets several ranks share one GPU in tests
+    backend = os.environ.get("MBK_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     if use_cuda:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
     if not dist.is_initialized():
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
-        if use_cuda:
+        if use_cuda and backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
         dist.init_process_group(**kw)
     return DistInfo(rank, world, local, backend)

@@ -99,9 +99,13 @@ class GpuActorRuntime:
     def _policy_step(self):
         io = self.io
         m = self.infer_model
-        logits, value = m.policy_value(io["in_obs"])
-        cell_head.sample_gpu(logits, io["in_mask"], self.rng, action_out=io["out_action"],
-                             cell_logp=self._cell_logp, logp_out=io["out_logp"])
+        if hasattr(m, "_use_hip") and m._use_hip(io["in_obs"]):
+            _, _, value = m.act(io["in_obs"], io["in_mask"], self.rng,
+                                action_out=io["out_action"], logp_out=io["out_logp"])
+        else:
+            logits, value = m.policy_value(io["in_obs"])
+            cell_head.sample_gpu(logits, io["in_mask"], self.rng, action_out=io["out_action"],
+                                 cell_logp=self._cell_logp, logp_out=io["out_logp"])
         io["out_value"].copy_(value)
 
     def _capture(self):

@@ -61,14 +61,25 @@ def test_single_conv_layers_exact_structure(cuda):
     L0 = enc.layers[0]
     obs = _random_obs_bits(3, 256, seed=5)
     cfull = torch.empty(3, 16, 16, 16, dtype=torch.bfloat16, device=cuda)
+    pidx = torch.empty(3, 8, 8, 16, dtype=torch.uint8, device=cuda)
     b0 = torch.randn(16) * 0.1
-    p = enc._fwd(L0, obs.to(cuda), b0.to(cuda), y_full=cfull)
+    p = enc._fwd(L0, obs.to(cuda), b0.to(cuda), y_full=cfull, pool_idx=pidx)
     from microbeast_amd.ops.obs import bits_to_planes
     planes = bits_to_planes(obs, 16, 16)
     cr = F.conv2d(planes, ws[0].bfloat16().float(), b0, padding=1)
     torch.testing.assert_close(cfull.float().cpu().permute(0, 3, 1, 2), cr, rtol=2e-2, atol=2e-2)
-    pr = F.max_pool2d(cfull.float().cpu().permute(0, 3, 1, 2), 3, 2, 1)
+    pr, ir = F.max_pool2d(cfull.float().cpu().permute(0, 3, 1, 2), 3, 2, 1, return_indices=True)
     torch.testing.assert_close(p.float().cpu().permute(0, 3, 1, 2), pr, rtol=0, atol=0)
+    # pool-index backward == autograd of max_pool2d
+    dp = torch.randn(3, 8, 8, 16).bfloat16()
+    dpg = dp.to(cuda)
+    dc = torch.empty(3, 16, 16, 16, dtype=torch.bfloat16, device=cuda)
+    from microbeast_amd import _native as N
+    N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dpg.data_ptr(), 3, 16, 16, 16,
+                                         dc.data_ptr(), N.stream_ptr()), "pool_bwd_idx")
+    ct = cfull.float().cpu().permute(0, 3, 1, 2).clone().requires_grad_(True)
+    F.max_pool2d(ct, 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
 
 
 def test_pool_bwd_and_l0_wgrad(cuda):

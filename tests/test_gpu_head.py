@@ -1,0 +1,77 @@
+"""Sparse grouped-GEMM head (head.hip) vs the dense fp32 torch reference of the reference's
+Linear(256, 78*S) + CategoricalMasked head."""
+import pytest
+import torch
+
+from microbeast_amd.ops import cell_head
+from microbeast_amd.ops.cell_head import pack_mask
+from microbeast_amd.ops.head import SparseHead, sparse_sample, sparse_score
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(F, S, p_active=0.08, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    X = (torch.randn(F, 256, generator=g) * 0.5).bfloat16()
+    W = torch.randn(S * 78, 256, generator=g) * 0.05
+    b = torch.randn(S * 78, generator=g) * 0.1
+    active = torch.rand(F, S, generator=g) < p_active
+    m = (torch.rand(F, S, 78, generator=g) < 0.5) & active[..., None]
+    m[..., 0] |= active  # active cells can always no-op
+    a = torch.zeros(F, S, 7, dtype=torch.uint8)
+    for k in range(7):
+        o0, o1 = cell_head.OFFS[k], cell_head.OFFS[k + 1]
+        w = m[..., o0:o1].float() + 1e-9
+        a[..., k] = torch.multinomial(w.view(-1, o1 - o0), 1, generator=g).view(F, S).to(torch.uint8)
+    a[~active] = 0
+    return X, W, b, m, a
+
+
+@pytest.mark.parametrize("F,S", [(300, 64), (1000, 256)])
+def test_sparse_score_fwd_bwd(cuda, F, S):
+    X, W, b, m, a = _problem(F, S)
+    head = SparseHead(S, cuda)
+    Xg = X.to(cuda).requires_grad_(True)
+    Wg = W.to(cuda).requires_grad_(True)
+    bg = b.to(cuda).requires_grad_(True)
+    lp, ent = sparse_score(Xg, Wg, bg, pack_mask(m).to(cuda), a.to(cuda), head)
+    Xr = X.float().clone().requires_grad_(True)
+    Wr = W.bfloat16().float().clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    logits = Xr @ Wr.T + br
+    _, lpr, entr = cell_head.cell_head_torch(logits, m, a)
+    torch.testing.assert_close(lp.cpu(), lpr, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(ent.cpu(), entr, rtol=1e-4, atol=2e-3)
+    gl, ge = torch.randn(F), torch.randn(F)
+    ((lp * gl.to(cuda)).sum() + (ent * ge.to(cuda)).sum()).backward()
+    ((lpr * gl).sum() + (entr * ge).sum()).backward()
+    rel = lambda x, y: ((x - y).norm() / (y.norm() + 1e-12)).item()  # noqa: E731
+    assert rel(bg.grad.cpu(), br.grad) < 1e-3
+    assert rel(Wg.grad.cpu(), Wr.grad) < 1e-2  # dZ rounded to bf16 for the MFMA
+    assert rel(Xg.grad.float().cpu(), Xr.grad) < 1.5e-2
+    # deterministic: a second identical call gives bit-identical gradients
+    g1 = Wg.grad.clone()
+    Wg.grad = None
+    lp2, ent2 = sparse_score(Xg, Wg, bg, pack_mask(m).to(cuda), a.to(cuda), head)
+    ((lp2 * gl.to(cuda)).sum() + (ent2 * ge.to(cuda)).sum()).backward()
+    assert torch.equal(g1, Wg.grad)
+
+
+def test_sparse_sample(cuda):
+    F, S = 500, 256
+    X, W, b, m, _ = _problem(F, S, seed=3)
+    head = SparseHead(S, cuda)
+    rng = torch.tensor([7, 0], dtype=torch.int64, device=cuda)
+    mb = pack_mask(m).to(cuda)
+    a, lp = sparse_sample(X.to(cuda), W.to(cuda), b.to(cuda), mb, rng, head)
+    assert int(rng[1].item()) == 1
+    act = m.any(-1).to(cuda)
+    assert torch.all(a[~act] == 0)
+    for k in range(7):
+        o0, o1 = cell_head.OFFS[k], cell_head.OFFS[k + 1]
+        seg = m[..., o0:o1].to(cuda)
+        has = seg.any(-1)
+        ok = seg.gather(-1, a[..., k:k + 1].long()).squeeze(-1) | ~has
+        assert bool(ok.all())
+    lp2, _ = sparse_score(X.to(cuda), W.to(cuda), b.to(cuda), mb, a, head)
+    torch.testing.assert_close(lp, lp2, rtol=1e-5, atol=1e-4)
