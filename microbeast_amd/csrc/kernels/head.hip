@@ -73,7 +73,11 @@ __global__ __launch_bounds__(256) void head_count_kernel(const uint32_t* __restr
 
 // exclusive scan in (c, b) order + per-cell groups + 16-pair unit list
 constexpr int CHUNK = 512;  // pairs per backward work item (heavy cells are split)
+constexpr int MAX_S = 1024; // cells per map supported by the single-block scan (32x32)
 
+// Exclusive scan in (c, b) order + per-cell groups + 16-pair unit list + CHUNK list.
+// One workgroup: a wave owns a cell at a time (lanes split its frame blocks), then a
+// block-wide scan over per-cell totals. All loops are lane-parallel.
 __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__ cnt, int S, int nfb,
                                                          int* __restrict__ off,
                                                          int* __restrict__ grp_start,
@@ -84,61 +88,75 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
                                                          int* __restrict__ chunk_row,
                                                          int* __restrict__ chunk_start,
                                                          int* __restrict__ totals /* [3] */) {
-  __shared__ int part[1024];
-  __shared__ int upart[1024];
-  __shared__ int cpart[1024];
-  const int tid = threadIdx.x;
-  // each thread owns a contiguous range of cells
-  const int per = (S + 1023) / 1024;
-  const int c0 = min(S, tid * per), c1 = min(S, c0 + per);
-  int s = 0, u = 0, q = 0;
-  for (int c = c0; c < c1; ++c) {
+  __shared__ int tot[MAX_S], ust[MAX_S], cst[MAX_S];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  // phase 1: per-cell totals
+  for (int c = wave; c < S; c += nw) {
     int n = 0;
-    for (int b = 0; b < nfb; ++b) n += cnt[c * nfb + b];
-    s += n;
-    u += (n + 15) / 16;
-    q += (n + CHUNK - 1) / CHUNK;
+    for (int b = lane; b < nfb; b += 64) n += cnt[c * nfb + b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+    if (lane == 0) tot[c] = n;
   }
-  part[tid] = s;
-  upart[tid] = u;
-  cpart[tid] = q;
   __syncthreads();
-  // Hillis-Steele inclusive scans (1024 entries)
+  // phase 2: exclusive scans of pairs, 16-pair units and chunks over cells
+  int v = 0, u = 0, q = 0;
+  if (tid < S) {
+    v = tot[tid];
+    u = (v + 15) / 16;
+    q = (v + CHUNK - 1) / CHUNK;
+  }
+  __shared__ int sv[1024], su[1024], sq[1024];
+  sv[tid] = v; su[tid] = u; sq[tid] = q;
+  __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
-    int a = tid >= o ? part[tid - o] : 0, bq = tid >= o ? upart[tid - o] : 0;
-    int cq = tid >= o ? cpart[tid - o] : 0;
+    const int a = tid >= o ? sv[tid - o] : 0, b = tid >= o ? su[tid - o] : 0,
+              d = tid >= o ? sq[tid - o] : 0;
     __syncthreads();
-    part[tid] += a;
-    upart[tid] += bq;
-    cpart[tid] += cq;
+    sv[tid] += a; su[tid] += b; sq[tid] += d;
     __syncthreads();
   }
-  int pos = part[tid] - s, upos = upart[tid] - u, cpos = cpart[tid] - q;
-  for (int c = c0; c < c1; ++c) {
-    grp_start[c] = pos;
-    int n = 0;
-    for (int b = 0; b < nfb; ++b) {
-      off[c * nfb + b] = pos + n;
-      n += cnt[c * nfb + b];
-    }
-    grp_count[c] = n;
-    for (int r = 0; r < n; r += 16) {
-      unit_cell[upos] = c;
-      unit_row[upos] = pos + r;
-      ++upos;
-    }
-    chunk_start[c] = cpos;
-    for (int r = 0; r < n; r += CHUNK) {
-      chunk_cell[cpos] = c;
-      chunk_row[cpos] = pos + r;
-      ++cpos;
-    }
-    pos += n;
+  if (tid < S) {
+    const int gs = sv[tid] - v;
+    grp_start[tid] = gs;
+    grp_count[tid] = v;
+    chunk_start[tid] = sq[tid] - q;
+    tot[tid] = gs;            // reuse: group start
+    ust[tid] = su[tid] - u;   // unit start
+    cst[tid] = sq[tid] - q;   // chunk start
   }
   if (tid == 1023) {
-    totals[0] = part[1023];
-    totals[1] = upart[1023];
-    totals[2] = cpart[1023];
+    totals[0] = sv[1023];
+    totals[1] = su[1023];
+    totals[2] = sq[1023];
+  }
+  __syncthreads();
+  // phase 3: per-cell frame-block offsets (wave scan with carry) + unit / chunk lists
+  for (int c = wave; c < S; c += nw) {
+    int carry = tot[c];
+    for (int b0 = 0; b0 < nfb; b0 += 64) {
+      const int b = b0 + lane;
+      const int x = b < nfb ? cnt[c * nfb + b] : 0;
+      int incl = x;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      if (b < nfb) off[c * nfb + b] = carry + incl - x;
+      carry += __shfl(incl, 63, 64);
+    }
+    const int gs = tot[c], n = sv[c] - gs;  // inclusive scan - start (LDS, no global re-read)
+    for (int r = lane * 16; r < n; r += 64 * 16) {
+      const int k = ust[c] + r / 16;
+      unit_cell[k] = c;
+      unit_row[k] = gs + r;
+    }
+    for (int r = lane * CHUNK; r < n; r += 64 * CHUNK) {
+      const int k = cst[c] + r / CHUNK;
+      chunk_cell[k] = c;
+      chunk_row[k] = gs + r;
+    }
   }
 }
 
@@ -503,6 +521,7 @@ extern "C" int mbk_head_compact(const uint32_t* mask, int F, int S, int* cnt, in
                                 int* chunk_cell, int* chunk_row, int* chunk_start,
                                 int* totals, int* pairs, int* pidx, uint8_t* action_zero,
                                 float* cell_lp, float* cell_ent, hipStream_t stream) {
+  if (S > MAX_S) return (int)hipErrorInvalidValue;
   const int FB = mbk_head_fb(F);
   const int nfb = (F + FB - 1) / FB;
   dim3 g1(nfb, (S + 255) / 256);
