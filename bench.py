@@ -40,6 +40,9 @@ def parse(argv=None):
     p.add_argument("--threads", type=int, default=0, help="env worker threads per rank (0=auto)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--verbose", action="store_true", help="per-step progress on stderr")
+    p.add_argument("--learner_cu_reserve", type=int, default=0,
+                   help="run the learner on a CU-masked stream leaving every k-th CU to the "
+                        "policy stream (0 = off)")
     p.add_argument("--profile_phases", action="store_true",
                    help="also report per-phase learner timings (adds syncs; not for the headline)")
     return p.parse_args(argv)
@@ -76,6 +79,12 @@ def main(argv=None):
                          env_index_base=info.rank * envs_total)
     rt.start(learner.flat)
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
+    if args.learner_cu_reserve > 0:
+        from microbeast_amd import _native as N
+        h = N.runtime().create_cu_masked_stream(dev.index, args.learner_cu_reserve)
+        learner_stream = torch.cuda.ExternalStream(h, device=dev)
+        learner_stream.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(learner_stream)
 
     nstep = [0]
 

@@ -65,6 +65,8 @@ _SIGS = {
                      c_void_p, c_void_p],
     "mbk_head_dx_gather": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "mbk_head_pack": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mbk_decode_obs_mask": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
 }
 
 

@@ -1,23 +1,21 @@
 // Synthetic gym-microRTS simulator. See microrts_sim.h for the contract.
 #include "microrts_sim.h"
+#include "../include/microrts_rules.h"
 #include <algorithm>
 #include <cstring>
 #include <cstdlib>
 
 namespace mb {
 
-//                       hp cost dmg rng move atk produce
-const UnitSpec kSpec[8] = {
-    {0, 0, 0, 0, 0, 0, 0},      // none
-    {1, 0, 0, 0, 0, 0, 0},      // resource
-    {16, 10, 0, 0, 0, 0, 60},   // base
-    {6, 5, 0, 0, 0, 0, 40},     // barracks
-    {1, 1, 1, 1, 4, 3, 14},     // worker
-    {4, 2, 2, 1, 3, 3, 22},     // light
-    {4, 3, 4, 1, 5, 3, 30},     // heavy
-    {1, 2, 1, 3, 4, 3, 26},     // ranged
-};
-static constexpr int kHarvestT = 5, kReturnT = 3;
+// single source of truth shared with the GPU mask kernel (include/microrts_rules.h)
+#define MB_SPEC(t)                                                                          \
+  {(int16_t)mbr::spec_hp(t), (int16_t)mbr::spec_cost(t), (int16_t)mbr::spec_damage(t),      \
+   (int16_t)mbr::spec_range(t), (int16_t)mbr::spec_move_t(t), (int16_t)mbr::spec_attack_t(t), \
+   (int16_t)mbr::spec_produce_t(t)}
+const UnitSpec kSpec[8] = {MB_SPEC(0), MB_SPEC(1), MB_SPEC(2), MB_SPEC(3),
+                           MB_SPEC(4), MB_SPEC(5), MB_SPEC(6), MB_SPEC(7)};
+#undef MB_SPEC
+static constexpr int kHarvestT = mbr::kHarvestT, kReturnT = mbr::kReturnT;
 static constexpr int kDX[4] = {0, 1, 0, -1};
 static constexpr int kDY[4] = {-1, 0, 1, 0};
 
@@ -37,6 +35,7 @@ MicroRTSSim::MicroRTSSim(int size, int max_steps, int bot, uint64_t seed, const 
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
   rng_ = (z ^ (z >> 31)) | 1ull;
   grid_.assign(s_ * s_, -1);
+  act_buf_.assign((size_t)s_ * s_ * kActComps, 0);
   mask_.assign(s_ * s_ * kMaskWords, 0u);
   mask_p1_.assign(s_ * s_ * kMaskWords, 0u);
   opp_actions_.assign(s_ * s_ * kActComps, 0);
@@ -90,7 +89,7 @@ void MicroRTSSim::reset() {
     add_unit(WORKER, p, X(o), Y(b == 1 ? 0 : o), 0);
     if (s_ >= 12) add_unit(WORKER, p, X(b + 1), Y(b), 0);
   }
-  compute_mask(0, mask_);
+  if (validate_) compute_mask(0, mask_);
   if (external_opp_) compute_mask(1, mask_p1_);
 }
 
@@ -243,8 +242,8 @@ bool MicroRTSSim::exec(int uid, const uint8_t* a, float* rw) {
       resources_[player] -= kSpec[t].cost;
       int nu = add_unit(t, player, nx, ny);
       Unit& uu = units_[uid];  // add_unit may reallocate
-      units_[nu].busy = kSpec[t].produce_t;  // "under construction"
-      units_[nu].act = A_NOOP;
+      units_[nu].busy = kSpec[t].produce_t;  // under construction: shown as "produce"
+      units_[nu].act = A_PRODUCE;            // so busy > 0 <=> act != noop (GPU mask relies on it)
       uu.busy = kSpec[t].produce_t; uu.act = A_PRODUCE;
       if (rw) {
         if (t == WORKER) rw[R_WORKER] += 1.f;
@@ -475,6 +474,10 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
     const Unit& u = units_[g];
     if (u.owner != 0 || u.busy > 0) continue;
     const uint8_t* a = actions + (size_t)c * kActComps;
+    if (!validate_) {  // the mask lives on the GPU; exec() re-checks feasibility itself
+      if (a[0] < 6) exec(g, a, rw);
+      continue;
+    }
     const uint32_t* m = &mask_[(size_t)c * kMaskWords];
     if (a[0] >= 6 || !getbit(m, a[0])) continue;
     // the chosen type's parameter must be legal too
@@ -536,10 +539,28 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
   if (d) {
     reset();
   } else {
-    compute_mask(0, mask_);
+    if (validate_) compute_mask(0, mask_);
     if (external_opp_) compute_mask(1, mask_p1_);
   }
   return r;
+}
+
+float MicroRTSSim::step_packed(const uint16_t* env_actions, bool* done) {
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c) mbr::unpack_env_action(env_actions[c], &act_buf_[(size_t)c * kActComps]);
+  return step(act_buf_.data(), done, nullptr);
+}
+
+void MicroRTSSim::write_obs_codes(uint16_t* out) const {
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c) {
+    const int g = grid_[c];
+    if (g < 0) { out[c] = mbr::cell_code(0, 0, 0, 0, 0); continue; }
+    const Unit& u = units_[g];
+    const int own = u.owner < 0 ? 0 : (u.owner == 0 ? 1 : 2);
+    out[c] = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
+                            std::min<int>(std::max<int>(u.res, 0), 4), own, u.type, u.act);
+  }
 }
 
 // ---------------------------------------------------------------- observations

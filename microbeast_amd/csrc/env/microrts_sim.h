@@ -80,6 +80,13 @@ class MicroRTSSim {
   void write_obs_p1(uint32_t* out) const;
   void write_mask_p1(uint32_t* out) const;
   void set_opponent_actions(const uint8_t* actions_p1);
+  // GPU-engine fast path: 16-bit cell codes out, 16-bit packed env actions in, and no
+  // CPU-side mask (the GPU derives it from the codes + resources, see
+  // include/microrts_rules.h); exec() still validates every action's feasibility.
+  void set_validate(bool on) { validate_ = on; if (on) compute_mask(0, mask_); }
+  float step_packed(const uint16_t* env_actions, bool* done);
+  void write_obs_codes(uint16_t* out) const;
+  int resources(int player) const { return resources_[player]; }
 
  private:
   int s_, max_steps_, bot_;
@@ -89,6 +96,8 @@ class MicroRTSSim {
   int resources_[2] = {0, 0};
   int last_winner_ = -1;
   bool external_opp_ = false;
+  bool validate_ = true;
+  std::vector<uint8_t> act_buf_;
   std::vector<Unit> units_;
   std::vector<int16_t> grid_;     // unit index per cell, -1 empty
   std::vector<uint32_t> mask_;    // cached agent mask (s*s*3)

@@ -7,6 +7,8 @@
 
 #include <memory>
 
+#include <hip/hip_runtime_api.h>
+
 #include "engine.h"
 #include "shm_ring.h"
 #include "vec_env.h"
@@ -100,7 +102,23 @@ PYBIND11_MODULE(_mbrt, m) {
              for (int i = 0; i < e.env->num_envs(); ++i)
                e.env->sim(i).set_opponent_actions(P<uint8_t>(act) + i * S * kActComps);
            })
-      .def("ticks", [](PyVecEnv& e, int i) { return e.env->sim(i).ticks(); });
+      .def("ticks", [](PyVecEnv& e, int i) { return e.env->sim(i).ticks(); })
+      .def("set_validate", [](PyVecEnv& e, bool on) { e.env->set_validate(on); })
+      .def("obs_codes",
+           [](PyVecEnv& e, uintptr_t codes, uintptr_t res) {
+             const size_t S = (size_t)e.env->size() * e.env->size();
+             for (int i = 0; i < e.env->num_envs(); ++i) {
+               e.env->sim(i).write_obs_codes(P<uint16_t>(codes) + i * S);
+               P<int32_t>(res)[i] = e.env->sim(i).resources(0);
+             }
+           })
+      .def("step_codes",
+           [](PyVecEnv& e, uintptr_t act16, uintptr_t codes, uintptr_t res, uintptr_t rew,
+              uintptr_t done) {
+             py::gil_scoped_release g;
+             e.env->step_range_codes(0, e.env->num_envs(), P<uint16_t>(act16), P<uint16_t>(codes),
+                                     P<int32_t>(res), P<float>(rew), P<uint8_t>(done), &e.log);
+           });
 
   py::class_<IndexRing>(m, "IndexRing")
       .def(py::init([](uintptr_t addr, size_t cap, bool init) {
@@ -150,6 +168,24 @@ PYBIND11_MODULE(_mbrt, m) {
         py::arg("ver"), py::arg("src"), py::arg("dst"), py::arg("nbytes"),
         py::arg("max_tries") = 1000);
 
+  // A stream restricted to a subset of CUs (MI355X: 256 CUs in 8 XCDs). Used for the
+  // learner so that every `reserve_every`-th CU stays free for the latency-critical
+  // policy stream; CU ids are spread so every XCD / shader engine keeps some free.
+  m.def("create_cu_masked_stream", [](int device, int reserve_every) -> uintptr_t {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+      throw std::runtime_error("hipGetDeviceProperties failed");
+    const int ncu = prop.multiProcessorCount;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int i = 0; i < ncu; ++i)
+      if (reserve_every <= 0 || (i % reserve_every) != 0) mask[i / 32] |= 1u << (i % 32);
+    hipSetDevice(device);
+    hipStream_t st = nullptr;
+    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess)
+      throw std::runtime_error("hipExtStreamCreateWithCUMask failed");
+    return (uintptr_t)st;
+  });
+
   py::class_<GpuEngine>(m, "GpuEngine")
       .def(py::init([](py::dict c, py::dict b) {
         EngineConfig cfg;
@@ -178,6 +214,9 @@ PYBIND11_MODULE(_mbrt, m) {
         buf.out_action = b["out_action"].cast<uintptr_t>();
         buf.out_logp = b["out_logp"].cast<uintptr_t>();
         buf.out_value = b["out_value"].cast<uintptr_t>();
+        buf.in_codes = b["in_codes"].cast<uintptr_t>();
+        buf.in_res = b["in_res"].cast<uintptr_t>();
+        buf.out_act16 = b["out_act16"].cast<uintptr_t>();
         return new GpuEngine(cfg, buf);
       }))
       .def("start", &GpuEngine::start, py::arg("graph_exec"))

@@ -46,17 +46,18 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   int prio_least = 0, prio_greatest = 0;
   CTOR_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
   CTOR_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_greatest));
-  CTOR_CHECK(hipHostMalloc((void**)&h_obs_, (size_t)total * S_ * 4, hipHostMallocDefault));
-  CTOR_CHECK(hipHostMalloc((void**)&h_mask_, (size_t)total * S_ * 4 * kMaskWords,
-                           hipHostMallocDefault));
-  CTOR_CHECK(hipHostMalloc((void**)&h_action_, (size_t)total * S_ * kActComps,
-                           hipHostMallocDefault));
+  if (!buf_.in_codes || !buf_.in_res || !buf_.out_act16)
+    throw std::runtime_error("GpuEngine: in_codes / in_res / out_act16 buffers required");
+  CTOR_CHECK(hipHostMalloc((void**)&h_codes_, (size_t)total * S_ * 2, hipHostMallocDefault));
+  CTOR_CHECK(hipHostMalloc((void**)&h_res_, (size_t)total * 4, hipHostMallocDefault));
+  CTOR_CHECK(hipHostMalloc((void**)&h_act16_, (size_t)total * S_ * 2, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_reward_, (size_t)total * 4, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_done_, (size_t)total, hipHostMallocDefault));
   CTOR_CHECK(hipMalloc((void**)&d_rd_, E * 4 + E + 64));
   std::memset(h_reward_, 0, (size_t)total * 4);
   std::memset(h_done_, 0, (size_t)total);
-  env_->reset(h_obs_, h_mask_);
+  env_->set_validate(false);  // masks are derived on the GPU from the codes
+  env_->reset_codes(h_codes_, h_res_);
   for (int g = 0; g < cfg_.n_groups; ++g) {
     groups_.emplace_back(new Group());
     CTOR_CHECK(hipEventCreateWithFlags(&groups_[g]->ev, hipEventDisableTiming));
@@ -87,9 +88,9 @@ GpuEngine::~GpuEngine() {
   if (pub_ready_) hipEventDestroy(pub_ready_);
   if (pub_consumed_) hipEventDestroy(pub_consumed_);
   if (pub_staging_) hipFree(pub_staging_);
-  if (h_obs_) hipHostFree(h_obs_);
-  if (h_mask_) hipHostFree(h_mask_);
-  if (h_action_) hipHostFree(h_action_);
+  if (h_codes_) hipHostFree(h_codes_);
+  if (h_res_) hipHostFree(h_res_);
+  if (h_act16_) hipHostFree(h_act16_);
   if (h_reward_) hipHostFree(h_reward_);
   if (h_done_) hipHostFree(h_done_);
   if (d_rd_) hipFree(d_rd_);
@@ -157,8 +158,8 @@ void GpuEngine::worker_loop(int wid) {
         int e1 = std::min(e + chunk_, E);
         const int a0 = g * E;
         auto t0 = std::chrono::steady_clock::now();
-        env_->step_range(a0 + e, a0 + e1, 0, h_action_, h_obs_, h_mask_, h_reward_, h_done_,
-                         nullptr, nullptr, &log_);
+        env_->step_range_codes(a0 + e, a0 + e1, h_act16_, h_codes_, h_res_, h_reward_, h_done_,
+                               &log_);
         env_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                               std::chrono::steady_clock::now() - t0).count(),
                           std::memory_order_relaxed);
@@ -200,10 +201,10 @@ bool GpuEngine::enqueue_gpu(int g) {
     }
   }
   const size_t e0 = (size_t)g * E;
-  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_obs, h_obs_ + e0 * S_, E * S_ * 4,
+  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
                            hipMemcpyHostToDevice, stream_));
-  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_mask, h_mask_ + e0 * S_ * kMaskWords,
-                           E * S_ * 4 * kMaskWords, hipMemcpyHostToDevice, stream_));
+  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
+                           stream_));
   if (!G.first) {
     ENG_CHECK(hipMemcpyAsync(d_rd_, h_reward_ + e0, E * 4, hipMemcpyHostToDevice, stream_));
     ENG_CHECK(hipMemcpyAsync(d_rd_ + E * 4, h_done_ + e0, E, hipMemcpyHostToDevice, stream_));
@@ -256,8 +257,8 @@ bool GpuEngine::enqueue_gpu(int g) {
     full_cv_.notify_all();
     G.prev = -1;
   }
-  ENG_CHECK(hipMemcpyAsync(h_action_ + e0 * S_ * kActComps, (const void*)buf_.out_action,
-                           E * S_ * kActComps, hipMemcpyDeviceToHost, stream_));
+  ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)buf_.out_act16, E * S_ * 2,
+                           hipMemcpyDeviceToHost, stream_));
   ENG_CHECK(hipEventRecord(G.ev, stream_));
   gpu_steps_.fetch_add(1);
   G.t += 1;

@@ -61,8 +61,10 @@ struct EngineBuffers {
   uintptr_t value = 0;    // f32
   uintptr_t reward = 0;   // f32
   uintptr_t done = 0;     // u8
-  // inference graph I/O (fixed addresses)
+  // inference graph I/O (fixed addresses). The graph decodes in_codes/in_res into
+  // in_obs / in_mask (GPU-side mask) and packs out_action into out_act16.
   uintptr_t in_obs = 0, in_mask = 0, out_action = 0, out_logp = 0, out_value = 0;
+  uintptr_t in_codes = 0, in_res = 0, out_act16 = 0;
 };
 
 struct EngineStats {
@@ -116,11 +118,11 @@ class GpuEngine {
   hipGraphExec_t graph_ = nullptr;
   std::vector<std::unique_ptr<Group>> groups_;
   // pinned staging, all envs contiguous
-  uint32_t* h_obs_ = nullptr;
-  uint32_t* h_mask_ = nullptr;
+  uint16_t* h_codes_ = nullptr;  // 16-bit cell codes
+  int32_t* h_res_ = nullptr;     // player resources (GPU mask input)
   float* h_reward_ = nullptr;
   uint8_t* h_done_ = nullptr;
-  uint8_t* h_action_ = nullptr;
+  uint16_t* h_act16_ = nullptr;  // packed env actions
   uint8_t* d_rd_ = nullptr;  // device staging for reward+done of one group
 
   // slots

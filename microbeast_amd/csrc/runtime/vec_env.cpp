@@ -49,6 +49,41 @@ void VecEnv::step_range(int e0, int e1, int base, const uint8_t* actions, uint32
   }
 }
 
+void VecEnv::set_validate(bool on) {
+  for (auto& s : sims_) s->set_validate(on);
+}
+
+void VecEnv::reset_codes(uint16_t* codes, int32_t* res) {
+  const size_t S = (size_t)size_ * size_;
+  for (size_t i = 0; i < sims_.size(); ++i) {
+    sims_[i]->reset();
+    ep_ret_[i] = 0.f;
+    ep_len_[i] = 0;
+    if (codes) sims_[i]->write_obs_codes(codes + i * S);
+    if (res) res[i] = sims_[i]->resources(0);
+  }
+}
+
+void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t* codes,
+                              int32_t* res, float* reward, uint8_t* done, EpisodeLog* log) {
+  const size_t S = (size_t)size_ * size_;
+  for (int i = e0; i < e1; ++i) {
+    bool d = false;
+    const float r = sims_[i]->step_packed(actions + (size_t)i * S, &d);
+    ep_ret_[i] += r;
+    ep_len_[i] += 1;
+    if (d) {
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner()});
+      ep_ret_[i] = 0.f;
+      ep_len_[i] = 0;
+    }
+    reward[i] = r;
+    done[i] = d ? 1 : 0;
+    sims_[i]->write_obs_codes(codes + (size_t)i * S);
+    res[i] = sims_[i]->resources(0);
+  }
+}
+
 void VecEnv::dense_obs(float* out) const {
   const size_t S = (size_t)size_ * size_;
   for (size_t i = 0; i < sims_.size(); ++i) sims_[i]->write_obs_dense(out + i * S * kPlanes);

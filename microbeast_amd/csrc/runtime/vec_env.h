@@ -54,6 +54,12 @@ class VecEnv {
   void step_range(int e0, int e1, int base, const uint8_t* actions, uint32_t* obs,
                   uint32_t* mask, float* reward, uint8_t* done, float* ep_return,
                   int32_t* ep_step, EpisodeLog* log);
+  // GPU-engine fast path (16-bit cell codes + per-env resources out, packed 16-bit env
+  // actions in, no CPU mask): 0.5 KB H2D + 0.5 KB D2H per 16x16 env step.
+  void set_validate(bool on);
+  void reset_codes(uint16_t* codes, int32_t* res);
+  void step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t* codes, int32_t* res,
+                        float* reward, uint8_t* done, EpisodeLog* log);
   // Dense reference layout for parity tools: obs f32 (n,s,s,27), mask u8 (n,s*s*78)
   void dense_obs(float* out) const;
   void dense_mask(uint8_t* out) const;

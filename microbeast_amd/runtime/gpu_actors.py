@@ -6,6 +6,9 @@ processes (microbeast.py:30-105, 179-191) and get_batch (libs/utils.py:166-218):
 * rollout slots are allocated once in HBM, time-major ``[n_slots, T+1, E, ...]``
   with compact dtypes (obs uint32 bit planes, mask 3 x uint32 bits, actions
   uint8) — ~6 KB per 16x16 frame instead of ~170 KB in the reference layout;
+* PCIe carries only 16-bit cell codes + the resource count in and one packed
+  16-bit action per cell out (~1 KB per env step); the observation planes and
+  the 78-bit action masks are derived on the GPU (``obs_mask.hip``);
 * the policy step (encoder + head + masked sampling) for one env group is
   captured once into a hipGraph; the C++ driver thread replays it, so acting
   costs no Python and no GIL;
@@ -68,6 +71,11 @@ class GpuActorRuntime:
             "done": torch.zeros(NS, T1, E, dtype=torch.uint8, device=dev),
         }
         self.io = {
+            # what crosses PCIe: 16-bit cell codes + resources in, packed actions out
+            "in_codes": torch.zeros(E, S, dtype=torch.int16, device=dev),
+            "in_res": torch.zeros(E, dtype=torch.int32, device=dev),
+            "out_act16": torch.zeros(E, S, dtype=torch.int16, device=dev),
+            # decoded on the GPU inside the policy graph
             "in_obs": torch.zeros(E, S, dtype=torch.int32, device=dev),
             "in_mask": torch.zeros(E, S, 3, dtype=torch.int32, device=dev),
             "out_action": torch.zeros(E, S, 7, dtype=torch.uint8, device=dev),
@@ -99,6 +107,11 @@ class GpuActorRuntime:
     def _policy_step(self):
         io = self.io
         m = self.infer_model
+        k = N.kernels()
+        st = N.stream_ptr()
+        N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(), self.E,
+                                      self.size, self.size, io["in_obs"].data_ptr(),
+                                      io["in_mask"].data_ptr(), st), "decode_obs_mask")
         if hasattr(m, "_use_hip") and m._use_hip(io["in_obs"]):
             _, _, value = m.act(io["in_obs"], io["in_mask"], self.rng,
                                 action_out=io["out_action"], logp_out=io["out_logp"])
@@ -107,6 +120,9 @@ class GpuActorRuntime:
             cell_head.sample_gpu(logits, io["in_mask"], self.rng, action_out=io["out_action"],
                                  cell_logp=self._cell_logp, logp_out=io["out_logp"])
         io["out_value"].copy_(value)
+        N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
+                                       io["out_act16"].data_ptr(), N.stream_ptr()),
+                "pack_env_actions")
 
     def _capture(self):
         s = torch.cuda.Stream(device=self.device)
