@@ -32,7 +32,7 @@ def main():
     dev = torch.device("cuda", 0)
     s = a.size
     mk = lambda: Agent((s, s, 27))  # noqa: E731
-    for E in [int(x) for x in a.E.split(",")]:
+    for E in [int(x) for x in a.E.split(",") if x]:
         rt = GpuActorRuntime(mk, s, 1, E, 8, 1, dev, n_threads=1)
         # realistic inputs: run the env once to get observations / masks
         env = rt.engine.env  if hasattr(rt.engine, "env") else None  # noqa: F841
