@@ -29,6 +29,8 @@
 #include "../include/mbk_api.h"
 #include "common.h"
 
+#include <algorithm>
+
 using namespace mbk;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -75,150 +77,225 @@ struct ConvFwdArgs {
 };
 
 // ------------------------------------------------------------------ forward / dgrad
+// Persistent: the grid is sized to the CUs' occupancy and each workgroup walks image
+// groups blockIdx.x, +gridDim.x, ... holding the weights in VGPRs for the whole launch
+// (a per-group launch re-read all B fragments from L2 for every 1-16 images). The next
+// group's interior pixels are loaded into registers (kPF per thread) while the current
+// group computes; the halo ring of the LDS tile is zeroed once and never rewritten.
+// MFMA operands are (A = weights, B = pixels), so a lane's accumulators are 4
+// consecutive channels of one pixel and the epilogue moves 8-byte vectors.
+constexpr int kPF = 8;
+
+template <int CIN, bool BITS>
+__device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
+  // interior staging element e -> byte offset of its slot in the halo'd LDS tile
+  const int Hp = H + 2, Wp = W + 2, HW = H * W;
+  if (BITS) {
+    const int im = e / HW, r = e - im * HW, y = r / W, x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * 4;
+  } else {
+    constexpr int CH16 = CIN / 8;
+    const int q = e % CH16, p = e / CH16;
+    const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * Geo<CIN>::PIXB + q * 16;
+  }
+}
+
 template <int CIN, int COUT, bool BITS>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NCH = Geo<CIN>::NCH;
   constexpr int PIXB = BITS ? 4 : Geo<CIN>::PIXB;
   constexpr int NB = COUT / 16;
+  constexpr int EPP = BITS ? 1 : CIN / 8;  // staging elements per pixel (u32 / uint4)
+  constexpr int OSTR = COUT + 4;           // pool staging row stride (floats, bank spread)
   const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
-  const int img0 = blockIdx.x * a.imgs;
-  const int nimg = min(a.imgs, a.N - img0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
   char* tile = smem;
   const int tile_bytes = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
+  float* otile = (float*)(smem + tile_bytes);  // pool staging [imgs*HW][OSTR] fp32
+  const int ngroups = (a.N + a.imgs - 1) / a.imgs;
+  const int per_grp = a.imgs * HW * EPP;
 
-  // ---- stage halo'd input tile
-  if (BITS) {
-    const uint32_t* xb = (const uint32_t*)a.x + (size_t)img0 * HW;
-    uint32_t* t32 = (uint32_t*)tile;
-    const int tot = nimg * Hp * Wp;
-    for (int e = tid; e < tot; e += kThreads) {
-      const int im = e / (Hp * Wp), r = e - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
-      const int y = py - 1, x = px - 1;
-      t32[e] = (y >= 0 && y < H && x >= 0 && x < W) ? xb[im * HW + y * W + x] : 0u;
-    }
-  } else {
-    constexpr int CH16 = CIN / 8;  // 16-byte chunks per pixel
-    const uint4* xg = (const uint4*)((const bf16*)a.x + (size_t)img0 * HW * CIN);
-    const int tot = nimg * Hp * Wp * CH16;
-    for (int e = tid; e < tot; e += kThreads) {
-      const int q = e % CH16, pos = e / CH16;
-      const int im = pos / (Hp * Wp), r = pos - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
-      const int y = py - 1, x = px - 1;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (y >= 0 && y < H && x >= 0 && x < W) {
-        v = xg[(im * HW + y * W + x) * CH16 + q];
-        if (a.relu_in) {
-          v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
-          v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
-        }
-      }
-      *(uint4*)(tile + pos * PIXB + q * 16) = v;
-    }
+  for (int e = tid; e < tile_bytes / 16; e += kThreads) ((uint4*)tile)[e] = make_uint4(0, 0, 0, 0);
+  int loff[kPF];
+#pragma unroll
+  for (int k = 0; k < kPF; ++k) {
+    const int e = tid + k * kThreads;
+    loff[k] = e < per_grp ? fwd_lds_off<CIN, BITS>(e, H, W) : 0;
   }
-
-  // ---- weights -> registers (B fragments): lane holds w[co = nb*16 + lane&15][c][8g..8g+7]
+  // ---- weights -> registers (A fragments): lane holds w[co = nb*16 + li][c][8g..8g+7]
   Frag8 bw[NCH][NB];
-  {
-    const int g = lane >> 4, col = lane & 15;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const uint4* wp = (const uint4*)(a.w + (size_t)(nb * 16 + col) * NCH * 32 + g * 8);
+  for (int nb = 0; nb < NB; ++nb) {
+    const uint4* wp = (const uint4*)(a.w + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
-    }
+    for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
   }
-  float bias_v[NB];
+  float bias_v[NB][4];
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) bias_v[nb] = a.bias ? a.bias[nb * 16 + (lane & 15)] : 0.f;
-  __syncthreads();
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias_v[nb][i] = a.bias ? a.bias[nb * 16 + 4 * g + i] : 0.f;
 
-  float* otile = (float*)(smem + tile_bytes);  // pool staging [nimg][H][W][COUT] fp32
-  const int M = nimg * HW;
-  const int nblk = (M + 15) >> 4;
-  const size_t gpix0 = (size_t)img0 * HW;
-  const int g = lane >> 4;
-  for (int pb = wave; pb < nblk; pb += kThreads / 64) {
-    const int m = pb * 16 + (lane & 15);
-    const bool valid = m < M;
-    const int mm = valid ? m : 0;
-    const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
-    const int base_pos = (im * Hp + y) * Wp + x;  // padded position of tap (0,0)
-    f32x4 acc[NB];
+  // ---- register prefetch of one group's interior pixels
+  uint4 pv[kPF];
+  uint32_t pw[kPF];
+  auto prefetch = [&](int grp) {
+    const size_t base = (size_t)grp * per_grp;
+    const int lim = min(per_grp, (a.N - grp * a.imgs) * HW * EPP);
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      Frag8 av;
-      int tap, ch0;
-      if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
-      else { tap = c; ch0 = 8 * g; }
-      const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
-      const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
-      if (BITS) {
-        const uint32_t bits = ((const uint32_t*)tile)[pos] >> ch0;
-        uint32_t w4[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
-                  (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
-        av.u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-      } else {
-        av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
-      }
-      if (!valid || (CIN == 16 && tap >= 9)) av.u = make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av.v, bw[c][nb].v, acc[nb], 0, 0, 0);
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      if (BITS) pw[k] = e < lim ? ((const uint32_t*)a.x)[base + e] : 0u;
+      else pv[k] = e < lim ? ((const uint4*)a.x)[base + e] : make_uint4(0, 0, 0, 0);
     }
-    // ---- epilogue: lane holds rows 4g+i (pixels), col lane&15 (channel)
+  };
+  auto put = [&](int off, uint4 v) {
+    if (a.relu_in) {
+      v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
+      v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
+    }
+    *(uint4*)(tile + off) = v;
+  };
+  if ((int)blockIdx.x < ngroups) prefetch(blockIdx.x);
+  __syncthreads();  // halo zeros visible
+
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * a.imgs;
+    const int nimg = min(a.imgs, a.N - img0);
+    const int lim = nimg * HW * EPP;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int co = nb * 16 + (lane & 15);
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      if (e < lim) {
+        if (BITS) *(uint32_t*)(tile + loff[k]) = pw[k];
+        else put(loff[k], pv[k]);
+      }
+    }
+    for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
+      const size_t src = (size_t)grp * per_grp + e;
+      if (BITS) *(uint32_t*)(tile + fwd_lds_off<CIN, BITS>(e, H, W)) = ((const uint32_t*)a.x)[src];
+      else put(fwd_lds_off<CIN, BITS>(e, H, W), ((const uint4*)a.x)[src]);
+    }
+    __syncthreads();
+    if (grp + (int)gridDim.x < ngroups) prefetch(grp + gridDim.x);
+
+    const int M = nimg * HW;
+    const int nblk = (M + 15) >> 4;
+    const size_t gpix0 = (size_t)img0 * HW;
+    for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+      const int m = pb * 16 + li;  // this lane's pixel (B column)
+      const bool valid = m < M;
+      const int mm = valid ? m : 0;
+      const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
+      const int base_pos = (im * Hp + y) * Wp + x;  // padded position of tap (0,0)
+      f32x4 acc[NB];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int pm = pb * 16 + 4 * g + i;
-        if (pm >= M) continue;
-        float v = acc[nb][i] + bias_v[nb];
-        const size_t gi = (gpix0 + pm) * COUT + co;
-        if (a.mask_src) v = bf2f(a.mask_src[gi]) > 0.f ? v : 0.f;
-        if (a.add) v += bf2f(a.add[gi]);
-        if (a.pool) {
-          // pool over the bf16-rounded values so a recomputed argmax (pool_bwd
-          // reads y_full) sees exactly what the forward compared
-          const bf16 vb = f2bf(v);
-          otile[pm * COUT + co] = bf2f(vb);
-          if (a.y_full) a.y_full[gi] = vb;
+      for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        Frag8 av;
+        int tap, ch0;
+        if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
+        else { tap = c; ch0 = 8 * g; }
+        const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
+        const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
+        if (BITS) {
+          const uint32_t bits = ((const uint32_t*)tile)[pos] >> ch0;
+          uint32_t w4[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
+                    (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
+          av.u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
         } else {
-          a.y[gi] = f2bf(v);
+          av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
+        }
+        if (!valid || (CIN == 16 && tap >= 9)) av.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, av.v, acc[nb], 0, 0, 0);
+      }
+      if (!valid) continue;
+      // ---- epilogue: lane holds channels nb*16 + 4g + i of pixel m
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int co0 = nb * 16 + 4 * g;
+        const size_t gi = (gpix0 + m) * COUT + co0;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bias_v[nb][i];
+        if (a.mask_src) {
+          const uint2 ms = *(const uint2*)(a.mask_src + gi);
+          const uint32_t mw[2] = {ms.x, ms.y};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            if (!(__uint_as_float(hb << 16) > 0.f)) v[i] = 0.f;
+          }
+        }
+        if (a.add) {
+          const uint2 ad = *(const uint2*)(a.add + gi);
+          const uint32_t aw[2] = {ad.x, ad.y};
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
+        }
+        uint32_t o[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(v[2 * j])) |
+                 ((uint32_t)__bfloat16_as_ushort(f2bf(v[2 * j + 1])) << 16);
+        if (a.pool) {
+          // pool over the bf16-rounded values (what y_full holds)
+          *(float4*)(otile + m * OSTR + co0) =
+              make_float4(__uint_as_float(o[0] << 16), __uint_as_float(o[0] & 0xFFFF0000u),
+                          __uint_as_float(o[1] << 16), __uint_as_float(o[1] & 0xFFFF0000u));
+          if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
+        } else {
+          *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
         }
       }
     }
-  }
-  if (!a.pool) return;
-  __syncthreads();
-  // ---- max_pool2d(kernel 3, stride 2, pad 1)
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-  const int tot = nimg * Ho * Wo * COUT;
-  bf16* yo = a.y + (size_t)img0 * Ho * Wo * COUT;
-  for (int e = tid; e < tot; e += kThreads) {
-    const int co = e % COUT, p = e / COUT;
-    const int im = p / (Ho * Wo), r = p - im * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
-    float mx = -INFINITY;
-    int am = -1;
-    for (int ky = 0; ky < 3; ++ky) {
-      const int yy = 2 * oy - 1 + ky;
-      if (yy < 0 || yy >= H) continue;
-      for (int kx = 0; kx < 3; ++kx) {
-        const int xx = 2 * ox - 1 + kx;
-        if (xx < 0 || xx >= W) continue;
-        const float v = otile[((im * H + yy) * W + xx) * COUT + co];
-        if (v > mx || am < 0) { mx = v; am = ky * 3 + kx; }  // first max in scan order (ATen)
+    if (a.pool) {
+      __syncthreads();
+      // ---- max_pool2d(kernel 3, stride 2, pad 1), 4 channels per thread
+      const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+      constexpr int C4 = COUT / 4;
+      const int tot = nimg * Ho * Wo * C4;
+      const size_t obase = (size_t)img0 * Ho * Wo * COUT;
+      for (int e = tid; e < tot; e += kThreads) {
+        const int c4 = e % C4, p = e / C4;
+        const int im = p / (Ho * Wo), r = p - im * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
+        float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int am[4] = {-1, -1, -1, -1};
+        for (int ky = 0; ky < 3; ++ky) {
+          const int yy = 2 * oy - 1 + ky;
+          if (yy < 0 || yy >= H) continue;
+          for (int kx = 0; kx < 3; ++kx) {
+            const int xx = 2 * ox - 1 + kx;
+            if (xx < 0 || xx >= W) continue;
+            const float4 v4 = *(const float4*)(otile + ((im * H + yy) * W + xx) * OSTR + 4 * c4);
+            const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)  // first max in scan order (ATen)
+              if (vv[j] > mx[j] || am[j] < 0) { mx[j] = vv[j]; am[j] = ky * 3 + kx; }
+          }
+        }
+        const size_t oi = obase + (size_t)p * COUT + 4 * c4;
+        const uint32_t o0 = (uint32_t)__bfloat16_as_ushort(f2bf(mx[0])) |
+                            ((uint32_t)__bfloat16_as_ushort(f2bf(mx[1])) << 16);
+        const uint32_t o1 = (uint32_t)__bfloat16_as_ushort(f2bf(mx[2])) |
+                            ((uint32_t)__bfloat16_as_ushort(f2bf(mx[3])) << 16);
+        *(uint2*)(a.y + oi) = make_uint2(o0, o1);
+        if (a.pool_idx)
+          *(uint32_t*)(a.pool_idx + oi) =
+              (uint32_t)am[0] | ((uint32_t)am[1] << 8) | ((uint32_t)am[2] << 16) | ((uint32_t)am[3] << 24);
       }
     }
-    yo[e] = f2bf(mx);
-    if (a.pool_idx) a.pool_idx[(size_t)img0 * Ho * Wo * COUT + e] = (uint8_t)am;
+    __syncthreads();  // tile / otile reads done before the next group is staged
   }
 }
 
@@ -235,6 +312,21 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
       (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
 }
 
+constexpr int kPFW = 4;  // wgrad prefetch slots per thread for X and for dY
+
+__device__ __forceinline__ uint4 expand_bits8(uint32_t bits) {
+  // 8 one-hot planes -> 8 bf16 (1.0 / 0.0)
+  uint32_t w4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
+            (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
+  return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+}
+
+// Persistent over image rounds (grid = occupancy-sized, one partial per workgroup).
+// Both GEMM operands come from plain NHWC LDS tiles through ds_read_b64_tr_b16; the
+// next round's X interior and dY are prefetched into registers during the MFMAs.
 template <int CIN, int COUT, bool BITS>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -244,87 +336,107 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int CB = CIN / 16;
   constexpr int NBLK = 9 * CB;
   constexpr int KTOT = 9 * CIN;
+  constexpr int XEPP = BITS ? 1 : CIN / 8;  // X staging elements per pixel (u32 / uint4)
+  constexpr int DCH = COUT / 8;             // dY uint4 per pixel
   const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = (lane >> 4), li = lane & 15;
-  // LDS carve: [X tile | zero row (64B) | dY tile | zero row]
+  // LDS carve: [X tile | zero row (64B) | dY tile | zero row]; reused for the final reduce
   const int xbytes = ((a.imgs * Hp * Wp * XPB) + 15) & ~15;
   char* xt = smem;
   char* xzero = smem + xbytes;
   char* dt = xzero + 64;
   const int dbytes = ((a.imgs * HW * DPB) + 15) & ~15;
   char* dzero = dt + dbytes;
-  float* red = (float*)(dzero + 64);  // [COUT][KTOT] reduction buffer
+  float* red = (float*)smem;  // [COUT][KTOT] after the loop
 
-  for (int e = tid; e < 16; e += kThreads) {
-    ((uint32_t*)xzero)[e] = 0u;
-    ((uint32_t*)dzero)[e] = 0u;
+  for (int e = tid; e < (xbytes + 64) / 16; e += kThreads) ((uint4*)xt)[e] = make_uint4(0, 0, 0, 0);
+  for (int e = tid; e < 4; e += kThreads) ((uint4*)dzero)[e] = make_uint4(0, 0, 0, 0);
+  const int xper = a.imgs * HW * XEPP, dper = a.imgs * HW * DCH;
+  int xoff[kPFW];
+#pragma unroll
+  for (int k = 0; k < kPFW; ++k) {
+    const int e = tid + k * kThreads;
+    int o = 0;
+    if (e < xper) {
+      const int q = e % XEPP, p = e / XEPP;
+      const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+      o = ((im * Hp + y + 1) * Wp + x + 1) * XPB + q * 16;
+    }
+    xoff[k] = o;
   }
   f32x4 acc[MB][NBLK];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < NBLK; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // bias grad: each thread always stages the same 8-channel group of dY
-  constexpr int DCH = COUT / 8;
+  // bias grad: each thread always stages the same 8-channel group of dY (256 % DCH == 0)
   float dbias[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
+  uint4 px[kPFW], pd[kPFW];
+  uint32_t pb[kPFW];
+  auto prefetch = [&](int rd) {
+    const int nimg = min(a.imgs, a.N - rd * a.imgs);
+    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH;
+    const size_t xb = (size_t)rd * xper, db = (size_t)rd * dper;
+#pragma unroll
+    for (int k = 0; k < kPFW; ++k) {
+      const int e = tid + k * kThreads;
+      if (BITS) pb[k] = e < xl ? ((const uint32_t*)a.x)[xb + e] : 0u;
+      else px[k] = e < xl ? ((const uint4*)a.x)[xb + e] : make_uint4(0, 0, 0, 0);
+      pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto put_x = [&](int off, uint4 v) {
+    if (a.relu_in) {
+      v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
+      v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
+    }
+    *(uint4*)(xt + off) = v;
+  };
+  auto put_bits = [&](int off, uint32_t bits) {  // one pixel's 32 planes -> 4 x uint4
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(uint4*)(xt + off + q * 16) = expand_bits8(bits >> (8 * q));
+  };
+  auto put_d = [&](int e, uint4 v) {
+    *(uint4*)(dt + e * 16) = v;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dbias[2 * j] += __uint_as_float(w[j] << 16);
+      dbias[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
+    }
+  };
+  auto xoff_of = [&](int e) {
+    const int q = e % XEPP, p = e / XEPP;
+    const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * XPB + q * 16;
+  };
+
   const int nrounds = (a.N + a.imgs - 1) / a.imgs;
+  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x);
+  __syncthreads();  // zero halo / zero rows visible
   for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
-    const int img0 = rd * a.imgs;
-    const int nimg = min(a.imgs, a.N - img0);
-    __syncthreads();  // previous round's reads done
-    // stage X (relu'd if the forward applied relu to its input), halo'd, NHWC bf16
-    if (BITS) {
-      const uint32_t* xb = (const uint32_t*)a.x + (size_t)img0 * HW;
-      const int tot = nimg * Hp * Wp * 4;  // 4 chunks of 8 channels
-      for (int e = tid; e < tot; e += kThreads) {
-        const int q = e & 3, pos = e >> 2;
-        const int im = pos / (Hp * Wp), r = pos - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
-        const int y = py - 1, x = px - 1;
-        uint32_t bits = (y >= 0 && y < H && x >= 0 && x < W) ? xb[im * HW + y * W + x] : 0u;
-        bits >>= 8 * q;
-        uint32_t w4[4];
+    const int nimg = min(a.imgs, a.N - rd * a.imgs);
+    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
-                  (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
-        *(uint4*)(xt + pos * XPB + q * 16) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+    for (int k = 0; k < kPFW; ++k) {
+      const int e = tid + k * kThreads;
+      if (e < xl) {
+        if (BITS) put_bits(xoff[k], pb[k]);
+        else put_x(xoff[k], px[k]);
       }
-    } else {
-      constexpr int CH16 = CIN / 8;
-      const uint4* xg = (const uint4*)((const bf16*)a.x + (size_t)img0 * HW * CIN);
-      const int tot = nimg * Hp * Wp * CH16;
-      for (int e = tid; e < tot; e += kThreads) {
-        const int q = e % CH16, pos = e / CH16;
-        const int im = pos / (Hp * Wp), r = pos - im * Hp * Wp, py = r / Wp, px = r - py * Wp;
-        const int y = py - 1, x = px - 1;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (y >= 0 && y < H && x >= 0 && x < W) {
-          v = xg[(im * HW + y * W + x) * CH16 + q];
-          if (a.relu_in) {
-            v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
-            v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
-          }
-        }
-        *(uint4*)(xt + pos * XPB + q * 16) = v;
-      }
+      if (e < dl) put_d(e, pd[k]);
     }
-    {  // stage dY (dense NHWC) + bias-grad partial sums
-      const uint4* dg = (const uint4*)(a.dy + (size_t)img0 * HW * COUT);
-      const int tot = nimg * HW * DCH;
-      for (int e = tid; e < tot; e += kThreads) {
-        const uint4 v = dg[e];
-        *(uint4*)(dt + e * 16) = v;
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dbias[2 * j] += __uint_as_float(w[j] << 16);
-          dbias[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
-        }
-      }
+    for (int e = tid + kPFW * kThreads; e < xl; e += kThreads) {
+      if (BITS) put_bits(xoff_of(e), ((const uint32_t*)a.x)[(size_t)rd * xper + e]);
+      else put_x(xoff_of(e), ((const uint4*)a.x)[(size_t)rd * xper + e]);
     }
+    for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
+      put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
     __syncthreads();
+    if (rd + (int)gridDim.x < nrounds) prefetch(rd + gridDim.x);
+
     const int M = nimg * HW;
     const int nk = (M + 31) >> 5;
     for (int kb = wave; kb < nk; kb += kThreads / 64) {
@@ -365,9 +477,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         }
       }
     }
+    __syncthreads();  // tile reads done before the next round is staged
   }
   // ---- reduce the 4 waves through LDS (sequential adds, no atomics)
-  __syncthreads();
   for (int w = 0; w < kThreads / 64; ++w) {
     if (wave == w) {
 #pragma unroll
@@ -385,7 +497,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
     __syncthreads();
   }
   float* out = a.partial + (size_t)blockIdx.x * (COUT * KTOT + COUT);
-  for (int e = tid; e < COUT * KTOT; e += kThreads) out[e] = red[e];
+  for (int e = tid; e < COUT * KTOT / 4; e += kThreads) ((float4*)out)[e] = ((const float4*)red)[e];
   // bias grad: thread tid staged channel group (tid % DCH) in every pass
   __syncthreads();
   float* bred = red;  // reuse: [kThreads][8]
@@ -401,24 +513,33 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
 }
 
 // partial[nparts][COUT*9*CIN + COUT] -> dw[co][ci][ky][kx] (+)=, db[co] (+)=
-// block = 64 output columns x 4 part-lanes; fixed summation order (deterministic)
+// block = 64 output columns x 4 part-lanes over parts [y*pps, (y+1)*pps); with `stage`
+// set the split sums go to stage[y][row] for a second pass (two-level: the persistent
+// wgrad writes up to a few thousand partial rows). Fixed summation order (deterministic).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial,
-                                                           int nparts, int cin, int cin_real,
-                                                           int cout, float* __restrict__ dw,
+                                                           int nparts, int pps,
+                                                           float* __restrict__ stage, int cin,
+                                                           int cin_real, int cout,
+                                                           float* __restrict__ dw,
                                                            float* __restrict__ db, int accumulate) {
   __shared__ float red[4][64];
   const int ktot = 9 * cin, row = cout * ktot + cout;
   const int col = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + col;
+  const int p0 = blockIdx.y * pps, p1 = min(nparts, p0 + pps);
   float s = 0.f;
   if (e < row) {
 #pragma unroll 4
-    for (int p = pl; p < nparts; p += 4) s += partial[(size_t)p * row + e];
+    for (int p = p0 + pl; p < p1; p += 4) s += partial[(size_t)p * row + e];
   }
   red[pl][col] = s;
   __syncthreads();
   if (pl != 0 || e >= row) return;
   s = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+  if (stage) {
+    stage[(size_t)blockIdx.y * row + e] = s;
+    return;
+  }
   if (e < cout * ktot) {
     const int co = e / ktot, r = e - co * ktot, t = r / cin, ci = r - t * cin;
     if (ci >= cin_real) return;
@@ -564,16 +685,37 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(PackJobs jobs) {
 inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool) {
   const int pixb = bits ? 4 : cin * 2 + 16;
   size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
-  if (pool) t += (size_t)imgs * H * W * cout * 4;
+  if (pool) t += (size_t)imgs * H * W * (cout + 4) * 4;
   return t;
 }
 
 inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W) {
   size_t x = (((size_t)imgs * (H + 2) * (W + 2) * cin * 2) + 15) & ~(size_t)15;
   size_t d = (((size_t)imgs * H * W * cout * 2) + 15) & ~(size_t)15;
+  size_t t = x + 64 + d + 64;
   size_t red = (size_t)cout * 9 * cin * 4;
   if (red < (size_t)kThreads * 8 * 4) red = (size_t)kThreads * 8 * 4;
-  return x + 64 + d + 64 + red;
+  return t > red ? t : red;
+}
+
+int g_grid_cap = 0;  // tests force multi-group workgroups with a small cap
+
+// resident workgroups the whole device holds for (kernel, dynamic LDS)
+int resident_blocks(const void* kfn, size_t sm) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  if (sm > 64 * 1024) hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
+    per = 1;
+  int r = cus * per;
+  if (g_grid_cap > 0 && r > g_grid_cap) r = g_grid_cap;
+  return r;
 }
 
 }  // namespace
@@ -582,17 +724,19 @@ extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const
                             const float* bias, const void* add, const void* mask_src, void* y,
                             void* y_full, void* pool_idx, int N, int H, int W, int imgs,
                             int relu_in, int pool, hipStream_t stream) {
+  if (N <= 0) return 0;
   ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
                 (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool};
   const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  dim3 grid((N + imgs - 1) / imgs);
+  const int ngroups = (N + imgs - 1) / imgs;
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
     auto kfn = conv_fwd_kernel<CI, CO, B>;                                                  \
     if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
-    hipLaunchKernelGGL(kfn, grid, dim3(kThreads), sm, stream, a);                           \
+    const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));              \
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);                     \
   } while (0)
   if (in_bits) {
     if (cout == 16) LAUNCH(32, 16, true);
@@ -607,12 +751,36 @@ extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const
   return (int)hipGetLastError();
 }
 
+#define WGRAD_DISPATCH(LAUNCH)                                                              \
+  if (in_bits) {                                                                            \
+    if (cout == 16) LAUNCH(32, 16, true);                                                   \
+    else if (cout == 32) LAUNCH(32, 32, true);                                              \
+    else return -(int)hipErrorInvalidValue;                                                 \
+  } else if (cin == 16 && cout == 16) LAUNCH(16, 16, false);                                \
+  else if (cin == 16 && cout == 32) LAUNCH(16, 32, false);                                  \
+  else if (cin == 32 && cout == 16) LAUNCH(32, 16, false);                                  \
+  else if (cin == 32 && cout == 32) LAUNCH(32, 32, false);                                  \
+  else return -(int)hipErrorInvalidValue;
+
+// number of partial rows mbk_conv_wgrad will write for this shape (<= nrounds)
+extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
+                                    int imgs) {
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
+  if (sm > 160 * 1024) return -(int)hipErrorInvalidValue;
+  const int nrounds = (N + imgs - 1) / imgs;
+  int res = 1;
+#define Q(CI, CO, B) res = resident_blocks((const void*)conv_wgrad_kernel<CI, CO, B>, sm)
+  WGRAD_DISPATCH(Q)
+#undef Q
+  return std::max(1, std::min(nrounds, res));
+}
+
 extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, const void* dy,
                               float* partial, int nparts, int N, int H, int W, int imgs,
                               int relu_in, hipStream_t stream) {
   ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in};
   const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
-  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (sm > 160 * 1024 || nparts < 1) return (int)hipErrorInvalidValue;
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
@@ -634,11 +802,26 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
   return (int)hipGetLastError();
 }
 
+extern "C" void mbk_conv_set_grid_cap(int cap) { g_grid_cap = cap; }
+
+// partial holds nparts rows plus ceil(nparts / kReducePps) scratch rows after them
 extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,
                                 float* dw, float* db, int accumulate, hipStream_t stream) {
+  constexpr int kReducePps = 32;
   const int row = cout * 9 * cin + cout;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row + 63) / 64), dim3(256), 0, stream, partial,
-                     nparts, cin, cin_real, cout, dw, db, accumulate);
+  const dim3 cols((row + 63) / 64);
+  if (nparts > 2 * kReducePps) {
+    const int splits = (nparts + kReducePps - 1) / kReducePps;
+    float* stage = (float*)partial + (size_t)nparts * row;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cols.x, splits), dim3(256), 0, stream, partial,
+                       nparts, kReducePps, stage, cin, cin_real, cout, dw, db, accumulate);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cols.x, 1), dim3(256), 0, stream,
+                       (const float*)stage, splits, splits, (float*)nullptr, cin, cin_real, cout,
+                       dw, db, accumulate);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cols.x, 1), dim3(256), 0, stream, partial,
+                       nparts, nparts, (float*)nullptr, cin, cin_real, cout, dw, db, accumulate);
+  }
   return (int)hipGetLastError();
 }
 

@@ -44,21 +44,36 @@ def _nch(c: int) -> int:
     return 5 if c == 16 else 9
 
 
+_PF_FWD = 8 * 256    # conv_fwd register-prefetch capacity (elements per group)
+_PF_WGRAD = 4 * 256  # conv_wgrad prefetch capacity, X and dY each
+
+
 def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool) -> int:
+    """Images per workgroup iteration: ~512 output pixels, <= 48 KB LDS (3 WGs / CU), and
+    one group's interior fits the register prefetch."""
     hw = layer.H * layer.W
-    imgs = max(1, 256 // hw)
+    epp = 1 if bits else cin // 8
+    pixb = 4 if bits else cin * 2 + 16
+    imgs = max(1, 512 // hw)
     while imgs > 1:
-        pixb = 4 if bits else cin * 2 + 16
-        sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * cout * 4 if pool else 0)
-        if sm <= 48 * 1024:
+        sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * (cout + 4) * 4 if pool else 0)
+        if sm <= 48 * 1024 and imgs * hw * epp <= _PF_FWD:
             break
         imgs //= 2
     return imgs
 
 
 def _imgs_wgrad(layer: ConvLayer) -> int:
-    per = (layer.H + 2) * (layer.W + 2) * layer.cin * 2 + layer.H * layer.W * layer.cout * 2
-    return max(1, min(64, (56 * 1024) // per))
+    hw = layer.H * layer.W
+    xepp = 1 if layer.bits else layer.cin // 8
+    dch = layer.cout // 8
+    imgs = max(1, min(_PF_WGRAD // (hw * xepp), _PF_WGRAD // (hw * dch)))
+    while imgs > 1:
+        per = (layer.H + 2) * (layer.W + 2) * layer.cin * 2 + hw * layer.cout * 2
+        if imgs * per <= 64 * 1024:
+            break
+        imgs //= 2
+    return imgs
 
 
 class HipEncoder:
@@ -123,9 +138,12 @@ class HipEncoder:
     def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor):
         n = x.shape[0]
         imgs = _imgs_wgrad(L)
-        nparts = max(1, min(256, (n + imgs - 1) // imgs))  # ~one workgroup per CU
+        # persistent grid: as many workgroups as the device keeps resident (<= rounds)
+        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs)
+        if nparts < 1:
+            raise RuntimeError(f"conv_wgrad: unsupported shape {L}")
         row = L.cout * 9 * L.cin + L.cout
-        need = nparts * row
+        need = (nparts + (nparts + 31) // 32) * row  # + the two-level reduce's scratch rows
         if self._partial is None or self._partial.numel() < need or self._partial.device != dy.device:
             self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=dy.device)
         k = N.kernels()

@@ -170,3 +170,33 @@ def test_encoder_fwd_bwd_matches_torch(cuda, s):
         errs[name] = _rel(p.grad.cpu(), q.grad)
     print(s, max(errs.values()), errs)
     assert max(errs.values()) < 4e-2, errs
+
+
+def test_persistent_grid_cap_matches(cuda):
+    """Capping the persistent grid makes every workgroup walk several image groups (and the
+    last group partial): forward must be bit-identical, weight grads equal up to the
+    partial-sum order."""
+    from microbeast_amd import _native as N
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(3)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(203, 256, seed=11).to(cuda)
+    m.features(obs[:2])
+    params = encoder_params(m.network, 3)
+    r = torch.randn(203, 2, 2, 32, device=cuda)
+    outs = []
+    try:
+        for cap in (0, 3):
+            N.kernels().mbk_conv_set_grid_cap(cap)
+            for p in params:
+                p.grad = None
+            y = encode(obs, m._hip_enc, params, True)
+            (y.float() * r).sum().backward()
+            outs.append((y.clone(), [p.grad.clone() for p in params]))
+    finally:
+        N.kernels().mbk_conv_set_grid_cap(0)
+    (y0, g0), (y1, g1) = outs
+    assert torch.equal(y0, y1)
+    for a, b in zip(g0, g1):
+        assert _rel(b.cpu(), a.cpu()) < 1e-4
