@@ -86,13 +86,23 @@ struct ConvFwdArgs {
 // consecutive channels of one pixel and the epilogue moves 8-byte vectors.
 constexpr int kPF = 8;
 
+__device__ __forceinline__ uint4 expand_bits8(uint32_t bits) {
+  // 8 one-hot planes -> 8 bf16 (1.0 / 0.0)
+  uint32_t w4[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
+            (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
+  return make_uint4(w4[0], w4[1], w4[2], w4[3]);
+}
+
 template <int CIN, bool BITS>
 __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
   // interior staging element e -> byte offset of its slot in the halo'd LDS tile
   const int Hp = H + 2, Wp = W + 2, HW = H * W;
-  if (BITS) {
+  if (BITS) {  // one u32 of bit planes per pixel, expanded to 32 bf16 channels
     const int im = e / HW, r = e - im * HW, y = r / W, x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * 4;
+    return ((im * Hp + y + 1) * Wp + x + 1) * Geo<CIN>::PIXB;
   } else {
     constexpr int CH16 = CIN / 8;
     const int q = e % CH16, p = e / CH16;
@@ -105,7 +115,7 @@ template <int CIN, int COUT, bool BITS>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NCH = Geo<CIN>::NCH;
-  constexpr int PIXB = BITS ? 4 : Geo<CIN>::PIXB;
+  constexpr int PIXB = Geo<CIN>::PIXB;  // bit planes are expanded to bf16 at staging
   constexpr int NB = COUT / 16;
   constexpr int EPP = BITS ? 1 : CIN / 8;  // staging elements per pixel (u32 / uint4)
   constexpr int OSTR = COUT + 4;           // pool staging row stride (floats, bank spread)
@@ -159,6 +169,10 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     }
     *(uint4*)(tile + off) = v;
   };
+  auto put_bits = [&](int off, uint32_t bits) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(uint4*)(tile + off + q * 16) = expand_bits8(bits >> (8 * q));
+  };
   if ((int)blockIdx.x < ngroups) prefetch(blockIdx.x);
   __syncthreads();  // halo zeros visible
 
@@ -170,13 +184,13 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     for (int k = 0; k < kPF; ++k) {
       const int e = tid + k * kThreads;
       if (e < lim) {
-        if (BITS) *(uint32_t*)(tile + loff[k]) = pw[k];
+        if (BITS) put_bits(loff[k], pw[k]);
         else put(loff[k], pv[k]);
       }
     }
     for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
       const size_t src = (size_t)grp * per_grp + e;
-      if (BITS) *(uint32_t*)(tile + fwd_lds_off<CIN, BITS>(e, H, W)) = ((const uint32_t*)a.x)[src];
+      if (BITS) put_bits(fwd_lds_off<CIN, BITS>(e, H, W), ((const uint32_t*)a.x)[src]);
       else put(fwd_lds_off<CIN, BITS>(e, H, W), ((const uint4*)a.x)[src]);
     }
     __syncthreads();
@@ -202,17 +216,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
         else { tap = c; ch0 = 8 * g; }
         const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
         const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
-        if (BITS) {
-          const uint32_t bits = ((const uint32_t*)tile)[pos] >> ch0;
-          uint32_t w4[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
-                    (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
-          av.u = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-        } else {
-          av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
-        }
+        av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
         if (!valid || (CIN == 16 && tap >= 9)) av.u = make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
@@ -313,16 +317,6 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
 }
 
 constexpr int kPFW = 4;  // wgrad prefetch slots per thread for X and for dY
-
-__device__ __forceinline__ uint4 expand_bits8(uint32_t bits) {
-  // 8 one-hot planes -> 8 bf16 (1.0 / 0.0)
-  uint32_t w4[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    w4[j] = (((bits >> (2 * j)) & 1u) ? 0x3F80u : 0u) |
-            (((bits >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
-  return make_uint4(w4[0], w4[1], w4[2], w4[3]);
-}
 
 // Persistent over image rounds (grid = occupancy-sized, one partial per workgroup).
 // Both GEMM operands come from plain NHWC LDS tiles through ds_read_b64_tr_b16; the
@@ -683,7 +677,8 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(PackJobs jobs) {
 }
 
 inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool) {
-  const int pixb = bits ? 4 : cin * 2 + 16;
+  (void)bits;  // bit planes are staged expanded (cin = 32)
+  const int pixb = cin * 2 + 16;
   size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
   if (pool) t += (size_t)imgs * H * W * (cout + 4) * 4;
   return t;

@@ -1,0 +1,197 @@
+// Split-K weight gradient of the trunk-tail dense layers: dW[O][I] = sum_n g[n][o] x[n][i].
+//
+// Reference: the backward of nn.Linear(32*h/8*w/8, 256) and of the critic
+// nn.Linear(256, 1) (model.py:119-137) on the learner batch, N = (T+1)*B ~ 266K rows.
+// The output has only O*I/256 MFMA tiles (128 for network.5, 16 for the critic), so a
+// library GEMM that parallelises over output tiles runs a handful of workgroups down a
+// 266K-long K (0.57 ms measured, profiles/06); batched split-K through aten::bmm
+// blocks the host. Here grid.x splits K, grid.y splits the output into 64x64 chunks,
+// both operands are staged row-major in LDS and read K-major with ds_read_b64_tr_b16,
+// fp32 partials are reduced by a deterministic two-level column sum. No host sync.
+#include "common.h"
+
+#include <algorithm>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __hip_bfloat16 bf16;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int MBC = 4;          // output row blocks (16) per workgroup: 64 rows of W
+constexpr int CBC = 4;          // output col blocks (16) per workgroup: 64 cols of W
+constexpr int OC = MBC * 16, IC = CBC * 16;
+constexpr int R = 128;          // K rows per LDS stage
+constexpr int GROW = OC * 2;    // g tile row bytes
+constexpr int XROW = IC * 2;    // x tile row bytes
+
+union Frag8 {
+  bf16x8 v;
+  s16x4 h[2];
+};
+
+__device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
+}
+
+// stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled
+template <int W, bool VEC>
+__device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, int c0, int ld,
+                                      int tid) {
+  constexpr int C8 = W / 8;
+  for (int e = tid; e < R * C8; e += kThreads) {
+    const int row = e / C8, c = c0 + (e % C8) * 8, n = r + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < N) {
+      if (VEC && c + 8 <= ld) {
+        v = *(const uint4*)(src + (size_t)n * ld + c);
+      } else {
+        uint16_t h[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          h[j] = c + j < ld ? __bfloat16_as_ushort(src[(size_t)n * ld + c + j]) : (uint16_t)0;
+        v = make_uint4(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,
+                       h[4] | (uint32_t)h[5] << 16, h[6] | (uint32_t)h[7] << 16);
+      }
+    }
+    *(uint4*)(t + e * 16) = v;
+  }
+}
+
+template <bool GVEC>
+__global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restrict__ g,
+                                                            const bf16* __restrict__ x, int N,
+                                                            int O, int I, int rows_per_part,
+                                                            float* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) char smem[R * GROW + R * XROW];
+  char* gt = smem;
+  char* xt = smem + R * GROW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int ncb = (I + IC - 1) / IC;
+  const int o0 = (blockIdx.y / ncb) * OC, i0 = (blockIdx.y % ncb) * IC;
+  const int r0 = blockIdx.x * rows_per_part, r1 = min(N, r0 + rows_per_part);
+  f32x4 acc[MBC][CBC];
+#pragma unroll
+  for (int mb = 0; mb < MBC; ++mb)
+#pragma unroll
+    for (int cb = 0; cb < CBC; ++cb) acc[mb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int rs = r0; rs < r1; rs += R) {
+    __syncthreads();  // previous stage's reads done
+    stage<OC, GVEC>(gt, g, rs, r1, o0, O, tid);
+    stage<IC, true>(xt, x, rs, r1, i0, I, tid);
+    __syncthreads();
+    const int nk = (min(R, r1 - rs) + 31) >> 5;
+    for (int kb = wave; kb < nk; kb += kThreads / 64) {
+      int prow[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) prow[h] = kb * 32 + 8 * G + 4 * h + (li >> 2);
+      Frag8 af[MBC];
+#pragma unroll
+      for (int mb = 0; mb < MBC; ++mb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          af[mb].h[h] = tr_read(gt + prow[h] * GROW + (mb * 16 + 4 * (li & 3)) * 2);
+#pragma unroll
+      for (int cb = 0; cb < CBC; ++cb) {
+        Frag8 bfr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          bfr.h[h] = tr_read(xt + prow[h] * XROW + (cb * 16 + 4 * (li & 3)) * 2);
+#pragma unroll
+        for (int mb = 0; mb < MBC; ++mb)
+          acc[mb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bfr.v, acc[mb][cb], 0, 0, 0);
+      }
+    }
+  }
+  // ---- reduce the 4 waves through LDS (fixed order), write this part's chunk
+  __syncthreads();
+  float* red = (float*)smem;  // [OC][IC] fp32 = 32 KB of the 48 KB stage buffers
+  static_assert(R * GROW + R * XROW >= OC * IC * 4, "reduction buffer");
+  for (int w = 0; w < kThreads / 64; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int mb = 0; mb < MBC; ++mb)
+#pragma unroll
+        for (int cb = 0; cb < CBC; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float* p = red + (mb * 16 + 4 * G + i) * IC + cb * 16 + li;
+            *p = (w == 0 ? 0.f : *p) + acc[mb][cb][i];
+          }
+    }
+    __syncthreads();
+  }
+  float* out = partial + (size_t)blockIdx.x * O * I;
+  for (int e = tid; e < OC * IC; e += kThreads) {
+    const int o = o0 + e / IC, i = i0 + e % IC;
+    if (o < O && i < I) out[(size_t)o * I + i] = red[e];
+  }
+}
+
+// out[e] (+)= sum_p partial[p][e] over parts [y*pps, (y+1)*pps); `stage` set: write the
+// split sums to stage[y][e] for a second pass. 64 columns x 4 part-lanes per block.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int nparts,
+                                                     int pps, long row, float* __restrict__ stage,
+                                                     float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int col = threadIdx.x & 63, pl = threadIdx.x >> 6;
+  const long e = (long)blockIdx.x * 64 + col;
+  const int p0 = blockIdx.y * pps, p1 = min(nparts, p0 + pps);
+  float s = 0.f;
+  if (e < row) {
+#pragma unroll 4
+    for (int p = p0 + pl; p < p1; p += 4) s += partial[(size_t)p * row + e];
+  }
+  red[pl][col] = s;
+  __syncthreads();
+  if (pl != 0 || e >= row) return;
+  s = red[0][col] + red[1][col] + red[2][col] + red[3][col];
+  if (stage) stage[(size_t)blockIdx.y * row + e] = s;
+  else out[e] = accumulate ? out[e] + s : s;
+}
+
+}  // namespace
+
+// number of K splits (partial rows) for an N x (O, I) problem
+extern "C" int mbk_fc_wgrad_parts(int N, int O, int I) {
+  (void)O;
+  (void)I;
+  const int stages = (N + R - 1) / R;
+  return std::max(1, std::min(512, stages / 8));  // >= 8 stages (1024 rows) per split
+}
+
+// partial: (nparts + ceil(nparts / 32)) * O * I floats of scratch; out: fp32 [O][I]
+extern "C" int mbk_fc_wgrad(const void* g, const void* x, int N, int O, int I, float* partial,
+                            int nparts, float* out, int accumulate, hipStream_t stream) {
+  if (N <= 0 || O <= 0 || I <= 0 || nparts < 1 || I % 8) return (int)hipErrorInvalidValue;
+  const int stages = (N + R - 1) / R;
+  const int rpp = ((stages + nparts - 1) / nparts) * R;
+  const int chunks = ((O + OC - 1) / OC) * ((I + IC - 1) / IC);
+  if (O % 8 == 0)
+    hipLaunchKernelGGL(fc_wgrad_kernel<true>, dim3(nparts, chunks), dim3(kThreads), 0, stream,
+                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial);
+  else  // e.g. the critic, O = 1
+    hipLaunchKernelGGL(fc_wgrad_kernel<false>, dim3(nparts, chunks), dim3(kThreads), 0, stream,
+                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial);
+  const long row = (long)O * I;
+  const unsigned cols = (unsigned)((row + 63) / 64);
+  constexpr int kPps = 32;
+  if (nparts > 2 * kPps) {
+    const int splits = (nparts + kPps - 1) / kPps;
+    float* st = partial + (size_t)nparts * row;
+    hipLaunchKernelGGL(colsum_kernel, dim3(cols, splits), dim3(256), 0, stream,
+                       (const float*)partial, nparts, kPps, row, st, (float*)nullptr, 0);
+    hipLaunchKernelGGL(colsum_kernel, dim3(cols, 1), dim3(256), 0, stream, (const float*)st,
+                       splits, splits, row, (float*)nullptr, out, accumulate);
+  } else {
+    hipLaunchKernelGGL(colsum_kernel, dim3(cols, 1), dim3(256), 0, stream,
+                       (const float*)partial, nparts, nparts, row, (float*)nullptr, out,
+                       accumulate);
+  }
+  return (int)hipGetLastError();
+}

@@ -467,16 +467,23 @@ __global__ __launch_bounds__(256) void head_dw_reduce_kernel(const float* __rest
 __global__ __launch_bounds__(256) void head_dx_gather_kernel(const float* __restrict__ dXp,
                                                              const int* __restrict__ pidx, int F,
                                                              int S, float* __restrict__ dX) {
+  // one wave per frame: 64 cells' pair indices per coalesced load, ballot the active
+  // ones (~1% of cells) and sum only their dXp rows
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= F) return;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int* pr = pidx + (size_t)f * S;
-  for (int c = 0; c < S; ++c) {
-    const int p = pr[c];
-    if (p < 0) continue;
-    const float4 v = ((const float4*)(dXp + (size_t)p * KD))[lane];
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    const int p = c0 + lane < S ? pr[c0 + lane] : -1;
+    uint64_t m = __ballot(p >= 0);
+    while (m) {
+      const int b = __builtin_ctzll(m);
+      m &= m - 1;
+      const int pp = __shfl(p, b);
+      const float4 v = ((const float4*)(dXp + (size_t)pp * KD))[lane];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
   }
   ((float4*)(dX + (size_t)f * KD))[lane] = acc;
 }

@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from ..ops import cell_head
 from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.head import SparseHead, sparse_sample, sparse_score
+from ..ops.linear import linear
 from ..ops.obs import bits_to_planes
 
 
@@ -135,12 +136,13 @@ class Agent(nn.Module):
             n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
             y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
                        encoder_params(self.network, len(self.channels)), torch.is_grad_enabled())
-            f = y.permute(0, 3, 1, 2).reshape(n, -1)
+            # ReLU -> network.5 -> ReLU on the NHWC rows: the Linear's input columns are
+            # permuted from the reference's NCHW flatten order instead of the activations
             nseq = len(self.channels)
-            with self._autocast(f):
-                f = self.network[nseq + 1](f)           # ReLU
-                f = self.network[nseq + 2](f)           # Linear (network.5)
-                return self.network[nseq + 3](f)        # ReLU
+            _, ho, wo, c = y.shape
+            f = F.relu(y.reshape(n, -1))
+            f = linear(f, self.network[nseq + 2], nhwc=(c, ho, wo))
+            return F.relu(f)
         x = self._planes(obs)
         with self._autocast(x):
             return self.network(x)
@@ -169,8 +171,7 @@ class Agent(nn.Module):
         if self._use_hip(obs):
             # sparse head: only cells with a legal action are computed (ops/head.py)
             f = self.features(obs)
-            with self._autocast(f):
-                value = self.critic(f).float().view(-1)
+            value = linear(f, self.critic).float().view(-1)
             n = f.shape[0]
             action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
                                          mask_bits.reshape(n, -1, 3), rng_state,
@@ -187,8 +188,11 @@ class Agent(nn.Module):
         all T+1 rows (bootstrap), the head only on the first T*B.
         """
         f = self.features(obs)
-        with self._autocast(f):
-            value = self.critic(f).float().view(-1)
+        if self._use_hip(obs):
+            value = linear(f, self.critic).float().view(-1)
+        else:
+            with self._autocast(f):
+                value = self.critic(f).float().view(-1)
         fh = f if n_score is None else f[:n_score]
         if self._use_hip(obs):
             logp, ent = sparse_score(fh.to(torch.bfloat16), self.actor.weight, self.actor.bias,

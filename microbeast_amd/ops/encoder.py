@@ -53,7 +53,7 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool) -> 
     one group's interior fits the register prefetch."""
     hw = layer.H * layer.W
     epp = 1 if bits else cin // 8
-    pixb = 4 if bits else cin * 2 + 16
+    pixb = cin * 2 + 16  # bit planes are expanded to bf16 in LDS
     imgs = max(1, 512 // hw)
     while imgs > 1:
         sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * (cout + 4) * 4 if pool else 0)
