@@ -54,9 +54,12 @@ class Flags:
     env: str = "synthetic"        # synthetic | microrts (gym-microrts adapter, if installed)
     opponents: str = "coac,coac,coac,random_biased,light_rush,worker_rush"
     reward_weight: str = "10,1,1,0.2,1,4"
-    self_play: bool = False       # league of past checkpoints as opponents
-    league_size: int = 4
-    league_update_every: int = 50
+    self_play: bool = False       # gpu runtime: self-play league (past snapshots as opponents)
+    selfplay_groups: int = 1      # with --self_play: env groups playing the league (rest: bots)
+    league_size: int = 16         # snapshots kept in HBM
+    league_update_every: int = 50  # updates between snapshots
+    pfsp_power: float = 2.0       # opponent weight (1 - win rate)^p
+    league_eps: float = 0.1       # uniform mixing of the matchmaking distribution
     # --- model
     arch: str = "impala_flat"     # impala_flat | gridnet | impala_deep
     channels: str = "16,32,32"

@@ -90,7 +90,7 @@ void MicroRTSSim::reset() {
     if (s_ >= 12) add_unit(WORKER, p, X(b + 1), Y(b), 0);
   }
   if (validate_) compute_mask(0, mask_);
-  if (external_opp_) compute_mask(1, mask_p1_);
+  if (external_opp_ && validate_) compute_mask(1, mask_p1_);
 }
 
 // ---------------------------------------------------------------- masks
@@ -502,8 +502,9 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
       if (g < 0) continue;
       const Unit& u = units_[g];
       if (u.owner != 1 || u.busy > 0) continue;
-      const uint32_t* m = &mask_p1_[(size_t)c * kMaskWords];
-      if (ap[0] >= 6 || !getbit(m, ap[0])) continue;
+      if (ap[0] >= 6) continue;
+      // fast path: the opponent's mask lives on the GPU; exec() re-checks feasibility
+      if (validate_ && !getbit(&mask_p1_[(size_t)c * kMaskWords], ap[0])) continue;
       uint8_t a[7];
       for (int k = 0; k < 7; ++k) a[k] = ap[k];
       for (int k = 1; k <= 4; ++k) a[k] = (uint8_t)((ap[k] + 2) & 3);
@@ -540,7 +541,7 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
     reset();
   } else {
     if (validate_) compute_mask(0, mask_);
-    if (external_opp_) compute_mask(1, mask_p1_);
+    if (external_opp_ && validate_) compute_mask(1, mask_p1_);
   }
   return r;
 }
@@ -551,13 +552,24 @@ float MicroRTSSim::step_packed(const uint16_t* env_actions, bool* done) {
   return step(act_buf_.data(), done, nullptr);
 }
 
-void MicroRTSSim::write_obs_codes(uint16_t* out) const {
+float MicroRTSSim::step_packed2(const uint16_t* env_actions, const uint16_t* opp_actions,
+                                bool* done) {
+  // the opponent's packed actions are in its own (mirrored) frame, as set_opponent_actions
+  const int nc = s_ * s_;
+  for (int c = 0; c < nc; ++c)
+    mbr::unpack_env_action(opp_actions[c], &opp_actions_[(size_t)c * kActComps]);
+  return step_packed(env_actions, done);
+}
+
+void MicroRTSSim::write_obs_codes_as(int player, uint16_t* out) const {
   const int nc = s_ * s_;
   for (int c = 0; c < nc; ++c) {
-    const int g = grid_[c];
+    int rx, ry;
+    map_xy(player, c % s_, c / s_, &rx, &ry);
+    const int g = grid_[cell(rx, ry)];
     if (g < 0) { out[c] = mbr::cell_code(0, 0, 0, 0, 0); continue; }
     const Unit& u = units_[g];
-    const int own = u.owner < 0 ? 0 : (u.owner == 0 ? 1 : 2);
+    const int own = u.owner < 0 ? 0 : (u.owner == player ? 1 : 2);
     out[c] = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
                             std::min<int>(std::max<int>(u.res, 0), 4), own, u.type, u.act);
   }

@@ -76,16 +76,30 @@ class MicroRTSSim {
   int ticks() const { return tick_; }
   // Self-play: opponent actions supplied externally (player-1 perspective,
   // coordinates mirrored so the same network can drive either side).
-  void set_external_opponent(bool on) { external_opp_ = on; }
+  void set_external_opponent(bool on) {
+    external_opp_ = on;
+    if (on && validate_) compute_mask(1, mask_p1_);
+  }
   void write_obs_p1(uint32_t* out) const;
   void write_mask_p1(uint32_t* out) const;
   void set_opponent_actions(const uint8_t* actions_p1);
   // GPU-engine fast path: 16-bit cell codes out, 16-bit packed env actions in, and no
   // CPU-side mask (the GPU derives it from the codes + resources, see
   // include/microrts_rules.h); exec() still validates every action's feasibility.
-  void set_validate(bool on) { validate_ = on; if (on) compute_mask(0, mask_); }
+  void set_validate(bool on) {
+    validate_ = on;
+    if (on) {
+      compute_mask(0, mask_);
+      if (external_opp_) compute_mask(1, mask_p1_);
+    }
+  }
   float step_packed(const uint16_t* env_actions, bool* done);
-  void write_obs_codes(uint16_t* out) const;
+  // self-play fast path: both players' packed actions, each in its own frame
+  float step_packed2(const uint16_t* env_actions, const uint16_t* opp_actions, bool* done);
+  void write_obs_codes(uint16_t* out) const { write_obs_codes_as(0, out); }
+  // codes from `player`'s perspective (player 1: mirrored frame, owner 1 = itself)
+  void write_obs_codes_as(int player, uint16_t* out) const;
+  bool external_opponent() const { return external_opp_; }
   int resources(int player) const { return resources_[player]; }
 
  private:

@@ -31,7 +31,7 @@ struct PyVecEnv {
 
 py::list records_to_list(const std::vector<EpisodeRecord>& recs) {
   py::list out;
-  for (const auto& r : recs) out.append(py::make_tuple(r.ep_return, r.ep_step, r.env_index, r.winner));
+  for (const auto& r : recs) out.append(py::make_tuple(r.ep_return, r.ep_step, r.env_index, r.winner, r.opponent));
   return out;
 }
 
@@ -111,6 +111,25 @@ PYBIND11_MODULE(_mbrt, m) {
                e.env->sim(i).write_obs_codes(P<uint16_t>(codes) + i * S);
                P<int32_t>(res)[i] = e.env->sim(i).resources(0);
              }
+           })
+      .def("set_external_opponent_range",
+           [](PyVecEnv& e, int e0, int e1, bool on) { e.env->set_external_opponent(e0, e1, on); })
+      .def("obs_codes_p1",
+           [](PyVecEnv& e, uintptr_t codes, uintptr_t res) {
+             const size_t S = (size_t)e.env->size() * e.env->size();
+             for (int i = 0; i < e.env->num_envs(); ++i) {
+               e.env->sim(i).write_obs_codes_as(1, P<uint16_t>(codes) + i * S);
+               P<int32_t>(res)[i] = e.env->sim(i).resources(1);
+             }
+           })
+      .def("step_codes_sp",
+           [](PyVecEnv& e, uintptr_t act16, uintptr_t opp16, uintptr_t codes, uintptr_t res,
+              uintptr_t codes_p1, uintptr_t res_p1, uintptr_t rew, uintptr_t done, int opponent) {
+             py::gil_scoped_release g;
+             e.env->step_range_codes_sp(0, e.env->num_envs(), P<uint16_t>(act16),
+                                        P<uint16_t>(opp16), P<uint16_t>(codes), P<int32_t>(res),
+                                        P<uint16_t>(codes_p1), P<int32_t>(res_p1), P<float>(rew),
+                                        P<uint8_t>(done), &e.log, opponent);
            })
       .def("step_codes",
            [](PyVecEnv& e, uintptr_t act16, uintptr_t codes, uintptr_t res, uintptr_t rew,
@@ -201,6 +220,7 @@ PYBIND11_MODULE(_mbrt, m) {
         cfg.reward_weight = c["reward_weight"].cast<std::vector<float>>();
         cfg.env_index_base = c["env_index_base"].cast<int>();
         cfg.device = c["device"].cast<int>();
+        if (c.contains("selfplay_groups")) cfg.selfplay_groups = c["selfplay_groups"].cast<int>();
         EngineBuffers buf;
         buf.obs = b["obs"].cast<uintptr_t>();
         buf.mask = b["mask"].cast<uintptr_t>();
@@ -217,9 +237,14 @@ PYBIND11_MODULE(_mbrt, m) {
         buf.in_codes = b["in_codes"].cast<uintptr_t>();
         buf.in_res = b["in_res"].cast<uintptr_t>();
         buf.out_act16 = b["out_act16"].cast<uintptr_t>();
+        if (b.contains("in_codes_p1")) {
+          buf.in_codes_p1 = b["in_codes_p1"].cast<uintptr_t>();
+          buf.in_res_p1 = b["in_res_p1"].cast<uintptr_t>();
+          buf.out_act16_p1 = b["out_act16_p1"].cast<uintptr_t>();
+        }
         return new GpuEngine(cfg, buf);
       }))
-      .def("start", &GpuEngine::start, py::arg("graph_exec"))
+      .def("start", &GpuEngine::start, py::arg("graph_exec"), py::arg("opp_graph_exec") = 0)
       .def("stop", [](GpuEngine& e) { py::gil_scoped_release g; e.stop(); })
       .def("get_full",
            [](GpuEngine& e, int n, double timeout) {
@@ -230,6 +255,7 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("stream_wait_full", &GpuEngine::stream_wait_full)
       .def("release", &GpuEngine::release)
       .def("publish", &GpuEngine::publish)
+      .def("publish_opponent", &GpuEngine::publish_opponent)
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
       .def("stream", &GpuEngine::stream)
       .def("failed", &GpuEngine::failed)
@@ -244,6 +270,8 @@ PYBIND11_MODULE(_mbrt, m) {
         d["slot_wait_s"] = s.slot_wait_s;
         d["env_s"] = s.env_s;
         d["publishes"] = s.publishes;
+        d["opp_publishes"] = s.opp_publishes;
+        d["opp_version"] = s.opp_version;
         return d;
       });
 }

@@ -56,11 +56,25 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   CTOR_CHECK(hipMalloc((void**)&d_rd_, E * 4 + E + 64));
   std::memset(h_reward_, 0, (size_t)total * 4);
   std::memset(h_done_, 0, (size_t)total);
+  if (cfg_.selfplay_groups < 0 || cfg_.selfplay_groups > cfg_.n_groups)
+    throw std::runtime_error("GpuEngine: bad selfplay_groups");
+  const int sp0 = cfg_.n_groups - cfg_.selfplay_groups;  // first self-play group
+  if (cfg_.selfplay_groups > 0) {
+    if (!buf_.in_codes_p1 || !buf_.in_res_p1 || !buf_.out_act16_p1)
+      throw std::runtime_error("GpuEngine: self-play needs in_codes_p1 / in_res_p1 / out_act16_p1");
+    CTOR_CHECK(hipHostMalloc((void**)&h_codes_p1_, (size_t)total * S_ * 2, hipHostMallocDefault));
+    CTOR_CHECK(hipHostMalloc((void**)&h_res_p1_, (size_t)total * 4, hipHostMallocDefault));
+    CTOR_CHECK(hipHostMalloc((void**)&h_act16_p1_, (size_t)total * S_ * 2, hipHostMallocDefault));
+    std::memset(h_act16_p1_, 0, (size_t)total * S_ * 2);
+    env_->set_external_opponent(sp0 * cfg_.envs_per_group, total, true);
+  }
   env_->set_validate(false);  // masks are derived on the GPU from the codes
   env_->reset_codes(h_codes_, h_res_);
+  if (cfg_.selfplay_groups > 0) env_->reset_codes_p1(h_codes_p1_, h_res_p1_);
   for (int g = 0; g < cfg_.n_groups; ++g) {
     groups_.emplace_back(new Group());
     CTOR_CHECK(hipEventCreateWithFlags(&groups_[g]->ev, hipEventDisableTiming));
+    groups_[g]->selfplay = g >= sp0;
     groups_[g]->phase.store(READY);  // reset observations are ready
   }
   full_ev_.resize(cfg_.n_slots);
@@ -71,10 +85,10 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     CTOR_CHECK(hipEventCreateWithFlags(&release_ev_[s], hipEventDisableTiming));
     free_slots_.push_back(s);
   }
-  CTOR_CHECK(hipEventCreateWithFlags(&pub_ready_, hipEventDisableTiming));
-  CTOR_CHECK(hipEventCreateWithFlags(&pub_consumed_, hipEventDisableTiming));
-  CTOR_CHECK(hipMalloc((void**)&pub_staging_, 16));
-  pub_staging_n_ = 0;
+  for (PubChan& c : pub_) {
+    CTOR_CHECK(hipEventCreateWithFlags(&c.ready, hipEventDisableTiming));
+    CTOR_CHECK(hipEventCreateWithFlags(&c.consumed, hipEventDisableTiming));
+  }
   // work chunk: enough chunks for every worker, at least 2 envs each
   chunk_ = std::max(1, std::min(16, cfg_.envs_per_group / std::max(1, 2 * cfg_.n_threads)));
 }
@@ -85,9 +99,14 @@ GpuEngine::~GpuEngine() {
   for (auto& g : groups_) if (g->ev) hipEventDestroy(g->ev);
   for (auto e : full_ev_) hipEventDestroy(e);
   for (auto e : release_ev_) hipEventDestroy(e);
-  if (pub_ready_) hipEventDestroy(pub_ready_);
-  if (pub_consumed_) hipEventDestroy(pub_consumed_);
-  if (pub_staging_) hipFree(pub_staging_);
+  for (PubChan& c : pub_) {
+    if (c.ready) hipEventDestroy(c.ready);
+    if (c.consumed) hipEventDestroy(c.consumed);
+    if (c.staging) hipFree(c.staging);
+  }
+  if (h_codes_p1_) hipHostFree(h_codes_p1_);
+  if (h_res_p1_) hipHostFree(h_res_p1_);
+  if (h_act16_p1_) hipHostFree(h_act16_p1_);
   if (h_codes_) hipHostFree(h_codes_);
   if (h_res_) hipHostFree(h_res_);
   if (h_act16_) hipHostFree(h_act16_);
@@ -113,9 +132,12 @@ std::string GpuEngine::error() const {
   return err_;
 }
 
-void GpuEngine::start(uintptr_t graph_exec) {
+void GpuEngine::start(uintptr_t graph_exec, uintptr_t opp_graph_exec) {
   if (running_.load()) return;
+  if (cfg_.selfplay_groups > 0 && !opp_graph_exec)
+    throw std::runtime_error("GpuEngine::start: self-play groups need the opponent graph");
   graph_ = (hipGraphExec_t)graph_exec;
+  opp_graph_ = (hipGraphExec_t)opp_graph_exec;
   running_.store(true);
   for (int w = 0; w < cfg_.n_threads; ++w) workers_.emplace_back(&GpuEngine::worker_loop, this, w);
   driver_ = std::thread(&GpuEngine::driver_loop, this);
@@ -158,8 +180,13 @@ void GpuEngine::worker_loop(int wid) {
         int e1 = std::min(e + chunk_, E);
         const int a0 = g * E;
         auto t0 = std::chrono::steady_clock::now();
-        env_->step_range_codes(a0 + e, a0 + e1, h_act16_, h_codes_, h_res_, h_reward_, h_done_,
-                               &log_);
+        if (G.selfplay)
+          env_->step_range_codes_sp(a0 + e, a0 + e1, h_act16_, h_act16_p1_, h_codes_, h_res_,
+                                    h_codes_p1_, h_res_p1_, h_reward_, h_done_, &log_,
+                                    G.opp_version);
+        else
+          env_->step_range_codes(a0 + e, a0 + e1, h_act16_, h_codes_, h_res_, h_reward_,
+                                 h_done_, &log_);
         env_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                               std::chrono::steady_clock::now() - t0).count(),
                           std::memory_order_relaxed);
@@ -189,15 +216,21 @@ bool GpuEngine::enqueue_gpu(int g) {
     if (release_pending_[slot]) ENG_CHECK(hipStreamWaitEvent(stream_, release_ev_[slot], 0));
     G.cur = slot;
   }
-  {  // apply a pending weight publish between two inference steps
+  {  // apply pending weight publishes between two inference steps
     std::lock_guard<std::mutex> l(pub_m_);
-    if (pub_pending_) {
-      ENG_CHECK(hipStreamWaitEvent(stream_, pub_ready_, 0));
-      ENG_CHECK(hipMemcpyAsync((void*)pub_dst_, pub_staging_, pub_n_, hipMemcpyDeviceToDevice,
-                               stream_));
-      ENG_CHECK(hipEventRecord(pub_consumed_, stream_));
-      pub_pending_ = false;
-      publishes_.fetch_add(1);
+    for (int c = 0; c < 2; ++c) {
+      PubChan& P = pub_[c];
+      if (!P.pending) continue;
+      ENG_CHECK(hipStreamWaitEvent(stream_, P.ready, 0));
+      ENG_CHECK(hipMemcpyAsync((void*)P.dst, P.staging, P.n, hipMemcpyDeviceToDevice, stream_));
+      ENG_CHECK(hipEventRecord(P.consumed, stream_));
+      P.pending = false;
+      if (c == 0) publishes_.fetch_add(1);
+      else {
+        opp_version_ = P.version;
+        opp_version_pub_.store(P.version);
+        opp_publishes_.fetch_add(1);
+      }
     }
   }
   const size_t e0 = (size_t)g * E;
@@ -210,6 +243,14 @@ bool GpuEngine::enqueue_gpu(int g) {
     ENG_CHECK(hipMemcpyAsync(d_rd_ + E * 4, h_done_ + e0, E, hipMemcpyHostToDevice, stream_));
   }
   ENG_CHECK(hipGraphLaunch(graph_, stream_));
+  if (G.selfplay) {  // the opponent acts on its own (mirrored) view with its own weights
+    ENG_CHECK(hipMemcpyAsync((void*)buf_.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
+                             hipMemcpyHostToDevice, stream_));
+    ENG_CHECK(hipMemcpyAsync((void*)buf_.in_res_p1, h_res_p1_ + e0, E * 4, hipMemcpyHostToDevice,
+                             stream_));
+    ENG_CHECK(hipGraphLaunch(opp_graph_, stream_));
+    G.opp_version = opp_version_;
+  }
 
   // scatter this step into the HBM rollout slot(s)
   MbkCopySeg seg[MBK_MAX_COPY_SEGS];
@@ -259,6 +300,9 @@ bool GpuEngine::enqueue_gpu(int g) {
   }
   ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)buf_.out_act16, E * S_ * 2,
                            hipMemcpyDeviceToHost, stream_));
+  if (G.selfplay)
+    ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)buf_.out_act16_p1, E * S_ * 2,
+                             hipMemcpyDeviceToHost, stream_));
   ENG_CHECK(hipEventRecord(G.ev, stream_));
   gpu_steps_.fetch_add(1);
   G.t += 1;
@@ -351,24 +395,27 @@ void GpuEngine::release(const std::vector<int>& slots, uintptr_t stream) {
   }
 }
 
-bool GpuEngine::publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream) {
+bool GpuEngine::publish_chan(int chan, uintptr_t src, uintptr_t dst, size_t nbytes,
+                             uintptr_t stream, int version) {
   std::lock_guard<std::mutex> l(pub_m_);
-  if (pub_pending_) return false;  // previous version not applied yet: skip this one
+  PubChan& P = pub_[chan];
+  if (P.pending) return false;  // previous version not applied yet: skip this one
   hipStream_t s = (hipStream_t)stream;
-  if (nbytes > pub_staging_n_) {
+  if (nbytes > P.staging_n) {
     // first publish (or growth): synchronous realloc is fine outside the hot loop
-    if (pub_staging_) { hipStreamSynchronize(stream_); hipFree(pub_staging_); }
-    if (hipMalloc((void**)&pub_staging_, nbytes) != hipSuccess)
+    if (P.staging) { hipStreamSynchronize(stream_); hipFree(P.staging); }
+    if (hipMalloc((void**)&P.staging, nbytes) != hipSuccess)
       throw std::runtime_error("publish: hipMalloc staging failed");
-    pub_staging_n_ = nbytes;
+    P.staging_n = nbytes;
   }
   // staging is reused only after the driver's previous copy-out has executed
-  hipStreamWaitEvent(s, pub_consumed_, 0);
-  hipMemcpyAsync(pub_staging_, (const void*)src, nbytes, hipMemcpyDeviceToDevice, s);
-  hipEventRecord(pub_ready_, s);
-  pub_dst_ = dst;
-  pub_n_ = nbytes;
-  pub_pending_ = true;
+  hipStreamWaitEvent(s, P.consumed, 0);
+  hipMemcpyAsync(P.staging, (const void*)src, nbytes, hipMemcpyDeviceToDevice, s);
+  hipEventRecord(P.ready, s);
+  P.dst = dst;
+  P.n = nbytes;
+  P.version = version;
+  P.pending = true;
   return true;
 }
 
@@ -379,6 +426,8 @@ EngineStats GpuEngine::stats() const {
   s.slots_full = slots_full_.load();
   s.env_s = env_ns_.load() * 1e-9;
   s.publishes = publishes_.load();
+  s.opp_publishes = opp_publishes_.load();
+  s.opp_version = opp_version_pub_.load();
   std::lock_guard<std::mutex> l(stats_m_);
   s.driver_idle_s = driver_idle_s_;
   s.slot_wait_s = slot_wait_s_;

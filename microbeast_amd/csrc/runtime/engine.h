@@ -13,7 +13,12 @@
 //     libs/utils.py:197-205 get_batch);
 //   * free/full slot hand-off with HIP events instead of pickled queue ints;
 //   * weight publish is a D2D copy applied between inference steps, ordered by
-//     events (no torn reads; reference libs/utils.py:337 had none).
+//     events (no torn reads; reference libs/utils.py:337 had none);
+//   * self-play league (BASELINE config 5): the last `selfplay_groups` groups play
+//     against an external opponent. Their envs also ship player-1 codes (mirrored
+//     frame), a second captured graph runs the opponent policy (a league snapshot,
+//     swapped in through a second publish channel) and both players' packed actions
+//     come back; finished episodes are tagged with the opponent's league id.
 //
 // Slot layout (time-major [T+1, E]): index t holds obs_t, mask_t, the action
 // a_t sampled at obs_t with its behaviour log-prob and value, and r_t/done_t
@@ -49,6 +54,7 @@ struct EngineConfig {
   std::vector<float> reward_weight;
   int env_index_base = 0;
   int device = 0;
+  int selfplay_groups = 0;  // groups [n_groups - selfplay_groups, n_groups) are self-play
 };
 
 // Device buffers owned by Python (torch tensors); raw addresses.
@@ -65,6 +71,8 @@ struct EngineBuffers {
   // in_obs / in_mask (GPU-side mask) and packs out_action into out_act16.
   uintptr_t in_obs = 0, in_mask = 0, out_action = 0, out_logp = 0, out_value = 0;
   uintptr_t in_codes = 0, in_res = 0, out_act16 = 0;
+  // opponent graph I/O (self-play groups only)
+  uintptr_t in_codes_p1 = 0, in_res_p1 = 0, out_act16_p1 = 0;
 };
 
 struct EngineStats {
@@ -75,20 +83,30 @@ struct EngineStats {
   double slot_wait_s = 0.0;    // groups stalled for a free slot (learner-bound)
   double env_s = 0.0;          // summed worker time inside env step
   int64_t publishes = 0;
+  int64_t opp_publishes = 0;
+  int opp_version = -1;
 };
 
 class GpuEngine {
  public:
   GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf);
   ~GpuEngine();
-  void start(uintptr_t graph_exec);
+  // opp_graph_exec: the opponent policy graph (required iff selfplay_groups > 0)
+  void start(uintptr_t graph_exec, uintptr_t opp_graph_exec = 0);
   void stop();
   // Blocks until n full slots are available (or timeout). Returns slot ids.
   std::vector<int> get_full(int n, double timeout_s);
   void stream_wait_full(uintptr_t stream, int slot);
   void release(const std::vector<int>& slots, uintptr_t stream);
   // Returns false if the previous publish has not been applied yet (skipped).
-  bool publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream);
+  bool publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream) {
+    return publish_chan(0, src, dst, nbytes, stream, -1);
+  }
+  // League: swap the opponent policy's weights to snapshot `version` (same ordering).
+  bool publish_opponent(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream,
+                        int version) {
+    return publish_chan(1, src, dst, nbytes, stream, version);
+  }
   std::vector<EpisodeRecord> drain_episodes() { return log_.drain(); }
   EngineStats stats() const;
   uintptr_t stream() const { return (uintptr_t)stream_; }
@@ -105,7 +123,19 @@ class GpuEngine {
     std::atomic<int> remaining{0};
     int cur = -1, prev = -1, t = 0;
     bool first = true;
+    bool selfplay = false;
+    int opp_version = -1;  // league id of the opponent that chose this step's p1 actions
     hipEvent_t ev = nullptr;
+  };
+  struct PubChan {  // event-ordered D2D weight publish, applied between policy steps
+    bool pending = false;
+    uintptr_t dst = 0;
+    size_t n = 0;
+    int version = -1;
+    hipEvent_t ready = nullptr;     // publisher stream: staging filled
+    hipEvent_t consumed = nullptr;  // engine stream: staging copied out
+    uint8_t* staging = nullptr;
+    size_t staging_n = 0;
   };
 
   EngineConfig cfg_;
@@ -116,6 +146,7 @@ class GpuEngine {
   EpisodeLog log_;
   hipStream_t stream_ = nullptr;
   hipGraphExec_t graph_ = nullptr;
+  hipGraphExec_t opp_graph_ = nullptr;
   std::vector<std::unique_ptr<Group>> groups_;
   // pinned staging, all envs contiguous
   uint16_t* h_codes_ = nullptr;  // 16-bit cell codes
@@ -123,6 +154,9 @@ class GpuEngine {
   float* h_reward_ = nullptr;
   uint8_t* h_done_ = nullptr;
   uint16_t* h_act16_ = nullptr;  // packed env actions
+  uint16_t* h_codes_p1_ = nullptr;  // self-play: opponent-perspective codes
+  int32_t* h_res_p1_ = nullptr;
+  uint16_t* h_act16_p1_ = nullptr;  // opponent's packed actions (its frame)
   uint8_t* d_rd_ = nullptr;  // device staging for reward+done of one group
 
   // slots
@@ -132,15 +166,12 @@ class GpuEngine {
   std::vector<hipEvent_t> full_ev_, release_ev_;
   std::vector<bool> release_pending_;
 
-  // publish
+  // publish channels: 0 = learner policy, 1 = league opponent
   std::mutex pub_m_;
-  bool pub_pending_ = false;
-  uintptr_t pub_dst_ = 0;
-  size_t pub_n_ = 0;
-  hipEvent_t pub_ready_ = nullptr;     // learner stream: staging filled
-  hipEvent_t pub_consumed_ = nullptr;  // engine stream: staging copied out
-  uint8_t* pub_staging_ = nullptr;
-  size_t pub_staging_n_ = 0;
+  PubChan pub_[2];
+  int opp_version_ = -1;  // driver thread only
+  bool publish_chan(int chan, uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream,
+                    int version);
 
   // workers
   std::vector<std::thread> workers_;
@@ -154,7 +185,8 @@ class GpuEngine {
   std::string err_;
 
   // stats
-  std::atomic<int64_t> frames_{0}, gpu_steps_{0}, slots_full_{0}, publishes_{0};
+  std::atomic<int64_t> frames_{0}, gpu_steps_{0}, slots_full_{0}, publishes_{0}, opp_publishes_{0};
+  std::atomic<int> opp_version_pub_{-1};
   std::atomic<int64_t> env_ns_{0};
   double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
   mutable std::mutex stats_m_;

@@ -38,7 +38,7 @@ void VecEnv::step_range(int e0, int e1, int base, const uint8_t* actions, uint32
     if (ep_return) ep_return[j] = ep_ret_[i];
     if (ep_step) ep_step[j] = ep_len_[i];
     if (d) {
-      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner()});
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner(), -1 - sims_[i]->bot()});
       ep_ret_[i] = 0.f;
       ep_len_[i] = 0;
     }
@@ -64,6 +64,15 @@ void VecEnv::reset_codes(uint16_t* codes, int32_t* res) {
   }
 }
 
+void VecEnv::reset_codes_p1(uint16_t* codes_p1, int32_t* res_p1) const {
+  const size_t S = (size_t)size_ * size_;
+  for (size_t i = 0; i < sims_.size(); ++i) {
+    if (!sims_[i]->external_opponent()) continue;
+    sims_[i]->write_obs_codes_as(1, codes_p1 + i * S);
+    res_p1[i] = sims_[i]->resources(1);
+  }
+}
+
 void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t* codes,
                               int32_t* res, float* reward, uint8_t* done, EpisodeLog* log) {
   const size_t S = (size_t)size_ * size_;
@@ -73,7 +82,7 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
     ep_ret_[i] += r;
     ep_len_[i] += 1;
     if (d) {
-      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner()});
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner(), -1 - sims_[i]->bot()});
       ep_ret_[i] = 0.f;
       ep_len_[i] = 0;
     }
@@ -82,6 +91,39 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
     sims_[i]->write_obs_codes(codes + (size_t)i * S);
     res[i] = sims_[i]->resources(0);
   }
+}
+
+void VecEnv::step_range_codes_sp(int e0, int e1, const uint16_t* actions,
+                                 const uint16_t* opp_actions, uint16_t* codes, int32_t* res,
+                                 uint16_t* codes_p1, int32_t* res_p1, float* reward,
+                                 uint8_t* done, EpisodeLog* log, int opponent) {
+  const size_t S = (size_t)size_ * size_;
+  for (int i = e0; i < e1; ++i) {
+    MicroRTSSim& sim = *sims_[i];
+    const bool sp = sim.external_opponent();
+    bool d = false;
+    const float r = sp ? sim.step_packed2(actions + (size_t)i * S, opp_actions + (size_t)i * S, &d)
+                       : sim.step_packed(actions + (size_t)i * S, &d);
+    ep_ret_[i] += r;
+    ep_len_[i] += 1;
+    if (d) {
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sim.winner(), sp ? opponent : -1 - sim.bot()});
+      ep_ret_[i] = 0.f;
+      ep_len_[i] = 0;
+    }
+    reward[i] = r;
+    done[i] = d ? 1 : 0;
+    sim.write_obs_codes(codes + (size_t)i * S);
+    res[i] = sim.resources(0);
+    if (sp) {
+      sim.write_obs_codes_as(1, codes_p1 + (size_t)i * S);
+      res_p1[i] = sim.resources(1);
+    }
+  }
+}
+
+void VecEnv::set_external_opponent(int e0, int e1, bool on) {
+  for (int i = e0; i < e1; ++i) sims_[i]->set_external_opponent(on);
 }
 
 void VecEnv::dense_obs(float* out) const {

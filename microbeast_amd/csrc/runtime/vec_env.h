@@ -17,6 +17,7 @@ struct EpisodeRecord {
   int32_t ep_step;
   int32_t env_index;
   int32_t winner;
+  int32_t opponent;  // league opponent id (self-play env) or -1 - bot id (scripted bot)
 };
 
 class EpisodeLog {
@@ -58,8 +59,17 @@ class VecEnv {
   // actions in, no CPU mask): 0.5 KB H2D + 0.5 KB D2H per 16x16 env step.
   void set_validate(bool on);
   void reset_codes(uint16_t* codes, int32_t* res);
+  // current player-1 codes / resources of the self-play envs (after reset_codes)
+  void reset_codes_p1(uint16_t* codes_p1, int32_t* res_p1) const;
   void step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t* codes, int32_t* res,
                         float* reward, uint8_t* done, EpisodeLog* log);
+  // Self-play variant: envs with an external opponent also take its packed actions
+  // (opp_actions, its mirrored frame) and emit its codes / resources; their finished
+  // episodes are tagged with `opponent` (the league snapshot that was playing).
+  void step_range_codes_sp(int e0, int e1, const uint16_t* actions, const uint16_t* opp_actions,
+                           uint16_t* codes, int32_t* res, uint16_t* codes_p1, int32_t* res_p1,
+                           float* reward, uint8_t* done, EpisodeLog* log, int opponent);
+  void set_external_opponent(int e0, int e1, bool on);
   // Dense reference layout for parity tools: obs f32 (n,s,s,27), mask u8 (n,s*s*78)
   void dense_obs(float* out) const;
   void dense_mask(uint8_t* out) const;

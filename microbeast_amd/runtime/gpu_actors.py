@@ -13,7 +13,11 @@ processes (microbeast.py:30-105, 179-191) and get_batch (libs/utils.py:166-218):
   captured once into a hipGraph; the C++ driver thread replays it, so acting
   costs no Python and no GIL;
 * the inference model is a separate parameter copy refreshed by an
-  event-ordered D2D publish after each update (bounded policy lag).
+  event-ordered D2D publish after each update (bounded policy lag);
+* self-play (``selfplay_groups``): those groups' envs play an external opponent;
+  a second captured graph runs the opponent policy (its own parameter copy, fed
+  from the league's snapshot pool, ``runtime/league.py``) on the opponent's
+  mirrored codes.
 """
 from __future__ import annotations
 
@@ -52,7 +56,7 @@ class GpuActorRuntime:
                  batch_slots: int, device: torch.device, n_threads: int | None = None,
                  n_slots: int | None = None, max_steps: int = 2000, seed: int = 1,
                  bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
-                 env_index_base: int = 0):
+                 env_index_base: int = 0, selfplay_groups: int = 0):
         rt = N.runtime()
         self.device = device
         self.size, self.S = size, size * size
@@ -70,7 +74,47 @@ class GpuActorRuntime:
             "reward": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
             "done": torch.zeros(NS, T1, E, dtype=torch.uint8, device=dev),
         }
-        self.io = {
+        self.io = self._make_io()
+        self.rng = torch.tensor([seed * 7919 + env_index_base, 0], dtype=torch.int64, device=dev)
+        self._cell_logp = torch.zeros(E * S, dtype=torch.float32, device=dev)
+        self.infer_model = make_model().to(dev)
+        self.infer_model.eval()
+        self.infer_flat = FlatParams(self.infer_model, dev)
+        self.graph = self._capture(self.io, self.infer_model, self.rng)
+        self.selfplay_groups = int(selfplay_groups)
+        self.opp_graph = None
+        if self.selfplay_groups > 0:
+            self.io_p1 = self._make_io()
+            self.rng_p1 = torch.tensor([seed * 7919 + env_index_base + 104729, 0],
+                                       dtype=torch.int64, device=dev)
+            self.opp_model = make_model().to(dev)
+            self.opp_model.eval()
+            self.opp_flat = FlatParams(self.opp_model, dev)
+            self.opp_graph = self._capture(self.io_p1, self.opp_model, self.rng_p1)
+        if n_threads is None:
+            n_threads = max(1, min(32, available_cpus() - 3))
+        self.n_threads = n_threads
+        cfg = dict(size=size, n_groups=n_groups, envs_per_group=E, unroll=self.T, n_slots=NS,
+                   n_threads=n_threads, max_steps=max_steps, seed=seed,
+                   bots=[BOT_IDS[b] if isinstance(b, str) else int(b) for b in bots],
+                   reward_weight=list(reward_weight), env_index_base=env_index_base,
+                   device=dev.index if dev.index is not None else torch.cuda.current_device(),
+                   selfplay_groups=self.selfplay_groups)
+        bufs = {k: v.data_ptr() for k, v in self.rb.items()}
+        bufs.update({k: v.data_ptr() for k, v in self.io.items()})
+        if self.selfplay_groups > 0:
+            bufs.update({"in_codes_p1": self.io_p1["in_codes"].data_ptr(),
+                         "in_res_p1": self.io_p1["in_res"].data_ptr(),
+                         "out_act16_p1": self.io_p1["out_act16"].data_ptr()})
+        torch.cuda.synchronize()
+        self.engine = rt.GpuEngine(cfg, bufs)
+        self.started = False
+        self.frames_per_slot = E * self.T
+
+    # ------------------------------------------------------------ inference graph
+    def _make_io(self):
+        E, S, dev = self.E, self.S, self.device
+        return {
             # what crosses PCIe: 16-bit cell codes + resources in, packed actions out
             "in_codes": torch.zeros(E, S, dtype=torch.int16, device=dev),
             "in_res": torch.zeros(E, dtype=torch.int32, device=dev),
@@ -82,69 +126,49 @@ class GpuActorRuntime:
             "out_logp": torch.zeros(E, dtype=torch.float32, device=dev),
             "out_value": torch.zeros(E, dtype=torch.float32, device=dev),
         }
-        self.rng = torch.tensor([seed * 7919 + env_index_base, 0], dtype=torch.int64, device=dev)
-        self._cell_logp = torch.zeros(E * S, dtype=torch.float32, device=dev)
-        self.infer_model = make_model().to(dev)
-        self.infer_model.eval()
-        self.infer_flat = FlatParams(self.infer_model, dev)
-        self.graph = self._capture()
-        if n_threads is None:
-            n_threads = max(1, min(32, available_cpus() - 3))
-        self.n_threads = n_threads
-        cfg = dict(size=size, n_groups=n_groups, envs_per_group=E, unroll=self.T, n_slots=NS,
-                   n_threads=n_threads, max_steps=max_steps, seed=seed,
-                   bots=[BOT_IDS[b] if isinstance(b, str) else int(b) for b in bots],
-                   reward_weight=list(reward_weight), env_index_base=env_index_base,
-                   device=dev.index if dev.index is not None else torch.cuda.current_device())
-        bufs = {k: v.data_ptr() for k, v in self.rb.items()}
-        bufs.update({k: v.data_ptr() for k, v in self.io.items()})
-        torch.cuda.synchronize()
-        self.engine = rt.GpuEngine(cfg, bufs)
-        self.started = False
-        self.frames_per_slot = E * self.T
 
-    # ------------------------------------------------------------ inference graph
-    def _policy_step(self):
-        io = self.io
-        m = self.infer_model
+    def _policy_step(self, io, m, rng):
         k = N.kernels()
         st = N.stream_ptr()
         N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(), self.E,
                                       self.size, self.size, io["in_obs"].data_ptr(),
                                       io["in_mask"].data_ptr(), st), "decode_obs_mask")
         if hasattr(m, "_use_hip") and m._use_hip(io["in_obs"]):
-            _, _, value = m.act(io["in_obs"], io["in_mask"], self.rng,
+            _, _, value = m.act(io["in_obs"], io["in_mask"], rng,
                                 action_out=io["out_action"], logp_out=io["out_logp"])
         else:
             logits, value = m.policy_value(io["in_obs"])
-            cell_head.sample_gpu(logits, io["in_mask"], self.rng, action_out=io["out_action"],
+            cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
                                  cell_logp=self._cell_logp, logp_out=io["out_logp"])
         io["out_value"].copy_(value)
         N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
                                        io["out_act16"].data_ptr(), N.stream_ptr()),
                 "pack_env_actions")
 
-    def _capture(self):
+    def _capture(self, io, model, rng):
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(3):  # warm up allocator / kernels outside capture
-                self._policy_step()
+                self._policy_step(io, model, rng)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s):
-            self._policy_step()
+            self._policy_step(io, model, rng)
         torch.cuda.synchronize()
-        self.rng[1] = 0
+        rng[1] = 0
         return g
 
     # ------------------------------------------------------------ control
     def start(self, learner_flat: FlatParams | None = None):
         if learner_flat is not None:
             self.infer_flat.data.copy_(learner_flat.data)
+            if self.selfplay_groups > 0:
+                self.opp_flat.data.copy_(learner_flat.data)  # until the league picks one
             torch.cuda.synchronize()
-        self.engine.start(int(self.graph.raw_cuda_graph_exec()))
+        opp = int(self.opp_graph.raw_cuda_graph_exec()) if self.opp_graph is not None else 0
+        self.engine.start(int(self.graph.raw_cuda_graph_exec()), opp)
         self.started = True
 
     def stop(self):
@@ -184,6 +208,15 @@ class GpuActorRuntime:
     def publish(self, learner_flat: FlatParams) -> bool:
         return self.engine.publish(learner_flat.data.data_ptr(), self.infer_flat.data.data_ptr(),
                                    learner_flat.numel * 4, N.stream_ptr())
+
+    def set_opponent(self, flat: torch.Tensor, version: int) -> bool:
+        """Swap the self-play opponent to league snapshot ``version`` (a flat fp32 buffer).
+        Returns False (and changes nothing) if the previous swap is still pending."""
+        if self.selfplay_groups <= 0:
+            raise RuntimeError("set_opponent: runtime has no self-play groups")
+        assert flat.numel() == self.opp_flat.numel and flat.dtype == torch.float32
+        return self.engine.publish_opponent(flat.data_ptr(), self.opp_flat.data.data_ptr(),
+                                            self.opp_flat.numel * 4, N.stream_ptr(), int(version))
 
     def drain_episodes(self):
         return self.engine.drain_episodes()

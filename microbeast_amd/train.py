@@ -48,6 +48,10 @@ def _gather_episodes(recs, info):
     return [r for part in out for r in (part or [])] if info.is_main else []
 
 
+def _league_extra(league):
+    return {"league": league.state_dict()} if league is not None else None
+
+
 def train(flags: Flags) -> dict:
     want_cuda = flags.device == "cuda" or (flags.device == "auto" and torch.cuda.is_available())
     info = D.init_distributed(use_cuda=want_cuda)
@@ -64,6 +68,7 @@ def train(flags: Flags) -> dict:
     learner = Learner(model, _hparams(flags), dev, info)
     step = n_update = 0
     ck_path = checkpoint_path(flags)
+    ck = None
     if flags.resume and os.path.exists(ck_path):
         ck = load_checkpoint(ck_path)
         step, n_update = restore(ck, learner.model, learner.opt)
@@ -71,17 +76,31 @@ def train(flags: Flags) -> dict:
         log(f"[microbeast_amd] resumed {ck_path} at step={step} update={n_update}")
     logger = CsvLogger(flags.savedir, flags.exp_name, enabled=info.is_main, append=flags.resume)
 
+    league = None
+    if flags.self_play and runtime != "gpu":
+        raise RuntimeError("--self_play needs the gpu runtime (the league plays on the GPU engine)")
     if runtime == "gpu":
         from .runtime.gpu_actors import GpuActorRuntime
 
         envs_total = flags.groups * flags.envs_per_group
+        sp_groups = min(flags.selfplay_groups, flags.groups) if flags.self_play else 0
         rt = GpuActorRuntime(lambda: make_model(flags, "cpu"), flags.env_size, flags.groups,
                              flags.envs_per_group, flags.unroll_length, flags.batch_size, dev,
                              n_threads=flags.actor_threads or None,
                              max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
                              bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
-                             env_index_base=info.rank * envs_total)
+                             env_index_base=info.rank * envs_total, selfplay_groups=sp_groups)
         rt.start(learner.flat)
+        if sp_groups:
+            from .runtime.league import League
+
+            league = League(capacity=flags.league_size, snapshot_every=flags.league_update_every,
+                            pfsp_power=flags.pfsp_power, eps=flags.league_eps,
+                            seed=flags.seed + info.rank)
+            if ck is not None and ck.get("league"):
+                league.load_state_dict(ck["league"], dev)
+            else:
+                league.add_snapshot(learner.flat.data)
         frames_per_update = flags.batch_size * flags.envs_per_group * flags.unroll_length
     else:
         from .runtime.mono import MonoRuntime
@@ -111,6 +130,12 @@ def train(flags: Flags) -> dict:
                 rt.publish(learner.flat.data)
             step += frames_per_update
             n_update += 1
+            if league is not None:
+                # freeze a snapshot now and then; re-draw the opponent (PFSP) every update
+                league.maybe_snapshot(n_update, learner.flat.data)
+                sid = league.sample()
+                if sid != league.current and rt.set_opponent(league.snapshot(sid), sid):
+                    league.current = sid
             if flags.fault_inject_every and runtime == "mono" and n_update % flags.fault_inject_every == 0:
                 rt.kill_random_actor()
             if n_update % flags.log_every == 0:
@@ -119,19 +144,25 @@ def train(flags: Flags) -> dict:
                 fps = frames_per_update / max(t2 - t0, 1e-9)
                 logger.losses(n_update, lv[0], lv[1], lv[2], lv[3], t2 - t0, step, fps, t1 - t0,
                               t2 - t1, lv[4])
-                logger.episodes(_gather_episodes(rt.drain_episodes(), info))
+                eps = rt.drain_episodes()
+                if league is not None:
+                    league.record(eps)  # each rank matches against its own league
+                logger.episodes(_gather_episodes(eps, info))
                 last = {"update": n_update, "step": step, "pg_loss": lv[0], "value_loss": lv[1],
                         "entropy": lv[2], "total_loss": lv[3], "fps": fps}
                 log(f"update {n_update} step {step} total_loss {lv[3]:.4f} pg {lv[0]:.4f} "
-                    f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {fps:,.0f}")
+                    f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {fps:,.0f}"
+                    + (f" league {len(league)} vs #{league.current}" if league is not None else ""))
             if flags.checkpoint_every and n_update % flags.checkpoint_every == 0:
                 if info.is_main:
-                    save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags)
+                    save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,
+                                    extra=_league_extra(league))
                 D.barrier(info)
     finally:
         rt.stop()
         if info.is_main:
-            save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags)
+            save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,
+                            extra=_league_extra(league))
         logger.close()
     wall = time.perf_counter() - t_start
     out = dict(last, updates=n_update, steps=step, wall_s=wall, checkpoint=ck_path,

@@ -1,6 +1,7 @@
 """CSV metrics — the reference's two streams, single-writer, correct dtypes.
 
-* ``{exp}.csv``: ``Return,steps`` (+ env_index, winner) — one row per finished
+* ``{exp}.csv``: ``Return,steps`` (+ env_index, winner, opponent: league snapshot id of a
+  self-play episode, or -1 - bot id) — one row per finished
   episode (reference microbeast.py:130-133, env_packer.py:66-75, where every
   actor process appended to the file concurrently and the header had one
   column fewer than the rows).
@@ -16,7 +17,7 @@ from __future__ import annotations
 import csv
 import os
 
-EPISODE_HEADER = ["Return", "steps", "env_index", "winner"]
+EPISODE_HEADER = ["Return", "steps", "env_index", "winner", "opponent"]
 LOSS_HEADER = ["update", "pg_loss", "value_loss", "entropy_loss", "total_loss", "update time",
                "frames", "fps", "wait_s", "learn_s", "mean_rho"]
 
@@ -49,8 +50,9 @@ class CsvLogger:
         if not self.enabled or not recs:
             return
         for r in recs:
-            ret, length, env_idx, winner = r
-            self._epw.writerow([float(ret), int(length), int(env_idx), int(winner)])
+            ret, length, env_idx, winner = r[:4]
+            opp = r[4] if len(r) > 4 else -1
+            self._epw.writerow([float(ret), int(length), int(env_idx), int(winner), int(opp)])
         self.n_episodes += len(recs)
         self._ep.flush()
 

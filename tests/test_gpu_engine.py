@@ -51,3 +51,53 @@ def test_engine_rollout_alignment_and_learn(cuda):
     torch.cuda.synchronize()
     d = (rt.infer_flat.data - learner.flat.data).abs().max().item()
     assert d < 1e-2
+
+
+def test_selfplay_league_engine(cuda):
+    """Self-play groups: the opponent graph drives player 1 from league snapshots; its
+    episodes come back tagged with the snapshot id; bot groups keep scripted opponents."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+    from microbeast_amd.runtime.league import League
+
+    s, T, E = 8, 8, 16
+
+    def mk():
+        return Agent((s, s, 27))
+
+    torch.manual_seed(1)
+    learner = Learner(mk(), LearnerHParams(), cuda)
+    rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=E, unroll=T, batch_slots=1,
+                         device=cuda, n_threads=2, max_steps=40, selfplay_groups=1)
+    league = League(capacity=4, snapshot_every=2, eps=0.5, seed=3)
+    league.add_snapshot(learner.flat.data)
+    rt.start(learner.flat)
+    episodes = []
+    try:
+        for it in range(16):
+            batch, slots = rt.get_batch()
+            losses = learner.learn(batch)
+            rt.release(slots)
+            rt.publish(learner.flat)
+            league.maybe_snapshot(it + 1, learner.flat.data)
+            sid = league.sample()
+            if sid != league.current and rt.set_opponent(league.snapshot(sid), sid):
+                league.current = sid
+            assert torch.isfinite(losses).all()
+            eps = rt.drain_episodes()
+            league.record(eps)
+            episodes += eps
+        st = rt.stats()
+    finally:
+        rt.stop()
+    assert st["opp_publishes"] >= 1 and st["opp_version"] in league.snaps
+    sp = [e for e in episodes if e[2] >= E]    # second group = self-play envs
+    bots = [e for e in episodes if e[2] < E]
+    assert sp and bots
+    assert all(e[4] >= 0 for e in sp) and all(e[4] < 0 for e in bots)
+    assert sum(league.games.values()) == len(sp)
+    # the opponent's weights are a league snapshot
+    torch.cuda.synchronize()
+    cur = st["opp_version"]
+    assert torch.equal(rt.opp_flat.data, league.snapshot(cur)) or cur != league.current

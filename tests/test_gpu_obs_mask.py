@@ -52,3 +52,39 @@ def test_gpu_mask_matches_simulator(cuda, s):
         torch.cuda.synchronize()
         env.step(a.data_ptr(), obs.data_ptr(), mask.data_ptr(), rew.data_ptr(), done.data_ptr())
     assert checked > 500
+
+
+def test_gpu_mask_of_player1_view_matches_simulator(cuda):
+    """Self-play: the opponent's mask decoded from its mirrored codes == the sim's p1 mask."""
+    rt = N.runtime()
+    s, n, S = 10, 16, 100
+    env = rt.VecEnv(s, n, 400, 4, [0])
+    env.set_external_opponent(True)
+    obs = torch.zeros(n, S, dtype=torch.int32)
+    mask = torch.zeros(n, S, 3, dtype=torch.int32)
+    env.reset(obs.data_ptr(), mask.data_ptr())
+    o1 = torch.zeros(n, S, dtype=torch.int32)
+    m1 = torch.zeros(n, S, 3, dtype=torch.int32)
+    c1 = torch.zeros(n, S, dtype=torch.int16)
+    r1 = torch.zeros(n, dtype=torch.int32)
+    rew, done = torch.zeros(n), torch.zeros(n, dtype=torch.uint8)
+    gen = torch.Generator().manual_seed(2)
+    k = N.kernels()
+    checked = 0
+    for step in range(150):
+        env.obs_p1(o1.data_ptr())
+        env.mask_p1(m1.data_ptr())
+        env.obs_codes_p1(c1.data_ptr(), r1.data_ptr())
+        cg, rg = c1.to(cuda), r1.to(cuda)
+        og = torch.empty(n, S, dtype=torch.int32, device=cuda)
+        mg = torch.empty(n, S, 3, dtype=torch.int32, device=cuda)
+        N.check(k.mbk_decode_obs_mask(cg.data_ptr(), rg.data_ptr(), n, s, s, og.data_ptr(),
+                                      mg.data_ptr(), N.stream_ptr()), "decode")
+        torch.cuda.synchronize()
+        assert torch.equal(og.cpu(), o1), f"p1 planes differ at step {step}"
+        assert torch.equal(mg.cpu(), m1), f"p1 mask differs at step {step}"
+        checked += int((m1 != 0).any(-1).sum())
+        a0, a1 = _legal(mask, gen), _legal(m1, gen)
+        env.set_opponent_actions(a1.data_ptr())
+        env.step(a0.data_ptr(), obs.data_ptr(), mask.data_ptr(), rew.data_ptr(), done.data_ptr())
+    assert checked > 200
