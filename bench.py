@@ -43,6 +43,11 @@ def parse(argv=None):
     p.add_argument("--learner_cu_reserve", type=int, default=0,
                    help="run the learner on a CU-masked stream leaving every k-th CU to the "
                         "policy stream (0 = off)")
+    p.add_argument("--selfplay_groups", type=int, default=0,
+                   help="BASELINE config 5: env groups playing a self-play league (opponent "
+                        "policy graph + PFSP over HBM snapshots) instead of scripted bots")
+    p.add_argument("--fp8_policy", action="store_true",
+                   help="acting trunk on the fp8 (e4m3) MFMA conv kernels (config 5)")
     p.add_argument("--profile_phases", action="store_true",
                    help="also report per-phase learner timings (adds syncs; not for the headline)")
     return p.parse_args(argv)
@@ -76,8 +81,14 @@ def main(argv=None):
     envs_total = args.groups * args.envs_per_group
     rt = GpuActorRuntime(make_model, s, args.groups, args.envs_per_group, args.unroll,
                          args.batch_slots, dev, n_threads=threads, seed=args.seed + 1000 * info.rank,
-                         env_index_base=info.rank * envs_total)
+                         env_index_base=info.rank * envs_total,
+                         selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy)
     rt.start(learner.flat)
+    league = None
+    if args.selfplay_groups > 0:
+        from microbeast_amd.runtime.league import League
+        league = League(capacity=16, snapshot_every=5, seed=args.seed + info.rank)
+        league.add_snapshot(learner.flat.data)
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
     if args.learner_cu_reserve > 0:
         from microbeast_amd import _native as N
@@ -97,6 +108,12 @@ def main(argv=None):
         losses = learner.learn(batch)
         rt.release(slots)
         rt.publish(learner.flat)
+        if league is not None:  # the full league loop is inside the timed step
+            league.maybe_snapshot(nstep[0], learner.flat.data)
+            league.record(rt.drain_episodes())
+            sid = league.sample()
+            if sid != league.current and rt.set_opponent(league.snapshot(sid), sid):
+                league.current = sid
         return losses
 
     for _ in range(args.warmup):
@@ -142,7 +159,7 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(fps / BASELINE_FPS, 1),
-            "dtype": "bf16",
+            "dtype": "bf16" + (" (fp8 e4m3 acting trunk)" if args.fp8_policy else ""),
             "data": "synthetic (native microRTS stand-in env, random-init weights)",
             "config": {
                 "model": f"impala_flat IMPALA-CNN 16/32/32 + FC256 + flat 78x{s}x{s} head "
@@ -151,6 +168,8 @@ def main(argv=None):
                 "global_batch": frames_per_step * info.world_size,
                 "seq_len": args.unroll,
                 "parallelism": f"dp{info.world_size}",
+                "opponents": (f"self-play league on {args.selfplay_groups}/{args.groups} groups"
+                              if args.selfplay_groups else "scripted bots"),
                 "envs_per_gpu": envs_total,
                 "env_threads_per_gpu": threads,
             },

@@ -46,6 +46,9 @@ _SIGS = {
     "mbk_conv_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_void_p],
+    "mbk_conv_fwd_fp8": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mbk_conv_pack_fp8": [c_void_p, c_int, c_void_p],
     "mbk_pool_bwd_idx": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                        c_int, c_int, c_int, c_void_p],

@@ -65,6 +65,7 @@ class Flags:
     channels: str = "16,32,32"
     hidden: int = 256
     dtype: str = "bf16"           # fp32 | bf16
+    fp8_policy: bool = False      # gpu runtime: acting trunk on fp8 (e4m3) MFMA convs
     # --- runtime
     runtime: str = "auto"         # auto | gpu (native engine) | mono (CPU actor processes)
     device: str = "auto"          # auto | cpu | cuda

@@ -29,6 +29,15 @@ typedef struct {
 
 int mbk_conv_pack(const MbkPackJob* jobs, int n, hipStream_t stream);
 
+typedef struct {
+  const float* w;  // fp32 [cout][cin_real][3][3]
+  void* q;         // e4m3 packed fwd weights [cout][nch][32]
+  float* scale;    // [cout] dequant multipliers
+  int cin, cin_real, cout;
+} MbkPackJob8;
+
+int mbk_conv_pack_fp8(const MbkPackJob8* jobs, int n, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -62,6 +62,7 @@ template <int CIN>
 struct Geo {
   static constexpr int NCH = CIN == 16 ? 5 : 9;  // K chunks of 32
   static constexpr int PIXB = CIN * 2 + 16;       // padded NHWC pixel stride in LDS (bytes)
+  static constexpr int PIXB8 = CIN + 8;           // fp8 tile pixel stride
 };
 
 struct ConvFwdArgs {
@@ -74,6 +75,7 @@ struct ConvFwdArgs {
   bf16* y_full;
   uint8_t* pool_idx;  // pooled argmax (0..8 in the 3x3 window) for the backward
   int N, H, W, imgs, relu_in, pool;
+  const float* wscale;  // fp8 path: per-output-channel dequant scale of the e4m3 weights
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -96,26 +98,58 @@ __device__ __forceinline__ uint4 expand_bits8(uint32_t bits) {
   return make_uint4(w4[0], w4[1], w4[2], w4[3]);
 }
 
-template <int CIN, bool BITS>
+__device__ __forceinline__ uint2 expand_bits8_fp8(uint32_t bits) {
+  // 8 one-hot planes -> 8 OCP e4m3 bytes (1.0 = 0x38)
+  uint32_t w2[2] = {0u, 0u};
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if ((bits >> j) & 1u) w2[j >> 2] |= 0x38u << (8 * (j & 3));
+  return make_uint2(w2[0], w2[1]);
+}
+
+__device__ __forceinline__ uint32_t cvt_fp8x4(float a, float b, float c, float d) {
+  // round-to-nearest-even into OCP e4m3 (gfx950), saturated to +-448
+  auto sat = [](float v) { return fminf(fmaxf(v, -448.f), 448.f); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(d), w, true);
+  return (uint32_t)w;
+}
+
+__device__ __forceinline__ uint2 bf16x8_to_fp8(uint4 v) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(w[j] << 16);
+    f[2 * j + 1] = __uint_as_float(w[j] & 0xFFFF0000u);
+  }
+  return make_uint2(cvt_fp8x4(f[0], f[1], f[2], f[3]), cvt_fp8x4(f[4], f[5], f[6], f[7]));
+}
+
+template <int CIN, bool BITS, bool F8>
 __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
   // interior staging element e -> byte offset of its slot in the halo'd LDS tile
+  constexpr int PIXB = F8 ? Geo<CIN>::PIXB8 : Geo<CIN>::PIXB;
   const int Hp = H + 2, Wp = W + 2, HW = H * W;
-  if (BITS) {  // one u32 of bit planes per pixel, expanded to 32 bf16 channels
+  if (BITS) {  // one u32 of bit planes per pixel, expanded to 32 channels
     const int im = e / HW, r = e - im * HW, y = r / W, x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * Geo<CIN>::PIXB;
+    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB;
   } else {
     constexpr int CH16 = CIN / 8;
     const int q = e % CH16, p = e / CH16;
     const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * Geo<CIN>::PIXB + q * 16;
+    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB + q * (F8 ? 8 : 16);
   }
 }
 
-template <int CIN, int COUT, bool BITS>
+// F8: the tile holds OCP e4m3 activations (converted at staging: half the LDS bytes and
+// read traffic), weights are e4m3 with a power-of-two per-output-channel scale, and the
+// MFMA is v_mfma_f32_16x16x32_fp8_fp8 (same lane map as the bf16 form). Inference only.
+template <int CIN, int COUT, bool BITS, bool F8>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NCH = Geo<CIN>::NCH;
-  constexpr int PIXB = Geo<CIN>::PIXB;  // bit planes are expanded to bf16 at staging
+  constexpr int PIXB = F8 ? Geo<CIN>::PIXB8 : Geo<CIN>::PIXB;  // bits expanded at staging
   constexpr int NB = COUT / 16;
   constexpr int EPP = BITS ? 1 : CIN / 8;  // staging elements per pixel (u32 / uint4)
   constexpr int OSTR = COUT + 4;           // pool staging row stride (floats, bank spread)
@@ -133,21 +167,31 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
   for (int k = 0; k < kPF; ++k) {
     const int e = tid + k * kThreads;
-    loff[k] = e < per_grp ? fwd_lds_off<CIN, BITS>(e, H, W) : 0;
+    loff[k] = e < per_grp ? fwd_lds_off<CIN, BITS, F8>(e, H, W) : 0;
   }
   // ---- weights -> registers (A fragments): lane holds w[co = nb*16 + li][c][8g..8g+7]
   Frag8 bw[NCH][NB];
+  long bw8[NCH][NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const uint4* wp = (const uint4*)(a.w + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
+    if constexpr (F8) {
+      const long* wp = (const long*)((const uint8_t*)a.w + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
+      for (int c = 0; c < NCH; ++c) bw8[c][nb] = wp[c * 4];
+    } else {
+      const uint4* wp = (const uint4*)(a.w + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
+    }
   }
-  float bias_v[NB][4];
+  float bias_v[NB][4], wsc[NB][4];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bias_v[nb][i] = a.bias ? a.bias[nb * 16 + 4 * g + i] : 0.f;
+    for (int i = 0; i < 4; ++i) {
+      bias_v[nb][i] = a.bias ? a.bias[nb * 16 + 4 * g + i] : 0.f;
+      wsc[nb][i] = F8 ? a.wscale[nb * 16 + 4 * g + i] : 1.f;
+    }
 
   // ---- register prefetch of one group's interior pixels
   uint4 pv[kPF];
@@ -167,11 +211,15 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       v.x = relu_bf16x2(v.x); v.y = relu_bf16x2(v.y);
       v.z = relu_bf16x2(v.z); v.w = relu_bf16x2(v.w);
     }
-    *(uint4*)(tile + off) = v;
+    if constexpr (F8) *(uint2*)(tile + off) = bf16x8_to_fp8(v);
+    else *(uint4*)(tile + off) = v;
   };
   auto put_bits = [&](int off, uint32_t bits) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *(uint4*)(tile + off + q * 16) = expand_bits8(bits >> (8 * q));
+    for (int q = 0; q < 4; ++q) {
+      if constexpr (F8) *(uint2*)(tile + off + q * 8) = expand_bits8_fp8(bits >> (8 * q));
+      else *(uint4*)(tile + off + q * 16) = expand_bits8(bits >> (8 * q));
+    }
   };
   if ((int)blockIdx.x < ngroups) prefetch(blockIdx.x);
   __syncthreads();  // halo zeros visible
@@ -190,8 +238,8 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     }
     for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
       const size_t src = (size_t)grp * per_grp + e;
-      if (BITS) put_bits(fwd_lds_off<CIN, BITS>(e, H, W), ((const uint32_t*)a.x)[src]);
-      else put(fwd_lds_off<CIN, BITS>(e, H, W), ((const uint4*)a.x)[src]);
+      if (BITS) put_bits(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint32_t*)a.x)[src]);
+      else put(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint4*)a.x)[src]);
     }
     __syncthreads();
     if (grp + (int)gridDim.x < ngroups) prefetch(grp + gridDim.x);
@@ -216,11 +264,20 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
         else { tap = c; ch0 = 8 * g; }
         const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
         const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
-        av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
-        if (!valid || (CIN == 16 && tap >= 9)) av.u = make_uint4(0, 0, 0, 0);
+        const bool zero = !valid || (CIN == 16 && tap >= 9);
+        if constexpr (F8) {
+          long a8 = *(const long*)(tile + pos * PIXB + ch0);
+          if (zero) a8 = 0;
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, av.v, acc[nb], 0, 0, 0);
+          for (int nb = 0; nb < NB; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bw8[c][nb], a8, acc[nb], 0, 0, 0);
+        } else {
+          av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
+          if (zero) av.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, av.v, acc[nb], 0, 0, 0);
+        }
       }
       if (!valid) continue;
       // ---- epilogue: lane holds channels nb*16 + 4g + i of pixel m
@@ -230,7 +287,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
         const size_t gi = (gpix0 + m) * COUT + co0;
         float v[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bias_v[nb][i];
+        for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] * wsc[nb][i] + bias_v[nb][i];
         if (a.mask_src) {
           const uint2 ms = *(const uint2*)(a.mask_src + gi);
           const uint32_t mw[2] = {ms.x, ms.y};
@@ -676,9 +733,61 @@ __global__ __launch_bounds__(256) void conv_pack_kernel(PackJobs jobs) {
   }
 }
 
-inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool) {
+// fp32 [cout][cin_real][3][3] -> e4m3 [cout][nch][32] (fwd layout) with a power-of-two
+// per-output-channel scale 2^k (amax * 2^k <= 224, exact dequant), one block per (co, job)
+struct PackJob8 {
+  const float* w;
+  uint8_t* q;
+  float* scale;  // [cout] dequant multipliers 2^-k
+  int cin, cin_real, cout;
+};
+struct PackJobs8 {
+  PackJob8 j[16];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv_pack_fp8_kernel(PackJobs8 jobs) {
+  if ((int)blockIdx.y >= jobs.n) return;
+  const PackJob8& J = jobs.j[blockIdx.y];
+  const int co = blockIdx.x;
+  if (co >= J.cout) return;
+  __shared__ float red[256];
+  const int nk = J.cin_real * 9;
+  const float* wr = J.w + (size_t)co * nk;
+  float m = 0.f;
+  for (int e = threadIdx.x; e < nk; e += blockDim.x) m = fmaxf(m, fabsf(wr[e]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if ((int)threadIdx.x < st) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + st]);
+    __syncthreads();
+  }
+  const float amax = red[0];
+  int k = 0;
+  if (amax > 0.f) {
+    k = (int)floorf(log2f(224.f / amax));
+    k = max(-30, min(30, k));
+  }
+  const float sc = ldexpf(1.f, k);
+  const int nch = J.cin == 16 ? 5 : 9;
+  for (int e = threadIdx.x; e < nch * 32; e += blockDim.x) {
+    const int c = e / 32, kk = e % 32;
+    int tap, ci;
+    if (J.cin == 16) { tap = 2 * c + kk / 16; ci = kk % 16; }
+    else { tap = c; ci = kk; }
+    float v = 0.f;
+    if (tap < 9 && ci < J.cin_real) v = wr[ci * 9 + tap] * sc;
+    v = fminf(fmaxf(v, -448.f), 448.f);
+    const int b = __builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false);
+    J.q[(size_t)co * nch * 32 + e] = (uint8_t)(b & 0xFF);
+  }
+  if (threadIdx.x == 0) J.scale[co] = ldexpf(1.f, -k);
+}
+
+inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool,
+                       bool fp8 = false) {
   (void)bits;  // bit planes are staged expanded (cin = 32)
-  const int pixb = cin * 2 + 16;
+  const int pixb = fp8 ? cin + 8 : cin * 2 + 16;
   size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
   if (pool) t += (size_t)imgs * H * W * (cout + 4) * 4;
   return t;
@@ -715,19 +824,21 @@ int resident_blocks(const void* kfn, size_t sm) {
 
 }  // namespace
 
-extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const void* w,
-                            const float* bias, const void* add, const void* mask_src, void* y,
-                            void* y_full, void* pool_idx, int N, int H, int W, int imgs,
-                            int relu_in, int pool, hipStream_t stream) {
+static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const void* w,
+                           const float* wscale, const float* bias, const void* add,
+                           const void* mask_src, void* y, void* y_full, void* pool_idx, int N,
+                           int H, int W, int imgs, int relu_in, int pool, bool fp8,
+                           hipStream_t stream) {
   if (N <= 0) return 0;
+  if (fp8 && !wscale) return (int)hipErrorInvalidValue;
   ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
-                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool};
-  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0);
+                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool, wscale};
+  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0, fp8);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const int ngroups = (N + imgs - 1) / imgs;
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
-    auto kfn = conv_fwd_kernel<CI, CO, B>;                                                  \
+    auto kfn = fp8 ? conv_fwd_kernel<CI, CO, B, true> : conv_fwd_kernel<CI, CO, B, false>;  \
     if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
     const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));              \
@@ -744,6 +855,24 @@ extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const
   else return (int)hipErrorInvalidValue;
 #undef LAUNCH
   return (int)hipGetLastError();
+}
+
+extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const void* w,
+                            const float* bias, const void* add, const void* mask_src, void* y,
+                            void* y_full, void* pool_idx, int N, int H, int W, int imgs,
+                            int relu_in, int pool, hipStream_t stream) {
+  return conv_fwd_launch(x, in_bits, cin, cout, w, nullptr, bias, add, mask_src, y, y_full,
+                         pool_idx, N, H, W, imgs, relu_in, pool, false, stream);
+}
+
+// Inference conv on fp8 MFMA: w = e4m3 packed weights (mbk_conv_pack_fp8), wscale = their
+// per-output-channel dequant scale; activations in / out stay bf16 NHWC.
+extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, const void* w,
+                                const float* wscale, const float* bias, const void* add, void* y,
+                                int N, int H, int W, int imgs, int relu_in, int pool,
+                                hipStream_t stream) {
+  return conv_fwd_launch(x, in_bits, cin, cout, w, wscale, bias, add, nullptr, y, nullptr,
+                         nullptr, N, H, W, imgs, relu_in, pool, true, stream);
 }
 
 #define WGRAD_DISPATCH(LAUNCH)                                                              \
@@ -838,6 +967,25 @@ extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, 
   if (blocks > 16384) blocks = 16384;
   hipLaunchKernelGGL(pool_bwd_idx_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
                      (const uint8_t*)pidx, (const bf16*)dp, N, H, W, C, (bf16*)dc);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_conv_pack_fp8(const MbkPackJob8* jobs, int n, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (n > 16) return (int)hipErrorInvalidValue;
+  PackJobs8 p;
+  int maxc = 1;
+  for (int i = 0; i < n; ++i) {
+    p.j[i].w = jobs[i].w;
+    p.j[i].q = (uint8_t*)jobs[i].q;
+    p.j[i].scale = jobs[i].scale;
+    p.j[i].cin = jobs[i].cin;
+    p.j[i].cin_real = jobs[i].cin_real;
+    p.j[i].cout = jobs[i].cout;
+    maxc = std::max(maxc, jobs[i].cout);
+  }
+  p.n = n;
+  hipLaunchKernelGGL(conv_pack_fp8_kernel, dim3(maxc, n), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }
 

@@ -90,6 +90,7 @@ class Agent(nn.Module):
         self.hip_kernels = hip_kernels
         self._hip_enc = None
         self._hip_head = None
+        self.fp8_inference = False  # acting trunk on the fp8 MFMA convs (see HipEncoder)
         h, w, c = obs_space_shape
         self.h, self.w, self.planes = h, w, c
         self.mapsize = mapsize if mapsize is not None else h * w
@@ -133,6 +134,9 @@ class Agent(nn.Module):
             # NCHW flatten order into network.5
             if self._hip_enc is None or self._hip_enc.packed_fwd.device != obs.device:
                 self._hip_enc = HipEncoder(self.h, self.w, self.planes, self.channels, obs.device)
+            # fp8 MFMA convs for no-grad (acting) forwards when enabled (config 5);
+            # gradient-carrying forwards always run the bf16 kernels
+            self._hip_enc.fp8 = self.fp8_inference
             n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
             y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
                        encoder_params(self.network, len(self.channels)), torch.is_grad_enabled())

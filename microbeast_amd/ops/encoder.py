@@ -40,6 +40,11 @@ class _Job(ctypes.Structure):
                 ("cin", ctypes.c_int), ("cin_real", ctypes.c_int), ("cout", ctypes.c_int)]
 
 
+class _Job8(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("q", ctypes.c_void_p), ("scale", ctypes.c_void_p),
+                ("cin", ctypes.c_int), ("cin_real", ctypes.c_int), ("cout", ctypes.c_int)]
+
+
 def _nch(c: int) -> int:
     return 5 if c == 16 else 9
 
@@ -48,12 +53,13 @@ _PF_FWD = 8 * 256    # conv_fwd register-prefetch capacity (elements per group)
 _PF_WGRAD = 4 * 256  # conv_wgrad prefetch capacity, X and dY each
 
 
-def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool) -> int:
+def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
+              fp8: bool = False) -> int:
     """Images per workgroup iteration: ~512 output pixels, <= 48 KB LDS (3 WGs / CU), and
     one group's interior fits the register prefetch."""
     hw = layer.H * layer.W
     epp = 1 if bits else cin // 8
-    pixb = cin * 2 + 16  # bit planes are expanded to bf16 in LDS
+    pixb = (cin + 8) if fp8 else (cin * 2 + 16)  # bit planes are expanded in LDS
     imgs = max(1, 512 // hw)
     while imgs > 1:
         sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * (cout + 4) * 4 if pool else 0)
@@ -79,7 +85,8 @@ def _imgs_wgrad(layer: ConvLayer) -> int:
 class HipEncoder:
     """Owns layer geometry, packed-weight buffers and backward workspace."""
 
-    def __init__(self, h: int, w: int, planes: int, channels=(16, 32, 32), device=None):
+    def __init__(self, h: int, w: int, planes: int, channels=(16, 32, 32), device=None,
+                 fp8: bool = False):
         assert planes <= 32, "bit-plane observations carry at most 32 planes"
         self.layers: list[ConvLayer] = []
         H, W, cin, cin_real, bits = h, w, 32, planes, True
@@ -101,6 +108,16 @@ class HipEncoder:
         self.packed_fwd = torch.zeros(off, dtype=torch.bfloat16, device=device)
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
+        # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
+        self.fp8 = fp8
+        self.packed_fwd8 = torch.zeros(off, dtype=torch.uint8, device=device)
+        self.scale8 = torch.zeros(sum(L.cout for L in self.layers), dtype=torch.float32,
+                                  device=device)
+        self._s_off = []
+        so = 0
+        for L in self.layers:
+            self._s_off.append(so)
+            so += L.cout
 
     # ------------------------------------------------------------ helpers
     def pack(self, weights: list[torch.Tensor], with_bwd: bool) -> None:
@@ -113,6 +130,29 @@ class HipEncoder:
                            L.cin_real, L.cout)
         N.check(k.mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), len(self.layers),
                                 N.stream_ptr()), "conv_pack")
+
+    def pack_fp8(self, weights: list[torch.Tensor]) -> None:
+        k = N.kernels()
+        jobs = (_Job8 * len(self.layers))()
+        for i, (L, wt) in enumerate(zip(self.layers, weights)):
+            assert wt.dtype == torch.float32 and wt.is_contiguous()
+            jobs[i] = _Job8(wt.data_ptr(), self.packed_fwd8.data_ptr() + L.w_off,
+                            self.scale8.data_ptr() + 4 * self._s_off[i], L.cin, L.cin_real, L.cout)
+        N.check(k.mbk_conv_pack_fp8(ctypes.cast(jobs, ctypes.c_void_p), len(self.layers),
+                                    N.stream_ptr()), "conv_pack_fp8")
+
+    def _fwd8(self, i: int, x, bias, add=None):
+        """Inference conv i on the fp8 MFMA kernel (bf16 activations in / out)."""
+        L = self.layers[i]
+        n = x.shape[0]
+        Ho, Wo = ((L.H + 1) // 2, (L.W + 1) // 2) if L.pool else (L.H, L.W)
+        y = torch.empty(n, Ho, Wo, L.cout, dtype=torch.bfloat16, device=x.device)
+        imgs = _imgs_fwd(L, L.cin, L.cout, L.bits, L.pool, fp8=True)
+        N.check(N.kernels().mbk_conv_fwd_fp8(
+            x.data_ptr(), int(L.bits), L.cin, L.cout, self.packed_fwd8.data_ptr() + L.w_off,
+            self.scale8.data_ptr() + 4 * self._s_off[i], N.ptr(bias), N.ptr(add), y.data_ptr(),
+            n, L.H, L.W, imgs, int(L.relu_in), int(L.pool), N.stream_ptr()), "conv_fwd_fp8")
+        return y
 
     def _fwd(self, L: ConvLayer, x, bias, add=None, mask_src=None, y_full=None, dgrad=False,
              pool_idx=None):
@@ -158,8 +198,18 @@ class HipEncoder:
     def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool):
         """params: [w0, b0, w1, b1, ...] fp32 in layer order. Returns (out NHWC bf16, saved)."""
         ws, bs = params[0::2], params[1::2]
-        self.pack([w.detach() for w in ws], with_bwd=save)
         x = obs_bits.contiguous()
+        if self.fp8 and not save:
+            self.pack_fp8([w.detach() for w in ws])
+            for st in range(len(self.layers) // 5):
+                i = 5 * st
+                p = self._fwd8(i, x, bs[i].detach())
+                u0 = self._fwd8(i + 1, p, bs[i + 1].detach())
+                y0 = self._fwd8(i + 2, u0, bs[i + 2].detach(), add=p)
+                u1 = self._fwd8(i + 3, y0, bs[i + 3].detach())
+                x = self._fwd8(i + 4, u1, bs[i + 4].detach(), add=y0)
+            return x, []
+        self.pack([w.detach() for w in ws], with_bwd=save)
         saved = []
         li = 0
         n = x.shape[0]

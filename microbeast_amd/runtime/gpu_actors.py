@@ -56,7 +56,7 @@ class GpuActorRuntime:
                  batch_slots: int, device: torch.device, n_threads: int | None = None,
                  n_slots: int | None = None, max_steps: int = 2000, seed: int = 1,
                  bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
-                 env_index_base: int = 0, selfplay_groups: int = 0):
+                 env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False):
         rt = N.runtime()
         self.device = device
         self.size, self.S = size, size * size
@@ -79,6 +79,9 @@ class GpuActorRuntime:
         self._cell_logp = torch.zeros(E * S, dtype=torch.float32, device=dev)
         self.infer_model = make_model().to(dev)
         self.infer_model.eval()
+        self.fp8_policy = fp8_policy
+        if fp8_policy:  # acting trunk on fp8 MFMA; V-trace corrects the behaviour/learner gap
+            self.infer_model.fp8_inference = True
         self.infer_flat = FlatParams(self.infer_model, dev)
         self.graph = self._capture(self.io, self.infer_model, self.rng)
         self.selfplay_groups = int(selfplay_groups)
@@ -89,6 +92,7 @@ class GpuActorRuntime:
                                        dtype=torch.int64, device=dev)
             self.opp_model = make_model().to(dev)
             self.opp_model.eval()
+            self.opp_model.fp8_inference = fp8_policy
             self.opp_flat = FlatParams(self.opp_model, dev)
             self.opp_graph = self._capture(self.io_p1, self.opp_model, self.rng_p1)
         if n_threads is None:

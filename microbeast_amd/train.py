@@ -89,7 +89,8 @@ def train(flags: Flags) -> dict:
                              n_threads=flags.actor_threads or None,
                              max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
                              bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
-                             env_index_base=info.rank * envs_total, selfplay_groups=sp_groups)
+                             env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
+                             fp8_policy=flags.fp8_policy)
         rt.start(learner.flat)
         if sp_groups:
             from .runtime.league import League

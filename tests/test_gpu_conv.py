@@ -200,3 +200,57 @@ def test_persistent_grid_cap_matches(cuda):
     assert torch.equal(y0, y1)
     for a, b in zip(g0, g1):
         assert _rel(b.cpu(), a.cpu()) < 1e-4
+
+
+def _q8(t):
+    """round to OCP e4m3 (saturating) like the kernels"""
+    return t.clamp(-448, 448).to(torch.float8_e4m3fn).float()
+
+
+def test_fp8_conv_matches_quantized_reference(cuda):
+    """One fp8 MFMA conv (relu-in + residual, and the bit-plane stage conv + pool) vs an fp32
+    conv on the same e4m3-quantized operands: isolates layout / scale bugs from fp8 error."""
+    from microbeast_amd.ops.encoder import HipEncoder
+    from microbeast_amd.ops.obs import bits_to_planes
+    torch.manual_seed(4)
+    enc = HipEncoder(16, 16, 27, (16, 32, 32), cuda, fp8=True)
+    ws = [torch.randn(L.cout, L.cin_real, 3, 3) * 0.1 for L in enc.layers]
+    enc.pack_fp8([t.to(cuda).contiguous() for t in ws])
+    scale = enc.scale8.cpu()
+    so = enc._s_off
+    # the per-channel scales are powers of two and the packed bytes are e4m3(w / scale)
+    assert torch.all(torch.log2(scale) == torch.round(torch.log2(scale)))
+    for i in (1, 6):  # res conv 16->16 @8x8, res conv 32->32 @4x4
+        L = enc.layers[i]
+        sc = scale[so[i]:so[i] + L.cout].view(-1, 1, 1, 1)
+        wq = _q8(ws[i] / sc) * sc
+        x = torch.randn(5, L.H, L.W, L.cin).bfloat16()
+        add = torch.randn(5, L.H, L.W, L.cout).bfloat16()
+        b = torch.randn(L.cout) * 0.1
+        y = enc._fwd8(i, x.to(cuda), b.to(cuda), add=add.to(cuda))
+        xr = _q8(F.relu(x.float())).permute(0, 3, 1, 2)
+        yr = F.conv2d(xr, wq, b, padding=1).permute(0, 2, 3, 1) + add.float()
+        torch.testing.assert_close(y.float().cpu(), yr, rtol=2e-2, atol=2e-2)
+    L0 = enc.layers[0]
+    obs = _random_obs_bits(3, 256, seed=6)
+    b0 = torch.randn(16) * 0.1
+    p = enc._fwd8(0, obs.to(cuda), b0.to(cuda))
+    sc0 = scale[:16].view(-1, 1, 1, 1)
+    cr = F.conv2d(bits_to_planes(obs, 16, 16), _q8(ws[0] / sc0) * sc0, b0, padding=1)
+    pr = F.max_pool2d(cr.bfloat16().float(), 3, 2, 1)
+    torch.testing.assert_close(p.float().cpu().permute(0, 3, 1, 2), pr, rtol=2e-2, atol=2e-2)
+
+
+def test_fp8_trunk_close_to_bf16_trunk(cuda):
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(5)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(64, 256, seed=8).to(cuda)
+    m.features(obs[:2])
+    params = encoder_params(m.network, 3)
+    y16 = encode(obs, m._hip_enc, params, False).float()
+    m._hip_enc.fp8 = True
+    y8 = encode(obs, m._hip_enc, params, False).float()
+    rel = ((y8 - y16).norm() / y16.norm()).item()
+    assert rel < 0.08, rel
