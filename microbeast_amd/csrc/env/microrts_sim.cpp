@@ -299,7 +299,8 @@ int MicroRTSSim::dir_toward(const Unit& u, int tx, int ty) const {
 // Scripted opponents (stand-ins for coacAI, randomBiasedAI, lightRushAI,
 // workerRushAI — libs/utils.py:69-72). They act through exec() with the same
 // validity rules as the learning agent.
-void MicroRTSSim::bot_unit(int uid, int player, float* rwo) {
+void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n_barracks,
+                           int widx) {
   Unit& u = units_[uid];
   uint8_t a[7] = {0, 0, 0, 0, 0, 0, 0};
   const int enemy = 1 - player;
@@ -361,19 +362,6 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo) {
     if (e < 0) return false;
     return move_to(units_[e].x, units_[e].y);
   };
-
-  // count own workers / barracks for the build orders
-  int n_workers = 0, n_barracks = 0;
-  for (const Unit& t : units_)
-    if (t.alive && t.owner == player) {
-      n_workers += t.type == WORKER;
-      n_barracks += t.type == BARRACKS;
-    }
-  // index of this worker among own workers (first one harvests)
-  int widx = 0;
-  if (u.type == WORKER)
-    for (int i = 0; i < uid; ++i)
-      if (units_[i].alive && units_[i].owner == player && units_[i].type == WORKER) ++widx;
 
   switch (bot_) {
     case BOT_PASSIVE: return;
@@ -453,10 +441,22 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo) {
 }
 
 void MicroRTSSim::bot_act(int player, float* rwo) {
+  // own worker / barracks counts for the build orders (taken once per tick), and each
+  // worker's index among own workers in unit order (the first ones harvest)
+  int n_workers = 0, n_barracks = 0;
+  for (const Unit& t : units_)
+    if (t.alive && t.owner == player) {
+      n_workers += t.type == WORKER;
+      n_barracks += t.type == BARRACKS;
+    }
   const size_t n = units_.size();
+  int widx = 0;
   for (size_t i = 0; i < n; ++i) {
-    if (!units_[i].alive || units_[i].owner != player || units_[i].busy > 0) continue;
-    bot_unit((int)i, player, rwo);
+    const Unit& u = units_[i];
+    if (!u.alive || u.owner != player) continue;
+    const bool worker = u.type == WORKER;
+    if (u.busy == 0) bot_unit((int)i, player, rwo, n_workers, n_barracks, widx);
+    widx += worker;
   }
 }
 
@@ -473,7 +473,12 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
     if (g < 0) continue;
     const Unit& u = units_[g];
     if (u.owner != 0 || u.busy > 0) continue;
+    uint8_t tmp[kActComps];
     const uint8_t* a = actions + (size_t)c * kActComps;
+    if (p16_) {  // packed fast path: decode only cells that hold an idle own unit
+      mbr::unpack_env_action(p16_[c], tmp);
+      a = tmp;
+    }
     if (!validate_) {  // the mask lives on the GPU; exec() re-checks feasibility itself
       if (a[0] < 6) exec(g, a, rw);
       continue;
@@ -495,13 +500,18 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
   if (external_opp_) {
     for (int c = 0; c < nc; ++c) {
       // opponent actions are given in its own (mirrored) frame
-      const uint8_t* ap = &opp_actions_[(size_t)c * kActComps];
       int rx, ry;
       map_xy(1, c % s_, c / s_, &rx, &ry);
       const int g = grid_[cell(rx, ry)];
       if (g < 0) continue;
       const Unit& u = units_[g];
       if (u.owner != 1 || u.busy > 0) continue;
+      uint8_t otmp[kActComps];
+      const uint8_t* ap = &opp_actions_[(size_t)c * kActComps];
+      if (opp16_) {
+        mbr::unpack_env_action(opp16_[c], otmp);
+        ap = otmp;
+      }
       if (ap[0] >= 6) continue;
       // fast path: the opponent's mask lives on the GPU; exec() re-checks feasibility
       if (validate_ && !getbit(&mask_p1_[(size_t)c * kMaskWords], ap[0])) continue;
@@ -547,31 +557,33 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
 }
 
 float MicroRTSSim::step_packed(const uint16_t* env_actions, bool* done) {
-  const int nc = s_ * s_;
-  for (int c = 0; c < nc; ++c) mbr::unpack_env_action(env_actions[c], &act_buf_[(size_t)c * kActComps]);
-  return step(act_buf_.data(), done, nullptr);
+  p16_ = env_actions;
+  const float r = step(nullptr, done, nullptr);
+  p16_ = nullptr;
+  return r;
 }
 
 float MicroRTSSim::step_packed2(const uint16_t* env_actions, const uint16_t* opp_actions,
                                 bool* done) {
   // the opponent's packed actions are in its own (mirrored) frame, as set_opponent_actions
-  const int nc = s_ * s_;
-  for (int c = 0; c < nc; ++c)
-    mbr::unpack_env_action(opp_actions[c], &opp_actions_[(size_t)c * kActComps]);
-  return step_packed(env_actions, done);
+  opp16_ = opp_actions;
+  const float r = step_packed(env_actions, done);
+  opp16_ = nullptr;
+  return r;
 }
 
 void MicroRTSSim::write_obs_codes_as(int player, uint16_t* out) const {
+  // empty cells are code 0: clear, then overlay the live units
   const int nc = s_ * s_;
-  for (int c = 0; c < nc; ++c) {
-    int rx, ry;
-    map_xy(player, c % s_, c / s_, &rx, &ry);
-    const int g = grid_[cell(rx, ry)];
-    if (g < 0) { out[c] = mbr::cell_code(0, 0, 0, 0, 0); continue; }
-    const Unit& u = units_[g];
+  std::memset(out, 0, (size_t)nc * sizeof(uint16_t));
+  for (const Unit& u : units_) {
+    if (!u.alive) continue;
+    int px, py;
+    map_xy(player, u.x, u.y, &px, &py);
     const int own = u.owner < 0 ? 0 : (u.owner == player ? 1 : 2);
-    out[c] = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
-                            std::min<int>(std::max<int>(u.res, 0), 4), own, u.type, u.act);
+    out[cell(px, py)] = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
+                                       std::min<int>(std::max<int>(u.res, 0), 4), own, u.type,
+                                       u.act);
   }
 }
 

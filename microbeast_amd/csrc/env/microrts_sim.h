@@ -117,6 +117,8 @@ class MicroRTSSim {
   std::vector<uint32_t> mask_;    // cached agent mask (s*s*3)
   std::vector<uint32_t> mask_p1_; // cached opponent mask (for self-play / validation)
   std::vector<uint8_t> opp_actions_;
+  const uint16_t* p16_ = nullptr;    // step_packed: agent actions decoded lazily per cell
+  const uint16_t* opp16_ = nullptr;  // step_packed2: opponent's packed actions
 
   uint32_t rand_u32();
   float rand_unit();
@@ -130,7 +132,7 @@ class MicroRTSSim {
   // Returns true if the action was valid and executed.
   bool exec(int uid, const uint8_t* a, float* rw);
   void bot_act(int player, float* rw_opp);
-  void bot_unit(int uid, int player, float* rw_opp);
+  void bot_unit(int uid, int player, float* rw_opp, int n_workers, int n_barracks, int widx);
   int nearest(int uid, int owner_filter, int type_filter, int* dist) const;
   int dir_toward(const Unit& u, int tx, int ty) const;
   void map_xy(int player, int x, int y, int* ox, int* oy) const;
