@@ -1,8 +1,9 @@
+# Bench sweep over engine pipelining parameters (one GPU). Usage: bash tools/gpu_sweep.sh
 set -o pipefail
-R=$GRAFT_REPO_ROOT
+R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
-timeout -k 10 200 python tools/microbench.py --E 256,1024,4096 --learn_B 1024 > gpurun_out/micro2.log 2>&1 || exit 1
-for cfg in "2 1024 1" "2 2048 1" "4 1024 1" "2 4096 1"; do
+for cfg in "2 4096 0" "3 4096 0" "4 2048 0" "4 4096 0" "2 4096 8" "3 4096 8" "6 2048 0"; do
   set -- $cfg
-  timeout -k 10 200 python bench.py --steps 15 --warmup 3 --groups $1 --envs_per_group $2 --batch_slots $3 > gpurun_out/sweep_$1_$2_$3.log 2>&1 || exit 2
+  timeout -k 10 200 python bench.py --steps 20 --warmup 4 --groups $1 --envs_per_group $2 \
+    --learner_cu_reserve $3 > gpurun_out/sweep2_$1_$2_$3.log 2>&1 || exit 2
 done

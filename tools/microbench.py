@@ -39,6 +39,8 @@ def main():
         g = rt.graph
         for _ in range(5):
             g.replay()
+        if os.environ.get("MBK_MICRO_POLICY_ITERS"):
+            a.iters = int(os.environ["MBK_MICRO_POLICY_ITERS"])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(a.iters):
@@ -53,7 +55,7 @@ def main():
     from microbeast_amd.envs.synthetic import create_env
 
     T = a.learn_T
-    for B in [int(x) for x in a.learn_B.split(",")]:
+    for B in [int(x) for x in a.learn_B.split(",") if x]:
         env = create_env(s, B, 2000, seed=1)
         S = s * s
         obs = torch.zeros(T + 1, B, S, dtype=torch.int32)
