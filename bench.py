@@ -33,7 +33,7 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--size", type=int, default=16)
-    p.add_argument("--groups", type=int, default=2)
+    p.add_argument("--groups", type=int, default=3)
     p.add_argument("--envs_per_group", type=int, default=4096)
     p.add_argument("--unroll", type=int, default=64)
     p.add_argument("--batch_slots", type=int, default=1)

@@ -244,7 +244,8 @@ PYBIND11_MODULE(_mbrt, m) {
         }
         return new GpuEngine(cfg, buf);
       }))
-      .def("start", &GpuEngine::start, py::arg("graph_exec"), py::arg("opp_graph_exec") = 0)
+      .def("start", &GpuEngine::start, py::arg("graph_exec"), py::arg("opp_graph_exec") = 0,
+           py::arg("pack_graph_exec") = 0, py::arg("opp_pack_graph_exec") = 0)
       .def("stop", [](GpuEngine& e) { py::gil_scoped_release g; e.stop(); })
       .def("get_full",
            [](GpuEngine& e, int n, double timeout) {

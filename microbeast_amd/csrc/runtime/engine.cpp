@@ -132,12 +132,15 @@ std::string GpuEngine::error() const {
   return err_;
 }
 
-void GpuEngine::start(uintptr_t graph_exec, uintptr_t opp_graph_exec) {
+void GpuEngine::start(uintptr_t graph_exec, uintptr_t opp_graph_exec, uintptr_t pack_graph_exec,
+                      uintptr_t opp_pack_graph_exec) {
   if (running_.load()) return;
   if (cfg_.selfplay_groups > 0 && !opp_graph_exec)
     throw std::runtime_error("GpuEngine::start: self-play groups need the opponent graph");
   graph_ = (hipGraphExec_t)graph_exec;
   opp_graph_ = (hipGraphExec_t)opp_graph_exec;
+  pack_graph_[0] = (hipGraphExec_t)pack_graph_exec;
+  pack_graph_[1] = (hipGraphExec_t)opp_pack_graph_exec;
   running_.store(true);
   for (int w = 0; w < cfg_.n_threads; ++w) workers_.emplace_back(&GpuEngine::worker_loop, this, w);
   driver_ = std::thread(&GpuEngine::driver_loop, this);
@@ -224,6 +227,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       ENG_CHECK(hipStreamWaitEvent(stream_, P.ready, 0));
       ENG_CHECK(hipMemcpyAsync((void*)P.dst, P.staging, P.n, hipMemcpyDeviceToDevice, stream_));
       ENG_CHECK(hipEventRecord(P.consumed, stream_));
+      if (pack_graph_[c]) ENG_CHECK(hipGraphLaunch(pack_graph_[c], stream_));
       P.pending = false;
       if (c == 0) publishes_.fetch_add(1);
       else {

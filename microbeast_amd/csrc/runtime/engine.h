@@ -91,8 +91,12 @@ class GpuEngine {
  public:
   GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf);
   ~GpuEngine();
-  // opp_graph_exec: the opponent policy graph (required iff selfplay_groups > 0)
-  void start(uintptr_t graph_exec, uintptr_t opp_graph_exec = 0);
+  // opp_graph_exec: the opponent policy graph (required iff selfplay_groups > 0).
+  // pack_graph_exec / opp_pack_graph_exec (optional): replayed right after a publish on the
+  // matching channel lands, to rebuild the derived inference weights (packed conv / head
+  // blocks, bf16 copies) so the policy graph itself never re-packs.
+  void start(uintptr_t graph_exec, uintptr_t opp_graph_exec = 0, uintptr_t pack_graph_exec = 0,
+             uintptr_t opp_pack_graph_exec = 0);
   void stop();
   // Blocks until n full slots are available (or timeout). Returns slot ids.
   std::vector<int> get_full(int n, double timeout_s);
@@ -147,6 +151,7 @@ class GpuEngine {
   hipStream_t stream_ = nullptr;
   hipGraphExec_t graph_ = nullptr;
   hipGraphExec_t opp_graph_ = nullptr;
+  hipGraphExec_t pack_graph_[2] = {nullptr, nullptr};
   std::vector<std::unique_ptr<Group>> groups_;
   // pinned staging, all envs contiguous
   uint16_t* h_codes_ = nullptr;  // 16-bit cell codes

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from ..ops import cell_head
 from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.head import SparseHead, sparse_sample, sparse_score
-from ..ops.linear import linear
+from ..ops.linear import linear, nhwc_weight
 from ..ops.obs import bits_to_planes
 
 
@@ -91,6 +91,8 @@ class Agent(nn.Module):
         self._hip_enc = None
         self._hip_head = None
         self.fp8_inference = False  # acting trunk on the fp8 MFMA convs (see HipEncoder)
+        self._prepacked = False     # inference copy: derived weight buffers are current
+        self._fc_cache = None
         h, w, c = obs_space_shape
         self.h, self.w, self.planes = h, w, c
         self.mapsize = mapsize if mapsize is not None else h * w
@@ -138,14 +140,17 @@ class Agent(nn.Module):
             # gradient-carrying forwards always run the bf16 kernels
             self._hip_enc.fp8 = self.fp8_inference
             n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
+            grad = torch.is_grad_enabled()
+            pre = self._prepacked and not grad
             y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
-                       encoder_params(self.network, len(self.channels)), torch.is_grad_enabled())
+                       encoder_params(self.network, len(self.channels)), grad, prepacked=pre)
             # ReLU -> network.5 -> ReLU on the NHWC rows: the Linear's input columns are
             # permuted from the reference's NCHW flatten order instead of the activations
             nseq = len(self.channels)
             _, ho, wo, c = y.shape
             f = F.relu(y.reshape(n, -1))
-            f = linear(f, self.network[nseq + 2], nhwc=(c, ho, wo))
+            f = linear(f, self.network[nseq + 2], nhwc=(c, ho, wo),
+                       cached=(self._fc_cache["w5"], self._fc_cache["b5"]) if pre else None)
             return F.relu(f)
         x = self._planes(obs)
         with self._autocast(x):
@@ -163,6 +168,41 @@ class Agent(nn.Module):
         return tuple()
 
     # ------------------------------------------------------------ acting / learning
+    @torch.no_grad()
+    def pack_inference(self, device) -> None:
+        """Refresh every derived inference buffer from the fp32 parameters: packed conv
+        weights (bf16 or fp8), the sparse head's packed blocks and bf16 FC/critic weights.
+        After the first call, no-grad forwards skip all per-call packing (the acting graph
+        is then only compute; the GPU engine replays a captured pack graph after each
+        weight publish). Only for an inference copy whose weights change through publish."""
+        dev = torch.device(device)
+        if self._hip_enc is None or self._hip_enc.packed_fwd.device != dev:
+            self._hip_enc = HipEncoder(self.h, self.w, self.planes, self.channels, dev)
+        enc = self._hip_enc
+        enc.fp8 = self.fp8_inference
+        ws = [p.detach() for p in encoder_params(self.network, len(self.channels))[0::2]]
+        if enc.fp8:
+            enc.pack_fp8(ws)
+        else:
+            enc.pack(ws, with_bwd=False)
+        self._head(dev).pack(self.actor.weight, self.actor.bias, with_t=False)
+        nseq = len(self.channels)
+        fc = self.network[nseq + 2]
+        w5 = nhwc_weight(fc.weight.detach(), (enc.out_c,) + tuple(enc.out_hw))
+        if self._fc_cache is None:
+            self._fc_cache = {"w5": torch.empty(w5.shape, dtype=torch.bfloat16, device=dev),
+                              "b5": torch.empty(fc.bias.shape, dtype=torch.bfloat16, device=dev),
+                              "wc": torch.empty(self.critic.weight.shape, dtype=torch.bfloat16,
+                                                device=dev),
+                              "bc": torch.empty(self.critic.bias.shape, dtype=torch.bfloat16,
+                                                device=dev)}
+        c = self._fc_cache
+        c["w5"].copy_(w5)
+        c["b5"].copy_(fc.bias.detach())
+        c["wc"].copy_(self.critic.weight.detach())
+        c["bc"].copy_(self.critic.bias.detach())
+        self._prepacked = True
+
     def _head(self, dev) -> SparseHead:
         if self._hip_head is None or self._hip_head.device != dev:
             self._hip_head = SparseHead(self.h * self.w, dev)
@@ -175,11 +215,14 @@ class Agent(nn.Module):
         if self._use_hip(obs):
             # sparse head: only cells with a legal action are computed (ops/head.py)
             f = self.features(obs)
-            value = linear(f, self.critic).float().view(-1)
+            pre = self._prepacked
+            value = linear(f, self.critic, cached=(self._fc_cache["wc"], self._fc_cache["bc"])
+                           if pre else None).float().view(-1)
             n = f.shape[0]
             action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
                                          mask_bits.reshape(n, -1, 3), rng_state,
-                                         self._head(f.device), action_out, logp_out)
+                                         self._head(f.device), action_out, logp_out,
+                                         prepacked=pre)
             return action, logp, value
         logits, value = self.policy_value(obs)
         action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)

@@ -195,12 +195,15 @@ class HipEncoder:
                                    dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
 
     # ------------------------------------------------------------ passes
-    def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool):
-        """params: [w0, b0, w1, b1, ...] fp32 in layer order. Returns (out NHWC bf16, saved)."""
+    def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool,
+                prepacked: bool = False):
+        """params: [w0, b0, w1, b1, ...] fp32 in layer order. Returns (out NHWC bf16, saved).
+        prepacked: the packed weight buffers are current (inference after pack_inference)."""
         ws, bs = params[0::2], params[1::2]
         x = obs_bits.contiguous()
         if self.fp8 and not save:
-            self.pack_fp8([w.detach() for w in ws])
+            if not prepacked:
+                self.pack_fp8([w.detach() for w in ws])
             for st in range(len(self.layers) // 5):
                 i = 5 * st
                 p = self._fwd8(i, x, bs[i].detach())
@@ -209,7 +212,8 @@ class HipEncoder:
                 u1 = self._fwd8(i + 3, y0, bs[i + 3].detach())
                 x = self._fwd8(i + 4, u1, bs[i + 4].detach(), add=y0)
             return x, []
-        self.pack([w.detach() for w in ws], with_bwd=save)
+        if not prepacked or save:
+            self.pack([w.detach() for w in ws], with_bwd=save)
         saved = []
         li = 0
         n = x.shape[0]
@@ -289,9 +293,10 @@ def encoder_params(network: torch.nn.Sequential, n_stages: int) -> list[torch.nn
 
 
 def encode(obs_bits: torch.Tensor, enc: HipEncoder, params: list[torch.Tensor],
-           need_grad: bool) -> torch.Tensor:
+           need_grad: bool, prepacked: bool = False) -> torch.Tensor:
     """NHWC bf16 trunk output [N, Ho, Wo, C]."""
     if need_grad:
         return _EncoderFn.apply(obs_bits, enc, *params)
     with torch.no_grad():
-        return enc.forward(obs_bits, [p.detach() for p in params], save=False)[0]
+        return enc.forward(obs_bits, [p.detach() for p in params], save=False,
+                           prepacked=prepacked)[0]

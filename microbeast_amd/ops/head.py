@@ -151,11 +151,13 @@ def sparse_score(X, W, b, mask_bits, action, head: SparseHead):
 
 
 @torch.no_grad()
-def sparse_sample(X, W, b, mask_bits, rng, head: SparseHead, action_out=None, logp_out=None):
+def sparse_sample(X, W, b, mask_bits, rng, head: SparseHead, action_out=None, logp_out=None,
+                  prepacked: bool = False):
     F = X.shape[0]
     if action_out is None:
         action_out = torch.empty(F, head.S, 7, dtype=torch.uint8, device=X.device)
-    head.pack(W, b, with_t=False)
+    if not prepacked:
+        head.pack(W, b, with_t=False)
     logp, _ = head.forward(X.contiguous(), mask_bits.contiguous(), action_out, sample=True,
                            rng=rng, logp_out=logp_out, want_ent=False)
     return action_out, logp

@@ -56,11 +56,18 @@ class _Linear(torch.autograd.Function):
         return gx, gw, gb
 
 
+def nhwc_weight(w: torch.Tensor, nhwc: tuple[int, int, int] | None) -> torch.Tensor:
+    """Permute a Linear weight's input columns from NCHW to NHWC flatten order."""
+    if nhwc is None:
+        return w
+    c, h, wd = nhwc
+    return w.view(w.shape[0], c, h, wd).permute(0, 2, 3, 1).reshape(w.shape[0], -1)
+
+
 def linear(x: torch.Tensor, layer: torch.nn.Linear, dtype=torch.bfloat16,
-           nhwc: tuple[int, int, int] | None = None) -> torch.Tensor:
-    """``layer(x)`` computed in ``dtype`` with the split-K weight gradient."""
-    w = layer.weight
-    if nhwc is not None:
-        c, h, wd = nhwc
-        w = w.view(w.shape[0], c, h, wd).permute(0, 2, 3, 1).reshape(w.shape[0], -1)
-    return _Linear.apply(x.to(dtype), w, layer.bias)
+           nhwc: tuple[int, int, int] | None = None, cached=None) -> torch.Tensor:
+    """``layer(x)`` computed in ``dtype`` with the split-K weight gradient.
+    cached: (weight, bias) already converted (inference with prepacked weights)."""
+    if cached is not None:
+        return torch.nn.functional.linear(x.to(dtype), cached[0], cached[1])
+    return _Linear.apply(x.to(dtype), nhwc_weight(layer.weight, nhwc), layer.bias)

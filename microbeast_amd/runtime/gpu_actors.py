@@ -83,6 +83,7 @@ class GpuActorRuntime:
         if fp8_policy:  # acting trunk on fp8 MFMA; V-trace corrects the behaviour/learner gap
             self.infer_model.fp8_inference = True
         self.infer_flat = FlatParams(self.infer_model, dev)
+        self.pack_graph = self._capture_pack(self.infer_model)
         self.graph = self._capture(self.io, self.infer_model, self.rng)
         self.selfplay_groups = int(selfplay_groups)
         self.opp_graph = None
@@ -94,6 +95,7 @@ class GpuActorRuntime:
             self.opp_model.eval()
             self.opp_model.fp8_inference = fp8_policy
             self.opp_flat = FlatParams(self.opp_model, dev)
+            self.opp_pack_graph = self._capture_pack(self.opp_model)
             self.opp_graph = self._capture(self.io_p1, self.opp_model, self.rng_p1)
         if n_threads is None:
             n_threads = max(1, min(32, available_cpus() - 3))
@@ -149,6 +151,23 @@ class GpuActorRuntime:
                                        io["out_act16"].data_ptr(), N.stream_ptr()),
                 "pack_env_actions")
 
+    def _capture_pack(self, model):
+        """Graph of ``model.pack_inference`` (derived weight buffers), replayed by the engine
+        after each publish; the policy graph then never re-packs (None: model has none)."""
+        if not hasattr(model, "pack_inference"):
+            return None
+        s = torch.cuda.Stream(device=self.device)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            model.pack_inference(self.device)  # allocates the persistent buffers
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            model.pack_inference(self.device)
+        torch.cuda.synchronize()
+        return g
+
     def _capture(self, io, model, rng):
         s = torch.cuda.Stream(device=self.device)
         s.wait_stream(torch.cuda.current_stream())
@@ -170,9 +189,13 @@ class GpuActorRuntime:
             self.infer_flat.data.copy_(learner_flat.data)
             if self.selfplay_groups > 0:
                 self.opp_flat.data.copy_(learner_flat.data)  # until the league picks one
-            torch.cuda.synchronize()
-        opp = int(self.opp_graph.raw_cuda_graph_exec()) if self.opp_graph is not None else 0
-        self.engine.start(int(self.graph.raw_cuda_graph_exec()), opp)
+        for pg in (self.pack_graph, getattr(self, "opp_pack_graph", None)):
+            if pg is not None:
+                pg.replay()
+        torch.cuda.synchronize()
+        ex = lambda g: int(g.raw_cuda_graph_exec()) if g is not None else 0  # noqa: E731
+        self.engine.start(ex(self.graph), ex(self.opp_graph), ex(self.pack_graph),
+                          ex(getattr(self, "opp_pack_graph", None)))
         self.started = True
 
     def stop(self):
