@@ -74,6 +74,11 @@ _SIGS = {
     "mbk_head_dx_gather": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "mbk_head_pack": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_decode_obs_mask": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_decode_obs_mask_bucket": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mbk_head_units": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p],
+    "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
 }
 

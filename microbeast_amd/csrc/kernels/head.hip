@@ -188,6 +188,43 @@ __global__ __launch_bounds__(256) void head_scatter_kernel(
   }
 }
 
+// Acting path: per-cell bucket counters (filled by decode_obs_mask's BUCKET variant) ->
+// group ranges (cell c's pairs are bucket[c*E, c*E + cnt)) and the 16-pair unit list; the
+// counters are reset for the next step. One workgroup, S <= MAX_S.
+__global__ __launch_bounds__(1024) void head_units_kernel(int* __restrict__ cnt, int S, int E,
+                                                          int* __restrict__ grp_start,
+                                                          int* __restrict__ grp_count,
+                                                          int* __restrict__ unit_cell,
+                                                          int* __restrict__ unit_row,
+                                                          int* __restrict__ totals) {
+  __shared__ int su[1024];
+  const int tid = threadIdx.x;
+  int v = 0, u = 0;
+  if (tid < S) {
+    v = cnt[tid];
+    u = (v + 15) / 16;
+  }
+  su[tid] = u;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int b = tid >= o ? su[tid - o] : 0;
+    __syncthreads();
+    su[tid] += b;
+    __syncthreads();
+  }
+  if (tid < S) {
+    grp_start[tid] = tid * E;
+    grp_count[tid] = v;
+    cnt[tid] = 0;
+    const int u0 = su[tid] - u;
+    for (int k = 0; k < u; ++k) {
+      unit_cell[u0 + k] = tid;
+      unit_row[u0 + k] = tid * E + 16 * k;
+    }
+  }
+  if (tid == 1023) totals[1] = su[1023];
+}
+
 // ------------------------------------------------------------------ forward
 // Persistent: each wave takes 16-pair units until none is left.
 __global__ __launch_bounds__(256) void head_fwd_kernel(
@@ -538,6 +575,14 @@ extern "C" int mbk_head_compact(const uint32_t* mask, int F, int S, int* cnt, in
                      totals);
   hipLaunchKernelGGL(head_scatter_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, off, pairs,
                      pidx, action_zero, cell_lp, cell_ent);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_head_units(int* bucket_cnt, int S, int E, int* grp_start, int* grp_count,
+                              int* unit_cell, int* unit_row, int* totals, hipStream_t stream) {
+  if (S > MAX_S) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_units_kernel, dim3(1), dim3(1024), 0, stream, bucket_cnt, S, E,
+                     grp_start, grp_count, unit_cell, unit_row, totals);
   return (int)hipGetLastError();
 }
 

@@ -108,8 +108,10 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
 
 // Per-sample sums of per-cell values: out[n] = sum_c in[n, c] (one wave per sample).
 __global__ __launch_bounds__(256) void row_sum_kernel(const float* __restrict__ in, int64_t rows,
-                                                       int cols, float* __restrict__ out) {
+                                                       int cols, float* __restrict__ out,
+                                                       uint64_t* __restrict__ rng) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (rng && blockIdx.x == 0 && threadIdx.x == 0) rng[1] += 1;  // fused sampler step advance
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   if (r >= rows) return;
   float s = 0.f;
@@ -157,7 +159,17 @@ extern "C" int mbk_masked_cell_bwd(const void* logits, int logits_bf16, const ui
 extern "C" int mbk_row_sum(const float* in, int64_t rows, int cols, float* out,
                            hipStream_t stream) {
   dim3 grid((unsigned)((rows + 3) / 4));
-  hipLaunchKernelGGL(row_sum_kernel, grid, dim3(256), 0, stream, in, rows, cols, out);
+  hipLaunchKernelGGL(row_sum_kernel, grid, dim3(256), 0, stream, in, rows, cols, out,
+                     (uint64_t*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// row sums + advance the sampler's step counter (after the sampling kernel read it)
+extern "C" int mbk_row_sum_rng(const float* in, int64_t rows, int cols, float* out, uint64_t* rng,
+                               hipStream_t stream) {
+  if (rows <= 0) return 0;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipLaunchKernelGGL(row_sum_kernel, grid, dim3(256), 0, stream, in, rows, cols, out, rng);
   return (int)hipGetLastError();
 }
 

@@ -17,12 +17,26 @@ using namespace mbr;
 
 __device__ __forceinline__ void setb(uint32_t w[3], int j) { w[j >> 5] |= 1u << (j & 31); }
 
+// Per-step sparse-head bookkeeping for acting (BUCKET): every active (env, cell) pair is
+// appended to its cell's bucket (bucket[c * E + slot], slot from an atomic counter; order
+// inside a bucket is irrelevant for sampling: the RNG is keyed by (frame, cell)), and the
+// outputs of inactive cells (action, cell log-prob) are zeroed here instead of by a
+// separate pass. head.hip's head_units_kernel turns the counters into the unit list.
+struct Buckets {
+  int* cnt;        // [S] (zero on entry; reset by head_units_kernel)
+  int* bucket;     // [S][E]
+  float* cell_lp;  // [E*S]
+  uint8_t* action; // [E*S*7]
+};
+
 // one workgroup per env; LDS copy of the env's codes
+template <bool BUCKET>
 __global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __restrict__ codes,
                                                               const int32_t* __restrict__ res,
                                                               int H, int W,
                                                               uint32_t* __restrict__ obs,
-                                                              uint32_t* __restrict__ mask) {
+                                                              uint32_t* __restrict__ mask,
+                                                              Buckets bk) {
   extern __shared__ uint16_t cs[];
   const int S = H * W;
   const size_t e = blockIdx.x;
@@ -97,6 +111,17 @@ __global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __
     m[0] = w[0];
     m[1] = w[1];
     m[2] = w[2];
+    if (BUCKET) {
+      const size_t fc = e * S + c;
+      if (w[0] | w[1] | w[2]) {
+        const int slot = atomicAdd(&bk.cnt[c], 1);
+        bk.bucket[(size_t)c * gridDim.x + slot] = (int)e;
+      } else {
+        bk.cell_lp[fc] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) bk.action[fc * 7 + k] = 0;
+      }
+    }
   }
 }
 
@@ -117,8 +142,18 @@ __global__ __launch_bounds__(256) void pack_env_actions_kernel(const uint8_t* __
 extern "C" int mbk_decode_obs_mask(const uint16_t* codes, const int32_t* res, int n_envs, int H,
                                    int W, uint32_t* obs, uint32_t* mask, hipStream_t stream) {
   if (n_envs <= 0) return 0;
-  hipLaunchKernelGGL(decode_obs_mask_kernel, dim3(n_envs), dim3(256), H * W * 2, stream, codes,
-                     res, H, W, obs, mask);
+  hipLaunchKernelGGL(decode_obs_mask_kernel<false>, dim3(n_envs), dim3(256), H * W * 2, stream,
+                     codes, res, H, W, obs, mask, Buckets{nullptr, nullptr, nullptr, nullptr});
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_decode_obs_mask_bucket(const uint16_t* codes, const int32_t* res, int n_envs,
+                                          int H, int W, uint32_t* obs, uint32_t* mask,
+                                          int* bucket_cnt, int* bucket, float* cell_lp,
+                                          uint8_t* action, hipStream_t stream) {
+  if (n_envs <= 0) return 0;
+  hipLaunchKernelGGL(decode_obs_mask_kernel<true>, dim3(n_envs), dim3(256), H * W * 2, stream,
+                     codes, res, H, W, obs, mask, Buckets{bucket_cnt, bucket, cell_lp, action});
   return (int)hipGetLastError();
 }
 

@@ -210,8 +210,9 @@ class Agent(nn.Module):
 
     @torch.no_grad()
     def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
-            logp_out=None):
-        """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N])."""
+            logp_out=None, bucketed: bool = False):
+        """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N]).
+        bucketed: the head's active pairs were bucketed by mbk_decode_obs_mask_bucket."""
         if self._use_hip(obs):
             # sparse head: only cells with a legal action are computed (ops/head.py)
             f = self.features(obs)
@@ -222,7 +223,7 @@ class Agent(nn.Module):
             action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
                                          mask_bits.reshape(n, -1, 3), rng_state,
                                          self._head(f.device), action_out, logp_out,
-                                         prepacked=pre)
+                                         prepacked=pre, bucketed=bucketed)
             return action, logp, value
         logits, value = self.policy_value(obs)
         action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)

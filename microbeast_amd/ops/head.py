@@ -52,6 +52,35 @@ class SparseHead:
         self.cell_ent = torch.zeros(F * S, dtype=torch.float32, device=dev)
         self._F = F
 
+    # ------------------------------------------------------------ acting (bucketed) path
+    def ensure_buckets(self, E: int):
+        """Per-cell pair buckets filled by ``mbk_decode_obs_mask_bucket`` (acting only)."""
+        self._ensure(E)
+        if getattr(self, "_bucket_E", -1) != E:
+            self.bucket_cnt = torch.zeros(self.S, dtype=torch.int32, device=self.device)
+            self.bucket = torch.zeros(self.S * E, dtype=torch.int32, device=self.device)
+            self._bucket_E = E
+
+    def sample_bucketed(self, X: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor,
+                        rng: torch.Tensor, logp_out: torch.Tensor) -> torch.Tensor:
+        """Sample with the buckets the decode kernel built this step (no sort: 3 launches)."""
+        F = X.shape[0]
+        assert F == self._bucket_E
+        k = N.kernels()
+        st = N.stream_ptr()
+        N.check(k.mbk_head_units(self.bucket_cnt.data_ptr(), self.S, F, self.grp_start.data_ptr(),
+                                 self.grp_count.data_ptr(), self.unit_cell.data_ptr(),
+                                 self.unit_row.data_ptr(), self.totals.data_ptr(), st), "head_units")
+        N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
+                               mask_bits.data_ptr(), action.data_ptr(), rng.data_ptr(), 1,
+                               self.bucket.data_ptr(), self.unit_cell.data_ptr(),
+                               self.unit_row.data_ptr(), self.grp_start.data_ptr(),
+                               self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
+                               self.fwd_grid, self.cell_lp.data_ptr(), None, st), "head_fwd")
+        N.check(k.mbk_row_sum_rng(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
+                                  rng.data_ptr(), st), "row_sum_rng")
+        return logp_out
+
     def pack(self, W: torch.Tensor, b: torch.Tensor, with_t: bool):
         N.check(N.kernels().mbk_head_pack(W.data_ptr(), b.data_ptr(), self.S,
                                           self.Wp.data_ptr(), self.bp.data_ptr(),
@@ -152,12 +181,17 @@ def sparse_score(X, W, b, mask_bits, action, head: SparseHead):
 
 @torch.no_grad()
 def sparse_sample(X, W, b, mask_bits, rng, head: SparseHead, action_out=None, logp_out=None,
-                  prepacked: bool = False):
+                  prepacked: bool = False, bucketed: bool = False):
     F = X.shape[0]
     if action_out is None:
         action_out = torch.empty(F, head.S, 7, dtype=torch.uint8, device=X.device)
     if not prepacked:
         head.pack(W, b, with_t=False)
+    if bucketed:  # pairs were bucketed by the decode kernel (GPU actor engine)
+        if logp_out is None:
+            logp_out = torch.empty(F, dtype=torch.float32, device=X.device)
+        return action_out, head.sample_bucketed(X.contiguous(), mask_bits.contiguous(),
+                                                action_out, rng, logp_out)
     logp, _ = head.forward(X.contiguous(), mask_bits.contiguous(), action_out, sample=True,
                            rng=rng, logp_out=logp_out, want_ent=False)
     return action_out, logp

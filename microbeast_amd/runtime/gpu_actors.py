@@ -136,13 +136,22 @@ class GpuActorRuntime:
     def _policy_step(self, io, m, rng):
         k = N.kernels()
         st = N.stream_ptr()
-        N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(), self.E,
-                                      self.size, self.size, io["in_obs"].data_ptr(),
-                                      io["in_mask"].data_ptr(), st), "decode_obs_mask")
-        if hasattr(m, "_use_hip") and m._use_hip(io["in_obs"]):
-            _, _, value = m.act(io["in_obs"], io["in_mask"], rng,
-                                action_out=io["out_action"], logp_out=io["out_logp"])
+        hip = hasattr(m, "_use_hip") and m._use_hip(io["in_obs"])
+        if hip:
+            # decode + bucket the sparse head's active pairs by cell in the same pass
+            head = m._head(self.device)
+            head.ensure_buckets(self.E)
+            N.check(k.mbk_decode_obs_mask_bucket(
+                io["in_codes"].data_ptr(), io["in_res"].data_ptr(), self.E, self.size, self.size,
+                io["in_obs"].data_ptr(), io["in_mask"].data_ptr(), head.bucket_cnt.data_ptr(),
+                head.bucket.data_ptr(), head.cell_lp.data_ptr(), io["out_action"].data_ptr(),
+                st), "decode_obs_mask_bucket")
+            _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
+                                logp_out=io["out_logp"], bucketed=True)
         else:
+            N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
+                                          self.E, self.size, self.size, io["in_obs"].data_ptr(),
+                                          io["in_mask"].data_ptr(), st), "decode_obs_mask")
             logits, value = m.policy_value(io["in_obs"])
             cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
                                  cell_logp=self._cell_logp, logp_out=io["out_logp"])

@@ -75,3 +75,58 @@ def test_sparse_sample(cuda):
         assert bool(ok.all())
     lp2, _ = sparse_score(X.to(cuda), W.to(cuda), b.to(cuda), mb, a, head)
     torch.testing.assert_close(lp, lp2, rtol=1e-5, atol=1e-4)
+
+
+def test_bucketed_acting_path_matches_sorted_path(cuda):
+    """decode_obs_mask_bucket + head_units (atomic per-cell buckets) samples exactly the
+    actions / log-probs of the deterministic counting-sort path (same Philox keys)."""
+    from microbeast_amd import _native as N
+    from microbeast_amd.models.agent import Agent
+    rt = N.runtime()
+    s, E = 16, 300
+    S = s * s
+    env = rt.VecEnv(s, E, 400, 2, [0, 1, 2, 3])
+    env.set_validate(False)
+    codes = torch.zeros(E, S, dtype=torch.int16)
+    res = torch.zeros(E, dtype=torch.int32)
+    rew, done = torch.zeros(E), torch.zeros(E, dtype=torch.uint8)
+    env.reset(0, 0)
+    g = torch.Generator().manual_seed(0)
+    for _ in range(30):  # advance the games so there are many active cells
+        a16 = torch.randint(0, 1 << 14, (E, S), generator=g, dtype=torch.int32).to(torch.int16)
+        env.step_codes(a16.data_ptr(), codes.data_ptr(), res.data_ptr(), rew.data_ptr(),
+                       done.data_ptr())
+    torch.manual_seed(0)
+    m = Agent((s, s, 27)).to(cuda)
+    torch.nn.init.normal_(m.actor.weight, std=0.05)
+    cg, rg = codes.to(cuda), res.to(cuda)
+    obs = torch.empty(E, S, dtype=torch.int32, device=cuda)
+    mask = torch.empty(E, S, 3, dtype=torch.int32, device=cuda)
+    k = N.kernels()
+    N.check(k.mbk_decode_obs_mask(cg.data_ptr(), rg.data_ptr(), E, s, s, obs.data_ptr(),
+                                  mask.data_ptr(), N.stream_ptr()), "decode")
+    rng1 = torch.tensor([123, 7], dtype=torch.int64, device=cuda)
+    a1, lp1, v1 = m.act(obs, mask, rng1)
+    # bucketed path (prepacked weights as the engine uses them)
+    m.pack_inference(cuda)
+    head = m._head(cuda)
+    head.ensure_buckets(E)
+    obs2 = torch.empty_like(obs)
+    mask2 = torch.empty_like(mask)
+    a2 = torch.full((E, S, 7), 9, dtype=torch.uint8, device=cuda)
+    lp2 = torch.empty(E, device=cuda)
+    N.check(k.mbk_decode_obs_mask_bucket(cg.data_ptr(), rg.data_ptr(), E, s, s, obs2.data_ptr(),
+                                         mask2.data_ptr(), head.bucket_cnt.data_ptr(),
+                                         head.bucket.data_ptr(), head.cell_lp.data_ptr(),
+                                         a2.data_ptr(), N.stream_ptr()), "decode_bucket")
+    rng2 = torch.tensor([123, 7], dtype=torch.int64, device=cuda)
+    _, _, v2 = m.act(obs2, mask2, rng2, action_out=a2, logp_out=lp2, bucketed=True)
+    torch.cuda.synchronize()
+    assert torch.equal(obs, obs2) and torch.equal(mask, mask2)
+    active = int((mask != 0).any(-1).sum())
+    assert active > 100
+    assert torch.equal(a1, a2)
+    torch.testing.assert_close(lp1, lp2, rtol=0, atol=0)
+    torch.testing.assert_close(v1, v2, rtol=1e-2, atol=1e-2)
+    assert rng1.tolist() == rng2.tolist() == [123, 8]
+    assert int(head.bucket_cnt.sum()) == 0  # counters reset for the next step
