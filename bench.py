@@ -83,12 +83,12 @@ def main(argv=None):
                          args.batch_slots, dev, n_threads=threads, seed=args.seed + 1000 * info.rank,
                          env_index_base=info.rank * envs_total,
                          selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy)
-    rt.start(learner.flat)
     league = None
     if args.selfplay_groups > 0:
         from microbeast_amd.runtime.league import League
         league = League(capacity=16, snapshot_every=5, seed=args.seed + info.rank)
-        league.add_snapshot(learner.flat.data)
+        league.current = league.add_snapshot(learner.flat.data)
+    rt.start(learner.flat, opponent_version=league.current if league is not None else -1)
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
     if args.learner_cu_reserve > 0:
         from microbeast_amd import _native as N

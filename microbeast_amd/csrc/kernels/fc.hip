@@ -155,7 +155,106 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   else out[e] = accumulate ? out[e] + s : s;
 }
 
+// Acting-path trunk tail, one launch: f = relu(relu(x) . W5^T + b5) (bf16 out) and the
+// critic v = f . wc + bc (fp32 out). One workgroup per 16 frames; its 4 waves split the
+// O hidden units (O/64 independent 16-wide blocks each). MFMA operands (A = W5 rows,
+// B = x rows) so a lane holds 4 consecutive hidden units of one frame: 8-byte stores of
+// f; critic partials reduce over lanes (shuffles) and waves (LDS). W5 (bf16,
+// NHWC-permuted) is read through L2; x rows are relu'd at load, once per wave.
+template <int O>
+__global__ __launch_bounds__(256) void fc_fwd_kernel(const bf16* __restrict__ x, int relu_in,
+                                                     const bf16* __restrict__ w5,
+                                                     const float* __restrict__ b5,
+                                                     const float* __restrict__ wc,
+                                                     const float* __restrict__ bc, int F, int I,
+                                                     bf16* __restrict__ f_out,
+                                                     float* __restrict__ v_out) {
+  constexpr int NBW = O / 64;  // 16-wide hidden blocks per wave
+  __shared__ float vred[4][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int r0 = blockIdx.x * 16;
+  const int row = r0 + li;
+  const bool valid = row < F;
+  const uint4* xr = (const uint4*)(x + (size_t)(valid ? row : r0) * I) + G;
+  const int nks = I / 32;
+  f32x4 acc[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ks = 0; ks < nks; ++ks) {
+    uint4 xv = valid ? xr[ks * 4] : make_uint4(0, 0, 0, 0);
+    if (relu_in) {
+      uint32_t w[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = (w[j] & 0x8000u) ? 0u : (w[j] & 0xFFFFu);
+        const uint32_t hi = (w[j] & 0x80000000u) ? 0u : (w[j] & 0xFFFF0000u);
+        w[j] = lo | hi;
+      }
+      xv = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    Frag8 b;
+    __builtin_memcpy(&b, &xv, 16);
+    uint4 wv[NBW];
+#pragma unroll
+    for (int j = 0; j < NBW; ++j)
+      wv[j] = ((const uint4*)(w5 + (size_t)((wave * NBW + j) * 16 + li) * I) + G)[ks * 4];
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      Frag8 a;
+      __builtin_memcpy(&a, &wv[j], 16);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[j], 0, 0, 0);
+    }
+  }
+  float vpart = 0.f;
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    const int h0 = (wave * NBW + j) * 16 + 4 * G;  // lane: hidden units h0..h0+3 of `row`
+    float hv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      // the critic consumes the bf16-rounded activations (what the head sees)
+      hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + b5[h0 + i], 0.f)));
+      vpart += hv[i] * wc[h0 + i];
+    }
+    uint32_t o[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
+             ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
+    if (valid) *(uint2*)(f_out + (size_t)row * O + h0) = make_uint2(o[0], o[1]);
+  }
+  vpart += __shfl_xor(vpart, 16, 64);
+  vpart += __shfl_xor(vpart, 32, 64);
+  if (G == 0) vred[wave][li] = vpart;
+  __syncthreads();
+  if (threadIdx.x < 16 && r0 + (int)threadIdx.x < F) {
+    const int t = threadIdx.x;
+    v_out[r0 + t] = vred[0][t] + vred[1][t] + vred[2][t] + vred[3][t] + bc[0];
+  }
+}
+
 }  // namespace
+
+extern "C" int mbk_fc_fwd(const void* x, int relu_in, const void* w5, const float* b5,
+                          const float* wc, const float* bc, int F, int I, int O, void* f_out,
+                          float* v_out, hipStream_t stream) {
+  if (F <= 0) return 0;
+  if (I % 32) return (int)hipErrorInvalidValue;
+  const int blocks = (F + 15) / 16;
+  if (O == 256)
+    hipLaunchKernelGGL(fc_fwd_kernel<256>, dim3(blocks), dim3(256), 0, stream, (const bf16*)x,
+                       relu_in, (const bf16*)w5, b5, wc, bc, F, I, (bf16*)f_out, v_out);
+  else if (O == 128)
+    hipLaunchKernelGGL(fc_fwd_kernel<128>, dim3(blocks), dim3(256), 0, stream, (const bf16*)x,
+                       relu_in, (const bf16*)w5, b5, wc, bc, F, I, (bf16*)f_out, v_out);
+  else if (O == 512)
+    hipLaunchKernelGGL(fc_fwd_kernel<512>, dim3(blocks), dim3(256), 0, stream, (const bf16*)x,
+                       relu_in, (const bf16*)w5, b5, wc, bc, F, I, (bf16*)f_out, v_out);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
 
 // number of K splits (partial rows) for an N x (O, I) problem
 extern "C" int mbk_fc_wgrad_parts(int N, int O, int I) {

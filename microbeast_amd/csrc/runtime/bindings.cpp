@@ -257,6 +257,7 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("release", &GpuEngine::release)
       .def("publish", &GpuEngine::publish)
       .def("publish_opponent", &GpuEngine::publish_opponent)
+      .def("set_initial_opponent", &GpuEngine::set_initial_opponent)
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
       .def("stream", &GpuEngine::stream)
       .def("failed", &GpuEngine::failed)

@@ -106,6 +106,8 @@ class GpuEngine {
   bool publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream) {
     return publish_chan(0, src, dst, nbytes, stream, -1);
   }
+  // League id of the opponent weights in place at start (before any publish_opponent).
+  void set_initial_opponent(int version) { opp_version_ = version; opp_version_pub_.store(version); }
   // League: swap the opponent policy's weights to snapshot `version` (same ordering).
   bool publish_opponent(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream,
                         int version) {

@@ -130,6 +130,27 @@ class Agent(nn.Module):
         return (self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32
                 and all(c in (16, 32) for c in self.channels))
 
+    def _act_features(self, obs: torch.Tensor):
+        """Acting forward with prepacked weights: conv trunk, then ONE fused launch for
+        relu -> network.5 -> relu -> critic (fc.hip). Returns (f bf16 [N,256], value fp32)."""
+        from .. import _native as N
+        n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
+        y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
+                   encoder_params(self.network, len(self.channels)), False, prepacked=True)
+        fc = self.network[len(self.channels) + 2]
+        I = y[0].numel()
+        if fc.out_features not in (128, 256, 512):  # no fused kernel instance: cached GEMMs
+            c = self._fc_cache
+            f = F.relu(linear(F.relu(y.reshape(n, -1)), fc, cached=(c["w5"], c["b5"])))
+            return f, linear(f, self.critic, cached=(c["wc"], c["bc"])).float().view(-1)
+        f = torch.empty(n, fc.out_features, dtype=torch.bfloat16, device=y.device)
+        v = torch.empty(n, dtype=torch.float32, device=y.device)
+        N.check(N.kernels().mbk_fc_fwd(y.data_ptr(), 1, self._fc_cache["w5"].data_ptr(),
+                                       fc.bias.data_ptr(), self.critic.weight.data_ptr(),
+                                       self.critic.bias.data_ptr(), n, I, fc.out_features,
+                                       f.data_ptr(), v.data_ptr(), N.stream_ptr()), "fc_fwd")
+        return f, v
+
     def features(self, obs: torch.Tensor) -> torch.Tensor:
         if self._use_hip(obs):
             # conv trunk on the HIP MFMA kernels (NHWC bf16), then the reference's
@@ -215,10 +236,13 @@ class Agent(nn.Module):
         bucketed: the head's active pairs were bucketed by mbk_decode_obs_mask_bucket."""
         if self._use_hip(obs):
             # sparse head: only cells with a legal action are computed (ops/head.py)
-            f = self.features(obs)
             pre = self._prepacked
-            value = linear(f, self.critic, cached=(self._fc_cache["wc"], self._fc_cache["bc"])
-                           if pre else None).float().view(-1)
+            if pre:
+                self._hip_enc.fp8 = self.fp8_inference
+                f, value = self._act_features(obs)
+            else:
+                f = self.features(obs)
+                value = linear(f, self.critic).float().view(-1)
             n = f.shape[0]
             action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
                                          mask_bits.reshape(n, -1, 3), rng_state,

@@ -193,7 +193,11 @@ class GpuActorRuntime:
         return g
 
     # ------------------------------------------------------------ control
-    def start(self, learner_flat: FlatParams | None = None):
+    def start(self, learner_flat: FlatParams | None = None, opponent_version: int = -1):
+        """opponent_version: league id of the starting opponent weights (self-play groups
+        start against a copy of ``learner_flat``; tag their episodes with this id)."""
+        if self.selfplay_groups > 0:
+            self.engine.set_initial_opponent(int(opponent_version))
         if learner_flat is not None:
             self.infer_flat.data.copy_(learner_flat.data)
             if self.selfplay_groups > 0:

@@ -91,7 +91,6 @@ def train(flags: Flags) -> dict:
                              bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
                              env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
                              fp8_policy=flags.fp8_policy)
-        rt.start(learner.flat)
         if sp_groups:
             from .runtime.league import League
 
@@ -102,6 +101,11 @@ def train(flags: Flags) -> dict:
                 league.load_state_dict(ck["league"], dev)
             else:
                 league.add_snapshot(learner.flat.data)
+            league.current = league.next_id - 1
+        rt.start(learner.flat, opponent_version=league.current if league is not None else -1)
+        if league is not None and ck is not None and ck.get("league"):
+            # resumed: play the restored snapshot instead of the learner copy
+            rt.set_opponent(league.snapshot(league.current), league.current)
         frames_per_update = flags.batch_size * flags.envs_per_group * flags.unroll_length
     else:
         from .runtime.mono import MonoRuntime

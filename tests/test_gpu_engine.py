@@ -69,13 +69,13 @@ def test_selfplay_league_engine(cuda):
     torch.manual_seed(1)
     learner = Learner(mk(), LearnerHParams(), cuda)
     rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=E, unroll=T, batch_slots=1,
-                         device=cuda, n_threads=2, max_steps=40, selfplay_groups=1)
+                         device=cuda, n_threads=2, max_steps=12, selfplay_groups=1)
     league = League(capacity=4, snapshot_every=2, eps=0.5, seed=3)
-    league.add_snapshot(learner.flat.data)
-    rt.start(learner.flat)
+    sid0 = league.add_snapshot(learner.flat.data)
+    rt.start(learner.flat, opponent_version=sid0)
     episodes = []
     try:
-        for it in range(16):
+        for it in range(24):  # >= 12 slots of T=8 per group: every env ends >= 4 episodes
             batch, slots = rt.get_batch()
             losses = learner.learn(batch)
             rt.release(slots)
@@ -94,6 +94,7 @@ def test_selfplay_league_engine(cuda):
     assert st["opp_publishes"] >= 1 and st["opp_version"] in league.snaps
     sp = [e for e in episodes if e[2] >= E]    # second group = self-play envs
     bots = [e for e in episodes if e[2] < E]
+    print("episodes", len(episodes), "selfplay", len(sp), "bots", len(bots), st)
     assert sp and bots
     assert all(e[4] >= 0 for e in sp) and all(e[4] < 0 for e in bots)
     assert sum(league.games.values()) == len(sp)

@@ -105,10 +105,10 @@ def test_bucketed_acting_path_matches_sorted_path(cuda):
     k = N.kernels()
     N.check(k.mbk_decode_obs_mask(cg.data_ptr(), rg.data_ptr(), E, s, s, obs.data_ptr(),
                                   mask.data_ptr(), N.stream_ptr()), "decode")
+    # prepacked weights as the engine uses them; path 1 = counting-sort compaction
+    m.pack_inference(cuda)
     rng1 = torch.tensor([123, 7], dtype=torch.int64, device=cuda)
     a1, lp1, v1 = m.act(obs, mask, rng1)
-    # bucketed path (prepacked weights as the engine uses them)
-    m.pack_inference(cuda)
     head = m._head(cuda)
     head.ensure_buckets(E)
     obs2 = torch.empty_like(obs)
@@ -130,3 +130,24 @@ def test_bucketed_acting_path_matches_sorted_path(cuda):
     torch.testing.assert_close(v1, v2, rtol=1e-2, atol=1e-2)
     assert rng1.tolist() == rng2.tolist() == [123, 8]
     assert int(head.bucket_cnt.sum()) == 0  # counters reset for the next step
+
+
+def test_fused_fc_forward_matches_torch(cuda):
+    """fc.hip fc_fwd: f = relu(relu(x) W5^T + b5) (bf16), v = f . wc + bc, vs fp32 torch."""
+    from microbeast_amd import _native as N
+    torch.manual_seed(3)
+    for n, I in ((1000, 128), (77, 32), (300, 288)):
+        x = torch.randn(n, I, device=cuda).bfloat16()
+        w5 = (torch.randn(256, I, device=cuda) * 0.1).bfloat16()
+        b5 = torch.randn(256, device=cuda) * 0.1
+        wc = torch.randn(256, device=cuda) * 0.1
+        bc = torch.randn(1, device=cuda)
+        f = torch.empty(n, 256, dtype=torch.bfloat16, device=cuda)
+        v = torch.empty(n, device=cuda)
+        N.check(N.kernels().mbk_fc_fwd(x.data_ptr(), 1, w5.data_ptr(), b5.data_ptr(),
+                                       wc.data_ptr(), bc.data_ptr(), n, I, 256, f.data_ptr(),
+                                       v.data_ptr(), N.stream_ptr()), "fc_fwd")
+        fr = torch.relu(torch.relu(x.float()) @ w5.float().t() + b5)
+        vr = fr.bfloat16().float() @ wc + bc
+        torch.testing.assert_close(f.float(), fr, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(v, vr, rtol=1e-3, atol=1e-3)
