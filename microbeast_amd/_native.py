@@ -81,6 +81,7 @@ _SIGS = {
     "mbk_head_units": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p],
     "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_trunk_tail": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
 }
 

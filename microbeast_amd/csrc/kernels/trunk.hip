@@ -1,0 +1,303 @@
+// Fused acting trunk: everything of the IMPALA encoder after the stage-0 conv + pool in
+// ONE persistent launch (reference model.py:56-107: 2 residual blocks, then two more
+// ConvSequences of conv -> maxpool -> 2 residual blocks; 14 convs, 2 pools, 12 relus,
+// 6 residual adds).
+//
+// Per-layer launches (conv.hip) round-trip every activation through HBM and pay a
+// launch each: at the acting batch (E = 4096 frames) the 14 convs cost ~125 us of the
+// ~195 us policy step, mostly fixed latency. Here a workgroup owns TNI images at a time
+// and keeps all of their activations in two LDS regions that the stages alias:
+//
+//   R1: X0 (stage-0 residual stream, 16 ch) -> X1 (32 ch) -> X2 (32 ch)
+//   R2: U0 (inner conv output)  -> stage-1 pre-pool staging -> U1 -> stage-2 staging -> U2
+//
+// Tiles are halo'd NHWC (pixel stride 2*C + 16 bytes); a producer phase zeroes the halo
+// of the tile it fills (disjoint from the interior it writes), so regions can change
+// layout between stages without extra passes. Each conv is an implicit GEMM on
+// v_mfma_f32_16x16x32_bf16 with (A = weights from L2 into VGPRs, B = pixels from LDS),
+// so a lane ends with 4 consecutive channels of one pixel. ReLU-on-input is applied to
+// the B fragments; the residual add reads the output tile in place. Inference only
+// (no saved activations); numerics identical to the per-layer kernels (bf16 storage,
+// fp32 accumulation, pool over bf16-rounded values).
+#include "../include/mbk_api.h"
+#include "common.h"
+
+#include <algorithm>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __hip_bfloat16 bf16;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int TNI = 4;  // images per workgroup iteration
+
+union Frag8 {
+  bf16x8 v;
+  uint4 u;
+};
+
+__device__ __forceinline__ uint32_t relu2(uint32_t w) {
+  const uint32_t lo = (w & 0x8000u) ? 0u : (w & 0xFFFFu);
+  const uint32_t hi = (w & 0x80000000u) ? 0u : (w & 0xFFFF0000u);
+  return lo | hi;
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(a)) |
+         ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(b)) << 16);
+}
+__device__ __forceinline__ float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
+template <int C>
+struct TG {
+  static constexpr int PIXB = C * 2 + 16;
+  static constexpr int NCH = C == 16 ? 5 : 9;
+};
+
+// zero the halo ring of a halo'd tile [nimg][(H+2)][(W+2)] of PIXB-byte pixels
+__device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W, int pixb) {
+  const int Hp = H + 2, Wp = W + 2;
+  const int per = 2 * Wp + 2 * H;  // halo pixels per image
+  const int q16 = pixb / 16;
+  const int tot = nimg * per * q16;
+  for (int e = threadIdx.x; e < tot; e += kThreads) {
+    const int q = e % q16, r = e / q16;
+    const int im = r / per, k = r - im * per;
+    int py, px;
+    if (k < Wp) { py = 0; px = k; }
+    else if (k < 2 * Wp) { py = Hp - 1; px = k - Wp; }
+    else { const int j = k - 2 * Wp; py = 1 + (j >> 1); px = (j & 1) ? Wp - 1 : 0; }
+    *(uint4*)(t + ((im * Hp + py) * Wp + px) * pixb + q * 16) = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// conv3x3 (pad 1) of a halo'd LDS tile. Output either into a halo'd tile (with optional
+// in-place residual add from the same tile) or into a dense bf16 staging [nimg][H][W][COUT]
+// (for the pool). relu_in applies to the input fragments.
+template <int CIN, int COUT>
+// noinline: works around an LLVM CGSCC-pass crash (ROCm 7.2) when fully force-inlined
+__device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W, int nimg, const bf16* __restrict__ w,
+                         const float* __restrict__ bias, bool relu_in, char* out, bool add,
+                         bf16* stg) {
+  constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
+  constexpr int PI = TG<CIN>::PIXB, PO = TG<COUT>::PIXB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int Hp = H + 2, Wp = W + 2, HW = H * W;
+  Frag8 bw[NCH][NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const uint4* wp = (const uint4*)(w + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
+  }
+  float bv[NB][4];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[nb][i] = bias[nb * 16 + 4 * g + i];
+  const int M = nimg * HW, nblk = (M + 15) >> 4;
+  for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+    const int m = pb * 16 + li;
+    const bool valid = m < M;
+    const int mm = valid ? m : 0;
+    const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
+    const int base = (im * Hp + y) * Wp + x;
+    f32x4 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      int tap, ch0;
+      if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
+      else { tap = c; ch0 = 8 * g; }
+      const int tapc = tap < 9 ? tap : 8;
+      Frag8 a;
+      a.u = *(const uint4*)(in + (base + (tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2);
+      if (relu_in) a.u = make_uint4(relu2(a.u.x), relu2(a.u.y), relu2(a.u.z), relu2(a.u.w));
+      if (!valid || (CIN == 16 && tap >= 9)) a.u = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, a.v, acc[nb], 0, 0, 0);
+    }
+    if (!valid) continue;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co0 = nb * 16 + 4 * g;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bv[nb][i];
+      if (stg) {
+        *(uint2*)(stg + (size_t)m * COUT + co0) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      } else {
+        char* p = out + (((im * Hp + y + 1) * Wp + x + 1) * PO + co0 * 2);
+        if (add) {
+          const uint2 ad = *(const uint2*)p;
+          v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
+        }
+        *(uint2*)p = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      }
+    }
+  }
+}
+
+// max_pool2d(3, 2, 1) of staging [nimg][H][W][C] into the interior of a halo'd tile
+template <int C>
+__device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg, char* out) {
+  constexpr int PO = TG<C>::PIXB, C4 = C / 4;
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  const int tot = nimg * Ho * Wo * C4;
+  for (int e = threadIdx.x; e < tot; e += kThreads) {
+    const int c4 = e % C4, p = e / C4;
+    const int im = p / (Ho * Wo), r = p - im * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
+    float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (int ky = 0; ky < 3; ++ky) {
+      const int yy = 2 * oy - 1 + ky;
+      if (yy < 0 || yy >= H) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int xx = 2 * ox - 1 + kx;
+        if (xx < 0 || xx >= W) continue;
+        const uint2 v = *(const uint2*)(stg + ((size_t)(im * H + yy) * W + xx) * C + 4 * c4);
+        mx[0] = fmaxf(mx[0], lo_f(v.x)); mx[1] = fmaxf(mx[1], hi_f(v.x));
+        mx[2] = fmaxf(mx[2], lo_f(v.y)); mx[3] = fmaxf(mx[3], hi_f(v.y));
+      }
+    }
+    *(uint2*)(out + (((im * (Ho + 2) + oy + 1) * (Wo + 2) + ox + 1) * PO + c4 * 8)) =
+        make_uint2(pack2(mx[0], mx[1]), pack2(mx[2], mx[3]));
+  }
+}
+
+struct TrunkArgs {
+  const bf16* x;        // stage-0 pooled output [N][H0][W0][16]
+  bf16* y;              // trunk output [N][H2][W2][32]
+  const bf16* w[14];    // packed fwd weights of layers 1..14 (HipEncoder order)
+  const float* b[14];
+  int N, H0, W0;
+  int r1_bytes;         // region sizes (host computed)
+};
+
+__global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* R1 = smem;
+  char* R2 = smem + a.r1_bytes;
+  const int H0 = a.H0, W0 = a.W0, H1 = (H0 + 1) >> 1, W1 = (W0 + 1) >> 1;
+  const int H2 = (H1 + 1) >> 1, W2 = (W1 + 1) >> 1;
+  const int ngroups = (a.N + TNI - 1) / TNI;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
+    // ---- stage 0: X0 <- input (R1), U0 halo zero (R2)
+    {
+      constexpr int PX = TG<16>::PIXB;
+      const int tot = nimg * H0 * W0 * 2;  // 16-byte chunks
+      const uint4* src = (const uint4*)(a.x + (size_t)img0 * H0 * W0 * 16);
+      for (int e = threadIdx.x; e < tot; e += kThreads) {
+        const int q = e & 1, p = e >> 1;
+        const int im = p / (H0 * W0), r = p - im * H0 * W0, y = r / W0, x = r - y * W0;
+        *(uint4*)(R1 + ((im * (H0 + 2) + y + 1) * (W0 + 2) + x + 1) * PX + q * 16) = src[e];
+      }
+      zero_halo(R1, nimg, H0, W0, PX);
+      zero_halo(R2, nimg, H0, W0, PX);
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      conv_lds<16, 16>(R1, H0, W0, nimg, a.w[2 * rb], a.b[2 * rb], true, R2, false, nullptr);
+      __syncthreads();
+      conv_lds<16, 16>(R2, H0, W0, nimg, a.w[2 * rb + 1], a.b[2 * rb + 1], true, R1, true, nullptr);
+      __syncthreads();
+    }
+    // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1)
+    conv_lds<16, 32>(R1, H0, W0, nimg, a.w[4], a.b[4], false, nullptr, false, (bf16*)R2);
+    __syncthreads();
+    pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
+    zero_halo(R1, nimg, H1, W1, TG<32>::PIXB);
+    __syncthreads();
+    zero_halo(R2, nimg, H1, W1, TG<32>::PIXB);  // U1 layout (staging consumed)
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      conv_lds<32, 32>(R1, H1, W1, nimg, a.w[5 + 2 * rb], a.b[5 + 2 * rb], true, R2, false, nullptr);
+      __syncthreads();
+      conv_lds<32, 32>(R2, H1, W1, nimg, a.w[6 + 2 * rb], a.b[6 + 2 * rb], true, R1, true, nullptr);
+      __syncthreads();
+    }
+    // ---- stage 2
+    conv_lds<32, 32>(R1, H1, W1, nimg, a.w[9], a.b[9], false, nullptr, false, (bf16*)R2);
+    __syncthreads();
+    pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
+    zero_halo(R1, nimg, H2, W2, TG<32>::PIXB);
+    __syncthreads();
+    zero_halo(R2, nimg, H2, W2, TG<32>::PIXB);
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      conv_lds<32, 32>(R1, H2, W2, nimg, a.w[10 + 2 * rb], a.b[10 + 2 * rb], true, R2, false, nullptr);
+      __syncthreads();
+      conv_lds<32, 32>(R2, H2, W2, nimg, a.w[11 + 2 * rb], a.b[11 + 2 * rb], true, R1, true, nullptr);
+      __syncthreads();
+    }
+    // ---- X2 interior -> global NHWC
+    {
+      constexpr int PX = TG<32>::PIXB;
+      const int tot = nimg * H2 * W2 * 4;
+      uint4* dst = (uint4*)(a.y + (size_t)img0 * H2 * W2 * 32);
+      for (int e = threadIdx.x; e < tot; e += kThreads) {
+        const int q = e & 3, p = e >> 2;
+        const int im = p / (H2 * W2), r = p - im * H2 * W2, y = r / W2, x = r - y * W2;
+        dst[e] = *(const uint4*)(R1 + ((im * (H2 + 2) + y + 1) * (W2 + 2) + x + 1) * PX + q * 16);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+size_t region_bytes(int H0, int W0) {
+  const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2, H2 = (H1 + 1) / 2, W2 = (W1 + 1) / 2;
+  size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB;                 // X0 / U0
+  r = std::max(r, (size_t)TNI * H0 * W0 * 32 * 2);                            // stage-1 staging
+  r = std::max(r, (size_t)TNI * (H1 + 2) * (W1 + 2) * TG<32>::PIXB);          // X1 / U1
+  r = std::max(r, (size_t)TNI * (H2 + 2) * (W2 + 2) * TG<32>::PIXB);          // X2 / U2
+  return (r + 15) & ~(size_t)15;
+}
+
+}  // namespace
+
+// x: stage-0 pooled activations [N][H0][W0][16] bf16; w/b: layers 1..14 of the
+// (16, 32, 32) IMPALA trunk (packed fwd weights, fp32 biases); y: [N][H2][W2][32] bf16.
+extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* const* b, int N,
+                              int H0, int W0, void* y, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (H0 < 1 || W0 < 1 || H0 > 16 || W0 > 16) return (int)hipErrorInvalidValue;
+  TrunkArgs a;
+  a.x = (const bf16*)x;
+  a.y = (bf16*)y;
+  for (int i = 0; i < 14; ++i) {
+    a.w[i] = (const bf16*)w[i];
+    a.b[i] = b[i];
+  }
+  a.N = N;
+  a.H0 = H0;
+  a.W0 = W0;
+  const size_t r = region_bytes(H0, W0);
+  a.r1_bytes = (int)r;
+  const size_t sm = 2 * r;
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  auto kfn = trunk_tail_kernel;
+  if (sm > 64 * 1024)
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
+          hipSuccess || per < 1)
+    per = 1;
+  const int ngroups = (N + TNI - 1) / TNI;
+  const int grid = std::min(ngroups, cus * per);
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
+  return (int)hipGetLastError();
+}

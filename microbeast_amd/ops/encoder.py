@@ -106,6 +106,10 @@ class HipEncoder:
                 L.wb_off = boff
                 boff += L.cin * _nch(L.cout) * 32
         self.packed_fwd = torch.zeros(off, dtype=torch.bfloat16, device=device)
+        # acting forward: layers 1..14 in one fused launch (trunk.hip) when the trunk is the
+        # reference (16, 32, 32) shape
+        self.fused_tail = (tuple(channels) == (16, 32, 32) and self.layers[1].H <= 16
+                           and self.layers[1].W <= 16)
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
@@ -152,6 +156,19 @@ class HipEncoder:
             x.data_ptr(), int(L.bits), L.cin, L.cout, self.packed_fwd8.data_ptr() + L.w_off,
             self.scale8.data_ptr() + 4 * self._s_off[i], N.ptr(bias), N.ptr(add), y.data_ptr(),
             n, L.H, L.W, imgs, int(L.relu_in), int(L.pool), N.stream_ptr()), "conv_fwd_fp8")
+        return y
+
+    def _tail(self, p: torch.Tensor, bs: list[torch.Tensor]) -> torch.Tensor:
+        """Layers 1..14 on the fused trunk kernel (inference): p = stage-0 pooled output."""
+        L1, Ll = self.layers[1], self.layers[-1]
+        n = p.shape[0]
+        y = torch.empty(n, Ll.H, Ll.W, Ll.cout, dtype=torch.bfloat16, device=p.device)
+        base = self.packed_fwd.data_ptr()
+        wp = (ctypes.c_void_p * 14)(*[base + 2 * L.w_off for L in self.layers[1:15]])
+        bp = (ctypes.c_void_p * 14)(*[b.data_ptr() for b in bs[1:15]])
+        N.check(N.kernels().mbk_trunk_tail(p.data_ptr(), ctypes.cast(wp, ctypes.c_void_p),
+                                           ctypes.cast(bp, ctypes.c_void_p), n, L1.H, L1.W,
+                                           y.data_ptr(), N.stream_ptr()), "trunk_tail")
         return y
 
     def _fwd(self, L: ConvLayer, x, bias, add=None, mask_src=None, y_full=None, dgrad=False,
@@ -214,6 +231,9 @@ class HipEncoder:
             return x, []
         if not prepacked or save:
             self.pack([w.detach() for w in ws], with_bwd=save)
+        if not save and self.fused_tail:
+            p = self._fwd(self.layers[0], x, bs[0].detach())
+            return self._tail(p, bs), []
         saved = []
         li = 0
         n = x.shape[0]

@@ -254,3 +254,24 @@ def test_fp8_trunk_close_to_bf16_trunk(cuda):
     y8 = encode(obs, m._hip_enc, params, False).float()
     rel = ((y8 - y16).norm() / y16.norm()).item()
     assert rel < 0.08, rel
+
+
+@pytest.mark.parametrize("s", [16, 10, 8])
+def test_fused_trunk_tail_matches_per_layer_kernels(cuda, s):
+    """trunk.hip (layers 1..14 in one launch, LDS-resident) == the per-layer conv kernels."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(7)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(203, s * s, seed=9).to(cuda)
+    m.features(obs[:2])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    assert enc.fused_tail
+    y_fused = encode(obs, enc, params, False)
+    enc.fused_tail = False
+    y_ref = encode(obs, enc, params, False)
+    enc.fused_tail = True
+    assert y_fused.shape == y_ref.shape
+    # same bf16 storage points and fp32 accumulation order per pixel -> bit-identical
+    assert torch.equal(y_fused, y_ref), (y_fused.float() - y_ref.float()).abs().max()
