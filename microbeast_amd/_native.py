@@ -48,11 +48,13 @@ _SIGS = {
                      c_void_p],
     "mbk_conv_fwd_fp8": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mbk_conv_dgrad_unpool": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
+                              c_int, c_int, c_void_p],
     "mbk_conv_pack_fp8": [c_void_p, c_int, c_void_p],
     "mbk_pool_bwd_idx": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                       c_int, c_int, c_int, c_void_p],
-    "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "mbk_conv_set_grid_cap": [c_int],
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],
     "mbk_fc_wgrad": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,

@@ -76,6 +76,9 @@ struct ConvFwdArgs {
   uint8_t* pool_idx;  // pooled argmax (0..8 in the 3x3 window) for the backward
   int N, H, W, imgs, relu_in, pool;
   const float* wscale;  // fp8 path: per-output-channel dequant scale of the e4m3 weights
+  // pool-fused input (dgrad of a stage conv): x = max_pool2d backward of dp through pidx
+  const bf16* dp;       // [N][Ho][Wo][CIN]
+  const uint8_t* pidx;  // [N][Ho][Wo][CIN]
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -126,6 +129,40 @@ __device__ __forceinline__ uint2 bf16x8_to_fp8(uint4 v) {
   return make_uint2(cvt_fp8x4(f[0], f[1], f[2], f[3]), cvt_fp8x4(f[4], f[5], f[6], f[7]));
 }
 
+// max_pool2d(3, 2, 1) backward folded into the consumer's staging: 8 channels
+// [8q, 8q+8) of the pre-pool gradient at pixel (y, x) of image im = the sum of the pooled
+// gradients of the (<= 4) windows whose stored argmax (0..8 in the window) is (y, x).
+// P / I: that round's pooled grads (bf16) and argmax bytes, dense [img][Ho][Wo][C] in LDS.
+__device__ __forceinline__ uint4 unpool8(const char* P, const char* I, int im, int y, int x,
+                                         int q, int H, int W, int C) {
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int oy = max(0, y / 2 - 1); oy <= min(Ho - 1, (y + 1) / 2); ++oy) {
+    const int ky = y - (2 * oy - 1);
+    if (ky < 0 || ky > 2) continue;
+    for (int ox = max(0, x / 2 - 1); ox <= min(Wo - 1, (x + 1) / 2); ++ox) {
+      const int kx = x - (2 * ox - 1);
+      if (kx < 0 || kx > 2) continue;
+      const uint32_t me = (uint32_t)(ky * 3 + kx);
+      const int o = ((im * Ho + oy) * Wo + ox) * C + q * 8;
+      const uint2 ids = *(const uint2*)(I + o);
+      const uint4 dv = *(const uint4*)(P + o * 2);
+      const uint32_t iw[2] = {ids.x, ids.y};
+      const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (((iw[j >> 2] >> (8 * (j & 3))) & 0xFFu) == me)
+          g[j] += __uint_as_float(((dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) << 16);
+    }
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(g[2 * j])) |
+           ((uint32_t)__bfloat16_as_ushort(f2bf(g[2 * j + 1])) << 16);
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <int CIN, bool BITS, bool F8>
 __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
   // interior staging element e -> byte offset of its slot in the halo'd LDS tile
@@ -161,6 +198,12 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   float* otile = (float*)(smem + tile_bytes);  // pool staging [imgs*HW][OSTR] fp32
   const int ngroups = (a.N + a.imgs - 1) / a.imgs;
   const int per_grp = a.imgs * HW * EPP;
+  // pool-fused input: pooled grads + argmax of the group, dense, after the tile
+  const bool unpool = !BITS && !F8 && a.dp != nullptr;
+  const int Hq = (H + 1) >> 1, Wq = (W + 1) >> 1;
+  const int pper = a.imgs * Hq * Wq * EPP;
+  char* sP = smem + tile_bytes;  // (no pool staging in this mode)
+  char* sI = sP + (((a.imgs * Hq * Wq * CIN * 2) + 15) & ~15);
 
   for (int e = tid; e < tile_bytes / 16; e += kThreads) ((uint4*)tile)[e] = make_uint4(0, 0, 0, 0);
   int loff[kPF];
@@ -193,10 +236,22 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       wsc[nb][i] = F8 ? a.wscale[nb * 16 + 4 * g + i] : 1.f;
     }
 
-  // ---- register prefetch of one group's interior pixels
+  // ---- register prefetch of one group's interior pixels (pooled grads when unpool)
   uint4 pv[kPF];
   uint32_t pw[kPF];
+  uint2 pi[kPF];
   auto prefetch = [&](int grp) {
+    if (unpool) {
+      const size_t base = (size_t)grp * pper;
+      const int lim = min(pper, (a.N - grp * a.imgs) * Hq * Wq * EPP);
+#pragma unroll
+      for (int k = 0; k < kPF; ++k) {
+        const int e = tid + k * kThreads;
+        pv[k] = e < lim ? ((const uint4*)a.dp)[base + e] : make_uint4(0, 0, 0, 0);
+        pi[k] = e < lim ? ((const uint2*)a.pidx)[base + e] : make_uint2(0, 0);
+      }
+      return;
+    }
     const size_t base = (size_t)grp * per_grp;
     const int lim = min(per_grp, (a.N - grp * a.imgs) * HW * EPP);
 #pragma unroll
@@ -228,18 +283,40 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     const int img0 = grp * a.imgs;
     const int nimg = min(a.imgs, a.N - img0);
     const int lim = nimg * HW * EPP;
+    if (unpool) {
+      const int plim = nimg * Hq * Wq * EPP;
 #pragma unroll
-    for (int k = 0; k < kPF; ++k) {
-      const int e = tid + k * kThreads;
-      if (e < lim) {
-        if (BITS) put_bits(loff[k], pw[k]);
-        else put(loff[k], pv[k]);
+      for (int k = 0; k < kPF; ++k) {
+        const int e = tid + k * kThreads;
+        if (e < plim) {
+          *(uint4*)(sP + e * 16) = pv[k];
+          *(uint2*)(sI + e * 8) = pi[k];
+        }
       }
-    }
-    for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
-      const size_t src = (size_t)grp * per_grp + e;
-      if (BITS) put_bits(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint32_t*)a.x)[src]);
-      else put(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint4*)a.x)[src]);
+      for (int e = tid + kPF * kThreads; e < plim; e += kThreads) {
+        *(uint4*)(sP + e * 16) = ((const uint4*)a.dp)[(size_t)grp * pper + e];
+        *(uint2*)(sI + e * 8) = ((const uint2*)a.pidx)[(size_t)grp * pper + e];
+      }
+      __syncthreads();
+      for (int e = tid; e < lim; e += kThreads) {  // expand into the tile interior
+        const int q = e % EPP, p = e / EPP;
+        const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+        put(fwd_lds_off<CIN, BITS, F8>(e, H, W), unpool8(sP, sI, im, y, x, q, H, W, CIN));
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPF; ++k) {
+        const int e = tid + k * kThreads;
+        if (e < lim) {
+          if (BITS) put_bits(loff[k], pw[k]);
+          else put(loff[k], pv[k]);
+        }
+      }
+      for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
+        const size_t src = (size_t)grp * per_grp + e;
+        if (BITS) put_bits(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint32_t*)a.x)[src]);
+        else put(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint4*)a.x)[src]);
+      }
     }
     __syncthreads();
     if (grp + (int)gridDim.x < ngroups) prefetch(grp + gridDim.x);
@@ -366,6 +443,9 @@ struct ConvWgradArgs {
   const bf16* dy;
   float* partial;  // [gridDim.x][COUT*9*CIN + COUT]
   int N, H, W, imgs, relu_in;
+  // pool-fused mode (dy == nullptr): dY is the max-pool backward of dp through pidx
+  const bf16* dp;         // [N][Ho][Wo][COUT] pooled gradient
+  const uint8_t* pidx;    // [N][Ho][Wo][COUT] argmax in the 3x3 window
 };
 
 __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
@@ -400,10 +480,16 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int dbytes = ((a.imgs * HW * DPB) + 15) & ~15;
   char* dzero = dt + dbytes;
   float* red = (float*)smem;  // [COUT][KTOT] after the loop
+  // pool-fused: the round's pooled grads (bf16) and argmax bytes, dense [img][Ho][Wo][C]
+  const bool unpool = a.dp != nullptr;
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  char* sP = dzero + 64;
+  char* sI = sP + (((a.imgs * Ho * Wo * COUT * 2) + 15) & ~15);
 
   for (int e = tid; e < (xbytes + 64) / 16; e += kThreads) ((uint4*)xt)[e] = make_uint4(0, 0, 0, 0);
   for (int e = tid; e < 4; e += kThreads) ((uint4*)dzero)[e] = make_uint4(0, 0, 0, 0);
   const int xper = a.imgs * HW * XEPP, dper = a.imgs * HW * DCH;
+  const int pper = a.imgs * Ho * Wo * DCH;  // pooled 8-channel chunks per round
   int xoff[kPFW];
 #pragma unroll
   for (int k = 0; k < kPFW; ++k) {
@@ -425,17 +511,23 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   float dbias[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
   uint4 px[kPFW], pd[kPFW];
+  uint2 pi[kPFW];
   uint32_t pb[kPFW];
   auto prefetch = [&](int rd) {
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
-    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH;
-    const size_t xb = (size_t)rd * xper, db = (size_t)rd * dper;
+    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH, pl = nimg * Ho * Wo * DCH;
+    const size_t xb = (size_t)rd * xper, db = (size_t)rd * dper, pbase = (size_t)rd * pper;
 #pragma unroll
     for (int k = 0; k < kPFW; ++k) {
       const int e = tid + k * kThreads;
       if (BITS) pb[k] = e < xl ? ((const uint32_t*)a.x)[xb + e] : 0u;
       else px[k] = e < xl ? ((const uint4*)a.x)[xb + e] : make_uint4(0, 0, 0, 0);
-      pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
+      if (unpool) {
+        pd[k] = e < pl ? ((const uint4*)a.dp)[pbase + e] : make_uint4(0, 0, 0, 0);
+        pi[k] = e < pl ? ((const uint2*)a.pidx)[pbase + e] : make_uint2(0, 0);
+      } else {
+        pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
+      }
     }
   };
   auto put_x = [&](int off, uint4 v) {
@@ -469,7 +561,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   __syncthreads();  // zero halo / zero rows visible
   for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
-    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH;
+    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH, pl = nimg * Ho * Wo * DCH;
 #pragma unroll
     for (int k = 0; k < kPFW; ++k) {
       const int e = tid + k * kThreads;
@@ -477,14 +569,35 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         if (BITS) put_bits(xoff[k], pb[k]);
         else put_x(xoff[k], px[k]);
       }
-      if (e < dl) put_d(e, pd[k]);
+      if (unpool) {
+        if (e < pl) {
+          *(uint4*)(sP + e * 16) = pd[k];
+          *(uint2*)(sI + e * 8) = pi[k];
+        }
+      } else if (e < dl) {
+        put_d(e, pd[k]);
+      }
     }
     for (int e = tid + kPFW * kThreads; e < xl; e += kThreads) {
       if (BITS) put_bits(xoff_of(e), ((const uint32_t*)a.x)[(size_t)rd * xper + e]);
       else put_x(xoff_of(e), ((const uint4*)a.x)[(size_t)rd * xper + e]);
     }
-    for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
-      put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
+    if (unpool) {
+      for (int e = tid + kPFW * kThreads; e < pl; e += kThreads) {
+        *(uint4*)(sP + e * 16) = ((const uint4*)a.dp)[(size_t)rd * pper + e];
+        *(uint2*)(sI + e * 8) = ((const uint2*)a.pidx)[(size_t)rd * pper + e];
+      }
+      __syncthreads();
+      // expand: dY chunk e = (pixel, 8-channel group) from the pooled grads
+      for (int e = tid; e < dl; e += kThreads) {
+        const int q = e % DCH, p = e / DCH;
+        const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+        put_d(e, unpool8(sP, sI, im, y, x, q, H, W, COUT));
+      }
+    } else {
+      for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
+        put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
+    }
     __syncthreads();
     if (rd + (int)gridDim.x < nrounds) prefetch(rd + gridDim.x);
 
@@ -785,18 +898,26 @@ __global__ __launch_bounds__(256) void conv_pack_fp8_kernel(PackJobs8 jobs) {
 }
 
 inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool,
-                       bool fp8 = false) {
+                       bool fp8 = false, bool unpool = false) {
   (void)bits;  // bit planes are staged expanded (cin = 32)
   const int pixb = fp8 ? cin + 8 : cin * 2 + 16;
   size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
   if (pool) t += (size_t)imgs * H * W * (cout + 4) * 4;
+  if (unpool) {
+    const size_t pp = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * cin;
+    t += ((pp * 2 + 15) & ~(size_t)15) + ((pp + 15) & ~(size_t)15);
+  }
   return t;
 }
 
-inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W) {
+inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool = false) {
   size_t x = (((size_t)imgs * (H + 2) * (W + 2) * cin * 2) + 15) & ~(size_t)15;
   size_t d = (((size_t)imgs * H * W * cout * 2) + 15) & ~(size_t)15;
   size_t t = x + 64 + d + 64;
+  if (unpool) {
+    const size_t pp = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * cout;
+    t += ((pp * 2 + 15) & ~(size_t)15) + ((pp + 15) & ~(size_t)15);
+  }
   size_t red = (size_t)cout * 9 * cin * 4;
   if (red < (size_t)kThreads * 8 * 4) red = (size_t)kThreads * 8 * 4;
   return t > red ? t : red;
@@ -828,12 +949,16 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
                            const float* wscale, const float* bias, const void* add,
                            const void* mask_src, void* y, void* y_full, void* pool_idx, int N,
                            int H, int W, int imgs, int relu_in, int pool, bool fp8,
-                           hipStream_t stream) {
+                           hipStream_t stream, const void* dp = nullptr,
+                           const void* pidx = nullptr) {
   if (N <= 0) return 0;
   if (fp8 && !wscale) return (int)hipErrorInvalidValue;
+  const bool unpool = dp != nullptr;
+  if (unpool && (in_bits || fp8 || pool || !pidx)) return (int)hipErrorInvalidValue;
   ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
-                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool, wscale};
-  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0, fp8);
+                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool, wscale,
+                (const bf16*)dp, (const uint8_t*)pidx};
+  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0, fp8, unpool);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const int ngroups = (N + imgs - 1) / imgs;
 #define LAUNCH(CI, CO, B)                                                                   \
@@ -865,6 +990,15 @@ extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const
                          pool_idx, N, H, W, imgs, relu_in, pool, false, stream);
 }
 
+// Data gradient of a pooled stage conv with the max-pool backward folded in: the input
+// (the pre-pool gradient, cin channels at H x W) is rebuilt per tile from dp / pidx.
+extern "C" int mbk_conv_dgrad_unpool(const void* dp, const void* pidx, int cin, int cout,
+                                     const void* w, void* y, int N, int H, int W, int imgs,
+                                     hipStream_t stream) {
+  return conv_fwd_launch(nullptr, 0, cin, cout, w, nullptr, nullptr, nullptr, nullptr, y,
+                         nullptr, nullptr, N, H, W, imgs, 0, 0, false, stream, dp, pidx);
+}
+
 // Inference conv on fp8 MFMA: w = e4m3 packed weights (mbk_conv_pack_fp8), wscale = their
 // per-output-channel dequant scale; activations in / out stay bf16 NHWC.
 extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, const void* w,
@@ -888,8 +1022,8 @@ extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, c
 
 // number of partial rows mbk_conv_wgrad will write for this shape (<= nrounds)
 extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
-                                    int imgs) {
-  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
+                                    int imgs, int unpool) {
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W, unpool != 0);
   if (sm > 160 * 1024) return -(int)hipErrorInvalidValue;
   const int nrounds = (N + imgs - 1) / imgs;
   int res = 1;
@@ -899,11 +1033,14 @@ extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H
   return std::max(1, std::min(nrounds, res));
 }
 
+// dy == nullptr: pool-fused mode, dY = max_pool2d backward of dp through pidx
 extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, const void* dy,
-                              float* partial, int nparts, int N, int H, int W, int imgs,
-                              int relu_in, hipStream_t stream) {
-  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in};
-  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
+                              const void* dp, const void* pidx, float* partial, int nparts, int N,
+                              int H, int W, int imgs, int relu_in, hipStream_t stream) {
+  if (!dy && (!dp || !pidx)) return (int)hipErrorInvalidValue;
+  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in,
+                  dy ? nullptr : (const bf16*)dp, dy ? nullptr : (const uint8_t*)pidx};
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W, dy == nullptr);
   if (sm > 160 * 1024 || nparts < 1) return (int)hipErrorInvalidValue;
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \

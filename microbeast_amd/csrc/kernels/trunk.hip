@@ -30,8 +30,9 @@ typedef __hip_bfloat16 bf16;
 
 namespace {
 
-constexpr int kThreads = 256;
-constexpr int TNI = 4;  // images per workgroup iteration
+constexpr int kThreads = 512;  // 8 waves: 2 per SIMD even at one workgroup per CU
+constexpr int kMaxTNI = 16;  // images per workgroup iteration (host picks <= this)
+constexpr int kWBufBytes = 32 * (9 * 64 + 16);  // one staged layer (largest: 32x32)
 
 union Frag8 {
   bf16x8 v;
@@ -76,9 +77,34 @@ __device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W, int p
 // conv3x3 (pad 1) of a halo'd LDS tile. Output either into a halo'd tile (with optional
 // in-place residual add from the same tile) or into a dense bf16 staging [nimg][H][W][COUT]
 // (for the pool). relu_in applies to the input fragments.
+// A layer's packed weights [COUT][NCH][32] bf16 live in LDS with each output row padded
+// by 16 bytes (row stride NCH*64 + 16: the 16 rows a wave reads hit distinct banks).
+template <int CIN>
+__device__ __forceinline__ int wrow_bytes() { return TG<CIN>::NCH * 64 + 16; }
+
+constexpr int kWRegs = 3;  // uint4 per thread to stage the largest layer (32x9x32 bf16)
+
+// global -> registers (issued early, overlapping the current conv)
+__device__ __forceinline__ void wload(const bf16* __restrict__ gw, int n16, uint4 r[kWRegs]) {
+#pragma unroll
+  for (int k = 0; k < kWRegs; ++k) {
+    const int e = threadIdx.x + k * kThreads;
+    r[k] = e < n16 ? ((const uint4*)gw)[e] : make_uint4(0, 0, 0, 0);
+  }
+}
+// registers -> padded LDS rows
+__device__ __forceinline__ void wstore(char* lw, int n16, int nch, const uint4 r[kWRegs]) {
+  const int per_row = nch * 4, stride = nch * 64 + 16;
+#pragma unroll
+  for (int k = 0; k < kWRegs; ++k) {
+    const int e = threadIdx.x + k * kThreads;
+    if (e < n16) *(uint4*)(lw + (e / per_row) * stride + (e % per_row) * 16) = r[k];
+  }
+}
+
 template <int CIN, int COUT>
 // noinline: works around an LLVM CGSCC-pass crash (ROCm 7.2) when fully force-inlined
-__device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W, int nimg, const bf16* __restrict__ w,
+__device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W, int nimg, const char* lw,
                          const float* __restrict__ bias, bool relu_in, char* out, bool add,
                          bf16* stg) {
   constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
@@ -89,9 +115,9 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
   Frag8 bw[NCH][NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const uint4* wp = (const uint4*)(w + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
+    const char* wr = lw + (nb * 16 + li) * wrow_bytes<CIN>() + g * 16;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) bw[c][nb].u = wp[c * 4];
+    for (int c = 0; c < NCH; ++c) bw[c][nb].u = *(const uint4*)(wr + c * 64);
   }
   float bv[NB][4];
 #pragma unroll
@@ -175,16 +201,40 @@ struct TrunkArgs {
   const bf16* w[14];    // packed fwd weights of layers 1..14 (HipEncoder order)
   const float* b[14];
   int N, H0, W0;
+  int tni;              // images per workgroup iteration
   int r1_bytes;         // region sizes (host computed)
 };
+
+// layer l of the tail (0..13): CIN / COUT of the (16, 32, 32) trunk
+__device__ __forceinline__ int tail_cin(int l) { return l < 5 ? 16 : 32; }
+__device__ __forceinline__ int tail_cout(int l) { return l < 4 ? 16 : 32; }
+__device__ __forceinline__ int tail_n16(int l) {
+  return tail_cout(l) * TG<16>::NCH * 4 * (tail_cin(l) == 16 ? 1 : 0) +
+         tail_cout(l) * TG<32>::NCH * 4 * (tail_cin(l) == 32 ? 1 : 0);
+}
 
 __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* R1 = smem;
   char* R2 = smem + a.r1_bytes;
+  char* WB[2] = {smem + 2 * a.r1_bytes, smem + 2 * a.r1_bytes + kWBufBytes};
   const int H0 = a.H0, W0 = a.W0, H1 = (H0 + 1) >> 1, W1 = (W0 + 1) >> 1;
   const int H2 = (H1 + 1) >> 1, W2 = (W1 + 1) >> 1;
+  const int TNI = a.tni;
   const int ngroups = (a.N + TNI - 1) / TNI;
+  uint4 wr[kWRegs];
+  // layer 0's weights for the first iteration
+  wload(a.w[0], tail_n16(0), wr);
+  wstore(WB[0], tail_n16(0), TG<16>::NCH, wr);
+  // phase helper: prefetch layer l+1 (wrapping to 0 for the next group) into registers,
+  // run conv l from WB[l & 1], park l+1 in the other buffer, barrier
+#define TAIL_PHASE(l, CI, CO, ...)                                                          \
+  do {                                                                                      \
+    const int ln = ((l) + 1) % 14;                                                          \
+    wload(a.w[ln], tail_n16(ln), wr);                                                       \
+    conv_lds<CI, CO>(__VA_ARGS__);                                                          \
+    wstore(WB[ln & 1], tail_n16(ln), ln < 5 ? TG<16>::NCH : TG<32>::NCH, wr);               \
+  } while (0)
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
     // ---- stage 0: X0 <- input (R1), U0 halo zero (R2)
@@ -203,13 +253,14 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     __syncthreads();
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      conv_lds<16, 16>(R1, H0, W0, nimg, a.w[2 * rb], a.b[2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(2 * rb, 16, 16, R1, H0, W0, nimg, WB[0], a.b[2 * rb], true, R2, false, nullptr);
       __syncthreads();
-      conv_lds<16, 16>(R2, H0, W0, nimg, a.w[2 * rb + 1], a.b[2 * rb + 1], true, R1, true, nullptr);
+      TAIL_PHASE(2 * rb + 1, 16, 16, R2, H0, W0, nimg, WB[1], a.b[2 * rb + 1], true, R1, true,
+                 nullptr);
       __syncthreads();
     }
     // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1)
-    conv_lds<16, 32>(R1, H0, W0, nimg, a.w[4], a.b[4], false, nullptr, false, (bf16*)R2);
+    TAIL_PHASE(4, 16, 32, R1, H0, W0, nimg, WB[0], a.b[4], false, nullptr, false, (bf16*)R2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
     zero_halo(R1, nimg, H1, W1, TG<32>::PIXB);
@@ -217,13 +268,15 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     zero_halo(R2, nimg, H1, W1, TG<32>::PIXB);  // U1 layout (staging consumed)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      conv_lds<32, 32>(R1, H1, W1, nimg, a.w[5 + 2 * rb], a.b[5 + 2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(5 + 2 * rb, 32, 32, R1, H1, W1, nimg, WB[1], a.b[5 + 2 * rb], true, R2, false,
+                 nullptr);
       __syncthreads();
-      conv_lds<32, 32>(R2, H1, W1, nimg, a.w[6 + 2 * rb], a.b[6 + 2 * rb], true, R1, true, nullptr);
+      TAIL_PHASE(6 + 2 * rb, 32, 32, R2, H1, W1, nimg, WB[0], a.b[6 + 2 * rb], true, R1, true,
+                 nullptr);
       __syncthreads();
     }
     // ---- stage 2
-    conv_lds<32, 32>(R1, H1, W1, nimg, a.w[9], a.b[9], false, nullptr, false, (bf16*)R2);
+    TAIL_PHASE(9, 32, 32, R1, H1, W1, nimg, WB[1], a.b[9], false, nullptr, false, (bf16*)R2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
     zero_halo(R1, nimg, H2, W2, TG<32>::PIXB);
@@ -231,11 +284,14 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     zero_halo(R2, nimg, H2, W2, TG<32>::PIXB);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      conv_lds<32, 32>(R1, H2, W2, nimg, a.w[10 + 2 * rb], a.b[10 + 2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(10 + 2 * rb, 32, 32, R1, H2, W2, nimg, WB[0], a.b[10 + 2 * rb], true, R2, false,
+                 nullptr);
       __syncthreads();
-      conv_lds<32, 32>(R2, H2, W2, nimg, a.w[11 + 2 * rb], a.b[11 + 2 * rb], true, R1, true, nullptr);
+      TAIL_PHASE(11 + 2 * rb, 32, 32, R2, H2, W2, nimg, WB[1], a.b[11 + 2 * rb], true, R1, true,
+                 nullptr);
       __syncthreads();
     }
+#undef TAIL_PHASE
     // ---- X2 interior -> global NHWC
     {
       constexpr int PX = TG<32>::PIXB;
@@ -251,7 +307,7 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   }
 }
 
-size_t region_bytes(int H0, int W0) {
+size_t region_bytes(int H0, int W0, int TNI) {
   const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2, H2 = (H1 + 1) / 2, W2 = (W1 + 1) / 2;
   size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB;                 // X0 / U0
   r = std::max(r, (size_t)TNI * H0 * W0 * 32 * 2);                            // stage-1 staging
@@ -278,13 +334,6 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
   a.N = N;
   a.H0 = H0;
   a.W0 = W0;
-  const size_t r = region_bytes(H0, W0);
-  a.r1_bytes = (int)r;
-  const size_t sm = 2 * r;
-  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  auto kfn = trunk_tail_kernel;
-  if (sm > 64 * 1024)
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -292,11 +341,25 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
+  // images per iteration: as many as LDS allows (each conv phase pays one L2 round trip
+  // for its weights, so more images amortise it) while keeping >= one group per CU
+  int tni = 1;
+  while (tni < kMaxTNI && 2 * region_bytes(H0, W0, tni * 2) + 2 * kWBufBytes <= 160 * 1024 &&
+         (N + tni * 2 - 1) / (tni * 2) >= cus)
+    tni *= 2;
+  a.tni = tni;
+  const size_t r = region_bytes(H0, W0, tni);
+  a.r1_bytes = (int)r;
+  const size_t sm = 2 * r + 2 * kWBufBytes;
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  auto kfn = trunk_tail_kernel;
+  if (sm > 64 * 1024)
+    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
           hipSuccess || per < 1)
     per = 1;
-  const int ngroups = (N + TNI - 1) / TNI;
+  const int ngroups = (N + tni - 1) / tni;
   const int grid = std::min(ngroups, cus * per);
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();

@@ -178,6 +178,12 @@ PYBIND11_MODULE(_mbrt, m) {
   m.def("seqlock_write_begin",
         [](uintptr_t ver) { return seqlock_write_begin(P<std::atomic<uint64_t>>(ver)); });
   m.def("seqlock_write_end", [](uintptr_t ver) { seqlock_write_end(P<std::atomic<uint64_t>>(ver)); });
+  m.def("seqlock_write",
+        [](uintptr_t ver, uintptr_t src, uintptr_t dst, size_t n) {
+          py::gil_scoped_release g;
+          seqlock_write(P<std::atomic<uint64_t>>(ver), P<const void>(src), P<void>(dst), n);
+        },
+        py::arg("ver"), py::arg("src"), py::arg("dst"), py::arg("nbytes"));
   m.def("seqlock_read",
         [](uintptr_t ver, uintptr_t src, uintptr_t dst, size_t n, int tries) {
           py::gil_scoped_release g;

@@ -137,12 +137,39 @@ void seqlock_write_end(std::atomic<uint64_t>* ver) {
   ver->store(ver->load(std::memory_order_relaxed) + 1, std::memory_order_release);
 }
 
+// The protected region is copied through relaxed atomic 8-byte accesses on both sides
+// (plain moves on x86), so concurrent readers and the writer never race in the C++
+// memory-model sense; the version check makes a torn copy detectable. n % 8 tail bytes
+// go through atomic byte accesses.
+static void atomic_copy_out(const void* src, void* dst, size_t n) {
+  const uint64_t* s = (const uint64_t*)src;
+  uint64_t* d = (uint64_t*)dst;
+  const size_t w = n / 8;
+  for (size_t i = 0; i < w; ++i) d[i] = __atomic_load_n(s + i, __ATOMIC_RELAXED);
+  for (size_t i = w * 8; i < n; ++i)
+    ((uint8_t*)dst)[i] = __atomic_load_n((const uint8_t*)src + i, __ATOMIC_RELAXED);
+}
+static void atomic_copy_in(const void* src, void* dst, size_t n) {
+  const uint64_t* s = (const uint64_t*)src;
+  uint64_t* d = (uint64_t*)dst;
+  const size_t w = n / 8;
+  for (size_t i = 0; i < w; ++i) __atomic_store_n(d + i, s[i], __ATOMIC_RELAXED);
+  for (size_t i = w * 8; i < n; ++i)
+    __atomic_store_n((uint8_t*)dst + i, ((const uint8_t*)src)[i], __ATOMIC_RELAXED);
+}
+
+void seqlock_write(std::atomic<uint64_t>* ver, const void* src, void* dst, size_t n) {
+  seqlock_write_begin(ver);
+  atomic_copy_in(src, dst, n);
+  seqlock_write_end(ver);
+}
+
 uint64_t seqlock_read(const std::atomic<uint64_t>* ver, const void* src, void* dst, size_t n,
                       int max_tries) {
   for (int i = 0; i < max_tries; ++i) {
     uint64_t v0 = ver->load(std::memory_order_acquire);
     if (v0 & 1) { std::this_thread::yield(); continue; }
-    std::memcpy(dst, src, n);
+    atomic_copy_out(src, dst, n);
     std::atomic_thread_fence(std::memory_order_acquire);
     uint64_t v1 = ver->load(std::memory_order_relaxed);
     if (v0 == v1) return v0 + 1;  // version + 1, so 0 always means failure

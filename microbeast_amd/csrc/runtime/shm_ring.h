@@ -57,6 +57,8 @@ class IndexRing {
 // Seqlock over a shared byte region. Writer: begin (odd) -> copy -> end (even).
 uint64_t seqlock_write_begin(std::atomic<uint64_t>* ver);
 void seqlock_write_end(std::atomic<uint64_t>* ver);
+// begin + copy src -> dst (the shared region) + end, race-free against seqlock_read
+void seqlock_write(std::atomic<uint64_t>* ver, const void* src, void* dst, size_t n);
 // Copies src->dst consistently; returns (version read + 1), or 0 if it could
 // not get a stable copy within max_tries.
 uint64_t seqlock_read(const std::atomic<uint64_t>* ver, const void* src, void* dst, size_t n,

@@ -110,6 +110,7 @@ class HipEncoder:
         # reference (16, 32, 32) shape
         self.fused_tail = (tuple(channels) == (16, 32, 32) and self.layers[1].H <= 16
                            and self.layers[1].W <= 16)
+        self.fused_pool_bwd = True  # max-pool backward folded into the stage conv's wgrad/dgrad
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
@@ -158,6 +159,16 @@ class HipEncoder:
             n, L.H, L.W, imgs, int(L.relu_in), int(L.pool), N.stream_ptr()), "conv_fwd_fp8")
         return y
 
+    def _dgrad_unpool(self, L: ConvLayer, dp: torch.Tensor, pidx: torch.Tensor) -> torch.Tensor:
+        """Input gradient of a pooled stage conv straight from the pooled gradient."""
+        n = dp.shape[0]
+        y = torch.empty(n, L.H, L.W, L.cin, dtype=torch.bfloat16, device=dp.device)
+        imgs = _imgs_fwd(L, L.cout, L.cin, False, False)
+        N.check(N.kernels().mbk_conv_dgrad_unpool(
+            dp.data_ptr(), pidx.data_ptr(), L.cout, L.cin, self.packed_bwd.data_ptr() + 2 * L.wb_off,
+            y.data_ptr(), n, L.H, L.W, imgs, N.stream_ptr()), "conv_dgrad_unpool")
+        return y
+
     def _tail(self, p: torch.Tensor, bs: list[torch.Tensor]) -> torch.Tensor:
         """Layers 1..14 on the fused trunk kernel (inference): p = stage-0 pooled output."""
         L1, Ll = self.layers[1], self.layers[-1]
@@ -192,21 +203,24 @@ class HipEncoder:
             "conv_fwd")
         return y
 
-    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor):
+    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor, dp=None, pidx=None):
+        """dy=None: pool-fused, dY is max_pool2d's backward of dp through the argmax pidx."""
         n = x.shape[0]
         imgs = _imgs_wgrad(L)
+        unpool = dy is None
         # persistent grid: as many workgroups as the device keeps resident (<= rounds)
-        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs)
+        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs,
+                                                  int(unpool))
         if nparts < 1:
             raise RuntimeError(f"conv_wgrad: unsupported shape {L}")
         row = L.cout * 9 * L.cin + L.cout
         need = (nparts + (nparts + 31) // 32) * row  # + the two-level reduce's scratch rows
-        if self._partial is None or self._partial.numel() < need or self._partial.device != dy.device:
-            self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=dy.device)
+        if self._partial is None or self._partial.numel() < need or self._partial.device != x.device:
+            self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=x.device)
         k = N.kernels()
         st = N.stream_ptr()
-        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, dy.data_ptr(),
-                                 self._partial.data_ptr(), nparts, n, L.H, L.W, imgs,
+        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, N.ptr(dy), N.ptr(dp),
+                                 N.ptr(pidx), self._partial.data_ptr(), nparts, n, L.H, L.W, imgs,
                                  int(L.relu_in), st), "conv_wgrad")
         N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
                                    dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
@@ -274,6 +288,12 @@ class HipEncoder:
             dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
+            if self.fused_pool_bwd:
+                # max_pool2d backward folded into both consumers' LDS staging: the
+                # pre-pool gradient is never materialised in HBM
+                self._wgrad(Ls, x, None, grads[2 * li], grads[2 * li + 1], dp=dp, pidx=pidx)
+                g = self._dgrad_unpool(Ls, dp, pidx) if s > 0 else None
+                continue
             dc = torch.empty(pidx.shape[0], Ls.H, Ls.W, Ls.cout, dtype=torch.bfloat16,
                              device=pidx.device)
             N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dp.data_ptr(), pidx.shape[0],

@@ -132,9 +132,10 @@ class MonoRuntime:
         src = flat_data.detach()
         if src.is_cuda:
             src = src.cpu()
-        rt.seqlock_write_begin(self.version.data_ptr())
-        self.weights.copy_(src)
-        rt.seqlock_write_end(self.version.data_ptr())
+        src = src.contiguous()
+        assert src.numel() == self.weights.numel() and src.dtype == self.weights.dtype
+        rt.seqlock_write(self.version.data_ptr(), src.data_ptr(), self.weights.data_ptr(),
+                         src.numel() * src.element_size())
 
     def _spawn(self, i: int):
         fd = {k: getattr(self.flags, k) for k in self.flags.__dataclass_fields__}

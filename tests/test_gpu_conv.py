@@ -275,3 +275,31 @@ def test_fused_trunk_tail_matches_per_layer_kernels(cuda, s):
     assert y_fused.shape == y_ref.shape
     # same bf16 storage points and fp32 accumulation order per pixel -> bit-identical
     assert torch.equal(y_fused, y_ref), (y_fused.float() - y_ref.float()).abs().max()
+
+
+@pytest.mark.parametrize("s", [16, 10])
+def test_pool_bwd_fused_into_wgrad_dgrad(cuda, s):
+    """max-pool backward folded into the stage conv's wgrad / dgrad staging == the separate
+    pool_bwd kernel path (same bf16 dc values; only partial-sum order may differ)."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(11)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(150, s * s, seed=13).to(cuda)
+    m.features(obs[:2])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    r = None
+    grads = []
+    for fused in (False, True):
+        enc.fused_pool_bwd = fused
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True)
+        if r is None:
+            r = torch.randn_like(y.float())
+        (y.float() * r).sum().backward()
+        grads.append([p.grad.clone() for p in params])
+    enc.fused_pool_bwd = True
+    for a, b in zip(*grads):
+        assert _rel(b.cpu(), a.cpu()) < 1e-4, _rel(b.cpu(), a.cpu())
