@@ -64,7 +64,7 @@ class Flags:
     arch: str = "impala_flat"     # impala_flat | gridnet | impala_deep
     channels: str = "16,32,32"
     hidden: int = 256
-    dtype: str = "bf16"           # fp32 | bf16
+    dtype: str = "bf16"           # fp32 | bf16 | fp8 (= bf16 learner + fp8 acting trunk)
     fp8_policy: bool = False      # gpu runtime: acting trunk on fp8 (e4m3) MFMA convs
     # --- runtime
     runtime: str = "auto"         # auto | gpu (native engine) | mono (CPU actor processes)
@@ -75,6 +75,8 @@ class Flags:
     seed: int = 1
     nproc_per_node: int = 1       # informative; launch with torchrun for DP
     bucket_mb: float = 8.0
+    allreduce_dtype: str = "fp32"  # fp32 | bf16 gradient all-reduce payload (fp32 master grads)
+    profile_updates: int = 0      # >0: torch.profiler trace of that many updates -> savedir
     # --- io / robustness
     savedir: str = "."
     checkpoint_every: int = 100   # updates

@@ -182,7 +182,7 @@ __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
 // F8: the tile holds OCP e4m3 activations (converted at staging: half the LDS bytes and
 // read traffic), weights are e4m3 with a power-of-two per-output-channel scale, and the
 // MFMA is v_mfma_f32_16x16x32_fp8_fp8 (same lane map as the bf16 form). Inference only.
-template <int CIN, int COUT, bool BITS, bool F8>
+template <int CIN, int COUT, bool BITS, bool F8, bool UNPOOL = false>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NCH = Geo<CIN>::NCH;
@@ -199,7 +199,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   const int ngroups = (a.N + a.imgs - 1) / a.imgs;
   const int per_grp = a.imgs * HW * EPP;
   // pool-fused input: pooled grads + argmax of the group, dense, after the tile
-  const bool unpool = !BITS && !F8 && a.dp != nullptr;
+  constexpr bool unpool = UNPOOL && !BITS && !F8;  // compile-time: keeps other variants lean
   const int Hq = (H + 1) >> 1, Wq = (W + 1) >> 1;
   const int pper = a.imgs * Hq * Wq * EPP;
   char* sP = smem + tile_bytes;  // (no pool staging in this mode)
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   uint32_t pw[kPF];
   uint2 pi[kPF];
   auto prefetch = [&](int grp) {
-    if (unpool) {
+    if constexpr (unpool) {
       const size_t base = (size_t)grp * pper;
       const int lim = min(pper, (a.N - grp * a.imgs) * Hq * Wq * EPP);
 #pragma unroll
@@ -283,7 +283,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     const int img0 = grp * a.imgs;
     const int nimg = min(a.imgs, a.N - img0);
     const int lim = nimg * HW * EPP;
-    if (unpool) {
+    if constexpr (unpool) {
       const int plim = nimg * Hq * Wq * EPP;
 #pragma unroll
       for (int k = 0; k < kPF; ++k) {
@@ -458,7 +458,7 @@ constexpr int kPFW = 4;  // wgrad prefetch slots per thread for X and for dY
 // Persistent over image rounds (grid = occupancy-sized, one partial per workgroup).
 // Both GEMM operands come from plain NHWC LDS tiles through ds_read_b64_tr_b16; the
 // next round's X interior and dY are prefetched into registers during the MFMAs.
-template <int CIN, int COUT, bool BITS>
+template <int CIN, int COUT, bool BITS, bool UNPOOL = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int XPB = CIN * 2;       // X tile pixel stride (bytes), NHWC bf16
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   char* dzero = dt + dbytes;
   float* red = (float*)smem;  // [COUT][KTOT] after the loop
   // pool-fused: the round's pooled grads (bf16) and argmax bytes, dense [img][Ho][Wo][C]
-  const bool unpool = a.dp != nullptr;
+  constexpr bool unpool = UNPOOL;  // compile-time: keeps the plain variants lean
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
   char* sP = dzero + 64;
   char* sI = sP + (((a.imgs * Ho * Wo * COUT * 2) + 15) & ~15);
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
       const int e = tid + k * kThreads;
       if (BITS) pb[k] = e < xl ? ((const uint32_t*)a.x)[xb + e] : 0u;
       else px[k] = e < xl ? ((const uint4*)a.x)[xb + e] : make_uint4(0, 0, 0, 0);
-      if (unpool) {
+      if constexpr (unpool) {
         pd[k] = e < pl ? ((const uint4*)a.dp)[pbase + e] : make_uint4(0, 0, 0, 0);
         pi[k] = e < pl ? ((const uint2*)a.pidx)[pbase + e] : make_uint2(0, 0);
       } else {
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         if (BITS) put_bits(xoff[k], pb[k]);
         else put_x(xoff[k], px[k]);
       }
-      if (unpool) {
+      if constexpr (unpool) {
         if (e < pl) {
           *(uint4*)(sP + e * 16) = pd[k];
           *(uint2*)(sI + e * 8) = pi[k];
@@ -582,7 +582,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
       if (BITS) put_bits(xoff_of(e), ((const uint32_t*)a.x)[(size_t)rd * xper + e]);
       else put_x(xoff_of(e), ((const uint4*)a.x)[(size_t)rd * xper + e]);
     }
-    if (unpool) {
+    if constexpr (unpool) {
       for (int e = tid + kPFW * kThreads; e < pl; e += kThreads) {
         *(uint4*)(sP + e * 16) = ((const uint4*)a.dp)[(size_t)rd * pper + e];
         *(uint2*)(sI + e * 8) = ((const uint2*)a.pidx)[(size_t)rd * pper + e];
@@ -969,6 +969,17 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));              \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);                     \
   } while (0)
+  if (unpool) {  // dgrad of a pooled stage conv (cin = that conv's cout)
+    auto kfn = cin == 32 && cout == 16   ? conv_fwd_kernel<32, 16, false, false, true>
+               : cin == 32 && cout == 32 ? conv_fwd_kernel<32, 32, false, false, true>
+                                         : nullptr;
+    if (!kfn) return (int)hipErrorInvalidValue;
+    if (sm > 64 * 1024)
+      hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
+    return (int)hipGetLastError();
+  }
   if (in_bits) {
     if (cout == 16) LAUNCH(32, 16, true);
     else if (cout == 32) LAUNCH(32, 32, true);
@@ -1027,7 +1038,9 @@ extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H
   if (sm > 160 * 1024) return -(int)hipErrorInvalidValue;
   const int nrounds = (N + imgs - 1) / imgs;
   int res = 1;
-#define Q(CI, CO, B) res = resident_blocks((const void*)conv_wgrad_kernel<CI, CO, B>, sm)
+#define Q(CI, CO, B)                                                                  \
+  res = resident_blocks(unpool ? (const void*)conv_wgrad_kernel<CI, CO, B, true>       \
+                               : (const void*)conv_wgrad_kernel<CI, CO, B>, sm)
   WGRAD_DISPATCH(Q)
 #undef Q
   return std::max(1, std::min(nrounds, res));
@@ -1045,7 +1058,7 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
-    auto kfn = conv_wgrad_kernel<CI, CO, B>;                                                \
+    auto kfn = dy ? conv_wgrad_kernel<CI, CO, B> : conv_wgrad_kernel<CI, CO, B, true>;      \
     if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
     hipLaunchKernelGGL(kfn, grid, dim3(kThreads), sm, stream, a);                           \

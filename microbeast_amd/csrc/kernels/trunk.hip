@@ -23,6 +23,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
+#include <string>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -104,9 +106,10 @@ __device__ __forceinline__ void wstore(char* lw, int n16, int nch, const uint4 r
 
 template <int CIN, int COUT>
 // noinline: works around an LLVM CGSCC-pass crash (ROCm 7.2) when fully force-inlined
+// lw: the layer's weights, rows of wstride bytes (LDS-staged, padded) or global (packed)
 __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W, int nimg, const char* lw,
-                         const float* __restrict__ bias, bool relu_in, char* out, bool add,
-                         bf16* stg) {
+                         int wstride, const float* __restrict__ bias, bool relu_in, char* out,
+                         bool add, bf16* stg) {
   constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
   constexpr int PI = TG<CIN>::PIXB, PO = TG<COUT>::PIXB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -115,7 +118,7 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
   Frag8 bw[NCH][NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const char* wr = lw + (nb * 16 + li) * wrow_bytes<CIN>() + g * 16;
+    const char* wr = lw + (nb * 16 + li) * wstride + g * 16;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) bw[c][nb].u = *(const uint4*)(wr + c * 64);
   }
@@ -213,6 +216,7 @@ __device__ __forceinline__ int tail_n16(int l) {
          tail_cout(l) * TG<32>::NCH * 4 * (tail_cin(l) == 32 ? 1 : 0);
 }
 
+template <bool LDSW>  // weights staged in LDS (double-buffered) vs read through L2
 __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* R1 = smem;
@@ -223,17 +227,22 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   const int TNI = a.tni;
   const int ngroups = (a.N + TNI - 1) / TNI;
   uint4 wr[kWRegs];
-  // layer 0's weights for the first iteration
-  wload(a.w[0], tail_n16(0), wr);
-  wstore(WB[0], tail_n16(0), TG<16>::NCH, wr);
-  // phase helper: prefetch layer l+1 (wrapping to 0 for the next group) into registers,
-  // run conv l from WB[l & 1], park l+1 in the other buffer, barrier
-#define TAIL_PHASE(l, CI, CO, ...)                                                          \
+  if (LDSW) {  // layer 0's weights for the first iteration
+    wload(a.w[0], tail_n16(0), wr);
+    wstore(WB[0], tail_n16(0), TG<16>::NCH, wr);
+  }
+  // phase helper (LDSW): prefetch layer l+1 (wrapping to 0 for the next group) into
+  // registers, run conv l from WB[l & 1], park l+1 in the other buffer
+#define TAIL_PHASE(l, CI, CO, IN, H_, W_, WBUF, ...)                                        \
   do {                                                                                      \
-    const int ln = ((l) + 1) % 14;                                                          \
-    wload(a.w[ln], tail_n16(ln), wr);                                                       \
-    conv_lds<CI, CO>(__VA_ARGS__);                                                          \
-    wstore(WB[ln & 1], tail_n16(ln), ln < 5 ? TG<16>::NCH : TG<32>::NCH, wr);               \
+    if (LDSW) {                                                                             \
+      const int ln = ((l) + 1) % 14;                                                        \
+      wload(a.w[ln], tail_n16(ln), wr);                                                     \
+      conv_lds<CI, CO>(IN, H_, W_, nimg, WBUF, wrow_bytes<CI>(), __VA_ARGS__);              \
+      wstore(WB[ln & 1], tail_n16(ln), ln < 5 ? TG<16>::NCH : TG<32>::NCH, wr);             \
+    } else {                                                                                \
+      conv_lds<CI, CO>(IN, H_, W_, nimg, (const char*)a.w[l], TG<CI>::NCH * 64, __VA_ARGS__); \
+    }                                                                                       \
   } while (0)
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
@@ -253,14 +262,13 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     __syncthreads();
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(2 * rb, 16, 16, R1, H0, W0, nimg, WB[0], a.b[2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(2 * rb, 16, 16, R1, H0, W0, WB[0], a.b[2 * rb], true, R2, false, nullptr);
       __syncthreads();
-      TAIL_PHASE(2 * rb + 1, 16, 16, R2, H0, W0, nimg, WB[1], a.b[2 * rb + 1], true, R1, true,
-                 nullptr);
+      TAIL_PHASE(2 * rb + 1, 16, 16, R2, H0, W0, WB[1], a.b[2 * rb + 1], true, R1, true, nullptr);
       __syncthreads();
     }
     // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1)
-    TAIL_PHASE(4, 16, 32, R1, H0, W0, nimg, WB[0], a.b[4], false, nullptr, false, (bf16*)R2);
+    TAIL_PHASE(4, 16, 32, R1, H0, W0, WB[0], a.b[4], false, nullptr, false, (bf16*)R2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
     zero_halo(R1, nimg, H1, W1, TG<32>::PIXB);
@@ -268,15 +276,13 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     zero_halo(R2, nimg, H1, W1, TG<32>::PIXB);  // U1 layout (staging consumed)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(5 + 2 * rb, 32, 32, R1, H1, W1, nimg, WB[1], a.b[5 + 2 * rb], true, R2, false,
-                 nullptr);
+      TAIL_PHASE(5 + 2 * rb, 32, 32, R1, H1, W1, WB[1], a.b[5 + 2 * rb], true, R2, false, nullptr);
       __syncthreads();
-      TAIL_PHASE(6 + 2 * rb, 32, 32, R2, H1, W1, nimg, WB[0], a.b[6 + 2 * rb], true, R1, true,
-                 nullptr);
+      TAIL_PHASE(6 + 2 * rb, 32, 32, R2, H1, W1, WB[0], a.b[6 + 2 * rb], true, R1, true, nullptr);
       __syncthreads();
     }
     // ---- stage 2
-    TAIL_PHASE(9, 32, 32, R1, H1, W1, nimg, WB[1], a.b[9], false, nullptr, false, (bf16*)R2);
+    TAIL_PHASE(9, 32, 32, R1, H1, W1, WB[1], a.b[9], false, nullptr, false, (bf16*)R2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
     zero_halo(R1, nimg, H2, W2, TG<32>::PIXB);
@@ -284,11 +290,9 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     zero_halo(R2, nimg, H2, W2, TG<32>::PIXB);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(10 + 2 * rb, 32, 32, R1, H2, W2, nimg, WB[0], a.b[10 + 2 * rb], true, R2, false,
-                 nullptr);
+      TAIL_PHASE(10 + 2 * rb, 32, 32, R1, H2, W2, WB[0], a.b[10 + 2 * rb], true, R2, false, nullptr);
       __syncthreads();
-      TAIL_PHASE(11 + 2 * rb, 32, 32, R2, H2, W2, nimg, WB[1], a.b[11 + 2 * rb], true, R1, true,
-                 nullptr);
+      TAIL_PHASE(11 + 2 * rb, 32, 32, R2, H2, W2, WB[1], a.b[11 + 2 * rb], true, R1, true, nullptr);
       __syncthreads();
     }
 #undef TAIL_PHASE
@@ -343,16 +347,26 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
   }
   // images per iteration: as many as LDS allows (each conv phase pays one L2 round trip
   // for its weights, so more images amortise it) while keeping >= one group per CU
+  static int variant = -1, force_tni = 0;  // tuning knobs (A/B in tools/microbench.py)
+  if (variant < 0) {
+    const char* v = std::getenv("MBK_TRUNK_VARIANT");
+    variant = (v && std::string(v) == "l2") ? 0 : 1;
+    const char* t = std::getenv("MBK_TRUNK_TNI");
+    force_tni = t ? std::atoi(t) : 0;
+  }
+  const bool ldsw = variant == 1;
+  const size_t wb = ldsw ? 2 * kWBufBytes : 0;
   int tni = 1;
-  while (tni < kMaxTNI && 2 * region_bytes(H0, W0, tni * 2) + 2 * kWBufBytes <= 160 * 1024 &&
+  while (tni < kMaxTNI && 2 * region_bytes(H0, W0, tni * 2) + wb <= 160 * 1024 &&
          (N + tni * 2 - 1) / (tni * 2) >= cus)
     tni *= 2;
+  if (force_tni > 0) tni = std::min(force_tni, kMaxTNI);
   a.tni = tni;
   const size_t r = region_bytes(H0, W0, tni);
   a.r1_bytes = (int)r;
-  const size_t sm = 2 * r + 2 * kWBufBytes;
+  const size_t sm = 2 * r + wb;
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  auto kfn = trunk_tail_kernel;
+  auto kfn = ldsw ? trunk_tail_kernel<true> : trunk_tail_kernel<false>;
   if (sm > 64 * 1024)
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;

@@ -38,6 +38,7 @@ class LearnerHParams:
     reward_clip: float = 0.0    # reference: none
     max_grad_norm: float = 0.0  # reference: none
     bucket_mb: float = 8.0
+    allreduce_dtype: str = "fp32"  # fp32 | bf16 (gradient all-reduce payload)
 
 
 class Learner:
@@ -50,7 +51,9 @@ class Learner:
         self.flat = FlatParams(self.model, device)
         broadcast_flat(self.flat, self.info)
         self.opt = FlatAdam(self.flat, lr=hp.lr, eps=hp.adam_eps, max_grad_norm=hp.max_grad_norm)
-        self.reducer = GradAllReducer(self.flat, self.info, hp.bucket_mb)
+        self.reducer = GradAllReducer(
+            self.flat, self.info, hp.bucket_mb,
+            torch.bfloat16 if hp.allreduce_dtype == "bf16" else torch.float32)
         self.ws = VTraceWorkspace()
         self.n_updates = 0
         self.timing = {}

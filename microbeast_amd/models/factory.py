@@ -11,7 +11,7 @@ ARCHS = ("impala_flat", "impala_deep", "gridnet")
 
 def make_model(flags, device: torch.device | str = "cpu") -> torch.nn.Module:
     s = flags.env_size
-    dt = torch.bfloat16 if flags.dtype == "bf16" else torch.float32
+    dt = torch.bfloat16 if flags.dtype in ("bf16", "fp8") else torch.float32
     if flags.arch == "impala_flat":
         m = Agent((s, s, 27), channels=flags.channel_list(), hidden=flags.hidden, compute_dtype=dt)
     elif flags.arch == "impala_deep":

@@ -75,8 +75,13 @@ def broadcast_flat(flat: FlatParams, info: DistInfo) -> None:
 class GradAllReducer:
     """Bucketed, backward-overlapped gradient all-reduce over a FlatParams grad."""
 
-    def __init__(self, flat: FlatParams, info: DistInfo, bucket_mb: float = 8.0):
+    def __init__(self, flat: FlatParams, info: DistInfo, bucket_mb: float = 8.0,
+                 comm_dtype: torch.dtype = torch.float32):
+        """comm_dtype=bfloat16 all-reduces a bf16 copy of each bucket (half the xGMI bytes);
+        the result is written back into the fp32 gradient buffer (fp32 master grads)."""
         self.flat, self.info = flat, info
+        self.comm_dtype = comm_dtype
+        self.bufs: list = []
         self.buckets: list[tuple[int, int]] = []
         self.param_bucket: dict[int, int] = {}
         self.works = []
@@ -121,13 +126,19 @@ class GradAllReducer:
     def _launch(self, b: int):
         s, e = self.buckets[b]
         self.fired[b] = True
-        self.works.append(dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM, async_op=True))
+        g = self.flat.grad[s:e]
+        if self.comm_dtype != torch.float32:
+            buf = g.to(self.comm_dtype)
+            self.bufs.append((s, e, buf))
+            g = buf
+        self.works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, async_op=True))
 
     def start_step(self):
         if self.info.enabled:
             self.count = [0] * len(self.buckets)
             self.fired = [False] * len(self.buckets)
             self.works = []
+            self.bufs = []
 
     def finish(self):
         """Launch any bucket whose params got no gradient, wait, average."""
@@ -139,6 +150,9 @@ class GradAllReducer:
         for w in self.works:
             w.wait()
         self.works = []
+        for s, e, buf in self.bufs:
+            self.flat.grad[s:e].copy_(buf)
+        self.bufs = []
         self.flat.grad.mul_(1.0 / self.info.world_size)
 
 

@@ -33,7 +33,7 @@ def _hparams(flags: Flags) -> LearnerHParams:
                           baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost,
                           rho_bar=flags.rho_bar, c_bar=flags.c_bar, pg_rho_bar=flags.pg_rho_bar,
                           reward_clip=flags.reward_clip, max_grad_norm=flags.max_grad_norm,
-                          bucket_mb=flags.bucket_mb)
+                          bucket_mb=flags.bucket_mb, allreduce_dtype=flags.allreduce_dtype)
 
 
 def checkpoint_path(flags: Flags) -> str:
@@ -46,6 +46,32 @@ def _gather_episodes(recs, info):
     out = [None] * info.world_size
     torch.distributed.all_gather_object(out, recs)
     return [r for part in out for r in (part or [])] if info.is_main else []
+
+
+_PROFILE_START = 3  # skip the first updates (graph capture, allocator warm-up)
+
+
+def _profile_tick(prof, n_update: int, flags: Flags, cuda: bool):
+    """Start the torch.profiler at update _PROFILE_START, stop after profile_updates updates
+    (or at shutdown: n_update = -1) and write {exp}_trace.json + {exp}_profile.txt."""
+    from torch.profiler import ProfilerActivity, profile
+    end = _PROFILE_START + flags.profile_updates
+    if prof is None and n_update == _PROFILE_START:
+        acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if cuda else [])
+        prof = profile(activities=acts, record_shapes=False)
+        prof.__enter__()
+        return prof
+    if prof is not None and (n_update == end or n_update < 0):
+        if cuda:
+            torch.cuda.synchronize()
+        prof.__exit__(None, None, None)
+        base = os.path.join(flags.savedir, flags.exp_name)
+        prof.export_chrome_trace(base + "_trace.json")
+        sort = "self_cuda_time_total" if cuda else "self_cpu_time_total"
+        with open(base + "_profile.txt", "w") as f:
+            f.write(prof.key_averages().table(sort_by=sort, row_limit=40))
+        return None
+    return prof
 
 
 def _league_extra(league):
@@ -90,7 +116,7 @@ def train(flags: Flags) -> dict:
                              max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
                              bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
                              env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
-                             fp8_policy=flags.fp8_policy)
+                             fp8_policy=flags.fp8_policy or flags.dtype == "fp8")
         if sp_groups:
             from .runtime.league import League
 
@@ -116,10 +142,13 @@ def train(flags: Flags) -> dict:
         frames_per_update = flags.batch_size * flags.n_envs * flags.unroll_length
     frames_per_update *= info.world_size
 
+    prof = None  # --profile_updates: torch.profiler timeline of a few steady-state updates
     t_start = time.perf_counter()
     last = {}
     try:
         while step < flags.total_steps and (flags.max_updates <= 0 or n_update < flags.max_updates):
+            if flags.profile_updates > 0 and info.is_main:
+                prof = _profile_tick(prof, n_update, flags, want_cuda)
             t0 = time.perf_counter()
             if runtime == "gpu":
                 batch, slots = rt.get_batch(timeout=flags.batch_timeout)
@@ -164,6 +193,8 @@ def train(flags: Flags) -> dict:
                                     extra=_league_extra(league))
                 D.barrier(info)
     finally:
+        if prof is not None:
+            _profile_tick(prof, -1, flags, want_cuda)
         rt.stop()
         if info.is_main:
             save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,

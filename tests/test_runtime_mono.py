@@ -39,3 +39,11 @@ def test_watchdog_respawns_killed_actors(tmp_path):
     out = train(_flags(tmp_path, "--max_updates", "6", "--fault_inject_every", "2",
                        "--actor_restarts", "10", "--batch_timeout", "120"))
     assert out["updates"] == 6
+
+
+def test_profiler_trace_written(tmp_path):
+    from microbeast_amd.train import train
+    out = train(_flags(tmp_path, "--max_updates", "6", "--profile_updates", "2"))
+    assert out["updates"] == 6
+    assert os.path.getsize(tmp_path / "plumb_trace.json") > 0
+    assert "Name" in open(tmp_path / "plumb_profile.txt").read()

@@ -22,6 +22,9 @@ def main():
     p.add_argument("--learn_T", type=int, default=64)
     p.add_argument("--learn_B", type=str, default="512,1024")
     p.add_argument("--iters", type=int, default=50)
+    p.add_argument("--variants", type=str, default="",
+                   help="comma list of encoder toggles to A/B in the same process: "
+                        "nofusedpool, nofusedtail")
     a = p.parse_args()
     import torch
 
@@ -77,20 +80,25 @@ def main():
                  "logp": torch.zeros(T + 1, B, device=dev), "reward": rew.to(dev),
                  "done": done.to(dev)}
         active = int((mask.view(-1, 3) != 0).any(-1).sum())
-        for _ in range(3):
-            learner.learn(batch)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        n = max(3, a.iters // 5)
-        for _ in range(n):
-            learner.learn(batch)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / n
-        learner.learn(batch, sync_timing=True)
-        print(json.dumps({"what": "learner_update", "frames": T * B, "ms": round(dt * 1e3, 3),
-                          "frames_per_s": round(T * B / dt, 1),
-                          "active_cells_frac": round(active / ((T + 1) * B * S), 4),
-                          "phases_s": learner.timing}), flush=True)
+        for variant in [""] + [v for v in a.variants.split(",") if v]:
+            enc = learner.model._hip_enc
+            if enc is not None:
+                enc.fused_pool_bwd = variant != "nofusedpool"
+            for _ in range(3):
+                learner.learn(batch)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            n = max(3, a.iters // 5)
+            for _ in range(n):
+                learner.learn(batch)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / n
+            learner.learn(batch, sync_timing=True)
+            print(json.dumps({"what": "learner_update", "variant": variant or "default",
+                              "frames": T * B, "ms": round(dt * 1e3, 3),
+                              "frames_per_s": round(T * B / dt, 1),
+                              "active_cells_frac": round(active / ((T + 1) * B * S), 4),
+                              "phases_s": learner.timing}), flush=True)
 
 
 if __name__ == "__main__":
