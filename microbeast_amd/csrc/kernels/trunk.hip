@@ -350,7 +350,7 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
   static int variant = -1, force_tni = 0;  // tuning knobs (A/B in tools/microbench.py)
   if (variant < 0) {
     const char* v = std::getenv("MBK_TRUNK_VARIANT");
-    variant = (v && std::string(v) == "l2") ? 0 : 1;
+    variant = (v && std::string(v) == "lds") ? 1 : 0;  // measured: L2 + 16 images is faster
     const char* t = std::getenv("MBK_TRUNK_TNI");
     force_tni = t ? std::atoi(t) : 0;
   }
@@ -360,7 +360,10 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
   while (tni < kMaxTNI && 2 * region_bytes(H0, W0, tni * 2) + wb <= 160 * 1024 &&
          (N + tni * 2 - 1) / (tni * 2) >= cus)
     tni *= 2;
-  if (force_tni > 0) tni = std::min(force_tni, kMaxTNI);
+  if (force_tni > 0) {
+    tni = std::min(force_tni, kMaxTNI);
+    while (tni > 1 && 2 * region_bytes(H0, W0, tni) + wb > 160 * 1024) tni /= 2;
+  }
   a.tni = tni;
   const size_t r = region_bytes(H0, W0, tni);
   a.r1_bytes = (int)r;

@@ -110,7 +110,10 @@ class HipEncoder:
         # reference (16, 32, 32) shape
         self.fused_tail = (tuple(channels) == (16, 32, 32) and self.layers[1].H <= 16
                            and self.layers[1].W <= 16)
-        self.fused_pool_bwd = True  # max-pool backward folded into the stage conv's wgrad/dgrad
+        # max-pool backward folded into the stage conv's wgrad / dgrad staging: saves the
+        # pre-pool gradient's HBM round trip but measured 6 % slower per update on MI355X
+        # (extra expand phase + a 1-wave/SIMD dgrad variant), so off by default
+        self.fused_pool_bwd = False
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
