@@ -24,7 +24,7 @@ def main():
     p.add_argument("--iters", type=int, default=50)
     p.add_argument("--variants", type=str, default="",
                    help="comma list of encoder toggles to A/B in the same process: "
-                        "nofusedpool, nofusedtail")
+                        "fusedpool, nofusedpool")
     a = p.parse_args()
     import torch
 
@@ -82,8 +82,8 @@ def main():
         active = int((mask.view(-1, 3) != 0).any(-1).sum())
         for variant in [""] + [v for v in a.variants.split(",") if v]:
             enc = learner.model._hip_enc
-            if enc is not None:
-                enc.fused_pool_bwd = variant != "nofusedpool"
+            if enc is not None and variant in ("fusedpool", "nofusedpool"):
+                enc.fused_pool_bwd = variant == "fusedpool"
             for _ in range(3):
                 learner.learn(batch)
             torch.cuda.synchronize()
