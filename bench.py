@@ -92,6 +92,10 @@ def main(argv=None):
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
     if args.learner_cu_reserve > 0:
         from microbeast_amd import _native as N
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        # persistent learner grids sized for the CUs the masked stream may use
+        N.kernels().mbk_set_cu_budget(ncu - (ncu + args.learner_cu_reserve - 1)
+                                      // args.learner_cu_reserve)
         h = N.runtime().create_cu_masked_stream(dev.index, args.learner_cu_reserve)
         learner_stream = torch.cuda.ExternalStream(h, device=dev)
         learner_stream.wait_stream(torch.cuda.current_stream())

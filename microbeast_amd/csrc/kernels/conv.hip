@@ -923,7 +923,9 @@ inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool 
   return t > red ? t : red;
 }
 
-int g_grid_cap = 0;  // tests force multi-group workgroups with a small cap
+int g_grid_cap = 0;    // tests force multi-group workgroups with a small cap
+int g_cu_budget = 0;   // CUs a persistent grid is sized for (0 = all); set when the learner
+                       // runs on a CU-masked stream so its grid fits the masked CUs exactly
 
 // resident workgroups the whole device holds for (kernel, dynamic LDS)
 int resident_blocks(const void* kfn, size_t sm) {
@@ -938,7 +940,8 @@ int resident_blocks(const void* kfn, size_t sm) {
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
     per = 1;
-  int r = cus * per;
+  const int ncu = g_cu_budget > 0 ? std::min(g_cu_budget, cus) : cus;
+  int r = ncu * per;
   if (g_grid_cap > 0 && r > g_grid_cap) r = g_grid_cap;
   return r;
 }
@@ -1077,6 +1080,7 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
 }
 
 extern "C" void mbk_conv_set_grid_cap(int cap) { g_grid_cap = cap; }
+extern "C" void mbk_set_cu_budget(int n) { g_cu_budget = n; }
 
 // partial holds nparts rows plus ceil(nparts / kReducePps) scratch rows after them
 extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,
