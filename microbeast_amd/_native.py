@@ -62,6 +62,8 @@ _SIGS = {
                      c_void_p],
     "mbk_fc_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                    c_void_p, c_void_p, c_void_p],
+    "mbk_gemm_nt": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                    c_int, c_int, c_int, c_int, c_void_p],
     "mbk_wgrad_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                          c_void_p],
     "mbk_pool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -44,13 +44,22 @@ class _Linear(torch.autograd.Function):
         wc = w.to(x.dtype)
         ctx.save_for_backward(x, wc)
         ctx.w_dtype = w.dtype
+        if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+            from .gemm import gemm_nt_raw  # hand-written MFMA GEMM (gemm.hip)
+            return gemm_nt_raw(x.contiguous(), wc.contiguous(), b)
         return torch.nn.functional.linear(x, wc, b.to(x.dtype) if b is not None else None)
 
     @staticmethod
     def backward(ctx, g):
         x, wc = ctx.saved_tensors
         g = g.contiguous()
-        gx = g @ wc if ctx.needs_input_grad[0] else None
+        gx = None
+        if ctx.needs_input_grad[0]:
+            if g.is_cuda and g.dtype == torch.bfloat16 and wc.shape[0] % 8 == 0:
+                from .gemm import gemm_nt_raw
+                gx = gemm_nt_raw(g, wc.t().contiguous())
+            else:
+                gx = g @ wc
         gw = weight_grad(g, x).to(ctx.w_dtype) if ctx.needs_input_grad[1] else None
         gb = g.float().sum(0) if ctx.needs_input_grad[2] else None
         return gx, gw, gb
