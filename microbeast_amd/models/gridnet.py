@@ -17,13 +17,17 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import cell_head
+from ..ops.gridconv import conv3x3, conv_transpose3x3s2, maxpool3x3s2
+from ..ops.linear import linear
 from ..ops.obs import bits_to_planes
 from .agent import layer_init
 
 
 class GridNetAgent(nn.Module):
-    def __init__(self, obs_space_shape=(16, 16, 27), compute_dtype=torch.bfloat16):
+    def __init__(self, obs_space_shape=(16, 16, 27), compute_dtype=torch.bfloat16,
+                 hip_kernels: bool = True):
         super().__init__()
+        self.hip_kernels = hip_kernels
         h, w, c = obs_space_shape
         self.h, self.w, self.planes = h, w, c
         self.ph, self.pw = -(-h // 16) * 16, -(-w // 16) * 16
@@ -58,7 +62,36 @@ class GridNetAgent(nn.Module):
                               enabled=t.is_cuda and self.compute_dtype != torch.float32,
                               cache_enabled=False)
 
+    def _use_hip(self, obs) -> bool:
+        return self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32
+
+    def _policy_value_hip(self, obs):
+        """Every conv / transposed conv on the MFMA GEMM (ops/gridconv.py), NHWC bf16.
+        relu(maxpool(conv)) is computed as maxpool(relu-fused conv): identical values."""
+        n = obs.numel() // (self.h * self.w)
+        bits = obs.reshape(n, self.h, self.w, 1)
+        sh = torch.arange(32, device=obs.device, dtype=torch.int32)
+        x = ((bits >> sh) & 1).to(torch.bfloat16)  # planes 27..31 are zero: Cin 27 -> 32
+        if (self.ph, self.pw) != (self.h, self.w):
+            x = F.pad(x, (0, 0, 0, self.pw - self.w, 0, self.ph - self.h))
+        for i in (0, 3, 6, 9):
+            conv = self.encoder[i]
+            x = maxpool3x3s2(conv3x3(x, conv.weight, conv.bias, relu=True))
+        z = x  # NHWC [n, ph/16, pw/16, 256]
+        y = z
+        for j, i in enumerate((0, 2, 4, 6)):
+            ct = self.actor[i]
+            last = j == 3
+            y = conv_transpose3x3s2(y, ct.weight, ct.bias, relu=not last, nchw_out=last)
+        logits = y[:, :, :self.h, :self.w].permute(0, 2, 3, 1).reshape(n, -1).float()
+        zf = z.permute(0, 3, 1, 2).reshape(n, -1)  # the reference's NCHW flatten order
+        hdn = F.relu(linear(zf, self.critic[1]))
+        v = linear(hdn, self.critic[3])
+        return logits, v.float().view(-1)
+
     def policy_value(self, obs):
+        if self._use_hip(obs):
+            return self._policy_value_hip(obs)
         x = self._planes(obs)
         with self._autocast(x):
             z = self.encoder(x)

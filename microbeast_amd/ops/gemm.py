@@ -22,7 +22,13 @@ def gemm_nt_raw(a: torch.Tensor, b: torch.Tensor, bias: torch.Tensor | None = No
                 out_dtype=torch.bfloat16, accumulate: bool = False) -> torch.Tensor:
     """No-grad launch. a [M,K] / b [N,K] bf16 with K-contiguous rows (K % 8 == 0)."""
     assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16
-    assert a.stride(1) == 1 and b.stride(1) == 1 and a.shape[1] == b.shape[1]
+    assert a.shape[1] == b.shape[1]
+    K = a.shape[1]
+    if K % 8 or a.stride(1) != 1 or b.stride(1) != 1 or a.stride(0) % 8 or b.stride(0) % 8:
+        # the kernel reads 8-element K vectors: zero-pad K (adds nothing to the products)
+        kp = -(-K // 8) * 8
+        a = torch.nn.functional.pad(a, (0, kp - K))
+        b = torch.nn.functional.pad(b, (0, kp - K))
     M, K = a.shape
     Nn = b.shape[0]
     if out is None:
