@@ -37,15 +37,17 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
       (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
 }
 
-// stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled
+// stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled;
+// row n is read from source row n + shift (zero outside [0, nsrc))
 template <int W, bool VEC>
 __device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, int c0, int ld,
-                                      int tid) {
+                                      int tid, int shift = 0, int nsrc = 0x7fffffff) {
   constexpr int C8 = W / 8;
   for (int e = tid; e < R * C8; e += kThreads) {
-    const int row = e / C8, c = c0 + (e % C8) * 8, n = r + row;
+    const int row = e / C8, c = c0 + (e % C8) * 8;
+    const int n = r + row + shift;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (n < N) {
+    if (r + row < N && n >= 0 && n < nsrc) {
       if (VEC && c + 8 <= ld) {
         v = *(const uint4*)(src + (size_t)n * ld + c);
       } else {
@@ -61,18 +63,31 @@ __device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, in
   }
 }
 
+// Row shifts of the x operand, one per output column block ("tap"): dW[o][t*I + i] =
+// sum_n g[n][o] x[n + shift_t][i] -- the weight gradient of the shifted-row (implicit
+// im2col) convolution GEMM in gemm.hip, all taps in one launch.
+constexpr int kMaxTaps = 9;
+struct XShifts {
+  int s[kMaxTaps];
+  int ntap;
+};
+
 template <bool GVEC>
 __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restrict__ g,
                                                             const bf16* __restrict__ x, int N,
                                                             int O, int I, int rows_per_part,
-                                                            float* __restrict__ partial) {
+                                                            float* __restrict__ partial,
+                                                            XShifts xs) {
   __shared__ __attribute__((aligned(16))) char smem[R * GROW + R * XROW];
   char* gt = smem;
   char* xt = smem + R * GROW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = lane >> 4, li = lane & 15;
   const int ncb = (I + IC - 1) / IC;
-  const int o0 = (blockIdx.y / ncb) * OC, i0 = (blockIdx.y % ncb) * IC;
+  const int nch = ncb * ((O + OC - 1) / OC);
+  const int tap = blockIdx.y / nch, by = blockIdx.y - tap * nch;
+  const int o0 = (by / ncb) * OC, i0 = (by % ncb) * IC;
+  const int xshift = xs.s[tap];
   const int r0 = blockIdx.x * rows_per_part, r1 = min(N, r0 + rows_per_part);
   f32x4 acc[MBC][CBC];
 #pragma unroll
@@ -83,7 +98,7 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
   for (int rs = r0; rs < r1; rs += R) {
     __syncthreads();  // previous stage's reads done
     stage<OC, GVEC>(gt, g, rs, r1, o0, O, tid);
-    stage<IC, true>(xt, x, rs, r1, i0, I, tid);
+    stage<IC, true>(xt, x, rs, r1, i0, I, tid, xshift, N);
     __syncthreads();
     const int nk = (min(R, r1 - rs) + 31) >> 5;
     for (int kb = wave; kb < nk; kb += kThreads / 64) {
@@ -126,10 +141,11 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
     }
     __syncthreads();
   }
-  float* out = partial + (size_t)blockIdx.x * O * I;
+  const int TI = xs.ntap * I;  // output row width
+  float* out = partial + (size_t)blockIdx.x * O * TI + (size_t)tap * I;
   for (int e = tid; e < OC * IC; e += kThreads) {
     const int o = o0 + e / IC, i = i0 + e % IC;
-    if (o < O && i < I) out[(size_t)o * I + i] = red[e];
+    if (o < O && i < I) out[(size_t)o * TI + i] = red[e];
   }
 }
 
@@ -264,20 +280,20 @@ extern "C" int mbk_fc_wgrad_parts(int N, int O, int I) {
   return std::max(1, std::min(512, stages / 8));  // >= 8 stages (1024 rows) per split
 }
 
-// partial: (nparts + ceil(nparts / 32)) * O * I floats of scratch; out: fp32 [O][I]
-extern "C" int mbk_fc_wgrad(const void* g, const void* x, int N, int O, int I, float* partial,
-                            int nparts, float* out, int accumulate, hipStream_t stream) {
+namespace {
+int fc_wgrad_impl(const void* g, const void* x, int N, int O, int I, const XShifts& xs,
+                  float* partial, int nparts, float* out, int accumulate, hipStream_t stream) {
   if (N <= 0 || O <= 0 || I <= 0 || nparts < 1 || I % 8) return (int)hipErrorInvalidValue;
   const int stages = (N + R - 1) / R;
   const int rpp = ((stages + nparts - 1) / nparts) * R;
-  const int chunks = ((O + OC - 1) / OC) * ((I + IC - 1) / IC);
+  const int chunks = ((O + OC - 1) / OC) * ((I + IC - 1) / IC) * xs.ntap;
   if (O % 8 == 0)
     hipLaunchKernelGGL(fc_wgrad_kernel<true>, dim3(nparts, chunks), dim3(kThreads), 0, stream,
-                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial);
+                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial, xs);
   else  // e.g. the critic, O = 1
     hipLaunchKernelGGL(fc_wgrad_kernel<false>, dim3(nparts, chunks), dim3(kThreads), 0, stream,
-                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial);
-  const long row = (long)O * I;
+                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial, xs);
+  const long row = (long)O * I * xs.ntap;
   const unsigned cols = (unsigned)((row + 63) / 64);
   constexpr int kPps = 32;
   if (nparts > 2 * kPps) {
@@ -293,4 +309,25 @@ extern "C" int mbk_fc_wgrad(const void* g, const void* x, int N, int O, int I, f
                        accumulate);
   }
   return (int)hipGetLastError();
+}
+}  // namespace
+
+// partial: (nparts + ceil(nparts / 32)) * O * I floats of scratch; out: fp32 [O][I]
+extern "C" int mbk_fc_wgrad(const void* g, const void* x, int N, int O, int I, float* partial,
+                            int nparts, float* out, int accumulate, hipStream_t stream) {
+  XShifts xs{};
+  xs.ntap = 1;
+  return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
+}
+
+// Shifted-row weight gradient: out fp32 [O][ntap * I], block t = sum_n g[n][:]^T x[n + shift_t][:]
+// (x rows outside [0, N) are zero). Scratch: (nparts + ceil(nparts / 32)) * O * ntap * I floats.
+extern "C" int mbk_fc_wgrad_taps(const void* g, const void* x, int N, int O, int I,
+                                 const int* shifts, int ntap, float* partial, int nparts,
+                                 float* out, int accumulate, hipStream_t stream) {
+  if (ntap < 1 || ntap > kMaxTaps) return (int)hipErrorInvalidValue;
+  XShifts xs{};
+  for (int t = 0; t < ntap; ++t) xs.s[t] = shifts[t];
+  xs.ntap = ntap;
+  return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
 }

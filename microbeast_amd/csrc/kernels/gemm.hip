@@ -43,6 +43,34 @@ __device__ __forceinline__ void load_tile(const bf16* __restrict__ g, int rows, 
                                  : make_uint4(0, 0, 0, 0);
   }
 }
+
+// Shifted-row A operand ("implicit im2col"): K is split into ntap blocks of tk columns
+// (tk % 32 == 0, so a 32-wide K step never straddles two taps); block t reads row
+// m + shift[t] of its own matrix base[t] ([rows][lda], K-contiguous), zero outside [0, rows).
+// A 3x3 conv over a zero-padded NHWC grid is then ONE GEMM (tap shifts dy*Wp + dx), and a
+// stride-2 transposed conv is four sub-pixel phase GEMMs of 1 / 2 / 2 / 4 taps.
+constexpr int kMaxTaps = 9;
+struct ATaps {
+  const bf16* base[kMaxTaps];
+  int shift[kMaxTaps];
+  int ntap, tk;
+};
+
+__device__ __forceinline__ void load_tile_taps(const ATaps& t, int rows, int ld, int r0, int k0,
+                                               uint4 r[2]) {
+  const int tap = k0 / t.tk, kin = k0 - tap * t.tk;
+  const bf16* g = t.base[tap];
+  const int sh = t.shift[tap];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int e = threadIdx.x + j * kThreads;
+    const int row = e >> 2, q = e & 3;
+    const int gr = r0 + row + sh;
+    r[j] = (gr >= 0 && gr < rows && tap < t.ntap)
+               ? *(const uint4*)(g + (size_t)gr * ld + kin + q * 8)
+               : make_uint4(0, 0, 0, 0);
+  }
+}
 __device__ __forceinline__ void store_tile(char* t, const uint4 r[2]) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -51,11 +79,11 @@ __device__ __forceinline__ void store_tile(char* t, const uint4 r[2]) {
   }
 }
 
-template <bool OUT_BF16>
+template <bool OUT_BF16, bool TAPS>
 __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int relu,
-    int accumulate) {
+    int accumulate, ATaps taps) {
   __shared__ __attribute__((aligned(16))) char sm[2][2][TM * ROWB];  // [buf][A|B]
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -67,7 +95,8 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   uint4 ra[2], rb[2];
-  load_tile(A, M, lda, m0, 0, K, ra);
+  if (TAPS) load_tile_taps(taps, M, lda, m0, 0, ra);
+  else load_tile(A, M, lda, m0, 0, K, ra);
   load_tile(B, N, ldb, n0, 0, K, rb);
   store_tile(sm[0][0], ra);
   store_tile(sm[0][1], rb);
@@ -76,7 +105,8 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
   for (int kk = 0; kk < nk; ++kk) {
     const int cur = kk & 1;
     if (kk + 1 < nk) {  // prefetch the next K step into registers
-      load_tile(A, M, lda, m0, (kk + 1) * TK, K, ra);
+      if (TAPS) load_tile_taps(taps, M, lda, m0, (kk + 1) * TK, ra);
+      else load_tile(A, M, lda, m0, (kk + 1) * TK, K, ra);
       load_tile(B, N, ldb, n0, (kk + 1) * TK, K, rb);
     }
     const char* ta = sm[cur][0];
@@ -134,11 +164,43 @@ extern "C" int mbk_gemm_nt(const void* A, const void* B, void* C, const float* b
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % 8 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN);
+  ATaps none{};
   if (out_bf16)
-    hipLaunchKernelGGL(gemm_nt_kernel<true>, grid, dim3(kThreads), 0, stream, (const bf16*)A,
-                       (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, 0);
+    hipLaunchKernelGGL((gemm_nt_kernel<true, false>), grid, dim3(kThreads), 0, stream,
+                       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, 0,
+                       none);
   else
-    hipLaunchKernelGGL(gemm_nt_kernel<false>, grid, dim3(kThreads), 0, stream, (const bf16*)A,
-                       (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, accumulate);
+    hipLaunchKernelGGL((gemm_nt_kernel<false, false>), grid, dim3(kThreads), 0, stream,
+                       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu,
+                       accumulate, none);
+  return (int)hipGetLastError();
+}
+
+// Shifted-row ("implicit im2col") GEMM: C[M][N] = sum_t A_t[m + shift_t][:] . B[:, t*tk ...]^T
+// A_t: bases[t] [M][lda] bf16 (rows outside [0, M) read as zero), tk % 32 == 0,
+// B: [N][ntap*tk] bf16 (tap-major K).
+extern "C" int mbk_gemm_nt_taps(const void* const* bases, const int* shifts, int ntap, int tk,
+                                const void* B, void* C, const float* bias, int M, int N, int lda,
+                                int ldb, int ldc, int relu, int out_bf16, int accumulate,
+                                hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (ntap < 1 || ntap > kMaxTaps || tk % 32 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
+  ATaps t{};
+  for (int i = 0; i < ntap; ++i) {
+    t.base[i] = (const bf16*)bases[i];
+    t.shift[i] = shifts[i];
+  }
+  t.ntap = ntap;
+  t.tk = tk;
+  const int K = ntap * tk;
+  dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN);
+  if (out_bf16)
+    hipLaunchKernelGGL((gemm_nt_kernel<true, true>), grid, dim3(kThreads), 0, stream,
+                       (const bf16*)nullptr, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc,
+                       relu, 0, t);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<false, true>), grid, dim3(kThreads), 0, stream,
+                       (const bf16*)nullptr, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc,
+                       relu, accumulate, t);
   return (int)hipGetLastError();
 }

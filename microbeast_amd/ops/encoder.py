@@ -130,24 +130,31 @@ class HipEncoder:
     # ------------------------------------------------------------ helpers
     def pack(self, weights: list[torch.Tensor], with_bwd: bool) -> None:
         k = N.kernels()
-        jobs = (_Job * len(self.layers))()
-        for i, (L, wt) in enumerate(zip(self.layers, weights)):
-            assert wt.dtype == torch.float32 and wt.is_contiguous()
-            bwd = (self.packed_bwd.data_ptr() + 2 * L.wb_off) if (with_bwd and L.wb_off >= 0) else None
-            jobs[i] = _Job(wt.data_ptr(), self.packed_fwd.data_ptr() + 2 * L.w_off, bwd, L.cin,
-                           L.cin_real, L.cout)
-        N.check(k.mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), len(self.layers),
-                                N.stream_ptr()), "conv_pack")
+        for c0 in range(0, len(self.layers), 16):  # one launch packs up to 16 layers
+            layers = self.layers[c0:c0 + 16]
+            jobs = (_Job * len(layers))()
+            for i, (L, wt) in enumerate(zip(layers, weights[c0:c0 + 16])):
+                assert wt.dtype == torch.float32 and wt.is_contiguous()
+                bwd = ((self.packed_bwd.data_ptr() + 2 * L.wb_off)
+                       if (with_bwd and L.wb_off >= 0) else None)
+                jobs[i] = _Job(wt.data_ptr(), self.packed_fwd.data_ptr() + 2 * L.w_off, bwd,
+                               L.cin, L.cin_real, L.cout)
+            N.check(k.mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), len(layers),
+                                    N.stream_ptr()), "conv_pack")
 
     def pack_fp8(self, weights: list[torch.Tensor]) -> None:
         k = N.kernels()
-        jobs = (_Job8 * len(self.layers))()
-        for i, (L, wt) in enumerate(zip(self.layers, weights)):
-            assert wt.dtype == torch.float32 and wt.is_contiguous()
-            jobs[i] = _Job8(wt.data_ptr(), self.packed_fwd8.data_ptr() + L.w_off,
-                            self.scale8.data_ptr() + 4 * self._s_off[i], L.cin, L.cin_real, L.cout)
-        N.check(k.mbk_conv_pack_fp8(ctypes.cast(jobs, ctypes.c_void_p), len(self.layers),
-                                    N.stream_ptr()), "conv_pack_fp8")
+        for c0 in range(0, len(self.layers), 16):
+            idx = list(range(c0, min(c0 + 16, len(self.layers))))
+            jobs = (_Job8 * len(idx))()
+            for j, i in enumerate(idx):
+                L, wt = self.layers[i], weights[i]
+                assert wt.dtype == torch.float32 and wt.is_contiguous()
+                jobs[j] = _Job8(wt.data_ptr(), self.packed_fwd8.data_ptr() + L.w_off,
+                                self.scale8.data_ptr() + 4 * self._s_off[i], L.cin, L.cin_real,
+                                L.cout)
+            N.check(k.mbk_conv_pack_fp8(ctypes.cast(jobs, ctypes.c_void_p), len(idx),
+                                        N.stream_ptr()), "conv_pack_fp8")
 
     def _fwd8(self, i: int, x, bias, add=None):
         """Inference conv i on the fp8 MFMA kernel (bf16 activations in / out)."""

@@ -136,7 +136,9 @@ class GpuActorRuntime:
     def _policy_step(self, io, m, rng):
         k = N.kernels()
         st = N.stream_ptr()
-        hip = hasattr(m, "_use_hip") and m._use_hip(io["in_obs"])
+        # sparse-head models (flat IMPALA head) bucket their active pairs in the decode pass;
+        # dense-head models (GridNet) sample with the masked-cell kernel
+        hip = hasattr(m, "_head") and m._use_hip(io["in_obs"])
         if hip:
             # decode + bucket the sparse head's active pairs by cell in the same pass
             head = m._head(self.device)

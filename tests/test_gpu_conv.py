@@ -172,6 +172,28 @@ def test_encoder_fwd_bwd_matches_torch(cuda, s):
     assert max(errs.values()) < 4e-2, errs
 
 
+def test_deep_encoder_24x24_matches_torch(cuda):
+    """4-stage trunk (impala_deep, BASELINE config 4): 20 conv layers, so the inference
+    weight pack runs in several launches (<= 16 jobs each)."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    from microbeast_amd.ops.obs import bits_to_planes
+    torch.manual_seed(0)
+    s = 24
+    m = Agent((s, s, 27), channels=(16, 32, 32, 32)).to(cuda)
+    ref = copy.deepcopy(m).cpu().float()
+    obs = _random_obs_bits(8, s * s)
+    m.features(obs.to(cuda))
+    params = encoder_params(m.network, 4)
+    y = encode(obs.to(cuda), m._hip_enc, params, True).float()
+    yr = _ref_trunk(ref.network, bits_to_planes(obs, s, s), 4).permute(0, 2, 3, 1)
+    assert _rel(y.cpu(), yr) < 1e-2, _rel(y.cpu(), yr)
+    m.pack_inference(cuda)  # 20 layers -> chunked pack launches
+    with torch.no_grad():
+        yp = encode(obs.to(cuda), m._hip_enc, params, False, prepacked=True).float()
+    assert _rel(yp, y.detach()) < 1e-3, _rel(yp, y.detach())
+
+
 def test_persistent_grid_cap_matches(cuda):
     """Capping the persistent grid makes every workgroup walk several image groups (and the
     last group partial): forward must be bit-identical, weight grads equal up to the
