@@ -63,7 +63,7 @@ _SIGS = {
     "mbk_fc_wgrad_taps": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                           c_int, c_void_p, c_int, c_void_p],
     "mbk_gemm_nt_taps": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_fc_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                    c_void_p, c_void_p, c_void_p],
     "mbk_gemm_nt": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,

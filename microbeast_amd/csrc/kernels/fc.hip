@@ -10,6 +10,8 @@
 // fp32 partials are reduced by a deterministic two-level column sum. No host sync.
 #include "common.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -37,17 +39,15 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
       (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
 }
 
-// stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled;
-// row n is read from source row n + shift (zero outside [0, nsrc))
+// stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled
 template <int W, bool VEC>
 __device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, int c0, int ld,
-                                      int tid, int shift = 0, int nsrc = 0x7fffffff) {
+                                      int tid) {
   constexpr int C8 = W / 8;
   for (int e = tid; e < R * C8; e += kThreads) {
-    const int row = e / C8, c = c0 + (e % C8) * 8;
-    const int n = r + row + shift;
+    const int row = e / C8, c = c0 + (e % C8) * 8, n = r + row;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (r + row < N && n >= 0 && n < nsrc) {
+    if (n < N) {
       if (VEC && c + 8 <= ld) {
         v = *(const uint4*)(src + (size_t)n * ld + c);
       } else {
@@ -63,6 +63,7 @@ __device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, in
   }
 }
 
+
 // Row shifts of the x operand, one per output column block ("tap"): dW[o][t*I + i] =
 // sum_n g[n][o] x[n + shift_t][i] -- the weight gradient of the shifted-row (implicit
 // im2col) convolution GEMM in gemm.hip, all taps in one launch.
@@ -72,23 +73,42 @@ struct XShifts {
   int ntap;
 };
 
+// x tile of the shifted-row weight gradient: output column c (of ntap * I) is channel
+// c % I of tap c / I, i.e. x row n + shift[c / I]; each 8-column group lies in one tap
+__device__ __forceinline__ void stage_taps(char* t, const bf16* src, int r, int N, int c0,
+                                           int I, int TI, const XShifts& xs, int nsrc, int tid) {
+  constexpr int C8 = IC / 8;
+  for (int e = tid; e < R * C8; e += kThreads) {
+    const int row = e / C8, c = c0 + (e % C8) * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r + row < N && c < TI) {
+      const int tap = c / I;
+      const int n = r + row + xs.s[tap];
+      if (n >= 0 && n < nsrc) v = *(const uint4*)(src + (size_t)n * I + (c - tap * I));
+    }
+    *(uint4*)(t + e * 16) = v;
+  }
+}
+
 template <bool GVEC>
 __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restrict__ g,
                                                             const bf16* __restrict__ x, int N,
                                                             int O, int I, int rows_per_part,
                                                             float* __restrict__ partial,
-                                                            XShifts xs) {
+                                                            XShifts xs, int chunk_fast) {
   __shared__ __attribute__((aligned(16))) char smem[R * GROW + R * XROW];
   char* gt = smem;
   char* xt = smem + R * GROW;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = lane >> 4, li = lane & 15;
-  const int ncb = (I + IC - 1) / IC;
-  const int nch = ncb * ((O + OC - 1) / OC);
-  const int tap = blockIdx.y / nch, by = blockIdx.y - tap * nch;
-  const int o0 = (by / ncb) * OC, i0 = (by % ncb) * IC;
-  const int xshift = xs.s[tap];
-  const int r0 = blockIdx.x * rows_per_part, r1 = min(N, r0 + rows_per_part);
+  const int TI = xs.ntap * I;  // output row width: ntap blocks of I columns
+  const int ncb = (TI + IC - 1) / IC;
+  // chunk_fast: blockIdx.x = output chunk (fastest in dispatch order: the chunks of one row
+  // range run together and share its g / x rows through L2 / MALL), blockIdx.y = row range
+  const int chunk = chunk_fast ? blockIdx.x : blockIdx.y;
+  const int part = chunk_fast ? blockIdx.y : blockIdx.x;
+  const int o0 = (chunk / ncb) * OC, i0 = (chunk % ncb) * IC;
+  const int r0 = part * rows_per_part, r1 = min(N, r0 + rows_per_part);
   f32x4 acc[MBC][CBC];
 #pragma unroll
   for (int mb = 0; mb < MBC; ++mb)
@@ -98,7 +118,8 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
   for (int rs = r0; rs < r1; rs += R) {
     __syncthreads();  // previous stage's reads done
     stage<OC, GVEC>(gt, g, rs, r1, o0, O, tid);
-    stage<IC, true>(xt, x, rs, r1, i0, I, tid, xshift, N);
+    if (xs.ntap == 1) stage<IC, true>(xt, x, rs, r1, i0, I, tid);
+    else stage_taps(xt, x, rs, r1, i0, I, TI, xs, N, tid);
     __syncthreads();
     const int nk = (min(R, r1 - rs) + 31) >> 5;
     for (int kb = wave; kb < nk; kb += kThreads / 64) {
@@ -141,11 +162,10 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
     }
     __syncthreads();
   }
-  const int TI = xs.ntap * I;  // output row width
-  float* out = partial + (size_t)blockIdx.x * O * TI + (size_t)tap * I;
+  float* out = partial + (size_t)part * O * TI;
   for (int e = tid; e < OC * IC; e += kThreads) {
     const int o = o0 + e / IC, i = i0 + e % IC;
-    if (o < O && i < I) out[(size_t)o * TI + i] = red[e];
+    if (o < O && i < TI) out[(size_t)o * TI + i] = red[e];
   }
 }
 
@@ -286,13 +306,21 @@ int fc_wgrad_impl(const void* g, const void* x, int N, int O, int I, const XShif
   if (N <= 0 || O <= 0 || I <= 0 || nparts < 1 || I % 8) return (int)hipErrorInvalidValue;
   const int stages = (N + R - 1) / R;
   const int rpp = ((stages + nparts - 1) / nparts) * R;
-  const int chunks = ((O + OC - 1) / OC) * ((I + IC - 1) / IC) * xs.ntap;
+  const int chunks = ((O + OC - 1) / OC) * ((xs.ntap * I + IC - 1) / IC);
+  // dispatch order: chunk-fastest for the shifted (conv) form, whose chunks re-read the same
+  // rows; MBK_WGRAD_ORDER=chunk|part overrides (A/B knob)
+  static const int order = [] {
+    const char* e = getenv("MBK_WGRAD_ORDER");
+    return e ? (e[0] == 'c' ? 1 : 0) : -1;
+  }();
+  const int cf = order >= 0 ? order : (xs.ntap > 1 ? 1 : 0);
+  const dim3 grid = cf ? dim3(chunks, nparts) : dim3(nparts, chunks);
   if (O % 8 == 0)
-    hipLaunchKernelGGL(fc_wgrad_kernel<true>, dim3(nparts, chunks), dim3(kThreads), 0, stream,
-                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial, xs);
+    hipLaunchKernelGGL(fc_wgrad_kernel<true>, grid, dim3(kThreads), 0, stream, (const bf16*)g,
+                       (const bf16*)x, N, O, I, rpp, partial, xs, cf);
   else  // e.g. the critic, O = 1
-    hipLaunchKernelGGL(fc_wgrad_kernel<false>, dim3(nparts, chunks), dim3(kThreads), 0, stream,
-                       (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial, xs);
+    hipLaunchKernelGGL(fc_wgrad_kernel<false>, grid, dim3(kThreads), 0, stream, (const bf16*)g,
+                       (const bf16*)x, N, O, I, rpp, partial, xs, cf);
   const long row = (long)O * I * xs.ntap;
   const unsigned cols = (unsigned)((row + 63) / 64);
   constexpr int kPps = 32;

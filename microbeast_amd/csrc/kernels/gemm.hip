@@ -7,7 +7,8 @@
 // gradient (g^T x, K = batch) is the split-K kernel in fc.hip.
 //
 // Tiling: 128 x 128 output tile per 256-thread workgroup (4 waves as 2 x 2, each 64 x 64 =
-// 4 x 4 MFMA tiles), K step 32, A / B tiles double-buffered in LDS with a 16-byte row pad
+// 4 x 4 MFMA tiles), or 256 x 64 / 256 x 32 for narrow N (GridNet's 32 / 64-channel layers;
+// waves stacked along M), K step 32, A / B tiles double-buffered in LDS with a 16-byte row pad
 // (conflict-free ds_read_b128 of the 8-element fragments). Global loads for step k+1 are
 // issued before the MFMAs of step k. Edges are zero-filled, so any M, N and K % 8 == 0 work.
 // blockIdx.x walks M (the large dimension in every use) and XCD-interleaves nothing: the
@@ -23,7 +24,7 @@ typedef __hip_bfloat16 bf16;
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int TM = 128, TN = 128, TK = 32;
+constexpr int TK = 32;
 constexpr int ROWB = TK * 2 + 16;  // LDS row stride (bytes): 32 bf16 + pad
 
 union Frag8 {
@@ -31,16 +32,23 @@ union Frag8 {
   uint4 u;
 };
 
-// one 128 x 32 bf16 tile = 512 uint4; each thread moves 2
+// K step TK of a ROWS-row tile = ROWS * 4 uint4; thread e moves elements e, e + 256, ...
+template <int ROWS>
+struct TileRegs {
+  static constexpr int kN = (ROWS * 4 + kThreads - 1) / kThreads;
+  uint4 r[kN];
+};
+
+template <int ROWS>
 __device__ __forceinline__ void load_tile(const bf16* __restrict__ g, int rows, int ld, int r0,
-                                          int k0, int K, uint4 r[2]) {
+                                          int k0, int K, TileRegs<ROWS>& t) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < TileRegs<ROWS>::kN; ++j) {
     const int e = threadIdx.x + j * kThreads;
     const int row = e >> 2, q = e & 3;
     const int gr = r0 + row, gk = k0 + q * 8;
-    r[j] = (gr < rows && gk < K) ? *(const uint4*)(g + (size_t)gr * ld + gk)
-                                 : make_uint4(0, 0, 0, 0);
+    t.r[j] = (row < ROWS && gr < rows && gk < K) ? *(const uint4*)(g + (size_t)gr * ld + gk)
+                                                 : make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -54,78 +62,100 @@ struct ATaps {
   const bf16* base[kMaxTaps];
   int shift[kMaxTaps];
   int ntap, tk;
+  // Output row remap (remap != 0): rows m = (b * Hp + y) * Wp + x of the padded input grid;
+  // border rows are dropped, interior rows go to output row
+  // b * ob + ((y - 1) * sy + oy0) * ow + (x - 1) * sx + ox0 -- a plain or padded NHWC
+  // output, or one stride-2 phase of a transposed conv's output, with no crop / scatter copy.
+  int remap, Hp, Wp, ob, ow, sy, sx, oy0, ox0;
 };
 
+template <int ROWS>
 __device__ __forceinline__ void load_tile_taps(const ATaps& t, int rows, int ld, int r0, int k0,
-                                               uint4 r[2]) {
+                                               TileRegs<ROWS>& tr) {
   const int tap = k0 / t.tk, kin = k0 - tap * t.tk;
   const bf16* g = t.base[tap];
   const int sh = t.shift[tap];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+  for (int j = 0; j < TileRegs<ROWS>::kN; ++j) {
     const int e = threadIdx.x + j * kThreads;
     const int row = e >> 2, q = e & 3;
     const int gr = r0 + row + sh;
-    r[j] = (gr >= 0 && gr < rows && tap < t.ntap)
-               ? *(const uint4*)(g + (size_t)gr * ld + kin + q * 8)
-               : make_uint4(0, 0, 0, 0);
-  }
-}
-__device__ __forceinline__ void store_tile(char* t, const uint4 r[2]) {
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int e = threadIdx.x + j * kThreads;
-    *(uint4*)(t + (e >> 2) * ROWB + (e & 3) * 16) = r[j];
+    tr.r[j] = (row < ROWS && gr >= 0 && gr < rows && tap < t.ntap)
+                  ? *(const uint4*)(g + (size_t)gr * ld + kin + q * 8)
+                  : make_uint4(0, 0, 0, 0);
   }
 }
 
-template <bool OUT_BF16, bool TAPS>
+template <int ROWS>
+__device__ __forceinline__ void store_tile(char* t, const TileRegs<ROWS>& tr) {
+#pragma unroll
+  for (int j = 0; j < TileRegs<ROWS>::kN; ++j) {
+    const int e = threadIdx.x + j * kThreads;
+    if (e < ROWS * 4) *(uint4*)(t + (e >> 2) * ROWB + (e & 3) * 16) = tr.r[j];
+  }
+}
+
+// Tile shapes: TN = 128 -> 128 x 128 tile, waves 2 x 2 of 64 x 64; TN = 64 / 32 (GridNet's
+// narrow layers) -> 256 x TN tile, waves stacked along M, 64 x TN each, so no MFMA work is
+// spent on padding columns.
+template <int TN_>
+struct Shape {
+  static constexpr int TM = TN_ == 128 ? 128 : 256;
+  static constexpr int WN = TN_ == 128 ? 2 : 1;  // waves along N
+  static constexpr int NJ = TN_ / WN / 16;      // 16-col MFMA tiles per wave
+};
+
+template <bool OUT_BF16, bool TAPS, int TN_>
 __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int relu,
     int accumulate, ATaps taps) {
-  __shared__ __attribute__((aligned(16))) char sm[2][2][TM * ROWB];  // [buf][A|B]
+  using S = Shape<TN_>;
+  constexpr int TM_ = S::TM, NJ = S::NJ;
+  __shared__ __attribute__((aligned(16))) char sa[2][TM_ * ROWB];
+  __shared__ __attribute__((aligned(16))) char sb[2][TN_ * ROWB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves of 64 x 64
-  const int m0 = blockIdx.x * TM, n0 = blockIdx.y * TN;
-  f32x4 acc[4][4];
+  const int wm = wave / S::WN, wn = wave % S::WN;
+  const int m0 = blockIdx.x * TM_, n0 = blockIdx.y * TN_;
+  f32x4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  uint4 ra[2], rb[2];
-  if (TAPS) load_tile_taps(taps, M, lda, m0, 0, ra);
-  else load_tile(A, M, lda, m0, 0, K, ra);
-  load_tile(B, N, ldb, n0, 0, K, rb);
-  store_tile(sm[0][0], ra);
-  store_tile(sm[0][1], rb);
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  TileRegs<TM_> ra;
+  TileRegs<TN_> rb;
+  if (TAPS) load_tile_taps<TM_>(taps, M, lda, m0, 0, ra);
+  else load_tile<TM_>(A, M, lda, m0, 0, K, ra);
+  load_tile<TN_>(B, N, ldb, n0, 0, K, rb);
+  store_tile<TM_>(sa[0], ra);
+  store_tile<TN_>(sb[0], rb);
   __syncthreads();
   const int nk = (K + TK - 1) / TK;
   for (int kk = 0; kk < nk; ++kk) {
     const int cur = kk & 1;
     if (kk + 1 < nk) {  // prefetch the next K step into registers
-      if (TAPS) load_tile_taps(taps, M, lda, m0, (kk + 1) * TK, ra);
-      else load_tile(A, M, lda, m0, (kk + 1) * TK, K, ra);
-      load_tile(B, N, ldb, n0, (kk + 1) * TK, K, rb);
+      if (TAPS) load_tile_taps<TM_>(taps, M, lda, m0, (kk + 1) * TK, ra);
+      else load_tile<TM_>(A, M, lda, m0, (kk + 1) * TK, K, ra);
+      load_tile<TN_>(B, N, ldb, n0, (kk + 1) * TK, K, rb);
     }
-    const char* ta = sm[cur][0];
-    const char* tb = sm[cur][1];
-    Frag8 fa[4], fb[4];
+    const char* ta = sa[cur];
+    const char* tb = sb[cur];
+    Frag8 fa[4], fb[NJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       fa[i].u = *(const uint4*)(ta + (wm * 64 + i * 16 + li) * ROWB + g * 16);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      fb[j].u = *(const uint4*)(tb + (wn * 64 + j * 16 + li) * ROWB + g * 16);
+    for (int j = 0; j < NJ; ++j)
+      fb[j].u = *(const uint4*)(tb + (wn * NJ * 16 + j * 16 + li) * ROWB + g * 16);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, fb[j].v, acc[i][j], 0, 0, 0);
     if (kk + 1 < nk) {
-      store_tile(sm[cur ^ 1][0], ra);
-      store_tile(sm[cur ^ 1][1], rb);
+      store_tile<TM_>(sa[cur ^ 1], ra);
+      store_tile<TN_>(sb[cur ^ 1], rb);
     }
     __syncthreads();
   }
@@ -133,17 +163,24 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = n0 + wn * 64 + j * 16 + li;
-      if (col >= N) continue;
-      const float bv = bias ? bias[col] : 0.f;
+    for (int r = 0; r < 4; ++r) {
+      const int row = m0 + wm * 64 + i * 16 + 4 * g + r;
+      if (row >= M) continue;
+      size_t orow = row;
+      if (TAPS && taps.remap) {
+        const int x = row % taps.Wp, t = row / taps.Wp;
+        const int y = t % taps.Hp, b = t / taps.Hp;
+        if (y == 0 || y == taps.Hp - 1 || x == 0 || x == taps.Wp - 1) continue;
+        orow = (size_t)b * taps.ob + (size_t)((y - 1) * taps.sy + taps.oy0) * taps.ow +
+               (x - 1) * taps.sx + taps.ox0;
+      }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * 64 + i * 16 + 4 * g + r;
-        if (row >= M) continue;
-        float v = acc[i][j][r] + bv;
+      for (int j = 0; j < NJ; ++j) {
+        const int col = n0 + wn * NJ * 16 + j * 16 + li;
+        if (col >= N) continue;
+        float v = acc[i][j][r] + (bias ? bias[col] : 0.f);
         if (relu) v = fmaxf(v, 0.f);
-        const size_t o = (size_t)row * ldc + col;
+        const size_t o = orow * ldc + col;
         if (OUT_BF16) {
           ((bf16*)C)[o] = __float2bfloat16(v);
         } else {
@@ -152,6 +189,34 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
         }
       }
     }
+}
+
+template <bool TAPS, int TN_>
+void launch(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
+            int lda, int ldb, int ldc, int relu, int out_bf16, int accumulate, const ATaps& t,
+            hipStream_t stream) {
+  dim3 grid((M + Shape<TN_>::TM - 1) / Shape<TN_>::TM, (N + TN_ - 1) / TN_);
+  if (out_bf16)
+    hipLaunchKernelGGL((gemm_nt_kernel<true, TAPS, TN_>), grid, dim3(kThreads), 0, stream,
+                       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, 0,
+                       t);
+  else
+    hipLaunchKernelGGL((gemm_nt_kernel<false, TAPS, TN_>), grid, dim3(kThreads), 0, stream,
+                       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu,
+                       accumulate, t);
+}
+
+// narrowest tile that covers N (N = 78 -> one 128-wide tile rather than two of 64)
+template <bool TAPS>
+void launch_any(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
+                int lda, int ldb, int ldc, int relu, int out_bf16, int accumulate,
+                const ATaps& t, hipStream_t stream) {
+  if (N <= 32)
+    launch<TAPS, 32>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
+  else if (N <= 64)
+    launch<TAPS, 64>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
+  else
+    launch<TAPS, 128>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
 }
 
 }  // namespace
@@ -163,26 +228,20 @@ extern "C" int mbk_gemm_nt(const void* A, const void* B, void* C, const float* b
                            int accumulate, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % 8 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
-  dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN);
   ATaps none{};
-  if (out_bf16)
-    hipLaunchKernelGGL((gemm_nt_kernel<true, false>), grid, dim3(kThreads), 0, stream,
-                       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, 0,
-                       none);
-  else
-    hipLaunchKernelGGL((gemm_nt_kernel<false, false>), grid, dim3(kThreads), 0, stream,
-                       (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu,
-                       accumulate, none);
+  launch_any<false>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, none,
+                    stream);
   return (int)hipGetLastError();
 }
 
 // Shifted-row ("implicit im2col") GEMM: C[M][N] = sum_t A_t[m + shift_t][:] . B[:, t*tk ...]^T
 // A_t: bases[t] [M][lda] bf16 (rows outside [0, M) read as zero), tk % 32 == 0,
 // B: [N][ntap*tk] bf16 (tap-major K).
+// remap: null, or 8 ints {Hp, Wp, ob, ow, sy, sx, oy0, ox0} (see ATaps)
 extern "C" int mbk_gemm_nt_taps(const void* const* bases, const int* shifts, int ntap, int tk,
                                 const void* B, void* C, const float* bias, int M, int N, int lda,
                                 int ldb, int ldc, int relu, int out_bf16, int accumulate,
-                                hipStream_t stream) {
+                                const int* remap, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (ntap < 1 || ntap > kMaxTaps || tk % 32 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
   ATaps t{};
@@ -192,15 +251,12 @@ extern "C" int mbk_gemm_nt_taps(const void* const* bases, const int* shifts, int
   }
   t.ntap = ntap;
   t.tk = tk;
-  const int K = ntap * tk;
-  dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN);
-  if (out_bf16)
-    hipLaunchKernelGGL((gemm_nt_kernel<true, true>), grid, dim3(kThreads), 0, stream,
-                       (const bf16*)nullptr, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc,
-                       relu, 0, t);
-  else
-    hipLaunchKernelGGL((gemm_nt_kernel<false, true>), grid, dim3(kThreads), 0, stream,
-                       (const bf16*)nullptr, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc,
-                       relu, accumulate, t);
+  if (remap) {
+    t.remap = 1;
+    t.Hp = remap[0], t.Wp = remap[1], t.ob = remap[2], t.ow = remap[3];
+    t.sy = remap[4], t.sx = remap[5], t.oy0 = remap[6], t.ox0 = remap[7];
+  }
+  launch_any<true>(nullptr, B, C, bias, M, N, ntap * tk, lda, ldb, ldc, relu, out_bf16,
+                   accumulate, t, stream);
   return (int)hipGetLastError();
 }

@@ -9,14 +9,17 @@ more HBM traffic than the MFMA work itself, so neither is materialised here:
   p = (b, y, x). At every padded position, out[p] = sum_t xp[p + s_t] . W_t with
   s_t = (ky-1)*(W+2) + (kx-1). That is ONE GEMM whose A operand reads, for the K block of
   tap t, rows shifted by s_t (``mbk_gemm_nt_taps``, gemm.hip). Bias and relu are fused in
-  the epilogue, and the interior is cropped. Border outputs are computed and thrown away
-  (1.27x work at 16x16). In exchange, no A operand is ever materialised.
+  the epilogue, whose row remap writes only interior rows, straight to their NHWC
+  position. Border outputs are computed but never stored (1.27x work at 16x16). In
+  exchange, no A operand is ever materialised.
 * ``conv_transpose3x3s2``: output pixel (2j+a, 2i+b) gets taps from input rows j / j+1
   only (sub-pixel decomposition). Each of the 4 phases (a, b) is a shifted-row GEMM of
-  1, 2, 2 or 4 taps, written straight into the strided phase of the NHWC output.
+  1, 2, 2 or 4 taps, whose epilogue remap writes the phase's stride-2 pixels of the NHWC
+  output directly (no scatter copy).
 * Backward: dX is one more shifted-row GEMM with negated shifts (all 9 taps, for the
   transposed conv across the 4 phase gradients). dW is the split-K kernel of fc.hip with
-  shifted x rows (``mbk_fc_wgrad_taps``), all taps in one launch. db is a column sum.
+  shifted x rows (``mbk_fc_wgrad_taps``): all taps in one launch, with column chunks that
+  span taps, so 32-channel layers fill whole 64-wide tiles. db is a column sum.
 
 Channel counts are zero-padded to multiples of 32, so a 32-wide K step never straddles
 two taps. Off-GPU, the same shifted-row maths runs in plain torch (``_taps_gemm_ref`` /
@@ -43,8 +46,11 @@ def _pad_grid(x: torch.Tensor, cp: int) -> torch.Tensor:
     return F.pad(x.to(_BF), (0, cp - C, 1, 1, 1, 1)).reshape(B * (H + 2) * (W + 2), cp)
 
 
-def _crop(yf: torch.Tensor, B: int, H: int, W: int) -> torch.Tensor:
-    return yf.view(B, H + 2, W + 2, -1)[:, 1:H + 1, 1:W + 1, :]
+def _dx(B, H, W, cp, C, bases, shifts, bm):
+    """input gradient [B, H, W, C] from a shifted-row GEMM over the padded gradient grid"""
+    dx = torch.empty(B, H, W, cp, dtype=_BF, device=bm.device)
+    taps_gemm(bases, shifts, bm, out=dx.view(-1, cp), remap=(H + 2, W + 2, H * W, W, 1, 1, 0, 0))
+    return dx if C == cp else dx[..., :C].contiguous()
 
 
 # ----------------------------------------------------------------------------- launchers
@@ -58,7 +64,19 @@ def _shift_rows(a: torch.Tensor, s: int) -> torch.Tensor:
     return out
 
 
-def _taps_gemm_ref(bases, shifts, b, bias, relu, out_dtype):
+def _remap_index(M, remap, device):
+    """(src rows, dst rows) of the epilogue row remap (gemm.hip ATaps): interior rows of the
+    padded grid -> b*ob + ((y-1)*sy + oy0)*ow + (x-1)*sx + ox0."""
+    Hp, Wp, ob, ow, sy, sx, oy0, ox0 = remap
+    m = torch.arange(M, device=device)
+    x, t = m % Wp, m // Wp
+    y, b = t % Hp, t // Hp
+    keep = (y > 0) & (y < Hp - 1) & (x > 0) & (x < Wp - 1)
+    m, x, y, b = m[keep], x[keep], y[keep], b[keep]
+    return m, b * ob + ((y - 1) * sy + oy0) * ow + (x - 1) * sx + ox0
+
+
+def _taps_gemm_ref(bases, shifts, b, bias, relu, out_dtype, out=None, remap=None):
     tk = bases[0].shape[1]
     acc = None
     for t, (a, s) in enumerate(zip(bases, shifts)):
@@ -68,29 +86,47 @@ def _taps_gemm_ref(bases, shifts, b, bias, relu, out_dtype):
         acc = acc + bias.float()
     if relu:
         acc = acc.clamp_min(0)
-    return acc.to(out_dtype)
+    if remap is None:
+        if out is None:
+            return acc.to(out_dtype)
+        out.copy_(acc)
+        return out
+    src, dst = _remap_index(acc.shape[0], remap, acc.device)
+    out[dst] = acc[src].to(out.dtype)
+    return out
 
 
-def taps_gemm(bases, shifts, b, bias=None, relu=False, out_dtype=_BF):
+def taps_gemm(bases, shifts, b, bias=None, relu=False, out_dtype=_BF, out=None, remap=None):
     """C[M, N] = sum_t A_t[m + shift_t] . B[:, t*tk:(t+1)*tk]^T (+bias)(+relu).
-    bases: list of [M, tk] bf16 (contiguous, tk % 32 == 0); b: [N, ntap*tk] bf16."""
+    bases: list of [M, tk] bf16 (contiguous, tk % 32 == 0); b: [N, ntap*tk] bf16.
+    remap (Hp, Wp, ob, ow, sy, sx, oy0, ox0): write only the interior rows of the padded
+    grid, each to its output row (see gemm.hip ATaps); ``out`` is then required
+    ([rows, N] with unit column stride)."""
     M, tk = bases[0].shape
     assert tk % 32 == 0 and b.shape[1] == len(bases) * tk and len(bases) <= 9
+    assert remap is None or out is not None
     if not b.is_cuda:
-        return _taps_gemm_ref(bases, shifts, b, bias, relu, out_dtype)
+        return _taps_gemm_ref(bases, shifts, b, bias, relu, out_dtype, out, remap)
     from .. import _native as N
     for a in bases:
         assert a.shape == (M, tk) and a.is_contiguous() and a.dtype == _BF
     b = b.to(_BF).contiguous()
-    out = torch.empty(M, b.shape[0], dtype=out_dtype, device=b.device)
+    if out is None:
+        out = torch.empty(M, b.shape[0], dtype=out_dtype, device=b.device)
+    assert out.stride(-1) == 1 and out.shape[-1] == b.shape[0]
+    if remap is not None:
+        Hp, Wp, ob, ow, sy, sx, oy0, ox0 = remap
+        last = (M // (Hp * Wp) - 1) * ob + ((Hp - 3) * sy + oy0) * ow + (Wp - 3) * sx + ox0
+        assert M % (Hp * Wp) == 0 and last < out.shape[0], "remap writes out of bounds"
     ptrs = (ctypes.c_void_p * 9)(*[a.data_ptr() for a in bases])
     sh = (ctypes.c_int * 9)(*shifts)
+    rm = (ctypes.c_int * 8)(*remap) if remap is not None else None
     if bias is not None:
         bias = bias.float().contiguous()
     N.check(N.kernels().mbk_gemm_nt_taps(ptrs, sh, len(bases), tk, b.data_ptr(),
                                          out.data_ptr(), N.ptr(bias), M, b.shape[0], tk,
-                                         b.shape[1], b.shape[0], int(relu),
-                                         int(out_dtype == _BF), 0, N.stream_ptr()),
+                                         b.shape[1], out.stride(-2), int(relu),
+                                         int(out.dtype == _BF), 0, rm, N.stream_ptr()),
             "gemm_nt_taps")
     return out
 
@@ -136,8 +172,9 @@ class _Conv3x3(torch.autograd.Function):
         wk = F.pad(w.detach(), (0, 0, 0, 0, 0, cp - Cw)).permute(0, 2, 3, 1)
         wk = wk.reshape(Cout, 9 * cp).to(_BF).contiguous()  # tap-major K (ky, kx, ci)
         sh = _conv_shifts(W)
-        yf = taps_gemm([xp] * 9, sh, wk, b.detach() if b is not None else None, relu)
-        y = _crop(yf, B, H, W).contiguous()
+        y = torch.empty(B, H, W, Cout, dtype=_BF, device=x.device)
+        taps_gemm([xp] * 9, sh, wk, b.detach() if b is not None else None, relu,
+                  out=y.view(-1, Cout), remap=(H + 2, W + 2, H * W, W, 1, 1, 0, 0))
         ctx.save_for_backward(xp, wk, y if relu else None)
         ctx.meta = (B, H, W, C, Cw, cp, relu, b is not None, w.dtype)
         return y
@@ -158,8 +195,7 @@ class _Conv3x3(torch.autograd.Function):
             # dxp[q] = sum_t g[q - s_t] . W_t : B operand [cp, 9*cop], block t = W_t^T
             wt = wk.view(Cout, 9, cp).permute(2, 1, 0)  # [cp, 9, Cout]
             wt = F.pad(wt, (0, cop - Cout)).reshape(cp, 9 * cop).contiguous()
-            dxf = taps_gemm([gp] * 9, [-s for s in sh], wt)
-            gx = _crop(dxf, B, H, W)[..., :C].contiguous()
+            gx = _dx(B, H, W, cp, C, [gp] * 9, [-s for s in sh], wt)
         if ctx.needs_input_grad[1]:
             dw = taps_wgrad(gp, xp, sh)[:Cout]  # [Cout, 9*cp]
             gw = dw.view(Cout, 3, 3, cp).permute(0, 3, 1, 2)[:, :Cw].contiguous().to(wdt)
@@ -208,8 +244,8 @@ class _ConvT3x3s2(torch.autograd.Function):
         bias = b.detach() if b is not None else None
         for a, bb, taps in _phase_taps(W):
             bm = torch.cat([wb[:, :, ky, kx].t() for ky, kx, _ in taps], dim=1).contiguous()
-            yf = taps_gemm([xp] * len(taps), [s for _, _, s in taps], bm, bias, relu)
-            y[:, a::2, bb::2, :] = _crop(yf, B, H, W)
+            taps_gemm([xp] * len(taps), [s for _, _, s in taps], bm, bias, relu,
+                      out=y.view(-1, Cout), remap=(H + 2, W + 2, 4 * H * W, 2 * W, 2, 2, a, bb))
         ctx.save_for_backward(xp, wb, y if relu else None)
         ctx.meta = (B, H, W, Cin, cip, relu, b is not None, w.dtype)
         return y
@@ -234,8 +270,7 @@ class _ConvT3x3s2(torch.autograd.Function):
                     bases.append(gp)
                     shifts.append(-s)
                     blocks.append(F.pad(wb[:, :, ky, kx], (0, cop - Cout)))  # [cip, cop]
-            dxf = taps_gemm(bases, shifts, torch.cat(blocks, dim=1).contiguous())
-            gx = _crop(dxf, B, H, W)[..., :Cin].contiguous()
+            gx = _dx(B, H, W, cip, Cin, bases, shifts, torch.cat(blocks, dim=1).contiguous())
         if ctx.needs_input_grad[1]:
             gw = torch.zeros(cip, Cout, 3, 3, dtype=torch.float32, device=g.device)
             for gp, (_, _, taps) in zip(gps, phases):

@@ -44,9 +44,10 @@ class _Linear(torch.autograd.Function):
         wc = w.to(x.dtype)
         ctx.save_for_backward(x, wc)
         ctx.w_dtype = w.dtype
-        if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
-            from .gemm import gemm_nt_raw  # hand-written MFMA GEMM (gemm.hip)
-            return gemm_nt_raw(x.contiguous(), wc.contiguous(), b)
+        if x.is_cuda and x.dtype == torch.bfloat16:
+            from .gemm import gemm_nt_raw  # hand-written MFMA GEMM (gemm.hip; pads K % 8)
+            return gemm_nt_raw(x.reshape(-1, x.shape[-1]), wc.contiguous(),
+                               b).view(*x.shape[:-1], wc.shape[0])
         return torch.nn.functional.linear(x, wc, b.to(x.dtype) if b is not None else None)
 
     @staticmethod
@@ -55,9 +56,10 @@ class _Linear(torch.autograd.Function):
         g = g.contiguous()
         gx = None
         if ctx.needs_input_grad[0]:
-            if g.is_cuda and g.dtype == torch.bfloat16 and wc.shape[0] % 8 == 0:
-                from .gemm import gemm_nt_raw
-                gx = gemm_nt_raw(g, wc.t().contiguous())
+            if g.is_cuda and g.dtype == torch.bfloat16:
+                from .gemm import gemm_nt_raw  # K = out_features (1 for the critic): padded
+                gx = gemm_nt_raw(g.reshape(-1, g.shape[-1]), wc.t().contiguous())
+                gx = gx.view(*g.shape[:-1], wc.shape[1])
             else:
                 gx = g @ wc
         gw = weight_grad(g, x).to(ctx.w_dtype) if ctx.needs_input_grad[1] else None
@@ -78,5 +80,8 @@ def linear(x: torch.Tensor, layer: torch.nn.Linear, dtype=torch.bfloat16,
     """``layer(x)`` computed in ``dtype`` with the split-K weight gradient.
     cached: (weight, bias) already converted (inference with prepacked weights)."""
     if cached is not None:
+        if x.is_cuda and dtype == torch.bfloat16:
+            from .gemm import gemm_nt_raw
+            return gemm_nt_raw(x.to(dtype).reshape(-1, x.shape[-1]), cached[0], cached[1])
         return torch.nn.functional.linear(x.to(dtype), cached[0], cached[1])
     return _Linear.apply(x.to(dtype), nhwc_weight(layer.weight, nhwc), layer.bias)

@@ -10,7 +10,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 256, 128), (257, 77, 40), (5, 1, 256), (4096, 384, 288),
-                                   (130, 130, 8)])
+                                   (130, 130, 8), (1000, 32, 64), (700, 64, 96), (513, 20, 32),
+                                   (300, 40, 288)])
 def test_gemm_nt_forward(cuda, M, N, K):
     from microbeast_amd.ops.gemm import gemm_nt_raw
     torch.manual_seed(M + N + K)
