@@ -756,49 +756,76 @@ __global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16* __restrict__ 
   }
 }
 
-// dc[n][y][x][c..c+7] = sum of dp over the (<= 4) windows whose stored argmax is (y, x)
+// dc[n][y][x][c..c+7] = sum of dp over the (<= 4) windows whose stored argmax is (y, x).
+// One thread per (image, 2x2 input block, 8 channels): the block's pixels are fed only by
+// windows (oy, ox) in {j, j+1} x {k, k+1}, so four 24-byte window loads cover four
+// pixels and the tap each window must match is a compile-time constant. 32-bit index
+// math (the host splits launches that would overflow it).
+template <int C>
 __global__ __launch_bounds__(256) void pool_bwd_idx_kernel(const uint8_t* __restrict__ pidx,
                                                            const bf16* __restrict__ dp, int N,
-                                                           int H, int W, int C,
+                                                           int H, int W,
                                                            bf16* __restrict__ dc) {
+  constexpr int C8 = C / 8;
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-  const int C8 = C / 8;
-  const size_t tot = (size_t)N * H * W * C8;
-  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < tot;
-       e += (size_t)gridDim.x * blockDim.x) {
+  const uint32_t tot = (uint32_t)N * Ho * Wo * C8;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
     const int c8 = e % C8;
-    const size_t p = e / C8;
-    const int x = p % W, y = (p / W) % H;
-    const size_t n = p / ((size_t)H * W);
-    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int oy = max(0, y / 2 - 1); oy <= min(Ho - 1, (y + 1) / 2); ++oy) {
-      const int ky = y - (2 * oy - 1);
-      if (ky < 0 || ky > 2) continue;
-      for (int ox = max(0, x / 2 - 1); ox <= min(Wo - 1, (x + 1) / 2); ++ox) {
-        const int kx = x - (2 * ox - 1);
-        if (kx < 0 || kx > 2) continue;
-        const uint8_t me = (uint8_t)(ky * 3 + kx);
-        const size_t q = ((n * Ho + oy) * Wo + ox) * C + c8 * 8;
-        const uint2 ids = *(const uint2*)(pidx + q);
-        const uint4 dv = *(const uint4*)(dp + q);
-        const uint32_t iw[2] = {ids.x, ids.y};
-        const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
+    uint32_t q = e / C8;
+    const int k = q % Wo;
+    q /= Wo;
+    const int j = q % Ho;
+    const uint32_t n = q / Ho;
+    uint32_t ids[2][2][2];
+    uint32_t dv[2][2][4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint8_t id = (uint8_t)(iw[j >> 2] >> (8 * (j & 3)));
-          const uint32_t hb = (dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-          if (id == me) g[j] += __uint_as_float(hb << 16);
+    for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+      for (int dk = 0; dk < 2; ++dk) {
+        const int oy = j + dj, ox = k + dk;
+        if (oy < Ho && ox < Wo) {
+          const uint32_t o = ((n * Ho + oy) * Wo + ox) * C + c8 * 8;
+          const uint2 iv = *(const uint2*)(pidx + o);
+          const uint4 d = *(const uint4*)(dp + o);
+          ids[dj][dk][0] = iv.x; ids[dj][dk][1] = iv.y;
+          dv[dj][dk][0] = d.x; dv[dj][dk][1] = d.y; dv[dj][dk][2] = d.z; dv[dj][dk][3] = d.w;
+        } else {  // tap id 0xFF never matches
+          ids[dj][dk][0] = ids[dj][dk][1] = 0xFFFFFFFFu;
+          dv[dj][dk][0] = dv[dj][dk][1] = dv[dj][dk][2] = dv[dj][dk][3] = 0u;
         }
       }
-    }
-    uint32_t o[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t lo = __bfloat16_as_ushort(f2bf(g[2 * j]));
-      const uint32_t hi = __bfloat16_as_ushort(f2bf(g[2 * j + 1]));
-      o[j] = lo | (hi << 16);
-    }
-    *(uint4*)(dc + p * C + c8 * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int y = 2 * j + a, x = 2 * k + b;
+        if (y >= H || x >= W) continue;
+        float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        // window (j+dj, k+dk) sees this pixel at tap (a+1-2dj, b+1-2dk) when in [0, 2]
+#pragma unroll
+        for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+          for (int dk = 0; dk < 2; ++dk) {
+            const int ky = a + 1 - 2 * dj, kx = b + 1 - 2 * dk;
+            if (ky < 0 || kx < 0) continue;
+            const uint32_t me = (uint32_t)(ky * 3 + kx);
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+              const uint32_t id = (ids[dj][dk][t >> 2] >> (8 * (t & 3))) & 0xFFu;
+              const uint32_t hb = (dv[dj][dk][t >> 1] >> (16 * (t & 1))) & 0xFFFFu;
+              if (id == me) g[t] += __uint_as_float(hb << 16);
+            }
+          }
+        uint32_t o[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          const uint32_t lo = __bfloat16_as_ushort(f2bf(g[2 * t]));
+          const uint32_t hi = __bfloat16_as_ushort(f2bf(g[2 * t + 1]));
+          o[t] = lo | (hi << 16);
+        }
+        *(uint4*)(dc + ((size_t)(n * H + y) * W + x) * C + c8 * 8) =
+            make_uint4(o[0], o[1], o[2], o[3]);
+      }
   }
 }
 
@@ -1115,12 +1142,26 @@ extern "C" int mbk_pool_bwd(const void* cfull, const void* dp, int N, int H, int
 
 extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, int W, int C,
                                 void* dc, hipStream_t stream) {
-  if (C % 8) return (int)hipErrorInvalidValue;
-  const size_t tot = (size_t)N * H * W * (C / 8);
-  size_t blocks = (tot + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(pool_bwd_idx_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
-                     (const uint8_t*)pidx, (const bf16*)dp, N, H, W, C, (bf16*)dc);
+  if (C != 16 && C != 32) return (int)hipErrorInvalidValue;
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  const size_t per_img_in = (size_t)H * W * C, per_img_out = (size_t)Ho * Wo * C;
+  // keep every 32-bit index of one launch (input elements) below 2^31
+  const int chunk = (int)std::max<size_t>(1, ((size_t)1 << 31) / per_img_in - 1);
+  for (int n0 = 0; n0 < N; n0 += chunk) {
+    const int n = std::min(chunk, N - n0);
+    const size_t tot = (size_t)n * Ho * Wo * (C / 8);
+    size_t blocks = (tot + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    const uint8_t* pi = (const uint8_t*)pidx + n0 * per_img_out;
+    const bf16* d = (const bf16*)dp + n0 * per_img_out;
+    bf16* o = (bf16*)dc + n0 * per_img_in;
+    if (C == 16)
+      hipLaunchKernelGGL(pool_bwd_idx_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, stream, pi,
+                         d, n, H, W, o);
+    else
+      hipLaunchKernelGGL(pool_bwd_idx_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, stream, pi,
+                         d, n, H, W, o);
+  }
   return (int)hipGetLastError();
 }
 

@@ -325,3 +325,29 @@ def test_pool_bwd_fused_into_wgrad_dgrad(cuda, s):
     enc.fused_pool_bwd = False
     for a, b in zip(*grads):
         assert _rel(b.cpu(), a.cpu()) < 1e-4, _rel(b.cpu(), a.cpu())
+
+
+@pytest.mark.parametrize("H,W,C", [(16, 16, 16), (8, 8, 32), (5, 5, 32), (3, 3, 32), (10, 10, 16),
+                                   (12, 12, 32), (6, 6, 32)])
+def test_pool_bwd_idx_shapes(cuda, H, W, C):
+    """Stored-argmax pool backward on odd / even maps and both channel widths vs autograd."""
+    from microbeast_amd import _native as N
+    torch.manual_seed(H * 100 + C)
+    n = 7
+    c = torch.randn(n, C, H, W).bfloat16().float()
+    pr, ir = F.max_pool2d(c, 3, 2, 1, return_indices=True)
+    Ho, Wo = pr.shape[2:]
+    # flat input index -> tap id ky*3+kx of the window (oy, ox)
+    iy, ix = ir // W, ir % W
+    oy = torch.arange(Ho).view(1, 1, Ho, 1)
+    ox = torch.arange(Wo).view(1, 1, 1, Wo)
+    tap = ((iy - (2 * oy - 1)) * 3 + (ix - (2 * ox - 1))).to(torch.uint8)
+    pidx = tap.permute(0, 2, 3, 1).contiguous().to(cuda)
+    dp = torch.randn(n, Ho, Wo, C).bfloat16()
+    dpg = dp.to(cuda)
+    dc = torch.empty(n, H, W, C, dtype=torch.bfloat16, device=cuda)
+    N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dpg.data_ptr(), n, H, W, C,
+                                         dc.data_ptr(), N.stream_ptr()), "pool_bwd_idx")
+    ct = c.clone().requires_grad_(True)
+    F.max_pool2d(ct, 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
+    torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)

@@ -9,6 +9,39 @@ import os
 import sys
 
 
+def busy_report(trace_csv, window_frac=0.5):
+    """GPU busy fraction (union of kernel intervals) over the last ``window_frac`` of the
+    trace span, i.e. the steady state after warm-up, plus the busiest kernels there."""
+    iv = []
+    for r in csv.DictReader(open(trace_csv)):
+        try:
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "?")))
+        except (KeyError, ValueError):
+            continue
+    if not iv:
+        return []
+    iv.sort()
+    t_end = max(e for _, e, _ in iv)
+    t0 = iv[0][0] + int((t_end - iv[0][0]) * (1.0 - window_frac))
+    busy, cur_s, cur_e = 0, None, None
+    for s, e, _ in iv:
+        if e <= t0:
+            continue
+        s = max(s, t0)
+        if cur_e is None or s > cur_e:
+            if cur_e is not None:
+                busy += cur_e - cur_s
+            cur_s, cur_e = s, e
+        else:
+            cur_e = max(cur_e, e)
+    if cur_e is not None:
+        busy += cur_e - cur_s
+    span = t_end - t0
+    return [f"### steady-state window ({os.path.basename(trace_csv)}, last {window_frac:.0%} of span)\n",
+            f"span {span / 1e6:.2f} ms, GPU busy (union of kernels) {busy / 1e6:.2f} ms "
+            f"= {100.0 * busy / max(span, 1):.1f} %\n"]
+
+
 def main():
     d, out = sys.argv[1], sys.argv[2]
     stats = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True))
@@ -29,6 +62,8 @@ def main():
             c = int(r.get("Calls", 0) or 0)
             lines.append(f"| `{name}` | {c} | {t / 1e6:.3f} | {t / max(c, 1) / 1e3:.2f} | {100 * t / max(tot, 1):.1f} |")
         lines.append("")
+    for f in sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)):
+        lines.extend(busy_report(f))
     open(out, "w").write("\n".join(lines) + "\n")
     if "--drop-trace" in sys.argv:
         for f in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True):
