@@ -72,6 +72,9 @@ class Flags:
     groups: int = 2               # gpu runtime: env groups pipelined through the GPU
     envs_per_group: int = 256
     actor_threads: int = 0        # gpu runtime: native env worker threads (0 = auto)
+    actor_inference: str = "auto"  # mono runtime: server (batched policy in the learner
+                                   # process) | local (CPU policy per actor) | auto
+    inference_wait_ms: float = 2.0  # mono runtime server: dynamic-batching window
     seed: int = 1
     nproc_per_node: int = 1       # informative; launch with torchrun for DP
     bucket_mb: float = 8.0

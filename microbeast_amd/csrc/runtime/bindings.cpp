@@ -193,6 +193,16 @@ PYBIND11_MODULE(_mbrt, m) {
         py::arg("ver"), py::arg("src"), py::arg("dst"), py::arg("nbytes"),
         py::arg("max_tries") = 1000);
 
+  // Page-lock an existing host range (e.g. a POSIX shared-memory rollout slot written by
+  // CPU actor processes) so hipMemcpyAsync moves it by DMA instead of staging through a
+  // driver bounce buffer. Returns the hipError_t (0 = registered).
+  m.def("host_register", [](uintptr_t addr, size_t nbytes) -> int {
+    return (int)hipHostRegister(P<void>(addr), nbytes, hipHostRegisterDefault);
+  });
+  m.def("host_unregister", [](uintptr_t addr) -> int {
+    return (int)hipHostUnregister(P<void>(addr));
+  });
+
   // A stream restricted to a subset of CUs (MI355X: 256 CUs in 8 XCDs). Used for the
   // learner so that every `reserve_every`-th CU stays free for the latency-critical
   // policy stream; CU ids are spread so every XCD / shader engine keeps some free.

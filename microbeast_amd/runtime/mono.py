@@ -12,7 +12,11 @@ reference for the native GPU engine. Fixed on the way:
 * the index hand-off is the native shm ring (no pickling / busy spin);
 * a watchdog respawns dead actors and recycles the slot they held; an
   optional fault injector kills actors to exercise it;
-* clean shutdown: rings are closed, actors exit, processes are joined.
+* clean shutdown: rings are closed, actors exit, processes are joined;
+* with a GPU learner (BASELINE config 2) actors send observations to a
+  dynamic-batching policy server in the learner process instead of running a CPU
+  policy each (``runtime/inference.py``), and full slots reach HBM through pinned
+  DMA on a copy stream one batch ahead of the learner (``runtime/staging.py``).
 """
 from __future__ import annotations
 
@@ -30,8 +34,9 @@ from ..utils.buffers import ShmRing, create_buffers, get_batch
 
 def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, full_ring: ShmRing,
                 weights: torch.Tensor, version: torch.Tensor, cur_slot: torch.Tensor,
-                episode_q, seed: int):
-    """Child process: step a vec-env with a CPU copy of the policy, fill slots."""
+                episode_q, seed: int, client=None):
+    """Child process: step a vec-env, fill slots. Actions come from a CPU copy of the
+    policy, or from the learner process's inference server when ``client`` is given."""
     os.environ["OMP_NUM_THREADS"] = "1"
     torch.set_num_threads(1)
     from ..config import Flags
@@ -47,13 +52,17 @@ def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, fu
     env = create_env(s, n, flags.max_episode_steps, seed=seed, opponents=flags.opponent_list(),
                      reward_weight=flags.reward_weights(), env_index_base=actor_id * n,
                      env=flags.env)
-    model = make_model(flags, torch.device("cpu"))
-    model.eval()
-    flat = FlatParams(model, "cpu")
+    model = flat = None
+    if client is None:
+        model = make_model(flags, torch.device("cpu"))
+        model.eval()
+        flat = FlatParams(model, "cpu")
     my_version = -1
 
     def refresh():
         nonlocal my_version
+        if flat is None:
+            return  # the server applies weight publishes itself
         v = int(version[0].item())
         if v == my_version:
             return
@@ -63,8 +72,11 @@ def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, fu
             my_version = got - 1
 
     S = s * s
-    obs = torch.zeros(n, S, dtype=torch.int32)
-    mask = torch.zeros(n, S, 3, dtype=torch.int32)
+    if client is not None:  # the env writes straight into this actor's request rows
+        obs, mask = client.obs, client.mask
+    else:
+        obs = torch.zeros(n, S, dtype=torch.int32)
+        mask = torch.zeros(n, S, 3, dtype=torch.int32)
     rew = torch.zeros(n)
     done = torch.zeros(n, dtype=torch.uint8)
     env.reset_compact(obs, mask)
@@ -82,7 +94,13 @@ def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, fu
                 buffers["obs"][idx][t].copy_(obs)
                 buffers["action_mask"][idx][t].copy_(mask)
                 buffers["last_action"][idx][t].copy_(last_action)
-                a, lp, v = model.act(obs, mask, generator=gen)
+                if client is None:
+                    a, lp, v = model.act(obs, mask, generator=gen)
+                else:
+                    got = client.act()
+                    if got is None:  # server shut down
+                        return
+                    a, lp, v = got
                 buffers["action"][idx][t].copy_(a)
                 buffers["logprobs"][idx][t].copy_(lp)
                 buffers["baseline"][idx][t].copy_(v)
@@ -110,8 +128,9 @@ def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, fu
 class MonoRuntime:
     """Owns buffers, rings, actor processes and the watchdog."""
 
-    def __init__(self, flags, model_numel: int):
+    def __init__(self, flags, model_numel: int, device=None, make_model=None):
         self.flags = flags
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
         n_buf = flags.resolved_n_buffers()
         self.buffers = create_buffers(n_buf, flags.n_envs, flags.unroll_length, flags.env_size)
         self.free = ShmRing(n_buf + 1)
@@ -126,8 +145,31 @@ class MonoRuntime:
         self.procs: list = [None] * flags.n_actors
         self.restarts = 0
         self.frames_per_slot = flags.n_envs * flags.unroll_length
+        mode = getattr(flags, "actor_inference", "auto")
+        if mode == "auto":
+            mode = "server" if self.device.type == "cuda" else "local"
+        if mode not in ("server", "local"):
+            raise ValueError(f"--actor_inference must be auto|server|local, got {mode!r}")
+        self.server = None
+        if mode == "server":
+            from .inference import InferenceServer
+            if make_model is None:
+                raise ValueError("the inference server needs make_model")
+            self.server = InferenceServer(make_model, flags.n_actors, flags.n_envs,
+                                          flags.env_size, self.device,
+                                          max_wait_ms=getattr(flags, "inference_wait_ms", 2.0),
+                                          seed=flags.seed)
+        self.prefetcher = None
+
+    def enable_prefetch(self, device, depth: int = 2):
+        """GPU learner: pinned-DMA slot uploads one batch ahead (runtime/staging.py)."""
+        from .staging import PinnedPrefetcher
+        self.prefetcher = PinnedPrefetcher(self, device, depth, self.flags.batch_timeout)
 
     def publish(self, flat_data: torch.Tensor) -> None:
+        if self.server is not None:
+            self.server.publish(flat_data)
+            return
         rt = N.runtime()
         src = flat_data.detach()
         if src.is_cuda:
@@ -142,12 +184,15 @@ class MonoRuntime:
         p = self.ctx.Process(target=_actor_main,
                              args=(i, fd, self.buffers, self.free, self.full, self.weights,
                                    self.version, self.cur_slot, self.episode_q,
-                                   self.flags.seed * 1009 + i + 97 * self.restarts),
+                                   self.flags.seed * 1009 + i + 97 * self.restarts,
+                                   self.server.client(i) if self.server is not None else None),
                              daemon=True)
         p.start()
         self.procs[i] = p
 
     def start(self):
+        if self.server is not None:
+            self.server.start()
         for i in range(self.flags.n_actors):
             self._spawn(i)
 
@@ -174,6 +219,10 @@ class MonoRuntime:
             p.join(5)
 
     def get_batch(self, timeout: float):
+        if self.server is not None:
+            self.server.check()
+        if self.prefetcher is not None:
+            return self.prefetcher.get_batch(timeout)
         return get_batch(self.flags.batch_size, self.free, self.full, self.buffers,
                          timeout=timeout, on_wait=self.watchdog)
 
@@ -184,8 +233,12 @@ class MonoRuntime:
         return out
 
     def stop(self):
+        if self.prefetcher is not None:
+            self.prefetcher.stop()
         self.free.close()
         self.full.close()
+        if self.server is not None:
+            self.server.stop()
         for p in self.procs:
             if p is not None:
                 p.join(5)

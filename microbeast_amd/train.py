@@ -136,9 +136,12 @@ def train(flags: Flags) -> dict:
     else:
         from .runtime.mono import MonoRuntime
 
-        rt = MonoRuntime(flags, learner.flat.numel)
+        rt = MonoRuntime(flags, learner.flat.numel, device=dev,
+                         make_model=lambda: make_model(flags, "cpu"))
         rt.publish(learner.flat.data)
         rt.start()
+        if want_cuda:  # pinned DMA of full slots into HBM, one batch ahead of the learner
+            rt.enable_prefetch(dev)
         frames_per_update = flags.batch_size * flags.n_envs * flags.unroll_length
     frames_per_update *= info.world_size
 
@@ -154,7 +157,8 @@ def train(flags: Flags) -> dict:
                 batch, slots = rt.get_batch(timeout=flags.batch_timeout)
             else:
                 batch, slots = rt.get_batch(flags.batch_timeout)
-                batch = {k: v.to(dev, non_blocking=True) for k, v in batch.items()}
+                if not want_cuda:
+                    batch = {k: v.to(dev) for k, v in batch.items()}
             t1 = time.perf_counter()
             losses = learner.learn(batch)
             if runtime == "gpu":

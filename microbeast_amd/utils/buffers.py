@@ -105,6 +105,30 @@ class ShmRing:
                 pass
 
 
+LEARNER_KEYS = {"obs": "obs", "action_mask": "mask", "action": "action", "logprobs": "logp",
+                "reward": "reward", "done": "done", "baseline": "baseline"}
+
+
+def pop_full(batch_size: int, full_ring: ShmRing, timeout: float = 600.0, on_wait=None,
+             stop=None) -> list[int]:
+    """Pop ``batch_size`` full slot indices (``on_wait`` about once a second while waiting;
+    ``stop()`` true or a closed ring -> return what was popped so far)."""
+    idx = []
+    t0 = time.perf_counter()
+    while len(idx) < batch_size:
+        v = full_ring.pop(1.0)
+        if v is None:
+            if on_wait is not None:
+                on_wait()
+            if (stop is not None and stop()) or full_ring.ring.closed():
+                return idx
+            if time.perf_counter() - t0 > timeout:
+                raise TimeoutError(f"get_batch: no full slot within {timeout}s")
+            continue
+        idx.append(int(v))
+    return idx
+
+
 def get_batch(batch_size: int, free_ring: ShmRing, full_ring: ShmRing, buffers: Buffers,
               timeout: float = 600.0, on_wait=None, release: bool = True):
     """Pop ``batch_size`` full slots, return (time-major batch, indices).
@@ -114,20 +138,11 @@ def get_batch(batch_size: int, free_ring: ShmRing, full_ring: ShmRing, buffers: 
     waiting (watchdog hook). With ``release`` the slots go straight back to the
     free ring after the copy (CPU learner); otherwise the caller releases them.
     """
-    idx = []
-    t0 = time.perf_counter()
-    while len(idx) < batch_size:
-        v = full_ring.pop(1.0)
-        if v is None:
-            if on_wait is not None:
-                on_wait()
-            if time.perf_counter() - t0 > timeout:
-                raise TimeoutError(f"get_batch: no full slot within {timeout}s")
-            continue
-        idx.append(int(v))
-    names = {"obs": "obs", "action_mask": "mask", "action": "action", "logprobs": "logp",
-             "reward": "reward", "done": "done", "baseline": "baseline"}
-    batch = {dst: torch.cat([buffers[src][m] for m in idx], dim=1) for src, dst in names.items()}
+    idx = pop_full(batch_size, full_ring, timeout, on_wait)
+    if len(idx) < batch_size:
+        raise RuntimeError("get_batch: rollout ring closed")
+    batch = {dst: torch.cat([buffers[src][m] for m in idx], dim=1)
+             for src, dst in LEARNER_KEYS.items()}
     if release:
         for m in idx:
             free_ring.push(m)
