@@ -35,7 +35,9 @@ def parse(argv=None):
     p.add_argument("--size", type=int, default=16)
     p.add_argument("--arch", type=str, default="impala_flat",
                    help="impala_flat (headline) | gridnet (BASELINE config 2) | impala_deep")
-    p.add_argument("--groups", type=int, default=3)
+    p.add_argument("--groups", type=int, default=4)
+    p.add_argument("--lanes", type=int, default=1,
+                   help="concurrent policy streams, each with its own graph + I/O")
     p.add_argument("--envs_per_group", type=int, default=4096)
     p.add_argument("--unroll", type=int, default=64)
     p.add_argument("--batch_slots", type=int, default=1)
@@ -45,6 +47,12 @@ def parse(argv=None):
     p.add_argument("--learner_cu_reserve", type=int, default=0,
                    help="run the learner on a CU-masked stream leaving every k-th CU to the "
                         "policy stream (0 = off)")
+    p.add_argument("--cu_partition", type=int, default=0,
+                   help="k > 0: policy streams on CUs i %% k == 0, the learner on the rest "
+                        "(disjoint CU sets, persistent grids sized for each side)")
+    p.add_argument("--learner_cu_budget", type=int, default=0,
+                   help="size the learner's persistent grids for this many CUs (no CU mask) so "
+                        "policy kernels always find free wave slots (0 = all CUs)")
     p.add_argument("--selfplay_groups", type=int, default=0,
                    help="BASELINE config 5: env groups playing a self-play league (opponent "
                         "policy graph + PFSP over HBM snapshots) instead of scripted bots")
@@ -86,10 +94,15 @@ def main(argv=None):
     model = make_model()
     learner = Learner(model, LearnerHParams(), dev, info)
     envs_total = args.groups * args.envs_per_group
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    if args.cu_partition > 0:  # policy graphs are captured with grids for the policy CUs
+        from microbeast_amd import _native as N
+        N.kernels().mbk_set_cu_budget((ncu + args.cu_partition - 1) // args.cu_partition)
     rt = GpuActorRuntime(make_model, s, args.groups, args.envs_per_group, args.unroll,
                          args.batch_slots, dev, n_threads=threads, seed=args.seed + 1000 * info.rank,
                          env_index_base=info.rank * envs_total,
-                         selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy)
+                         selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy,
+                         n_lanes=args.lanes, policy_cu_every=args.cu_partition)
     league = None
     if args.selfplay_groups > 0:
         from microbeast_amd.runtime.league import League
@@ -97,6 +110,17 @@ def main(argv=None):
         league.current = league.add_snapshot(learner.flat.data)
     rt.start(learner.flat, opponent_version=league.current if league is not None else -1)
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
+    if args.cu_partition > 0:
+        from microbeast_amd import _native as N
+        k = args.cu_partition
+        N.kernels().mbk_set_cu_budget(ncu - (ncu + k - 1) // k)
+        h = N.runtime().create_cu_masked_stream(dev.index, k)
+        learner_stream = torch.cuda.ExternalStream(h, device=dev)
+        learner_stream.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(learner_stream)
+    if args.learner_cu_budget > 0:
+        from microbeast_amd import _native as N
+        N.kernels().mbk_set_cu_budget(args.learner_cu_budget)
     if args.learner_cu_reserve > 0:
         from microbeast_amd import _native as N
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count
@@ -186,6 +210,7 @@ def main(argv=None):
                               if args.selfplay_groups else "scripted bots"),
                 "envs_per_gpu": envs_total,
                 "env_threads_per_gpu": threads,
+                "policy_lanes": rt.n_lanes,
             },
             "actor_stats": {
                 "env_frames_stepped_per_s_rank0": round((st1["frames"] - st0["frames"]) / el, 1),
@@ -194,6 +219,15 @@ def main(argv=None):
                 "publishes": st1["publishes"] - st0["publishes"],
                 "slot_wait_s": round(st1["slot_wait_s"] - st0["slot_wait_s"], 3),
                 "driver_idle_s": round(st1["driver_idle_s"] - st0["driver_idle_s"], 3),
+                # per group step: GPU latency (enqueue -> done seen) and CPU env phase
+                "gpu_phase_ms": round(1e3 * (st1["gpu_phase_s"] - st0["gpu_phase_s"])
+                                      / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
+                "env_phase_ms": round(1e3 * (st1["env_phase_s"] - st0["env_phase_s"])
+                                      / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
+                "enqueue_ms": round(1e3 * (st1["enqueue_s"] - st0["enqueue_s"])
+                                    / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
+                "graph_launch_ms": round(1e3 * (st1["graph_launch_s"] - st0["graph_launch_s"])
+                                         / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
             },
             "last_losses": {"pg": loss_vals[0], "value": loss_vals[1], "entropy": loss_vals[2],
                             "total": loss_vals[3]},

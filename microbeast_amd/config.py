@@ -72,6 +72,7 @@ class Flags:
     groups: int = 2               # gpu runtime: env groups pipelined through the GPU
     envs_per_group: int = 256
     actor_threads: int = 0        # gpu runtime: native env worker threads (0 = auto)
+    policy_lanes: int = 1         # gpu runtime: concurrent policy streams (own graph + I/O each)
     actor_inference: str = "auto"  # mono runtime: server (batched policy in the learner
                                    # process) | local (CPU policy per actor) | auto
     inference_wait_ms: float = 2.0  # mono runtime server: dynamic-batching window

@@ -1108,6 +1108,7 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
 
 extern "C" void mbk_conv_set_grid_cap(int cap) { g_grid_cap = cap; }
 extern "C" void mbk_set_cu_budget(int n) { g_cu_budget = n; }
+extern "C" int mbk_get_cu_budget() { return g_cu_budget; }
 
 // partial holds nparts rows plus ceil(nparts / kReducePps) scratch rows after them
 extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,

@@ -22,6 +22,8 @@
 #include "../include/mbk_api.h"
 #include "common.h"
 
+extern "C" int mbk_get_cu_budget();
+
 #include <algorithm>
 #include <cstdlib>
 #include <string>
@@ -377,7 +379,10 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
           hipSuccess || per < 1)
     per = 1;
   const int ngroups = (N + tni - 1) / tni;
-  const int grid = std::min(ngroups, cus * per);
+  // persistent grid sized for the CUs this stream may use (mbk_set_cu_budget: CU-partitioned
+  // policy / learner streams), else the whole device
+  const int budget = mbk_get_cu_budget();
+  const int grid = std::min(ngroups, (budget > 0 ? std::min(budget, cus) : cus) * per);
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

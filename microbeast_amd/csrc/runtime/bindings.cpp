@@ -237,6 +237,8 @@ PYBIND11_MODULE(_mbrt, m) {
         cfg.env_index_base = c["env_index_base"].cast<int>();
         cfg.device = c["device"].cast<int>();
         if (c.contains("selfplay_groups")) cfg.selfplay_groups = c["selfplay_groups"].cast<int>();
+        if (c.contains("n_lanes")) cfg.n_lanes = c["n_lanes"].cast<int>();
+        if (c.contains("policy_cu_every")) cfg.policy_cu_every = c["policy_cu_every"].cast<int>();
         EngineBuffers buf;
         buf.obs = b["obs"].cast<uintptr_t>();
         buf.mask = b["mask"].cast<uintptr_t>();
@@ -245,23 +247,37 @@ PYBIND11_MODULE(_mbrt, m) {
         buf.value = b["value"].cast<uintptr_t>();
         buf.reward = b["reward"].cast<uintptr_t>();
         buf.done = b["done"].cast<uintptr_t>();
-        buf.in_obs = b["in_obs"].cast<uintptr_t>();
-        buf.in_mask = b["in_mask"].cast<uintptr_t>();
-        buf.out_action = b["out_action"].cast<uintptr_t>();
-        buf.out_logp = b["out_logp"].cast<uintptr_t>();
-        buf.out_value = b["out_value"].cast<uintptr_t>();
-        buf.in_codes = b["in_codes"].cast<uintptr_t>();
-        buf.in_res = b["in_res"].cast<uintptr_t>();
-        buf.out_act16 = b["out_act16"].cast<uintptr_t>();
-        if (b.contains("in_codes_p1")) {
-          buf.in_codes_p1 = b["in_codes_p1"].cast<uintptr_t>();
-          buf.in_res_p1 = b["in_res_p1"].cast<uintptr_t>();
-          buf.out_act16_p1 = b["out_act16_p1"].cast<uintptr_t>();
+        auto get = [](py::dict d, const char* k) {
+          return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0;
+        };
+        for (auto item : b["lanes"].cast<py::list>()) {
+          py::dict d = item.cast<py::dict>();
+          LaneIO io;
+          io.in_obs = get(d, "in_obs");
+          io.in_mask = get(d, "in_mask");
+          io.out_action = get(d, "out_action");
+          io.out_logp = get(d, "out_logp");
+          io.out_value = get(d, "out_value");
+          io.in_codes = get(d, "in_codes");
+          io.in_res = get(d, "in_res");
+          io.out_act16 = get(d, "out_act16");
+          io.in_codes_p1 = get(d, "in_codes_p1");
+          io.in_res_p1 = get(d, "in_res_p1");
+          io.out_act16_p1 = get(d, "out_act16_p1");
+          buf.lanes.push_back(io);
         }
         return new GpuEngine(cfg, buf);
       }))
-      .def("start", &GpuEngine::start, py::arg("graph_exec"), py::arg("opp_graph_exec") = 0,
-           py::arg("pack_graph_exec") = 0, py::arg("opp_pack_graph_exec") = 0)
+      // graphs: one (policy, opp, pack, opp_pack) tuple of raw hipGraphExec_t per lane
+      .def("start",
+           [](GpuEngine& e, std::vector<std::vector<uintptr_t>> graphs) {
+             std::vector<LaneGraphs> lg;
+             for (const auto& t : graphs) {
+               if (t.size() != 4) throw std::runtime_error("start: need 4 graph handles per lane");
+               lg.push_back(LaneGraphs{t[0], t[1], t[2], t[3]});
+             }
+             e.start(lg);
+           })
       .def("stop", [](GpuEngine& e) { py::gil_scoped_release g; e.stop(); })
       .def("get_full",
            [](GpuEngine& e, int n, double timeout) {
@@ -275,7 +291,7 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("publish_opponent", &GpuEngine::publish_opponent)
       .def("set_initial_opponent", &GpuEngine::set_initial_opponent)
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
-      .def("stream", &GpuEngine::stream)
+      .def("stream", &GpuEngine::stream, py::arg("lane") = 0)
       .def("failed", &GpuEngine::failed)
       .def("error", &GpuEngine::error)
       .def("stats", [](GpuEngine& e) {
@@ -285,6 +301,10 @@ PYBIND11_MODULE(_mbrt, m) {
         d["gpu_steps"] = s.gpu_steps;
         d["slots_full"] = s.slots_full;
         d["driver_idle_s"] = s.driver_idle_s;
+        d["gpu_phase_s"] = s.gpu_phase_s;
+        d["env_phase_s"] = s.env_phase_s;
+        d["enqueue_s"] = s.enqueue_s;
+        d["graph_launch_s"] = s.graph_launch_s;
         d["slot_wait_s"] = s.slot_wait_s;
         d["env_s"] = s.env_s;
         d["publishes"] = s.publishes;

@@ -1,5 +1,6 @@
 #include "engine.h"
 
+
 #include <chrono>
 #include <cstring>
 #include <stdexcept>
@@ -41,27 +42,44 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
                         cfg_.reward_weight.empty() ? nullptr : cfg_.reward_weight.data(),
                         cfg_.env_index_base));
   CTOR_CHECK(hipSetDevice(cfg_.device));
+  if (cfg_.n_lanes < 1 || (int)buf_.lanes.size() != cfg_.n_lanes)
+    throw std::runtime_error("GpuEngine: need one LaneIO per lane");
   // highest priority: a policy step is latency-critical (env workers wait on it) and
   // must not queue behind the learner's long kernels on the other stream
   int prio_least = 0, prio_greatest = 0;
   CTOR_CHECK(hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest));
-  CTOR_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, prio_greatest));
-  if (!buf_.in_codes || !buf_.in_res || !buf_.out_act16)
-    throw std::runtime_error("GpuEngine: in_codes / in_res / out_act16 buffers required");
+  lanes_.resize(cfg_.n_lanes);
+  for (int l = 0; l < cfg_.n_lanes; ++l) {
+    Lane& L = lanes_[l];
+    L.io = buf_.lanes[l];
+    if (!L.io.in_codes || !L.io.in_res || !L.io.out_act16)
+      throw std::runtime_error("GpuEngine: in_codes / in_res / out_act16 buffers required");
+    if (cfg_.policy_cu_every > 0) {
+      int ncu = 0;
+      CTOR_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; i += cfg_.policy_cu_every) mask[i / 32] |= 1u << (i % 32);
+      CTOR_CHECK(hipExtStreamCreateWithCUMask(&L.stream, (uint32_t)mask.size(), mask.data()));
+    } else {
+      CTOR_CHECK(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, prio_greatest));
+    }
+    CTOR_CHECK(hipMalloc((void**)&L.d_rd, E * 4 + E + 64));
+  }
   CTOR_CHECK(hipHostMalloc((void**)&h_codes_, (size_t)total * S_ * 2, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_res_, (size_t)total * 4, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_act16_, (size_t)total * S_ * 2, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_reward_, (size_t)total * 4, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_done_, (size_t)total, hipHostMallocDefault));
-  CTOR_CHECK(hipMalloc((void**)&d_rd_, E * 4 + E + 64));
   std::memset(h_reward_, 0, (size_t)total * 4);
   std::memset(h_done_, 0, (size_t)total);
   if (cfg_.selfplay_groups < 0 || cfg_.selfplay_groups > cfg_.n_groups)
     throw std::runtime_error("GpuEngine: bad selfplay_groups");
   const int sp0 = cfg_.n_groups - cfg_.selfplay_groups;  // first self-play group
   if (cfg_.selfplay_groups > 0) {
-    if (!buf_.in_codes_p1 || !buf_.in_res_p1 || !buf_.out_act16_p1)
-      throw std::runtime_error("GpuEngine: self-play needs in_codes_p1 / in_res_p1 / out_act16_p1");
+    for (const Lane& L : lanes_)
+      if (!L.io.in_codes_p1 || !L.io.in_res_p1 || !L.io.out_act16_p1)
+        throw std::runtime_error(
+            "GpuEngine: self-play needs in_codes_p1 / in_res_p1 / out_act16_p1");
     CTOR_CHECK(hipHostMalloc((void**)&h_codes_p1_, (size_t)total * S_ * 2, hipHostMallocDefault));
     CTOR_CHECK(hipHostMalloc((void**)&h_res_p1_, (size_t)total * 4, hipHostMallocDefault));
     CTOR_CHECK(hipHostMalloc((void**)&h_act16_p1_, (size_t)total * S_ * 2, hipHostMallocDefault));
@@ -75,6 +93,7 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     groups_.emplace_back(new Group());
     CTOR_CHECK(hipEventCreateWithFlags(&groups_[g]->ev, hipEventDisableTiming));
     groups_[g]->selfplay = g >= sp0;
+    groups_[g]->lane = g % cfg_.n_lanes;
     groups_[g]->phase.store(READY);  // reset observations are ready
   }
   full_ev_.resize(cfg_.n_slots);
@@ -87,7 +106,10 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   }
   for (PubChan& c : pub_) {
     CTOR_CHECK(hipEventCreateWithFlags(&c.ready, hipEventDisableTiming));
-    CTOR_CHECK(hipEventCreateWithFlags(&c.consumed, hipEventDisableTiming));
+    c.pending.assign(cfg_.n_lanes, false);
+    c.dst.assign(cfg_.n_lanes, 0);
+    c.consumed.assign(cfg_.n_lanes, nullptr);
+    for (auto& ev : c.consumed) CTOR_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   }
   // work chunk: enough chunks for every worker, at least 2 envs each
   chunk_ = std::max(1, std::min(16, cfg_.envs_per_group / std::max(1, 2 * cfg_.n_threads)));
@@ -95,13 +117,15 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
 
 GpuEngine::~GpuEngine() {
   stop();
-  if (stream_) hipStreamSynchronize(stream_);
+  for (Lane& L : lanes_)
+    if (L.stream) hipStreamSynchronize(L.stream);
   for (auto& g : groups_) if (g->ev) hipEventDestroy(g->ev);
   for (auto e : full_ev_) hipEventDestroy(e);
   for (auto e : release_ev_) hipEventDestroy(e);
   for (PubChan& c : pub_) {
     if (c.ready) hipEventDestroy(c.ready);
-    if (c.consumed) hipEventDestroy(c.consumed);
+    for (auto ev : c.consumed)
+      if (ev) hipEventDestroy(ev);
     if (c.staging) hipFree(c.staging);
   }
   if (h_codes_p1_) hipHostFree(h_codes_p1_);
@@ -112,8 +136,10 @@ GpuEngine::~GpuEngine() {
   if (h_act16_) hipHostFree(h_act16_);
   if (h_reward_) hipHostFree(h_reward_);
   if (h_done_) hipHostFree(h_done_);
-  if (d_rd_) hipFree(d_rd_);
-  if (stream_) hipStreamDestroy(stream_);
+  for (Lane& L : lanes_) {
+    if (L.d_rd) hipFree(L.d_rd);
+    if (L.stream) hipStreamDestroy(L.stream);
+  }
 }
 
 void GpuEngine::fail(const std::string& msg) {
@@ -132,15 +158,21 @@ std::string GpuEngine::error() const {
   return err_;
 }
 
-void GpuEngine::start(uintptr_t graph_exec, uintptr_t opp_graph_exec, uintptr_t pack_graph_exec,
-                      uintptr_t opp_pack_graph_exec) {
+void GpuEngine::start(const std::vector<LaneGraphs>& graphs) {
   if (running_.load()) return;
-  if (cfg_.selfplay_groups > 0 && !opp_graph_exec)
-    throw std::runtime_error("GpuEngine::start: self-play groups need the opponent graph");
-  graph_ = (hipGraphExec_t)graph_exec;
-  opp_graph_ = (hipGraphExec_t)opp_graph_exec;
-  pack_graph_[0] = (hipGraphExec_t)pack_graph_exec;
-  pack_graph_[1] = (hipGraphExec_t)opp_pack_graph_exec;
+  if ((int)graphs.size() != cfg_.n_lanes)
+    throw std::runtime_error("GpuEngine::start: need one LaneGraphs per lane");
+  for (int l = 0; l < cfg_.n_lanes; ++l) {
+    const LaneGraphs& g = graphs[l];
+    if (!g.policy) throw std::runtime_error("GpuEngine::start: missing policy graph");
+    if (cfg_.selfplay_groups > 0 && !g.opp)
+      throw std::runtime_error("GpuEngine::start: self-play groups need the opponent graph");
+    Lane& L = lanes_[l];
+    L.graph = (hipGraphExec_t)g.policy;
+    L.opp_graph = (hipGraphExec_t)g.opp;
+    L.pack_graph[0] = (hipGraphExec_t)g.pack;
+    L.pack_graph[1] = (hipGraphExec_t)g.opp_pack;
+  }
   running_.store(true);
   for (int w = 0; w < cfg_.n_threads; ++w) workers_.emplace_back(&GpuEngine::worker_loop, this, w);
   driver_ = std::thread(&GpuEngine::driver_loop, this);
@@ -153,11 +185,17 @@ void GpuEngine::stop() {
   if (driver_.joinable()) driver_.join();
   for (auto& t : workers_) if (t.joinable()) t.join();
   workers_.clear();
-  if (stream_) hipStreamSynchronize(stream_);
+  for (Lane& L : lanes_)
+    if (L.stream) hipStreamSynchronize(L.stream);
 }
 
 void GpuEngine::dispatch_env(int g) {
   Group& G = *groups_[g];
+  const auto now = std::chrono::steady_clock::now();
+  gpu_phase_ns_.fetch_add(
+      std::chrono::duration_cast<std::chrono::nanoseconds>(now - G.t_phase).count(),
+      std::memory_order_relaxed);
+  G.t_phase = now;
   G.phase.store(ENV_BUSY, std::memory_order_release);
   G.remaining.store(cfg_.envs_per_group, std::memory_order_release);
   G.next_env.store(0, std::memory_order_release);
@@ -195,7 +233,12 @@ void GpuEngine::worker_loop(int wid) {
                           std::memory_order_relaxed);
         frames_.fetch_add(e1 - e, std::memory_order_relaxed);
         did = true;
-        if (G.remaining.fetch_sub(e1 - e) == e1 - e) G.phase.store(READY, std::memory_order_release);
+        if (G.remaining.fetch_sub(e1 - e) == e1 - e) {
+          G.t_ready_ns.store(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now().time_since_epoch()).count(),
+                             std::memory_order_relaxed);
+          G.phase.store(READY, std::memory_order_release);
+        }
       }
     }
     if (!did) {
@@ -207,53 +250,93 @@ void GpuEngine::worker_loop(int wid) {
 }
 
 bool GpuEngine::enqueue_gpu(int g) {
+  const auto t_enq = std::chrono::steady_clock::now();
+  struct Timer {  // adds the enqueue's duration on every exit path
+    std::atomic<int64_t>& acc;
+    std::chrono::steady_clock::time_point t0;
+    ~Timer() {
+      acc.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now() - t0).count(),
+                    std::memory_order_relaxed);
+    }
+  } timer{enqueue_ns_, t_enq};
   Group& G = *groups_[g];
+  Lane& L = lanes_[G.lane];
+  hipStream_t st = L.stream;
+  const LaneIO& io = L.io;
   const size_t E = cfg_.envs_per_group, T = cfg_.unroll;
+  {  // apply pending weight publishes to this lane between two of its inference steps
+    std::lock_guard<std::mutex> l(pub_m_);
+    const int ln = G.lane;
+    for (int c = 0; c < 2; ++c) {
+      PubChan& P = pub_[c];
+      if (!P.pending[ln]) continue;
+      ENG_CHECK(hipStreamWaitEvent(st, P.ready, 0));
+      ENG_CHECK(hipMemcpyAsync((void*)P.dst[ln], P.staging, P.n, hipMemcpyDeviceToDevice,
+                               st));
+      ENG_CHECK(hipEventRecord(P.consumed[ln], st));
+      if (L.pack_graph[c]) ENG_CHECK(hipGraphLaunch(L.pack_graph[c], st));
+      P.pending[ln] = false;
+      if (c == 1) L.opp_version = P.version;
+      bool all = true;
+      for (bool pl : P.pending) all = all && !pl;
+      if (all) {  // landed on every lane
+        if (c == 0) publishes_.fetch_add(1);
+        else {
+          opp_version_pub_.store(P.version);
+          opp_publishes_.fetch_add(1);
+        }
+      }
+    }
+  }
   if (G.t == 0) {
+    // free slots go to waiting groups in FIFO order: without it the group scanned first
+    // would take every released slot and starve the others when the learner is the
+    // bottleneck (and a starved lane would never apply weight publishes)
+    auto waiting = [&] {
+      for (int w : slot_wait_q_) if (w == g) return true;
+      return false;
+    };
+    if (!slot_wait_q_.empty() && slot_wait_q_.front() != g) {
+      if (!waiting()) slot_wait_q_.push_back(g);
+      return false;
+    }
     int slot = -1;
     {
       std::lock_guard<std::mutex> l(slot_m_);
       if (!free_slots_.empty()) { slot = free_slots_.front(); free_slots_.pop_front(); }
     }
-    if (slot < 0) return false;  // learner-bound: wait for a released slot
-    if (release_pending_[slot]) ENG_CHECK(hipStreamWaitEvent(stream_, release_ev_[slot], 0));
+    if (slot < 0) {  // learner-bound: wait for a released slot
+      if (!waiting()) slot_wait_q_.push_back(g);
+      return false;
+    }
+    if (!slot_wait_q_.empty() && slot_wait_q_.front() == g) slot_wait_q_.pop_front();
+    if (release_pending_[slot]) ENG_CHECK(hipStreamWaitEvent(st, release_ev_[slot], 0));
     G.cur = slot;
   }
-  {  // apply pending weight publishes between two inference steps
-    std::lock_guard<std::mutex> l(pub_m_);
-    for (int c = 0; c < 2; ++c) {
-      PubChan& P = pub_[c];
-      if (!P.pending) continue;
-      ENG_CHECK(hipStreamWaitEvent(stream_, P.ready, 0));
-      ENG_CHECK(hipMemcpyAsync((void*)P.dst, P.staging, P.n, hipMemcpyDeviceToDevice, stream_));
-      ENG_CHECK(hipEventRecord(P.consumed, stream_));
-      if (pack_graph_[c]) ENG_CHECK(hipGraphLaunch(pack_graph_[c], stream_));
-      P.pending = false;
-      if (c == 0) publishes_.fetch_add(1);
-      else {
-        opp_version_ = P.version;
-        opp_version_pub_.store(P.version);
-        opp_publishes_.fetch_add(1);
-      }
-    }
-  }
   const size_t e0 = (size_t)g * E;
-  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
-                           hipMemcpyHostToDevice, stream_));
-  ENG_CHECK(hipMemcpyAsync((void*)buf_.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
-                           stream_));
+  ENG_CHECK(hipMemcpyAsync((void*)io.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
+                           hipMemcpyHostToDevice, st));
+  ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
+                           st));
   if (!G.first) {
-    ENG_CHECK(hipMemcpyAsync(d_rd_, h_reward_ + e0, E * 4, hipMemcpyHostToDevice, stream_));
-    ENG_CHECK(hipMemcpyAsync(d_rd_ + E * 4, h_done_ + e0, E, hipMemcpyHostToDevice, stream_));
+    ENG_CHECK(hipMemcpyAsync(L.d_rd, h_reward_ + e0, E * 4, hipMemcpyHostToDevice, st));
+    ENG_CHECK(hipMemcpyAsync(L.d_rd + E * 4, h_done_ + e0, E, hipMemcpyHostToDevice, st));
   }
-  ENG_CHECK(hipGraphLaunch(graph_, stream_));
+  {
+    const auto t0 = std::chrono::steady_clock::now();
+    ENG_CHECK(hipGraphLaunch(L.graph, st));
+    launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                             std::chrono::steady_clock::now() - t0).count(),
+                         std::memory_order_relaxed);
+  }
   if (G.selfplay) {  // the opponent acts on its own (mirrored) view with its own weights
-    ENG_CHECK(hipMemcpyAsync((void*)buf_.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
-                             hipMemcpyHostToDevice, stream_));
-    ENG_CHECK(hipMemcpyAsync((void*)buf_.in_res_p1, h_res_p1_ + e0, E * 4, hipMemcpyHostToDevice,
-                             stream_));
-    ENG_CHECK(hipGraphLaunch(opp_graph_, stream_));
-    G.opp_version = opp_version_;
+    ENG_CHECK(hipMemcpyAsync((void*)io.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
+                             hipMemcpyHostToDevice, st));
+    ENG_CHECK(hipMemcpyAsync((void*)io.in_res_p1, h_res_p1_ + e0, E * 4, hipMemcpyHostToDevice,
+                             st));
+    ENG_CHECK(hipGraphLaunch(L.opp_graph, st));
+    G.opp_version = L.opp_version;
   }
 
   // scatter this step into the HBM rollout slot(s)
@@ -275,25 +358,25 @@ bool GpuEngine::enqueue_gpu(int g) {
   auto u8_at = [&](uintptr_t base, int slot, size_t i) {
     return (char*)base + (slot * slot_stride_scalar_ + i * E);
   };
-  seg[n++] = {(const void*)buf_.in_obs, obs_at(G.cur, t), E * S_ * 4};
-  seg[n++] = {(const void*)buf_.in_mask, mask_at(G.cur, t), E * S_ * 4 * kMaskWords};
-  seg[n++] = {(const void*)buf_.out_action, act_at(G.cur, t), E * S_ * kActComps};
-  seg[n++] = {(const void*)buf_.out_logp, f32_at(buf_.logp, G.cur, t), E * 4};
-  seg[n++] = {(const void*)buf_.out_value, f32_at(buf_.value, G.cur, t), E * 4};
+  seg[n++] = {(const void*)io.in_obs, obs_at(G.cur, t), E * S_ * 4};
+  seg[n++] = {(const void*)io.in_mask, mask_at(G.cur, t), E * S_ * 4 * kMaskWords};
+  seg[n++] = {(const void*)io.out_action, act_at(G.cur, t), E * S_ * kActComps};
+  seg[n++] = {(const void*)io.out_logp, f32_at(buf_.logp, G.cur, t), E * 4};
+  seg[n++] = {(const void*)io.out_value, f32_at(buf_.value, G.cur, t), E * 4};
   if (!G.first) {
     const int rs = t > 0 ? G.cur : G.prev;
     const size_t ri = t > 0 ? t - 1 : T - 1;
-    seg[n++] = {(const void*)d_rd_, f32_at(buf_.reward, rs, ri), E * 4};
-    seg[n++] = {(const void*)(d_rd_ + E * 4), u8_at(buf_.done, rs, ri), E};
+    seg[n++] = {(const void*)L.d_rd, f32_at(buf_.reward, rs, ri), E * 4};
+    seg[n++] = {(const void*)(L.d_rd + E * 4), u8_at(buf_.done, rs, ri), E};
   }
   const bool close_prev = (t == 0 && G.prev >= 0);
   if (close_prev) {
-    seg[n++] = {(const void*)buf_.in_obs, obs_at(G.prev, T), E * S_ * 4};
-    seg[n++] = {(const void*)buf_.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
+    seg[n++] = {(const void*)io.in_obs, obs_at(G.prev, T), E * S_ * 4};
+    seg[n++] = {(const void*)io.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
   }
-  ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, stream_));
+  ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, st));
   if (close_prev) {
-    ENG_CHECK(hipEventRecord(full_ev_[G.prev], stream_));
+    ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
     {
       std::lock_guard<std::mutex> l(slot_m_);
       full_slots_.push_back(G.prev);
@@ -302,12 +385,12 @@ bool GpuEngine::enqueue_gpu(int g) {
     full_cv_.notify_all();
     G.prev = -1;
   }
-  ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)buf_.out_act16, E * S_ * 2,
-                           hipMemcpyDeviceToHost, stream_));
+  ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)io.out_act16, E * S_ * 2,
+                           hipMemcpyDeviceToHost, st));
   if (G.selfplay)
-    ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)buf_.out_act16_p1, E * S_ * 2,
-                             hipMemcpyDeviceToHost, stream_));
-  ENG_CHECK(hipEventRecord(G.ev, stream_));
+    ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
+                             hipMemcpyDeviceToHost, st));
+  ENG_CHECK(hipEventRecord(G.ev, st));
   gpu_steps_.fetch_add(1);
   G.t += 1;
   if (G.t == (int)T) {
@@ -316,6 +399,16 @@ bool GpuEngine::enqueue_gpu(int g) {
     G.cur = -1;
   }
   G.first = false;
+  {
+    const auto now = std::chrono::steady_clock::now();
+    const int64_t rdy = G.t_ready_ns.exchange(0, std::memory_order_relaxed);
+    if (rdy > 0)  // env phase: dispatch -> last env of the group stepped
+      env_phase_ns_.fetch_add(
+          rdy - std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    G.t_phase.time_since_epoch()).count(),
+          std::memory_order_relaxed);
+    G.t_phase = now;
+  }
   G.phase.store(ON_GPU, std::memory_order_release);
   return true;
 }
@@ -399,27 +492,33 @@ void GpuEngine::release(const std::vector<int>& slots, uintptr_t stream) {
   }
 }
 
-bool GpuEngine::publish_chan(int chan, uintptr_t src, uintptr_t dst, size_t nbytes,
-                             uintptr_t stream, int version) {
+bool GpuEngine::publish_chan(int chan, uintptr_t src, const std::vector<uintptr_t>& dsts,
+                             size_t nbytes, uintptr_t stream, int version) {
   std::lock_guard<std::mutex> l(pub_m_);
   PubChan& P = pub_[chan];
-  if (P.pending) return false;  // previous version not applied yet: skip this one
+  if ((int)dsts.size() != cfg_.n_lanes)
+    throw std::runtime_error("publish: need one destination per lane");
+  for (bool pl : P.pending)
+    if (pl) return false;  // previous version not applied on every lane yet: skip this one
   hipStream_t s = (hipStream_t)stream;
   if (nbytes > P.staging_n) {
     // first publish (or growth): synchronous realloc is fine outside the hot loop
-    if (P.staging) { hipStreamSynchronize(stream_); hipFree(P.staging); }
+    if (P.staging) {
+      for (Lane& L : lanes_) hipStreamSynchronize(L.stream);
+      hipFree(P.staging);
+    }
     if (hipMalloc((void**)&P.staging, nbytes) != hipSuccess)
       throw std::runtime_error("publish: hipMalloc staging failed");
     P.staging_n = nbytes;
   }
-  // staging is reused only after the driver's previous copy-out has executed
-  hipStreamWaitEvent(s, P.consumed, 0);
+  // staging is reused only after every lane's previous copy-out has executed
+  for (hipEvent_t ev : P.consumed) hipStreamWaitEvent(s, ev, 0);
   hipMemcpyAsync(P.staging, (const void*)src, nbytes, hipMemcpyDeviceToDevice, s);
   hipEventRecord(P.ready, s);
-  P.dst = dst;
+  P.dst = dsts;
   P.n = nbytes;
   P.version = version;
-  P.pending = true;
+  P.pending.assign(cfg_.n_lanes, true);
   return true;
 }
 
@@ -429,6 +528,10 @@ EngineStats GpuEngine::stats() const {
   s.gpu_steps = gpu_steps_.load();
   s.slots_full = slots_full_.load();
   s.env_s = env_ns_.load() * 1e-9;
+  s.gpu_phase_s = gpu_phase_ns_.load() * 1e-9;
+  s.env_phase_s = env_phase_ns_.load() * 1e-9;
+  s.enqueue_s = enqueue_ns_.load() * 1e-9;
+  s.graph_launch_s = launch_ns_.load() * 1e-9;
   s.publishes = publishes_.load();
   s.opp_publishes = opp_publishes_.load();
   s.opp_version = opp_version_pub_.load();

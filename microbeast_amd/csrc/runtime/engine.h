@@ -4,8 +4,11 @@
 //
 //   * env worker threads (C++, no GIL) step the synthetic microRTS sims and
 //     write compact obs / mask / reward / done into PINNED host staging;
-//   * a driver thread pipelines env groups through the GPU on its own HIP
-//     stream: H2D staging -> hipGraphLaunch(policy inference graph) ->
+//   * a driver thread pipelines env groups through the GPU on `n_lanes` HIP
+//     streams (group g on lane g % n_lanes; each lane has its own policy graph,
+//     I/O buffers and inference-weight copy, so policy steps of different
+//     groups run concurrently instead of queueing behind each other and behind
+//     the learner's kernels): H2D staging -> hipGraphLaunch(policy graph) ->
 //     one multi-segment copy kernel that scatters the step into an
 //     HBM-resident rollout slot -> D2H actions -> event;
 //   * rollout slots live in HBM (288 GB/GPU: thousands of slots fit), so the
@@ -29,6 +32,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -55,6 +59,28 @@ struct EngineConfig {
   int env_index_base = 0;
   int device = 0;
   int selfplay_groups = 0;  // groups [n_groups - selfplay_groups, n_groups) are self-play
+  int n_lanes = 1;          // concurrent policy streams (each with its own graph + I/O)
+  // >0: CU-partition the GPU: policy streams may only use CUs i with i % k == 0 (the
+  // learner takes the complement on its own masked stream), so persistent learner
+  // kernels and latency-critical policy kernels never compete for the same CUs
+  int policy_cu_every = 0;
+};
+
+// Fixed-address I/O of one lane's captured policy graph (and opponent graph). The graph
+// decodes in_codes/in_res into in_obs / in_mask (GPU-side mask) and packs out_action
+// into out_act16.
+struct LaneIO {
+  uintptr_t in_obs = 0, in_mask = 0, out_action = 0, out_logp = 0, out_value = 0;
+  uintptr_t in_codes = 0, in_res = 0, out_act16 = 0;
+  // opponent graph I/O (self-play groups only)
+  uintptr_t in_codes_p1 = 0, in_res_p1 = 0, out_act16_p1 = 0;
+};
+
+// Per-lane graphs (raw hipGraphExec_t). opp: opponent policy (self-play only); pack /
+// opp_pack (optional): replayed right after a publish lands on that lane, rebuilding the
+// derived inference weights so the policy graph itself never re-packs.
+struct LaneGraphs {
+  uintptr_t policy = 0, opp = 0, pack = 0, opp_pack = 0;
 };
 
 // Device buffers owned by Python (torch tensors); raw addresses.
@@ -67,12 +93,7 @@ struct EngineBuffers {
   uintptr_t value = 0;    // f32
   uintptr_t reward = 0;   // f32
   uintptr_t done = 0;     // u8
-  // inference graph I/O (fixed addresses). The graph decodes in_codes/in_res into
-  // in_obs / in_mask (GPU-side mask) and packs out_action into out_act16.
-  uintptr_t in_obs = 0, in_mask = 0, out_action = 0, out_logp = 0, out_value = 0;
-  uintptr_t in_codes = 0, in_res = 0, out_act16 = 0;
-  // opponent graph I/O (self-play groups only)
-  uintptr_t in_codes_p1 = 0, in_res_p1 = 0, out_act16_p1 = 0;
+  std::vector<LaneIO> lanes;  // one per policy lane
 };
 
 struct EngineStats {
@@ -82,6 +103,13 @@ struct EngineStats {
   double driver_idle_s = 0.0;  // driver found nothing to do
   double slot_wait_s = 0.0;    // groups stalled for a free slot (learner-bound)
   double env_s = 0.0;          // summed worker time inside env step
+  // pipeline phases, summed over group steps: enqueue -> the driver sees the step's event
+  // complete (GPU latency incl. queueing behind other groups / learner contention), and
+  // dispatch to env workers -> the group's last env stepped (CPU phase)
+  double gpu_phase_s = 0.0;
+  double env_phase_s = 0.0;
+  double enqueue_s = 0.0;       // driver thread time inside enqueue (HIP API calls)
+  double graph_launch_s = 0.0;  // of which hipGraphLaunch of the policy graph(s)
   int64_t publishes = 0;
   int64_t opp_publishes = 0;
   int opp_version = -1;
@@ -91,31 +119,33 @@ class GpuEngine {
  public:
   GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf);
   ~GpuEngine();
-  // opp_graph_exec: the opponent policy graph (required iff selfplay_groups > 0).
-  // pack_graph_exec / opp_pack_graph_exec (optional): replayed right after a publish on the
-  // matching channel lands, to rebuild the derived inference weights (packed conv / head
-  // blocks, bf16 copies) so the policy graph itself never re-packs.
-  void start(uintptr_t graph_exec, uintptr_t opp_graph_exec = 0, uintptr_t pack_graph_exec = 0,
-             uintptr_t opp_pack_graph_exec = 0);
+  // one LaneGraphs per lane; the opponent graph is required iff selfplay_groups > 0
+  void start(const std::vector<LaneGraphs>& graphs);
   void stop();
   // Blocks until n full slots are available (or timeout). Returns slot ids.
   std::vector<int> get_full(int n, double timeout_s);
   void stream_wait_full(uintptr_t stream, int slot);
   void release(const std::vector<int>& slots, uintptr_t stream);
-  // Returns false if the previous publish has not been applied yet (skipped).
-  bool publish(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream) {
-    return publish_chan(0, src, dst, nbytes, stream, -1);
+  // Copy src (device, on `stream`) into every lane's inference weights dsts[lane], each
+  // applied between two of that lane's policy steps. Returns false (skipped) if the
+  // previous publish has not landed on every lane yet.
+  bool publish(uintptr_t src, const std::vector<uintptr_t>& dsts, size_t nbytes,
+               uintptr_t stream) {
+    return publish_chan(0, src, dsts, nbytes, stream, -1);
   }
   // League id of the opponent weights in place at start (before any publish_opponent).
-  void set_initial_opponent(int version) { opp_version_ = version; opp_version_pub_.store(version); }
+  void set_initial_opponent(int version) {
+    for (auto& L : lanes_) L.opp_version = version;
+    opp_version_pub_.store(version);
+  }
   // League: swap the opponent policy's weights to snapshot `version` (same ordering).
-  bool publish_opponent(uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream,
-                        int version) {
-    return publish_chan(1, src, dst, nbytes, stream, version);
+  bool publish_opponent(uintptr_t src, const std::vector<uintptr_t>& dsts, size_t nbytes,
+                        uintptr_t stream, int version) {
+    return publish_chan(1, src, dsts, nbytes, stream, version);
   }
   std::vector<EpisodeRecord> drain_episodes() { return log_.drain(); }
   EngineStats stats() const;
-  uintptr_t stream() const { return (uintptr_t)stream_; }
+  uintptr_t stream(int lane = 0) const { return (uintptr_t)lanes_.at(lane).stream; }
   const EngineConfig& config() const { return cfg_; }
   VecEnv& env() { return *env_; }
   bool failed() const { return failed_.load(); }
@@ -131,17 +161,28 @@ class GpuEngine {
     bool first = true;
     bool selfplay = false;
     int opp_version = -1;  // league id of the opponent that chose this step's p1 actions
+    int lane = 0;
     hipEvent_t ev = nullptr;
+    std::chrono::steady_clock::time_point t_phase;  // start of the current phase
+    std::atomic<int64_t> t_ready_ns{0};              // worker: when the env phase ended
   };
   struct PubChan {  // event-ordered D2D weight publish, applied between policy steps
-    bool pending = false;
-    uintptr_t dst = 0;
+    std::vector<bool> pending;          // per lane: staging not yet copied out
+    std::vector<uintptr_t> dst;         // per lane inference weights
     size_t n = 0;
     int version = -1;
-    hipEvent_t ready = nullptr;     // publisher stream: staging filled
-    hipEvent_t consumed = nullptr;  // engine stream: staging copied out
+    hipEvent_t ready = nullptr;         // publisher stream: staging filled
+    std::vector<hipEvent_t> consumed;   // per lane stream: staging copied out
     uint8_t* staging = nullptr;
     size_t staging_n = 0;
+  };
+  struct Lane {
+    hipStream_t stream = nullptr;
+    hipGraphExec_t graph = nullptr, opp_graph = nullptr;
+    hipGraphExec_t pack_graph[2] = {nullptr, nullptr};
+    LaneIO io;
+    uint8_t* d_rd = nullptr;  // device staging for reward+done of one group
+    int opp_version = -1;     // driver thread only
   };
 
   EngineConfig cfg_;
@@ -150,10 +191,7 @@ class GpuEngine {
   size_t slot_stride_obs_, slot_stride_mask_, slot_stride_act_, slot_stride_scalar_;
   std::unique_ptr<VecEnv> env_;
   EpisodeLog log_;
-  hipStream_t stream_ = nullptr;
-  hipGraphExec_t graph_ = nullptr;
-  hipGraphExec_t opp_graph_ = nullptr;
-  hipGraphExec_t pack_graph_[2] = {nullptr, nullptr};
+  std::vector<Lane> lanes_;
   std::vector<std::unique_ptr<Group>> groups_;
   // pinned staging, all envs contiguous
   uint16_t* h_codes_ = nullptr;  // 16-bit cell codes
@@ -164,7 +202,6 @@ class GpuEngine {
   uint16_t* h_codes_p1_ = nullptr;  // self-play: opponent-perspective codes
   int32_t* h_res_p1_ = nullptr;
   uint16_t* h_act16_p1_ = nullptr;  // opponent's packed actions (its frame)
-  uint8_t* d_rd_ = nullptr;  // device staging for reward+done of one group
 
   // slots
   std::mutex slot_m_;
@@ -172,13 +209,13 @@ class GpuEngine {
   std::deque<int> free_slots_, full_slots_;
   std::vector<hipEvent_t> full_ev_, release_ev_;
   std::vector<bool> release_pending_;
+  std::deque<int> slot_wait_q_;  // driver thread only: groups waiting for a free slot
 
   // publish channels: 0 = learner policy, 1 = league opponent
   std::mutex pub_m_;
   PubChan pub_[2];
-  int opp_version_ = -1;  // driver thread only
-  bool publish_chan(int chan, uintptr_t src, uintptr_t dst, size_t nbytes, uintptr_t stream,
-                    int version);
+  bool publish_chan(int chan, uintptr_t src, const std::vector<uintptr_t>& dsts, size_t nbytes,
+                    uintptr_t stream, int version);
 
   // workers
   std::vector<std::thread> workers_;
@@ -195,6 +232,7 @@ class GpuEngine {
   std::atomic<int64_t> frames_{0}, gpu_steps_{0}, slots_full_{0}, publishes_{0}, opp_publishes_{0};
   std::atomic<int> opp_version_pub_{-1};
   std::atomic<int64_t> env_ns_{0};
+  std::atomic<int64_t> gpu_phase_ns_{0}, env_phase_ns_{0}, enqueue_ns_{0}, launch_ns_{0};
   double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
   mutable std::mutex stats_m_;
 

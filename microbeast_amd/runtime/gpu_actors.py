@@ -56,7 +56,8 @@ class GpuActorRuntime:
                  batch_slots: int, device: torch.device, n_threads: int | None = None,
                  n_slots: int | None = None, max_steps: int = 2000, seed: int = 1,
                  bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
-                 env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False):
+                 env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False,
+                 n_lanes: int | None = None, policy_cu_every: int = 0):
         rt = N.runtime()
         self.device = device
         self.size, self.S = size, size * size
@@ -74,29 +75,46 @@ class GpuActorRuntime:
             "reward": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
             "done": torch.zeros(NS, T1, E, dtype=torch.uint8, device=dev),
         }
-        self.io = self._make_io()
-        self.rng = torch.tensor([seed * 7919 + env_index_base, 0], dtype=torch.int64, device=dev)
-        self._cell_logp = torch.zeros(E * S, dtype=torch.float32, device=dev)
-        self.infer_model = make_model().to(dev)
-        self.infer_model.eval()
+        # policy lanes: group g steps on lane g % n_lanes; every lane has its own stream,
+        # captured graph, I/O buffers, RNG stream and inference-weight copy, so policy steps
+        # of different groups can run concurrently. Measured on one MI355X (4 x 4096 envs,
+        # same box, back to back): 1 lane 6.22 M frames/s, 2 lanes 5.78 M, 4 lanes 5.68 M:
+        # the GPU, not the single stream, is the limit there, so the default is one lane
+        self.n_lanes = max(1, min(n_groups, n_lanes if n_lanes is not None else 1))
         self.fp8_policy = fp8_policy
-        if fp8_policy:  # acting trunk on fp8 MFMA; V-trace corrects the behaviour/learner gap
-            self.infer_model.fp8_inference = True
-        self.infer_flat = FlatParams(self.infer_model, dev)
-        self.pack_graph = self._capture_pack(self.infer_model)
-        self.graph = self._capture(self.io, self.infer_model, self.rng)
         self.selfplay_groups = int(selfplay_groups)
-        self.opp_graph = None
+        self.lanes = []
+        for ln in range(self.n_lanes):
+            lane = {"io": self._make_io(),
+                    "rng": torch.tensor([seed * 7919 + env_index_base + 15485863 * ln, 0],
+                                        dtype=torch.int64, device=dev),
+                    "model": make_model().to(dev)}
+            lane["model"].eval()
+            if fp8_policy:  # acting trunk on fp8 MFMA; V-trace corrects the behaviour gap
+                lane["model"].fp8_inference = True
+            lane["flat"] = FlatParams(lane["model"], dev)
+            lane["pack_graph"] = self._capture_pack(lane["model"])
+            lane["graph"] = self._capture(lane["io"], lane["model"], lane["rng"])
+            if self.selfplay_groups > 0:
+                lane["io_p1"] = self._make_io()
+                lane["rng_p1"] = torch.tensor(
+                    [seed * 7919 + env_index_base + 104729 + 15485863 * ln, 0],
+                    dtype=torch.int64, device=dev)
+                lane["opp_model"] = make_model().to(dev)
+                lane["opp_model"].eval()
+                lane["opp_model"].fp8_inference = fp8_policy
+                lane["opp_flat"] = FlatParams(lane["opp_model"], dev)
+                lane["opp_pack_graph"] = self._capture_pack(lane["opp_model"])
+                lane["opp_graph"] = self._capture(lane["io_p1"], lane["opp_model"],
+                                                  lane["rng_p1"])
+            self.lanes.append(lane)
+        # lane-0 aliases (tests / tools)
+        l0 = self.lanes[0]
+        self.io, self.rng, self.infer_model = l0["io"], l0["rng"], l0["model"]
+        self.infer_flat, self.pack_graph, self.graph = l0["flat"], l0["pack_graph"], l0["graph"]
+        self.opp_graph = l0.get("opp_graph")
         if self.selfplay_groups > 0:
-            self.io_p1 = self._make_io()
-            self.rng_p1 = torch.tensor([seed * 7919 + env_index_base + 104729, 0],
-                                       dtype=torch.int64, device=dev)
-            self.opp_model = make_model().to(dev)
-            self.opp_model.eval()
-            self.opp_model.fp8_inference = fp8_policy
-            self.opp_flat = FlatParams(self.opp_model, dev)
-            self.opp_pack_graph = self._capture_pack(self.opp_model)
-            self.opp_graph = self._capture(self.io_p1, self.opp_model, self.rng_p1)
+            self.opp_flat, self.opp_model = l0["opp_flat"], l0["opp_model"]
         if n_threads is None:
             n_threads = max(1, min(32, available_cpus() - 3))
         self.n_threads = n_threads
@@ -105,13 +123,17 @@ class GpuActorRuntime:
                    bots=[BOT_IDS[b] if isinstance(b, str) else int(b) for b in bots],
                    reward_weight=list(reward_weight), env_index_base=env_index_base,
                    device=dev.index if dev.index is not None else torch.cuda.current_device(),
-                   selfplay_groups=self.selfplay_groups)
+                   selfplay_groups=self.selfplay_groups, n_lanes=self.n_lanes,
+                   policy_cu_every=int(policy_cu_every))
         bufs = {k: v.data_ptr() for k, v in self.rb.items()}
-        bufs.update({k: v.data_ptr() for k, v in self.io.items()})
-        if self.selfplay_groups > 0:
-            bufs.update({"in_codes_p1": self.io_p1["in_codes"].data_ptr(),
-                         "in_res_p1": self.io_p1["in_res"].data_ptr(),
-                         "out_act16_p1": self.io_p1["out_act16"].data_ptr()})
+        bufs["lanes"] = []
+        for lane in self.lanes:
+            d = {k: v.data_ptr() for k, v in lane["io"].items()}
+            if self.selfplay_groups > 0:
+                d.update({"in_codes_p1": lane["io_p1"]["in_codes"].data_ptr(),
+                          "in_res_p1": lane["io_p1"]["in_res"].data_ptr(),
+                          "out_act16_p1": lane["io_p1"]["out_act16"].data_ptr()})
+            bufs["lanes"].append(d)
         torch.cuda.synchronize()
         self.engine = rt.GpuEngine(cfg, bufs)
         self.started = False
@@ -131,6 +153,8 @@ class GpuActorRuntime:
             "out_action": torch.zeros(E, S, 7, dtype=torch.uint8, device=dev),
             "out_logp": torch.zeros(E, dtype=torch.float32, device=dev),
             "out_value": torch.zeros(E, dtype=torch.float32, device=dev),
+            # dense-head (GridNet) sampling workspace, per lane
+            "cell_logp": torch.zeros(E * S, dtype=torch.float32, device=dev),
         }
 
     def _policy_step(self, io, m, rng):
@@ -156,7 +180,7 @@ class GpuActorRuntime:
                                           io["in_mask"].data_ptr(), st), "decode_obs_mask")
             logits, value = m.policy_value(io["in_obs"])
             cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
-                                 cell_logp=self._cell_logp, logp_out=io["out_logp"])
+                                 cell_logp=io["cell_logp"], logp_out=io["out_logp"])
         io["out_value"].copy_(value)
         N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
                                        io["out_act16"].data_ptr(), N.stream_ptr()),
@@ -200,17 +224,18 @@ class GpuActorRuntime:
         start against a copy of ``learner_flat``; tag their episodes with this id)."""
         if self.selfplay_groups > 0:
             self.engine.set_initial_opponent(int(opponent_version))
-        if learner_flat is not None:
-            self.infer_flat.data.copy_(learner_flat.data)
-            if self.selfplay_groups > 0:
-                self.opp_flat.data.copy_(learner_flat.data)  # until the league picks one
-        for pg in (self.pack_graph, getattr(self, "opp_pack_graph", None)):
-            if pg is not None:
-                pg.replay()
+        for lane in self.lanes:
+            if learner_flat is not None:
+                lane["flat"].data.copy_(learner_flat.data)
+                if self.selfplay_groups > 0:  # until the league picks one
+                    lane["opp_flat"].data.copy_(learner_flat.data)
+            for pg in (lane["pack_graph"], lane.get("opp_pack_graph")):
+                if pg is not None:
+                    pg.replay()
         torch.cuda.synchronize()
         ex = lambda g: int(g.raw_cuda_graph_exec()) if g is not None else 0  # noqa: E731
-        self.engine.start(ex(self.graph), ex(self.opp_graph), ex(self.pack_graph),
-                          ex(getattr(self, "opp_pack_graph", None)))
+        self.engine.start([[ex(ln["graph"]), ex(ln.get("opp_graph")), ex(ln["pack_graph"]),
+                            ex(ln.get("opp_pack_graph"))] for ln in self.lanes])
         self.started = True
 
     def stop(self):
@@ -248,7 +273,8 @@ class GpuActorRuntime:
         self.engine.release(list(slots), N.stream_ptr())
 
     def publish(self, learner_flat: FlatParams) -> bool:
-        return self.engine.publish(learner_flat.data.data_ptr(), self.infer_flat.data.data_ptr(),
+        return self.engine.publish(learner_flat.data.data_ptr(),
+                                   [ln["flat"].data.data_ptr() for ln in self.lanes],
                                    learner_flat.numel * 4, N.stream_ptr())
 
     def set_opponent(self, flat: torch.Tensor, version: int) -> bool:
@@ -257,7 +283,8 @@ class GpuActorRuntime:
         if self.selfplay_groups <= 0:
             raise RuntimeError("set_opponent: runtime has no self-play groups")
         assert flat.numel() == self.opp_flat.numel and flat.dtype == torch.float32
-        return self.engine.publish_opponent(flat.data_ptr(), self.opp_flat.data.data_ptr(),
+        return self.engine.publish_opponent(flat.data_ptr(),
+                                            [ln["opp_flat"].data.data_ptr() for ln in self.lanes],
                                             self.opp_flat.numel * 4, N.stream_ptr(), int(version))
 
     def drain_episodes(self):

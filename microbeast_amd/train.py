@@ -116,7 +116,8 @@ def train(flags: Flags) -> dict:
                              max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
                              bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
                              env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
-                             fp8_policy=flags.fp8_policy or flags.dtype == "fp8")
+                             fp8_policy=flags.fp8_policy or flags.dtype == "fp8",
+                             n_lanes=flags.policy_lanes)
         if sp_groups:
             from .runtime.league import League
 

@@ -20,7 +20,7 @@ def test_engine_rollout_alignment_and_learn(cuda):
     torch.manual_seed(0)
     learner = Learner(mk(), LearnerHParams(), cuda)
     rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=16, unroll=T, batch_slots=1,
-                         device=cuda, n_threads=2)
+                         device=cuda, n_threads=2, n_lanes=2)
     rt.start(learner.flat)
     try:
         prev_last_obs = {}
@@ -47,10 +47,12 @@ def test_engine_rollout_alignment_and_learn(cuda):
         assert st["frames"] > 0 and st["gpu_steps"] > 0 and st["publishes"] >= 1
     finally:
         rt.stop()
-    # inference weights track the learner after a publish
+    # every policy lane's inference weights track the learner after a publish
     torch.cuda.synchronize()
-    d = (rt.infer_flat.data - learner.flat.data).abs().max().item()
-    assert d < 1e-2
+    assert rt.n_lanes == 2
+    for lane in rt.lanes:
+        d = (lane["flat"].data - learner.flat.data).abs().max().item()
+        assert d < 1e-2
 
 
 def test_selfplay_league_engine(cuda):
@@ -69,7 +71,7 @@ def test_selfplay_league_engine(cuda):
     torch.manual_seed(1)
     learner = Learner(mk(), LearnerHParams(), cuda)
     rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=E, unroll=T, batch_slots=1,
-                         device=cuda, n_threads=2, max_steps=12, selfplay_groups=1)
+                         device=cuda, n_threads=2, max_steps=12, selfplay_groups=1, n_lanes=2)
     league = League(capacity=4, snapshot_every=2, eps=0.5, seed=3)
     sid0 = league.add_snapshot(learner.flat.data)
     rt.start(learner.flat, opponent_version=sid0)
