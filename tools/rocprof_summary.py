@@ -15,16 +15,17 @@ def busy_report(trace_csv, window_frac=0.5):
     iv = []
     for r in csv.DictReader(open(trace_csv)):
         try:
-            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "?")))
+            iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", "?"),
+                       r.get("Kernel_Name", "?")))
         except (KeyError, ValueError):
             continue
     if not iv:
         return []
     iv.sort()
-    t_end = max(e for _, e, _ in iv)
+    t_end = max(x[1] for x in iv)
     t0 = iv[0][0] + int((t_end - iv[0][0]) * (1.0 - window_frac))
     busy, cur_s, cur_e = 0, None, None
-    for s, e, _ in iv:
+    for s, e, _, _ in iv:
         if e <= t0:
             continue
         s = max(s, t0)
@@ -37,9 +38,32 @@ def busy_report(trace_csv, window_frac=0.5):
     if cur_e is not None:
         busy += cur_e - cur_s
     span = t_end - t0
-    return [f"### steady-state window ({os.path.basename(trace_csv)}, last {window_frac:.0%} of span)\n",
-            f"span {span / 1e6:.2f} ms, GPU busy (union of kernels) {busy / 1e6:.2f} ms "
-            f"= {100.0 * busy / max(span, 1):.1f} %\n"]
+    out = [f"### steady-state window ({os.path.basename(trace_csv)}, last {window_frac:.0%} of span)\n",
+           f"span {span / 1e6:.2f} ms, GPU busy (union of kernels) {busy / 1e6:.2f} ms "
+           f"= {100.0 * busy / max(span, 1):.1f} %\n"]
+    # per hardware queue (policy stream vs learner stream vs RCCL): union of its kernels
+    for q in sorted({x[2] for x in iv}):
+        qb, cs, ce = 0, None, None
+        names = {}
+        for s, e, qq, nm in iv:
+            if qq != q or e <= t0:
+                continue
+            names[nm] = names.get(nm, 0) + e - max(s, t0)
+            s = max(s, t0)
+            if ce is None or s > ce:
+                if ce is not None:
+                    qb += ce - cs
+                cs, ce = s, e
+            else:
+                ce = max(ce, e)
+        if ce is not None:
+            qb += ce - cs
+        if qb > 0.01 * span:
+            top = max(names, key=names.get).replace("(anonymous namespace)::", "")[:60]
+            out.append(f"- queue {q}: busy {qb / 1e6:.2f} ms = {100.0 * qb / max(span, 1):.1f} % "
+                       f"(largest kernel: `{top}`)")
+    out.append("")
+    return out
 
 
 def main():
