@@ -466,13 +466,21 @@ void MicroRTSSim::set_opponent_actions(const uint8_t* a) {
 
 float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
   float rw[kNumRewards] = {0, 0, 0, 0, 0, 0};
-  // 1) agent actions for idle units, validated against the mask it observed
+  // 1) agent actions for idle units, validated against the mask it observed. Applied in
+  // cell (row-major) order like the per-cell action array, but found from the unit list
+  // (~10-30 units) instead of a scan of every cell: units an action creates are busy and
+  // own units cannot be removed by own actions, so the set is fixed at this point and
+  // exec() re-checks idleness. Same semantics as the scan, a fraction of the memory traffic.
   const int nc = s_ * s_;
-  for (int c = 0; c < nc; ++c) {
-    const int g = grid_[c];
-    if (g < 0) continue;
-    const Unit& u = units_[g];
-    if (u.owner != 0 || u.busy > 0) continue;
+  idle_.clear();
+  for (size_t i = 0; i < units_.size(); ++i) {
+    const Unit& u = units_[i];
+    if (u.alive && u.owner == 0 && u.busy == 0)
+      idle_.push_back(((uint32_t)cell(u.x, u.y) << 16) | (uint32_t)i);
+  }
+  std::sort(idle_.begin(), idle_.end());
+  for (const uint32_t key : idle_) {
+    const int c = (int)(key >> 16), g = (int)(key & 0xFFFFu);
     uint8_t tmp[kActComps];
     const uint8_t* a = actions + (size_t)c * kActComps;
     if (p16_) {  // packed fast path: decode only cells that hold an idle own unit

@@ -70,6 +70,15 @@ class MicroRTSSim {
   void write_obs_dense(float* out) const;   // s*s*27
   void write_mask_dense(uint8_t* out) const;// s*s*78
   int size() const { return s_; }
+  // Software prefetch of the per-step working set (unit list + occupancy grid): the
+  // vec-env steps thousands of sims whose state is cold in cache, and the step is a
+  // chain of dependent misses otherwise
+  void prefetch() const {
+    const char* u = (const char*)units_.data();
+    for (size_t o = 0; o < units_.size() * sizeof(Unit); o += 64) __builtin_prefetch(u + o);
+    const char* g = (const char*)grid_.data();
+    for (size_t o = 0; o < grid_.size() * sizeof(int16_t); o += 64) __builtin_prefetch(g + o);
+  }
   int bot() const { return bot_; }
   void set_bot(int b) { bot_ = b; }
   int winner() const { return last_winner_; }
@@ -117,6 +126,7 @@ class MicroRTSSim {
   std::vector<uint32_t> mask_;    // cached agent mask (s*s*3)
   std::vector<uint32_t> mask_p1_; // cached opponent mask (for self-play / validation)
   std::vector<uint8_t> opp_actions_;
+  std::vector<uint32_t> idle_;    // step scratch: (cell << 16 | unit) of idle agent units
   const uint16_t* p16_ = nullptr;    // step_packed: agent actions decoded lazily per cell
   const uint16_t* opp16_ = nullptr;  // step_packed2: opponent's packed actions
 

@@ -189,13 +189,15 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int PIXB = F8 ? Geo<CIN>::PIXB8 : Geo<CIN>::PIXB;  // bits expanded at staging
   constexpr int NB = COUT / 16;
   constexpr int EPP = BITS ? 1 : CIN / 8;  // staging elements per pixel (u32 / uint4)
-  constexpr int OSTR = COUT + 4;           // pool staging row stride (floats, bank spread)
+  constexpr int OSTR = COUT + 4;           // pool staging row stride (bf16, bank spread)
   const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   char* tile = smem;
   const int tile_bytes = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
-  float* otile = (float*)(smem + tile_bytes);  // pool staging [imgs*HW][OSTR] fp32
+  // pool staging [imgs*HW][OSTR] of the bf16-rounded conv outputs (what y_full holds and
+  // what the pool compares): half the LDS of an fp32 tile, so more images per iteration
+  bf16* otile = (bf16*)(smem + tile_bytes);
   const int ngroups = (a.N + a.imgs - 1) / a.imgs;
   const int per_grp = a.imgs * HW * EPP;
   // pool-fused input: pooled grads + argmax of the group, dense, after the tile
@@ -330,6 +332,15 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       const int mm = valid ? m : 0;
       const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
       const int base_pos = (im * Hp + y) * Wp + x;  // padded position of tap (0,0)
+      // epilogue operands (residual / relu-mask source) requested before the MFMA chain so
+      // their global-load latency overlaps it instead of stalling each block's epilogue
+      uint2 ep_ms[NB], ep_ad[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const size_t gi = (gpix0 + mm) * COUT + nb * 16 + 4 * g;
+        ep_ms[nb] = (a.mask_src && valid) ? *(const uint2*)(a.mask_src + gi) : make_uint2(0, 0);
+        ep_ad[nb] = (a.add && valid) ? *(const uint2*)(a.add + gi) : make_uint2(0, 0);
+      }
       f32x4 acc[NB];
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] * wsc[nb][i] + bias_v[nb][i];
         if (a.mask_src) {
-          const uint2 ms = *(const uint2*)(a.mask_src + gi);
+          const uint2 ms = ep_ms[nb];
           const uint32_t mw[2] = {ms.x, ms.y};
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -375,7 +386,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
           }
         }
         if (a.add) {
-          const uint2 ad = *(const uint2*)(a.add + gi);
+          const uint2 ad = ep_ad[nb];
           const uint32_t aw[2] = {ad.x, ad.y};
 #pragma unroll
           for (int i = 0; i < 4; ++i)
@@ -388,9 +399,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
                  ((uint32_t)__bfloat16_as_ushort(f2bf(v[2 * j + 1])) << 16);
         if (a.pool) {
           // pool over the bf16-rounded values (what y_full holds)
-          *(float4*)(otile + m * OSTR + co0) =
-              make_float4(__uint_as_float(o[0] << 16), __uint_as_float(o[0] & 0xFFFF0000u),
-                          __uint_as_float(o[1] << 16), __uint_as_float(o[1] & 0xFFFF0000u));
+          *(uint2*)(otile + m * OSTR + co0) = make_uint2(o[0], o[1]);
           if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
         } else {
           *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
@@ -415,8 +424,9 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
           for (int kx = 0; kx < 3; ++kx) {
             const int xx = 2 * ox - 1 + kx;
             if (xx < 0 || xx >= W) continue;
-            const float4 v4 = *(const float4*)(otile + ((im * H + yy) * W + xx) * OSTR + 4 * c4);
-            const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+            const uint2 u2 = *(const uint2*)(otile + ((im * H + yy) * W + xx) * OSTR + 4 * c4);
+            const float vv[4] = {__uint_as_float(u2.x << 16), __uint_as_float(u2.x & 0xFFFF0000u),
+                                 __uint_as_float(u2.y << 16), __uint_as_float(u2.y & 0xFFFF0000u)};
 #pragma unroll
             for (int j = 0; j < 4; ++j)  // first max in scan order (ATen)
               if (vv[j] > mx[j] || am[j] < 0) { mx[j] = vv[j]; am[j] = ky * 3 + kx; }
@@ -929,7 +939,7 @@ inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, boo
   (void)bits;  // bit planes are staged expanded (cin = 32)
   const int pixb = fp8 ? cin + 8 : cin * 2 + 16;
   size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
-  if (pool) t += (size_t)imgs * H * W * (cout + 4) * 4;
+  if (pool) t += (size_t)imgs * H * W * (cout + 4) * 2;
   if (unpool) {
     const size_t pp = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * cin;
     t += ((pp * 2 + 15) & ~(size_t)15) + ((pp + 15) & ~(size_t)15);

@@ -77,6 +77,15 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
                               int32_t* res, float* reward, uint8_t* done, EpisodeLog* log) {
   const size_t S = (size_t)size_ * size_;
   for (int i = e0; i < e1; ++i) {
+    // two envs ahead: the sim object; one ahead: its unit list and grid
+    if (i + 2 < e1) __builtin_prefetch(sims_[i + 2].get());
+    if (i + 1 < e1) {
+      sims_[i + 1]->prefetch();
+      for (size_t o = 0; o < S * 2; o += 64) {  // next env's action row + codes row (write)
+        __builtin_prefetch((const char*)(actions + (i + 1) * S) + o);
+        __builtin_prefetch((char*)(codes + (i + 1) * S) + o, 1);
+      }
+    }
     bool d = false;
     const float r = sims_[i]->step_packed(actions + (size_t)i * S, &d);
     ep_ret_[i] += r;
@@ -99,6 +108,8 @@ void VecEnv::step_range_codes_sp(int e0, int e1, const uint16_t* actions,
                                  uint8_t* done, EpisodeLog* log, int opponent) {
   const size_t S = (size_t)size_ * size_;
   for (int i = e0; i < e1; ++i) {
+    if (i + 2 < e1) __builtin_prefetch(sims_[i + 2].get());
+    if (i + 1 < e1) sims_[i + 1]->prefetch();
     MicroRTSSim& sim = *sims_[i];
     const bool sp = sim.external_opponent();
     bool d = false;

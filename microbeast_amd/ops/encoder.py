@@ -62,7 +62,7 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
     pixb = (cin + 8) if fp8 else (cin * 2 + 16)  # bit planes are expanded in LDS
     imgs = max(1, 512 // hw)
     while imgs > 1:
-        sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * (cout + 4) * 4 if pool else 0)
+        sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * (cout + 4) * 2 if pool else 0)
         if sm <= 48 * 1024 and imgs * hw * epp <= _PF_FWD:
             break
         imgs //= 2
