@@ -63,7 +63,6 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     } else {
       CTOR_CHECK(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, prio_greatest));
     }
-    CTOR_CHECK(hipMalloc((void**)&L.d_rd, E * 4 + E + 64));
   }
   CTOR_CHECK(hipHostMalloc((void**)&h_codes_, (size_t)total * S_ * 2, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_res_, (size_t)total * 4, hipHostMallocDefault));
@@ -137,7 +136,6 @@ GpuEngine::~GpuEngine() {
   if (h_reward_) hipHostFree(h_reward_);
   if (h_done_) hipHostFree(h_done_);
   for (Lane& L : lanes_) {
-    if (L.d_rd) hipFree(L.d_rd);
     if (L.stream) hipStreamDestroy(L.stream);
   }
 }
@@ -319,10 +317,6 @@ bool GpuEngine::enqueue_gpu(int g) {
                            hipMemcpyHostToDevice, st));
   ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
                            st));
-  if (!G.first) {
-    ENG_CHECK(hipMemcpyAsync(L.d_rd, h_reward_ + e0, E * 4, hipMemcpyHostToDevice, st));
-    ENG_CHECK(hipMemcpyAsync(L.d_rd + E * 4, h_done_ + e0, E, hipMemcpyHostToDevice, st));
-  }
   {
     const auto t0 = std::chrono::steady_clock::now();
     ENG_CHECK(hipGraphLaunch(L.graph, st));
@@ -364,10 +358,13 @@ bool GpuEngine::enqueue_gpu(int g) {
   seg[n++] = {(const void*)io.out_logp, f32_at(buf_.logp, G.cur, t), E * 4};
   seg[n++] = {(const void*)io.out_value, f32_at(buf_.value, G.cur, t), E * 4};
   if (!G.first) {
+    // reward / done of the env step that just finished, read by the scatter kernel straight
+    // from pinned host memory (two fewer blit launches per step); the group's envs do not
+    // write them again before G.ev, which is recorded after this kernel
     const int rs = t > 0 ? G.cur : G.prev;
     const size_t ri = t > 0 ? t - 1 : T - 1;
-    seg[n++] = {(const void*)L.d_rd, f32_at(buf_.reward, rs, ri), E * 4};
-    seg[n++] = {(const void*)(L.d_rd + E * 4), u8_at(buf_.done, rs, ri), E};
+    seg[n++] = {(const void*)(h_reward_ + e0), f32_at(buf_.reward, rs, ri), E * 4};
+    seg[n++] = {(const void*)(h_done_ + e0), u8_at(buf_.done, rs, ri), E};
   }
   const bool close_prev = (t == 0 && G.prev >= 0);
   if (close_prev) {

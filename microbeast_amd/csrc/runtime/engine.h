@@ -181,7 +181,6 @@ class GpuEngine {
     hipGraphExec_t graph = nullptr, opp_graph = nullptr;
     hipGraphExec_t pack_graph[2] = {nullptr, nullptr};
     LaneIO io;
-    uint8_t* d_rd = nullptr;  // device staging for reward+done of one group
     int opp_version = -1;     // driver thread only
   };
 
