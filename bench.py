@@ -35,10 +35,10 @@ def parse(argv=None):
     p.add_argument("--size", type=int, default=16)
     p.add_argument("--arch", type=str, default="impala_flat",
                    help="impala_flat (headline) | gridnet (BASELINE config 2) | impala_deep")
-    p.add_argument("--groups", type=int, default=4)
+    p.add_argument("--groups", type=int, default=2)
     p.add_argument("--lanes", type=int, default=1,
                    help="concurrent policy streams, each with its own graph + I/O")
-    p.add_argument("--envs_per_group", type=int, default=4096)
+    p.add_argument("--envs_per_group", type=int, default=8192)
     p.add_argument("--unroll", type=int, default=64)
     p.add_argument("--batch_slots", type=int, default=1)
     p.add_argument("--threads", type=int, default=0, help="env worker threads per rank (0=auto)")
