@@ -234,6 +234,11 @@ def main(argv=None):
         }
         if phase:
             out["learner_phase_s"] = phase
+        nt = st1.get("timed_steps", 0) - st0.get("timed_steps", 0)
+        if nt > 0:  # MBK_STEP_TIMING=1: GPU-side split of a policy step's own stream time
+            out["policy_step_gpu_ms"] = {
+                k: round(1e3 * (st1[f"step_{k}_s"] - st0[f"step_{k}_s"]) / nt, 3)
+                for k in ("h2d", "graph", "out")}
         print(json.dumps(out), flush=True)
     D.destroy(info)
     return 0

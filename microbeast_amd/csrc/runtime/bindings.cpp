@@ -302,6 +302,10 @@ PYBIND11_MODULE(_mbrt, m) {
         d["slots_full"] = s.slots_full;
         d["driver_idle_s"] = s.driver_idle_s;
         d["gpu_phase_s"] = s.gpu_phase_s;
+        d["step_h2d_s"] = s.step_h2d_s;
+        d["step_graph_s"] = s.step_graph_s;
+        d["step_out_s"] = s.step_out_s;
+        d["timed_steps"] = s.timed_steps;
         d["env_phase_s"] = s.env_phase_s;
         d["enqueue_s"] = s.enqueue_s;
         d["graph_launch_s"] = s.graph_launch_s;

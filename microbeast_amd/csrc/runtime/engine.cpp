@@ -2,6 +2,7 @@
 
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -88,9 +89,15 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   env_->set_validate(false);  // masks are derived on the GPU from the codes
   env_->reset_codes(h_codes_, h_res_);
   if (cfg_.selfplay_groups > 0) env_->reset_codes_p1(h_codes_p1_, h_res_p1_);
+  {
+    const char* st = std::getenv("MBK_STEP_TIMING");
+    step_timing_ = st && st[0] == '1';
+  }
   for (int g = 0; g < cfg_.n_groups; ++g) {
     groups_.emplace_back(new Group());
     CTOR_CHECK(hipEventCreateWithFlags(&groups_[g]->ev, hipEventDisableTiming));
+    if (step_timing_)
+      for (auto& e : groups_[g]->tev) CTOR_CHECK(hipEventCreate(&e));
     groups_[g]->selfplay = g >= sp0;
     groups_[g]->lane = g % cfg_.n_lanes;
     groups_[g]->phase.store(READY);  // reset observations are ready
@@ -118,7 +125,11 @@ GpuEngine::~GpuEngine() {
   stop();
   for (Lane& L : lanes_)
     if (L.stream) hipStreamSynchronize(L.stream);
-  for (auto& g : groups_) if (g->ev) hipEventDestroy(g->ev);
+  for (auto& g : groups_) {
+    if (g->ev) hipEventDestroy(g->ev);
+    for (auto e : g->tev)
+      if (e) hipEventDestroy(e);
+  }
   for (auto e : full_ev_) hipEventDestroy(e);
   for (auto e : release_ev_) hipEventDestroy(e);
   for (PubChan& c : pub_) {
@@ -194,6 +205,19 @@ void GpuEngine::dispatch_env(int g) {
       std::chrono::duration_cast<std::chrono::nanoseconds>(now - G.t_phase).count(),
       std::memory_order_relaxed);
   G.t_phase = now;
+  if (G.timed) {  // the step's events are complete (G.ev, recorded after them, is)
+    float ms[3] = {0.f, 0.f, 0.f};
+    bool ok = true;
+    for (int i = 0; i < 3; ++i)
+      ok = ok && hipEventElapsedTime(&ms[i], G.tev[i], G.tev[i + 1]) == hipSuccess;
+    if (ok) {
+      step_h2d_ns_.fetch_add((int64_t)(ms[0] * 1e6), std::memory_order_relaxed);
+      step_graph_ns_.fetch_add((int64_t)(ms[1] * 1e6), std::memory_order_relaxed);
+      step_out_ns_.fetch_add((int64_t)(ms[2] * 1e6), std::memory_order_relaxed);
+      timed_steps_.fetch_add(1, std::memory_order_relaxed);
+    }
+    G.timed = false;
+  }
   G.phase.store(ENV_BUSY, std::memory_order_release);
   G.remaining.store(cfg_.envs_per_group, std::memory_order_release);
   G.next_env.store(0, std::memory_order_release);
@@ -313,10 +337,13 @@ bool GpuEngine::enqueue_gpu(int g) {
     G.cur = slot;
   }
   const size_t e0 = (size_t)g * E;
+  G.timed = step_timing_;
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], st));
   ENG_CHECK(hipMemcpyAsync((void*)io.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
                            hipMemcpyHostToDevice, st));
   ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
                            st));
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
   {
     const auto t0 = std::chrono::steady_clock::now();
     ENG_CHECK(hipGraphLaunch(L.graph, st));
@@ -333,6 +360,7 @@ bool GpuEngine::enqueue_gpu(int g) {
     G.opp_version = L.opp_version;
   }
 
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[2], st));
   // scatter this step into the HBM rollout slot(s)
   MbkCopySeg seg[MBK_MAX_COPY_SEGS];
   int n = 0;
@@ -387,6 +415,7 @@ bool GpuEngine::enqueue_gpu(int g) {
   if (G.selfplay)
     ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
                              hipMemcpyDeviceToHost, st));
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], st));
   ENG_CHECK(hipEventRecord(G.ev, st));
   gpu_steps_.fetch_add(1);
   G.t += 1;
@@ -526,6 +555,10 @@ EngineStats GpuEngine::stats() const {
   s.slots_full = slots_full_.load();
   s.env_s = env_ns_.load() * 1e-9;
   s.gpu_phase_s = gpu_phase_ns_.load() * 1e-9;
+  s.step_h2d_s = step_h2d_ns_.load() * 1e-9;
+  s.step_graph_s = step_graph_ns_.load() * 1e-9;
+  s.step_out_s = step_out_ns_.load() * 1e-9;
+  s.timed_steps = timed_steps_.load();
   s.env_phase_s = env_phase_ns_.load() * 1e-9;
   s.enqueue_s = enqueue_ns_.load() * 1e-9;
   s.graph_launch_s = launch_ns_.load() * 1e-9;

@@ -110,6 +110,10 @@ struct EngineStats {
   double env_phase_s = 0.0;
   double enqueue_s = 0.0;       // driver thread time inside enqueue (HIP API calls)
   double graph_launch_s = 0.0;  // of which hipGraphLaunch of the policy graph(s)
+  // MBK_STEP_TIMING=1: GPU-side split of each policy step's own stream time (timing events):
+  // H2D of codes/resources, policy graph(s), rollout scatter + D2H of actions
+  double step_h2d_s = 0.0, step_graph_s = 0.0, step_out_s = 0.0;
+  int64_t timed_steps = 0;
   int64_t publishes = 0;
   int64_t opp_publishes = 0;
   int opp_version = -1;
@@ -163,6 +167,8 @@ class GpuEngine {
     int opp_version = -1;  // league id of the opponent that chose this step's p1 actions
     int lane = 0;
     hipEvent_t ev = nullptr;
+    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};  // MBK_STEP_TIMING events
+    bool timed = false;                                         // tev recorded this step
     std::chrono::steady_clock::time_point t_phase;  // start of the current phase
     std::atomic<int64_t> t_ready_ns{0};              // worker: when the env phase ended
   };
@@ -232,6 +238,8 @@ class GpuEngine {
   std::atomic<int> opp_version_pub_{-1};
   std::atomic<int64_t> env_ns_{0};
   std::atomic<int64_t> gpu_phase_ns_{0}, env_phase_ns_{0}, enqueue_ns_{0}, launch_ns_{0};
+  bool step_timing_ = false;
+  std::atomic<int64_t> step_h2d_ns_{0}, step_graph_ns_{0}, step_out_ns_{0}, timed_steps_{0};
   double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
   mutable std::mutex stats_m_;
 
