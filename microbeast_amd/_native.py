@@ -56,6 +56,7 @@ _SIGS = {
                        c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "mbk_conv_set_grid_cap": [c_int],
+    "mbk_conv0_row_set": [c_int],
     "mbk_set_cu_budget": [c_int],
     "mbk_get_cu_budget": [],
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],

@@ -447,6 +447,153 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   }
 }
 
+
+// ------------------------------------------------------------------ first conv, W == 16
+// Stage-0 conv of the 16-wide maps straight from the uint32 bit planes, without an LDS
+// im2col tile. One image row is exactly one 16-pixel MFMA block (lane li = pixel x), so a
+// wave owns one image and walks its rows keeping the expanded input rows y-1 .. y+2 in
+// VGPRs: every input pixel is read from HBM and expanded once (the generic kernel issues
+// 9 LDS fragment reads per 16-pixel block, profile 12: LDS-bound at 11 % MFMA). The kx = 0
+// and kx = 2 taps are the same row shifted by one pixel: DPP row_shr:1 / row_shl:1 move
+// lane x-1 / x+1 into lane x inside each 16-lane row, and their zero fill at the row ends
+// is the conv's zero padding. Two output rows per iteration give two independent MFMA
+// chains; each chain runs the taps in the generic kernel's order, so results are
+// bit-identical to it. Conv outputs (+bias, bf16) go to an LDS staging tile and the
+// 3x3/2 max-pool (+argmax) runs over the workgroup's images as in conv_fwd_kernel.
+constexpr int kRowImgs = kThreads / 64;  // images per workgroup iteration: one per wave
+
+__device__ __forceinline__ uint32_t dpp_shr1(uint32_t v) {  // lane x <- lane x-1 (x=0: 0)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_shl1(uint32_t v) {  // lane x <- lane x+1 (x=15: 0)
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xF, 0xF, false);
+}
+__device__ __forceinline__ bf16x8 shr_px(const Frag8& f) {
+  Frag8 o;
+  o.u = make_uint4(dpp_shr1(f.u.x), dpp_shr1(f.u.y), dpp_shr1(f.u.z), dpp_shr1(f.u.w));
+  return o.v;
+}
+__device__ __forceinline__ bf16x8 shl_px(const Frag8& f) {
+  Frag8 o;
+  o.u = make_uint4(dpp_shl1(f.u.x), dpp_shl1(f.u.y), dpp_shl1(f.u.z), dpp_shl1(f.u.w));
+  return o.v;
+}
+
+__global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int COUT = 16, OSTR = COUT + 4, W = 16;
+  const int H = a.H, HW = H * W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  bf16* otile = (bf16*)smem;  // [kRowImgs * HW][OSTR] bf16 conv outputs (pool mode)
+  Frag8 bw[9];                // A fragments: w[co = li][tap][8g .. 8g+7]
+  {
+    const uint4* wp = (const uint4*)(a.w + (size_t)li * 9 * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < 9; ++c) bw[c].u = wp[c * 4];
+  }
+  float bias_v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias_v[i] = a.bias ? a.bias[4 * g + i] : 0.f;
+  const int ngroups = (a.N + kRowImgs - 1) / kRowImgs;
+
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * kRowImgs;
+    const int nimg = min(kRowImgs, a.N - img0);
+    if (wave < nimg) {
+      const int im = wave;
+      const uint32_t* xb = (const uint32_t*)a.x + (size_t)(img0 + im) * HW + li;
+      auto row = [&](uint32_t bits) {
+        Frag8 f;
+        f.u = expand_bits8(bits >> (8 * g));
+        return f;
+      };
+      Frag8 r[4];  // expanded input rows y-1, y, y+1, y+2 (zero outside the image)
+      r[0].u = make_uint4(0, 0, 0, 0);
+      r[1] = row(xb[0]);
+      r[2] = row(H > 1 ? xb[W] : 0u);
+      r[3] = row(H > 2 ? xb[2 * W] : 0u);
+      for (int y = 0; y < H; y += 2) {
+        const uint32_t n0 = y + 3 < H ? xb[(y + 3) * W] : 0u;  // next iteration's rows
+        const uint32_t n1 = y + 4 < H ? xb[(y + 4) * W] : 0u;
+        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const bf16x8 l0 = shr_px(r[ky]), l1 = shr_px(r[ky + 1]);
+          const bf16x8 h0 = shl_px(r[ky]), h1 = shl_px(r[ky + 1]);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky].v, l0, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky].v, l1, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 1].v, r[ky].v, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 1].v, r[ky + 1].v, acc1, 0, 0, 0);
+          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 2].v, h0, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 2].v, h1, acc1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int yy = y + h;
+          if (yy >= H) break;
+          const f32x4& acc = h ? acc1 : acc0;
+          uint32_t o[2];
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j] * 1.f + bias_v[2 * j])) |
+                   ((uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j + 1] * 1.f + bias_v[2 * j + 1]))
+                    << 16);
+          const int m = yy * W + li;
+          const size_t gi = ((size_t)(img0 + im) * HW + m) * COUT + 4 * g;
+          if (a.pool) {
+            *(uint2*)(otile + (im * HW + m) * OSTR + 4 * g) = make_uint2(o[0], o[1]);
+            if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
+          } else {
+            *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
+          }
+        }
+        r[0] = r[2];
+        r[1] = r[3];
+        r[2] = row(n0);
+        r[3] = row(n1);
+      }
+    }
+    if (a.pool) {
+      __syncthreads();
+      const int Ho = (H + 1) >> 1, Wo = W >> 1;
+      constexpr int C4 = COUT / 4;
+      const int tot = nimg * Ho * Wo * C4;
+      const size_t obase = (size_t)img0 * Ho * Wo * COUT;
+      for (int e = tid; e < tot; e += kThreads) {
+        const int c4 = e % C4, p = e / C4;
+        const int im = p / (Ho * Wo), rr = p - im * Ho * Wo, oy = rr / Wo, ox = rr - oy * Wo;
+        float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        int am[4] = {-1, -1, -1, -1};
+        for (int ky = 0; ky < 3; ++ky) {
+          const int yy = 2 * oy - 1 + ky;
+          if (yy < 0 || yy >= H) continue;
+          for (int kx = 0; kx < 3; ++kx) {
+            const int xx = 2 * ox - 1 + kx;
+            if (xx < 0 || xx >= W) continue;
+            const uint2 u2 = *(const uint2*)(otile + ((im * H + yy) * W + xx) * OSTR + 4 * c4);
+            const float vv[4] = {__uint_as_float(u2.x << 16), __uint_as_float(u2.x & 0xFFFF0000u),
+                                 __uint_as_float(u2.y << 16), __uint_as_float(u2.y & 0xFFFF0000u)};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)  // first max in scan order (ATen)
+              if (vv[j] > mx[j] || am[j] < 0) { mx[j] = vv[j]; am[j] = ky * 3 + kx; }
+          }
+        }
+        const size_t oi = obase + (size_t)p * COUT + 4 * c4;
+        const uint32_t o0 = (uint32_t)__bfloat16_as_ushort(f2bf(mx[0])) |
+                            ((uint32_t)__bfloat16_as_ushort(f2bf(mx[1])) << 16);
+        const uint32_t o1 = (uint32_t)__bfloat16_as_ushort(f2bf(mx[2])) |
+                            ((uint32_t)__bfloat16_as_ushort(f2bf(mx[3])) << 16);
+        *(uint2*)(a.y + oi) = make_uint2(o0, o1);
+        if (a.pool_idx)
+          *(uint32_t*)(a.pool_idx + oi) =
+              (uint32_t)am[0] | ((uint32_t)am[1] << 8) | ((uint32_t)am[2] << 16) | ((uint32_t)am[3] << 24);
+      }
+      __syncthreads();  // otile reads done before the next group overwrites it
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 struct ConvWgradArgs {
   const void* x;
@@ -961,6 +1108,7 @@ inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool 
 }
 
 int g_grid_cap = 0;    // tests force multi-group workgroups with a small cap
+int g_conv0_row = 1;   // stage-0 conv of 16-wide maps on conv0_row_kernel (0: generic kernel)
 int g_cu_budget = 0;   // CUs a persistent grid is sized for (0 = all); set when the learner
                        // runs on a CU-masked stream so its grid fits the masked CUs exactly
 
@@ -1018,6 +1166,15 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
       hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
+    return (int)hipGetLastError();
+  }
+  if (in_bits && cout == 16 && W == 16 && !fp8 && g_conv0_row && !add && !mask_src &&
+      !relu_in) {
+    const size_t sm0 = pool ? (size_t)kRowImgs * H * 16 * (16 + 4) * 2 : 0;
+    if (sm0 > 160 * 1024) return (int)hipErrorInvalidValue;
+    const int grid = std::min((N + kRowImgs - 1) / kRowImgs,
+                              resident_blocks((const void*)conv0_row_kernel, sm0));
+    hipLaunchKernelGGL(conv0_row_kernel, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();
   }
   if (in_bits) {
@@ -1117,6 +1274,7 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
 }
 
 extern "C" void mbk_conv_set_grid_cap(int cap) { g_grid_cap = cap; }
+extern "C" void mbk_conv0_row_set(int on) { g_conv0_row = on; }
 extern "C" void mbk_set_cu_budget(int n) { g_cu_budget = n; }
 extern "C" int mbk_get_cu_budget() { return g_cu_budget; }
 

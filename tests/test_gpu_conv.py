@@ -351,3 +351,45 @@ def test_pool_bwd_idx_shapes(cuda, H, W, C):
     ct = c.clone().requires_grad_(True)
     F.max_pool2d(ct, 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
     torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,pool", [(203, True), (7, True), (9, False)])
+def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool):
+    """The 16-wide stage-0 conv (register row window + DPP pixel shifts) runs the MFMA taps
+    in the generic kernel's order: outputs, pre-pool values and argmax bytes are identical."""
+    from microbeast_amd import _native as N
+    from microbeast_amd.ops.encoder import HipEncoder
+    torch.manual_seed(3)
+    enc = HipEncoder(16, 16, 27, (16, 32, 32), cuda)
+    ws = [torch.randn(L.cout, L.cin_real, 3, 3, device=cuda) * 0.2 for L in enc.layers]
+    enc.pack(ws, with_bwd=False)
+    L0 = enc.layers[0]
+    obs = _random_obs_bits(n, 256, seed=n).to(cuda)
+    b0 = torch.randn(16, device=cuda) * 0.1
+    outs = []
+    for on in (1, 0):
+        N.kernels().mbk_conv0_row_set(on)
+        try:
+            if pool:
+                cfull = torch.full((n, 16, 16, 16), 7.0, dtype=torch.bfloat16, device=cuda)
+                pidx = torch.full((n, 8, 8, 16), 255, dtype=torch.uint8, device=cuda)
+                p = enc._fwd(L0, obs, b0, y_full=cfull, pool_idx=pidx)
+                outs.append((p, cfull, pidx))
+            else:  # raw launch without the pool (the encoder always pools stage convs)
+                y = torch.empty(n, 16, 16, 16, dtype=torch.bfloat16, device=cuda)
+                N.check(N.kernels().mbk_conv_fwd(
+                    obs.data_ptr(), 1, L0.cin, L0.cout, enc.packed_fwd.data_ptr() + 2 * L0.w_off,
+                    b0.data_ptr(), 0, 0, y.data_ptr(), 0, 0, n, 16, 16, 4, 0, 0,
+                    N.stream_ptr()), "conv_fwd")
+                outs.append((y,))
+        finally:
+            N.kernels().mbk_conv0_row_set(1)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    if not pool:
+        from microbeast_amd.ops.obs import bits_to_planes
+        cr = F.conv2d(bits_to_planes(obs.cpu(), 16, 16), ws[0].cpu().bfloat16().float(), b0.cpu(),
+                      padding=1)
+        torch.testing.assert_close(outs[0][0].float().cpu().permute(0, 3, 1, 2), cr, rtol=2e-2,
+                                   atol=2e-2)
