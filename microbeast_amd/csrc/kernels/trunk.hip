@@ -130,30 +130,15 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
 #pragma unroll
     for (int i = 0; i < 4; ++i) bv[nb][i] = bias[nb * 16 + 4 * g + i];
   const int M = nimg * HW, nblk = (M + 15) >> 4;
-  for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+  constexpr int NW = kThreads / 64;
+  // Two pixel blocks per wave iteration (pb, pb + NW): two independent MFMA chains and
+  // their LDS fragment reads interleave, so neither the MFMA dependency latency of one
+  // accumulator chain nor the LDS read latency is exposed per block. Each chain runs the
+  // taps in the same order as before (bit-identical results).
+  auto epilogue = [&](int pb, const f32x4* acc) {
     const int m = pb * 16 + li;
-    const bool valid = m < M;
-    const int mm = valid ? m : 0;
-    const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
-    const int base = (im * Hp + y) * Wp + x;
-    f32x4 acc[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      int tap, ch0;
-      if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
-      else { tap = c; ch0 = 8 * g; }
-      const int tapc = tap < 9 ? tap : 8;
-      Frag8 a;
-      a.u = *(const uint4*)(in + (base + (tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2);
-      if (relu_in) a.u = make_uint4(relu2(a.u.x), relu2(a.u.y), relu2(a.u.z), relu2(a.u.w));
-      if (!valid || (CIN == 16 && tap >= 9)) a.u = make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, a.v, acc[nb], 0, 0, 0);
-    }
-    if (!valid) continue;
+    if (pb >= nblk || m >= M) return;
+    const int im = m / HW, r = m - im * HW, y = r / W, x = r - y * W;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const int co0 = nb * 16 + 4 * g;
@@ -171,6 +156,45 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
         *(uint2*)p = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
+  };
+  for (int pb0 = wave; pb0 < nblk; pb0 += 2 * NW) {
+    int base[2];
+    bool valid[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = (pb0 + j * NW) * 16 + li;
+      valid[j] = m < M;
+      const int mm = valid[j] ? m : 0;
+      const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
+      base[j] = (im * Hp + y) * Wp + x;
+    }
+    f32x4 acc[2][NB];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[j][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      int tap, ch0;
+      if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
+      else { tap = c; ch0 = 8 * g; }
+      const int tapc = tap < 9 ? tap : 8;
+      const int toff = (tapc / 3) * Wp + (tapc % 3);
+      Frag8 a[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        a[j].u = *(const uint4*)(in + (base[j] + toff) * PI + ch0 * 2);
+        if (relu_in) a[j].u = make_uint4(relu2(a[j].u.x), relu2(a[j].u.y), relu2(a[j].u.z), relu2(a[j].u.w));
+        if (!valid[j] || (CIN == 16 && tap >= 9)) a[j].u = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, a[j].v, acc[j][nb], 0, 0, 0);
+    }
+    epilogue(pb0, acc[0]);
+    epilogue(pb0 + NW, acc[1]);
   }
 }
 
