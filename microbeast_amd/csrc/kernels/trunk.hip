@@ -43,10 +43,15 @@ union Frag8 {
   uint4 u;
 };
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+// relu of a bf16 pair in ONE v_pk_max_i16: a bf16 with the sign bit set is a negative
+// int16 (-0.0 = 0x8000 too), a non-negative one a non-negative int16, so the signed max
+// with 0 is exactly relu (the bit-select form costs ~6 VALU per dword, and the trunk
+// re-applies relu for all 9 taps of every input pixel: profile 15, VALU-bound)
 __device__ __forceinline__ uint32_t relu2(uint32_t w) {
-  const uint32_t lo = (w & 0x8000u) ? 0u : (w & 0xFFFFu);
-  const uint32_t hi = (w & 0x80000000u) ? 0u : (w & 0xFFFF0000u);
-  return lo | hi;
+  s16x2 v = __builtin_bit_cast(s16x2, w);
+  v = __builtin_elementwise_max(v, s16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, v);
 }
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(a)) |
@@ -135,10 +140,15 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
   // their LDS fragment reads interleave, so neither the MFMA dependency latency of one
   // accumulator chain nor the LDS read latency is exposed per block. Each chain runs the
   // taps in the same order as before (bit-identical results).
+  // pixel -> (image, y, x) with float reciprocals (exact for m < 2^16, HW <= 1024: the
+  // distance of (m + 0.5) / HW to an integer is >= 0.5 / HW, far above the rounding error);
+  // the integer divisions by runtime H*W / W cost ~20 VALU per block (profile 15: VALU-bound)
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   auto epilogue = [&](int pb, const f32x4* acc) {
     const int m = pb * 16 + li;
     if (pb >= nblk || m >= M) return;
-    const int im = m / HW, r = m - im * HW, y = r / W, x = r - y * W;
+    const int im = (int)(((float)m + 0.5f) * inv_hw), r = m - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       const int co0 = nb * 16 + 4 * g;
@@ -159,13 +169,12 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
   };
   for (int pb0 = wave; pb0 < nblk; pb0 += 2 * NW) {
     int base[2];
-    bool valid[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int m = (pb0 + j * NW) * 16 + li;
-      valid[j] = m < M;
-      const int mm = valid[j] ? m : 0;
-      const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
+      const int mm = m < M ? m : 0;  // rows past M compute garbage that is never stored
+      const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+      const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
       base[j] = (im * Hp + y) * Wp + x;
     }
     f32x4 acc[2][NB];
@@ -185,7 +194,8 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
       for (int j = 0; j < 2; ++j) {
         a[j].u = *(const uint4*)(in + (base[j] + toff) * PI + ch0 * 2);
         if (relu_in) a[j].u = make_uint4(relu2(a[j].u.x), relu2(a[j].u.y), relu2(a[j].u.z), relu2(a[j].u.w));
-        if (!valid[j] || (CIN == 16 && tap >= 9)) a[j].u = make_uint4(0, 0, 0, 0);
+        // (CIN 16, tap 9 = the pad half of chunk 4: its packed weights are zero, so the
+        // finite pixel read for it adds exactly 0 and needs no zeroing)
       }
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
