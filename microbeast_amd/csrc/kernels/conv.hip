@@ -45,11 +45,13 @@ constexpr int kThreads = 256;
 __device__ __forceinline__ float bf2f(bf16 v) { return __bfloat162float(v); }
 __device__ __forceinline__ bf16 f2bf(float v) { return __float2bfloat16(v); }
 
+typedef short s16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t relu_bf16x2(uint32_t w) {
-  // bf16 pair: negative (sign bit set) -> +0; NaN propagates as is (never produced)
-  uint32_t lo = (w & 0x8000u) ? 0u : (w & 0xFFFFu);
-  uint32_t hi = (w & 0x80000000u) ? 0u : (w & 0xFFFF0000u);
-  return lo | hi;
+  // bf16 pair: sign bit set (negative, -0) -> +0 as ONE v_pk_max_i16 (a bf16 with the
+  // sign bit set is a negative int16, a non-negative one a non-negative int16)
+  s16x2 v = __builtin_bit_cast(s16x2, w);
+  v = __builtin_elementwise_max(v, s16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 union Frag8 {
@@ -191,6 +193,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   constexpr int EPP = BITS ? 1 : CIN / 8;  // staging elements per pixel (u32 / uint4)
   constexpr int OSTR = COUT + 4;           // pool staging row stride (bf16, bank spread)
   const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   char* tile = smem;
@@ -329,8 +332,11 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     for (int pb = wave; pb < nblk; pb += kThreads / 64) {
       const int m = pb * 16 + li;  // this lane's pixel (B column)
       const bool valid = m < M;
-      const int mm = valid ? m : 0;
-      const int im = mm / HW, r = mm - im * HW, y = r / W, x = r - y * W;
+      const int mm = valid ? m : 0;  // rows past M compute garbage that is never stored
+      // float-reciprocal index math (exact here, see trunk.hip conv_lds): the integer
+      // divisions by runtime H*W / W are ~20 VALU per block
+      const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+      const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
       const int base_pos = (im * Hp + y) * Wp + x;  // padded position of tap (0,0)
       // epilogue operands (residual / relu-mask source) requested before the MFMA chain so
       // their global-load latency overlaps it instead of stalling each block's epilogue
@@ -352,16 +358,15 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
         else { tap = c; ch0 = 8 * g; }
         const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
         const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
-        const bool zero = !valid || (CIN == 16 && tap >= 9);
+        // no zeroing: the CIN-16 pad tap has zero packed weights and rows past M are not
+        // stored, so the (finite) fragment read for them cannot change a stored output
         if constexpr (F8) {
           long a8 = *(const long*)(tile + pos * PIXB + ch0);
-          if (zero) a8 = 0;
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bw8[c][nb], a8, acc[nb], 0, 0, 0);
         } else {
           av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
-          if (zero) av.u = make_uint4(0, 0, 0, 0);
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, av.v, acc[nb], 0, 0, 0);
