@@ -632,6 +632,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int XEPP = BITS ? 1 : CIN / 8;  // X staging elements per pixel (u32 / uint4)
   constexpr int DCH = COUT / 8;             // dY uint4 per pixel
   const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = (lane >> 4), li = lane & 15;
   // LDS carve: [X tile | zero row (64B) | dY tile | zero row]; reused for the final reduce
@@ -775,7 +776,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         const int p = kb * 32 + 8 * G + 4 * h + (li >> 2);
         ok[h] = p < M;
         const int pp = ok[h] ? p : 0;
-        const int im = pp / HW, r = pp - im * HW, y = r / W, x = r - y * W;
+        // float-reciprocal index math (exact here, see conv_fwd_kernel)
+        const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
         xpos[h] = (im * Hp + y) * Wp + x;
         dptr[h] = ok[h] ? dt + pp * DPB : dzero;
       }
