@@ -111,16 +111,24 @@ __global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __
     m[0] = w[0];
     m[1] = w[1];
     m[2] = w[2];
-    if (BUCKET) {
-      const size_t fc = e * S + c;
-      if (w[0] | w[1] | w[2]) {
-        const int slot = atomicAdd(&bk.cnt[c], 1);
-        bk.bucket[(size_t)c * gridDim.x + slot] = (int)e;
-      } else {
-        bk.cell_lp[fc] = 0.f;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) bk.action[fc * 7 + k] = 0;
-      }
+    if (BUCKET && (w[0] | w[1] | w[2])) {
+      const int slot = atomicAdd(&bk.cnt[c], 1);
+      bk.bucket[(size_t)c * gridDim.x + slot] = (int)e;
+    }
+  }
+  if (BUCKET) {
+    // every cell's log-prob and 7 action bytes start at zero; the sparse head overwrites the
+    // active cells later in stream order. Whole-env zeroing with 16-byte stores (the env's
+    // S*7 action bytes and S floats are contiguous) instead of 1 + 7 scalar byte stores per
+    // inactive cell: profile 18, decode was 10 % of the bench's GPU time
+    if ((S & 15) == 0 && (((uintptr_t)bk.action | (uintptr_t)bk.cell_lp) & 15) == 0) {
+      uint4* act4 = (uint4*)(bk.action + e * S * 7);
+      uint4* lp4 = (uint4*)(bk.cell_lp + e * S);
+      for (int i = threadIdx.x; i < S * 7 / 16; i += blockDim.x) act4[i] = make_uint4(0, 0, 0, 0);
+      for (int i = threadIdx.x; i < S / 4; i += blockDim.x) lp4[i] = make_uint4(0, 0, 0, 0);
+    } else {
+      for (int i = threadIdx.x; i < S * 7; i += blockDim.x) bk.action[e * S * 7 + i] = 0;
+      for (int i = threadIdx.x; i < S; i += blockDim.x) bk.cell_lp[e * S + i] = 0.f;
     }
   }
 }
