@@ -15,6 +15,12 @@ available offline) and random-init weights of the reference architecture
 (IMPALA-CNN 16/32/32 + 256 FC + flat 78*16*16 head, 5.27 M params).
 
     python bench.py --gpus N --steps K --warmup W
+
+With ``--gpus N > 1`` and no torchrun environment, bench.py launches N ranks
+itself (``torch.distributed.run`` as a child process, parallel/launch.py) and
+fails if fewer than N GPUs are visible. Each rank pins itself (and its env
+worker / driver threads) to its share of the physical cores on its GPU's NUMA
+node before starting them.
 """
 from __future__ import annotations
 
@@ -62,26 +68,44 @@ def parse(argv=None):
                    help="acting trunk on the fp8 (e4m3) MFMA conv kernels (config 5)")
     p.add_argument("--profile_phases", action="store_true",
                    help="also report per-phase learner timings (adds syncs; not for the headline)")
+    p.add_argument("--oversubscribe", action="store_true",
+                   help="rehearsal only: allow more ranks than GPUs (ranks share a GPU over gloo)")
+    p.add_argument("--allreduce_dtype", type=str, default="fp32", help="fp32 | bf16 payload")
+    p.add_argument("--bucket_mb", type=float, default=8.0)
     return p.parse_args(argv)
 
 
 def main(argv=None):
     args = parse(argv)
+    from microbeast_amd.parallel import launch
+
+    if args.oversubscribe:
+        os.environ.setdefault("MBK_DIST_BACKEND", "gloo")  # RCCL refuses 2 ranks per GPU
+    rc = launch.relaunch(args.gpus, sys.argv[1:] if argv is None else list(argv),
+                         script=os.path.abspath(__file__), shared_gpu=args.oversubscribe)
+    if rc is not None:
+        return rc
     import torch
 
     from microbeast_amd.learner import Learner, LearnerHParams
     from microbeast_amd.models.agent import Agent, num_params
     from microbeast_amd.parallel import dist as D
-    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime, available_cpus
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
 
     if not torch.cuda.is_available():
         print("bench.py needs a GPU", file=sys.stderr)
         return 2
     info = D.init_distributed(use_cuda=True)
+    if info.world_size != args.gpus and info.is_main:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {info.world_size}; reporting "
+              f"{info.world_size}", file=sys.stderr)
     dev = torch.device("cuda", info.local_rank)
     torch.set_num_threads(2)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(info.world_size)))
-    threads = args.threads or max(2, min(24, available_cpus() // max(1, local_world) - 3))
+    # NUMA/core placement BEFORE any native thread exists (they inherit the affinity)
+    cpus = launch.pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local_world, dev.index)
+    budget = launch.rank_cpu_budget(local_world)
+    threads = args.threads or max(2, min(24, budget - 3))
     s = args.size
 
     def make_model():
@@ -94,7 +118,8 @@ def main(argv=None):
 
     torch.manual_seed(args.seed)
     model = make_model()
-    learner = Learner(model, LearnerHParams(), dev, info)
+    learner = Learner(model, LearnerHParams(bucket_mb=args.bucket_mb,
+                                            allreduce_dtype=args.allreduce_dtype), dev, info)
     envs_total = args.groups * args.envs_per_group
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.cu_partition > 0:  # policy graphs are captured with grids for the policy CUs
@@ -135,6 +160,7 @@ def main(argv=None):
         torch.cuda.set_stream(learner_stream)
 
     nstep = [0]
+    lags = []
 
     def step():
         batch, slots = rt.get_batch(timeout=120.0)
@@ -142,9 +168,11 @@ def main(argv=None):
         if args.verbose:
             print(f"[rank {info.rank}] step {nstep[0]} slots {slots} {rt.stats()}",
                   file=sys.stderr, flush=True)
+        lags.append(rt.policy_lag(slots, learner.n_updates))
         losses = learner.learn(batch)
         rt.release(slots)
-        rt.publish(learner.flat)
+        rt.publish(learner.flat, version=learner.n_updates)
+        learner.phases.mark("publish")
         if league is not None:  # the full league loop is inside the timed step
             league.maybe_snapshot(nstep[0], learner.flat.data)
             league.record(rt.drain_episodes())
@@ -165,6 +193,7 @@ def main(argv=None):
         rt.engine.release(slots, torch.cuda.current_stream().cuda_stream)
     D.barrier(info)
     st0 = rt.stats()
+    lags.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         losses = step()
@@ -179,6 +208,7 @@ def main(argv=None):
     total_frames = frames_per_step * args.steps * info.world_size
     fps = total_frames / el
     loss_vals = [float(x) for x in losses.tolist()]
+    phase_ms = learner.phases.read()  # HIP-event split of the last timed update (no sync)
     phase = None
     if args.profile_phases:
         learner.learn(rt.get_batch()[0], sync_timing=True)
@@ -212,7 +242,9 @@ def main(argv=None):
                               if args.selfplay_groups else "scripted bots"),
                 "envs_per_gpu": envs_total,
                 "env_threads_per_gpu": threads,
+                "cpus_per_rank": len(cpus),
                 "policy_lanes": rt.n_lanes,
+                "allreduce": f"{args.allreduce_dtype} {args.bucket_mb:g}MB buckets",
             },
             "actor_stats": {
                 "env_frames_stepped_per_s_rank0": round((st1["frames"] - st0["frames"]) / el, 1),
@@ -231,6 +263,9 @@ def main(argv=None):
                 "graph_launch_ms": round(1e3 * (st1["graph_launch_s"] - st0["graph_launch_s"])
                                          / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
             },
+            "learner_phase_ms_rank0": {k: round(v, 3) for k, v in phase_ms.items()},
+            "policy_lag_updates": ({"mean": round(sum(lags) / len(lags), 2), "max": max(lags)}
+                                   if lags else None),
             "last_losses": {"pg": loss_vals[0], "value": loss_vals[1], "entropy": loss_vals[2],
                             "total": loss_vals[3]},
         }

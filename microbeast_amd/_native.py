@@ -39,9 +39,9 @@ _SIGS = {
     "mbk_vtrace": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                    c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
-    "mbk_grad_clip_scale": [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p],
+    "mbk_grad_clip_scale": [c_void_p, c_int64, c_float, c_float, c_void_p, c_void_p, c_void_p],
     "mbk_adam": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
-                 c_float, c_float, c_float, c_int64, c_void_p, c_void_p],
+                 c_float, c_float, c_float, c_int64, c_void_p, c_float, c_void_p],
     "mbk_to_bf16": [c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_conv_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -77,7 +77,7 @@ class Flags:
                                    # process) | local (CPU policy per actor) | auto
     inference_wait_ms: float = 2.0  # mono runtime server: dynamic-batching window
     seed: int = 1
-    nproc_per_node: int = 1       # informative; launch with torchrun for DP
+    nproc_per_node: int = 1       # >1: launch that many DP ranks (one per GPU) over RCCL
     bucket_mb: float = 8.0
     allreduce_dtype: str = "fp32"  # fp32 | bf16 gradient all-reduce payload (fp32 master grads)
     profile_updates: int = 0      # >0: torch.profiler trace of that many updates -> savedir

@@ -32,14 +32,15 @@ __global__ __launch_bounds__(256) void sqnorm_partial_kernel(const float* __rest
   if (threadIdx.x == 0) partials[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-// scale[0] = min(1, max_norm / (norm + 1e-6)), scale[1] = norm
+// scale[0] = min(1, max_norm / (norm + 1e-6)), scale[1] = norm (of g * gmul)
 __global__ __launch_bounds__(64) void clip_scale_kernel(const float* __restrict__ partials, int nb,
-                                                        float max_norm, float* __restrict__ scale) {
+                                                        float max_norm, float gmul,
+                                                        float* __restrict__ scale) {
   float s = 0.f;
   for (int i = threadIdx.x; i < nb; i += 64) s += partials[i];
   s = wave_sum(s);
   if (threadIdx.x == 0) {
-    const float norm = sqrtf(s);
+    const float norm = sqrtf(s) * gmul;  // norm of the gradient Adam will see (g * gmul)
     scale[0] = max_norm > 0.f ? fminf(1.f, max_norm / (norm + 1e-6f)) : 1.f;
     scale[1] = norm;
   }
@@ -50,8 +51,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
                                                    __hip_bfloat16* __restrict__ p_bf16, int64_t n,
                                                    float lr, float b1, float b2, float eps,
                                                    float wd, float bc1, float bc2,
-                                                   const float* __restrict__ gscale) {
-  const float sc = gscale ? gscale[0] : 1.f;
+                                                   const float* __restrict__ gscale, float gmul) {
+  // gmul folds the data-parallel 1/world average into this pass (no separate scaling
+  // sweep over the gradient buffer); gscale is the optional clip factor
+  const float sc = (gscale ? gscale[0] : 1.f) * gmul;
   const float step = lr / bc1;
   const float rbc2 = 1.f / sqrtf(bc2);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
@@ -85,24 +88,24 @@ inline unsigned grid_for(int64_t n) {
 
 }  // namespace
 
-extern "C" int mbk_grad_clip_scale(const float* g, int64_t n, float max_norm,
+extern "C" int mbk_grad_clip_scale(const float* g, int64_t n, float max_norm, float gmul,
                                    float* partials /* >= 1024 */, float* scale /* 2 */,
                                    hipStream_t stream) {
   unsigned nb = grid_for(n / 4 + 1);
   if (nb > 1024) nb = 1024;
   hipLaunchKernelGGL(sqnorm_partial_kernel, dim3(nb), dim3(256), 0, stream, g, n, partials);
   hipLaunchKernelGGL(clip_scale_kernel, dim3(1), dim3(64), 0, stream, partials, (int)nb, max_norm,
-                     scale);
+                     gmul, scale);
   return (int)hipGetLastError();
 }
 
 extern "C" int mbk_adam(float* p, const float* g, float* m, float* v, void* p_bf16, int64_t n,
                         float lr, float b1, float b2, float eps, float wd, int64_t step,
-                        const float* gscale, hipStream_t stream) {
+                        const float* gscale, float gmul, hipStream_t stream) {
   const float bc1 = 1.f - powf(b1, (float)step);
   const float bc2 = 1.f - powf(b2, (float)step);
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, stream, p, g, m, v,
-                     (__hip_bfloat16*)p_bf16, n, lr, b1, b2, eps, wd, bc1, bc2, gscale);
+                     (__hip_bfloat16*)p_bf16, n, lr, b1, b2, eps, wd, bc1, bc2, gscale, gmul);
   return (int)hipGetLastError();
 }
 

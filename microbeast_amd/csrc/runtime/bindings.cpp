@@ -287,7 +287,9 @@ PYBIND11_MODULE(_mbrt, m) {
            py::arg("n"), py::arg("timeout") = -1.0)
       .def("stream_wait_full", &GpuEngine::stream_wait_full)
       .def("release", &GpuEngine::release)
-      .def("publish", &GpuEngine::publish)
+      .def("publish", &GpuEngine::publish, py::arg("src"), py::arg("dsts"), py::arg("nbytes"),
+           py::arg("stream"), py::arg("version") = -1)
+      .def("slot_version", &GpuEngine::slot_version)
       .def("publish_opponent", &GpuEngine::publish_opponent)
       .def("set_initial_opponent", &GpuEngine::set_initial_opponent)
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })

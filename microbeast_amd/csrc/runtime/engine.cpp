@@ -105,6 +105,7 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   full_ev_.resize(cfg_.n_slots);
   release_ev_.resize(cfg_.n_slots);
   release_pending_.assign(cfg_.n_slots, false);
+  slot_version_.assign(cfg_.n_slots, 0);
   for (int s = 0; s < cfg_.n_slots; ++s) {
     CTOR_CHECK(hipEventCreateWithFlags(&full_ev_[s], hipEventDisableTiming));
     CTOR_CHECK(hipEventCreateWithFlags(&release_ev_[s], hipEventDisableTiming));
@@ -300,6 +301,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       if (L.pack_graph[c]) ENG_CHECK(hipGraphLaunch(L.pack_graph[c], st));
       P.pending[ln] = false;
       if (c == 1) L.opp_version = P.version;
+      else if (P.version >= 0) L.policy_version = P.version;
       bool all = true;
       for (bool pl : P.pending) all = all && !pl;
       if (all) {  // landed on every lane
@@ -335,6 +337,7 @@ bool GpuEngine::enqueue_gpu(int g) {
     if (!slot_wait_q_.empty() && slot_wait_q_.front() == g) slot_wait_q_.pop_front();
     if (release_pending_[slot]) ENG_CHECK(hipStreamWaitEvent(st, release_ev_[slot], 0));
     G.cur = slot;
+    slot_version_[slot] = L.policy_version;
   }
   const size_t e0 = (size_t)g * E;
   G.timed = step_timing_;

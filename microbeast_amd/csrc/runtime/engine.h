@@ -133,10 +133,14 @@ class GpuEngine {
   // Copy src (device, on `stream`) into every lane's inference weights dsts[lane], each
   // applied between two of that lane's policy steps. Returns false (skipped) if the
   // previous publish has not landed on every lane yet.
+  // version: the learner update these weights come from (tags the rollout slots that
+  // act with them, so the learner can measure its policy lag); -1 = untagged
   bool publish(uintptr_t src, const std::vector<uintptr_t>& dsts, size_t nbytes,
-               uintptr_t stream) {
-    return publish_chan(0, src, dsts, nbytes, stream, -1);
+               uintptr_t stream, int version = -1) {
+    return publish_chan(0, src, dsts, nbytes, stream, version);
   }
+  // Version of the behaviour weights a slot's FIRST step acted with (the oldest in it).
+  int slot_version(int slot) const { return slot_version_.at(slot); }
   // League id of the opponent weights in place at start (before any publish_opponent).
   void set_initial_opponent(int version) {
     for (auto& L : lanes_) L.opp_version = version;
@@ -188,6 +192,7 @@ class GpuEngine {
     hipGraphExec_t pack_graph[2] = {nullptr, nullptr};
     LaneIO io;
     int opp_version = -1;     // driver thread only
+    int policy_version = 0;   // learner update of the weights landed on this lane
   };
 
   EngineConfig cfg_;
@@ -214,6 +219,7 @@ class GpuEngine {
   std::deque<int> free_slots_, full_slots_;
   std::vector<hipEvent_t> full_ev_, release_ev_;
   std::vector<bool> release_pending_;
+  std::vector<int> slot_version_;  // written when a group takes the slot (driver thread)
   std::deque<int> slot_wait_q_;  // driver thread only: groups waiting for a free slot
 
   // publish channels: 0 = learner policy, 1 = league opponent

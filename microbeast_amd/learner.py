@@ -23,6 +23,7 @@ import torch
 from .ops.optim import FlatAdam, FlatParams
 from .ops.vtrace import VTraceWorkspace, vtrace
 from .parallel.dist import DistInfo, GradAllReducer, broadcast_flat
+from .utils.metrics import PhaseTimer
 
 
 @dataclass
@@ -57,12 +58,16 @@ class Learner:
         self.ws = VTraceWorkspace()
         self.n_updates = 0
         self.timing = {}
+        # HIP-event split fwd / bwd / allreduce(wait) / optim (+ publish marked by the
+        # caller), read one update late without a host sync
+        self.phases = PhaseTimer(enabled=device.type == "cuda")
 
     def learn(self, batch: dict, sync_timing: bool = False) -> torch.Tensor:
         """batch keys (time-major): obs [T+1,B,...], mask [T+1,B,S,3] int32,
         action [T+1,B,S,7] uint8, logp [T+1,B], reward [T+1,B], done [T+1,B].
         Returns the device tensor [5] = pg, value, entropy, total, mean rho."""
         t0 = time.perf_counter()
+        self.phases.start()
         obs, mask, action = batch["obs"], batch["mask"], batch["action"]
         T1, B = batch["logp"].shape[:2]
         T = T1 - 1
@@ -78,17 +83,21 @@ class Learner:
                     c_bar=self.hp.c_bar, pg_rho_bar=self.hp.pg_rho_bar,
                     baseline_cost=self.hp.baseline_cost, entropy_cost=self.hp.entropy_cost,
                     reward_clip=self.hp.reward_clip, ws=self.ws)
+        self.phases.mark("fwd")
         if sync_timing and logp.is_cuda:
             torch.cuda.synchronize()
         t1 = time.perf_counter()
         torch.autograd.backward(
             [logp, value, ent],
             [vt.g_logp.reshape(-1), vt.g_value.reshape(-1), torch.full_like(ent, vt.g_ent)])
+        self.phases.mark("bwd")
         self.reducer.finish()
+        self.phases.mark("allreduce")
         if sync_timing and logp.is_cuda:
             torch.cuda.synchronize()
         t2 = time.perf_counter()
-        self.opt.step()
+        self.opt.step(grad_scale=self.reducer.grad_scale)
+        self.phases.mark("optim")
         if sync_timing and logp.is_cuda:
             torch.cuda.synchronize()
         t3 = time.perf_counter()

@@ -84,7 +84,9 @@ class FlatAdam:
         self.v.copy_(sd["v"])
         self.step_count = int(sd["step"])
 
-    def step(self):
+    def step(self, grad_scale: float = 1.0):
+        """grad_scale multiplies the gradient inside the update (the data-parallel 1/world
+        average is folded in here instead of a separate pass over the buffer)."""
         self.step_count += 1
         b1, b2 = self.betas
         f = self.flat
@@ -94,15 +96,16 @@ class FlatAdam:
             scale = None
             if self.max_grad_norm > 0:
                 N.check(k.mbk_grad_clip_scale(f.grad.data_ptr(), f.numel, self.max_grad_norm,
-                                              self._partials.data_ptr(), self._scale.data_ptr(),
+                                              grad_scale, self._partials.data_ptr(), self._scale.data_ptr(),
                                               st), "grad_clip_scale")
                 scale = self._scale.data_ptr()
                 self.last_grad_norm = self._scale[1]
             N.check(k.mbk_adam(f.data.data_ptr(), f.grad.data_ptr(), self.m.data_ptr(),
                                self.v.data_ptr(), N.ptr(self.shadow), f.numel, self.lr, b1, b2,
-                               self.eps, self.wd, self.step_count, scale, st), "adam")
+                               self.eps, self.wd, self.step_count, scale, grad_scale, st),
+                    "adam")
             return
-        g = f.grad
+        g = f.grad if grad_scale == 1.0 else f.grad * grad_scale
         if self.max_grad_norm > 0:
             norm = g.norm()
             self.last_grad_norm = norm

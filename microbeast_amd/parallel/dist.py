@@ -13,8 +13,17 @@ point-to-point links per GPU, ring collectives per-link bound):
   and launched from post-accumulate-grad hooks as soon as their last
   gradient lands, so the 20 MB actor-head bucket's all-reduce overlaps the
   encoder backward;
-* ``finish()`` waits on the async work (stream-ordered, no host sync) and
-  averages.
+* ``finish()`` waits on the async work (stream-ordered, no host sync); the
+  1/world average is folded into the Adam kernel (``grad_scale``), not a
+  separate pass over the gradient buffer;
+* host-side objects (episode rows for the rank-0 CSV) travel over a separate
+  gloo group, so gathering them never enqueues anything on a GPU stream or
+  waits for the learner's kernels.
+
+``MBK_FORCE_PG=1`` (or ``init_distributed(force_pg=True)``) creates a real
+process group even at world size 1, so the RCCL path — broadcast, hook-fired
+bucketed all-reduce, barrier, object gather — runs on a single-GPU box
+(tests/test_gpu_dist_rccl.py).
 """
 from __future__ import annotations
 
@@ -34,22 +43,27 @@ class DistInfo:
     world_size: int = 1
     local_rank: int = 0
     backend: str = "none"
+    pg: bool = False          # a process group exists (world > 1, or forced at world 1)
+    host_group: object = None  # gloo group for host objects (None: the default group is gloo)
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.pg
 
     @property
     def is_main(self) -> bool:
         return self.rank == 0
 
 
-def init_distributed(use_cuda: bool, timeout_s: float = 600.0) -> DistInfo:
+def init_distributed(use_cuda: bool, timeout_s: float = 600.0,
+                     force_pg: bool | None = None) -> DistInfo:
     """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world <= 1:
+    if force_pg is None:
+        force_pg = os.environ.get("MBK_FORCE_PG", "0") == "1"
+    if world <= 1 and not force_pg:
         if use_cuda:
             torch.cuda.set_device(local)
         return DistInfo(rank, world, local, "none")
@@ -63,8 +77,12 @@ def init_distributed(use_cuda: bool, timeout_s: float = 600.0) -> DistInfo:
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if use_cuda and backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
+        if "MASTER_PORT" not in os.environ:  # forced single-rank group outside torchrun
+            from .launch import free_port
+            kw.update(init_method=f"tcp://127.0.0.1:{free_port()}", rank=rank, world_size=world)
         dist.init_process_group(**kw)
-    return DistInfo(rank, world, local, backend)
+    host = dist.new_group(backend="gloo") if backend != "gloo" else None
+    return DistInfo(rank, world, local, backend, pg=True, host_group=host)
 
 
 def broadcast_flat(flat: FlatParams, info: DistInfo) -> None:
@@ -81,7 +99,8 @@ class GradAllReducer:
         the result is written back into the fp32 gradient buffer (fp32 master grads)."""
         self.flat, self.info = flat, info
         self.comm_dtype = comm_dtype
-        self.bufs: list = []
+        self.grad_scale = 1.0 / max(1, info.world_size)  # applied inside Adam
+        self.comm = None  # persistent low-precision payload (comm_dtype != fp32)
         self.buckets: list[tuple[int, int]] = []
         self.param_bucket: dict[int, int] = {}
         self.works = []
@@ -112,6 +131,8 @@ class GradAllReducer:
                      for b in range(len(self.buckets))]
         self.count = [0] * len(self.buckets)
         self.fired = [False] * len(self.buckets)
+        if comm_dtype != torch.float32:
+            self.comm = torch.empty(flat.numel, dtype=comm_dtype, device=flat.grad.device)
         for i, p in enumerate(flat.params):
             p.register_post_accumulate_grad_hook(self._make_hook(i))
 
@@ -127,10 +148,10 @@ class GradAllReducer:
         s, e = self.buckets[b]
         self.fired[b] = True
         g = self.flat.grad[s:e]
-        if self.comm_dtype != torch.float32:
-            buf = g.to(self.comm_dtype)
-            self.bufs.append((s, e, buf))
-            g = buf
+        if self.comm is not None:
+            c = self.comm[s:e]
+            c.copy_(g)
+            g = c
         self.works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, async_op=True))
 
     def start_step(self):
@@ -138,10 +159,11 @@ class GradAllReducer:
             self.count = [0] * len(self.buckets)
             self.fired = [False] * len(self.buckets)
             self.works = []
-            self.bufs = []
 
     def finish(self):
-        """Launch any bucket whose params got no gradient, wait, average."""
+        """Launch any bucket whose params got no gradient and make the current stream wait
+        for all of them (no host sync). The gradient is left as the SUM over ranks: the
+        optimizer applies ``grad_scale`` (1/world) in its own pass."""
         if not self.info.enabled:
             return
         for b in range(len(self.buckets)):
@@ -150,10 +172,8 @@ class GradAllReducer:
         for w in self.works:
             w.wait()
         self.works = []
-        for s, e, buf in self.bufs:
-            self.flat.grad[s:e].copy_(buf)
-        self.bufs = []
-        self.flat.grad.mul_(1.0 / self.info.world_size)
+        if self.comm is not None:
+            self.flat.grad.copy_(self.comm)
 
 
 def all_reduce_mean(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
@@ -161,6 +181,17 @@ def all_reduce_mean(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         t.div_(info.world_size)
     return t
+
+
+def gather_objects(obj, info: DistInfo) -> list:
+    """Rank 0 receives every rank's ``obj`` (others get []), over the gloo host group: a
+    CPU-only exchange that never waits on a GPU stream (RCCL's object collectives would
+    stage through device memory and synchronise)."""
+    if not info.enabled:
+        return [obj]
+    out = [None] * info.world_size if info.is_main else None
+    dist.gather_object(obj, out, dst=0, group=info.host_group)
+    return out if info.is_main else []
 
 
 def barrier(info: DistInfo) -> None:

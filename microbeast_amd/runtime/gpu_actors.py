@@ -272,10 +272,18 @@ class GpuActorRuntime:
     def release(self, slots):
         self.engine.release(list(slots), N.stream_ptr())
 
-    def publish(self, learner_flat: FlatParams) -> bool:
+    def publish(self, learner_flat: FlatParams, version: int = -1) -> bool:
+        """Event-ordered copy of the learner weights into every lane's inference copy.
+        version: learner update count of these weights (tags the slots that act with them,
+        see ``policy_lag``)."""
         return self.engine.publish(learner_flat.data.data_ptr(),
                                    [ln["flat"].data.data_ptr() for ln in self.lanes],
-                                   learner_flat.numel * 4, N.stream_ptr())
+                                   learner_flat.numel * 4, N.stream_ptr(), int(version))
+
+    def policy_lag(self, slots, learner_version: int) -> int:
+        """Learner updates between the oldest behaviour weights in ``slots`` and
+        ``learner_version`` (the update about to consume them); IMPALA's off-policy gap."""
+        return int(learner_version) - min(self.engine.slot_version(int(s)) for s in slots)
 
     def set_opponent(self, flat: torch.Tensor, version: int) -> bool:
         """Swap the self-play opponent to league snapshot ``version`` (a flat fp32 buffer).

@@ -49,8 +49,10 @@ def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, fu
     torch.manual_seed(seed)
     gen = torch.Generator().manual_seed(seed)
     s, n, T = flags.env_size, flags.n_envs, flags.unroll_length
+    rank = int(os.environ.get("RANK", "0"))  # DP: every rank owns its own actor pool
     env = create_env(s, n, flags.max_episode_steps, seed=seed, opponents=flags.opponent_list(),
-                     reward_weight=flags.reward_weights(), env_index_base=actor_id * n,
+                     reward_weight=flags.reward_weights(),
+                     env_index_base=(rank * flags.n_actors + actor_id) * n,
                      env=flags.env)
     model = flat = None
     if client is None:
@@ -184,7 +186,8 @@ class MonoRuntime:
         p = self.ctx.Process(target=_actor_main,
                              args=(i, fd, self.buffers, self.free, self.full, self.weights,
                                    self.version, self.cur_slot, self.episode_q,
-                                   self.flags.seed * 1009 + i + 97 * self.restarts,
+                                   self.flags.seed * 1009 + i + 97 * self.restarts
+                                   + 7919 * int(os.environ.get("RANK", "0")),
                                    self.server.client(i) if self.server is not None else None),
                              daemon=True)
         p.start()

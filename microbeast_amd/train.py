@@ -41,11 +41,39 @@ def checkpoint_path(flags: Flags) -> str:
 
 
 def _gather_episodes(recs, info):
-    if not info.enabled:
-        return recs
-    out = [None] * info.world_size
-    torch.distributed.all_gather_object(out, recs)
-    return [r for part in out for r in (part or [])] if info.is_main else []
+    """Every rank's finished episodes to rank 0 (gloo host group: no GPU-stream sync)."""
+    parts = D.gather_objects(recs, info)
+    return [r for part in parts for r in (part or [])]
+
+
+class _LossReadout:
+    """Loss values reach the host one update late: an async D2H copy into pinned memory
+    plus an event, polled with ``query()``. The learner loop therefore never waits for the
+    GPU to finish an update before enqueueing the next one (the reference read floats
+    synchronously every update, libs/utils.py:340)."""
+
+    def __init__(self, cuda: bool):
+        self.cuda = cuda
+        self.q = []
+
+    def push(self, vals: torch.Tensor, meta: dict):
+        if self.cuda:
+            host = torch.empty(vals.numel(), dtype=vals.dtype, pin_memory=True)
+            host.copy_(vals, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = vals.clone(), None
+        self.q.append((host, ev, meta))
+
+    def pop(self, wait: bool = False):
+        out = []
+        while self.q and (wait or self.q[0][1] is None or self.q[0][1].query()):
+            host, ev, meta = self.q.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            out.append((host.tolist(), meta))
+        return out
 
 
 _PROFILE_START = 3  # skip the first updates (graph capture, allocator warm-up)
@@ -85,6 +113,14 @@ def train(flags: Flags) -> dict:
     runtime = flags.runtime if flags.runtime != "auto" else ("gpu" if want_cuda else "mono")
     if runtime == "gpu" and not want_cuda:
         raise RuntimeError("--runtime gpu needs a GPU")
+    actor_threads = flags.actor_threads
+    if runtime == "gpu":
+        from .parallel.launch import pin_rank, rank_cpu_budget
+
+        # NUMA/core placement before the engine starts its env worker / driver threads
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(info.world_size)))
+        pin_rank(info.local_rank, local_world, dev.index)
+        actor_threads = actor_threads or max(1, min(32, rank_cpu_budget(local_world) - 3))
     torch.manual_seed(flags.seed + info.rank)
     log = (lambda *a: None) if (flags.quiet or not info.is_main) else (lambda *a: print(*a, flush=True))
     log(f"[microbeast_amd] exp={flags.exp_name} runtime={runtime} device={dev} "
@@ -112,7 +148,7 @@ def train(flags: Flags) -> dict:
         sp_groups = min(flags.selfplay_groups, flags.groups) if flags.self_play else 0
         rt = GpuActorRuntime(lambda: make_model(flags, "cpu"), flags.env_size, flags.groups,
                              flags.envs_per_group, flags.unroll_length, flags.batch_size, dev,
-                             n_threads=flags.actor_threads or None,
+                             n_threads=actor_threads,
                              max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
                              bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
                              env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
@@ -148,7 +184,21 @@ def train(flags: Flags) -> dict:
 
     prof = None  # --profile_updates: torch.profiler timeline of a few steady-state updates
     t_start = time.perf_counter()
+    t_prev = t_start
     last = {}
+    readout = _LossReadout(want_cuda)
+
+    def flush(wait=False):
+        for lv, m in readout.pop(wait):
+            logger.losses(m["update"], lv[0], lv[1], lv[2], lv[3], m["period"], m["step"],
+                          m["fps"], m["wait_s"], m["learn_s"], lv[4], phase_ms=m["phase"],
+                          policy_lag=m["lag"])
+            last.update(update=m["update"], step=m["step"], pg_loss=lv[0], value_loss=lv[1],
+                        entropy=lv[2], total_loss=lv[3], fps=m["fps"])
+            log(f"update {m['update']} step {m['step']} total_loss {lv[3]:.4f} pg {lv[0]:.4f} "
+                f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {m['fps']:,.0f} lag {m['lag']}"
+                + (f" league {m['league']}" if m.get("league") else ""))
+
     try:
         while step < flags.total_steps and (flags.max_updates <= 0 or n_update < flags.max_updates):
             if flags.profile_updates > 0 and info.is_main:
@@ -156,17 +206,20 @@ def train(flags: Flags) -> dict:
             t0 = time.perf_counter()
             if runtime == "gpu":
                 batch, slots = rt.get_batch(timeout=flags.batch_timeout)
+                lag = rt.policy_lag(slots, n_update)
             else:
                 batch, slots = rt.get_batch(flags.batch_timeout)
+                lag = -1
                 if not want_cuda:
                     batch = {k: v.to(dev) for k, v in batch.items()}
             t1 = time.perf_counter()
             losses = learner.learn(batch)
             if runtime == "gpu":
                 rt.release(slots)
-                rt.publish(learner.flat)
+                rt.publish(learner.flat, version=n_update + 1)
             else:
                 rt.publish(learner.flat.data)
+            learner.phases.mark("publish")
             step += frames_per_update
             n_update += 1
             if league is not None:
@@ -178,20 +231,20 @@ def train(flags: Flags) -> dict:
             if flags.fault_inject_every and runtime == "mono" and n_update % flags.fault_inject_every == 0:
                 rt.kill_random_actor()
             if n_update % flags.log_every == 0:
-                lv = D.all_reduce_mean(losses.detach().clone(), info).tolist()
                 t2 = time.perf_counter()
-                fps = frames_per_update / max(t2 - t0, 1e-9)
-                logger.losses(n_update, lv[0], lv[1], lv[2], lv[3], t2 - t0, step, fps, t1 - t0,
-                              t2 - t1, lv[4])
+                period = (t2 - t_prev) / flags.log_every  # loop period, as the reference timed it
+                t_prev = t2
+                readout.push(D.all_reduce_mean(losses.detach().clone(), info), {
+                    "update": n_update, "step": step, "period": period,
+                    "fps": frames_per_update / max(period, 1e-9), "wait_s": t1 - t0,
+                    "learn_s": t2 - t1, "phase": learner.phases.read(), "lag": lag,
+                    "league": (f"{len(league)} vs #{league.current}" if league is not None
+                               else None)})
                 eps = rt.drain_episodes()
                 if league is not None:
                     league.record(eps)  # each rank matches against its own league
                 logger.episodes(_gather_episodes(eps, info))
-                last = {"update": n_update, "step": step, "pg_loss": lv[0], "value_loss": lv[1],
-                        "entropy": lv[2], "total_loss": lv[3], "fps": fps}
-                log(f"update {n_update} step {step} total_loss {lv[3]:.4f} pg {lv[0]:.4f} "
-                    f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {fps:,.0f}"
-                    + (f" league {len(league)} vs #{league.current}" if league is not None else ""))
+            flush()
             if flags.checkpoint_every and n_update % flags.checkpoint_every == 0:
                 if info.is_main:
                     save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,
@@ -200,6 +253,7 @@ def train(flags: Flags) -> dict:
     finally:
         if prof is not None:
             _profile_tick(prof, -1, flags, want_cuda)
+        flush(wait=True)
         rt.stop()
         if info.is_main:
             save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,

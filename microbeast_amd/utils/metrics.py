@@ -7,7 +7,11 @@
   column fewer than the rows).
 * ``{exp}Losses.csv``: ``update,pg_loss,value_loss,entropy_loss,total_loss,
   update time`` (reference microbeast.py:135-139, 233-239) + trailing columns
-  frames, fps, wait_s, learn_s, mean_rho.
+  frames, fps, wait_s, learn_s, mean_rho and the GPU phase split of the update
+  (fwd_ms, bwd_ms, allreduce_ms, optim_ms, publish_ms: HIP-event times read one
+  update late, so logging them never synchronises the host with the GPU) and
+  policy_lag (learner updates between the rollout's behaviour weights and the
+  update that consumed it).
 
 Only rank 0 writes (DP); rows are flushed per write so a killed run keeps
 its log.
@@ -18,8 +22,58 @@ import csv
 import os
 
 EPISODE_HEADER = ["Return", "steps", "env_index", "winner", "opponent"]
+PHASES = ("fwd", "bwd", "allreduce", "optim", "publish")
 LOSS_HEADER = ["update", "pg_loss", "value_loss", "entropy_loss", "total_loss", "update time",
-               "frames", "fps", "wait_s", "learn_s", "mean_rho"]
+               "frames", "fps", "wait_s", "learn_s", "mean_rho"] + [f"{p}_ms" for p in PHASES] + [
+               "policy_lag"]
+
+
+class PhaseTimer:
+    """GPU-side phase split of a learner update with HIP events, never blocking the host.
+
+    ``start()`` / ``mark(name)`` record events on the current stream; ``read()`` returns
+    {name: ms since the previous mark} of the most recent update whose events have
+    COMPLETED (``query()``, not ``synchronize()``), i.e. typically the previous update.
+    Double-buffered, so recording update k never overwrites events of k-1 still in flight.
+    (Reference: only wall-clock per update, microbeast.py:223-231)
+    """
+
+    def __init__(self, enabled: bool = True):
+        import torch
+
+        self.enabled = enabled and torch.cuda.is_available()
+        self._sets = [[], []]
+        self._cur = 0
+        self._last: dict = {}
+
+    def start(self):
+        if not self.enabled:
+            return
+        import torch
+
+        self._cur ^= 1
+        self._sets[self._cur] = [("start", torch.cuda.Event(enable_timing=True))]
+        self._sets[self._cur][0][1].record()
+
+    def mark(self, name: str):
+        if not self.enabled or not self._sets[self._cur]:
+            return
+        import torch
+
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self._sets[self._cur].append((name, ev))
+
+    def read(self) -> dict:
+        if not self.enabled:
+            return {}
+        for idx in (self._cur, self._cur ^ 1):
+            evs = self._sets[idx]
+            if len(evs) > 1 and evs[-1][1].query():
+                self._last = {n: evs[i - 1][1].elapsed_time(e) for i, (n, e) in enumerate(evs)
+                              if i > 0}
+                break
+        return dict(self._last)
 
 
 class CsvLogger:
@@ -58,11 +112,14 @@ class CsvLogger:
 
     def losses(self, update: int, pg: float, value: float, entropy: float, total: float,
                update_time: float, frames: int, fps: float, wait_s: float, learn_s: float,
-               mean_rho: float) -> None:
+               mean_rho: float, phase_ms: dict | None = None, policy_lag: float = -1) -> None:
         if not self.enabled:
             return
+        ph = phase_ms or {}
         self._lossw.writerow([update, pg, value, entropy, total, update_time, frames,
-                              round(fps, 2), round(wait_s, 6), round(learn_s, 6), mean_rho])
+                              round(fps, 2), round(wait_s, 6), round(learn_s, 6), mean_rho]
+                             + [round(ph[p], 4) if p in ph else "" for p in PHASES]
+                             + [policy_lag])
         self._loss.flush()
 
     def close(self):

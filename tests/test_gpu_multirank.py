@@ -1,9 +1,10 @@
-"""Multi-rank bench path on the single-GPU box: 2 DP ranks sharing cuda:0 over gloo
-(RCCL refuses two ranks on one device). Exercises torchrun env parsing, broadcast,
-bucketed all-reduce of CUDA grads, barriers, MAX-time reduction and rank-0 JSON."""
+"""Multi-rank bench path on the single-GPU box: ``bench.py --gpus 2`` with no torchrun
+environment launches its 2 DP ranks itself (parallel/launch.py); ``--oversubscribe`` lets
+them share cuda:0 over gloo (RCCL refuses two ranks on one device). Exercises the
+self-launch, torchrun env parsing, rank pinning, broadcast, bucketed all-reduce of CUDA
+grads, barriers, MAX-time reduction and rank-0 JSON. (RCCL itself: test_gpu_dist_rccl.)"""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -14,18 +15,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 def test_bench_two_ranks_one_gpu(cuda):
-    env = dict(os.environ, MBK_DIST_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--oversubscribe",
            "--steps", "3", "--warmup", "1", "--groups", "2", "--envs_per_group", "128",
            "--unroll", "16", "--threads", "2"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
@@ -35,3 +28,14 @@ def test_bench_two_ranks_one_gpu(cuda):
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     assert out["value"] > 0 and out["config"]["global_batch"] == 2 * 128 * 16
+    assert out["policy_lag_updates"]["max"] >= 0
+    assert set(out["learner_phase_ms_rank0"]) >= {"fwd", "bwd", "allreduce", "optim"}
+
+
+def test_bench_refuses_more_gpus_than_visible(cuda):
+    import torch
+    n = torch.cuda.device_count() + 1
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK")}
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(n), "--steps", "1"], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "visible GPUs" in r.stderr
