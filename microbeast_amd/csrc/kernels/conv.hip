@@ -333,8 +333,8 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       const int m = pb * 16 + li;  // this lane's pixel (B column)
       const bool valid = m < M;
       const int mm = valid ? m : 0;  // rows past M compute garbage that is never stored
-      // float-reciprocal index math (exact here, see trunk.hip conv_lds): the integer
-      // divisions by runtime H*W / W are ~20 VALU per block
+      // float-reciprocal index math (exact: index_math_ok() bounds imgs*H*W at launch): the
+      // integer divisions by runtime H*W / W are ~20 VALU per block
       const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
       const int base_pos = (im * Hp + y) * Wp + x;  // padded position of tap (0,0)
@@ -1139,6 +1139,15 @@ int resident_blocks(const void* kfn, size_t sm) {
   return r;
 }
 
+// The kernels map a tile-local pixel index m in [0, imgs*H*W) to (image, y, x) with float
+// reciprocals ((m + 0.5) * (1/HW)): exact while imgs*H*W < 2^22 (the product's rounding
+// error stays below the 0.5/HW distance to the next integer). LDS capacity keeps today's
+// shapes far below that; this check turns a future larger-tile / larger-map config into a
+// launch error instead of silently wrong indices.
+bool index_math_ok(int imgs, int H, int W) {
+  return H > 0 && W > 0 && H * W <= 1024 && (int64_t)imgs * H * W < (int64_t(1) << 22);
+}
+
 }  // namespace
 
 static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const void* w,
@@ -1149,6 +1158,7 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
                            const void* pidx = nullptr) {
   if (N <= 0) return 0;
   if (fp8 && !wscale) return (int)hipErrorInvalidValue;
+  if (!index_math_ok(imgs, H, W)) return (int)hipErrorInvalidValue;
   const bool unpool = dp != nullptr;
   if (unpool && (in_bits || fp8 || pool || !pidx)) return (int)hipErrorInvalidValue;
   ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
@@ -1240,7 +1250,7 @@ extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, c
 extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
                                     int imgs, int unpool) {
   const size_t sm = wgrad_smem(cin, cout, imgs, H, W, unpool != 0);
-  if (sm > 160 * 1024) return -(int)hipErrorInvalidValue;
+  if (sm > 160 * 1024 || !index_math_ok(imgs, H, W)) return -(int)hipErrorInvalidValue;
   const int nrounds = (N + imgs - 1) / imgs;
   int res = 1;
 #define Q(CI, CO, B)                                                                  \
@@ -1259,7 +1269,8 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
   ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in,
                   dy ? nullptr : (const bf16*)dp, dy ? nullptr : (const uint8_t*)pidx};
   const size_t sm = wgrad_smem(cin, cout, imgs, H, W, dy == nullptr);
-  if (sm > 160 * 1024 || nparts < 1) return (int)hipErrorInvalidValue;
+  if (sm > 160 * 1024 || nparts < 1 || !index_math_ok(imgs, H, W))
+    return (int)hipErrorInvalidValue;
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \

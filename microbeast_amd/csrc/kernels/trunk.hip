@@ -141,7 +141,8 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
   // accumulator chain nor the LDS read latency is exposed per block. Each chain runs the
   // taps in the same order as before (bit-identical results).
   // pixel -> (image, y, x) with float reciprocals (exact for m < 2^16, HW <= 1024: the
-  // distance of (m + 0.5) / HW to an integer is >= 0.5 / HW, far above the rounding error);
+  // distance of (m + 0.5) / HW to an integer is >= 0.5 / HW, far above the rounding error;
+  // mbk_trunk_tail refuses shapes outside that bound);
   // the integer divisions by runtime H*W / W cost ~20 VALU per block (profile 15: VALU-bound)
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   auto epilogue = [&](int pb, const f32x4* acc) {
@@ -401,6 +402,9 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
     while (tni > 1 && 2 * region_bytes(H0, W0, tni) + wb > 160 * 1024) tni /= 2;
   }
   a.tni = tni;
+  // float-reciprocal pixel index math in the kernel is exact only for tni*H0*W0 < 2^16
+  if (H0 * W0 > 1024 || (int64_t)tni * H0 * W0 >= (int64_t(1) << 16))
+    return (int)hipErrorInvalidValue;
   const size_t r = region_bytes(H0, W0, tni);
   a.r1_bytes = (int)r;
   const size_t sm = 2 * r + wb;

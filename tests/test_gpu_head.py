@@ -77,13 +77,16 @@ def test_sparse_sample(cuda):
     torch.testing.assert_close(lp, lp2, rtol=1e-5, atol=1e-4)
 
 
-def test_bucketed_acting_path_matches_sorted_path(cuda):
+@pytest.mark.parametrize("s", [16, 10])
+def test_bucketed_acting_path_matches_sorted_path(cuda, s):
     """decode_obs_mask_bucket + head_units (atomic per-cell buckets) samples exactly the
-    actions / log-probs of the deterministic counting-sort path (same Philox keys)."""
+    actions / log-probs of the deterministic counting-sort path (same Philox keys).
+    s=16: the vectorised 16-byte zeroing of inactive envs; s=10 (S % 16 != 0): the scalar
+    fallback. The action buffer is pre-filled with 9s so a missed zero store fails."""
     from microbeast_amd import _native as N
     from microbeast_amd.models.agent import Agent
     rt = N.runtime()
-    s, E = 16, 300
+    E = 300
     S = s * s
     env = rt.VecEnv(s, E, 400, 2, [0, 1, 2, 3])
     env.set_validate(False)

@@ -1,0 +1,92 @@
+"""The user-facing GPU entry point ``microbeast.py --runtime gpu`` end to end on the MI355X
+(reference microbeast.py:109-278 ``train()`` / ``main()``): rank-0 CSVs in the reference
+formats, checkpoint, ``--resume`` (CSV append, step / update restore), ``--test``
+evaluation on the GPU, the self-play league's state through a checkpoint, and a
+short-budget run whose episode return and win rate must improve (the reference's logged
+runs stay flat: experiments/5_ener/5_enero.csv)."""
+import csv
+import os
+
+import pytest
+import torch
+
+from microbeast_amd.cli import main
+from microbeast_amd.utils.checkpoint import load_checkpoint
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(tmp, name, *extra):
+    return ["--exp_name", name, "--runtime", "gpu", "--env_size", "8", "--groups", "2",
+            "--envs_per_group", "32", "--unroll_length", "8", "--batch_size", "1",
+            "--savedir", str(tmp), "--quiet", "--max_episode_steps", "10", *extra]
+
+
+def _rows(path):
+    with open(path) as f:
+        return list(csv.DictReader(f))
+
+
+def test_gpu_train_checkpoint_resume_and_eval(cuda, tmp_path):
+    assert main(_args(tmp_path, "g", "--max_updates", "4", "--checkpoint_every", "2")) == 0
+    ck = load_checkpoint(os.path.join(tmp_path, "g.ckpt"))
+    frames = 32 * 8
+    assert ck["n_update"] == 4 and ck["step"] == 4 * frames
+    loss = _rows(tmp_path / "gLosses.csv")
+    assert [int(r["update"]) for r in loss] == [1, 2, 3, 4]
+    assert all(int(r["policy_lag"]) >= 0 for r in loss)
+    assert all(float(r["fwd_ms"]) > 0 for r in loss[1:])  # HIP-event phase split, read late
+    eps = _rows(tmp_path / "g.csv")
+    assert eps and set(eps[0]) >= {"Return", "steps"}
+    w0 = ck["model_state_dict"]["actor.weight"].clone()
+    assert main(_args(tmp_path, "g", "--max_updates", "6", "--resume")) == 0
+    ck2 = load_checkpoint(os.path.join(tmp_path, "g.ckpt"))
+    assert ck2["n_update"] == 6 and ck2["step"] == 6 * frames
+    assert not torch.equal(ck2["model_state_dict"]["actor.weight"], w0)  # it kept learning
+    assert ck2["optimizer_state_dict"]["step"] == 6  # Adam moments / step restored, not reset
+    loss = _rows(tmp_path / "gLosses.csv")
+    assert [int(r["update"]) for r in loss] == [1, 2, 3, 4, 5, 6]  # appended, no new header
+    assert main(_args(tmp_path, "g", "--test", "--eval_episodes", "3", "--n_envs", "3")) == 0
+    ev = _rows(tmp_path / "g_eval.csv")
+    assert len(ev) == 3
+
+
+def test_gpu_selfplay_league_survives_resume(cuda, tmp_path):
+    a = ["--self_play", "--selfplay_groups", "1", "--league_update_every", "1",
+         "--league_size", "4"]
+    assert main(_args(tmp_path, "sp", "--max_updates", "3", *a)) == 0
+    ck = load_checkpoint(os.path.join(tmp_path, "sp.ckpt"))
+    lg = ck["league"]
+    n0 = len(lg["snaps"])
+    assert n0 >= 2 and lg["next_id"] == 4  # initial + a snapshot every update (capacity 4)
+    assert main(_args(tmp_path, "sp", "--max_updates", "5", "--resume", *a)) == 0
+    ck2 = load_checkpoint(os.path.join(tmp_path, "sp.ckpt"))
+    lg2 = ck2["league"]
+    # the pool, ids and results continued from the checkpoint instead of restarting
+    assert ck2["n_update"] == 5 and lg2["next_id"] == 6 and len(lg2["snaps"]) == 4
+    assert sum(lg2["games"].values()) >= sum(lg["games"].values())
+    eps = _rows(tmp_path / "sp.csv")
+    assert any(int(e["opponent"]) >= 0 for e in eps)  # league-tagged self-play episodes
+
+
+def test_gpu_training_improves_return_and_win_rate(cuda, tmp_path):
+    """8x8 against the passive bot, 1500 updates of 16K frames (~15 s): the second half's
+    episodes must beat the first 15 % on mean return and on win rate."""
+    assert main(["--exp_name", "learn", "--runtime", "gpu", "--env_size", "8", "--opponents",
+                 "passive", "--groups", "2", "--envs_per_group", "256", "--unroll_length", "64",
+                 "--batch_size", "1", "--max_updates", "1500", "--max_episode_steps", "400",
+                 "--savedir", str(tmp_path), "--quiet", "--log_every", "50",
+                 "--checkpoint_every", "0"]) == 0
+    eps = _rows(tmp_path / "learn.csv")
+    n = len(eps)
+    assert n > 2000
+    first, last = eps[:int(0.15 * n)], eps[n // 2:]
+
+    def stats(rows):
+        ret = sum(float(r["Return"]) for r in rows) / len(rows)
+        win = sum(r["winner"] == "0" for r in rows) / len(rows)
+        return ret, win
+
+    (r0, w0), (r1, w1) = stats(first), stats(last)
+    print(f"return {r0:.1f} -> {r1:.1f}, win rate {w0:.3f} -> {w1:.3f} over {n} episodes")
+    assert r1 > 1.1 * r0 and w1 > w0
