@@ -29,108 +29,163 @@ struct Buckets {
   uint8_t* action; // [E*S*7]
 };
 
-// one workgroup per env; LDS copy of the env's codes
+// 78-bit action mask of cell c (real frame, player 1 = "own" in the code) from the env's
+// codes in LDS, exactly the simulator's rules (include/microrts_rules.h).
+__device__ __forceinline__ void cell_mask(const uint16_t* cs, int c, int H, int W, int r,
+                                          uint32_t w[3]) {
+  w[0] = w[1] = w[2] = 0u;
+  const uint16_t code = cs[c];
+  const int t = code_type(code);
+  // own (owner 1), idle (act noop <=> busy == 0), not a resource
+  if (!(code_owner(code) == 1 && code_act(code) == A_NOOP && t != RESOURCE && t != NONE)) return;
+  const int y = c / W, x = c - y * W;
+  setb(w, kSegOff[0] + A_NOOP);
+  bool any_move = false, any_harv = false, any_ret = false, any_prod = false, any_att = false;
+  const bool mobile = t >= WORKER;
+  const int carried = code_res(code);
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int nx = x + kDX[d], ny = y + kDY[d];
+    if (nx < 0 || ny < 0 || nx >= W || ny >= H) continue;
+    const uint16_t nc = cs[ny * W + nx];
+    const int nt = code_type(nc);
+    if (nt == NONE) {
+      if (mobile) { setb(w, kSegOff[1] + d); any_move = true; }
+      const bool can_prod = (t == BASE && r >= spec_cost(WORKER)) ||
+                            (t == BARRACKS && r >= spec_cost(LIGHT)) ||
+                            (t == WORKER && r >= spec_cost(BARRACKS));
+      if (can_prod) { setb(w, kSegOff[4] + d); any_prod = true; }
+    } else {
+      if (t == WORKER && nt == RESOURCE && carried == 0 && code_res(nc) > 0) {
+        setb(w, kSegOff[2] + d); any_harv = true;
+      }
+      if (t == WORKER && nt == BASE && code_owner(nc) == 1 && carried > 0) {
+        setb(w, kSegOff[3] + d); any_ret = true;
+      }
+    }
+  }
+  if (any_prod) {
+    if (t == BASE) setb(w, kSegOff[5] + (WORKER - 1));
+    if (t == BARRACKS) {
+      if (r >= spec_cost(LIGHT)) setb(w, kSegOff[5] + (LIGHT - 1));
+      if (r >= spec_cost(HEAVY)) setb(w, kSegOff[5] + (HEAVY - 1));
+      if (r >= spec_cost(RANGED)) setb(w, kSegOff[5] + (RANGED - 1));
+    }
+    if (t == WORKER) {
+      if (r >= spec_cost(BASE)) setb(w, kSegOff[5] + (BASE - 1));
+      if (r >= spec_cost(BARRACKS)) setb(w, kSegOff[5] + (BARRACKS - 1));
+    }
+  }
+  if (spec_damage(t) > 0) {
+    const int R = spec_range(t);
+    for (int ay = -3; ay <= 3; ++ay)
+      for (int ax = -3; ax <= 3; ++ax) {
+        if (ax * ax + ay * ay > R * R || (ax == 0 && ay == 0)) continue;
+        const int tx = x + ax, ty = y + ay;
+        if (tx < 0 || ty < 0 || tx >= W || ty >= H) continue;
+        if (code_owner(cs[ty * W + tx]) == 2) {
+          setb(w, kSegOff[6] + (ay + 3) * 7 + (ax + 3)); any_att = true;
+        }
+      }
+  }
+  if (any_move) setb(w, kSegOff[0] + A_MOVE);
+  if (any_harv) setb(w, kSegOff[0] + A_HARVEST);
+  if (any_ret) setb(w, kSegOff[0] + A_RETURN);
+  if (any_prod) setb(w, kSegOff[0] + A_PRODUCE);
+  if (any_att) setb(w, kSegOff[0] + A_ATTACK);
+}
+
+// One WAVE per env, kEnvsPerWG envs per workgroup, persistent over env groups (grid sized
+// to the device). A lane owns Q = ceil(S/64) consecutive cells, so an env's obs words and
+// mask triples leave as contiguous 16-byte vector stores (Q = 4 at 16x16: one uint4 of obs
+// and three uint4 of mask per lane) and the inactive-output zeroing is a few wave-wide
+// 16-byte stores. The previous form (one 256-thread workgroup per env, one cell per thread,
+// 3 scalar mask stores per cell) ran at ~0.4-0.6 TB/s: 8192 short workgroups per step, each
+// a global-load -> barrier -> store chain (profiles/16: ~99 us per 8192-env step).
+constexpr int kEnvsPerWG = 4;
+
 template <bool BUCKET>
 __global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __restrict__ codes,
                                                               const int32_t* __restrict__ res,
-                                                              int H, int W,
+                                                              int E, int H, int W,
                                                               uint32_t* __restrict__ obs,
                                                               uint32_t* __restrict__ mask,
                                                               Buckets bk) {
-  extern __shared__ uint16_t cs[];
+  extern __shared__ uint16_t smem_codes[];
   const int S = H * W;
-  const size_t e = blockIdx.x;
-  const uint16_t* ce = codes + e * S;
-  for (int c = threadIdx.x; c < S; c += blockDim.x) cs[c] = ce[c];
-  __syncthreads();
-  const int r = res[e];
-  for (int c = threadIdx.x; c < S; c += blockDim.x) {
-    const uint16_t code = cs[c];
-    obs[e * S + c] = code_bits(code);
-    uint32_t w[3] = {0u, 0u, 0u};
-    const int t = code_type(code);
-    // own (owner 1), idle (act noop <=> busy == 0), not a resource
-    if (code_owner(code) == 1 && code_act(code) == A_NOOP && t != RESOURCE && t != NONE) {
-      const int x = c % W, y = c / W;
-      setb(w, kSegOff[0] + A_NOOP);
-      bool any_move = false, any_harv = false, any_ret = false, any_prod = false, any_att = false;
-      const bool mobile = t >= WORKER;
-      const int carried = code_res(code);
-#pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int nx = x + kDX[d], ny = y + kDY[d];
-        if (nx < 0 || ny < 0 || nx >= W || ny >= H) continue;
-        const uint16_t nc = cs[ny * W + nx];
-        const int nt = code_type(nc);
-        if (nt == NONE) {
-          if (mobile) { setb(w, kSegOff[1] + d); any_move = true; }
-          const bool can_prod = (t == BASE && r >= spec_cost(WORKER)) ||
-                                (t == BARRACKS && r >= spec_cost(LIGHT)) ||
-                                (t == WORKER && r >= spec_cost(BARRACKS));
-          if (can_prod) { setb(w, kSegOff[4] + d); any_prod = true; }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint16_t* cs = smem_codes + wave * S;
+  const int Q = (S + 63) >> 6;  // cells per lane
+  const int c0 = lane * Q, c1 = min(S, c0 + Q);
+  const bool vec4 = Q == 4 && (S & 3) == 0;  // 16x16: whole-lane vector stores
+  const int ngroups = (E + kEnvsPerWG - 1) / kEnvsPerWG;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {  // uniform trip count
+    const int e = grp * kEnvsPerWG + wave;
+    const bool live = e < E;
+    if (live) {
+      const uint16_t* ce = codes + (size_t)e * S;
+      if (vec4) *(uint2*)(cs + c0) = *(const uint2*)(ce + c0);
+      else
+        for (int c = c0; c < c1; ++c) cs[c] = ce[c];
+    }
+    __syncthreads();
+    if (live) {
+      const int r = res[e];
+      uint32_t ob[4], mk[12];
+      for (int c = c0; c < c1; ++c) {
+        uint32_t w[3];
+        cell_mask(cs, c, H, W, r, w);
+        const uint32_t bits = code_bits(cs[c]);
+        if (vec4) {
+          const int j = c - c0;
+          ob[j] = bits;
+          mk[3 * j] = w[0]; mk[3 * j + 1] = w[1]; mk[3 * j + 2] = w[2];
         } else {
-          if (t == WORKER && nt == RESOURCE && carried == 0 && code_res(nc) > 0) {
-            setb(w, kSegOff[2] + d); any_harv = true;
-          }
-          if (t == WORKER && nt == BASE && code_owner(nc) == 1 && carried > 0) {
-            setb(w, kSegOff[3] + d); any_ret = true;
-          }
+          obs[(size_t)e * S + c] = bits;
+          uint32_t* m = mask + ((size_t)e * S + c) * 3;
+          m[0] = w[0]; m[1] = w[1]; m[2] = w[2];
+        }
+        if (BUCKET && (w[0] | w[1] | w[2])) {
+          const int slot = atomicAdd(&bk.cnt[c], 1);
+          bk.bucket[(size_t)c * E + slot] = e;
         }
       }
-      if (any_prod) {
-        if (t == BASE) setb(w, kSegOff[5] + (WORKER - 1));
-        if (t == BARRACKS) {
-          if (r >= spec_cost(LIGHT)) setb(w, kSegOff[5] + (LIGHT - 1));
-          if (r >= spec_cost(HEAVY)) setb(w, kSegOff[5] + (HEAVY - 1));
-          if (r >= spec_cost(RANGED)) setb(w, kSegOff[5] + (RANGED - 1));
-        }
-        if (t == WORKER) {
-          if (r >= spec_cost(BASE)) setb(w, kSegOff[5] + (BASE - 1));
-          if (r >= spec_cost(BARRACKS)) setb(w, kSegOff[5] + (BARRACKS - 1));
+      if (vec4) {
+        *(uint4*)(obs + (size_t)e * S + c0) = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        uint4* m4 = (uint4*)(mask + ((size_t)e * S + c0) * 3);
+        m4[0] = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+        m4[1] = make_uint4(mk[4], mk[5], mk[6], mk[7]);
+        m4[2] = make_uint4(mk[8], mk[9], mk[10], mk[11]);
+      }
+      if (BUCKET) {
+        // every cell's log-prob and 7 action bytes start at zero; the sparse head overwrites
+        // the active cells later in stream order (whole-env 16-byte zeroing: the env's S*7
+        // action bytes and S floats are contiguous)
+        if ((S & 15) == 0 && (((uintptr_t)bk.action | (uintptr_t)bk.cell_lp) & 15) == 0) {
+          uint4* act4 = (uint4*)(bk.action + (size_t)e * S * 7);
+          uint4* lp4 = (uint4*)(bk.cell_lp + (size_t)e * S);
+          for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = make_uint4(0, 0, 0, 0);
+          for (int i = lane; i < S / 4; i += 64) lp4[i] = make_uint4(0, 0, 0, 0);
+        } else {
+          for (int i = lane; i < S * 7; i += 64) bk.action[(size_t)e * S * 7 + i] = 0;
+          for (int i = lane; i < S; i += 64) bk.cell_lp[(size_t)e * S + i] = 0.f;
         }
       }
-      if (spec_damage(t) > 0) {
-        const int R = spec_range(t);
-        for (int ay = -3; ay <= 3; ++ay)
-          for (int ax = -3; ax <= 3; ++ax) {
-            if (ax * ax + ay * ay > R * R || (ax == 0 && ay == 0)) continue;
-            const int tx = x + ax, ty = y + ay;
-            if (tx < 0 || ty < 0 || tx >= W || ty >= H) continue;
-            if (code_owner(cs[ty * W + tx]) == 2) {
-              setb(w, kSegOff[6] + (ay + 3) * 7 + (ax + 3)); any_att = true;
-            }
-          }
-      }
-      if (any_move) setb(w, kSegOff[0] + A_MOVE);
-      if (any_harv) setb(w, kSegOff[0] + A_HARVEST);
-      if (any_ret) setb(w, kSegOff[0] + A_RETURN);
-      if (any_prod) setb(w, kSegOff[0] + A_PRODUCE);
-      if (any_att) setb(w, kSegOff[0] + A_ATTACK);
     }
-    uint32_t* m = mask + (e * S + c) * 3;
-    m[0] = w[0];
-    m[1] = w[1];
-    m[2] = w[2];
-    if (BUCKET && (w[0] | w[1] | w[2])) {
-      const int slot = atomicAdd(&bk.cnt[c], 1);
-      bk.bucket[(size_t)c * gridDim.x + slot] = (int)e;
-    }
+    __syncthreads();  // cs reused by the next group
   }
-  if (BUCKET) {
-    // every cell's log-prob and 7 action bytes start at zero; the sparse head overwrites the
-    // active cells later in stream order. Whole-env zeroing with 16-byte stores (the env's
-    // S*7 action bytes and S floats are contiguous) instead of 1 + 7 scalar byte stores per
-    // inactive cell: profile 18, decode was 10 % of the bench's GPU time
-    if ((S & 15) == 0 && (((uintptr_t)bk.action | (uintptr_t)bk.cell_lp) & 15) == 0) {
-      uint4* act4 = (uint4*)(bk.action + e * S * 7);
-      uint4* lp4 = (uint4*)(bk.cell_lp + e * S);
-      for (int i = threadIdx.x; i < S * 7 / 16; i += blockDim.x) act4[i] = make_uint4(0, 0, 0, 0);
-      for (int i = threadIdx.x; i < S / 4; i += blockDim.x) lp4[i] = make_uint4(0, 0, 0, 0);
-    } else {
-      for (int i = threadIdx.x; i < S * 7; i += blockDim.x) bk.action[e * S * 7 + i] = 0;
-      for (int i = threadIdx.x; i < S; i += blockDim.x) bk.cell_lp[e * S + i] = 0.f;
-    }
+}
+
+int decode_grid(int E) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
   }
+  const int ngroups = (E + kEnvsPerWG - 1) / kEnvsPerWG;
+  return max(1, min(ngroups, cus * 8));  // 8 resident 256-thread workgroups per CU
 }
 
 __global__ __launch_bounds__(256) void pack_env_actions_kernel(const uint8_t* __restrict__ act,
@@ -150,8 +205,10 @@ __global__ __launch_bounds__(256) void pack_env_actions_kernel(const uint8_t* __
 extern "C" int mbk_decode_obs_mask(const uint16_t* codes, const int32_t* res, int n_envs, int H,
                                    int W, uint32_t* obs, uint32_t* mask, hipStream_t stream) {
   if (n_envs <= 0) return 0;
-  hipLaunchKernelGGL(decode_obs_mask_kernel<false>, dim3(n_envs), dim3(256), H * W * 2, stream,
-                     codes, res, H, W, obs, mask, Buckets{nullptr, nullptr, nullptr, nullptr});
+  if (H * W > 4096) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(decode_obs_mask_kernel<false>, dim3(decode_grid(n_envs)), dim3(256),
+                     kEnvsPerWG * H * W * 2, stream, codes, res, n_envs, H, W, obs, mask,
+                     Buckets{nullptr, nullptr, nullptr, nullptr});
   return (int)hipGetLastError();
 }
 
@@ -160,8 +217,10 @@ extern "C" int mbk_decode_obs_mask_bucket(const uint16_t* codes, const int32_t* 
                                           int* bucket_cnt, int* bucket, float* cell_lp,
                                           uint8_t* action, hipStream_t stream) {
   if (n_envs <= 0) return 0;
-  hipLaunchKernelGGL(decode_obs_mask_kernel<true>, dim3(n_envs), dim3(256), H * W * 2, stream,
-                     codes, res, H, W, obs, mask, Buckets{bucket_cnt, bucket, cell_lp, action});
+  if (H * W > 4096) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(decode_obs_mask_kernel<true>, dim3(decode_grid(n_envs)), dim3(256),
+                     kEnvsPerWG * H * W * 2, stream, codes, res, n_envs, H, W, obs, mask,
+                     Buckets{bucket_cnt, bucket, cell_lp, action});
   return (int)hipGetLastError();
 }
 
