@@ -29,7 +29,9 @@ from ..ops import cell_head
 from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.head import SparseHead, sparse_sample, sparse_score
 from ..ops.linear import linear, nhwc_weight
-from ..ops.obs import bits_to_planes
+from ..ops.obs import bits_to_planes, dense_to_bits
+
+HIP_CHANNELS = (16, 32)  # conv widths the HIP trunk kernels are instantiated for
 
 
 def layer_init(layer: nn.Module, std: float = math.sqrt(2), bias_const: float = 0.0) -> nn.Module:
@@ -127,8 +129,32 @@ class Agent(nn.Module):
                               cache_enabled=False)
 
     def _use_hip(self, obs: torch.Tensor) -> bool:
-        return (self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32
-                and all(c in (16, 32) for c in self.channels))
+        if not (self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32):
+            return False
+        if not all(c in HIP_CHANNELS for c in self.channels):
+            # no silent vendor-library fallback on the GPU: say what to do instead
+            raise RuntimeError(
+                f"HIP conv kernels exist for channel widths {HIP_CHANNELS}, this Agent has "
+                f"{self.channels}; construct it with hip_kernels=False to run the PyTorch "
+                f"(MIOpen) path instead")
+        return True
+
+    def _compact_obs(self, obs: torch.Tensor) -> torch.Tensor:
+        """Reference-layout float one-hot obs (N, h, w, planes) on the GPU -> the uint32
+        bit-plane form the HIP kernels read, so the reference API runs on the same kernels
+        as the engine (not on MIOpen / hipBLASLt). Other inputs pass through unchanged."""
+        if (self.hip_kernels and obs.is_cuda and obs.is_floating_point()
+                and obs.shape[-1] == self.planes and self.planes <= 32):
+            return dense_to_bits(obs.reshape(-1, self.h, self.w, self.planes))
+        return obs
+
+    def _rng(self, device) -> torch.Tensor:
+        """Philox (seed, step) state for the reference API's on-device sampling."""
+        r = getattr(self, "_api_rng", None)
+        if r is None or r.device != device:
+            seed = int(torch.randint(0, 2**31 - 1, (1,)).item())
+            r = self._api_rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
+        return r
 
     def _act_features(self, obs: torch.Tensor):
         """Acting forward with prepacked weights: conv trunk, then ONE fused launch for
@@ -178,7 +204,11 @@ class Agent(nn.Module):
             return self.network(x)
 
     def policy_value(self, obs: torch.Tensor):
+        """(dense logits [N, 78*h*w], value [N]). On the HIP path both heads run on the
+        hand-written MFMA GEMM (gemm.hip), never on hipBLASLt."""
         f = self.features(obs)
+        if self._use_hip(obs):
+            return linear(f, self.actor), linear(f, self.critic).float().view(-1)
         with self._autocast(f):
             logits = self.actor(f)
             value = self.critic(f)
@@ -282,6 +312,9 @@ class Agent(nn.Module):
         input_dict["obs"]: (1,1,n,h,w,27) when acting, (N,h,w,27) when learning;
         ["action_mask"]: (1,n,78hw) / (N,78hw); ["action"] (N,7hw) when learning.
         Returns ({action, policy_logits, logprobs, baseline[, entropy]}, ()).
+        On the GPU the one-hot obs are packed to bit planes and the whole call runs on the
+        HIP kernels: conv trunk, gemm.hip for the dense actor logits (the reference output
+        includes them), masked_cell.hip for the per-cell masked categoricals.
         """
         obs = input_dict["obs"]
         mask = input_dict["action_mask"]
@@ -289,10 +322,26 @@ class Agent(nn.Module):
             obs = obs.reshape(-1, self.h, self.w, self.planes)
             mask = mask.reshape(obs.shape[0], -1)
         n = obs.shape[0]
-        maskb = mask.reshape(n, self.h * self.w, cell_head.CELL).bool()
+        S = self.h * self.w
+        maskb = mask.reshape(n, S, cell_head.CELL).bool()
+        obs = self._compact_obs(obs)
         logits, value = self.policy_value(obs)
+        if self._use_hip(obs):
+            mbits = cell_head.pack_mask(maskb)
+            lg = logits.float()
+            if learning:
+                a = input_dict["action"].reshape(n, S, cell_head.COMPS).to(torch.uint8)
+                logp, ent = cell_head.score(lg, mbits, a)
+                out = dict(action=a.view(n, -1).long(), policy_logits=lg, logprobs=logp,
+                           baseline=value.view(1, -1), entropy=ent)
+            else:
+                with torch.no_grad():
+                    act, logp = cell_head.sample(lg, mbits, self._rng(lg.device))
+                out = dict(action=act.view(n, -1).long(), policy_logits=lg, logprobs=logp,
+                           baseline=value.view(1, -1))
+            return out, ()
         if learning:
-            a = input_dict["action"].reshape(n, self.h * self.w, cell_head.COMPS)
+            a = input_dict["action"].reshape(n, S, cell_head.COMPS)
             act, logp, ent = cell_head.cell_head_torch(logits.float(), maskb, a)
             out = dict(action=act.view(n, -1).long(), policy_logits=logits.float(), logprobs=logp,
                        baseline=value.view(1, -1), entropy=ent)
@@ -307,7 +356,7 @@ class Agent(nn.Module):
         obs = input_dict["obs"]
         if not learning:
             obs = obs.reshape(-1, self.h, self.w, self.planes)
-        return self.policy_value(obs)[1].view(-1, 1)
+        return self.policy_value(self._compact_obs(obs))[1].view(-1, 1)
 
 
 def num_params(model: nn.Module) -> int:

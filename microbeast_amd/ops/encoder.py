@@ -14,6 +14,7 @@ inner conv output.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 
 import torch
@@ -51,6 +52,10 @@ def _nch(c: int) -> int:
 
 _PF_FWD = 8 * 256    # conv_fwd register-prefetch capacity (elements per group)
 _PF_WGRAD = 4 * 256  # conv_wgrad prefetch capacity, X and dY each
+# conv_fwd workgroup sizing knobs (A/B via tools/microbench.py): LDS budget per workgroup
+# (48 KB = 3 workgroups per CU) and the target output pixels per image group
+_FWD_LDS = int(os.environ.get("MBK_CONV_LDS_KB", "48")) * 1024
+_FWD_PIX = int(os.environ.get("MBK_CONV_PIX", "512"))
 
 
 def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
@@ -60,10 +65,10 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
     hw = layer.H * layer.W
     epp = 1 if bits else cin // 8
     pixb = (cin + 8) if fp8 else (cin * 2 + 16)  # bit planes are expanded in LDS
-    imgs = max(1, 512 // hw)
+    imgs = max(1, _FWD_PIX // hw)
     while imgs > 1:
         sm = imgs * (layer.H + 2) * (layer.W + 2) * pixb + (imgs * hw * (cout + 4) * 2 if pool else 0)
-        if sm <= 48 * 1024 and imgs * hw * epp <= _PF_FWD:
+        if sm <= _FWD_LDS and imgs * hw * epp <= _PF_FWD:
             break
         imgs //= 2
     return imgs

@@ -39,6 +39,8 @@ def _actor_main(actor_id: int, flags_dict: dict, buffers, free_ring: ShmRing, fu
     policy, or from the learner process's inference server when ``client`` is given."""
     os.environ["OMP_NUM_THREADS"] = "1"
     torch.set_num_threads(1)
+    if not (free_ring.alive and full_ring.alive):
+        return  # the runtime stopped before this actor finished spawning
     from ..config import Flags
     from ..envs.synthetic import create_env
     from ..models.factory import make_model

@@ -78,7 +78,17 @@ class ShmRing:
         return {"capacity": self.capacity, "name": self.name}
 
     def __setstate__(self, st):
-        self.__init__(st["capacity"], st["name"], create=False)
+        try:
+            self.__init__(st["capacity"], st["name"], create=False)
+        except FileNotFoundError:
+            # the owner already shut down and unlinked the ring while this (slow-spawning)
+            # child was still starting: come up as a dead handle, the child then exits quietly
+            self.capacity, self.name, self._owner = st["capacity"], st["name"], False
+            self.shm = self.ring = None
+
+    @property
+    def alive(self) -> bool:
+        return self.ring is not None
 
     def push(self, v: int, timeout: float = -1.0) -> bool:
         return self.ring.push(int(v), timeout)
@@ -94,6 +104,8 @@ class ShmRing:
 
     def unlink(self):
         self.ring = None
+        if self.shm is None:
+            return
         try:
             self.shm.close()
         except BufferError:

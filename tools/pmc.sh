@@ -6,13 +6,15 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 name=$1; shift
+script=$1; shift
+case $script in /*) ;; *) script=$R/$script ;; esac  # the passes run from /tmp
 cd /tmp && export TMPDIR=/tmp
 run() {  # run <dir> <counters...>
   local d=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace -d /tmp/${name}_$d -o run \
     --output-format csv -- python "${ARGS[@]}" > $R/gpurun_out/${name}_$d.log 2>&1
 }
-ARGS=("$@")
+ARGS=("$script" "$@")
 run p1 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS GRBM_GUI_ACTIVE || exit 2
 run p2 FETCH_SIZE || exit 3
 run p3 WRITE_SIZE || exit 4
