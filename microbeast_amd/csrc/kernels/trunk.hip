@@ -111,12 +111,24 @@ __device__ __forceinline__ void wstore(char* lw, int n16, int nch, const uint4 r
   }
 }
 
-template <int CIN, int COUT>
+// The whole dynamic LDS of trunk_tail_kernel. conv_lds below is noinline (see there), so it
+// must address the tiles through this LDS array with 32-bit offsets: a generic char*
+// argument lowered every fragment read / epilogue store to flat_load / flat_store with
+// 64-bit address math and s_waitcnt vmcnt(0) lgkmcnt(0) (it could be global memory).
+extern __shared__ __attribute__((aligned(16))) char trunk_smem[];
+
+enum ConvOut : int { OUT_TILE = 0, OUT_TILE_ADD = 1, OUT_STAGE = 2 };
+
+template <int CIN, int COUT, bool RELU, int MODE, bool WLDS>
 // noinline: works around an LLVM CGSCC-pass crash (ROCm 7.2) when fully force-inlined
-// lw: the layer's weights, rows of wstride bytes (LDS-staged, padded) or global (packed)
-__device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W, int nimg, const char* lw,
-                         int wstride, const float* __restrict__ bias, bool relu_in, char* out,
-                         bool add, bf16* stg) {
+// in / out: byte offsets of halo'd tiles in trunk_smem (out of a MODE == OUT_STAGE call: a
+// dense bf16 staging [nimg][H][W][COUT]); weights: LDS offset (WLDS, rows of wstride bytes)
+// or the packed global buffer [COUT][NCH][32] (read as global memory, address space 1)
+__device__ __attribute__((noinline)) void conv_lds(int in, int H, int W, int nimg, int lw_off,
+                                                   const bf16* gw, int wstride,
+                                                   const float* __restrict__ bias, int out) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef const __attribute__((address_space(1))) u32x4* GU4;
   constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
   constexpr int PI = TG<CIN>::PIXB, PO = TG<COUT>::PIXB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -125,15 +137,26 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
   Frag8 bw[NCH][NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const char* wr = lw + (nb * 16 + li) * wstride + g * 16;
+    if constexpr (WLDS) {
+      const int wr = lw_off + (nb * 16 + li) * wstride + g * 16;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) bw[c][nb].u = *(const uint4*)(wr + c * 64);
+      for (int c = 0; c < NCH; ++c) bw[c][nb].u = *(const uint4*)(trunk_smem + wr + c * 64);
+    } else {
+      GU4 wr = (GU4)((const char*)gw + (nb * 16 + li) * wstride + g * 16);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const u32x4 v = wr[c * 4];
+        bw[c][nb].u = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    }
   }
+  typedef const __attribute__((address_space(1))) f32x4* GF4;
   float bv[NB][4];
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bv[nb][i] = bias[nb * 16 + 4 * g + i];
+  for (int nb = 0; nb < NB; ++nb) {
+    const f32x4 b4 = ((GF4)bias)[(nb * 16 + 4 * g) / 4];
+    bv[nb][0] = b4[0]; bv[nb][1] = b4[1]; bv[nb][2] = b4[2]; bv[nb][3] = b4[3];
+  }
   const int M = nimg * HW, nblk = (M + 15) >> 4;
   constexpr int NW = kThreads / 64;
   // Two pixel blocks per wave iteration (pb, pb + NW): two independent MFMA chains and
@@ -156,11 +179,12 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bv[nb][i];
-      if (stg) {
-        *(uint2*)(stg + (size_t)m * COUT + co0) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      if constexpr (MODE == OUT_STAGE) {
+        *(uint2*)(trunk_smem + out + (m * COUT + co0) * 2) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       } else {
-        char* p = out + (((im * Hp + y + 1) * Wp + x + 1) * PO + co0 * 2);
-        if (add) {
+        char* p = trunk_smem + out + (((im * Hp + y + 1) * Wp + x + 1) * PO + co0 * 2);
+        if constexpr (MODE == OUT_TILE_ADD) {
           const uint2 ad = *(const uint2*)p;
           v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
         }
@@ -176,7 +200,7 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
       const int mm = m < M ? m : 0;  // rows past M compute garbage that is never stored
       const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-      base[j] = (im * Hp + y) * Wp + x;
+      base[j] = in + ((im * Hp + y) * Wp + x) * PI;
     }
     f32x4 acc[2][NB];
 #pragma unroll
@@ -189,12 +213,13 @@ __device__ __attribute__((noinline)) void conv_lds(const char* in, int H, int W,
       if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
       else { tap = c; ch0 = 8 * g; }
       const int tapc = tap < 9 ? tap : 8;
-      const int toff = (tapc / 3) * Wp + (tapc % 3);
+      const int toff = ((tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2;
       Frag8 a[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        a[j].u = *(const uint4*)(in + (base[j] + toff) * PI + ch0 * 2);
-        if (relu_in) a[j].u = make_uint4(relu2(a[j].u.x), relu2(a[j].u.y), relu2(a[j].u.z), relu2(a[j].u.w));
+        a[j].u = *(const uint4*)(trunk_smem + base[j] + toff);
+        if constexpr (RELU)
+          a[j].u = make_uint4(relu2(a[j].u.x), relu2(a[j].u.y), relu2(a[j].u.z), relu2(a[j].u.w));
         // (CIN 16, tap 9 = the pad half of chunk 4: its packed weights are zero, so the
         // finite pixel read for it adds exactly 0 and needs no zeroing)
       }
@@ -255,10 +280,12 @@ __device__ __forceinline__ int tail_n16(int l) {
 
 template <bool LDSW>  // weights staged in LDS (double-buffered) vs read through L2
 __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* R1 = smem;
-  char* R2 = smem + a.r1_bytes;
-  char* WB[2] = {smem + 2 * a.r1_bytes, smem + 2 * a.r1_bytes + kWBufBytes};
+  char* smem = trunk_smem;
+  const int oR1 = 0, oR2 = a.r1_bytes;  // region offsets for conv_lds
+  const int oWB[2] = {2 * a.r1_bytes, 2 * a.r1_bytes + kWBufBytes};
+  char* R1 = smem + oR1;
+  char* R2 = smem + oR2;
+  char* WB[2] = {smem + oWB[0], smem + oWB[1]};
   const int H0 = a.H0, W0 = a.W0, H1 = (H0 + 1) >> 1, W1 = (W0 + 1) >> 1;
   const int H2 = (H1 + 1) >> 1, W2 = (W1 + 1) >> 1;
   const int TNI = a.tni;
@@ -270,15 +297,17 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   }
   // phase helper (LDSW): prefetch layer l+1 (wrapping to 0 for the next group) into
   // registers, run conv l from WB[l & 1], park l+1 in the other buffer
-#define TAIL_PHASE(l, CI, CO, IN, H_, W_, WBUF, ...)                                        \
+#define TAIL_PHASE(l, CI, CO, RELU, MODE, IN, H_, W_, WBUF, OUT)                          \
   do {                                                                                      \
     if (LDSW) {                                                                             \
       const int ln = ((l) + 1) % 14;                                                        \
       wload(a.w[ln], tail_n16(ln), wr);                                                     \
-      conv_lds<CI, CO>(IN, H_, W_, nimg, WBUF, wrow_bytes<CI>(), __VA_ARGS__);              \
+      conv_lds<CI, CO, RELU, MODE, true>(IN, H_, W_, nimg, WBUF, nullptr, wrow_bytes<CI>(), \
+                                         a.b[l], OUT);                                      \
       wstore(WB[ln & 1], tail_n16(ln), ln < 5 ? TG<16>::NCH : TG<32>::NCH, wr);             \
     } else {                                                                                \
-      conv_lds<CI, CO>(IN, H_, W_, nimg, (const char*)a.w[l], TG<CI>::NCH * 64, __VA_ARGS__); \
+      conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, a.w[l], TG<CI>::NCH * 64,    \
+                                          a.b[l], OUT);                                     \
     }                                                                                       \
   } while (0)
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
@@ -299,13 +328,13 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     __syncthreads();
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(2 * rb, 16, 16, R1, H0, W0, WB[0], a.b[2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(2 * rb, 16, 16, true, OUT_TILE, oR1, H0, W0, oWB[0], oR2);
       __syncthreads();
-      TAIL_PHASE(2 * rb + 1, 16, 16, R2, H0, W0, WB[1], a.b[2 * rb + 1], true, R1, true, nullptr);
+      TAIL_PHASE(2 * rb + 1, 16, 16, true, OUT_TILE_ADD, oR2, H0, W0, oWB[1], oR1);
       __syncthreads();
     }
     // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1)
-    TAIL_PHASE(4, 16, 32, R1, H0, W0, WB[0], a.b[4], false, nullptr, false, (bf16*)R2);
+    TAIL_PHASE(4, 16, 32, false, OUT_STAGE, oR1, H0, W0, oWB[0], oR2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
     zero_halo(R1, nimg, H1, W1, TG<32>::PIXB);
@@ -313,13 +342,13 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     zero_halo(R2, nimg, H1, W1, TG<32>::PIXB);  // U1 layout (staging consumed)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(5 + 2 * rb, 32, 32, R1, H1, W1, WB[1], a.b[5 + 2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(5 + 2 * rb, 32, 32, true, OUT_TILE, oR1, H1, W1, oWB[1], oR2);
       __syncthreads();
-      TAIL_PHASE(6 + 2 * rb, 32, 32, R2, H1, W1, WB[0], a.b[6 + 2 * rb], true, R1, true, nullptr);
+      TAIL_PHASE(6 + 2 * rb, 32, 32, true, OUT_TILE_ADD, oR2, H1, W1, oWB[0], oR1);
       __syncthreads();
     }
     // ---- stage 2
-    TAIL_PHASE(9, 32, 32, R1, H1, W1, WB[1], a.b[9], false, nullptr, false, (bf16*)R2);
+    TAIL_PHASE(9, 32, 32, false, OUT_STAGE, oR1, H1, W1, oWB[1], oR2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
     zero_halo(R1, nimg, H2, W2, TG<32>::PIXB);
@@ -327,9 +356,9 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     zero_halo(R2, nimg, H2, W2, TG<32>::PIXB);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(10 + 2 * rb, 32, 32, R1, H2, W2, WB[0], a.b[10 + 2 * rb], true, R2, false, nullptr);
+      TAIL_PHASE(10 + 2 * rb, 32, 32, true, OUT_TILE, oR1, H2, W2, oWB[0], oR2);
       __syncthreads();
-      TAIL_PHASE(11 + 2 * rb, 32, 32, R2, H2, W2, WB[1], a.b[11 + 2 * rb], true, R1, true, nullptr);
+      TAIL_PHASE(11 + 2 * rb, 32, 32, true, OUT_TILE_ADD, oR2, H2, W2, oWB[1], oR1);
       __syncthreads();
     }
 #undef TAIL_PHASE
