@@ -247,6 +247,13 @@ PYBIND11_MODULE(_mbrt, m) {
         buf.value = b["value"].cast<uintptr_t>();
         buf.reward = b["reward"].cast<uintptr_t>();
         buf.done = b["done"].cast<uintptr_t>();
+        auto opt = [&](const char* k) {
+          return b.contains(k) ? b[k].cast<uintptr_t>() : (uintptr_t)0;
+        };
+        buf.ep_return = opt("ep_return");
+        buf.ep_step = opt("ep_step");
+        buf.last_action0 = opt("last_action0");
+        buf.logits = opt("policy_logits");
         auto get = [](py::dict d, const char* k) {
           return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0;
         };
@@ -264,6 +271,7 @@ PYBIND11_MODULE(_mbrt, m) {
           io.in_codes_p1 = get(d, "in_codes_p1");
           io.in_res_p1 = get(d, "in_res_p1");
           io.out_act16_p1 = get(d, "out_act16_p1");
+          io.out_logits = get(d, "out_logits");
           buf.lanes.push_back(io);
         }
         return new GpuEngine(cfg, buf);
@@ -295,6 +303,7 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
       .def("stream", &GpuEngine::stream, py::arg("lane") = 0)
       .def("failed", &GpuEngine::failed)
+      .def("inject_fault", &GpuEngine::inject_fault)
       .def("error", &GpuEngine::error)
       .def("stats", [](GpuEngine& e) {
         EngineStats s = e.stats();

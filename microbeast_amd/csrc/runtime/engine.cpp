@@ -72,6 +72,12 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   CTOR_CHECK(hipHostMalloc((void**)&h_done_, (size_t)total, hipHostMallocDefault));
   std::memset(h_reward_, 0, (size_t)total * 4);
   std::memset(h_done_, 0, (size_t)total);
+  if (buf_.ep_return || buf_.ep_step) {
+    CTOR_CHECK(hipHostMalloc((void**)&h_ep_return_, (size_t)total * 4, hipHostMallocDefault));
+    CTOR_CHECK(hipHostMalloc((void**)&h_ep_step_, (size_t)total * 4, hipHostMallocDefault));
+    std::memset(h_ep_return_, 0, (size_t)total * 4);
+    std::memset(h_ep_step_, 0, (size_t)total * 4);
+  }
   if (cfg_.selfplay_groups < 0 || cfg_.selfplay_groups > cfg_.n_groups)
     throw std::runtime_error("GpuEngine: bad selfplay_groups");
   const int sp0 = cfg_.n_groups - cfg_.selfplay_groups;  // first self-play group
@@ -146,6 +152,8 @@ GpuEngine::~GpuEngine() {
   if (h_res_) hipHostFree(h_res_);
   if (h_act16_) hipHostFree(h_act16_);
   if (h_reward_) hipHostFree(h_reward_);
+  if (h_ep_return_) hipHostFree(h_ep_return_);
+  if (h_ep_step_) hipHostFree(h_ep_step_);
   if (h_done_) hipHostFree(h_done_);
   for (Lane& L : lanes_) {
     if (L.stream) hipStreamDestroy(L.stream);
@@ -244,13 +252,23 @@ void GpuEngine::worker_loop(int wid) {
         int e1 = std::min(e + chunk_, E);
         const int a0 = g * E;
         auto t0 = std::chrono::steady_clock::now();
-        if (G.selfplay)
-          env_->step_range_codes_sp(a0 + e, a0 + e1, h_act16_, h_act16_p1_, h_codes_, h_res_,
-                                    h_codes_p1_, h_res_p1_, h_reward_, h_done_, &log_,
-                                    G.opp_version);
-        else
-          env_->step_range_codes(a0 + e, a0 + e1, h_act16_, h_codes_, h_res_, h_reward_,
-                                 h_done_, &log_);
+        try {
+          if (inject_fault_.exchange(0) != 0)
+            throw std::runtime_error("injected env-worker fault (--fault_inject_every)");
+          if (G.selfplay)
+            env_->step_range_codes_sp(a0 + e, a0 + e1, h_act16_, h_act16_p1_, h_codes_, h_res_,
+                                      h_codes_p1_, h_res_p1_, h_reward_, h_done_, &log_,
+                                      G.opp_version, h_ep_return_, h_ep_step_);
+          else
+            env_->step_range_codes(a0 + e, a0 + e1, h_act16_, h_codes_, h_res_, h_reward_,
+                                   h_done_, &log_, h_ep_return_, h_ep_step_);
+        } catch (const std::exception& ex) {
+          // a failing env worker must not std::terminate the learner process: the engine
+          // stops, get_full() wakes up, and Python (GpuActorRuntime.check) raises with this
+          // message so the trainer can rebuild the actor side (train.py recovery)
+          fail("env worker " + std::to_string(wid) + ": " + ex.what());
+          return;
+        }
         env_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                               std::chrono::steady_clock::now() - t0).count(),
                           std::memory_order_relaxed);
@@ -396,8 +414,20 @@ bool GpuEngine::enqueue_gpu(int g) {
     const size_t ri = t > 0 ? t - 1 : T - 1;
     seg[n++] = {(const void*)(h_reward_ + e0), f32_at(buf_.reward, rs, ri), E * 4};
     seg[n++] = {(const void*)(h_done_ + e0), u8_at(buf_.done, rs, ri), E};
+    if (buf_.ep_return)
+      seg[n++] = {(const void*)(h_ep_return_ + e0), f32_at(buf_.ep_return, rs, ri), E * 4};
+    if (buf_.ep_step)
+      seg[n++] = {(const void*)(h_ep_step_ + e0), f32_at(buf_.ep_step, rs, ri), E * 4};
   }
+  if (buf_.logits && io.out_logits)
+    seg[n++] = {(const void*)io.out_logits,
+                (char*)buf_.logits + (G.cur * slot_stride_scalar_ + t * E) * (size_t)S_ * 78 * 4,
+                E * (size_t)S_ * 78 * 4};
   const bool close_prev = (t == 0 && G.prev >= 0);
+  if (close_prev && buf_.last_action0)  // the action taken just before this slot's row 0
+    seg[n++] = {(const void*)act_at(G.prev, T - 1),
+                (char*)buf_.last_action0 + (size_t)G.cur * E * S_ * kActComps,
+                E * S_ * kActComps};
   if (close_prev) {
     seg[n++] = {(const void*)io.in_obs, obs_at(G.prev, T), E * S_ * 4};
     seg[n++] = {(const void*)io.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};

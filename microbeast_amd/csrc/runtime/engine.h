@@ -74,6 +74,7 @@ struct LaneIO {
   uintptr_t in_codes = 0, in_res = 0, out_act16 = 0;
   // opponent graph I/O (self-play groups only)
   uintptr_t in_codes_p1 = 0, in_res_p1 = 0, out_act16_p1 = 0;
+  uintptr_t out_logits = 0;  // dense policy logits [E][78*S] f32 (reference keys only)
 };
 
 // Per-lane graphs (raw hipGraphExec_t). opp: opponent policy (self-play only); pack /
@@ -93,6 +94,11 @@ struct EngineBuffers {
   uintptr_t value = 0;    // f32
   uintptr_t reward = 0;   // f32
   uintptr_t done = 0;     // u8
+  // optional reference buffer keys (libs/utils.py:34-46); 0 = not emitted
+  uintptr_t ep_return = 0;     // f32 [.., E]   running episode return after the step
+  uintptr_t ep_step = 0;       // i32 [.., E]   running episode length after the step
+  uintptr_t last_action0 = 0;  // u8 [n_slots, E, S, 7]: the action before row 0 of a slot
+  uintptr_t logits = 0;        // f32 [.., E, 78*S] dense policy logits
   std::vector<LaneIO> lanes;  // one per policy lane
 };
 
@@ -157,6 +163,8 @@ class GpuEngine {
   const EngineConfig& config() const { return cfg_; }
   VecEnv& env() { return *env_; }
   bool failed() const { return failed_.load(); }
+  // Fault injection (tests / --fault_inject_every): the next env step of some worker throws.
+  void inject_fault() { inject_fault_.store(1); }
   std::string error() const;
 
  private:
@@ -212,6 +220,8 @@ class GpuEngine {
   uint16_t* h_codes_p1_ = nullptr;  // self-play: opponent-perspective codes
   int32_t* h_res_p1_ = nullptr;
   uint16_t* h_act16_p1_ = nullptr;  // opponent's packed actions (its frame)
+  float* h_ep_return_ = nullptr;     // reference keys: per-env episode return / length
+  int32_t* h_ep_step_ = nullptr;
 
   // slots
   std::mutex slot_m_;
@@ -236,6 +246,7 @@ class GpuEngine {
   std::atomic<uint64_t> work_epoch_{0};
   std::atomic<bool> running_{false};
   std::atomic<bool> failed_{false};
+  std::atomic<int> inject_fault_{0};
   mutable std::mutex err_m_;
   std::string err_;
 

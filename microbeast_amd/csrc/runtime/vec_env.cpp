@@ -74,7 +74,8 @@ void VecEnv::reset_codes_p1(uint16_t* codes_p1, int32_t* res_p1) const {
 }
 
 void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t* codes,
-                              int32_t* res, float* reward, uint8_t* done, EpisodeLog* log) {
+                              int32_t* res, float* reward, uint8_t* done, EpisodeLog* log,
+                              float* ep_return, int32_t* ep_step) {
   const size_t S = (size_t)size_ * size_;
   for (int i = e0; i < e1; ++i) {
     // two envs ahead: the sim object; one ahead: its unit list and grid
@@ -90,6 +91,8 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
     const float r = sims_[i]->step_packed(actions + (size_t)i * S, &d);
     ep_ret_[i] += r;
     ep_len_[i] += 1;
+    if (ep_return) ep_return[i] = ep_ret_[i];
+    if (ep_step) ep_step[i] = ep_len_[i];
     if (d) {
       if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner(), -1 - sims_[i]->bot()});
       ep_ret_[i] = 0.f;
@@ -105,7 +108,8 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
 void VecEnv::step_range_codes_sp(int e0, int e1, const uint16_t* actions,
                                  const uint16_t* opp_actions, uint16_t* codes, int32_t* res,
                                  uint16_t* codes_p1, int32_t* res_p1, float* reward,
-                                 uint8_t* done, EpisodeLog* log, int opponent) {
+                                 uint8_t* done, EpisodeLog* log, int opponent,
+                                 float* ep_return, int32_t* ep_step) {
   const size_t S = (size_t)size_ * size_;
   for (int i = e0; i < e1; ++i) {
     if (i + 2 < e1) __builtin_prefetch(sims_[i + 2].get());
@@ -117,6 +121,8 @@ void VecEnv::step_range_codes_sp(int e0, int e1, const uint16_t* actions,
                        : sim.step_packed(actions + (size_t)i * S, &d);
     ep_ret_[i] += r;
     ep_len_[i] += 1;
+    if (ep_return) ep_return[i] = ep_ret_[i];
+    if (ep_step) ep_step[i] = ep_len_[i];
     if (d) {
       if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sim.winner(), sp ? opponent : -1 - sim.bot()});
       ep_ret_[i] = 0.f;

@@ -61,14 +61,18 @@ class VecEnv {
   void reset_codes(uint16_t* codes, int32_t* res);
   // current player-1 codes / resources of the self-play envs (after reset_codes)
   void reset_codes_p1(uint16_t* codes_p1, int32_t* res_p1) const;
+  // ep_return / ep_step (optional, per env): running episode return / length after the step
+  // (before the reset of a finished episode), the reference's Env_Packer keys
   void step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t* codes, int32_t* res,
-                        float* reward, uint8_t* done, EpisodeLog* log);
+                        float* reward, uint8_t* done, EpisodeLog* log,
+                        float* ep_return = nullptr, int32_t* ep_step = nullptr);
   // Self-play variant: envs with an external opponent also take its packed actions
   // (opp_actions, its mirrored frame) and emit its codes / resources; their finished
   // episodes are tagged with `opponent` (the league snapshot that was playing).
   void step_range_codes_sp(int e0, int e1, const uint16_t* actions, const uint16_t* opp_actions,
                            uint16_t* codes, int32_t* res, uint16_t* codes_p1, int32_t* res_p1,
-                           float* reward, uint8_t* done, EpisodeLog* log, int opponent);
+                           float* reward, uint8_t* done, EpisodeLog* log, int opponent,
+                           float* ep_return = nullptr, int32_t* ep_step = nullptr);
   void set_external_opponent(int e0, int e1, bool on);
   // Dense reference layout for parity tools: obs f32 (n,s,s,27), mask u8 (n,s*s*78)
   void dense_obs(float* out) const;

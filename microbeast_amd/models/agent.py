@@ -261,9 +261,11 @@ class Agent(nn.Module):
 
     @torch.no_grad()
     def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
-            logp_out=None, bucketed: bool = False):
+            logp_out=None, bucketed: bool = False, logits_out=None):
         """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N]).
-        bucketed: the head's active pairs were bucketed by mbk_decode_obs_mask_bucket."""
+        bucketed: the head's active pairs were bucketed by mbk_decode_obs_mask_bucket.
+        logits_out: also write the dense policy logits [N, 78*h*w] (reference 'policy_logits';
+        one extra dense head GEMM on gemm.hip, the sparse sampler does not need them)."""
         if self._use_hip(obs):
             # sparse head: only cells with a legal action are computed (ops/head.py)
             pre = self._prepacked
@@ -274,12 +276,16 @@ class Agent(nn.Module):
                 f = self.features(obs)
                 value = linear(f, self.critic).float().view(-1)
             n = f.shape[0]
+            if logits_out is not None:
+                logits_out.copy_(linear(f.to(torch.bfloat16), self.actor).float())
             action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
                                          mask_bits.reshape(n, -1, 3), rng_state,
                                          self._head(f.device), action_out, logp_out,
                                          prepacked=pre, bucketed=bucketed)
             return action, logp, value
         logits, value = self.policy_value(obs)
+        if logits_out is not None:
+            logits_out.copy_(logits.float())
         action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)
         return action, logp, value
 

@@ -51,13 +51,23 @@ def available_cpus() -> int:
     return n
 
 
+class EngineFailure(RuntimeError):
+    """The native engine stopped (an env worker raised, or a HIP call failed); the learner
+    process is intact and may rebuild the actor side (train.py)."""
+
+
 class GpuActorRuntime:
     def __init__(self, make_model, size: int, n_groups: int, envs_per_group: int, unroll: int,
                  batch_slots: int, device: torch.device, n_threads: int | None = None,
                  n_slots: int | None = None, max_steps: int = 2000, seed: int = 1,
                  bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
                  env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False,
-                 n_lanes: int | None = None, policy_cu_every: int = 0):
+                 n_lanes: int | None = None, policy_cu_every: int = 0,
+                 reference_keys: bool = False, policy_logits: bool = False):
+        """reference_keys: also emit the reference buffer keys ep_return / ep_step /
+        last_action (libs/utils.py:34-46) into the slots; policy_logits: plus the dense
+        78*h*w policy logits of every step (the sparse acting head never needs them, so
+        this adds one dense head GEMM per policy step and 312*h*w bytes per frame)."""
         rt = N.runtime()
         self.device = device
         self.size, self.S = size, size * size
@@ -75,6 +85,15 @@ class GpuActorRuntime:
             "reward": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
             "done": torch.zeros(NS, T1, E, dtype=torch.uint8, device=dev),
         }
+        self.reference_keys = reference_keys or policy_logits
+        self.emit_logits = policy_logits
+        if self.reference_keys:
+            self.rb["ep_return"] = torch.zeros(NS, T1, E, dtype=torch.float32, device=dev)
+            self.rb["ep_step"] = torch.zeros(NS, T1, E, dtype=torch.int32, device=dev)
+            self.rb["last_action0"] = torch.zeros(NS, E, S, 7, dtype=torch.uint8, device=dev)
+        if policy_logits:
+            self.rb["policy_logits"] = torch.zeros(NS, T1, E, S * 78, dtype=torch.float32,
+                                                   device=dev)
         # policy lanes: group g steps on lane g % n_lanes; every lane has its own stream,
         # captured graph, I/O buffers, RNG stream and inference-weight copy, so policy steps
         # of different groups can run concurrently. Measured on one MI355X (4 x 4096 envs,
@@ -155,7 +174,8 @@ class GpuActorRuntime:
             "out_value": torch.zeros(E, dtype=torch.float32, device=dev),
             # dense-head (GridNet) sampling workspace, per lane
             "cell_logp": torch.zeros(E * S, dtype=torch.float32, device=dev),
-        }
+        } | ({"out_logits": torch.zeros(E, S * 78, dtype=torch.float32, device=dev)}
+             if getattr(self, "emit_logits", False) else {})
 
     def _policy_step(self, io, m, rng):
         k = N.kernels()
@@ -173,12 +193,15 @@ class GpuActorRuntime:
                 head.bucket.data_ptr(), head.cell_lp.data_ptr(), io["out_action"].data_ptr(),
                 st), "decode_obs_mask_bucket")
             _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
-                                logp_out=io["out_logp"], bucketed=True)
+                                logp_out=io["out_logp"], bucketed=True,
+                                logits_out=io.get("out_logits"))
         else:
             N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
                                           self.E, self.size, self.size, io["in_obs"].data_ptr(),
                                           io["in_mask"].data_ptr(), st), "decode_obs_mask")
             logits, value = m.policy_value(io["in_obs"])
+            if "out_logits" in io:
+                io["out_logits"].copy_(logits.reshape(io["out_logits"].shape))
             cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
                                  cell_logp=io["cell_logp"], logp_out=io["out_logp"])
         io["out_value"].copy_(value)
@@ -245,7 +268,11 @@ class GpuActorRuntime:
 
     def check(self):
         if self.engine.failed():
-            raise RuntimeError(f"GPU actor engine failed: {self.engine.error()}")
+            raise EngineFailure(f"GPU actor engine failed: {self.engine.error()}")
+
+    def inject_fault(self):
+        """Make the next env step of some worker throw (fault-injection tests)."""
+        self.engine.inject_fault()
 
     def get_batch(self, n_slots: int | None = None, timeout: float = 600.0):
         """Block until n full rollout slots exist; return (batch dict, slot ids).
@@ -254,6 +281,7 @@ class GpuActorRuntime:
         events; no host synchronisation with the GPU happens here.
         """
         n = n_slots or self.batch_slots
+        self.check()
         slots = self.engine.get_full(n, timeout)
         self.check()
         if len(slots) < n:
@@ -262,11 +290,18 @@ class GpuActorRuntime:
         sp = N.stream_ptr()
         for s in slots:
             self.engine.stream_wait_full(sp, s)
+        keys = [k for k in self.rb if k != "last_action0"]
         if n == 1:
             s = slots[0]
-            batch = {k: v[s] for k, v in self.rb.items()}
+            batch = {k: self.rb[k][s] for k in keys}
         else:
-            batch = {k: torch.cat([v[s] for s in slots], dim=1) for k, v in self.rb.items()}
+            batch = {k: torch.cat([self.rb[k][s] for s in slots], dim=1) for k in keys}
+        if self.reference_keys:
+            # last_action[t] = the action taken before obs_t: a_{t-1}, row 0 from the group's
+            # previous slot (reference Env_Packer 'last_action'); materialised on request only
+            la = [torch.cat([self.rb["last_action0"][s][None], self.rb["action"][s][:-1]])
+                  for s in slots]
+            batch["last_action"] = la[0] if n == 1 else torch.cat(la, dim=1)
         return batch, slots
 
     def release(self, slots):

@@ -142,18 +142,25 @@ def train(flags: Flags) -> dict:
     if flags.self_play and runtime != "gpu":
         raise RuntimeError("--self_play needs the gpu runtime (the league plays on the GPU engine)")
     if runtime == "gpu":
-        from .runtime.gpu_actors import GpuActorRuntime
+        from .runtime.gpu_actors import EngineFailure, GpuActorRuntime
 
         envs_total = flags.groups * flags.envs_per_group
         sp_groups = min(flags.selfplay_groups, flags.groups) if flags.self_play else 0
-        rt = GpuActorRuntime(lambda: make_model(flags, "cpu"), flags.env_size, flags.groups,
-                             flags.envs_per_group, flags.unroll_length, flags.batch_size, dev,
-                             n_threads=actor_threads,
-                             max_steps=flags.max_episode_steps, seed=flags.seed + 1000 * info.rank,
-                             bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
-                             env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
-                             fp8_policy=flags.fp8_policy or flags.dtype == "fp8",
-                             n_lanes=flags.policy_lanes)
+
+        def make_gpu_runtime(restart: int):
+            """(Re)build the actor side: env workers, policy graphs, HBM slots. A restart
+            gets fresh env seeds; the learner (weights, Adam, league) is untouched."""
+            return GpuActorRuntime(lambda: make_model(flags, "cpu"), flags.env_size,
+                                   flags.groups, flags.envs_per_group, flags.unroll_length,
+                                   flags.batch_size, dev, n_threads=actor_threads,
+                                   max_steps=flags.max_episode_steps,
+                                   seed=flags.seed + 1000 * info.rank + 7777 * restart,
+                                   bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
+                                   env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
+                                   fp8_policy=flags.fp8_policy or flags.dtype == "fp8",
+                                   n_lanes=flags.policy_lanes)
+
+        rt = make_gpu_runtime(0)
         if sp_groups:
             from .runtime.league import League
 
@@ -182,6 +189,7 @@ def train(flags: Flags) -> dict:
         frames_per_update = flags.batch_size * flags.n_envs * flags.unroll_length
     frames_per_update *= info.world_size
 
+    engine_restarts = 0
     prof = None  # --profile_updates: torch.profiler timeline of a few steady-state updates
     t_start = time.perf_counter()
     t_prev = t_start
@@ -205,7 +213,24 @@ def train(flags: Flags) -> dict:
                 prof = _profile_tick(prof, n_update, flags, want_cuda)
             t0 = time.perf_counter()
             if runtime == "gpu":
-                batch, slots = rt.get_batch(timeout=flags.batch_timeout)
+                try:
+                    batch, slots = rt.get_batch(timeout=flags.batch_timeout)
+                except EngineFailure as ex:
+                    # a dead env worker stops the native engine; rebuild the
+                    # actor side and keep training (bounded by --actor_restarts)
+                    if engine_restarts >= flags.actor_restarts:
+                        raise
+                    engine_restarts += 1
+                    log(f"[microbeast_amd] {ex}; restarting the actor engine "
+                        f"({engine_restarts}/{flags.actor_restarts})")
+                    rt.stop()
+                    del rt
+                    rt = make_gpu_runtime(engine_restarts)
+                    rt.start(learner.flat,
+                             opponent_version=league.current if league is not None else -1)
+                    if league is not None:
+                        rt.set_opponent(league.snapshot(league.current), league.current)
+                    continue
                 lag = rt.policy_lag(slots, n_update)
             else:
                 batch, slots = rt.get_batch(flags.batch_timeout)
@@ -228,8 +253,11 @@ def train(flags: Flags) -> dict:
                 sid = league.sample()
                 if sid != league.current and rt.set_opponent(league.snapshot(sid), sid):
                     league.current = sid
-            if flags.fault_inject_every and runtime == "mono" and n_update % flags.fault_inject_every == 0:
-                rt.kill_random_actor()
+            if flags.fault_inject_every and n_update % flags.fault_inject_every == 0:
+                if runtime == "mono":
+                    rt.kill_random_actor()
+                else:
+                    rt.inject_fault()
             if n_update % flags.log_every == 0:
                 t2 = time.perf_counter()
                 period = (t2 - t_prev) / flags.log_every  # loop period, as the reference timed it
@@ -261,7 +289,7 @@ def train(flags: Flags) -> dict:
         logger.close()
     wall = time.perf_counter() - t_start
     out = dict(last, updates=n_update, steps=step, wall_s=wall, checkpoint=ck_path,
-               mean_fps=step / max(wall, 1e-9))
+               mean_fps=step / max(wall, 1e-9), engine_restarts=engine_restarts)
     log(f"[microbeast_amd] done: {out}")
     D.destroy(info)
     return out

@@ -104,3 +104,56 @@ def test_selfplay_league_engine(cuda):
     torch.cuda.synchronize()
     cur = st["opp_version"]
     assert torch.equal(rt.opp_flat.data, league.snapshot(cur)) or cur != league.current
+
+
+def test_engine_reference_keys(cuda):
+    """Optional reference buffer keys (libs/utils.py:34-46) from the engine: ep_step counts
+    1, 2, ... and restarts after done; ep_return is the running sum of reward; last_action[t]
+    is the action of row t-1 (row 0: the previous slot's last action); policy_logits are the
+    dense head's logits, whose masked log-softmax at the sampled action sums to the
+    behaviour log-prob."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.cell_head import cell_head_torch
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+
+    s, T = 8, 8
+
+    def mk():
+        m = Agent((s, s, 27))
+        torch.nn.init.normal_(m.actor.weight, std=0.02)
+        return m
+
+    torch.manual_seed(0)
+    learner = Learner(mk(), LearnerHParams(), cuda)
+    rt = GpuActorRuntime(mk, s, n_groups=1, envs_per_group=16, unroll=T, batch_slots=1,
+                         device=cuda, n_threads=2, max_steps=12, reference_keys=True,
+                         policy_logits=True)
+    rt.start(learner.flat)
+    try:
+        b1, sl1 = rt.get_batch()
+        torch.cuda.synchronize()
+        first = {k: v.clone() for k, v in b1.items()}
+        rt.release(sl1)
+        b2, sl2 = rt.get_batch()
+        torch.cuda.synchronize()
+        second = {k: v.clone() for k, v in b2.items()}
+        rt.release(sl2)
+    finally:
+        rt.stop()
+    for b in (first, second):
+        st, ret = b["ep_step"][:T].cpu(), b["ep_return"][:T].cpu()
+        rew, done = b["reward"][:T].cpu(), b["done"][:T].cpu().bool()
+        for t in range(1, T):
+            prev_done = done[t - 1]
+            exp_step = torch.where(prev_done, torch.ones_like(st[t]), st[t - 1] + 1)
+            assert torch.equal(st[t], exp_step)
+            exp_ret = torch.where(prev_done, rew[t], ret[t - 1] + rew[t])
+            torch.testing.assert_close(ret[t], exp_ret)
+        assert torch.equal(b["last_action"][1:T], b["action"][:T - 1])
+    assert torch.equal(second["last_action"][0], first["action"][T - 1])
+    # behaviour log-prob from the emitted dense logits (fp32 torch semantics)
+    lg = second["policy_logits"][:T].reshape(T * 16, -1).cpu()
+    _, lp, _ = cell_head_torch(lg, second["mask"][:T].reshape(T * 16, s * s, 3).cpu(),
+                               second["action"][:T].reshape(T * 16, s * s, 7).cpu())
+    torch.testing.assert_close(lp, second["logp"][:T].reshape(-1).cpu(), rtol=2e-2, atol=5e-2)

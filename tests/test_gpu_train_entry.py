@@ -90,3 +90,27 @@ def test_gpu_training_improves_return_and_win_rate(cuda, tmp_path):
     (r0, w0), (r1, w1) = stats(first), stats(last)
     print(f"return {r0:.1f} -> {r1:.1f}, win rate {w0:.3f} -> {w1:.3f} over {n} episodes")
     assert r1 > 1.1 * r0 and w1 > w0
+
+
+def test_gpu_engine_fault_injection_recovers(cuda, tmp_path):
+    """SURVEY §5.3 on the flagship runtime: an env worker that throws stops the native
+    engine (instead of terminating the process); train() rebuilds the actor side from the
+    live learner and keeps going, bounded by --actor_restarts."""
+    from microbeast_amd.config import parse_flags
+    from microbeast_amd.train import train
+    out = train(parse_flags(_args(tmp_path, "fi", "--max_updates", "6", "--fault_inject_every",
+                                  "2", "--actor_restarts", "5", "--batch_timeout", "120"),
+                            interactive=False))
+    assert out["updates"] == 6 and out["engine_restarts"] >= 2
+    loss = _rows(tmp_path / "fiLosses.csv")
+    assert [int(r["update"]) for r in loss] == [1, 2, 3, 4, 5, 6]
+
+
+def test_gpu_engine_failure_surfaces_without_restarts(cuda, tmp_path):
+    from microbeast_amd.config import parse_flags
+    from microbeast_amd.runtime.gpu_actors import EngineFailure
+    from microbeast_amd.train import train
+    with pytest.raises(EngineFailure, match="injected env-worker fault"):
+        train(parse_flags(_args(tmp_path, "fx", "--max_updates", "6", "--fault_inject_every",
+                                "2", "--actor_restarts", "0", "--batch_timeout", "120"),
+                          interactive=False))

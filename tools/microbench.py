@@ -22,6 +22,8 @@ def main():
     p.add_argument("--learn_T", type=int, default=64)
     p.add_argument("--learn_B", type=str, default="512,1024")
     p.add_argument("--iters", type=int, default=50)
+    p.add_argument("--policy_eager", action="store_true",
+                   help="also run the policy step eagerly (no graph) so rocprof sees its kernels")
     p.add_argument("--variants", type=str, default="",
                    help="comma list of encoder toggles to A/B in the same process: "
                         "fusedpool, nofusedpool")
@@ -52,6 +54,10 @@ def main():
         dt = (time.perf_counter() - t0) / a.iters
         print(json.dumps({"what": "policy_step_graph", "E": E, "ms": round(dt * 1e3, 4),
                           "frames_per_s": round(E / dt, 1)}), flush=True)
+        if a.policy_eager:
+            for _ in range(a.iters):
+                rt._policy_step(rt.io, rt.infer_model, rt.rng)
+            torch.cuda.synchronize()
         del rt
     torch.manual_seed(0)
     learner = Learner(mk(), LearnerHParams(), dev)
