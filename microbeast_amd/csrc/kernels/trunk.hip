@@ -66,20 +66,23 @@ struct TG {
   static constexpr int NCH = C == 16 ? 5 : 9;
 };
 
-// zero the halo ring of a halo'd tile [nimg][(H+2)][(W+2)] of PIXB-byte pixels
-__device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W, int pixb) {
+// zero the halo ring of a halo'd tile [nimg][(H+2)][(W+2)] of PIXB-byte pixels (index math
+// by float reciprocals: exact for these tiny ranges, no runtime integer division)
+template <int PIXB>
+__device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W) {
   const int Hp = H + 2, Wp = W + 2;
   const int per = 2 * Wp + 2 * H;  // halo pixels per image
-  const int q16 = pixb / 16;
+  constexpr int q16 = PIXB / 16;
   const int tot = nimg * per * q16;
+  const float inv_per = 1.f / (float)per;
   for (int e = threadIdx.x; e < tot; e += kThreads) {
-    const int q = e % q16, r = e / q16;
-    const int im = r / per, k = r - im * per;
+    const int r = e / q16, q = e - r * q16;  // q16 is a compile-time constant
+    const int im = (int)(((float)r + 0.5f) * inv_per), k = r - im * per;
     int py, px;
     if (k < Wp) { py = 0; px = k; }
     else if (k < 2 * Wp) { py = Hp - 1; px = k - Wp; }
     else { const int j = k - 2 * Wp; py = 1 + (j >> 1); px = (j & 1) ? Wp - 1 : 0; }
-    *(uint4*)(t + ((im * Hp + py) * Wp + px) * pixb + q * 16) = make_uint4(0, 0, 0, 0);
+    *(uint4*)(t + ((im * Hp + py) * Wp + px) * PIXB + q * 16) = make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -117,7 +120,10 @@ __device__ __forceinline__ void wstore(char* lw, int n16, int nch, const uint4 r
 // 64-bit address math and s_waitcnt vmcnt(0) lgkmcnt(0) (it could be global memory).
 extern __shared__ __attribute__((aligned(16))) char trunk_smem[];
 
-enum ConvOut : int { OUT_TILE = 0, OUT_TILE_ADD = 1, OUT_STAGE = 2 };
+// OUT_TILE_RELU: the inner activation U of a residual block is consumed only by the block's
+// second conv, through a relu: store relu(U) once in the epilogue instead of re-applying it
+// to every one of U's 9 tap reads (bit-identical: relu commutes with the bf16 rounding)
+enum ConvOut : int { OUT_TILE = 0, OUT_TILE_ADD = 1, OUT_STAGE = 2, OUT_TILE_RELU = 3 };
 
 template <int CIN, int COUT, bool RELU, int MODE, bool WLDS>
 // noinline: works around an LLVM CGSCC-pass crash (ROCm 7.2) when fully force-inlined
@@ -188,7 +194,9 @@ __device__ __attribute__((noinline)) void conv_lds(int in, int H, int W, int nim
           const uint2 ad = *(const uint2*)p;
           v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
         }
-        *(uint2*)p = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        uint2 o = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if constexpr (MODE == OUT_TILE_RELU) o = make_uint2(relu2(o.x), relu2(o.y));
+        *(uint2*)p = o;
       }
     }
   };
@@ -238,11 +246,13 @@ __device__ __attribute__((noinline)) void conv_lds(int in, int H, int W, int nim
 template <int C>
 __device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg, char* out) {
   constexpr int PO = TG<C>::PIXB, C4 = C / 4;
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-  const int tot = nimg * Ho * Wo * C4;
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1, HWo = Ho * Wo;
+  const int tot = nimg * HWo * C4;
+  const float inv_hwo = 1.f / (float)HWo, inv_wo = 1.f / (float)Wo;
   for (int e = threadIdx.x; e < tot; e += kThreads) {
-    const int c4 = e % C4, p = e / C4;
-    const int im = p / (Ho * Wo), r = p - im * Ho * Wo, oy = r / Wo, ox = r - oy * Wo;
+    const int c4 = e % C4, p = e / C4;  // C4: compile-time power of two
+    const int im = (int)(((float)p + 0.5f) * inv_hwo), r = p - im * HWo;
+    const int oy = (int)(((float)r + 0.5f) * inv_wo), ox = r - oy * Wo;
     float mx[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
     for (int ky = 0; ky < 3; ++ky) {
       const int yy = 2 * oy - 1 + ky;
@@ -317,48 +327,50 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
       constexpr int PX = TG<16>::PIXB;
       const int tot = nimg * H0 * W0 * 2;  // 16-byte chunks
       const uint4* src = (const uint4*)(a.x + (size_t)img0 * H0 * W0 * 16);
+      const float ihw = 1.f / (float)(H0 * W0), iw = 1.f / (float)W0;
       for (int e = threadIdx.x; e < tot; e += kThreads) {
         const int q = e & 1, p = e >> 1;
-        const int im = p / (H0 * W0), r = p - im * H0 * W0, y = r / W0, x = r - y * W0;
+        const int im = (int)(((float)p + 0.5f) * ihw), r = p - im * H0 * W0;
+        const int y = (int)(((float)r + 0.5f) * iw), x = r - y * W0;
         *(uint4*)(R1 + ((im * (H0 + 2) + y + 1) * (W0 + 2) + x + 1) * PX + q * 16) = src[e];
       }
-      zero_halo(R1, nimg, H0, W0, PX);
-      zero_halo(R2, nimg, H0, W0, PX);
+      zero_halo<PX>(R1, nimg, H0, W0);
+      zero_halo<PX>(R2, nimg, H0, W0);
     }
     __syncthreads();
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(2 * rb, 16, 16, true, OUT_TILE, oR1, H0, W0, oWB[0], oR2);
+      TAIL_PHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, oR1, H0, W0, oWB[0], oR2);
       __syncthreads();
-      TAIL_PHASE(2 * rb + 1, 16, 16, true, OUT_TILE_ADD, oR2, H0, W0, oWB[1], oR1);
+      TAIL_PHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, oR2, H0, W0, oWB[1], oR1);
       __syncthreads();
     }
     // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1)
     TAIL_PHASE(4, 16, 32, false, OUT_STAGE, oR1, H0, W0, oWB[0], oR2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
-    zero_halo(R1, nimg, H1, W1, TG<32>::PIXB);
+    zero_halo<TG<32>::PIXB>(R1, nimg, H1, W1);
     __syncthreads();
-    zero_halo(R2, nimg, H1, W1, TG<32>::PIXB);  // U1 layout (staging consumed)
+    zero_halo<TG<32>::PIXB>(R2, nimg, H1, W1);  // U1 layout (staging consumed)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(5 + 2 * rb, 32, 32, true, OUT_TILE, oR1, H1, W1, oWB[1], oR2);
+      TAIL_PHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H1, W1, oWB[1], oR2);
       __syncthreads();
-      TAIL_PHASE(6 + 2 * rb, 32, 32, true, OUT_TILE_ADD, oR2, H1, W1, oWB[0], oR1);
+      TAIL_PHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H1, W1, oWB[0], oR1);
       __syncthreads();
     }
     // ---- stage 2
     TAIL_PHASE(9, 32, 32, false, OUT_STAGE, oR1, H1, W1, oWB[1], oR2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
-    zero_halo(R1, nimg, H2, W2, TG<32>::PIXB);
+    zero_halo<TG<32>::PIXB>(R1, nimg, H2, W2);
     __syncthreads();
-    zero_halo(R2, nimg, H2, W2, TG<32>::PIXB);
+    zero_halo<TG<32>::PIXB>(R2, nimg, H2, W2);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL_PHASE(10 + 2 * rb, 32, 32, true, OUT_TILE, oR1, H2, W2, oWB[0], oR2);
+      TAIL_PHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H2, W2, oWB[0], oR2);
       __syncthreads();
-      TAIL_PHASE(11 + 2 * rb, 32, 32, true, OUT_TILE_ADD, oR2, H2, W2, oWB[1], oR1);
+      TAIL_PHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H2, W2, oWB[1], oR1);
       __syncthreads();
     }
 #undef TAIL_PHASE
@@ -367,9 +379,11 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
       constexpr int PX = TG<32>::PIXB;
       const int tot = nimg * H2 * W2 * 4;
       uint4* dst = (uint4*)(a.y + (size_t)img0 * H2 * W2 * 32);
+      const float ihw = 1.f / (float)(H2 * W2), iw = 1.f / (float)W2;
       for (int e = threadIdx.x; e < tot; e += kThreads) {
         const int q = e & 3, p = e >> 2;
-        const int im = p / (H2 * W2), r = p - im * H2 * W2, y = r / W2, x = r - y * W2;
+        const int im = (int)(((float)p + 0.5f) * ihw), r = p - im * H2 * W2;
+        const int y = (int)(((float)r + 0.5f) * iw), x = r - y * W2;
         dst[e] = *(const uint4*)(R1 + ((im * (H2 + 2) + y + 1) * (W2 + 2) + x + 1) * PX + q * 16);
       }
     }
