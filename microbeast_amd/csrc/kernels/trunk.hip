@@ -125,16 +125,34 @@ extern __shared__ __attribute__((aligned(16))) char trunk_smem[];
 // to every one of U's 9 tap reads (bit-identical: relu commutes with the bf16 rounding)
 enum ConvOut : int { OUT_TILE = 0, OUT_TILE_ADD = 1, OUT_STAGE = 2, OUT_TILE_RELU = 3 };
 
-template <int CIN, int COUT, bool RELU, int MODE, bool WLDS>
-// noinline: works around an LLVM CGSCC-pass crash (ROCm 7.2) when fully force-inlined
-// in / out: byte offsets of halo'd tiles in trunk_smem (out of a MODE == OUT_STAGE call: a
-// dense bf16 staging [nimg][H][W][COUT]); weights: LDS offset (WLDS, rows of wstride bytes)
-// or the packed global buffer [COUT][NCH][32] (read as global memory, address space 1)
-__device__ __attribute__((noinline)) void conv_lds(int in, int H, int W, int nimg, int lw_off,
-                                                   const bf16* gw, int wstride,
-                                                   const float* __restrict__ bias, int out) {
+constexpr int kWFrag = 18;  // this lane's weight fragments of the largest layer (9 x 2)
+
+// A lane's packed-weight fragments of tail layer l, (chunk c, block nb) at c * NB + nb.
+// Issued one layer ahead by the kernel, so the L2 latency of a layer's weights hides
+// behind the previous layer's MFMAs (loading them at the top of each conv exposed it 14
+// times per image group).
+__device__ __forceinline__ void wfetch(const bf16* gw, int cin, int cout, uint4 w[kWFrag]) {
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
   typedef const __attribute__((address_space(1))) u32x4* GU4;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int nch = cin == 16 ? TG<16>::NCH : TG<32>::NCH, nb = cout / 16;
+#pragma unroll
+  for (int k = 0; k < kWFrag; ++k) {
+    const int c = k / 2, b = k % 2;  // fixed (c, nb) slot layout: c * 2 + nb
+    if (c < nch && b < nb) {
+      const u32x4 v = ((GU4)((const char*)gw + ((b * 16 + li) * nch * 64 + g * 16)))[c * 4];
+      w[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  }
+}
+
+template <int CIN, int COUT, bool RELU, int MODE, bool WLDS>
+// in / out: byte offsets of halo'd tiles in trunk_smem (out of a MODE == OUT_STAGE call: a
+// dense bf16 staging [nimg][H][W][COUT]); weights: LDS offset (WLDS, rows of wstride bytes)
+// or this lane's fragments prefetched into registers by wfetch (wreg)
+__device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_off,
+                                         const uint4* wreg, int wstride,
+                                         const float* __restrict__ bias, int out) {
   constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
   constexpr int PI = TG<CIN>::PIXB, PO = TG<COUT>::PIXB;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -148,12 +166,8 @@ __device__ __attribute__((noinline)) void conv_lds(int in, int H, int W, int nim
 #pragma unroll
       for (int c = 0; c < NCH; ++c) bw[c][nb].u = *(const uint4*)(trunk_smem + wr + c * 64);
     } else {
-      GU4 wr = (GU4)((const char*)gw + (nb * 16 + li) * wstride + g * 16);
 #pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const u32x4 v = wr[c * 4];
-        bw[c][nb].u = make_uint4(v.x, v.y, v.z, v.w);
-      }
+      for (int c = 0; c < NCH; ++c) bw[c][nb].u = wreg[c * 2 + nb];
     }
   }
   typedef const __attribute__((address_space(1))) f32x4* GF4;
@@ -301,6 +315,8 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   const int TNI = a.tni;
   const int ngroups = (a.N + TNI - 1) / TNI;
   uint4 wr[kWRegs];
+  uint4 wnext[kWFrag];  // register prefetch of the next layer's weights (L2 variant)
+  if (!LDSW) wfetch(a.w[0], tail_cin(0), tail_cout(0), wnext);
   if (LDSW) {  // layer 0's weights for the first iteration
     wload(a.w[0], tail_n16(0), wr);
     wstore(WB[0], tail_n16(0), TG<16>::NCH, wr);
@@ -316,7 +332,13 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
                                          a.b[l], OUT);                                      \
       wstore(WB[ln & 1], tail_n16(ln), ln < 5 ? TG<16>::NCH : TG<32>::NCH, wr);             \
     } else {                                                                                \
-      conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, a.w[l], TG<CI>::NCH * 64,    \
+      uint4 wc[kWFrag];                                                                     \
+      _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];                  \
+      {                                                                                     \
+        const int ln = ((l) + 1) % 14;                                                      \
+        wfetch(a.w[ln], tail_cin(ln), tail_cout(ln), wnext);                                \
+      }                                                                                     \
+      conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, wc, TG<CI>::NCH * 64,        \
                                           a.b[l], OUT);                                     \
     }                                                                                       \
   } while (0)
