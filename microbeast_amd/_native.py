@@ -94,7 +94,13 @@ _SIGS = {
     "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_trunk_tail": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
+    "mbk_res_bwd16_parts": [c_int, c_int, c_int, c_int],
+    "mbk_res_bwd16_partial_floats": [c_int],
+    "mbk_res_bwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                      c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                      c_void_p],
 }
+_RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64}
 
 
 def _ensure_built() -> None:
@@ -119,7 +125,7 @@ def kernels():
             for name, args in _SIGS.items():
                 fn = getattr(lib, name)  # a missing symbol is a build error: fail loudly
                 fn.argtypes = args
-                fn.restype = c_int
+                fn.restype = _RESTYPE.get(name, c_int)
             _kern = _Checked(lib)
     return _kern
 

@@ -1,0 +1,393 @@
+// Fused residual-block backward for 16-channel blocks (IMPALA stage 0: 8x8 maps at 16x16).
+//
+// Reference block (model.py:56-73): y = x + conv1(relu(conv0(relu(x)))), u = conv0(relu x).
+// Given g = dL/dy the per-layer path (ops/encoder.py) ran four launches per block, each
+// round-tripping a full activation tensor through HBM:
+//   wgrad1(relu u, g) | du = conv1^T(g) * [u > 0] | wgrad0(relu x, du) | dx = conv0^T(du) * [x > 0] + g
+// = 12 B of HBM traffic per activation byte (x, u, g read twice or more, du written and
+// re-read). Here one persistent kernel stages x, u, g of an image group into LDS once
+// (relu'd where the consumer wants relu), computes du into an LDS tile, then dx, and keeps
+// both weight gradients in MFMA accumulators for the whole launch: 4 B of HBM per
+// activation byte (read x, u, g; write dx). Profile 18 timed the four launches at ~2.3 ms
+// per block per 524K frames, near the HBM roofline for that traffic.
+//
+// MFMA mapping (v_mfma_f32_16x16x32_bf16), identical to conv.hip so dx / du are
+// bit-identical to the per-layer kernels:
+//   dgrad : A = packed transposed weights (VGPRs), B = 16 pixels x 32 K from the halo'd
+//           tile (K chunk = 2 taps x 16 channels), acc lane = 4 channels of one pixel;
+//   wgrad : A = dY (16 co x 32 pixels) and B = X taps (32 pixels x 16 ci), both read with
+//           ds_read_b64_tr_b16 from the same halo'd tiles; acc over the 9 taps.
+// Weight grads go out as per-workgroup fp32 partial rows [2][16*144 + 16] reduced by
+// conv.hip's deterministic wgrad_reduce (bias grads included).
+#include "../include/mbk_api.h"
+#include "common.h"
+
+#include <algorithm>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __hip_bfloat16 bf16;
+
+extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real,
+                                int cout, float* dw, float* db, int accumulate,
+                                hipStream_t stream);
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int C = 16;                  // channels (in = out)
+constexpr int PIXB = C * 2 + 16;       // halo'd tile pixel stride, bytes (bank spread)
+constexpr int NCH = 5;                 // dgrad K chunks of 32 (2 taps x 16 ch; chunk 4 padded)
+constexpr int KTOT = 9 * C;            // wgrad K per output channel
+constexpr int ROW = C * KTOT + C;      // one partial row (weights + bias)
+constexpr int kPF = 2;                 // staging prefetch slots per thread per tensor (imgs*HW <= 256)
+
+union Frag8 {
+  bf16x8 v;
+  uint4 u;
+  s16x4 h[2];
+};
+
+__device__ __forceinline__ uint32_t relu2(uint32_t w) {
+  s16x2 v = __builtin_bit_cast(s16x2, w);
+  v = __builtin_elementwise_max(v, s16x2{0, 0});
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ uint4 relu8(uint4 v) {
+  return make_uint4(relu2(v.x), relu2(v.y), relu2(v.z), relu2(v.w));
+}
+__device__ __forceinline__ float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(a)) |
+         ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(b)) << 16);
+}
+__device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
+}
+
+struct ResBwdArgs {
+  const bf16* x;     // block input (pre-relu)      [N][H][W][16]
+  const bf16* u;     // conv0 output (pre-relu)     [N][H][W][16]
+  const bf16* g;     // dL/dy                        [N][H][W][16]
+  bf16* dx;          // dL/dx                        [N][H][W][16]
+  const bf16* w1t;   // conv1 packed dgrad weights [16][5][32] (conv.hip packed_bwd layout)
+  const bf16* w0t;   // conv0 packed dgrad weights
+  float* partial;    // layer l's row of workgroup b at partial + l * lstride + b * ROW
+  int64_t lstride;   // floats per layer block: (nparts + reduce scratch rows) * ROW
+  int N, H, W, imgs;
+};
+
+__global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int tb = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
+  char* Tg = smem;            // g          (dgrad1 input, wgrad1 dY, + g of dx)
+  char* Tu = smem + tb;       // relu(u)    (wgrad1 X, du mask)
+  char* Tx = smem + 2 * tb;   // relu(x)    (wgrad0 X, dx mask)
+  char* Td = smem + 3 * tb;   // du         (dgrad0 input, wgrad0 dY)
+  char* zero = smem + 4 * tb; // 64 zero bytes for out-of-range wgrad pixels
+  float* red = (float*)smem;  // [C][KTOT] reduction after the loop
+
+  for (int e = tid; e < (4 * tb + 64) / 16; e += kThreads) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
+
+  // dgrad weights (A fragments): lane holds w[co = li][chunk c][8g .. 8g+7]
+  Frag8 w1[NCH], w0[NCH];
+  {
+    const uint4* p1 = (const uint4*)(a.w1t + (size_t)li * NCH * 32 + g * 8);
+    const uint4* p0 = (const uint4*)(a.w0t + (size_t)li * NCH * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      w1[c].u = p1[c * 4];
+      w0[c].u = p0[c * 4];
+    }
+  }
+  f32x4 acc1[9], acc0[9];  // wgrad accumulators, tap t: rows co = 4G + i, cols ci = li
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  float db1[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum g: this thread's 8-channel half (tid & 1)
+  float db0[4] = {0, 0, 0, 0};              // sum du: channels 4g .. 4g+3 (dgrad lane map)
+
+  const int per = a.imgs * HW * 2;  // uint4 staging elements per tensor per round
+  const int nrounds = (a.N + a.imgs - 1) / a.imgs;
+  uint4 px[kPF], pu[kPF], pg[kPF];
+  auto prefetch = [&](int rd) {
+    const int lim = min(per, (a.N - rd * a.imgs) * HW * 2);
+    const size_t base = (size_t)rd * per;
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      const bool ok = e < lim;
+      px[k] = ok ? ((const uint4*)a.x)[base + e] : make_uint4(0, 0, 0, 0);
+      pu[k] = ok ? ((const uint4*)a.u)[base + e] : make_uint4(0, 0, 0, 0);
+      pg[k] = ok ? ((const uint4*)a.g)[base + e] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lds_off = [&](int e) {  // staging element -> byte offset in a halo'd tile
+    const int q = e & 1, p = e >> 1;
+    const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB + q * 16;
+  };
+  auto put = [&](int e, uint4 vx, uint4 vu, uint4 vg) {
+    const int o = lds_off(e);
+    *(uint4*)(Tx + o) = relu8(vx);
+    *(uint4*)(Tu + o) = relu8(vu);
+    *(uint4*)(Tg + o) = vg;
+    const uint32_t w[4] = {vg.x, vg.y, vg.z, vg.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      db1[2 * j] += lo_f(w[j]);
+      db1[2 * j + 1] += hi_f(w[j]);
+    }
+  };
+
+  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x);
+  __syncthreads();  // zeroed tiles visible
+  for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
+    const int img0 = rd * a.imgs, nimg = min(a.imgs, a.N - img0);
+    const int lim = nimg * HW * 2;
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      if (e < lim) put(e, px[k], pu[k], pg[k]);
+    }
+    for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {
+      const size_t s = (size_t)rd * per + e;
+      put(e, ((const uint4*)a.x)[s], ((const uint4*)a.u)[s], ((const uint4*)a.g)[s]);
+    }
+    __syncthreads();
+    if (rd + (int)gridDim.x < nrounds) prefetch(rd + gridDim.x);
+
+    const int M = nimg * HW, nblk = (M + 15) >> 4, nk = (M + 31) >> 5;
+    // ---------------- phase A: du = conv1^T(g) * [u > 0] -> Td;  dW1 += relu(u) (x) g
+    for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+      const int m = pb * 16 + li;
+      const bool valid = m < M;
+      const int mm = valid ? m : 0;
+      const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+      const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+      const int base = (im * Hp + y) * Wp + x;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int tap = 2 * c + (g >> 1), ch0 = 8 * (g & 1);
+        const int tapc = tap < 9 ? tap : 8;  // chunk 4's pad half: zero packed weights
+        Frag8 av;
+        av.u = *(const uint4*)(Tg + (base + (tapc / 3) * Wp + (tapc % 3)) * PIXB + ch0 * 2);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[c].v, av.v, acc, 0, 0, 0);
+      }
+      if (!valid) continue;
+      const int o = (base + Wp + 1) * PIXB + 4 * g * 2;  // interior pixel, channels 4g..
+      const uint2 mu = *(const uint2*)(Tu + o);
+      const uint32_t mw[2] = {mu.x, mu.y};
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[i] : 0.f;
+      }
+      const uint2 du = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      *(uint2*)(Td + o) = du;
+      db0[0] += lo_f(du.x); db0[1] += hi_f(du.x); db0[2] += lo_f(du.y); db0[3] += hi_f(du.y);
+    }
+    for (int kb = wave; kb < nk; kb += kThreads / 64) {
+      const char* dptr[2];
+      int xpos[2];
+      bool ok[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = kb * 32 + 8 * g + 4 * h + (li >> 2);
+        ok[h] = p < M;
+        const int pp = ok[h] ? p : 0;
+        const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        xpos[h] = (im * Hp + y) * Wp + x;
+        dptr[h] = ok[h] ? Tg + (xpos[h] + Wp + 1) * PIXB : zero;
+      }
+      Frag8 af;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = (t / 3) * Wp + (t % 3);
+        Frag8 bf;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          bf.h[h] = tr_read((ok[h] ? Tu + (xpos[h] + off) * PIXB : zero) + (4 * (li & 3)) * 2);
+        acc1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bf.v, acc1[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // Td complete
+    // ---------------- phase B: dx = conv0^T(du) * [x > 0] + g -> HBM;  dW0 += relu(x) (x) du
+    const size_t gpix0 = (size_t)img0 * HW;
+    for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+      const int m = pb * 16 + li;
+      const bool valid = m < M;
+      const int mm = valid ? m : 0;
+      const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+      const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+      const int base = (im * Hp + y) * Wp + x;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        const int tap = 2 * c + (g >> 1), ch0 = 8 * (g & 1);
+        const int tapc = tap < 9 ? tap : 8;
+        Frag8 av;
+        av.u = *(const uint4*)(Td + (base + (tapc / 3) * Wp + (tapc % 3)) * PIXB + ch0 * 2);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[c].v, av.v, acc, 0, 0, 0);
+      }
+      if (!valid) continue;
+      const int o = (base + Wp + 1) * PIXB + 4 * g * 2;
+      const uint2 mx = *(const uint2*)(Tx + o), ad = *(const uint2*)(Tg + o);
+      const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[i] : 0.f;
+        v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
+      }
+      *(uint2*)(a.dx + (gpix0 + m) * C + 4 * g) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+    }
+    for (int kb = wave; kb < nk; kb += kThreads / 64) {
+      const char* dptr[2];
+      int xpos[2];
+      bool ok[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = kb * 32 + 8 * g + 4 * h + (li >> 2);
+        ok[h] = p < M;
+        const int pp = ok[h] ? p : 0;
+        const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        xpos[h] = (im * Hp + y) * Wp + x;
+        dptr[h] = ok[h] ? Td + (xpos[h] + Wp + 1) * PIXB : zero;
+      }
+      Frag8 af;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int off = (t / 3) * Wp + (t % 3);
+        Frag8 bf;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          bf.h[h] = tr_read((ok[h] ? Tx + (xpos[h] + off) * PIXB : zero) + (4 * (li & 3)) * 2);
+        acc0[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bf.v, acc0[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();  // tiles consumed before the next round is staged
+  }
+  // ---- per-workgroup partial rows: the 4 waves' accumulators summed through LDS in a fixed
+  // order (deterministic), then the bias sums
+  for (int which = 0; which < 2; ++which) {
+    float* out = a.partial + which * a.lstride + (size_t)blockIdx.x * ROW;
+    for (int w = 0; w < kThreads / 64; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int co = 4 * g + i, n = t * C + li;
+            float* p = red + co * KTOT + n;
+            const float v = which == 0 ? acc1[t][i] : acc0[t][i];
+            *p = (w == 0 ? 0.f : *p) + v;
+          }
+      }
+      __syncthreads();
+    }
+    for (int e = tid; e < C * KTOT / 4; e += kThreads) ((float4*)out)[e] = ((const float4*)red)[e];
+    __syncthreads();
+  }
+  float* out1 = a.partial + (size_t)blockIdx.x * ROW;
+  float* out0 = a.partial + a.lstride + (size_t)blockIdx.x * ROW;
+  // bias grads: db1 per thread covers channels 8 * (tid & 1) .. +8; db0 per lane channels 4g..
+  float* bred = red;  // [kThreads][12]
+#pragma unroll
+  for (int j = 0; j < 8; ++j) bred[tid * 12 + j] = db1[j];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bred[tid * 12 + 8 + j] = db0[j];
+  __syncthreads();
+  if (tid < C) {
+    const int half = tid / 8, j = tid % 8;
+    float s = 0.f;
+    for (int t = half; t < kThreads; t += 2) s += bred[t * 12 + j];
+    out1[C * KTOT + tid] = s;  // conv1 bias
+    const int gq = tid / 4, i = tid % 4;  // channel tid = 4 * gq + i lives in lanes g == gq
+    float s0 = 0.f;
+    for (int t = 0; t < kThreads; ++t)
+      if (((t & 63) >> 4) == gq) s0 += bred[t * 12 + 8 + i];
+    out0[C * KTOT + tid] = s0;  // conv0 bias
+  }
+}
+
+size_t res_smem(int imgs, int H, int W) {
+  const size_t tb = ((size_t)imgs * (H + 2) * (W + 2) * PIXB + 15) & ~(size_t)15;
+  return 4 * tb + 64;
+}
+
+int res_grid(int N, int H, int W, int imgs) {
+  const size_t sm = res_smem(imgs, H, W);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const void* kfn = (const void*)res_bwd16_kernel;
+  if (sm > 64 * 1024) (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
+    per = 1;
+  const int nrounds = (N + imgs - 1) / imgs;
+  return std::max(1, std::min(nrounds, cus * per));
+}
+
+}  // namespace
+
+// Number of partial row PAIRS mbk_res_bwd16 writes (= its grid); <= 0: unsupported shape.
+extern "C" int mbk_res_bwd16_parts(int N, int H, int W, int imgs) {
+  if (N <= 0 || imgs < 1 || H * W > 1024 || (int64_t)imgs * H * W >= (int64_t(1) << 22))
+    return -1;
+  if (res_smem(imgs, H, W) > 160 * 1024) return -1;
+  if ((int64_t)imgs * H * W * 2 > (int64_t)kPF * kThreads * 4) return -1;  // sane staging
+  return res_grid(N, H, W, imgs);
+}
+
+// floats mbk_res_bwd16 needs in ``partial``: per layer, nparts rows + the two-level
+// reduce's scratch rows (conv.hip wgrad_reduce stages its split sums after the rows)
+extern "C" int64_t mbk_res_bwd16_partial_floats(int nparts) {
+  return 2 * (int64_t)(nparts + (nparts + 31) / 32) * ROW;
+}
+
+// dx = conv0^T(conv1^T(g) * [u>0]) * [x>0] + g and both layers' weight / bias gradients.
+// partial: mbk_res_bwd16_partial_floats(nparts) floats. dw1/db1/dw0/db0: fp32 parameter
+// gradients [16][16][3][3] / [16] (overwritten).
+extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* dx,
+                             const void* w1t, const void* w0t, float* partial, int nparts,
+                             float* dw1, float* db1, float* dw0, float* db0, int N, int H, int W,
+                             int imgs, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (nparts < 1 || nparts != mbk_res_bwd16_parts(N, H, W, imgs)) return (int)hipErrorInvalidValue;
+  const size_t sm = res_smem(imgs, H, W);
+  const int64_t lstride = (int64_t)(nparts + (nparts + 31) / 32) * ROW;
+  ResBwdArgs a{(const bf16*)x, (const bf16*)u, (const bf16*)g, (bf16*)dx,
+               (const bf16*)w1t, (const bf16*)w0t, partial, lstride, N, H, W, imgs};
+  hipLaunchKernelGGL(res_bwd16_kernel, dim3(nparts), dim3(kThreads), sm, stream, a);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, 0, stream);
+  if (rc) return rc;
+  return mbk_wgrad_reduce(partial + lstride, nparts, C, C, C, dw0, db0, 0, stream);
+}

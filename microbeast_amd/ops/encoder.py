@@ -119,6 +119,10 @@ class HipEncoder:
         # pre-pool gradient's HBM round trip but measured 6 % slower per update on MI355X
         # (extra expand phase + a 1-wave/SIMD dgrad variant), so off by default
         self.fused_pool_bwd = False
+        # 16-channel residual blocks (stage 0): one fused backward launch per block
+        # (resblock.hip) instead of wgrad1 / dgrad1 / wgrad0 / dgrad0 (MBK_FUSED_RES=0: off)
+        self.fused_res_bwd = os.environ.get("MBK_FUSED_RES", "1") == "1"
+        self._partial_rb = None
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
@@ -240,6 +244,28 @@ class HipEncoder:
         N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
                                    dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
 
+    def _res_bwd16(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
+        """Fused backward of a 16-channel residual block y = x + conv1(relu(conv0(relu x))),
+        u = conv0(relu x): returns dx; writes both layers' weight / bias gradients."""
+        n = x.shape[0]
+        H, W = L0.H, L0.W
+        k = N.kernels()
+        imgs = max(1, min(8, (80 * 1024) // (4 * (H + 2) * (W + 2) * 48)))
+        nparts = k.mbk_res_bwd16_parts(n, H, W, imgs)
+        if nparts < 1:
+            raise RuntimeError(f"res_bwd16: unsupported shape {H}x{W}")
+        need = k.mbk_res_bwd16_partial_floats(nparts)
+        if self._partial_rb is None or self._partial_rb.numel() < need:
+            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        base = self.packed_bwd.data_ptr()
+        N.check(k.mbk_res_bwd16(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
+                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
+                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs,
+                                N.stream_ptr()), "res_bwd16")
+        return dx
+
     # ------------------------------------------------------------ passes
     def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool,
                 prepacked: bool = False):
@@ -291,16 +317,25 @@ class HipEncoder:
             li = 5 * s
             x, pidx, p, u0, y0, u1 = saved[6 * s:6 * s + 6]
             L = self.layers
-            # res block 1: y1 = y0 + conv4(relu(u1)), u1 = conv3(relu(y0))
-            self._wgrad(L[li + 4], u1, g, grads[2 * (li + 4)], grads[2 * (li + 4) + 1])
-            du1 = self._fwd(L[li + 4], g, None, mask_src=u1, dgrad=True)
-            self._wgrad(L[li + 3], y0, du1, grads[2 * (li + 3)], grads[2 * (li + 3) + 1])
-            dy0 = self._fwd(L[li + 3], du1, None, mask_src=y0, add=g, dgrad=True)
-            # res block 0
-            self._wgrad(L[li + 2], u0, dy0, grads[2 * (li + 2)], grads[2 * (li + 2) + 1])
-            du0 = self._fwd(L[li + 2], dy0, None, mask_src=u0, dgrad=True)
-            self._wgrad(L[li + 1], p, du0, grads[2 * (li + 1)], grads[2 * (li + 1) + 1])
-            dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
+            if self.fused_res_bwd and L[li + 1].cin == 16 and x.is_cuda:
+                # both residual blocks of a 16-channel stage: one launch each (resblock.hip)
+                dy0 = self._res_bwd16(L[li + 3], L[li + 4], y0, u1, g, grads[2 * (li + 4)],
+                                      grads[2 * (li + 4) + 1], grads[2 * (li + 3)],
+                                      grads[2 * (li + 3) + 1])
+                dp = self._res_bwd16(L[li + 1], L[li + 2], p, u0, dy0, grads[2 * (li + 2)],
+                                     grads[2 * (li + 2) + 1], grads[2 * (li + 1)],
+                                     grads[2 * (li + 1) + 1])
+            else:
+                # res block 1: y1 = y0 + conv4(relu(u1)), u1 = conv3(relu(y0))
+                self._wgrad(L[li + 4], u1, g, grads[2 * (li + 4)], grads[2 * (li + 4) + 1])
+                du1 = self._fwd(L[li + 4], g, None, mask_src=u1, dgrad=True)
+                self._wgrad(L[li + 3], y0, du1, grads[2 * (li + 3)], grads[2 * (li + 3) + 1])
+                dy0 = self._fwd(L[li + 3], du1, None, mask_src=y0, add=g, dgrad=True)
+                # res block 0
+                self._wgrad(L[li + 2], u0, dy0, grads[2 * (li + 2)], grads[2 * (li + 2) + 1])
+                du0 = self._fwd(L[li + 2], dy0, None, mask_src=u0, dgrad=True)
+                self._wgrad(L[li + 1], p, du0, grads[2 * (li + 1)], grads[2 * (li + 1) + 1])
+                dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
             if self.fused_pool_bwd:

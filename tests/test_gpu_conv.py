@@ -393,3 +393,35 @@ def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool):
                       padding=1)
         torch.testing.assert_close(outs[0][0].float().cpu().permute(0, 3, 1, 2), cr, rtol=2e-2,
                                    atol=2e-2)
+
+
+@pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 5)])
+def test_fused_res_bwd16_matches_per_layer_kernels(cuda, s, n):
+    """resblock.hip (one launch per 16-channel residual block backward) against the four
+    per-layer kernels: the input gradients flowing on are bit-identical (same MFMA chains,
+    same bf16 rounding), so the stage conv's grads are too; the residual-block weight grads
+    differ only by fp32 summation order."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(1)
+    chans = (16, 32, 32, 32) if s == 24 else (16, 32, 32)
+    m = Agent((s, s, 27), channels=chans).to(cuda)
+    obs = _random_obs_bits(n, s * s).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = encoder_params(m.network, len(chans))
+    grads = {}
+    for fused in (False, True):
+        enc.fused_res_bwd = fused
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(5)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[fused] = [p.grad.detach().clone() for p in params]
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        if i < 2:  # stage conv (weight, bias): downstream of bit-identical dp
+            assert torch.equal(a, b), i
+        else:
+            torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6)
