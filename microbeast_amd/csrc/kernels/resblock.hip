@@ -81,9 +81,13 @@ struct ResBwdArgs {
   int N, H, W, imgs;
 };
 
+// WC > 0: the map width as a compile-time constant (IMPALA stage-0 shapes), so every tap
+// offset is an immediate of the LDS instruction instead of per-lane multiply-adds
+// (PMC: the runtime-width form issued ~15 VALU per MFMA); WC == 0: any width
+template <int WC>
 __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -113,6 +117,14 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
   for (int t = 0; t < 9; ++t) {
     acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // per-lane byte offset of dgrad chunk c relative to the block's tap-(0,0) position: this
+  // lane's K group (g) reads tap 2c + (g >> 1), channels 8 (g & 1) .. +8
+  int coff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int tap = 2 * c + (g >> 1), tapc = tap < 9 ? tap : 8;  // chunk 4's pad half
+    coff[c] = ((tapc / 3) * Wp + (tapc % 3)) * PIXB + 16 * (g & 1);
   }
   float db1[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum g: this thread's 8-channel half (tid & 1)
   float db0[4] = {0, 0, 0, 0};              // sum du: channels 4g .. 4g+3 (dgrad lane map)
@@ -178,12 +190,11 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
       const int base = (im * Hp + y) * Wp + x;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* bp = Tg + base * PIXB;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        const int tap = 2 * c + (g >> 1), ch0 = 8 * (g & 1);
-        const int tapc = tap < 9 ? tap : 8;  // chunk 4's pad half: zero packed weights
         Frag8 av;
-        av.u = *(const uint4*)(Tg + (base + (tapc / 3) * Wp + (tapc % 3)) * PIXB + ch0 * 2);
+        av.u = *(const uint4*)(bp + coff[c]);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[c].v, av.v, acc, 0, 0, 0);
       }
       if (!valid) continue;
@@ -217,13 +228,16 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
       Frag8 af;
 #pragma unroll
       for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
+      // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (A)
+      // is zero, so they add exactly nothing and need no per-tap zero select
+      const char* xb0 = Tu + xpos[0] * PIXB + 8 * (li & 3);
+      const char* xb1 = Tu + xpos[1] * PIXB + 8 * (li & 3);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int off = (t / 3) * Wp + (t % 3);
+        const int off = ((t / 3) * Wp + (t % 3)) * PIXB;
         Frag8 bf;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          bf.h[h] = tr_read((ok[h] ? Tu + (xpos[h] + off) * PIXB : zero) + (4 * (li & 3)) * 2);
+        bf.h[0] = tr_read(xb0 + off);
+        bf.h[1] = tr_read(xb1 + off);
         acc1[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bf.v, acc1[t], 0, 0, 0);
       }
     }
@@ -238,12 +252,11 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
       const int base = (im * Hp + y) * Wp + x;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* bp = Td + base * PIXB;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
-        const int tap = 2 * c + (g >> 1), ch0 = 8 * (g & 1);
-        const int tapc = tap < 9 ? tap : 8;
         Frag8 av;
-        av.u = *(const uint4*)(Td + (base + (tapc / 3) * Wp + (tapc % 3)) * PIXB + ch0 * 2);
+        av.u = *(const uint4*)(bp + coff[c]);
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[c].v, av.v, acc, 0, 0, 0);
       }
       if (!valid) continue;
@@ -276,13 +289,16 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
       Frag8 af;
 #pragma unroll
       for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
+      // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (A)
+      // is zero, so they add exactly nothing and need no per-tap zero select
+      const char* xb0 = Tx + xpos[0] * PIXB + 8 * (li & 3);
+      const char* xb1 = Tx + xpos[1] * PIXB + 8 * (li & 3);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int off = (t / 3) * Wp + (t % 3);
+        const int off = ((t / 3) * Wp + (t % 3)) * PIXB;
         Frag8 bf;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          bf.h[h] = tr_read((ok[h] ? Tx + (xpos[h] + off) * PIXB : zero) + (4 * (li & 3)) * 2);
+        bf.h[0] = tr_read(xb0 + off);
+        bf.h[1] = tr_read(xb1 + off);
         acc0[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bf.v, acc0[t], 0, 0, 0);
       }
     }
@@ -345,7 +361,7 @@ int res_grid(int N, int H, int W, int imgs) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const void* kfn = (const void*)res_bwd16_kernel;
+  const void* kfn = (const void*)res_bwd16_kernel<0>;  // same resources for every width
   if (sm > 64 * 1024) (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
@@ -384,7 +400,11 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
   const int64_t lstride = (int64_t)(nparts + (nparts + 31) / 32) * ROW;
   ResBwdArgs a{(const bf16*)x, (const bf16*)u, (const bf16*)g, (bf16*)dx,
                (const bf16*)w1t, (const bf16*)w0t, partial, lstride, N, H, W, imgs};
-  hipLaunchKernelGGL(res_bwd16_kernel, dim3(nparts), dim3(kThreads), sm, stream, a);
+  auto kfn = W == 8 ? res_bwd16_kernel<8> : W == 5 ? res_bwd16_kernel<5>
+           : W == 12 ? res_bwd16_kernel<12> : W == 4 ? res_bwd16_kernel<4> : res_bwd16_kernel<0>;
+  if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  hipLaunchKernelGGL(kfn, dim3(nparts), dim3(kThreads), sm, stream, a);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, 0, stream);
