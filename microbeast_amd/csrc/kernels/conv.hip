@@ -281,6 +281,18 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       else *(uint4*)(tile + off + q * 16) = expand_bits8(bits >> (8 * q));
     }
   };
+  // per-lane byte offset of K chunk c from the block's tap-(0,0) pixel: this lane's K group
+  // (g) reads tap 2c + (g >> 1), channels 8 (g & 1).. (CIN 16) or tap c, channels 8g.. (CIN
+  // 32); computed once instead of per chunk and block (the kernels were VALU-bound, profile 15)
+  int coff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int tap, ch0;
+    if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
+    else { tap = c; ch0 = 8 * g; }
+    const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
+    coff[c] = ((tapc / 3) * Wp + (tapc % 3)) * PIXB + (F8 ? ch0 : ch0 * 2);
+  }
   if ((int)blockIdx.x < ngroups) prefetch(blockIdx.x);
   __syncthreads();  // halo zeros visible
 
@@ -350,23 +362,19 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       f32x4 acc[NB];
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* bp = tile + base_pos * PIXB;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         Frag8 av;
-        int tap, ch0;
-        if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
-        else { tap = c; ch0 = 8 * g; }
-        const int tapc = tap < 9 ? tap : 8;  // CIN=16 pads chunk 4 with a zero tap
-        const int pos = base_pos + (tapc / 3) * Wp + (tapc % 3);
         // no zeroing: the CIN-16 pad tap has zero packed weights and rows past M are not
         // stored, so the (finite) fragment read for them cannot change a stored output
         if constexpr (F8) {
-          long a8 = *(const long*)(tile + pos * PIXB + ch0);
+          long a8 = *(const long*)(bp + coff[c]);
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bw8[c][nb], a8, acc[nb], 0, 0, 0);
         } else {
-          av.u = *(const uint4*)(tile + pos * PIXB + ch0 * 2);
+          av.u = *(const uint4*)(bp + coff[c]);
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, av.v, acc[nb], 0, 0, 0);
@@ -788,17 +796,18 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
           af[mb].h[h] = tr_read(dptr[h] + (mb * 16 + 4 * (li & 3)) * 2);
+      // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (the A
+      // operand, dzero) is zero, so they add exactly nothing and need no per-tap zero select
+      const char* xb0 = xt + xpos[0] * XPB + 8 * (li & 3);
+      const char* xb1 = xt + xpos[1] * XPB + 8 * (li & 3);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int off = (t / 3) * Wp + (t % 3);
+        const int off = ((t / 3) * Wp + (t % 3)) * XPB;
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           Frag8 bf;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const char* p = ok[h] ? xt + (xpos[h] + off) * XPB : xzero;
-            bf.h[h] = tr_read(p + (cb * 16 + 4 * (li & 3)) * 2);
-          }
+          bf.h[0] = tr_read(xb0 + off + cb * 32);
+          bf.h[1] = tr_read(xb1 + off + cb * 32);
 #pragma unroll
           for (int mb = 0; mb < MB; ++mb)
             acc[mb][t * CB + cb] =
