@@ -381,6 +381,163 @@ extern "C" int mbk_res_bwd16_parts(int N, int H, int W, int imgs) {
   return res_grid(N, H, W, imgs);
 }
 
+namespace {
+
+// ------------------------------------------------------------------ fused forward
+// Both residual blocks of a 16-channel stage in one launch, saving what the backward needs:
+//   u0 = conv0(relu p); y0 = p + conv1(relu u0); u1 = conv2(relu y0); y1 = y0 + conv3(relu u1)
+// Writes u0, y0, u1, y1 (bf16) once each and reads p once (5 activation passes instead of the
+// per-layer path's 10: every layer re-read its input and the residual from HBM). The stream
+// tile Tx holds p, then y0 (updated in place: a conv's residual add touches only its own
+// output pixel), the inner tile Tu holds relu(u) for the second conv of each block.
+// Accumulation order = conv.hip's conv_fwd chains, so outputs are bit-identical.
+struct ResFwdArgs {
+  const bf16* p;                 // [N][H][W][16] block-pair input
+  bf16 *u0, *y0, *u1, *y1;       // outputs (saved activations + stage output)
+  const bf16* w[4];              // packed fwd weights [16][5][32] of conv0..conv3
+  const float* b[4];             // fp32 biases
+  int N, H, W, imgs;
+};
+
+template <int WC>
+__global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int tb = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
+  char* Tx = smem;       // residual stream p -> y0 (raw)
+  char* Tu = smem + tb;  // relu(u) of the current block
+  for (int e = tid; e < 2 * tb / 16; e += kThreads) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
+  Frag8 w[4][NCH];
+  float bv[4][4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const uint4* wp = (const uint4*)(a.w[l] + (size_t)li * NCH * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) w[l][c].u = wp[c * 4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[l][i] = a.b[l][4 * g + i];
+  }
+  int coff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int tap = 2 * c + (g >> 1), tapc = tap < 9 ? tap : 8;
+    coff[c] = ((tapc / 3) * Wp + (tapc % 3)) * PIXB + 16 * (g & 1);
+  }
+  const int per = a.imgs * HW * 2;
+  const int nrounds = (a.N + a.imgs - 1) / a.imgs;
+  uint4 pp[kPF];
+  auto prefetch = [&](int rd) {
+    const int lim = min(per, (a.N - rd * a.imgs) * HW * 2);
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      pp[k] = e < lim ? ((const uint4*)a.p)[(size_t)rd * per + e] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lds_off = [&](int e) {
+    const int q = e & 1, p = e >> 1;
+    const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB + q * 16;
+  };
+  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x);
+  __syncthreads();
+  for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
+    const int img0 = rd * a.imgs, nimg = min(a.imgs, a.N - img0);
+    const int lim = nimg * HW * 2;
+#pragma unroll
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      if (e < lim) *(uint4*)(Tx + lds_off(e)) = pp[k];
+    }
+    for (int e = tid + kPF * kThreads; e < lim; e += kThreads)
+      *(uint4*)(Tx + lds_off(e)) = ((const uint4*)a.p)[(size_t)rd * per + e];
+    __syncthreads();
+    if (rd + (int)gridDim.x < nrounds) prefetch(rd + gridDim.x);
+    const int M = nimg * HW, nblk = (M + 15) >> 4;
+    const size_t gpix0 = (size_t)img0 * HW;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const bool inner = (l & 1) == 0;  // conv0 / conv2: relu(Tx) -> u;  conv1 / conv3: + Tx
+      const char* src = inner ? Tx : Tu;
+      bf16* gout = l == 0 ? a.u0 : l == 1 ? a.y0 : l == 2 ? a.u1 : a.y1;
+      for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+        const int m = pb * 16 + li;
+        const bool valid = m < M;
+        const int mm = valid ? m : 0;
+        const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        const int base = (im * Hp + y) * Wp + x;
+        const char* bp = src + base * PIXB;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          Frag8 av;
+          av.u = *(const uint4*)(bp + coff[c]);
+          if (inner) av.u = relu8(av.u);  // Tu already holds relu(u)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[l][c].v, av.v, acc, 0, 0, 0);
+        }
+        if (!valid) continue;
+        const int o = (base + Wp + 1) * PIXB + 4 * g * 2;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[i] + bv[l][i];
+        if (!inner) {
+          const uint2 ad = *(const uint2*)(Tx + o);
+          v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
+        }
+        const uint2 out = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        *(uint2*)(gout + (gpix0 + m) * C + 4 * g) = out;
+        if (inner) *(uint2*)(Tu + o) = make_uint2(relu2(out.x), relu2(out.y));
+        else if (l == 1) *(uint2*)(Tx + o) = out;  // y0 replaces p as the residual stream
+      }
+      __syncthreads();
+    }
+  }
+}
+
+size_t resf_smem(int imgs, int H, int W) {
+  return 2 * (((size_t)imgs * (H + 2) * (W + 2) * PIXB + 15) & ~(size_t)15);
+}
+
+}  // namespace
+
+// Forward of both residual blocks of a 16-channel stage (see res_fwd16_kernel).
+extern "C" int mbk_res_fwd16(const void* p, void* u0, void* y0, void* u1, void* y1,
+                             const void* const* w, const float* const* b, int N, int H, int W,
+                             int imgs, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (imgs < 1 || H * W > 1024 || (int64_t)imgs * H * W >= (int64_t(1) << 22))
+    return (int)hipErrorInvalidValue;
+  const size_t sm = resf_smem(imgs, H, W);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  ResFwdArgs a{(const bf16*)p, (bf16*)u0, (bf16*)y0, (bf16*)u1, (bf16*)y1,
+               {(const bf16*)w[0], (const bf16*)w[1], (const bf16*)w[2], (const bf16*)w[3]},
+               {b[0], b[1], b[2], b[3]}, N, H, W, imgs};
+  auto kfn = W == 8 ? res_fwd16_kernel<8> : W == 5 ? res_fwd16_kernel<5>
+           : W == 12 ? res_fwd16_kernel<12> : W == 4 ? res_fwd16_kernel<4> : res_fwd16_kernel<0>;
+  if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
+          hipSuccess || per < 1)
+    per = 1;
+  const int nrounds = (N + imgs - 1) / imgs;
+  hipLaunchKernelGGL(kfn, dim3(std::max(1, std::min(nrounds, cus * per))), dim3(kThreads), sm,
+                     stream, a);
+  return (int)hipGetLastError();
+}
+
 // floats mbk_res_bwd16 needs in ``partial``: per layer, nparts rows + the two-level
 // reduce's scratch rows (conv.hip wgrad_reduce stages its split sums after the rows)
 extern "C" int64_t mbk_res_bwd16_partial_floats(int nparts) {

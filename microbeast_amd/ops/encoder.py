@@ -122,6 +122,7 @@ class HipEncoder:
         # 16-channel residual blocks (stage 0): one fused backward launch per block
         # (resblock.hip) instead of wgrad1 / dgrad1 / wgrad0 / dgrad0 (MBK_FUSED_RES=0: off)
         self.fused_res_bwd = os.environ.get("MBK_FUSED_RES", "1") == "1"
+        self.fused_res_fwd = os.environ.get("MBK_FUSED_RES_FWD", "1") == "1"
         self._partial_rb = None
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
@@ -244,6 +245,20 @@ class HipEncoder:
         N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
                                    dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
 
+    def _res_fwd16(self, li: int, p: torch.Tensor, bs: list[torch.Tensor]):
+        """Both residual blocks of a 16-channel stage in one launch (resblock.hip): returns
+        (u0, y0, u1, y1), bit-identical to four conv_fwd launches."""
+        n, H, W, C = p.shape
+        outs = [torch.empty_like(p) for _ in range(4)]
+        base = self.packed_fwd.data_ptr()
+        wp = (ctypes.c_void_p * 4)(*[base + 2 * self.layers[li + 1 + j].w_off for j in range(4)])
+        bp = (ctypes.c_void_p * 4)(*[bs[li + 1 + j].data_ptr() for j in range(4)])
+        N.check(N.kernels().mbk_res_fwd16(p.data_ptr(), *[o.data_ptr() for o in outs],
+                                          ctypes.cast(wp, ctypes.c_void_p),
+                                          ctypes.cast(bp, ctypes.c_void_p), n, H, W, 4,
+                                          N.stream_ptr()), "res_fwd16")
+        return outs
+
     def _res_bwd16(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
         """Fused backward of a 16-channel residual block y = x + conv1(relu(conv0(relu x))),
         u = conv0(relu x): returns dx; writes both layers' weight / bias gradients."""
@@ -299,10 +314,13 @@ class HipEncoder:
             pidx = (torch.empty(n, Ho, Wo, L.cout, dtype=torch.uint8, device=x.device)
                     if save else None)
             p = self._fwd(L, x, bs[li].detach(), pool_idx=pidx)
-            u0 = self._fwd(self.layers[li + 1], p, bs[li + 1].detach())
-            y0 = self._fwd(self.layers[li + 2], u0, bs[li + 2].detach(), add=p)
-            u1 = self._fwd(self.layers[li + 3], y0, bs[li + 3].detach())
-            y1 = self._fwd(self.layers[li + 4], u1, bs[li + 4].detach(), add=y0)
+            if self.fused_res_fwd and L.cout == 16 and p.is_cuda:
+                u0, y0, u1, y1 = self._res_fwd16(li, p, [b.detach() for b in bs])
+            else:
+                u0 = self._fwd(self.layers[li + 1], p, bs[li + 1].detach())
+                y0 = self._fwd(self.layers[li + 2], u0, bs[li + 2].detach(), add=p)
+                u1 = self._fwd(self.layers[li + 3], y0, bs[li + 3].detach())
+                y1 = self._fwd(self.layers[li + 4], u1, bs[li + 4].detach(), add=y0)
             if save:
                 saved += [x, pidx, p, u0, y0, u1]
             x = y1

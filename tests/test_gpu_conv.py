@@ -425,3 +425,25 @@ def test_fused_res_bwd16_matches_per_layer_kernels(cuda, s, n):
             assert torch.equal(a, b), i
         else:
             torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("s,n", [(16, 37), (10, 21)])
+def test_fused_res_fwd16_bit_identical(cuda, s, n):
+    """resblock.hip res_fwd16 (both 16-channel residual blocks in one launch) writes the
+    same u0 / y0 / u1 / y1 bits as four conv_fwd launches."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encoder_params
+    torch.manual_seed(2)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(n, s * s).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = [p.detach() for p in encoder_params(m.network, 3)]
+    outs = {}
+    for fused in (False, True):
+        enc.fused_res_fwd = fused
+        y, saved = enc.forward(obs, params, save=True)
+        torch.cuda.synchronize()
+        outs[fused] = [t.clone() for t in saved[:6]] + [y.clone()]
+    for a, b in zip(outs[False], outs[True]):
+        assert torch.equal(a, b)
