@@ -30,6 +30,8 @@ c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int6
 
 _SIGS = {
     "mbk_multi_copy": [c_void_p, c_int, c_void_p],
+    "mbk_row_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p],
+    "mbk_memset": [c_void_p, c_int, c_int64, c_void_p],
     "mbk_masked_cell_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64,
                             c_void_p, c_void_p, c_void_p],
     "mbk_masked_cell_bwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
@@ -101,6 +103,19 @@ _SIGS = {
     "mbk_res_bwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                       c_void_p],
+    # gridnet.hip
+    "mbk_bits_grid": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_pool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                     c_void_p],
+    "mbk_pool_bwd_grid": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
+                          c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_grid_gather": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "mbk_colsum_parts": [c_int64],
+    "mbk_colsum": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                   c_void_p],
+    "mbk_map_gather": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mbk_value_bwd_parts": [c_int],
+    "mbk_value_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
 }
 _RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64}
 

@@ -3,6 +3,8 @@
 #include "../include/mbk_api.h"
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 struct SegPack {
@@ -37,7 +39,43 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(SegPack p) {
   }
 }
 
+// Row gather: dst row i = src row idx[i] (rows of row_bytes, 16- or 4-byte granules).
+// blockIdx.y = output row. The dynamic-batching policy server's request gather.
+template <typename V>
+__global__ __launch_bounds__(256) void row_gather_kernel(const V* __restrict__ src,
+                                                         V* __restrict__ dst,
+                                                         const int64_t* __restrict__ idx,
+                                                         int nv) {
+  const int64_t r = idx[blockIdx.y];
+  const V* s = src + r * nv;
+  V* d = dst + (int64_t)blockIdx.y * nv;
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < nv; j += gridDim.x * 256) d[j] = s[j];
+}
+
 }  // namespace
+
+// dst[i] = src[idx[i]] for i < k (idx: device int64), rows of row_bytes (% 4 == 0)
+extern "C" int mbk_row_gather(const void* src, void* dst, const int64_t* idx, int k,
+                              int64_t row_bytes, hipStream_t stream) {
+  if (k <= 0) return 0;
+  if (row_bytes <= 0 || row_bytes % 4 || row_bytes / 4 > (1LL << 30)) return (int)hipErrorInvalidValue;
+  const bool v16 = row_bytes % 16 == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0;
+  const int nv = (int)(row_bytes / (v16 ? 16 : 4));
+  unsigned bx = (unsigned)std::min<int64_t>(64, (nv + 255) / 256);
+  if (v16)
+    hipLaunchKernelGGL(row_gather_kernel<uint4>, dim3(bx, k), dim3(256), 0, stream,
+                       (const uint4*)src, (uint4*)dst, idx, nv);
+  else
+    hipLaunchKernelGGL(row_gather_kernel<uint32_t>, dim3(bx, k), dim3(256), 0, stream,
+                       (const uint32_t*)src, (uint32_t*)dst, idx, nv);
+  return (int)hipGetLastError();
+}
+
+// Byte fill (hipMemsetAsync), for zero-initialised buffers without an ATen fill kernel
+extern "C" int mbk_memset(void* dst, int value, int64_t bytes, hipStream_t stream) {
+  if (bytes <= 0) return 0;
+  return (int)hipMemsetAsync(dst, value, (size_t)bytes, stream);
+}
 
 extern "C" int mbk_multi_copy(const MbkCopySeg* segs, int n, hipStream_t stream) {
   if (n <= 0) return 0;

@@ -66,7 +66,11 @@ struct ATaps {
   // border rows are dropped, interior rows go to output row
   // b * ob + ((y - 1) * sy + oy0) * ow + (x - 1) * sx + ox0 -- a plain or padded NHWC
   // output, or one stride-2 phase of a transposed conv's output, with no crop / scatter copy.
-  int remap, Hp, Wp, ob, ow, sy, sx, oy0, ox0;
+  // Output pixels (Y, X) = ((y - 1) * sy + oy0, (x - 1) * sx + ox0) outside [0, lim_h) x
+  // [0, lim_w) are not written (crop). zero_border: border rows are not dropped but write
+  // zeros at their (Y, X), which fills the zero border of a padded output grid exactly
+  // (for a stride-2 transposed conv, across its 4 phases).
+  int remap, Hp, Wp, ob, ow, sy, sx, oy0, ox0, lim_h, lim_w, zero_border;
 };
 
 template <int ROWS>
@@ -167,12 +171,15 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
       const int row = m0 + wm * 64 + i * 16 + 4 * g + r;
       if (row >= M) continue;
       size_t orow = row;
+      bool zero = false;
       if (TAPS && taps.remap) {
         const int x = row % taps.Wp, t = row / taps.Wp;
         const int y = t % taps.Hp, b = t / taps.Hp;
-        if (y == 0 || y == taps.Hp - 1 || x == 0 || x == taps.Wp - 1) continue;
-        orow = (size_t)b * taps.ob + (size_t)((y - 1) * taps.sy + taps.oy0) * taps.ow +
-               (x - 1) * taps.sx + taps.ox0;
+        zero = y == 0 || y == taps.Hp - 1 || x == 0 || x == taps.Wp - 1;
+        if (zero && !taps.zero_border) continue;
+        const int Y = (y - 1) * taps.sy + taps.oy0, X = (x - 1) * taps.sx + taps.ox0;
+        if (Y < 0 || Y >= taps.lim_h || X < 0 || X >= taps.lim_w) continue;
+        orow = (size_t)b * taps.ob + (size_t)Y * taps.ow + X;
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
@@ -180,6 +187,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
         if (col >= N) continue;
         float v = acc[i][j][r] + (bias ? bias[col] : 0.f);
         if (relu) v = fmaxf(v, 0.f);
+        if (zero) v = 0.f;
         const size_t o = orow * ldc + col;
         if (OUT_BF16) {
           ((bf16*)C)[o] = __float2bfloat16(v);
@@ -237,7 +245,8 @@ extern "C" int mbk_gemm_nt(const void* A, const void* B, void* C, const float* b
 // Shifted-row ("implicit im2col") GEMM: C[M][N] = sum_t A_t[m + shift_t][:] . B[:, t*tk ...]^T
 // A_t: bases[t] [M][lda] bf16 (rows outside [0, M) read as zero), tk % 32 == 0,
 // B: [N][ntap*tk] bf16 (tap-major K).
-// remap: null, or 8 ints {Hp, Wp, ob, ow, sy, sx, oy0, ox0} (see ATaps)
+// remap: null, or 11 ints {Hp, Wp, ob, ow, sy, sx, oy0, ox0, lim_h, lim_w, zero_border}
+// (see ATaps)
 extern "C" int mbk_gemm_nt_taps(const void* const* bases, const int* shifts, int ntap, int tk,
                                 const void* B, void* C, const float* bias, int M, int N, int lda,
                                 int ldb, int ldc, int relu, int out_bf16, int accumulate,
@@ -255,6 +264,7 @@ extern "C" int mbk_gemm_nt_taps(const void* const* bases, const int* shifts, int
     t.remap = 1;
     t.Hp = remap[0], t.Wp = remap[1], t.ob = remap[2], t.ow = remap[3];
     t.sy = remap[4], t.sx = remap[5], t.oy0 = remap[6], t.ox0 = remap[7];
+    t.lim_h = remap[8], t.lim_w = remap[9], t.zero_border = remap[10];
   }
   launch_any<true>(nullptr, B, C, bias, M, N, ntap * tk, lda, ldb, ldc, relu, out_bf16,
                    accumulate, t, stream);

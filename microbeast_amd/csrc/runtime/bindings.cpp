@@ -202,6 +202,14 @@ PYBIND11_MODULE(_mbrt, m) {
   m.def("host_unregister", [](uintptr_t addr) -> int {
     return (int)hipHostUnregister(P<void>(addr));
   });
+  // Strided DMA (hipMemcpy2DAsync): `height` rows of `width` bytes, e.g. one actor slot's
+  // [T+1][row] rollout into column j of a time-major [T+1][B][row] learner batch, so the
+  // batch lands in its final layout with no device-side transpose copy.
+  m.def("memcpy2d_async", [](uintptr_t dst, size_t dpitch, uintptr_t src, size_t spitch,
+                             size_t width, size_t height, uintptr_t stream) -> int {
+    return (int)hipMemcpy2DAsync(P<void>(dst), dpitch, P<const void>(src), spitch, width, height,
+                                 hipMemcpyDefault, (hipStream_t)stream);
+  });
 
   // A stream restricted to a subset of CUs (MI355X: 256 CUs in 8 XCDs). Used for the
   // learner so that every `reserve_every`-th CU stays free for the latency-critical

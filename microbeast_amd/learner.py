@@ -20,6 +20,7 @@ from dataclasses import dataclass
 
 import torch
 
+from .ops.copy import full
 from .ops.optim import FlatAdam, FlatParams
 from .ops.vtrace import VTraceWorkspace, vtrace
 from .parallel.dist import DistInfo, GradAllReducer, broadcast_flat
@@ -88,8 +89,11 @@ class Learner:
             torch.cuda.synchronize()
         t1 = time.perf_counter()
         torch.autograd.backward(
-            [logp, value, ent],
-            [vt.g_logp.reshape(-1), vt.g_value.reshape(-1), torch.full_like(ent, vt.g_ent)])
+            [logp, value, ent], [vt.g_logp.reshape(-1), vt.g_value.reshape(-1),
+                                 self._const_grad(ent, vt.g_ent)])
+        if self.flat.adopt_grads() and self.info.enabled:
+            raise RuntimeError("a direct-gradient parameter's gradient was not written into "
+                               "its flat slot; its all-reduce bucket went out stale")
         self.phases.mark("bwd")
         self.reducer.finish()
         self.phases.mark("allreduce")
@@ -104,6 +108,14 @@ class Learner:
         self.n_updates += 1
         self.timing = {"fwd_s": t1 - t0, "bwd_allreduce_s": t2 - t1, "optim_s": t3 - t2}
         return vt.losses
+
+    def _const_grad(self, like: torch.Tensor, value: float) -> torch.Tensor:
+        """constant seed gradient (entropy term), filled once per shape / value"""
+        c = getattr(self, "_cg", None)
+        if c is None or c[0] != (like.shape, like.device, value):
+            c = ((like.shape, like.device, value), full(like.shape, value, like.dtype, like.device))
+            self._cg = c
+        return c[1]
 
     def state_dict(self):
         return {"model": self.model.state_dict(), "optim": self.opt.state_dict(),

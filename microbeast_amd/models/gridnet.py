@@ -17,8 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import cell_head
-from ..ops.gridconv import conv3x3, conv_transpose3x3s2, maxpool3x3s2
-from ..ops.linear import linear
+from ..ops.gridconv import GridPlan, gridnet_forward
 from ..ops.obs import bits_to_planes
 from .agent import layer_init
 
@@ -46,6 +45,10 @@ class GridNetAgent(nn.Module):
                                     layer_init(nn.Linear(128, 1), std=1))
         self.compute_dtype = compute_dtype
         self.nvec = list(cell_head.NVEC) * (h * w)
+        self.emulate = False      # run the grid path's torch emulation off-GPU (tests)
+        self._grid_plan = None
+        for p in self.parameters():  # grid-path kernels write gradients into flat slots
+            p._mbk_direct_grad = True
 
     def _planes(self, obs):
         if obs.dtype == torch.int32:
@@ -63,31 +66,24 @@ class GridNetAgent(nn.Module):
                               cache_enabled=False)
 
     def _use_hip(self, obs) -> bool:
-        return self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32
+        return self.hip_kernels and obs.dtype == torch.int32 and (obs.is_cuda or self.emulate)
 
-    def _policy_value_hip(self, obs):
-        """Every conv / transposed conv on the MFMA GEMM (ops/gridconv.py), NHWC bf16.
-        relu(maxpool(conv)) is computed as maxpool(relu-fused conv): identical values."""
+    def _plan(self, device) -> GridPlan:
+        if self._grid_plan is None or self._grid_plan.device != device:
+            convs = [self.encoder[i] for i in (0, 3, 6, 9)]
+            convts = [self.actor[i] for i in (0, 2, 4, 6)]
+            self._grid_plan = GridPlan(convs, convts, self.critic[1], self.critic[3],
+                                       (self.ph // 16, self.pw // 16, 256), device)
+        return self._grid_plan
+
+    def _policy_value_hip(self, obs, n_logits=None):
+        """The whole network on padded NHWC grids (ops/gridconv.py): MFMA GEMMs + the
+        gridnet.hip data-movement kernels, no ATen kernel. relu(maxpool(conv)) is computed as
+        maxpool(relu-fused conv): identical values. Logits are bf16 and cell-major, cropped
+        to the map by the last GEMM's epilogue, and go to the masked-cell kernels as they are."""
         n = obs.numel() // (self.h * self.w)
-        bits = obs.reshape(n, self.h, self.w, 1)
-        sh = torch.arange(32, device=obs.device, dtype=torch.int32)
-        x = ((bits >> sh) & 1).to(torch.bfloat16)  # planes 27..31 are zero: Cin 27 -> 32
-        if (self.ph, self.pw) != (self.h, self.w):
-            x = F.pad(x, (0, 0, 0, self.pw - self.w, 0, self.ph - self.h))
-        for i in (0, 3, 6, 9):
-            conv = self.encoder[i]
-            x = maxpool3x3s2(conv3x3(x, conv.weight, conv.bias, relu=True))
-        z = x  # NHWC [n, ph/16, pw/16, 256]
-        y = z
-        for j, i in enumerate((0, 2, 4, 6)):
-            ct = self.actor[i]
-            last = j == 3
-            y = conv_transpose3x3s2(y, ct.weight, ct.bias, relu=not last, nchw_out=last)
-        logits = y[:, :, :self.h, :self.w].permute(0, 2, 3, 1).reshape(n, -1).float()
-        zf = z.permute(0, 3, 1, 2).reshape(n, -1)  # the reference's NCHW flatten order
-        hdn = F.relu(linear(zf, self.critic[1]))
-        v = linear(hdn, self.critic[3])
-        return logits, v.float().view(-1)
+        return gridnet_forward(self._plan(obs.device), obs.reshape(n, self.h * self.w),
+                               self.h, self.w, self.ph, self.pw, n_logits)
 
     def policy_value(self, obs):
         if self._use_hip(obs):
@@ -110,8 +106,11 @@ class GridNetAgent(nn.Module):
         return action, logp, value
 
     def evaluate(self, obs, mask_bits, action, n_score: int | None = None):
-        logits, value = self.policy_value(obs)
-        if n_score is not None:
-            logits = logits[:n_score]
+        if self._use_hip(obs):  # logits of the scored rows only (no slice-backward copy)
+            logits, value = self._policy_value_hip(obs, n_score)
+        else:
+            logits, value = self.policy_value(obs)
+            if n_score is not None:
+                logits = logits[:n_score]
         logp, ent = cell_head.score(logits, mask_bits, action)
         return logp, ent, value

@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native as N
+from .copy import zero_, zeros
 
 _ALIGN = 64  # elements: every parameter starts 256-B aligned
 
@@ -29,8 +30,8 @@ class FlatParams:
             offs.append(off)
             off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
         self.numel = off
-        self.data = torch.zeros(off, dtype=torch.float32, device=dev)
-        self.grad = torch.zeros(off, dtype=torch.float32, device=dev)
+        self.data = zeros(off, torch.float32, dev)
+        self.grad = zeros(off, torch.float32, dev)
         self.slices = []
         names = {id(p): n for n, p in module.named_parameters()}
         for p, o in zip(params, offs):
@@ -39,19 +40,63 @@ class FlatParams:
             view.copy_(p.data.to(dev))
             p.data = view
             p.grad = self.grad[o:o + n].view_as(p)
+            p._mbk_grad_at = (self.grad, o, n)
             self.slices.append((names.get(id(p), "?"), o, n, tuple(p.shape)))
         self.params = params
+        # "direct" parameters: their backward kernels write the gradient straight into the
+        # flat slot (``grad_out``) and autograd adopts that view as .grad -- no zero fill of
+        # the buffer, no AccumulateGrad add kernel per parameter
+        self.direct = [bool(getattr(p, "_mbk_direct_grad", False)) for p in params]
 
     def zero_grad(self):
-        self.grad.zero_()
+        if not any(self.direct):
+            zero_(self.grad)
+        else:
+            if not all(self.direct):
+                zero_(self.grad)
+            for p, d in zip(self.params, self.direct):
+                if d:
+                    p.grad = None
         # autograd may have replaced a .grad (e.g. after set_to_none elsewhere): re-bind views
-        for p, (_, o, n, _) in zip(self.params, self.slices):
-            if p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr():
+        for p, d, (_, o, n, _) in zip(self.params, self.direct, self.slices):
+            if not d and (p.grad is None or p.grad.data_ptr() != self.grad[o:].data_ptr()):
                 p.grad = self.grad[o:o + n].view_as(p)
+
+    def adopt_grads(self) -> int:
+        """After backward: bind every direct parameter's .grad to its flat slot (copying a
+        gradient autograd did not adopt in place, zeroing one that got none). Returns the
+        number of such fix-ups (0 on the fast path)."""
+        fixed = 0
+        for p, d, (_, o, n, _) in zip(self.params, self.direct, self.slices):
+            if not d:
+                continue
+            g = p.grad
+            if g is not None and g.data_ptr() == self.grad[o:].data_ptr():
+                continue
+            slot = self.grad[o:o + n].view_as(p)
+            if g is None:
+                zero_(slot)
+            else:
+                slot.copy_(g)
+            p.grad = slot
+            fixed += 1
+        return fixed
 
     def check_grad_views(self) -> bool:
         return all(p.grad is not None and p.grad.data_ptr() == self.grad[o:].data_ptr()
                    for p, (_, o, _, _) in zip(self.params, self.slices))
+
+
+def grad_out(p: torch.Tensor) -> torch.Tensor:
+    """fp32 buffer a backward kernel writes p's gradient into: p's flat gradient slot when p
+    is a direct-gradient parameter awaiting its gradient (autograd then adopts the returned
+    view as p.grad without a copy or an add), else a fresh tensor. A direct parameter must
+    receive its gradient from exactly one autograd node per backward."""
+    at = getattr(p, "_mbk_grad_at", None)
+    if at is not None and p.grad is None and getattr(p, "_mbk_direct_grad", False):
+        buf, o, n = at
+        return buf[o:o + n].view(p.shape)
+    return torch.empty(p.shape, dtype=torch.float32, device=p.device)
 
 
 class FlatAdam:
@@ -67,8 +112,8 @@ class FlatAdam:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
         dev = flat.data.device
-        self.m = torch.zeros_like(flat.data)
-        self.v = torch.zeros_like(flat.data)
+        self.m = zeros(flat.data.shape, torch.float32, flat.data.device)
+        self.v = zeros(flat.data.shape, torch.float32, flat.data.device)
         self.step_count = 0
         self.shadow = torch.empty(flat.numel, dtype=torch.bfloat16, device=dev) if bf16_shadow else None
         self._partials = torch.empty(1024, dtype=torch.float32, device=dev)

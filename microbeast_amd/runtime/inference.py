@@ -31,6 +31,7 @@ import time
 import torch
 
 from .. import _native as N
+from ..ops.copy import row_gather
 from ..ops.optim import FlatParams
 from ..utils.buffers import ShmRing
 
@@ -196,8 +197,8 @@ class InferenceServer:
                 self.d_obs.copy_(self.req_obs, non_blocking=True)
                 self.d_mask.copy_(self.req_mask, non_blocking=True)
                 idx = self.h_ids[:k].to(self.device, non_blocking=True)
-                obs = self.d_obs.index_select(0, idx).view(k * n, S)
-                mask = self.d_mask.index_select(0, idx).view(k * n, S, 3)
+                obs = row_gather(self.d_obs, idx, k).view(k * n, S)
+                mask = row_gather(self.d_mask, idx, k).view(k * n, S, 3)
                 a, lp, v = self.model.act(obs, mask, rng_state=self.rng)
                 self.h_action[:k * n].copy_(a.view(k * n, S, 7), non_blocking=True)
                 self.h_logp[:k * n].copy_(lp.view(-1), non_blocking=True)

@@ -67,13 +67,21 @@ class PinnedPrefetcher:
                         self.rt.free.push(m, 0.0)
                     return
                 out = {}
+                rtn = N.runtime()
+                st = self.copy_stream.cuda_stream
                 with torch.cuda.stream(self.copy_stream):
                     for src, dst in LEARNER_KEYS.items():
-                        s0 = bufs[src][idx[0]]
-                        d = torch.empty((self.B,) + tuple(s0.shape), dtype=s0.dtype,
+                        s0 = bufs[src][idx[0]]            # [T+1, n, ...] of one slot
+                        T1 = s0.shape[0]
+                        row = s0[0].numel() * s0.element_size()
+                        # time-major [T+1, B, n, ...]: slot j is a strided column block
+                        d = torch.empty((T1, self.B) + tuple(s0.shape[1:]), dtype=s0.dtype,
                                         device=self.device)
                         for j, m in enumerate(idx):
-                            d[j].copy_(bufs[src][m], non_blocking=True)
+                            err = rtn.memcpy2d_async(d.data_ptr() + j * row, self.B * row,
+                                                     bufs[src][m].data_ptr(), row, row, T1, st)
+                            if err != 0:
+                                raise RuntimeError(f"hipMemcpy2DAsync of '{src}' failed ({err})")
                             self.h2d_bytes += s0.numel() * s0.element_size()
                         out[dst] = d
                     ev = torch.cuda.Event()
@@ -109,8 +117,7 @@ class PinnedPrefetcher:
         batch = {}
         for k, d in out.items():
             d.record_stream(cur)
-            t = d.transpose(0, 1)  # [T+1, B, n, ...]
-            batch[k] = t.reshape((t.shape[0], t.shape[1] * t.shape[2]) + tuple(t.shape[3:]))
+            batch[k] = d.view((d.shape[0], d.shape[1] * d.shape[2]) + tuple(d.shape[3:]))
         return batch, []
 
     def stop(self):
