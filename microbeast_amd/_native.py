@@ -115,7 +115,12 @@ _SIGS = {
                    c_void_p],
     "mbk_map_gather": [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_value_bwd_parts": [c_int],
-    "mbk_value_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_value_bwd": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                      c_int, c_int, c_void_p],
+    "mbk_fc_wgrad_ex": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
+                        c_int, c_void_p],
+    "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
+                         c_int, c_int, c_int, c_void_p, c_void_p],
 }
 _RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64}
 

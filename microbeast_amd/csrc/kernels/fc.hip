@@ -39,10 +39,21 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
       (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
 }
 
+// relu of 8 packed bf16 (sign bit set -> 0)
+__device__ __forceinline__ uint4 relu8(uint4 v) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w[j] = ((w[j] & 0x8000u) ? 0u : (w[j] & 0xFFFFu)) |
+           ((w[j] & 0x80000000u) ? 0u : (w[j] & 0xFFFF0000u));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled
+// (relu: the staged values are relu'd, e.g. the trunk output feeding network.5)
 template <int W, bool VEC>
 __device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, int c0, int ld,
-                                      int tid) {
+                                      int tid, bool relu = false) {
   constexpr int C8 = W / 8;
   for (int e = tid; e < R * C8; e += kThreads) {
     const int row = e / C8, c = c0 + (e % C8) * 8, n = r + row;
@@ -59,7 +70,7 @@ __device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, in
                        h[4] | (uint32_t)h[5] << 16, h[6] | (uint32_t)h[7] << 16);
       }
     }
-    *(uint4*)(t + e * 16) = v;
+    *(uint4*)(t + e * 16) = relu ? relu8(v) : v;
   }
 }
 
@@ -71,6 +82,7 @@ constexpr int kMaxTaps = 9;
 struct XShifts {
   int s[kMaxTaps];
   int ntap;
+  int relu_x;  // ntap == 1 only: dW = g^T relu(x)
 };
 
 // x tile of the shifted-row weight gradient: output column c (of ntap * I) is channel
@@ -118,7 +130,7 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
   for (int rs = r0; rs < r1; rs += R) {
     __syncthreads();  // previous stage's reads done
     stage<OC, GVEC>(gt, g, rs, r1, o0, O, tid);
-    if (xs.ntap == 1) stage<IC, true>(xt, x, rs, r1, i0, I, tid);
+    if (xs.ntap == 1) stage<IC, true>(xt, x, rs, r1, i0, I, tid, xs.relu_x != 0);
     else stage_taps(xt, x, rs, r1, i0, I, TI, xs, N, tid);
     __syncthreads();
     const int nk = (min(R, r1 - rs) + 31) >> 5;
@@ -345,6 +357,16 @@ extern "C" int mbk_fc_wgrad(const void* g, const void* x, int N, int O, int I, f
                             int nparts, float* out, int accumulate, hipStream_t stream) {
   XShifts xs{};
   xs.ntap = 1;
+  return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
+}
+
+// mbk_fc_wgrad with relu_x: dW = g^T relu(x) (the pre-relu trunk output is what is saved)
+extern "C" int mbk_fc_wgrad_ex(const void* g, const void* x, int N, int O, int I, float* partial,
+                               int nparts, float* out, int accumulate, int relu_x,
+                               hipStream_t stream) {
+  XShifts xs{};
+  xs.ntap = 1;
+  xs.relu_x = relu_x;
   return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
 }
 

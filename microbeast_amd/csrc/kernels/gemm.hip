@@ -71,6 +71,8 @@ struct ATaps {
   // zeros at their (Y, X), which fills the zero border of a padded output grid exactly
   // (for a stride-2 transposed conv, across its 4 phases).
   int remap, Hp, Wp, ob, ow, sy, sx, oy0, ox0, lim_h, lim_w, zero_border;
+  // optional relu-backward mask in the output's layout: C[o] = 0 where mask[o] <= 0
+  const bf16* mask;
 };
 
 template <int ROWS>
@@ -189,6 +191,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
         if (relu) v = fmaxf(v, 0.f);
         if (zero) v = 0.f;
         const size_t o = orow * ldc + col;
+        if (taps.mask && !(__bfloat162float(taps.mask[o]) > 0.f)) v = 0.f;
         if (OUT_BF16) {
           ((bf16*)C)[o] = __float2bfloat16(v);
         } else {
@@ -239,6 +242,19 @@ extern "C" int mbk_gemm_nt(const void* A, const void* B, void* C, const float* b
   ATaps none{};
   launch_any<false>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, none,
                     stream);
+  return (int)hipGetLastError();
+}
+
+// mbk_gemm_nt with a relu-backward mask: C[m][n] = 0 where mask[m * ldc + n] <= 0 (bf16,
+// the forward activation in C's layout), e.g. dX of network.5 through the trunk-output relu
+extern "C" int mbk_gemm_nt_mask(const void* A, const void* B, void* C, const float* bias, int M,
+                                int N, int K, int lda, int ldb, int ldc, int relu, int out_bf16,
+                                const void* mask, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || K % 8 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
+  ATaps t{};
+  t.mask = (const bf16*)mask;
+  launch_any<false>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, 0, t, stream);
   return (int)hipGetLastError();
 }
 

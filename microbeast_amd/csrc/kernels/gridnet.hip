@@ -15,7 +15,8 @@
 //   colsum        deterministic two-stage column sums (bias gradients), bf16 or fp32 in
 //   map_gather    multi-segment index gather (weight packing into the GEMM operand layouts,
 //                 weight-gradient unpacking into the parameters' own layouts), one launch
-//   value_bwd     critic output layer backward: dh = dv * w2 * (h > 0), partial dW2 / db2
+//   value_bwd     critic output layer backward: dh = (dv * w2 + g_head) * (h > 0), partial
+//                 dW2 / db2 (also the IMPALA trunk tail's, models/agent.py)
 //
 // All index maths is 32-bit; the launchers check that every element count fits.
 #include "common.h"
@@ -293,11 +294,15 @@ __global__ __launch_bounds__(kThreads) void map_gather_kernel(MapSegs a) {
 //   dh[r][k] = bf16(dv[r] * w2[k]) where h > 0 (the hidden relu folded in), else 0;
 //   partial[part][k] = sum_r dv[r] * h[r][k] (dW2), partial[part][K] = sum_r dv[r] (db2).
 // Thread = (row slot, 8 columns): G = K/8 column groups, 256/G rows per pass.
+// gadd (optional, rows < gadd_rows): a second gradient of h added before the relu mask
+// (fp32 or bf16 [gadd_rows][K]) -- the IMPALA actor head's dX, which consumes h too.
 __global__ __launch_bounds__(kThreads) void value_bwd_kernel(const float* __restrict__ dv,
                                                              const bf16* __restrict__ h,
                                                              const float* __restrict__ w2, int R,
                                                              int K, int rpp, bf16* __restrict__ dh,
-                                                             float* __restrict__ partial) {
+                                                             float* __restrict__ partial,
+                                                             const void* __restrict__ gadd,
+                                                             int gadd_rows, int gadd_f32) {
   __shared__ float red[kThreads][9];
   const int G = K >> 3, rows = kThreads / G;
   const int cg = threadIdx.x % G, rs = threadIdx.x / G;
@@ -310,11 +315,27 @@ __global__ __launch_bounds__(kThreads) void value_bwd_kernel(const float* __rest
       const float d = dv[r];
       const uint4 u = *(const uint4*)(h + (size_t)r * K + 8 * cg);
       const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+      float ga[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ga[j] = 0.f;
+      if (r < gadd_rows) {
+        if (gadd_f32) {
+          const float4* gp = (const float4*)((const float*)gadd + (size_t)r * K + 8 * cg);
+          const float4 a = gp[0], b = gp[1];
+          ga[0] = a.x, ga[1] = a.y, ga[2] = a.z, ga[3] = a.w;
+          ga[4] = b.x, ga[5] = b.y, ga[6] = b.z, ga[7] = b.w;
+        } else {
+          const uint4 gv = *(const uint4*)((const bf16*)gadd + (size_t)r * K + 8 * cg);
+          const uint32_t gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+          for (int j = 0; j < 8; ++j) ga[j] = (j & 1) ? bf_hi(gg[j >> 1]) : bf_lo(gg[j >> 1]);
+        }
+      }
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const float hj = (j & 1) ? bf_hi(uu[j >> 1]) : bf_lo(uu[j >> 1]);
-        o[j] = hj > 0.f ? d * w[j] : 0.f;
+        o[j] = hj > 0.f ? d * w[j] + ga[j] : 0.f;
         sw[j] += d * hj;
       }
       sb += d;
@@ -445,14 +466,16 @@ extern "C" int mbk_map_gather(int nseg, const void* const* src, void* const* dst
 int value_parts(int R) { return std::max(1, std::min(256, (R + 1023) / 1024)); }
 extern "C" int mbk_value_bwd_parts(int R) { return value_parts(R); }
 
-// dh [R][K] bf16, partial [value_parts(R)][K+1] fp32; K % 8 == 0, K <= 2048
+// dh [R][K] bf16, partial [value_parts(R)][K+1] fp32; K % 8 == 0, K <= 2048;
+// gadd: null or [gadd_rows][K] (fp32 if gadd_f32 else bf16)
 extern "C" int mbk_value_bwd(const float* dv, const void* h, const float* w2, int R, int K,
-                             void* dh, float* partial, hipStream_t stream) {
+                             void* dh, float* partial, const void* gadd, int gadd_rows,
+                             int gadd_f32, hipStream_t stream) {
   if (R <= 0) return 0;
-  if (K % 8 || K > 8 * kThreads) return (int)hipErrorInvalidValue;
+  if (K % 8 || K > 8 * kThreads || gadd_rows > R) return (int)hipErrorInvalidValue;
   const int P = value_parts(R);
   const int rpp = (R + P - 1) / P;
   hipLaunchKernelGGL(value_bwd_kernel, dim3(P), dim3(kThreads), 0, stream, dv, (const bf16*)h, w2,
-                     R, K, rpp, (bf16*)dh, partial);
+                     R, K, rpp, (bf16*)dh, partial, gadd, gadd ? gadd_rows : 0, gadd_f32);
   return (int)hipGetLastError();
 }

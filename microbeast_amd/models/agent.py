@@ -30,6 +30,7 @@ from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.head import SparseHead, sparse_sample, sparse_score
 from ..ops.linear import linear, nhwc_weight
 from ..ops.obs import bits_to_planes, dense_to_bits
+from ..ops.tail import TailMaps, impala_tail
 
 HIP_CHANNELS = (16, 32)  # conv widths the HIP trunk kernels are instantiated for
 
@@ -112,6 +113,9 @@ class Agent(nn.Module):
         self.actor = layer_init(nn.Linear(hidden, sum(self.nvec)), std=0.0)
         self.critic = layer_init(nn.Linear(hidden, 1), std=1)
         self.compute_dtype = compute_dtype
+        self._tail_maps = None
+        for p in self.parameters():  # the HIP learner path writes grads into flat slots
+            p._mbk_direct_grad = True
         self.to(device)
 
     # ------------------------------------------------------------ encoder
@@ -127,6 +131,12 @@ class Agent(nn.Module):
         # casts must not leak across hipGraph capture boundaries
         return torch.autocast("cuda", dtype=self.compute_dtype, enabled=enabled,
                               cache_enabled=False)
+
+    def direct_grad_ok(self, device) -> bool:
+        """the learner's backward writes every gradient into its flat slot (ops/tail.py,
+        ops/encoder.py) -- the HIP path on a GPU"""
+        return (self.hip_kernels and torch.device(device).type == "cuda"
+                and all(c in HIP_CHANNELS for c in self.channels))
 
     def _use_hip(self, obs: torch.Tensor) -> bool:
         if not (self.hip_kernels and obs.is_cuda and obs.dtype == torch.int32):
@@ -177,20 +187,26 @@ class Agent(nn.Module):
                                        f.data_ptr(), v.data_ptr(), N.stream_ptr()), "fc_fwd")
         return f, v
 
+    def _trunk(self, obs: torch.Tensor) -> torch.Tensor:
+        """HIP conv trunk (NHWC bf16 [n, ho, wo, c], before the reference's Flatten/ReLU)."""
+        if self._hip_enc is None or self._hip_enc.packed_fwd.device != obs.device:
+            self._hip_enc = HipEncoder(self.h, self.w, self.planes, self.channels, obs.device)
+        # fp8 MFMA convs for no-grad (acting) forwards when enabled (config 5);
+        # gradient-carrying forwards always run the bf16 kernels
+        self._hip_enc.fp8 = self.fp8_inference
+        n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
+        grad = torch.is_grad_enabled()
+        pre = self._prepacked and not grad
+        return encode(obs.reshape(n, self.h * self.w), self._hip_enc,
+                      encoder_params(self.network, len(self.channels)), grad, prepacked=pre)
+
     def features(self, obs: torch.Tensor) -> torch.Tensor:
         if self._use_hip(obs):
             # conv trunk on the HIP MFMA kernels (NHWC bf16), then the reference's
             # NCHW flatten order into network.5
-            if self._hip_enc is None or self._hip_enc.packed_fwd.device != obs.device:
-                self._hip_enc = HipEncoder(self.h, self.w, self.planes, self.channels, obs.device)
-            # fp8 MFMA convs for no-grad (acting) forwards when enabled (config 5);
-            # gradient-carrying forwards always run the bf16 kernels
-            self._hip_enc.fp8 = self.fp8_inference
-            n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
-            grad = torch.is_grad_enabled()
-            pre = self._prepacked and not grad
-            y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
-                       encoder_params(self.network, len(self.channels)), grad, prepacked=pre)
+            y = self._trunk(obs)
+            n = y.shape[0]
+            pre = self._prepacked and not torch.is_grad_enabled()
             # ReLU -> network.5 -> ReLU on the NHWC rows: the Linear's input columns are
             # permuted from the reference's NCHW flatten order instead of the activations
             nseq = len(self.channels)
@@ -295,6 +311,21 @@ class Agent(nn.Module):
         Used by the learner on a time-major (T+1)*B batch: values are needed on
         all T+1 rows (bootstrap), the head only on the first T*B.
         """
+        if self._use_hip(obs) and torch.is_grad_enabled():
+            # learner: trunk, then ONE autograd node for network.5 + head + critic whose
+            # backward kernels write every gradient (ops/tail.py)
+            y = self._trunk(obs)
+            n = y.shape[0]
+            ns = n if n_score is None else n_score
+            _, ho, wo, c = y.shape
+            fc = self.network[len(self.channels) + 2]
+            key = (fc.out_features, c, ho, wo)
+            if (self._tail_maps is None or self._tail_maps.key != key
+                    or self._tail_maps.device != y.device):
+                self._tail_maps = TailMaps(*key, y.device)
+            return impala_tail(y, fc, self.critic, self.actor, mask_bits.reshape(ns, -1, 3),
+                               action.reshape(ns, -1, 7), ns, self._head(y.device),
+                               self._tail_maps)
         f = self.features(obs)
         if self._use_hip(obs):
             value = linear(f, self.critic).float().view(-1)

@@ -65,6 +65,10 @@ class GridNetAgent(nn.Module):
                               enabled=t.is_cuda and self.compute_dtype != torch.float32,
                               cache_enabled=False)
 
+    def direct_grad_ok(self, device) -> bool:
+        """the grid path's backward writes every gradient into its flat slot"""
+        return self.hip_kernels and (torch.device(device).type == "cuda" or self.emulate)
+
     def _use_hip(self, obs) -> bool:
         return self.hip_kernels and obs.dtype == torch.int32 and (obs.is_cuda or self.emulate)
 

@@ -49,7 +49,10 @@ def zero_(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
-def zeros(shape, dtype=torch.float32, device=None) -> torch.Tensor:
+def zeros(*shape, dtype=torch.float32, device=None) -> torch.Tensor:
+    """torch.zeros without an ATen fill kernel on the GPU (hipMemsetAsync)."""
+    if len(shape) == 1 and isinstance(shape[0], (tuple, list, torch.Size)):
+        shape = tuple(shape[0])
     return zero_(torch.empty(shape, dtype=dtype, device=device))
 
 

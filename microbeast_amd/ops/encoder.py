@@ -20,6 +20,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import _native as N
+from .optim import grad_out
 
 
 @dataclass
@@ -328,7 +329,8 @@ class HipEncoder:
         return x, saved
 
     def backward(self, g: torch.Tensor, saved: list[torch.Tensor], params: list[torch.Tensor]):
-        grads = [torch.empty_like(p) for p in params]
+        # each gradient goes straight into its parameter's flat slot when it can (optim.py)
+        grads = [grad_out(p) for p in params]
         nst = len(self.layers) // 5
         g = g.contiguous()
         for s in range(nst - 1, -1, -1):
@@ -378,14 +380,14 @@ class _EncoderFn(torch.autograd.Function):
         out, saved = enc.forward(obs_bits, list(params), save=True)
         ctx.enc = enc
         ctx.nsaved = len(saved)
-        ctx.save_for_backward(*saved, *params)
+        ctx.save_for_backward(*saved)
+        ctx.params = params
         return out
 
     @staticmethod
     def backward(ctx, g):
-        t = ctx.saved_tensors
-        saved, params = list(t[:ctx.nsaved]), list(t[ctx.nsaved:])
-        grads = ctx.enc.backward(g.to(torch.bfloat16), saved, params)
+        saved = list(ctx.saved_tensors)
+        grads = ctx.enc.backward(g.to(torch.bfloat16), saved, list(ctx.params))
         return (None, None, *grads)
 
 

@@ -348,23 +348,32 @@ def map_gather(segs):
 
 
 def value_bwd(dv: torch.Tensor, h: torch.Tensor, w2: torch.Tensor, gw2: torch.Tensor,
-              gb2: torch.Tensor) -> torch.Tensor:
+              gb2: torch.Tensor, gadd: torch.Tensor | None = None) -> torch.Tensor:
     """Critic output layer v = h . w2 + b2 with h = relu(.): returns dh (bf16, relu mask
-    applied) and writes dW2 / db2 (fp32) into gw2 / gb2."""
+    applied) and writes dW2 / db2 (fp32) into gw2 / gb2. gadd: another gradient of the first
+    gadd.shape[0] rows of h (fp32 / bf16), added before the relu mask."""
     R, K = h.shape
     if not h.is_cuda:
         dvf = dv.float().reshape(R, 1)
         gw2.view(-1).copy_((dvf * h.float()).sum(0))
         gb2.view(-1).copy_(dvf.sum())
-        return ((dvf * w2.reshape(1, K)) * (h > 0)).to(_BF)
+        d = dvf * w2.reshape(1, K)
+        if gadd is not None:
+            d[:gadd.shape[0]] += gadd.float()
+        return (d * (h > 0)).to(_BF)
     N = _N()
     k = N.kernels()
     assert dv.dtype == torch.float32 and dv.is_contiguous() and h.is_contiguous()
     parts = k.mbk_value_bwd_parts(R)
     partial = torch.empty(parts, K + 1, dtype=torch.float32, device=h.device)
     dh = torch.empty(R, K, dtype=_BF, device=h.device)
+    if gadd is not None:
+        assert gadd.is_contiguous() and gadd.shape[1] == K and gadd.dtype in (torch.float32, _BF)
     N.check(k.mbk_value_bwd(dv.data_ptr(), h.data_ptr(), w2.data_ptr(), R, K, dh.data_ptr(),
-                            partial.data_ptr(), N.stream_ptr()), "value_bwd")
+                            partial.data_ptr(), N.ptr(gadd),
+                            gadd.shape[0] if gadd is not None else 0,
+                            int(gadd is not None and gadd.dtype == torch.float32),
+                            N.stream_ptr()), "value_bwd")
     colsum(partial, K + 1, gw2, K, gb2)
     return dh
 

@@ -122,8 +122,9 @@ class SparseHead:
             N.check(k.mbk_rng_advance(rng.data_ptr(), st), "rng_advance")
         return logp, ent
 
-    def backward(self, X, mask_bits, action, g_logp, g_ent):
-        """Returns (dX fp32 [F,256], dW fp32 [S*78,256], db fp32 [S*78]).
+    def backward(self, X, mask_bits, action, g_logp, g_ent, dW=None, db=None):
+        """Returns (dX fp32 [F,256], dW fp32 [S*78,256], db fp32 [S*78]); dW / db may be
+        given (e.g. the parameters' flat gradient slots).
 
         Relies on the compaction left by the matching forward (same batch)."""
         F = X.shape[0]
@@ -134,8 +135,11 @@ class SparseHead:
         dXp = torch.empty(max(P, 1), KD, dtype=torch.float32, device=X.device)
         dWp = torch.empty(max(nch, 1), 78, KD, dtype=torch.float32, device=X.device)
         dbp = torch.empty(max(nch, 1), 78, dtype=torch.float32, device=X.device)
-        dW = torch.empty(self.S * 78, KD, dtype=torch.float32, device=X.device)
-        db = torch.empty(self.S * 78, dtype=torch.float32, device=X.device)
+        if dW is None:
+            dW = torch.empty(self.S * 78, KD, dtype=torch.float32, device=X.device)
+        if db is None:
+            db = torch.empty(self.S * 78, dtype=torch.float32, device=X.device)
+        assert dW.is_contiguous() and db.is_contiguous() and dW.numel() == self.S * 78 * KD
         grid = max(1, min(nch, self.fwd_grid // 2))
         N.check(k.mbk_head_bwd(X.data_ptr(), self.Wp.data_ptr(), self.WpT.data_ptr(),
                                self.bp.data_ptr(), mask_bits.data_ptr(), action.data_ptr(),

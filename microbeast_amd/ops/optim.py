@@ -15,7 +15,7 @@ import torch
 import torch.nn as nn
 
 from .. import _native as N
-from .copy import zero_, zeros
+from .copy import full, zero_, zeros
 
 _ALIGN = 64  # elements: every parameter starts 256-B aligned
 
@@ -30,8 +30,8 @@ class FlatParams:
             offs.append(off)
             off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
         self.numel = off
-        self.data = zeros(off, torch.float32, dev)
-        self.grad = zeros(off, torch.float32, dev)
+        self.data = zeros(off, device=dev)
+        self.grad = zeros(off, device=dev)
         self.slices = []
         names = {id(p): n for n, p in module.named_parameters()}
         for p, o in zip(params, offs):
@@ -46,7 +46,10 @@ class FlatParams:
         # "direct" parameters: their backward kernels write the gradient straight into the
         # flat slot (``grad_out``) and autograd adopts that view as .grad -- no zero fill of
         # the buffer, no AccumulateGrad add kernel per parameter
-        self.direct = [bool(getattr(p, "_mbk_direct_grad", False)) for p in params]
+        # (only when the module says its backward will take that path on this device)
+        ok = getattr(module, "direct_grad_ok", None)
+        allow = bool(ok(dev)) if ok is not None else False
+        self.direct = [allow and bool(getattr(p, "_mbk_direct_grad", False)) for p in params]
 
     def zero_grad(self):
         if not any(self.direct):
@@ -112,12 +115,12 @@ class FlatAdam:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_grad_norm = max_grad_norm
         dev = flat.data.device
-        self.m = zeros(flat.data.shape, torch.float32, flat.data.device)
-        self.v = zeros(flat.data.shape, torch.float32, flat.data.device)
+        self.m = zeros(flat.data.shape, device=flat.data.device)
+        self.v = zeros(flat.data.shape, device=flat.data.device)
         self.step_count = 0
         self.shadow = torch.empty(flat.numel, dtype=torch.bfloat16, device=dev) if bf16_shadow else None
         self._partials = torch.empty(1024, dtype=torch.float32, device=dev)
-        self._scale = torch.ones(2, dtype=torch.float32, device=dev)
+        self._scale = full((2,), 1.0, device=dev)
         self.last_grad_norm = None
 
     def state_dict(self):

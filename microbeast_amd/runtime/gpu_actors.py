@@ -27,6 +27,7 @@ import torch
 
 from .. import _native as N
 from ..ops import cell_head
+from ..ops.copy import zeros
 from ..ops.optim import FlatParams
 
 BOT_IDS = {"coac": 0, "random_biased": 1, "light_rush": 2, "worker_rush": 3, "passive": 4,
@@ -77,22 +78,22 @@ class GpuActorRuntime:
         S, E, T1, NS = self.S, self.E, self.T + 1, self.n_slots
         dev = device
         self.rb = {
-            "obs": torch.zeros(NS, T1, E, S, dtype=torch.int32, device=dev),
-            "mask": torch.zeros(NS, T1, E, S, 3, dtype=torch.int32, device=dev),
-            "action": torch.zeros(NS, T1, E, S, 7, dtype=torch.uint8, device=dev),
-            "logp": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
-            "value": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
-            "reward": torch.zeros(NS, T1, E, dtype=torch.float32, device=dev),
-            "done": torch.zeros(NS, T1, E, dtype=torch.uint8, device=dev),
+            "obs": zeros(NS, T1, E, S, dtype=torch.int32, device=dev),
+            "mask": zeros(NS, T1, E, S, 3, dtype=torch.int32, device=dev),
+            "action": zeros(NS, T1, E, S, 7, dtype=torch.uint8, device=dev),
+            "logp": zeros(NS, T1, E, dtype=torch.float32, device=dev),
+            "value": zeros(NS, T1, E, dtype=torch.float32, device=dev),
+            "reward": zeros(NS, T1, E, dtype=torch.float32, device=dev),
+            "done": zeros(NS, T1, E, dtype=torch.uint8, device=dev),
         }
         self.reference_keys = reference_keys or policy_logits
         self.emit_logits = policy_logits
         if self.reference_keys:
-            self.rb["ep_return"] = torch.zeros(NS, T1, E, dtype=torch.float32, device=dev)
-            self.rb["ep_step"] = torch.zeros(NS, T1, E, dtype=torch.int32, device=dev)
-            self.rb["last_action0"] = torch.zeros(NS, E, S, 7, dtype=torch.uint8, device=dev)
+            self.rb["ep_return"] = zeros(NS, T1, E, dtype=torch.float32, device=dev)
+            self.rb["ep_step"] = zeros(NS, T1, E, dtype=torch.int32, device=dev)
+            self.rb["last_action0"] = zeros(NS, E, S, 7, dtype=torch.uint8, device=dev)
         if policy_logits:
-            self.rb["policy_logits"] = torch.zeros(NS, T1, E, S * 78, dtype=torch.float32,
+            self.rb["policy_logits"] = zeros(NS, T1, E, S * 78, dtype=torch.float32,
                                                    device=dev)
         # policy lanes: group g steps on lane g % n_lanes; every lane has its own stream,
         # captured graph, I/O buffers, RNG stream and inference-weight copy, so policy steps
@@ -163,18 +164,18 @@ class GpuActorRuntime:
         E, S, dev = self.E, self.S, self.device
         return {
             # what crosses PCIe: 16-bit cell codes + resources in, packed actions out
-            "in_codes": torch.zeros(E, S, dtype=torch.int16, device=dev),
-            "in_res": torch.zeros(E, dtype=torch.int32, device=dev),
-            "out_act16": torch.zeros(E, S, dtype=torch.int16, device=dev),
+            "in_codes": zeros(E, S, dtype=torch.int16, device=dev),
+            "in_res": zeros(E, dtype=torch.int32, device=dev),
+            "out_act16": zeros(E, S, dtype=torch.int16, device=dev),
             # decoded on the GPU inside the policy graph
-            "in_obs": torch.zeros(E, S, dtype=torch.int32, device=dev),
-            "in_mask": torch.zeros(E, S, 3, dtype=torch.int32, device=dev),
-            "out_action": torch.zeros(E, S, 7, dtype=torch.uint8, device=dev),
-            "out_logp": torch.zeros(E, dtype=torch.float32, device=dev),
-            "out_value": torch.zeros(E, dtype=torch.float32, device=dev),
+            "in_obs": zeros(E, S, dtype=torch.int32, device=dev),
+            "in_mask": zeros(E, S, 3, dtype=torch.int32, device=dev),
+            "out_action": zeros(E, S, 7, dtype=torch.uint8, device=dev),
+            "out_logp": zeros(E, dtype=torch.float32, device=dev),
+            "out_value": zeros(E, dtype=torch.float32, device=dev),
             # dense-head (GridNet) sampling workspace, per lane
-            "cell_logp": torch.zeros(E * S, dtype=torch.float32, device=dev),
-        } | ({"out_logits": torch.zeros(E, S * 78, dtype=torch.float32, device=dev)}
+            "cell_logp": zeros(E * S, dtype=torch.float32, device=dev),
+        } | ({"out_logits": zeros(E, S * 78, dtype=torch.float32, device=dev)}
              if getattr(self, "emit_logits", False) else {})
 
     def _policy_step(self, io, m, rng):
