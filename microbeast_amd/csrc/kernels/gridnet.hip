@@ -48,17 +48,19 @@ int grid_for(long work) {
 // bits [n][h*w] (plane p = bit p, p < 32) -> out [n][Hp][Wp][32] bf16; pixel (y, x) of the
 // map sits at (y + 1, x + 1); the border and the area past (h, w) (maps padded up to a
 // multiple of 16) are zero. Thread = (pixel, 8 planes): one 16-byte store.
+template <typename IDX>
 __global__ __launch_bounds__(kThreads) void bits_grid_kernel(const uint32_t* __restrict__ bits,
                                                              int n, int h, int w, int Hp, int Wp,
                                                              uint4* __restrict__ out) {
-  const int total = n * Hp * Wp * 4;
-  for (int e = blockIdx.x * kThreads + threadIdx.x; e < total; e += gridDim.x * kThreads) {
-    const int q = e & 3, p = e >> 2;
+  const IDX total = (IDX)n * Hp * Wp * 4;
+  for (IDX e = (IDX)blockIdx.x * kThreads + threadIdx.x; e < total; e += (IDX)gridDim.x * kThreads) {
+    const int q = (int)(e & 3);
+    const int p = (int)(e >> 2);
     const int x = p % Wp, t = p / Wp;
     const int y = t % Hp, b = t / Hp;
     uint32_t v = 0;
     if (y >= 1 && y <= h && x >= 1 && x <= w)
-      v = (bits[b * h * w + (y - 1) * w + (x - 1)] >> (8 * q)) & 0xFFu;
+      v = (bits[(size_t)b * h * w + (y - 1) * w + (x - 1)] >> (8 * q)) & 0xFFu;
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -72,6 +74,7 @@ __global__ __launch_bounds__(kThreads) void bits_grid_kernel(const uint32_t* __r
 // [B][Ho+2][Wo+2][C] (zero border), idx [B][Ho][Wo][C] = ky*3+kx of the first maximum in
 // scan order (ATen's tie rule). Thread = (pixel of the padded grid if out_pad, else of the
 // plain grid; 8 channels).
+template <typename IDX>
 __global__ __launch_bounds__(kThreads) void pool_fwd_kernel(const bf16* __restrict__ y, int B,
                                                             int H, int W, int C, int Ho, int Wo,
                                                             bf16* __restrict__ out,
@@ -80,9 +83,9 @@ __global__ __launch_bounds__(kThreads) void pool_fwd_kernel(const bf16* __restri
   const int C8 = C >> 3;
   const int pad = out_pad ? 1 : 0;
   const int Hg = Ho + 2 * pad, Wg = Wo + 2 * pad;
-  const int total = B * Hg * Wg * C8;
-  for (int e = blockIdx.x * kThreads + threadIdx.x; e < total; e += gridDim.x * kThreads) {
-    const int c8 = e % C8, p = e / C8;
+  const IDX total = (IDX)B * Hg * Wg * C8;
+  for (IDX e = (IDX)blockIdx.x * kThreads + threadIdx.x; e < total; e += (IDX)gridDim.x * kThreads) {
+    const int c8 = (int)(e % C8), p = (int)(e / C8);
     const int gx = p % Wg, t = p / Wg;
     const int gy = t % Hg, b = t / Hg;
     const int oy = gy - pad, ox = gx - pad;
@@ -129,15 +132,16 @@ __global__ __launch_bounds__(kThreads) void pool_fwd_kernel(const bf16* __restri
 // relu of the conv output; pooled = the argmax element's value) and go to the argmax
 // position. Output: dy on the padded conv-output grid [B][H+2][W+2][C] (zero border), i.e.
 // directly the operand of the conv's dgrad / wgrad GEMMs. Thread = (padded pixel, 8 ch).
+template <typename IDX>
 __global__ __launch_bounds__(kThreads) void pool_bwd_kernel(
     const bf16* __restrict__ g1, int pad1, const bf16* __restrict__ g2, int pad2,
     const bf16* __restrict__ pooled, int padp, const uint8_t* __restrict__ idx, int B, int H,
     int W, int C, int Ho, int Wo, bf16* __restrict__ dy) {
   const int C8 = C >> 3;
   const int Hp = H + 2, Wp = W + 2;
-  const int total = B * Hp * Wp * C8;
-  for (int e = blockIdx.x * kThreads + threadIdx.x; e < total; e += gridDim.x * kThreads) {
-    const int c8 = e % C8, p = e / C8;
+  const IDX total = (IDX)B * Hp * Wp * C8;
+  for (IDX e = (IDX)blockIdx.x * kThreads + threadIdx.x; e < total; e += (IDX)gridDim.x * kThreads) {
+    const int c8 = (int)(e % C8), p = (int)(e / C8);
     const int x = p % Wp, t = p / Wp;
     const int y = t % Hp, b = t / Hp;
     const int Y = y - 1, X = x - 1;
@@ -194,19 +198,23 @@ __global__ __launch_bounds__(kThreads) void pool_bwd_kernel(
 // stride), so plain, padded (offset base) and cropped layouts are all one case.
 struct GatherArgs {
   const void* src;
-  int src_f32, sb, sy, sx;
+  int src_f32;
+  int64_t sb;
+  int sy, sx;
   int Hv, Wv, Cs;
   const bf16* mask;
-  int mb, my, mx;
+  int64_t mb;
+  int my, mx;
   bf16* dst;
   int S, B, Hd, Wd, Cd;
 };
 
+template <typename IDX>
 __global__ __launch_bounds__(kThreads) void grid_gather_kernel(GatherArgs a) {
   const int Hp = a.Hd + 2, Wp = a.Wd + 2, C8 = a.Cd >> 3;
-  const int total = a.S * a.S * a.B * Hp * Wp * C8;
-  for (int e = blockIdx.x * kThreads + threadIdx.x; e < total; e += gridDim.x * kThreads) {
-    const int c8 = e % C8, p = e / C8;
+  const IDX total = (IDX)a.S * a.S * a.B * Hp * Wp * C8;
+  for (IDX e = (IDX)blockIdx.x * kThreads + threadIdx.x; e < total; e += (IDX)gridDim.x * kThreads) {
+    const int c8 = (int)(e % C8), p = (int)(e / C8);
     const int x = p % Wp, t = p / Wp;
     const int y = t % Hp, t2 = t / Hp;
     const int b = t2 % a.B, ph = t2 / a.B;
@@ -215,8 +223,8 @@ __global__ __launch_bounds__(kThreads) void grid_gather_kernel(GatherArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = 0.f;
     if (y >= 1 && y <= a.Hd && x >= 1 && x <= a.Wd && Y < a.Hv && X < a.Wv) {
-      const int so = b * a.sb + Y * a.sy + X * a.sx;
-      const int mo = b * a.mb + Y * a.my + X * a.mx;
+      const int64_t so = b * a.sb + (int64_t)Y * a.sy + X * a.sx;
+      const int64_t mo = b * a.mb + (int64_t)Y * a.my + X * a.mx;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int ch = 8 * c8 + j;
@@ -252,17 +260,63 @@ __global__ __launch_bounds__(kThreads) void colsum_part_kernel(const T* __restri
     partial[(size_t)blockIdx.x * C + col] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-// Stage 2: out[c] = sum_p partial[p][c]; columns [0, c0) -> out0, [c0, C) -> out1 (so one
-// reduction can fill two separate parameter gradients, e.g. dW2 and db2)
+// Stage 1, vector form for bf16 rows (ld % 8 == 0, C <= 256): thread = (8-column group cg,
+// row slot); 16-byte loads, 256 / CG rows per pass, fixed-order LDS combine per block.
+__global__ __launch_bounds__(kThreads) void colsum_part_vec_kernel(const bf16* __restrict__ x,
+                                                                   int R, int C, int ld, int rpp,
+                                                                   float* __restrict__ partial) {
+  __shared__ float red[kThreads][8];
+  const int CG = (C + 7) >> 3, slots = kThreads / CG;
+  const int cg = threadIdx.x % CG, rs = threadIdx.x / CG;
+  const int r0 = blockIdx.x * rpp, r1 = min(R, r0 + rpp);
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  if (rs < slots)
+    for (int r = r0 + rs; r < r1; r += slots) {
+      const uint4 u = *(const uint4*)(x + (size_t)r * ld + 8 * cg);
+      const uint32_t uu[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (j & 1) ? bf_hi(uu[j >> 1]) : bf_lo(uu[j >> 1]);
+    }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[threadIdx.x][j] = acc[j];
+  __syncthreads();
+  if (threadIdx.x < CG) {
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = 0.f;
+    for (int q = 0; q < slots; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s[j] += red[q * CG + threadIdx.x][j];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = 8 * threadIdx.x + j;
+      if (c < C) partial[(size_t)blockIdx.x * C + c] = s[j];
+    }
+  }
+}
+
+// Stage 2: out[c] = sum_p partial[p][c] (block per column, fixed-order tree); columns
+// [0, c0) -> out0, [c0, C) -> out1 (so one reduction can fill two separate parameter
+// gradients, e.g. dW2 and db2)
 __global__ __launch_bounds__(kThreads) void colsum_fin_kernel(const float* __restrict__ partial,
                                                               int P, int C, float* out0, int c0,
                                                               float* out1) {
-  const int c = blockIdx.x * kThreads + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[kThreads];
+  const int c = blockIdx.x;
   float s = 0.f;
-  for (int p = 0; p < P; ++p) s += partial[(size_t)p * C + c];
-  if (c < c0) out0[c] = s;
-  else out1[c - c0] = s;
+  for (int p = threadIdx.x; p < P; p += kThreads) s += partial[(size_t)p * C + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (c < c0) out0[c] = red[0];
+    else out1[c - c0] = red[0];
+  }
 }
 
 // ------------------------------------------------------------------ multi-segment gather
@@ -361,6 +415,16 @@ __global__ __launch_bounds__(kThreads) void value_bwd_kernel(const float* __rest
 }
 
 bool fits(long v) { return v >= 0 && v < INT_MAX; }
+// element counts past 2^31 (e.g. 262K-row learner batches) take the 64-bit index variant;
+// pixel counts must still fit 32 bits
+#define MBK_LAUNCH_IDX(kern, total, ...)                                                  \
+  do {                                                                                   \
+    if (fits(total))                                                                     \
+      hipLaunchKernelGGL(kern<int>, dim3(grid_for(total)), dim3(kThreads), 0, __VA_ARGS__); \
+    else                                                                                 \
+      hipLaunchKernelGGL(kern<int64_t>, dim3(grid_for(total)), dim3(kThreads), 0,          \
+                         __VA_ARGS__);                                                   \
+  } while (0)
 
 }  // namespace
 
@@ -368,9 +432,9 @@ extern "C" int mbk_bits_grid(const void* bits, int n, int h, int w, int Hp, int 
                              hipStream_t stream) {
   const long total = (long)n * Hp * Wp * 4;
   if (n <= 0) return 0;
-  if (!fits(total) || Hp < h + 2 || Wp < w + 2) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bits_grid_kernel, dim3(grid_for(total)), dim3(kThreads), 0, stream,
-                     (const uint32_t*)bits, n, h, w, Hp, Wp, (uint4*)out);
+  if (!fits((long)n * Hp * Wp) || Hp < h + 2 || Wp < w + 2) return (int)hipErrorInvalidValue;
+  MBK_LAUNCH_IDX(bits_grid_kernel, total, stream, (const uint32_t*)bits, n, h, w, Hp, Wp,
+                 (uint4*)out);
   return (int)hipGetLastError();
 }
 
@@ -379,10 +443,11 @@ extern "C" int mbk_pool_fwd(const void* y, int B, int H, int W, int C, void* out
                             void* idx, hipStream_t stream) {
   if (B <= 0) return 0;
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
-  const long total = (long)B * (Ho + 2) * (Wo + 2) * C;
-  if (C % 8 || !fits(total) || (!out && !out_pad) || !idx) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(pool_fwd_kernel, dim3(grid_for(total / 8)), dim3(kThreads), 0, stream,
-                     (const bf16*)y, B, H, W, C, Ho, Wo, (bf16*)out, (bf16*)out_pad, (uint8_t*)idx);
+  const long total = (long)B * (Ho + 2) * (Wo + 2) * (C / 8);
+  if (C % 8 || !fits((long)B * (H + 2) * (W + 2)) || (!out && !out_pad) || !idx)
+    return (int)hipErrorInvalidValue;
+  MBK_LAUNCH_IDX(pool_fwd_kernel, total, stream, (const bf16*)y, B, H, W, C, Ho, Wo, (bf16*)out,
+                 (bf16*)out_pad, (uint8_t*)idx);
   return (int)hipGetLastError();
 }
 
@@ -392,11 +457,10 @@ extern "C" int mbk_pool_bwd_grid(const void* g1, int pad1, const void* g2, int p
                                  int W, int C, void* dy, hipStream_t stream) {
   if (B <= 0) return 0;
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
-  const long total = (long)B * (H + 2) * (W + 2) * C;
-  if (C % 8 || !fits(total)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(pool_bwd_kernel, dim3(grid_for(total / 8)), dim3(kThreads), 0, stream,
-                     (const bf16*)g1, pad1, (const bf16*)g2, pad2, (const bf16*)pooled, padp,
-                     (const uint8_t*)idx, B, H, W, C, Ho, Wo, (bf16*)dy);
+  const long total = (long)B * (H + 2) * (W + 2) * (C / 8);
+  if (C % 8 || !fits((long)B * (H + 2) * (W + 2))) return (int)hipErrorInvalidValue;
+  MBK_LAUNCH_IDX(pool_bwd_kernel, total, stream, (const bf16*)g1, pad1, (const bf16*)g2, pad2,
+                 (const bf16*)pooled, padp, (const uint8_t*)idx, B, H, W, C, Ho, Wo, (bf16*)dy);
   return (int)hipGetLastError();
 }
 
@@ -413,15 +477,14 @@ extern "C" int mbk_grid_gather(const void* src, const void* mask, const int* geo
   a.dst = (bf16*)dst;
   a.Cd = Cd;
   if (a.B <= 0) return 0;
-  const long total = (long)a.S * a.S * a.B * (a.Hd + 2) * (a.Wd + 2) * Cd;
-  const long last_src = (long)(a.B - 1) * a.sb + (long)(a.Hv - 1) * a.sy + (long)(a.Wv - 1) * a.sx + a.Cs;
-  if (Cd % 8 || (a.S != 1 && a.S != 2) || a.Cs > Cd || !fits(total) || !fits(last_src))
+  const long pixels = (long)a.S * a.S * a.B * (a.Hd + 2) * (a.Wd + 2);
+  if (Cd % 8 || (a.S != 1 && a.S != 2) || a.Cs > Cd || !fits(pixels))
     return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(grid_gather_kernel, dim3(grid_for(total / 8)), dim3(kThreads), 0, stream, a);
+  MBK_LAUNCH_IDX(grid_gather_kernel, pixels * (Cd / 8), stream, a);
   return (int)hipGetLastError();
 }
 
-int colsum_parts(long R) { return (int)std::max(1L, std::min(256L, (R + 4095) / 4096)); }
+int colsum_parts(long R) { return (int)std::max(1L, std::min(2048L, (R + 1023) / 1024)); }
 
 // Column sums of x [R][ld] (x_f32: fp32, else bf16) into out0[0:c0] / out1[0:C-c0]
 // (out1 may be null when c0 >= C). partial: colsum_parts(R) * C floats of scratch.
@@ -432,14 +495,17 @@ extern "C" int mbk_colsum(const void* x, int x_f32, int R, int C, int ld, float*
   const int P = colsum_parts(R);
   const int rpp = std::max(1, (R + P - 1) / P);
   const dim3 g1(P, (C + 63) / 64);
-  if (x_f32)
+  if (!x_f32 && ld % 8 == 0 && C <= 256 && ((uintptr_t)x & 15) == 0)
+    hipLaunchKernelGGL(colsum_part_vec_kernel, dim3(P), dim3(kThreads), 0, stream, (const bf16*)x,
+                       R, C, ld, rpp, partial);
+  else if (x_f32)
     hipLaunchKernelGGL(colsum_part_kernel<float>, g1, dim3(kThreads), 0, stream, (const float*)x,
                        R, C, ld, rpp, partial);
   else
     hipLaunchKernelGGL(colsum_part_kernel<bf16>, g1, dim3(kThreads), 0, stream, (const bf16*)x, R,
                        C, ld, rpp, partial);
-  hipLaunchKernelGGL(colsum_fin_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0,
-                     stream, (const float*)partial, P, C, out0, c0, out1);
+  hipLaunchKernelGGL(colsum_fin_kernel, dim3(C), dim3(kThreads), 0, stream, (const float*)partial,
+                     P, C, out0, c0, out1);
   return (int)hipGetLastError();
 }
 

@@ -1,5 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-bash tools/gpu_suite.sh s1 || exit $?
-timeout -k 10 300 python tools/aten_audit.py --arch impala_flat --size 16 --batch 2048 > gpurun_out/audit_i.log 2>&1 || exit $?
-tail -12 gpurun_out/audit_i.log
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_gridconv.py tests/test_gpu_gridnet.py > gpurun_out/gt.log 2>&1 || exit $?
+tail -1 gpurun_out/gt.log
+timeout -k 10 300 python bench.py --arch gridnet --size 10 --steps 10 --warmup 3 > gpurun_out/c2e.log 2>&1 || exit $?
+tail -1 gpurun_out/c2e.log | cut -c1-400
+bash tools/prof.sh prof_c2e bench.py --arch gridnet --size 10 --steps 4 --warmup 2 || exit $?
+grep -c "at::native\|Cijk" gpurun_out/prof_c2e_summary.md
