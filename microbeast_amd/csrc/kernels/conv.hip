@@ -1148,6 +1148,19 @@ int resident_blocks(const void* kfn, size_t sm) {
   return r;
 }
 
+// Forward / dgrad grids: resident_blocks x g_fwd_mult workgroups. mult = 1 is persistent
+// (each workgroup walks many image groups); larger values make workgroups retire while the
+// kernel runs, so a concurrently queued high-priority kernel (the acting policy step) gets
+// CU slots without waiting for the whole learner kernel. MBK_FWD_GRID_MULT overrides.
+int fwd_grid(int ngroups, const void* kfn, size_t sm) {
+  static const int mult = [] {
+    const char* e = getenv("MBK_FWD_GRID_MULT");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  const long r = (long)resident_blocks(kfn, sm) * mult;
+  return (int)std::max(1L, std::min((long)ngroups, r));
+}
+
 // The kernels map a tile-local pixel index m in [0, imgs*H*W) to (image, y, x) with float
 // reciprocals ((m + 0.5) * (1/HW)): exact while imgs*H*W < 2^22 (the product's rounding
 // error stays below the 0.5/HW distance to the next integer). LDS capacity keeps today's
@@ -1181,7 +1194,7 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     auto kfn = fp8 ? conv_fwd_kernel<CI, CO, B, true> : conv_fwd_kernel<CI, CO, B, false>;  \
     if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
-    const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));              \
+    const int grid = fwd_grid(ngroups, (const void*)kfn, sm);                               \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);                     \
   } while (0)
   if (unpool) {  // dgrad of a pooled stage conv (cin = that conv's cout)
@@ -1191,7 +1204,7 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     if (!kfn) return (int)hipErrorInvalidValue;
     if (sm > 64 * 1024)
       hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    const int grid = std::min(ngroups, resident_blocks((const void*)kfn, sm));
+    const int grid = fwd_grid(ngroups, (const void*)kfn, sm);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
     return (int)hipGetLastError();
   }
@@ -1199,8 +1212,7 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
       !relu_in) {
     const size_t sm0 = pool ? (size_t)kRowImgs * H * 16 * (16 + 4) * 2 : 0;
     if (sm0 > 160 * 1024) return (int)hipErrorInvalidValue;
-    const int grid = std::min((N + kRowImgs - 1) / kRowImgs,
-                              resident_blocks((const void*)conv0_row_kernel, sm0));
+    const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)conv0_row_kernel, sm0);
     hipLaunchKernelGGL(conv0_row_kernel, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();
   }
@@ -1267,7 +1279,11 @@ extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H
                                : (const void*)conv_wgrad_kernel<CI, CO, B>, sm)
   WGRAD_DISPATCH(Q)
 #undef Q
-  return std::max(1, std::min(nrounds, res));
+  static const int mult = [] {  // see fwd_grid: more, shorter-lived workgroups (+ partials)
+    const char* e = getenv("MBK_WGRAD_GRID_MULT");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  return (int)std::max(1L, std::min((long)nrounds, (long)res * mult));
 }
 
 // dy == nullptr: pool-fused mode, dY = max_pool2d backward of dp through pidx

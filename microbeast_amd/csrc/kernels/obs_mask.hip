@@ -95,32 +95,51 @@ __device__ __forceinline__ void cell_mask(const uint16_t* cs, int c, int H, int 
   if (any_att) setb(w, kSegOff[0] + A_ATTACK);
 }
 
-// One WAVE per env, kEnvsPerWG envs per workgroup, persistent over env groups (grid sized
+// One WAVE per env, EPW envs per workgroup, persistent over env groups (grid sized
 // to the device). A lane owns Q = ceil(S/64) consecutive cells, so an env's obs words and
 // mask triples leave as contiguous 16-byte vector stores (Q = 4 at 16x16: one uint4 of obs
 // and three uint4 of mask per lane) and the inactive-output zeroing is a few wave-wide
 // 16-byte stores. The previous form (one 256-thread workgroup per env, one cell per thread,
 // 3 scalar mask stores per cell) ran at ~0.4-0.6 TB/s: 8192 short workgroups per step, each
 // a global-load -> barrier -> store chain (profiles/16: ~99 us per 8192-env step).
+//
+// BUCKET: the (env, cell) pairs are first counted per cell in LDS (LDS atomics) and listed in
+// LDS; after the workgroup's last env group, ONE global atomicAdd per (workgroup, active
+// cell) reserves the workgroup's range of that cell's bucket. Unit start positions are the
+// same in every env, so direct per-pair global atomics all hit a handful of counters
+// (8192-way contention on the base cells: the kernel ran at 109 us, profile 20).
 constexpr int kEnvsPerWG = 4;
+constexpr int kBucketEPW = 8;          // envs per pass of the bucketing variant (512 threads)
+constexpr int kBucketGroupsPerWG = 2;  // passes per workgroup before its bucket flush
+constexpr int kMaxLocalPairs = 2048;   // LDS pair list; overflow takes the direct atomic path
 
 template <bool BUCKET>
-__global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __restrict__ codes,
+__global__ __launch_bounds__(512) void decode_obs_mask_kernel(const uint16_t* __restrict__ codes,
                                                               const int32_t* __restrict__ res,
                                                               int E, int H, int W,
                                                               uint32_t* __restrict__ obs,
                                                               uint32_t* __restrict__ mask,
                                                               Buckets bk) {
-  extern __shared__ uint16_t smem_codes[];
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem_codes[];
+  constexpr int EPW = BUCKET ? kBucketEPW : kEnvsPerWG;
   const int S = H * W;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint16_t* cs = smem_codes + wave * S;
+  // BUCKET LDS: per-cell counts, then the pair list (cell << 19 | local slot, env)
+  int* lcnt = (int*)(smem_codes + ((EPW * S + 7) & ~7));
+  int* npairs = lcnt + S;
+  int2* pairs = (int2*)(npairs + 2);
   const int Q = (S + 63) >> 6;  // cells per lane
   const int c0 = lane * Q, c1 = min(S, c0 + Q);
   const bool vec4 = Q == 4 && (S & 3) == 0;  // 16x16: whole-lane vector stores
-  const int ngroups = (E + kEnvsPerWG - 1) / kEnvsPerWG;
+  const int ngroups = (E + EPW - 1) / EPW;
+  if (BUCKET) {
+    for (int c = threadIdx.x; c < S; c += blockDim.x) lcnt[c] = 0;
+    if (threadIdx.x == 0) *npairs = 0;
+    __syncthreads();
+  }
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {  // uniform trip count
-    const int e = grp * kEnvsPerWG + wave;
+    const int e = grp * EPW + wave;
     const bool live = e < E;
     if (live) {
       const uint16_t* ce = codes + (size_t)e * S;
@@ -146,8 +165,13 @@ __global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __
           m[0] = w[0]; m[1] = w[1]; m[2] = w[2];
         }
         if (BUCKET && (w[0] | w[1] | w[2])) {
-          const int slot = atomicAdd(&bk.cnt[c], 1);
-          bk.bucket[(size_t)c * E + slot] = e;
+          const int i = atomicAdd(npairs, 1);
+          if (i < kMaxLocalPairs) {
+            pairs[i] = make_int2((c << 19) | atomicAdd(&lcnt[c], 1), e);
+          } else {  // list full: direct global slot
+            const int slot = atomicAdd(&bk.cnt[c], 1);
+            bk.bucket[(size_t)c * E + slot] = e;
+          }
         }
       }
       if (vec4) {
@@ -174,9 +198,23 @@ __global__ __launch_bounds__(256) void decode_obs_mask_kernel(const uint16_t* __
     }
     __syncthreads();  // cs reused by the next group
   }
+  if (BUCKET) {
+    // one global reservation per active cell of this workgroup; lcnt becomes the base
+    for (int c = threadIdx.x; c < S; c += blockDim.x) {
+      const int n = lcnt[c];
+      if (n > 0) lcnt[c] = atomicAdd(&bk.cnt[c], n);
+    }
+    __syncthreads();
+    const int np = min(*npairs, kMaxLocalPairs);
+    for (int i = threadIdx.x; i < np; i += blockDim.x) {
+      const int2 pr = pairs[i];
+      const int c = pr.x >> 19, slot = pr.x & 0x7FFFF;
+      bk.bucket[(size_t)c * E + lcnt[c] + slot] = pr.y;
+    }
+  }
 }
 
-int decode_grid(int E) {
+int device_cus() {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -184,8 +222,21 @@ int decode_grid(int E) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
+  return cus;
+}
+
+int decode_grid(int E) {
   const int ngroups = (E + kEnvsPerWG - 1) / kEnvsPerWG;
-  return max(1, min(ngroups, cus * 8));  // 8 resident 256-thread workgroups per CU
+  return max(1, min(ngroups, device_cus() * 8));  // 8 resident 256-thread workgroups per CU
+}
+
+int bucket_grid(int E) {
+  const int ngroups = (E + kBucketEPW - 1) / kBucketEPW;
+  return max(1, (ngroups + kBucketGroupsPerWG - 1) / kBucketGroupsPerWG);
+}
+
+size_t bucket_smem(int S) {
+  return (size_t)((kBucketEPW * S + 7) & ~7) * 2 + (size_t)(S + 2) * 4 + (size_t)kMaxLocalPairs * 8;
 }
 
 __global__ __launch_bounds__(256) void pack_env_actions_kernel(const uint8_t* __restrict__ act,
@@ -218,8 +269,12 @@ extern "C" int mbk_decode_obs_mask_bucket(const uint16_t* codes, const int32_t* 
                                           uint8_t* action, hipStream_t stream) {
   if (n_envs <= 0) return 0;
   if (H * W > 4096) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(decode_obs_mask_kernel<true>, dim3(decode_grid(n_envs)), dim3(256),
-                     kEnvsPerWG * H * W * 2, stream, codes, res, n_envs, H, W, obs, mask,
+  const size_t sm = bucket_smem(H * W);
+  if (sm > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)decode_obs_mask_kernel<true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  hipLaunchKernelGGL(decode_obs_mask_kernel<true>, dim3(bucket_grid(n_envs)),
+                     dim3(64 * kBucketEPW), sm, stream, codes, res, n_envs, H, W, obs, mask,
                      Buckets{bucket_cnt, bucket, cell_lp, action});
   return (int)hipGetLastError();
 }

@@ -366,8 +366,19 @@ int res_grid(int N, int H, int W, int imgs) {
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
     per = 1;
+  // workgroups per CU the grid is sized for: at 2 (its occupancy) the kernel fills every
+  // CU's LDS and VGPRs, so nothing else (the acting policy step) can start until it ends
+  static const int cap = [] {
+    const char* e = getenv("MBK_RES_BWD_PER_CU");
+    return e ? std::max(1, atoi(e)) : 0;
+  }();
+  if (cap > 0) per = std::min(per, cap);
   const int nrounds = (N + imgs - 1) / imgs;
-  return std::max(1, std::min(nrounds, cus * per));
+  static const int mult = [] {  // see conv.hip fwd_grid / mbk_conv_wgrad_parts
+    const char* e = getenv("MBK_WGRAD_GRID_MULT");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  return (int)std::max(1L, std::min((long)nrounds, (long)cus * per * mult));
 }
 
 }  // namespace
@@ -533,8 +544,12 @@ extern "C" int mbk_res_fwd16(const void* p, void* u0, void* y0, void* u1, void* 
           hipSuccess || per < 1)
     per = 1;
   const int nrounds = (N + imgs - 1) / imgs;
-  hipLaunchKernelGGL(kfn, dim3(std::max(1, std::min(nrounds, cus * per))), dim3(kThreads), sm,
-                     stream, a);
+  static const int mult = [] {  // see conv.hip fwd_grid
+    const char* e = getenv("MBK_FWD_GRID_MULT");
+    return e ? std::max(1, atoi(e)) : 1;
+  }();
+  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)cus * per * mult))),
+                     dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }
 
