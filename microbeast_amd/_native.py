@@ -95,6 +95,8 @@ _SIGS = {
                        c_void_p],
     "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_trunk_tail": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_trunk_tail_fc": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_res_bwd16_parts": [c_int, c_int, c_int, c_int],
     "mbk_res_fwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,

@@ -24,6 +24,8 @@
 
 #include <algorithm>
 
+extern "C" int mbk_get_cu_budget();  // conv.hip: CUs the learner's persistent grids target
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x2 __attribute__((ext_vector_type(2)));
@@ -361,6 +363,7 @@ int res_grid(int N, int H, int W, int imgs) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
+  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
   const void* kfn = (const void*)res_bwd16_kernel<0>;  // same resources for every width
   if (sm > 64 * 1024) (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
@@ -378,7 +381,7 @@ int res_grid(int N, int H, int W, int imgs) {
     const char* e = getenv("MBK_WGRAD_GRID_MULT");
     return e ? std::max(1, atoi(e)) : 1;
   }();
-  return (int)std::max(1L, std::min((long)nrounds, (long)cus * per * mult));
+  return (int)std::max(1L, std::min((long)nrounds, (long)ncu * per * mult));
 }
 
 }  // namespace
@@ -539,6 +542,7 @@ extern "C" int mbk_res_fwd16(const void* p, void* u0, void* y0, void* u1, void* 
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
+  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
           hipSuccess || per < 1)
@@ -548,7 +552,7 @@ extern "C" int mbk_res_fwd16(const void* p, void* u0, void* y0, void* u1, void* 
     const char* e = getenv("MBK_FWD_GRID_MULT");
     return e ? std::max(1, atoi(e)) : 1;
   }();
-  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)cus * per * mult))),
+  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)ncu * per * mult))),
                      dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

@@ -286,7 +286,15 @@ __device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg
 
 struct TrunkArgs {
   const bf16* x;        // stage-0 pooled output [N][H0][W0][16]
-  bf16* y;              // trunk output [N][H2][W2][32]
+  bf16* y;              // trunk output [N][H2][W2][32] (null: not stored)
+  // fused trunk head (f_out != null): f = relu(W5 relu(y) + b5) [N][256] bf16 and the
+  // critic v = wc . f + bc [N] fp32, from the LDS-resident X2 tile (fc.hip fc_fwd's maths)
+  const bf16* w5;       // [256][H2*W2*32], columns in NHWC flatten order
+  const float* b5;
+  const float* wc;
+  const float* bc;
+  bf16* f_out;
+  float* v_out;
   const bf16* w[14];    // packed fwd weights of layers 1..14 (HipEncoder order)
   const float* b[14];
   int N, H0, W0;
@@ -302,7 +310,78 @@ __device__ __forceinline__ int tail_n16(int l) {
          tail_cout(l) * TG<32>::NCH * 4 * (tail_cin(l) == 32 ? 1 : 0);
 }
 
-template <bool LDSW>  // weights staged in LDS (double-buffered) vs read through L2
+__device__ __forceinline__ uint4 relu8(uint4 v) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    w[j] = ((w[j] & 0x8000u) ? 0u : (w[j] & 0xFFFFu)) |
+           ((w[j] & 0x80000000u) ? 0u : (w[j] & 0xFFFF0000u));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// relu -> network.5 (256 hidden) -> relu -> critic on the group's X2 tile (halo'd NHWC in
+// LDS at x2): the same MFMA tiling, K order and value reduction as fc.hip fc_fwd_kernel<256>
+// (waves 0-3 take images [0,16), waves 4-7 images [16,32) of each 32-image chunk; 4 hidden
+// blocks of 16 per wave), so f and v match the separate launch bit for bit.
+__device__ __forceinline__ void trunk_fc(const char* x2, int H2, int W2, int nimg, int img0,
+                                         const TrunkArgs& a, float* vred) {
+  constexpr int O = 256, NBW = 4, PX = TG<32>::PIXB;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int half = wave >> 2, wq = wave & 3;
+  const int I = H2 * W2 * 32, nks = H2 * W2;
+  for (int c0 = 0; c0 < nimg; c0 += 32) {
+    const int im = c0 + half * 16 + li;
+    const bool valid = im < nimg;
+    // one hidden block at a time (4 accumulators live, not 16): the head runs at the end of
+    // a 256-VGPR kernel; x fragments are re-read from LDS per block instead
+    float vpart = 0.f;
+#pragma unroll 1
+    for (int j = 0; j < NBW; ++j) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const uint4* wrow = (const uint4*)(a.w5 + (size_t)((wq * NBW + j) * 16 + li) * I) + G;
+#pragma unroll 1
+      for (int ks = 0; ks < nks; ++ks) {  // K step = one pixel's 32 channels
+        const int py = ks / W2, px = ks - py * W2;
+        Frag8 b, w;
+        b.u = make_uint4(0, 0, 0, 0);
+        if (valid)
+          b.u = relu8(*(const uint4*)(x2 + ((im * (H2 + 2) + py + 1) * (W2 + 2) + px + 1) * PX +
+                                      G * 16));
+        w.u = wrow[ks * 4];
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.v, b.v, acc, 0, 0, 0);
+      }
+      const int h0 = (wq * NBW + j) * 16 + 4 * G;
+      float hv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
+        vpart += hv[i] * a.wc[h0 + i];
+      }
+      uint32_t o[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
+               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
+      if (valid) *(uint2*)(a.f_out + (size_t)(img0 + im) * O + h0) = make_uint2(o[0], o[1]);
+    }
+    vpart += __shfl_xor(vpart, 16, 64);
+    vpart += __shfl_xor(vpart, 32, 64);
+    if (G == 0) vred[(half * 4 + wq) * 16 + li] = vpart;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+      const int hh = threadIdx.x >> 4, t = threadIdx.x & 15, r = c0 + hh * 16 + t;
+      const float* vr = vred + hh * 64;
+      if (r < nimg) a.v_out[img0 + r] = vr[t] + vr[16 + t] + vr[32 + t] + vr[48 + t] + a.bc[0];
+    }
+    __syncthreads();
+  }
+}
+
+// LDSW: weights staged in LDS (double-buffered) vs read through L2. FC: the fused trunk
+// head runs after the last conv; the next group's first weight fetch then waits until after
+// it (keeps the prefetch registers free across the head: no spills).
+template <bool LDSW, bool FC>
 __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   char* smem = trunk_smem;
   const int oR1 = 0, oR2 = a.r1_bytes;  // region offsets for conv_lds
@@ -334,7 +413,7 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
     } else {                                                                                \
       uint4 wc[kWFrag];                                                                     \
       _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];                  \
-      {                                                                                     \
+      if (!(FC && (l) == 13)) {                                                             \
         const int ln = ((l) + 1) % 14;                                                      \
         wfetch(a.w[ln], tail_cin(ln), tail_cout(ln), wnext);                                \
       }                                                                                     \
@@ -396,8 +475,12 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
       __syncthreads();
     }
 #undef TAIL_PHASE
+    if (FC) {
+      trunk_fc(R1, H2, W2, nimg, img0, a, (float*)R2);
+      wfetch(a.w[0], tail_cin(0), tail_cout(0), wnext);  // next group's layer 0
+    }
     // ---- X2 interior -> global NHWC
-    {
+    if (a.y) {
       constexpr int PX = TG<32>::PIXB;
       const int tot = nimg * H2 * W2 * 4;
       uint4* dst = (uint4*)(a.y + (size_t)img0 * H2 * W2 * 32);
@@ -424,19 +507,50 @@ size_t region_bytes(int H0, int W0, int TNI) {
 
 }  // namespace
 
+static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream);
+
 // x: stage-0 pooled activations [N][H0][W0][16] bf16; w/b: layers 1..14 of the
 // (16, 32, 32) IMPALA trunk (packed fwd weights, fp32 biases); y: [N][H2][W2][32] bf16.
 extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* const* b, int N,
                               int H0, int W0, void* y, hipStream_t stream) {
-  if (N <= 0) return 0;
-  if (H0 < 1 || W0 < 1 || H0 > 16 || W0 > 16) return (int)hipErrorInvalidValue;
-  TrunkArgs a;
+  TrunkArgs a{};
   a.x = (const bf16*)x;
   a.y = (bf16*)y;
   for (int i = 0; i < 14; ++i) {
     a.w[i] = (const bf16*)w[i];
     a.b[i] = b[i];
   }
+  return trunk_launch(a, N, H0, W0, stream);
+}
+
+// mbk_trunk_tail + the fused trunk head: f_out [N][256] bf16 = relu(W5 relu(y) + b5),
+// v_out [N] = wc . f + bc (fc.hip mbk_fc_fwd's result); y may be null (not stored).
+// w5: [256][H2*W2*32] bf16, NHWC column order.
+extern "C" int mbk_trunk_tail_fc(const void* x, const void* const* w, const float* const* b,
+                                 int N, int H0, int W0, void* y, const void* w5, const float* b5,
+                                 const float* wc, const float* bc, int hidden, void* f_out,
+                                 float* v_out, hipStream_t stream) {
+  if (hidden != 256 || !w5 || !b5 || !wc || !bc || !f_out || !v_out)
+    return (int)hipErrorInvalidValue;
+  TrunkArgs a{};
+  a.x = (const bf16*)x;
+  a.y = (bf16*)y;
+  for (int i = 0; i < 14; ++i) {
+    a.w[i] = (const bf16*)w[i];
+    a.b[i] = b[i];
+  }
+  a.w5 = (const bf16*)w5;
+  a.b5 = b5;
+  a.wc = wc;
+  a.bc = bc;
+  a.f_out = (bf16*)f_out;
+  a.v_out = v_out;
+  return trunk_launch(a, N, H0, W0, stream);
+}
+
+static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (H0 < 1 || W0 < 1 || H0 > 16 || W0 > 16) return (int)hipErrorInvalidValue;
   a.N = N;
   a.H0 = H0;
   a.W0 = W0;
@@ -456,7 +570,7 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
     const char* t = std::getenv("MBK_TRUNK_TNI");
     force_tni = t ? std::atoi(t) : 0;
   }
-  const bool ldsw = variant == 1;
+  const bool ldsw = variant == 1 && a.f_out == nullptr;  // the fused head uses the L2 variant
   const size_t wb = ldsw ? 2 * kWBufBytes : 0;
   int tni = 1;
   while (tni < kMaxTNI && 2 * region_bytes(H0, W0, tni * 2) + wb <= 160 * 1024 &&
@@ -474,7 +588,9 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
   a.r1_bytes = (int)r;
   const size_t sm = 2 * r + wb;
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  auto kfn = ldsw ? trunk_tail_kernel<true> : trunk_tail_kernel<false>;
+  const bool fc = a.f_out != nullptr;
+  auto kfn = fc ? trunk_tail_kernel<false, true>
+                : ldsw ? trunk_tail_kernel<true, false> : trunk_tail_kernel<false, false>;
   if (sm > 64 * 1024)
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
@@ -482,10 +598,9 @@ extern "C" int mbk_trunk_tail(const void* x, const void* const* w, const float* 
           hipSuccess || per < 1)
     per = 1;
   const int ngroups = (N + tni - 1) / tni;
-  // persistent grid sized for the CUs this stream may use (mbk_set_cu_budget: CU-partitioned
-  // policy / learner streams), else the whole device
-  const int budget = mbk_get_cu_budget();
-  const int grid = std::min(ngroups, (budget > 0 ? std::min(budget, cus) : cus) * per);
+  // persistent grid over the whole device (the CU budget, mbk_set_cu_budget, sizes the
+  // LEARNER's persistent grids; this is the acting kernel)
+  const int grid = std::min(ngroups, cus * per);
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

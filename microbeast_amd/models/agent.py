@@ -20,6 +20,7 @@ or the reference dense float (N, h, w, 27) layout.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -30,9 +31,16 @@ from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.head import SparseHead, sparse_sample, sparse_score
 from ..ops.linear import linear, nhwc_weight
 from ..ops.obs import bits_to_planes, dense_to_bits
+from ..ops.gridconv import map_gather
 from ..ops.tail import TailMaps, impala_tail
 
 HIP_CHANNELS = (16, 32)  # conv widths the HIP trunk kernels are instantiated for
+
+
+# network.5 + critic fused into the acting trunk kernel (trunk.hip, MBK_TRUNK_HEAD=1) vs the
+# separate fc.hip launch (default): measured 0.208 vs 0.200 ms per 8192-env policy step in
+# isolation and no gain under the learner (the fused variant spills 8 VGPRs)
+_TRUNK_HEAD = os.environ.get("MBK_TRUNK_HEAD", "0") == "1"
 
 
 def layer_init(layer: nn.Module, std: float = math.sqrt(2), bias_const: float = 0.0) -> nn.Module:
@@ -171,9 +179,15 @@ class Agent(nn.Module):
         relu -> network.5 -> relu -> critic (fc.hip). Returns (f bf16 [N,256], value fp32)."""
         from .. import _native as N
         n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
-        y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
-                   encoder_params(self.network, len(self.channels)), False, prepacked=True)
         fc = self.network[len(self.channels) + 2]
+        head = None
+        if fc.out_features == 256 and not self._hip_enc.fp8 and _TRUNK_HEAD:  # in trunk_tail
+            head = (self._fc_cache["w5"], fc.bias, self.critic.weight, self.critic.bias)
+        y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
+                   encoder_params(self.network, len(self.channels)), False, prepacked=True,
+                   head=head)
+        if isinstance(y, tuple):
+            return y
         I = y[0].numel()
         if fc.out_features not in (128, 256, 512):  # no fused kernel instance: cached GEMMs
             c = self._fc_cache
@@ -213,7 +227,9 @@ class Agent(nn.Module):
             _, ho, wo, c = y.shape
             f = F.relu(y.reshape(n, -1))
             f = linear(f, self.network[nseq + 2], nhwc=(c, ho, wo),
-                       cached=(self._fc_cache["w5"], self._fc_cache["b5"]) if pre else None)
+                       cached=(self._fc_cache["w5"],
+                               self._fc_cache.get("b5", self.network[nseq + 2].bias.detach()))
+                       if pre else None)
             return F.relu(f)
         x = self._planes(obs)
         with self._autocast(x):
@@ -255,8 +271,21 @@ class Agent(nn.Module):
         self._head(dev).pack(self.actor.weight, self.actor.bias, with_t=False)
         nseq = len(self.channels)
         fc = self.network[nseq + 2]
+        if fc.out_features == 256:
+            # the fused trunk head (trunk.hip) reads fp32 b5 / wc / bc itself: only W5's
+            # NHWC bf16 operand is derived, by one index-map gather (no ATen copies)
+            key = (fc.out_features, enc.out_c) + tuple(enc.out_hw)
+            if (self._tail_maps is None or self._tail_maps.key != key
+                    or self._tail_maps.device != dev):
+                self._tail_maps = TailMaps(*key, dev)
+            if self._fc_cache is None or "w5" not in self._fc_cache:
+                self._fc_cache = {"w5": torch.empty(self._tail_maps.fwd.shape,
+                                                    dtype=torch.bfloat16, device=dev)}
+            map_gather([(fc.weight.detach(), self._fc_cache["w5"], self._tail_maps.fwd)])
+            self._prepacked = True
+            return
         w5 = nhwc_weight(fc.weight.detach(), (enc.out_c,) + tuple(enc.out_hw))
-        if self._fc_cache is None:
+        if self._fc_cache is None or "b5" not in self._fc_cache:
             self._fc_cache = {"w5": torch.empty(w5.shape, dtype=torch.bfloat16, device=dev),
                               "b5": torch.empty(fc.bias.shape, dtype=torch.bfloat16, device=dev),
                               "wc": torch.empty(self.critic.weight.shape, dtype=torch.bfloat16,

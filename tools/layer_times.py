@@ -40,7 +40,7 @@ def main(argv=None):
     for i, (s, e, k) in enumerate(seg):
         d = (e - s) / 1e3
         tot += d
-        name = k.split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
+        name = k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         lines.append(f"| {i} | {(s - t0) / 1e3:.1f} | {d:.1f} | `{name[:90]}` |")
     span = (seg[-1][1] - t0) / 1e3
     lines.append("")
