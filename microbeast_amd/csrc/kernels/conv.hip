@@ -492,13 +492,35 @@ __device__ __forceinline__ bf16x8 shl_px(const Frag8& f) {
   return o.v;
 }
 
+// Bit-plane expansion through a 256-entry LDS table (byte -> 8 bf16, 4 KB) instead of ~24
+// VALU bit ops per row, and the kx = 0 / 2 taps from DPP-shifted 32-bit BIT words (2 DPP
+// per row instead of 8 on the expanded fragments, each needing a zeroed destination): the
+// kernel was VALU-bound (72 % VALU busy, 15 VALU per MFMA, counters in profile 20).
+// HT > 0: compile-time map height, all HT input rows of an image loaded in one batch;
+// HT == 0: runtime height, rows loaded one pair ahead.
+constexpr int kLutBytes = 256 * 16;
+
+__device__ __forceinline__ uint32_t dpp_shr1_b(uint32_t v) {  // lane x <- lane x-1 (x=0: 0)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x111, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t dpp_shl1_b(uint32_t v) {  // lane x <- lane x+1 (x=15: 0)
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xF, 0xF, true);
+}
+
+struct Row3 {  // one input row's bit words for pixels x-1 (l), x (c), x+1 (h) of lane x
+  uint32_t l, c, h;
+};
+
+template <int HT>
 __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int COUT = 16, OSTR = COUT + 4, W = 16;
-  const int H = a.H, HW = H * W;
+  const int H = HT > 0 ? HT : a.H, HW = H * W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  bf16* otile = (bf16*)smem;  // [kRowImgs * HW][OSTR] bf16 conv outputs (pool mode)
+  uint4* lut = (uint4*)smem;                 // [256] byte -> 8 bf16 planes
+  bf16* otile = (bf16*)(smem + kLutBytes);   // [kRowImgs * HW][OSTR] conv outputs (pool mode)
+  for (int i = tid; i < 256; i += kThreads) lut[i] = expand_bits8((uint32_t)i);
   Frag8 bw[9];                // A fragments: w[co = li][tap][8g .. 8g+7]
   {
     const uint4* wp = (const uint4*)(a.w + (size_t)li * 9 * 32 + g * 8);
@@ -509,62 +531,98 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) bias_v[i] = a.bias ? a.bias[4 * g + i] : 0.f;
   const int ngroups = (a.N + kRowImgs - 1) / kRowImgs;
+  __syncthreads();  // LUT ready
+  const int sh = 8 * g;
+  auto row = [&](uint32_t bits) {  // bytes this lane's 8 planes (group g) take from the LUT
+    Row3 r;
+    r.c = ((bits >> sh) & 0xFFu) * 16u;
+    r.l = ((dpp_shr1_b(bits) >> sh) & 0xFFu) * 16u;
+    r.h = ((dpp_shl1_b(bits) >> sh) & 0xFFu) * 16u;
+    return r;
+  };
+  const char* lutb = (const char*)lut;
+  // one output row pair (y, y+1) from input rows y-1 .. y+2; each (row, kx) fragment is
+  // expanded once (one LDS read) and feeds both rows' MFMA chains in their tap order
+  auto row_pair = [&](const Row3 r[4], int y, int im, int img0) {
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        Frag8 f;
+        f.u = *(const uint4*)(lutb + (kx == 0 ? r[q].l : kx == 1 ? r[q].c : r[q].h));
+        if (q < 3) acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * q + kx].v, f.v, acc0, 0, 0, 0);
+        if (q > 0) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * (q - 1) + kx].v, f.v, acc1, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int yy = y + h;
+      if (yy >= H) break;
+      const f32x4& acc = h ? acc1 : acc0;
+      uint32_t o[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j] * 1.f + bias_v[2 * j])) |
+               ((uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j + 1] * 1.f + bias_v[2 * j + 1]))
+                << 16);
+      const int m = yy * W + li;
+      const size_t gi = ((size_t)(img0 + im) * HW + m) * COUT + 4 * g;
+      if (a.pool) {
+        *(uint2*)(otile + (im * HW + m) * OSTR + 4 * g) = make_uint2(o[0], o[1]);
+        if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
+      } else {
+        *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
+      }
+    }
+  };
+  constexpr int NR = HT > 0 ? HT : 1;
+  uint32_t rows[NR];  // HT: this wave's image, all rows (lane: column li)
+  auto load_rows = [&](int grp, uint32_t* dst) {
+    const int img = grp * kRowImgs + wave;
+    const bool ok = grp < ngroups && img < a.N;
+    const uint32_t* xb = (const uint32_t*)a.x + (size_t)(ok ? img : 0) * HW + li;
+#pragma unroll
+    for (int y = 0; y < NR; ++y) dst[y] = ok ? xb[y * W] : 0u;
+  };
+  const Row3 zero3 = {0u, 0u, 0u};  // LUT entry 0 = all-zero planes
 
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * kRowImgs;
     const int nimg = min(kRowImgs, a.N - img0);
-    if (wave < nimg) {
+    if (HT > 0) {
+      load_rows(grp, rows);
+      if (wave < nimg) {
+        Row3 r[4];
+        r[0] = zero3;
+        r[1] = row(rows[0]);
+        r[2] = NR > 1 ? row(rows[1 % NR]) : zero3;
+        r[3] = NR > 2 ? row(rows[2 % NR]) : zero3;
+#pragma unroll
+        for (int y = 0; y < NR; y += 2) {
+          row_pair(r, y, wave, img0);
+          r[0] = r[2];
+          r[1] = r[3];
+          r[2] = y + 3 < NR ? row(rows[(y + 3) % NR]) : zero3;
+          r[3] = y + 4 < NR ? row(rows[(y + 4) % NR]) : zero3;
+        }
+      }
+    } else if (wave < nimg) {
       const int im = wave;
       const uint32_t* xb = (const uint32_t*)a.x + (size_t)(img0 + im) * HW + li;
-      auto row = [&](uint32_t bits) {
-        Frag8 f;
-        f.u = expand_bits8(bits >> (8 * g));
-        return f;
-      };
-      Frag8 r[4];  // expanded input rows y-1, y, y+1, y+2 (zero outside the image)
-      r[0].u = make_uint4(0, 0, 0, 0);
+      Row3 r[4];  // expanded input rows y-1, y, y+1, y+2 (zero outside the image)
+      r[0] = zero3;
       r[1] = row(xb[0]);
-      r[2] = row(H > 1 ? xb[W] : 0u);
-      r[3] = row(H > 2 ? xb[2 * W] : 0u);
+      r[2] = H > 1 ? row(xb[W]) : zero3;
+      r[3] = H > 2 ? row(xb[2 * W]) : zero3;
       for (int y = 0; y < H; y += 2) {
         const uint32_t n0 = y + 3 < H ? xb[(y + 3) * W] : 0u;  // next iteration's rows
         const uint32_t n1 = y + 4 < H ? xb[(y + 4) * W] : 0u;
-        f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const bf16x8 l0 = shr_px(r[ky]), l1 = shr_px(r[ky + 1]);
-          const bf16x8 h0 = shl_px(r[ky]), h1 = shl_px(r[ky + 1]);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky].v, l0, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky].v, l1, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 1].v, r[ky].v, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 1].v, r[ky + 1].v, acc1, 0, 0, 0);
-          acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 2].v, h0, acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * ky + 2].v, h1, acc1, 0, 0, 0);
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int yy = y + h;
-          if (yy >= H) break;
-          const f32x4& acc = h ? acc1 : acc0;
-          uint32_t o[2];
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j] * 1.f + bias_v[2 * j])) |
-                   ((uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j + 1] * 1.f + bias_v[2 * j + 1]))
-                    << 16);
-          const int m = yy * W + li;
-          const size_t gi = ((size_t)(img0 + im) * HW + m) * COUT + 4 * g;
-          if (a.pool) {
-            *(uint2*)(otile + (im * HW + m) * OSTR + 4 * g) = make_uint2(o[0], o[1]);
-            if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
-          } else {
-            *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
-          }
-        }
+        row_pair(r, y, im, img0);
         r[0] = r[2];
         r[1] = r[3];
-        r[2] = row(n0);
-        r[3] = row(n1);
+        r[2] = y + 3 < H ? row(n0) : zero3;
+        r[3] = y + 4 < H ? row(n1) : zero3;
       }
     }
     if (a.pool) {
@@ -1210,10 +1268,15 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
   }
   if (in_bits && cout == 16 && W == 16 && !fp8 && g_conv0_row && !add && !mask_src &&
       !relu_in) {
-    const size_t sm0 = pool ? (size_t)kRowImgs * H * 16 * (16 + 4) * 2 : 0;
+    const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * 16 * (16 + 4) * 2 : 0);
     if (sm0 > 160 * 1024) return (int)hipErrorInvalidValue;
-    const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)conv0_row_kernel, sm0);
-    hipLaunchKernelGGL(conv0_row_kernel, dim3(grid), dim3(kThreads), sm0, stream, a);
+    static const bool batch_rows = [] {  // A/B knob: MBK_CONV0_BATCH_ROWS=0 -> pairwise loads
+      const char* e = getenv("MBK_CONV0_BATCH_ROWS");
+      return !(e && e[0] == '0');
+    }();
+    const auto kfn = H == 16 && batch_rows ? conv0_row_kernel<16> : conv0_row_kernel<0>;
+    const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)kfn, sm0);
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();
   }
   if (in_bits) {

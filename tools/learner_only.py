@@ -1,0 +1,62 @@
+#!/usr/bin/env python
+"""Learner updates only (synthetic engine-shaped batch), for kernel traces / counter passes
+without acting kernels in the trace.
+
+    python tools/learner_only.py --batch 8192 --T 64 --steps 2
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arch", default="impala_flat")
+    ap.add_argument("--size", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--T", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=2)
+    a = ap.parse_args()
+    import torch
+
+    from microbeast_amd.config import parse_flags
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.factory import make_model
+
+    dev = torch.device("cuda", 0)
+    flags = parse_flags(["--device", "cuda", "--arch", a.arch, "--env_size", str(a.size),
+                         "--quiet"], interactive=False)
+    torch.manual_seed(0)
+    learner = Learner(make_model(flags, dev), LearnerHParams(), dev)
+    S, T, B = a.size * a.size, a.T, a.batch
+    g = torch.Generator(device=dev).manual_seed(1)
+    # ~0.7 % active cells like the engine's rollouts: sparse legal-action masks
+    mask = torch.zeros(T + 1, B, S, 3, dtype=torch.int32, device=dev)
+    act = torch.rand(T + 1, B, S, device=dev, generator=g) < 0.007
+    mask[..., 0] = torch.where(act, torch.randint(1, 2 ** 31 - 1, (T + 1, B, S), device=dev,
+                                                  generator=g, dtype=torch.int32), 0)
+    batch = {
+        "obs": torch.randint(0, 2 ** 26, (T + 1, B, S), dtype=torch.int32, device=dev, generator=g),
+        "mask": mask,
+        "action": torch.zeros(T + 1, B, S, 7, dtype=torch.uint8, device=dev),
+        "logp": -torch.rand(T + 1, B, device=dev, generator=g),
+        "reward": torch.randn(T + 1, B, device=dev, generator=g),
+        "done": torch.zeros(T + 1, B, dtype=torch.uint8, device=dev),
+    }
+    learner.learn(batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        learner.learn(batch)
+    torch.cuda.synchronize()
+    print(f"{(time.perf_counter() - t0) / a.steps * 1e3:.3f} ms per update "
+          f"({(T * B) / 1e3:.0f}K frames)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
