@@ -18,7 +18,9 @@ __host__ __device__ constexpr int seg_off(int k) {
 }
 
 __device__ __forceinline__ bool mask_bit(const uint32_t m[3], int j) {
-  return (m[j >> 5] >> (j & 31)) & 1u;
+  // selects, not m[j >> 5]: a runtime index would put the caller's m[] in scratch memory
+  const uint32_t w = j < 32 ? m[0] : (j < 64 ? m[1] : m[2]);
+  return (w >> (j & 31)) & 1u;
 }
 
 // ------------------------------------------------------------------ Philox4x32-10

@@ -302,15 +302,18 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
 }
 
 // ------------------------------------------------------------------ backward
-// One workgroup (4 waves) per cell; 64-pair tiles.
-// LDS: Wc [80][256] bf16 | X tile [64][256] bf16 | dZ tile [64][96] bf16 | z [64][81] f32
+// One workgroup (4 waves) per 512-pair chunk of a cell; 64-pair tiles.
+// LDS: X tile [64][256] bf16 | dZ tile [64][96] bf16 | z [64][81] f32 (65 KB: two
+// workgroups per CU, so one's gather / scalar softmax-backward phase overlaps the other's
+// MFMA phases -- at one per CU (W_c staged in LDS too, 105 KB) the kernel was 80 % waits).
+// W_c (40 KB) is read through L2 like W_c^T in the dX GEMM.
 constexpr int BW_TM = 64;
-constexpr int LDS_WC = NP * KD * 2;
+constexpr int LDS_WC = 0;
 constexpr int LDS_XT = BW_TM * KD * 2;
 constexpr int LDS_DZ = BW_TM * NPT * 2;
 constexpr int LDS_Z = BW_TM * (NP + 1) * 4;
 
-__global__ __launch_bounds__(256) void head_bwd_kernel(
+__global__ __launch_bounds__(256, 2) void head_bwd_kernel(
     const bf16* __restrict__ X, const bf16* __restrict__ Wp, const bf16* __restrict__ WpT,
     const float* __restrict__ bp, const uint32_t* __restrict__ mask,
     const uint8_t* __restrict__ action, const int* __restrict__ pairs,
@@ -333,11 +336,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   const int gn = min(CHUNK, grp_start[c] + grp_count[c] - g0);
   __syncthreads();  // previous chunk's LDS reads done
 
-  // stage W_c (80 x 256 bf16 = 40 KB)
-  {
-    const uint4* src = (const uint4*)(Wp + (size_t)c * NP * KD);
-    for (int e = tid; e < NP * KD / 8; e += 256) ((uint4*)wc_l)[e] = src[e];
-  }
+  const bf16* wcg = Wp + (size_t)c * NP * KD;  // W_c rows [80][256] (L2)
   f32x4 accw[5][4];  // dW_c rows 16mb.., cols 64*wave + 16nb..
 #pragma unroll
   for (int mb = 0; mb < 5; ++mb)
@@ -361,14 +360,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       f32x4 acc[5];
 #pragma unroll
       for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
+#pragma unroll 2  // bounded: every W_c fragment of an unrolled K loop would be in flight
       for (int ks = 0; ks < KD / 32; ++ks) {
         Frag8 a;
         a.u = *(const uint4*)(xt + ((16 * wave + li) * KD + ks * 32 + 8 * G) * 2);
 #pragma unroll
         for (int nb = 0; nb < 5; ++nb) {
           Frag8 b;
-          b.u = *(const uint4*)(wc_l + ((nb * 16 + li) * KD + ks * 32 + 8 * G) * 2);
+          b.u = *(const uint4*)(wcg + (nb * 16 + li) * KD + ks * 32 + 8 * G);
           acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
         }
       }
@@ -411,30 +410,34 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       dbias += s;
     }
     __syncthreads();
-    // ---- dX_pair = dZ . Wc (wave w: rows 16w..16w+15, 256 cols; K = 96)
+    // ---- dX_pair = dZ . Wc (wave w: rows 16w..16w+15, 256 cols; K = 96), in two halves of
+    // 128 columns (8 accumulators + 8 fragments in flight instead of 16 + 48)
     {
-      f32x4 acc[16];
-#pragma unroll
-      for (int nb = 0; nb < 16; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
       const bf16* wt = WpT + (size_t)c * KD * NPT;
+#pragma unroll 1
+      for (int hc = 0; hc < 2; ++hc) {
+        f32x4 acc[8];
 #pragma unroll
-      for (int ks = 0; ks < NPT / 32; ++ks) {
-        Frag8 a;
-        a.u = *(const uint4*)(dzt + ((16 * wave + li) * NPT + ks * 32 + 8 * G) * 2);
+        for (int nb = 0; nb < 8; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+        for (int ks = 0; ks < NPT / 32; ++ks) {
+          Frag8 a;
+          a.u = *(const uint4*)(dzt + ((16 * wave + li) * NPT + ks * 32 + 8 * G) * 2);
 #pragma unroll
-        for (int nb = 0; nb < 16; ++nb) {
-          Frag8 b;
-          b.u = *((const uint4*)(wt + (size_t)(nb * 16 + li) * NPT + ks * 32) + G);
-          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+          for (int nb = 0; nb < 8; ++nb) {
+            Frag8 b;
+            b.u = *((const uint4*)(wt + (size_t)((hc * 8 + nb) * 16 + li) * NPT + ks * 32) + G);
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+          }
         }
-      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = 16 * wave + 4 * G + i;
-        if (row < nr) {
-          float* dst = dXp + (size_t)(g0 + t0 + row) * KD;
+        for (int i = 0; i < 4; ++i) {
+          const int row = 16 * wave + 4 * G + i;
+          if (row < nr) {
+            float* dst = dXp + (size_t)(g0 + t0 + row) * KD + hc * 128;
 #pragma unroll
-          for (int nb = 0; nb < 16; ++nb) dst[nb * 16 + li] = acc[nb][i];
+            for (int nb = 0; nb < 8; ++nb) dst[nb * 16 + li] = acc[nb][i];
+          }
         }
       }
     }

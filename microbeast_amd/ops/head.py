@@ -140,7 +140,7 @@ class SparseHead:
         if db is None:
             db = torch.empty(self.S * 78, dtype=torch.float32, device=X.device)
         assert dW.is_contiguous() and db.is_contiguous() and dW.numel() == self.S * 78 * KD
-        grid = max(1, min(nch, self.fwd_grid // 2))
+        grid = max(1, min(nch, self.fwd_grid))  # two 65 KB-LDS workgroups per CU
         N.check(k.mbk_head_bwd(X.data_ptr(), self.Wp.data_ptr(), self.WpT.data_ptr(),
                                self.bp.data_ptr(), mask_bits.data_ptr(), action.data_ptr(),
                                self.pairs.data_ptr(), self.grp_start.data_ptr(),
