@@ -75,11 +75,39 @@ __global__ __launch_bounds__(256) void head_count_kernel(const uint32_t* __restr
 constexpr int CHUNK = 512;  // pairs per backward work item (heavy cells are split)
 constexpr int MAX_S = 1024; // cells per map supported by the single-block scan (32x32)
 
-// Exclusive scan in (c, b) order + per-cell groups + 16-pair unit list + CHUNK list.
-// One workgroup: a wave owns a cell at a time (lanes split its frame blocks), then a
-// block-wide scan over per-cell totals. All loops are lane-parallel.
-__global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__ cnt, int S, int nfb,
-                                                         int* __restrict__ off,
+// Per-cell frame-block scan: one workgroup per cell. off[c][b] = active pairs of cell c in
+// frame blocks < b (relative to the cell's group start; head_scatter adds grp_start[c]),
+// tot[c] = the cell's total. Block-wide scan of 256-element tiles with a carry.
+__global__ __launch_bounds__(256) void head_cell_scan_kernel(const int* __restrict__ cnt, int nfb,
+                                                             int* __restrict__ off,
+                                                             int* __restrict__ tot) {
+  __shared__ int ws[4];
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int carry = 0;
+  for (int b0 = 0; b0 < nfb; b0 += 256) {
+    const int b = b0 + tid;
+    const int x = b < nfb ? cnt[c * nfb + b] : 0;
+    int incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane == 63) ws[wave] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wave; ++w) wbase += ws[w];
+    const int total = ws[0] + ws[1] + ws[2] + ws[3];
+    if (b < nfb) off[c * nfb + b] = carry + wbase + incl - x;
+    carry += total;
+    __syncthreads();  // ws reused
+  }
+  if (tid == 0) tot[c] = carry;
+}
+
+// Exclusive scans over cells of pairs / 16-pair units / CHUNK-pair chunks -> per-cell
+// groups, the unit list and the chunk list. One workgroup (S <= 1024).
+__global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__ cell_tot, int S,
                                                          int* __restrict__ grp_start,
                                                          int* __restrict__ grp_count,
                                                          int* __restrict__ unit_cell,
@@ -88,25 +116,15 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
                                                          int* __restrict__ chunk_row,
                                                          int* __restrict__ chunk_start,
                                                          int* __restrict__ totals /* [3] */) {
-  __shared__ int tot[MAX_S], ust[MAX_S], cst[MAX_S];
+  __shared__ int ust[MAX_S], cst[MAX_S], gst[MAX_S];
+  __shared__ int sv[1024], su[1024], sq[1024];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  // phase 1: per-cell totals
-  for (int c = wave; c < S; c += nw) {
-    int n = 0;
-    for (int b = lane; b < nfb; b += 64) n += cnt[c * nfb + b];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-    if (lane == 0) tot[c] = n;
-  }
-  __syncthreads();
-  // phase 2: exclusive scans of pairs, 16-pair units and chunks over cells
   int v = 0, u = 0, q = 0;
   if (tid < S) {
-    v = tot[tid];
+    v = cell_tot[tid];
     u = (v + 15) / 16;
     q = (v + CHUNK - 1) / CHUNK;
   }
-  __shared__ int sv[1024], su[1024], sq[1024];
   sv[tid] = v; su[tid] = u; sq[tid] = q;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {
@@ -121,9 +139,9 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
     grp_start[tid] = gs;
     grp_count[tid] = v;
     chunk_start[tid] = sq[tid] - q;
-    tot[tid] = gs;            // reuse: group start
-    ust[tid] = su[tid] - u;   // unit start
-    cst[tid] = sq[tid] - q;   // chunk start
+    gst[tid] = gs;
+    ust[tid] = su[tid] - u;
+    cst[tid] = sq[tid] - q;
   }
   if (tid == 1023) {
     totals[0] = sv[1023];
@@ -131,22 +149,8 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
     totals[2] = sq[1023];
   }
   __syncthreads();
-  // phase 3: per-cell frame-block offsets (wave scan with carry) + unit / chunk lists
-  for (int c = wave; c < S; c += nw) {
-    int carry = tot[c];
-    for (int b0 = 0; b0 < nfb; b0 += 64) {
-      const int b = b0 + lane;
-      const int x = b < nfb ? cnt[c * nfb + b] : 0;
-      int incl = x;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      if (b < nfb) off[c * nfb + b] = carry + incl - x;
-      carry += __shfl(incl, 63, 64);
-    }
-    const int gs = tot[c], n = sv[c] - gs;  // inclusive scan - start (LDS, no global re-read)
+  for (int c = wave; c < S; c += nw) {  // unit / chunk lists, lane-parallel per cell
+    const int gs = gst[c], n = sv[c] - gs;
     for (int r = lane * 16; r < n; r += 64 * 16) {
       const int k = ust[c] + r / 16;
       unit_cell[k] = c;
@@ -163,13 +167,14 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
 // pairs[] (frame ids, grouped by cell), pidx[f][c]; zero outputs of inactive cells
 __global__ __launch_bounds__(256) void head_scatter_kernel(
     const uint32_t* __restrict__ mask, int F, int S, int FB, const int* __restrict__ off,
+    const int* __restrict__ grp_start,
     int* __restrict__ pairs, int* __restrict__ pidx, uint8_t* __restrict__ action_zero,
     float* __restrict__ cell_lp, float* __restrict__ cell_ent) {
   const int b = blockIdx.x, nfb = gridDim.x;
   const int c = blockIdx.y * 256 + threadIdx.x;
   if (c >= S) return;
   const int f0 = b * FB, f1 = min(F, f0 + FB);
-  int pos = off[c * nfb + b];
+  int pos = grp_start[c] + off[c * nfb + b];
   for (int f = f0; f < f1; ++f) {
     const size_t fc = (size_t)f * S + c;
     if (active3(mask + fc * 3)) {
@@ -233,7 +238,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     int sample, const int* __restrict__ pairs, const int* __restrict__ unit_cell,
     const int* __restrict__ unit_row, const int* __restrict__ grp_start,
     const int* __restrict__ grp_count, const int* __restrict__ totals, int S,
-    float* __restrict__ cell_lp, float* __restrict__ cell_ent) {
+    float* __restrict__ cell_lp, float* __restrict__ cell_ent, int pair_out) {
   __shared__ float zs[4][16][NP + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
@@ -294,10 +299,54 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
 #pragma unroll
         for (int k = 0; k < kComps; ++k) action[fc * kComps + k] = a[k];
       }
-      cell_lp[fc] = lp;
-      if (cell_ent) cell_ent[fc] = ent;
+      // pair_out: results indexed by pair (the learner's scoring: per-frame sums come from
+      // head_pair_rowsum over pidx, so inactive cells are never written or read)
+      const size_t o = pair_out ? (size_t)r : fc;
+      cell_lp[o] = lp;
+      if (cell_ent) cell_ent[o] = ent;
     }
     __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// logp[f] = sum over f's active cells of the pair log-probs (ent likewise): one wave per
+// frame walking pidx[f][:] (4 B per cell instead of reading dense per-cell outputs that
+// head_scatter had to zero), fixed-order butterfly reduction (deterministic)
+__global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __restrict__ pidx, int F,
+                                                               int S, const float* __restrict__ plp,
+                                                               const float* __restrict__ pent,
+                                                               float* __restrict__ logp,
+                                                               float* __restrict__ ent) {
+  const int lane = threadIdx.x & 63;
+  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (f >= F) return;
+  float a = 0.f, b = 0.f;
+  const int* pr = pidx + (size_t)f * S;
+  auto add = [&](int p) {
+    if (p >= 0) {
+      a += plp[p];
+      if (pent) b += pent[p];
+    }
+  };
+  if ((S & 3) == 0) {  // 16-byte loads: 4 cells per lane per pass
+    for (int c = 4 * lane; c < S; c += 256) {
+      const int4 q = *(const int4*)(pr + c);
+      add(q.x);
+      add(q.y);
+      add(q.z);
+      add(q.w);
+    }
+  } else {
+    for (int c = lane; c < S; c += 64) add(pr[c]);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+  }
+  if (lane == 0) {
+    logp[f] = a;
+    if (ent) ent[f] = b;
   }
 }
 
@@ -573,11 +622,13 @@ extern "C" int mbk_head_compact(const uint32_t* mask, int F, int S, int* cnt, in
   const int nfb = (F + FB - 1) / FB;
   dim3 g1(nfb, (S + 255) / 256);
   hipLaunchKernelGGL(head_count_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, cnt);
-  hipLaunchKernelGGL(head_scan_kernel, dim3(1), dim3(1024), 0, stream, cnt, S, nfb, off,
-                     grp_start, grp_count, unit_cell, unit_row, chunk_cell, chunk_row, chunk_start,
-                     totals);
-  hipLaunchKernelGGL(head_scatter_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, off, pairs,
-                     pidx, action_zero, cell_lp, cell_ent);
+  // per-cell totals go to grp_count (overwritten with the same values by the scan)
+  hipLaunchKernelGGL(head_cell_scan_kernel, dim3(S), dim3(256), 0, stream, cnt, nfb, off,
+                     grp_count);
+  hipLaunchKernelGGL(head_scan_kernel, dim3(1), dim3(1024), 0, stream, grp_count, S, grp_start,
+                     grp_count, unit_cell, unit_row, chunk_cell, chunk_row, chunk_start, totals);
+  hipLaunchKernelGGL(head_scatter_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, off,
+                     grp_start, pairs, pidx, action_zero, cell_lp, cell_ent);
   return (int)hipGetLastError();
 }
 
@@ -593,10 +644,19 @@ extern "C" int mbk_head_fwd(const void* X, const void* Wp, const float* bp, cons
                             uint8_t* action, const uint64_t* rng, int sample, const int* pairs,
                             const int* unit_cell, const int* unit_row, const int* grp_start,
                             const int* grp_count, const int* totals, int S, int grid,
-                            float* cell_lp, float* cell_ent, hipStream_t stream) {
+                            float* cell_lp, float* cell_ent, int pair_out, hipStream_t stream) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const bf16*)X,
                      (const bf16*)Wp, bp, mask, action, rng, sample, pairs, unit_cell, unit_row,
-                     grp_start, grp_count, totals, S, cell_lp, cell_ent);
+                     grp_start, grp_count, totals, S, cell_lp, cell_ent, pair_out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_head_pair_rowsum(const int* pidx, int F, int S, const float* plp,
+                                    const float* pent, float* logp, float* ent,
+                                    hipStream_t stream) {
+  if (F <= 0) return 0;
+  hipLaunchKernelGGL(head_pair_rowsum_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, pidx, F, S,
+                     plp, pent, logp, ent);
   return (int)hipGetLastError();
 }
 

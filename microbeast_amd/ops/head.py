@@ -76,7 +76,8 @@ class SparseHead:
                                self.bucket.data_ptr(), self.unit_cell.data_ptr(),
                                self.unit_row.data_ptr(), self.grp_start.data_ptr(),
                                self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
-                               self.fwd_grid, self.cell_lp.data_ptr(), None, st), "head_fwd")
+                               self.fwd_grid, self.cell_lp.data_ptr(), None, 0, st),
+                "head_fwd")
         N.check(k.mbk_row_sum_rng(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
                                   rng.data_ptr(), st), "row_sum_rng")
         return logp_out
@@ -87,15 +88,19 @@ class SparseHead:
                                           self.WpT.data_ptr() if with_t else None,
                                           N.stream_ptr()), "head_pack")
 
-    def compact(self, mask_bits: torch.Tensor, F: int, action_zero: torch.Tensor | None):
+    def compact(self, mask_bits: torch.Tensor, F: int, action_zero: torch.Tensor | None,
+                dense_out: bool = True):
+        """dense_out: zero the per-cell log-prob / entropy of inactive cells (sampling);
+        scoring keeps pair-indexed outputs and sums them through pidx instead."""
         self._ensure(F)
         N.check(N.kernels().mbk_head_compact(
             mask_bits.data_ptr(), F, self.S, self.cnt.data_ptr(), self.off.data_ptr(),
             self.grp_start.data_ptr(), self.grp_count.data_ptr(), self.unit_cell.data_ptr(),
             self.unit_row.data_ptr(), self.chunk_cell.data_ptr(), self.chunk_row.data_ptr(),
             self.chunk_start.data_ptr(), self.totals.data_ptr(), self.pairs.data_ptr(),
-            self.pidx.data_ptr(), N.ptr(action_zero), self.cell_lp.data_ptr(),
-            self.cell_ent.data_ptr(), N.stream_ptr()), "head_compact")
+            self.pidx.data_ptr(), N.ptr(action_zero),
+            self.cell_lp.data_ptr() if dense_out else None,
+            self.cell_ent.data_ptr() if dense_out else None, N.stream_ptr()), "head_compact")
 
     def forward(self, X: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor,
                 sample: bool, rng: torch.Tensor | None, logp_out: torch.Tensor | None = None,
@@ -104,20 +109,31 @@ class SparseHead:
         F = X.shape[0]
         k = N.kernels()
         st = N.stream_ptr()
-        self.compact(mask_bits, F, action if sample else None)
+        pair_out = not sample  # scoring: pair-indexed outputs, summed per frame through pidx
+        self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out)
         N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
                                mask_bits.data_ptr(), action.data_ptr(), N.ptr(rng), int(sample),
                                self.pairs.data_ptr(), self.unit_cell.data_ptr(),
                                self.unit_row.data_ptr(), self.grp_start.data_ptr(),
                                self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
                                self.fwd_grid, self.cell_lp.data_ptr(),
-                               self.cell_ent.data_ptr() if want_ent else None, st), "head_fwd")
+                               self.cell_ent.data_ptr() if want_ent else None, int(pair_out),
+                               st), "head_fwd")
         logp = logp_out if logp_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
-        N.check(k.mbk_row_sum(self.cell_lp.data_ptr(), F, self.S, logp.data_ptr(), st), "row_sum")
         ent = None
         if want_ent:
             ent = ent_out if ent_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
-            N.check(k.mbk_row_sum(self.cell_ent.data_ptr(), F, self.S, ent.data_ptr(), st), "row_sum")
+        if pair_out:
+            N.check(k.mbk_head_pair_rowsum(self.pidx.data_ptr(), F, self.S,
+                                           self.cell_lp.data_ptr(),
+                                           self.cell_ent.data_ptr() if want_ent else None,
+                                           logp.data_ptr(), N.ptr(ent), st), "head_pair_rowsum")
+        else:
+            N.check(k.mbk_row_sum(self.cell_lp.data_ptr(), F, self.S, logp.data_ptr(), st),
+                    "row_sum")
+            if want_ent:
+                N.check(k.mbk_row_sum(self.cell_ent.data_ptr(), F, self.S, ent.data_ptr(), st),
+                        "row_sum")
         if sample:
             N.check(k.mbk_rng_advance(rng.data_ptr(), st), "rng_advance")
         return logp, ent
