@@ -513,6 +513,142 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
   }
 }
 
+// One 32-channel residual block per launch (stages 1-2 of the IMPALA trunk):
+//   u = conv0(relu x); y = x + conv1(relu u)
+// x is staged once into a halo'd LDS tile (and serves as the residual), relu(u) stays in
+// LDS for conv1; u and y are written once (3 activation passes instead of the per-layer
+// path's 5). Both layers' weight fragments (2 x 9 K-chunks x 2 output blocks) stay in VGPRs
+// for the whole persistent launch; all four 32-channel layers would not fit. Accumulation
+// order = conv.hip's conv_fwd<32, 32> chains, so outputs are bit-identical to it.
+constexpr int C32 = 32, PIXB32 = C32 * 2 + 16, NCH32 = 9, NB32 = 2;
+
+struct ResBlk32Args {
+  const bf16* x;     // [N][H][W][32] block input (pre-relu)
+  bf16 *u, *y;       // outputs
+  const bf16* w[2];  // packed fwd weights [32][9][32] of conv0, conv1
+  const float* b[2];
+  int N, H, W, imgs;
+};
+
+template <int WC>
+__global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int tb = ((a.imgs * Hp * Wp * PIXB32) + 15) & ~15;
+  char* Tx = smem;       // x (raw): conv0's input (relu at read) and the residual
+  char* Tu = smem + tb;  // relu(u): conv1's input
+  for (int e = tid; e < 2 * tb / 16; e += kThreads) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
+  Frag8 w[2][NCH32][NB32];
+  float bv[2][NB32][4];
+#pragma unroll
+  for (int l = 0; l < 2; ++l)
+#pragma unroll
+    for (int nb = 0; nb < NB32; ++nb) {
+      const uint4* wp = (const uint4*)(a.w[l] + (size_t)(nb * 16 + li) * NCH32 * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH32; ++c) w[l][c][nb].u = wp[c * 4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[l][nb][i] = a.b[l][nb * 16 + 4 * g + i];
+    }
+  int coff[NCH32];  // K chunk c = tap c, channels 8g.. of this lane
+#pragma unroll
+  for (int c = 0; c < NCH32; ++c) coff[c] = ((c / 3) * Wp + (c % 3)) * PIXB32 + 16 * g;
+  constexpr int EPP = C32 / 8;  // uint4 per pixel
+  const int per = a.imgs * HW * EPP;
+  const int nrounds = (a.N + a.imgs - 1) / a.imgs;
+  auto lds_off = [&](int e) {
+    const int q = e & (EPP - 1), p = e / EPP;
+    const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB32 + q * 16;
+  };
+  // The next round's x is fetched into registers while this round computes (when a round
+  // is at most kPF uint4 per thread), so the global-load latency leaves the critical path.
+  constexpr int kPF = 4;
+  const bool pf_ok = per <= kPF * kThreads;
+  uint4 pf0, pf1, pf2, pf3;
+#define MBK_RB32_FETCH(RD)                                                        \
+  {                                                                               \
+    const int lim_ = min(a.imgs, a.N - (RD) * a.imgs) * HW * EPP;                 \
+    const uint4* src_ = (const uint4*)a.x + (size_t)(RD) * per + tid;             \
+    if (tid < lim_) pf0 = src_[0];                                                \
+    if (tid + kThreads < lim_) pf1 = src_[kThreads];                              \
+    if (tid + 2 * kThreads < lim_) pf2 = src_[2 * kThreads];                      \
+    if (tid + 3 * kThreads < lim_) pf3 = src_[3 * kThreads];                      \
+  }
+  if (pf_ok && (int)blockIdx.x < nrounds) MBK_RB32_FETCH((int)blockIdx.x)
+  __syncthreads();
+  for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
+    const int img0 = rd * a.imgs, nimg = min(a.imgs, a.N - img0);
+    const int lim = nimg * HW * EPP;
+    if (pf_ok) {
+      if (tid < lim) *(uint4*)(Tx + lds_off(tid)) = pf0;
+      if (tid + kThreads < lim) *(uint4*)(Tx + lds_off(tid + kThreads)) = pf1;
+      if (tid + 2 * kThreads < lim) *(uint4*)(Tx + lds_off(tid + 2 * kThreads)) = pf2;
+      if (tid + 3 * kThreads < lim) *(uint4*)(Tx + lds_off(tid + 3 * kThreads)) = pf3;
+    } else {
+      for (int e = tid; e < lim; e += kThreads)
+        *(uint4*)(Tx + lds_off(e)) = ((const uint4*)a.x)[(size_t)rd * per + e];
+    }
+    __syncthreads();
+    if (pf_ok && rd + (int)gridDim.x < nrounds) MBK_RB32_FETCH(rd + (int)gridDim.x)
+    const int M = nimg * HW, nblk = (M + 15) >> 4;
+    const size_t gpix0 = (size_t)img0 * HW;
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const char* src = l == 0 ? Tx : Tu;
+      bf16* gout = l == 0 ? a.u : a.y;
+      for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+        const int m = pb * 16 + li;
+        const bool valid = m < M;
+        const int mm = valid ? m : 0;
+        const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        const int base = (im * Hp + y) * Wp + x;
+        const char* bp = src + base * PIXB32;
+        f32x4 acc[NB32];
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH32; ++c) {
+          Frag8 av;
+          av.u = *(const uint4*)(bp + coff[c]);
+          if (l == 0) av.u = relu8(av.u);  // Tu already holds relu(u)
+#pragma unroll
+          for (int nb = 0; nb < NB32; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[l][c][nb].v, av.v, acc[nb], 0, 0, 0);
+        }
+        if (!valid) continue;
+        const int o = (base + Wp + 1) * PIXB32;
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) {
+          const int co0 = nb * 16 + 4 * g;
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bv[l][nb][i];
+          if (l == 1) {
+            const uint2 ad = *(const uint2*)(Tx + o + co0 * 2);
+            v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
+          }
+          const uint2 out = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          *(uint2*)(gout + (gpix0 + m) * C32 + co0) = out;
+          if (l == 0) *(uint2*)(Tu + o + co0 * 2) = make_uint2(relu2(out.x), relu2(out.y));
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+#undef MBK_RB32_FETCH
+
+size_t resb32_smem(int imgs, int H, int W) {
+  return 2 * (((size_t)imgs * (H + 2) * (W + 2) * PIXB32 + 15) & ~(size_t)15);
+}
+
 size_t resf_smem(int imgs, int H, int W) {
   return 2 * (((size_t)imgs * (H + 2) * (W + 2) * PIXB + 15) & ~(size_t)15);
 }
@@ -586,4 +722,39 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
   rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, 0, stream);
   if (rc) return rc;
   return mbk_wgrad_reduce(partial + lstride, nparts, C, C, C, dw0, db0, 0, stream);
+}
+
+// One 32-channel residual block's forward (see res_blk32_kernel): u = conv0(relu x),
+// y = x + conv1(relu u), bit-identical to two conv_fwd<32, 32> launches.
+extern "C" int mbk_res_blk32_fwd(const void* x, void* u, void* y, const void* const* w,
+                                 const float* const* b, int N, int H, int W, int imgs,
+                                 hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (imgs < 1 || H * W > 1024 || (int64_t)imgs * H * W >= (int64_t(1) << 22))
+    return (int)hipErrorInvalidValue;
+  const size_t sm = resb32_smem(imgs, H, W);
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  ResBlk32Args a{(const bf16*)x, (bf16*)u, (bf16*)y, {(const bf16*)w[0], (const bf16*)w[1]},
+                 {b[0], b[1]}, N, H, W, imgs};
+  auto kfn = W == 4 ? res_blk32_kernel<4> : W == 2 ? res_blk32_kernel<2>
+           : W == 8 ? res_blk32_kernel<8> : W == 3 ? res_blk32_kernel<3>
+           : W == 6 ? res_blk32_kernel<6> : res_blk32_kernel<0>;
+  if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
+          hipSuccess || per < 1)
+    per = 1;
+  const int nrounds = (N + imgs - 1) / imgs;
+  hipLaunchKernelGGL(kfn, dim3(std::max(1, std::min(nrounds, ncu * per))), dim3(kThreads), sm,
+                     stream, a);
+  return (int)hipGetLastError();
 }

@@ -124,6 +124,7 @@ class HipEncoder:
         # (resblock.hip) instead of wgrad1 / dgrad1 / wgrad0 / dgrad0 (MBK_FUSED_RES=0: off)
         self.fused_res_bwd = os.environ.get("MBK_FUSED_RES", "1") == "1"
         self.fused_res_fwd = os.environ.get("MBK_FUSED_RES_FWD", "1") == "1"
+        self.fused_res_fwd32 = os.environ.get("MBK_FUSED_RES_FWD32", "1") == "1"
         self._partial_rb = None
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
@@ -273,6 +274,21 @@ class HipEncoder:
                                           N.stream_ptr()), "res_fwd16")
         return outs
 
+    def _res_blk32(self, l0: int, x: torch.Tensor, bs: list[torch.Tensor]):
+        """One 32-channel residual block (layers l0, l0+1) in one launch (resblock.hip):
+        returns (u, y), bit-identical to two conv_fwd launches."""
+        n, H, W, C = x.shape
+        u, y = torch.empty_like(x), torch.empty_like(x)
+        base = self.packed_fwd.data_ptr()
+        wp = (ctypes.c_void_p * 2)(*[base + 2 * self.layers[l0 + j].w_off for j in range(2)])
+        bp = (ctypes.c_void_p * 2)(*[bs[l0 + j].detach().data_ptr() for j in range(2)])
+        imgs = max(1, min(16, (80 * 1024) // (2 * (H + 2) * (W + 2) * 80)))
+        N.check(N.kernels().mbk_res_blk32_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(),
+                                              ctypes.cast(wp, ctypes.c_void_p),
+                                              ctypes.cast(bp, ctypes.c_void_p), n, H, W, imgs,
+                                              N.stream_ptr()), "res_blk32_fwd")
+        return u, y
+
     def _res_bwd16(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
         """Fused backward of a 16-channel residual block y = x + conv1(relu(conv0(relu x))),
         u = conv0(relu x): returns dx; writes both layers' weight / bias gradients."""
@@ -330,6 +346,9 @@ class HipEncoder:
             p = self._fwd(L, x, bs[li].detach(), pool_idx=pidx)
             if self.fused_res_fwd and L.cout == 16 and p.is_cuda:
                 u0, y0, u1, y1 = self._res_fwd16(li, p, [b.detach() for b in bs])
+            elif self.fused_res_fwd32 and L.cout == 32 and p.is_cuda:
+                u0, y0 = self._res_blk32(li + 1, p, bs)
+                u1, y1 = self._res_blk32(li + 3, y0, bs)
             else:
                 u0 = self._fwd(self.layers[li + 1], p, bs[li + 1].detach())
                 y0 = self._fwd(self.layers[li + 2], u0, bs[li + 2].detach(), add=p)

@@ -447,3 +447,27 @@ def test_fused_res_fwd16_bit_identical(cuda, s, n):
         outs[fused] = [t.clone() for t in saved[:6]] + [y.clone()]
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 9)])
+def test_fused_res_blk32_bit_identical(cuda, s, n):
+    """resblock.hip res_blk32 (one 32-channel residual block per launch, weights of both
+    layers in registers) writes the same bits for every saved activation as the per-layer
+    conv_fwd path."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encoder_params
+    torch.manual_seed(3)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(n, s * s).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = [p.detach() for p in encoder_params(m.network, 3)]
+    outs = {}
+    for fused in (False, True):
+        enc.fused_res_fwd32 = fused
+        y, saved = enc.forward(obs, params, save=True)
+        torch.cuda.synchronize()
+        outs[fused] = [t.clone() for t in saved if torch.is_tensor(t)] + [y.clone()]
+    assert len(outs[False]) == len(outs[True])
+    for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+        assert torch.equal(a, b), i
