@@ -241,6 +241,7 @@ def main(argv=None):
                 "opponents": (f"self-play league on {args.selfplay_groups}/{args.groups} groups"
                               if args.selfplay_groups else "scripted bots"),
                 "envs_per_gpu": envs_total,
+                "env_groups": f"{args.groups} x {args.envs_per_group}",
                 "env_threads_per_gpu": threads,
                 "cpus_per_rank": len(cpus),
                 "policy_lanes": rt.n_lanes,
