@@ -89,6 +89,9 @@ _SIGS = {
                      c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p],
     "mbk_head_dx_gather": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "mbk_head_dx_value_parts": [c_int],
+    "mbk_head_dx_value": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                          c_void_p, c_void_p, c_int, c_void_p],
     "mbk_head_pack": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_decode_obs_mask": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_decode_obs_mask_bucket": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,

@@ -49,31 +49,29 @@ __device__ __forceinline__ uint4 relu8(uint4 v) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// stage rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld] matrix, zero-filled
-// (relu: the staged values are relu'd, e.g. the trunk output feeding network.5)
+// element e of the staged tile rows [r, r+R) x cols [c0, c0+W) of a row-major bf16 [N][ld]
+// matrix (16 bytes: 8 columns of one row), zero-filled outside it
 template <int W, bool VEC>
-__device__ __forceinline__ void stage(char* t, const bf16* src, int r, int N, int c0, int ld,
-                                      int tid, bool relu = false) {
+__device__ __forceinline__ uint4 stage_elem(const bf16* src, int r, int N, int c0, int ld, int e) {
   constexpr int C8 = W / 8;
-  for (int e = tid; e < R * C8; e += kThreads) {
-    const int row = e / C8, c = c0 + (e % C8) * 8, n = r + row;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (n < N) {
-      if (VEC && c + 8 <= ld) {
-        v = *(const uint4*)(src + (size_t)n * ld + c);
-      } else {
-        uint16_t h[8];
+  const int row = e / C8, c = c0 + (e % C8) * 8, n = r + row;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (n < N) {
+    if (VEC && c + 8 <= ld) {
+      v = *(const uint4*)(src + (size_t)n * ld + c);
+    } else {
+      uint16_t h[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          h[j] = c + j < ld ? __bfloat16_as_ushort(src[(size_t)n * ld + c + j]) : (uint16_t)0;
-        v = make_uint4(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,
-                       h[4] | (uint32_t)h[5] << 16, h[6] | (uint32_t)h[7] << 16);
-      }
+      for (int j = 0; j < 8; ++j)
+        h[j] = c + j < ld ? __bfloat16_as_ushort(src[(size_t)n * ld + c + j]) : (uint16_t)0;
+      v = make_uint4(h[0] | (uint32_t)h[1] << 16, h[2] | (uint32_t)h[3] << 16,
+                     h[4] | (uint32_t)h[5] << 16, h[6] | (uint32_t)h[7] << 16);
     }
-    *(uint4*)(t + e * 16) = relu ? relu8(v) : v;
   }
+  return v;
 }
-
+// tile elements per thread per stage (R rows x 64 columns / 8 per element / kThreads)
+constexpr int kSPF = R * 8 / kThreads;
 
 // Row shifts of the x operand, one per output column block ("tap"): dW[o][t*I + i] =
 // sum_n g[n][o] x[n + shift_t][i] -- the weight gradient of the shifted-row (implicit
@@ -85,21 +83,19 @@ struct XShifts {
   int relu_x;  // ntap == 1 only: dW = g^T relu(x)
 };
 
-// x tile of the shifted-row weight gradient: output column c (of ntap * I) is channel
-// c % I of tap c / I, i.e. x row n + shift[c / I]; each 8-column group lies in one tap
-__device__ __forceinline__ void stage_taps(char* t, const bf16* src, int r, int N, int c0,
-                                           int I, int TI, const XShifts& xs, int nsrc, int tid) {
+// x tile element of the shifted-row weight gradient: output column c (of ntap * I) is
+// channel c % I of tap c / I, i.e. x row n + shift[c / I]; each 8-column group lies in one tap
+__device__ __forceinline__ uint4 stage_taps_elem(const bf16* src, int r, int N, int c0, int I,
+                                                 int TI, const XShifts& xs, int nsrc, int e) {
   constexpr int C8 = IC / 8;
-  for (int e = tid; e < R * C8; e += kThreads) {
-    const int row = e / C8, c = c0 + (e % C8) * 8;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r + row < N && c < TI) {
-      const int tap = c / I;
-      const int n = r + row + xs.s[tap];
-      if (n >= 0 && n < nsrc) v = *(const uint4*)(src + (size_t)n * I + (c - tap * I));
-    }
-    *(uint4*)(t + e * 16) = v;
+  const int row = e / C8, c = c0 + (e % C8) * 8;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (r + row < N && c < TI) {
+    const int tap = c / I;
+    const int n = r + row + xs.s[tap];
+    if (n >= 0 && n < nsrc) v = *(const uint4*)(src + (size_t)n * I + (c - tap * I));
   }
+  return v;
 }
 
 template <bool GVEC>
@@ -127,12 +123,29 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
 #pragma unroll
     for (int cb = 0; cb < CBC; ++cb) acc[mb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // the next stage's g / x tile elements are loaded into registers before this stage's
+  // MFMAs (the loads were issued between two barriers and exposed every stage)
+  uint4 pg[kSPF], px[kSPF];
+  auto load = [&](int rs) {
+#pragma unroll
+    for (int k = 0; k < kSPF; ++k) {
+      const int e = tid + k * kThreads;
+      pg[k] = stage_elem<OC, GVEC>(g, rs, r1, o0, O, e);
+      px[k] = xs.ntap == 1 ? stage_elem<IC, true>(x, rs, r1, i0, I, e)
+                           : stage_taps_elem(x, rs, r1, i0, I, TI, xs, N, e);
+    }
+  };
+  if (r0 < r1) load(r0);
   for (int rs = r0; rs < r1; rs += R) {
     __syncthreads();  // previous stage's reads done
-    stage<OC, GVEC>(gt, g, rs, r1, o0, O, tid);
-    if (xs.ntap == 1) stage<IC, true>(xt, x, rs, r1, i0, I, tid, xs.relu_x != 0);
-    else stage_taps(xt, x, rs, r1, i0, I, TI, xs, N, tid);
+#pragma unroll
+    for (int k = 0; k < kSPF; ++k) {
+      const int e = tid + k * kThreads;
+      *(uint4*)(gt + e * 16) = pg[k];
+      *(uint4*)(xt + e * 16) = xs.relu_x ? relu8(px[k]) : px[k];
+    }
     __syncthreads();
+    if (rs + R < r1) load(rs + R);
     const int nk = (min(R, r1 - rs) + 31) >> 5;
     for (int kb = wave; kb < nk; kb += kThreads / 64) {
       int prow[2];
@@ -282,6 +295,100 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(const bf16* __restrict__ x,
   }
 }
 
+// fc_fwd_kernel's maths (same MFMA operands, K order and critic reduction: bit-identical)
+// for small I (NKS = I / 32 <= 4, the 16x16 IMPALA trunk's I = 128): the workgroup is
+// persistent over 16-row blocks and keeps its wave's W5 fragments (NBW x NKS uint4) and the
+// bias / critic weights in VGPRs for the whole launch. fc_fwd_kernel re-read all of W5
+// (64 KB at O = 256) through L2 for every 16 rows: 2.1 GB of L2 reads per 524K-row learner
+// batch, which bound it (0.38 ms vs ~0.1 ms of HBM traffic). The next row block's x
+// fragments are loaded before the current block's MFMAs.
+template <int O, int NKS>
+__global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__ x, int relu_in,
+                                                        const bf16* __restrict__ w5,
+                                                        const float* __restrict__ b5,
+                                                        const float* __restrict__ wc,
+                                                        const float* __restrict__ bc, int F,
+                                                        bf16* __restrict__ f_out,
+                                                        float* __restrict__ v_out) {
+  constexpr int NBW = O / 64, I = NKS * 32;
+  __shared__ float vred[2][4][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int nrb = (F + 15) / 16;
+  Frag8 wf[NBW][NKS];
+  float bb[NBW][4], ww[NBW][4];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    const uint4* wr = (const uint4*)(w5 + (size_t)((wave * NBW + j) * 16 + li) * I) + G;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const uint4 v = wr[ks * 4];
+      __builtin_memcpy(&wf[j][ks], &v, 16);
+    }
+    const int h0 = (wave * NBW + j) * 16 + 4 * G;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bb[j][i] = b5[h0 + i];
+      ww[j][i] = wc[h0 + i];
+    }
+  }
+  const float bcv = bc[0];
+  auto load_x = [&](int rb, uint4* xv) {
+    const int row = rb * 16 + li;
+    const uint4* xr = (const uint4*)(x + (size_t)(row < F ? row : 0) * I) + G;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) xv[ks] = xr[ks * 4];
+  };
+  uint4 xn[NKS];
+  if ((int)blockIdx.x < nrb) load_x(blockIdx.x, xn);
+  int buf = 0;
+  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x, buf ^= 1) {
+    const int row = rb * 16 + li;
+    const bool valid = row < F;
+    uint4 xv[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) xv[ks] = valid ? xn[ks] : make_uint4(0, 0, 0, 0);
+    if (rb + (int)gridDim.x < nrb) load_x(rb + gridDim.x, xn);
+    f32x4 acc[NBW];
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      uint4 v = relu_in ? relu8(xv[ks]) : xv[ks];
+      Frag8 b;
+      __builtin_memcpy(&b, &v, 16);
+#pragma unroll
+      for (int j = 0; j < NBW; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][ks].v, b.v, acc[j], 0, 0, 0);
+    }
+    float vpart = 0.f;
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) {
+      const int h0 = (wave * NBW + j) * 16 + 4 * G;
+      float hv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + bb[j][i], 0.f)));
+        vpart += hv[i] * ww[j][i];
+      }
+      uint32_t o[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
+               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
+      if (valid) *(uint2*)(f_out + (size_t)row * O + h0) = make_uint2(o[0], o[1]);
+    }
+    vpart += __shfl_xor(vpart, 16, 64);
+    vpart += __shfl_xor(vpart, 32, 64);
+    if (G == 0) vred[buf][wave][li] = vpart;
+    __syncthreads();  // (double-buffered: the next block's writes go to the other half)
+    if (threadIdx.x < 16 && rb * 16 + (int)threadIdx.x < F) {
+      const int t = threadIdx.x;
+      v_out[rb * 16 + t] = vred[buf][0][t] + vred[buf][1][t] + vred[buf][2][t] + vred[buf][3][t] + bcv;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" int mbk_fc_fwd(const void* x, int relu_in, const void* w5, const float* b5,
@@ -290,6 +397,34 @@ extern "C" int mbk_fc_fwd(const void* x, int relu_in, const void* w5, const floa
   if (F <= 0) return 0;
   if (I % 32) return (int)hipErrorInvalidValue;
   const int blocks = (F + 15) / 16;
+  static const bool rb_on = [] {
+    const char* e = getenv("MBK_FC_RB");
+    return !(e && e[0] == '0');
+  }();
+  if (rb_on && (O == 256 || O == 128) && I <= 128) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+    }
+    const int grid = std::min(blocks, cus * 2);  // 2 workgroups per CU (146 VGPRs)
+#define FC_RB(OO, KS)                                                                        \
+  hipLaunchKernelGGL((fc_fwd_rb_kernel<OO, KS>), dim3(grid), dim3(256), 0, stream,          \
+                     (const bf16*)x, relu_in, (const bf16*)w5, b5, wc, bc, F, (bf16*)f_out, \
+                     v_out)
+    const int nks = I / 32;
+    if (O == 256) {
+      if (nks == 1) FC_RB(256, 1); else if (nks == 2) FC_RB(256, 2);
+      else if (nks == 3) FC_RB(256, 3); else FC_RB(256, 4);
+    } else {
+      if (nks == 1) FC_RB(128, 1); else if (nks == 2) FC_RB(128, 2);
+      else if (nks == 3) FC_RB(128, 3); else FC_RB(128, 4);
+    }
+#undef FC_RB
+    return (int)hipGetLastError();
+  }
   if (O == 256)
     hipLaunchKernelGGL(fc_fwd_kernel<256>, dim3(blocks), dim3(256), 0, stream, (const bf16*)x,
                        relu_in, (const bf16*)w5, b5, wc, bc, F, I, (bf16*)f_out, v_out);

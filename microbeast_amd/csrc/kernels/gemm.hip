@@ -115,11 +115,15 @@ template <bool OUT_BF16, bool TAPS, int TN_>
 __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int relu,
-    int accumulate, ATaps taps) {
+    int accumulate, ATaps taps, int vec_out) {
   using S = Shape<TN_>;
   constexpr int TM_ = S::TM, NJ = S::NJ;
-  __shared__ __attribute__((aligned(16))) char sa[2][TM_ * ROWB];
-  __shared__ __attribute__((aligned(16))) char sb[2][TN_ * ROWB];
+  // A / B double buffers; the bf16 output tile of the vectorised epilogue reuses them
+  constexpr int kAB = 2 * TM_ * ROWB + 2 * TN_ * ROWB, OROW = TN_ * 2 + 16;
+  static_assert(kAB >= TM_ * OROW, "output tile");
+  __shared__ __attribute__((aligned(16))) char sab[kAB];
+  char (*sa)[TM_ * ROWB] = (char (*)[TM_ * ROWB])sab;
+  char (*sb)[TN_ * ROWB] = (char (*)[TN_ * ROWB])(sab + 2 * TM_ * ROWB);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int wm = wave / S::WN, wn = wave % S::WN;
@@ -165,6 +169,49 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     }
     __syncthreads();
   }
+  if constexpr (OUT_BF16 && !TAPS) {
+    if (vec_out) {
+      // bf16 output through an LDS tile: 16-byte mask loads and C stores (the per-element
+      // form issued 2-byte loads / stores, 64 of each per lane: the masked dX GEMM of
+      // network.5 ran at ~1/3 of its HBM roofline). Same values: bias / relu before the
+      // bf16 rounding, the mask zeroes a rounded value.
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int trow = wm * 64 + i * 16 + 4 * g + r;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int tcol = wn * NJ * 16 + j * 16 + li, col = n0 + tcol;
+            float v = acc[i][j][r] + ((bias && col < N) ? bias[col] : 0.f);
+            if (relu) v = fmaxf(v, 0.f);
+            *(bf16*)(sab + trow * OROW + tcol * 2) = __float2bfloat16(v);
+          }
+        }
+      __syncthreads();
+      constexpr int C8 = TN_ / 8;
+      for (int e = threadIdx.x; e < TM_ * C8; e += kThreads) {
+        const int trow = e / C8, c8 = e % C8, row = m0 + trow, col = n0 + c8 * 8;
+        if (row >= M || col >= N) continue;
+        uint4 v = *(const uint4*)(sab + trow * OROW + c8 * 16);
+        const size_t o = (size_t)row * ldc + col;
+        if (taps.mask) {
+          const uint4 mk = *(const uint4*)(taps.mask + o);
+          const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
+          uint32_t vw[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint32_t keep = (__uint_as_float(mw[q] << 16) > 0.f ? 0xFFFFu : 0u) |
+                                  (__uint_as_float(mw[q] & 0xFFFF0000u) > 0.f ? 0xFFFF0000u : 0u);
+            vw[q] &= keep;
+          }
+          v = make_uint4(vw[0], vw[1], vw[2], vw[3]);
+        }
+        *(uint4*)((bf16*)C + o) = v;
+      }
+      return;
+    }
+  }
   // epilogue: C layout row = 4g + r (M), col = li (N) within each 16 x 16 tile
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -207,14 +254,17 @@ void launch(const void* A, const void* B, void* C, const float* bias, int M, int
             int lda, int ldb, int ldc, int relu, int out_bf16, int accumulate, const ATaps& t,
             hipStream_t stream) {
   dim3 grid((M + Shape<TN_>::TM - 1) / Shape<TN_>::TM, (N + TN_ - 1) / TN_);
+  // 16-byte output rows (and mask rows) for the vectorised bf16 epilogue
+  const int vec = (!TAPS && out_bf16 && N % 8 == 0 && ldc % 8 == 0 &&
+                   ((uintptr_t)C & 15) == 0 && ((uintptr_t)t.mask & 15) == 0) ? 1 : 0;
   if (out_bf16)
     hipLaunchKernelGGL((gemm_nt_kernel<true, TAPS, TN_>), grid, dim3(kThreads), 0, stream,
                        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, 0,
-                       t);
+                       t, vec);
   else
     hipLaunchKernelGGL((gemm_nt_kernel<false, TAPS, TN_>), grid, dim3(kThreads), 0, stream,
                        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu,
-                       accumulate, t);
+                       accumulate, t, 0);
 }
 
 // narrowest tile that covers N (N = 78 -> one 128-wide tile rather than two of 64)

@@ -577,6 +577,87 @@ __global__ __launch_bounds__(256) void head_dx_gather_kernel(const float* __rest
   ((float4*)(dX + (size_t)f * KD))[lane] = acc;
 }
 
+// head_dx_gather fused with the critic's backward (gridnet.hip value_bwd, same maths):
+//   dh[r][:] = (dv[r] * wc[:] + sum of frame r's active pair rows of dXp) * (h[r][:] > 0)
+// written once as bf16, plus per-workgroup partial rows [K + 1] of dWc = sum dv h and
+// dbc = sum dv (reduced by the caller's column sum). Frames r >= F (rows the head did not
+// score) take only the value term. The fp32 dX [F][256] of the separate kernels (1 KB per
+// frame written, then re-read with h by value_bwd) never exists. One wave per frame row,
+// a lane owns hidden units 4 lane .. 4 lane + 3 (the gather's float4 layout).
+__global__ __launch_bounds__(256) void head_dx_value_kernel(const float* __restrict__ dXp,
+                                                            const int* __restrict__ pidx, int F,
+                                                            int S, const float* __restrict__ dv,
+                                                            const bf16* __restrict__ h,
+                                                            const float* __restrict__ wc, int R,
+                                                            bf16* __restrict__ dh,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[4][KD + 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const float4 w = ((const float4*)wc)[lane];
+  float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb = 0.f;
+  // the next frame's dv, h and pair-index row are loaded before this frame's gathers (one
+  // wave walks ~R / (4 * grid) frames: without it every frame paid two dependent HBM trips)
+  constexpr int kMaxCh = MAX_S / 64;
+  const int nch = (S + 63) / 64;
+  const int stride = gridDim.x * 4;
+  float dn = 0.f;
+  uint2 hn = make_uint2(0, 0);
+  int pn[kMaxCh];
+  auto fetch = [&](int r) {
+    dn = dv[r];
+    hn = ((const uint2*)(h + (size_t)r * KD))[lane];
+    const int* pr = pidx + (size_t)r * S;
+#pragma unroll
+    for (int q = 0; q < kMaxCh; ++q)
+      pn[q] = (r < F && q < nch && q * 64 + lane < S) ? pr[q * 64 + lane] : -1;
+  };
+  const int rfirst = blockIdx.x * 4 + wave;
+  if (rfirst < R) fetch(rfirst);
+  for (int r = rfirst; r < R; r += stride) {
+    const float d = dn;
+    const uint2 hv = hn;
+    int pc[kMaxCh];
+#pragma unroll
+    for (int q = 0; q < kMaxCh; ++q) pc[q] = pn[q];
+    if (r + stride < R) fetch(r + stride);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < kMaxCh; ++q) {
+      if (q >= nch) break;
+      const int p = pc[q];
+      uint64_t m = __ballot(p >= 0);
+      while (m) {
+        const int b = __builtin_ctzll(m);
+        m &= m - 1;
+        const int pp = __shfl(p, b);
+        const float4 v = ((const float4*)(dXp + (size_t)pp * KD))[lane];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    const float hj[4] = {__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xFFFF0000u),
+                         __uint_as_float(hv.y << 16), __uint_as_float(hv.y & 0xFFFF0000u)};
+    const float wj[4] = {w.x, w.y, w.z, w.w}, gj[4] = {acc.x, acc.y, acc.z, acc.w};
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[i] = hj[i] > 0.f ? d * wj[i] + gj[i] : 0.f;
+      sw[i] += d * hj[i];
+    }
+    sb += d;
+    const uint32_t o0 = (uint32_t)__bfloat16_as_ushort(f2bf(o[0])) |
+                        ((uint32_t)__bfloat16_as_ushort(f2bf(o[1])) << 16);
+    const uint32_t o1 = (uint32_t)__bfloat16_as_ushort(f2bf(o[2])) |
+                        ((uint32_t)__bfloat16_as_ushort(f2bf(o[3])) << 16);
+    ((uint2*)(dh + (size_t)r * KD))[lane] = make_uint2(o0, o1);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][4 * lane + i] = sw[i];
+  if (lane == 0) red[wave][KD] = sb;
+  __syncthreads();
+  for (int e = threadIdx.x; e < KD + 1; e += 256)
+    partial[(size_t)blockIdx.x * (KD + 1) + e] = red[0][e] + red[1][e] + red[2][e] + red[3][e];
+}
+
 // W [S*78][256] fp32, b [S*78] -> Wp [S][80][256] bf16, bp [S][80], WpT [S][256][96] bf16
 __global__ __launch_bounds__(256) void head_pack_kernel(const float* __restrict__ W,
                                                         const float* __restrict__ b, int S,
@@ -682,6 +763,31 @@ extern "C" int mbk_head_dx_gather(const float* dXp, const int* pidx, int F, int 
                                   hipStream_t stream) {
   hipLaunchKernelGGL(head_dx_gather_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, dXp, pidx, F,
                      S, dX);
+  return (int)hipGetLastError();
+}
+
+// partial rows mbk_head_dx_value writes ([parts][257] fp32)
+extern "C" int mbk_head_dx_value_parts(int R) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int need = (R + 3) / 4;
+  return need < 1 ? 1 : (need < cus * 4 ? need : cus * 4);
+}
+
+// dh [R][256] bf16 = (dv wc + gathered head dX) * (h > 0); partial [parts][257] fp32 rows of
+// (dWc, dbc); rows >= F take the value term only. parts = mbk_head_dx_value_parts(R).
+extern "C" int mbk_head_dx_value(const float* dXp, const int* pidx, int F, int S, const float* dv,
+                                 const void* h, const float* wc, int R, void* dh, float* partial,
+                                 int parts, hipStream_t stream) {
+  if (R <= 0) return 0;
+  if (F > R || parts < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_dx_value_kernel, dim3(parts), dim3(256), 0, stream, dXp, pidx, F, S, dv,
+                     (const bf16*)h, wc, R, (bf16*)dh, partial);
   return (int)hipGetLastError();
 }
 

@@ -119,7 +119,12 @@ class HipEncoder:
         # max-pool backward folded into the stage conv's wgrad / dgrad staging: saves the
         # pre-pool gradient's HBM round trip but measured 6 % slower per update on MI355X
         # (extra expand phase + a 1-wave/SIMD dgrad variant), so off by default
-        self.fused_pool_bwd = False
+        # MBK_FUSED_POOL_BWD: 0 (default) | 1 (every stage) | s0 (stage 0 only: wgrad only,
+        # the observation layer has no dgrad)
+        _fp = os.environ.get("MBK_FUSED_POOL_BWD", "0")
+        self.fused_pool_bwd_stages = ({0, 1, 2, 3} if _fp == "1" else {0} if _fp == "s0"
+                                      else set())
+        self.fused_pool_bwd = bool(self.fused_pool_bwd_stages)
         # 16-channel residual blocks (stage 0): one fused backward launch per block
         # (resblock.hip) instead of wgrad1 / dgrad1 / wgrad0 / dgrad0 (MBK_FUSED_RES=0: off)
         self.fused_res_bwd = os.environ.get("MBK_FUSED_RES", "1") == "1"
@@ -390,7 +395,7 @@ class HipEncoder:
                 dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
-            if self.fused_pool_bwd:
+            if self.fused_pool_bwd and s in self.fused_pool_bwd_stages:
                 # max_pool2d backward folded into both consumers' LDS staging: the
                 # pre-pool gradient is never materialised in HBM
                 self._wgrad(Ls, x, None, grads[2 * li], grads[2 * li + 1], dp=dp, pidx=pidx)

@@ -138,9 +138,14 @@ class SparseHead:
             N.check(k.mbk_rng_advance(rng.data_ptr(), st), "rng_advance")
         return logp, ent
 
-    def backward(self, X, mask_bits, action, g_logp, g_ent, dW=None, db=None):
+    def backward(self, X, mask_bits, action, g_logp, g_ent, dW=None, db=None, value=None):
         """Returns (dX fp32 [F,256], dW fp32 [S*78,256], db fp32 [S*78]); dW / db may be
         given (e.g. the parameters' flat gradient slots).
+
+        value = (dv fp32 [R], h bf16 [R, 256], wc fp32 [256], partial fp32 [parts, 257]) with
+        R >= F (h's first F rows are X): instead of dX, returns the critic-fused input
+        gradient dh = (dv wc + dX) * (h > 0) as bf16 [R, 256] (mbk_head_dx_value) and writes
+        the critic's (dWc, dbc) partial rows for a column sum.
 
         Relies on the compaction left by the matching forward (same batch)."""
         F = X.shape[0]
@@ -165,6 +170,16 @@ class SparseHead:
                                self.totals.data_ptr(), g_logp.data_ptr(), N.ptr(g_ent), self.S,
                                grid, dXp.data_ptr(), dWp.data_ptr(), dbp.data_ptr(),
                                dW.data_ptr(), db.data_ptr(), st), "head_bwd")
+        if value is not None:
+            dv, h, wc, partial = value
+            R = h.shape[0]
+            assert h.is_contiguous() and h.shape[1] == KD and dv.dtype == torch.float32
+            dh = torch.empty(R, KD, dtype=torch.bfloat16, device=X.device)
+            N.check(k.mbk_head_dx_value(dXp.data_ptr(), self.pidx.data_ptr(), F, self.S,
+                                        dv.data_ptr(), h.data_ptr(), wc.data_ptr(), R,
+                                        dh.data_ptr(), partial.data_ptr(), partial.shape[0], st),
+                    "head_dx_value")
+            return dh, dW, db
         dX = torch.empty(F, KD, dtype=torch.float32, device=X.device)
         N.check(k.mbk_head_dx_gather(dXp.data_ptr(), self.pidx.data_ptr(), F, self.S,
                                      dX.data_ptr(), st), "head_dx_gather")

@@ -18,6 +18,8 @@ first ``n_score`` rows of f. Backward:
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native as N
@@ -25,6 +27,8 @@ from .gridconv import colsum, critic_maps, map_gather, value_bwd
 from .optim import grad_out
 
 _BF = torch.bfloat16
+# MBK_FUSED_DX_VALUE=0: separate head_dx_gather + value_bwd launches (A/B, tests)
+_FUSED_DX_VALUE = os.environ.get("MBK_FUSED_DX_VALUE", "1") == "1"
 
 
 class TailMaps:
@@ -79,12 +83,22 @@ class _ImpalaTail(torch.autograd.Function):
         if g_v is None:
             g_v = zeros(n, device=dev)
         gwa, gba = grad_out(wa), grad_out(ba)
-        dX, _, _ = head.backward(f[:n_score], mask, action, g_logp.float().contiguous(),
-                                 None if g_ent is None else g_ent.float().contiguous(),
-                                 gwa, gba.view(-1))
         gwc, gbc = grad_out(wc), grad_out(bc)
-        dh = value_bwd(g_v.float().contiguous(), f, wc.detach(), gwc, gbc, gadd=dX)
         k = N.kernels()
+        g_v = g_v.float().contiguous()
+        if f.is_cuda and f.shape[1] == 256 and _FUSED_DX_VALUE:
+            # head dX gather + critic backward in one pass (head.hip head_dx_value)
+            partial = torch.empty(k.mbk_head_dx_value_parts(n), 257, dtype=torch.float32,
+                                  device=dev)
+            dh, _, _ = head.backward(f[:n_score], mask, action, g_logp.float().contiguous(),
+                                     None if g_ent is None else g_ent.float().contiguous(),
+                                     gwa, gba.view(-1), value=(g_v, f, wc.detach(), partial))
+            colsum(partial, 257, gwc, 256, gbc)
+        else:
+            dX, _, _ = head.backward(f[:n_score], mask, action, g_logp.float().contiguous(),
+                                     None if g_ent is None else g_ent.float().contiguous(),
+                                     gwa, gba.view(-1))
+            dh = value_bwd(g_v, f, wc.detach(), gwc, gbc, gadd=dX)
         st = N.stream_ptr()
         dy = torch.empty(n, I, dtype=_BF, device=dev)
         O = dh.shape[1]

@@ -52,3 +52,21 @@ def test_gemm_nt_autograd(cuda):
     assert _rel(a.grad, ar.grad) < 1e-2
     assert _rel(w.grad, wr.grad) < 1e-2
     assert _rel(bias.grad, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 128, 256), (300, 40, 64), (129, 77, 32)])
+def test_gemm_nt_mask_matches_torch(cuda, M, N, K):
+    """mbk_gemm_nt_mask (relu-backward mask in the epilogue; N % 8 == 0 takes the LDS-staged
+    16-byte epilogue, N = 77 the per-element one) vs fp32 torch."""
+    from microbeast_amd import _native as Nn
+    torch.manual_seed(M + N)
+    a = torch.randn(M, K, device=cuda).bfloat16()
+    b = torch.randn(N, K, device=cuda).bfloat16()
+    mask = torch.randn(M, N, device=cuda).bfloat16()
+    c = torch.full((M, N), 7.0, device=cuda).bfloat16()
+    Nn.check(Nn.kernels().mbk_gemm_nt_mask(a.data_ptr(), b.data_ptr(), c.data_ptr(), None, M, N,
+                                           K, K, K, N, 0, 1, mask.data_ptr(), Nn.stream_ptr()),
+             "gemm_nt_mask")
+    ref = (a.float() @ b.float().t()) * (mask.float() > 0)
+    assert _rel(c, ref) < 5e-3
+    assert bool(((mask.float() > 0) | (c.float() == 0)).all())

@@ -78,3 +78,32 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
     d = (Lh.flat.data.cpu() - Lr.flat.data).abs()
     assert float(d.max()) <= 2.0 * hp.lr + 1e-6
     assert float((d > 0.5 * hp.lr).float().mean()) < 0.02
+
+
+def test_fused_dx_value_matches_separate_kernels(cuda):
+    """head.hip head_dx_value (head dX gather + critic backward in one pass, bf16 dh) gives
+    the same update as head_dx_gather (fp32 dX) + gridnet.hip value_bwd."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops import tail
+
+    batches = engine_batches(cuda, 16, 1, envs=32, T=8, seed=3)
+    torch.manual_seed(5)
+    base = Agent((16, 16, 27))
+    with torch.no_grad():
+        base.actor.weight.normal_(0, 0.02)
+    grads = []
+    for fused in (True, False):
+        tail._FUSED_DX_VALUE = fused
+        try:
+            L = Learner(copy.deepcopy(base), LearnerHParams(), cuda)
+            L.learn(batches[0])
+            torch.cuda.synchronize()
+            grads.append((L.flat.grad.cpu().clone(), L.flat.slices))
+        finally:
+            tail._FUSED_DX_VALUE = True
+    (ga, slices), (gb, _) = grads
+    for name, o, n, _ in slices:
+        a, b = ga[o:o + n], gb[o:o + n]
+        scale = float(b.abs().max()) + 1e-12
+        assert float((a - b).abs().max()) <= 1e-3 * scale + 1e-7, name
