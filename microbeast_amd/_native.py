@@ -104,6 +104,11 @@ _SIGS = {
                           c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_res_bwd16_parts": [c_int, c_int, c_int, c_int],
+    "mbk_res_bwd32_parts": [c_int, c_int, c_int, c_int],
+    "mbk_res_bwd32_partial_floats": [c_int],
+    "mbk_res_bwd32": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                      c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                      c_void_p],
     "mbk_res_fwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_int, c_int, c_int, c_void_p],
     "mbk_res_blk32_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -131,7 +136,7 @@ _SIGS = {
     "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_void_p, c_void_p],
 }
-_RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64}
+_RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64, "mbk_res_bwd32_partial_floats": c_int64}
 
 
 def _ensure_built() -> None:

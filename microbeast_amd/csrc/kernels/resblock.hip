@@ -645,6 +645,278 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
 
 #undef MBK_RB32_FETCH
 
+// ------------------------------------------------------------------ fused backward, 32 ch
+// Backward of one 32-channel residual block (stages 1-2), the res_bwd16 dataflow
+// (x, u, g staged once; du kept in LDS; dx written once) with the 32-channel operands split
+// over 8 waves so that no wave holds more than one layer's weights and 9 wgrad tiles:
+//   phase A: waves 0-3  du = conv1^T(g) * [u > 0] -> Td   (conv1 dgrad weights in VGPRs)
+//            waves 4-7  dW1[cb][cib] += relu(u) (x) g      (9 tap tiles each)
+//   phase B: waves 4-7  dx = conv0^T(du) * [x > 0] + g     (conv0 dgrad weights in VGPRs)
+//            waves 0-3  dW0[cb][cib] += relu(x) (x) du
+// (cb, cib) = this wave's 16-channel output / input block of the 32 x 32 weight, so every
+// weight-gradient tile has exactly one owner: no cross-wave reduction, partial rows are
+// written straight from the accumulators. dgrad = conv_fwd<32, 32> chains on the packed
+// transposed weights (bit-identical du / dx to the per-layer kernels); wgrad = the
+// ds_read_b64_tr_b16 operand form of res_bwd16 / conv_wgrad.
+constexpr int kT32 = 512;                      // 8 waves
+constexpr int KTOT32 = 9 * C32;                // wgrad K per output channel
+constexpr int ROW32 = C32 * KTOT32 + C32;      // one partial row (weights + bias)
+constexpr int kPF32 = 2;                       // staging prefetch slots per thread per tensor
+
+struct ResBwd32Args {
+  const bf16* x;     // block input (pre-relu)      [N][H][W][32]
+  const bf16* u;     // conv0 output (pre-relu)     [N][H][W][32]
+  const bf16* g;     // dL/dy                        [N][H][W][32]
+  bf16* dx;          // dL/dx                        [N][H][W][32]
+  const bf16* w1t;   // conv1 packed dgrad weights [32][9][32]
+  const bf16* w0t;   // conv0 packed dgrad weights
+  float* partial;    // layer l (0: conv1, 1: conv0) row of workgroup b at l * lstride + b * ROW32
+  int64_t lstride;
+  int N, H, W, imgs;
+};
+
+template <int WC>
+__global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const bool lo = wave < 4;          // waves 0-3: dgrad1 (A) + wgrad0 (B)
+  const int wq = wave & 3;           // rank inside the half
+  const int cb = wq >> 1, cib = wq & 1;
+  const int tb = ((a.imgs * Hp * Wp * PIXB32) + 15) & ~15;
+  char* Tg = smem;
+  char* Tu = smem + tb;       // relu(u)
+  char* Tx = smem + 2 * tb;   // relu(x)
+  char* Td = smem + 3 * tb;   // du
+  char* zero = smem + 4 * tb; // 128 zero bytes for out-of-range wgrad pixels
+  for (int e = tid; e < (4 * tb + 128) / 16; e += kT32) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
+
+  // this wave's dgrad weights (lane: rows nb * 16 + li, chunk c, elements 8g..8g+7)
+  Frag8 w[NCH32][NB32];
+  {
+    const bf16* wt = lo ? a.w1t : a.w0t;
+#pragma unroll
+    for (int nb = 0; nb < NB32; ++nb) {
+      const uint4* wp = (const uint4*)(wt + (size_t)(nb * 16 + li) * NCH32 * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH32; ++c) w[c][nb].u = wp[c * 4];
+    }
+  }
+  f32x4 acc[9];  // this wave's wgrad tiles (tap t): rows co = cb*16 + 4g + i, cols ci = cib*16 + li
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int coff[NCH32];  // K chunk c = tap c, channels 8g.. of this lane
+#pragma unroll
+  for (int c = 0; c < NCH32; ++c) coff[c] = ((c / 3) * Wp + (c % 3)) * PIXB32 + 16 * g;
+  float db1[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum g: channels 8 (tid & 3) .. +8 (staging)
+  float db0[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum du: channels nb*16 + 4g + i (waves 0-3)
+
+  constexpr int EPP = C32 / 8;
+  const int per = a.imgs * HW * EPP;  // uint4 per tensor per round
+  const int nrounds = (a.N + a.imgs - 1) / a.imgs;
+  uint4 px[kPF32], pu[kPF32], pg[kPF32];
+  auto prefetch = [&](int rd) {
+    const int lim = min(per, (a.N - rd * a.imgs) * HW * EPP);
+    const size_t base = (size_t)rd * per;
+#pragma unroll
+    for (int k = 0; k < kPF32; ++k) {
+      const int e = tid + k * kT32;
+      const bool ok = e < lim;
+      px[k] = ok ? ((const uint4*)a.x)[base + e] : make_uint4(0, 0, 0, 0);
+      pu[k] = ok ? ((const uint4*)a.u)[base + e] : make_uint4(0, 0, 0, 0);
+      pg[k] = ok ? ((const uint4*)a.g)[base + e] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto lds_off = [&](int e) {
+    const int q = e & (EPP - 1), p = e / EPP;
+    const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB32 + q * 16;
+  };
+  auto put = [&](int e, uint4 vx, uint4 vu, uint4 vg) {
+    const int o = lds_off(e);
+    *(uint4*)(Tx + o) = relu8(vx);
+    *(uint4*)(Tu + o) = relu8(vu);
+    *(uint4*)(Tg + o) = vg;
+    const uint32_t wv[4] = {vg.x, vg.y, vg.z, vg.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      db1[2 * j] += lo_f(wv[j]);
+      db1[2 * j + 1] += hi_f(wv[j]);
+    }
+  };
+  // wgrad K block kb (32 pixels) of this wave's tile: dY tile D (block cb), X taps from X
+  auto wgrad_kb = [&](int kb, int M, const char* D, const char* X) {
+    const char* dptr[2];
+    int xpos[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int p = kb * 32 + 8 * g + 4 * h + (li >> 2);
+      const bool ok = p < M;
+      const int pp = ok ? p : 0;
+      const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
+      const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+      xpos[h] = (im * Hp + y) * Wp + x;
+      dptr[h] = ok ? D + (xpos[h] + Wp + 1) * PIXB32 + cb * 32 : zero;
+    }
+    Frag8 af;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
+    // out-of-range pixels read pixel 0's (finite) X values against a zero dY column
+    const char* xb0 = X + xpos[0] * PIXB32 + cib * 32 + 8 * (li & 3);
+    const char* xb1 = X + xpos[1] * PIXB32 + cib * 32 + 8 * (li & 3);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int off = ((t / 3) * Wp + (t % 3)) * PIXB32;
+      Frag8 bf;
+      bf.h[0] = tr_read(xb0 + off);
+      bf.h[1] = tr_read(xb1 + off);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bf.v, acc[t], 0, 0, 0);
+    }
+  };
+
+  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x);
+  __syncthreads();  // zeroed tiles visible
+  for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
+    const int img0 = rd * a.imgs, nimg = min(a.imgs, a.N - img0);
+    const int lim = nimg * HW * EPP;
+#pragma unroll
+    for (int k = 0; k < kPF32; ++k) {
+      const int e = tid + k * kT32;
+      if (e < lim) put(e, px[k], pu[k], pg[k]);
+    }
+    for (int e = tid + kPF32 * kT32; e < lim; e += kT32) {
+      const size_t s = (size_t)rd * per + e;
+      put(e, ((const uint4*)a.x)[s], ((const uint4*)a.u)[s], ((const uint4*)a.g)[s]);
+    }
+    __syncthreads();
+    if (rd + (int)gridDim.x < nrounds) prefetch(rd + gridDim.x);
+    const int M = nimg * HW, nblk = (M + 15) >> 4, nk = (M + 31) >> 5;
+    const size_t gpix0 = (size_t)img0 * HW;
+    // ---------------- phase A
+    if (lo) {  // du = conv1^T(g) * [u > 0]
+      for (int pb = wq; pb < nblk; pb += 4) {
+        const int m = pb * 16 + li;
+        const bool valid = m < M;
+        const int mm = valid ? m : 0;
+        const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        const int base = (im * Hp + y) * Wp + x;
+        const char* bp = Tg + base * PIXB32;
+        f32x4 ac[NB32];
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) ac[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH32; ++c) {
+          Frag8 av;
+          av.u = *(const uint4*)(bp + coff[c]);
+#pragma unroll
+          for (int nb = 0; nb < NB32; ++nb)
+            ac[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av.v, ac[nb], 0, 0, 0);
+        }
+        if (!valid) continue;
+        const int o = (base + Wp + 1) * PIXB32;
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) {
+          const int co0 = nb * 16 + 4 * g;
+          const uint2 mu = *(const uint2*)(Tu + o + co0 * 2);
+          const uint32_t mw[2] = {mu.x, mu.y};
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            v[i] = (__uint_as_float(hb << 16) > 0.f) ? ac[nb][i] : 0.f;
+          }
+          const uint2 du = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          *(uint2*)(Td + o + co0 * 2) = du;
+          db0[nb * 4 + 0] += lo_f(du.x); db0[nb * 4 + 1] += hi_f(du.x);
+          db0[nb * 4 + 2] += lo_f(du.y); db0[nb * 4 + 3] += hi_f(du.y);
+        }
+      }
+    } else {  // dW1 += relu(u) (x) g
+      for (int kb = 0; kb < nk; ++kb) wgrad_kb(kb, M, Tg, Tu);  // this wave's tile: every K block
+    }
+    __syncthreads();  // Td complete
+    // ---------------- phase B
+    if (!lo) {  // dx = conv0^T(du) * [x > 0] + g
+      for (int pb = wq; pb < nblk; pb += 4) {
+        const int m = pb * 16 + li;
+        const bool valid = m < M;
+        const int mm = valid ? m : 0;
+        const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        const int base = (im * Hp + y) * Wp + x;
+        const char* bp = Td + base * PIXB32;
+        f32x4 ac[NB32];
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) ac[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH32; ++c) {
+          Frag8 av;
+          av.u = *(const uint4*)(bp + coff[c]);
+#pragma unroll
+          for (int nb = 0; nb < NB32; ++nb)
+            ac[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av.v, ac[nb], 0, 0, 0);
+        }
+        if (!valid) continue;
+        const int o = (base + Wp + 1) * PIXB32;
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) {
+          const int co0 = nb * 16 + 4 * g;
+          const uint2 mx = *(const uint2*)(Tx + o + co0 * 2), ad = *(const uint2*)(Tg + o + co0 * 2);
+          const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
+          float v[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            v[i] = (__uint_as_float(hb << 16) > 0.f) ? ac[nb][i] : 0.f;
+            v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
+          }
+          *(uint2*)(a.dx + (gpix0 + m) * C32 + co0) =
+              make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        }
+      }
+    } else {  // dW0 += relu(x) (x) du
+      for (int kb = 0; kb < nk; ++kb) wgrad_kb(kb, M, Td, Tx);
+    }
+    __syncthreads();  // tiles consumed before the next round is staged
+  }
+  // ---- partial rows: each tile straight from its owner wave (layer 1 = waves 4-7 -> block 0)
+  float* out = a.partial + (lo ? a.lstride : 0) + (size_t)blockIdx.x * ROW32;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      out[(cb * 16 + 4 * g + i) * KTOT32 + t * C32 + cib * 16 + li] = acc[t][i];
+  // bias grads through LDS (fixed order): red1[tid][8] = db1, red0[tid][8] = db0 (waves 0-3)
+  float* red = (float*)smem;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[tid * 16 + j] = db1[j];
+    red[tid * 16 + 8 + j] = db0[j];
+  }
+  __syncthreads();
+  if (tid < C32) {
+    float s = 0.f;  // conv1 bias: channel tid = 8 q + j lives in threads with (t & 3) == q
+    const int q = tid >> 3, j = tid & 7;
+    for (int t = q; t < kT32; t += 4) s += red[t * 16 + j];
+    a.partial[(size_t)blockIdx.x * ROW32 + C32 * KTOT32 + tid] = s;
+    // conv0 bias: channel tid = nb * 16 + 4 G + i lives in waves 0-3, lanes with g == G
+    const int nb = tid >> 4, G = (tid & 15) >> 2, i = tid & 3;
+    float s0 = 0.f;
+    for (int t = 0; t < 256; ++t)
+      if (((t & 63) >> 4) == G) s0 += red[t * 16 + 8 + nb * 4 + i];
+    a.partial[a.lstride + (size_t)blockIdx.x * ROW32 + C32 * KTOT32 + tid] = s0;
+  }
+}
+
+size_t res32b_smem(int imgs, int H, int W) {
+  const size_t tb = ((size_t)imgs * (H + 2) * (W + 2) * PIXB32 + 15) & ~(size_t)15;
+  return std::max(4 * tb + 128, (size_t)kT32 * 16 * 4);
+}
+
 size_t resb32_smem(int imgs, int H, int W) {
   return 2 * (((size_t)imgs * (H + 2) * (W + 2) * PIXB32 + 15) & ~(size_t)15);
 }
@@ -722,6 +994,53 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
   rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, 0, stream);
   if (rc) return rc;
   return mbk_wgrad_reduce(partial + lstride, nparts, C, C, C, dw0, db0, 0, stream);
+}
+
+// Partial-row PAIRS mbk_res_bwd32 writes (= its grid: one 8-wave workgroup per CU);
+// <= 0: unsupported shape.
+extern "C" int mbk_res_bwd32_parts(int N, int H, int W, int imgs) {
+  if (N <= 0 || imgs < 1 || H * W > 1024 || (int64_t)imgs * H * W >= (int64_t(1) << 22))
+    return -1;
+  if (res32b_smem(imgs, H, W) > 160 * 1024) return -1;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
+  const int nrounds = (N + imgs - 1) / imgs;
+  return std::max(1, std::min(nrounds, ncu));
+}
+
+extern "C" int64_t mbk_res_bwd32_partial_floats(int nparts) {
+  return 2 * (int64_t)(nparts + (nparts + 31) / 32) * ROW32;
+}
+
+// 32-channel block backward (see res_bwd32_kernel): dx and both layers' weight / bias
+// gradients dw1/db1/dw0/db0 (fp32 [32][32][3][3] / [32], overwritten).
+extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* dx,
+                             const void* w1t, const void* w0t, float* partial, int nparts,
+                             float* dw1, float* db1, float* dw0, float* db0, int N, int H, int W,
+                             int imgs, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (nparts < 1 || nparts != mbk_res_bwd32_parts(N, H, W, imgs)) return (int)hipErrorInvalidValue;
+  const size_t sm = res32b_smem(imgs, H, W);
+  const int64_t lstride = (int64_t)(nparts + (nparts + 31) / 32) * ROW32;
+  ResBwd32Args a{(const bf16*)x, (const bf16*)u, (const bf16*)g, (bf16*)dx,
+                 (const bf16*)w1t, (const bf16*)w0t, partial, lstride, N, H, W, imgs};
+  auto kfn = W == 4 ? res_bwd32_kernel<4> : W == 2 ? res_bwd32_kernel<2>
+           : W == 8 ? res_bwd32_kernel<8> : W == 3 ? res_bwd32_kernel<3>
+           : W == 6 ? res_bwd32_kernel<6> : res_bwd32_kernel<0>;
+  if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  hipLaunchKernelGGL(kfn, dim3(nparts), dim3(kT32), sm, stream, a);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
+  rc = mbk_wgrad_reduce(partial, nparts, C32, C32, C32, dw1, db1, 0, stream);
+  if (rc) return rc;
+  return mbk_wgrad_reduce(partial + lstride, nparts, C32, C32, C32, dw0, db0, 0, stream);
 }
 
 // One 32-channel residual block's forward (see res_blk32_kernel): u = conv0(relu x),

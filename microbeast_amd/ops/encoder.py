@@ -128,6 +128,8 @@ class HipEncoder:
         # 16-channel residual blocks (stage 0): one fused backward launch per block
         # (resblock.hip) instead of wgrad1 / dgrad1 / wgrad0 / dgrad0 (MBK_FUSED_RES=0: off)
         self.fused_res_bwd = os.environ.get("MBK_FUSED_RES", "1") == "1"
+        # 32-channel residual blocks (stages 1-2): one fused backward launch per block
+        self.fused_res_bwd32 = os.environ.get("MBK_FUSED_RES32", "1") == "1"
         self.fused_res_fwd = os.environ.get("MBK_FUSED_RES_FWD", "1") == "1"
         self.fused_res_fwd32 = os.environ.get("MBK_FUSED_RES_FWD32", "1") == "1"
         self._partial_rb = None
@@ -316,6 +318,28 @@ class HipEncoder:
                                 N.stream_ptr()), "res_bwd16")
         return dx
 
+    def _res_bwd32(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
+        """Fused backward of a 32-channel residual block (resblock.hip res_bwd32): returns dx;
+        writes both layers' weight / bias gradients."""
+        n = x.shape[0]
+        H, W = L0.H, L0.W
+        k = N.kernels()
+        imgs = max(1, min(128 // (H * W), (100 * 1024 - 128) // (4 * (H + 2) * (W + 2) * 80)))
+        nparts = k.mbk_res_bwd32_parts(n, H, W, imgs)
+        if nparts < 1:
+            raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")
+        need = k.mbk_res_bwd32_partial_floats(nparts)
+        if self._partial_rb is None or self._partial_rb.numel() < need:
+            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        base = self.packed_bwd.data_ptr()
+        N.check(k.mbk_res_bwd32(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
+                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
+                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs,
+                                N.stream_ptr()), "res_bwd32")
+        return dx
+
     # ------------------------------------------------------------ passes
     def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool,
                 prepacked: bool = False, head=None):
@@ -380,6 +404,13 @@ class HipEncoder:
                                       grads[2 * (li + 4) + 1], grads[2 * (li + 3)],
                                       grads[2 * (li + 3) + 1])
                 dp = self._res_bwd16(L[li + 1], L[li + 2], p, u0, dy0, grads[2 * (li + 2)],
+                                     grads[2 * (li + 2) + 1], grads[2 * (li + 1)],
+                                     grads[2 * (li + 1) + 1])
+            elif self.fused_res_bwd32 and L[li + 1].cin == 32 and x.is_cuda:
+                dy0 = self._res_bwd32(L[li + 3], L[li + 4], y0, u1, g, grads[2 * (li + 4)],
+                                      grads[2 * (li + 4) + 1], grads[2 * (li + 3)],
+                                      grads[2 * (li + 3) + 1])
+                dp = self._res_bwd32(L[li + 1], L[li + 2], p, u0, dy0, grads[2 * (li + 2)],
                                      grads[2 * (li + 2) + 1], grads[2 * (li + 1)],
                                      grads[2 * (li + 1) + 1])
             else:

@@ -473,3 +473,37 @@ def test_fused_res_blk32_bit_identical(cuda, s, n):
     assert len(outs[False]) == len(outs[True])
     for i, (a, b) in enumerate(zip(outs[False], outs[True])):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 9)])
+def test_fused_res_bwd32_matches_per_layer_kernels(cuda, s, n):
+    """resblock.hip res_bwd32 (one 8-wave launch per 32-channel residual block backward)
+    against the per-layer wgrad / dgrad kernels: input gradients flowing on are
+    bit-identical (same dgrad MFMA chains and bf16 rounding), so every non-residual weight
+    gradient is too; the 32-channel residual weight grads differ by fp32 summation order."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(4)
+    chans = (16, 32, 32, 32) if s == 24 else (16, 32, 32)
+    m = Agent((s, s, 27), channels=chans).to(cuda)
+    obs = _random_obs_bits(n, s * s).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = encoder_params(m.network, len(chans))
+    grads = {}
+    for fused in (False, True):
+        enc.fused_res_bwd32 = fused
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(6)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[fused] = [p.grad.detach().clone() for p in params]
+    enc.fused_res_bwd32 = True
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        layer = i // 2
+        if layer >= 5 and layer % 5 != 0:  # 32-channel residual conv
+            torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6)
+        else:
+            assert torch.equal(a, b), i
