@@ -57,6 +57,11 @@ _PF_WGRAD = 4 * 256  # conv_wgrad prefetch capacity, X and dY each
 # (48 KB = 3 workgroups per CU) and the target output pixels per image group
 _FWD_LDS = int(os.environ.get("MBK_CONV_LDS_KB", "48")) * 1024
 _FWD_PIX = int(os.environ.get("MBK_CONV_PIX", "512"))
+# res_bwd32 round size: output pixels per round and the LDS budget (KB) of its four tiles
+# (maps of <= 2x2 pixels are mostly halo: their own budget)
+_RES32_PIX = int(os.environ.get("MBK_RES32_PIX", "256"))
+_RES32_LDS_KB = int(os.environ.get("MBK_RES32_LDS_KB", "100"))
+_RES32_LDS_KB_SMALL = int(os.environ.get("MBK_RES32_LDS_KB_SMALL", "150"))
 
 
 def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
@@ -324,7 +329,8 @@ class HipEncoder:
         n = x.shape[0]
         H, W = L0.H, L0.W
         k = N.kernels()
-        imgs = max(1, min(128 // (H * W), (100 * 1024 - 128) // (4 * (H + 2) * (W + 2) * 80)))
+        lds_kb = _RES32_LDS_KB if H * W > 4 else _RES32_LDS_KB_SMALL
+        imgs = max(1, min(_RES32_PIX // (H * W), (lds_kb * 1024 - 128) // (4 * (H + 2) * (W + 2) * 80)))
         nparts = k.mbk_res_bwd32_parts(n, H, W, imgs)
         if nparts < 1:
             raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")

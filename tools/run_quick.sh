@@ -1,8 +1,9 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-timeout -k 10 120 python tools/dbg/res32_check.py 4 37 2>&1 | head -4
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_conv.py -k "res_bwd32 or res_bwd16 or res_blk32" > gpurun_out/t3.log 2>&1 || { tail -40 gpurun_out/t3.log; exit 1; }
-tail -2 gpurun_out/t3.log
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_learner_parity.py > gpurun_out/t3b.log 2>&1 || { tail -40 gpurun_out/t3b.log; exit 1; }
-tail -2 gpurun_out/t3b.log
-LT=1 bash tools/ab_bench.sh ab4 "" "MBK_FUSED_RES32=0"
+for v in "MBK_RES32_PIX=128" "MBK_RES32_PIX=256 MBK_RES32_LDS_KB_SMALL=150" "MBK_RES32_PIX=64" "MBK_RES32_PIX=96 MBK_RES32_LDS_KB_SMALL=150"; do
+  cd /tmp && export TMPDIR=/tmp && rm -rf /tmp/lt
+  env $v timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/lt -o run --output-format csv \
+    -- python $GRAFT_REPO_ROOT/tools/learner_only.py --steps 2 > $GRAFT_REPO_ROOT/gpurun_out/r32.log 2>&1 || exit $?
+  python $GRAFT_REPO_ROOT/tools/layer_times.py /tmp/lt --out $GRAFT_REPO_ROOT/gpurun_out/r32.md > /dev/null || exit $?
+  echo "$v"; python $GRAFT_REPO_ROOT/tools/lt_agg.py $GRAFT_REPO_ROOT/gpurun_out/r32.md | grep "res_bwd32\|total"
+done
