@@ -72,6 +72,9 @@ def parse(argv=None):
                    help="rehearsal only: allow more ranks than GPUs (ranks share a GPU over gloo)")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", help="fp32 | bf16 payload")
     p.add_argument("--bucket_mb", type=float, default=8.0)
+    p.add_argument("--policy_gate", type=int, default=-1,
+                   help="1: learner launches wait while a policy step's kernels run (engine "
+                        "policy gate); 0: off; -1: MBK_POLICY_GATE (default off)")
     return p.parse_args(argv)
 
 
@@ -129,7 +132,8 @@ def main(argv=None):
                          args.batch_slots, dev, n_threads=threads, seed=args.seed + 1000 * info.rank,
                          env_index_base=info.rank * envs_total,
                          selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy,
-                         n_lanes=args.lanes, policy_cu_every=args.cu_partition)
+                         n_lanes=args.lanes, policy_cu_every=args.cu_partition,
+                         policy_gate=None if args.policy_gate < 0 else bool(args.policy_gate))
     league = None
     if args.selfplay_groups > 0:
         from microbeast_amd.runtime.league import League
@@ -246,6 +250,7 @@ def main(argv=None):
                 "cpus_per_rank": len(cpus),
                 "policy_lanes": rt.n_lanes,
                 "allreduce": f"{args.allreduce_dtype} {args.bucket_mb:g}MB buckets",
+                "policy_gate": rt.policy_gate,
             },
             "actor_stats": {
                 "env_frames_stepped_per_s_rank0": round((st1["frames"] - st0["frames"]) / el, 1),

@@ -30,6 +30,7 @@ c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int6
 
 _SIGS = {
     "mbk_multi_copy": [c_void_p, c_int, c_void_p],
+    "mbk_stream_wait_zero": [c_void_p, c_void_p],
     "mbk_row_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p],
     "mbk_memset": [c_void_p, c_int, c_int64, c_void_p],
     "mbk_masked_cell_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64,
@@ -100,6 +101,8 @@ _SIGS = {
                        c_void_p],
     "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_trunk_tail": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_trunk_tail_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                           c_void_p],
     "mbk_trunk_tail_fc": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_pack_env_actions": [c_void_p, c_int64, c_void_p, c_void_p],
@@ -108,15 +111,18 @@ _SIGS = {
     "mbk_res_bwd32_partial_floats": [c_int],
     "mbk_res_bwd32": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                      c_void_p],
+                      c_int, c_void_p],
     "mbk_res_fwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_int, c_int, c_int, c_void_p],
+    "mbk_res_fwd16_stage": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                            c_void_p],
     "mbk_res_blk32_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                           c_void_p],
     "mbk_res_bwd16_partial_floats": [c_int],
     "mbk_res_bwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
-                      c_void_p],
+                      c_int, c_void_p],
     # gridnet.hip
     "mbk_bits_grid": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_pool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
@@ -166,16 +172,47 @@ def kernels():
     return _kern
 
 
+# Policy gate (runtime/engine.h EngineConfig::policy_gate): while a GPU actor runtime has
+# registered its gate flag (set_policy_gate, after every policy graph is captured), each
+# kernel launcher called from Python first makes its stream (the launchers' last argument)
+# wait for the flag to read 0, i.e. for the in-flight policy step's kernels to finish. The
+# policy steps themselves run from captured graphs in the engine and never pass through here.
+# (Process-wide, not per thread: custom autograd backward nodes run on torch's device thread.)
+_gate_ptr = [None]
+
+
+def set_policy_gate(ptr: int | None) -> None:
+    _gate_ptr[0] = ptr or None
+
+
+def _gate_launch(lib, fn):
+    wait = lib.mbk_stream_wait_zero
+
+    def call(*args):
+        g = _gate_ptr[0]
+        if g is not None:
+            check(wait(g, args[-1]), "stream_wait_zero (policy gate)")
+        return fn(*args)
+
+    return call
+
+
 class _Checked:
     """Only signature-declared launchers are reachable (ctypes' default int
     conversion would silently truncate 64-bit device pointers)."""
 
     def __init__(self, lib):
         self._lib = lib
+        # every launcher takes its hipStream_t last (c_void_p); the query / setter helpers
+        # (int-returning *_parts, cu budget) do not launch and are not gated
+        self._gated = {n: _gate_launch(lib, getattr(lib, n)) for n, a in _SIGS.items()
+                       if a and a[-1] is c_void_p and n != "mbk_stream_wait_zero"}
 
     def __getattr__(self, name):
         if name not in _SIGS:
             raise AttributeError(f"{name}: no ctypes signature declared in _native._SIGS")
+        if _gate_ptr[0] is not None and name in self._gated:
+            return self._gated[name]
         return getattr(self._lib, name)
 
 

@@ -185,68 +185,6 @@ __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
 // read traffic), weights are e4m3 with a power-of-two per-output-channel scale, and the
 // MFMA is v_mfma_f32_16x16x32_fp8_fp8 (same lane map as the bf16 form). Inference only.
 
-// max_pool2d(3, 2, 1) of the workgroup's conv outputs staged in LDS (otile [(im*H+y)*W+x]
-// [OSTR] bf16) -> pooled y + per-channel argmax (ky*3+kx, first maximum in scan order as
-// ATen). Branch-free: the centre tap (always inside the map) seeds the max, the later taps
-// replace it only when strictly greater and the earlier ones (visited last to first) also
-// when equal, which leaves the smallest maximising tap; out-of-map taps read as -inf.
-// Index maths by float reciprocals (exact: pixel counts are tiny, see index_math_ok).
-template <int COUT, int OSTR>
-__device__ __forceinline__ void pool_tile(const bf16* __restrict__ otile, int H, int W, int nimg,
-                                          size_t obase, bf16* __restrict__ y,
-                                          uint8_t* __restrict__ pool_idx, int tid) {
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1, HoWo = Ho * Wo;
-  constexpr int C4 = COUT / 4;
-  const int tot = nimg * HoWo * C4;
-  const float inv_howo = 1.f / (float)HoWo, inv_wo = 1.f / (float)Wo;
-  for (int e = tid; e < tot; e += kThreads) {
-    const int c4 = e % C4, p = e / C4;
-    const int im = (int)(((float)p + 0.5f) * inv_howo), r = p - im * HoWo;
-    const int oy = (int)(((float)r + 0.5f) * inv_wo), ox = r - oy * Wo;
-    const int cy = 2 * oy, cx = 2 * ox;
-    const bf16* base = otile + ((im * H + cy) * W + cx) * OSTR + 4 * c4;
-    auto tap = [&](int dy, int dx, float v[4]) {
-      const bool ok = cy + dy >= 0 && cy + dy < H && cx + dx >= 0 && cx + dx < W;
-      const uint2 u2 = *(const uint2*)(base + (ok ? (dy * W + dx) * OSTR : 0));
-      v[0] = __uint_as_float(u2.x << 16);
-      v[1] = __uint_as_float(u2.x & 0xFFFF0000u);
-      v[2] = __uint_as_float(u2.y << 16);
-      v[3] = __uint_as_float(u2.y & 0xFFFF0000u);
-      if (!ok) v[0] = v[1] = v[2] = v[3] = -INFINITY;
-    };
-    float mx[4];
-    int am[4];
-    tap(0, 0, mx);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) am[j] = 4;
-#pragma unroll
-    for (int t = 5; t < 9; ++t) {  // after the centre in scan order: strictly greater
-      float v[4];
-      tap(t / 3 - 1, t % 3 - 1, v);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (v[j] > mx[j]) { mx[j] = v[j]; am[j] = t; }
-    }
-#pragma unroll
-    for (int t = 3; t >= 0; --t) {  // before the centre, last to first: greater or equal
-      float v[4];
-      tap(t / 3 - 1, t % 3 - 1, v);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (v[j] >= mx[j]) { mx[j] = v[j]; am[j] = t; }
-    }
-    const size_t oi = obase + (size_t)p * COUT + 4 * c4;
-    const uint32_t o0 = (uint32_t)__bfloat16_as_ushort(f2bf(mx[0])) |
-                        ((uint32_t)__bfloat16_as_ushort(f2bf(mx[1])) << 16);
-    const uint32_t o1 = (uint32_t)__bfloat16_as_ushort(f2bf(mx[2])) |
-                        ((uint32_t)__bfloat16_as_ushort(f2bf(mx[3])) << 16);
-    *(uint2*)(y + oi) = make_uint2(o0, o1);
-    if (pool_idx)
-      *(uint32_t*)(pool_idx + oi) =
-          (uint32_t)am[0] | ((uint32_t)am[1] << 8) | ((uint32_t)am[2] << 16) | ((uint32_t)am[3] << 24);
-  }
-}
-
 template <int CIN, int COUT, bool BITS, bool F8, bool UNPOOL = false>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -486,7 +424,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       __syncthreads();
       // ---- max_pool2d(kernel 3, stride 2, pad 1), 4 channels per thread
       const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-      pool_tile<COUT, OSTR>(otile, H, W, nimg, (size_t)img0 * Ho * Wo * COUT, a.y, a.pool_idx,
+      mbk::pool_tile<COUT, OSTR, kThreads>(otile, H, W, nimg, (size_t)img0 * Ho * Wo * COUT, a.y, a.pool_idx,
                             tid);
     }
     __syncthreads();  // tile / otile reads done before the next group is staged
@@ -661,7 +599,7 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
     if (a.pool) {
       __syncthreads();
       const int Ho = (H + 1) >> 1, Wo = W >> 1;
-      pool_tile<COUT, OSTR>(otile, H, W, nimg, (size_t)img0 * Ho * Wo * COUT, a.y, a.pool_idx,
+      mbk::pool_tile<COUT, OSTR, kThreads>(otile, H, W, nimg, (size_t)img0 * Ho * Wo * COUT, a.y, a.pool_idx,
                             tid);
       __syncthreads();  // otile reads done before the next group overwrites it
     }

@@ -95,3 +95,11 @@ extern "C" int mbk_multi_copy(const MbkCopySeg* segs, int n, hipStream_t stream)
   hipLaunchKernelGGL(multi_copy_kernel, grid, dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }
+
+// Learner-side half of the engine's policy gate (runtime/engine.h EngineConfig::policy_gate):
+// `stream` waits until the flag reads 0 (no policy step's kernels in flight) before its next
+// launch. A stream wait-value packet, polled by the command processor.
+extern "C" int mbk_stream_wait_zero(const void* flag, hipStream_t stream) {
+  return (int)hipStreamWaitValue32(stream, const_cast<void*>(flag), 0u, hipStreamWaitValueEq,
+                                   0xFFFFFFFFu);
+}

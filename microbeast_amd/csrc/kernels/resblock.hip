@@ -411,9 +411,19 @@ struct ResFwdArgs {
   const bf16* w[4];              // packed fwd weights [16][5][32] of conv0..conv3
   const float* b[4];             // fp32 biases
   int N, H, W, imgs;
+  // STAGE: the next stage's conv (16 -> 32, no input relu) + max_pool2d(3, 2, 1) on y1 while
+  // it is in LDS: ps [N][Ho][Wo][32] pooled output, pidx its argmax bytes (may be null)
+  const bf16* ws;                // packed fwd weights [32][5][32]
+  const float* bs;
+  bf16* ps;
+  uint8_t* pidx;
 };
 
-template <int WC>
+// STAGE: + the next ConvSequence's conv and pool (conv.hip conv_fwd<16, 32> with its pooled
+// epilogue, bit-identical): its input y1 never goes back through HBM and the 8x8 maps'
+// launch (profile 20: ~1.5 ms per 524K frames, latency-bound at 4 images per group) is gone.
+// The pre-pool staging tile aliases Tu (relu(u1) is dead after conv3).
+template <int WC, bool STAGE>
 __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
@@ -506,8 +516,57 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
         const uint2 out = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         *(uint2*)(gout + (gpix0 + m) * C + 4 * g) = out;
         if (inner) *(uint2*)(Tu + o) = make_uint2(relu2(out.x), relu2(out.y));
-        else if (l == 1) *(uint2*)(Tx + o) = out;  // y0 replaces p as the residual stream
+        else if (l == 1 || STAGE) *(uint2*)(Tx + o) = out;  // y0 (y1) replaces the stream
       }
+      __syncthreads();
+    }
+    if constexpr (STAGE) {
+      // ---- next stage's conv (16 -> 32) over y1 in Tx -> bf16 staging (Tu) -> pooled output
+      constexpr int NB = 2, OSTR = 2 * C + 4;
+      bf16* otile = (bf16*)Tu;
+      Frag8 ws[NCH][NB];  // L2 reads per round (10 KB, every workgroup): keeps the persistent
+      float bsv[NB][4];   // registers at the 4-layer set (occupancy 3 waves / SIMD)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const uint4* wp = (const uint4*)(a.ws + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) ws[c][nb].u = wp[c * 4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bsv[nb][i] = a.bs[nb * 16 + 4 * g + i];
+      }
+      for (int pb = wave; pb < nblk; pb += kThreads / 64) {
+        const int m = pb * 16 + li;
+        const bool valid = m < M;
+        const int mm = valid ? m : 0;
+        const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+        const char* bp = Tx + ((im * Hp + y) * Wp + x) * PIXB;
+        f32x4 acc[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          Frag8 av;
+          av.u = *(const uint4*)(bp + coff[c]);
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ws[c][nb].v, av.v, acc[nb], 0, 0, 0);
+        }
+        if (!valid) continue;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          *(uint2*)(otile + m * OSTR + nb * 16 + 4 * g) =
+              make_uint2(pack2(acc[nb][0] + bsv[nb][0], acc[nb][1] + bsv[nb][1]),
+                         pack2(acc[nb][2] + bsv[nb][2], acc[nb][3] + bsv[nb][3]));
+      }
+      __syncthreads();
+      const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+      mbk::pool_tile<2 * C, OSTR, kThreads>(otile, H, W, nimg, (size_t)img0 * Ho * Wo * 2 * C,
+                                            a.ps, a.pidx, tid);
+      __syncthreads();  // Tu / Tx reads done before the next round restages them
+      // (Tu's halo ring, which the staging overwrote, is never read before conv0 rewrites the
+      // interior... the halo must be zero for conv1's taps: restored below)
+      for (int e = tid; e < tb / 16; e += kThreads) ((uint4*)Tu)[e] = make_uint4(0, 0, 0, 0);
       __syncthreads();
     }
   }
@@ -927,20 +986,49 @@ size_t resf_smem(int imgs, int H, int W) {
 
 }  // namespace
 
+static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream);
+
 // Forward of both residual blocks of a 16-channel stage (see res_fwd16_kernel).
 extern "C" int mbk_res_fwd16(const void* p, void* u0, void* y0, void* u1, void* y1,
                              const void* const* w, const float* const* b, int N, int H, int W,
                              int imgs, hipStream_t stream) {
+  ResFwdArgs a{(const bf16*)p, (bf16*)u0, (bf16*)y0, (bf16*)u1, (bf16*)y1,
+               {(const bf16*)w[0], (const bf16*)w[1], (const bf16*)w[2], (const bf16*)w[3]},
+               {b[0], b[1], b[2], b[3]}, N, H, W, imgs, nullptr, nullptr, nullptr, nullptr};
+  return res_fwd16_launch(a, stream);
+}
+
+// mbk_res_fwd16 + the next stage's conv (16 -> 32, packed fwd weights ws, bias bs) and
+// max_pool2d(3, 2, 1): ps [N][(H+1)/2][(W+1)/2][32] bf16, pidx the same shape of argmax
+// bytes (null: not written); conv.hip's pooled conv_fwd results bit for bit.
+extern "C" int mbk_res_fwd16_stage(const void* p, void* u0, void* y0, void* u1, void* y1,
+                                   const void* const* w, const float* const* b, const void* ws,
+                                   const float* bs, void* ps, void* pidx, int N, int H, int W,
+                                   int imgs, hipStream_t stream) {
+  if (!ws || !bs || !ps) return (int)hipErrorInvalidValue;
+  ResFwdArgs a{(const bf16*)p, (bf16*)u0, (bf16*)y0, (bf16*)u1, (bf16*)y1,
+               {(const bf16*)w[0], (const bf16*)w[1], (const bf16*)w[2], (const bf16*)w[3]},
+               {b[0], b[1], b[2], b[3]}, N, H, W, imgs, (const bf16*)ws, bs, (bf16*)ps,
+               (uint8_t*)pidx};
+  return res_fwd16_launch(a, stream);
+}
+
+static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
+  const int N = a.N, H = a.H, W = a.W, imgs = a.imgs;
   if (N <= 0) return 0;
   if (imgs < 1 || H * W > 1024 || (int64_t)imgs * H * W >= (int64_t(1) << 22))
     return (int)hipErrorInvalidValue;
   const size_t sm = resf_smem(imgs, H, W);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  ResFwdArgs a{(const bf16*)p, (bf16*)u0, (bf16*)y0, (bf16*)u1, (bf16*)y1,
-               {(const bf16*)w[0], (const bf16*)w[1], (const bf16*)w[2], (const bf16*)w[3]},
-               {b[0], b[1], b[2], b[3]}, N, H, W, imgs};
-  auto kfn = W == 8 ? res_fwd16_kernel<8> : W == 5 ? res_fwd16_kernel<5>
-           : W == 12 ? res_fwd16_kernel<12> : W == 4 ? res_fwd16_kernel<4> : res_fwd16_kernel<0>;
+  const bool st = a.ws != nullptr;
+  // the stage conv's pre-pool staging [imgs*H*W][36] bf16 lives in Tu
+  if (st && (size_t)imgs * H * W * (2 * C + 4) * 2 > sm / 2) return (int)hipErrorInvalidValue;
+  auto kfn = st ? (W == 8 ? res_fwd16_kernel<8, true> : W == 5 ? res_fwd16_kernel<5, true>
+                   : W == 12 ? res_fwd16_kernel<12, true> : W == 4 ? res_fwd16_kernel<4, true>
+                   : res_fwd16_kernel<0, true>)
+                : (W == 8 ? res_fwd16_kernel<8, false> : W == 5 ? res_fwd16_kernel<5, false>
+                   : W == 12 ? res_fwd16_kernel<12, false> : W == 4 ? res_fwd16_kernel<4, false>
+                   : res_fwd16_kernel<0, false>);
   if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   static int cus = 0;
@@ -977,7 +1065,7 @@ extern "C" int64_t mbk_res_bwd16_partial_floats(int nparts) {
 extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* dx,
                              const void* w1t, const void* w0t, float* partial, int nparts,
                              float* dw1, float* db1, float* dw0, float* db0, int N, int H, int W,
-                             int imgs, hipStream_t stream) {
+                             int imgs, int accumulate, hipStream_t stream) {
   if (N <= 0) return 0;
   if (nparts < 1 || nparts != mbk_res_bwd16_parts(N, H, W, imgs)) return (int)hipErrorInvalidValue;
   const size_t sm = res_smem(imgs, H, W);
@@ -991,9 +1079,9 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
   hipLaunchKernelGGL(kfn, dim3(nparts), dim3(kThreads), sm, stream, a);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, 0, stream);
+  rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, accumulate, stream);
   if (rc) return rc;
-  return mbk_wgrad_reduce(partial + lstride, nparts, C, C, C, dw0, db0, 0, stream);
+  return mbk_wgrad_reduce(partial + lstride, nparts, C, C, C, dw0, db0, accumulate, stream);
 }
 
 // Partial-row PAIRS mbk_res_bwd32 writes (= its grid: one 8-wave workgroup per CU);
@@ -1023,7 +1111,7 @@ extern "C" int64_t mbk_res_bwd32_partial_floats(int nparts) {
 extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* dx,
                              const void* w1t, const void* w0t, float* partial, int nparts,
                              float* dw1, float* db1, float* dw0, float* db0, int N, int H, int W,
-                             int imgs, hipStream_t stream) {
+                             int imgs, int accumulate, hipStream_t stream) {
   if (N <= 0) return 0;
   if (nparts < 1 || nparts != mbk_res_bwd32_parts(N, H, W, imgs)) return (int)hipErrorInvalidValue;
   const size_t sm = res32b_smem(imgs, H, W);
@@ -1038,9 +1126,9 @@ extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* 
   hipLaunchKernelGGL(kfn, dim3(nparts), dim3(kT32), sm, stream, a);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
-  rc = mbk_wgrad_reduce(partial, nparts, C32, C32, C32, dw1, db1, 0, stream);
+  rc = mbk_wgrad_reduce(partial, nparts, C32, C32, C32, dw1, db1, accumulate, stream);
   if (rc) return rc;
-  return mbk_wgrad_reduce(partial + lstride, nparts, C32, C32, C32, dw0, db0, 0, stream);
+  return mbk_wgrad_reduce(partial + lstride, nparts, C32, C32, C32, dw0, db0, accumulate, stream);
 }
 
 // One 32-channel residual block's forward (see res_blk32_kernel): u = conv0(relu x),

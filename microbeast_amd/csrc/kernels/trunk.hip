@@ -63,27 +63,46 @@ __device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0
 template <int C>
 struct TG {
   static constexpr int PIXB = C * 2 + 16;
+  static constexpr int PIXB8 = C + 8;  // fp8 (e4m3) tile pixel stride, as conv.hip's fp8 tile
   static constexpr int NCH = C == 16 ? 5 : 9;
 };
 
 // zero the halo ring of a halo'd tile [nimg][(H+2)][(W+2)] of PIXB-byte pixels (index math
-// by float reciprocals: exact for these tiny ranges, no runtime integer division)
+// by float reciprocals: exact for these tiny ranges, no runtime integer division); 16-byte
+// stores, or 8-byte ones for the fp8 tiles (PIXB = C + 8)
 template <int PIXB>
 __device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W) {
   const int Hp = H + 2, Wp = W + 2;
   const int per = 2 * Wp + 2 * H;  // halo pixels per image
-  constexpr int q16 = PIXB / 16;
-  const int tot = nimg * per * q16;
+  constexpr int U = PIXB % 16 == 0 ? 16 : 8;
+  constexpr int qn = PIXB / U;
+  const int tot = nimg * per * qn;
   const float inv_per = 1.f / (float)per;
   for (int e = threadIdx.x; e < tot; e += kThreads) {
-    const int r = e / q16, q = e - r * q16;  // q16 is a compile-time constant
+    const int r = e / qn, q = e - r * qn;  // qn is a compile-time constant
     const int im = (int)(((float)r + 0.5f) * inv_per), k = r - im * per;
     int py, px;
     if (k < Wp) { py = 0; px = k; }
     else if (k < 2 * Wp) { py = Hp - 1; px = k - Wp; }
     else { const int j = k - 2 * Wp; py = 1 + (j >> 1); px = (j & 1) ? Wp - 1 : 0; }
-    *(uint4*)(t + ((im * Hp + py) * Wp + px) * PIXB + q * 16) = make_uint4(0, 0, 0, 0);
+    char* p = t + ((im * Hp + py) * Wp + px) * PIXB + q * U;
+    if constexpr (U == 16) *(uint4*)p = make_uint4(0, 0, 0, 0);
+    else *(uint2*)p = make_uint2(0, 0);
   }
+}
+
+// 4 floats -> 4 OCP e4m3 bytes, round-to-nearest-even saturated to +-448 (conv.hip's
+// cvt_fp8x4: the per-layer fp8 kernel's staging conversion, so the fused fp8 trunk matches it)
+__device__ __forceinline__ uint32_t fp8x4(float a, float b, float c, float d) {
+  auto sat = [](float v) { return fminf(fmaxf(v, -448.f), 448.f); };
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(d), w, true);
+  return (uint32_t)w;
+}
+// 4 bf16 (two packed words) -> e4m3, optionally through relu
+__device__ __forceinline__ uint32_t bf16x4_fp8(uint2 o, bool relu) {
+  if (relu) o = make_uint2(relu2(o.x), relu2(o.y));
+  return fp8x4(lo_f(o.x), hi_f(o.x), lo_f(o.y), hi_f(o.y));
 }
 
 // conv3x3 (pad 1) of a halo'd LDS tile. Output either into a halo'd tile (with optional
@@ -145,23 +164,51 @@ __device__ __forceinline__ void wfetch(const bf16* gw, int cin, int cout, uint4 
     }
   }
 }
+// the same for e4m3 packed weights [COUT][NCH][32] bytes (conv.hip conv_pack_fp8 layout):
+// 8 bytes per (chunk, block) fragment
+__device__ __forceinline__ void wfetch8(const uint8_t* gw, int cin, int cout, long w[kWFrag]) {
+  typedef const __attribute__((address_space(1))) long* GL;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int nch = cin == 16 ? TG<16>::NCH : TG<32>::NCH, nb = cout / 16;
+#pragma unroll
+  for (int k = 0; k < kWFrag; ++k) {
+    const int c = k / 2, b = k % 2;
+    if (c < nch && b < nb) w[k] = ((GL)(gw + ((b * 16 + li) * nch * 32 + g * 8)))[c * 4];
+  }
+}
 
-template <int CIN, int COUT, bool RELU, int MODE, bool WLDS>
+// F8 (fp8 trunk, conv.hip's per-layer fp8 numerics): the input tile holds e4m3 activations
+// (pixel stride CIN + 8, already relu'd by their producer, so RELU is false), wreg8 holds the
+// lane's e4m3 weight fragments, acc is dequantised by the per-output-channel wscale, and
+//   MODE OUT_TILE_RELU writes fp8(relu(bf16(v))) into an fp8 tile (out, stride COUT + 8);
+//   MODE OUT_TILE_ADD writes the bf16 residual stream (out) and, for cp = 1 / 2, its fp8 copy
+//   relu'd / as is into the fp8 tile at out8 (the next conv's input).
+template <int CIN, int COUT, bool RELU, int MODE, bool WLDS, bool F8 = false>
 // in / out: byte offsets of halo'd tiles in trunk_smem (out of a MODE == OUT_STAGE call: a
 // dense bf16 staging [nimg][H][W][COUT]); weights: LDS offset (WLDS, rows of wstride bytes)
 // or this lane's fragments prefetched into registers by wfetch (wreg)
 __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_off,
                                          const uint4* wreg, int wstride,
-                                         const float* __restrict__ bias, int out) {
+                                         const float* __restrict__ bias, int out,
+                                         const long* wreg8 = nullptr,
+                                         const float* __restrict__ wscale = nullptr,
+                                         int out8 = 0, int cp = 0) {
   constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
-  constexpr int PI = TG<CIN>::PIXB, PO = TG<COUT>::PIXB;
+  constexpr int PI = F8 ? TG<CIN>::PIXB8 : TG<CIN>::PIXB;
+  constexpr int PO = (F8 && MODE == OUT_TILE_RELU) ? TG<COUT>::PIXB8 : TG<COUT>::PIXB;
+  constexpr int PO8 = TG<COUT>::PIXB8;
+  static_assert(!(F8 && (RELU || WLDS)), "fp8 tiles are stored relu'd; weights from L2");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int Hp = H + 2, Wp = W + 2, HW = H * W;
   Frag8 bw[NCH][NB];
+  long bw8[NCH][NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    if constexpr (WLDS) {
+    if constexpr (F8) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) bw8[c][nb] = wreg8[c * 2 + nb];
+    } else if constexpr (WLDS) {
       const int wr = lw_off + (nb * 16 + li) * wstride + g * 16;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) bw[c][nb].u = *(const uint4*)(trunk_smem + wr + c * 64);
@@ -171,11 +218,15 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
     }
   }
   typedef const __attribute__((address_space(1))) f32x4* GF4;
-  float bv[NB][4];
+  float bv[NB][4], wsc[NB][4];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const f32x4 b4 = ((GF4)bias)[(nb * 16 + 4 * g) / 4];
     bv[nb][0] = b4[0]; bv[nb][1] = b4[1]; bv[nb][2] = b4[2]; bv[nb][3] = b4[3];
+    if constexpr (F8) {
+      const f32x4 s4 = ((GF4)wscale)[(nb * 16 + 4 * g) / 4];
+      wsc[nb][0] = s4[0]; wsc[nb][1] = s4[1]; wsc[nb][2] = s4[2]; wsc[nb][3] = s4[3];
+    }
   }
   const int M = nimg * HW, nblk = (M + 15) >> 4;
   constexpr int NW = kThreads / 64;
@@ -198,12 +249,19 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
       const int co0 = nb * 16 + 4 * g;
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bv[nb][i];
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (F8) v[i] = acc[nb][i] * wsc[nb][i] + bv[nb][i];
+        else v[i] = acc[nb][i] + bv[nb][i];
+      }
+      const int pix = (im * Hp + y + 1) * Wp + x + 1;
       if constexpr (MODE == OUT_STAGE) {
         *(uint2*)(trunk_smem + out + (m * COUT + co0) * 2) =
             make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      } else if constexpr (F8 && MODE == OUT_TILE_RELU) {
+        *(uint32_t*)(trunk_smem + out + pix * PO + co0) =
+            bf16x4_fp8(make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3])), true);
       } else {
-        char* p = trunk_smem + out + (((im * Hp + y + 1) * Wp + x + 1) * PO + co0 * 2);
+        char* p = trunk_smem + out + (pix * PO + co0 * 2);
         if constexpr (MODE == OUT_TILE_ADD) {
           const uint2 ad = *(const uint2*)p;
           v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
@@ -211,6 +269,8 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
         uint2 o = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
         if constexpr (MODE == OUT_TILE_RELU) o = make_uint2(relu2(o.x), relu2(o.y));
         *(uint2*)p = o;
+        if constexpr (F8)
+          if (cp) *(uint32_t*)(trunk_smem + out8 + pix * PO8 + co0) = bf16x4_fp8(o, cp == 1);
       }
     }
   };
@@ -235,7 +295,18 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
       if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
       else { tap = c; ch0 = 8 * g; }
       const int tapc = tap < 9 ? tap : 8;
-      const int toff = ((tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2;
+      const int toff = ((tapc / 3) * Wp + (tapc % 3)) * PI + (F8 ? ch0 : ch0 * 2);
+      if constexpr (F8) {
+        long a8[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) a8[j] = *(const long*)(trunk_smem + base[j] + toff);
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bw8[c][nb], a8[j], acc[j][nb], 0, 0, 0);
+        continue;
+      }
       Frag8 a[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -256,9 +327,11 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
   }
 }
 
-// max_pool2d(3, 2, 1) of staging [nimg][H][W][C] into the interior of a halo'd tile
-template <int C>
-__device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg, char* out) {
+// max_pool2d(3, 2, 1) of staging [nimg][H][W][C] into the interior of a halo'd tile (F8: and
+// fp8(relu(.)) into the fp8 tile out8, the next residual block's conv input)
+template <int C, bool F8 = false>
+__device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg, char* out,
+                                         char* out8 = nullptr) {
   constexpr int PO = TG<C>::PIXB, C4 = C / 4;
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1, HWo = Ho * Wo;
   const int tot = nimg * HWo * C4;
@@ -279,8 +352,10 @@ __device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg
         mx[2] = fmaxf(mx[2], lo_f(v.y)); mx[3] = fmaxf(mx[3], hi_f(v.y));
       }
     }
-    *(uint2*)(out + (((im * (Ho + 2) + oy + 1) * (Wo + 2) + ox + 1) * PO + c4 * 8)) =
-        make_uint2(pack2(mx[0], mx[1]), pack2(mx[2], mx[3]));
+    const int pix = (im * (Ho + 2) + oy + 1) * (Wo + 2) + ox + 1;
+    const uint2 o = make_uint2(pack2(mx[0], mx[1]), pack2(mx[2], mx[3]));
+    *(uint2*)(out + pix * PO + c4 * 8) = o;
+    if constexpr (F8) *(uint32_t*)(out8 + pix * TG<C>::PIXB8 + c4 * 4) = bf16x4_fp8(o, true);
   }
 }
 
@@ -297,6 +372,8 @@ struct TrunkArgs {
   float* v_out;
   const bf16* w[14];    // packed fwd weights of layers 1..14 (HipEncoder order)
   const float* b[14];
+  const uint8_t* w8[14];  // fp8 trunk: e4m3 packed weights (conv_pack_fp8) ...
+  const float* ws[14];    // ... and their per-output-channel dequant scales
   int N, H0, W0;
   int tni;              // images per workgroup iteration
   int r1_bytes;         // region sizes (host computed)
@@ -378,6 +455,45 @@ __device__ __forceinline__ void trunk_fc(const char* x2, int H2, int W2, int nim
   }
 }
 
+// group input (stage-0 pooled output, bf16 NHWC) -> interior of the halo'd X0 tile; F8: also
+// fp8(relu(x)) into the fp8 tile f (layer 1's input)
+template <bool F8>
+__device__ __forceinline__ void load_input(const TrunkArgs& a, int img0, int nimg, char* x0,
+                                           char* f) {
+  constexpr int PX = TG<16>::PIXB, PX8 = TG<16>::PIXB8;
+  const int H0 = a.H0, W0 = a.W0;
+  const int tot = nimg * H0 * W0 * 2;  // 16-byte chunks
+  const uint4* src = (const uint4*)(a.x + (size_t)img0 * H0 * W0 * 16);
+  const float ihw = 1.f / (float)(H0 * W0), iw = 1.f / (float)W0;
+  for (int e = threadIdx.x; e < tot; e += kThreads) {
+    const int q = e & 1, p = e >> 1;
+    const int im = (int)(((float)p + 0.5f) * ihw), r = p - im * H0 * W0;
+    const int y = (int)(((float)r + 0.5f) * iw), x = r - y * W0;
+    const int pix = (im * (H0 + 2) + y + 1) * (W0 + 2) + x + 1;
+    const uint4 v = src[e];
+    *(uint4*)(x0 + pix * PX + q * 16) = v;
+    if constexpr (F8)
+      *(uint2*)(f + pix * PX8 + q * 8) = make_uint2(bf16x4_fp8(make_uint2(v.x, v.y), true),
+                                                    bf16x4_fp8(make_uint2(v.z, v.w), true));
+  }
+}
+
+// X2 tile interior -> global NHWC trunk output (if requested)
+__device__ __forceinline__ void store_output(const TrunkArgs& a, int img0, int nimg, int H2,
+                                             int W2, const char* x2) {
+  if (!a.y) return;
+  constexpr int PX = TG<32>::PIXB;
+  const int tot = nimg * H2 * W2 * 4;
+  uint4* dst = (uint4*)(a.y + (size_t)img0 * H2 * W2 * 32);
+  const float ihw = 1.f / (float)(H2 * W2), iw = 1.f / (float)W2;
+  for (int e = threadIdx.x; e < tot; e += kThreads) {
+    const int q = e & 3, p = e >> 2;
+    const int im = (int)(((float)p + 0.5f) * ihw), r = p - im * H2 * W2;
+    const int y = (int)(((float)r + 0.5f) * iw), x = r - y * W2;
+    dst[e] = *(const uint4*)(x2 + ((im * (H2 + 2) + y + 1) * (W2 + 2) + x + 1) * PX + q * 16);
+  }
+}
+
 // LDSW: weights staged in LDS (double-buffered) vs read through L2. FC: the fused trunk
 // head runs after the last conv; the next group's first weight fetch then waits until after
 // it (keeps the prefetch registers free across the head: no spills).
@@ -424,20 +540,9 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
     // ---- stage 0: X0 <- input (R1), U0 halo zero (R2)
-    {
-      constexpr int PX = TG<16>::PIXB;
-      const int tot = nimg * H0 * W0 * 2;  // 16-byte chunks
-      const uint4* src = (const uint4*)(a.x + (size_t)img0 * H0 * W0 * 16);
-      const float ihw = 1.f / (float)(H0 * W0), iw = 1.f / (float)W0;
-      for (int e = threadIdx.x; e < tot; e += kThreads) {
-        const int q = e & 1, p = e >> 1;
-        const int im = (int)(((float)p + 0.5f) * ihw), r = p - im * H0 * W0;
-        const int y = (int)(((float)r + 0.5f) * iw), x = r - y * W0;
-        *(uint4*)(R1 + ((im * (H0 + 2) + y + 1) * (W0 + 2) + x + 1) * PX + q * 16) = src[e];
-      }
-      zero_halo<PX>(R1, nimg, H0, W0);
-      zero_halo<PX>(R2, nimg, H0, W0);
-    }
+    load_input<false>(a, img0, nimg, R1, nullptr);
+    zero_halo<TG<16>::PIXB>(R1, nimg, H0, W0);
+    zero_halo<TG<16>::PIXB>(R2, nimg, H0, W0);
     __syncthreads();
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
@@ -480,18 +585,89 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
       wfetch(a.w[0], tail_cin(0), tail_cout(0), wnext);  // next group's layer 0
     }
     // ---- X2 interior -> global NHWC
-    if (a.y) {
-      constexpr int PX = TG<32>::PIXB;
-      const int tot = nimg * H2 * W2 * 4;
-      uint4* dst = (uint4*)(a.y + (size_t)img0 * H2 * W2 * 32);
-      const float ihw = 1.f / (float)(H2 * W2), iw = 1.f / (float)W2;
-      for (int e = threadIdx.x; e < tot; e += kThreads) {
-        const int q = e & 3, p = e >> 2;
-        const int im = (int)(((float)p + 0.5f) * ihw), r = p - im * H2 * W2;
-        const int y = (int)(((float)r + 0.5f) * iw), x = r - y * W2;
-        dst[e] = *(const uint4*)(R1 + ((im * (H2 + 2) + y + 1) * (W2 + 2) + x + 1) * PX + q * 16);
-      }
+    store_output(a, img0, nimg, H2, W2, R1);
+    __syncthreads();
+  }
+}
+
+// fp8 trunk (BASELINE config 5's fp8 acting path, inference): the 14 convs on
+// v_mfma_f32_16x16x32_fp8_fp8, numerics of the per-layer fp8 kernel (conv.hip F8: e4m3
+// activations converted from the bf16-rounded producer output, relu before the
+// conversion, per-output-channel weight scales, bf16 outputs / residual stream). LDS:
+//   R1: residual stream X (bf16, halo'd): the residual adds and the trunk output read it
+//   R2: U (inner activation, fp8 relu'd) / stage conv staging (dense bf16)
+//   R3: F = fp8 copy of X as the next conv consumes it (relu'd for a residual block, as is
+//       for the next stage's conv), written by the producer's epilogue / the pool
+// so each conv reads 8-byte fragments with no per-tap relu. Weights are fetched one layer
+// ahead into registers (half the VGPRs of the bf16 prefetch).
+__global__ __launch_bounds__(kThreads) void trunk_tail8_kernel(TrunkArgs a) {
+  char* smem = trunk_smem;
+  const int oR1 = 0, oR2 = a.r1_bytes, oF = 2 * a.r1_bytes;
+  char* R1 = smem + oR1;
+  char* R2 = smem + oR2;
+  char* F = smem + oF;
+  const int H0 = a.H0, W0 = a.W0, H1 = (H0 + 1) >> 1, W1 = (W0 + 1) >> 1;
+  const int H2 = (H1 + 1) >> 1, W2 = (W1 + 1) >> 1;
+  const int TNI = a.tni;
+  const int ngroups = (a.N + TNI - 1) / TNI;
+  long wnext[kWFrag];
+  wfetch8(a.w8[0], tail_cin(0), tail_cout(0), wnext);
+#define TAIL8(l, CI, CO, MODE, IN, H_, W_, OUT, CP)                                    \
+  do {                                                                               \
+    long wc[kWFrag];                                                                 \
+    _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];             \
+    const int ln = ((l) + 1) % 14;                                                   \
+    wfetch8(a.w8[ln], tail_cin(ln), tail_cout(ln), wnext);                           \
+    conv_lds<CI, CO, false, MODE, false, true>(IN, H_, W_, nimg, 0, nullptr, 0, a.b[l], \
+                                               OUT, wc, a.ws[l], oF, CP);            \
+  } while (0)
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
+    // ---- stage 0: X0 <- input (R1), F <- fp8(relu(X0)); halos of R1 / U (R2) / F
+    load_input<true>(a, img0, nimg, R1, F);
+    zero_halo<TG<16>::PIXB>(R1, nimg, H0, W0);
+    zero_halo<TG<16>::PIXB8>(R2, nimg, H0, W0);
+    zero_halo<TG<16>::PIXB8>(F, nimg, H0, W0);
+    __syncthreads();
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      TAIL8(2 * rb, 16, 16, OUT_TILE_RELU, oF, H0, W0, oR2, 0);
+      __syncthreads();
+      TAIL8(2 * rb + 1, 16, 16, OUT_TILE_ADD, oR2, H0, W0, oR1, rb == 0 ? 1 : 2);
+      __syncthreads();
     }
+    // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1) + F
+    TAIL8(4, 16, 32, OUT_STAGE, oF, H0, W0, oR2, 0);
+    __syncthreads();
+    pool_lds<32, true>((const bf16*)R2, H0, W0, nimg, R1, F);
+    zero_halo<TG<32>::PIXB>(R1, nimg, H1, W1);
+    zero_halo<TG<32>::PIXB8>(F, nimg, H1, W1);
+    __syncthreads();
+    zero_halo<TG<32>::PIXB8>(R2, nimg, H1, W1);  // U1 layout (staging consumed)
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      TAIL8(5 + 2 * rb, 32, 32, OUT_TILE_RELU, oF, H1, W1, oR2, 0);
+      __syncthreads();
+      TAIL8(6 + 2 * rb, 32, 32, OUT_TILE_ADD, oR2, H1, W1, oR1, rb == 0 ? 1 : 2);
+      __syncthreads();
+    }
+    // ---- stage 2
+    TAIL8(9, 32, 32, OUT_STAGE, oF, H1, W1, oR2, 0);
+    __syncthreads();
+    pool_lds<32, true>((const bf16*)R2, H1, W1, nimg, R1, F);
+    zero_halo<TG<32>::PIXB>(R1, nimg, H2, W2);
+    zero_halo<TG<32>::PIXB8>(F, nimg, H2, W2);
+    __syncthreads();
+    zero_halo<TG<32>::PIXB8>(R2, nimg, H2, W2);
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      TAIL8(10 + 2 * rb, 32, 32, OUT_TILE_RELU, oF, H2, W2, oR2, 0);
+      __syncthreads();
+      TAIL8(11 + 2 * rb, 32, 32, OUT_TILE_ADD, oR2, H2, W2, oR1, rb == 0 ? 1 : 0);
+      __syncthreads();
+    }
+#undef TAIL8
+    store_output(a, img0, nimg, H2, W2, R1);
     __syncthreads();
   }
 }
@@ -503,6 +679,16 @@ size_t region_bytes(int H0, int W0, int TNI) {
   r = std::max(r, (size_t)TNI * (H1 + 2) * (W1 + 2) * TG<32>::PIXB);          // X1 / U1
   r = std::max(r, (size_t)TNI * (H2 + 2) * (W2 + 2) * TG<32>::PIXB);          // X2 / U2
   return (r + 15) & ~(size_t)15;
+}
+// the fp8 trunk's F tile (fp8 X copy) at its largest stage
+size_t region8_bytes(int H0, int W0, int TNI) {
+  const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;
+  size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB8;
+  r = std::max(r, (size_t)TNI * (H1 + 2) * (W1 + 2) * TG<32>::PIXB8);
+  return (r + 15) & ~(size_t)15;
+}
+size_t trunk_smem_bytes(int H0, int W0, int TNI, size_t wb, bool f8) {
+  return 2 * region_bytes(H0, W0, TNI) + wb + (f8 ? region8_bytes(H0, W0, TNI) : 0);
 }
 
 }  // namespace
@@ -548,6 +734,23 @@ extern "C" int mbk_trunk_tail_fc(const void* x, const void* const* w, const floa
   return trunk_launch(a, N, H0, W0, stream);
 }
 
+// fp8 trunk: w8 = e4m3 packed weights of layers 1..14 (mbk_conv_pack_fp8), ws = their
+// per-output-channel dequant scales; activations in / out bf16 as mbk_trunk_tail.
+extern "C" int mbk_trunk_tail_fp8(const void* x, const void* const* w8, const float* const* ws,
+                                  const float* const* b, int N, int H0, int W0, void* y,
+                                  hipStream_t stream) {
+  TrunkArgs a{};
+  a.x = (const bf16*)x;
+  a.y = (bf16*)y;
+  for (int i = 0; i < 14; ++i) {
+    if (!w8[i] || !ws[i] || !b[i]) return (int)hipErrorInvalidValue;
+    a.w8[i] = (const uint8_t*)w8[i];
+    a.ws[i] = ws[i];
+    a.b[i] = b[i];
+  }
+  return trunk_launch(a, N, H0, W0, stream);
+}
+
 static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) {
   if (N <= 0) return 0;
   if (H0 < 1 || W0 < 1 || H0 > 16 || W0 > 16) return (int)hipErrorInvalidValue;
@@ -570,15 +773,17 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
     const char* t = std::getenv("MBK_TRUNK_TNI");
     force_tni = t ? std::atoi(t) : 0;
   }
-  const bool ldsw = variant == 1 && a.f_out == nullptr;  // the fused head uses the L2 variant
+  const bool f8 = a.w8[0] != nullptr;
+  // the fused head and the fp8 trunk use the L2 variant
+  const bool ldsw = variant == 1 && a.f_out == nullptr && !f8;
   const size_t wb = ldsw ? 2 * kWBufBytes : 0;
   int tni = 1;
-  while (tni < kMaxTNI && 2 * region_bytes(H0, W0, tni * 2) + wb <= 160 * 1024 &&
+  while (tni < kMaxTNI && trunk_smem_bytes(H0, W0, tni * 2, wb, f8) <= 160 * 1024 &&
          (N + tni * 2 - 1) / (tni * 2) >= cus)
     tni *= 2;
   if (force_tni > 0) {
     tni = std::min(force_tni, kMaxTNI);
-    while (tni > 1 && 2 * region_bytes(H0, W0, tni) + wb > 160 * 1024) tni /= 2;
+    while (tni > 1 && trunk_smem_bytes(H0, W0, tni, wb, f8) > 160 * 1024) tni /= 2;
   }
   a.tni = tni;
   // float-reciprocal pixel index math in the kernel is exact only for tni*H0*W0 < 2^16
@@ -586,11 +791,13 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
     return (int)hipErrorInvalidValue;
   const size_t r = region_bytes(H0, W0, tni);
   a.r1_bytes = (int)r;
-  const size_t sm = 2 * r + wb;
+  const size_t sm = trunk_smem_bytes(H0, W0, tni, wb, f8);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const bool fc = a.f_out != nullptr;
-  auto kfn = fc ? trunk_tail_kernel<false, true>
-                : ldsw ? trunk_tail_kernel<true, false> : trunk_tail_kernel<false, false>;
+  if (fc && f8) return (int)hipErrorInvalidValue;
+  auto kfn = f8 ? trunk_tail8_kernel
+             : fc ? trunk_tail_kernel<false, true>
+                  : ldsw ? trunk_tail_kernel<true, false> : trunk_tail_kernel<false, false>;
   if (sm > 64 * 1024)
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;

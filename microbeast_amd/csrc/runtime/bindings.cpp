@@ -247,6 +247,7 @@ PYBIND11_MODULE(_mbrt, m) {
         if (c.contains("selfplay_groups")) cfg.selfplay_groups = c["selfplay_groups"].cast<int>();
         if (c.contains("n_lanes")) cfg.n_lanes = c["n_lanes"].cast<int>();
         if (c.contains("policy_cu_every")) cfg.policy_cu_every = c["policy_cu_every"].cast<int>();
+        if (c.contains("policy_gate")) cfg.policy_gate = c["policy_gate"].cast<bool>();
         EngineBuffers buf;
         buf.obs = b["obs"].cast<uintptr_t>();
         buf.mask = b["mask"].cast<uintptr_t>();
@@ -311,6 +312,7 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
       .def("stream", &GpuEngine::stream, py::arg("lane") = 0)
       .def("failed", &GpuEngine::failed)
+      .def("gate_ptr", &GpuEngine::gate_ptr)
       .def("inject_fault", &GpuEngine::inject_fault)
       .def("error", &GpuEngine::error)
       .def("stats", [](GpuEngine& e) {

@@ -126,6 +126,10 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   }
   // work chunk: enough chunks for every worker, at least 2 envs each
   chunk_ = std::max(1, std::min(16, cfg_.envs_per_group / std::max(1, 2 * cfg_.n_threads)));
+  if (cfg_.policy_gate && cfg_.n_lanes == 1) {
+    CTOR_CHECK(hipMalloc((void**)&gate_, sizeof(uint32_t)));
+    CTOR_CHECK(hipMemset(gate_, 0, sizeof(uint32_t)));
+  }
 }
 
 GpuEngine::~GpuEngine() {
@@ -155,6 +159,7 @@ GpuEngine::~GpuEngine() {
   if (h_ep_return_) hipHostFree(h_ep_return_);
   if (h_ep_step_) hipHostFree(h_ep_step_);
   if (h_done_) hipHostFree(h_done_);
+  if (gate_) hipFree(gate_);
   for (Lane& L : lanes_) {
     if (L.stream) hipStreamDestroy(L.stream);
   }
@@ -205,6 +210,9 @@ void GpuEngine::stop() {
   workers_.clear();
   for (Lane& L : lanes_)
     if (L.stream) hipStreamSynchronize(L.stream);
+  // an enqueue that failed between the gate's set and clear must not leave the learner's
+  // stream waiting forever
+  if (gate_) hipMemset(gate_, 0, sizeof(uint32_t));
 }
 
 void GpuEngine::dispatch_env(int g) {
@@ -365,6 +373,8 @@ bool GpuEngine::enqueue_gpu(int g) {
   ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
                            st));
   if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
+  // learner launches hold from here (the H2D above is SDMA: no CUs) to the scatter's end
+  if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
   {
     const auto t0 = std::chrono::steady_clock::now();
     ENG_CHECK(hipGraphLaunch(L.graph, st));
@@ -433,6 +443,7 @@ bool GpuEngine::enqueue_gpu(int g) {
     seg[n++] = {(const void*)io.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
   }
   ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, st));
+  if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));  // (the D2H is SDMA)
   if (close_prev) {
     ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
     {

@@ -64,6 +64,11 @@ struct EngineConfig {
   // learner takes the complement on its own masked stream), so persistent learner
   // kernels and latency-critical policy kernels never compete for the same CUs
   int policy_cu_every = 0;
+  // policy gate (one lane only): the lane stream sets a device flag to 1 for the span of
+  // each policy step's kernels (stream write-value packets) and the learner's stream waits
+  // for it to read 0 before each launch (mbk_stream_wait_zero), so a policy step never
+  // queues behind more than the one learner kernel already running
+  bool policy_gate = false;
 };
 
 // Fixed-address I/O of one lane's captured policy graph (and opponent graph). The graph
@@ -132,6 +137,8 @@ class GpuEngine {
   // one LaneGraphs per lane; the opponent graph is required iff selfplay_groups > 0
   void start(const std::vector<LaneGraphs>& graphs);
   void stop();
+  // device address of the policy gate flag (0: gating off)
+  uintptr_t gate_ptr() const { return (uintptr_t)gate_; }
   // Blocks until n full slots are available (or timeout). Returns slot ids.
   std::vector<int> get_full(int n, double timeout_s);
   void stream_wait_full(uintptr_t stream, int slot);
@@ -266,6 +273,7 @@ class GpuEngine {
   void dispatch_env(int g);
   void fail(const std::string& msg);
   int chunk_;
+  uint32_t* gate_ = nullptr;  // policy gate flag (device), see EngineConfig
 };
 
 }  // namespace mb

@@ -80,6 +80,11 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
     return imgs
 
 
+def _at(t: torch.Tensor | None, i0: int) -> int | None:
+    """Device address of image i0 of an image-major tensor (None passes through)."""
+    return None if t is None else t[i0:].data_ptr()
+
+
 def _imgs_wgrad(layer: ConvLayer) -> int:
     hw = layer.H * layer.W
     xepp = 1 if layer.bits else layer.cin // 8
@@ -137,11 +142,19 @@ class HipEncoder:
         self.fused_res_bwd32 = os.environ.get("MBK_FUSED_RES32", "1") == "1"
         self.fused_res_fwd = os.environ.get("MBK_FUSED_RES_FWD", "1") == "1"
         self.fused_res_fwd32 = os.environ.get("MBK_FUSED_RES_FWD32", "1") == "1"
+        # stage-0 residual kernel also runs stage 1's conv + pool (MBK_FUSED_STAGE_FWD=0: off)
+        self.fused_stage_fwd = os.environ.get("MBK_FUSED_STAGE_FWD", "1") == "1"
+        # learner launches over at most this many images each (0: one launch per layer): the
+        # persistent per-image kernels then hold the CUs for ~0.3 ms instead of 1-3 ms, so a
+        # policy step (high-priority stream, engine policy gate) waits less behind them
+        self.chunk = int(os.environ.get("MBK_LEARN_CHUNK", "0"))
         self._partial_rb = None
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
         self.fp8 = fp8
+        # fp8 layers 1..14 in one fused launch (MBK_TRUNK8=0: the 14 per-layer fp8 launches)
+        self.fused_tail8 = os.environ.get("MBK_TRUNK8", "1") == "1"
         self.packed_fwd8 = torch.zeros(off, dtype=torch.uint8, device=device)
         self.scale8 = torch.zeros(sum(L.cout for L in self.layers), dtype=torch.float32,
                                   device=device)
@@ -152,6 +165,13 @@ class HipEncoder:
             so += L.cout
 
     # ------------------------------------------------------------ helpers
+    def _spans(self, n: int) -> list[tuple[int, int]]:
+        """Image ranges of the launches a learner kernel over n images is split into."""
+        c = self.chunk
+        if c <= 0 or n <= c:
+            return [(0, n)]
+        return [(i, min(n, i + c)) for i in range(0, n, c)]
+
     def pack(self, weights: list[torch.Tensor], with_bwd: bool) -> None:
         k = N.kernels()
         for c0 in range(0, len(self.layers), 16):  # one launch packs up to 16 layers
@@ -229,6 +249,22 @@ class HipEncoder:
                                  y.data_ptr(), N.stream_ptr()), "trunk_tail")
         return y
 
+    def _tail8(self, p: torch.Tensor, bs: list[torch.Tensor]) -> torch.Tensor:
+        """Layers 1..14 on the fused fp8 trunk kernel (trunk.hip trunk_tail8_kernel): the
+        per-layer fp8 numerics of ``_fwd8`` in one launch; p = stage-0 pooled output (bf16)."""
+        L1, Ll = self.layers[1], self.layers[-1]
+        n = p.shape[0]
+        base, sbase = self.packed_fwd8.data_ptr(), self.scale8.data_ptr()
+        wp = (ctypes.c_void_p * 14)(*[base + L.w_off for L in self.layers[1:15]])
+        sp = (ctypes.c_void_p * 14)(*[sbase + 4 * self._s_off[i] for i in range(1, 15)])
+        bp = (ctypes.c_void_p * 14)(*[b.data_ptr() for b in bs[1:15]])
+        y = torch.empty(n, Ll.H, Ll.W, Ll.cout, dtype=torch.bfloat16, device=p.device)
+        N.check(N.kernels().mbk_trunk_tail_fp8(
+            p.data_ptr(), ctypes.cast(wp, ctypes.c_void_p), ctypes.cast(sp, ctypes.c_void_p),
+            ctypes.cast(bp, ctypes.c_void_p), n, L1.H, L1.W, y.data_ptr(), N.stream_ptr()),
+            "trunk_tail_fp8")
+        return y
+
     def _fwd(self, L: ConvLayer, x, bias, add=None, mask_src=None, y_full=None, dgrad=False,
              pool_idx=None):
         n = x.shape[0]
@@ -243,11 +279,13 @@ class HipEncoder:
         Ho, Wo = ((H + 1) // 2, (W + 1) // 2) if pool else (H, W)
         y = torch.empty(n, Ho, Wo, cout, dtype=torch.bfloat16, device=x.device)
         imgs = _imgs_fwd(L, cin, cout, bits, pool)
-        N.check(N.kernels().mbk_conv_fwd(
-            x.data_ptr(), int(bits), cin, cout, w, N.ptr(bias), N.ptr(add), N.ptr(mask_src),
-            y.data_ptr(), N.ptr(y_full), N.ptr(pool_idx), n, H, W, imgs, int(relu), int(pool),
-            N.stream_ptr()),
-            "conv_fwd")
+        k = N.kernels()
+        for i0, i1 in self._spans(n):
+            N.check(k.mbk_conv_fwd(
+                _at(x, i0), int(bits), cin, cout, w, N.ptr(bias), _at(add, i0),
+                _at(mask_src, i0), _at(y, i0), _at(y_full, i0), _at(pool_idx, i0), i1 - i0, H, W,
+                imgs, int(relu), int(pool), N.stream_ptr()),
+                "conv_fwd")
         return y
 
     def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor, dp=None, pidx=None):
@@ -266,25 +304,49 @@ class HipEncoder:
             self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=x.device)
         k = N.kernels()
         st = N.stream_ptr()
-        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, N.ptr(dy), N.ptr(dp),
-                                 N.ptr(pidx), self._partial.data_ptr(), nparts, n, L.H, L.W, imgs,
-                                 int(L.relu_in), st), "conv_wgrad")
-        N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
-                                   dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
+        for c, (i0, i1) in enumerate(self._spans(n)):
+            if c:
+                nparts = k.mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, i1 - i0, L.H, L.W,
+                                                imgs, int(unpool))
+            N.check(k.mbk_conv_wgrad(_at(x, i0), int(L.bits), L.cin, L.cout, _at(dy, i0),
+                                     _at(dp, i0), _at(pidx, i0), self._partial.data_ptr(), nparts,
+                                     i1 - i0, L.H, L.W, imgs, int(L.relu_in), st), "conv_wgrad")
+            # later chunks add their sums into the gradient (fp32)
+            N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real,
+                                       L.cout, dw.data_ptr(), db.data_ptr(), int(c > 0), st),
+                    "wgrad_reduce")
 
-    def _res_fwd16(self, li: int, p: torch.Tensor, bs: list[torch.Tensor]):
+    def _res_fwd16(self, li: int, p: torch.Tensor, bs: list[torch.Tensor], stage=None):
         """Both residual blocks of a 16-channel stage in one launch (resblock.hip): returns
-        (u0, y0, u1, y1), bit-identical to four conv_fwd launches."""
+        (u0, y0, u1, y1), bit-identical to four conv_fwd launches. stage (not None): the same
+        launch also runs the next stage's conv + pool on y1 from LDS and returns
+        (u0, y0, u1, y1, (p_next, pidx_next)); stage=True also writes the argmax bytes."""
         n, H, W, C = p.shape
         outs = [torch.empty_like(p) for _ in range(4)]
         base = self.packed_fwd.data_ptr()
         wp = (ctypes.c_void_p * 4)(*[base + 2 * self.layers[li + 1 + j].w_off for j in range(4)])
         bp = (ctypes.c_void_p * 4)(*[bs[li + 1 + j].data_ptr() for j in range(4)])
-        N.check(N.kernels().mbk_res_fwd16(p.data_ptr(), *[o.data_ptr() for o in outs],
+        k = N.kernels()
+        if stage is None:
+            for i0, i1 in self._spans(n):
+                N.check(k.mbk_res_fwd16(_at(p, i0), *[_at(o, i0) for o in outs],
+                                        ctypes.cast(wp, ctypes.c_void_p),
+                                        ctypes.cast(bp, ctypes.c_void_p), i1 - i0, H, W, 4,
+                                        N.stream_ptr()), "res_fwd16")
+            return outs
+        Ln = self.layers[li + 5]
+        Ho, Wo = (H + 1) // 2, (W + 1) // 2
+        pn = torch.empty(n, Ho, Wo, Ln.cout, dtype=torch.bfloat16, device=p.device)
+        pidx = (torch.empty(n, Ho, Wo, Ln.cout, dtype=torch.uint8, device=p.device)
+                if stage else None)
+        for i0, i1 in self._spans(n):
+            N.check(k.mbk_res_fwd16_stage(_at(p, i0), *[_at(o, i0) for o in outs],
                                           ctypes.cast(wp, ctypes.c_void_p),
-                                          ctypes.cast(bp, ctypes.c_void_p), n, H, W, 4,
-                                          N.stream_ptr()), "res_fwd16")
-        return outs
+                                          ctypes.cast(bp, ctypes.c_void_p),
+                                          base + 2 * Ln.w_off, bs[li + 5].data_ptr(),
+                                          _at(pn, i0), _at(pidx, i0), i1 - i0, H, W, 4,
+                                          N.stream_ptr()), "res_fwd16_stage")
+        return (*outs, (pn, pidx))
 
     def _res_blk32(self, l0: int, x: torch.Tensor, bs: list[torch.Tensor]):
         """One 32-channel residual block (layers l0, l0+1) in one launch (resblock.hip):
@@ -295,10 +357,11 @@ class HipEncoder:
         wp = (ctypes.c_void_p * 2)(*[base + 2 * self.layers[l0 + j].w_off for j in range(2)])
         bp = (ctypes.c_void_p * 2)(*[bs[l0 + j].detach().data_ptr() for j in range(2)])
         imgs = max(1, min(16, (80 * 1024) // (2 * (H + 2) * (W + 2) * 80)))
-        N.check(N.kernels().mbk_res_blk32_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(),
-                                              ctypes.cast(wp, ctypes.c_void_p),
-                                              ctypes.cast(bp, ctypes.c_void_p), n, H, W, imgs,
-                                              N.stream_ptr()), "res_blk32_fwd")
+        for i0, i1 in self._spans(n):
+            N.check(N.kernels().mbk_res_blk32_fwd(_at(x, i0), _at(u, i0), _at(y, i0),
+                                                  ctypes.cast(wp, ctypes.c_void_p),
+                                                  ctypes.cast(bp, ctypes.c_void_p), i1 - i0, H, W,
+                                                  imgs, N.stream_ptr()), "res_blk32_fwd")
         return u, y
 
     def _res_bwd16(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
@@ -308,19 +371,20 @@ class HipEncoder:
         H, W = L0.H, L0.W
         k = N.kernels()
         imgs = max(1, min(8, (80 * 1024) // (4 * (H + 2) * (W + 2) * 48)))
-        nparts = k.mbk_res_bwd16_parts(n, H, W, imgs)
-        if nparts < 1:
-            raise RuntimeError(f"res_bwd16: unsupported shape {H}x{W}")
-        need = k.mbk_res_bwd16_partial_floats(nparts)
-        if self._partial_rb is None or self._partial_rb.numel() < need:
-            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         base = self.packed_bwd.data_ptr()
-        N.check(k.mbk_res_bwd16(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
-                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
-                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
-                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs,
-                                N.stream_ptr()), "res_bwd16")
+        for c, (i0, i1) in enumerate(self._spans(n)):
+            nparts = k.mbk_res_bwd16_parts(i1 - i0, H, W, imgs)
+            if nparts < 1:
+                raise RuntimeError(f"res_bwd16: unsupported shape {H}x{W}")
+            need = k.mbk_res_bwd16_partial_floats(nparts)
+            if self._partial_rb is None or self._partial_rb.numel() < need:
+                self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+            N.check(k.mbk_res_bwd16(_at(x, i0), _at(u, i0), _at(g, i0), _at(dx, i0),
+                                    base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                    self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
+                                    db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), i1 - i0, H, W,
+                                    imgs, int(c > 0), N.stream_ptr()), "res_bwd16")
         return dx
 
     def _res_bwd32(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
@@ -331,19 +395,20 @@ class HipEncoder:
         k = N.kernels()
         lds_kb = _RES32_LDS_KB if H * W > 4 else _RES32_LDS_KB_SMALL
         imgs = max(1, min(_RES32_PIX // (H * W), (lds_kb * 1024 - 128) // (4 * (H + 2) * (W + 2) * 80)))
-        nparts = k.mbk_res_bwd32_parts(n, H, W, imgs)
-        if nparts < 1:
-            raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")
-        need = k.mbk_res_bwd32_partial_floats(nparts)
-        if self._partial_rb is None or self._partial_rb.numel() < need:
-            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x)
         base = self.packed_bwd.data_ptr()
-        N.check(k.mbk_res_bwd32(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
-                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
-                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
-                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs,
-                                N.stream_ptr()), "res_bwd32")
+        for c, (i0, i1) in enumerate(self._spans(n)):
+            nparts = k.mbk_res_bwd32_parts(i1 - i0, H, W, imgs)
+            if nparts < 1:
+                raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")
+            need = k.mbk_res_bwd32_partial_floats(nparts)
+            if self._partial_rb is None or self._partial_rb.numel() < need:
+                self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+            N.check(k.mbk_res_bwd32(_at(x, i0), _at(u, i0), _at(g, i0), _at(dx, i0),
+                                    base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                    self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
+                                    db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), i1 - i0, H, W,
+                                    imgs, int(c > 0), N.stream_ptr()), "res_bwd32")
         return dx
 
     # ------------------------------------------------------------ passes
@@ -356,6 +421,9 @@ class HipEncoder:
         if self.fp8 and not save:
             if not prepacked:
                 self.pack_fp8([w.detach() for w in ws])
+            if self.fused_tail and self.fused_tail8:
+                p = self._fwd8(0, x, bs[0].detach())
+                return self._tail8(p, bs), []
             for st in range(len(self.layers) // 5):
                 i = 5 * st
                 p = self._fwd8(i, x, bs[i].detach())
@@ -372,15 +440,28 @@ class HipEncoder:
         saved = []
         li = 0
         n = x.shape[0]
+        nxt = None  # (p, pidx) of the next stage when the residual kernel ran its conv
         for _stage in range(len(self.layers) // 5):
             L = self.layers[li]
             Ho, Wo = (L.H + 1) // 2, (L.W + 1) // 2
             # pooled argmax (1 byte) instead of the full-resolution conv output
             pidx = (torch.empty(n, Ho, Wo, L.cout, dtype=torch.uint8, device=x.device)
                     if save else None)
-            p = self._fwd(L, x, bs[li].detach(), pool_idx=pidx)
+            if nxt is not None:  # computed by the previous stage's fused residual kernel
+                p, pidx = nxt
+                nxt = None
+            else:
+                p = self._fwd(L, x, bs[li].detach(), pool_idx=pidx)
             if self.fused_res_fwd and L.cout == 16 and p.is_cuda:
-                u0, y0, u1, y1 = self._res_fwd16(li, p, [b.detach() for b in bs])
+                Ln = self.layers[li + 5] if li + 5 < len(self.layers) else None
+                if (self.fused_stage_fwd and Ln is not None and Ln.cin == 16 and Ln.cout == 32
+                        and Ln.pool and not Ln.bits
+                        # its pre-pool staging aliases the relu(u) tile (8x8, 5x5: fits)
+                        and Ln.H * Ln.W * 72 <= (Ln.H + 2) * (Ln.W + 2) * 48):
+                    u0, y0, u1, y1, nxt = self._res_fwd16(li, p, [b.detach() for b in bs],
+                                                          stage=save)
+                else:
+                    u0, y0, u1, y1 = self._res_fwd16(li, p, [b.detach() for b in bs])
             elif self.fused_res_fwd32 and L.cout == 32 and p.is_cuda:
                 u0, y0 = self._res_blk32(li + 1, p, bs)
                 u1, y1 = self._res_blk32(li + 3, y0, bs)
@@ -440,9 +521,10 @@ class HipEncoder:
                 continue
             dc = torch.empty(pidx.shape[0], Ls.H, Ls.W, Ls.cout, dtype=torch.bfloat16,
                              device=pidx.device)
-            N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dp.data_ptr(), pidx.shape[0],
-                                                 Ls.H, Ls.W, Ls.cout, dc.data_ptr(),
-                                                 N.stream_ptr()), "pool_bwd_idx")
+            for i0, i1 in self._spans(pidx.shape[0]):
+                N.check(N.kernels().mbk_pool_bwd_idx(_at(pidx, i0), _at(dp, i0), i1 - i0, Ls.H,
+                                                     Ls.W, Ls.cout, _at(dc, i0), N.stream_ptr()),
+                        "pool_bwd_idx")
             self._wgrad(Ls, x, dc, grads[2 * li], grads[2 * li + 1])
             g = self._fwd(Ls, dc, None, dgrad=True) if s > 0 else None
         return grads

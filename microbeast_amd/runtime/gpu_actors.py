@@ -64,7 +64,8 @@ class GpuActorRuntime:
                  bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
                  env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False,
                  n_lanes: int | None = None, policy_cu_every: int = 0,
-                 reference_keys: bool = False, policy_logits: bool = False):
+                 reference_keys: bool = False, policy_logits: bool = False,
+                 policy_gate: bool | None = None):
         """reference_keys: also emit the reference buffer keys ep_return / ep_step /
         last_action (libs/utils.py:34-46) into the slots; policy_logits: plus the dense
         78*h*w policy logits of every step (the sparse acting head never needs them, so
@@ -135,6 +136,11 @@ class GpuActorRuntime:
         self.opp_graph = l0.get("opp_graph")
         if self.selfplay_groups > 0:
             self.opp_flat, self.opp_model = l0["opp_flat"], l0["opp_model"]
+        # policy gate (engine.h EngineConfig::policy_gate): learner launches wait while a
+        # policy step's kernels are in flight (one lane only; MBK_POLICY_GATE=0/1)
+        if policy_gate is None:
+            policy_gate = os.environ.get("MBK_POLICY_GATE", "0") == "1"
+        self.policy_gate = bool(policy_gate) and self.n_lanes == 1
         if n_threads is None:
             n_threads = max(1, min(32, available_cpus() - 3))
         self.n_threads = n_threads
@@ -144,7 +150,7 @@ class GpuActorRuntime:
                    reward_weight=list(reward_weight), env_index_base=env_index_base,
                    device=dev.index if dev.index is not None else torch.cuda.current_device(),
                    selfplay_groups=self.selfplay_groups, n_lanes=self.n_lanes,
-                   policy_cu_every=int(policy_cu_every))
+                   policy_cu_every=int(policy_cu_every), policy_gate=self.policy_gate)
         bufs = {k: v.data_ptr() for k, v in self.rb.items()}
         bufs["lanes"] = []
         for lane in self.lanes:
@@ -261,9 +267,12 @@ class GpuActorRuntime:
         self.engine.start([[ex(ln["graph"]), ex(ln.get("opp_graph")), ex(ln["pack_graph"]),
                             ex(ln.get("opp_pack_graph"))] for ln in self.lanes])
         self.started = True
+        if self.policy_gate:  # every policy graph is captured: gate the learner's launches
+            N.set_policy_gate(self.engine.gate_ptr())
 
     def stop(self):
         if self.started:
+            N.set_policy_gate(None)
             self.engine.stop()
             self.started = False
 

@@ -279,6 +279,30 @@ def test_fp8_trunk_close_to_bf16_trunk(cuda):
 
 
 @pytest.mark.parametrize("s", [16, 10, 8])
+def test_fused_fp8_trunk_matches_per_layer_fp8_kernels(cuda, s):
+    """trunk.hip trunk_tail8 (fp8 layers 1..14 in one launch, e4m3 LDS tiles, bf16 residual
+    stream) == the 14 per-layer fp8 MFMA conv launches: same conversion points, scales and
+    fp32 accumulation order -> bit-identical."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(17)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(203, s * s, seed=19).to(cuda)
+    m.features(obs[:2])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    enc.fp8 = True
+    assert enc.fused_tail and enc.fused_tail8
+    y_fused = encode(obs, enc, params, False)
+    enc.fused_tail8 = False
+    y_ref = encode(obs, enc, params, False)
+    enc.fused_tail8 = True
+    enc.fp8 = False
+    assert y_fused.shape == y_ref.shape
+    assert torch.equal(y_fused, y_ref), (y_fused.float() - y_ref.float()).abs().max()
+
+
+@pytest.mark.parametrize("s", [16, 10, 8])
 def test_fused_trunk_tail_matches_per_layer_kernels(cuda, s):
     """trunk.hip (layers 1..14 in one launch, LDS-resident) == the per-layer conv kernels."""
     from microbeast_amd.models.agent import Agent
@@ -449,6 +473,61 @@ def test_fused_res_fwd16_bit_identical(cuda, s, n):
         outs[fused] = [t.clone() for t in saved[:6]] + [y.clone()]
     for a, b in zip(outs[False], outs[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 9)])
+def test_fused_stage_conv_in_res_fwd16_bit_identical(cuda, s, n):
+    """res_fwd16_stage (the stage-0 residual kernel also runs stage 1's conv 16->32 + max-pool
+    from LDS) writes the same pooled output and argmax bytes, and every other saved
+    activation, as the separate pooled conv_fwd launch."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encoder_params
+    torch.manual_seed(6)
+    chans = (16, 32, 32, 32) if s == 24 else (16, 32, 32)
+    m = Agent((s, s, 27), channels=chans).to(cuda)
+    obs = _random_obs_bits(n, s * s, seed=3).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = [p.detach() for p in encoder_params(m.network, len(chans))]
+    outs = {}
+    for fused in (False, True):
+        enc.fused_stage_fwd = fused
+        y, saved = enc.forward(obs, params, save=True)
+        torch.cuda.synchronize()
+        outs[fused] = [t.clone() for t in saved if torch.is_tensor(t)] + [y.clone()]
+    enc.fused_stage_fwd = True
+    assert len(outs[False]) == len(outs[True])
+    for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+        assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("s,n", [(16, 37), (10, 21)])
+def test_chunked_learner_launches_match_whole_batch(cuda, s, n):
+    """MBK_LEARN_CHUNK: the learner's per-image kernels launched over image ranges (ragged
+    last range) give the same activations bit for bit, and weight gradients equal up to the
+    fp32 order of the per-range partial sums."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(8)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(n, s * s, seed=4).to(cuda)
+    m.features(obs[:2])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    res = {}
+    for chunk in (0, 8):
+        enc.chunk = chunk
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True)
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).to(cuda)
+        (y.float() * r).sum().backward()
+        torch.cuda.synchronize()
+        res[chunk] = (y.clone(), [p.grad.clone() for p in params])
+    enc.chunk = 0
+    assert torch.equal(res[0][0], res[8][0])
+    for a, b in zip(res[0][1], res[8][1]):
+        torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 9)])

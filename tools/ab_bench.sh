@@ -19,7 +19,8 @@ import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 a = d["actor_stats"]; l = d["learner_phase_ms_rank0"]
 print(f"[{sys.argv[1]}] {d['value']/1e6:.3f}M fps, {d['ms_per_step']} ms/step, gpu_phase {a['gpu_phase_ms']} "
-      f"env_phase {a['env_phase_ms']} busy {a['env_worker_busy_frac']} fwd {l.get('fwd')} bwd {l.get('bwd')}")
+      f"env_phase {a['env_phase_ms']} busy {a['env_worker_busy_frac']} fwd {l.get('fwd')} bwd {l.get('bwd')}"
+      + (f" step_split {d['policy_step_gpu_ms']}" if "policy_step_gpu_ms" in d else ""))
 EOF
 done
 if [ -n "$LT" ]; then

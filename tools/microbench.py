@@ -24,6 +24,8 @@ def main():
     p.add_argument("--iters", type=int, default=50)
     p.add_argument("--policy_eager", action="store_true",
                    help="also run the policy step eagerly (no graph) so rocprof sees its kernels")
+    p.add_argument("--fp8", action="store_true", help="policy step on the fp8 acting trunk")
+    p.add_argument("--no_learner", action="store_true", help="policy step timings only")
     p.add_argument("--variants", type=str, default="",
                    help="comma list of encoder toggles to A/B in the same process: "
                         "fusedpool, nofusedpool")
@@ -38,7 +40,7 @@ def main():
     s = a.size
     mk = lambda: Agent((s, s, 27))  # noqa: E731
     for E in [int(x) for x in a.E.split(",") if x]:
-        rt = GpuActorRuntime(mk, s, 1, E, 8, 1, dev, n_threads=1)
+        rt = GpuActorRuntime(mk, s, 1, E, 8, 1, dev, n_threads=1, fp8_policy=a.fp8)
         # realistic inputs: run the env once to get observations / masks
         env = rt.engine.env  if hasattr(rt.engine, "env") else None  # noqa: F841
         g = rt.graph
@@ -52,13 +54,16 @@ def main():
             g.replay()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.iters
-        print(json.dumps({"what": "policy_step_graph", "E": E, "ms": round(dt * 1e3, 4),
+        print(json.dumps({"what": "policy_step_graph", "E": E, "fp8": a.fp8,
+                          "trunk8": os.environ.get("MBK_TRUNK8", "1"), "ms": round(dt * 1e3, 4),
                           "frames_per_s": round(E / dt, 1)}), flush=True)
         if a.policy_eager:
             for _ in range(a.iters):
                 rt._policy_step(rt.io, rt.infer_model, rt.rng)
             torch.cuda.synchronize()
         del rt
+    if a.no_learner:
+        return
     torch.manual_seed(0)
     learner = Learner(mk(), LearnerHParams(), dev)
     from microbeast_amd.envs.synthetic import create_env
