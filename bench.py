@@ -41,9 +41,10 @@ def parse(argv=None):
     p.add_argument("--size", type=int, default=16)
     p.add_argument("--arch", type=str, default="impala_flat",
                    help="impala_flat (headline) | gridnet (BASELINE config 2) | impala_deep")
-    p.add_argument("--groups", type=int, default=3,
-                   help="env groups pipelined through the policy stream (profile 15 sweep: 3 x 8192 "
-                        "beats 2 x 8192 once the policy step is 0.24 ms)")
+    p.add_argument("--groups", type=int, default=4,
+                   help="env groups pipelined through the policy stream (profile 21 same-box "
+                        "sweep: 4 x 8192 9.83-9.94M vs 3 x 8192 9.51-9.56M frames/s; the "
+                        "policy lane is ~72%% busy with 3, the group cycle's latency bound)")
     p.add_argument("--lanes", type=int, default=1,
                    help="concurrent policy streams, each with its own graph + I/O")
     p.add_argument("--envs_per_group", type=int, default=8192)

@@ -377,6 +377,7 @@ struct TrunkArgs {
   int N, H0, W0;
   int tni;              // images per workgroup iteration
   int r1_bytes;         // region sizes (host computed)
+  int r2_bytes;         // (fp8 trunk: A = r1_bytes, B = r2_bytes)
 };
 
 // layer l of the tail (0..13): CIN / COUT of the (16, 32, 32) trunk
@@ -601,10 +602,13 @@ __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
 // so each conv reads 8-byte fragments with no per-tap relu. Weights are fetched one layer
 // ahead into registers (half the VGPRs of the bf16 prefetch).
 __global__ __launch_bounds__(kThreads) void trunk_tail8_kernel(TrunkArgs a) {
+  // regions (trunk8_region_*): A = X0 (bf16) in stage 0, then the pool staging and U (fp8)
+  // of stages 1-2; B = U0 (fp8) in stage 0, then X1 / X2 (bf16); F = the fp8 conv input.
+  // Swapping the roles after stage 0 keeps the 16-image group of the bf16 trunk in LDS.
   char* smem = trunk_smem;
-  const int oR1 = 0, oR2 = a.r1_bytes, oF = 2 * a.r1_bytes;
-  char* R1 = smem + oR1;
-  char* R2 = smem + oR2;
+  const int oA = 0, oB = a.r1_bytes, oF = a.r1_bytes + a.r2_bytes;
+  char* A = smem + oA;
+  char* B = smem + oB;
   char* F = smem + oF;
   const int H0 = a.H0, W0 = a.W0, H1 = (H0 + 1) >> 1, W1 = (W0 + 1) >> 1;
   const int H2 = (H1 + 1) >> 1, W2 = (W1 + 1) >> 1;
@@ -623,51 +627,51 @@ __global__ __launch_bounds__(kThreads) void trunk_tail8_kernel(TrunkArgs a) {
   } while (0)
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
-    // ---- stage 0: X0 <- input (R1), F <- fp8(relu(X0)); halos of R1 / U (R2) / F
-    load_input<true>(a, img0, nimg, R1, F);
-    zero_halo<TG<16>::PIXB>(R1, nimg, H0, W0);
-    zero_halo<TG<16>::PIXB8>(R2, nimg, H0, W0);
+    // ---- stage 0: X0 <- input (A), F <- fp8(relu(X0)); halos of A / U0 (B) / F
+    load_input<true>(a, img0, nimg, A, F);
+    zero_halo<TG<16>::PIXB>(A, nimg, H0, W0);
+    zero_halo<TG<16>::PIXB8>(B, nimg, H0, W0);
     zero_halo<TG<16>::PIXB8>(F, nimg, H0, W0);
     __syncthreads();
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL8(2 * rb, 16, 16, OUT_TILE_RELU, oF, H0, W0, oR2, 0);
+      TAIL8(2 * rb, 16, 16, OUT_TILE_RELU, oF, H0, W0, oB, 0);
       __syncthreads();
-      TAIL8(2 * rb + 1, 16, 16, OUT_TILE_ADD, oR2, H0, W0, oR1, rb == 0 ? 1 : 2);
+      TAIL8(2 * rb + 1, 16, 16, OUT_TILE_ADD, oB, H0, W0, oA, rb == 0 ? 1 : 2);
       __syncthreads();
     }
-    // ---- stage 1: conv 16->32 (staging in R2) -> pool -> X1 (R1) + F
-    TAIL8(4, 16, 32, OUT_STAGE, oF, H0, W0, oR2, 0);
+    // ---- stage 1: conv 16->32 (staging in A: X0 is dead) -> pool -> X1 (B) + F
+    TAIL8(4, 16, 32, OUT_STAGE, oF, H0, W0, oA, 0);
     __syncthreads();
-    pool_lds<32, true>((const bf16*)R2, H0, W0, nimg, R1, F);
-    zero_halo<TG<32>::PIXB>(R1, nimg, H1, W1);
+    pool_lds<32, true>((const bf16*)A, H0, W0, nimg, B, F);
+    zero_halo<TG<32>::PIXB>(B, nimg, H1, W1);
     zero_halo<TG<32>::PIXB8>(F, nimg, H1, W1);
     __syncthreads();
-    zero_halo<TG<32>::PIXB8>(R2, nimg, H1, W1);  // U1 layout (staging consumed)
+    zero_halo<TG<32>::PIXB8>(A, nimg, H1, W1);  // U1 layout (staging consumed)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL8(5 + 2 * rb, 32, 32, OUT_TILE_RELU, oF, H1, W1, oR2, 0);
+      TAIL8(5 + 2 * rb, 32, 32, OUT_TILE_RELU, oF, H1, W1, oA, 0);
       __syncthreads();
-      TAIL8(6 + 2 * rb, 32, 32, OUT_TILE_ADD, oR2, H1, W1, oR1, rb == 0 ? 1 : 2);
+      TAIL8(6 + 2 * rb, 32, 32, OUT_TILE_ADD, oA, H1, W1, oB, rb == 0 ? 1 : 2);
       __syncthreads();
     }
-    // ---- stage 2
-    TAIL8(9, 32, 32, OUT_STAGE, oF, H1, W1, oR2, 0);
+    // ---- stage 2 (X1 in B is dead once F holds its copy)
+    TAIL8(9, 32, 32, OUT_STAGE, oF, H1, W1, oA, 0);
     __syncthreads();
-    pool_lds<32, true>((const bf16*)R2, H1, W1, nimg, R1, F);
-    zero_halo<TG<32>::PIXB>(R1, nimg, H2, W2);
+    pool_lds<32, true>((const bf16*)A, H1, W1, nimg, B, F);
+    zero_halo<TG<32>::PIXB>(B, nimg, H2, W2);
     zero_halo<TG<32>::PIXB8>(F, nimg, H2, W2);
     __syncthreads();
-    zero_halo<TG<32>::PIXB8>(R2, nimg, H2, W2);
+    zero_halo<TG<32>::PIXB8>(A, nimg, H2, W2);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
-      TAIL8(10 + 2 * rb, 32, 32, OUT_TILE_RELU, oF, H2, W2, oR2, 0);
+      TAIL8(10 + 2 * rb, 32, 32, OUT_TILE_RELU, oF, H2, W2, oA, 0);
       __syncthreads();
-      TAIL8(11 + 2 * rb, 32, 32, OUT_TILE_ADD, oR2, H2, W2, oR1, rb == 0 ? 1 : 0);
+      TAIL8(11 + 2 * rb, 32, 32, OUT_TILE_ADD, oA, H2, W2, oB, rb == 0 ? 1 : 0);
       __syncthreads();
     }
 #undef TAIL8
-    store_output(a, img0, nimg, H2, W2, R1);
+    store_output(a, img0, nimg, H2, W2, B);
     __syncthreads();
   }
 }
@@ -680,15 +684,34 @@ size_t region_bytes(int H0, int W0, int TNI) {
   r = std::max(r, (size_t)TNI * (H2 + 2) * (W2 + 2) * TG<32>::PIXB);          // X2 / U2
   return (r + 15) & ~(size_t)15;
 }
-// the fp8 trunk's F tile (fp8 X copy) at its largest stage
-size_t region8_bytes(int H0, int W0, int TNI) {
+// fp8 trunk regions (see trunk_tail8_kernel): A, B and the fp8 conv-input tile F
+size_t trunk8_region_a(int H0, int W0, int TNI) {
+  const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2, H2 = (H1 + 1) / 2, W2 = (W1 + 1) / 2;
+  size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB;          // X0
+  r = std::max(r, (size_t)TNI * H0 * W0 * 32 * 2);                     // stage-1 staging
+  r = std::max(r, (size_t)TNI * (H1 + 2) * (W1 + 2) * TG<32>::PIXB8);  // U1
+  r = std::max(r, (size_t)TNI * H1 * W1 * 32 * 2);                     // stage-2 staging
+  r = std::max(r, (size_t)TNI * (H2 + 2) * (W2 + 2) * TG<32>::PIXB8);  // U2
+  return (r + 15) & ~(size_t)15;
+}
+size_t trunk8_region_b(int H0, int W0, int TNI) {
+  const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2, H2 = (H1 + 1) / 2, W2 = (W1 + 1) / 2;
+  size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB8;         // U0
+  r = std::max(r, (size_t)TNI * (H1 + 2) * (W1 + 2) * TG<32>::PIXB);   // X1
+  r = std::max(r, (size_t)TNI * (H2 + 2) * (W2 + 2) * TG<32>::PIXB);   // X2
+  return (r + 15) & ~(size_t)15;
+}
+size_t trunk8_region_f(int H0, int W0, int TNI) {
   const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2;
   size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB8;
   r = std::max(r, (size_t)TNI * (H1 + 2) * (W1 + 2) * TG<32>::PIXB8);
   return (r + 15) & ~(size_t)15;
 }
 size_t trunk_smem_bytes(int H0, int W0, int TNI, size_t wb, bool f8) {
-  return 2 * region_bytes(H0, W0, TNI) + wb + (f8 ? region8_bytes(H0, W0, TNI) : 0);
+  if (f8)
+    return trunk8_region_a(H0, W0, TNI) + trunk8_region_b(H0, W0, TNI) +
+           trunk8_region_f(H0, W0, TNI);
+  return 2 * region_bytes(H0, W0, TNI) + wb;
 }
 
 }  // namespace
@@ -790,7 +813,8 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
   if (H0 * W0 > 1024 || (int64_t)tni * H0 * W0 >= (int64_t(1) << 16))
     return (int)hipErrorInvalidValue;
   const size_t r = region_bytes(H0, W0, tni);
-  a.r1_bytes = (int)r;
+  a.r1_bytes = f8 ? (int)trunk8_region_a(H0, W0, tni) : (int)r;
+  a.r2_bytes = f8 ? (int)trunk8_region_b(H0, W0, tni) : (int)r;
   const size_t sm = trunk_smem_bytes(H0, W0, tni, wb, f8);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const bool fc = a.f_out != nullptr;
