@@ -281,6 +281,9 @@ PYBIND11_MODULE(_mbrt, m) {
           io.in_res_p1 = get(d, "in_res_p1");
           io.out_act16_p1 = get(d, "out_act16_p1");
           io.out_logits = get(d, "out_logits");
+          io.in_codes_b = get(d, "in_codes_b");
+          io.in_res_b = get(d, "in_res_b");
+          io.out_act16_b = get(d, "out_act16_b");
           buf.lanes.push_back(io);
         }
         return new GpuEngine(cfg, buf);
@@ -290,8 +293,9 @@ PYBIND11_MODULE(_mbrt, m) {
            [](GpuEngine& e, std::vector<std::vector<uintptr_t>> graphs) {
              std::vector<LaneGraphs> lg;
              for (const auto& t : graphs) {
-               if (t.size() != 4) throw std::runtime_error("start: need 4 graph handles per lane");
-               lg.push_back(LaneGraphs{t[0], t[1], t[2], t[3]});
+               if (t.size() != 4 && t.size() != 5)
+                 throw std::runtime_error("start: need 4 (or 5) graph handles per lane");
+               lg.push_back(LaneGraphs{t[0], t[1], t[2], t[3], t.size() == 5 ? t[4] : 0});
              }
              e.start(lg);
            })

@@ -64,6 +64,16 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     } else {
       CTOR_CHECK(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, prio_greatest));
     }
+    L.overlap = L.io.in_codes_b && L.io.in_res_b && L.io.out_act16_b && cfg_.selfplay_groups == 0;
+    if (L.overlap) {
+      CTOR_CHECK(hipStreamCreateWithPriority(&L.s_in, hipStreamNonBlocking, prio_greatest));
+      CTOR_CHECK(hipStreamCreateWithPriority(&L.s_out, hipStreamNonBlocking, prio_greatest));
+      for (int p = 0; p < 2; ++p) {
+        CTOR_CHECK(hipEventCreateWithFlags(&L.ev_h2d[p], hipEventDisableTiming));
+        CTOR_CHECK(hipEventCreateWithFlags(&L.ev_done[p], hipEventDisableTiming));
+        CTOR_CHECK(hipEventCreateWithFlags(&L.ev_d2h[p], hipEventDisableTiming));
+      }
+    }
   }
   CTOR_CHECK(hipHostMalloc((void**)&h_codes_, (size_t)total * S_ * 2, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_res_, (size_t)total * 4, hipHostMallocDefault));
@@ -134,8 +144,11 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
 
 GpuEngine::~GpuEngine() {
   stop();
-  for (Lane& L : lanes_)
+  for (Lane& L : lanes_) {
     if (L.stream) hipStreamSynchronize(L.stream);
+    if (L.s_in) hipStreamSynchronize(L.s_in);
+    if (L.s_out) hipStreamSynchronize(L.s_out);
+  }
   for (auto& g : groups_) {
     if (g->ev) hipEventDestroy(g->ev);
     for (auto e : g->tev)
@@ -161,6 +174,13 @@ GpuEngine::~GpuEngine() {
   if (h_done_) hipHostFree(h_done_);
   if (gate_) hipFree(gate_);
   for (Lane& L : lanes_) {
+    for (int p = 0; p < 2; ++p) {
+      if (L.ev_h2d[p]) hipEventDestroy(L.ev_h2d[p]);
+      if (L.ev_done[p]) hipEventDestroy(L.ev_done[p]);
+      if (L.ev_d2h[p]) hipEventDestroy(L.ev_d2h[p]);
+    }
+    if (L.s_in) hipStreamDestroy(L.s_in);
+    if (L.s_out) hipStreamDestroy(L.s_out);
     if (L.stream) hipStreamDestroy(L.stream);
   }
 }
@@ -195,6 +215,9 @@ void GpuEngine::start(const std::vector<LaneGraphs>& graphs) {
     L.opp_graph = (hipGraphExec_t)g.opp;
     L.pack_graph[0] = (hipGraphExec_t)g.pack;
     L.pack_graph[1] = (hipGraphExec_t)g.opp_pack;
+    L.graph_b = (hipGraphExec_t)g.policy_b;
+    if (L.overlap && !L.graph_b)
+      throw std::runtime_error("GpuEngine::start: copy overlap needs the second policy graph");
   }
   running_.store(true);
   for (int w = 0; w < cfg_.n_threads; ++w) workers_.emplace_back(&GpuEngine::worker_loop, this, w);
@@ -208,8 +231,11 @@ void GpuEngine::stop() {
   if (driver_.joinable()) driver_.join();
   for (auto& t : workers_) if (t.joinable()) t.join();
   workers_.clear();
-  for (Lane& L : lanes_)
+  for (Lane& L : lanes_) {
     if (L.stream) hipStreamSynchronize(L.stream);
+    if (L.s_in) hipStreamSynchronize(L.s_in);
+    if (L.s_out) hipStreamSynchronize(L.s_out);
+  }
   // an enqueue that failed between the gate's set and clear must not leave the learner's
   // stream waiting forever
   if (gate_) hipMemset(gate_, 0, sizeof(uint32_t));
@@ -367,17 +393,31 @@ bool GpuEngine::enqueue_gpu(int g) {
   }
   const size_t e0 = (size_t)g * E;
   G.timed = step_timing_;
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], st));
-  ENG_CHECK(hipMemcpyAsync((void*)io.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
-                           hipMemcpyHostToDevice, st));
-  ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice,
-                           st));
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
+  // copy overlap: this step's PCIe buffers (parity p) and the streams its copies run on
+  const int par = L.par;
+  const uintptr_t in_codes = (L.overlap && par) ? io.in_codes_b : io.in_codes;
+  const uintptr_t in_res = (L.overlap && par) ? io.in_res_b : io.in_res;
+  const uintptr_t out_act16 = (L.overlap && par) ? io.out_act16_b : io.out_act16;
+  hipStream_t s_in = L.overlap ? L.s_in : st;
+  if (L.overlap) {
+    // parity p's inputs were consumed by the step two back (its graph + scatter are done)
+    ENG_CHECK(hipStreamWaitEvent(s_in, L.ev_done[par], 0));
+  }
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], s_in));
+  ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
+                           hipMemcpyHostToDevice, s_in));
+  ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], s_in));
+  if (L.overlap) {
+    ENG_CHECK(hipEventRecord(L.ev_h2d[par], s_in));
+    ENG_CHECK(hipStreamWaitEvent(st, L.ev_h2d[par], 0));
+    ENG_CHECK(hipStreamWaitEvent(st, L.ev_d2h[par], 0));  // act16[p] copied out two steps back
+  }
   // learner launches hold from here (the H2D above is SDMA: no CUs) to the scatter's end
   if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
   {
     const auto t0 = std::chrono::steady_clock::now();
-    ENG_CHECK(hipGraphLaunch(L.graph, st));
+    ENG_CHECK(hipGraphLaunch((L.overlap && par) ? L.graph_b : L.graph, st));
     launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                              std::chrono::steady_clock::now() - t0).count(),
                          std::memory_order_relaxed);
@@ -444,6 +484,13 @@ bool GpuEngine::enqueue_gpu(int g) {
   }
   ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, st));
   if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));  // (the D2H is SDMA)
+  hipStream_t s_out = st;
+  if (L.overlap) {  // D2H on the copy-out stream once this step's graph + scatter are done
+    ENG_CHECK(hipEventRecord(L.ev_done[par], st));
+    s_out = L.s_out;
+    ENG_CHECK(hipStreamWaitEvent(s_out, L.ev_done[par], 0));
+    L.par ^= 1;
+  }
   if (close_prev) {
     ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
     {
@@ -454,13 +501,14 @@ bool GpuEngine::enqueue_gpu(int g) {
     full_cv_.notify_all();
     G.prev = -1;
   }
-  ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)io.out_act16, E * S_ * 2,
-                           hipMemcpyDeviceToHost, st));
+  ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
+                           hipMemcpyDeviceToHost, s_out));
   if (G.selfplay)
     ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
                              hipMemcpyDeviceToHost, st));
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], st));
-  ENG_CHECK(hipEventRecord(G.ev, st));
+  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], s_out));
+  if (L.overlap) ENG_CHECK(hipEventRecord(L.ev_d2h[par], s_out));
+  ENG_CHECK(hipEventRecord(G.ev, s_out));
   gpu_steps_.fetch_add(1);
   G.t += 1;
   if (G.t == (int)T) {

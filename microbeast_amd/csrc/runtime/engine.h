@@ -80,6 +80,10 @@ struct LaneIO {
   // opponent graph I/O (self-play groups only)
   uintptr_t in_codes_p1 = 0, in_res_p1 = 0, out_act16_p1 = 0;
   uintptr_t out_logits = 0;  // dense policy logits [E][78*S] f32 (reference keys only)
+  // copy overlap (no self-play): a second set of the PCIe-facing buffers, read / written by a
+  // second captured graph; steps alternate between the two sets so the H2D of the next step
+  // and the D2H of the last one run on copy streams while the lane computes
+  uintptr_t in_codes_b = 0, in_res_b = 0, out_act16_b = 0;
 };
 
 // Per-lane graphs (raw hipGraphExec_t). opp: opponent policy (self-play only); pack /
@@ -87,6 +91,7 @@ struct LaneIO {
 // derived inference weights so the policy graph itself never re-packs.
 struct LaneGraphs {
   uintptr_t policy = 0, opp = 0, pack = 0, opp_pack = 0;
+  uintptr_t policy_b = 0;  // copy overlap: the graph on the second buffer set (LaneIO *_b)
 };
 
 // Device buffers owned by Python (torch tensors); raw addresses.
@@ -204,6 +209,15 @@ class GpuEngine {
   struct Lane {
     hipStream_t stream = nullptr;
     hipGraphExec_t graph = nullptr, opp_graph = nullptr;
+    // copy overlap (LaneIO *_b set): H2D / D2H copy streams, the parity of the next step and
+    // per parity: H2D landed, graph + scatter done (its inputs consumed, its act16 final),
+    // D2H done (its act16 buffer free again)
+    bool overlap = false;
+    hipGraphExec_t graph_b = nullptr;
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+    hipEvent_t ev_d2h[2] = {nullptr, nullptr};
+    int par = 0;
     hipGraphExec_t pack_graph[2] = {nullptr, nullptr};
     LaneIO io;
     int opp_version = -1;     // driver thread only

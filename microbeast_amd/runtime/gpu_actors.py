@@ -104,6 +104,10 @@ class GpuActorRuntime:
         self.n_lanes = max(1, min(n_groups, n_lanes if n_lanes is not None else 1))
         self.fp8_policy = fp8_policy
         self.selfplay_groups = int(selfplay_groups)
+        # double-buffered PCIe I/O with H2D / D2H on copy streams (MBK_COPY_OVERLAP=0: off;
+        # self-play lanes keep the single-stream step)
+        self.copy_overlap = (os.environ.get("MBK_COPY_OVERLAP", "0") == "1"
+                             and self.selfplay_groups == 0)
         self.lanes = []
         for ln in range(self.n_lanes):
             lane = {"io": self._make_io(),
@@ -116,6 +120,15 @@ class GpuActorRuntime:
             lane["flat"] = FlatParams(lane["model"], dev)
             lane["pack_graph"] = self._capture_pack(lane["model"])
             lane["graph"] = self._capture(lane["io"], lane["model"], lane["rng"])
+            if self.copy_overlap:
+                # second set of the PCIe-facing buffers + its own graph (engine.h LaneIO *_b):
+                # the engine alternates steps between the two so the next step's H2D and the
+                # last one's D2H run on copy streams while the lane computes
+                io_b = dict(lane["io"])
+                for k in ("in_codes", "in_res", "out_act16"):
+                    io_b[k] = torch.zeros_like(lane["io"][k])
+                lane["io_b"] = io_b
+                lane["graph_b"] = self._capture(io_b, lane["model"], lane["rng"])
             if self.selfplay_groups > 0:
                 lane["io_p1"] = self._make_io()
                 lane["rng_p1"] = torch.tensor(
@@ -155,6 +168,9 @@ class GpuActorRuntime:
         bufs["lanes"] = []
         for lane in self.lanes:
             d = {k: v.data_ptr() for k, v in lane["io"].items()}
+            if self.copy_overlap:
+                d.update({k + "_b": lane["io_b"][k].data_ptr()
+                          for k in ("in_codes", "in_res", "out_act16")})
             if self.selfplay_groups > 0:
                 d.update({"in_codes_p1": lane["io_p1"]["in_codes"].data_ptr(),
                           "in_res_p1": lane["io_p1"]["in_res"].data_ptr(),
@@ -265,7 +281,8 @@ class GpuActorRuntime:
         torch.cuda.synchronize()
         ex = lambda g: int(g.raw_cuda_graph_exec()) if g is not None else 0  # noqa: E731
         self.engine.start([[ex(ln["graph"]), ex(ln.get("opp_graph")), ex(ln["pack_graph"]),
-                            ex(ln.get("opp_pack_graph"))] for ln in self.lanes])
+                            ex(ln.get("opp_pack_graph")), ex(ln.get("graph_b"))]
+                           for ln in self.lanes])
         self.started = True
         if self.policy_gate:  # every policy graph is captured: gate the learner's launches
             N.set_policy_gate(self.engine.gate_ptr())
