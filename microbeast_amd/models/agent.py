@@ -174,9 +174,10 @@ class Agent(nn.Module):
             r = self._api_rng = torch.tensor([seed, 0], dtype=torch.int64, device=device)
         return r
 
-    def _act_features(self, obs: torch.Tensor):
+    def _act_features(self, obs: torch.Tensor, value_out: torch.Tensor | None = None):
         """Acting forward with prepacked weights: conv trunk, then ONE fused launch for
-        relu -> network.5 -> relu -> critic (fc.hip). Returns (f bf16 [N,256], value fp32)."""
+        relu -> network.5 -> relu -> critic (fc.hip). Returns (f bf16 [N,256], value fp32);
+        value_out: fp32 [N] the fused kernel writes the value into (no copy launch)."""
         from .. import _native as N
         n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
         fc = self.network[len(self.channels) + 2]
@@ -185,7 +186,7 @@ class Agent(nn.Module):
             head = (self._fc_cache["w5"], fc.bias, self.critic.weight, self.critic.bias)
         y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
                    encoder_params(self.network, len(self.channels)), False, prepacked=True,
-                   head=head)
+                   head=head, value_out=value_out)
         if isinstance(y, tuple):
             return y
         I = y[0].numel()
@@ -194,7 +195,8 @@ class Agent(nn.Module):
             f = F.relu(linear(F.relu(y.reshape(n, -1)), fc, cached=(c["w5"], c["b5"])))
             return f, linear(f, self.critic, cached=(c["wc"], c["bc"])).float().view(-1)
         f = torch.empty(n, fc.out_features, dtype=torch.bfloat16, device=y.device)
-        v = torch.empty(n, dtype=torch.float32, device=y.device)
+        v = value_out if value_out is not None else torch.empty(n, dtype=torch.float32,
+                                                                 device=y.device)
         N.check(N.kernels().mbk_fc_fwd(y.data_ptr(), 1, self._fc_cache["w5"].data_ptr(),
                                        fc.bias.data_ptr(), self.critic.weight.data_ptr(),
                                        self.critic.bias.data_ptr(), n, I, fc.out_features,
@@ -306,7 +308,7 @@ class Agent(nn.Module):
 
     @torch.no_grad()
     def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
-            logp_out=None, bucketed: bool = False, logits_out=None):
+            logp_out=None, bucketed: bool = False, logits_out=None, value_out=None):
         """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N]).
         bucketed: the head's active pairs were bucketed by mbk_decode_obs_mask_bucket.
         logits_out: also write the dense policy logits [N, 78*h*w] (reference 'policy_logits';
@@ -316,7 +318,7 @@ class Agent(nn.Module):
             pre = self._prepacked
             if pre:
                 self._hip_enc.fp8 = self.fp8_inference
-                f, value = self._act_features(obs)
+                f, value = self._act_features(obs, value_out=value_out)
             else:
                 f = self.features(obs)
                 value = linear(f, self.critic).float().view(-1)

@@ -223,7 +223,7 @@ class HipEncoder:
             y.data_ptr(), n, L.H, L.W, imgs, N.stream_ptr()), "conv_dgrad_unpool")
         return y
 
-    def _tail(self, p: torch.Tensor, bs: list[torch.Tensor], head=None):
+    def _tail(self, p: torch.Tensor, bs: list[torch.Tensor], head=None, value_out=None):
         """Layers 1..14 on the fused trunk kernel (inference): p = stage-0 pooled output.
         head = (w5 NHWC bf16, b5, wc, bc): also network.5 + critic in the same launch;
         returns (f [n, 256] bf16, value [n] fp32) instead of the trunk output."""
@@ -236,7 +236,8 @@ class HipEncoder:
         if head is not None:
             w5, b5, wc, bc = head
             f = torch.empty(n, w5.shape[0], dtype=torch.bfloat16, device=p.device)
-            v = torch.empty(n, dtype=torch.float32, device=p.device)
+            v = (value_out if value_out is not None
+                 else torch.empty(n, dtype=torch.float32, device=p.device))
             N.check(k.mbk_trunk_tail_fc(p.data_ptr(), ctypes.cast(wp, ctypes.c_void_p),
                                         ctypes.cast(bp, ctypes.c_void_p), n, L1.H, L1.W, None,
                                         w5.data_ptr(), b5.data_ptr(), wc.data_ptr(),
@@ -413,7 +414,7 @@ class HipEncoder:
 
     # ------------------------------------------------------------ passes
     def forward(self, obs_bits: torch.Tensor, params: list[torch.Tensor], save: bool,
-                prepacked: bool = False, head=None):
+                prepacked: bool = False, head=None, value_out=None):
         """params: [w0, b0, w1, b1, ...] fp32 in layer order. Returns (out NHWC bf16, saved).
         prepacked: the packed weight buffers are current (inference after pack_inference)."""
         ws, bs = params[0::2], params[1::2]
@@ -436,7 +437,7 @@ class HipEncoder:
             self.pack([w.detach() for w in ws], with_bwd=save)
         if not save and self.fused_tail:
             p = self._fwd(self.layers[0], x, bs[0].detach())
-            return self._tail(p, bs, head), []
+            return self._tail(p, bs, head, value_out), []
         saved = []
         li = 0
         n = x.shape[0]
@@ -559,10 +560,11 @@ def encoder_params(network: torch.nn.Sequential, n_stages: int) -> list[torch.nn
 
 
 def encode(obs_bits: torch.Tensor, enc: HipEncoder, params: list[torch.Tensor],
-           need_grad: bool, prepacked: bool = False, head=None):
-    """NHWC bf16 trunk output [N, Ho, Wo, C]."""
+           need_grad: bool, prepacked: bool = False, head=None, value_out=None):
+    """NHWC bf16 trunk output [N, Ho, Wo, C] (head: (f, value) of the fused trunk head;
+    value_out: the fp32 [N] buffer that value is written into)."""
     if need_grad:
         return _EncoderFn.apply(obs_bits, enc, *params)
     with torch.no_grad():
         return enc.forward(obs_bits, [p.detach() for p in params], save=False,
-                           prepacked=prepacked, head=head)[0]
+                           prepacked=prepacked, head=head, value_out=value_out)[0]

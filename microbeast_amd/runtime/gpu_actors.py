@@ -217,7 +217,7 @@ class GpuActorRuntime:
                 st), "decode_obs_mask_bucket")
             _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
                                 logp_out=io["out_logp"], bucketed=True,
-                                logits_out=io.get("out_logits"))
+                                logits_out=io.get("out_logits"), value_out=io["out_value"])
         else:
             N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
                                           self.E, self.size, self.size, io["in_obs"].data_ptr(),
@@ -227,7 +227,8 @@ class GpuActorRuntime:
                 io["out_logits"].copy_(logits.reshape(io["out_logits"].shape))
             cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
                                  cell_logp=io["cell_logp"], logp_out=io["out_logp"])
-        io["out_value"].copy_(value)
+        if value.data_ptr() != io["out_value"].data_ptr():  # (written in place when fused)
+            io["out_value"].copy_(value.view(-1))
         N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
                                        io["out_act16"].data_ptr(), N.stream_ptr()),
                 "pack_env_actions")
