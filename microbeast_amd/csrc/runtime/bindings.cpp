@@ -317,6 +317,10 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("stream", &GpuEngine::stream, py::arg("lane") = 0)
       .def("failed", &GpuEngine::failed)
       .def("gate_ptr", &GpuEngine::gate_ptr)
+      .def("host_codes", &GpuEngine::host_codes)
+      .def("host_res", &GpuEngine::host_res)
+      .def("host_act16", &GpuEngine::host_act16)
+      .def("set_group_graphs", &GpuEngine::set_group_graphs)
       .def("inject_fault", &GpuEngine::inject_fault)
       .def("error", &GpuEngine::error)
       .def("stats", [](GpuEngine& e) {

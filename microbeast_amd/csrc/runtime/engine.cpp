@@ -224,6 +224,16 @@ void GpuEngine::start(const std::vector<LaneGraphs>& graphs) {
   driver_ = std::thread(&GpuEngine::driver_loop, this);
 }
 
+void GpuEngine::set_group_graphs(const std::vector<uintptr_t>& graphs) {
+  if (running_.load()) throw std::runtime_error("set_group_graphs: engine running");
+  if (!graphs.empty() && (int)graphs.size() != cfg_.n_groups)
+    throw std::runtime_error("set_group_graphs: need one graph per group");
+  if (!graphs.empty() && cfg_.selfplay_groups > 0)
+    throw std::runtime_error("set_group_graphs: not with self-play groups");
+  group_graph_.clear();
+  for (uintptr_t h : graphs) group_graph_.push_back((hipGraphExec_t)h);
+}
+
 void GpuEngine::stop() {
   running_.store(false);
   work_cv_.notify_all();
@@ -393,6 +403,10 @@ bool GpuEngine::enqueue_gpu(int g) {
   }
   const size_t e0 = (size_t)g * E;
   G.timed = step_timing_;
+  // zero-copy step: the group's own graph reads its codes from / writes its actions to the
+  // pinned host staging (PCIe inside the decode / pack kernels: no SDMA commands, and no
+  // copy<->compute engine hand-offs on the lane)
+  hipGraphExec_t zc = group_graph_.empty() ? nullptr : group_graph_[g];
   // copy overlap: this step's PCIe buffers (parity p) and the streams its copies run on
   const int par = L.par;
   const uintptr_t in_codes = (L.overlap && par) ? io.in_codes_b : io.in_codes;
@@ -404,9 +418,11 @@ bool GpuEngine::enqueue_gpu(int g) {
     ENG_CHECK(hipStreamWaitEvent(s_in, L.ev_done[par], 0));
   }
   if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], s_in));
-  ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
-                           hipMemcpyHostToDevice, s_in));
-  ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
+  if (!zc) {
+    ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
+                             hipMemcpyHostToDevice, s_in));
+    ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
+  }
   if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], s_in));
   if (L.overlap) {
     ENG_CHECK(hipEventRecord(L.ev_h2d[par], s_in));
@@ -417,7 +433,7 @@ bool GpuEngine::enqueue_gpu(int g) {
   if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
   {
     const auto t0 = std::chrono::steady_clock::now();
-    ENG_CHECK(hipGraphLaunch((L.overlap && par) ? L.graph_b : L.graph, st));
+    ENG_CHECK(hipGraphLaunch(zc ? zc : (L.overlap && par) ? L.graph_b : L.graph, st));
     launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                              std::chrono::steady_clock::now() - t0).count(),
                          std::memory_order_relaxed);
@@ -501,8 +517,9 @@ bool GpuEngine::enqueue_gpu(int g) {
     full_cv_.notify_all();
     G.prev = -1;
   }
-  ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
-                           hipMemcpyDeviceToHost, s_out));
+  if (!zc)
+    ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
+                             hipMemcpyDeviceToHost, s_out));
   if (G.selfplay)
     ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
                              hipMemcpyDeviceToHost, st));

@@ -172,6 +172,15 @@ class GpuEngine {
   std::vector<EpisodeRecord> drain_episodes() { return log_.drain(); }
   EngineStats stats() const;
   uintptr_t stream(int lane = 0) const { return (uintptr_t)lanes_.at(lane).stream; }
+  // pinned host staging (all envs contiguous): 16-bit cell codes [n_envs][S], resources
+  // [n_envs], packed actions [n_envs][S] -- device-addressable (coherent hipHostMalloc)
+  uintptr_t host_codes() const { return (uintptr_t)h_codes_; }
+  uintptr_t host_res() const { return (uintptr_t)h_res_; }
+  uintptr_t host_act16() const { return (uintptr_t)h_act16_; }
+  // zero-copy policy steps: one captured graph per group that reads the group's codes /
+  // resources straight from pinned host memory and writes its packed actions there (no
+  // H2D / D2H copy commands on the lane); set before start(), 0 entries = copy path
+  void set_group_graphs(const std::vector<uintptr_t>& graphs);
   const EngineConfig& config() const { return cfg_; }
   VecEnv& env() { return *env_; }
   bool failed() const { return failed_.load(); }
@@ -288,6 +297,7 @@ class GpuEngine {
   void fail(const std::string& msg);
   int chunk_;
   uint32_t* gate_ = nullptr;  // policy gate flag (device), see EngineConfig
+  std::vector<hipGraphExec_t> group_graph_;  // zero-copy graphs per group (may be empty)
 };
 
 }  // namespace mb

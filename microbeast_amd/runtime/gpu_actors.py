@@ -57,6 +57,17 @@ class EngineFailure(RuntimeError):
     process is intact and may rebuild the actor side (train.py)."""
 
 
+class _HostView:
+    """A raw device-addressable host pointer where the policy step expects a tensor (only
+    ``data_ptr()`` is used): the engine's pinned staging for zero-copy graphs."""
+
+    def __init__(self, ptr: int):
+        self._ptr = int(ptr)
+
+    def data_ptr(self) -> int:
+        return self._ptr
+
+
 class GpuActorRuntime:
     def __init__(self, make_model, size: int, n_groups: int, envs_per_group: int, unroll: int,
                  batch_slots: int, device: torch.device, n_threads: int | None = None,
@@ -178,6 +189,26 @@ class GpuActorRuntime:
             bufs["lanes"].append(d)
         torch.cuda.synchronize()
         self.engine = rt.GpuEngine(cfg, bufs)
+        # zero-copy policy steps (engine.h set_group_graphs): one graph per group whose decode
+        # reads the group's codes / resources from the engine's pinned host staging and whose
+        # pack writes its actions there (MBK_ZERO_COPY=1; self-play keeps the copy path)
+        self.zero_copy = (os.environ.get("MBK_ZERO_COPY", "0") == "1"
+                          and self.selfplay_groups == 0)
+        if self.zero_copy:
+            hc, hr, ha = (self.engine.host_codes(), self.engine.host_res(),
+                          self.engine.host_act16())
+            gg = []
+            for g in range(n_groups):
+                lane = self.lanes[g % self.n_lanes]
+                e0 = g * E
+                io_g = dict(lane["io"])
+                io_g["in_codes"] = _HostView(hc + e0 * self.S * 2)
+                io_g["in_res"] = _HostView(hr + e0 * 4)
+                io_g["out_act16"] = _HostView(ha + e0 * self.S * 2)
+                lane.setdefault("group_graphs", []).append(
+                    self._capture(io_g, lane["model"], lane["rng"]))
+                gg.append(lane["group_graphs"][-1])
+            self.engine.set_group_graphs([int(x.raw_cuda_graph_exec()) for x in gg])
         self.started = False
         self.frames_per_slot = E * self.T
 

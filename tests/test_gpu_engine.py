@@ -7,12 +7,19 @@ from microbeast_amd.ops.cell_head import OFFS, unpack_mask
 pytestmark = pytest.mark.gpu
 
 
-def test_engine_rollout_alignment_and_learn(cuda):
+@pytest.mark.parametrize("variant", ["lanes2", "zero_copy", "copy_overlap", "policy_gate"])
+def test_engine_rollout_alignment_and_learn(cuda, variant, monkeypatch):
+    """Slot alignment / action legality / learn / publish through every engine step form:
+    two lanes; zero-copy group graphs (codes and actions through pinned host memory); double-
+    buffered I/O on copy streams; the policy gate (learner launches wait on the step flag)."""
     from microbeast_amd.learner import Learner, LearnerHParams
     from microbeast_amd.models.agent import Agent
     from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
 
     s, T = 8, 8
+    monkeypatch.setenv("MBK_ZERO_COPY", "1" if variant == "zero_copy" else "0")
+    monkeypatch.setenv("MBK_COPY_OVERLAP", "1" if variant == "copy_overlap" else "0")
+    lanes = 2 if variant == "lanes2" else 1
 
     def mk():
         return Agent((s, s, 27))
@@ -20,7 +27,11 @@ def test_engine_rollout_alignment_and_learn(cuda):
     torch.manual_seed(0)
     learner = Learner(mk(), LearnerHParams(), cuda)
     rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=16, unroll=T, batch_slots=1,
-                         device=cuda, n_threads=2, n_lanes=2)
+                         device=cuda, n_threads=2, n_lanes=lanes,
+                         policy_gate=variant == "policy_gate")
+    assert rt.zero_copy == (variant == "zero_copy")
+    assert rt.copy_overlap == (variant == "copy_overlap")
+    assert rt.policy_gate == (variant == "policy_gate")
     rt.start(learner.flat)
     try:
         prev_last_obs = {}
@@ -49,7 +60,7 @@ def test_engine_rollout_alignment_and_learn(cuda):
         rt.stop()
     # every policy lane's inference weights track the learner after a publish
     torch.cuda.synchronize()
-    assert rt.n_lanes == 2
+    assert rt.n_lanes == lanes
     for lane in rt.lanes:
         d = (lane["flat"].data - learner.flat.data).abs().max().item()
         assert d < 1e-2
