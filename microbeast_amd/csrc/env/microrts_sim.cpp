@@ -380,13 +380,26 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
         at = n ? c[rand_u32() % n] : A_NOOP;
       }
       a[0] = (uint8_t)at;
-      for (int comp = 1; comp < 7; ++comp) {
+      // draw only the parameters the chosen type reads (exec ignores the others): the
+      // 49-bit attack component was scanned for every unit every tick (random_biased cost
+      // ~1.6 us per env step vs ~0.8 for the scripted bots)
+      int comps[2] = {0, 0}, nc = 0;
+      switch (at) {
+        case A_MOVE: comps[nc++] = 1; break;
+        case A_HARVEST: comps[nc++] = 2; break;
+        case A_RETURN: comps[nc++] = 3; break;
+        case A_PRODUCE: comps[nc++] = 4; comps[nc++] = 5; break;
+        case A_ATTACK: comps[nc++] = 6; break;
+        default: break;
+      }
+      for (int k = 0; k < nc; ++k) {
+        const int comp = comps[k];
         int cand[49], n = 0;
         for (int j = 0; j < kNvec[comp]; ++j)
           if (getbit(w, kNvecOff[comp] + j)) cand[n++] = j;
         a[comp] = n ? (uint8_t)cand[rand_u32() % n] : 0;
       }
-      exec(uid, a, rwo);
+      if (at != A_NOOP) exec(uid, a, rwo);
       return;
     }
     case BOT_WORKER_RUSH: {
