@@ -110,7 +110,7 @@ def main(argv=None):
     cpus = launch.pin_rank(int(os.environ.get("LOCAL_RANK", "0")), local_world, dev.index)
     budget = launch.rank_cpu_budget(local_world)
     # env workers: the rank's CPU budget less one (the engine driver thread spins between
-    # policy steps); profile 22 sweep on a 16-CPU share: 15 threads halve the env phase vs 13
+    # policy steps); profile 23 sweep on a 16-CPU share: 15 threads halve the env phase vs 13
     threads = args.threads or max(2, min(24, budget - 1))
     s = args.size
 

@@ -166,7 +166,7 @@ class GpuActorRuntime:
             policy_gate = os.environ.get("MBK_POLICY_GATE", "0") == "1"
         self.policy_gate = bool(policy_gate) and self.n_lanes == 1
         if n_threads is None:
-            n_threads = max(1, min(32, available_cpus() - 3))
+            n_threads = max(1, min(32, available_cpus() - 1))
         self.n_threads = n_threads
         cfg = dict(size=size, n_groups=n_groups, envs_per_group=E, unroll=self.T, n_slots=NS,
                    n_threads=n_threads, max_steps=max_steps, seed=seed,

@@ -120,7 +120,9 @@ def train(flags: Flags) -> dict:
         # NUMA/core placement before the engine starts its env worker / driver threads
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(info.world_size)))
         pin_rank(info.local_rank, local_world, dev.index)
-        actor_threads = actor_threads or max(1, min(32, rank_cpu_budget(local_world) - 3))
+        # the rank's CPU budget less one for the spinning engine driver (bench.py: 15 env
+        # threads on a 16-CPU share halve the env phase vs 13, profile 23)
+        actor_threads = actor_threads or max(1, min(32, rank_cpu_budget(local_world) - 1))
     torch.manual_seed(flags.seed + info.rank)
     log = (lambda *a: None) if (flags.quiet or not info.is_main) else (lambda *a: print(*a, flush=True))
     log(f"[microbeast_amd] exp={flags.exp_name} runtime={runtime} device={dev} "
