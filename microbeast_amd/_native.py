@@ -100,6 +100,8 @@ _SIGS = {
     "mbk_head_units": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p],
     "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_row_sum_pack": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                         c_void_p],
     "mbk_trunk_tail": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_trunk_tail_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                            c_void_p],

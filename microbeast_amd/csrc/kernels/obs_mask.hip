@@ -251,7 +251,45 @@ __global__ __launch_bounds__(256) void pack_env_actions_kernel(const uint8_t* __
   }
 }
 
+// Policy-step finale in one launch (one wave per env): the env's log-prob = sum of its
+// cells' log-probs (masked_cell.hip row_sum's lane-strided sum + wave_sum, bit-identical),
+// its cells' 7 action bytes packed into the 16-bit codes the env reads, and the sampler's
+// step counter advanced (block 0) -- row_sum_rng + pack_env_actions without the second
+// launch (each dependent launch of the policy graph waits for CUs behind the learner).
+__global__ __launch_bounds__(256) void row_sum_pack_kernel(const float* __restrict__ cell_lp,
+                                                           int64_t rows, int cols,
+                                                           float* __restrict__ logp,
+                                                           uint64_t* __restrict__ rng,
+                                                           const uint8_t* __restrict__ act,
+                                                           uint16_t* __restrict__ act16) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (rng && blockIdx.x == 0 && threadIdx.x == 0) rng[1] += 1;
+  const int64_t r = (int64_t)blockIdx.x * 4 + wave;
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += cell_lp[r * cols + c];
+  s = mbk::wave_sum(s);
+  if (lane == 0) logp[r] = s;
+  for (int c = lane; c < cols; c += 64) {
+    const int64_t i = r * cols + c;
+    uint8_t a[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) a[k] = act[i * 7 + k];
+    act16[i] = pack_env_action(a);
+  }
+}
+
 }  // namespace
+
+// logp[r] = sum_c cell_lp[r][c], act16[r][c] = packed act[r][c][0..6], rng step advance.
+extern "C" int mbk_row_sum_pack(const float* cell_lp, int64_t rows, int cols, float* logp,
+                                uint64_t* rng, const uint8_t* act, uint16_t* act16,
+                                hipStream_t stream) {
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(row_sum_pack_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
+                     cell_lp, rows, cols, logp, rng, act, act16);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mbk_decode_obs_mask(const uint16_t* codes, const int32_t* res, int n_envs, int H,
                                    int W, uint32_t* obs, uint32_t* mask, hipStream_t stream) {

@@ -308,7 +308,8 @@ class Agent(nn.Module):
 
     @torch.no_grad()
     def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
-            logp_out=None, bucketed: bool = False, logits_out=None, value_out=None):
+            logp_out=None, bucketed: bool = False, logits_out=None, value_out=None,
+            act16_out=None):
         """Sample under the mask. Returns (action [N,S,7] u8, logp [N], value [N]).
         bucketed: the head's active pairs were bucketed by mbk_decode_obs_mask_bucket.
         logits_out: also write the dense policy logits [N, 78*h*w] (reference 'policy_logits';
@@ -328,7 +329,7 @@ class Agent(nn.Module):
             action, logp = sparse_sample(f.to(torch.bfloat16), self.actor.weight, self.actor.bias,
                                          mask_bits.reshape(n, -1, 3), rng_state,
                                          self._head(f.device), action_out, logp_out,
-                                         prepacked=pre, bucketed=bucketed)
+                                         prepacked=pre, bucketed=bucketed, act16_out=act16_out)
             return action, logp, value
         logits, value = self.policy_value(obs)
         if logits_out is not None:

@@ -62,8 +62,10 @@ class SparseHead:
             self._bucket_E = E
 
     def sample_bucketed(self, X: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor,
-                        rng: torch.Tensor, logp_out: torch.Tensor) -> torch.Tensor:
-        """Sample with the buckets the decode kernel built this step (no sort: 3 launches)."""
+                        rng: torch.Tensor, logp_out: torch.Tensor,
+                        act16_out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sample with the buckets the decode kernel built this step (no sort: 3 launches).
+        act16_out: also pack the actions into the env's 16-bit codes in the last launch."""
         F = X.shape[0]
         assert F == self._bucket_E
         k = N.kernels()
@@ -78,6 +80,11 @@ class SparseHead:
                                self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
                                self.fwd_grid, self.cell_lp.data_ptr(), None, 0, st),
                 "head_fwd")
+        if act16_out is not None:
+            N.check(k.mbk_row_sum_pack(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
+                                       rng.data_ptr(), action.data_ptr(), act16_out.data_ptr(),
+                                       st), "row_sum_pack")
+            return logp_out
         N.check(k.mbk_row_sum_rng(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
                                   rng.data_ptr(), st), "row_sum_rng")
         return logp_out
@@ -216,7 +223,7 @@ def sparse_score(X, W, b, mask_bits, action, head: SparseHead):
 
 @torch.no_grad()
 def sparse_sample(X, W, b, mask_bits, rng, head: SparseHead, action_out=None, logp_out=None,
-                  prepacked: bool = False, bucketed: bool = False):
+                  prepacked: bool = False, bucketed: bool = False, act16_out=None):
     F = X.shape[0]
     if action_out is None:
         action_out = torch.empty(F, head.S, 7, dtype=torch.uint8, device=X.device)
@@ -226,7 +233,7 @@ def sparse_sample(X, W, b, mask_bits, rng, head: SparseHead, action_out=None, lo
         if logp_out is None:
             logp_out = torch.empty(F, dtype=torch.float32, device=X.device)
         return action_out, head.sample_bucketed(X.contiguous(), mask_bits.contiguous(),
-                                                action_out, rng, logp_out)
+                                                action_out, rng, logp_out, act16_out)
     logp, _ = head.forward(X.contiguous(), mask_bits.contiguous(), action_out, sample=True,
                            rng=rng, logp_out=logp_out, want_ent=False)
     return action_out, logp

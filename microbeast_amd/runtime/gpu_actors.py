@@ -237,6 +237,7 @@ class GpuActorRuntime:
         # sparse-head models (flat IMPALA head) bucket their active pairs in the decode pass;
         # dense-head models (GridNet) sample with the masked-cell kernel
         hip = hasattr(m, "_head") and m._use_hip(io["in_obs"])
+        packed = False
         if hip:
             # decode + bucket the sparse head's active pairs by cell in the same pass
             head = m._head(self.device)
@@ -246,9 +247,12 @@ class GpuActorRuntime:
                 io["in_obs"].data_ptr(), io["in_mask"].data_ptr(), head.bucket_cnt.data_ptr(),
                 head.bucket.data_ptr(), head.cell_lp.data_ptr(), io["out_action"].data_ptr(),
                 st), "decode_obs_mask_bucket")
+            # the head's last launch also packs the env action codes (row_sum_pack)
             _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
                                 logp_out=io["out_logp"], bucketed=True,
-                                logits_out=io.get("out_logits"), value_out=io["out_value"])
+                                logits_out=io.get("out_logits"), value_out=io["out_value"],
+                                act16_out=io["out_act16"])
+            packed = True
         else:
             N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
                                           self.E, self.size, self.size, io["in_obs"].data_ptr(),
@@ -260,9 +264,10 @@ class GpuActorRuntime:
                                  cell_logp=io["cell_logp"], logp_out=io["out_logp"])
         if value.data_ptr() != io["out_value"].data_ptr():  # (written in place when fused)
             io["out_value"].copy_(value.view(-1))
-        N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
-                                       io["out_act16"].data_ptr(), N.stream_ptr()),
-                "pack_env_actions")
+        if not packed:
+            N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
+                                           io["out_act16"].data_ptr(), N.stream_ptr()),
+                    "pack_env_actions")
 
     def _capture_pack(self, model):
         """Graph of ``model.pack_inference`` (derived weight buffers), replayed by the engine

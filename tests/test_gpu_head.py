@@ -154,3 +154,30 @@ def test_fused_fc_forward_matches_torch(cuda):
         vr = fr.bfloat16().float() @ wc + bc
         torch.testing.assert_close(f.float(), fr, rtol=1e-2, atol=1e-2)
         torch.testing.assert_close(v, vr, rtol=1e-3, atol=1e-3)
+
+
+def test_policy_step_fused_pack_matches_pack_kernel(cuda):
+    """The policy step's last head launch (row_sum_pack) writes the env's 16-bit action codes:
+    equal to pack_env_actions over the step's action bytes; the per-env log-prob equals the
+    row sum of the step's per-cell log-probs."""
+    from microbeast_amd import _native as N
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+
+    s = 10
+    rt = GpuActorRuntime(lambda: Agent((s, s, 27)), s, n_groups=1, envs_per_group=96, unroll=4,
+                         batch_slots=1, device=cuda, n_threads=1)
+    io, m = rt.io, rt.infer_model
+    torch.nn.init.normal_(m.actor.weight, std=0.05)
+    m.pack_inference(cuda)
+    io["out_act16"].fill_(0x5555)
+    rt._policy_step(io, m, rt.rng)
+    torch.cuda.synchronize()
+    ref = torch.empty_like(io["out_act16"])
+    N.check(N.kernels().mbk_pack_env_actions(io["out_action"].data_ptr(), 96 * s * s,
+                                             ref.data_ptr(), N.stream_ptr()), "pack")
+    torch.cuda.synchronize()
+    assert torch.equal(io["out_act16"], ref)
+    head = m._head(cuda)
+    lp = head.cell_lp[:96 * s * s].view(96, s * s).sum(1)
+    torch.testing.assert_close(io["out_logp"], lp, rtol=1e-5, atol=1e-5)
