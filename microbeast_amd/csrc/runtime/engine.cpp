@@ -247,8 +247,16 @@ void GpuEngine::stop() {
     if (L.s_out) hipStreamSynchronize(L.s_out);
   }
   // an enqueue that failed between the gate's set and clear must not leave the learner's
-  // stream waiting forever
-  if (gate_) hipMemset(gate_, 0, sizeof(uint32_t));
+  // stream waiting forever. On a non-blocking stream: a plain hipMemset would queue on the
+  // null stream behind the very learner work that is waiting for the flag
+  if (gate_) {
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
+      (void)hipMemsetAsync(gate_, 0, sizeof(uint32_t), s);
+      (void)hipStreamSynchronize(s);
+      (void)hipStreamDestroy(s);
+    }
+  }
 }
 
 void GpuEngine::dispatch_env(int g) {
