@@ -101,7 +101,9 @@ _SIGS = {
                        c_void_p],
     "mbk_row_sum_rng": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_row_sum_pack": [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p],
+                         c_void_p, c_int, c_void_p],
+    "mbk_head_fwd_counts": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                            c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_trunk_tail": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_trunk_tail_fp8": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                            c_void_p],

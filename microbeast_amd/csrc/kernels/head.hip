@@ -232,21 +232,70 @@ __global__ __launch_bounds__(1024) void head_units_kernel(int* __restrict__ cnt,
 
 // ------------------------------------------------------------------ forward
 // Persistent: each wave takes 16-pair units until none is left.
+// cnt != null (acting, decode-bucketed pairs): the unit list is derived in every workgroup from
+// the per-cell bucket counts (a 16-pair-unit prefix over the S cells in LDS, then a binary
+// search per unit) -- head_units_kernel's unit_cell / unit_row / grp_* / totals without its
+// launch; the counters are reset by the step's last launch (row_sum_pack).
+constexpr int kMaxUnitCells = 1024;
 __global__ __launch_bounds__(256) void head_fwd_kernel(
     const bf16* __restrict__ X, const bf16* __restrict__ Wp, const float* __restrict__ bp,
     const uint32_t* __restrict__ mask, uint8_t* __restrict__ action, const uint64_t* __restrict__ rng,
     int sample, const int* __restrict__ pairs, const int* __restrict__ unit_cell,
     const int* __restrict__ unit_row, const int* __restrict__ grp_start,
     const int* __restrict__ grp_count, const int* __restrict__ totals, int S,
-    float* __restrict__ cell_lp, float* __restrict__ cell_ent, int pair_out) {
+    float* __restrict__ cell_lp, float* __restrict__ cell_ent, int pair_out,
+    const int* __restrict__ cnt, int E) {
   __shared__ float zs[4][16][NP + 1];
+  __shared__ int upre[kMaxUnitCells + 1];  // count mode: units before cell c
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
-  const int nunits = totals[1];
+  int nunits;
+  if (cnt) {
+    // exclusive prefix of ceil(cnt / 16) over the S cells: wave 0, 16 cells per lane
+    if (wave == 0) {
+      int loc[16], run = 0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int c = lane * 16 + k;
+        loc[k] = run;
+        run += c < S ? (cnt[c] + 15) / 16 : 0;
+      }
+      int x = run;  // inclusive wave scan of the lane totals
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      const int base = x - run;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int c = lane * 16 + k;
+        if (c <= S) upre[c] = base + loc[k];
+      }
+      if (lane == 63) upre[kMaxUnitCells] = x;
+    }
+    __syncthreads();
+    nunits = upre[kMaxUnitCells];
+  } else {
+    nunits = totals[1];
+  }
   float (*z)[NP + 1] = zs[wave];
   for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
-    const int c = unit_cell[u], r0 = unit_row[u];
-    const int gend = grp_start[c] + grp_count[c];
+    int c, r0, gend;
+    if (cnt) {  // last cell whose prefix <= u (cells without units share the next one's)
+      int lo = 0, hi = S - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (upre[mid] <= u) lo = mid; else hi = mid - 1;
+      }
+      c = lo;
+      r0 = c * E + 16 * (u - upre[c]);
+      gend = c * E + cnt[c];
+    } else {
+      c = unit_cell[u];
+      r0 = unit_row[u];
+      gend = grp_start[c] + grp_count[c];
+    }
     const int r = r0 + li;
     const bool valid = r < gend;
     const int f = valid ? pairs[r] : pairs[r0];
@@ -728,7 +777,23 @@ extern "C" int mbk_head_fwd(const void* X, const void* Wp, const float* bp, cons
                             float* cell_lp, float* cell_ent, int pair_out, hipStream_t stream) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const bf16*)X,
                      (const bf16*)Wp, bp, mask, action, rng, sample, pairs, unit_cell, unit_row,
-                     grp_start, grp_count, totals, S, cell_lp, cell_ent, pair_out);
+                     grp_start, grp_count, totals, S, cell_lp, cell_ent, pair_out,
+                     (const int*)nullptr, 0);
+  return (int)hipGetLastError();
+}
+
+// Acting head on decode-bucketed pairs (cell c's pairs at bucket[c * E, + cnt[c])) without
+// head_units: every workgroup derives the 16-pair units from cnt (left for the caller to
+// reset: mbk_row_sum_pack's cnt argument). S <= 1024.
+extern "C" int mbk_head_fwd_counts(const void* X, const void* Wp, const float* bp,
+                                   const uint32_t* mask, uint8_t* action, const uint64_t* rng,
+                                   const int* bucket, const int* cnt, int E, int S, int grid,
+                                   float* cell_lp, hipStream_t stream) {
+  if (S < 1 || S > kMaxUnitCells - 1 || !cnt) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid), dim3(256), 0, stream, (const bf16*)X,
+                     (const bf16*)Wp, bp, mask, action, rng, 1, bucket, (const int*)nullptr,
+                     (const int*)nullptr, (const int*)nullptr, (const int*)nullptr,
+                     (const int*)nullptr, S, cell_lp, (float*)nullptr, 0, cnt, E);
   return (int)hipGetLastError();
 }
 

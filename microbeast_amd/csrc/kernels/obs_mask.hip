@@ -261,9 +261,13 @@ __global__ __launch_bounds__(256) void row_sum_pack_kernel(const float* __restri
                                                            float* __restrict__ logp,
                                                            uint64_t* __restrict__ rng,
                                                            const uint8_t* __restrict__ act,
-                                                           uint16_t* __restrict__ act16) {
+                                                           uint16_t* __restrict__ act16,
+                                                           int* __restrict__ cnt, int ncnt) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (rng && blockIdx.x == 0 && threadIdx.x == 0) rng[1] += 1;
+  // the decode kernel's per-cell bucket counters, read by the head launch before this one
+  if (cnt && blockIdx.x == 0)
+    for (int c = threadIdx.x; c < ncnt; c += blockDim.x) cnt[c] = 0;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   if (r >= rows) return;
   float s = 0.f;
@@ -282,12 +286,13 @@ __global__ __launch_bounds__(256) void row_sum_pack_kernel(const float* __restri
 }  // namespace
 
 // logp[r] = sum_c cell_lp[r][c], act16[r][c] = packed act[r][c][0..6], rng step advance.
+// cnt (may be null): ncnt bucket counters zeroed for the next step (head_fwd_counts mode).
 extern "C" int mbk_row_sum_pack(const float* cell_lp, int64_t rows, int cols, float* logp,
-                                uint64_t* rng, const uint8_t* act, uint16_t* act16,
-                                hipStream_t stream) {
+                                uint64_t* rng, const uint8_t* act, uint16_t* act16, int* cnt,
+                                int ncnt, hipStream_t stream) {
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(row_sum_pack_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, stream,
-                     cell_lp, rows, cols, logp, rng, act, act16);
+                     cell_lp, rows, cols, logp, rng, act, act16, cnt, ncnt);
   return (int)hipGetLastError();
 }
 

@@ -33,6 +33,9 @@ class SparseHead:
         self._F = -1
         n_cu = torch.cuda.get_device_properties(device).multi_processor_count if device.type == "cuda" else 1
         self.fwd_grid = 2 * n_cu
+        # acting: derive the 16-pair units from the decode's bucket counts inside head_fwd
+        # (no head_units launch); False: the separate head_units kernel (reference path)
+        self.count_units = True
 
     def _ensure(self, F: int):
         if F <= self._F:
@@ -70,6 +73,18 @@ class SparseHead:
         assert F == self._bucket_E
         k = N.kernels()
         st = N.stream_ptr()
+        if act16_out is not None and self.count_units and self.S < 1024:
+            # 2 launches: the head derives its units from the bucket counts itself, the
+            # finale sums log-probs, packs the env actions and resets the counts
+            N.check(k.mbk_head_fwd_counts(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
+                                          mask_bits.data_ptr(), action.data_ptr(),
+                                          rng.data_ptr(), self.bucket.data_ptr(),
+                                          self.bucket_cnt.data_ptr(), F, self.S, self.fwd_grid,
+                                          self.cell_lp.data_ptr(), st), "head_fwd_counts")
+            N.check(k.mbk_row_sum_pack(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
+                                       rng.data_ptr(), action.data_ptr(), act16_out.data_ptr(),
+                                       self.bucket_cnt.data_ptr(), self.S, st), "row_sum_pack")
+            return logp_out
         N.check(k.mbk_head_units(self.bucket_cnt.data_ptr(), self.S, F, self.grp_start.data_ptr(),
                                  self.grp_count.data_ptr(), self.unit_cell.data_ptr(),
                                  self.unit_row.data_ptr(), self.totals.data_ptr(), st), "head_units")
@@ -83,7 +98,7 @@ class SparseHead:
         if act16_out is not None:
             N.check(k.mbk_row_sum_pack(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
                                        rng.data_ptr(), action.data_ptr(), act16_out.data_ptr(),
-                                       st), "row_sum_pack")
+                                       None, 0, st), "row_sum_pack")
             return logp_out
         N.check(k.mbk_row_sum_rng(self.cell_lp.data_ptr(), F, self.S, logp_out.data_ptr(),
                                   rng.data_ptr(), st), "row_sum_rng")

@@ -181,3 +181,16 @@ def test_policy_step_fused_pack_matches_pack_kernel(cuda):
     head = m._head(cuda)
     lp = head.cell_lp[:96 * s * s].view(96, s * s).sum(1)
     torch.testing.assert_close(io["out_logp"], lp, rtol=1e-5, atol=1e-5)
+    # same step through head_units + head_fwd + row_sum_rng + pack (counts not derived in the
+    # head): identical actions, log-probs and codes from the same RNG state
+    got = {k: io[k].clone() for k in ("out_action", "out_logp", "out_act16")}
+    rt.rng[1] -= 1
+    head.count_units = False
+    try:
+        rt._policy_step(io, m, rt.rng)
+        torch.cuda.synchronize()
+    finally:
+        head.count_units = True
+    for k, v in got.items():
+        assert torch.equal(io[k], v), k
+    assert int(head.bucket_cnt.abs().sum()) == 0  # counters reset for the next step
