@@ -136,6 +136,10 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   }
   // work chunk: enough chunks for every worker, at least 2 envs each
   chunk_ = std::max(1, std::min(16, cfg_.envs_per_group / std::max(1, 2 * cfg_.n_threads)));
+  if (const char* c = std::getenv("MBK_ENV_CHUNK")) {  // envs per work item (A/B knob)
+    const int v = std::atoi(c);
+    if (v > 0) chunk_ = std::max(1, std::min(v, cfg_.envs_per_group));
+  }
   if (cfg_.policy_gate && cfg_.n_lanes == 1) {
     CTOR_CHECK(hipMalloc((void**)&gate_, sizeof(uint32_t)));
     CTOR_CHECK(hipMemset(gate_, 0, sizeof(uint32_t)));
