@@ -3,6 +3,9 @@
 
 #include <chrono>
 #include <cstdlib>
+
+#include <pthread.h>
+#include <sched.h>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -293,7 +296,35 @@ void GpuEngine::dispatch_env(int g) {
   work_cv_.notify_all();
 }
 
+// MBK_PIN_WORKERS=1: env worker w runs on the w-th CPU of the process's affinity set (the
+// rank's NUMA-local share, parallel/launch.py pin_rank), so the scheduler never migrates a
+// worker mid-group-step; the driver and Python keep the whole set
+static void pin_worker(int wid) {
+  static const bool on = [] {
+    const char* e = std::getenv("MBK_PIN_WORKERS");
+    return e && e[0] == '1';
+  }();
+  if (!on) return;
+  cpu_set_t all;
+  CPU_ZERO(&all);
+  if (sched_getaffinity(0, sizeof(all), &all) != 0) return;
+  const int n = CPU_COUNT(&all);
+  if (n < 2) return;
+  int k = wid % n;
+  for (int c = 0; c < CPU_SETSIZE; ++c) {
+    if (!CPU_ISSET(c, &all)) continue;
+    if (k-- == 0) {
+      cpu_set_t one;
+      CPU_ZERO(&one);
+      CPU_SET(c, &one);
+      (void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+      return;
+    }
+  }
+}
+
 void GpuEngine::worker_loop(int wid) {
+  pin_worker(wid);
   const int E = cfg_.envs_per_group, NG = cfg_.n_groups;
   while (running_.load(std::memory_order_relaxed)) {
     const uint64_t epoch = work_epoch_.load();
