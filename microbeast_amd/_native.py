@@ -143,6 +143,10 @@ _SIGS = {
                       c_int, c_int, c_void_p],
     "mbk_fc_wgrad_ex": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                         c_int, c_void_p],
+    # fused acting step (ops/act.py): (const MbkActModel*, const MbkActStep*, stream)
+    "mbk_act_step": [c_void_p, c_void_p, c_void_p],
+    "mbk_act_trunk": [c_void_p, c_void_p, c_void_p],
+    "mbk_act_head": [c_void_p, c_void_p, c_void_p],
     "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_void_p, c_void_p],
 }

@@ -38,6 +38,59 @@ typedef struct {
 
 int mbk_conv_pack_fp8(const MbkPackJob8* jobs, int n, hipStream_t stream);
 
+// ---- fused acting step (act.hip-level API; kernels in trunk.hip + head.hip) ----------------
+// One policy step of the flat IMPALA agent on a 16x16 map in TWO launches:
+//   A (trunk.hip act_trunk_kernel): per 16-env tile, 16-bit codes -> obs bit planes + 78-bit
+//     masks (written straight into the rollout row), per-cell buckets of active pairs, stage-0
+//     conv with the max-pool in registers, the 14 trunk convs in LDS, network.5 + critic;
+//   B (head.hip head_act_kernel): sparse head GEMM + masked sampling per 16-pair unit, per-env
+//     completion counters: the wave that finishes an env's last active cell sums its log-prob
+//     and writes its packed 16-bit actions; the last workgroup resets the buckets and advances
+//     the sampler's step counter.
+// Model / workspace pointers are fixed per policy lane; step pointers change every step.
+typedef struct {
+  const void* w0;          // stage-0 conv packed fwd weights [16][9][32] bf16
+  const float* b0;         // [16]
+  const void* w[14];       // trunk layers 1..14 packed fwd weights (bf16)
+  const float* b[14];
+  const void* w5;          // network.5 [256][H2*W2*32] bf16, NHWC column order
+  const float* b5;         // [256]
+  const float* wc;         // critic [256]
+  const float* bc;         // [1]
+  const void* Wp;          // sparse head [S][80][256] bf16
+  const float* bp;         // [S][80]
+  uint64_t* rng;           // Philox (seed, step)
+  void* feat;              // workspace: network.5 output [E][256] bf16
+  int* bucket_cnt;         // [S], zero between steps
+  int* bucket;             // [S][E]
+  uint64_t* cellx;         // [E][S] per-cell {log-prob bits, packed action} of the step
+  int* pending;            // [E] active cells not yet sampled
+  unsigned* done_ctr;      // [1], zero between steps
+  int E, H, W;
+} MbkActModel;
+
+typedef struct {
+  const uint16_t* codes;   // [E][S] (device or pinned host)
+  const int32_t* res;      // [E]
+  uint32_t* obs;           // rollout row [E][S]
+  uint32_t* mask;          // [E][S][3]
+  uint32_t* obs2;          // optional second destination (previous slot's bootstrap row)
+  uint32_t* mask2;
+  uint8_t* action;         // [E][S][7]
+  float* logp;             // [E]
+  float* value;            // [E]
+  uint16_t* act16;         // [E][S] (device or pinned host)
+  const float* reward_src; // optional reward / done of the previous env step -> dst
+  const uint8_t* done_src;
+  float* reward_dst;
+  uint8_t* done_dst;
+} MbkActStep;
+
+int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
+// the two launches separately (mbk_act_step = A then B)
+int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
+int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

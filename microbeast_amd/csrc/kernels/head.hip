@@ -25,6 +25,7 @@
 //                actor.weight/bias gradient rows of that cell (deterministic).
 //   head_dx_gather : dX[f] = sum of dX_pair over f's active cells (no atomics).
 #include "../include/mbk_api.h"
+#include "../include/microrts_rules.h"
 #include "common.h"
 
 using namespace mbk;
@@ -230,13 +231,72 @@ __global__ __launch_bounds__(1024) void head_units_kernel(int* __restrict__ cnt,
   if (tid == 1023) totals[1] = su[1023];
 }
 
+// Z[16 pairs][80] of one 16-pair unit of cell c into the wave's LDS tile z: the X rows of the
+// unit's frames times W_c^T + b_c on v_mfma_f32_16x16x32_bf16 (C layout: row = pair 4G+i,
+// col = logit nb*16 + li). Shared by head_fwd_kernel and the acting step's head_act_kernel.
+__device__ __forceinline__ void unit_z(const bf16* __restrict__ X, const bf16* __restrict__ Wp,
+                                       const float* __restrict__ bp, int f, bool valid, int c,
+                                       float (*z)[NP + 1]) {
+  const int lane = threadIdx.x & 63, G = lane >> 4, li = lane & 15;
+  f32x4 acc[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint4* xrow = (const uint4*)(X + (size_t)f * KD) + G;  // 8 bf16 per uint4
+  const bf16* wc = Wp + (size_t)c * NP * KD;
+#pragma unroll
+  for (int ks = 0; ks < KD / 32; ++ks) {
+    Frag8 a;
+    a.u = valid ? xrow[ks * 4] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      Frag8 b;
+      b.u = *((const uint4*)(wc + (size_t)(nb * 16 + li) * KD + ks * 32) + G);
+      acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) {
+    const int col = nb * 16 + li;
+    const float bias = bp[c * NP + col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[4 * G + i][col] = acc[nb][i] + bias;
+  }
+}
+
+// exclusive prefix of ceil(cnt / 16) over the S <= kMaxUnitCells cells into upre (wave 0, 16
+// cells per lane; upre[kMaxUnitCells] = the unit total). Caller barriers before reading it.
+constexpr int kMaxUnitCells = 1024;
+__device__ __forceinline__ void unit_prefix(const int* __restrict__ cnt, int S, int* upre) {
+  const int lane = threadIdx.x & 63;
+  if ((threadIdx.x >> 6) != 0) return;
+  int loc[16], run = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = lane * 16 + k;
+    loc[k] = run;
+    run += c < S ? (cnt[c] + 15) / 16 : 0;
+  }
+  int x = run;  // inclusive wave scan of the lane totals
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  const int base = x - run;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = lane * 16 + k;
+    if (c <= S) upre[c] = base + loc[k];
+  }
+  if (lane == 63) upre[kMaxUnitCells] = x;
+}
+
 // ------------------------------------------------------------------ forward
 // Persistent: each wave takes 16-pair units until none is left.
 // cnt != null (acting, decode-bucketed pairs): the unit list is derived in every workgroup from
 // the per-cell bucket counts (a 16-pair-unit prefix over the S cells in LDS, then a binary
 // search per unit) -- head_units_kernel's unit_cell / unit_row / grp_* / totals without its
 // launch; the counters are reset by the step's last launch (row_sum_pack).
-constexpr int kMaxUnitCells = 1024;
 __global__ __launch_bounds__(256) void head_fwd_kernel(
     const bf16* __restrict__ X, const bf16* __restrict__ Wp, const float* __restrict__ bp,
     const uint32_t* __restrict__ mask, uint8_t* __restrict__ action, const uint64_t* __restrict__ rng,
@@ -251,29 +311,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
   const int G = lane >> 4, li = lane & 15;
   int nunits;
   if (cnt) {
-    // exclusive prefix of ceil(cnt / 16) over the S cells: wave 0, 16 cells per lane
-    if (wave == 0) {
-      int loc[16], run = 0;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int c = lane * 16 + k;
-        loc[k] = run;
-        run += c < S ? (cnt[c] + 15) / 16 : 0;
-      }
-      int x = run;  // inclusive wave scan of the lane totals
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      const int base = x - run;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int c = lane * 16 + k;
-        if (c <= S) upre[c] = base + loc[k];
-      }
-      if (lane == 63) upre[kMaxUnitCells] = x;
-    }
+    unit_prefix(cnt, S, upre);
     __syncthreads();
     nunits = upre[kMaxUnitCells];
   } else {
@@ -299,30 +337,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     const int r = r0 + li;
     const bool valid = r < gend;
     const int f = valid ? pairs[r] : pairs[r0];
-    f32x4 acc[5];
-#pragma unroll
-    for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const uint4* xrow = (const uint4*)(X + (size_t)f * KD) + G;  // 8 bf16 per uint4
-    const bf16* wc = Wp + (size_t)c * NP * KD;
-#pragma unroll
-    for (int ks = 0; ks < KD / 32; ++ks) {
-      Frag8 a;
-      a.u = valid ? xrow[ks * 4] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int nb = 0; nb < 5; ++nb) {
-        Frag8 b;
-        b.u = *((const uint4*)(wc + (size_t)(nb * 16 + li) * KD + ks * 32) + G);
-        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
-      }
-    }
-    // C layout: row (pair) 4G+i, col (logit) nb*16 + li
-#pragma unroll
-    for (int nb = 0; nb < 5; ++nb) {
-      const int col = nb * 16 + li;
-      const float bias = bp[c * NP + col];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) z[4 * G + i][col] = acc[nb][i] + bias;
-    }
+    unit_z(X, Wp, bp, f, valid, c, z);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of this wave visible
     __builtin_amdgcn_wave_barrier();
     if (lane < 16 && valid) {
@@ -355,6 +370,120 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
       if (cell_ent) cell_ent[o] = ent;
     }
     __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------ acting step, launch B
+// head_fwd_kernel's count-mode sampling (same units, GEMM, Philox stream and cell epilogue) with
+// the policy step's finale folded in, so a step is two launches (trunk.hip act_trunk_kernel +
+// this one) instead of head + row_sum_pack:
+//   * each sampled pair stores {log-prob, packed env action} as ONE 8-byte write-through (sc1)
+//     granule in its env's per-cell row, drains it (vmcnt(0)), then decrements its env's
+//     pending-cell counter (agent-scope atomic, set by launch A);
+//   * the lane whose decrement empties the counter hands the env to its wave, which reads the
+//     env's row with sc1 loads only (no fence: MI355X_MICROARCH.md "Valid forms" -- every byte
+//     stored sc1 and drained before the signal, every load of it sc1) and writes the env's
+//     log-prob (row_sum_pack's lane-strided sum + wave_sum: bit-identical) and its 16-bit
+//     action codes (one coalesced 128-byte store per 64 cells, also to pinned host memory);
+//   * the workgroup whose arrival ticket comes last resets the per-cell bucket counters and
+//     advances the sampler's step counter (every other workgroup has read both by then).
+struct HeadActArgs {
+  const bf16* X;
+  const bf16* Wp;
+  const float* bp;
+  const uint32_t* mask;
+  uint8_t* action;
+  uint64_t* rng;
+  const int* bucket;
+  int* cnt;
+  uint64_t* cellx;
+  uint16_t* act16;
+  float* logp;
+  int* pending;
+  unsigned* done_ctr;
+  int S, E;
+};
+
+__global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
+  __shared__ float zs[4][16][NP + 1];
+  __shared__ int upre[kMaxUnitCells + 1];
+  __shared__ int last_wg;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int li = lane & 15;
+  const int S = a.S, E = a.E;
+  unit_prefix(a.cnt, S, upre);
+  __syncthreads();
+  const int nunits = upre[kMaxUnitCells];
+  const uint64_t seed = a.rng[0], step = a.rng[1];
+  float (*z)[NP + 1] = zs[wave];
+  for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
+    int lo = 0, hi = S - 1;  // last cell whose prefix <= u
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (upre[mid] <= u) lo = mid; else hi = mid - 1;
+    }
+    const int c = lo;
+    const int r0 = c * E + 16 * (u - upre[c]);
+    const int gend = c * E + a.cnt[c];
+    const int r = r0 + li;
+    const bool valid = r < gend;
+    const int f = valid ? a.bucket[r] : a.bucket[r0];
+    unit_z(a.X, a.Wp, a.bp, f, valid, c, z);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of this wave visible
+    __builtin_amdgcn_wave_barrier();
+    const bool mine = lane < 16 && valid;
+    if (mine) {
+      const size_t fc = (size_t)f * S + c;
+      uint32_t m[3] = {a.mask[fc * 3], a.mask[fc * 3 + 1], a.mask[fc * 3 + 2]};
+      uint8_t act[kComps];
+      float uu[kComps];
+      u32x4 ctr = {(uint32_t)fc, (uint32_t)(fc >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
+      u32x4 q0 = philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+      ctr.y ^= 0x80000000u;
+      u32x4 q1 = philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+      uu[0] = u01(q0.x); uu[1] = u01(q0.y); uu[2] = u01(q0.z); uu[3] = u01(q0.w);
+      uu[4] = u01(q1.x); uu[5] = u01(q1.y); uu[6] = u01(q1.z);
+      float lp, ent;
+      cell_forward(&z[lane][0], m, act, true, uu, &lp, &ent);
+#pragma unroll
+      for (int k = 0; k < kComps; ++k) a.action[fc * kComps + k] = act[k];
+      const uint64_t x = (uint64_t)__float_as_uint(lp) |
+                         ((uint64_t)mbr::pack_env_action(act) << 32);
+      __hip_atomic_store(a.cellx + fc, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every granule drained before its signal
+    bool fin = false;
+    if (mine)
+      fin = __hip_atomic_fetch_add(a.pending + f, -1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == 1;
+    uint64_t bm = __ballot(fin);
+    while (bm) {  // envs whose last active cell this wave sampled
+      const int l = __builtin_ctzll(bm);
+      bm &= bm - 1;
+      const int fe = __shfl(f, l, 64);
+      const uint64_t* row = a.cellx + (size_t)fe * S;
+      float s = 0.f;
+      for (int cc = lane; cc < S; cc += 64) {
+        const uint64_t x = __hip_atomic_load(row + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s += __uint_as_float((uint32_t)x);
+        a.act16[(size_t)fe * S + cc] = (uint16_t)(x >> 32);
+      }
+      s = wave_sum(s);
+      if (lane == 0) a.logp[fe] = s;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();  // this workgroup is done with cnt and rng
+  if (threadIdx.x == 0)
+    last_wg = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+              gridDim.x - 1;
+  __syncthreads();
+  if (last_wg) {
+    for (int c = threadIdx.x; c < S; c += blockDim.x) a.cnt[c] = 0;
+    if (threadIdx.x == 0) {
+      a.rng[1] = step + 1;
+      *a.done_ctr = 0u;
+    }
   }
 }
 
@@ -864,4 +993,49 @@ extern "C" int mbk_head_pack(const float* W, const float* b, int S, void* Wp, fl
   hipLaunchKernelGGL(head_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, W, b, S,
                      (bf16*)Wp, bp, (bf16*)WpT);
   return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ fused acting step, launch B
+extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
+  if (!m || !s || m->E <= 0) return (int)hipErrorInvalidValue;
+  const int S = m->H * m->W;
+  if (S < 1 || S > kMaxUnitCells - 1 || (S & 3)) return (int)hipErrorInvalidValue;
+  if (!m->feat || !m->Wp || !m->bp || !m->rng || !m->bucket || !m->bucket_cnt || !m->cellx ||
+      !m->pending || !m->done_ctr || !s->mask || !s->action || !s->act16 || !s->logp)
+    return (int)hipErrorInvalidValue;
+  if ((uintptr_t)m->cellx & 7) return (int)hipErrorInvalidValue;
+  HeadActArgs a{};
+  a.X = (const bf16*)m->feat;
+  a.Wp = (const bf16*)m->Wp;
+  a.bp = m->bp;
+  a.mask = s->mask;
+  a.action = s->action;
+  a.rng = m->rng;
+  a.bucket = m->bucket;
+  a.cnt = m->bucket_cnt;
+  a.cellx = m->cellx;
+  a.act16 = s->act16;
+  a.logp = s->logp;
+  a.pending = m->pending;
+  a.done_ctr = m->done_ctr;
+  a.S = S;
+  a.E = m->E;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  hipLaunchKernelGGL(head_act_kernel, dim3(2 * cus), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
+
+// the whole acting step: A (decode + trunk + network.5 + critic) then B (sample + finale)
+extern "C" int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
+  const int rc = mbk_act_trunk(m, s, stream);
+  if (rc) return rc;
+  return mbk_act_head(m, s, stream);
 }

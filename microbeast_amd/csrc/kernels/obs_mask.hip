@@ -10,12 +10,12 @@
 #include "../include/mbk_api.h"
 #include "../include/microrts_rules.h"
 #include "common.h"
+#include "decode.h"
 
 namespace {
 
 using namespace mbr;
-
-__device__ __forceinline__ void setb(uint32_t w[3], int j) { w[j >> 5] |= 1u << (j & 31); }
+using mbk::cell_mask;
 
 // Per-step sparse-head bookkeeping for acting (BUCKET): every active (env, cell) pair is
 // appended to its cell's bucket (bucket[c * E + slot], slot from an atomic counter; order
@@ -28,72 +28,6 @@ struct Buckets {
   float* cell_lp;  // [E*S]
   uint8_t* action; // [E*S*7]
 };
-
-// 78-bit action mask of cell c (real frame, player 1 = "own" in the code) from the env's
-// codes in LDS, exactly the simulator's rules (include/microrts_rules.h).
-__device__ __forceinline__ void cell_mask(const uint16_t* cs, int c, int H, int W, int r,
-                                          uint32_t w[3]) {
-  w[0] = w[1] = w[2] = 0u;
-  const uint16_t code = cs[c];
-  const int t = code_type(code);
-  // own (owner 1), idle (act noop <=> busy == 0), not a resource
-  if (!(code_owner(code) == 1 && code_act(code) == A_NOOP && t != RESOURCE && t != NONE)) return;
-  const int y = c / W, x = c - y * W;
-  setb(w, kSegOff[0] + A_NOOP);
-  bool any_move = false, any_harv = false, any_ret = false, any_prod = false, any_att = false;
-  const bool mobile = t >= WORKER;
-  const int carried = code_res(code);
-#pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const int nx = x + kDX[d], ny = y + kDY[d];
-    if (nx < 0 || ny < 0 || nx >= W || ny >= H) continue;
-    const uint16_t nc = cs[ny * W + nx];
-    const int nt = code_type(nc);
-    if (nt == NONE) {
-      if (mobile) { setb(w, kSegOff[1] + d); any_move = true; }
-      const bool can_prod = (t == BASE && r >= spec_cost(WORKER)) ||
-                            (t == BARRACKS && r >= spec_cost(LIGHT)) ||
-                            (t == WORKER && r >= spec_cost(BARRACKS));
-      if (can_prod) { setb(w, kSegOff[4] + d); any_prod = true; }
-    } else {
-      if (t == WORKER && nt == RESOURCE && carried == 0 && code_res(nc) > 0) {
-        setb(w, kSegOff[2] + d); any_harv = true;
-      }
-      if (t == WORKER && nt == BASE && code_owner(nc) == 1 && carried > 0) {
-        setb(w, kSegOff[3] + d); any_ret = true;
-      }
-    }
-  }
-  if (any_prod) {
-    if (t == BASE) setb(w, kSegOff[5] + (WORKER - 1));
-    if (t == BARRACKS) {
-      if (r >= spec_cost(LIGHT)) setb(w, kSegOff[5] + (LIGHT - 1));
-      if (r >= spec_cost(HEAVY)) setb(w, kSegOff[5] + (HEAVY - 1));
-      if (r >= spec_cost(RANGED)) setb(w, kSegOff[5] + (RANGED - 1));
-    }
-    if (t == WORKER) {
-      if (r >= spec_cost(BASE)) setb(w, kSegOff[5] + (BASE - 1));
-      if (r >= spec_cost(BARRACKS)) setb(w, kSegOff[5] + (BARRACKS - 1));
-    }
-  }
-  if (spec_damage(t) > 0) {
-    const int R = spec_range(t);
-    for (int ay = -3; ay <= 3; ++ay)
-      for (int ax = -3; ax <= 3; ++ax) {
-        if (ax * ax + ay * ay > R * R || (ax == 0 && ay == 0)) continue;
-        const int tx = x + ax, ty = y + ay;
-        if (tx < 0 || ty < 0 || tx >= W || ty >= H) continue;
-        if (code_owner(cs[ty * W + tx]) == 2) {
-          setb(w, kSegOff[6] + (ay + 3) * 7 + (ax + 3)); any_att = true;
-        }
-      }
-  }
-  if (any_move) setb(w, kSegOff[0] + A_MOVE);
-  if (any_harv) setb(w, kSegOff[0] + A_HARVEST);
-  if (any_ret) setb(w, kSegOff[0] + A_RETURN);
-  if (any_prod) setb(w, kSegOff[0] + A_PRODUCE);
-  if (any_att) setb(w, kSegOff[0] + A_ATTACK);
-}
 
 // One WAVE per env, EPW envs per workgroup, persistent over env groups (grid sized
 // to the device). A lane owns Q = ceil(S/64) consecutive cells, so an env's obs words and

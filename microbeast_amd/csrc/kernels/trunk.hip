@@ -21,6 +21,7 @@
 // fp32 accumulation, pool over bf16-rounded values).
 #include "../include/mbk_api.h"
 #include "common.h"
+#include "decode.h"
 
 extern "C" int mbk_get_cu_budget();
 
@@ -676,6 +677,302 @@ __global__ __launch_bounds__(kThreads) void trunk_tail8_kernel(TrunkArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ fused acting step, launch A
+// Everything of a policy step up to the sparse head in ONE launch (reference model.py:152-160,
+// 205, 219-220, on the engine's compact codes instead of float planes). Per tile of TNI envs a
+// workgroup
+//   P1  reads the envs' 16-bit cell codes + resources (device or pinned host) into LDS;
+//   P2  decodes them (one wave per env, 4 consecutive cells per lane: obs_mask.hip's maths) into
+//       the obs bit planes and the 78-bit masks, stored straight into the rollout row (and the
+//       previous slot's bootstrap row), lists the active (env, cell) pairs in LDS, zeroes the
+//       env's action row and per-cell step scratch and sets its pending-cell count;
+//   P3  reserves each active cell's bucket range with one global atomic per (tile, cell) and runs
+//       the stage-0 conv (conv0_row_kernel's maths: bit planes through an LDS byte table, the
+//       kx = 0 / 2 taps by DPP) with its 3x3/2 max-pool in registers (vertical max over the row
+//       pair and the previous row, horizontal max by DPP row shifts with -inf fill), writing the
+//       pooled 8x8x16 map into the X0 tile, so the stage-0 output never leaves LDS;
+// then the 14 trunk convs + network.5 + critic exactly as trunk_tail_kernel<false, true>. The
+// prologue's scratch lives in region R2, which stage 0 needs only from its first conv on.
+struct ActTrunkArgs {
+  TrunkArgs t;  // layers 1..14 and the fused head: f_out = feat, v_out = the rollout row's values
+  const bf16* w0;  // stage-0 conv, packed [16][9][32]
+  const float* b0;
+  const uint16_t* codes;
+  const int32_t* res;
+  uint32_t* obs;
+  uint32_t* mask;
+  uint32_t* obs2;
+  uint32_t* mask2;
+  uint8_t* action;
+  uint64_t* cellx;
+  float* logp;
+  uint16_t* act16;
+  int* pending;
+  int* bucket_cnt;
+  int* bucket;
+  const float* reward_src;
+  const uint8_t* done_src;
+  float* reward_dst;
+  uint8_t* done_dst;
+};
+
+constexpr int kActS = 256;  // 16x16 maps: one map row = one 16-pixel MFMA block
+struct ActLayout {          // byte offsets of the prologue scratch inside R2, tile of tni envs
+  int codes, bits, lut, cnt, np, res, pairs, end;
+};
+__host__ __device__ constexpr ActLayout act_layout(int tni) {
+  ActLayout L{};
+  L.codes = 0;
+  L.bits = L.codes + tni * kActS * 2;
+  L.lut = L.bits + tni * kActS * 4;
+  L.cnt = L.lut + 256 * 16;
+  L.np = L.cnt + kActS * 4;
+  L.res = L.np + 16;
+  L.pairs = L.res + ((tni * 4 + 15) & ~15);
+  L.end = L.pairs + tni * kActS * 8;
+  return L;
+}
+
+__device__ __forceinline__ float bf16_round(float v) { return lo_f(pack2(v, 0.f)); }
+
+// stage-0 conv of one 16x16 image (bit planes [256] u32 in LDS) + max_pool2d(3, 2, 1), into the
+// interior of the halo'd X0 tile at x0 (image im). A wave owns the image; lane (g, li) = column
+// li, channels 4g .. 4g+3. MFMA order per output row = conv0_row_kernel's, values rounded to
+// bf16 before the pool as it pools the bf16 staging tile, so the pooled map is bit-identical.
+__device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* lut,
+                                          const Frag8 bw[9], const float bias[4], char* x0,
+                                          int im) {
+  constexpr int H0 = 8, W0 = 8, PX = TG<16>::PIXB;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int sh = 8 * g;
+  struct R3 {
+    uint32_t l, c, h;
+  };
+  auto row = [&](uint32_t b) {  // LUT offsets of pixels x-1, x, x+1 (this lane's plane byte)
+    R3 r;
+    r.c = ((b >> sh) & 0xFFu) * 16u;
+    r.l = ((mbk::dpp_shr1_zero(b) >> sh) & 0xFFu) * 16u;
+    r.h = ((mbk::dpp_shl1_zero(b) >> sh) & 0xFFu) * 16u;
+    return r;
+  };
+  uint32_t rows[16];
+#pragma unroll
+  for (int y = 0; y < 16; ++y) rows[y] = bits_img[y * 16 + li];
+  const R3 zero3 = {0u, 0u, 0u};  // LUT entry 0 = all-zero planes
+  R3 r[4];
+  r[0] = zero3;
+  r[1] = row(rows[0]);
+  r[2] = row(rows[1]);
+  r[3] = row(rows[2]);
+  float prev[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};  // conv row y-1
+#pragma unroll
+  for (int y = 0; y < 16; y += 2) {
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        Frag8 f;
+        f.u = *(const uint4*)(lut + (kx == 0 ? r[q].l : kx == 1 ? r[q].c : r[q].h));
+        if (q < 3) acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * q + kx].v, f.v, acc0, 0, 0, 0);
+        if (q > 0) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * (q - 1) + kx].v, f.v, acc1, 0, 0, 0);
+      }
+    }
+    float hm[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float o0 = bf16_round(acc0[i] + bias[i]), o1 = bf16_round(acc1[i] + bias[i]);
+      const float vm = fmaxf(fmaxf(prev[i], o0), o1);  // pooled row y/2: conv rows y-1 .. y+1
+      prev[i] = o1;
+      hm[i] = fmaxf(fmaxf(mbk::dpp_shr1_ninf(vm), vm), mbk::dpp_shl1_ninf(vm));
+    }
+    if ((li & 1) == 0) {
+      const int oy = y >> 1, ox = li >> 1;
+      *(uint2*)(x0 + ((im * (H0 + 2) + oy + 1) * (W0 + 2) + ox + 1) * PX + 8 * g) =
+          make_uint2(pack2(hm[0], hm[1]), pack2(hm[2], hm[3]));
+    }
+    r[0] = r[2];
+    r[1] = r[3];
+    r[2] = y + 3 < 16 ? row(rows[(y + 3) % 16]) : zero3;
+    r[3] = y + 4 < 16 ? row(rows[(y + 4) % 16]) : zero3;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
+  char* smem = trunk_smem;
+  const TrunkArgs& t = a.t;
+  const int oR1 = 0, oR2 = t.r1_bytes;
+  char* R1 = smem + oR1;
+  char* R2 = smem + oR2;
+  constexpr int H = 16, W = 16, S = kActS, H0 = 8, W0 = 8, H1 = 4, W1 = 4, H2 = 2, W2 = 2;
+  constexpr int NW = kThreads / 64;
+  const int TNI = t.tni, E = t.N;
+  const ActLayout L = act_layout(TNI);
+  uint16_t* lcodes = (uint16_t*)(R2 + L.codes);
+  uint32_t* lbits = (uint32_t*)(R2 + L.bits);
+  const char* lut = R2 + L.lut;
+  int* lcnt = (int*)(R2 + L.cnt);
+  int* npairs = (int*)(R2 + L.np);
+  int* lres = (int*)(R2 + L.res);
+  int2* lpairs = (int2*)(R2 + L.pairs);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int ngroups = (E + TNI - 1) / TNI;
+  uint4 wnext[kWFrag];  // layer l+1's weight fragments, fetched during layer l
+#define ACT_PHASE(l, CI, CO, RELU, MODE, IN, H_, W_, OUT)                                  \
+  do {                                                                                   \
+    uint4 wc[kWFrag];                                                                    \
+    _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];                 \
+    if ((l) != 13) wfetch(t.w[(l) + 1], tail_cin((l) + 1), tail_cout((l) + 1), wnext);   \
+    conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, wc, TG<CI>::NCH * 64, t.b[l], \
+                                        OUT);                                            \
+  } while (0)
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * TNI, nimg = min(TNI, E - img0);
+    // stage-0 conv weights (A = w[co = li][tap][8g .. 8g+7]) and bias: issued first, their L2
+    // latency hides behind the code loads and the decode
+    Frag8 bw0[9];
+    {
+      const uint4* wp = (const uint4*)(a.w0 + (size_t)li * 9 * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < 9; ++c) bw0[c].u = wp[c * 4];
+    }
+    float bias0[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias0[i] = a.b0[4 * g + i];
+    // ---- P1: codes / resources -> LDS, byte LUT, counters; reward / done of the last env step
+    for (int i = tid; i < nimg * (S / 8); i += kThreads) {  // 16 B = 8 codes per thread
+      const int im = i / (S / 8), q = i - im * (S / 8);
+      ((uint4*)lcodes)[i] = ((const uint4*)(a.codes + (size_t)(img0 + im) * S))[q];
+    }
+    if (tid < 256) ((uint4*)lut)[tid] = mbk::bits8_bf16((uint32_t)tid);
+    for (int c = tid; c < S; c += kThreads) lcnt[c] = 0;
+    if (tid == 0) *npairs = 0;
+    if (tid < nimg) {
+      lres[tid] = a.res[img0 + tid];
+      if (a.reward_dst) a.reward_dst[img0 + tid] = a.reward_src[img0 + tid];
+      if (a.done_dst) a.done_dst[img0 + tid] = a.done_src[img0 + tid];
+    }
+    __syncthreads();
+    // ---- P2: decode, one wave per env
+    for (int el = wave; el < nimg; el += NW) {
+      const int e = img0 + el;
+      const uint16_t* cs = lcodes + el * S;
+      const int r = lres[el];
+      const int c0 = lane * 4;
+      uint32_t ob[4], mk[12];
+      int nact = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        uint32_t w3[3];
+        mbk::cell_mask(cs, c, H, W, r, w3);
+        ob[j] = mbr::code_bits(cs[c]);
+        mk[3 * j] = w3[0];
+        mk[3 * j + 1] = w3[1];
+        mk[3 * j + 2] = w3[2];
+        if (w3[0] | w3[1] | w3[2]) {
+          ++nact;
+          const int i = atomicAdd(npairs, 1);
+          lpairs[i] = make_int2((c << 19) | atomicAdd(&lcnt[c], 1), e);
+        }
+      }
+      const uint4 o4 = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+      const uint4 m0 = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+      const uint4 m1 = make_uint4(mk[4], mk[5], mk[6], mk[7]);
+      const uint4 m2 = make_uint4(mk[8], mk[9], mk[10], mk[11]);
+      *(uint4*)(lbits + el * S + c0) = o4;
+      const size_t eo = (size_t)e * S + c0;
+      *(uint4*)(a.obs + eo) = o4;
+      uint4* mp = (uint4*)(a.mask + eo * 3);
+      mp[0] = m0;
+      mp[1] = m1;
+      mp[2] = m2;
+      if (a.obs2) {  // the same row is the previous slot's bootstrap row T
+        *(uint4*)(a.obs2 + eo) = o4;
+        uint4* mp2 = (uint4*)(a.mask2 + eo * 3);
+        mp2[0] = m0;
+        mp2[1] = m1;
+        mp2[2] = m2;
+      }
+      // the env's action row and per-cell step scratch start at zero: the head overwrites the
+      // active cells, whose count is its completion counter
+      const uint4 z4 = make_uint4(0, 0, 0, 0);
+      uint4* act4 = (uint4*)(a.action + (size_t)e * S * 7);
+      for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = z4;
+      uint4* cx4 = (uint4*)(a.cellx + (size_t)e * S);
+      for (int i = lane; i < S / 2; i += 64) cx4[i] = z4;
+      int n = nact;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+      if (lane == 0) {
+        a.pending[e] = n;
+        if (n == 0) a.logp[e] = 0.f;
+      }
+      if (n == 0) *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);  // nothing to sample: no-ops
+    }
+    __syncthreads();
+    // ---- P3: one global bucket reservation per active cell of the tile (lcnt -> its base) ...
+    for (int c = tid; c < S; c += kThreads) {
+      const int n = lcnt[c];
+      if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
+    }
+    // ... while the stage-0 conv + pool runs, wave w on images w, w + NW
+    for (int im = wave; im < nimg; im += NW) act_conv0(lbits + im * S, lut, bw0, bias0, R1, im);
+    // layer 1's weights: fetched once the prologue's registers are dead (earlier, they spill)
+    wfetch(t.w[0], tail_cin(0), tail_cout(0), wnext);
+    __syncthreads();
+    {
+      const int np = *npairs;
+      for (int i = tid; i < np; i += kThreads) {
+        const int2 pr = lpairs[i];
+        const int c = pr.x >> 19, slot = pr.x & 0x7FFFF;
+        a.bucket[(size_t)c * E + lcnt[c] + slot] = pr.y;
+      }
+    }
+    zero_halo<TG<16>::PIXB>(R1, nimg, H0, W0);
+    __syncthreads();  // the prologue scratch in R2 is dead from here
+    zero_halo<TG<16>::PIXB>(R2, nimg, H0, W0);
+    __syncthreads();
+    // ---- stage 0 residual blocks, stages 1 and 2, network.5 + critic (trunk_tail_kernel)
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      ACT_PHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, oR1, H0, W0, oR2);
+      __syncthreads();
+      ACT_PHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, oR2, H0, W0, oR1);
+      __syncthreads();
+    }
+    ACT_PHASE(4, 16, 32, false, OUT_STAGE, oR1, H0, W0, oR2);
+    __syncthreads();
+    pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
+    zero_halo<TG<32>::PIXB>(R1, nimg, H1, W1);
+    __syncthreads();
+    zero_halo<TG<32>::PIXB>(R2, nimg, H1, W1);
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      ACT_PHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H1, W1, oR2);
+      __syncthreads();
+      ACT_PHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H1, W1, oR1);
+      __syncthreads();
+    }
+    ACT_PHASE(9, 32, 32, false, OUT_STAGE, oR1, H1, W1, oR2);
+    __syncthreads();
+    pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
+    zero_halo<TG<32>::PIXB>(R1, nimg, H2, W2);
+    __syncthreads();
+    zero_halo<TG<32>::PIXB>(R2, nimg, H2, W2);
+#pragma unroll 1
+    for (int rb = 0; rb < 2; ++rb) {
+      ACT_PHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H2, W2, oR2);
+      __syncthreads();
+      ACT_PHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H2, W2, oR1);
+      __syncthreads();
+    }
+    trunk_fc(R1, H2, W2, nimg, img0, t, (float*)R2);  // ends with a barrier
+  }
+#undef ACT_PHASE
+}
+
 size_t region_bytes(int H0, int W0, int TNI) {
   const int H1 = (H0 + 1) / 2, W1 = (W0 + 1) / 2, H2 = (H1 + 1) / 2, W2 = (W1 + 1) / 2;
   size_t r = (size_t)TNI * (H0 + 2) * (W0 + 2) * TG<16>::PIXB;                 // X0 / U0
@@ -833,5 +1130,99 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
   // LEARNER's persistent grids; this is the acting kernel)
   const int grid = std::min(ngroups, cus * per);
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ fused acting step, launch A
+static int act_tni() {
+  static int tni = 0;
+  if (!tni) {  // MBK_ACT_TNI=8: half-size tiles (77 KB of LDS, so a tile can share a CU)
+    const char* v = std::getenv("MBK_ACT_TNI");
+    tni = (v && std::atoi(v) == 8) ? 8 : kMaxTNI;
+  }
+  return tni;
+}
+
+static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
+  if (!m || !s || m->E <= 0 || m->H != 16 || m->W != 16) return (int)hipErrorInvalidValue;
+  if (!m->w0 || !m->b0 || !m->w5 || !m->b5 || !m->wc || !m->bc || !m->feat || !m->cellx ||
+      !m->pending || !m->bucket_cnt || !m->bucket)
+    return (int)hipErrorInvalidValue;
+  if (!s->codes || !s->res || !s->obs || !s->mask || !s->action || !s->logp || !s->value ||
+      !s->act16)
+    return (int)hipErrorInvalidValue;
+  if ((s->obs2 == nullptr) != (s->mask2 == nullptr) ||
+      (s->reward_dst == nullptr) != (s->reward_src == nullptr) ||
+      (s->done_dst == nullptr) != (s->done_src == nullptr))
+    return (int)hipErrorInvalidValue;
+  // 16-byte vector accesses of whole rows (S = 256 cells per env)
+  if (!al16(s->codes) || !al16(s->obs) || !al16(s->mask) || !al16(s->action) ||
+      !al16(m->cellx) || !al16(m->w0) || !al16(m->feat) || ((uintptr_t)s->act16 & 7) ||
+      (s->obs2 && (!al16(s->obs2) || !al16(s->mask2))))
+    return (int)hipErrorInvalidValue;
+  ActTrunkArgs a{};
+  TrunkArgs& t = a.t;
+  for (int i = 0; i < 14; ++i) {
+    if (!m->w[i] || !m->b[i]) return (int)hipErrorInvalidValue;
+    t.w[i] = (const bf16*)m->w[i];
+    t.b[i] = m->b[i];
+  }
+  t.w5 = (const bf16*)m->w5;
+  t.b5 = m->b5;
+  t.wc = m->wc;
+  t.bc = m->bc;
+  t.f_out = (bf16*)m->feat;
+  t.v_out = s->value;
+  t.N = m->E;
+  t.H0 = 8;
+  t.W0 = 8;
+  const int tni = act_tni();
+  t.tni = tni;
+  const size_t r =
+      (std::max(region_bytes(8, 8, tni), (size_t)act_layout(tni).end) + 15) & ~(size_t)15;
+  t.r1_bytes = t.r2_bytes = (int)r;
+  const size_t sm = 2 * r;
+  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  a.w0 = (const bf16*)m->w0;
+  a.b0 = m->b0;
+  a.codes = s->codes;
+  a.res = s->res;
+  a.obs = s->obs;
+  a.mask = s->mask;
+  a.obs2 = s->obs2;
+  a.mask2 = s->mask2;
+  a.action = s->action;
+  a.cellx = m->cellx;
+  a.logp = s->logp;
+  a.act16 = s->act16;
+  a.pending = m->pending;
+  a.bucket_cnt = m->bucket_cnt;
+  a.bucket = m->bucket;
+  a.reward_src = s->reward_src;
+  a.done_src = s->done_src;
+  a.reward_dst = s->reward_dst;
+  a.done_dst = s->done_dst;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)act_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr = true;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)act_trunk_kernel, kThreads,
+                                                   sm) != hipSuccess || per < 1)
+    per = 1;
+  const int ngroups = (m->E + tni - 1) / tni;
+  const int grid = std::min(ngroups, cus * per);
+  hipLaunchKernelGGL(act_trunk_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

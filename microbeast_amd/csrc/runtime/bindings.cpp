@@ -2,6 +2,7 @@
 // as raw addresses (torch tensor .data_ptr()), so the same calls work on
 // pinned host tensors, shared-memory tensors and numpy arrays; every
 // potentially long call releases the GIL.
+#include <cstring>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -321,6 +322,25 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("host_res", &GpuEngine::host_res)
       .def("host_act16", &GpuEngine::host_act16)
       .def("set_group_graphs", &GpuEngine::set_group_graphs)
+      // fused acting steps: one packed MbkActModel (mbk_api.h, built by ops/act.py) per lane
+      .def("set_act_models",
+           [](GpuEngine& e, std::vector<py::bytes> blocks, bool copy) {
+             std::vector<MbkActModel> ms;
+             for (const py::bytes& b : blocks) {
+               const std::string raw = b;
+               if (raw.size() != sizeof(MbkActModel))
+                 throw std::runtime_error("set_act_models: block size " +
+                                          std::to_string(raw.size()) + " != sizeof(MbkActModel) " +
+                                          std::to_string(sizeof(MbkActModel)));
+               MbkActModel m;
+               std::memcpy(&m, raw.data(), sizeof(m));
+               ms.push_back(m);
+             }
+             e.set_act_models(ms, copy);
+           },
+           py::arg("blocks"), py::arg("copy") = false)
+      .def("act_mode", &GpuEngine::act_mode)
+      .def_static("act_model_size", [] { return (int)sizeof(MbkActModel); })
       .def("inject_fault", &GpuEngine::inject_fault)
       .def("error", &GpuEngine::error)
       .def("stats", [](GpuEngine& e) {

@@ -241,6 +241,20 @@ void GpuEngine::set_group_graphs(const std::vector<uintptr_t>& graphs) {
   for (uintptr_t h : graphs) group_graph_.push_back((hipGraphExec_t)h);
 }
 
+void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy) {
+  if (running_.load()) throw std::runtime_error("set_act_models: engine running");
+  if (!models.empty() && (int)models.size() != cfg_.n_lanes)
+    throw std::runtime_error("set_act_models: need one model per lane");
+  if (!models.empty() && (cfg_.selfplay_groups > 0 || buf_.ep_return || buf_.ep_step ||
+                          buf_.last_action0 || buf_.logits))
+    throw std::runtime_error("set_act_models: not with self-play or reference buffer keys");
+  for (const MbkActModel& m : models)
+    if (m.E != cfg_.envs_per_group || m.H != cfg_.size || m.W != cfg_.size)
+      throw std::runtime_error("set_act_models: model block shape mismatch");
+  act_models_ = models;
+  act_copy_ = copy;
+}
+
 void GpuEngine::stop() {
   running_.store(false);
   work_cv_.notify_all();
@@ -446,54 +460,6 @@ bool GpuEngine::enqueue_gpu(int g) {
   }
   const size_t e0 = (size_t)g * E;
   G.timed = step_timing_;
-  // zero-copy step: the group's own graph reads its codes from / writes its actions to the
-  // pinned host staging (PCIe inside the decode / pack kernels: no SDMA commands, and no
-  // copy<->compute engine hand-offs on the lane)
-  hipGraphExec_t zc = group_graph_.empty() ? nullptr : group_graph_[g];
-  // copy overlap: this step's PCIe buffers (parity p) and the streams its copies run on
-  const int par = L.par;
-  const uintptr_t in_codes = (L.overlap && par) ? io.in_codes_b : io.in_codes;
-  const uintptr_t in_res = (L.overlap && par) ? io.in_res_b : io.in_res;
-  const uintptr_t out_act16 = (L.overlap && par) ? io.out_act16_b : io.out_act16;
-  hipStream_t s_in = L.overlap ? L.s_in : st;
-  if (L.overlap) {
-    // parity p's inputs were consumed by the step two back (its graph + scatter are done)
-    ENG_CHECK(hipStreamWaitEvent(s_in, L.ev_done[par], 0));
-  }
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], s_in));
-  if (!zc) {
-    ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
-                             hipMemcpyHostToDevice, s_in));
-    ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
-  }
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], s_in));
-  if (L.overlap) {
-    ENG_CHECK(hipEventRecord(L.ev_h2d[par], s_in));
-    ENG_CHECK(hipStreamWaitEvent(st, L.ev_h2d[par], 0));
-    ENG_CHECK(hipStreamWaitEvent(st, L.ev_d2h[par], 0));  // act16[p] copied out two steps back
-  }
-  // learner launches hold from here (the H2D above is SDMA: no CUs) to the scatter's end
-  if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
-  {
-    const auto t0 = std::chrono::steady_clock::now();
-    ENG_CHECK(hipGraphLaunch(zc ? zc : (L.overlap && par) ? L.graph_b : L.graph, st));
-    launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
-                             std::chrono::steady_clock::now() - t0).count(),
-                         std::memory_order_relaxed);
-  }
-  if (G.selfplay) {  // the opponent acts on its own (mirrored) view with its own weights
-    ENG_CHECK(hipMemcpyAsync((void*)io.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
-                             hipMemcpyHostToDevice, st));
-    ENG_CHECK(hipMemcpyAsync((void*)io.in_res_p1, h_res_p1_ + e0, E * 4, hipMemcpyHostToDevice,
-                             st));
-    ENG_CHECK(hipGraphLaunch(L.opp_graph, st));
-    G.opp_version = L.opp_version;
-  }
-
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[2], st));
-  // scatter this step into the HBM rollout slot(s)
-  MbkCopySeg seg[MBK_MAX_COPY_SEGS];
-  int n = 0;
   const size_t t = G.t;
   auto obs_at = [&](int slot, size_t i) {
     return (char*)buf_.obs + slot * slot_stride_obs_ + i * E * S_ * 4;
@@ -510,65 +476,173 @@ bool GpuEngine::enqueue_gpu(int g) {
   auto u8_at = [&](uintptr_t base, int slot, size_t i) {
     return (char*)base + (slot * slot_stride_scalar_ + i * E);
   };
-  seg[n++] = {(const void*)io.in_obs, obs_at(G.cur, t), E * S_ * 4};
-  seg[n++] = {(const void*)io.in_mask, mask_at(G.cur, t), E * S_ * 4 * kMaskWords};
-  seg[n++] = {(const void*)io.out_action, act_at(G.cur, t), E * S_ * kActComps};
-  seg[n++] = {(const void*)io.out_logp, f32_at(buf_.logp, G.cur, t), E * 4};
-  seg[n++] = {(const void*)io.out_value, f32_at(buf_.value, G.cur, t), E * 4};
-  if (!G.first) {
-    // reward / done of the env step that just finished, read by the scatter kernel straight
-    // from pinned host memory (two fewer blit launches per step); the group's envs do not
-    // write them again before G.ev, which is recorded after this kernel
-    const int rs = t > 0 ? G.cur : G.prev;
-    const size_t ri = t > 0 ? t - 1 : T - 1;
-    seg[n++] = {(const void*)(h_reward_ + e0), f32_at(buf_.reward, rs, ri), E * 4};
-    seg[n++] = {(const void*)(h_done_ + e0), u8_at(buf_.done, rs, ri), E};
-    if (buf_.ep_return)
-      seg[n++] = {(const void*)(h_ep_return_ + e0), f32_at(buf_.ep_return, rs, ri), E * 4};
-    if (buf_.ep_step)
-      seg[n++] = {(const void*)(h_ep_step_ + e0), f32_at(buf_.ep_step, rs, ri), E * 4};
-  }
-  if (buf_.logits && io.out_logits)
-    seg[n++] = {(const void*)io.out_logits,
-                (char*)buf_.logits + (G.cur * slot_stride_scalar_ + t * E) * (size_t)S_ * 78 * 4,
-                E * (size_t)S_ * 78 * 4};
   const bool close_prev = (t == 0 && G.prev >= 0);
-  if (close_prev && buf_.last_action0)  // the action taken just before this slot's row 0
-    seg[n++] = {(const void*)act_at(G.prev, T - 1),
-                (char*)buf_.last_action0 + (size_t)G.cur * E * S_ * kActComps,
-                E * S_ * kActComps};
-  if (close_prev) {
-    seg[n++] = {(const void*)io.in_obs, obs_at(G.prev, T), E * S_ * 4};
-    seg[n++] = {(const void*)io.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
-  }
-  ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, st));
-  if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));  // (the D2H is SDMA)
-  hipStream_t s_out = st;
-  if (L.overlap) {  // D2H on the copy-out stream once this step's graph + scatter are done
-    ENG_CHECK(hipEventRecord(L.ev_done[par], st));
-    s_out = L.s_out;
-    ENG_CHECK(hipStreamWaitEvent(s_out, L.ev_done[par], 0));
-    L.par ^= 1;
-  }
-  if (close_prev) {
-    ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
-    {
-      std::lock_guard<std::mutex> l(slot_m_);
-      full_slots_.push_back(G.prev);
+  // the step that just finished (its reward / done rows): the last row of this slot, or of the
+  // previous slot at t == 0
+  const int rs = t > 0 ? G.cur : G.prev;
+  const size_t ri = t > 0 ? t - 1 : T - 1;
+  if (act_mode()) {
+    // fused acting step: 2 launches decode the codes, run the trunk, sample, and write the
+    // rollout row (obs, mask, action, log-prob, value, previous reward / done) in place
+    const MbkActModel& M = act_models_[G.lane];
+    const bool zc = !act_copy_;
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], st));
+    if (!zc) {
+      ENG_CHECK(hipMemcpyAsync((void*)io.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
+                               hipMemcpyHostToDevice, st));
+      ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, st));
     }
-    slots_full_.fetch_add(1);
-    full_cv_.notify_all();
-    G.prev = -1;
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
+    MbkActStep a{};
+    a.codes = zc ? h_codes_ + e0 * S_ : (const uint16_t*)io.in_codes;
+    a.res = zc ? h_res_ + e0 : (const int32_t*)io.in_res;
+    a.obs = (uint32_t*)obs_at(G.cur, t);
+    a.mask = (uint32_t*)mask_at(G.cur, t);
+    if (close_prev) {  // this row is also the previous slot's bootstrap row T
+      a.obs2 = (uint32_t*)obs_at(G.prev, T);
+      a.mask2 = (uint32_t*)mask_at(G.prev, T);
+    }
+    a.action = (uint8_t*)act_at(G.cur, t);
+    a.logp = (float*)f32_at(buf_.logp, G.cur, t);
+    a.value = (float*)f32_at(buf_.value, G.cur, t);
+    a.act16 = zc ? h_act16_ + e0 * S_ : (uint16_t*)io.out_act16;
+    if (!G.first) {
+      a.reward_src = h_reward_ + e0;
+      a.done_src = h_done_ + e0;
+      a.reward_dst = (float*)f32_at(buf_.reward, rs, ri);
+      a.done_dst = (uint8_t*)u8_at(buf_.done, rs, ri);
+    }
+    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
+    {
+      const auto t0 = std::chrono::steady_clock::now();
+      ENG_CHECK((hipError_t)mbk_act_step(&M, &a, st));
+      launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - t0).count(),
+                           std::memory_order_relaxed);
+    }
+    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[2], st));
+    if (close_prev) {
+      ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
+      {
+        std::lock_guard<std::mutex> l(slot_m_);
+        full_slots_.push_back(G.prev);
+      }
+      slots_full_.fetch_add(1);
+      full_cv_.notify_all();
+      G.prev = -1;
+    }
+    if (!zc)
+      ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)io.out_act16, E * S_ * 2,
+                               hipMemcpyDeviceToHost, st));
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], st));
+    ENG_CHECK(hipEventRecord(G.ev, st));
+  } else {
+    // zero-copy step: the group's own graph reads its codes from / writes its actions to the
+    // pinned host staging (PCIe inside the decode / pack kernels: no SDMA commands, and no
+    // copy<->compute engine hand-offs on the lane)
+    hipGraphExec_t zc = group_graph_.empty() ? nullptr : group_graph_[g];
+    // copy overlap: this step's PCIe buffers (parity p) and the streams its copies run on
+    const int par = L.par;
+    const uintptr_t in_codes = (L.overlap && par) ? io.in_codes_b : io.in_codes;
+    const uintptr_t in_res = (L.overlap && par) ? io.in_res_b : io.in_res;
+    const uintptr_t out_act16 = (L.overlap && par) ? io.out_act16_b : io.out_act16;
+    hipStream_t s_in = L.overlap ? L.s_in : st;
+    if (L.overlap) {
+      // parity p's inputs were consumed by the step two back (its graph + scatter are done)
+      ENG_CHECK(hipStreamWaitEvent(s_in, L.ev_done[par], 0));
+    }
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], s_in));
+    if (!zc) {
+      ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
+                               hipMemcpyHostToDevice, s_in));
+      ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
+    }
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], s_in));
+    if (L.overlap) {
+      ENG_CHECK(hipEventRecord(L.ev_h2d[par], s_in));
+      ENG_CHECK(hipStreamWaitEvent(st, L.ev_h2d[par], 0));
+      ENG_CHECK(hipStreamWaitEvent(st, L.ev_d2h[par], 0));  // act16[p] copied out two steps back
+    }
+    // learner launches hold from here (the H2D above is SDMA: no CUs) to the scatter's end
+    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
+    {
+      const auto t0 = std::chrono::steady_clock::now();
+      ENG_CHECK(hipGraphLaunch(zc ? zc : (L.overlap && par) ? L.graph_b : L.graph, st));
+      launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::steady_clock::now() - t0).count(),
+                           std::memory_order_relaxed);
+    }
+    if (G.selfplay) {  // the opponent acts on its own (mirrored) view with its own weights
+      ENG_CHECK(hipMemcpyAsync((void*)io.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
+                               hipMemcpyHostToDevice, st));
+      ENG_CHECK(hipMemcpyAsync((void*)io.in_res_p1, h_res_p1_ + e0, E * 4, hipMemcpyHostToDevice,
+                               st));
+      ENG_CHECK(hipGraphLaunch(L.opp_graph, st));
+      G.opp_version = L.opp_version;
+    }
+
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[2], st));
+    // scatter this step into the HBM rollout slot(s)
+    MbkCopySeg seg[MBK_MAX_COPY_SEGS];
+    int n = 0;
+    seg[n++] = {(const void*)io.in_obs, obs_at(G.cur, t), E * S_ * 4};
+    seg[n++] = {(const void*)io.in_mask, mask_at(G.cur, t), E * S_ * 4 * kMaskWords};
+    seg[n++] = {(const void*)io.out_action, act_at(G.cur, t), E * S_ * kActComps};
+    seg[n++] = {(const void*)io.out_logp, f32_at(buf_.logp, G.cur, t), E * 4};
+    seg[n++] = {(const void*)io.out_value, f32_at(buf_.value, G.cur, t), E * 4};
+    if (!G.first) {
+      // reward / done of the env step that just finished, read by the scatter kernel straight
+      // from pinned host memory (two fewer blit launches per step); the group's envs do not
+      // write them again before G.ev, which is recorded after this kernel
+      seg[n++] = {(const void*)(h_reward_ + e0), f32_at(buf_.reward, rs, ri), E * 4};
+      seg[n++] = {(const void*)(h_done_ + e0), u8_at(buf_.done, rs, ri), E};
+      if (buf_.ep_return)
+        seg[n++] = {(const void*)(h_ep_return_ + e0), f32_at(buf_.ep_return, rs, ri), E * 4};
+      if (buf_.ep_step)
+        seg[n++] = {(const void*)(h_ep_step_ + e0), f32_at(buf_.ep_step, rs, ri), E * 4};
+    }
+    if (buf_.logits && io.out_logits)
+      seg[n++] = {(const void*)io.out_logits,
+                  (char*)buf_.logits + (G.cur * slot_stride_scalar_ + t * E) * (size_t)S_ * 78 * 4,
+                  E * (size_t)S_ * 78 * 4};
+    if (close_prev && buf_.last_action0)  // the action taken just before this slot's row 0
+      seg[n++] = {(const void*)act_at(G.prev, T - 1),
+                  (char*)buf_.last_action0 + (size_t)G.cur * E * S_ * kActComps,
+                  E * S_ * kActComps};
+    if (close_prev) {
+      seg[n++] = {(const void*)io.in_obs, obs_at(G.prev, T), E * S_ * 4};
+      seg[n++] = {(const void*)io.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
+    }
+    ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, st));
+    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));  // (the D2H is SDMA)
+    hipStream_t s_out = st;
+    if (L.overlap) {  // D2H on the copy-out stream once this step's graph + scatter are done
+      ENG_CHECK(hipEventRecord(L.ev_done[par], st));
+      s_out = L.s_out;
+      ENG_CHECK(hipStreamWaitEvent(s_out, L.ev_done[par], 0));
+      L.par ^= 1;
+    }
+    if (close_prev) {
+      ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
+      {
+        std::lock_guard<std::mutex> l(slot_m_);
+        full_slots_.push_back(G.prev);
+      }
+      slots_full_.fetch_add(1);
+      full_cv_.notify_all();
+      G.prev = -1;
+    }
+    if (!zc)
+      ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
+                               hipMemcpyDeviceToHost, s_out));
+    if (G.selfplay)
+      ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
+                               hipMemcpyDeviceToHost, st));
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], s_out));
+    if (L.overlap) ENG_CHECK(hipEventRecord(L.ev_d2h[par], s_out));
+    ENG_CHECK(hipEventRecord(G.ev, s_out));
   }
-  if (!zc)
-    ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
-                             hipMemcpyDeviceToHost, s_out));
-  if (G.selfplay)
-    ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
-                             hipMemcpyDeviceToHost, st));
-  if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], s_out));
-  if (L.overlap) ENG_CHECK(hipEventRecord(L.ev_d2h[par], s_out));
-  ENG_CHECK(hipEventRecord(G.ev, s_out));
   gpu_steps_.fetch_add(1);
   G.t += 1;
   if (G.t == (int)T) {

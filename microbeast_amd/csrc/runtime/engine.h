@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "vec_env.h"
+#include "../include/mbk_api.h"
 
 namespace mb {
 
@@ -181,6 +182,12 @@ class GpuEngine {
   // resources straight from pinned host memory and writes its packed actions there (no
   // H2D / D2H copy commands on the lane); set before start(), 0 entries = copy path
   void set_group_graphs(const std::vector<uintptr_t>& graphs);
+  // fused acting steps (mbk_act_step: two kernel launches per step, writing the rollout row
+  // directly -- no policy graph, no scatter copy): one model / workspace block per lane, set
+  // before start(). copy: H2D / D2H the codes and actions through the lane's device buffers
+  // instead of reading / writing the pinned host staging from the kernels.
+  void set_act_models(const std::vector<MbkActModel>& models, bool copy);
+  bool act_mode() const { return !act_models_.empty(); }
   const EngineConfig& config() const { return cfg_; }
   VecEnv& env() { return *env_; }
   bool failed() const { return failed_.load(); }
@@ -298,6 +305,8 @@ class GpuEngine {
   int chunk_;
   uint32_t* gate_ = nullptr;  // policy gate flag (device), see EngineConfig
   std::vector<hipGraphExec_t> group_graph_;  // zero-copy graphs per group (may be empty)
+  std::vector<MbkActModel> act_models_;      // fused acting steps per lane (may be empty)
+  bool act_copy_ = false;
 };
 
 }  // namespace mb

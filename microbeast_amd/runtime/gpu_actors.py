@@ -26,6 +26,7 @@ import os
 import torch
 
 from .. import _native as N
+from ..ops import act as act_ops
 from ..ops import cell_head
 from ..ops.copy import zeros
 from ..ops.optim import FlatParams
@@ -66,6 +67,66 @@ class _HostView:
 
     def data_ptr(self) -> int:
         return self._ptr
+
+
+def graph_policy_step(io: dict, m, rng: torch.Tensor, E: int, size: int, device) -> None:
+    """The captured graph's policy step (6 launches for the flat agent: decode + bucket, stage-0
+    conv, trunk, network.5 + critic, head, finale) on fixed-address I/O ``io`` (``make_io``).
+    The fused two-launch step (ops/act.py) is pinned bit-identical to it."""
+    k = N.kernels()
+    st = N.stream_ptr()
+    # sparse-head models (flat IMPALA head) bucket their active pairs in the decode pass;
+    # dense-head models (GridNet) sample with the masked-cell kernel
+    hip = hasattr(m, "_head") and m._use_hip(io["in_obs"])
+    packed = False
+    if hip:
+        # decode + bucket the sparse head's active pairs by cell in the same pass
+        head = m._head(device)
+        head.ensure_buckets(E)
+        N.check(k.mbk_decode_obs_mask_bucket(
+            io["in_codes"].data_ptr(), io["in_res"].data_ptr(), E, size, size,
+            io["in_obs"].data_ptr(), io["in_mask"].data_ptr(), head.bucket_cnt.data_ptr(),
+            head.bucket.data_ptr(), head.cell_lp.data_ptr(), io["out_action"].data_ptr(),
+            st), "decode_obs_mask_bucket")
+        # the head's last launch also packs the env action codes (row_sum_pack)
+        _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
+                            logp_out=io["out_logp"], bucketed=True,
+                            logits_out=io.get("out_logits"), value_out=io["out_value"],
+                            act16_out=io["out_act16"])
+        packed = True
+    else:
+        N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
+                                      E, size, size, io["in_obs"].data_ptr(),
+                                      io["in_mask"].data_ptr(), st), "decode_obs_mask")
+        logits, value = m.policy_value(io["in_obs"])
+        if "out_logits" in io:
+            io["out_logits"].copy_(logits.reshape(io["out_logits"].shape))
+        cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
+                             cell_logp=io["cell_logp"], logp_out=io["out_logp"])
+    if value.data_ptr() != io["out_value"].data_ptr():  # (written in place when fused)
+        io["out_value"].copy_(value.view(-1))
+    if not packed:
+        N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), E * size * size,
+                                       io["out_act16"].data_ptr(), N.stream_ptr()),
+                "pack_env_actions")
+
+
+def make_io(E: int, S: int, device, logits: bool = False) -> dict:
+    """Fixed-address I/O of one policy lane's captured graph."""
+    return {
+        # what crosses PCIe: 16-bit cell codes + resources in, packed actions out
+        "in_codes": zeros(E, S, dtype=torch.int16, device=device),
+        "in_res": zeros(E, dtype=torch.int32, device=device),
+        "out_act16": zeros(E, S, dtype=torch.int16, device=device),
+        # decoded on the GPU inside the policy graph
+        "in_obs": zeros(E, S, dtype=torch.int32, device=device),
+        "in_mask": zeros(E, S, 3, dtype=torch.int32, device=device),
+        "out_action": zeros(E, S, 7, dtype=torch.uint8, device=device),
+        "out_logp": zeros(E, dtype=torch.float32, device=device),
+        "out_value": zeros(E, dtype=torch.float32, device=device),
+        # dense-head (GridNet) sampling workspace, per lane
+        "cell_logp": zeros(E * S, dtype=torch.float32, device=device),
+    } | ({"out_logits": zeros(E, S * 78, dtype=torch.float32, device=device)} if logits else {})
 
 
 class GpuActorRuntime:
@@ -189,11 +250,26 @@ class GpuActorRuntime:
             bufs["lanes"].append(d)
         torch.cuda.synchronize()
         self.engine = rt.GpuEngine(cfg, bufs)
+        # fused acting steps (ops/act.py): 2 launches per policy step that write the rollout
+        # row in place, instead of the captured 6-launch graph + scatter copy. Headline agent
+        # shape only (16x16, bf16 trunk); MBK_FUSED_ACT=0 keeps the graph path, MBK_ACT_COPY=1
+        # moves codes / actions through device buffers with H2D / D2H copies
+        self.fused_act = (os.environ.get("MBK_FUSED_ACT", "1") == "1"
+                          and self.selfplay_groups == 0 and not self.reference_keys
+                          and not self.copy_overlap
+                          and all(act_ops.supported(ln["model"], size, fp8_policy)
+                                  for ln in self.lanes))
+        if self.fused_act:
+            for lane in self.lanes:
+                lane["act"] = act_ops.ActWorkspace(lane["model"], E, lane["rng"], dev)
+            torch.cuda.synchronize()
+            self.engine.set_act_models([ln["act"].block() for ln in self.lanes],
+                                       os.environ.get("MBK_ACT_COPY", "0") == "1")
         # zero-copy policy steps (engine.h set_group_graphs): one graph per group whose decode
         # reads the group's codes / resources from the engine's pinned host staging and whose
         # pack writes its actions there (MBK_ZERO_COPY=1; self-play keeps the copy path)
         self.zero_copy = (os.environ.get("MBK_ZERO_COPY", "0") == "1"
-                          and self.selfplay_groups == 0)
+                          and self.selfplay_groups == 0 and not self.fused_act)
         if self.zero_copy:
             hc, hr, ha = (self.engine.host_codes(), self.engine.host_res(),
                           self.engine.host_act16())
@@ -214,60 +290,10 @@ class GpuActorRuntime:
 
     # ------------------------------------------------------------ inference graph
     def _make_io(self):
-        E, S, dev = self.E, self.S, self.device
-        return {
-            # what crosses PCIe: 16-bit cell codes + resources in, packed actions out
-            "in_codes": zeros(E, S, dtype=torch.int16, device=dev),
-            "in_res": zeros(E, dtype=torch.int32, device=dev),
-            "out_act16": zeros(E, S, dtype=torch.int16, device=dev),
-            # decoded on the GPU inside the policy graph
-            "in_obs": zeros(E, S, dtype=torch.int32, device=dev),
-            "in_mask": zeros(E, S, 3, dtype=torch.int32, device=dev),
-            "out_action": zeros(E, S, 7, dtype=torch.uint8, device=dev),
-            "out_logp": zeros(E, dtype=torch.float32, device=dev),
-            "out_value": zeros(E, dtype=torch.float32, device=dev),
-            # dense-head (GridNet) sampling workspace, per lane
-            "cell_logp": zeros(E * S, dtype=torch.float32, device=dev),
-        } | ({"out_logits": zeros(E, S * 78, dtype=torch.float32, device=dev)}
-             if getattr(self, "emit_logits", False) else {})
+        return make_io(self.E, self.S, self.device, getattr(self, "emit_logits", False))
 
     def _policy_step(self, io, m, rng):
-        k = N.kernels()
-        st = N.stream_ptr()
-        # sparse-head models (flat IMPALA head) bucket their active pairs in the decode pass;
-        # dense-head models (GridNet) sample with the masked-cell kernel
-        hip = hasattr(m, "_head") and m._use_hip(io["in_obs"])
-        packed = False
-        if hip:
-            # decode + bucket the sparse head's active pairs by cell in the same pass
-            head = m._head(self.device)
-            head.ensure_buckets(self.E)
-            N.check(k.mbk_decode_obs_mask_bucket(
-                io["in_codes"].data_ptr(), io["in_res"].data_ptr(), self.E, self.size, self.size,
-                io["in_obs"].data_ptr(), io["in_mask"].data_ptr(), head.bucket_cnt.data_ptr(),
-                head.bucket.data_ptr(), head.cell_lp.data_ptr(), io["out_action"].data_ptr(),
-                st), "decode_obs_mask_bucket")
-            # the head's last launch also packs the env action codes (row_sum_pack)
-            _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
-                                logp_out=io["out_logp"], bucketed=True,
-                                logits_out=io.get("out_logits"), value_out=io["out_value"],
-                                act16_out=io["out_act16"])
-            packed = True
-        else:
-            N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
-                                          self.E, self.size, self.size, io["in_obs"].data_ptr(),
-                                          io["in_mask"].data_ptr(), st), "decode_obs_mask")
-            logits, value = m.policy_value(io["in_obs"])
-            if "out_logits" in io:
-                io["out_logits"].copy_(logits.reshape(io["out_logits"].shape))
-            cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
-                                 cell_logp=io["cell_logp"], logp_out=io["out_logp"])
-        if value.data_ptr() != io["out_value"].data_ptr():  # (written in place when fused)
-            io["out_value"].copy_(value.view(-1))
-        if not packed:
-            N.check(k.mbk_pack_env_actions(io["out_action"].data_ptr(), self.E * self.S,
-                                           io["out_act16"].data_ptr(), N.stream_ptr()),
-                    "pack_env_actions")
+        graph_policy_step(io, m, rng, self.E, self.size, self.device)
 
     def _capture_pack(self, model):
         """Graph of ``model.pack_inference`` (derived weight buffers), replayed by the engine

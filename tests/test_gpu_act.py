@@ -1,0 +1,147 @@
+"""Fused two-launch acting step (ops/act.py, mbk_act_step) == the captured 6-launch graph step.
+
+Same codes, same weights, same Philox state: obs planes, masks, sampled actions, behaviour
+log-probs, values and the packed env actions must match bit for bit, and the sampler's step
+counter must advance identically (reference act path: model.py:165-216)."""
+import pytest
+import torch
+
+from microbeast_amd import _native as N
+
+pytestmark = pytest.mark.gpu
+
+
+def _codes_stream(E, steps, seed):
+    """Codes of E real 16x16 simulator envs over `steps` steps of random legal play."""
+    from microbeast_amd.ops.cell_head import OFFS, unpack_mask
+    rt = N.runtime()
+    S = 256
+    env = rt.VecEnv(16, E, 300, seed, [0, 1, 2, 3, 5])
+    obs = torch.zeros(E, S, dtype=torch.int32)
+    mask = torch.zeros(E, S, 3, dtype=torch.int32)
+    env.reset(obs.data_ptr(), mask.data_ptr())
+    codes = torch.zeros(E, S, dtype=torch.int16)
+    res = torch.zeros(E, dtype=torch.int32)
+    rew, done = torch.zeros(E), torch.zeros(E, dtype=torch.uint8)
+    gen = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(steps):
+        env.obs_codes(codes.data_ptr(), res.data_ptr())
+        out.append((codes.clone(), res.clone()))
+        mb = unpack_mask(mask)
+        a = torch.zeros(E, S, 7, dtype=torch.uint8)
+        for k in range(7):
+            seg = mb[..., OFFS[k]:OFFS[k + 1]].float() + 1e-6
+            a[..., k] = torch.multinomial(seg.view(-1, seg.shape[-1]), 1,
+                                          generator=gen).view(E, S)
+        env.step(a.data_ptr(), obs.data_ptr(), mask.data_ptr(), rew.data_ptr(), done.data_ptr())
+    return out
+
+
+def _model(cuda, seed):
+    from microbeast_amd.models.agent import Agent
+    torch.manual_seed(seed)
+    m = Agent((16, 16, 27))
+    torch.nn.init.normal_(m.actor.weight, std=0.05)  # a non-uniform policy
+    torch.nn.init.normal_(m.actor.bias, std=0.5)
+    m = m.to(cuda).eval()
+    m.pack_inference(cuda)
+    return m
+
+
+@pytest.mark.parametrize("E", [96, 520])
+def test_fused_act_step_bit_identical(cuda, E):
+    from microbeast_amd.ops.act import ActWorkspace
+    from microbeast_amd.runtime.gpu_actors import graph_policy_step, make_io
+
+    S = 256
+    m = _model(cuda, 3)
+    rng_a = torch.tensor([12345, 7], dtype=torch.int64, device=cuda)
+    rng_b = rng_a.clone()
+    io = make_io(E, S, cuda)
+    ws = ActWorkspace(m, E, rng_b, cuda)
+    obs = torch.empty(E, S, dtype=torch.int32, device=cuda)
+    mask = torch.empty(E, S, 3, dtype=torch.int32, device=cuda)
+    obs2, mask2 = torch.empty_like(obs), torch.empty_like(mask)
+    action = torch.full((E, S, 7), 0xAB, dtype=torch.uint8, device=cuda)
+    logp = torch.full((E,), float("nan"), device=cuda)
+    value = torch.full((E,), float("nan"), device=cuda)
+    act16 = torch.full((E, S), -1, dtype=torch.int16, device=cuda)
+    reward = torch.randn(E, device=cuda)
+    done = (torch.rand(E, device=cuda) < 0.3).to(torch.uint8)
+    rdst, ddst = torch.zeros_like(reward), torch.zeros_like(done)
+    n_active = 0
+    for i, (codes, res) in enumerate(_codes_stream(E, 24, seed=E)):
+        io["in_codes"].copy_(codes)
+        io["in_res"].copy_(res)
+        graph_policy_step(io, m, rng_a, E, 16, cuda)
+        second = i % 3 == 0
+        ws.step(io["in_codes"], io["in_res"], obs, mask, action, logp, value, act16,
+                obs2=obs2 if second else None, mask2=mask2 if second else None,
+                reward=reward, done=done, reward_dst=rdst, done_dst=ddst)
+        torch.cuda.synchronize()
+        assert torch.equal(obs, io["in_obs"]), f"obs planes differ at step {i}"
+        assert torch.equal(mask, io["in_mask"]), f"masks differ at step {i}"
+        if second:
+            assert torch.equal(obs2, obs) and torch.equal(mask2, mask)
+        assert torch.equal(action, io["out_action"]), f"actions differ at step {i}"
+        assert torch.equal(act16, io["out_act16"]), f"packed actions differ at step {i}"
+        assert torch.equal(logp.view(torch.int32), io["out_logp"].view(torch.int32)), \
+            f"log-probs differ at step {i}: {(logp - io['out_logp']).abs().max().item()}"
+        assert torch.equal(value.view(torch.int32), io["out_value"].view(torch.int32)), \
+            f"values differ at step {i}"
+        assert torch.equal(rng_a, rng_b), f"sampler state differs after step {i}"
+        assert torch.equal(rdst, reward) and torch.equal(ddst, done)
+        # between steps the bucket counters and the arrival ticket are back at zero
+        assert int(ws.head.bucket_cnt.abs().sum()) == 0 and int(ws.done_ctr.abs().sum()) == 0
+        assert int(ws.pending.abs().sum()) == 0
+        n_active += int((mask != 0).any(-1).sum())
+    assert n_active > 50 * 24  # the head actually sampled
+    assert int(rng_b[1]) == 7 + 24
+
+
+def test_engine_fused_act_learns(cuda, monkeypatch):
+    """The engine's fused step form on a 16x16 map: rollout rows written in place are aligned
+    (legal actions under the mask of the same row), learn / publish work, two lanes."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.cell_head import OFFS, unpack_mask
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+
+    s, T, E = 16, 8, 64
+    monkeypatch.setenv("MBK_FUSED_ACT", "1")
+
+    def mk():
+        return Agent((s, s, 27))
+
+    torch.manual_seed(0)
+    learner = Learner(mk(), LearnerHParams(), cuda)
+    rt = GpuActorRuntime(mk, s, n_groups=3, envs_per_group=E, unroll=T, batch_slots=1,
+                         device=cuda, n_threads=2, n_lanes=2)
+    assert rt.fused_act and rt.engine.act_mode()
+    rt.start(learner.flat)
+    try:
+        for it in range(5):
+            batch, slots = rt.get_batch()
+            torch.cuda.synchronize()
+            obs, mask, act = batch["obs"], batch["mask"], batch["action"]
+            bits = obs.cpu().view(-1).numpy().view("uint32")
+            assert set(int(bin(int(x)).count("1")) for x in bits[:5000]) == {5}
+            mb = unpack_mask(mask[:T].cpu())
+            a = act[:T].cpu().long()
+            for k in range(7):
+                seg = mb[..., OFFS[k]:OFFS[k + 1]]
+                has = seg.any(-1)
+                ok = seg.gather(-1, a[..., k:k + 1]).squeeze(-1) | ~has
+                assert bool(ok.all()), f"illegal action component {k}"
+            # inactive cells carry action 0; active ones at least one legal choice
+            assert int(a[~mb.any(-1)].abs().sum()) == 0
+            assert torch.isfinite(batch["logp"][:T]).all() and (batch["logp"][:T] <= 0).all()
+            losses = learner.learn(batch)
+            rt.release(slots)
+            rt.publish(learner.flat, version=it + 1)
+            assert torch.isfinite(losses).all()
+        st = rt.stats()
+        assert st["frames"] > 0 and st["gpu_steps"] > 0 and st["publishes"] >= 1
+    finally:
+        rt.stop()
