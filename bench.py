@@ -8,7 +8,8 @@ and a data-parallel learner (RCCL all-reduce). A timed step = one learner
 update (forward, V-trace, backward, bucketed all-reduce, Adam, weight
 publish) consuming ``batch_slots * envs_per_group * unroll`` fresh env frames
 per rank that the actors produced concurrently; value = frames consumed by all
-learners / wall time (weak scaling: per-GPU work fixed).
+learners / wall time. Weak scaling (default): per-GPU work fixed, the global batch grows
+with N. ``--scaling strong``: the 1-GPU problem (envs and frames per update) split over N.
 
 Synthetic environment (native microRTS stand-in; gym-microrts/Java is not
 available offline) and random-init weights of the reference architecture
@@ -73,6 +74,11 @@ def parse(argv=None):
                    help="rehearsal only: allow more ranks than GPUs (ranks share a GPU over gloo)")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", help="fp32 | bf16 payload")
     p.add_argument("--bucket_mb", type=float, default=8.0)
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                   help="weak: every rank runs --groups x --envs_per_group envs and consumes "
+                        "one slot per update (global batch grows with N); strong: the global "
+                        "problem of 1 GPU (the same groups x envs_per_group envs, one update "
+                        "of envs_per_group x unroll frames) is split over the N ranks")
     p.add_argument("--policy_gate", type=int, default=-1,
                    help="1: learner launches wait while a policy step's kernels run (engine "
                         "policy gate); 0: off; -1: MBK_POLICY_GATE (default off)")
@@ -100,6 +106,14 @@ def main(argv=None):
         print("bench.py needs a GPU", file=sys.stderr)
         return 2
     info = D.init_distributed(use_cuda=True)
+    if args.scaling == "strong" and info.world_size > 1:
+        # fixed global problem: each rank steps 1/N of the envs and its update consumes 1/N of
+        # the global batch (the all-reduced gradient is the full batch's)
+        if args.envs_per_group % info.world_size:
+            print(f"--scaling strong: --envs_per_group {args.envs_per_group} is not divisible "
+                  f"by {info.world_size} ranks", file=sys.stderr)
+            return 2
+        args.envs_per_group //= info.world_size
     if info.world_size != args.gpus and info.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {info.world_size}; reporting "
               f"{info.world_size}", file=sys.stderr)
@@ -231,7 +245,7 @@ def main(argv=None):
             "warmup": args.warmup,
             "ms_per_step": round(1000.0 * el / args.steps, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             # BASELINE.md's 38.9 fps is quoted on the 16x16 IMPALA config only
             "vs_baseline": (round(fps / BASELINE_FPS, 1)
                             if args.arch == "impala_flat" and s == 16 else None),
@@ -250,7 +264,8 @@ def main(argv=None):
                 "envs_per_gpu": envs_total,
                 "env_groups": f"{args.groups} x {args.envs_per_group}",
                 "env_threads_per_gpu": threads,
-                "cpus_per_rank": len(cpus),
+                "cpus_per_rank": budget,  # the rank's quota-limited CPU budget
+                "cpu_affinity_per_rank": len(cpus),
                 "policy_lanes": rt.n_lanes,
                 "allreduce": f"{args.allreduce_dtype} {args.bucket_mb:g}MB buckets",
                 "policy_gate": rt.policy_gate,

@@ -46,6 +46,7 @@ _SIGS = {
     "mbk_adam": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float,
                  c_float, c_float, c_float, c_int64, c_void_p, c_float, c_void_p],
     "mbk_to_bf16": [c_void_p, c_int64, c_void_p, c_void_p],
+    "mbk_from_bf16": [c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_conv_fwd": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int,
                      c_void_p],

@@ -69,8 +69,8 @@ class Flags:
     # --- runtime
     runtime: str = "auto"         # auto | gpu (native engine) | mono (CPU actor processes)
     device: str = "auto"          # auto | cpu | cuda
-    groups: int = 2               # gpu runtime: env groups pipelined through the GPU
-    envs_per_group: int = 256
+    groups: int = 4               # gpu runtime: env groups pipelined through the GPU
+    envs_per_group: int = 8192    # (4 x 8192 = the benched headline config, bench.py)
     actor_threads: int = 0        # gpu runtime: native env worker threads (0 = auto)
     policy_lanes: int = 1         # gpu runtime: concurrent policy streams (own graph + I/O each)
     actor_inference: str = "auto"  # mono runtime: server (batched policy in the learner
@@ -80,6 +80,10 @@ class Flags:
     nproc_per_node: int = 1       # >1: launch that many DP ranks (one per GPU) over RCCL
     bucket_mb: float = 8.0
     allreduce_dtype: str = "fp32"  # fp32 | bf16 gradient all-reduce payload (fp32 master grads)
+    rccl_high_priority: bool = True  # RCCL collectives on a high-priority stream
+    lr_scaling: str = "none"      # none | sqrt | linear: lr *= (frames per update / lr_base_batch)^k
+    lr_base_batch: int = 524288   # frames per update the base lr is tuned for (1 GPU, 4 x 8192 x 64 / 4)
+    episode_sync_every: int = 10  # DP: gather finished episodes to rank 0 every N updates
     profile_updates: int = 0      # >0: torch.profiler trace of that many updates -> savedir
     # --- io / robustness
     savedir: str = "."

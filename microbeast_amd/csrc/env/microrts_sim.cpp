@@ -608,6 +608,19 @@ void MicroRTSSim::write_obs_codes_as(int player, uint16_t* out) const {
   }
 }
 
+int MicroRTSSim::write_obs_code_list(uint32_t* entries) const {
+  int n = 0;
+  for (const Unit& u : units_) {
+    if (!u.alive) continue;
+    const int own = u.owner < 0 ? 0 : (u.owner == 0 ? 1 : 2);
+    const uint16_t code = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
+                                         std::min<int>(std::max<int>(u.res, 0), 4), own, u.type,
+                                         u.act);
+    entries[n++] = (uint32_t)cell(u.x, u.y) | ((uint32_t)code << 16);
+  }
+  return n;
+}
+
 // ---------------------------------------------------------------- observations
 static inline uint32_t unit_bits(const Unit* u, int player) {
   // empty cell: hp0, res0, owner none, type none, action noop

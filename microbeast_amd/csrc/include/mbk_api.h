@@ -70,8 +70,12 @@ typedef struct {
 } MbkActModel;
 
 typedef struct {
+  // input: dense codes + resources, or (code_list != null) the sparse rows of list_stride
+  // uint32 per env: word 0 = n | resources << 16, then n entries cell | code << 16 (occupied
+  // cells only: empty cells are code 0)
   const uint16_t* codes;   // [E][S] (device or pinned host)
   const int32_t* res;      // [E]
+  const uint32_t* code_list;
   uint32_t* obs;           // rollout row [E][S]
   uint32_t* mask;          // [E][S][3]
   uint32_t* obs2;          // optional second destination (previous slot's bootstrap row)
@@ -79,7 +83,11 @@ typedef struct {
   uint8_t* action;         // [E][S][7]
   float* logp;             // [E]
   float* value;            // [E]
-  uint16_t* act16;         // [E][S] (device or pinned host)
+  // output actions: dense packed codes [E][S] (device or pinned host), or (act_list != null)
+  // sparse rows: word 0 = n, then n entries cell | code << 16 for the non-noop cells
+  uint16_t* act16;
+  uint32_t* act_list;
+  int list_stride;
   const float* reward_src; // optional reward / done of the previous env step -> dst
   const uint8_t* done_src;
   float* reward_dst;

@@ -16,9 +16,12 @@ enum : int { NONE = 0, RESOURCE = 1, BASE = 2, BARRACKS = 3, WORKER = 4, LIGHT =
              RANGED = 7 };
 enum : int { A_NOOP = 0, A_MOVE = 1, A_HARVEST = 2, A_RETURN = 3, A_PRODUCE = 4, A_ATTACK = 5 };
 
-// per unit type: hp, cost, damage, attack range, move / attack / produce ticks
+// per unit type: hp, cost, damage, attack range, move / attack / produce ticks -- the values of
+// microRTS's UnitTypeTable (the Java engine gym-microrts wraps; one env step = one game tick),
+// so a uniform-random agent's episodes against the reference bot mix have the length, return and
+// win share of the reference's logged runs (tools/calibrate_env.py, docs/DESIGN.md section 9a)
 MB_HD constexpr int spec_hp(int t) {
-  return t == RESOURCE ? 1 : t == BASE ? 16 : t == BARRACKS ? 6 : t == WORKER ? 1 : t == LIGHT ? 4
+  return t == RESOURCE ? 1 : t == BASE ? 10 : t == BARRACKS ? 4 : t == WORKER ? 1 : t == LIGHT ? 4
        : t == HEAVY ? 4 : t == RANGED ? 1 : 0;
 }
 MB_HD constexpr int spec_cost(int t) {
@@ -30,14 +33,14 @@ MB_HD constexpr int spec_damage(int t) {
 }
 MB_HD constexpr int spec_range(int t) { return t == RANGED ? 3 : (t >= WORKER ? 1 : 0); }
 MB_HD constexpr int spec_move_t(int t) {
-  return t == WORKER ? 4 : t == LIGHT ? 3 : t == HEAVY ? 5 : t == RANGED ? 4 : 0;
+  return t == WORKER ? 10 : t == LIGHT ? 8 : t == HEAVY ? 12 : t == RANGED ? 10 : 0;
 }
-MB_HD constexpr int spec_attack_t(int t) { return t >= WORKER ? 3 : 0; }
+MB_HD constexpr int spec_attack_t(int t) { return t >= WORKER ? 5 : 0; }
 MB_HD constexpr int spec_produce_t(int t) {
-  return t == BASE ? 60 : t == BARRACKS ? 40 : t == WORKER ? 14 : t == LIGHT ? 22 : t == HEAVY ? 30
-       : t == RANGED ? 26 : 0;
+  return t == BASE ? 250 : t == BARRACKS ? 200 : t == WORKER ? 50 : t == LIGHT ? 80 : t == HEAVY ? 120
+       : t == RANGED ? 100 : 0;
 }
-constexpr int kHarvestT = 5, kReturnT = 3;
+constexpr int kHarvestT = 20, kReturnT = 10;
 
 // 16-bit cell code: hp(3) | res(3) << 3 | owner(2) << 6 | type(3) << 8 | act(3) << 11
 // owner: 0 none, 1 = the observing player, 2 = the opponent. hp / res capped at 4.

@@ -114,3 +114,20 @@ extern "C" int mbk_to_bf16(const float* x, int64_t n, void* y, hipStream_t strea
                      (__hip_bfloat16*)y);
   return (int)hipGetLastError();
 }
+
+namespace {
+__global__ __launch_bounds__(256) void from_bf16_kernel(const __hip_bfloat16* __restrict__ x,
+                                                        int64_t n, float* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    y[i] = __bfloat162float(x[i]);
+}
+}  // namespace
+
+// bf16 -> fp32 widening copy (the bf16 gradient all-reduce payload back into the fp32 master
+// gradient buffer, parallel/dist.py), instead of an ATen copy kernel
+extern "C" int mbk_from_bf16(const void* x, int64_t n, float* y, hipStream_t stream) {
+  hipLaunchKernelGGL(from_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, stream,
+                     (const __hip_bfloat16*)x, n, y);
+  return (int)hipGetLastError();
+}

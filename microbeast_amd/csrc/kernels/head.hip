@@ -398,6 +398,8 @@ struct HeadActArgs {
   int* cnt;
   uint64_t* cellx;
   uint16_t* act16;
+  uint32_t* act_list;  // sparse action rows (mbk_api.h) instead of act16, or null
+  int list_stride;
   float* logp;
   int* pending;
   unsigned* done_ctr;
@@ -463,13 +465,26 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
       const int fe = __shfl(f, l, 64);
       const uint64_t* row = a.cellx + (size_t)fe * S;
       float s = 0.f;
+      int nz = 0;  // sparse rows: entries written so far
+      uint32_t* lrow = a.act_list ? a.act_list + (size_t)fe * a.list_stride : nullptr;
       for (int cc = lane; cc < S; cc += 64) {
         const uint64_t x = __hip_atomic_load(row + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s += __uint_as_float((uint32_t)x);
-        a.act16[(size_t)fe * S + cc] = (uint16_t)(x >> 32);
+        const uint32_t code = (uint32_t)(x >> 32);
+        if (lrow) {  // only the non-noop cells travel back to the env
+          const uint64_t bal = __ballot(code != 0u);
+          const int pos = nz + __popcll(bal & ((1ull << lane) - 1ull));
+          if (code != 0u) lrow[1 + pos] = (uint32_t)cc | (code << 16);
+          nz += __popcll(bal);
+        } else {
+          a.act16[(size_t)fe * S + cc] = (uint16_t)code;
+        }
       }
       s = wave_sum(s);
-      if (lane == 0) a.logp[fe] = s;
+      if (lane == 0) {
+        a.logp[fe] = s;
+        if (lrow) lrow[0] = (uint32_t)nz;
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -1001,7 +1016,8 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
   const int S = m->H * m->W;
   if (S < 1 || S > kMaxUnitCells - 1 || (S & 3)) return (int)hipErrorInvalidValue;
   if (!m->feat || !m->Wp || !m->bp || !m->rng || !m->bucket || !m->bucket_cnt || !m->cellx ||
-      !m->pending || !m->done_ctr || !s->mask || !s->action || !s->act16 || !s->logp)
+      !m->pending || !m->done_ctr || !s->mask || !s->action || (!s->act16 && !s->act_list) ||
+      !s->logp)
     return (int)hipErrorInvalidValue;
   if ((uintptr_t)m->cellx & 7) return (int)hipErrorInvalidValue;
   HeadActArgs a{};
@@ -1015,6 +1031,8 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
   a.cnt = m->bucket_cnt;
   a.cellx = m->cellx;
   a.act16 = s->act16;
+  a.act_list = s->act_list;
+  a.list_stride = s->list_stride;
   a.logp = s->logp;
   a.pending = m->pending;
   a.done_ctr = m->done_ctr;

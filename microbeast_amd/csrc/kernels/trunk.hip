@@ -699,6 +699,9 @@ struct ActTrunkArgs {
   const float* b0;
   const uint16_t* codes;
   const int32_t* res;
+  const uint32_t* code_list;  // sparse input rows (mbk_api.h MbkActStep), or null
+  uint32_t* act_list;         // sparse action rows: A writes n = 0 for envs with nothing to act
+  int list_stride;
   uint32_t* obs;
   uint32_t* mask;
   uint32_t* obs2;
@@ -841,15 +844,37 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias0[i] = a.b0[4 * g + i];
     // ---- P1: codes / resources -> LDS, byte LUT, counters; reward / done of the last env step
-    for (int i = tid; i < nimg * (S / 8); i += kThreads) {  // 16 B = 8 codes per thread
-      const int im = i / (S / 8), q = i - im * (S / 8);
-      ((uint4*)lcodes)[i] = ((const uint4*)(a.codes + (size_t)(img0 + im) * S))[q];
+    if (a.code_list) {
+      // sparse rows (occupied cells only, ~3-8x fewer PCIe bytes than the dense codes): one
+      // wave per env reads the count word and the first 63 entries in one access, scatters
+      // them into the zeroed LDS code row, and reads further entries only if there are more
+      for (int el = wave; el < nimg; el += NW) {
+        uint16_t* cs = lcodes + el * S;
+        for (int c = lane * 4; c < S; c += 256) *(uint2*)(cs + c) = make_uint2(0u, 0u);
+        const uint32_t* row = a.code_list + (size_t)(img0 + el) * a.list_stride;
+        const uint32_t w = lane <= S ? row[lane] : 0u;
+        const uint32_t w0 = (uint32_t)__shfl((int)w, 0, 64);
+        const int n = min((int)(w0 & 0xFFFFu), S);
+        if (lane == 0) lres[el] = (int)(w0 >> 16);
+        __builtin_amdgcn_wave_barrier();
+        if (lane >= 1 && lane <= n && (w & 0xFFFFu) < (uint32_t)S)
+          cs[w & 0xFFFFu] = (uint16_t)(w >> 16);
+        for (int k = 64 + lane; k <= n; k += 64) {
+          const uint32_t x = row[k];
+          if ((x & 0xFFFFu) < (uint32_t)S) cs[x & 0xFFFFu] = (uint16_t)(x >> 16);
+        }
+      }
+    } else {
+      for (int i = tid; i < nimg * (S / 8); i += kThreads) {  // 16 B = 8 codes per thread
+        const int im = i / (S / 8), q = i - im * (S / 8);
+        ((uint4*)lcodes)[i] = ((const uint4*)(a.codes + (size_t)(img0 + im) * S))[q];
+      }
+      if (tid < nimg) lres[tid] = a.res[img0 + tid];
     }
     if (tid < 256) ((uint4*)lut)[tid] = mbk::bits8_bf16((uint32_t)tid);
     for (int c = tid; c < S; c += kThreads) lcnt[c] = 0;
     if (tid == 0) *npairs = 0;
     if (tid < nimg) {
-      lres[tid] = a.res[img0 + tid];
       if (a.reward_dst) a.reward_dst[img0 + tid] = a.reward_src[img0 + tid];
       if (a.done_dst) a.done_dst[img0 + tid] = a.done_src[img0 + tid];
     }
@@ -909,7 +934,13 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
         a.pending[e] = n;
         if (n == 0) a.logp[e] = 0.f;
       }
-      if (n == 0) *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);  // nothing to sample: no-ops
+      if (n == 0) {  // nothing to sample: all no-ops
+        if (a.act_list) {
+          if (lane == 0) a.act_list[(size_t)e * a.list_stride] = 0u;
+        } else {
+          *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
+        }
+      }
     }
     __syncthreads();
     // ---- P3: one global bucket reservation per active cell of the tile (lcnt -> its base) ...
@@ -1150,15 +1181,17 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   if (!m->w0 || !m->b0 || !m->w5 || !m->b5 || !m->wc || !m->bc || !m->feat || !m->cellx ||
       !m->pending || !m->bucket_cnt || !m->bucket)
     return (int)hipErrorInvalidValue;
-  if (!s->codes || !s->res || !s->obs || !s->mask || !s->action || !s->logp || !s->value ||
-      !s->act16)
+  if ((!s->code_list && (!s->codes || !s->res)) || (!s->act_list && !s->act16) || !s->obs ||
+      !s->mask || !s->action || !s->logp || !s->value)
+    return (int)hipErrorInvalidValue;
+  if ((s->code_list || s->act_list) && s->list_stride < m->H * m->W + 1)
     return (int)hipErrorInvalidValue;
   if ((s->obs2 == nullptr) != (s->mask2 == nullptr) ||
       (s->reward_dst == nullptr) != (s->reward_src == nullptr) ||
       (s->done_dst == nullptr) != (s->done_src == nullptr))
     return (int)hipErrorInvalidValue;
   // 16-byte vector accesses of whole rows (S = 256 cells per env)
-  if (!al16(s->codes) || !al16(s->obs) || !al16(s->mask) || !al16(s->action) ||
+  if ((s->codes && !al16(s->codes)) || !al16(s->obs) || !al16(s->mask) || !al16(s->action) ||
       !al16(m->cellx) || !al16(m->w0) || !al16(m->feat) || ((uintptr_t)s->act16 & 7) ||
       (s->obs2 && (!al16(s->obs2) || !al16(s->mask2))))
     return (int)hipErrorInvalidValue;
@@ -1189,6 +1222,9 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.b0 = m->b0;
   a.codes = s->codes;
   a.res = s->res;
+  a.code_list = s->code_list;
+  a.act_list = s->act_list;
+  a.list_stride = s->list_stride;
   a.obs = s->obs;
   a.mask = s->mask;
   a.obs2 = s->obs2;

@@ -312,6 +312,7 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("publish", &GpuEngine::publish, py::arg("src"), py::arg("dsts"), py::arg("nbytes"),
            py::arg("stream"), py::arg("version") = -1)
       .def("slot_version", &GpuEngine::slot_version)
+      .def("set_policy_version", &GpuEngine::set_policy_version)
       .def("publish_opponent", &GpuEngine::publish_opponent)
       .def("set_initial_opponent", &GpuEngine::set_initial_opponent)
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })

@@ -179,6 +179,8 @@ GpuEngine::~GpuEngine() {
   if (h_ep_return_) hipHostFree(h_ep_return_);
   if (h_ep_step_) hipHostFree(h_ep_step_);
   if (h_done_) hipHostFree(h_done_);
+  if (h_code_list_) hipHostFree(h_code_list_);
+  if (h_act_list_) hipHostFree(h_act_list_);
   if (gate_) hipFree(gate_);
   for (Lane& L : lanes_) {
     for (int p = 0; p < 2; ++p) {
@@ -253,6 +255,17 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
       throw std::runtime_error("set_act_models: model block shape mismatch");
   act_models_ = models;
   act_copy_ = copy;
+  sparse_ = !models.empty() && !copy;
+  if (sparse_ && !h_code_list_) {
+    const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
+    list_stride_ = (S_ + 1 + 3) & ~3;  // word 0 + up to S entries, 16-byte rows
+    const size_t bytes = total * list_stride_ * 4;
+    if (hipHostMalloc((void**)&h_code_list_, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h_act_list_, bytes, hipHostMallocDefault) != hipSuccess)
+      throw std::runtime_error("set_act_models: hipHostMalloc of the sparse staging failed");
+    std::memset(h_act_list_, 0, bytes);
+    env_->write_code_lists(h_code_list_, list_stride_);  // the reset state, as lists
+  }
 }
 
 void GpuEngine::stop() {
@@ -356,7 +369,10 @@ void GpuEngine::worker_loop(int wid) {
         try {
           if (inject_fault_.exchange(0) != 0)
             throw std::runtime_error("injected env-worker fault (--fault_inject_every)");
-          if (G.selfplay)
+          if (sparse_)
+            env_->step_range_lists(a0 + e, a0 + e1, h_act_list_, h_code_list_, list_stride_,
+                                   h_reward_, h_done_, &log_);
+          else if (G.selfplay)
             env_->step_range_codes_sp(a0 + e, a0 + e1, h_act16_, h_act16_p1_, h_codes_, h_res_,
                                       h_codes_p1_, h_res_p1_, h_reward_, h_done_, &log_,
                                       G.opp_version, h_ep_return_, h_ep_step_);
@@ -494,8 +510,15 @@ bool GpuEngine::enqueue_gpu(int g) {
     }
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
     MbkActStep a{};
-    a.codes = zc ? h_codes_ + e0 * S_ : (const uint16_t*)io.in_codes;
-    a.res = zc ? h_res_ + e0 : (const int32_t*)io.in_res;
+    if (sparse_) {
+      a.code_list = h_code_list_ + e0 * list_stride_;
+      a.act_list = h_act_list_ + e0 * list_stride_;
+      a.list_stride = list_stride_;
+    } else {
+      a.codes = zc ? h_codes_ + e0 * S_ : (const uint16_t*)io.in_codes;
+      a.res = zc ? h_res_ + e0 : (const int32_t*)io.in_res;
+      a.act16 = zc ? h_act16_ + e0 * S_ : (uint16_t*)io.out_act16;
+    }
     a.obs = (uint32_t*)obs_at(G.cur, t);
     a.mask = (uint32_t*)mask_at(G.cur, t);
     if (close_prev) {  // this row is also the previous slot's bootstrap row T
@@ -505,7 +528,6 @@ bool GpuEngine::enqueue_gpu(int g) {
     a.action = (uint8_t*)act_at(G.cur, t);
     a.logp = (float*)f32_at(buf_.logp, G.cur, t);
     a.value = (float*)f32_at(buf_.value, G.cur, t);
-    a.act16 = zc ? h_act16_ + e0 * S_ : (uint16_t*)io.out_act16;
     if (!G.first) {
       a.reward_src = h_reward_ + e0;
       a.done_src = h_done_ + e0;

@@ -160,6 +160,11 @@ class GpuEngine {
   }
   // Version of the behaviour weights a slot's FIRST step acted with (the oldest in it).
   int slot_version(int slot) const { return slot_version_.at(slot); }
+  // Learner update of the weights the lanes start with (a restarted engine acts with the
+  // learner's current weights, not version 0); before start().
+  void set_policy_version(int version) {
+    for (auto& L : lanes_) L.policy_version = version;
+  }
   // League id of the opponent weights in place at start (before any publish_opponent).
   void set_initial_opponent(int version) {
     for (auto& L : lanes_) L.opp_version = version;
@@ -178,6 +183,10 @@ class GpuEngine {
   uintptr_t host_codes() const { return (uintptr_t)h_codes_; }
   uintptr_t host_res() const { return (uintptr_t)h_res_; }
   uintptr_t host_act16() const { return (uintptr_t)h_act16_; }
+  // sparse fused-step staging (0 unless set_act_models(.., copy=false)) and its row stride
+  uintptr_t host_code_list() const { return (uintptr_t)h_code_list_; }
+  uintptr_t host_act_list() const { return (uintptr_t)h_act_list_; }
+  int list_stride() const { return list_stride_; }
   // zero-copy policy steps: one captured graph per group that reads the group's codes /
   // resources straight from pinned host memory and writes its packed actions there (no
   // H2D / D2H copy commands on the lane); set before start(), 0 entries = copy path
@@ -307,6 +316,12 @@ class GpuEngine {
   std::vector<hipGraphExec_t> group_graph_;  // zero-copy graphs per group (may be empty)
   std::vector<MbkActModel> act_models_;      // fused acting steps per lane (may be empty)
   bool act_copy_ = false;
+  // sparse PCIe form of the fused zero-copy step (VecEnv::step_range_lists): pinned rows of
+  // list_stride_ uint32 per env, occupied-cell codes in, non-noop actions out
+  bool sparse_ = false;
+  int list_stride_ = 0;
+  uint32_t* h_code_list_ = nullptr;
+  uint32_t* h_act_list_ = nullptr;
 };
 
 }  // namespace mb

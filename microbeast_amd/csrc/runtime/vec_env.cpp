@@ -1,5 +1,7 @@
 #include "vec_env.h"
 
+#include <algorithm>
+
 namespace mb {
 
 VecEnv::VecEnv(int size, int n_envs, int max_steps, uint64_t seed, const std::vector<int>& bots,
@@ -102,6 +104,52 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
     done[i] = d ? 1 : 0;
     sims_[i]->write_obs_codes(codes + (size_t)i * S);
     res[i] = sims_[i]->resources(0);
+  }
+}
+
+void VecEnv::write_code_lists(uint32_t* lists, int stride) const {
+  for (size_t i = 0; i < sims_.size(); ++i) {
+    uint32_t* row = lists + i * (size_t)stride;
+    const int n = sims_[i]->write_obs_code_list(row + 1);
+    row[0] = (uint32_t)n | ((uint32_t)sims_[i]->resources(0) << 16);
+  }
+}
+
+void VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,
+                              int stride, float* reward, uint8_t* done, EpisodeLog* log) {
+  const size_t S = (size_t)size_ * size_;
+  thread_local std::vector<uint16_t> dense;  // the listed actions expanded to a cell row
+  dense.assign(S, 0);
+  for (int i = e0; i < e1; ++i) {
+    if (i + 2 < e1) __builtin_prefetch(sims_[i + 2].get());
+    if (i + 1 < e1) {
+      sims_[i + 1]->prefetch();
+      __builtin_prefetch(act_lists + (size_t)(i + 1) * stride);
+    }
+    const uint32_t* arow = act_lists + (size_t)i * stride;
+    const uint32_t na = std::min<uint32_t>(arow[0] & 0xFFFFu, (uint32_t)S);
+    for (uint32_t k = 1; k <= na; ++k) {
+      const uint32_t c = arow[k] & 0xFFFFu;
+      if (c < S) dense[c] = (uint16_t)(arow[k] >> 16);
+    }
+    bool d = false;
+    const float r = sims_[i]->step_packed(dense.data(), &d);
+    for (uint32_t k = 1; k <= na; ++k) {  // back to all-noop for the next env
+      const uint32_t c = arow[k] & 0xFFFFu;
+      if (c < S) dense[c] = 0;
+    }
+    ep_ret_[i] += r;
+    ep_len_[i] += 1;
+    if (d) {
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sims_[i]->winner(), -1 - sims_[i]->bot()});
+      ep_ret_[i] = 0.f;
+      ep_len_[i] = 0;
+    }
+    reward[i] = r;
+    done[i] = d ? 1 : 0;
+    uint32_t* crow = code_lists + (size_t)i * stride;
+    const int n = sims_[i]->write_obs_code_list(crow + 1);
+    crow[0] = (uint32_t)n | ((uint32_t)sims_[i]->resources(0) << 16);
   }
 }
 

@@ -85,14 +85,30 @@ class MicroRTSAdapter:
         self.env.close()
 
 
+# --opponents names (config.py, the native stand-in's bots) -> gym_microrts.microrts_ai members
+# (reference libs/utils.py:69-72 builds ai2s from coacAI, randomBiasedAI, lightRushAI,
+# workerRushAI); microrts_ai names pass through unchanged
+MICRORTS_AI = {"coac": "coacAI", "random_biased": "randomBiasedAI", "light_rush": "lightRushAI",
+               "worker_rush": "workerRushAI", "passive": "passiveAI", "random": "randomAI"}
+REFERENCE_AI2S = ["coacAI"] * 3 + ["randomBiasedAI", "lightRushAI", "workerRushAI"]
+
+
+def microrts_ai_names(opponents) -> list[str]:
+    return [MICRORTS_AI.get(n, n) for n in (opponents or REFERENCE_AI2S)]
+
+
 def create_microrts_env(size, n_envs, max_steps, opponents=None, reward_weight=None):
+    """The reference's create_env (libs/utils.py:59-76) on the real gym-microRTS."""
     if not gym_microrts_available():
         raise RuntimeError("env=microrts needs gym-microrts (Java microRTS); it is not installed. "
                            "Use --env synthetic.")
     from gym_microrts import microrts_ai
     from gym_microrts.envs.vec_env import MicroRTSGridModeVecEnv
 
-    names = opponents or ["coacAI"] * 3 + ["randomBiasedAI", "lightRushAI", "workerRushAI"]
+    names = microrts_ai_names(opponents)
+    missing = [n for n in names if not hasattr(microrts_ai, n)]
+    if missing:
+        raise ValueError(f"gym_microrts.microrts_ai has no {missing} (--opponents)")
     ai2s = [getattr(microrts_ai, n) for n in names][:n_envs]
     while len(ai2s) < n_envs:
         ai2s.append(ai2s[len(ai2s) % len(names)])

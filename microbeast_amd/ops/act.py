@@ -40,10 +40,38 @@ class MbkActModel(ctypes.Structure):
 
 
 class MbkActStep(ctypes.Structure):
-    _fields_ = [("codes", c_void_p), ("res", c_void_p), ("obs", c_void_p), ("mask", c_void_p),
-                ("obs2", c_void_p), ("mask2", c_void_p), ("action", c_void_p), ("logp", c_void_p),
-                ("value", c_void_p), ("act16", c_void_p), ("reward_src", c_void_p),
-                ("done_src", c_void_p), ("reward_dst", c_void_p), ("done_dst", c_void_p)]
+    _fields_ = [("codes", c_void_p), ("res", c_void_p), ("code_list", c_void_p),
+                ("obs", c_void_p), ("mask", c_void_p), ("obs2", c_void_p), ("mask2", c_void_p),
+                ("action", c_void_p), ("logp", c_void_p), ("value", c_void_p),
+                ("act16", c_void_p), ("act_list", c_void_p), ("list_stride", c_int),
+                ("reward_src", c_void_p), ("done_src", c_void_p), ("reward_dst", c_void_p),
+                ("done_dst", c_void_p)]
+
+
+def code_lists(codes: torch.Tensor, res: torch.Tensor, stride: int) -> torch.Tensor:
+    """Dense 16-bit codes [E, S] + resources [E] -> the sparse input rows of the fused step
+    (word 0 = n | res << 16, then cell | code << 16 per occupied cell; the engine's env
+    workers write this form directly, VecEnv::step_range_lists)."""
+    E, S = codes.shape
+    out = torch.zeros(E, stride, dtype=torch.int64)
+    c = codes.cpu().to(torch.int64) & 0xFFFF
+    for e in range(E):
+        nz = torch.nonzero(c[e]).view(-1)
+        out[e, 0] = len(nz) | (int(res[e]) << 16)
+        out[e, 1:1 + len(nz)] = nz | (c[e, nz] << 16)
+    return out.to(torch.int32)
+
+
+def dense_actions(act_list: torch.Tensor, S: int) -> torch.Tensor:
+    """Sparse action rows (word 0 = n, then cell | code << 16) -> dense int16 [E, S] codes."""
+    a = act_list.cpu().to(torch.int64) & 0xFFFFFFFF
+    E = a.shape[0]
+    out = torch.zeros(E, S, dtype=torch.int64)
+    for e in range(E):
+        n = int(a[e, 0])
+        ent = a[e, 1:1 + n]
+        out[e, ent & 0xFFFF] = ent >> 16
+    return out.to(torch.int16)
 
 
 def supported(model, size: int, fp8: bool = False) -> bool:
@@ -104,17 +132,22 @@ class ActWorkspace:
         return bytes(self.struct)
 
     def step(self, codes, res, obs, mask, action, logp, value, act16, obs2=None, mask2=None,
-             reward=None, done=None, reward_dst=None, done_dst=None) -> None:
-        """One fused policy step on the current stream. codes int16 [E, S], res int32 [E];
-        outputs obs int32 [E, S], mask int32 [E, S, 3], action uint8 [E, S, 7], logp / value
-        fp32 [E], act16 int16 [E, S]; optional second obs / mask destination and the reward /
-        done copy of the previous env step."""
+             reward=None, done=None, reward_dst=None, done_dst=None, code_list=None,
+             act_list=None) -> None:
+        """One fused policy step on the current stream. codes int16 [E, S], res int32 [E]
+        (or code_list int32 [E, stride] sparse rows, ``code_lists``); outputs obs int32 [E, S],
+        mask int32 [E, S, 3], action uint8 [E, S, 7], logp / value fp32 [E], act16 int16
+        [E, S] (or act_list int32 [E, stride] sparse rows); optional second obs / mask
+        destination and the reward / done copy of the previous env step."""
         s = MbkActStep()
-        s.codes, s.res = codes.data_ptr(), res.data_ptr()
+        s.codes, s.res = N.ptr(codes), N.ptr(res)
+        s.code_list, s.act_list = N.ptr(code_list), N.ptr(act_list)
+        stride = (code_list if code_list is not None else act_list)
+        s.list_stride = int(stride.shape[1]) if stride is not None else 0
         s.obs, s.mask = obs.data_ptr(), mask.data_ptr()
         s.obs2, s.mask2 = N.ptr(obs2), N.ptr(mask2)
         s.action, s.logp, s.value = action.data_ptr(), logp.data_ptr(), value.data_ptr()
-        s.act16 = act16.data_ptr()
+        s.act16 = N.ptr(act16)
         s.reward_src, s.done_src = N.ptr(reward), N.ptr(done)
         s.reward_dst, s.done_dst = N.ptr(reward_dst), N.ptr(done_dst)
         N.check(N.kernels().mbk_act_step(ctypes.addressof(self.struct), ctypes.addressof(s),

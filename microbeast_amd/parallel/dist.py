@@ -56,8 +56,12 @@ class DistInfo:
 
 
 def init_distributed(use_cuda: bool, timeout_s: float = 600.0,
-                     force_pg: bool | None = None) -> DistInfo:
-    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*)."""
+                     force_pg: bool | None = None, high_priority: bool | None = None) -> DistInfo:
+    """Initialise from torchrun-style env vars (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*).
+
+    high_priority (default: MBK_RCCL_HIGH_PRIORITY, on): RCCL runs its collectives on a
+    high-priority internal stream, so hook-fired all-reduce kernels do not queue behind the
+    learner's long persistent backward kernels on the default-priority queues."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -77,6 +81,12 @@ def init_distributed(use_cuda: bool, timeout_s: float = 600.0,
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if use_cuda and backend == "nccl":
             kw["device_id"] = torch.device("cuda", local)
+            if high_priority is None:
+                high_priority = os.environ.get("MBK_RCCL_HIGH_PRIORITY", "1") == "1"
+            if high_priority:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                kw["pg_options"] = opts
         if "MASTER_PORT" not in os.environ:  # forced single-rank group outside torchrun
             from .launch import free_port
             kw.update(init_method=f"tcp://127.0.0.1:{free_port()}", rank=rank, world_size=world)
@@ -150,7 +160,12 @@ class GradAllReducer:
         g = self.flat.grad[s:e]
         if self.comm is not None:
             c = self.comm[s:e]
-            c.copy_(g)
+            if g.is_cuda and c.dtype == torch.bfloat16:  # native narrowing copy (no ATen)
+                from .. import _native as N
+                N.check(N.kernels().mbk_to_bf16(g.data_ptr(), e - s, c.data_ptr(),
+                                                N.stream_ptr()), "to_bf16")
+            else:
+                c.copy_(g)
             g = c
         self.works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, async_op=True))
 
@@ -173,7 +188,13 @@ class GradAllReducer:
             w.wait()
         self.works = []
         if self.comm is not None:
-            self.flat.grad.copy_(self.comm)
+            if self.comm.is_cuda and self.comm.dtype == torch.bfloat16:
+                from .. import _native as N
+                N.check(N.kernels().mbk_from_bf16(self.comm.data_ptr(), self.flat.numel,
+                                                  self.flat.grad.data_ptr(), N.stream_ptr()),
+                        "from_bf16")
+            else:
+                self.flat.grad.copy_(self.comm)
 
 
 def all_reduce_mean(t: torch.Tensor, info: DistInfo) -> torch.Tensor:
@@ -192,6 +213,19 @@ def gather_objects(obj, info: DistInfo) -> list:
     out = [None] * info.world_size if info.is_main else None
     dist.gather_object(obj, out, dst=0, group=info.host_group)
     return out if info.is_main else []
+
+
+def all_ok(ok: bool, info: DistInfo) -> bool:
+    """True iff every rank passes ``ok`` (a MIN all-reduce of one int over the gloo host
+    group: CPU only, never waits on a GPU stream). Called once per update before the
+    gradient collectives, so a rank that cannot continue (engine restarts exhausted) makes
+    every rank stop at the same point instead of leaving its peers blocked in an RCCL
+    all-reduce until the process-group timeout."""
+    if not info.enabled:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=info.host_group)
+    return bool(t.item())
 
 
 def barrier(info: DistInfo) -> None:

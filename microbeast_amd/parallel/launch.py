@@ -11,7 +11,8 @@ pieces make that launchable by hand and fast on an 8-GPU node:
   ``torch.distributed.run`` with N ranks as a CHILD process and returns its
   exit code. It runs before anything touches the GPU (counting devices does
   not initialise HIP on this image) and never ``exec``s.
-* ``pin_rank`` — restricts a rank (and every thread it starts afterwards: the
+* ``pin_rank`` — restricts a rank (every thread it already runs -- HIP runtime,
+  RCCL / gloo, torch's pools -- and every thread it starts afterwards: the
   native env workers, the engine's driver thread, the pinned-staging first
   touch) to whole physical cores on the NUMA node its GPU hangs off. Ranks that
   share a node split its cores into disjoint sets, so env workers of two GPUs
@@ -155,9 +156,25 @@ def plan_affinity(local_rank: int, local_world: int, allowed: list[int],
     return mine if len(mine) >= min(min_cpus, len(fallback)) else fallback
 
 
+def set_process_affinity(cpus: list[int]) -> None:
+    """sched_setaffinity on EVERY thread of this process (``os.sched_setaffinity(0)`` only
+    moves the calling thread and the threads it creates later; the HIP runtime, RCCL / gloo
+    and torch's intra-op pool may already be running)."""
+    os.sched_setaffinity(0, cpus)
+    try:
+        tids = os.listdir("/proc/self/task")
+    except OSError:
+        return
+    for t in tids:
+        try:
+            os.sched_setaffinity(int(t), cpus)
+        except (OSError, ValueError):
+            pass  # a thread that exited meanwhile
+
+
 def pin_rank(local_rank: int, local_world: int, device_index: int | None = None) -> list[int]:
-    """Pin the calling thread (and threads it starts later) to this rank's CPU share.
-    Returns the CPU list (unchanged affinity if pinning is disabled or impossible)."""
+    """Pin every thread of this process (and threads it starts later) to this rank's CPU
+    share. Returns the CPU list (unchanged affinity if pinning is disabled or impossible)."""
     allowed = sorted(os.sched_getaffinity(0))
     if os.environ.get("MBK_NUMA_PIN", "1") == "0":
         return allowed
@@ -177,7 +194,7 @@ def pin_rank(local_rank: int, local_world: int, device_index: int | None = None)
                          min_cpus=share)
     if mine:
         try:
-            os.sched_setaffinity(0, mine)
+            set_process_affinity(mine)
         except OSError:
             return allowed
     return mine or allowed

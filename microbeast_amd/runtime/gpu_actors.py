@@ -328,9 +328,13 @@ class GpuActorRuntime:
         return g
 
     # ------------------------------------------------------------ control
-    def start(self, learner_flat: FlatParams | None = None, opponent_version: int = -1):
+    def start(self, learner_flat: FlatParams | None = None, opponent_version: int = -1,
+              version: int = 0):
         """opponent_version: league id of the starting opponent weights (self-play groups
-        start against a copy of ``learner_flat``; tag their episodes with this id)."""
+        start against a copy of ``learner_flat``; tag their episodes with this id).
+        version: learner update count of ``learner_flat`` (a restarted engine's slots are
+        tagged with it, so policy_lag stays the true lag)."""
+        self.engine.set_policy_version(int(version))
         if self.selfplay_groups > 0:
             self.engine.set_initial_opponent(int(opponent_version))
         for lane in self.lanes:

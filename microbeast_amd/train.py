@@ -15,6 +15,7 @@ checkpoints and shuts its actors down.
 """
 from __future__ import annotations
 
+import gc
 import os
 import time
 
@@ -24,12 +25,23 @@ from .config import Flags
 from .learner import Learner, LearnerHParams
 from .models.factory import make_model
 from .parallel import dist as D
-from .utils.checkpoint import load_checkpoint, restore, save_checkpoint
+from .utils.checkpoint import (load_checkpoint, load_league_shard, restore, save_checkpoint,
+                               save_league_shard)
 from .utils.metrics import CsvLogger
 
 
-def _hparams(flags: Flags) -> LearnerHParams:
-    return LearnerHParams(lr=flags.lr, adam_eps=flags.adam_eps, gamma=flags.gamma,
+def scaled_lr(flags: Flags, frames_per_update: int) -> float:
+    """--lr_scaling: the base --lr is tuned for --lr_base_batch frames per update (the reference
+    2.5e-4 at one GPU's 524,288); weak-scaled DP multiplies the global batch by the world size
+    (and --batch_size by its value), so the step size can follow it: sqrt (Adam's usual rule)
+    or linear in the batch ratio, or stay (none)."""
+    r = frames_per_update / max(1, flags.lr_base_batch)
+    k = {"none": 0.0, "sqrt": 0.5, "linear": 1.0}[flags.lr_scaling]
+    return flags.lr * (r ** k)
+
+
+def _hparams(flags: Flags, lr: float | None = None) -> LearnerHParams:
+    return LearnerHParams(lr=flags.lr if lr is None else lr, adam_eps=flags.adam_eps, gamma=flags.gamma,
                           baseline_cost=flags.baseline_cost, entropy_cost=flags.entropy_cost,
                           rho_bar=flags.rho_bar, c_bar=flags.c_bar, pg_rho_bar=flags.pg_rho_bar,
                           reward_clip=flags.reward_clip, max_grad_norm=flags.max_grad_norm,
@@ -102,13 +114,31 @@ def _profile_tick(prof, n_update: int, flags: Flags, cuda: bool):
     return prof
 
 
+def restart_runtime(rt, make, learner_flat, n_update: int, league=None):
+    """Replace a failed GPU actor runtime: stop it and drop every reference to it, collect,
+    return its cached HBM to the allocator, THEN build and start the new one (acting with
+    the learner's current weights, tagged with update ``n_update``). The caller must not
+    hold references into the old runtime (e.g. a batch that views its rollout slots)."""
+    rt.stop()
+    rt = None
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.empty_cache()
+    new = make()
+    new.start(learner_flat, opponent_version=league.current if league is not None else -1,
+              version=n_update)
+    if league is not None and league.current in league.snaps:
+        new.set_opponent(league.snapshot(league.current), league.current)
+    return new
+
+
 def _league_extra(league):
     return {"league": league.state_dict()} if league is not None else None
 
 
 def train(flags: Flags) -> dict:
     want_cuda = flags.device == "cuda" or (flags.device == "auto" and torch.cuda.is_available())
-    info = D.init_distributed(use_cuda=want_cuda)
+    info = D.init_distributed(use_cuda=want_cuda, high_priority=flags.rccl_high_priority)
     dev = torch.device("cuda", info.local_rank) if want_cuda else torch.device("cpu")
     runtime = flags.runtime if flags.runtime != "auto" else ("gpu" if want_cuda else "mono")
     if runtime == "gpu" and not want_cuda:
@@ -129,7 +159,11 @@ def train(flags: Flags) -> dict:
         f"world={info.world_size} map={flags.env_size}x{flags.env_size} arch={flags.arch}")
 
     model = make_model(flags, dev)
-    learner = Learner(model, _hparams(flags), dev, info)
+    per_rank = (flags.envs_per_group if runtime == "gpu" else flags.n_envs)
+    lr = scaled_lr(flags, flags.batch_size * per_rank * flags.unroll_length * info.world_size)
+    if lr != flags.lr:
+        log(f"[microbeast_amd] lr {flags.lr:g} -> {lr:g} (--lr_scaling {flags.lr_scaling})")
+    learner = Learner(model, _hparams(flags, lr), dev, info)
     step = n_update = 0
     ck_path = checkpoint_path(flags)
     ck = None
@@ -169,12 +203,16 @@ def train(flags: Flags) -> dict:
             league = League(capacity=flags.league_size, snapshot_every=flags.league_update_every,
                             pfsp_power=flags.pfsp_power, eps=flags.league_eps,
                             seed=flags.seed + info.rank)
-            if ck is not None and ck.get("league"):
+            shard = load_league_shard(ck_path, info.rank) if ck is not None else None
+            if shard is not None:  # this rank's own league (DP runs save one per rank)
+                league.load_state_dict(shard, dev)
+            elif ck is not None and ck.get("league"):
                 league.load_state_dict(ck["league"], dev)
             else:
                 league.add_snapshot(learner.flat.data)
             league.current = league.next_id - 1
-        rt.start(learner.flat, opponent_version=league.current if league is not None else -1)
+        rt.start(learner.flat, opponent_version=league.current if league is not None else -1,
+                 version=n_update)
         if league is not None and ck is not None and ck.get("league"):
             # resumed: play the restored snapshot instead of the learner copy
             rt.set_opponent(league.snapshot(league.current), league.current)
@@ -190,6 +228,15 @@ def train(flags: Flags) -> dict:
             rt.enable_prefetch(dev)
         frames_per_update = flags.batch_size * flags.n_envs * flags.unroll_length
     frames_per_update *= info.world_size
+
+    def save_all(step_, n_update_):
+        """Rank 0 writes the checkpoint; every rank with a league writes its own league shard
+        (snapshots + PFSP results: each DP rank matches against its own league)."""
+        if info.is_main:
+            save_checkpoint(ck_path, learner.model, learner.opt, step_, n_update_, flags,
+                            extra=_league_extra(league))
+        if league is not None and info.enabled:
+            save_league_shard(ck_path, info.rank, league.state_dict())
 
     engine_restarts = 0
     prof = None  # --profile_updates: torch.profiler timeline of a few steady-state updates
@@ -209,30 +256,45 @@ def train(flags: Flags) -> dict:
                 f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {m['fps']:,.0f} lag {m['lag']}"
                 + (f" league {m['league']}" if m.get("league") else ""))
 
+    pending_eps = []  # finished episodes since the last rank-0 gather (DP: batched exchange)
+
+    def sync_episodes(force=False):
+        # rank 0 writes every rank's episodes; under DP they travel every
+        # --episode_sync_every updates in one gloo gather instead of one per update
+        if not info.enabled or force or n_update % max(1, flags.episode_sync_every) == 0:
+            logger.episodes(_gather_episodes(list(pending_eps), info))
+            pending_eps.clear()
+
     try:
         while step < flags.total_steps and (flags.max_updates <= 0 or n_update < flags.max_updates):
             if flags.profile_updates > 0 and info.is_main:
                 prof = _profile_tick(prof, n_update, flags, want_cuda)
             t0 = time.perf_counter()
+            failure = None
             if runtime == "gpu":
                 try:
                     batch, slots = rt.get_batch(timeout=flags.batch_timeout)
                 except EngineFailure as ex:
+                    failure = str(ex)  # (the exception's frames hold the old runtime: drop it)
+                if failure is not None and engine_restarts < flags.actor_restarts:
                     # a dead env worker stops the native engine; rebuild the
-                    # actor side and keep training (bounded by --actor_restarts)
-                    if engine_restarts >= flags.actor_restarts:
-                        raise
+                    # actor side and keep training (bounded by --actor_restarts). The old
+                    # runtime (HBM slots, pinned staging, graphs) is freed BEFORE the new one
+                    # is allocated, so a restart never needs two runtimes' memory
                     engine_restarts += 1
-                    log(f"[microbeast_amd] {ex}; restarting the actor engine "
+                    log(f"[microbeast_amd] {failure}; restarting the actor engine "
                         f"({engine_restarts}/{flags.actor_restarts})")
-                    rt.stop()
-                    del rt
-                    rt = make_gpu_runtime(engine_restarts)
-                    rt.start(learner.flat,
-                             opponent_version=league.current if league is not None else -1)
-                    if league is not None:
-                        rt.set_opponent(league.snapshot(league.current), league.current)
+                    batch = slots = None  # (views of the old runtime's rollout slots)
+                    rt = restart_runtime(rt, lambda: make_gpu_runtime(engine_restarts),
+                                         learner.flat, n_update, league)
                     continue
+            # every rank agrees to go on before the update's gradient collectives, so one
+            # that cannot (restarts exhausted) stops all of them now, not at the PG timeout
+            if not D.all_ok(failure is None, info):
+                if failure is not None:
+                    raise EngineFailure(failure)
+                raise RuntimeError("another data-parallel rank stopped (engine failure)")
+            if runtime == "gpu":
                 lag = rt.policy_lag(slots, n_update)
             else:
                 batch, slots = rt.get_batch(flags.batch_timeout)
@@ -273,21 +335,19 @@ def train(flags: Flags) -> dict:
                 eps = rt.drain_episodes()
                 if league is not None:
                     league.record(eps)  # each rank matches against its own league
-                logger.episodes(_gather_episodes(eps, info))
+                pending_eps.extend(eps)
+                sync_episodes()
             flush()
             if flags.checkpoint_every and n_update % flags.checkpoint_every == 0:
-                if info.is_main:
-                    save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,
-                                    extra=_league_extra(league))
+                save_all(step, n_update)
                 D.barrier(info)
+        sync_episodes(force=True)
     finally:
         if prof is not None:
             _profile_tick(prof, -1, flags, want_cuda)
         flush(wait=True)
         rt.stop()
-        if info.is_main:
-            save_checkpoint(ck_path, learner.model, learner.opt, step, n_update, flags,
-                            extra=_league_extra(league))
+        save_all(step, n_update)
         logger.close()
     wall = time.perf_counter() - t_start
     out = dict(last, updates=n_update, steps=step, wall_s=wall, checkpoint=ck_path,

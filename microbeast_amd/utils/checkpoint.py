@@ -62,3 +62,30 @@ def restore(ck: dict, model: torch.nn.Module, optimizer=None) -> tuple[int, int]
     if "rng_state" in ck and ck["rng_state"] is not None:
         torch.set_rng_state(ck["rng_state"])
     return int(ck.get("step", 0)), int(ck.get("n_update", 0))
+
+
+def league_shard_path(path: str, rank: int) -> str:
+    """Per-rank league state next to the main checkpoint: every DP rank plays (and matches
+    opponents from) its own league, so each one's snapshots and PFSP results are saved."""
+    return f"{path}.league{rank}"
+
+
+def save_league_shard(path: str, rank: int, league_state: dict) -> str:
+    p = league_shard_path(path, rank)
+    d = os.path.dirname(os.path.abspath(p))
+    os.makedirs(d, exist_ok=True)
+    st = {k: (v.detach().cpu().clone() if torch.is_tensor(v) else v)
+          for k, v in league_state.items()}
+    if isinstance(st.get("snaps"), dict):
+        st["snaps"] = {k: v.detach().cpu().clone() for k, v in st["snaps"].items()}
+    tmp = p + ".tmp"
+    torch.save({"format": FORMAT, "rank": int(rank), "league": st}, tmp)
+    os.replace(tmp, p)
+    return p
+
+
+def load_league_shard(path: str, rank: int) -> dict | None:
+    p = league_shard_path(path, rank)
+    if not os.path.exists(p):
+        return None
+    return torch.load(p, map_location="cpu", weights_only=True).get("league")

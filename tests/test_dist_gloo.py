@@ -74,3 +74,39 @@ def test_dp_allreduce_equals_single_process(tmp_path, comm):
         assert float(d.max()) <= 2 * 2.5e-4
         assert float((d > 1e-6).float().mean()) < 0.02
         assert float(d.mean()) < 1e-6
+
+
+def _worker_ok_league(rank, world, port, outdir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from microbeast_amd.parallel.dist import all_ok, barrier, destroy, init_distributed
+    from microbeast_amd.runtime.league import League
+    from microbeast_amd.utils.checkpoint import load_league_shard, save_league_shard
+    info = init_distributed(use_cuda=False)
+    res = [all_ok(True, info), all_ok(rank != 1, info), all_ok(True, info)]
+    # every rank checkpoints its own league (snapshots + PFSP results) next to the main file
+    lg = League(capacity=4, snapshot_every=1, seed=rank)
+    for k in range(3):
+        lg.add_snapshot(torch.full((8,), float(10 * rank + k)))
+    lg.record([(1.0, 10, 0, 0, 1), (0.0, 10, 0, 1, 1 + rank)])
+    ck = os.path.join(outdir, "run.ckpt")
+    save_league_shard(ck, info.rank, lg.state_dict())
+    barrier(info)
+    back = League()
+    back.load_state_dict(load_league_shard(ck, info.rank))
+    torch.save({"ok": res, "games": back.games, "snap2": back.snapshot(2)},
+               os.path.join(outdir, f"ok{rank}.pt"))
+    destroy(info)
+
+
+def test_fail_fast_flag_and_per_rank_league_shards(tmp_path):
+    """all_ok: one rank that cannot continue stops every rank at the same update (gloo host
+    group); each rank's league is checkpointed and restored from its own shard."""
+    world = 2
+    mp.start_processes(_worker_ok_league, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    for r in range(world):
+        d = torch.load(tmp_path / f"ok{r}.pt")
+        assert d["ok"] == [True, False, True]
+        assert torch.equal(d["snap2"], torch.full((8,), float(10 * r + 2)))
+        assert d["games"][1] == (2.0 if r == 0 else 1.0)

@@ -49,9 +49,11 @@ def _model(cuda, seed):
     return m
 
 
-@pytest.mark.parametrize("E", [96, 520])
-def test_fused_act_step_bit_identical(cuda, E):
-    from microbeast_amd.ops.act import ActWorkspace
+@pytest.mark.parametrize("E,sparse", [(96, False), (520, False), (200, True)])
+def test_fused_act_step_bit_identical(cuda, E, sparse):
+    """sparse: the PCIe-light form the engine uses (occupied-cell code rows in, non-noop action
+    rows out) must give the same step as the dense codes / dense packed actions."""
+    from microbeast_amd.ops.act import ActWorkspace, code_lists, dense_actions
     from microbeast_amd.runtime.gpu_actors import graph_policy_step, make_io
 
     S = 256
@@ -67,6 +69,8 @@ def test_fused_act_step_bit_identical(cuda, E):
     logp = torch.full((E,), float("nan"), device=cuda)
     value = torch.full((E,), float("nan"), device=cuda)
     act16 = torch.full((E, S), -1, dtype=torch.int16, device=cuda)
+    stride = S + 4
+    act_list = torch.full((E, stride), -1, dtype=torch.int32, device=cuda)
     reward = torch.randn(E, device=cuda)
     done = (torch.rand(E, device=cuda) < 0.3).to(torch.uint8)
     rdst, ddst = torch.zeros_like(reward), torch.zeros_like(done)
@@ -76,9 +80,21 @@ def test_fused_act_step_bit_identical(cuda, E):
         io["in_res"].copy_(res)
         graph_policy_step(io, m, rng_a, E, 16, cuda)
         second = i % 3 == 0
-        ws.step(io["in_codes"], io["in_res"], obs, mask, action, logp, value, act16,
-                obs2=obs2 if second else None, mask2=mask2 if second else None,
-                reward=reward, done=done, reward_dst=rdst, done_dst=ddst)
+        if sparse:
+            cl = code_lists(codes, res, stride).to(cuda)
+            ws.step(None, None, obs, mask, action, logp, value, None,
+                    obs2=obs2 if second else None, mask2=mask2 if second else None,
+                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst, code_list=cl,
+                    act_list=act_list)
+            torch.cuda.synchronize()
+            act16 = dense_actions(act_list, S).to(cuda)
+            n = act_list[:, 0].cpu()
+            assert int(n.max()) <= S and bool((act_list[:, 1:].cpu().view(-1) >> 16 != 0)
+                                              .view(E, -1)[:, :int(n.min())].all())
+        else:
+            ws.step(io["in_codes"], io["in_res"], obs, mask, action, logp, value, act16,
+                    obs2=obs2 if second else None, mask2=mask2 if second else None,
+                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst)
         torch.cuda.synchronize()
         assert torch.equal(obs, io["in_obs"]), f"obs planes differ at step {i}"
         assert torch.equal(mask, io["in_mask"]), f"masks differ at step {i}"

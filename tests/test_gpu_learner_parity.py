@@ -20,6 +20,10 @@ from helpers import engine_batches
 
 pytestmark = pytest.mark.gpu
 
+# the one layer whose gradient may pass on direction + norm instead of the noise-floor bound
+# (bf16 vs fp32 sign flips of its relu gate on 2x2 maps, see the comment in the test)
+_TIE_LAYER = "network.2.res_block1.conv0."
+
 
 @pytest.mark.parametrize("S", [8, 16])
 def test_learn_hip_matches_fp32_torch(cuda, S):
@@ -70,7 +74,8 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
         cos = float(torch.dot(a, b)) / (float(a.norm()) * nb + 1e-30)
         rows.append((name, rel, floor, cos))
         # cos bound consistent with the rel bound (rel ~ sqrt(2 (1 - cos)) for small errors).
-        # Second way to pass: direction within cos 0.995 of fp32 and norm within 5 %. Needed by the stage-2 block-1
+        # Second way to pass, for the named layer ONLY (_TIE_LAYER): direction within cos 0.995
+        # of fp32 and norm within 5 %. Needed by the stage-2 block-1
         # conv0 on 2x2 maps: its du is gated by [u1 > 0] and 0.24 % of u1's signs differ
         # between bf16 and fp32 (u1 rel 0.4 %, trunk-output grad rel 3.3 %), which puts its
         # rel at 0.08-0.09 vs a bf16-torch floor of 0.0125 while cos stays 0.996 (probe:
@@ -78,7 +83,8 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
         # on the same operands, tools/dbg/dgrad_2x2_check.py)
         ok = rel < max(3.0 * floor, 3e-2) and cos > 1.0 - 0.5 * max(3.0 * floor, 3e-2) ** 2
         ratio = float(a.norm()) / nb
-        if not (ok or (cos > 0.995 and abs(ratio - 1.0) < 0.05)):
+        tie_ok = name.startswith(_TIE_LAYER) and cos > 0.995 and abs(ratio - 1.0) < 0.05
+        if not (ok or tie_ok):
             bad.append(name)
     for r in rows:  # full table on failure (pytest -s shows it always)
         print(f"{r[0]:40s} rel {r[1]:.3e}  torch-bf16 floor {r[2]:.3e}  cos {r[3]:.5f}")

@@ -114,3 +114,44 @@ def test_gpu_engine_failure_surfaces_without_restarts(cuda, tmp_path):
         train(parse_flags(_args(tmp_path, "fx", "--max_updates", "6", "--fault_inject_every",
                                 "2", "--actor_restarts", "0", "--batch_timeout", "120"),
                           interactive=False))
+
+
+def test_engine_restart_frees_the_old_runtime_first(cuda):
+    """train.restart_runtime: the failed runtime's HBM (rollout slots, I/O, graphs) is released
+    before the new one is allocated, so a restart peaks at about ONE runtime's footprint, and
+    the new engine's slots carry the learner's current update (policy lag 0, not n_update)."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+    from microbeast_amd.train import restart_runtime
+
+    torch.cuda.synchronize()
+    learner = Learner(Agent((8, 8, 27)), LearnerHParams(), cuda)
+
+    def mk():
+        return GpuActorRuntime(lambda: Agent((8, 8, 27)), 8, 2, 256, 16, 1, cuda, n_threads=2)
+
+    torch.cuda.synchronize()
+    m0 = torch.cuda.memory_allocated()
+    rt = mk()
+    rt.start(learner.flat)
+    batch, slots = rt.get_batch(timeout=120)
+    rt.release(slots)
+    del batch
+    torch.cuda.synchronize()
+    m1 = torch.cuda.memory_allocated()
+    one = m1 - m0
+    torch.cuda.reset_peak_memory_stats()
+    rt = restart_runtime(rt, mk, learner.flat, 7)
+    torch.cuda.synchronize()
+    peak, m2 = torch.cuda.max_memory_allocated(), torch.cuda.memory_allocated()
+    print(f"runtime {one / 2**20:.1f} MiB, after restart {(m2 - m0) / 2**20:.1f} MiB, "
+          f"restart peak {(peak - m0) / 2**20:.1f} MiB")
+    try:
+        assert abs(m2 - m1) < 0.1 * one
+        assert peak - m0 < 1.3 * one
+        batch, slots = rt.get_batch(timeout=120)
+        assert rt.policy_lag(slots, 7) == 0
+        rt.release(slots)
+    finally:
+        rt.stop()

@@ -4,8 +4,9 @@
 usage: python tools/timeline.py <rocprof_out_dir> [window_frac]
 
 Splits the steady-state window (last ``window_frac`` of the span) by hardware queue: the
-policy queue is the one running ``trunk_tail`` kernels, everything else with kernels is
-"learner". A policy step starts at its ``decode_obs_mask`` kernel. Reports per-step stream
+policy queue is the one running ``trunk_tail`` / ``act_trunk`` kernels, everything else with kernels is
+"learner". A policy step starts at its ``decode_obs_mask`` (graph step) or ``act_trunk`` (fused step)
+kernel. Reports per-step stream
 time inside vs outside learner activity, per-queue busy and idle time, and the union.
 """
 import csv
@@ -57,14 +58,14 @@ def main():
     t0 = rows[0][0] + int((t_end - rows[0][0]) * (1 - frac))
     rows = [r for r in rows if r[0] >= t0]
     span = t_end - t0
-    pq = {r[2] for r in rows if "trunk_tail" in r[3]}
+    pq = {r[2] for r in rows if "trunk_tail" in r[3] or "act_trunk" in r[3]}
     pol = [r for r in rows if r[2] in pq]
     lea = [r for r in rows if r[2] not in pq]
     lea_m = merge([(s, e) for s, e, _, _ in lea], tol=20_000)  # gaps < 20 us = still active
     lea_busy = sum(e - s for s, e in merge([(s, e) for s, e, _, _ in lea]))
     pol_busy = sum(e - s for s, e in merge([(s, e) for s, e, _, _ in pol]))
     all_busy = sum(e - s for s, e in merge([(s, e) for s, e, _, _ in rows]))
-    starts = [i for i, r in enumerate(pol) if "decode_obs_mask" in r[3]]
+    starts = [i for i, r in enumerate(pol) if "decode_obs_mask" in r[3] or "act_trunk" in r[3]]
     steps = []
     for a, b in zip(starts, starts[1:]):
         s = pol[a][0]
