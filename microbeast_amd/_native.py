@@ -148,6 +148,7 @@ _SIGS = {
     "mbk_act_step": [c_void_p, c_void_p, c_void_p],
     "mbk_act_trunk": [c_void_p, c_void_p, c_void_p],
     "mbk_act_head": [c_void_p, c_void_p, c_void_p],
+    "mbk_act_set_stamps": [c_void_p],
     "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_void_p, c_void_p],
 }
@@ -215,7 +216,8 @@ class _Checked:
         # every launcher takes its hipStream_t last (c_void_p); the query / setter helpers
         # (int-returning *_parts, cu budget) do not launch and are not gated
         self._gated = {n: _gate_launch(lib, getattr(lib, n)) for n, a in _SIGS.items()
-                       if a and a[-1] is c_void_p and n != "mbk_stream_wait_zero"}
+                       if a and a[-1] is c_void_p
+                       and n not in ("mbk_stream_wait_zero", "mbk_act_set_stamps")}
 
     def __getattr__(self, name):
         if name not in _SIGS:

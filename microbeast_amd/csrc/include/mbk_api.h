@@ -63,8 +63,8 @@ typedef struct {
   void* feat;              // workspace: network.5 output [E][256] bf16
   int* bucket_cnt;         // [S], zero between steps
   int* bucket;             // [S][E]
-  uint64_t* cellx;         // [E][S] per-cell {log-prob bits, packed action} of the step
-  int* pending;            // [E] active cells not yet sampled
+  uint64_t* cellx;         // [E][S] per active cell (rank k): {log-prob, cell | action << 16}
+  int* pending;            // [2E]: active cells not yet sampled, then each env's total
   unsigned* done_ctr;      // [1], zero between steps
   int E, H, W;
 } MbkActModel;

@@ -429,7 +429,8 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
     const int gend = c * E + a.cnt[c];
     const int r = r0 + li;
     const bool valid = r < gend;
-    const int f = valid ? a.bucket[r] : a.bucket[r0];
+    const int ent = valid ? a.bucket[r] : a.bucket[r0];
+    const int f = ent & 0xFFFF, rank = ent >> 16;  // env, rank among its active cells
     unit_z(a.X, a.Wp, a.bp, f, valid, c, z);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of this wave visible
     __builtin_amdgcn_wave_barrier();
@@ -450,8 +451,10 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
 #pragma unroll
       for (int k = 0; k < kComps; ++k) a.action[fc * kComps + k] = act[k];
       const uint64_t x = (uint64_t)__float_as_uint(lp) |
-                         ((uint64_t)mbr::pack_env_action(act) << 32);
-      __hip_atomic_store(a.cellx + fc, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                         ((uint64_t)((uint32_t)c | ((uint32_t)mbr::pack_env_action(act) << 16))
+                          << 32);
+      __hip_atomic_store(a.cellx + (size_t)f * S + rank, x, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every granule drained before its signal
     bool fin = false;
@@ -463,21 +466,33 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
       const int l = __builtin_ctzll(bm);
       bm &= bm - 1;
       const int fe = __shfl(f, l, 64);
+      // the env's n granules (rank k = k-th active cell in cell order), sc1 loads only
       const uint64_t* row = a.cellx + (size_t)fe * S;
+      const int n = a.pending[E + fe];
       float s = 0.f;
       int nz = 0;  // sparse rows: entries written so far
       uint32_t* lrow = a.act_list ? a.act_list + (size_t)fe * a.list_stride : nullptr;
-      for (int cc = lane; cc < S; cc += 64) {
-        const uint64_t x = __hip_atomic_load(row + cc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s += __uint_as_float((uint32_t)x);
-        const uint32_t code = (uint32_t)(x >> 32);
+      for (int k0 = 0; k0 < n; k0 += 64) {
+        const int k = k0 + lane;
+        const uint64_t x = k < n ? __hip_atomic_load(row + k, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        const uint32_t hi = (uint32_t)(x >> 32);
+        // row_sum_pack's lane-strided sum (lane l adds cells l, l + 64, ... in order) without
+        // its +0.0 terms: walk the granules in cell order, each lane keeps its own cells
+        const int kn = min(64, n - k0);
+        for (int q = 0; q < kn; ++q) {
+          const uint32_t lo_q = (uint32_t)__shfl((int)(uint32_t)x, q, 64);
+          const uint32_t hi_q = (uint32_t)__shfl((int)hi, q, 64);
+          if ((int)(hi_q & 63u) == lane) s += __uint_as_float(lo_q);
+        }
+        const uint32_t code = hi >> 16;
         if (lrow) {  // only the non-noop cells travel back to the env
-          const uint64_t bal = __ballot(code != 0u);
+          const uint64_t bal = __ballot(k < n && code != 0u);
           const int pos = nz + __popcll(bal & ((1ull << lane) - 1ull));
-          if (code != 0u) lrow[1 + pos] = (uint32_t)cc | (code << 16);
+          if (k < n && code != 0u) lrow[1 + pos] = (hi & 0xFFFFu) | (code << 16);
           nz += __popcll(bal);
-        } else {
-          a.act16[(size_t)fe * S + cc] = (uint16_t)code;
+        } else if (k < n) {
+          a.act16[(size_t)fe * S + (hi & 0xFFFFu)] = (uint16_t)code;
         }
       }
       s = wave_sum(s);

@@ -707,19 +707,20 @@ struct ActTrunkArgs {
   uint32_t* obs2;
   uint32_t* mask2;
   uint8_t* action;
-  uint64_t* cellx;
   float* logp;
   uint16_t* act16;
-  int* pending;
+  int* pending;  // [2E]: pending active cells, then the env's active-cell total
   int* bucket_cnt;
   int* bucket;
   const float* reward_src;
   const uint8_t* done_src;
   float* reward_dst;
   uint8_t* done_dst;
+  uint64_t* stamps;  // diagnostic phase stamps (null: off)
 };
 
 constexpr int kActS = 256;  // 16x16 maps: one map row = one 16-pixel MFMA block
+constexpr int kActPre = kMaxTNI / (kThreads / 64);  // envs per wave and tile (2)
 struct ActLayout {          // byte offsets of the prologue scratch inside R2, tile of tni envs
   int codes, bits, lut, cnt, np, res, pairs, end;
 };
@@ -801,6 +802,17 @@ __device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* 
   }
 }
 
+// diagnostic phase stamps (a.stamps != null, tools/act_phases.py): wave 0 of each workgroup
+// records the 100 MHz real-time counter at the phase boundaries of its first tile; the
+// stamped run's total is not a timing (the stamps serialise nothing, but read their shares)
+#define ACT_STAMP(k)                                                                     \
+  do {                                                                                   \
+    if (a.stamps && grp == (int)blockIdx.x && threadIdx.x < 64)                          \
+      a.stamps[(size_t)blockIdx.x * 64 * kActStamps + (k) * 64 + threadIdx.x] =           \
+          __builtin_amdgcn_s_memrealtime();                                              \
+  } while (0)
+constexpr int kActStamps = 8;
+
 __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
   char* smem = trunk_smem;
   const TrunkArgs& t = a.t;
@@ -822,6 +834,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
   const int g = lane >> 4, li = lane & 15;
   const int ngroups = (E + TNI - 1) / TNI;
   uint4 wnext[kWFrag];  // layer l+1's weight fragments, fetched during layer l
+  uint32_t pre[kActPre] = {0u, 0u};  // sparse input: this lane's word of the next tile's rows
 #define ACT_PHASE(l, CI, CO, RELU, MODE, IN, H_, W_, OUT)                                  \
   do {                                                                                   \
     uint4 wc[kWFrag];                                                                    \
@@ -843,16 +856,19 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
     float bias0[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias0[i] = a.b0[4 * g + i];
+    ACT_STAMP(0);
     // ---- P1: codes / resources -> LDS, byte LUT, counters; reward / done of the last env step
     if (a.code_list) {
       // sparse rows (occupied cells only, ~3-8x fewer PCIe bytes than the dense codes): one
       // wave per env reads the count word and the first 63 entries in one access, scatters
       // them into the zeroed LDS code row, and reads further entries only if there are more
-      for (int el = wave; el < nimg; el += NW) {
+      for (int el = wave, j = 0; el < nimg; el += NW, ++j) {
         uint16_t* cs = lcodes + el * S;
         for (int c = lane * 4; c < S; c += 256) *(uint2*)(cs + c) = make_uint2(0u, 0u);
         const uint32_t* row = a.code_list + (size_t)(img0 + el) * a.list_stride;
-        const uint32_t w = lane <= S ? row[lane] : 0u;
+        // the first 64 words of the row: prefetched during the previous tile's trunk
+        const uint32_t w = grp == (int)blockIdx.x ? (lane <= S ? row[lane] : 0u)
+                         : pre[j & (kActPre - 1)];
         const uint32_t w0 = (uint32_t)__shfl((int)w, 0, 64);
         const int n = min((int)(w0 & 0xFFFFu), S);
         if (lane == 0) lres[el] = (int)(w0 >> 16);
@@ -879,6 +895,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       if (a.done_dst) a.done_dst[img0 + tid] = a.done_src[img0 + tid];
     }
     __syncthreads();
+    ACT_STAMP(1);
     // ---- P2: decode, one wave per env
     for (int el = wave; el < nimg; el += NW) {
       const int e = img0 + el;
@@ -896,10 +913,26 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
         mk[3 * j] = w3[0];
         mk[3 * j + 1] = w3[1];
         mk[3 * j + 2] = w3[2];
-        if (w3[0] | w3[1] | w3[2]) {
-          ++nact;
+        nact += (w3[0] | w3[1] | w3[2]) != 0u;
+      }
+      // each active cell's rank k among the env's active cells, in cell order (exclusive scan
+      // of the lanes' counts): the head stores the cell's result in the env's k-th granule, so
+      // the finisher reads n granules instead of a whole cell row
+      int kx = nact;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(kx, o, 64);
+        if (lane >= o) kx += y;
+      }
+      const int n = __shfl(kx, 63, 64);
+      kx -= nact;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (mk[3 * j] | mk[3 * j + 1] | mk[3 * j + 2]) {
+          const int c = c0 + j;
           const int i = atomicAdd(npairs, 1);
-          lpairs[i] = make_int2((c << 19) | atomicAdd(&lcnt[c], 1), e);
+          lpairs[i] = make_int2((c << 19) | atomicAdd(&lcnt[c], 1), e | (kx << 16));
+          ++kx;
         }
       }
       const uint4 o4 = make_uint4(ob[0], ob[1], ob[2], ob[3]);
@@ -920,29 +953,24 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
         mp2[1] = m1;
         mp2[2] = m2;
       }
-      // the env's action row and per-cell step scratch start at zero: the head overwrites the
-      // active cells, whose count is its completion counter
+      // the env's action row starts at zero (the head overwrites the active cells); n is the
+      // head's completion counter for the env and the number of its granules
       const uint4 z4 = make_uint4(0, 0, 0, 0);
       uint4* act4 = (uint4*)(a.action + (size_t)e * S * 7);
       for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = z4;
-      uint4* cx4 = (uint4*)(a.cellx + (size_t)e * S);
-      for (int i = lane; i < S / 2; i += 64) cx4[i] = z4;
-      int n = nact;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
       if (lane == 0) {
         a.pending[e] = n;
+        a.pending[E + e] = n;
         if (n == 0) a.logp[e] = 0.f;
       }
-      if (n == 0) {  // nothing to sample: all no-ops
-        if (a.act_list) {
-          if (lane == 0) a.act_list[(size_t)e * a.list_stride] = 0u;
-        } else {
-          *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
-        }
+      if (a.act_list) {  // nothing to sample: an empty action row
+        if (n == 0 && lane == 0) a.act_list[(size_t)e * a.list_stride] = 0u;
+      } else {  // dense packed actions: all cells no-op until the head writes the active ones
+        *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
       }
     }
     __syncthreads();
+    ACT_STAMP(2);
     // ---- P3: one global bucket reservation per active cell of the tile (lcnt -> its base) ...
     for (int c = tid; c < S; c += kThreads) {
       const int n = lcnt[c];
@@ -952,6 +980,15 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
     for (int im = wave; im < nimg; im += NW) act_conv0(lbits + im * S, lut, bw0, bias0, R1, im);
     // layer 1's weights: fetched once the prologue's registers are dead (earlier, they spill)
     wfetch(t.w[0], tail_cin(0), tail_cout(0), wnext);
+    if (a.code_list) {  // the next tile's sparse rows, in flight during this tile's trunk
+      const int img0n = img0 + gridDim.x * TNI;
+#pragma unroll
+      for (int j = 0; j < kActPre; ++j) {
+        const int el = wave + j * NW;
+        pre[j] = (el < TNI && img0n + el < E && lane <= S)
+                     ? a.code_list[(size_t)(img0n + el) * a.list_stride + lane] : 0u;
+      }
+    }
     __syncthreads();
     {
       const int np = *npairs;
@@ -965,6 +1002,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
     __syncthreads();  // the prologue scratch in R2 is dead from here
     zero_halo<TG<16>::PIXB>(R2, nimg, H0, W0);
     __syncthreads();
+    ACT_STAMP(3);
     // ---- stage 0 residual blocks, stages 1 and 2, network.5 + critic (trunk_tail_kernel)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
@@ -973,6 +1011,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       ACT_PHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, oR2, H0, W0, oR1);
       __syncthreads();
     }
+    ACT_STAMP(4);
     ACT_PHASE(4, 16, 32, false, OUT_STAGE, oR1, H0, W0, oR2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
@@ -986,6 +1025,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       ACT_PHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H1, W1, oR1);
       __syncthreads();
     }
+    ACT_STAMP(5);
     ACT_PHASE(9, 32, 32, false, OUT_STAGE, oR1, H1, W1, oR2);
     __syncthreads();
     pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
@@ -999,7 +1039,9 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       ACT_PHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H2, W2, oR1);
       __syncthreads();
     }
+    ACT_STAMP(6);
     trunk_fc(R1, H2, W2, nimg, img0, t, (float*)R2);  // ends with a barrier
+    ACT_STAMP(7);
   }
 #undef ACT_PHASE
 }
@@ -1176,6 +1218,13 @@ static int act_tni() {
 
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
+static uint64_t* g_act_stamps = nullptr;  // diagnostic phase stamps (tools/act_phases.py)
+// stamps: device buffer of grid x 8 x 64 uint64 (null: off); returns the stamps per workgroup
+extern "C" int mbk_act_set_stamps(void* stamps) {
+  g_act_stamps = (uint64_t*)stamps;
+  return kActStamps;
+}
+
 extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
   if (!m || !s || m->E <= 0 || m->H != 16 || m->W != 16) return (int)hipErrorInvalidValue;
   if (!m->w0 || !m->b0 || !m->w5 || !m->b5 || !m->wc || !m->bc || !m->feat || !m->cellx ||
@@ -1192,7 +1241,7 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
     return (int)hipErrorInvalidValue;
   // 16-byte vector accesses of whole rows (S = 256 cells per env)
   if ((s->codes && !al16(s->codes)) || !al16(s->obs) || !al16(s->mask) || !al16(s->action) ||
-      !al16(m->cellx) || !al16(m->w0) || !al16(m->feat) || ((uintptr_t)s->act16 & 7) ||
+      !al16(m->w0) || !al16(m->feat) || ((uintptr_t)s->act16 & 7) ||
       (s->obs2 && (!al16(s->obs2) || !al16(s->mask2))))
     return (int)hipErrorInvalidValue;
   ActTrunkArgs a{};
@@ -1230,7 +1279,6 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.obs2 = s->obs2;
   a.mask2 = s->mask2;
   a.action = s->action;
-  a.cellx = m->cellx;
   a.logp = s->logp;
   a.act16 = s->act16;
   a.pending = m->pending;
@@ -1240,6 +1288,7 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.done_src = s->done_src;
   a.reward_dst = s->reward_dst;
   a.done_dst = s->done_dst;
+  a.stamps = g_act_stamps;
   static int cus = 0;
   if (!cus) {
     int dev = 0;

@@ -255,7 +255,10 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
       throw std::runtime_error("set_act_models: model block shape mismatch");
   act_models_ = models;
   act_copy_ = copy;
-  sparse_ = !models.empty() && !copy;
+  // MBK_ACT_SPARSE=0: dense zero-copy codes / actions (4 + 4 MB of PCIe per 8192-env step
+  // instead of ~0.5-1 MB)
+  const char* sp = std::getenv("MBK_ACT_SPARSE");
+  sparse_ = !models.empty() && !copy && !(sp && sp[0] == '0');
   if (sparse_ && !h_code_list_) {
     const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
     list_stride_ = (S_ + 1 + 3) & ~3;  // word 0 + up to S entries, 16-byte rows

@@ -100,7 +100,7 @@ class ActWorkspace:
         self.head = head
         self.feat = torch.empty(E, 256, dtype=torch.bfloat16, device=device)
         self.cellx = torch.zeros(E * S, dtype=torch.int64, device=device)
-        self.pending = torch.zeros(E, dtype=torch.int32, device=device)
+        self.pending = torch.zeros(2 * E, dtype=torch.int32, device=device)  # + active totals
         self.done_ctr = torch.zeros(4, dtype=torch.int32, device=device)
         self.rng = rng
         params = encoder_params(model.network, len(model.channels))

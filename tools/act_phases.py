@@ -1,0 +1,116 @@
+#!/usr/bin/env python
+"""Where the fused acting step's time goes (ops/act.py, mbk_act_step) on one MI355X.
+
+Runs the two launches standalone on E envs of real simulator codes (sparse rows in pinned host
+memory, as the engine feeds them, or in device memory), times each launch with HIP events, then
+re-runs launch A with the diagnostic phase stamps (trunk.hip ACT_STAMP) and prints the mean
+share of each prologue / trunk phase over the workgroups' first tiles.
+
+  python tools/act_phases.py [--envs 8192] [--steps 20] [--device_rows]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PHASES = ["P1 codes->LDS", "P2 decode", "P3 buckets+conv0", "stage 0 res", "stage 1",
+          "stage 2", "fc + critic"]
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--envs", type=int, default=8192)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warm", type=int, default=30, help="env steps before sampling codes")
+    p.add_argument("--device_rows", action="store_true", help="sparse rows in HBM, not pinned")
+    a = p.parse_args()
+    from microbeast_amd import _native as N
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.act import ActWorkspace, MbkActStep
+
+    dev = torch.device("cuda", 0)
+    rt = N.runtime()
+    E, S = a.envs, 256
+    env = rt.VecEnv(16, E, 2000, 1, [0, 0, 0, 1, 2, 3])
+    obs = torch.zeros(E, S, dtype=torch.int32)
+    mask = torch.zeros(E, S, 3, dtype=torch.int32)
+    env.reset(obs.data_ptr(), mask.data_ptr())
+    zero = torch.zeros(E, S, 7, dtype=torch.uint8)
+    rew, done = torch.zeros(E), torch.zeros(E, dtype=torch.uint8)
+    for _ in range(a.warm):  # no-op agent: the bots play, units spread over the map
+        env.step(zero.data_ptr(), obs.data_ptr(), mask.data_ptr(), rew.data_ptr(), done.data_ptr())
+    stride = S + 4
+    rows = torch.zeros(E, stride, dtype=torch.int32)
+    codes = torch.zeros(E, S, dtype=torch.int16)
+    res = torch.zeros(E, dtype=torch.int32)
+    env.obs_codes(codes.data_ptr(), res.data_ptr())
+    c = codes.to(torch.int64) & 0xFFFF
+    nz = c != 0
+    cnt = nz.sum(1)
+    rows[:, 0] = (cnt | (res.to(torch.int64) << 16)).to(torch.int32)
+    cells = torch.arange(S).expand(E, S)
+    order = torch.argsort((~nz).to(torch.int8), dim=1, stable=True)  # occupied cells first
+    ent = (torch.gather(cells, 1, order) | (torch.gather(c, 1, order) << 16))
+    keep = torch.arange(S)[None, :] < cnt[:, None]
+    rows[:, 1:1 + S] = torch.where(keep, ent, 0).to(torch.int32)
+    rows = rows.to(dev) if a.device_rows else rows.pin_memory()
+    print(f"occupied cells per env: mean {cnt.float().mean():.1f} max {int(cnt.max())}; "
+          f"active (idle own units) {float((mask != 0).any(-1).float().sum(1).mean()):.2f}")
+
+    torch.manual_seed(0)
+    m = Agent((16, 16, 27))
+    torch.nn.init.normal_(m.actor.weight, std=0.05)
+    m = m.to(dev).eval()
+    m.pack_inference(dev)
+    rng = torch.tensor([1, 0], dtype=torch.int64, device=dev)
+    ws = ActWorkspace(m, E, rng, dev)
+    o = torch.empty(E, S, dtype=torch.int32, device=dev)
+    mk = torch.empty(E, S, 3, dtype=torch.int32, device=dev)
+    act = torch.empty(E, S, 7, dtype=torch.uint8, device=dev)
+    lp = torch.empty(E, device=dev)
+    v = torch.empty(E, device=dev)
+    al = torch.zeros(E, stride, dtype=torch.int32).pin_memory()
+    st = MbkActStep()
+    st.code_list, st.act_list, st.list_stride = rows.data_ptr(), al.data_ptr(), stride
+    st.obs, st.mask, st.action, st.logp, st.value = (o.data_ptr(), mk.data_ptr(), act.data_ptr(),
+                                                     lp.data_ptr(), v.data_ptr())
+    k = N.kernels()
+    args = (ctypes.addressof(ws.struct), ctypes.addressof(st))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    ta = tb = 0.0
+    for i in range(a.steps + 3):
+        ev[0].record()
+        N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk")
+        ev[1].record()
+        N.check(k.mbk_act_head(*args, N.stream_ptr()), "act_head")
+        ev[2].record()
+        torch.cuda.synchronize()
+        if i >= 3:
+            ta += ev[0].elapsed_time(ev[1])
+            tb += ev[1].elapsed_time(ev[2])
+    n = a.steps
+    print(f"launch A (decode + trunk + critic) {1e3 * ta / n:.1f} us, launch B (head + finale) "
+          f"{1e3 * tb / n:.1f} us, rows in {'HBM' if a.device_rows else 'pinned host memory'}")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    stamps = torch.zeros(ncu * 4 * 8 * 64, dtype=torch.int64, device=dev)
+    nst = k.mbk_act_set_stamps(stamps.data_ptr())
+    N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk (stamped)")
+    torch.cuda.synchronize()
+    k.mbk_act_set_stamps(None)
+    t = stamps.view(-1, nst, 64)[:, :, 0].cpu().double()
+    t = t[t[:, 0] > 0]
+    d = (t[:, 1:] - t[:, :-1]) * 10.0 / 1e3  # 100 MHz ticks -> us
+    tot = float(d.sum(1).mean())
+    print(f"first tile of {len(t)} workgroups: {tot:.1f} us")
+    for i, name in enumerate(PHASES):
+        print(f"  {name:18s} {float(d[:, i].mean()):7.2f} us  {float(d[:, i].mean()) / tot:6.1%}")
+
+
+if __name__ == "__main__":
+    main()

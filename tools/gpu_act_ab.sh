@@ -1,7 +1,10 @@
-# Fused acting step variants on the headline bench (A/B), then a kernel-trace timeline.
+# Fused acting step: GPU tests, then variants on the headline bench (A/B), then a timeline.
 set -o pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
-for v in "MBK_ACT_COPY=0" "MBK_ACT_COPY=1" "MBK_ACT_TNI=8" "MBK_ACT_TNI=8 MBK_ACT_COPY=1" "MBK_FUSED_ACT=0"; do
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_act.py > gpurun_out/act_tests.log 2>&1 || { tail -40 gpurun_out/act_tests.log; exit 1; }
+grep -E "PASS|FAIL" gpurun_out/act_tests.log | tail -6
+for v in ${AB_VARIANTS:-"MBK_ACT_SPARSE=1" "MBK_ACT_SPARSE=0" "MBK_FUSED_ACT=0"}; do
   env $v timeout -k 10 240 python -u bench.py --steps 20 --warmup 5 > gpurun_out/ab.log 2>&1 || { tail -30 gpurun_out/ab.log; exit 1; }
   echo "$v $(python -c "import json,sys; d=json.loads(open('gpurun_out/ab.log').read().strip().splitlines()[-1]); a=d['actor_stats']; l=d['learner_phase_ms_rank0']; print(round(d['value']/1e6,3), 'gpu', a['gpu_phase_ms'], 'env', a['env_phase_ms'], 'fwd', l['fwd'], 'bwd', l['bwd'])")"
 done
