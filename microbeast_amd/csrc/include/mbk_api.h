@@ -59,13 +59,14 @@ typedef struct {
   const float* bc;         // [1]
   const void* Wp;          // sparse head [S][80][256] bf16
   const float* bp;         // [S][80]
-  uint64_t* rng;           // Philox (seed, step)
+  uint64_t* rng;           // Philox (seed, step): the step is MbkActStep.step; [1] is set
+                           // to step + 1 after the step (the graph path's counter)
   void* feat;              // workspace: network.5 output [E][256] bf16
-  int* bucket_cnt;         // [S], zero between steps
+  int* bucket_cnt;         // [2][S]: step t counts in half t & 1; launch A of step t zeroes
+                           // the other half (step t-1's, read by its launch B)
   int* bucket;             // [S][E]
   uint64_t* cellx;         // [E][S] per active cell (rank k): {log-prob, cell | action << 16}
   int* pending;            // [2E]: active cells not yet sampled, then each env's total
-  unsigned* done_ctr;      // [1], zero between steps
   int E, H, W;
 } MbkActModel;
 
@@ -92,6 +93,7 @@ typedef struct {
   const uint8_t* done_src;
   float* reward_dst;
   uint8_t* done_dst;
+  uint64_t step;           // Philox step of this policy step (the lane's step count)
 } MbkActStep;
 
 int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);

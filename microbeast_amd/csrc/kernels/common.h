@@ -146,6 +146,18 @@ __device__ __forceinline__ void cell_backward(const ZPtr z, const uint32_t m[3],
   }
 }
 
+// ------------------------------------------------------------------ barriers
+// Workgroup barrier that orders LDS only: the fences are restricted to the local address space,
+// so no s_waitcnt vmcnt(0) is emitted and the waves' global stores stay in flight across it
+// (__syncthreads() drains every outstanding global access of every wave first). For phases
+// whose cross-wave hand-off is through LDS and whose global writes nobody in the workgroup
+// reads back.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // ------------------------------------------------------------------ reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -385,8 +385,9 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
 //     stored sc1 and drained before the signal, every load of it sc1) and writes the env's
 //     log-prob (row_sum_pack's lane-strided sum + wave_sum: bit-identical) and its 16-bit
 //     action codes (one coalesced 128-byte store per 64 cells, also to pinned host memory);
-//   * the workgroup whose arrival ticket comes last resets the per-cell bucket counters and
-//     advances the sampler's step counter (every other workgroup has read both by then).
+//   * the bucket counters are double-buffered by step parity (launch A of the next step zeroes
+//     this step's half) and the Philox step comes from the host, so no workgroup waits for or
+//     counts the others (a 512-way arrival ticket cost ~6 us).
 struct HeadActArgs {
   const bf16* X;
   const bf16* Wp;
@@ -402,21 +403,22 @@ struct HeadActArgs {
   int list_stride;
   float* logp;
   int* pending;
-  unsigned* done_ctr;
+  uint64_t step;  // Philox step (the host's per-lane step count)
   int S, E;
 };
 
 __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
   __shared__ float zs[4][16][NP + 1];
   __shared__ int upre[kMaxUnitCells + 1];
-  __shared__ int last_wg;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int li = lane & 15;
   const int S = a.S, E = a.E;
   unit_prefix(a.cnt, S, upre);
   __syncthreads();
   const int nunits = upre[kMaxUnitCells];
-  const uint64_t seed = a.rng[0], step = a.rng[1];
+  const uint64_t seed = a.rng[0], step = a.step;
+  // the device copy of the step counter follows the graph path's (nobody reads it in here)
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.rng[1] = step + 1;
   float (*z)[NP + 1] = zs[wave];
   for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
     int lo = 0, hi = S - 1;  // last cell whose prefix <= u
@@ -502,18 +504,6 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
       }
     }
     __builtin_amdgcn_wave_barrier();
-  }
-  __syncthreads();  // this workgroup is done with cnt and rng
-  if (threadIdx.x == 0)
-    last_wg = __hip_atomic_fetch_add(a.done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              gridDim.x - 1;
-  __syncthreads();
-  if (last_wg) {
-    for (int c = threadIdx.x; c < S; c += blockDim.x) a.cnt[c] = 0;
-    if (threadIdx.x == 0) {
-      a.rng[1] = step + 1;
-      *a.done_ctr = 0u;
-    }
   }
 }
 
@@ -1031,7 +1021,7 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
   const int S = m->H * m->W;
   if (S < 1 || S > kMaxUnitCells - 1 || (S & 3)) return (int)hipErrorInvalidValue;
   if (!m->feat || !m->Wp || !m->bp || !m->rng || !m->bucket || !m->bucket_cnt || !m->cellx ||
-      !m->pending || !m->done_ctr || !s->mask || !s->action || (!s->act16 && !s->act_list) ||
+      !m->pending || !s->mask || !s->action || (!s->act16 && !s->act_list) ||
       !s->logp)
     return (int)hipErrorInvalidValue;
   if ((uintptr_t)m->cellx & 7) return (int)hipErrorInvalidValue;
@@ -1043,14 +1033,14 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
   a.action = s->action;
   a.rng = m->rng;
   a.bucket = m->bucket;
-  a.cnt = m->bucket_cnt;
+  a.cnt = m->bucket_cnt + (s->step & 1) * S;  // this step's half (launch A filled it)
   a.cellx = m->cellx;
   a.act16 = s->act16;
   a.act_list = s->act_list;
   a.list_stride = s->list_stride;
   a.logp = s->logp;
   a.pending = m->pending;
-  a.done_ctr = m->done_ctr;
+  a.step = s->step;
   a.S = S;
   a.E = m->E;
   static int cus = 0;

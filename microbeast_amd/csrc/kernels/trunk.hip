@@ -710,7 +710,8 @@ struct ActTrunkArgs {
   float* logp;
   uint16_t* act16;
   int* pending;  // [2E]: pending active cells, then the env's active-cell total
-  int* bucket_cnt;
+  int* bucket_cnt;  // this step's half of the [2][S] counters
+  int* bucket_cnt_prev;  // the previous step's half: zeroed by workgroup 0
   int* bucket;
   const float* reward_src;
   const uint8_t* done_src;
@@ -721,6 +722,9 @@ struct ActTrunkArgs {
 
 constexpr int kActS = 256;  // 16x16 maps: one map row = one 16-pixel MFMA block
 constexpr int kActPre = kMaxTNI / (kThreads / 64);  // envs per wave and tile (2)
+// words of a sparse input row read in the first access (count + 31 entries: most envs); the
+// rest only for envs with more occupied cells
+constexpr int kActSpec = 32;
 struct ActLayout {          // byte offsets of the prologue scratch inside R2, tile of tni envs
   int codes, bits, lut, cnt, np, res, pairs, end;
 };
@@ -867,15 +871,15 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
         for (int c = lane * 4; c < S; c += 256) *(uint2*)(cs + c) = make_uint2(0u, 0u);
         const uint32_t* row = a.code_list + (size_t)(img0 + el) * a.list_stride;
         // the first 64 words of the row: prefetched during the previous tile's trunk
-        const uint32_t w = grp == (int)blockIdx.x ? (lane <= S ? row[lane] : 0u)
+        const uint32_t w = grp == (int)blockIdx.x ? (lane < kActSpec && lane <= S ? row[lane] : 0u)
                          : pre[j & (kActPre - 1)];
         const uint32_t w0 = (uint32_t)__shfl((int)w, 0, 64);
         const int n = min((int)(w0 & 0xFFFFu), S);
         if (lane == 0) lres[el] = (int)(w0 >> 16);
         __builtin_amdgcn_wave_barrier();
-        if (lane >= 1 && lane <= n && (w & 0xFFFFu) < (uint32_t)S)
+        if (lane >= 1 && lane < kActSpec && lane <= n && (w & 0xFFFFu) < (uint32_t)S)
           cs[w & 0xFFFFu] = (uint16_t)(w >> 16);
-        for (int k = 64 + lane; k <= n; k += 64) {
+        for (int k = kActSpec + lane; k <= n; k += 64) {
           const uint32_t x = row[k];
           if ((x & 0xFFFFu) < (uint32_t)S) cs[x & 0xFFFFu] = (uint16_t)(x >> 16);
         }
@@ -888,13 +892,15 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       if (tid < nimg) lres[tid] = a.res[img0 + tid];
     }
     if (tid < 256) ((uint4*)lut)[tid] = mbk::bits8_bf16((uint32_t)tid);
+    if (blockIdx.x == 0 && grp == 0)  // the previous step's launch B is done with these
+      for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
     for (int c = tid; c < S; c += kThreads) lcnt[c] = 0;
     if (tid == 0) *npairs = 0;
     if (tid < nimg) {
       if (a.reward_dst) a.reward_dst[img0 + tid] = a.reward_src[img0 + tid];
       if (a.done_dst) a.done_dst[img0 + tid] = a.done_src[img0 + tid];
     }
-    __syncthreads();
+    mbk::lds_barrier();
     ACT_STAMP(1);
     // ---- P2: decode, one wave per env
     for (int el = wave; el < nimg; el += NW) {
@@ -969,7 +975,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
         *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
       }
     }
-    __syncthreads();
+    mbk::lds_barrier();
     ACT_STAMP(2);
     // ---- P3: one global bucket reservation per active cell of the tile (lcnt -> its base) ...
     for (int c = tid; c < S; c += kThreads) {
@@ -985,11 +991,11 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
 #pragma unroll
       for (int j = 0; j < kActPre; ++j) {
         const int el = wave + j * NW;
-        pre[j] = (el < TNI && img0n + el < E && lane <= S)
+        pre[j] = (el < TNI && img0n + el < E && lane < kActSpec && lane <= S)
                      ? a.code_list[(size_t)(img0n + el) * a.list_stride + lane] : 0u;
       }
     }
-    __syncthreads();
+    mbk::lds_barrier();
     {
       const int np = *npairs;
       for (int i = tid; i < np; i += kThreads) {
@@ -999,45 +1005,45 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       }
     }
     zero_halo<TG<16>::PIXB>(R1, nimg, H0, W0);
-    __syncthreads();  // the prologue scratch in R2 is dead from here
+    mbk::lds_barrier();  // the prologue scratch in R2 is dead from here
     zero_halo<TG<16>::PIXB>(R2, nimg, H0, W0);
-    __syncthreads();
+    mbk::lds_barrier();
     ACT_STAMP(3);
     // ---- stage 0 residual blocks, stages 1 and 2, network.5 + critic (trunk_tail_kernel)
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
       ACT_PHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, oR1, H0, W0, oR2);
-      __syncthreads();
+      mbk::lds_barrier();
       ACT_PHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, oR2, H0, W0, oR1);
-      __syncthreads();
+      mbk::lds_barrier();
     }
     ACT_STAMP(4);
     ACT_PHASE(4, 16, 32, false, OUT_STAGE, oR1, H0, W0, oR2);
-    __syncthreads();
+    mbk::lds_barrier();
     pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
     zero_halo<TG<32>::PIXB>(R1, nimg, H1, W1);
-    __syncthreads();
+    mbk::lds_barrier();
     zero_halo<TG<32>::PIXB>(R2, nimg, H1, W1);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
       ACT_PHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H1, W1, oR2);
-      __syncthreads();
+      mbk::lds_barrier();
       ACT_PHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H1, W1, oR1);
-      __syncthreads();
+      mbk::lds_barrier();
     }
     ACT_STAMP(5);
     ACT_PHASE(9, 32, 32, false, OUT_STAGE, oR1, H1, W1, oR2);
-    __syncthreads();
+    mbk::lds_barrier();
     pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
     zero_halo<TG<32>::PIXB>(R1, nimg, H2, W2);
-    __syncthreads();
+    mbk::lds_barrier();
     zero_halo<TG<32>::PIXB>(R2, nimg, H2, W2);
 #pragma unroll 1
     for (int rb = 0; rb < 2; ++rb) {
       ACT_PHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H2, W2, oR2);
-      __syncthreads();
+      mbk::lds_barrier();
       ACT_PHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H2, W2, oR1);
-      __syncthreads();
+      mbk::lds_barrier();
     }
     ACT_STAMP(6);
     trunk_fc(R1, H2, W2, nimg, img0, t, (float*)R2);  // ends with a barrier
@@ -1282,7 +1288,9 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.logp = s->logp;
   a.act16 = s->act16;
   a.pending = m->pending;
-  a.bucket_cnt = m->bucket_cnt;
+  const int S = m->H * m->W;
+  a.bucket_cnt = m->bucket_cnt + (s->step & 1) * S;
+  a.bucket_cnt_prev = m->bucket_cnt + ((s->step + 1) & 1) * S;
   a.bucket = m->bucket;
   a.reward_src = s->reward_src;
   a.done_src = s->done_src;

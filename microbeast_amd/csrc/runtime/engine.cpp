@@ -537,6 +537,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       a.reward_dst = (float*)f32_at(buf_.reward, rs, ri);
       a.done_dst = (uint8_t*)u8_at(buf_.done, rs, ri);
     }
+    a.step = L.act_step++;
     if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
     {
       const auto t0 = std::chrono::steady_clock::now();

@@ -247,6 +247,7 @@ class GpuEngine {
     LaneIO io;
     int opp_version = -1;     // driver thread only
     int policy_version = 0;   // learner update of the weights landed on this lane
+    uint64_t act_step = 0;    // fused steps: Philox step of the lane's next policy step
   };
 
   EngineConfig cfg_;

@@ -35,8 +35,7 @@ class MbkActModel(ctypes.Structure):
                 ("w5", c_void_p), ("b5", c_void_p), ("wc", c_void_p), ("bc", c_void_p),
                 ("Wp", c_void_p), ("bp", c_void_p), ("rng", c_void_p), ("feat", c_void_p),
                 ("bucket_cnt", c_void_p), ("bucket", c_void_p), ("cellx", c_void_p),
-                ("pending", c_void_p), ("done_ctr", c_void_p), ("E", c_int), ("H", c_int),
-                ("W", c_int)]
+                ("pending", c_void_p), ("E", c_int), ("H", c_int), ("W", c_int)]
 
 
 class MbkActStep(ctypes.Structure):
@@ -45,7 +44,7 @@ class MbkActStep(ctypes.Structure):
                 ("action", c_void_p), ("logp", c_void_p), ("value", c_void_p),
                 ("act16", c_void_p), ("act_list", c_void_p), ("list_stride", c_int),
                 ("reward_src", c_void_p), ("done_src", c_void_p), ("reward_dst", c_void_p),
-                ("done_dst", c_void_p)]
+                ("done_dst", c_void_p), ("step", ctypes.c_uint64)]
 
 
 def code_lists(codes: torch.Tensor, res: torch.Tensor, stride: int) -> torch.Tensor:
@@ -101,7 +100,8 @@ class ActWorkspace:
         self.feat = torch.empty(E, 256, dtype=torch.bfloat16, device=device)
         self.cellx = torch.zeros(E * S, dtype=torch.int64, device=device)
         self.pending = torch.zeros(2 * E, dtype=torch.int32, device=device)  # + active totals
-        self.done_ctr = torch.zeros(4, dtype=torch.int32, device=device)
+        # per-cell bucket counters, double-buffered by step parity (mbk_api.h bucket_cnt)
+        self.bucket_cnt = torch.zeros(2 * S, dtype=torch.int32, device=device)
         self.rng = rng
         params = encoder_params(model.network, len(model.channels))
         base = enc.packed_fwd.data_ptr()
@@ -120,9 +120,8 @@ class ActWorkspace:
         m.Wp, m.bp = head.Wp.data_ptr(), head.bp.data_ptr()
         m.rng = rng.data_ptr()
         m.feat = self.feat.data_ptr()
-        m.bucket_cnt, m.bucket = head.bucket_cnt.data_ptr(), head.bucket.data_ptr()
+        m.bucket_cnt, m.bucket = self.bucket_cnt.data_ptr(), head.bucket.data_ptr()
         m.cellx, m.pending = self.cellx.data_ptr(), self.pending.data_ptr()
-        m.done_ctr = self.done_ctr.data_ptr()
         m.E, m.H, m.W = E, model.h, model.w
         self.struct = m
         self._keep = (model, params)  # the pointers above stay valid while this lives
@@ -133,12 +132,14 @@ class ActWorkspace:
 
     def step(self, codes, res, obs, mask, action, logp, value, act16, obs2=None, mask2=None,
              reward=None, done=None, reward_dst=None, done_dst=None, code_list=None,
-             act_list=None) -> None:
+             act_list=None, step: int | None = None) -> None:
         """One fused policy step on the current stream. codes int16 [E, S], res int32 [E]
         (or code_list int32 [E, stride] sparse rows, ``code_lists``); outputs obs int32 [E, S],
         mask int32 [E, S, 3], action uint8 [E, S, 7], logp / value fp32 [E], act16 int16
         [E, S] (or act_list int32 [E, stride] sparse rows); optional second obs / mask
-        destination and the reward / done copy of the previous env step."""
+        destination and the reward / done copy of the previous env step. step: the Philox
+        step (default: the device counter rng[1], one host sync; the engine counts steps per
+        lane itself)."""
         s = MbkActStep()
         s.codes, s.res = N.ptr(codes), N.ptr(res)
         s.code_list, s.act_list = N.ptr(code_list), N.ptr(act_list)
@@ -149,6 +150,7 @@ class ActWorkspace:
         s.action, s.logp, s.value = action.data_ptr(), logp.data_ptr(), value.data_ptr()
         s.act16 = N.ptr(act16)
         s.reward_src, s.done_src = N.ptr(reward), N.ptr(done)
+        s.step = int(self.rng[1]) if step is None else int(step)
         s.reward_dst, s.done_dst = N.ptr(reward_dst), N.ptr(done_dst)
         N.check(N.kernels().mbk_act_step(ctypes.addressof(self.struct), ctypes.addressof(s),
                                          N.stream_ptr()), "act_step")

@@ -85,6 +85,7 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     ta = tb = 0.0
     for i in range(a.steps + 3):
+        st.step = i  # the Philox step selects the bucket counters' half (step parity)
         ev[0].record()
         N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk")
         ev[1].record()
@@ -100,6 +101,7 @@ def main():
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     stamps = torch.zeros(ncu * 4 * 8 * 64, dtype=torch.int64, device=dev)
     nst = k.mbk_act_set_stamps(stamps.data_ptr())
+    st.step = a.steps + 3
     N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk (stamped)")
     torch.cuda.synchronize()
     k.mbk_act_set_stamps(None)
