@@ -83,6 +83,21 @@ struct ResBwdArgs {
   int N, H, W, imgs;
 };
 
+// Halo'd tile layout of the 16-channel backward kernel: byte offset of halo'd pixel (yy, xx) of
+// image im = im * imgb + yy * rowb + xx * pb. For 8-wide maps (IMPALA stage 0 at 16x16) the
+// pixels are 32 bytes in 512-byte rows: the dgrad's ds_read_b128 lane groups (16 pixels of two
+// map rows, two 16-byte channel halves) then hit 64 distinct banks, which the 48-byte stride
+// with 480-byte rows served in 3 cycles instead of 1 (profile 22: 35 % extra LDS cycles; bank
+// model in tools/lds_banks.py). The last row holds only its 10 pixels.
+struct Lay16 {
+  int pb, rowb, imgb;
+};
+__host__ __device__ inline Lay16 lay16(int H, int W) {
+  const int Hp = H + 2, Wp = W + 2;
+  if (W == 8) return {32, 512, ((Hp - 1) * 512 + Wp * 32 + 15) & ~15};
+  return {PIXB, Wp * PIXB, Hp * Wp * PIXB};
+}
+
 // WC > 0: the map width as a compile-time constant (IMPALA stage-0 shapes), so every tap
 // offset is an immediate of the LDS instruction instead of per-lane multiply-adds
 // (PMC: the runtime-width form issued ~15 VALU per MFMA); WC == 0: any width
@@ -93,7 +108,11 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int tb = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
+  // tile layout: 8-wide maps use 32-byte pixels in 512-byte rows (no bank conflicts for the
+  // dgrad ds_read_b128 or the staging writes, lay16); other widths the 48-byte pixel stride
+  const Lay16 L = lay16(H, W);
+  const int PB = L.pb, RB = L.rowb;
+  const int tb = ((a.imgs * L.imgb) + 15) & ~15;
   char* Tg = smem;            // g          (dgrad1 input, wgrad1 dY, + g of dx)
   char* Tu = smem + tb;       // relu(u)    (wgrad1 X, du mask)
   char* Tx = smem + 2 * tb;   // relu(x)    (wgrad0 X, dx mask)
@@ -126,7 +145,7 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int tap = 2 * c + (g >> 1), tapc = tap < 9 ? tap : 8;  // chunk 4's pad half
-    coff[c] = ((tapc / 3) * Wp + (tapc % 3)) * PIXB + 16 * (g & 1);
+    coff[c] = (tapc / 3) * RB + (tapc % 3) * PB + 16 * (g & 1);
   }
   float db1[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum g: this thread's 8-channel half (tid & 1)
   float db0[4] = {0, 0, 0, 0};              // sum du: channels 4g .. 4g+3 (dgrad lane map)
@@ -150,7 +169,7 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
     const int q = e & 1, p = e >> 1;
     const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
     const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB + q * 16;
+    return im * L.imgb + (y + 1) * RB + (x + 1) * PB + q * 16;
   };
   auto put = [&](int e, uint4 vx, uint4 vu, uint4 vg) {
     const int o = lds_off(e);
@@ -190,9 +209,9 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
       const int mm = valid ? m : 0;
       const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-      const int base = (im * Hp + y) * Wp + x;
+      const int base = im * L.imgb + y * RB + x * PB;  // byte offset of tap (0, 0)
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      const char* bp = Tg + base * PIXB;
+      const char* bp = Tg + base;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         Frag8 av;
@@ -200,7 +219,7 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1[c].v, av.v, acc, 0, 0, 0);
       }
       if (!valid) continue;
-      const int o = (base + Wp + 1) * PIXB + 4 * g * 2;  // interior pixel, channels 4g..
+      const int o = base + RB + PB + 4 * g * 2;  // interior pixel, channels 4g..
       const uint2 mu = *(const uint2*)(Tu + o);
       const uint32_t mw[2] = {mu.x, mu.y};
       float v[4];
@@ -224,19 +243,19 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
         const int pp = ok[h] ? p : 0;
         const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        xpos[h] = (im * Hp + y) * Wp + x;
-        dptr[h] = ok[h] ? Tg + (xpos[h] + Wp + 1) * PIXB : zero;
+        xpos[h] = im * L.imgb + y * RB + x * PB;  // byte offset of tap (0, 0)
+        dptr[h] = ok[h] ? Tg + xpos[h] + RB + PB : zero;
       }
       Frag8 af;
 #pragma unroll
       for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
       // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (A)
       // is zero, so they add exactly nothing and need no per-tap zero select
-      const char* xb0 = Tu + xpos[0] * PIXB + 8 * (li & 3);
-      const char* xb1 = Tu + xpos[1] * PIXB + 8 * (li & 3);
+      const char* xb0 = Tu + xpos[0] + 8 * (li & 3);
+      const char* xb1 = Tu + xpos[1] + 8 * (li & 3);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int off = ((t / 3) * Wp + (t % 3)) * PIXB;
+        const int off = (t / 3) * RB + (t % 3) * PB;
         Frag8 bf;
         bf.h[0] = tr_read(xb0 + off);
         bf.h[1] = tr_read(xb1 + off);
@@ -252,9 +271,9 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
       const int mm = valid ? m : 0;
       const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-      const int base = (im * Hp + y) * Wp + x;
+      const int base = im * L.imgb + y * RB + x * PB;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      const char* bp = Td + base * PIXB;
+      const char* bp = Td + base;
 #pragma unroll
       for (int c = 0; c < NCH; ++c) {
         Frag8 av;
@@ -262,7 +281,7 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0[c].v, av.v, acc, 0, 0, 0);
       }
       if (!valid) continue;
-      const int o = (base + Wp + 1) * PIXB + 4 * g * 2;
+      const int o = base + RB + PB + 4 * g * 2;
       const uint2 mx = *(const uint2*)(Tx + o), ad = *(const uint2*)(Tg + o);
       const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
       float v[4];
@@ -285,19 +304,19 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
         const int pp = ok[h] ? p : 0;
         const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        xpos[h] = (im * Hp + y) * Wp + x;
-        dptr[h] = ok[h] ? Td + (xpos[h] + Wp + 1) * PIXB : zero;
+        xpos[h] = im * L.imgb + y * RB + x * PB;  // byte offset of tap (0, 0)
+        dptr[h] = ok[h] ? Td + xpos[h] + RB + PB : zero;
       }
       Frag8 af;
 #pragma unroll
       for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
       // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (A)
       // is zero, so they add exactly nothing and need no per-tap zero select
-      const char* xb0 = Tx + xpos[0] * PIXB + 8 * (li & 3);
-      const char* xb1 = Tx + xpos[1] * PIXB + 8 * (li & 3);
+      const char* xb0 = Tx + xpos[0] + 8 * (li & 3);
+      const char* xb1 = Tx + xpos[1] + 8 * (li & 3);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
-        const int off = ((t / 3) * Wp + (t % 3)) * PIXB;
+        const int off = (t / 3) * RB + (t % 3) * PB;
         Frag8 bf;
         bf.h[0] = tr_read(xb0 + off);
         bf.h[1] = tr_read(xb1 + off);
@@ -350,7 +369,7 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
 }
 
 size_t res_smem(int imgs, int H, int W) {
-  const size_t tb = ((size_t)imgs * (H + 2) * (W + 2) * PIXB + 15) & ~(size_t)15;
+  const size_t tb = ((size_t)imgs * lay16(H, W).imgb + 15) & ~(size_t)15;
   return 4 * tb + 64;
 }
 
@@ -430,7 +449,9 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int tb = ((a.imgs * Hp * Wp * PIXB) + 15) & ~15;
+  const Lay16 L = lay16(H, W);  // res_bwd16's bank-conflict-free layout for 8-wide maps
+  const int PB = L.pb, RB = L.rowb;
+  const int tb = ((a.imgs * L.imgb) + 15) & ~15;
   char* Tx = smem;       // residual stream p -> y0 (raw)
   char* Tu = smem + tb;  // relu(u) of the current block
   for (int e = tid; e < 2 * tb / 16; e += kThreads) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
@@ -448,7 +469,7 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int tap = 2 * c + (g >> 1), tapc = tap < 9 ? tap : 8;
-    coff[c] = ((tapc / 3) * Wp + (tapc % 3)) * PIXB + 16 * (g & 1);
+    coff[c] = (tapc / 3) * RB + (tapc % 3) * PB + 16 * (g & 1);
   }
   const int per = a.imgs * HW * 2;
   const int nrounds = (a.N + a.imgs - 1) / a.imgs;
@@ -465,7 +486,7 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
     const int q = e & 1, p = e >> 1;
     const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
     const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB + q * 16;
+    return im * L.imgb + (y + 1) * RB + (x + 1) * PB + q * 16;
   };
   if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x);
   __syncthreads();
@@ -494,8 +515,8 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
         const int mm = valid ? m : 0;
         const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        const int base = (im * Hp + y) * Wp + x;
-        const char* bp = src + base * PIXB;
+        const int base = im * L.imgb + y * RB + x * PB;  // byte offset of tap (0, 0)
+        const char* bp = src + base;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
@@ -505,7 +526,7 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[l][c].v, av.v, acc, 0, 0, 0);
         }
         if (!valid) continue;
-        const int o = (base + Wp + 1) * PIXB + 4 * g * 2;
+        const int o = base + RB + PB + 4 * g * 2;
         float v[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[i] + bv[l][i];
@@ -540,7 +561,7 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
         const int mm = valid ? m : 0;
         const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        const char* bp = Tx + ((im * Hp + y) * Wp + x) * PIXB;
+        const char* bp = Tx + im * L.imgb + y * RB + x * PB;
         f32x4 acc[NB];
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -981,7 +1002,7 @@ size_t resb32_smem(int imgs, int H, int W) {
 }
 
 size_t resf_smem(int imgs, int H, int W) {
-  return 2 * (((size_t)imgs * (H + 2) * (W + 2) * PIXB + 15) & ~(size_t)15);
+  return 2 * (((size_t)imgs * lay16(H, W).imgb + 15) & ~(size_t)15);
 }
 
 }  // namespace
