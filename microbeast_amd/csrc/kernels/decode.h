@@ -58,7 +58,17 @@ __device__ __forceinline__ void cell_mask(const uint16_t* cs, int c, int H, int 
       if (r >= spec_cost(BARRACKS)) setb3(w, kSegOff[5] + (BARRACKS - 1));
     }
   }
-  if (spec_damage(t) > 0) {
+  if (spec_damage(t) > 0 && spec_range(t) == 1) {
+    // range 1 (workers, light, heavy): the 4 neighbours only, not the 7x7 scan (same bits)
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int tx = x + kDX[d], ty = y + kDY[d];
+      if (tx < 0 || ty < 0 || tx >= W || ty >= H) continue;
+      if (code_owner(cs[ty * W + tx]) == 2) {
+        setb3(w, kSegOff[6] + (kDY[d] + 3) * 7 + (kDX[d] + 3)); any_att = true;
+      }
+    }
+  } else if (spec_damage(t) > 0) {
     const int R = spec_range(t);
     for (int ay = -3; ay <= 3; ++ay)
       for (int ax = -3; ax <= 3; ++ax) {
