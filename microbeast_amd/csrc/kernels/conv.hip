@@ -624,10 +624,38 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
 
 constexpr int kPFW = 4;  // wgrad prefetch slots per thread for X and for dY
 
+// Band layout of the weight-gradient tiles (WT > 0: compile-time map width 8 or 16, H % 4
+// == 0). A tr read gives lanes 0-31 32 bytes of 4 consecutive pixels each for the lane
+// groups G = 0 and 1. In the plain layout (WT = 0) the two groups read pixels 8 apart in
+// one row, which sit on the same banks (2 LDS cycles per half-wave: the 41.7 % conflict
+// rate of profile 22). Here the 32 pixels of a K block are 4 rows x 8 columns and group G
+// takes row G, so G = 1 reads one row below G = 0; rows are padded so that one row down is
+// the other half of the 256-byte bank window: every tr read is conflict-free
+// (tools/lds_banks.py --wgrad) and every tap / channel-block offset is an immediate.
+template <int XPB, int WT>
+constexpr int wg_rbx() {  // X tile row bytes (halo'd row + pad)
+  return (WT + 2) * XPB + (XPB == 64 ? 32 : 64);
+}
+template <int DPB, int WT>
+constexpr int wg_rbd() {  // dY tile row bytes
+  return WT * DPB + (DPB == 64 ? 32 : 128);
+}
+inline size_t wg_tile_bytes(int cin, int cout, int imgs, int H, int W, int wt) {
+  if (wt == 0)
+    return ((((size_t)imgs * (H + 2) * (W + 2) * cin * 2) + 15) & ~(size_t)15) + 64 +
+           ((((size_t)imgs * H * W * cout * 2) + 15) & ~(size_t)15) + 64;
+  const int rbx = (wt + 2) * cin * 2 + (cin == 32 ? 32 : 64);
+  const int rbd = wt * cout * 2 + (cout == 32 ? 32 : 128);
+  return (size_t)imgs * (H + 2) * rbx + 64 + (size_t)imgs * H * rbd + 64;
+}
+// the band-layout instantiation for this shape (0: the plain layout)
+inline int wg_band_w(int H, int W) { return (W == 16 || W == 8) && H % 4 == 0 ? W : 0; }
+
 // Persistent over image rounds (grid = occupancy-sized, one partial per workgroup).
-// Both GEMM operands come from plain NHWC LDS tiles through ds_read_b64_tr_b16; the
-// next round's X interior and dY are prefetched into registers during the MFMAs.
-template <int CIN, int COUT, bool BITS, bool UNPOOL = false>
+// Both GEMM operands come from NHWC LDS tiles through ds_read_b64_tr_b16 (band layout
+// above when WT > 0); the next round's X interior and dY are prefetched into registers
+// during the MFMAs.
+template <int CIN, int COUT, bool BITS, bool UNPOOL = false, int WT = 0>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int XPB = CIN * 2;       // X tile pixel stride (bytes), NHWC bf16
@@ -638,16 +666,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int KTOT = 9 * CIN;
   constexpr int XEPP = BITS ? 1 : CIN / 8;  // X staging elements per pixel (u32 / uint4)
   constexpr int DCH = COUT / 8;             // dY uint4 per pixel
-  const int H = a.H, W = a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  constexpr bool band = WT > 0;
+  constexpr int RBX = wg_rbx<XPB, WT>(), RBD = wg_rbd<DPB, WT>();
+  const int H = a.H, W = band ? WT : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = (lane >> 4), li = lane & 15;
+  const int IMGX = Hp * RBX, IMGD = H * RBD;  // band layout image strides
   // LDS carve: [X tile | zero row (64B) | dY tile | zero row]; reused for the final reduce
-  const int xbytes = ((a.imgs * Hp * Wp * XPB) + 15) & ~15;
+  const int xbytes = band ? a.imgs * IMGX : ((a.imgs * Hp * Wp * XPB) + 15) & ~15;
   char* xt = smem;
   char* xzero = smem + xbytes;
   char* dt = xzero + 64;
-  const int dbytes = ((a.imgs * HW * DPB) + 15) & ~15;
+  const int dbytes = band ? a.imgs * IMGD : ((a.imgs * HW * DPB) + 15) & ~15;
   char* dzero = dt + dbytes;
   float* red = (float*)smem;  // [COUT][KTOT] after the loop
   // pool-fused: the round's pooled grads (bf16) and argmax bytes, dense [img][Ho][Wo][C]
@@ -655,9 +686,13 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
   char* sP = dzero + 64;
   char* sI = sP + (((a.imgs * Ho * Wo * COUT * 2) + 15) & ~15);
+  // bit-plane staging: byte -> 8 bf16 lookup table (4 KB) after the tiles
+  uint4* lut = (uint4*)(unpool ? sI + (((a.imgs * Ho * Wo * COUT) + 15) & ~15) : dzero + 64);
 
   for (int e = tid; e < (xbytes + 64) / 16; e += kThreads) ((uint4*)xt)[e] = make_uint4(0, 0, 0, 0);
   for (int e = tid; e < 4; e += kThreads) ((uint4*)dzero)[e] = make_uint4(0, 0, 0, 0);
+  if constexpr (BITS)
+    for (int e = tid; e < 256; e += kThreads) lut[e] = expand_bits8((uint32_t)e);
   const int xper = a.imgs * HW * XEPP, dper = a.imgs * HW * DCH;
   const int pper = a.imgs * Ho * Wo * DCH;  // pooled 8-channel chunks per round
   int xoff[kPFW];
@@ -668,7 +703,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
     if (e < xper) {
       const int q = e % XEPP, p = e / XEPP;
       const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
-      o = ((im * Hp + y + 1) * Wp + x + 1) * XPB + q * 16;
+      o = band ? im * IMGX + (y + 1) * RBX + (x + 1) * XPB + q * 16
+               : ((im * Hp + y + 1) * Wp + x + 1) * XPB + q * 16;
     }
     xoff[k] = o;
   }
@@ -677,13 +713,25 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < NBLK; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // bias grad: each thread always stages the same 8-channel group of dY (256 % DCH == 0)
-  float dbias[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // bias grad = dY^T . ones: one more MFMA per K block against a constant all-ones fragment
+  // (every column of accb holds the channel sums) instead of VALU adds in the staging
+  f32x4 accb[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) accb[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag8 ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
 
-  uint4 px[kPFW], pd[kPFW];
-  uint2 pi[kPFW];
-  uint32_t pb[kPFW];
-  auto prefetch = [&](int rd) {
+  // two register prefetch buffers: round rd + 2 * grid loads while round rd computes, so
+  // twice the bytes are in flight (the tile loads are HBM-latency bound at one round ahead)
+  struct PF {
+    uint4 px[kPFW], pd[kPFW];
+    uint2 pi[kPFW];
+    uint32_t pb[kPFW];
+  };
+  PF pf0, pf1;
+  auto prefetch = [&](int rd, PF& f) {
+    uint4 (&px)[kPFW] = f.px; uint4 (&pd)[kPFW] = f.pd;
+    uint2 (&pi)[kPFW] = f.pi; uint32_t (&pb)[kPFW] = f.pb;
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
     const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH, pl = nimg * Ho * Wo * DCH;
     const size_t xb = (size_t)rd * xper, db = (size_t)rd * dper, pbase = (size_t)rd * pper;
@@ -708,28 +756,37 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
     *(uint4*)(xt + off) = v;
   };
   auto put_bits = [&](int off, uint32_t bits) {  // one pixel's 32 planes -> 4 x uint4
+    // lanes (consecutive pixels, 64 B apart) rotate their chunk order so that each 8-lane
+    // store group covers 8 distinct 16-byte slots of the 128-byte store bank window
+    const int rot = band ? (lane >> 1) & 3 : 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) *(uint4*)(xt + off + q * 16) = expand_bits8(bits >> (8 * q));
-  };
-  auto put_d = [&](int e, uint4 v) {
-    *(uint4*)(dt + e * 16) = v;
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      dbias[2 * j] += __uint_as_float(w[j] << 16);
-      dbias[2 * j + 1] += __uint_as_float(w[j] & 0xFFFF0000u);
+    for (int i = 0; i < 4; ++i) {
+      const int q = (i + rot) & 3;
+      *(uint4*)(xt + off + q * 16) = lut[(bits >> (8 * q)) & 255u];
     }
   };
+  auto doff_of = [&](int e) {  // dY tile byte offset of staging chunk e
+    if constexpr (!band) return e * 16;
+    const int q = e % DCH, p = e / DCH;
+    const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+    return im * IMGD + y * RBD + x * DPB + q * 16;
+  };
+  auto put_d = [&](int e, uint4 v) { *(uint4*)(dt + doff_of(e)) = v; };
   auto xoff_of = [&](int e) {
     const int q = e % XEPP, p = e / XEPP;
     const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
+    if constexpr (band) return im * IMGX + (y + 1) * RBX + (x + 1) * XPB + q * 16;
     return ((im * Hp + y + 1) * Wp + x + 1) * XPB + q * 16;
   };
 
   const int nrounds = (a.N + a.imgs - 1) / a.imgs;
-  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x);
+  const int gstep = gridDim.x;
+  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x, pf0);
+  if ((int)blockIdx.x + gstep < nrounds) prefetch(blockIdx.x + gstep, pf1);
   __syncthreads();  // zero halo / zero rows visible
-  for (int rd = blockIdx.x; rd < nrounds; rd += gridDim.x) {
+  auto round = [&](int rd, PF& f) {
+    uint4 (&px)[kPFW] = f.px; uint4 (&pd)[kPFW] = f.pd;
+    uint2 (&pi)[kPFW] = f.pi; uint32_t (&pb)[kPFW] = f.pb;
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
     const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH, pl = nimg * Ho * Wo * DCH;
 #pragma unroll
@@ -769,52 +826,95 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
     }
     __syncthreads();
-    if (rd + (int)gridDim.x < nrounds) prefetch(rd + gridDim.x);
+    if (rd + 2 * gstep < nrounds) prefetch(rd + 2 * gstep, f);
 
-    const int M = nimg * HW;
-    const int nk = (M + 31) >> 5;
-    for (int kb = wave; kb < nk; kb += kThreads / 64) {
-      // this lane's two pixels (rows q = li>>2 of halves h = 0, 1)
-      const char* dptr[2];
-      int xpos[2];
-      bool ok[2];
+    if constexpr (band) {
+      // K block kb = (image, 4-row band, 8-column chunk); lane group G takes row G of the
+      // band, h the column half, li >> 2 the column: every pixel of the block is real
+      constexpr int CPR = WT / 8;
+      const int bpi = (H >> 2) * CPR;
+      const int nk = nimg * bpi;
+      for (int kb = wave; kb < nk; kb += kThreads / 64) {
+        const int im = kb / bpi, rem = kb - im * bpi;
+        const int y = (rem / CPR) * 4 + G, x0 = (rem % CPR) * 8 + (li >> 2);
+        const char* db = dt + im * IMGD + y * RBD + x0 * DPB + 8 * (li & 3);
+        const char* xb = xt + im * IMGX + y * RBX + x0 * XPB + 8 * (li & 3);
+        Frag8 af[MB];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int p = kb * 32 + 8 * G + 4 * h + (li >> 2);
-        ok[h] = p < M;
-        const int pp = ok[h] ? p : 0;
-        // float-reciprocal index math (exact here, see conv_fwd_kernel)
-        const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
-        const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        xpos[h] = (im * Hp + y) * Wp + x;
-        dptr[h] = ok[h] ? dt + pp * DPB : dzero;
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) af[mb].h[h] = tr_read(db + h * 4 * DPB + mb * 32);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          accb[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, ones.v, accb[mb], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            Frag8 bf;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              bf.h[h] = tr_read(xb + (t / 3) * RBX + (t % 3 + 4 * h) * XPB + cb * 32);
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+              acc[mb][t * CB + cb] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bf.v, acc[mb][t * CB + cb], 0, 0, 0);
+          }
+        }
       }
-      Frag8 af[MB];
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          af[mb].h[h] = tr_read(dptr[h] + (mb * 16 + 4 * (li & 3)) * 2);
-      // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (the A
-      // operand, dzero) is zero, so they add exactly nothing and need no per-tap zero select
-      const char* xb0 = xt + xpos[0] * XPB + 8 * (li & 3);
-      const char* xb1 = xt + xpos[1] * XPB + 8 * (li & 3);
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int off = ((t / 3) * Wp + (t % 3)) * XPB;
-#pragma unroll
-        for (int cb = 0; cb < CB; ++cb) {
-          Frag8 bf;
-          bf.h[0] = tr_read(xb0 + off + cb * 32);
-          bf.h[1] = tr_read(xb1 + off + cb * 32);
-#pragma unroll
-          for (int mb = 0; mb < MB; ++mb)
-            acc[mb][t * CB + cb] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bf.v, acc[mb][t * CB + cb], 0, 0, 0);
+    } else {
+      const int M = nimg * HW;
+      const int nk = (M + 31) >> 5;
+      for (int kb = wave; kb < nk; kb += kThreads / 64) {
+        // this lane's two pixels (rows q = li>>2 of halves h = 0, 1)
+        const char* dptr[2];
+        int xpos[2];
+        bool ok[2];
+  #pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int p = kb * 32 + 8 * G + 4 * h + (li >> 2);
+          ok[h] = p < M;
+          const int pp = ok[h] ? p : 0;
+          // float-reciprocal index math (exact here, see conv_fwd_kernel)
+          const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
+          const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+          xpos[h] = (im * Hp + y) * Wp + x;
+          dptr[h] = ok[h] ? dt + pp * DPB : dzero;
+        }
+        Frag8 af[MB];
+  #pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+  #pragma unroll
+          for (int h = 0; h < 2; ++h)
+            af[mb].h[h] = tr_read(dptr[h] + (mb * 16 + 4 * (li & 3)) * 2);
+  #pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          accb[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, ones.v, accb[mb], 0, 0, 0);
+        // X taps: out-of-range pixels read pixel 0's (finite) values; their dY column (the A
+        // operand, dzero) is zero, so they add exactly nothing and need no per-tap zero select
+        const char* xb0 = xt + xpos[0] * XPB + 8 * (li & 3);
+        const char* xb1 = xt + xpos[1] * XPB + 8 * (li & 3);
+  #pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const int off = ((t / 3) * Wp + (t % 3)) * XPB;
+  #pragma unroll
+          for (int cb = 0; cb < CB; ++cb) {
+            Frag8 bf;
+            bf.h[0] = tr_read(xb0 + off + cb * 32);
+            bf.h[1] = tr_read(xb1 + off + cb * 32);
+  #pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+              acc[mb][t * CB + cb] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bf.v, acc[mb][t * CB + cb], 0, 0, 0);
+          }
         }
       }
     }
     __syncthreads();  // tile reads done before the next round is staged
+  };
+  for (int rd = blockIdx.x; rd < nrounds; rd += 2 * gstep) {
+    round(rd, pf0);
+    if (rd + gstep < nrounds) round(rd + gstep, pf1);
   }
   // ---- reduce the 4 waves through LDS (sequential adds, no atomics)
   for (int w = 0; w < kThreads / 64; ++w) {
@@ -835,16 +935,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   }
   float* out = a.partial + (size_t)blockIdx.x * (COUT * KTOT + COUT);
   for (int e = tid; e < COUT * KTOT / 4; e += kThreads) ((float4*)out)[e] = ((const float4*)red)[e];
-  // bias grad: thread tid staged channel group (tid % DCH) in every pass
+  // bias grad: column 0 of each wave's accb (C layout: lane li = 0 holds rows 4G + i)
   __syncthreads();
-  float* bred = red;  // reuse: [kThreads][8]
+  float* bred = red;  // reuse: [4 waves][COUT]
+  if (li == 0) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) bred[tid * 8 + j] = dbias[j];
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bred[wave * COUT + mb * 16 + 4 * G + i] = accb[mb][i];
+  }
   __syncthreads();
   if (tid < COUT) {
-    const int grp = tid / 8, j = tid % 8;
     float s = 0.f;
-    for (int t = grp; t < kThreads; t += DCH) s += bred[t * 8 + j];
+    for (int w = 0; w < kThreads / 64; ++w) s += bred[w * COUT + tid];
     out[COUT * KTOT + tid] = s;
   }
 }
@@ -1111,15 +1214,13 @@ inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, boo
 }
 
 inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool = false) {
-  size_t x = (((size_t)imgs * (H + 2) * (W + 2) * cin * 2) + 15) & ~(size_t)15;
-  size_t d = (((size_t)imgs * H * W * cout * 2) + 15) & ~(size_t)15;
-  size_t t = x + 64 + d + 64;
+  size_t t = wg_tile_bytes(cin, cout, imgs, H, W, unpool ? 0 : wg_band_w(H, W));
   if (unpool) {
     const size_t pp = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * cout;
     t += ((pp * 2 + 15) & ~(size_t)15) + ((pp + 15) & ~(size_t)15);
   }
+  t += 4096;  // bit-plane lookup table (allocated for every variant: keeps the sizing simple)
   size_t red = (size_t)cout * 9 * cin * 4;
-  if (red < (size_t)kThreads * 8 * 4) red = (size_t)kThreads * 8 * 4;
   return t > red ? t : red;
 }
 
@@ -1271,6 +1372,18 @@ extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, c
   else if (cin == 32 && cout == 32) LAUNCH(32, 32, false);                                  \
   else return -(int)hipErrorInvalidValue;
 
+// the wgrad instantiation of (CI, CO, B) for this map width: band layout (WT = 8 / 16) or
+// the plain one (pool-fused mode always plain)
+template <int CI, int CO, bool B>
+const void* wgrad_kfn(int H, int W, bool unpool) {
+  if (unpool) return (const void*)conv_wgrad_kernel<CI, CO, B, true>;
+  switch (wg_band_w(H, W)) {
+    case 16: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 16>;
+    case 8: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 8>;
+    default: return (const void*)conv_wgrad_kernel<CI, CO, B>;
+  }
+}
+
 // number of partial rows mbk_conv_wgrad will write for this shape (<= nrounds)
 extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
                                     int imgs, int unpool) {
@@ -1278,9 +1391,7 @@ extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H
   if (sm > 160 * 1024 || !index_math_ok(imgs, H, W)) return -(int)hipErrorInvalidValue;
   const int nrounds = (N + imgs - 1) / imgs;
   int res = 1;
-#define Q(CI, CO, B)                                                                  \
-  res = resident_blocks(unpool ? (const void*)conv_wgrad_kernel<CI, CO, B, true>       \
-                               : (const void*)conv_wgrad_kernel<CI, CO, B>, sm)
+#define Q(CI, CO, B) res = resident_blocks(wgrad_kfn<CI, CO, B>(H, W, unpool != 0), sm)
   WGRAD_DISPATCH(Q)
 #undef Q
   static const int mult = [] {  // see fwd_grid: more, shorter-lived workgroups (+ partials)
@@ -1303,10 +1414,11 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
-    auto kfn = dy ? conv_wgrad_kernel<CI, CO, B> : conv_wgrad_kernel<CI, CO, B, true>;      \
-    if (sm > 64 * 1024) hipFuncSetAttribute((const void*)kfn,                               \
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm); \
-    hipLaunchKernelGGL(kfn, grid, dim3(kThreads), sm, stream, a);                           \
+    const void* kfn = wgrad_kfn<CI, CO, B>(H, W, dy == nullptr);                            \
+    if (sm > 64 * 1024)                                                                     \
+      hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
+    void* args[] = {&a};                                                                    \
+    hipLaunchKernel(kfn, grid, dim3(kThreads), args, sm, stream);                           \
   } while (0)
   if (in_bits) {
     if (cout == 16) LAUNCH(32, 16, true);
