@@ -18,12 +18,15 @@
 //   head_fwd   : one wave per 16-pair unit: Z[16x80] = X[f rows] . W_c^T + b_c on
 //                v_mfma_f32_16x16x32_bf16 (W_c = that cell's 78 rows, padded to 80),
 //                then sample (Philox, inverse CDF) or score per row.
-//   head_bwd   : one workgroup per cell: recompute Z, dZ in the epilogue, then
-//                dX_pair = dZ . W_c (MFMA) and dW_c += dZ^T . X accumulated in
-//                registers over all the cell's pairs (both operands via
-//                ds_read_b64_tr_b16 from LDS tiles) -> written straight into the
-//                actor.weight/bias gradient rows of that cell (deterministic).
-//   head_dx_gather : dX[f] = sum of dX_pair over f's active cells (no atomics).
+//   head_bwd2  : one workgroup per CU over 512-pair chunks of a cell, 128-pair tiles: recompute
+//                Z, the masked-softmax backward from the MFMA C layout, dX_pair = dZ . W_c
+//                (bf16 pair rows) and dW_c += dZ^T . X in registers over the chunk (both
+//                operands via ds_read_b64_tr_b16); per-chunk partials reduced in a fixed
+//                order per cell by head_dw_reduce (deterministic).
+//   head_dx_gather : dX[f] = sum of dX_pair (bf16 rows) over f's active cells (no atomics).
+#include <cstdio>
+#include <vector>
+
 #include "../include/mbk_api.h"
 #include "../include/microrts_rules.h"
 #include "common.h"
@@ -549,183 +552,456 @@ __global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __rest
 }
 
 // ------------------------------------------------------------------ backward
-// One workgroup (4 waves) per 512-pair chunk of a cell; 64-pair tiles.
-// LDS: X tile [64][256] bf16 | dZ tile [64][96] bf16 | z [64][81] f32 (65 KB: two
-// workgroups per CU, so one's gather / scalar softmax-backward phase overlaps the other's
-// MFMA phases -- at one per CU (W_c staged in LDS too, 105 KB) the kernel was 80 % waits).
-// W_c (40 KB) is read through L2 like W_c^T in the dX GEMM.
-constexpr int BW_TM = 64;
-constexpr int LDS_WC = 0;
-constexpr int LDS_XT = BW_TM * KD * 2;
-constexpr int LDS_DZ = BW_TM * NPT * 2;
-constexpr int LDS_Z = BW_TM * (NP + 1) * 4;
+// ------------------------------------------------------------------ backward, v2
+// head_bwd2: 8 waves, 128-pair tiles, everything a tile needs in LDS:
+//   W_c  [96 rows][544 B]  the cell's 78 (+2 zero, +16 zero) logit rows, staged once per chunk
+//   X    [128][544 B]      the tile's gathered feature rows (next tile prefetched in registers)
+//   dZ   [128][288 B]      bf16 logit gradients
+// Z = X W_c^T + b on MFMA, then the masked-softmax backward straight from the MFMA C layout
+// (a row's 80 logits sit in the 16 lanes of one lane group, 5 registers: per-segment max /
+// sum / sum z*e are 16-lane DPP reductions; segments with no valid logit anywhere in the
+// wave are skipped), dX = dZ W_c (B operand = W_c through ds_read_b64_tr_b16), dW_c += dZ^T X.
+// Rows are stored at phi(r) (4-row blocks 1 and 2 of each 16 swapped) with a row stride of
+// 32 mod 256 bytes: the tr reads (rows r..r+3 and r+8..r+11 per half-wave) and the b128
+// row reads are then bank-conflict-free. The old kernel (one 64-row workgroup, W_c read from
+// L2 by every wave, a 64-thread scalar softmax backward) spent ~88 % of its wave cycles
+// waiting (profile 27).
+constexpr int HB_NW = 8;
+constexpr int HB_TM = 16 * HB_NW;
+constexpr int HB_RX = 544, HB_RW = 544, HB_RZ = 288;
+constexpr int HB_LW = 0, HB_LX = 96 * HB_RW, HB_LZ = HB_LX + HB_TM * HB_RX;
+constexpr int HB_LB = HB_LZ + HB_TM * HB_RZ;           // bias-grad reduce [8 waves][80] f32
+constexpr int HB_LDS = HB_LB + HB_NW * NP * 4;
 
-__global__ __launch_bounds__(256, 2) void head_bwd_kernel(
-    const bf16* __restrict__ X, const bf16* __restrict__ Wp, const bf16* __restrict__ WpT,
-    const float* __restrict__ bp, const uint32_t* __restrict__ mask,
-    const uint8_t* __restrict__ action, const int* __restrict__ pairs,
-    const int* __restrict__ grp_start, const int* __restrict__ grp_count,
-    const int* __restrict__ chunk_cell, const int* __restrict__ chunk_row,
-    const int* __restrict__ totals, const float* __restrict__ g_logp,
-    const float* __restrict__ g_ent, int S, float* __restrict__ dXp,
-    float* __restrict__ dWp /* [nchunks][78][256] */, float* __restrict__ dbp /* [nchunks][78] */) {
+__device__ __forceinline__ int hb_phi(int r) {
+  const int b = (r >> 2) & 3;
+  return (b == 1 || b == 2) ? r ^ 12 : r;
+}
+// (bound_ctrl set: these patterns never leave the row, and it lets the compiler fold the move
+// into the consuming add / max as a DPP operand)
+template <int CTRL>
+__device__ __forceinline__ float hb_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+// reductions over the 16 lanes of a DPP row (quad swaps, half-row mirror, row mirror) of N
+// independent values, interleaved step by step (no DPP read right after its VALU write)
+constexpr int kHbDpp[4] = {0xB1, 0x4E, 0x141, 0x140};
+template <int N>
+__device__ __forceinline__ void hb_max16(float (&v)[N]) {
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const float o = st == 0 ? hb_dpp<0xB1>(v[j]) : st == 1 ? hb_dpp<0x4E>(v[j])
+                    : st == 2 ? hb_dpp<0x141>(v[j]) : hb_dpp<0x140>(v[j]);
+      v[j] = fmaxf(v[j], o);
+    }
+}
+template <int N>
+__device__ __forceinline__ void hb_sum16(float (&v)[N]) {
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      const float o = st == 0 ? hb_dpp<0xB1>(v[j]) : st == 1 ? hb_dpp<0x4E>(v[j])
+                    : st == 2 ? hb_dpp<0x141>(v[j]) : hb_dpp<0x140>(v[j]);
+      v[j] += o;
+    }
+}
+
+__global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
+    const bf16* __restrict__ X, const bf16* __restrict__ Wp, const float* __restrict__ bp,
+    const uint32_t* __restrict__ mask, const uint8_t* __restrict__ action,
+    const int* __restrict__ pairs, const int* __restrict__ grp_start,
+    const int* __restrict__ grp_count, const int* __restrict__ chunk_cell,
+    const int* __restrict__ chunk_row, const int* __restrict__ totals,
+    const float* __restrict__ g_logp, const float* __restrict__ g_ent, int S,
+    bf16* __restrict__ dXp, float* __restrict__ dWp, float* __restrict__ dbp,
+    uint64_t* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* wc_l = smem;
-  char* xt = wc_l + LDS_WC;
-  char* dzt = xt + LDS_XT;
-  float* zb = (float*)(dzt + LDS_DZ);
+  char* wl = smem + HB_LW;
+  int nst = 0;  // diagnostic phase stamps (MBK_HB_STAMPS): thread 0, first 8 tiles
+#define HB_STAMP(k)                                                                        \
+  do {                                                                                     \
+    if (stamps && threadIdx.x == 0 && nst < 8)                                             \
+      stamps[((size_t)blockIdx.x * 8 + nst) * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  char* xl = smem + HB_LX;
+  char* zl = smem + HB_LZ;
+  float* bl = (float*)(smem + HB_LB);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = lane >> 4, li = lane & 15;
   const int nchunks = totals[2];
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-  const int c = chunk_cell[ch];
-  const int g0 = chunk_row[ch];
-  const int gn = min(CHUNK, grp_start[c] + grp_count[c] - g0);
-  __syncthreads();  // previous chunk's LDS reads done
+  if ((int)blockIdx.x >= nchunks) return;
+  // W rows 80..95 stay zero (the dX GEMM's K runs to 96)
+  for (int e = tid; e < 16 * HB_RW / 16; e += 64 * HB_NW)
+    ((uint4*)(wl + 80 * HB_RW))[e] = make_uint4(0, 0, 0, 0);
 
-  const bf16* wcg = Wp + (size_t)c * NP * KD;  // W_c rows [80][256] (L2)
-  f32x4 accw[5][4];  // dW_c rows 16mb.., cols 64*wave + 16nb..
+  // this lane's logit column per MFMA block: segment index and position inside it
+  int sk[5], so[5];
 #pragma unroll
-  for (int mb = 0; mb < 5; ++mb)
+  for (int nb = 0; nb < 5; ++nb) {
+    const int col = nb * 16 + li;
+    int k = 0;
 #pragma unroll
-    for (int nb = 0; nb < 4; ++nb) accw[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float dbias = 0.f;  // thread tid < 78 owns logit column tid
+    for (int q = 1; q < kComps; ++q) k += col >= seg_off(q) ? 1 : 0;
+    sk[nb] = col < kCell ? k : kComps;
+    so[nb] = col - seg_off(k);
+  }
 
-  for (int t0 = 0; t0 < gn; t0 += BW_TM) {
-    const int nr = min(BW_TM, gn - t0);
-    __syncthreads();  // previous tile fully consumed
-    // stage X rows of this tile (zero rows past the group end)
-    for (int e = tid; e < BW_TM * KD / 8; e += 256) {
-      const int row = e / (KD / 8), q = e % (KD / 8);
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (row < nr) v = ((const uint4*)(X + (size_t)pairs[g0 + t0 + row] * KD))[q];
-      ((uint4*)xt)[e] = v;
+  // staging map: thread -> 16-byte chunk q of rows r0 + 16 k
+  const int sq = tid & 31, sr0 = tid >> 5;
+  uint4 xr[8];
+  // tile cursor: chunk ch (cell c, first row g0, n rows), tile offset t0; ch >= nchunks = end
+  struct Cur {
+    int ch, t0, c, g0, n;
+  };
+  auto chunk_cur = [&](int ch) {
+    Cur u{ch, 0, 0, 0, 0};
+    if (ch < nchunks) {
+      u.c = chunk_cell[ch];
+      u.g0 = chunk_row[ch];
+      u.n = min(CHUNK, grp_start[u.c] + grp_count[u.c] - u.g0);
     }
-    __syncthreads();
-    // ---- Z = X . Wc^T + b (wave w: rows 16w..16w+15)
-    {
-      f32x4 acc[5];
+    return u;
+  };
+  auto advance = [&](const Cur& u) {
+    if (u.ch >= nchunks) return u;
+    if (u.t0 + HB_TM < u.n) return Cur{u.ch, u.t0 + HB_TM, u.c, u.g0, u.n};
+    return chunk_cur(u.ch + (int)gridDim.x);
+  };
+  // Per-row metadata (mask words, the aligned action words, g_logp, g_ent, frame) goes through
+  // the dZ tile's row padding (bytes 192..227 of each 288-byte row): threads 0..383 each load
+  // one third of one row's 9 words for the NEXT tile (3 loads instead of 32 per wave) and write
+  // them at the tile start; the epilogue reads its rows' 36 bytes back as broadcasts.
+  // fx / fr: frames of the rows this thread stages / loads metadata for, two tiles ahead.
+  const int mrow = tid / 3, mpart = tid - 3 * (tid / 3);
+  int fx[8], fr = -1;
+  uint32_t mt[3] = {0u, 0u, 0u};
+  auto load_fx = [&](const Cur& u) {
+    const int nr = u.ch < nchunks ? min(HB_TM, u.n - u.t0) : 0;
 #pragma unroll
-      for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 2  // bounded: every W_c fragment of an unrolled K loop would be in flight
-      for (int ks = 0; ks < KD / 32; ++ks) {
-        Frag8 a;
-        a.u = *(const uint4*)(xt + ((16 * wave + li) * KD + ks * 32 + 8 * G) * 2);
+    for (int k = 0; k < 8; ++k) fx[k] = sr0 + 16 * k < nr ? pairs[u.g0 + u.t0 + sr0 + 16 * k] : -1;
+    fr = tid < 3 * HB_TM && mrow < nr ? pairs[u.g0 + u.t0 + mrow] : -1;
+  };
+  auto load_meta = [&](int c) {  // this thread's third of row mrow's metadata (frame fr, cell c)
+    mt[0] = mt[1] = mt[2] = 0u;
+    if (fr < 0) {
+      if (mpart == 2) mt[2] = 0xFFFFFFFFu;  // frame -1: padding row
+      return;
+    }
+    const size_t fc = (size_t)fr * S + c;
+    if (mpart == 0) {
+      mt[0] = mask[fc * 3]; mt[1] = mask[fc * 3 + 1]; mt[2] = mask[fc * 3 + 2];
+    } else if (mpart == 1) {
+      // only words holding one of the row's 7 action bytes (never past the buffer's end)
+      const size_t ab0 = fc * kComps;
+      const uint32_t* aw4 = (const uint32_t*)(action + (ab0 & ~(size_t)3));
+      mt[0] = aw4[0]; mt[1] = aw4[1]; mt[2] = (ab0 & 3) >= 2 ? aw4[2] : 0u;
+    } else {
+      mt[0] = __float_as_uint(g_logp[fr]);
+      mt[1] = g_ent ? __float_as_uint(g_ent[fr]) : 0u;
+      mt[2] = (uint32_t)fr;
+    }
+  };
+  auto store_meta = [&]() {
+    if (tid < 3 * HB_TM) {
+      uint32_t* d = (uint32_t*)(zl + hb_phi(mrow) * HB_RZ + 192 + mpart * 12);
+      d[0] = mt[0]; d[1] = mt[1]; d[2] = mt[2];
+    }
+  };
+  auto load_x = [&]() {  // the rows of fx into registers
 #pragma unroll
-        for (int nb = 0; nb < 5; ++nb) {
-          Frag8 b;
-          b.u = *(const uint4*)(wcg + (nb * 16 + li) * KD + ks * 32 + 8 * G);
-          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
-        }
-      }
+    for (int k = 0; k < 8; ++k)
+      xr[k] = fx[k] >= 0 ? ((const uint4*)(X + (size_t)fx[k] * KD))[sq] : make_uint4(0, 0, 0, 0);
+  };
+  auto store_x = [&]() {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *(uint4*)(xl + hb_phi(sr0 + 16 * k) * HB_RX + sq * 16) = xr[k];
+  };
+  auto stage_w = [&](int c) {  // rows 0..79 of W_c
+    const uint4* src = (const uint4*)(Wp + (size_t)c * NP * KD);
+    uint4 v[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = src[(sr0 + 16 * k) * (KD / 8) + sq];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) *(uint4*)(wl + hb_phi(sr0 + 16 * k) * HB_RW + sq * 16) = v[k];
+  };
+
+  Cur cur = chunk_cur(blockIdx.x);
+  Cur nx1 = advance(cur);
+  load_fx(cur);
+  load_x();           // tile 0's rows and metadata
+  load_meta(cur.c);
+  load_fx(nx1);       // tile 1's frames
+  f32x4 accw[5][2];
+  float dbs[5], bcol[5];
+  bool new_chunk = true;
+  for (;;) {
+    const int ch = cur.ch, c = cur.c, g = cur.g0 + cur.t0, nr = min(HB_TM, cur.n - cur.t0);
+    HB_STAMP(0);
+    lds_barrier();  // previous tile's LDS reads done
+    store_x();
+    store_meta();
+    if (new_chunk) {
+      stage_w(c);
+#pragma unroll
+      for (int mb = 0; mb < 5; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) accw[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int nb = 0; nb < 5; ++nb) {
-        const int col = nb * 16 + li;
-        const float bias = bp[c * NP + col];
+        dbs[nb] = 0.f;
+        bcol[nb] = bp[(size_t)c * NP + nb * 16 + li];
+      }
+      new_chunk = false;
+    }
+    lds_barrier();
+    HB_STAMP(1);
+    const bool last = nx1.ch != ch, has_next = nx1.ch < nchunks;
+    // ---- Z = X W_c^T + b (this wave's 16 rows x 80)
+    f32x4 z[5];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) zb[(16 * wave + 4 * G + i) * (NP + 1) + col] = acc[nb][i] + bias;
+    for (int nb = 0; nb < 5; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* xa = xl + hb_phi(16 * wave + li) * HB_RX + 16 * G;
+#pragma unroll 2
+    for (int ks = 0; ks < KD / 32; ++ks) {
+      Frag8 a;
+      a.u = *(const uint4*)(xa + ks * 64);
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) {
+        Frag8 b;
+        b.u = *(const uint4*)(wl + hb_phi(nb * 16 + li) * HB_RW + ks * 64 + 16 * G);
+        z[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, z[nb], 0, 0, 0);
       }
     }
-    __syncthreads();
-    // ---- dZ per row (threads 0..63 one row each), in place in zb
-    if (tid < BW_TM) {
-      float* zr = zb + tid * (NP + 1);
-      if (tid < nr) {
-        const int f = pairs[g0 + t0 + tid];
-        const size_t fc = (size_t)f * S + c;
-        uint32_t m[3] = {mask[fc * 3], mask[fc * 3 + 1], mask[fc * 3 + 2]};
-        uint8_t a[kComps];
+
+    HB_STAMP(2);
+    // ---- dZ from the C layout: lane (li, G) holds column nb*16+li of rows 4G+i
+    // this wave's rows 16 wave + 4 G + i: metadata from the dZ tile's row padding
+    uint32_t mw[4][3], aw[4][3];
+    int ab[4];
+    float gl[4], ge[4];
 #pragma unroll
-        for (int k = 0; k < kComps; ++k) a[k] = action[fc * kComps + k];
-        cell_backward(zr, m, a, g_logp[f], g_ent ? g_ent[f] : 0.f, zr);
-      } else {
-        for (int j = 0; j < kCell; ++j) zr[j] = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t* m = (const uint32_t*)(zl + hb_phi(16 * wave + 4 * G + i) * HB_RZ + 192);
+      const uint4 q0 = *(const uint4*)m, q1 = *(const uint4*)(m + 4);
+      const uint32_t fw = m[8];
+      mw[i][0] = q0.x; mw[i][1] = q0.y; mw[i][2] = q0.z;
+      aw[i][0] = q0.w; aw[i][1] = q1.x; aw[i][2] = q1.y;
+      gl[i] = __uint_as_float(q1.z);
+      ge[i] = __uint_as_float(q1.w);
+      ab[i] = (int)((((size_t)(int)fw * S + c) * kComps) & 3);
+    }
+    // zz: the logits, overwritten in place by their gradient as each segment is finished
+    // (every logit belongs to exactly one segment); ok: valid (masked-in) logits
+    uint32_t okm = 0u;  // bit nb*4+i: logit (nb, i) valid
+    float zz[5][4];
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      const float b = bcol[nb];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zz[nb][i] = z[nb][i] + b;
+        const int bit = (nb & 1) * 16 + li;
+        okm |= (sk[nb] < kComps && ((mw[i][nb >> 1] >> bit) & 1u)) ? 1u << (nb * 4 + i) : 0u;
       }
-      zr[78] = 0.f;
-      zr[79] = 0.f;
     }
-    __syncthreads();
-    // ---- dZ -> bf16 tile [64][96] (cols >= 78 zero); bias grad column sums
-    for (int e = tid; e < BW_TM * NPT; e += 256) {
-      const int row = e / NPT, col = e % NPT;
-      const float v = col < kCell ? zb[row * (NP + 1) + col] : 0.f;
-      ((bf16*)dzt)[e] = f2bf(v);
-    }
-    if (tid < kCell) {
-      float s = 0.f;
-      for (int row = 0; row < nr; ++row) s += zb[row * (NP + 1) + tid];
-      dbias += s;
-    }
-    __syncthreads();
-    // ---- dX_pair = dZ . Wc (wave w: rows 16w..16w+15, 256 cols; K = 96), in two halves of
-    // 128 columns (8 accumulators + 8 fragments in flight instead of 16 + 48)
-    {
-      const bf16* wt = WpT + (size_t)c * KD * NPT;
-#pragma unroll 1
-      for (int hc = 0; hc < 2; ++hc) {
-        f32x4 acc[8];
 #pragma unroll
-        for (int nb = 0; nb < 8; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-        for (int ks = 0; ks < NPT / 32; ++ks) {
-          Frag8 a;
-          a.u = *(const uint4*)(dzt + ((16 * wave + li) * NPT + ks * 32 + 8 * G) * 2);
+    for (int k = 0; k < kComps; ++k) {
+      const int c0 = seg_off(k), c1 = seg_off(k + 1);
+      const int nb0 = c0 / 16, nb1 = (c1 - 1) / 16;
+      bool any = false;
 #pragma unroll
-          for (int nb = 0; nb < 8; ++nb) {
-            Frag8 b;
-            b.u = *((const uint4*)(wt + (size_t)((hc * 8 + nb) * 16 + li) * NPT + ks * 32) + G);
-            acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
-          }
+      for (int nb = nb0; nb <= nb1; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) any |= ((okm >> (nb * 4 + i)) & 1u) && sk[nb] == k;
+      if (__ballot(any) == 0ull) continue;  // wave-uniform: no valid logit of segment k
+      // the 4 rows' reductions interleaved
+      float mx[4], sm[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        mx[i] = -INFINITY;
+#pragma unroll
+        for (int nb = nb0; nb <= nb1; ++nb)
+          if (((okm >> (nb * 4 + i)) & 1u) && sk[nb] == k) mx[i] = fmaxf(mx[i], zz[nb][i]);
+      }
+      hb_max16(mx);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float e_s = 0.f, e_sz = 0.f;
+#pragma unroll
+        for (int nb = nb0; nb <= nb1; ++nb) {
+          const bool in = ((okm >> (nb * 4 + i)) & 1u) && sk[nb] == k;
+          const float e = in ? __expf(zz[nb][i] - mx[i]) : 0.f;
+          e_s += e;
+          e_sz += e * zz[nb][i];
         }
+        sm[2 * i] = e_s;
+        sm[2 * i + 1] = e_sz;
+      }
+      hb_sum16(sm);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = 16 * wave + 4 * G + i;
-          if (row < nr) {
-            float* dst = dXp + (size_t)(g0 + t0 + row) * KD + hc * 128;
+      for (int i = 0; i < 4; ++i) {
+        // lse = log sum exp, H = entropy = lse - sum p z; p = exp(z - lse)
+        const float lse = mx[i] + __logf(sm[2 * i]);
+        const float H = lse - sm[2 * i + 1] * __builtin_amdgcn_rcpf(sm[2 * i]);
+        // action of segment k in this row: byte ab + k of the 3 words
+        const int bi = ab[i] + k;
+        const uint32_t wsel = bi < 4 ? aw[i][0] : bi < 8 ? aw[i][1] : aw[i][2];
+        const int a = (int)((wsel >> (8 * (bi & 3))) & 0xFFu);
 #pragma unroll
-            for (int nb = 0; nb < 8; ++nb) dst[nb * 16 + li] = acc[nb][i];
-          }
+        for (int nb = nb0; nb <= nb1; ++nb) {
+          const bool in = ((okm >> (nb * 4 + i)) & 1u) && sk[nb] == k;
+          const float lp = zz[nb][i] - lse;
+          const float p = __expf(lp);
+          const float v = gl[i] * ((so[nb] == a ? 1.f : 0.f) - p) - ge[i] * p * (lp + H);
+          zz[nb][i] = in ? v : zz[nb][i];
         }
       }
     }
-    // ---- dW_c += dZ^T . X  (rows = logits, cols = features 64*wave.., K = 64 pairs)
+    float d[5][4];
 #pragma unroll
-    for (int ks = 0; ks < BW_TM / 32; ++ks) {
+    for (int nb = 0; nb < 5; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[nb][i] = ((okm >> (nb * 4 + i)) & 1u) ? zz[nb][i] : 0.f;
+    // dZ -> bf16 tile (rows phi(16 wave + 4 G + i), column nb*16 + li); bias-grad column sums
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      float cs = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * wave + 4 * G + i;
+        *(bf16*)(zl + hb_phi(r) * HB_RZ + (nb * 16 + li) * 2) = f2bf(d[nb][i]);
+        cs += d[nb][i];
+      }
+      dbs[nb] += cs;
+    }
+    // columns 80..95 of the dZ tile are the dX GEMM's zero K tail
+    if (li < 8) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = 16 * wave + 4 * G + i;
+        *(uint32_t*)(zl + hb_phi(r) * HB_RZ + 160 + li * 4) = 0u;
+      }
+    }
+    // next tile's rows and metadata: in flight through both GEMMs (issued after the epilogue,
+    // whose register peak they would otherwise add to)
+    if (has_next) {
+      load_x();
+      load_meta(nx1.c);
+    }
+    // then the tile after next: its cursor (scalar loads when it starts a chunk) and frames
+    // (fx / fr hold the next tile's frames until the two gathers above are issued)
+    const Cur nx2 = advance(nx1);
+    if (nx2.ch < nchunks) load_fx(nx2);
+    HB_STAMP(3);
+    lds_barrier();  // dZ tile complete
+    HB_STAMP(4);
+
+    // ---- dW_c += dZ^T X (logit rows x feature columns 32 wave.., K = the tile's rows)
+#pragma unroll 1
+    for (int ks = 0; ks < HB_TM / 32; ++ks) {
       Frag8 a[5];
 #pragma unroll
       for (int mb = 0; mb < 5; ++mb)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int prow = ks * 32 + 8 * G + 4 * h + (li >> 2);
-          a[mb].h[h] = tr_read(dzt + (prow * NPT + mb * 16 + 4 * (li & 3)) * 2);
+          const int pr = hb_phi(ks * 32 + 8 * G + 4 * h + (li >> 2));
+          a[mb].h[h] = tr_read(zl + pr * HB_RZ + (mb * 16 + 4 * (li & 3)) * 2);
         }
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) {
+      for (int nb = 0; nb < 2; ++nb) {
         Frag8 b;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const int prow = ks * 32 + 8 * G + 4 * h + (li >> 2);
-          b.h[h] = tr_read(xt + (prow * KD + 64 * wave + nb * 16 + 4 * (li & 3)) * 2);
+          const int pr = hb_phi(ks * 32 + 8 * G + 4 * h + (li >> 2));
+          b.h[h] = tr_read(xl + pr * HB_RX + (32 * wave + nb * 16 + 4 * (li & 3)) * 2);
         }
 #pragma unroll
         for (int mb = 0; mb < 5; ++mb)
           accw[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mb].v, b.v, accw[mb][nb], 0, 0, 0);
       }
     }
-  }
-  // ---- this chunk's partial dW / db (reduced per cell by head_dw_reduce)
+    // ---- dX_pair = dZ W_c (this wave's rows, 256 columns in two halves; K = 96), bf16. The
+    // X tile is free once every wave's dW is done: each wave stages its 16 x 256 rows there
+    // (C-layout 2-byte writes, 528-byte rows) and stores them as 16-byte chunks (the pair-row
+    // writes are this kernel's largest HBM traffic: 512 B per pair)
+    lds_barrier();
+    HB_STAMP(5);
+    const char* za = zl + hb_phi(16 * wave + li) * HB_RZ + 16 * G;
+    char* stg = xl + wave * 16 * 528;
+#pragma unroll 1
+    for (int hc = 0; hc < 2; ++hc) {
+      f32x4 acc[8];
 #pragma unroll
-  for (int mb = 0; mb < 5; ++mb)
+      for (int nb = 0; nb < 8; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+      for (int ks = 0; ks < NPT / 32; ++ks) {
+        Frag8 a;
+        a.u = *(const uint4*)(za + ks * 64);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = mb * 16 + 4 * G + i;
-      if (n >= kCell) continue;
-      float* dst = dWp + ((size_t)ch * kCell + n) * KD + 64 * wave;
+        for (int nb = 0; nb < 8; ++nb) {
+          Frag8 b;
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb) dst[nb * 16 + li] = accw[mb][nb][i];
+          for (int h = 0; h < 2; ++h) {
+            const int kr = ks * 32 + 8 * G + 4 * h + (li >> 2);
+            b.h[h] = tr_read(wl + hb_phi(kr) * HB_RW + ((hc * 8 + nb) * 16 + 4 * (li & 3)) * 2);
+          }
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[nb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int nb = 0; nb < 8; ++nb)
+          *(bf16*)(stg + (4 * G + i) * 528 + ((hc * 8 + nb) * 16 + li) * 2) = f2bf(acc[nb][i]);
     }
-  if (tid < kCell) dbp[(size_t)ch * kCell + tid] = dbias;
-  }  // chunks
+    // Every load of this wave is complete before the stores go out: vmcnt counts stores too,
+    // and a later wait on any load would otherwise also wait for these stores' completion
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // same wave, in-order LDS: the reads see the writes above; 2 rows x 512 B per instruction
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int rr = 2 * q + (lane >> 5), r = 16 * wave + rr;
+      const uint4 v = *(const uint4*)(stg + rr * 528 + (lane & 31) * 16);
+      if (r < nr) *(uint4*)(dXp + (size_t)(g + r) * KD + (lane & 31) * 8) = v;
+    }
+    HB_STAMP(6);
+    if (last) {
+      // ---- this chunk's partial dW / db (reduced per cell by head_dw_reduce)
+      // one base per lane, compile-time offsets (no per-row 64-bit pointers kept live)
+      float* dwb = dWp + ((size_t)ch * kCell + 4 * G) * KD + 32 * wave + li;
+#pragma unroll
+      for (int mb = 0; mb < 5; ++mb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (mb == 4 && 4 * G + i >= kCell - 64) continue;  // logit rows 78, 79
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb) dwb[(mb * 16 + i) * KD + nb * 16] = accw[mb][nb][i];
+        }
+      // bias grad: the 4 lane groups' column sums, then the 8 waves through LDS
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) {
+        float v = dbs[nb];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        if (G == 0) bl[wave * NP + nb * 16 + li] = v;
+      }
+      lds_barrier();
+      if (tid < kCell) {
+        float v = 0.f;
+        for (int w = 0; w < HB_NW; ++w) v += bl[w * NP + tid];
+        dbp[(size_t)ch * kCell + tid] = v;
+      }
+      if (!has_next) break;
+      new_chunk = true;
+    }
+    HB_STAMP(7);
+    ++nst;
+    cur = nx1;
+    nx1 = nx2;
+  }
 }
 
 // dW[c*78+n][d] = sum over the cell's chunks (fixed order); zero for idle cells
@@ -751,7 +1027,7 @@ __global__ __launch_bounds__(256) void head_dw_reduce_kernel(const float* __rest
 }
 
 // dX[f][:] = sum over active cells c of dXp[pidx[f][c]][:]; one wave per frame
-__global__ __launch_bounds__(256) void head_dx_gather_kernel(const float* __restrict__ dXp,
+__global__ __launch_bounds__(256) void head_dx_gather_kernel(const bf16* __restrict__ dXp,
                                                              const int* __restrict__ pidx, int F,
                                                              int S, float* __restrict__ dX) {
   // one wave per frame: 64 cells' pair indices per coalesced load, ballot the active
@@ -768,8 +1044,9 @@ __global__ __launch_bounds__(256) void head_dx_gather_kernel(const float* __rest
       const int b = __builtin_ctzll(m);
       m &= m - 1;
       const int pp = __shfl(p, b);
-      const float4 v = ((const float4*)(dXp + (size_t)pp * KD))[lane];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      const uint2 v = ((const uint2*)(dXp + (size_t)pp * KD))[lane];  // 4 bf16
+      acc.x += __uint_as_float(v.x << 16); acc.y += __uint_as_float(v.x & 0xFFFF0000u);
+      acc.z += __uint_as_float(v.y << 16); acc.w += __uint_as_float(v.y & 0xFFFF0000u);
     }
   }
   ((float4*)(dX + (size_t)f * KD))[lane] = acc;
@@ -782,7 +1059,7 @@ __global__ __launch_bounds__(256) void head_dx_gather_kernel(const float* __rest
 // score) take only the value term. The fp32 dX [F][256] of the separate kernels (1 KB per
 // frame written, then re-read with h by value_bwd) never exists. One wave per frame row,
 // a lane owns hidden units 4 lane .. 4 lane + 3 (the gather's float4 layout).
-__global__ __launch_bounds__(256) void head_dx_value_kernel(const float* __restrict__ dXp,
+__global__ __launch_bounds__(256) void head_dx_value_kernel(const bf16* __restrict__ dXp,
                                                             const int* __restrict__ pidx, int F,
                                                             int S, const float* __restrict__ dv,
                                                             const bf16* __restrict__ h,
@@ -828,8 +1105,9 @@ __global__ __launch_bounds__(256) void head_dx_value_kernel(const float* __restr
         const int b = __builtin_ctzll(m);
         m &= m - 1;
         const int pp = __shfl(p, b);
-        const float4 v = ((const float4*)(dXp + (size_t)pp * KD))[lane];
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        const uint2 v = ((const uint2*)(dXp + (size_t)pp * KD))[lane];  // 4 bf16
+        acc.x += __uint_as_float(v.x << 16); acc.y += __uint_as_float(v.x & 0xFFFF0000u);
+        acc.z += __uint_as_float(v.y << 16); acc.w += __uint_as_float(v.y & 0xFFFF0000u);
       }
     }
     const float hj[4] = {__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xFFFF0000u),
@@ -959,24 +1237,58 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
                             const uint32_t* mask, const uint8_t* action, const int* pairs,
                             const int* grp_start, const int* grp_count, const int* chunk_cell,
                             const int* chunk_row, const int* chunk_start, const int* totals,
-                            const float* g_logp, const float* g_ent, int S, int grid, float* dXp,
+                            const float* g_logp, const float* g_ent, int S, int grid, void* dXp,
                             float* dWp, float* dbp, float* dW, float* db, hipStream_t stream) {
-  const size_t sm = LDS_WC + LDS_XT + LDS_DZ + LDS_Z;
-  hipFuncSetAttribute((const void*)head_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                      (int)sm);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(grid), dim3(256), sm, stream, (const bf16*)X,
-                     (const bf16*)Wp, (const bf16*)WpT, bp, mask, action, pairs, grp_start,
-                     grp_count, chunk_cell, chunk_row, totals, g_logp, g_ent, S, dXp, dWp, dbp);
+  {
+    static int cus = 0;
+    static uint64_t* hb_stamps = nullptr;
+    if (!cus) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (cus <= 0) cus = 256;
+      hipFuncSetAttribute((const void*)head_bwd2_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, HB_LDS);
+      if (getenv("MBK_HB_STAMPS")) {
+        hipMalloc(&hb_stamps, (size_t)cus * 64 * 8);
+        hipMemset(hb_stamps, 0, (size_t)cus * 64 * 8);
+      }
+    }
+    // one 158 KB workgroup per CU; the caller's grid (chunk count bound) caps it
+    const int g2 = std::max(1, std::min(grid, cus));
+    hipLaunchKernelGGL(head_bwd2_kernel, dim3(g2), dim3(64 * HB_NW), HB_LDS, stream,
+                       (const bf16*)X, (const bf16*)Wp, bp, mask, action, pairs, grp_start,
+                       grp_count, chunk_cell, chunk_row, totals, g_logp, g_ent, S, (bf16*)dXp, dWp,
+                       dbp, hb_stamps);
+    if (hb_stamps) {  // per-phase mean over workgroups and their tiles 1..7 (us)
+      std::vector<uint64_t> h((size_t)g2 * 64);
+      hipMemcpyAsync(h.data(), hb_stamps, h.size() * 8, hipMemcpyDeviceToHost, stream);
+      hipStreamSynchronize(stream);
+      double acc[8] = {0};
+      int n = 0;
+      for (int b = 0; b < g2; ++b)
+        for (int t = 1; t < 8; ++t) {
+          const uint64_t* r = &h[((size_t)b * 8 + t) * 8];
+          if (!r[0] || !r[7]) continue;
+          for (int k = 0; k < 7; ++k) acc[k] += (double)(r[k + 1] - r[k]) * 0.01;
+          ++n;
+        }
+      fprintf(stderr, "head_bwd2 phases (us, %d tiles): store+W %.2f | loads+Z %.2f | dZ %.2f | "
+              "B2 %.2f | dX %.2f | dW %.2f | end %.2f\n", n, acc[0] / n, acc[1] / n, acc[2] / n,
+              acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n);
+      hipMemsetAsync(hb_stamps, 0, h.size() * 8, stream);
+    }
+  }
   dim3 g2((kCell * KD + kCell + 255) / 256, S);
   hipLaunchKernelGGL(head_dw_reduce_kernel, g2, dim3(256), 0, stream, dWp, dbp, chunk_start,
                      grp_count, S, dW, db);
   return (int)hipGetLastError();
 }
 
-extern "C" int mbk_head_dx_gather(const float* dXp, const int* pidx, int F, int S, float* dX,
+extern "C" int mbk_head_dx_gather(const void* dXp, const int* pidx, int F, int S, float* dX,
                                   hipStream_t stream) {
-  hipLaunchKernelGGL(head_dx_gather_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, dXp, pidx, F,
-                     S, dX);
+  hipLaunchKernelGGL(head_dx_gather_kernel, dim3((F + 3) / 4), dim3(256), 0, stream,
+                     (const bf16*)dXp, pidx, F, S, dX);
   return (int)hipGetLastError();
 }
 
@@ -995,13 +1307,13 @@ extern "C" int mbk_head_dx_value_parts(int R) {
 
 // dh [R][256] bf16 = (dv wc + gathered head dX) * (h > 0); partial [parts][257] fp32 rows of
 // (dWc, dbc); rows >= F take the value term only. parts = mbk_head_dx_value_parts(R).
-extern "C" int mbk_head_dx_value(const float* dXp, const int* pidx, int F, int S, const float* dv,
+extern "C" int mbk_head_dx_value(const void* dXp, const int* pidx, int F, int S, const float* dv,
                                  const void* h, const float* wc, int R, void* dh, float* partial,
                                  int parts, hipStream_t stream) {
   if (R <= 0) return 0;
   if (F > R || parts < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_dx_value_kernel, dim3(parts), dim3(256), 0, stream, dXp, pidx, F, S, dv,
-                     (const bf16*)h, wc, R, (bf16*)dh, partial);
+  hipLaunchKernelGGL(head_dx_value_kernel, dim3(parts), dim3(256), 0, stream, (const bf16*)dXp,
+                     pidx, F, S, dv, (const bf16*)h, wc, R, (bf16*)dh, partial);
   return (int)hipGetLastError();
 }
 

@@ -175,7 +175,7 @@ class SparseHead:
         st = N.stream_ptr()
         # one sync: sizes the pair-major dX and per-chunk dW buffers
         P, _, nch = (int(v) for v in self.totals.tolist())
-        dXp = torch.empty(max(P, 1), KD, dtype=torch.float32, device=X.device)
+        dXp = torch.empty(max(P, 1), KD, dtype=torch.bfloat16, device=X.device)  # pair rows
         dWp = torch.empty(max(nch, 1), 78, KD, dtype=torch.float32, device=X.device)
         dbp = torch.empty(max(nch, 1), 78, dtype=torch.float32, device=X.device)
         if dW is None:
@@ -183,7 +183,7 @@ class SparseHead:
         if db is None:
             db = torch.empty(self.S * 78, dtype=torch.float32, device=X.device)
         assert dW.is_contiguous() and db.is_contiguous() and dW.numel() == self.S * 78 * KD
-        grid = max(1, min(nch, self.fwd_grid))  # two 65 KB-LDS workgroups per CU
+        grid = max(1, min(nch, self.fwd_grid))  # the launcher caps it at one workgroup per CU
         N.check(k.mbk_head_bwd(X.data_ptr(), self.Wp.data_ptr(), self.WpT.data_ptr(),
                                self.bp.data_ptr(), mask_bits.data_ptr(), action.data_ptr(),
                                self.pairs.data_ptr(), self.grp_start.data_ptr(),

@@ -27,9 +27,11 @@ def _problem(F, S, p_active=0.08, seed=0):
     return X, W, b, m, a
 
 
-@pytest.mark.parametrize("F,S", [(300, 64), (1000, 256)])
-def test_sparse_score_fwd_bwd(cuda, F, S):
-    X, W, b, m, a = _problem(F, S)
+# (40000, 16, 0.25): ~10K pairs per cell, ~313 512-pair chunks: several 128-pair tiles per
+# chunk and several chunks per workgroup of head_bwd2 (its prefetch pipeline across both)
+@pytest.mark.parametrize("F,S,p", [(300, 64, 0.08), (1000, 256, 0.08), (40000, 16, 0.25)])
+def test_sparse_score_fwd_bwd(cuda, F, S, p):
+    X, W, b, m, a = _problem(F, S, p_active=p)
     head = SparseHead(S, cuda)
     Xg = X.to(cuda).requires_grad_(True)
     Wg = W.to(cuda).requires_grad_(True)
