@@ -360,6 +360,19 @@ class GpuActorRuntime:
             self.engine.stop()
             self.started = False
 
+    def close(self):
+        """Stop, then drop the engine and every device buffer / captured graph this runtime
+        owns, so its HBM goes back to the allocator even while a caller still holds the (now
+        empty) object (train.restart_runtime)."""
+        self.stop()
+        self.engine = None  # the native engine first: it points into the buffers below
+        self.lanes = []
+        self.rb = {}
+        for k in ("io", "rng", "infer_model", "infer_flat", "pack_graph", "graph", "opp_graph",
+                  "opp_flat", "opp_model"):
+            if hasattr(self, k):
+                setattr(self, k, None)
+
     def check(self):
         if self.engine.failed():
             raise EngineFailure(f"GPU actor engine failed: {self.engine.error()}")

@@ -117,9 +117,10 @@ def _profile_tick(prof, n_update: int, flags: Flags, cuda: bool):
 def restart_runtime(rt, make, learner_flat, n_update: int, league=None):
     """Replace a failed GPU actor runtime: stop it and drop every reference to it, collect,
     return its cached HBM to the allocator, THEN build and start the new one (acting with
-    the learner's current weights, tagged with update ``n_update``). The caller must not
-    hold references into the old runtime (e.g. a batch that views its rollout slots)."""
-    rt.stop()
+    the learner's current weights, tagged with update ``n_update``). ``rt.close()`` drops the
+    old runtime's buffers even though the caller's own variable still references it; the caller
+    must not hold other references into it (e.g. a batch that views its rollout slots)."""
+    rt.close()
     rt = None
     gc.collect()
     if torch.cuda.is_available():
