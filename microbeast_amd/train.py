@@ -33,9 +33,12 @@ from .utils.metrics import CsvLogger
 def scaled_lr(flags: Flags, frames_per_update: int) -> float:
     """--lr_scaling: the base --lr is tuned for --lr_base_batch frames per update (the reference
     2.5e-4 at one GPU's 524,288); weak-scaled DP multiplies the global batch by the world size
-    (and --batch_size by its value), so the step size can follow it: sqrt (Adam's usual rule)
-    or linear in the batch ratio, or stay (none)."""
-    r = frames_per_update / max(1, flags.lr_base_batch)
+    (and --batch_size by its value), so the step size can follow it: sqrt (Adam's usual rule,
+    the default) or linear in the batch ratio, or stay (none). Only batches LARGER than the
+    base are scaled: smaller configs keep the reference lr. Measured on 16x16 at 1.68 B frames
+    (experiments/README.md): 4.2 M frames per update reaches a 0.80 win rate with sqrt vs 0.47
+    unscaled (0.56 at 524 K frames per update)."""
+    r = max(1.0, frames_per_update / max(1, flags.lr_base_batch))
     k = {"none": 0.0, "sqrt": 0.5, "linear": 1.0}[flags.lr_scaling]
     return flags.lr * (r ** k)
 

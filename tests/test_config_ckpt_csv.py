@@ -69,3 +69,21 @@ def test_csv_logger_and_process(tmp_path):
     prow = open(out).read().splitlines()
     assert prow[0] == "Return,steps" and len(prow) == 3
     assert prow[2].split(",")[0] == "1"  # remainder row keeps its window index
+
+
+def test_lr_scaling_only_scales_batches_above_the_base():
+    """--lr_scaling (train.scaled_lr): sqrt by default; only global batches above
+    --lr_base_batch are scaled (the DP weak-scaling case), smaller configs keep --lr."""
+    from microbeast_amd.config import parse_flags
+    from microbeast_amd.train import scaled_lr
+
+    f = parse_flags(["--quiet"], interactive=False)
+    assert f.lr_scaling == "sqrt"
+    base = f.lr_base_batch
+    assert scaled_lr(f, base) == f.lr
+    assert scaled_lr(f, base // 32) == f.lr
+    assert abs(scaled_lr(f, 8 * base) - f.lr * 8 ** 0.5) < 1e-12
+    f.lr_scaling = "linear"
+    assert abs(scaled_lr(f, 4 * base) - 4 * f.lr) < 1e-12
+    f.lr_scaling = "none"
+    assert scaled_lr(f, 8 * base) == f.lr
