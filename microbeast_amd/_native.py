@@ -130,6 +130,8 @@ _SIGS = {
                       c_int, c_void_p],
     # gridnet.hip
     "mbk_bits_grid": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_bits_pad": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_crop_relu_mask": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_pool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                      c_void_p],
     "mbk_pool_bwd_grid": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,

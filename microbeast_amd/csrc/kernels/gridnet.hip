@@ -69,6 +69,49 @@ __global__ __launch_bounds__(kThreads) void bits_grid_kernel(const uint32_t* __r
   }
 }
 
+// int32 bit-plane obs [n][h*w] -> the same planes on the padded map [n][ph*pw] (zero outside the
+// h x w map): the first encoder layer then runs on conv.hip's bit-plane kernels
+template <typename IDX>
+__global__ __launch_bounds__(kThreads) void bits_pad_kernel(const uint32_t* __restrict__ bits,
+                                                            int n, int h, int w, int ph, int pw,
+                                                            uint32_t* __restrict__ out) {
+  const IDX total = (IDX)n * ph * pw;
+  for (IDX e = (IDX)blockIdx.x * kThreads + threadIdx.x; e < total; e += (IDX)gridDim.x * kThreads) {
+    const int x = (int)(e % pw), t = (int)(e / pw);
+    const int y = t % ph, b = t / ph;
+    out[e] = (y < h && x < w) ? bits[(size_t)b * h * w + y * w + x] : 0u;
+  }
+}
+
+// g_pad [B][H+2][W+2][C] interior * (p > 0) -> plain [B][H][W][C] (bf16, C % 8 == 0): the
+// pooled-output gradient of relu(pool(conv)) from the next layer's padded-grid dgrad
+template <typename IDX>
+__global__ __launch_bounds__(kThreads) void crop_relu_mask_kernel(const uint4* __restrict__ g,
+                                                                  const uint4* __restrict__ p,
+                                                                  int B, int H, int W, int C8,
+                                                                  uint4* __restrict__ out) {
+  const IDX total = (IDX)B * H * W * C8;
+  for (IDX e = (IDX)blockIdx.x * kThreads + threadIdx.x; e < total; e += (IDX)gridDim.x * kThreads) {
+    const int q = (int)(e % C8);
+    const IDX px = e / C8;
+    const int x = (int)(px % W), t = (int)(px / W);
+    const int y = t % H, b = t / H;
+    const uint4 gv = g[(((IDX)b * (H + 2) + y + 1) * (W + 2) + x + 1) * C8 + q];
+    const uint4 pv = p[e];
+    const uint32_t gw[4] = {gv.x, gv.y, gv.z, gv.w}, pw[4] = {pv.x, pv.y, pv.z, pv.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // bf16 > 0: sign bit clear and not +0 (per 16-bit half)
+      const uint32_t lo = (pw[j] & 0x8000u) == 0u && (pw[j] & 0x7FFFu) != 0u ? 0xFFFFu : 0u;
+      const uint32_t hi = (pw[j] & 0x80000000u) == 0u && (pw[j] & 0x7FFF0000u) != 0u
+                              ? 0xFFFF0000u : 0u;
+      o[j] = gw[j] & (lo | hi);
+    }
+    out[e] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // ------------------------------------------------------------------ max pool 3x3 / 2, pad 1
 // y [B][H][W][C] (relu'd conv output) -> out [B][Ho][Wo][C] and / or out_pad
 // [B][Ho+2][Wo+2][C] (zero border), idx [B][Ho][Wo][C] = ky*3+kx of the first maximum in
@@ -435,6 +478,26 @@ extern "C" int mbk_bits_grid(const void* bits, int n, int h, int w, int Hp, int 
   if (!fits((long)n * Hp * Wp) || Hp < h + 2 || Wp < w + 2) return (int)hipErrorInvalidValue;
   MBK_LAUNCH_IDX(bits_grid_kernel, total, stream, (const uint32_t*)bits, n, h, w, Hp, Wp,
                  (uint4*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_bits_pad(const void* bits, int n, int h, int w, int ph, int pw, void* out,
+                            hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (ph < h || pw < w) return (int)hipErrorInvalidValue;
+  const long total = (long)n * ph * pw;
+  MBK_LAUNCH_IDX(bits_pad_kernel, total, stream, (const uint32_t*)bits, n, h, w, ph, pw,
+                 (uint32_t*)out);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_crop_relu_mask(const void* g_pad, const void* p, int B, int H, int W, int C,
+                                  void* out, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (C % 8) return (int)hipErrorInvalidValue;
+  const long total = (long)B * H * W * (C / 8);
+  MBK_LAUNCH_IDX(crop_relu_mask_kernel, total, stream, (const uint4*)g_pad, (const uint4*)p, B, H,
+                 W, C / 8, (uint4*)out);
   return (int)hipGetLastError();
 }
 

@@ -3,9 +3,9 @@
 // CategoricalMasked objects per forward (model.py:168-200; 1,792 objects at
 // 16x16), each doing where(mask, l, -1e8) + logsumexp + sample/log_prob/entropy.
 //
-// One thread owns one cell (78 logits, 7 segments). A 64-cell tile of the
-// contiguous cell-major logits is staged through LDS with coalesced loads
-// into rows padded to 79 floats (odd stride => conflict-free per-lane reads).
+// One thread owns one cell (78 logits, 7 segments). The active cells of a 64-cell tile of the
+// contiguous cell-major logits are staged through LDS (one row per wave-wide load pair) into
+// rows padded to 79 floats (odd stride => conflict-free per-lane reads).
 // Used by the GridNet arch (logits from a deconv decoder) and as the parity
 // oracle of the fused GEMM+epilogue head (head.hip).
 #include "../include/mbk_api.h"
@@ -25,14 +25,20 @@ __device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p) {
   return __bfloat162float(*p);
 }
 
+// Only cells with a legal action are staged: a cell whose 78 mask bits are all zero takes no
+// logit read in cell_forward / cell_backward (log-prob 0, entropy 0, gradient 0 exactly), and
+// on real states ~1-5 % of cells are active, so the tile's logits (156 B per cell in bf16) are
+// read for those rows only. am: the tile's active-cell ballot (one wave per tile).
 template <typename TZ>
-__device__ __forceinline__ void stage_tile(const TZ* __restrict__ logits, int64_t c0, int ncell,
-                                           float* zs) {
-  const int64_t base = c0 * kCell;
-  const int total = ncell * kCell;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int r = e / kCell, c = e - r * kCell;
-    zs[r * kRow + c] = ld(logits + base + e);
+__device__ __forceinline__ void stage_active(const TZ* __restrict__ logits, int64_t c0,
+                                             uint64_t am, float* zs) {
+  const int lane = threadIdx.x;
+  while (am) {
+    const int r = __builtin_ctzll(am);
+    am &= am - 1;
+    const TZ* src = logits + (c0 + r) * kCell;
+    zs[r * kRow + lane] = ld(src + lane);
+    if (lane < kCell - 64) zs[r * kRow + 64 + lane] = ld(src + 64 + lane);
   }
 }
 
@@ -44,12 +50,13 @@ __global__ __launch_bounds__(kTile) void masked_cell_fwd_kernel(
   __shared__ float zs[kTile * kRow];
   const int64_t c0 = (int64_t)blockIdx.x * kTile;
   const int nc = (int)min((int64_t)kTile, ncells - c0);
-  stage_tile(logits, c0, nc, zs);
-  __syncthreads();
   const int i = threadIdx.x;
-  if (i >= nc) return;
   const int64_t cell = c0 + i;
-  uint32_t m[3] = {mask[cell * 3 + 0], mask[cell * 3 + 1], mask[cell * 3 + 2]};
+  uint32_t m[3] = {0u, 0u, 0u};
+  if (i < nc) { m[0] = mask[cell * 3 + 0]; m[1] = mask[cell * 3 + 1]; m[2] = mask[cell * 3 + 2]; }
+  stage_active(logits, c0, __ballot((m[0] | m[1] | m[2]) != 0u), zs);
+  __syncthreads();
+  if (i >= nc) return;
   uint8_t a[kComps];
   float u[kComps];
   if (sample) {
@@ -83,13 +90,18 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
   __shared__ float zs[kTile * kRow];
   const int64_t c0 = (int64_t)blockIdx.x * kTile;
   const int nc = (int)min((int64_t)kTile, ncells - c0);
-  stage_tile(logits, c0, nc, zs);
-  __syncthreads();
   const int i = threadIdx.x;
+  uint32_t m[3] = {0u, 0u, 0u};
   if (i < nc) {
     const int64_t cell = c0 + i;
+    m[0] = mask[cell * 3 + 0]; m[1] = mask[cell * 3 + 1]; m[2] = mask[cell * 3 + 2];
+  }
+  const uint64_t am = __ballot((m[0] | m[1] | m[2]) != 0u);
+  stage_active(logits, c0, am, zs);
+  __syncthreads();
+  if (i < nc && ((am >> i) & 1ull)) {
+    const int64_t cell = c0 + i;
     const int64_t smp = cell / cells_per_sample;
-    uint32_t m[3] = {mask[cell * 3 + 0], mask[cell * 3 + 1], mask[cell * 3 + 2]};
     uint8_t a[kComps];
 #pragma unroll
     for (int k = 0; k < kComps; ++k) a[k] = action[cell * kComps + k];
@@ -98,11 +110,12 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
     cell_backward(row, m, a, g_logp[smp], g_ent ? g_ent[smp] : 0.f, row);
   }
   __syncthreads();
+  // every cell's 78 gradients are written: inactive rows are exactly zero (not staged)
   const int64_t base = c0 * kCell;
   const int total = nc * kCell;
   for (int e = threadIdx.x; e < total; e += blockDim.x) {
     const int r = e / kCell, c = e - r * kCell;
-    dlogits[base + e] = (TD)zs[r * kRow + c];
+    dlogits[base + e] = (TD)(((am >> r) & 1ull) ? zs[r * kRow + c] : 0.f);
   }
 }
 

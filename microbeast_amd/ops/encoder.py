@@ -192,6 +192,18 @@ class HipEncoder:
             N.check(k.mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), len(layers),
                                     N.stream_ptr()), "conv_pack")
 
+    def pack_layer(self, i: int, weight: torch.Tensor, with_bwd: bool = False) -> None:
+        """Pack layer i's fp32 weight only (GridNet's first layer uses this encoder's stage-0
+        conv alone, ops/gridconv.py)."""
+        L = self.layers[i]
+        assert weight.dtype == torch.float32 and weight.is_contiguous()
+        bwd = ((self.packed_bwd.data_ptr() + 2 * L.wb_off)
+               if (with_bwd and L.wb_off >= 0) else None)
+        jobs = (_Job * 1)(_Job(weight.data_ptr(), self.packed_fwd.data_ptr() + 2 * L.w_off, bwd,
+                               L.cin, L.cin_real, L.cout))
+        N.check(N.kernels().mbk_conv_pack(ctypes.cast(jobs, ctypes.c_void_p), 1, N.stream_ptr()),
+                "conv_pack")
+
     def pack_fp8(self, weights: list[torch.Tensor]) -> None:
         k = N.kernels()
         for c0 in range(0, len(self.layers), 16):

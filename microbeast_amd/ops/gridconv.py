@@ -39,6 +39,7 @@ F.conv_transpose2d (tests/test_gridconv.py); tests/test_gpu_gridconv.py runs the
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -523,6 +524,55 @@ class _EncoderLayer(torch.autograd.Function):
         return gx, gw, gb, None, None, None, None
 
 
+class _BitsEncoderLayer(torch.autograd.Function):
+    """The first encoder layer (bit-plane input, 32 output channels) on conv.hip's stage-0
+    kernels instead of the shifted-row GEMM over the halo'd grid: conv3x3(+bias) with the
+    3x3/2 max-pool + argmax in its epilogue (``conv0_row`` on 16-wide maps), relu while
+    padding the pooled map into the next layer's grid (grid_gather with itself as the mask);
+    backward = relu mask + crop of the next layer's padded dgrad, the argmax max-pool backward
+    (``pool_bwd_idx``) and the bit-plane weight-gradient kernel (band layout, bias grad by
+    MFMA). No input gradient (the observation). Same maths as ``_EncoderLayer``:
+    relu(pool(conv)) == pool(relu(conv)), and the pool argmax only routes gradients where the
+    relu passes them."""
+
+    @staticmethod
+    def forward(ctx, bits_pad, w, b, enc):
+        ctx.set_materialize_grads(False)
+        L = enc.layers[0]
+        enc.pack_layer(0, w.detach().contiguous())
+        n = bits_pad.shape[0]
+        Ho, Wo = (L.H + 1) // 2, (L.W + 1) // 2
+        pidx = torch.empty(n, Ho, Wo, L.cout, dtype=torch.uint8, device=bits_pad.device)
+        p = enc._fwd(L, bits_pad, b.detach(), pool_idx=pidx)         # pooled, pre-relu
+        C = L.cout
+        pp = grid_gather(p, (0, Ho * Wo * C, Wo * C, C, Ho, Wo, C), p,
+                         (0, Ho * Wo * C, Wo * C, C), 1, n, Ho, Wo, C)[0]
+        ctx.save_for_backward(bits_pad, p, pidx)
+        ctx.enc = enc
+        ctx.params = (w, b)
+        return pp
+
+    @staticmethod
+    def backward(ctx, g_pad):
+        bits_pad, p, pidx = ctx.saved_tensors
+        enc = ctx.enc
+        L = enc.layers[0]
+        if g_pad is None or not (ctx.needs_input_grad[1] or ctx.needs_input_grad[2]):
+            return (None,) * 4
+        n, Ho, Wo, C = p.shape
+        k = _N().kernels()
+        st = _N().stream_ptr()
+        dp = torch.empty_like(p)
+        _N().check(k.mbk_crop_relu_mask(g_pad.contiguous().data_ptr(), p.data_ptr(), n, Ho, Wo,
+                                        C, dp.data_ptr(), st), "crop_relu_mask")
+        dc = torch.empty(n, L.H, L.W, C, dtype=_BF, device=p.device)
+        _N().check(k.mbk_pool_bwd_idx(pidx.data_ptr(), dp.data_ptr(), n, L.H, L.W, C,
+                                      dc.data_ptr(), st), "pool_bwd_idx")
+        gw, gb = _pgrad(ctx.params[0]), _pgrad(ctx.params[1])
+        enc._wgrad(L, bits_pad, dc, gw, gb)
+        return None, gw, gb, None
+
+
 class _DecoderLayer(torch.autograd.Function):
     """ConvTranspose2d(k3, s2, p1, op1)(+bias): padded grid in; out = padded grid of the
     relu'd output, or (``crop`` = (h, w)) the final layer's cell-major logits
@@ -667,6 +717,16 @@ class GridPlan:
             fwd, dgrad, grad, nfl = convt_maps(t.weight.shape[0], t.weight.shape[1])
             self.dec.append((dev(fwd), dev(dgrad), dev(grad), fwd.shape, dgrad.shape, nfl))
         hh, ww, c = zshape
+        # the bit-plane first layer on conv.hip (_BitsEncoderLayer) when it is the 32-plane ->
+        # 32-channel conv those kernels implement (CUDA only; the CPU emulation keeps the grid
+        # path)
+        c0 = convs[0]
+        self.enc0 = None
+        if (torch.device(device).type == "cuda" and c0.weight.shape[0] == 32
+                and c0.weight.shape[1] <= 32 and os.environ.get("MBK_GRID_E1_CONV", "1") == "1"):
+            from .encoder import HipEncoder
+            self.enc0 = HipEncoder(16 * hh, 16 * ww, c0.weight.shape[1], channels=(32,),
+                                   device=device)
         fwd, dgrad, grad = critic_maps(lin1.weight.shape[0], c, hh, ww)
         self.crit = (dev(fwd), dev(dgrad), dev(grad), fwd.shape, dgrad.shape)
         self.w2map = dev(torch.arange(lin2.weight.numel(), dtype=torch.int32))
@@ -704,11 +764,20 @@ def gridnet_forward(plan: GridPlan, bits: torch.Tensor, h: int, w: int, ph: int,
     grad = torch.is_grad_enabled()
     pk = plan.pack(grad)
     n = bits.shape[0]
-    x = bits_grid(bits.reshape(n, h * w).contiguous(), h, w, ph + 2, pw + 2)
+    fast0 = plan.enc0 is not None and bits.is_cuda
+    if fast0:
+        bp = torch.empty(n, ph * pw, dtype=torch.int32, device=bits.device)
+        _N().check(_N().kernels().mbk_bits_pad(bits.reshape(n, h * w).contiguous().data_ptr(),
+                                               n, h, w, ph, pw, bp.data_ptr(), _N().stream_ptr()),
+                   "bits_pad")
+    else:
+        x = bits_grid(bits.reshape(n, h * w).contiguous(), h, w, ph + 2, pw + 2)
     z = None
     nl = len(plan.convs)
     for i, (c, (wk, wt), (_, _, gm, _, _)) in enumerate(zip(plan.convs, pk["enc"], plan.enc)):
-        if i == nl - 1:
+        if i == 0 and fast0 and nl > 1:
+            x = _BitsEncoderLayer.apply(bp, c.weight, c.bias, plan.enc0)
+        elif i == nl - 1:
             x, z = _EncoderLayer.apply(x, c.weight, c.bias, wk, wt, gm, True)
         else:
             x = _EncoderLayer.apply(x, c.weight, c.bias, wk, wt, gm, False)
