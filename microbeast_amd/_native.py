@@ -38,6 +38,17 @@ _SIGS = {
     "mbk_masked_cell_bwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                             c_int64, c_void_p, c_int, c_void_p],
     "mbk_row_sum": [c_void_p, c_int64, c_int, c_void_p, c_void_p],
+    "mbk_masked_cell_fwd_pbc": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                c_int, c_int64, c_void_p, c_void_p, c_void_p],
+    "mbk_masked_cell_bwd_pbc": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                c_void_p, c_int64, c_void_p, c_void_p],
+    "mbk_pconv": [c_void_p, c_void_p],
+    "mbk_pwgrad": [c_void_p, c_void_p],
+    "mbk_pwgrad_parts": [c_int, c_int, c_int, c_int],
+    "mbk_reduce_map": [c_void_p, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p],
+    "mbk_ppool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_ppool_bwd": [c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
+                      c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_rng_advance": [c_void_p, c_void_p],
     "mbk_vtrace": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                    c_float, c_float, c_float, c_float, c_float, c_float, c_float, c_void_p,
@@ -66,10 +77,6 @@ _SIGS = {
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],
     "mbk_fc_wgrad": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                      c_void_p],
-    "mbk_fc_wgrad_taps": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
-                          c_int, c_void_p, c_int, c_void_p],
-    "mbk_gemm_nt_taps": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                         c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_fc_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
                    c_void_p, c_void_p, c_void_p],
     "mbk_gemm_nt": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
@@ -129,14 +136,7 @@ _SIGS = {
                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                       c_int, c_void_p],
     # gridnet.hip
-    "mbk_bits_grid": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_bits_pad": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_crop_relu_mask": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_pool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
-                     c_void_p],
-    "mbk_pool_bwd_grid": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_int, c_void_p, c_int,
-                          c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_grid_gather": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "mbk_colsum_parts": [c_int64],
     "mbk_colsum": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                    c_void_p],

@@ -194,111 +194,6 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
   }
 }
 
-// ------------------------------------------------------------------ all-taps weight gradient
-// dW[o][t*I + i] = sum_n g[n][o] x[n + s_t][i] for up to 9 row shifts, one launch, with the x
-// rows of a K stage staged ONCE for every tap (fc_wgrad_kernel's shifted form re-reads them
-// per 64-column output chunk, and there is one such chunk per tap: 9x the traffic) and the
-// output tile = 64 rows of W x (every tap x 32 input channels) per workgroup. Each wave owns
-// 16 output rows; per 32-row K block it reads its A fragment and the 2 x ntap B fragments
-// (taps are row offsets into the staged x range). K is permuted inside each 32-row block
-// (lane group G, half h, row j -> row 16 h + 4 G + j), so a half-wave's tr read covers 8
-// consecutive rows; row strides of 160 B (g) and 96 B (x) put 8 consecutive rows on 8
-// distinct 32-byte bank windows: conflict-free for any tap shift.
-constexpr int TW_R = 128;                 // K rows per stage
-constexpr int TW_OC = 64, TW_IC = 32;     // output tile: 64 W rows x (ntap x 32 channels)
-constexpr int TW_GROW = 160;              // g tile row bytes (128 data)
-constexpr int TW_XROW = 96;               // x tile row bytes (64 data)
-constexpr int TW_MAXH = 72;               // |shift| bound: (grid width + 1) of a 64+2-wide grid
-constexpr int TW_XR = TW_R + 2 * TW_MAXH; // staged x rows per stage
-
-__global__ __launch_bounds__(kThreads) void wgrad_taps_kernel(const bf16* __restrict__ g,
-                                                              const bf16* __restrict__ x, int N,
-                                                              int O, int I, int rows_per_part,
-                                                              float* __restrict__ partial,
-                                                              XShifts xs) {
-  __shared__ __attribute__((aligned(16))) char smem[TW_R * TW_GROW + TW_XR * TW_XROW];
-  char* gt = smem;
-  char* xt = smem + TW_R * TW_GROW;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int G = lane >> 4, li = lane & 15;
-  const int nt = xs.ntap, TI = nt * I;
-  int smin = 0, smax = 0;
-  for (int t = 0; t < nt; ++t) { smin = min(smin, xs.s[t]); smax = max(smax, xs.s[t]); }
-  const int XR = TW_R + smax - smin;  // staged x rows: [rs + smin, rs + R + smax)
-  const int nic = (I + TW_IC - 1) / TW_IC;
-  const int chunk = blockIdx.x, part = blockIdx.y;
-  const int o0 = (chunk / nic) * TW_OC, i0 = (chunk % nic) * TW_IC;
-  const int r0 = part * rows_per_part, r1 = min(N, r0 + rows_per_part);
-  const bool wave_on = o0 + 16 * wave < O;  // wave-uniform: this wave's 16 W rows exist
-  f32x4 acc[kMaxTaps][2];
-#pragma unroll
-  for (int t = 0; t < kMaxTaps; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // staging: g [R rows][64 cols] = 1024 16-byte elements, x [XR rows][32 cols] = 4 per row
-  auto stage = [&](int rs) {
-    for (int e = tid; e < TW_R * (TW_OC / 8); e += kThreads) {
-      const int row = e >> 3, c = o0 + (e & 7) * 8, n = rs + row;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (n < r1 && c < O) v = *(const uint4*)(g + (size_t)n * O + c);
-      *(uint4*)(gt + row * TW_GROW + (e & 7) * 16) = v;
-    }
-    for (int e = tid; e < XR * (TW_IC / 8); e += kThreads) {
-      const int row = e >> 2, c = i0 + (e & 3) * 8, n = rs + smin + row;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (n >= 0 && n < N && c < I) v = *(const uint4*)(x + (size_t)n * I + c);
-      *(uint4*)(xt + row * TW_XROW + (e & 3) * 16) = v;
-    }
-  };
-  for (int rs = r0; rs < r1; rs += TW_R) {
-    __syncthreads();  // previous stage's reads done
-    stage(rs);
-    __syncthreads();
-    if (!wave_on) continue;
-    const int nk = (min(TW_R, r1 - rs) + 31) >> 5;
-    for (int kb = 0; kb < nk; ++kb) {
-      Frag8 af;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int pr = kb * 32 + 16 * h + 4 * G + (li >> 2);  // permuted K row
-        af.h[h] = tr_read(gt + pr * TW_GROW + (16 * wave + 4 * (li & 3)) * 2);
-      }
-#pragma unroll
-      for (int t = 0; t < kMaxTaps; ++t) {
-        if (t < nt) {  // uniform; no early exit, so the loop unrolls and acc stays in registers
-          const int sh = xs.s[t] - smin;
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) {
-            Frag8 bf;
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-              const int pr = kb * 32 + 16 * h + 4 * G + (li >> 2) + sh;
-              bf.h[h] = tr_read(xt + pr * TW_XROW + (cb * 16 + 4 * (li & 3)) * 2);
-            }
-            acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bf.v, acc[t][cb], 0, 0, 0);
-          }
-        }
-      }
-    }
-  }
-  if (!wave_on) return;
-  // this part's rows: C layout row (W row) = o0 + 16 wave + 4 G + i, col = tap block + li
-  float* out = partial + (size_t)part * O * TI;
-#pragma unroll
-  for (int t = 0; t < kMaxTaps; ++t) {
-    if (t < nt) {
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const int ci = i0 + cb * 16 + li;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int o = o0 + 16 * wave + 4 * G + i;
-          if (o < O && ci < I) out[(size_t)o * TI + t * I + ci] = acc[t][cb][i];
-        }
-      }
-    }
-  }
-}
-
 // out[e] (+)= sum_p partial[p][e] over parts [y*pps, (y+1)*pps); `stage` set: write the
 // split sums to stage[y][e] for a second pass. 64 columns x 4 part-lanes per block.
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int nparts,
@@ -608,48 +503,4 @@ extern "C" int mbk_fc_wgrad_ex(const void* g, const void* x, int N, int O, int I
   xs.ntap = 1;
   xs.relu_x = relu_x;
   return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
-}
-
-// Shifted-row weight gradient: out fp32 [O][ntap * I], block t = sum_n g[n][:]^T x[n + shift_t][:]
-// (x rows outside [0, N) are zero). Scratch: (nparts + ceil(nparts / 32)) * O * ntap * I floats.
-extern "C" int mbk_fc_wgrad_taps(const void* g, const void* x, int N, int O, int I,
-                                 const int* shifts, int ntap, float* partial, int nparts,
-                                 float* out, int accumulate, hipStream_t stream) {
-  if (ntap < 1 || ntap > kMaxTaps) return (int)hipErrorInvalidValue;
-  XShifts xs{};
-  int smin = 0, smax = 0;
-  for (int t = 0; t < ntap; ++t) {
-    xs.s[t] = shifts[t];
-    smin = std::min(smin, shifts[t]);
-    smax = std::max(smax, shifts[t]);
-  }
-  xs.ntap = ntap;
-  static const bool all_taps = [] {  // MBK_WGRAD_TAPS=0: the per-chunk kernel (A/B)
-    const char* e = getenv("MBK_WGRAD_TAPS");
-    return !(e && e[0] == '0');
-  }();
-  if (!all_taps || ntap == 1 || O % 8 || I % 8 || smax - smin > 2 * TW_MAXH || N <= 0 ||
-      nparts < 1)
-    return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
-  const int stages = (N + TW_R - 1) / TW_R;
-  const int rpp = ((stages + nparts - 1) / nparts) * TW_R;
-  const int chunks = ((O + TW_OC - 1) / TW_OC) * ((I + TW_IC - 1) / TW_IC);
-  hipLaunchKernelGGL(wgrad_taps_kernel, dim3(chunks, nparts), dim3(kThreads), 0, stream,
-                     (const bf16*)g, (const bf16*)x, N, O, I, rpp, partial, xs);
-  const long row = (long)O * I * ntap;
-  const unsigned cols = (unsigned)((row + 63) / 64);
-  constexpr int kPps = 32;
-  if (nparts > 2 * kPps) {
-    const int splits = (nparts + kPps - 1) / kPps;
-    float* st = partial + (size_t)nparts * row;
-    hipLaunchKernelGGL(colsum_kernel, dim3(cols, splits), dim3(256), 0, stream,
-                       (const float*)partial, nparts, kPps, row, st, (float*)nullptr, 0);
-    hipLaunchKernelGGL(colsum_kernel, dim3(cols, 1), dim3(256), 0, stream, (const float*)st,
-                       splits, splits, row, (float*)nullptr, out, accumulate);
-  } else {
-    hipLaunchKernelGGL(colsum_kernel, dim3(cols, 1), dim3(256), 0, stream,
-                       (const float*)partial, nparts, nparts, row, (float*)nullptr, out,
-                       accumulate);
-  }
-  return (int)hipGetLastError();
 }

@@ -2,13 +2,13 @@
 // (+ relu), fp32 accumulation, bf16 or fp32 output (optionally accumulated into fp32 C).
 //
 // Both operands are K-contiguous ("NT"), the layout every caller here has natively:
-// Linear forward (x . W^T), its input gradient (g . W with W pre-transposed once per
-// call, a few hundred KB) and convolutions as im2col . W^T (GridNet). The weight
-// gradient (g^T x, K = batch) is the split-K kernel in fc.hip.
+// Linear forward (x . W^T) and its input gradient (g . W with W pre-transposed once per
+// call, a few hundred KB): the trunk tail's dX and GridNet's critic output layer. The weight
+// gradient (g^T x, K = batch) is the split-K kernel in fc.hip; GridNet's convolutions are
+// pixconv.hip.
 //
 // Tiling: 128 x 128 output tile per 256-thread workgroup (4 waves as 2 x 2, each 64 x 64 =
-// 4 x 4 MFMA tiles), or 256 x 64 / 256 x 32 for narrow N (GridNet's 32 / 64-channel layers;
-// waves stacked along M), K step 32, A / B tiles double-buffered in LDS with a 16-byte row pad
+// 4 x 4 MFMA tiles), or 256 x 64 / 256 x 32 for narrow N (waves stacked along M), K step 32, A / B tiles double-buffered in LDS with a 16-byte row pad
 // (conflict-free ds_read_b128 of the 8-element fragments). Global loads for step k+1 are
 // issued before the MFMAs of step k. Edges are zero-filled, so any M, N and K % 8 == 0 work.
 // blockIdx.x walks M (the large dimension in every use) and XCD-interleaves nothing: the
@@ -52,45 +52,11 @@ __device__ __forceinline__ void load_tile(const bf16* __restrict__ g, int rows, 
   }
 }
 
-// Shifted-row A operand ("implicit im2col"): K is split into ntap blocks of tk columns
-// (tk % 32 == 0, so a 32-wide K step never straddles two taps); block t reads row
-// m + shift[t] of its own matrix base[t] ([rows][lda], K-contiguous), zero outside [0, rows).
-// A 3x3 conv over a zero-padded NHWC grid is then ONE GEMM (tap shifts dy*Wp + dx), and a
-// stride-2 transposed conv is four sub-pixel phase GEMMs of 1 / 2 / 2 / 4 taps.
-constexpr int kMaxTaps = 9;
-struct ATaps {
-  const bf16* base[kMaxTaps];
-  int shift[kMaxTaps];
-  int ntap, tk;
-  // Output row remap (remap != 0): rows m = (b * Hp + y) * Wp + x of the padded input grid;
-  // border rows are dropped, interior rows go to output row
-  // b * ob + ((y - 1) * sy + oy0) * ow + (x - 1) * sx + ox0 -- a plain or padded NHWC
-  // output, or one stride-2 phase of a transposed conv's output, with no crop / scatter copy.
-  // Output pixels (Y, X) = ((y - 1) * sy + oy0, (x - 1) * sx + ox0) outside [0, lim_h) x
-  // [0, lim_w) are not written (crop). zero_border: border rows are not dropped but write
-  // zeros at their (Y, X), which fills the zero border of a padded output grid exactly
-  // (for a stride-2 transposed conv, across its 4 phases).
-  int remap, Hp, Wp, ob, ow, sy, sx, oy0, ox0, lim_h, lim_w, zero_border;
-  // optional relu-backward mask in the output's layout: C[o] = 0 where mask[o] <= 0
+// epilogue options: optional relu-backward mask in the output's layout (C[o] = 0 where
+// mask[o] <= 0)
+struct Epi {
   const bf16* mask;
 };
-
-template <int ROWS>
-__device__ __forceinline__ void load_tile_taps(const ATaps& t, int rows, int ld, int r0, int k0,
-                                               TileRegs<ROWS>& tr) {
-  const int tap = k0 / t.tk, kin = k0 - tap * t.tk;
-  const bf16* g = t.base[tap];
-  const int sh = t.shift[tap];
-#pragma unroll
-  for (int j = 0; j < TileRegs<ROWS>::kN; ++j) {
-    const int e = threadIdx.x + j * kThreads;
-    const int row = e >> 2, q = e & 3;
-    const int gr = r0 + row + sh;
-    tr.r[j] = (row < ROWS && gr >= 0 && gr < rows && tap < t.ntap)
-                  ? *(const uint4*)(g + (size_t)gr * ld + kin + q * 8)
-                  : make_uint4(0, 0, 0, 0);
-  }
-}
 
 template <int ROWS>
 __device__ __forceinline__ void store_tile(char* t, const TileRegs<ROWS>& tr) {
@@ -101,9 +67,9 @@ __device__ __forceinline__ void store_tile(char* t, const TileRegs<ROWS>& tr) {
   }
 }
 
-// Tile shapes: TN = 128 -> 128 x 128 tile, waves 2 x 2 of 64 x 64; TN = 64 / 32 (GridNet's
-// narrow layers) -> 256 x TN tile, waves stacked along M, 64 x TN each, so no MFMA work is
-// spent on padding columns.
+// Tile shapes: TN = 128 -> 128 x 128 tile, waves 2 x 2 of 64 x 64; TN = 64 / 32 (narrow N)
+// -> 256 x TN tile, waves stacked along M, 64 x TN each, so no MFMA work is spent on padding
+// columns.
 template <int TN_>
 struct Shape {
   static constexpr int TM = TN_ == 128 ? 128 : 256;
@@ -111,11 +77,11 @@ struct Shape {
   static constexpr int NJ = TN_ / WN / 16;      // 16-col MFMA tiles per wave
 };
 
-template <bool OUT_BF16, bool TAPS, int TN_>
+template <bool OUT_BF16, int TN_>
 __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     const bf16* __restrict__ A, const bf16* __restrict__ B, void* __restrict__ C,
     const float* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int relu,
-    int accumulate, ATaps taps, int vec_out) {
+    int accumulate, Epi epi, int vec_out) {
   using S = Shape<TN_>;
   constexpr int TM_ = S::TM, NJ = S::NJ;
   // A / B double buffers; the bf16 output tile of the vectorised epilogue reuses them
@@ -135,8 +101,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   TileRegs<TM_> ra;
   TileRegs<TN_> rb;
-  if (TAPS) load_tile_taps<TM_>(taps, M, lda, m0, 0, ra);
-  else load_tile<TM_>(A, M, lda, m0, 0, K, ra);
+  load_tile<TM_>(A, M, lda, m0, 0, K, ra);
   load_tile<TN_>(B, N, ldb, n0, 0, K, rb);
   store_tile<TM_>(sa[0], ra);
   store_tile<TN_>(sb[0], rb);
@@ -145,8 +110,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
   for (int kk = 0; kk < nk; ++kk) {
     const int cur = kk & 1;
     if (kk + 1 < nk) {  // prefetch the next K step into registers
-      if (TAPS) load_tile_taps<TM_>(taps, M, lda, m0, (kk + 1) * TK, ra);
-      else load_tile<TM_>(A, M, lda, m0, (kk + 1) * TK, K, ra);
+      load_tile<TM_>(A, M, lda, m0, (kk + 1) * TK, K, ra);
       load_tile<TN_>(B, N, ldb, n0, (kk + 1) * TK, K, rb);
     }
     const char* ta = sa[cur];
@@ -169,7 +133,7 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     }
     __syncthreads();
   }
-  if constexpr (OUT_BF16 && !TAPS) {
+  if constexpr (OUT_BF16) {
     if (vec_out) {
       // bf16 output through an LDS tile: 16-byte mask loads and C stores (the per-element
       // form issued 2-byte loads / stores, 64 of each per lane: the masked dX GEMM of
@@ -195,8 +159,8 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
         if (row >= M || col >= N) continue;
         uint4 v = *(const uint4*)(sab + trow * OROW + c8 * 16);
         const size_t o = (size_t)row * ldc + col;
-        if (taps.mask) {
-          const uint4 mk = *(const uint4*)(taps.mask + o);
+        if (epi.mask) {
+          const uint4 mk = *(const uint4*)(epi.mask + o);
           const uint32_t mw[4] = {mk.x, mk.y, mk.z, mk.w};
           uint32_t vw[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -219,26 +183,15 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     for (int r = 0; r < 4; ++r) {
       const int row = m0 + wm * 64 + i * 16 + 4 * g + r;
       if (row >= M) continue;
-      size_t orow = row;
-      bool zero = false;
-      if (TAPS && taps.remap) {
-        const int x = row % taps.Wp, t = row / taps.Wp;
-        const int y = t % taps.Hp, b = t / taps.Hp;
-        zero = y == 0 || y == taps.Hp - 1 || x == 0 || x == taps.Wp - 1;
-        if (zero && !taps.zero_border) continue;
-        const int Y = (y - 1) * taps.sy + taps.oy0, X = (x - 1) * taps.sx + taps.ox0;
-        if (Y < 0 || Y >= taps.lim_h || X < 0 || X >= taps.lim_w) continue;
-        orow = (size_t)b * taps.ob + (size_t)Y * taps.ow + X;
-      }
+      const size_t orow = row;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int col = n0 + wn * NJ * 16 + j * 16 + li;
         if (col >= N) continue;
         float v = acc[i][j][r] + (bias ? bias[col] : 0.f);
         if (relu) v = fmaxf(v, 0.f);
-        if (zero) v = 0.f;
         const size_t o = orow * ldc + col;
-        if (taps.mask && !(__bfloat162float(taps.mask[o]) > 0.f)) v = 0.f;
+        if (epi.mask && !(__bfloat162float(epi.mask[o]) > 0.f)) v = 0.f;
         if (OUT_BF16) {
           ((bf16*)C)[o] = __float2bfloat16(v);
         } else {
@@ -249,35 +202,34 @@ __global__ __launch_bounds__(kThreads) void gemm_nt_kernel(
     }
 }
 
-template <bool TAPS, int TN_>
+template <int TN_>
 void launch(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
-            int lda, int ldb, int ldc, int relu, int out_bf16, int accumulate, const ATaps& t,
+            int lda, int ldb, int ldc, int relu, int out_bf16, int accumulate, const Epi& t,
             hipStream_t stream) {
   dim3 grid((M + Shape<TN_>::TM - 1) / Shape<TN_>::TM, (N + TN_ - 1) / TN_);
   // 16-byte output rows (and mask rows) for the vectorised bf16 epilogue
-  const int vec = (!TAPS && out_bf16 && N % 8 == 0 && ldc % 8 == 0 &&
+  const int vec = (out_bf16 && N % 8 == 0 && ldc % 8 == 0 &&
                    ((uintptr_t)C & 15) == 0 && ((uintptr_t)t.mask & 15) == 0) ? 1 : 0;
   if (out_bf16)
-    hipLaunchKernelGGL((gemm_nt_kernel<true, TAPS, TN_>), grid, dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((gemm_nt_kernel<true, TN_>), grid, dim3(kThreads), 0, stream,
                        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu, 0,
                        t, vec);
   else
-    hipLaunchKernelGGL((gemm_nt_kernel<false, TAPS, TN_>), grid, dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL((gemm_nt_kernel<false, TN_>), grid, dim3(kThreads), 0, stream,
                        (const bf16*)A, (const bf16*)B, C, bias, M, N, K, lda, ldb, ldc, relu,
                        accumulate, t, 0);
 }
 
 // narrowest tile that covers N (N = 78 -> one 128-wide tile rather than two of 64)
-template <bool TAPS>
 void launch_any(const void* A, const void* B, void* C, const float* bias, int M, int N, int K,
                 int lda, int ldb, int ldc, int relu, int out_bf16, int accumulate,
-                const ATaps& t, hipStream_t stream) {
+                const Epi& t, hipStream_t stream) {
   if (N <= 32)
-    launch<TAPS, 32>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
+    launch<32>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
   else if (N <= 64)
-    launch<TAPS, 64>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
+    launch<64>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
   else
-    launch<TAPS, 128>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
+    launch<128>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, t, stream);
 }
 
 }  // namespace
@@ -289,8 +241,8 @@ extern "C" int mbk_gemm_nt(const void* A, const void* B, void* C, const float* b
                            int accumulate, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % 8 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
-  ATaps none{};
-  launch_any<false>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, none,
+  Epi none{};
+  launch_any(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, accumulate, none,
                     stream);
   return (int)hipGetLastError();
 }
@@ -302,37 +254,8 @@ extern "C" int mbk_gemm_nt_mask(const void* A, const void* B, void* C, const flo
                                 const void* mask, hipStream_t stream) {
   if (M <= 0 || N <= 0) return 0;
   if (K <= 0 || K % 8 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
-  ATaps t{};
+  Epi t{};
   t.mask = (const bf16*)mask;
-  launch_any<false>(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, 0, t, stream);
-  return (int)hipGetLastError();
-}
-
-// Shifted-row ("implicit im2col") GEMM: C[M][N] = sum_t A_t[m + shift_t][:] . B[:, t*tk ...]^T
-// A_t: bases[t] [M][lda] bf16 (rows outside [0, M) read as zero), tk % 32 == 0,
-// B: [N][ntap*tk] bf16 (tap-major K).
-// remap: null, or 11 ints {Hp, Wp, ob, ow, sy, sx, oy0, ox0, lim_h, lim_w, zero_border}
-// (see ATaps)
-extern "C" int mbk_gemm_nt_taps(const void* const* bases, const int* shifts, int ntap, int tk,
-                                const void* B, void* C, const float* bias, int M, int N, int lda,
-                                int ldb, int ldc, int relu, int out_bf16, int accumulate,
-                                const int* remap, hipStream_t stream) {
-  if (M <= 0 || N <= 0) return 0;
-  if (ntap < 1 || ntap > kMaxTaps || tk % 32 || lda % 8 || ldb % 8) return (int)hipErrorInvalidValue;
-  ATaps t{};
-  for (int i = 0; i < ntap; ++i) {
-    t.base[i] = (const bf16*)bases[i];
-    t.shift[i] = shifts[i];
-  }
-  t.ntap = ntap;
-  t.tk = tk;
-  if (remap) {
-    t.remap = 1;
-    t.Hp = remap[0], t.Wp = remap[1], t.ob = remap[2], t.ow = remap[3];
-    t.sy = remap[4], t.sx = remap[5], t.oy0 = remap[6], t.ox0 = remap[7];
-    t.lim_h = remap[8], t.lim_w = remap[9], t.zero_border = remap[10];
-  }
-  launch_any<true>(nullptr, B, C, bias, M, N, ntap * tk, lda, ldb, ldc, relu, out_bf16,
-                   accumulate, t, stream);
+  launch_any(A, B, C, bias, M, N, K, lda, ldb, ldc, relu, out_bf16, 0, t, stream);
   return (int)hipGetLastError();
 }

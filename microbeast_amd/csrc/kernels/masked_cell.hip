@@ -29,14 +29,24 @@ __device__ __forceinline__ float ld<__hip_bfloat16>(const __hip_bfloat16* p) {
 // logit read in cell_forward / cell_backward (log-prob 0, entropy 0, gradient 0 exactly), and
 // on real states ~1-5 % of cells are active, so the tile's logits (156 B per cell in bf16) are
 // read for those rows only. am: the tile's active-cell ballot (one wave per tile).
+// Logits layout: cell c = (sample, cell-of-map) -> row; element j of the cell at row * ld + j.
+// Cell-major (pbc_n == 0): row = c, ld = 78. Pixel-major GridNet logits (pbc_n = images):
+// [cell-of-map][image][ld] (ops/pixconv.py), row = (c % cps) * pbc_n + c / cps.
+struct Lay {
+  int cps, pbc_n, ld;
+  __device__ __forceinline__ int64_t row(int64_t c) const {
+    return pbc_n ? (c % cps) * pbc_n + c / cps : c;
+  }
+};
+
 template <typename TZ>
 __device__ __forceinline__ void stage_active(const TZ* __restrict__ logits, int64_t c0,
-                                             uint64_t am, float* zs) {
+                                             uint64_t am, float* zs, Lay L) {
   const int lane = threadIdx.x;
   while (am) {
     const int r = __builtin_ctzll(am);
     am &= am - 1;
-    const TZ* src = logits + (c0 + r) * kCell;
+    const TZ* src = logits + L.row(c0 + r) * L.ld;
     zs[r * kRow + lane] = ld(src + lane);
     if (lane < kCell - 64) zs[r * kRow + 64 + lane] = ld(src + 64 + lane);
   }
@@ -46,7 +56,7 @@ template <typename TZ>
 __global__ __launch_bounds__(kTile) void masked_cell_fwd_kernel(
     const TZ* __restrict__ logits, const uint32_t* __restrict__ mask, uint8_t* __restrict__ action,
     const uint64_t* __restrict__ rng, int sample, int64_t ncells, float* __restrict__ cell_logp,
-    float* __restrict__ cell_ent) {
+    float* __restrict__ cell_ent, Lay L) {
   __shared__ float zs[kTile * kRow];
   const int64_t c0 = (int64_t)blockIdx.x * kTile;
   const int nc = (int)min((int64_t)kTile, ncells - c0);
@@ -54,7 +64,7 @@ __global__ __launch_bounds__(kTile) void masked_cell_fwd_kernel(
   const int64_t cell = c0 + i;
   uint32_t m[3] = {0u, 0u, 0u};
   if (i < nc) { m[0] = mask[cell * 3 + 0]; m[1] = mask[cell * 3 + 1]; m[2] = mask[cell * 3 + 2]; }
-  stage_active(logits, c0, __ballot((m[0] | m[1] | m[2]) != 0u), zs);
+  stage_active(logits, c0, __ballot((m[0] | m[1] | m[2]) != 0u), zs, L);
   __syncthreads();
   if (i >= nc) return;
   uint8_t a[kComps];
@@ -86,7 +96,7 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
     const TZ* __restrict__ logits, const uint32_t* __restrict__ mask,
     const uint8_t* __restrict__ action, const float* __restrict__ g_logp,
     const float* __restrict__ g_ent, int cells_per_sample, int64_t ncells,
-    TD* __restrict__ dlogits) {
+    TD* __restrict__ dlogits, Lay L) {
   __shared__ float zs[kTile * kRow];
   const int64_t c0 = (int64_t)blockIdx.x * kTile;
   const int nc = (int)min((int64_t)kTile, ncells - c0);
@@ -97,7 +107,7 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
     m[0] = mask[cell * 3 + 0]; m[1] = mask[cell * 3 + 1]; m[2] = mask[cell * 3 + 2];
   }
   const uint64_t am = __ballot((m[0] | m[1] | m[2]) != 0u);
-  stage_active(logits, c0, am, zs);
+  stage_active(logits, c0, am, zs, L);
   __syncthreads();
   if (i < nc && ((am >> i) & 1ull)) {
     const int64_t cell = c0 + i;
@@ -110,12 +120,22 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
     cell_backward(row, m, a, g_logp[smp], g_ent ? g_ent[smp] : 0.f, row);
   }
   __syncthreads();
-  // every cell's 78 gradients are written: inactive rows are exactly zero (not staged)
-  const int64_t base = c0 * kCell;
-  const int total = nc * kCell;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int r = e / kCell, c = e - r * kCell;
-    dlogits[base + e] = (TD)(((am >> r) & 1ull) ? zs[r * kRow + c] : 0.f);
+  // every cell's gradients are written (ld columns: 78 + zero padding): inactive rows are
+  // exactly zero (not staged)
+  if (!L.pbc_n) {
+    const int64_t base = c0 * kCell;
+    const int total = nc * kCell;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int r = e / kCell, c = e - r * kCell;
+      dlogits[base + e] = (TD)(((am >> r) & 1ull) ? zs[r * kRow + c] : 0.f);
+    }
+  } else {
+    const int total = nc * L.ld;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int r = e / L.ld, c = e - r * L.ld;
+      dlogits[L.row(c0 + r) * L.ld + c] =
+          (TD)((c < kCell && ((am >> r) & 1ull)) ? zs[r * kRow + c] : 0.f);
+    }
   }
 }
 
@@ -145,10 +165,39 @@ extern "C" int mbk_masked_cell_fwd(const void* logits, int logits_bf16, const ui
   if (logits_bf16)
     hipLaunchKernelGGL(masked_cell_fwd_kernel<__hip_bfloat16>, grid, dim3(kTile), 0, stream,
                        (const __hip_bfloat16*)logits, mask, action, rng, sample, ncells, cell_logp,
-                       cell_ent);
+                       cell_ent, Lay{1, 0, kCell});
   else
     hipLaunchKernelGGL(masked_cell_fwd_kernel<float>, grid, dim3(kTile), 0, stream,
-                       (const float*)logits, mask, action, rng, sample, ncells, cell_logp, cell_ent);
+                       (const float*)logits, mask, action, rng, sample, ncells, cell_logp, cell_ent,
+                       Lay{1, 0, kCell});
+  return (int)hipGetLastError();
+}
+
+// pixel-major bf16 logits [cps][n][ld] (cell c of sample s at row (c % cps) * n + s)
+extern "C" int mbk_masked_cell_fwd_pbc(const void* logits, int cps, int n, int ld,
+                                       const uint32_t* mask, uint8_t* action, const uint64_t* rng,
+                                       int sample, int64_t ncells, float* cell_logp,
+                                       float* cell_ent, hipStream_t stream) {
+  if (ncells <= 0) return 0;
+  if (ld < kCell || ncells != (int64_t)cps * n) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((ncells + kTile - 1) / kTile));
+  hipLaunchKernelGGL(masked_cell_fwd_kernel<__hip_bfloat16>, grid, dim3(kTile), 0, stream,
+                     (const __hip_bfloat16*)logits, mask, action, rng, sample, ncells, cell_logp,
+                     cell_ent, Lay{cps, n, ld});
+  return (int)hipGetLastError();
+}
+
+// gradient of the pixel-major logits, written in the same layout (padding columns zero)
+extern "C" int mbk_masked_cell_bwd_pbc(const void* logits, int cps, int n, int ld,
+                                       const uint32_t* mask, const uint8_t* action,
+                                       const float* g_logp, const float* g_ent, int64_t ncells,
+                                       void* dlogits, hipStream_t stream) {
+  if (ncells <= 0) return 0;
+  if (ld < kCell || ncells != (int64_t)cps * n) return (int)hipErrorInvalidValue;
+  dim3 grid((unsigned)((ncells + kTile - 1) / kTile));
+  hipLaunchKernelGGL((masked_cell_bwd_kernel<__hip_bfloat16, __hip_bfloat16>), grid, dim3(kTile),
+                     0, stream, (const __hip_bfloat16*)logits, mask, action, g_logp, g_ent, cps,
+                     ncells, (__hip_bfloat16*)dlogits, Lay{cps, n, ld});
   return (int)hipGetLastError();
 }
 
@@ -160,7 +209,7 @@ extern "C" int mbk_masked_cell_bwd(const void* logits, int logits_bf16, const ui
 #define MBK_BWD(TZ, TD)                                                                        \
   hipLaunchKernelGGL((masked_cell_bwd_kernel<TZ, TD>), grid, dim3(kTile), 0, stream,           \
                      (const TZ*)logits, mask, action, g_logp, g_ent, cells_per_sample, ncells, \
-                     (TD*)dlogits)
+                     (TD*)dlogits, Lay{1, 0, kCell})
   if (logits_bf16 && dlogits_bf16) MBK_BWD(__hip_bfloat16, __hip_bfloat16);
   else if (logits_bf16) MBK_BWD(__hip_bfloat16, float);
   else if (dlogits_bf16) MBK_BWD(float, __hip_bfloat16);

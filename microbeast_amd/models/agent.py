@@ -31,7 +31,7 @@ from ..ops.encoder import HipEncoder, encode, encoder_params
 from ..ops.head import SparseHead, sparse_sample, sparse_score
 from ..ops.linear import linear, nhwc_weight
 from ..ops.obs import bits_to_planes, dense_to_bits
-from ..ops.gridconv import map_gather
+from ..ops.pixconv import map_gather
 from ..ops.tail import TailMaps, impala_tail
 
 HIP_CHANNELS = (16, 32)  # conv widths the HIP trunk kernels are instantiated for

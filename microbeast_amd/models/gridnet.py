@@ -17,7 +17,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import cell_head
-from ..ops.gridconv import GridPlan, gridnet_forward
+from ..ops.pixconv import PixPlan, gridnet_pbc, pbc_to_cell_major
 from ..ops.obs import bits_to_planes
 from .agent import layer_init
 
@@ -72,26 +72,28 @@ class GridNetAgent(nn.Module):
     def _use_hip(self, obs) -> bool:
         return self.hip_kernels and obs.dtype == torch.int32 and (obs.is_cuda or self.emulate)
 
-    def _plan(self, device) -> GridPlan:
-        if self._grid_plan is None or self._grid_plan.device != device:
+    def _plan(self, device) -> PixPlan:
+        if self._grid_plan is None or self._grid_plan.device != torch.device(device):
             convs = [self.encoder[i] for i in (0, 3, 6, 9)]
             convts = [self.actor[i] for i in (0, 2, 4, 6)]
-            self._grid_plan = GridPlan(convs, convts, self.critic[1], self.critic[3],
-                                       (self.ph // 16, self.pw // 16, 256), device)
+            self._grid_plan = PixPlan(convs, convts, self.critic[1], self.critic[3], self.ph,
+                                      self.pw, (self.h, self.w), device)
         return self._grid_plan
 
-    def _policy_value_hip(self, obs, n_logits=None):
-        """The whole network on padded NHWC grids (ops/gridconv.py): MFMA GEMMs + the
-        gridnet.hip data-movement kernels, no ATen kernel. relu(maxpool(conv)) is computed as
-        maxpool(relu-fused conv): identical values. Logits are bf16 and cell-major, cropped
-        to the map by the last GEMM's epilogue, and go to the masked-cell kernels as they are."""
+    def policy_value_pbc(self, obs, n_logits=None):
+        """The whole network on the pixel-major layout (ops/pixconv.py, pixconv.hip): per
+        output-pixel MFMA GEMMs with no padded halo, no ATen kernel. relu(maxpool(conv)) is
+        computed as maxpool(relu-fused conv): identical values. Returns (logits [h*w][n_s][96]
+        bf16 pixel-major -- what the masked-cell kernels read as they are --, value fp32 [n]);
+        the decoder runs on the first n_logits observations only."""
         n = obs.numel() // (self.h * self.w)
-        return gridnet_forward(self._plan(obs.device), obs.reshape(n, self.h * self.w),
-                               self.h, self.w, self.ph, self.pw, n_logits)
+        return gridnet_pbc(self._plan(obs.device), obs.reshape(n, self.h * self.w),
+                           self.h, self.w, self.ph, self.pw, n_logits)
 
     def policy_value(self, obs):
         if self._use_hip(obs):
-            return self._policy_value_hip(obs)
+            lg, v = self.policy_value_pbc(obs)
+            return pbc_to_cell_major(lg), v
         x = self._planes(obs)
         with self._autocast(x):
             z = self.encoder(x)
@@ -104,17 +106,24 @@ class GridNetAgent(nn.Module):
         return tuple()
 
     @torch.no_grad()
-    def act(self, obs, mask_bits, rng_state=None, generator=None):
+    def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
+            cell_logp=None, logp_out=None):
+        if self._use_hip(obs):
+            lg, value = self.policy_value_pbc(obs)
+            action, logp = cell_head.sample_pbc(lg, mask_bits, rng_state, generator, action_out,
+                                                cell_logp, logp_out)
+            return action, logp, value
         logits, value = self.policy_value(obs)
         action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)
         return action, logp, value
 
     def evaluate(self, obs, mask_bits, action, n_score: int | None = None):
-        if self._use_hip(obs):  # logits of the scored rows only (no slice-backward copy)
-            logits, value = self._policy_value_hip(obs, n_score)
-        else:
-            logits, value = self.policy_value(obs)
-            if n_score is not None:
-                logits = logits[:n_score]
+        if self._use_hip(obs):  # logits of the scored rows only
+            lg, value = self.policy_value_pbc(obs, n_score)
+            logp, ent = cell_head.score_pbc(lg, mask_bits, action)
+            return logp, ent, value
+        logits, value = self.policy_value(obs)
+        if n_score is not None:
+            logits = logits[:n_score]
         logp, ent = cell_head.score(logits, mask_bits, action)
         return logp, ent, value

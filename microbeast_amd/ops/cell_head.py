@@ -149,6 +149,94 @@ class _ScoreGPU(torch.autograd.Function):
         return d, None, None
 
 
+# ---------------------------------------------------------------- pixel-major logits
+# GridNet's decoder writes its logits pixel-major, [cell-of-map][sample][ld] bf16 (ld >= 78,
+# ops/pixconv.py); these run the same masked-cell kernels with that row mapping, and the
+# backward writes the logit gradient in the same layout (padding columns zero), which is the
+# decoder backward's A operand as it is.
+def _pbc_cm(logits: torch.Tensor) -> torch.Tensor:
+    S, n = logits.shape[:2]
+    return logits[:, :, :CELL].float().permute(1, 0, 2).reshape(n, S * CELL)
+
+
+class _ScorePBC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, mask_bits, action):
+        k = N.kernels()
+        S, n, ld = logits.shape
+        nc = S * n
+        dev = logits.device
+        assert logits.dtype == torch.bfloat16 and logits.is_contiguous()
+        assert mask_bits.numel() == nc * 3 and action.numel() == nc * COMPS
+        cl = torch.empty(nc, dtype=torch.float32, device=dev)
+        ce = torch.empty(nc, dtype=torch.float32, device=dev)
+        st = N.stream_ptr()
+        N.check(k.mbk_masked_cell_fwd_pbc(logits.data_ptr(), S, n, ld, mask_bits.data_ptr(),
+                                          action.data_ptr(), None, 0, nc, cl.data_ptr(),
+                                          ce.data_ptr(), st), "masked_cell_fwd_pbc")
+        logp = torch.empty(n, dtype=torch.float32, device=dev)
+        ent = torch.empty(n, dtype=torch.float32, device=dev)
+        N.check(k.mbk_row_sum(cl.data_ptr(), n, S, logp.data_ptr(), st), "row_sum")
+        N.check(k.mbk_row_sum(ce.data_ptr(), n, S, ent.data_ptr(), st), "row_sum")
+        ctx.save_for_backward(logits, mask_bits, action)
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        logits, mask_bits, action = ctx.saved_tensors
+        k = N.kernels()
+        S, n, ld = logits.shape
+        if g_logp is None:
+            g_logp = torch.zeros(n, device=logits.device)
+        if g_ent is None:
+            g_ent = torch.zeros(n, device=logits.device)
+        g_logp = g_logp.float().contiguous()
+        g_ent = g_ent.float().contiguous()
+        d = torch.empty_like(logits)
+        N.check(k.mbk_masked_cell_bwd_pbc(logits.data_ptr(), S, n, ld, mask_bits.data_ptr(),
+                                          action.data_ptr(), g_logp.data_ptr(), g_ent.data_ptr(),
+                                          S * n, d.data_ptr(), N.stream_ptr()),
+                "masked_cell_bwd_pbc")
+        return d, None, None
+
+
+def score_pbc(logits: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor):
+    """(logp [n], entropy [n]) of pixel-major logits [S][n][ld], differentiable in them."""
+    if logits.is_cuda:
+        return _ScorePBC.apply(logits, mask_bits.contiguous(), action.contiguous())
+    _, lp, ent = cell_head_torch(_pbc_cm(logits), mask_bits, action)
+    return lp, ent
+
+
+def sample_pbc(logits: torch.Tensor, mask_bits: torch.Tensor, rng_state: torch.Tensor | None = None,
+               generator: torch.Generator | None = None, action_out=None, cell_logp=None,
+               logp_out=None):
+    """(action [n,S,7] uint8, logp [n]) sampled from pixel-major logits [S][n][ld]."""
+    S, n, ld = logits.shape
+    if not logits.is_cuda:
+        with torch.no_grad():
+            a, lp, _ = cell_head_torch(_pbc_cm(logits), mask_bits, None, generator)
+        return a, lp
+    k = N.kernels()
+    nc = S * n
+    dev = logits.device
+    assert logits.dtype == torch.bfloat16 and logits.is_contiguous()
+    if action_out is None:
+        action_out = torch.empty(n, S, COMPS, dtype=torch.uint8, device=dev)
+    if cell_logp is None:
+        cell_logp = torch.empty(nc, dtype=torch.float32, device=dev)
+    if logp_out is None:
+        logp_out = torch.empty(n, dtype=torch.float32, device=dev)
+    assert action_out.numel() == nc * COMPS and cell_logp.numel() >= nc
+    st = N.stream_ptr()
+    N.check(k.mbk_masked_cell_fwd_pbc(logits.data_ptr(), S, n, ld, mask_bits.contiguous().data_ptr(),
+                                      action_out.data_ptr(), rng_state.data_ptr(), 1, nc,
+                                      cell_logp.data_ptr(), None, st), "masked_cell_fwd_pbc")
+    N.check(k.mbk_row_sum_rng(cell_logp.data_ptr(), n, S, logp_out.data_ptr(),
+                              rng_state.data_ptr(), st), "row_sum_rng")
+    return action_out, logp_out
+
+
 def score(logits: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor):
     """(logp [N], entropy [N]) of given actions, differentiable in logits."""
     if logits.is_cuda:

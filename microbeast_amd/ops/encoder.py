@@ -194,7 +194,7 @@ class HipEncoder:
 
     def pack_layer(self, i: int, weight: torch.Tensor, with_bwd: bool = False) -> None:
         """Pack layer i's fp32 weight only (GridNet's first layer uses this encoder's stage-0
-        conv alone, ops/gridconv.py)."""
+        conv alone, ops/pixconv.py)."""
         L = self.layers[i]
         assert weight.dtype == torch.float32 and weight.is_contiguous()
         bwd = ((self.packed_bwd.data_ptr() + 2 * L.wb_off)

@@ -23,7 +23,7 @@ import os
 import torch
 
 from .. import _native as N
-from .gridconv import colsum, critic_maps, map_gather, value_bwd
+from .pixconv import colsum, map_gather, value_bwd
 from .optim import grad_out
 
 _BF = torch.bfloat16
@@ -31,12 +31,31 @@ _BF = torch.bfloat16
 _FUSED_DX_VALUE = os.environ.get("MBK_FUSED_DX_VALUE", "1") == "1"
 
 
+def nhwc_linear_maps(k1: int, c: int, hh: int, ww: int):
+    """Linear(c*hh*ww -> k1) on an NHWC-flattened input, reference NCHW flatten of the weight
+    [k1, c*hh*ww]: fwd B [k1, hh*ww*c] (NHWC columns), dgrad B [hh*ww*c, k1], grad map
+    [k1*c*hh*ww] from the NHWC-ordered dW (int32 index maps)."""
+    f = c * hh * ww
+    k = torch.arange(k1).view(-1, 1, 1, 1)
+    y = torch.arange(hh).view(1, -1, 1, 1)
+    x = torch.arange(ww).view(1, 1, -1, 1)
+    ch = torch.arange(c).view(1, 1, 1, -1)
+    fwd = (k * f + ch * hh * ww + y * ww + x).reshape(k1, -1)         # [k1, hh, ww, c]
+    dgrad = fwd.t().contiguous()
+    kk = torch.arange(k1).view(-1, 1, 1, 1)
+    cc = torch.arange(c).view(1, -1, 1, 1)
+    yy = torch.arange(hh).view(1, 1, -1, 1)
+    xx = torch.arange(ww).view(1, 1, 1, -1)
+    grad = (kk * f + (yy * ww + xx) * c + cc).reshape(-1)            # dst (k, c, y, x)
+    return fwd.int(), dgrad.int(), grad.int()
+
+
 class TailMaps:
     """index maps of network.5's weight: NHWC-permuted fwd operand, its transpose (dgrad
     operand) and the NHWC dW -> parameter-layout map"""
 
     def __init__(self, out_features: int, c: int, ho: int, wo: int, device):
-        fwd, dgrad, grad = critic_maps(out_features, c, ho, wo)
+        fwd, dgrad, grad = nhwc_linear_maps(out_features, c, ho, wo)
         self.fwd, self.dgrad, self.grad = fwd.to(device), dgrad.to(device), grad.to(device)
         self.device = torch.device(device)
         self.key = (out_features, c, ho, wo)

@@ -27,6 +27,7 @@ import torch
 
 from .. import _native as N
 from ..ops import act as act_ops
+from ..ops.pixconv import pbc_to_cell_major
 from ..ops import cell_head
 from ..ops.copy import zeros
 from ..ops.optim import FlatParams
@@ -98,11 +99,19 @@ def graph_policy_step(io: dict, m, rng: torch.Tensor, E: int, size: int, device)
         N.check(k.mbk_decode_obs_mask(io["in_codes"].data_ptr(), io["in_res"].data_ptr(),
                                       E, size, size, io["in_obs"].data_ptr(),
                                       io["in_mask"].data_ptr(), st), "decode_obs_mask")
-        logits, value = m.policy_value(io["in_obs"])
-        if "out_logits" in io:
-            io["out_logits"].copy_(logits.reshape(io["out_logits"].shape))
-        cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
-                             cell_logp=io["cell_logp"], logp_out=io["out_logp"])
+        if hasattr(m, "policy_value_pbc") and m._use_hip(io["in_obs"]):
+            # GridNet: pixel-major logits straight into the masked-cell sampler
+            logits, value = m.policy_value_pbc(io["in_obs"])
+            if "out_logits" in io:
+                io["out_logits"].copy_(pbc_to_cell_major(logits).reshape(io["out_logits"].shape))
+            cell_head.sample_pbc(logits, io["in_mask"], rng, action_out=io["out_action"],
+                                 cell_logp=io["cell_logp"], logp_out=io["out_logp"])
+        else:
+            logits, value = m.policy_value(io["in_obs"])
+            if "out_logits" in io:
+                io["out_logits"].copy_(logits.reshape(io["out_logits"].shape))
+            cell_head.sample_gpu(logits, io["in_mask"], rng, action_out=io["out_action"],
+                                 cell_logp=io["cell_logp"], logp_out=io["out_logp"])
     if value.data_ptr() != io["out_value"].data_ptr():  # (written in place when fused)
         io["out_value"].copy_(value.view(-1))
     if not packed:

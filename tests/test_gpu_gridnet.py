@@ -1,4 +1,4 @@
-"""GridNet on the hand-written MFMA GEMM (ops/gridconv.py) vs the same model's PyTorch
+"""GridNet on the pixel-major HIP kernels (ops/pixconv.py) vs the same model's PyTorch
 path (fp32 reference with bf16-rounded weights): logits, value and gradients."""
 import copy
 
