@@ -129,12 +129,22 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
       const int r = e / kCell, c = e - r * kCell;
       dlogits[base + e] = (TD)(((am >> r) & 1ull) ? zs[r * kRow + c] : 0.f);
     }
-  } else {
-    const int total = nc * L.ld;
+  } else if constexpr (sizeof(TD) == 2) {
+    // pixel-major rows (ld % 8 == 0): 16-byte stores of 8 bf16, zero rows / padding unread
+    const int c8n = L.ld / 8, total = nc * c8n;
     for (int e = threadIdx.x; e < total; e += blockDim.x) {
-      const int r = e / L.ld, c = e - r * L.ld;
-      dlogits[L.row(c0 + r) * L.ld + c] =
-          (TD)((c < kCell && ((am >> r) & 1ull)) ? zs[r * kRow + c] : 0.f);
+      const int r = e / c8n, c8 = e - r * c8n;
+      const bool on = (am >> r) & 1ull;
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = c8 * 8 + 2 * q;
+        const float lo = (on && c < kCell) ? zs[r * kRow + c] : 0.f;
+        const float hi = (on && c + 1 < kCell) ? zs[r * kRow + c + 1] : 0.f;
+        w[q] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(lo)) |
+               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hi)) << 16);
+      }
+      *(uint4*)(dlogits + L.row(c0 + r) * L.ld + c8 * 8) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
 }
@@ -193,7 +203,8 @@ extern "C" int mbk_masked_cell_bwd_pbc(const void* logits, int cps, int n, int l
                                        const float* g_logp, const float* g_ent, int64_t ncells,
                                        void* dlogits, hipStream_t stream) {
   if (ncells <= 0) return 0;
-  if (ld < kCell || ncells != (int64_t)cps * n) return (int)hipErrorInvalidValue;
+  if (ld < kCell || ld % 8 || ((uintptr_t)dlogits & 15) || ncells != (int64_t)cps * n)
+    return (int)hipErrorInvalidValue;
   dim3 grid((unsigned)((ncells + kTile - 1) / kTile));
   hipLaunchKernelGGL((masked_cell_bwd_kernel<__hip_bfloat16, __hip_bfloat16>), grid, dim3(kTile),
                      0, stream, (const __hip_bfloat16*)logits, mask, action, g_logp, g_ent, cps,

@@ -1,9 +1,14 @@
+# GridNet (BASELINE config 2) check on the GPU box: pixconv tests, learner-only update time,
+# policy-step graph time, the engine bench at 10x10, a kernel profile of one learner update.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_pixconv.py tests/test_gpu_gridnet.py -x -v --timeout 200 --timeout-method thread > gpurun_out/gn1_pytest.log 2>&1; rc=$?
-tail -25 gpurun_out/gn1_pytest.log
-if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 200 python tools/learner_only.py --arch gridnet --size 10 --steps 3 > gpurun_out/gn1_lt.log 2>&1 || exit $?
-cat gpurun_out/gn1_lt.log
-bash tools/prof.sh gn1_prof tools/learner_only.py --arch gridnet --size 10 --steps 2 || exit $?
-head -30 gpurun_out/gn1_prof_summary.md
+tag=${1:-gn}
+timeout -k 10 400 python -u -m pytest tests/test_gpu_pixconv.py tests/test_gpu_gridnet.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${tag}_pytest.log 2>&1 || { tail -30 gpurun_out/${tag}_pytest.log; exit 1; }
+tail -2 gpurun_out/${tag}_pytest.log
+timeout -k 10 200 python tools/learner_only.py --arch gridnet --size 10 --steps 3 > gpurun_out/${tag}_lt.log 2>&1 || exit $?
+cat gpurun_out/${tag}_lt.log
+timeout -k 10 200 python tools/microbench.py --arch gridnet --size 10 --E 8192 --iters 20 --no_learner > gpurun_out/${tag}_micro.log 2>&1 || exit $?
+grep '"what"' gpurun_out/${tag}_micro.log
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --size 10 --arch gridnet > gpurun_out/${tag}_bench.log 2>&1 || exit $?
+tail -1 gpurun_out/${tag}_bench.log | cut -c1-300
+MBK_PROF_SEQ=120 bash tools/prof.sh ${tag}_prof tools/learner_only.py --arch gridnet --size 10 --steps 1 || exit $?

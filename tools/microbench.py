@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--size", type=int, default=16)
+    p.add_argument("--arch", default="impala_flat", help="impala_flat | gridnet")
     p.add_argument("--E", type=str, default="256,1024")
     p.add_argument("--learn_T", type=int, default=64)
     p.add_argument("--learn_B", type=str, default="512,1024")
@@ -38,7 +39,11 @@ def main():
 
     dev = torch.device("cuda", 0)
     s = a.size
-    mk = lambda: Agent((s, s, 27))  # noqa: E731
+    if a.arch == "gridnet":
+        from microbeast_amd.models.gridnet import GridNetAgent
+        mk = lambda: GridNetAgent((s, s, 27))  # noqa: E731
+    else:
+        mk = lambda: Agent((s, s, 27))  # noqa: E731
     for E in [int(x) for x in a.E.split(",") if x]:
         rt = GpuActorRuntime(mk, s, 1, E, 8, 1, dev, n_threads=1, fp8_policy=a.fp8)
         # realistic inputs: run the env once to get observations / masks
@@ -54,7 +59,7 @@ def main():
             g.replay()
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / a.iters
-        print(json.dumps({"what": "policy_step_graph", "E": E, "fp8": a.fp8,
+        print(json.dumps({"what": "policy_step_graph", "arch": a.arch, "E": E, "fp8": a.fp8,
                           "trunk8": os.environ.get("MBK_TRUNK8", "1"), "ms": round(dt * 1e3, 4),
                           "frames_per_s": round(E / dt, 1)}), flush=True)
         if a.policy_eager:

@@ -9,4 +9,4 @@ case $script in /*) ;; *) script=$R/$script ;; esac  # prof runs from /tmp
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d /tmp/$name -o run --output-format csv \
   -- python "$script" "$@" > $R/gpurun_out/$name.log 2>&1 || exit $?
-python $R/tools/rocprof_summary.py /tmp/$name $R/gpurun_out/${name}_summary.md --drop-trace
+python $R/tools/rocprof_summary.py /tmp/$name $R/gpurun_out/${name}_summary.md --drop-trace ${MBK_PROF_SEQ:+--seq=$MBK_PROF_SEQ}

@@ -66,8 +66,33 @@ def busy_report(trace_csv, window_frac=0.5):
     return out
 
 
+def seq_report(trace_csv, last_n):
+    """the last ``last_n`` dispatches in order: kernel, grid, duration (one learner update's
+    layer-by-layer timeline when the program ends with it)"""
+    rows = []
+    for r in csv.DictReader(open(trace_csv)):
+        try:
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "?"),
+                         "x".join(r.get(k, "?") for k in ("Grid_Size_X", "Grid_Size_Y", "Grid_Size_Z"))))
+        except (KeyError, ValueError):
+            continue
+    rows.sort()
+    rows = rows[-last_n:]
+    out = [f"### last {len(rows)} dispatches ({os.path.basename(trace_csv)})\n", "| # | kernel | grid | us |",
+           "|---|---|---|---|"]
+    for i, (s, e, nm, g) in enumerate(rows):
+        nm = nm.replace("(anonymous namespace)::", "")
+        out.append(f"| {i} | `{nm[:70]}` | {g} | {(e - s) / 1e3:.1f} |")
+    out.append("")
+    return out
+
+
 def main():
     d, out = sys.argv[1], sys.argv[2]
+    seq = 0
+    for a in sys.argv[3:]:
+        if a.startswith("--seq="):
+            seq = int(a.split("=", 1)[1])
     stats = sorted(glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True))
     lines = []
     for f in stats:
@@ -88,6 +113,8 @@ def main():
         lines.append("")
     for f in sorted(glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)):
         lines.extend(busy_report(f))
+        if seq:
+            lines.extend(seq_report(f, seq))
     open(out, "w").write("\n".join(lines) + "\n")
     if "--drop-trace" in sys.argv:
         for f in glob.glob(os.path.join(d, "**", "*.csv"), recursive=True):
