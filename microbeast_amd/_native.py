@@ -43,7 +43,17 @@ _SIGS = {
     "mbk_masked_cell_bwd_pbc": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_pconv": [c_void_p, c_void_p],
+    "mbk_cells_nchunk": [c_int],
+    "mbk_cells_compact": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mbk_rows_colsum": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p],
+    "mbk_masked_cell_rows_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_masked_cell_rows_bwd": [c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_pwgrad": [c_void_p, c_void_p],
+    "mbk_pwgrad_all": [c_void_p, c_void_p],
+    "mbk_pwgrad_all_parts": [c_int, c_int, c_int],
     "mbk_pwgrad_parts": [c_int, c_int, c_int, c_int],
     "mbk_reduce_map": [c_void_p, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_ppool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],

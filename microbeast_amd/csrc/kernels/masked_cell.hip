@@ -149,6 +149,103 @@ __global__ __launch_bounds__(kTile) void masked_cell_bwd_kernel(
   }
 }
 
+// Compact-row forms (sparse GridNet logits layer, ops/pixconv.py Cells): logits / gradients
+// are rows r < totals[0] of [rows][ld] bf16, row r = cell rowcell[r] (= sample * S + map cell,
+// every row active). Per-cell outputs go to the cell's index (the caller zeroes the others).
+// 64-row tiles per wave, grid-stride over tiles (the row count is on the device).
+__device__ __forceinline__ void stage_rows(const __hip_bfloat16* __restrict__ Z, int ld,
+                                           int64_t r0, int nr, float* zs) {
+  const int lane = threadIdx.x;
+  for (int r = 0; r < nr; ++r) {
+    const __hip_bfloat16* src = Z + (r0 + r) * ld;
+    zs[r * kRow + lane] = __bfloat162float(src[lane]);
+    if (lane < kCell - 64) zs[r * kRow + 64 + lane] = __bfloat162float(src[64 + lane]);
+  }
+}
+
+__global__ __launch_bounds__(kTile) void masked_cell_rows_fwd_kernel(
+    const __hip_bfloat16* __restrict__ Z, int ld, const int* __restrict__ rowcell,
+    const int* __restrict__ totals, const uint32_t* __restrict__ mask, uint8_t* __restrict__ action,
+    const uint64_t* __restrict__ rng, int sample, float* __restrict__ cell_logp,
+    float* __restrict__ cell_ent) {
+  __shared__ float zs[kTile * kRow];
+  const int64_t nrows = totals[0];
+  const int i = threadIdx.x;
+  for (int64_t r0 = (int64_t)blockIdx.x * kTile; r0 < nrows; r0 += (int64_t)gridDim.x * kTile) {
+    const int nr = (int)min((int64_t)kTile, nrows - r0);
+    __syncthreads();  // previous tile's reads done
+    stage_rows(Z, ld, r0, nr, zs);
+    __syncthreads();
+    if (i >= nr) continue;
+    const int64_t cell = rowcell[r0 + i];
+    const uint32_t m[3] = {mask[cell * 3 + 0], mask[cell * 3 + 1], mask[cell * 3 + 2]};
+    uint8_t a[kComps];
+    float u[kComps];
+    if (sample) {  // same Philox stream as the dense kernel: keyed by the cell index
+      const uint64_t seed = rng[0], step = rng[1];
+      u32x4 c = {(uint32_t)cell, (uint32_t)(cell >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
+      u32x4 q0 = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      c.y ^= 0x80000000u;
+      u32x4 q1 = philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+      u[0] = u01(q0.x); u[1] = u01(q0.y); u[2] = u01(q0.z); u[3] = u01(q0.w);
+      u[4] = u01(q1.x); u[5] = u01(q1.y); u[6] = u01(q1.z);
+    } else {
+#pragma unroll
+      for (int k = 0; k < kComps; ++k) a[k] = action[cell * kComps + k];
+    }
+    float lp, ent;
+    cell_forward(zs + i * kRow, m, a, sample != 0, u, &lp, &ent);
+    if (sample) {
+#pragma unroll
+      for (int k = 0; k < kComps; ++k) action[cell * kComps + k] = a[k];
+    }
+    cell_logp[cell] = lp;
+    if (cell_ent) cell_ent[cell] = ent;
+  }
+}
+
+__global__ __launch_bounds__(kTile) void masked_cell_rows_bwd_kernel(
+    const __hip_bfloat16* __restrict__ Z, int ld, const int* __restrict__ rowcell,
+    const int* __restrict__ totals, int cps, const uint32_t* __restrict__ mask,
+    const uint8_t* __restrict__ action, const float* __restrict__ g_logp,
+    const float* __restrict__ g_ent, __hip_bfloat16* __restrict__ dZ) {
+  __shared__ float zs[kTile * kRow];
+  const int64_t nrows = totals[0];
+  const int i = threadIdx.x;
+  for (int64_t r0 = (int64_t)blockIdx.x * kTile; r0 < nrows; r0 += (int64_t)gridDim.x * kTile) {
+    const int nr = (int)min((int64_t)kTile, nrows - r0);
+    __syncthreads();
+    stage_rows(Z, ld, r0, nr, zs);
+    __syncthreads();
+    if (i < nr) {
+      const int64_t cell = rowcell[r0 + i];
+      const int64_t smp = cell / cps;
+      const uint32_t m[3] = {mask[cell * 3 + 0], mask[cell * 3 + 1], mask[cell * 3 + 2]};
+      uint8_t a[kComps];
+#pragma unroll
+      for (int k = 0; k < kComps; ++k) a[k] = action[cell * kComps + k];
+      float* row = zs + i * kRow;
+      cell_backward(row, m, a, g_logp[smp], g_ent ? g_ent[smp] : 0.f, row);
+    }
+    __syncthreads();
+    // 16-byte stores of 8 bf16 per row chunk, padding columns zero
+    const int c8n = ld / 8, total = nr * c8n;
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int r = e / c8n, c8 = e - r * c8n;
+      uint32_t w[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = c8 * 8 + 2 * q;
+        const float lo = c < kCell ? zs[r * kRow + c] : 0.f;
+        const float hi = c + 1 < kCell ? zs[r * kRow + c + 1] : 0.f;
+        w[q] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(lo)) |
+               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hi)) << 16);
+      }
+      *(uint4*)(dZ + (r0 + r) * ld + c8 * 8) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
 // Per-sample sums of per-cell values: out[n] = sum_c in[n, c] (one wave per sample).
 __global__ __launch_bounds__(256) void row_sum_kernel(const float* __restrict__ in, int64_t rows,
                                                        int cols, float* __restrict__ out,
@@ -248,5 +345,30 @@ extern "C" int mbk_row_sum_rng(const float* in, int64_t rows, int cols, float* o
 
 extern "C" int mbk_rng_advance(uint64_t* rng, hipStream_t stream) {
   hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, stream, rng);
+  return (int)hipGetLastError();
+}
+
+// compact-row forms: Z / dZ [rows][ld] bf16 (ld % 8 == 0), rows = totals[0] on the device,
+// grid of nblk 64-thread workgroups
+extern "C" int mbk_masked_cell_rows_fwd(const void* Z, int ld, const int* rowcell,
+                                        const int* totals, int nblk, const uint32_t* mask,
+                                        uint8_t* action, const uint64_t* rng, int sample,
+                                        float* cell_logp, float* cell_ent, hipStream_t stream) {
+  if (ld < kCell || ld % 8 || nblk < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(masked_cell_rows_fwd_kernel, dim3(nblk), dim3(kTile), 0, stream,
+                     (const __hip_bfloat16*)Z, ld, rowcell, totals, mask, action, rng, sample,
+                     cell_logp, cell_ent);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_masked_cell_rows_bwd(const void* Z, int ld, const int* rowcell,
+                                        const int* totals, int nblk, int cps,
+                                        const uint32_t* mask, const uint8_t* action,
+                                        const float* g_logp, const float* g_ent, void* dZ,
+                                        hipStream_t stream) {
+  if (ld < kCell || ld % 8 || nblk < 1 || ((uintptr_t)dZ & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(masked_cell_rows_bwd_kernel, dim3(nblk), dim3(kTile), 0, stream,
+                     (const __hip_bfloat16*)Z, ld, rowcell, totals, cps, mask, action, g_logp,
+                     g_ent, (__hip_bfloat16*)dZ);
   return (int)hipGetLastError();
 }

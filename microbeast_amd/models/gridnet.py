@@ -12,12 +12,14 @@ times); logits of padding cells are dropped.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops import cell_head
-from ..ops.pixconv import PixPlan, gridnet_pbc, pbc_to_cell_major
+from ..ops.pixconv import Cells, PixPlan, gridnet_pbc, pbc_to_cell_major
 from ..ops.obs import bits_to_planes
 from .agent import layer_init
 
@@ -46,6 +48,8 @@ class GridNetAgent(nn.Module):
         self.compute_dtype = compute_dtype
         self.nvec = list(cell_head.NVEC) * (h * w)
         self.emulate = False      # run the grid path's torch emulation off-GPU (tests)
+        # logits of the active cells only (compact rows) when acting / scoring; 0: dense
+        self.sparse_logits = os.environ.get("MBK_GRID_SPARSE", "1") == "1"
         self._grid_plan = None
         for p in self.parameters():  # grid-path kernels write gradients into flat slots
             p._mbk_direct_grad = True
@@ -80,15 +84,16 @@ class GridNetAgent(nn.Module):
                                       self.pw, (self.h, self.w), device)
         return self._grid_plan
 
-    def policy_value_pbc(self, obs, n_logits=None):
+    def policy_value_pbc(self, obs, n_logits=None, cells=None):
         """The whole network on the pixel-major layout (ops/pixconv.py, pixconv.hip): per
         output-pixel MFMA GEMMs with no padded halo, no ATen kernel. relu(maxpool(conv)) is
         computed as maxpool(relu-fused conv): identical values. Returns (logits [h*w][n_s][96]
         bf16 pixel-major -- what the masked-cell kernels read as they are --, value fp32 [n]);
-        the decoder runs on the first n_logits observations only."""
+        the decoder runs on the first n_logits observations only. With ``cells`` the logits
+        are the compact rows of those active cells (ops/pixconv.py Cells)."""
         n = obs.numel() // (self.h * self.w)
         return gridnet_pbc(self._plan(obs.device), obs.reshape(n, self.h * self.w),
-                           self.h, self.w, self.ph, self.pw, n_logits)
+                           self.h, self.w, self.ph, self.pw, n_logits, cells)
 
     def policy_value(self, obs):
         if self._use_hip(obs):
@@ -109,6 +114,13 @@ class GridNetAgent(nn.Module):
     def act(self, obs, mask_bits, rng_state=None, generator=None, action_out=None,
             cell_logp=None, logp_out=None):
         if self._use_hip(obs):
+            n = obs.numel() // (self.h * self.w)
+            if self.sparse_logits:
+                cells = Cells(mask_bits, n, self.h * self.w)
+                zc, value = self.policy_value_pbc(obs, cells=cells)
+                action, logp = cell_head.sample_rows(zc, cells, mask_bits, rng_state, generator,
+                                                     action_out, cell_logp, logp_out)
+                return action, logp, value
             lg, value = self.policy_value_pbc(obs)
             action, logp = cell_head.sample_pbc(lg, mask_bits, rng_state, generator, action_out,
                                                 cell_logp, logp_out)
@@ -119,6 +131,12 @@ class GridNetAgent(nn.Module):
 
     def evaluate(self, obs, mask_bits, action, n_score: int | None = None):
         if self._use_hip(obs):  # logits of the scored rows only
+            if self.sparse_logits:
+                ns = obs.numel() // (self.h * self.w) if n_score is None else n_score
+                cells = Cells(mask_bits.reshape(ns, -1, 3).contiguous(), ns, self.h * self.w)
+                zc, value = self.policy_value_pbc(obs, n_score, cells)
+                logp, ent = cell_head.score_rows(zc, cells, mask_bits, action)
+                return logp, ent, value
             lg, value = self.policy_value_pbc(obs, n_score)
             logp, ent = cell_head.score_pbc(lg, mask_bits, action)
             return logp, ent, value

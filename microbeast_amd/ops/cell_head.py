@@ -237,6 +237,116 @@ def sample_pbc(logits: torch.Tensor, mask_bits: torch.Tensor, rng_state: torch.T
     return action_out, logp_out
 
 
+# ---------------------------------------------------------------- compact active-cell rows
+# The sparse GridNet logits layer (ops/pixconv.py Cells) produces logits only for the active
+# cells, as compact rows [cap][ld] bf16 (row r = cell cells.rowcell[r]); every other cell is
+# fully masked (log-prob 0, entropy 0, gradient 0, sampled action 0).
+def _rows_cm(Zc: torch.Tensor, cells) -> torch.Tensor:
+    """compact rows -> cell-major [n, S*78] fp32 (zeros at inactive cells), differentiable"""
+    nact = int(cells.totals[0])
+    idx = cells.rowcell[:nact].long()
+    cm = torch.zeros(cells.n * cells.S, CELL, dtype=torch.float32)
+    cm = cm.index_copy(0, idx, Zc[:nact, :CELL].float())
+    return cm.view(cells.n, cells.S * CELL)
+
+
+def _zero(t: torch.Tensor):
+    N.check(N.kernels().mbk_memset(t.data_ptr(), 0, t.numel() * t.element_size(), N.stream_ptr()),
+            "memset")
+
+
+class _ScoreRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Zc, cells, mask_bits, action):
+        k = N.kernels()
+        n, S = cells.n, cells.S
+        nc = n * S
+        dev = Zc.device
+        ld = Zc.shape[-1]
+        assert Zc.dtype == torch.bfloat16 and Zc.is_contiguous() and Zc.numel() == cells.cap * ld
+        assert mask_bits.numel() == nc * 3 and action.numel() == nc * COMPS
+        cl = torch.empty(nc, dtype=torch.float32, device=dev)
+        ce = torch.empty(nc, dtype=torch.float32, device=dev)
+        _zero(cl)
+        _zero(ce)
+        st = N.stream_ptr()
+        nblk = max(1, min(8192, -(-cells.cap // 64)))
+        N.check(k.mbk_masked_cell_rows_fwd(Zc.data_ptr(), ld, cells.rowcell.data_ptr(),
+                                           cells.totals.data_ptr(), nblk, mask_bits.data_ptr(),
+                                           action.data_ptr(), None, 0, cl.data_ptr(),
+                                           ce.data_ptr(), st), "masked_cell_rows_fwd")
+        logp = torch.empty(n, dtype=torch.float32, device=dev)
+        ent = torch.empty(n, dtype=torch.float32, device=dev)
+        N.check(k.mbk_row_sum(cl.data_ptr(), n, S, logp.data_ptr(), st), "row_sum")
+        N.check(k.mbk_row_sum(ce.data_ptr(), n, S, ent.data_ptr(), st), "row_sum")
+        ctx.save_for_backward(Zc, mask_bits, action)
+        ctx.cells = cells
+        return logp, ent
+
+    @staticmethod
+    def backward(ctx, g_logp, g_ent):
+        Zc, mask_bits, action = ctx.saved_tensors
+        cells = ctx.cells
+        k = N.kernels()
+        n = cells.n
+        if g_logp is None:
+            g_logp = torch.zeros(n, device=Zc.device)
+        if g_ent is None:
+            g_ent = torch.zeros(n, device=Zc.device)
+        g_logp = g_logp.float().contiguous()
+        g_ent = g_ent.float().contiguous()
+        d = torch.empty_like(Zc)     # rows >= totals[0] are never read
+        nblk = max(1, min(8192, -(-cells.cap // 64)))
+        N.check(k.mbk_masked_cell_rows_bwd(Zc.data_ptr(), Zc.shape[-1], cells.rowcell.data_ptr(),
+                                           cells.totals.data_ptr(), nblk, cells.S,
+                                           mask_bits.data_ptr(), action.data_ptr(),
+                                           g_logp.data_ptr(), g_ent.data_ptr(), d.data_ptr(),
+                                           N.stream_ptr()), "masked_cell_rows_bwd")
+        return d, None, None, None
+
+
+def score_rows(Zc: torch.Tensor, cells, mask_bits: torch.Tensor, action: torch.Tensor):
+    """(logp [n], entropy [n]) of compact active-cell logits, differentiable in them."""
+    if Zc.is_cuda:
+        return _ScoreRows.apply(Zc, cells, mask_bits.contiguous(), action.contiguous())
+    _, lp, ent = cell_head_torch(_rows_cm(Zc, cells), mask_bits, action)
+    return lp, ent
+
+
+def sample_rows(Zc: torch.Tensor, cells, mask_bits: torch.Tensor,
+                rng_state: torch.Tensor | None = None, generator: torch.Generator | None = None,
+                action_out=None, cell_logp=None, logp_out=None):
+    """(action [n,S,7] uint8, logp [n]) sampled from compact active-cell logits (same Philox
+    draws as the dense kernel: keyed by cell index)."""
+    n, S = cells.n, cells.S
+    if not Zc.is_cuda:
+        with torch.no_grad():
+            a, lp, _ = cell_head_torch(_rows_cm(Zc, cells), mask_bits, None, generator)
+        return a, lp
+    k = N.kernels()
+    nc = n * S
+    dev = Zc.device
+    if action_out is None:
+        action_out = torch.empty(n, S, COMPS, dtype=torch.uint8, device=dev)
+    if cell_logp is None:
+        cell_logp = torch.empty(nc, dtype=torch.float32, device=dev)
+    if logp_out is None:
+        logp_out = torch.empty(n, dtype=torch.float32, device=dev)
+    assert action_out.numel() == nc * COMPS and cell_logp.numel() >= nc
+    _zero(action_out)
+    _zero(cell_logp)
+    st = N.stream_ptr()
+    nblk = max(1, min(8192, -(-cells.cap // 64)))
+    N.check(k.mbk_masked_cell_rows_fwd(Zc.data_ptr(), Zc.shape[-1], cells.rowcell.data_ptr(),
+                                       cells.totals.data_ptr(), nblk,
+                                       mask_bits.contiguous().data_ptr(), action_out.data_ptr(),
+                                       rng_state.data_ptr(), 1, cell_logp.data_ptr(), None, st),
+            "masked_cell_rows_fwd")
+    N.check(k.mbk_row_sum_rng(cell_logp.data_ptr(), n, S, logp_out.data_ptr(),
+                              rng_state.data_ptr(), st), "row_sum_rng")
+    return action_out, logp_out
+
+
 def score(logits: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor):
     """(logp [N], entropy [N]) of given actions, differentiable in logits."""
     if logits.is_cuda:

@@ -148,16 +148,31 @@ def _fits(t: torch.Tensor, last_pix: int, ps: int, rows: int, bs: int, cols: int
 
 # ============================================================================ launchers
 def pconv(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias=None, relu=False, a_relu=False,
-          mask=None):
+          mask=None, cells=None, gather=None):
     """C[P][b][:N] = relu?(bias + sum_{(q, t)} relu?(A[q][b][:cin]) . B[t][:N][:cin]^T) for
     every table row (P = its output pixel), b < M; masked to 0 where mask (C's layout) <= 0.
-    Operands are addressed as (pixel stride, image stride) in elements; B is [ntap][N][cin]."""
-    _fits(A, tab.src_max, a_ps, M, a_bs, cin, "pconv A")
-    _fits(C, tab.dst_max, c_ps, M, c_bs, N, "pconv C")
+    Operands are addressed as (pixel stride, image stride) in elements; B is [ntap][N][cin].
+
+    cells (``Cells``, sparse rows): table row P computes only the compact rows of cell bucket P
+    (images cells.rowimg), written to C's compact rows (image stride c_bs; c_ps unused).
+    gather (``Cells``): A row of pair source P and image b is compact row cellrow[P][b] of A
+    (image stride a_bs; a_ps unused), zero when the cell is inactive."""
     assert (tab.tap_max + 1) * N * cin <= B.numel(), "pconv B too small"
+    if cells is not None:
+        _fits(A, tab.src_max, a_ps, M, a_bs, cin, "pconv A")
+        assert cells.cap * c_bs <= C.numel() and tab.shape[0] == cells.S and mask is None
+    elif gather is not None:
+        assert gather.cap * a_bs <= A.numel() and tab.src_max < gather.S and M == gather.n
+        _fits(C, tab.dst_max, c_ps, M, c_bs, N, "pconv C")
+    else:
+        _fits(A, tab.src_max, a_ps, M, a_bs, cin, "pconv A")
+        _fits(C, tab.dst_max, c_ps, M, c_bs, N, "pconv C")
     if mask is not None:
         _fits(mask, tab.dst_max, c_ps, M, c_bs, N, "pconv mask")
     if not C.is_cuda:
+        if cells is not None or gather is not None:
+            return _pconv_sparse_ref(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias, relu,
+                                     a_relu, mask, cells, gather)
         tabc = tab.t.cpu()
         for z in range(tabc.shape[0]):
             P, cnt = int(tabc[z, 0]), int(tabc[z, 1])
@@ -185,20 +200,150 @@ def pconv(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias=None, relu=False
         assert t is None or (t.dtype == _BF and t.is_contiguous())
     assert bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())
     assert tab.t.dtype == torch.int32 and tab.t.is_cuda
-    args = (ctypes.c_longlong * 17)(A.data_ptr(), a_ps, a_bs, cin, int(a_relu), B.data_ptr(),
-                                    tab.t.data_ptr(), tab.shape[1], tab.shape[0],
-                                    bias.data_ptr() if bias is not None else 0, int(relu),
-                                    C.data_ptr(), c_ps, c_bs,
-                                    mask.data_ptr() if mask is not None else 0, M, N)
+    mode, sp = (1, cells) if cells is not None else ((2, gather) if gather is not None else (0, None))
+    args = (ctypes.c_longlong * 26)(
+        A.data_ptr(), a_ps, a_bs, cin, int(a_relu), B.data_ptr(), tab.t.data_ptr(), tab.shape[1],
+        tab.shape[0], bias.data_ptr() if bias is not None else 0, int(relu), C.data_ptr(), c_ps,
+        c_bs, mask.data_ptr() if mask is not None else 0, M, N, mode,
+        sp.bucket_off.data_ptr() if mode == 1 else 0, sp.bucket_cnt.data_ptr() if mode == 1 else 0,
+        sp.tile_off.data_ptr() if mode == 1 else 0, sp.totals.data_ptr() if mode == 1 else 0,
+        sp.rowimg.data_ptr() if mode == 1 else 0, sp.S if mode == 1 else 0,
+        sp.cellrow.data_ptr() if mode == 2 else 0,
+        2048 if mode == 1 else tab.tap_max + 1)   # mode 1: persistent grid; 2: taps of B
     N_.check(N_.kernels().mbk_pconv(args, N_.stream_ptr()), "pconv")
     return C
 
 
-def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False):
+def _pconv_sparse_ref(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias, relu, a_relu, mask,
+                      cells, gather):
+    tabc = tab.t.cpu()
+    for z in range(tabc.shape[0]):
+        P, cnt = int(tabc[z, 0]), int(tabc[z, 1])
+        if cells is not None:
+            o, nr = int(cells.bucket_off[z]), int(cells.bucket_cnt[z])
+            imgs = cells.rowimg[o:o + nr].long()
+        else:
+            nr = M
+        acc = torch.zeros(nr, N, dtype=torch.float32)
+        for j in range(cnt):
+            e = int(tabc[z, 2 + j])
+            q, t = e >> 8, e & 255
+            if cells is not None:
+                a = _view(A, a_ps, a_bs, M, cin, q)[imgs].float()
+            else:
+                rows = gather.cellrow[q * M:(q + 1) * M].long()
+                src = torch.as_strided(A.reshape(-1), (gather.cap, cin), (a_bs, 1), 0)
+                a = torch.where((rows >= 0)[:, None], src[rows.clamp(min=0)].float(), 0.0)
+            if a_relu:
+                a = a.clamp_min(0)
+            b = B.reshape(-1)[t * N * cin:(t + 1) * N * cin].view(N, cin).float()
+            acc += a @ b.t()
+        if bias is not None:
+            acc += bias.float()
+        if relu:
+            acc = acc.clamp_min(0)
+        out = acc.to(C.dtype)
+        if cells is not None:
+            torch.as_strided(C.reshape(-1), (nr, N), (c_bs, 1), o * c_bs).copy_(out)
+        else:
+            if mask is not None:
+                m = _view(mask, c_ps, c_bs, M, N, P).float() > 0
+                out = torch.where(m, out, torch.zeros_like(out))
+            _view(C, c_ps, c_bs, M, N, P).copy_(out)
+    return C
+
+
+class Cells:
+    """The active cells (any legal action) of n samples x S map cells, compacted into rows in
+    (cell, sample) order and bucketed by cell: the sparse logits layer computes, scores and
+    back-propagates only these rows (``pixconv.hip`` cells_* kernels; torch on CPU).
+
+    rowimg / rowcell [cap]: sample and cell index (sample * S + cell) of each compact row;
+    cellrow [S * n]: compact row of (cell, sample) or -1; bucket_off / bucket_cnt [S],
+    tile_off [S + 1] (128-row tiles); totals = [rows, tiles] (device ints: nothing syncs)."""
+
+    TM = 128
+
+    def __init__(self, mask_bits: torch.Tensor, n: int, S: int):
+        self.n, self.S, self.cap = n, S, n * S
+        dev = mask_bits.device
+        m = mask_bits.reshape(n, S, 3)
+        if dev.type != "cuda":
+            act = (m != 0).any(-1)                       # [n, S]
+            pm = act.t().contiguous()                    # [S, n]
+            idx = pm.nonzero()                           # (P, b) sorted by P then b
+            P, b = idx[:, 0].int(), idx[:, 1].int()
+            nact = idx.shape[0]
+            self.rowimg = torch.zeros(self.cap, dtype=torch.int32)
+            self.rowcell = torch.zeros(self.cap, dtype=torch.int32)
+            self.rowimg[:nact] = b
+            self.rowcell[:nact] = b * S + P
+            self.bucket_cnt = pm.sum(1).int()
+            self.bucket_off = (torch.cumsum(self.bucket_cnt, 0) - self.bucket_cnt).int()
+            tiles = (self.bucket_cnt + self.TM - 1) // self.TM
+            self.tile_off = torch.cat([torch.zeros(1, dtype=torch.int64), torch.cumsum(tiles, 0)]).int()
+            self.cellrow = torch.full((S * n,), -1, dtype=torch.int32)
+            self.cellrow[(P.long() * n + b.long())] = torch.arange(nact, dtype=torch.int32)
+            self.totals = torch.tensor([nact, int(self.tile_off[-1])], dtype=torch.int32)
+            return
+        N_ = _N()
+        k = N_.kernels()
+        assert mask_bits.dtype == torch.int32 and mask_bits.is_contiguous()
+        nchunk = k.mbk_cells_nchunk(n)
+        i32 = dict(dtype=torch.int32, device=dev)
+        counts = torch.empty(S * nchunk, **i32)
+        offs = torch.empty(S * nchunk, **i32)
+        self.bucket_off = torch.empty(S, **i32)
+        self.bucket_cnt = torch.empty(S, **i32)
+        self.tile_off = torch.empty(S + 1, **i32)
+        self.totals = torch.empty(2, **i32)
+        self.rowimg = torch.empty(self.cap, **i32)
+        self.rowcell = torch.empty(self.cap, **i32)
+        self.cellrow = torch.empty(S * n, **i32)
+        N_.check(k.mbk_cells_compact(mask_bits.data_ptr(), n, S, self.TM, counts.data_ptr(),
+                                     offs.data_ptr(), self.bucket_off.data_ptr(),
+                                     self.bucket_cnt.data_ptr(), self.tile_off.data_ptr(),
+                                     self.totals.data_ptr(), self.rowimg.data_ptr(),
+                                     self.rowcell.data_ptr(), self.cellrow.data_ptr(),
+                                     N_.stream_ptr()), "cells_compact")
+
+    def rows_colsum(self, Z: torch.Tensor, ld: int, C: int, out: torch.Tensor):
+        """out[:C] = column sums of the compact rows of Z [cap][ld] (fp32, fixed order)"""
+        if not Z.is_cuda:
+            nact = int(self.totals[0])
+            out.view(-1).copy_(Z.view(-1, ld)[:nact, :C].float().sum(0))
+            return
+        N_ = _N()
+        k = N_.kernels()
+        nblk = 256
+        partial = torch.empty(nblk * C, dtype=torch.float32, device=Z.device)
+        N_.check(k.mbk_rows_colsum(Z.data_ptr(), ld, C, self.totals.data_ptr(), nblk,
+                                   partial.data_ptr(), N_.stream_ptr()), "rows_colsum")
+        ident = _ident_map(C, Z.device)
+        N_.check(k.mbk_reduce_map(partial.data_ptr(), nblk, C, ident.data_ptr(), C,
+                                  out.data_ptr(), N_.stream_ptr()), "reduce_map")
+
+
+_IDENT = {}
+
+
+def _ident_map(C: int, device) -> torch.Tensor:
+    key = (C, str(device))
+    if key not in _IDENT:
+        _IDENT[key] = torch.arange(C, dtype=torch.int32, device=device)
+    return _IDENT[key]
+
+
+def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False, cells=None):
     """out.flat[j] = dW[gmap[j]] (0 where gmap < 0), dW [ntap][O][I] fp32 with
-    dW[t] = sum_{(P, q) in tab[t]} sum_{b < M} g[P][b][:O]^T relu?(x[q][b][:I])."""
+    dW[t] = sum_{(P, q) in tab[t]} sum_{b < M} g[P][b][:O]^T relu?(x[q][b][:I]).
+    cells: g holds compact rows (image stride g_bs) and pair (P, q) runs over cell bucket P's
+    rows, x rows gathered by their images."""
     ntap = tab.shape[0]
-    _fits(g, tab.dst_max, g_ps, M, g_bs, O, "pwgrad g")
+    if cells is None:
+        _fits(g, tab.dst_max, g_ps, M, g_bs, O, "pwgrad g")
+    else:
+        assert cells.cap * g_bs <= g.numel() and tab.dst_max < cells.S and M == cells.n
     _fits(x, tab.src_max, x_ps, M, x_bs, I, "pwgrad x")
     if not out.is_cuda:
         tabc = tab.t.cpu()
@@ -207,7 +352,54 @@ def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False):
             for j in range(int(tabc[t, 0])):
                 e = int(tabc[t, 1 + j])
                 P, q = e >> 16, e & 0xFFFF
-                gv = _view(g, g_ps, g_bs, M, O, P).float()
+                if cells is not None:
+                    o, nr = int(cells.bucket_off[P]), int(cells.bucket_cnt[P])
+                    gv = torch.as_strided(g.reshape(-1), (nr, O), (g_bs, 1), o * g_bs).float()
+                    xv = _view(x, x_ps, x_bs, M, I, q)[cells.rowimg[o:o + nr].long()].float()
+                else:
+                    gv = _view(g, g_ps, g_bs, M, O, P).float()
+                    xv = _view(x, x_ps, x_bs, M, I, q).float()
+                if x_relu:
+                    xv = xv.clamp_min(0)
+                dw[t] += gv.t() @ xv
+        m = gmap.long()
+        out.view(-1).copy_(torch.where(m >= 0, dw.reshape(-1)[m.clamp(min=0)], 0.0))
+        return out
+    N_ = _N()
+    k = N_.kernels()
+    assert g.dtype == _BF and x.dtype == _BF and g.is_contiguous() and x.is_contiguous()
+    assert out.is_contiguous() and out.dtype == torch.float32 and gmap.numel() == out.numel()
+    # rows mode: fine row ranges (the buckets are small and uneven; empty ranges exit at once)
+    parts = min(512, max(1, -(-M // 1024))) if cells is not None else k.mbk_pwgrad_parts(M, O, I, ntap)
+    stride = ntap * O * I
+    partial = torch.empty(parts * stride, dtype=torch.float32, device=out.device)
+    args = (ctypes.c_longlong * 18)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
+                                    int(x_relu), tab.t.data_ptr(), tab.shape[1], ntap, M, parts,
+                                    partial.data_ptr(),
+                                    cells.bucket_off.data_ptr() if cells is not None else 0,
+                                    cells.bucket_cnt.data_ptr() if cells is not None else 0,
+                                    cells.rowimg.data_ptr() if cells is not None else 0)
+    N_.check(k.mbk_pwgrad(args, N_.stream_ptr()), "pwgrad")
+    N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
+                              out.data_ptr(), N_.stream_ptr()), "reduce_map")
+    return out
+
+
+def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_relu=False):
+    """``pwgrad`` over the forward pair table (per output pixel P: its (q, t) pairs): g[P] is
+    read once per 64-image stage for every tap of P (``pwgrad_all_kernel``); ntap <= 9."""
+    assert ntap <= 9 and ftab.tap_max < ntap
+    _fits(g, ftab.dst_max, g_ps, M, g_bs, O, "pwgrad_all g")
+    _fits(x, ftab.src_max, x_ps, M, x_bs, I, "pwgrad_all x")
+    if not out.is_cuda:
+        tabc = ftab.t.cpu()
+        dw = torch.zeros(ntap, O, I, dtype=torch.float32)
+        for z in range(tabc.shape[0]):
+            P = int(tabc[z, 0])
+            gv = _view(g, g_ps, g_bs, M, O, P).float()
+            for j in range(int(tabc[z, 1])):
+                e = int(tabc[z, 2 + j])
+                q, t = e >> 8, e & 255
                 xv = _view(x, x_ps, x_bs, M, I, q).float()
                 if x_relu:
                     xv = xv.clamp_min(0)
@@ -219,16 +411,29 @@ def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False):
     k = N_.kernels()
     assert g.dtype == _BF and x.dtype == _BF and g.is_contiguous() and x.is_contiguous()
     assert out.is_contiguous() and out.dtype == torch.float32 and gmap.numel() == out.numel()
-    parts = k.mbk_pwgrad_parts(M, O, I, ntap)
+    parts = k.mbk_pwgrad_all_parts(M, O, I)
     stride = ntap * O * I
     partial = torch.empty(parts * stride, dtype=torch.float32, device=out.device)
-    args = (ctypes.c_longlong * 15)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
-                                    int(x_relu), tab.t.data_ptr(), tab.shape[1], ntap, M, parts,
-                                    partial.data_ptr())
-    N_.check(k.mbk_pwgrad(args, N_.stream_ptr()), "pwgrad")
+    args = (ctypes.c_longlong * 16)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
+                                    int(x_relu), ftab.t.data_ptr(), ftab.shape[1], ftab.shape[0],
+                                    ntap, M, parts, partial.data_ptr())
+    N_.check(k.mbk_pwgrad_all(args, N_.stream_ptr()), "pwgrad_all")
     N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
                               out.data_ptr(), N_.stream_ptr()), "reduce_map")
     return out
+
+
+_WGRAD_ALL = os.environ.get("MBK_PWGRAD_ALL", "1") == "1"
+
+
+def _wgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L, ntap, M, out, x_relu=False):
+    """weight gradient of a dense layer: the all-taps form for the 3x3 convs (~7.6 pairs per
+    output pixel share one staged g row), the per-tap form for the transposed convs and the
+    critic (1-4 pairs per output pixel: nothing to share, measured 2x slower all-taps)"""
+    if _WGRAD_ALL and ntap <= 9 and L.mean_pairs >= 4.0:
+        return pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L.tf, ntap, M, L.gmap, out,
+                          x_relu=x_relu)
+    return pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L.tw, M, L.gmap, out, x_relu=x_relu)
 
 
 def ppool_fwd(y, H: int, W: int, n: int, C: int):
@@ -469,6 +674,7 @@ class PixPlan:
             L.cout, L.cin = c.weight.shape[0], c.weight.shape[1]
             fwd, dg, wg = conv_pairs(H, W)
             L.tf, L.td, L.tw = pconv_table(fwd, dev), pconv_table(dg, dev), wgrad_table(wg, dev)
+            L.mean_pairs = sum(len(e) for _, e in fwd) / len(fwd)
             L.cin_p = _ceil32(L.cin)
             fm, dm, gm, L.cop = conv_maps(L.cout, L.cin)
             if L.cin_p != L.cin:      # first layer (bit planes): K per pair padded to 32
@@ -495,6 +701,7 @@ class PixPlan:
             fwd, dg, wg = convt_pairs(H, W, L.crop)
             L.npix_out = len(fwd)
             L.tf, L.td, L.tw = pconv_table(fwd, dev), pconv_table(dg, dev), wgrad_table(wg, dev)
+            L.mean_pairs = sum(len(e) for _, e in fwd) / len(fwd)
             L.gO = LOGIT_LD if last else L.cout       # channel count of the output gradient
             fm, dm, gm = convt_maps(L.cin, L.cout, L.gO)
             L.fmap, L.dmap, L.gmap = fm.to(dev), dm.to(dev), gm.to(dev)
@@ -509,6 +716,7 @@ class PixPlan:
         L.k1, L.C, L.npix = k1, zc, npix
         fwd, dg, wg = critic_pairs(npix)
         L.tf, L.td, L.tw = pconv_table(fwd, dev), pconv_table(dg, dev), wgrad_table(wg, dev)
+        L.mean_pairs = 1.0      # one tap per z pixel per output row: the per-tap form
         fm, dm, gm = critic_maps(k1, zc, npix)
         L.fmap, L.dmap, L.gmap = fm.to(dev), dm.to(dev), gm.to(dev)
         L.fshape, L.dshape = (npix, k1, zc), (npix, zc, k1)
@@ -566,7 +774,7 @@ class _GridNetPBC(torch.autograd.Function):
     parameter's flat slot (direct-gradient parameters)."""
 
     @staticmethod
-    def forward(ctx, bits, plan, hw, n_s, grad, *params):
+    def forward(ctx, bits, plan, hw, n_s, grad, cells, *params):
         ctx.set_materialize_grads(False)
         h, w, ph, pw = hw
         n = bits.shape[0]
@@ -618,7 +826,11 @@ class _GridNetPBC(torch.autograd.Function):
         for j, (L, t) in enumerate(zip(plan.dec, plan.convts)):
             last = j == len(plan.dec) - 1
             xin = dx[-1]
-            if last:
+            if last and cells is not None:   # active cells only: compact rows
+                y = torch.empty(cells.cap, LOGIT_LD, dtype=_BF, device=dev)
+                pconv(xin[0], xin[1], xin[2], xin[3], pk["dec"][j][0], L.tf, L.cout, n_s, y,
+                      0, LOGIT_LD, bias=t.bias.detach(), cells=cells)
+            elif last:
                 y = torch.empty(L.npix_out, n_s, LOGIT_LD, dtype=_BF, device=dev)
                 pconv(xin[0], xin[1], xin[2], xin[3], pk["dec"][j][0], L.tf, L.cout, n_s, y,
                       n_s * LOGIT_LD, LOGIT_LD, bias=t.bias.detach())
@@ -630,6 +842,7 @@ class _GridNetPBC(torch.autograd.Function):
         logits = y
         ctx.plan, ctx.hw, ctx.n_s, ctx.n = plan, hw, n_s, n
         ctx.acts, ctx.pools, ctx.dx, ctx.hcrit, ctx.saved = acts, pools, dx, hcrit, saved
+        ctx.cells = cells
         ctx.params = params
         return logits, v
 
@@ -656,7 +869,7 @@ class _GridNetPBC(torch.autograd.Function):
                            pg(ic + 2), pg(ic + 3))
             colsum(dh, Lc.k1, pg(ic + 1))
             z = ctx.dx[0][0]
-            pwgrad(dh, 0, Lc.k1, Lc.k1, z, n * Lc.C, Lc.C, Lc.C, Lc.tw, n, Lc.gmap, pg(ic))
+            _wgrad(dh, 0, Lc.k1, Lc.k1, z, n * Lc.C, Lc.C, Lc.C, Lc, Lc.npix, n, pg(ic))
             dz_c = torch.empty(Lc.npix, n, Lc.C, dtype=_BF, device=dev)
             pconv(dh, 0, Lc.k1, Lc.k1, pk["w1d"], Lc.td, Lc.C, n, dz_c, n * Lc.C, Lc.C)
         # ---- decoder
@@ -664,21 +877,29 @@ class _GridNetPBC(torch.autograd.Function):
         if g_logits is not None:
             g = g_logits.contiguous()
             gC = LOGIT_LD
+            cells = ctx.cells
             for j in range(len(plan.dec) - 1, -1, -1):
                 L = plan.dec[j]
                 iw = 2 * nconv + 2 * j
                 xin = ctx.dx[j]
-                gflat = g.view(-1, gC)
-                colsum(gflat, L.cout, pg(iw + 1))
-                pwgrad(g, n_s * gC, gC, gC, xin[0], xin[1], xin[2], xin[3], L.tw, n_s, L.gmap,
-                       pg(iw))
                 cin = L.cin
                 gx = torch.empty(L.H * L.W, n_s, cin, dtype=_BF, device=dev)
                 # relu mask of the input (a decoder output); the pooled code z is masked by the
                 # pool backward
                 mask = xin[0] if j > 0 else None
-                pconv(g, n_s * gC, gC, gC, pk["dec"][j][1], L.td, cin, n_s, gx, n_s * cin, cin,
-                      mask=mask)
+                if j == len(plan.dec) - 1 and cells is not None:
+                    # sparse logits layer: g = compact rows of the active cells
+                    cells.rows_colsum(g, gC, L.cout, pg(iw + 1))
+                    pwgrad(g, 0, gC, gC, xin[0], xin[1], xin[2], xin[3], L.tw, n_s, L.gmap,
+                           pg(iw), cells=cells)
+                    pconv(g, 0, gC, gC, pk["dec"][j][1], L.td, cin, n_s, gx, n_s * cin, cin,
+                          mask=mask, gather=cells)
+                else:
+                    colsum(g.view(-1, gC), L.cout, pg(iw + 1))
+                    _wgrad(g, n_s * gC, gC, gC, xin[0], xin[1], xin[2], xin[3], L, 9, n_s,
+                           pg(iw))
+                    pconv(g, n_s * gC, gC, gC, pk["dec"][j][1], L.td, cin, n_s, gx, n_s * cin,
+                          cin, mask=mask)
                 g, gC = gx, cin
             dz_d = g
         # ---- encoder
@@ -705,8 +926,8 @@ class _GridNetPBC(torch.autograd.Function):
             dy = ppool_bwd(g1, n1, g2, n2, pooled, idx, L.H, L.W, n, L.cout)
             colsum(dy.view(-1, L.cout), L.cout, pg(iw + 1))
             xa = ctx.acts[i]
-            pwgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], L.tw, n, L.gmap,
-                   pg(iw), x_relu=xa[4])
+            _wgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], L, 9, n, pg(iw),
+                   x_relu=xa[4])
             if i == 0:
                 break
             if i == 1 and plan.enc0 is not None and ctx.acts[0] is None:
@@ -721,13 +942,17 @@ class _GridNetPBC(torch.autograd.Function):
                 pconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.td, L.cin, n, gx,
                       n * L.cin, L.cin)
             g1, n1, g2, n2 = gx, n, None, 0
-        return (None, None, None, None, None) + tuple(grads)
+        return (None, None, None, None, None, None) + tuple(grads)
 
 
 def gridnet_pbc(plan: PixPlan, bits: torch.Tensor, h: int, w: int, ph: int, pw: int,
-                n_logits: int | None = None):
+                n_logits: int | None = None, cells: Cells | None = None):
     """(logits [h*w][n_s][96] bf16 pixel-major, value fp32 [n]) of int32 bit-plane obs
-    [n, h*w]; the decoder runs on the first n_s = n_logits (default n) observations."""
+    [n, h*w]; the decoder runs on the first n_s = n_logits (default n) observations. With
+    ``cells`` (the active cells of those n_s samples) the logits are the compact rows
+    [cells.cap][96] of the active cells only."""
+    if cells is not None:
+        assert cells.n == (bits.shape[0] if n_logits is None else n_logits) and cells.S == h * w
     n = bits.shape[0]
     n_s = n if n_logits is None else n_logits
     params = []
@@ -738,7 +963,7 @@ def gridnet_pbc(plan: PixPlan, bits: torch.Tensor, h: int, w: int, ph: int, pw: 
     params += [plan.lin1.weight, plan.lin1.bias, plan.lin2.weight, plan.lin2.bias]
     grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
     return _GridNetPBC.apply(bits.reshape(n, h * w).contiguous(), plan, (h, w, ph, pw), n_s,
-                             grad, *params)
+                             grad, cells, *params)
 
 
 def pbc_to_cell_major(logits: torch.Tensor) -> torch.Tensor:

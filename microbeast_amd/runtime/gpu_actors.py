@@ -100,12 +100,14 @@ def graph_policy_step(io: dict, m, rng: torch.Tensor, E: int, size: int, device)
                                       E, size, size, io["in_obs"].data_ptr(),
                                       io["in_mask"].data_ptr(), st), "decode_obs_mask")
         if hasattr(m, "policy_value_pbc") and m._use_hip(io["in_obs"]):
-            # GridNet: pixel-major logits straight into the masked-cell sampler
-            logits, value = m.policy_value_pbc(io["in_obs"])
-            if "out_logits" in io:
+            if "out_logits" in io:   # dense logits requested: pixel-major path
+                logits, value = m.policy_value_pbc(io["in_obs"])
                 io["out_logits"].copy_(pbc_to_cell_major(logits).reshape(io["out_logits"].shape))
-            cell_head.sample_pbc(logits, io["in_mask"], rng, action_out=io["out_action"],
-                                 cell_logp=io["cell_logp"], logp_out=io["out_logp"])
+                cell_head.sample_pbc(logits, io["in_mask"], rng, action_out=io["out_action"],
+                                     cell_logp=io["cell_logp"], logp_out=io["out_logp"])
+            else:                    # GridNet: active-cell logits straight into the sampler
+                _, _, value = m.act(io["in_obs"], io["in_mask"], rng, action_out=io["out_action"],
+                                    cell_logp=io["cell_logp"], logp_out=io["out_logp"])
         else:
             logits, value = m.policy_value(io["in_obs"])
             if "out_logits" in io:

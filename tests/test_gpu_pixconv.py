@@ -150,3 +150,153 @@ def test_gpu_gridnet_pbc_matches_cpu_emulation(s):
     ((pc.pbc_to_cell_major(lc) * gl).sum() + (vc * gv).sum()).backward()
     for (name, p), (_, q) in zip(m.named_parameters(), cpu.named_parameters()):
         assert _rel(p.grad.cpu(), q.grad) < 5e-2, name
+
+
+def _sparse_mask(n, S, frac, seed, device="cpu"):
+    g = torch.Generator().manual_seed(seed)
+    m = torch.randint(0, 2 ** 31 - 1, (n, S, 3), generator=g, dtype=torch.int32)
+    m[..., 2] &= (1 << 14) - 1
+    m[torch.rand(n, S, generator=g) > frac] = 0
+    return m.to(device)
+
+
+def test_gpu_cells_compaction_matches_emulation():
+    n, S = 1000, 100
+    mask = _sparse_mask(n, S, 0.04, 0)
+    c = pc.Cells(mask, n, S)
+    g = pc.Cells(mask.cuda(), n, S)
+    torch.cuda.synchronize()
+    nact = int(c.totals[0])
+    assert torch.equal(g.totals.cpu(), c.totals)
+    for k in ("bucket_off", "bucket_cnt", "tile_off", "cellrow"):
+        assert torch.equal(getattr(g, k).cpu(), getattr(c, k)), k
+    assert torch.equal(g.rowimg[:nact].cpu(), c.rowimg[:nact])
+    assert torch.equal(g.rowcell[:nact].cpu(), c.rowcell[:nact])
+
+
+def test_gpu_sparse_pconv_pwgrad_match_emulation():
+    """rows mode (logits of the active cells), gather mode (their input gradient, zero-row
+    MFMA skipping) and the rows-mode weight gradient vs the torch emulation"""
+    torch.manual_seed(0)
+    M, S, cin = 700, 100, 32
+    fwd, dg, wg = pc.convt_pairs(8, 8, (10, 10))
+    mask = _sparse_mask(M, S, 0.05, 1)
+    cc, cg = pc.Cells(mask, M, S), pc.Cells(mask.cuda(), M, S)
+    x = torch.randn(64 * M * cin).to(BF)
+    B = (torch.randn(9 * 78 * cin) * 0.1).to(BF)
+    bias = torch.randn(78)
+    Zc = torch.zeros(cc.cap * 96, dtype=BF)
+    Zg = torch.zeros(cc.cap * 96, dtype=BF, device="cuda")
+    pc.pconv(x, M * cin, cin, cin, B, pc.pconv_table(fwd, "cpu"), 78, M, Zc, 0, 96, bias=bias,
+             cells=cc)
+    pc.pconv(x.cuda(), M * cin, cin, cin, B.cuda(), pc.pconv_table(fwd, "cuda"), 78, M, Zg, 0, 96,
+             bias=bias.cuda(), cells=cg)
+    nact = int(cc.totals[0])
+    a, b = Zg.view(-1, 96)[:nact, :78].cpu(), Zc.view(-1, 96)[:nact, :78]
+    assert _rel(a, b) < 1e-2
+    # gather-mode dgrad from compact dZ rows
+    dZ = torch.randn(cc.cap * 96).to(BF)
+    dZ.view(-1, 96)[:, 78:] = 0
+    Bd = (torch.randn(9 * 32 * 96) * 0.1).to(BF)
+    ym = torch.randn(64 * M * 32).to(BF)
+    gc_ = torch.zeros(64 * M * 32, dtype=BF)
+    gg = torch.zeros(64 * M * 32, dtype=BF, device="cuda")
+    pc.pconv(dZ, 0, 96, 96, Bd, pc.pconv_table(dg, "cpu"), 32, M, gc_, M * 32, 32, mask=ym,
+             gather=cc)
+    pc.pconv(dZ.cuda(), 0, 96, 96, Bd.cuda(), pc.pconv_table(dg, "cuda"), 32, M, gg, M * 32, 32,
+             mask=ym.cuda(), gather=cg)
+    torch.cuda.synchronize()
+    assert _rel(gg.cpu(), gc_) < 1e-2
+    # rows-mode weight gradient
+    gmap = torch.arange(9 * 96 * 32, dtype=torch.int32)
+    wc = torch.empty(9 * 96 * 32)
+    wgpu = torch.empty(9 * 96 * 32, device="cuda")
+    pc.pwgrad(dZ, 0, 96, 96, x, M * cin, cin, cin, pc.wgrad_table(wg, "cpu"), M, gmap, wc,
+              cells=cc)
+    pc.pwgrad(dZ.cuda(), 0, 96, 96, x.cuda(), M * cin, cin, cin, pc.wgrad_table(wg, "cuda"), M,
+              gmap.cuda(), wgpu, cells=cg)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(wgpu.cpu(), wc, rtol=2e-3, atol=2e-2)
+    out_c, out_g = torch.empty(78), torch.empty(78, device="cuda")
+    cc.rows_colsum(dZ, 96, 78, out_c)
+    cg.rows_colsum(dZ.cuda(), 96, 78, out_g)
+    torch.testing.assert_close(out_g.cpu(), out_c, rtol=1e-3, atol=1e-2)
+
+
+def test_gpu_masked_cell_rows_match_pbc():
+    """compact-row scoring / sampling / backward == the pixel-major kernels at every active
+    cell (same Philox draws), zero elsewhere"""
+    torch.manual_seed(0)
+    S, n = 100, 300
+    lg = torch.randn(S, n, pc.LOGIT_LD, device="cuda").to(BF)
+    mask = _sparse_mask(n, S, 0.08, 2, "cuda")
+    cells = pc.Cells(mask, n, S)
+    nact = int(cells.totals[0])
+    rc = cells.rowcell[:nact].long()
+    Zc = torch.zeros(cells.cap, pc.LOGIT_LD, dtype=BF, device="cuda")
+    Zc[:nact] = lg.permute(1, 0, 2).reshape(n * S, -1)[rc]
+    rng = torch.tensor([11, 5], dtype=torch.int64, device="cuda")
+    a1, lp1 = cell_head.sample_rows(Zc, cells, mask, rng.clone())
+    a2, lp2 = cell_head.sample_pbc(lg, mask, rng.clone())
+    assert torch.equal(a1, a2)
+    torch.testing.assert_close(lp1, lp2)
+    Zr = Zc.clone().requires_grad_(True)
+    lgr = lg.clone().requires_grad_(True)
+    lp, ent = cell_head.score_rows(Zr, cells, mask, a1)
+    lq, eq = cell_head.score_pbc(lgr, mask, a1)
+    torch.testing.assert_close(lp, lq)
+    torch.testing.assert_close(ent, eq)
+    gl, ge = torch.randn(n, device="cuda"), torch.randn(n, device="cuda")
+    ((lp * gl).sum() + (ent * ge).sum()).backward()
+    ((lq * gl).sum() + (eq * ge).sum()).backward()
+    d_dense = lgr.grad.permute(1, 0, 2).reshape(n * S, -1)
+    assert torch.equal(Zr.grad[:nact], d_dense[rc])
+
+
+@pytest.mark.parametrize("s", [10, 16])
+def test_gpu_gridnet_sparse_matches_dense(s):
+    """evaluate() through the active-cell rows == through the dense logits layer (GPU)"""
+    from microbeast_amd.models.gridnet import GridNetAgent
+    torch.manual_seed(0)
+    m = GridNetAgent((s, s, 27)).cuda()
+    d = copy.deepcopy(m)
+    d.sparse_logits = False
+    n, ns = 300, 256
+    obs = obs_bits(n, s * s, 5).cuda()
+    mask = _sparse_mask(ns, s * s, 0.05, 1, "cuda")
+    act = torch.randint(0, 4, (ns, s * s, 7), dtype=torch.uint8, device="cuda")
+    lp, ent, v = m.evaluate(obs, mask, act, ns)
+    lq, eq, vq = d.evaluate(obs, mask, act, ns)
+    torch.testing.assert_close(lp, lq)
+    torch.testing.assert_close(ent, eq)
+    torch.testing.assert_close(v, vq)
+    (lp.sum() + 0.3 * ent.sum() + v.sum()).backward()
+    (lq.sum() + 0.3 * eq.sum() + vq.sum()).backward()
+    for (name, p), (_, q) in zip(m.named_parameters(), d.named_parameters()):
+        assert _rel(p.grad, q.grad) < 1e-3, name
+
+
+@pytest.mark.parametrize("H,O,I,x_relu,crop", [(8, 64, 32, True, None), (4, 128, 64, False, None),
+                                                (2, 256, 128, False, None),
+                                                (4, 32, 64, False, (8, 8))])
+def test_gpu_pwgrad_all_matches_emulation(H, O, I, x_relu, crop):
+    torch.manual_seed(0)
+    M = 700
+    if crop is None:
+        fwd, _, _ = pc.conv_pairs(H, H)
+        npo = H * H
+    else:
+        fwd, _, _ = pc.convt_pairs(H, H, crop)
+        npo = crop[0] * crop[1]
+    g = torch.randn(npo * M * O).to(BF)
+    x = torch.randn(H * H * M * I).to(BF)
+    gmap = torch.arange(9 * O * I, dtype=torch.int32).flip(0)
+    gmap[::5] = -1
+    out_c = torch.empty(9 * O * I)
+    out_g = torch.empty(9 * O * I, device="cuda")
+    pc.pwgrad_all(g, M * O, O, O, x, M * I, I, I, pc.pconv_table(fwd, "cpu"), 9, M, gmap, out_c,
+                  x_relu=x_relu)
+    pc.pwgrad_all(g.cuda(), M * O, O, O, x.cuda(), M * I, I, I, pc.pconv_table(fwd, "cuda"), 9, M,
+                  gmap.cuda(), out_g, x_relu=x_relu)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out_g.cpu(), out_c, rtol=2e-3, atol=2e-2)

@@ -213,3 +213,96 @@ def test_direct_grads_learner_step_matches_accumulated():
             assert lr.flat.check_grad_views()
         outs.append(lr.flat.data.clone())
     torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=0)
+
+
+def _sparse_mask(n, S, frac, seed):
+    g = torch.Generator().manual_seed(seed)
+    m = torch.randint(0, 2 ** 31 - 1, (n, S, 3), generator=g, dtype=torch.int32)
+    m[..., 2] &= (1 << 14) - 1
+    m[torch.rand(n, S, generator=g) > frac] = 0
+    return m
+
+
+def test_cells_compaction_order_and_maps():
+    n, S = 7, 12
+    mask = _sparse_mask(n, S, 0.3, 0)
+    c = pc.Cells(mask, n, S)
+    act = (mask != 0).any(-1)
+    nact = int(act.sum())
+    assert int(c.totals[0]) == nact
+    cells = [int(x) for x in c.rowcell[:nact]]
+    assert cells == sorted(cells, key=lambda v: (v % S, v // S))       # (cell, sample) order
+    assert all(act[v // S, v % S] for v in cells)
+    assert torch.equal(c.rowimg[:nact], c.rowcell[:nact] // S)
+    for P in range(S):
+        o, k = int(c.bucket_off[P]), int(c.bucket_cnt[P])
+        assert all(int(v) % S == P for v in c.rowcell[o:o + k])
+    cr = c.cellrow.view(S, n)
+    for P in range(S):
+        for b in range(n):
+            r = int(cr[P, b])
+            assert (r >= 0) == bool(act[b, P]) and (r < 0 or int(c.rowcell[r]) == b * S + P)
+    assert int(c.tile_off[-1]) == int(c.totals[1])
+
+
+@pytest.mark.parametrize("s", [10, 16])
+def test_sparse_logits_match_dense(s):
+    """scoring through the compact active-cell rows == the dense pixel-major logits layer:
+    log-probs, entropies, values and every parameter gradient (emulated bf16 maths)"""
+    from microbeast_amd.models.gridnet import GridNetAgent
+    torch.manual_seed(0)
+    m = GridNetAgent((s, s, 27))
+    m.emulate = True
+    d = copy.deepcopy(m)
+    d.sparse_logits = False
+    n, ns = 6, 4
+    obs = obs_bits(n, s * s, 5)
+    mask = _sparse_mask(ns, s * s, 0.05, 1)
+    act = torch.randint(0, 4, (ns, s * s, 7), dtype=torch.uint8)
+    lp, ent, v = m.evaluate(obs, mask, act, ns)
+    lq, eq, vq = d.evaluate(obs, mask, act, ns)
+    torch.testing.assert_close(lp, lq)
+    torch.testing.assert_close(ent, eq)
+    torch.testing.assert_close(v, vq)
+    (lp.sum() + 0.3 * ent.sum() + v.sum()).backward()
+    (lq.sum() + 0.3 * eq.sum() + vq.sum()).backward()
+    for (name, p), (_, q) in zip(m.named_parameters(), d.named_parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6, msg=name)
+
+
+def test_sparse_act_matches_dense():
+    from microbeast_amd.models.gridnet import GridNetAgent
+    torch.manual_seed(0)
+    m = GridNetAgent((10, 10, 27))
+    m.emulate = True
+    d = copy.deepcopy(m)
+    d.sparse_logits = False
+    obs = obs_bits(5, 100, 2)
+    mask = _sparse_mask(5, 100, 0.1, 3)
+    a1, lp1, v1 = m.act(obs, mask, generator=torch.Generator().manual_seed(4))
+    a2, lp2, v2 = d.act(obs, mask, generator=torch.Generator().manual_seed(4))
+    active = (mask != 0).any(-1)
+    assert torch.equal(a1[active], a2[active])
+    torch.testing.assert_close(lp1, lp2)
+    torch.testing.assert_close(v1, v2)
+
+
+@pytest.mark.parametrize("H,crop", [(8, None), (4, None), (8, (10, 10))])
+def test_pwgrad_all_equals_per_tap(H, crop):
+    """the all-taps (forward-table) weight gradient == the per-tap form (emulation)"""
+    torch.manual_seed(0)
+    M, O, I = 40, 16, 8
+    if crop is None:
+        fwd, _, wg = pc.conv_pairs(H, H)
+        npo = H * H
+    else:
+        fwd, _, wg = pc.convt_pairs(H, H, crop)
+        npo = crop[0] * crop[1]
+    g = torch.randn(npo * M * O)
+    x = torch.randn(H * H * M * I)
+    gmap = torch.arange(9 * O * I, dtype=torch.int32)
+    a, b = torch.empty(9 * O * I), torch.empty(9 * O * I)
+    pc.pwgrad(g, M * O, O, O, x, M * I, I, I, pc.wgrad_table(wg, "cpu"), M, gmap, a, x_relu=True)
+    pc.pwgrad_all(g, M * O, O, O, x, M * I, I, I, pc.pconv_table(fwd, "cpu"), 9, M, gmap, b,
+                  x_relu=True)
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
