@@ -43,6 +43,7 @@ _SIGS = {
     "mbk_masked_cell_bwd_pbc": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
                                 c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_pconv": [c_void_p, c_void_p],
+    "mbk_imgconv": [c_void_p, c_int, c_void_p],
     "mbk_cells_nchunk": [c_int],
     "mbk_cells_compact": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

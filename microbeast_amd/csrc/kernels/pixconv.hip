@@ -417,6 +417,141 @@ __global__ __launch_bounds__(kThreads) void sparse_dgrad_kernel(PConvArgs a, int
   }
 }
 
+// ------------------------------------------------------------------ image-tile conv3x3
+// conv3x3 / stride 1 / pad 1 on H x H maps with the input of TI = 256 / H^2 whole images held
+// in a halo'd LDS tile, so all 9 taps read A from LDS (the per-pixel GEMM above re-reads every
+// input row once per tap through L2: 7.6x at 8x8). Rows = TI images x H^2 pixels (one image per
+// wave at 8x8), N = NOUT output channels, K = 9 taps x CIN. Input / output are addressed as
+// (pixel stride, image stride) like pconv (NHWC or pixel-major), with relu-on-load, bias, relu
+// and a relu-mask epilogue, so the same kernel runs GridNet conv2's forward (NHWC in, pixel-
+// major out) and its input gradient (pixel-major dY in, flipped / transposed weights, NHWC out
+// masked by the first layer's output). Weight fragments come from L1 / L2 (36 KB), so only the
+// image tile takes LDS (37 / 58 KB: 2-4 workgroups per CU); the next tile's input is
+// prefetched into registers during this tile's MFMAs.
+template <int CIN, int NOUT, int H>
+struct ImgCfg {
+  static constexpr int HP = H + 2, NPIX = H * H, TI = 256 / NPIX;
+  static constexpr int PST = CIN * 2 + 16;                 // LDS pixel stride (bytes)
+  static constexpr int IN_BYTES = TI * HP * HP * PST;
+  static constexpr int OROW = NOUT * 2 + 16;
+  static constexpr int OUT_BYTES = 256 * OROW;
+  static constexpr int TILE_BYTES = IN_BYTES > OUT_BYTES ? IN_BYTES : OUT_BYTES;
+  static constexpr int WROW = CIN * 2 + 16;
+  static constexpr int W_BYTES = 9 * NOUT * WROW;
+  static constexpr int C8 = CIN / 8;
+  static constexpr int LE = TI * NPIX * C8 / kThreads;     // 16-byte input chunks per thread
+  static constexpr int NJ = NOUT / 16;
+  static_assert(TI * NPIX == 256 && H * H % 16 == 0, "one 64-row slab per wave");
+  static_assert(TI * NPIX * C8 % kThreads == 0, "input staging");
+};
+
+template <int CIN, int NOUT, int H>
+__global__ __launch_bounds__(kThreads) void imgconv_kernel(PConvArgs a, int ntiles) {
+  using S = ImgCfg<CIN, NOUT, H>;
+  extern __shared__ __attribute__((aligned(16))) char ism[];
+  char* tile = ism;                       // input tile, then the output staging tile
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  // zero the whole input tile once: the halo ring is never written again
+  for (int e = tid * 16; e < S::IN_BYTES; e += kThreads * 16)
+    *(uint4*)(tile + e) = make_uint4(0, 0, 0, 0);
+  uint4 ra[S::LE];
+  auto load = [&](int t) {
+#pragma unroll
+    for (int j = 0; j < S::LE; ++j) {
+      const int e = tid + j * kThreads, c8 = e % S::C8, rp = e / S::C8;   // rp = (image, pixel)
+      const int i = rp / S::NPIX, p = rp - i * S::NPIX, m = t * S::TI + i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (m < a.M) v = *(const uint4*)(a.A + (long long)p * a.a_ps + (long long)m * a.a_bs + c8 * 8);
+      ra[j] = a.a_relu ? relu8(v) : v;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int j = 0; j < S::LE; ++j) {
+      const int e = tid + j * kThreads, c8 = e % S::C8, rp = e / S::C8;
+      const int i = rp / S::NPIX, p = rp - i * S::NPIX, y = p / H, x = p - y * H;
+      *(uint4*)(tile + ((i * S::HP + y + 1) * S::HP + x + 1) * S::PST + c8 * 16) = ra[j];
+    }
+  };
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  __syncthreads();   // weights + zeroed tile
+  for (; t < ntiles; t += gridDim.x) {
+    store();
+    __syncthreads();
+    if (t + gridDim.x < ntiles) load(t + gridDim.x);
+    // wave w: rows [64 w, 64 w + 64) = 4 row blocks of 16 (image / pixel from the row index)
+    f32x4 acc[4][S::NJ];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int j = 0; j < S::NJ; ++j) acc[mb][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int pbase[4];
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      const int r = wave * 64 + mb * 16 + li, i = r / S::NPIX, p = r - i * S::NPIX;
+      const int y = p / H, x = p - y * H;
+      pbase[mb] = ((i * S::HP + y) * S::HP + x) * S::PST;   // tap (0, 0) of this row
+    }
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      const int ky = tp / 3, kx = tp % 3, toff = (ky * S::HP + kx) * S::PST;
+#pragma unroll
+      for (int c0 = 0; c0 < CIN; c0 += 32) {
+        Frag8 fb[S::NJ];
+#pragma unroll
+        for (int j = 0; j < S::NJ; ++j)   // weights [9][NOUT][CIN]: 36 KB, L1 / L2 resident
+          fb[j].u = *(const uint4*)(a.B + (size_t)(tp * NOUT + j * 16 + li) * CIN + c0 + 8 * g);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+          Frag8 fa;
+          fa.u = *(const uint4*)(tile + pbase[mb] + toff + (c0 + 8 * g) * 2);
+#pragma unroll
+          for (int j = 0; j < S::NJ; ++j)
+            acc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa.v, fb[j].v, acc[mb][j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();   // all waves done reading the input tile: it becomes the output tile
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int trow = wave * 64 + mb * 16 + 4 * g + r;
+#pragma unroll
+        for (int j = 0; j < S::NJ; ++j) {
+          const int col = j * 16 + li;
+          float v = acc[mb][j][r] + (a.bias ? a.bias[col] : 0.f);
+          if (a.relu) v = fmaxf(v, 0.f);
+          *(bf16*)(tile + trow * S::OROW + col * 2) = __float2bfloat16(v);
+        }
+      }
+    __syncthreads();
+    constexpr int OC8 = NOUT / 8;
+    for (int e = tid; e < 256 * OC8; e += kThreads) {
+      const int trow = e / OC8, c8 = e - trow * OC8;
+      const int i = trow / S::NPIX, p = trow - i * S::NPIX, m = t * S::TI + i;
+      if (m >= a.M) continue;
+      const long long o = (long long)p * a.c_ps + (long long)m * a.c_bs + c8 * 8;
+      uint4 v = *(const uint4*)(tile + trow * S::OROW + c8 * 16);
+      if (a.mask) v = mask8(v, *(const uint4*)(a.mask + o));
+      *(uint4*)(a.C + o) = v;
+    }
+    __syncthreads();   // output tile read before the next input tile is stored
+    // (the halo ring of the input tile was overwritten by the output staging: re-zero it)
+    for (int e = tid; e < S::TI * (S::HP * S::HP - S::NPIX) * S::C8; e += kThreads) {
+      const int c8 = e % S::C8, hp = e / S::C8, i = hp / (S::HP * S::HP - S::NPIX);
+      int q = hp - i * (S::HP * S::HP - S::NPIX);      // q-th halo pixel of image i
+      int y, x;
+      if (q < S::HP) { y = 0; x = q; }
+      else if (q < 2 * S::HP) { y = S::HP - 1; x = q - S::HP; }
+      else { q -= 2 * S::HP; y = 1 + (q >> 1); x = (q & 1) ? S::HP - 1 : 0; }
+      *(uint4*)(tile + ((i * S::HP + y) * S::HP + x) * S::PST + c8 * 16) = make_uint4(0, 0, 0, 0);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 // partial[part][t][o][i] = sum over tap t's pairs (P, q) and this part's images b of
 // g[P][b][o] * x[q][b][i]. Output tile OC x IC per workgroup; a stage stages R images of one
@@ -1207,6 +1342,38 @@ extern "C" int mbk_pconv(const long long* v, hipStream_t st) {
     else if (a.N <= 96) launch_pconv<128, 96, 4, 1, 0>(a, nz, 0, st);
     else launch_pconv<128, 128, 2, 2, 0>(a, nz, 0, st);
   }
+  return (int)hipGetLastError();
+}
+
+// image-tile conv3x3 (args as mbk_pconv; B = [9][N][cin] in tap order 0..8, no table):
+// supported (cin, N, H) = (32, 64, 8), (64, 32, 8)
+extern "C" int mbk_imgconv(const long long* v, int H, hipStream_t st) {
+  PConvArgs a{};
+  a.A = (const bf16*)v[0]; a.a_ps = v[1]; a.a_bs = v[2]; a.cin = (int)v[3]; a.a_relu = (int)v[4];
+  a.B = (const bf16*)v[5];
+  a.bias = (const float*)v[9]; a.relu = (int)v[10];
+  a.C = (bf16*)v[11]; a.c_ps = v[12]; a.c_bs = v[13]; a.mask = (const bf16*)v[14];
+  a.M = (int)v[15]; a.N = (int)v[16];
+  if (a.M <= 0) return 0;
+  if (a.a_bs % 8 || a.a_ps % 8 || a.c_bs % 8 || a.c_ps % 8 || ((uintptr_t)a.A & 15) ||
+      ((uintptr_t)a.B & 15) || ((uintptr_t)a.C & 15) || ((uintptr_t)a.mask & 15))
+    return (int)hipErrorInvalidValue;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+#define MBK_IC(CI, NO, HH)                                                                       \
+  do {                                                                                           \
+    using S = ImgCfg<CI, NO, HH>;                                                                \
+    const size_t sm = S::TILE_BYTES;                                                             \
+    (void)hipFuncSetAttribute((const void*)imgconv_kernel<CI, NO, HH>,                            \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);              \
+    const int ntiles = (a.M + S::TI - 1) / S::TI;                                                \
+    const int grid = std::min(ntiles, ncu * std::min(4, (int)(160 * 1024 / sm)));                \
+    hipLaunchKernelGGL((imgconv_kernel<CI, NO, HH>), dim3(grid), dim3(kThreads), sm, st, a, ntiles); \
+  } while (0)
+  if (a.cin == 32 && a.N == 64 && H == 8) MBK_IC(32, 64, 8);
+  else if (a.cin == 64 && a.N == 32 && H == 8) MBK_IC(64, 32, 8);
+  else return (int)hipErrorInvalidValue;
+#undef MBK_IC
   return (int)hipGetLastError();
 }
 

@@ -334,6 +334,34 @@ def _ident_map(C: int, device) -> torch.Tensor:
     return _IDENT[key]
 
 
+def imgconv(A, a_ps, a_bs, cin, B, N, M, C, c_ps, c_bs, H, bias=None, relu=False, a_relu=False,
+            mask=None):
+    """conv3x3 / pad 1 on H x H maps with whole images in LDS (``imgconv_kernel``; GPU only):
+    C[P][b][:N] = relu?(bias + sum_t relu?(A[P + s_t][b]) . B[t]^T), B [9][N][cin] in tap order
+    (ky, kx) with source offset (ky - 1, kx - 1); (pixel stride, image stride) operands."""
+    assert A.is_cuda and 9 * N * cin <= B.numel()
+    _fits(A, H * H - 1, a_ps, M, a_bs, cin, "imgconv A")
+    _fits(C, H * H - 1, c_ps, M, c_bs, N, "imgconv C")
+    if mask is not None:
+        _fits(mask, H * H - 1, c_ps, M, c_bs, N, "imgconv mask")
+    N_ = _N()
+    args = (ctypes.c_longlong * 17)(A.data_ptr(), a_ps, a_bs, cin, int(a_relu), B.data_ptr(), 0,
+                                    0, 0, bias.data_ptr() if bias is not None else 0, int(relu),
+                                    C.data_ptr(), c_ps, c_bs,
+                                    mask.data_ptr() if mask is not None else 0, M, N)
+    N_.check(N_.kernels().mbk_imgconv(args, H, N_.stream_ptr()), "imgconv")
+    return C
+
+
+_IMGCONV = os.environ.get("MBK_GRID_IMGCONV", "1") == "1"
+
+
+def _imgconv_ok(L, dev) -> bool:
+    """the image-tile kernel covers GridNet's 8x8 32 -> 64 conv (forward and input gradient)"""
+    return (_IMGCONV and dev.type == "cuda" and L.H == 8 and L.W == 8 and L.cin == 32
+            and L.cout == 64)
+
+
 def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False, cells=None):
     """out.flat[j] = dW[gmap[j]] (0 where gmap < 0), dW [ntap][O][I] fp32 with
     dW[t] = sum_{(P, q) in tab[t]} sum_{b < M} g[P][b][:O]^T relu?(x[q][b][:I]).
@@ -688,6 +716,8 @@ class PixPlan:
                 gm = (tt * L.cout * L.cin_p + oo * L.cin_p + c3).reshape(-1).int()
             L.fmap, L.dmap, L.gmap = fm.to(dev), dm.to(dev), gm.to(dev)
             L.fshape, L.dshape = (9, L.cout, L.cin_p), (9, L.cin_p, L.cop)
+            # input gradient as a forward conv over dY: tap (ky, kx) uses W[2-ky, 2-kx]^T
+            L.dmap_flip = dm.view(9, -1, L.cop).flip(0).reshape(-1).contiguous().to(dev)
             self.enc.append(L)
             H, W = (H + 1) // 2, (W + 1) // 2
         self.zh, self.zw = H, W
@@ -743,7 +773,10 @@ class PixPlan:
         for i, (c, L) in enumerate(zip(self.convs, self.enc)):
             fw = seg(c.weight, L.fmap, L.fshape) if not (i == 0 and self.enc0 is not None) \
                 else None
-            dw = seg(c.weight, L.dmap, L.dshape) if with_dgrad and i > 0 else None
+            dw = None
+            if with_dgrad and i > 0:
+                dw = seg(c.weight, L.dmap_flip if _imgconv_ok(L, self.device) else L.dmap,
+                         L.dshape)
             out["enc"].append((fw, dw))
         for t, L in zip(self.convts, self.dec):
             out["dec"].append((seg(t.weight, L.fmap, L.fshape),
@@ -807,8 +840,12 @@ class _GridNetPBC(torch.autograd.Function):
         for i in range(start, len(plan.enc)):
             L, c = plan.enc[i], plan.convs[i]
             y = torch.empty(L.H * L.W, n, L.cout, dtype=_BF, device=dev)
-            pconv(x[0], x[1], x[2], x[3], pk["enc"][i][0], L.tf, L.cout, n, y, n * L.cout,
-                  L.cout, bias=c.bias.detach(), relu=True, a_relu=x[4])
+            if _imgconv_ok(L, dev):
+                imgconv(x[0], x[1], x[2], x[3], pk["enc"][i][0], L.cout, n, y, n * L.cout,
+                        L.cout, L.H, bias=c.bias.detach(), relu=True, a_relu=x[4])
+            else:
+                pconv(x[0], x[1], x[2], x[3], pk["enc"][i][0], L.tf, L.cout, n, y, n * L.cout,
+                      L.cout, bias=c.bias.detach(), relu=True, a_relu=x[4])
             pooled, idx = ppool_fwd(y, L.H, L.W, n, L.cout)
             del y
             acts.append(x)
@@ -935,12 +972,20 @@ class _GridNetPBC(torch.autograd.Function):
                 # its pre-relu pooled output
                 p = ctx.pools[0][0]
                 gx = torch.empty_like(p)
-                pconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.td, L.cin, n, gx,
-                      xa[1], xa[2], mask=p)
+                if _imgconv_ok(L, dev):
+                    imgconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.cin, n, gx,
+                            xa[1], xa[2], L.H, mask=p)
+                else:
+                    pconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.td, L.cin, n, gx,
+                          xa[1], xa[2], mask=p)
             else:
                 gx = torch.empty(L.H * L.W, n, L.cin, dtype=_BF, device=dev)
-                pconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.td, L.cin, n, gx,
-                      n * L.cin, L.cin)
+                if _imgconv_ok(L, dev):
+                    imgconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.cin, n, gx,
+                            n * L.cin, L.cin, L.H)
+                else:
+                    pconv(dy, n * L.cout, L.cout, L.cout, pk["enc"][i][1], L.td, L.cin, n, gx,
+                          n * L.cin, L.cin)
             g1, n1, g2, n2 = gx, n, None, 0
         return (None, None, None, None, None, None) + tuple(grads)
 

@@ -300,3 +300,31 @@ def test_gpu_pwgrad_all_matches_emulation(H, O, I, x_relu, crop):
                   gmap.cuda(), out_g, x_relu=x_relu)
     torch.cuda.synchronize()
     torch.testing.assert_close(out_g.cpu(), out_c, rtol=2e-3, atol=2e-2)
+
+
+@pytest.mark.parametrize("cin,N,layout", [(32, 64, "nhwc_in"), (64, 32, "nhwc_out")])
+def test_gpu_imgconv_matches_pconv(cin, N, layout):
+    """the image-tile conv3x3 (8x8) == the per-pixel GEMM over the same conv table: GridNet
+    conv2's forward (NHWC relu'd input -> pixel-major + bias + relu) and its input gradient
+    (pixel-major dY, flipped weights -> NHWC, relu-masked)"""
+    torch.manual_seed(0)
+    M, H = 301, 8
+    P = H * H
+    fwd, _, _ = pc.conv_pairs(H, H)
+    A = torch.randn(P * M * cin, device="cuda").to(BF)
+    B = (torch.randn(9 * N * cin, device="cuda") * 0.1).to(BF)
+    if layout == "nhwc_in":
+        a_ps, a_bs, c_ps, c_bs = cin, P * cin, M * N, N
+        kw = dict(bias=torch.randn(N, device="cuda"), relu=True, a_relu=True)
+        mask = None
+    else:
+        a_ps, a_bs, c_ps, c_bs = M * cin, cin, N, P * N
+        kw = {}
+        mask = torch.randn(P * M * N, device="cuda").to(BF)
+    C1 = torch.zeros(P * M * N, dtype=BF, device="cuda")
+    C2 = torch.zeros(P * M * N, dtype=BF, device="cuda")
+    pc.pconv(A, a_ps, a_bs, cin, B, pc.pconv_table(fwd, "cuda"), N, M, C1, c_ps, c_bs, mask=mask,
+             **kw)
+    pc.imgconv(A, a_ps, a_bs, cin, B, N, M, C2, c_ps, c_bs, H, mask=mask, **kw)
+    torch.cuda.synchronize()
+    assert _rel(C2, C1) < 1e-2
