@@ -44,6 +44,8 @@ _SIGS = {
                                 c_void_p, c_int64, c_void_p, c_void_p],
     "mbk_pconv": [c_void_p, c_void_p],
     "mbk_imgconv": [c_void_p, c_int, c_void_p],
+    "mbk_imgwgrad": [c_void_p, c_int, c_void_p],
+    "mbk_imgwgrad_parts": [],
     "mbk_cells_nchunk": [c_int],
     "mbk_cells_compact": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],

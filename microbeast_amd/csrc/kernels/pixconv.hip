@@ -850,6 +850,110 @@ __global__ __launch_bounds__(kThreads) void pwgrad_all_kernel(PWgradAllArgs a) {
   }
 }
 
+// Image-tile weight gradient of the 8x8 conv3x3 (GridNet conv2): dW[t][o][i] = sum over
+// images b and pixels P of dy[P][b][o] x[b][P + s_t][i]. A workgroup stages TI = 4 images at
+// a time -- dy as 256 K-rows (image, pixel) x O and x as a halo'd [4][10][10][I] tile -- and
+// every tap reads its shifted x rows straight from the tile (per-lane tr-read addresses), so
+// each input element is read from HBM once (the per-pixel forms read x once per tap or per
+// output pixel). Wave w owns W rows [16 w, 16 w + 16) and all 9 taps x I columns in registers;
+// persistent workgroups write one fp32 partial each (reduce_map sums them).
+template <int I_, int O_, int H>
+__global__ __launch_bounds__(kThreads) void imgwgrad_kernel(PWgradArgs a, int ntiles) {
+  constexpr int HP = H + 2, NPIX = H * H, TI = 256 / NPIX;
+  constexpr int XPST = I_ * 2 + 16, GROW = O_ * 2 + 16;
+  constexpr int XBYTES = TI * HP * HP * XPST;
+  constexpr int GE = 256 * (O_ / 8) / kThreads, XE = TI * NPIX * (I_ / 8) / kThreads;
+  constexpr int CBC = I_ / 16;
+  static_assert(O_ == 64 && TI * NPIX == 256, "4 waves x 16 W rows, 256 K rows per tile");
+  extern __shared__ __attribute__((aligned(16))) char wsm[];
+  char* xt = wsm;
+  char* gt = wsm + XBYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  for (int e = tid * 16; e < XBYTES; e += kThreads * 16) *(uint4*)(xt + e) = make_uint4(0, 0, 0, 0);
+  f32x4 acc[9][CBC];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int cb = 0; cb < CBC; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint4 pg[GE], px[XE];
+  auto load = [&](int tl) {
+#pragma unroll
+    for (int k = 0; k < GE; ++k) {
+      const int e = tid + k * kThreads, c8 = e % (O_ / 8), r = e / (O_ / 8);   // r = (img, P)
+      const int i = r / NPIX, P = r - i * NPIX, m = tl * TI + i;
+      pg[k] = m < a.M ? *(const uint4*)(a.g + (long long)P * a.g_ps + (long long)m * a.g_bs + c8 * 8)
+                      : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < XE; ++k) {
+      const int e = tid + k * kThreads, c8 = e % (I_ / 8), r = e / (I_ / 8);
+      const int i = r / NPIX, P = r - i * NPIX, m = tl * TI + i;
+      uint4 v = m < a.M ? *(const uint4*)(a.x + (long long)P * a.x_ps + (long long)m * a.x_bs + c8 * 8)
+                        : make_uint4(0, 0, 0, 0);
+      px[k] = a.x_relu ? relu8(v) : v;
+    }
+  };
+  int tl = blockIdx.x;
+  if (tl < ntiles) load(tl);
+  __syncthreads();   // zeroed halo
+  for (; tl < ntiles; tl += gridDim.x) {
+#pragma unroll
+    for (int k = 0; k < GE; ++k) {
+      const int e = tid + k * kThreads, c8 = e % (O_ / 8), r = e / (O_ / 8);
+      *(uint4*)(gt + r * GROW + c8 * 16) = pg[k];
+    }
+#pragma unroll
+    for (int k = 0; k < XE; ++k) {
+      const int e = tid + k * kThreads, c8 = e % (I_ / 8), r = e / (I_ / 8);
+      const int i = r / NPIX, P = r - i * NPIX, y = P / H, x = P - y * H;
+      *(uint4*)(xt + ((i * HP + y + 1) * HP + x + 1) * XPST + c8 * 16) = px[k];
+    }
+    __syncthreads();
+    if (tl + gridDim.x < ntiles) load(tl + gridDim.x);
+#pragma unroll 1
+    for (int kb = 0; kb < 256 / 32; ++kb) {
+      int prow[2], xrow[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int r = kb * 32 + 8 * G + 4 * hh + (li >> 2);
+        const int i = r / NPIX, P = r - i * NPIX, y = P / H, x = P - y * H;
+        prow[hh] = r * GROW;
+        xrow[hh] = ((i * HP + y) * HP + x) * XPST;          // tap (0, 0) source pixel
+      }
+      Frag8 af;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        af.h[hh] = tr_read(gt + prow[hh] + (16 * wave + 4 * (li & 3)) * 2);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int toff = ((t / 3) * HP + (t % 3)) * XPST;
+#pragma unroll
+        for (int cb = 0; cb < CBC; ++cb) {
+          Frag8 bfr;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+            bfr.h[hh] = tr_read(xt + xrow[hh] + toff + (cb * 16 + 4 * (li & 3)) * 2);
+          acc[t][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, bfr.v, acc[t][cb], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();   // tiles consumed before the next store
+  }
+  float* out = a.partial + (size_t)blockIdx.x * 9 * O_ * I_;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int cb = 0; cb < CBC; ++cb) {
+      const int ci = cb * 16 + li;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 16 * wave + 4 * G + i;
+        out[((size_t)t * O_ + o) * I_ + ci] = acc[t][cb][i];
+      }
+    }
+}
+
 // dst[j] = sum_p partial[p * stride + map[j]] (map[j] < 0: 0), fixed order: the weight
 // gradient in the parameter's own layout
 __global__ __launch_bounds__(kThreads) void reduce_map_kernel(const float* __restrict__ partial,
@@ -1485,6 +1589,34 @@ extern "C" int mbk_rows_colsum(const void* Z, int ld, int C, const int* totals, 
   if (C <= 0) return 0;
   hipLaunchKernelGGL(rows_colsum_kernel, dim3(nblk, (C + 63) / 64), dim3(kThreads), 0, st,
                      (const bf16*)Z, ld, C, totals, partial);
+  return (int)hipGetLastError();
+}
+
+// image-tile weight gradient (args as mbk_pwgrad minus the table: g = dY, x = input, both
+// (pixel stride, image stride); nparts = grid; partial [nparts][9][O][I]); supported
+// (I, O, H) = (32, 64, 8)
+extern "C" int mbk_imgwgrad_parts() {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+  return 2 * ncu;
+}
+extern "C" int mbk_imgwgrad(const long long* v, int H, hipStream_t st) {
+  PWgradArgs a{};
+  a.g = (const bf16*)v[0]; a.g_ps = v[1]; a.g_bs = v[2]; a.O = (int)v[3];
+  a.x = (const bf16*)v[4]; a.x_ps = v[5]; a.x_bs = v[6]; a.I = (int)v[7]; a.x_relu = (int)v[8];
+  a.M = (int)v[12];
+  const int nparts = (int)v[13];
+  a.partial = (float*)v[14];
+  if (a.M <= 0) return 0;
+  if (a.I != 32 || a.O != 64 || H != 8 || nparts < 1 || a.g_bs % 8 || a.x_bs % 8 ||
+      a.g_ps % 8 || a.x_ps % 8 || ((uintptr_t)a.g & 15) || ((uintptr_t)a.x & 15))
+    return (int)hipErrorInvalidValue;
+  constexpr int TI = 4;
+  const int ntiles = (a.M + TI - 1) / TI;
+  const size_t sm = (size_t)TI * 10 * 10 * (32 * 2 + 16) + 256 * (64 * 2 + 16);
+  (void)hipFuncSetAttribute((const void*)imgwgrad_kernel<32, 64, 8>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  hipLaunchKernelGGL((imgwgrad_kernel<32, 64, 8>), dim3(nparts), dim3(kThreads), sm, st, a, ntiles);
   return (int)hipGetLastError();
 }
 

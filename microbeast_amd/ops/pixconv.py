@@ -353,6 +353,25 @@ def imgconv(A, a_ps, a_bs, cin, B, N, M, C, c_ps, c_bs, H, bias=None, relu=False
     return C
 
 
+def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False):
+    """``pwgrad`` of a full conv3x3 on H x H maps with whole images in LDS
+    (``imgwgrad_kernel``; GPU only): dW [9][O][I] -> out via gmap."""
+    assert g.is_cuda and out.is_cuda
+    _fits(g, H * H - 1, g_ps, M, g_bs, O, "imgwgrad g")
+    _fits(x, H * H - 1, x_ps, M, x_bs, I, "imgwgrad x")
+    N_ = _N()
+    k = N_.kernels()
+    parts = k.mbk_imgwgrad_parts()
+    stride = 9 * O * I
+    partial = torch.empty(parts * stride, dtype=torch.float32, device=out.device)
+    args = (ctypes.c_longlong * 15)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
+                                    int(x_relu), 0, 0, 9, M, parts, partial.data_ptr())
+    N_.check(k.mbk_imgwgrad(args, H, N_.stream_ptr()), "imgwgrad")
+    N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
+                              out.data_ptr(), N_.stream_ptr()), "reduce_map")
+    return out
+
+
 _IMGCONV = os.environ.get("MBK_GRID_IMGCONV", "1") == "1"
 
 
@@ -963,8 +982,12 @@ class _GridNetPBC(torch.autograd.Function):
             dy = ppool_bwd(g1, n1, g2, n2, pooled, idx, L.H, L.W, n, L.cout)
             colsum(dy.view(-1, L.cout), L.cout, pg(iw + 1))
             xa = ctx.acts[i]
-            _wgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], L, 9, n, pg(iw),
-                   x_relu=xa[4])
+            if _imgconv_ok(L, dev):
+                imgwgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], n, L.gmap,
+                         pg(iw), L.H, x_relu=xa[4])
+            else:
+                _wgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], L, 9, n,
+                       pg(iw), x_relu=xa[4])
             if i == 0:
                 break
             if i == 1 and plan.enc0 is not None and ctx.acts[0] is None:

@@ -328,3 +328,23 @@ def test_gpu_imgconv_matches_pconv(cin, N, layout):
     pc.imgconv(A, a_ps, a_bs, cin, B, N, M, C2, c_ps, c_bs, H, mask=mask, **kw)
     torch.cuda.synchronize()
     assert _rel(C2, C1) < 1e-2
+
+
+@pytest.mark.parametrize("x_layout", ["nhwc", "pbc"])
+def test_gpu_imgwgrad_matches_pwgrad_all(x_layout):
+    """image-tile weight gradient of the 8x8 32 -> 64 conv == the all-taps per-pixel form"""
+    torch.manual_seed(0)
+    M, H, O, I = 301, 8, 64, 32
+    P = H * H
+    fwd, _, _ = pc.conv_pairs(H, H)
+    g = torch.randn(P * M * O, device="cuda").to(BF)
+    x = torch.randn(P * M * I, device="cuda").to(BF)
+    x_ps, x_bs = (I, P * I) if x_layout == "nhwc" else (M * I, I)
+    gmap = torch.arange(9 * O * I, dtype=torch.int32, device="cuda").flip(0)
+    a = torch.empty(9 * O * I, device="cuda")
+    b = torch.empty(9 * O * I, device="cuda")
+    pc.pwgrad_all(g, M * O, O, O, x, x_ps, x_bs, I, pc.pconv_table(fwd, "cuda"), 9, M, gmap, a,
+                  x_relu=True)
+    pc.imgwgrad(g, M * O, O, O, x, x_ps, x_bs, I, M, gmap, b, H, x_relu=True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(b, a, rtol=2e-3, atol=2e-2)
