@@ -74,13 +74,11 @@ __device__ __forceinline__ uint4 mask8(uint4 v, uint4 m) {
 }
 
 // ------------------------------------------------------------------ pixel GEMM (fwd / dgrad)
-// Sparse logits layer (MODE 1 / 2, ops/pixconv.py Cells): the active cells of a batch (any
-// legal action) are compacted into rows bucketed by map cell P, in (P, image) order
-// (cells_* kernels below). MODE 1 = the logits forward over those rows only: a persistent grid
-// walks the (bucket, 128-row) tiles, A rows are gathered by image, C rows are the compact
-// rows. MODE 2 = the logits layer's input gradient: dense output pixels, A = the compact
-// logit gradient gathered through cellrow[P][image] (-1 = inactive cell: a zero row that is
-// never loaded), and MFMAs whose 16 A rows are all inactive are skipped (per-wave flags).
+// Sparse logits layer (MODE 1, ops/pixconv.py Cells): the active cells of a batch (any legal
+// action) are compacted into rows bucketed by map cell P, in (P, image) order (cells_* kernels
+// below); the logits forward runs over those rows only: a persistent grid walks the (bucket,
+// 128-row) tiles, A rows are gathered by image, C rows are the compact rows. (Its input
+// gradient is sparse_dgrad_kernel.)
 struct PConvArgs {
   const bf16* A;
   long long a_ps, a_bs;  // A element (pixel q, image b, channel c) = A[q*a_ps + b*a_bs + c]
@@ -99,7 +97,7 @@ struct PConvArgs {
   // totals[1] = number of tiles
   const int *bucket_off, *bucket_cnt, *tile_off, *totals, *rowimg;
   int nbucket;
-  // MODE 2: compact A row of (source cell P, image m) = cellrow[P * M + m], -1 = zero row
+  // sparse_dgrad_kernel: compact A row of (source cell P, image m) = cellrow[P * M + m]
   const int* cellrow;
 };
 
@@ -112,15 +110,13 @@ struct PCfg {
   static_assert(WM * WN == 4, "4 waves");
   static_assert(MI >= 1 && NJ >= 1 && WR % 16 == 0 && WC % 16 == 0, "wave tile");
   static_assert(TM * (BK / 8) % kThreads == 0, "A staging");
-  static_assert(TM == 128, "MODE 2 row flags assume 128-row tiles");
 };
 
 // One (output pixel / bucket z, 128-row, TN-column) tile. Rows r < mcnt are valid; row r is
 // image m0 + r (MODE 0 / 2) or compact row rbase + m0 + r of image rowimg[..] (MODE 1).
 template <int TM, int TN, int WM, int WN, int MODE>
-__device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* stab,
-                                           uint16_t (*flg)[TM / 8], int z, int m0, int mcnt,
-                                           int nt, int rbase) {
+__device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* stab, int z,
+                                           int m0, int mcnt, int nt, int rbase) {
   using S = PCfg<TM, TN, WM, WN>;
   constexpr int MI = S::MI, NJ = S::NJ, AE = S::AE, BE = S::BE;
   constexpr int OROW = TN * 2 + 16;
@@ -151,7 +147,6 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[AE], rb[BE];
-  bool act[AE];
   auto load = [&](int kk) {
     const int k = kk * BK + h * 32;
     const int pair = k / a.cin, c = k - pair * a.cin + cs;
@@ -162,18 +157,7 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
 #pragma unroll
     for (int j = 0; j < AE; ++j) {
       uint4 v = make_uint4(0, 0, 0, 0);
-      act[j] = false;
-      if (on && img[j] >= 0) {
-        if (MODE == 2) {
-          const int row = a.cellrow[(long long)(ent >> 8) * a.M + img[j]];
-          if (row >= 0) {
-            v = *(const uint4*)(a.A + (long long)row * a.a_bs + c);
-            act[j] = true;
-          }
-        } else {
-          v = *(const uint4*)(ap + (long long)img[j] * a.a_bs);
-        }
-      }
+      if (on && img[j] >= 0) v = *(const uint4*)(ap + (long long)img[j] * a.a_bs);
       ra[j] = a.a_relu ? relu8(v) : v;
     }
 #pragma unroll
@@ -189,20 +173,6 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
     for (int j = 0; j < AE; ++j) {
       const int r = (tid + j * kThreads) >> 3;
       *(uint4*)(sa + buf * TM * ROWB + r * ROWB + seg * 16) = ra[j];
-      if (MODE == 2) {
-        // rows j*32 + wave*8 + (lane >> 3): bit r8 of byte h = any lane of that row and
-        // chunk loaded an active row
-        const uint64_t bal = __ballot(act[j]);
-        if (lane == 0) {
-          uint32_t f = 0;
-#pragma unroll
-          for (int r8 = 0; r8 < 8; ++r8) {
-            if ((bal >> (r8 * 8)) & 0x0Full) f |= 1u << r8;
-            if ((bal >> (r8 * 8 + 4)) & 0x0Full) f |= 1u << (8 + r8);
-          }
-          flg[buf][j * 4 + wave] = (uint16_t)f;
-        }
-      }
     }
 #pragma unroll
     for (int j = 0; j < BE; ++j) {
@@ -229,11 +199,6 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int r0 = wm * S::WR + i * 16;
-        if (MODE == 2) {
-          const int f = __builtin_amdgcn_readfirstlane(
-              (int)((flg[cur][r0 >> 3] | flg[cur][(r0 >> 3) + 1]) >> (kh * 8)) & 0xFF);
-          if (f == 0) continue;  // 16 inactive rows: zero A fragment
-        }
         fa[i].u = *(const uint4*)(ta + (r0 + li) * ROWB + kh * 64 + g * 16);
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
@@ -286,10 +251,9 @@ __global__ __launch_bounds__(kThreads) void pconv_kernel(PConvArgs a) {
   static_assert(kAB >= TM * OROW, "output tile");
   __shared__ __attribute__((aligned(16))) char sab[kAB];
   __shared__ int stab[2 + kMaxPairs];
-  __shared__ uint16_t flg[2][TM / 8];
   if (MODE != 1) {
     const int z = blockIdx.x / a.ntn, nt = blockIdx.x - z * a.ntn;
-    pconv_tile<TM, TN, WM, WN, MODE>(a, sab, stab, flg, z, blockIdx.y * TM, a.M, nt, 0);
+    pconv_tile<TM, TN, WM, WN, MODE>(a, sab, stab, z, blockIdx.y * TM, a.M, nt, 0);
     return;
   }
   // persistent walk over the (bucket, row tile, column tile) list; every workgroup ends when
@@ -303,7 +267,7 @@ __global__ __launch_bounds__(kThreads) void pconv_kernel(PConvArgs a) {
       if (a.tile_off[mid] <= tile) lo = mid; else hi = mid - 1;
     }
     const int m0 = (tile - a.tile_off[lo]) * TM;
-    pconv_tile<TM, TN, WM, WN, 1>(a, sab, stab, flg, lo, m0, a.bucket_cnt[lo], nt,
+    pconv_tile<TM, TN, WM, WN, 1>(a, sab, stab, lo, m0, a.bucket_cnt[lo], nt,
                                   a.bucket_off[lo]);
     __syncthreads();  // LDS reuse by the next tile
   }
