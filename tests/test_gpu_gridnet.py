@@ -51,3 +51,43 @@ def test_gridnet_hip_matches_torch(cuda, s):
             zip(m.named_parameters(), ref.named_parameters()) if p.grad is not None}
     assert len(errs) == len(list(m.parameters()))
     assert max(errs.values()) < 8e-2, errs
+
+
+@pytest.mark.parametrize("policy_logits", [False, True])
+def test_gridnet_engine_behaviour_logp_matches_learner(cuda, policy_logits):
+    """GridNet through the GPU actor engine: the captured policy step samples with the sparse
+    active-cell logits (policy_logits=False) or the dense pixel-major ones (True, the emitted
+    reference key); either way the behaviour log-prob of the first rollout equals what the
+    learner scores for the same weights, obs, masks and actions (ratio 1 up to bf16)."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.gridnet import GridNetAgent
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+
+    s, T, E = 10, 8, 32
+
+    def mk():
+        return GridNetAgent((s, s, 27))
+
+    torch.manual_seed(0)
+    learner = Learner(mk(), LearnerHParams(), cuda)
+    rt = GpuActorRuntime(mk, s, n_groups=1, envs_per_group=E, unroll=T, batch_slots=1,
+                         device=cuda, n_threads=2, max_steps=50, policy_logits=policy_logits)
+    rt.start(learner.flat)
+    try:
+        b, sl = rt.get_batch()
+        torch.cuda.synchronize()
+        batch = {k: v.clone() for k, v in b.items()}
+        rt.release(sl)
+    finally:
+        rt.stop()
+    m = learner.model
+    obs = batch["obs"].reshape((T + 1) * E, -1)
+    mask = batch["mask"][:T].reshape(T * E, s * s, 3)
+    act = batch["action"][:T].reshape(T * E, s * s, 7)
+    with torch.no_grad():
+        lp, _, _ = m.evaluate(obs, mask, act, n_score=T * E)
+    active = (mask != 0).any(-1).sum().item()
+    assert active > 0
+    torch.testing.assert_close(lp, batch["logp"][:T].reshape(-1), rtol=2e-2, atol=5e-2)
+    if policy_logits:
+        assert batch["policy_logits"].shape[-1] == s * s * 78
