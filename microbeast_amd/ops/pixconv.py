@@ -19,6 +19,14 @@ round 3), no MFMA work is spent on halo rows (1.6x..9x the useful work on the 8x
 the decoder needs no phase-gather pass, and the first layer's NHWC output (conv.hip stage-0
 kernels) is consumed in place through the (pixel stride, image stride) operand addressing.
 
+Two specialisations sit on top:
+
+* the 8x8 32 -> 64 conv runs on whole-image LDS tiles (``imgconv`` forward / input gradient,
+  ``imgwgrad``): all 9 taps read the input from LDS instead of re-reading it through L2;
+* the logits layer runs on the active cells only (``Cells``: compacted (cell, sample) rows;
+  ``pconv(cells=...)`` forward over them, compact masked-cell kernels in ``cell_head``,
+  ``pwgrad(cells=...)`` and the sparse input gradient ``pconv(gather=...)``).
+
 Every launcher has a plain-torch emulation of the same index maths (CPU tensors), so the whole
 network is unit-tested on CPU against the nn.Module (tests/test_pixconv.py); the GPU tests run
 the kernels against the emulation / fp32.
