@@ -103,13 +103,13 @@ struct PConvArgs {
 
 template <int TM, int TN, int WM, int WN>
 struct PCfg {
+  static constexpr int NT = WM * WN * 64;   // threads: 8 waves (2 per SIMD per workgroup)
   static constexpr int WR = TM / WM, WC = TN / WN;
   static constexpr int MI = WR / 16, NJ = WC / 16;
-  static constexpr int AE = TM * (BK / 8) / kThreads;
-  static constexpr int BE = (TN * (BK / 8) + kThreads - 1) / kThreads;
-  static_assert(WM * WN == 4, "4 waves");
+  static constexpr int AE = TM * (BK / 8) / NT;
+  static constexpr int BE = (TN * (BK / 8) + NT - 1) / NT;
   static_assert(MI >= 1 && NJ >= 1 && WR % 16 == 0 && WC % 16 == 0, "wave tile");
-  static_assert(TM * (BK / 8) % kThreads == 0, "A staging");
+  static_assert(TM * (BK / 8) % NT == 0, "A staging");
 };
 
 // One (output pixel / bucket z, 128-row, TN-column) tile. Rows r < mcnt are valid; row r is
@@ -136,7 +136,7 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
   int img[AE];
 #pragma unroll
   for (int j = 0; j < AE; ++j) {
-    const int r = (tid + j * kThreads) >> 3;
+    const int r = (tid + j * S::NT) >> 3;
     img[j] = r < mcnt - m0 ? (MODE == 1 ? a.rowimg[rbase + m0 + r] : m0 + r) : -1;
   }
 
@@ -162,7 +162,7 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
     }
 #pragma unroll
     for (int j = 0; j < BE; ++j) {
-      const int r = (tid + j * kThreads) >> 3, n = n0 + r;
+      const int r = (tid + j * S::NT) >> 3, n = n0 + r;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (on && r < TN && n < a.N) v = *(const uint4*)(bp + (size_t)n * a.cin);
       rb[j] = v;
@@ -171,12 +171,12 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
   auto store = [&](int buf) {
 #pragma unroll
     for (int j = 0; j < AE; ++j) {
-      const int r = (tid + j * kThreads) >> 3;
+      const int r = (tid + j * S::NT) >> 3;
       *(uint4*)(sa + buf * TM * ROWB + r * ROWB + seg * 16) = ra[j];
     }
 #pragma unroll
     for (int j = 0; j < BE; ++j) {
-      const int r = (tid + j * kThreads) >> 3;
+      const int r = (tid + j * S::NT) >> 3;
       if (r < TN) *(uint4*)(sb + buf * TN * ROWB + r * ROWB + seg * 16) = rb[j];
     }
   };
@@ -226,7 +226,7 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
   constexpr int C8 = TN / 8;
   bf16* cbase = a.C + (MODE == 1 ? (long long)rbase * a.c_bs : (long long)Pout * a.c_ps);
   const bf16* mbase = a.mask ? a.mask + (long long)Pout * a.c_ps : nullptr;
-  for (int e = tid; e < TM * C8; e += kThreads) {
+  for (int e = tid; e < TM * C8; e += S::NT) {
     const int trow = e / C8, c8 = e - trow * C8, m = m0 + trow, col = n0 + c8 * 8;
     if (m >= mcnt || col >= a.N) continue;
     const long long o = (long long)m * a.c_bs + col;
@@ -246,7 +246,7 @@ __device__ __forceinline__ void pconv_tile(const PConvArgs& a, char* sab, int* s
 }
 
 template <int TM, int TN, int WM, int WN, int MODE>
-__global__ __launch_bounds__(kThreads) void pconv_kernel(PConvArgs a) {
+__global__ __launch_bounds__(WM * WN * 64) void pconv_kernel(PConvArgs a) {
   constexpr int kAB = 2 * TM * ROWB + 2 * TN * ROWB, OROW = TN * 2 + 16;
   static_assert(kAB >= TM * OROW, "output tile");
   __shared__ __attribute__((aligned(16))) char sab[kAB];
@@ -1356,7 +1356,7 @@ void launch_pconv(PConvArgs& a, int nz, int grid_cap, hipStream_t st) {
   a.ntn = (a.N + TN - 1) / TN;
   dim3 grid(nz * a.ntn, (a.M + TM - 1) / TM);
   if (MODE == 1) grid = dim3(grid_cap);
-  hipLaunchKernelGGL((pconv_kernel<TM, TN, WM, WN, MODE>), grid, dim3(kThreads), 0, st, a);
+  hipLaunchKernelGGL((pconv_kernel<TM, TN, WM, WN, MODE>), grid, dim3(WM * WN * 64), 0, st, a);
 }
 
 }  // namespace
@@ -1388,8 +1388,8 @@ extern "C" int mbk_pconv(const long long* v, hipStream_t st) {
     if (!a.bucket_off || !a.bucket_cnt || !a.tile_off || !a.totals || !a.rowimg ||
         a.nbucket != nz || grid_cap < 1 || a.mask || a.N > 128)
       return (int)hipErrorInvalidValue;
-    if (a.N <= 96) launch_pconv<128, 96, 4, 1, 1>(a, nz, grid_cap, st);
-    else launch_pconv<128, 128, 2, 2, 1>(a, nz, grid_cap, st);
+    if (a.N <= 96) launch_pconv<128, 96, 4, 2, 1>(a, nz, grid_cap, st);
+    else launch_pconv<128, 128, 4, 2, 1>(a, nz, grid_cap, st);
   } else if (mode == 2) {
     // sparse input gradient: every pair's tap < ntap = (largest tap + 1) is read from B
     const int ntap = grid_cap;
@@ -1405,10 +1405,10 @@ extern "C" int mbk_pconv(const long long* v, hipStream_t st) {
     else
       hipLaunchKernelGGL(sparse_dgrad_kernel<64>, dim3(grid), dim3(kThreads), 0, st, a, ntm, ntap);
   } else {
-    if (a.N <= 32) launch_pconv<128, 32, 4, 1, 0>(a, nz, 0, st);
-    else if (a.N <= 64) launch_pconv<128, 64, 2, 2, 0>(a, nz, 0, st);
-    else if (a.N <= 96) launch_pconv<128, 96, 4, 1, 0>(a, nz, 0, st);
-    else launch_pconv<128, 128, 2, 2, 0>(a, nz, 0, st);
+    if (a.N <= 32) launch_pconv<128, 32, 8, 1, 0>(a, nz, 0, st);
+    else if (a.N <= 64) launch_pconv<128, 64, 4, 2, 0>(a, nz, 0, st);
+    else if (a.N <= 96) launch_pconv<128, 96, 4, 2, 0>(a, nz, 0, st);
+    else launch_pconv<128, 128, 4, 2, 0>(a, nz, 0, st);
   }
   return (int)hipGetLastError();
 }
