@@ -1405,7 +1405,7 @@ extern "C" int mbk_pconv(const long long* v, hipStream_t st) {
     else
       hipLaunchKernelGGL(sparse_dgrad_kernel<64>, dim3(grid), dim3(kThreads), 0, st, a, ntm, ntap);
   } else {
-    if (a.N <= 32) launch_pconv<128, 32, 8, 1, 0>(a, nz, 0, st);
+    if (a.N <= 32) launch_pconv<128, 32, 4, 1, 0>(a, nz, 0, st);
     else if (a.N <= 64) launch_pconv<128, 64, 4, 2, 0>(a, nz, 0, st);
     else if (a.N <= 96) launch_pconv<128, 96, 4, 2, 0>(a, nz, 0, st);
     else launch_pconv<128, 128, 4, 2, 0>(a, nz, 0, st);
