@@ -681,7 +681,9 @@ __global__ __launch_bounds__(kThreads) void pwgrad_kernel(PWgradArgs a) {
 // neighbouring pixels are re-read from L2. Wave w owns W rows [16 w, 16 w + 16) of the 64-row
 // chunk, all 32 input channels of the chunk and all taps (acc[tap][2 col blocks] in
 // registers; the tap loop is unrolled over a per-P slot table, so no dynamic register index).
-// Loads of the next (P, stage) are issued before this one's MFMAs.
+// Loads of the next (P, stage) are issued before this one's MFMAs. The I-chunk-0 workgroups
+// also sum g per output channel (one MFMA per K block against an all-ones fragment): the bias
+// gradient, stored after the ntap O I weight block of the part.
 constexpr int WA_R = 64;          // images per stage (K)
 constexpr int WA_OC = 64, WA_IC = 32;
 constexpr int WA_GROW = WA_OC * 2 + 16, WA_XROW = WA_IC * 2 + 16;
@@ -697,7 +699,7 @@ struct PWgradAllArgs {
   const int* tab;     // forward table rows [P_out, count, (q << 8 | t) x count]
   int tab_w, nrows;   // table width, number of output pixels
   int M, rows_per_part, nic;
-  float* partial;     // [part][ntap][O][I]
+  float* partial;     // [part][ntap O I + O]: weights, then the bias sums
   int ntap;
 };
 
@@ -716,6 +718,10 @@ __global__ __launch_bounds__(kThreads) void pwgrad_all_kernel(PWgradAllArgs a) {
   f32x4 acc[WA_MAXT][2];
 #pragma unroll
   for (int t = 0; t < WA_MAXT; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = i0 == 0;
+  f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag8 ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);   // bf16 1.0 x 8
   const int nst = b1 > b0 ? (b1 - b0 + WA_R - 1) / WA_R : 0;
   const int total = nst * a.nrows;
   uint4 pg[GE], px[WA_MAXT][XE];
@@ -782,6 +788,7 @@ __global__ __launch_bounds__(kThreads) void pwgrad_all_kernel(PWgradAllArgs a) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
         af.h[hh] = tr_read(gt + prow[hh] * WA_GROW + (16 * wave + 4 * (li & 3)) * 2);
+      if (do_bias) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, ones.v, accb, 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < WA_MAXT; ++t) {
         const int j = (int)((tmap >> (4 * t)) & 15u) - 1;
@@ -799,7 +806,13 @@ __global__ __launch_bounds__(kThreads) void pwgrad_all_kernel(PWgradAllArgs a) {
     }
   }
   if (!wave_on) return;
-  float* out = a.partial + (size_t)part * a.ntap * a.O * a.I;
+  float* out = a.partial + (size_t)part * (a.ntap * a.O * a.I + a.O);
+  if (do_bias && li == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = o0 + 16 * wave + 4 * G + i;
+      if (o < a.O) out[(size_t)a.ntap * a.O * a.I + o] = accb[i];
+    }
 #pragma unroll
   for (int t = 0; t < WA_MAXT; ++t) {
 #pragma unroll
@@ -820,7 +833,9 @@ __global__ __launch_bounds__(kThreads) void pwgrad_all_kernel(PWgradAllArgs a) {
 // every tap reads its shifted x rows straight from the tile (per-lane tr-read addresses), so
 // each input element is read from HBM once (the per-pixel forms read x once per tap or per
 // output pixel). Wave w owns W rows [16 w, 16 w + 16) and all 9 taps x I columns in registers;
-// persistent workgroups write one fp32 partial each (reduce_map sums them).
+// persistent workgroups write one fp32 partial each (reduce_map sums them). The bias
+// gradient sum_{b,P} dy[P][b][o] rides along as one more MFMA per K block against an all-ones
+// B fragment (stored after the 9 O I weight block), so dy is not read a second time for it.
 template <int I_, int O_, int H>
 __global__ __launch_bounds__(kThreads) void imgwgrad_kernel(PWgradArgs a, int ntiles) {
   constexpr int HP = H + 2, NPIX = H * H, TI = 256 / NPIX;
@@ -840,6 +855,9 @@ __global__ __launch_bounds__(kThreads) void imgwgrad_kernel(PWgradArgs a, int nt
   for (int t = 0; t < 9; ++t)
 #pragma unroll
     for (int cb = 0; cb < CBC; ++cb) acc[t][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag8 ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);   // bf16 1.0 x 8
   uint4 pg[GE], px[XE];
   auto load = [&](int tl) {
 #pragma unroll
@@ -889,6 +907,7 @@ __global__ __launch_bounds__(kThreads) void imgwgrad_kernel(PWgradArgs a, int nt
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh)
         af.h[hh] = tr_read(gt + prow[hh] + (16 * wave + 4 * (li & 3)) * 2);
+      accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af.v, ones.v, accb, 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         const int toff = ((t / 3) * HP + (t % 3)) * XPST;
@@ -904,7 +923,7 @@ __global__ __launch_bounds__(kThreads) void imgwgrad_kernel(PWgradArgs a, int nt
     }
     __syncthreads();   // tiles consumed before the next store
   }
-  float* out = a.partial + (size_t)blockIdx.x * 9 * O_ * I_;
+  float* out = a.partial + (size_t)blockIdx.x * (9 * O_ * I_ + O_);
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -916,6 +935,9 @@ __global__ __launch_bounds__(kThreads) void imgwgrad_kernel(PWgradArgs a, int nt
         out[((size_t)t * O_ + o) * I_ + ci] = acc[t][cb][i];
       }
     }
+  if (li == 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[9 * O_ * I_ + 16 * wave + 4 * G + i] = accb[i];
 }
 
 // dst[j] = sum_p partial[p * stride + map[j]] (map[j] < 0: 0), fixed order: the weight

@@ -361,22 +361,31 @@ def imgconv(A, a_ps, a_bs, cin, B, N, M, C, c_ps, c_bs, H, bias=None, relu=False
     return C
 
 
-def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False):
+_BIAS_MAPS: dict = {}
+
+
+def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False, bias_out=None):
     """``pwgrad`` of a full conv3x3 on H x H maps with whole images in LDS
-    (``imgwgrad_kernel``; GPU only): dW [9][O][I] -> out via gmap."""
+    (``imgwgrad_kernel``; GPU only): dW [9][O][I] -> out via gmap. The kernel also sums dy
+    per output channel (an all-ones MFMA column); ``bias_out`` receives that bias gradient."""
     assert g.is_cuda and out.is_cuda
     _fits(g, H * H - 1, g_ps, M, g_bs, O, "imgwgrad g")
     _fits(x, H * H - 1, x_ps, M, x_bs, I, "imgwgrad x")
     N_ = _N()
     k = N_.kernels()
     parts = k.mbk_imgwgrad_parts()
-    stride = 9 * O * I
+    stride = 9 * O * I + O
     partial = torch.empty(parts * stride, dtype=torch.float32, device=out.device)
     args = (ctypes.c_longlong * 15)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
                                     int(x_relu), 0, 0, 9, M, parts, partial.data_ptr())
     N_.check(k.mbk_imgwgrad(args, H, N_.stream_ptr()), "imgwgrad")
     N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
                               out.data_ptr(), N_.stream_ptr()), "reduce_map")
+    if bias_out is not None:
+        assert bias_out.numel() == O and bias_out.dtype == torch.float32
+        N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride,
+                                  _bias_map(O, 9 * O * I, out.device).data_ptr(), O,
+                                  bias_out.data_ptr(), N_.stream_ptr()), "reduce_map bias")
     return out
 
 
@@ -440,15 +449,27 @@ def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False, 
     return out
 
 
-def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_relu=False):
+def _bias_map(O: int, off: int, device) -> torch.Tensor:
+    key = (O, off, str(device))
+    m = _BIAS_MAPS.get(key)
+    if m is None:
+        m = _BIAS_MAPS[key] = (torch.arange(O, dtype=torch.int32) + off).to(device)
+    return m
+
+
+def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_relu=False,
+               bias_out=None):
     """``pwgrad`` over the forward pair table (per output pixel P: its (q, t) pairs): g[P] is
-    read once per 64-image stage for every tap of P (``pwgrad_all_kernel``); ntap <= 9."""
+    read once per 64-image stage for every tap of P (``pwgrad_all_kernel``); ntap <= 9.
+    ``bias_out`` (fp32 [O]) receives sum over the table's output pixels and images of g."""
     assert ntap <= 9 and ftab.tap_max < ntap
     _fits(g, ftab.dst_max, g_ps, M, g_bs, O, "pwgrad_all g")
     _fits(x, ftab.src_max, x_ps, M, x_bs, I, "pwgrad_all x")
     if not out.is_cuda:
         tabc = ftab.t.cpu()
         dw = torch.zeros(ntap, O, I, dtype=torch.float32)
+        if bias_out is not None:
+            bias_out.zero_()
         for z in range(tabc.shape[0]):
             P = int(tabc[z, 0])
             gv = _view(g, g_ps, g_bs, M, O, P).float()
@@ -459,6 +480,8 @@ def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_r
                 if x_relu:
                     xv = xv.clamp_min(0)
                 dw[t] += gv.t() @ xv
+            if bias_out is not None:
+                bias_out += gv.float().sum(0)
         m = gmap.long()
         out.view(-1).copy_(torch.where(m >= 0, dw.reshape(-1)[m.clamp(min=0)], 0.0))
         return out
@@ -467,7 +490,7 @@ def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_r
     assert g.dtype == _BF and x.dtype == _BF and g.is_contiguous() and x.is_contiguous()
     assert out.is_contiguous() and out.dtype == torch.float32 and gmap.numel() == out.numel()
     parts = k.mbk_pwgrad_all_parts(M, O, I)
-    stride = ntap * O * I
+    stride = ntap * O * I + O
     partial = torch.empty(parts * stride, dtype=torch.float32, device=out.device)
     args = (ctypes.c_longlong * 16)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
                                     int(x_relu), ftab.t.data_ptr(), ftab.shape[1], ftab.shape[0],
@@ -475,19 +498,27 @@ def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_r
     N_.check(k.mbk_pwgrad_all(args, N_.stream_ptr()), "pwgrad_all")
     N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
                               out.data_ptr(), N_.stream_ptr()), "reduce_map")
+    if bias_out is not None:
+        assert bias_out.numel() == O and bias_out.dtype == torch.float32
+        N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride,
+                                  _bias_map(O, ntap * O * I, out.device).data_ptr(), O,
+                                  bias_out.data_ptr(), N_.stream_ptr()), "reduce_map bias")
     return out
 
 
 _WGRAD_ALL = os.environ.get("MBK_PWGRAD_ALL", "1") == "1"
 
 
-def _wgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L, ntap, M, out, x_relu=False):
+def _wgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L, ntap, M, out, x_relu=False, bias_out=None):
     """weight gradient of a dense layer: the all-taps form for the 3x3 convs (~7.6 pairs per
-    output pixel share one staged g row), the per-tap form for the transposed convs and the
-    critic (1-4 pairs per output pixel: nothing to share, measured 2x slower all-taps)"""
+    output pixel share one staged g row; it also yields the bias gradient), the per-tap form
+    for the transposed convs and the critic (1-4 pairs per output pixel: nothing to share,
+    measured 2x slower all-taps). ``bias_out`` (with g as [pixels][M][O] rows): sum of g."""
     if _WGRAD_ALL and ntap <= 9 and L.mean_pairs >= 4.0:
         return pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L.tf, ntap, M, L.gmap, out,
-                          x_relu=x_relu)
+                          x_relu=x_relu, bias_out=bias_out)
+    if bias_out is not None:
+        colsum(g.view(-1, O), O, bias_out)
     return pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L.tw, M, L.gmap, out, x_relu=x_relu)
 
 
@@ -988,14 +1019,13 @@ class _GridNetPBC(torch.autograd.Function):
             if g1 is None:
                 break
             dy = ppool_bwd(g1, n1, g2, n2, pooled, idx, L.H, L.W, n, L.cout)
-            colsum(dy.view(-1, L.cout), L.cout, pg(iw + 1))
             xa = ctx.acts[i]
             if _imgconv_ok(L, dev):
                 imgwgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], n, L.gmap,
-                         pg(iw), L.H, x_relu=xa[4])
+                         pg(iw), L.H, x_relu=xa[4], bias_out=pg(iw + 1))
             else:
                 _wgrad(dy, n * L.cout, L.cout, L.cout, xa[0], xa[1], xa[2], xa[3], L, 9, n,
-                       pg(iw), x_relu=xa[4])
+                       pg(iw), x_relu=xa[4], bias_out=pg(iw + 1))
             if i == 0:
                 break
             if i == 1 and plan.enc0 is not None and ctx.acts[0] is None:

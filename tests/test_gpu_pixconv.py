@@ -294,12 +294,14 @@ def test_gpu_pwgrad_all_matches_emulation(H, O, I, x_relu, crop):
     gmap[::5] = -1
     out_c = torch.empty(9 * O * I)
     out_g = torch.empty(9 * O * I, device="cuda")
+    db_c, db_g = torch.empty(O), torch.empty(O, device="cuda")
     pc.pwgrad_all(g, M * O, O, O, x, M * I, I, I, pc.pconv_table(fwd, "cpu"), 9, M, gmap, out_c,
-                  x_relu=x_relu)
+                  x_relu=x_relu, bias_out=db_c)
     pc.pwgrad_all(g.cuda(), M * O, O, O, x.cuda(), M * I, I, I, pc.pconv_table(fwd, "cuda"), 9, M,
-                  gmap.cuda(), out_g, x_relu=x_relu)
+                  gmap.cuda(), out_g, x_relu=x_relu, bias_out=db_g)
     torch.cuda.synchronize()
     torch.testing.assert_close(out_g.cpu(), out_c, rtol=2e-3, atol=2e-2)
+    torch.testing.assert_close(db_g.cpu(), db_c, rtol=1e-3, atol=1e-2)   # fused bias gradient
 
 
 @pytest.mark.parametrize("cin,N,layout", [(32, 64, "nhwc_in"), (64, 32, "nhwc_out")])
@@ -345,6 +347,9 @@ def test_gpu_imgwgrad_matches_pwgrad_all(x_layout):
     b = torch.empty(9 * O * I, device="cuda")
     pc.pwgrad_all(g, M * O, O, O, x, x_ps, x_bs, I, pc.pconv_table(fwd, "cuda"), 9, M, gmap, a,
                   x_relu=True)
-    pc.imgwgrad(g, M * O, O, O, x, x_ps, x_bs, I, M, gmap, b, H, x_relu=True)
+    db = torch.empty(O, device="cuda")
+    pc.imgwgrad(g, M * O, O, O, x, x_ps, x_bs, I, M, gmap, b, H, x_relu=True, bias_out=db)
     torch.cuda.synchronize()
     torch.testing.assert_close(b, a, rtol=2e-3, atol=2e-2)
+    # fused bias gradient == fp32 per-channel sum of g (layout [P][M][O])
+    torch.testing.assert_close(db, g.float().view(-1, O).sum(0), rtol=1e-3, atol=1e-2)

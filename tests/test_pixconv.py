@@ -303,6 +303,8 @@ def test_pwgrad_all_equals_per_tap(H, crop):
     gmap = torch.arange(9 * O * I, dtype=torch.int32)
     a, b = torch.empty(9 * O * I), torch.empty(9 * O * I)
     pc.pwgrad(g, M * O, O, O, x, M * I, I, I, pc.wgrad_table(wg, "cpu"), M, gmap, a, x_relu=True)
+    db = torch.empty(O)
     pc.pwgrad_all(g, M * O, O, O, x, M * I, I, I, pc.pconv_table(fwd, "cpu"), 9, M, gmap, b,
-                  x_relu=True)
+                  x_relu=True, bias_out=db)
+    torch.testing.assert_close(db, g.view(-1, O).sum(0), rtol=1e-5, atol=1e-4)
     torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-4)
