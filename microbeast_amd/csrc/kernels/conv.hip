@@ -482,25 +482,28 @@ struct Row3 {  // one input row's bit words for pixels x-1 (l), x (c), x+1 (h) o
   uint32_t l, c, h;
 };
 
-template <int HT>
+template <int HT, int COUT>
 __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int COUT = 16, OSTR = COUT + 4, W = 16;
+  constexpr int OSTR = COUT + 4, W = 16, CB = COUT / 16;
   const int H = HT > 0 ? HT : a.H, HW = H * W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   uint4* lut = (uint4*)smem;                 // [256] byte -> 8 bf16 planes
   bf16* otile = (bf16*)(smem + kLutBytes);   // [kRowImgs * HW][OSTR] conv outputs (pool mode)
   for (int i = tid; i < 256; i += kThreads) lut[i] = expand_bits8((uint32_t)i);
-  Frag8 bw[9];                // A fragments: w[co = li][tap][8g .. 8g+7]
-  {
-    const uint4* wp = (const uint4*)(a.w + (size_t)li * 9 * 32 + g * 8);
+  Frag8 bw[CB][9];            // A fragments: w[co = 16 cb + li][tap][8g .. 8g+7]
 #pragma unroll
-    for (int c = 0; c < 9; ++c) bw[c].u = wp[c * 4];
+  for (int cb = 0; cb < CB; ++cb) {
+    const uint4* wp = (const uint4*)(a.w + (size_t)(16 * cb + li) * 9 * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < 9; ++c) bw[cb][c].u = wp[c * 4];
   }
-  float bias_v[4];
+  float bias_v[CB][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bias_v[i] = a.bias ? a.bias[4 * g + i] : 0.f;
+  for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias_v[cb][i] = a.bias ? a.bias[16 * cb + 4 * g + i] : 0.f;
   const int ngroups = (a.N + kRowImgs - 1) / kRowImgs;
   __syncthreads();  // LUT ready
   const int sh = 8 * g;
@@ -513,37 +516,49 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   };
   const char* lutb = (const char*)lut;
   // one output row pair (y, y+1) from input rows y-1 .. y+2; each (row, kx) fragment is
-  // expanded once (one LDS read) and feeds both rows' MFMA chains in their tap order
+  // expanded once (one LDS read) and feeds both rows' MFMA chains (and, for 32 output
+  // channels, both channel blocks) in their tap order
   auto row_pair = [&](const Row3 r[4], int y, int im, int img0) {
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc0[CB], acc1[CB];
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc0[cb] = acc1[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         Frag8 f;
         f.u = *(const uint4*)(lutb + (kx == 0 ? r[q].l : kx == 1 ? r[q].c : r[q].h));
-        if (q < 3) acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * q + kx].v, f.v, acc0, 0, 0, 0);
-        if (q > 0) acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[3 * (q - 1) + kx].v, f.v, acc1, 0, 0, 0);
+#pragma unroll
+        for (int cb = 0; cb < CB; ++cb) {
+          if (q < 3)
+            acc0[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[cb][3 * q + kx].v, f.v, acc0[cb], 0, 0, 0);
+          if (q > 0)
+            acc1[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[cb][3 * (q - 1) + kx].v, f.v, acc1[cb], 0, 0, 0);
+        }
       }
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int yy = y + h;
       if (yy >= H) break;
-      const f32x4& acc = h ? acc1 : acc0;
-      uint32_t o[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j] * 1.f + bias_v[2 * j])) |
-               ((uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j + 1] * 1.f + bias_v[2 * j + 1]))
-                << 16);
       const int m = yy * W + li;
-      const size_t gi = ((size_t)(img0 + im) * HW + m) * COUT + 4 * g;
-      if (a.pool) {
-        *(uint2*)(otile + (im * HW + m) * OSTR + 4 * g) = make_uint2(o[0], o[1]);
-        if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
-      } else {
-        *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        const f32x4& acc = h ? acc1[cb] : acc0[cb];
+        uint32_t o[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j] * 1.f + bias_v[cb][2 * j])) |
+                 ((uint32_t)__bfloat16_as_ushort(f2bf(acc[2 * j + 1] * 1.f + bias_v[cb][2 * j + 1]))
+                  << 16);
+        const int c = 16 * cb + 4 * g;
+        const size_t gi = ((size_t)(img0 + im) * HW + m) * COUT + c;
+        if (a.pool) {
+          *(uint2*)(otile + (im * HW + m) * OSTR + c) = make_uint2(o[0], o[1]);
+          if (a.y_full) *(uint2*)(a.y_full + gi) = make_uint2(o[0], o[1]);
+        } else {
+          *(uint2*)(a.y + gi) = make_uint2(o[0], o[1]);
+        }
       }
     }
   };
@@ -596,12 +611,17 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
         r[3] = y + 4 < H ? row(n1) : zero3;
       }
     }
-    if (a.pool) {
-      __syncthreads();
+    if (a.pool && wave < nimg) {
+      // each wave pools its own image's LDS rows: no workgroup barrier, so one wave's pool
+      // (VALU / LDS) overlaps the other waves' MFMA rows. LDS ops of a wave complete in
+      // order; the fences only keep the compiler from moving them across.
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
       const int Ho = (H + 1) >> 1, Wo = W >> 1;
-      mbk::pool_tile<COUT, OSTR, kThreads>(otile, H, W, nimg, (size_t)img0 * Ho * Wo * COUT, a.y, a.pool_idx,
-                            tid);
-      __syncthreads();  // otile reads done before the next group overwrites it
+      mbk::pool_tile<COUT, OSTR, 64>(otile + (size_t)wave * HW * OSTR, H, W, 1,
+                                     (size_t)(img0 + wave) * Ho * Wo * COUT, a.y, a.pool_idx, lane);
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();   // reads done before the next group's rows overwrite
     }
   }
 }
@@ -1308,15 +1328,17 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
     return (int)hipGetLastError();
   }
-  if (in_bits && cout == 16 && W == 16 && !fp8 && g_conv0_row && !add && !mask_src &&
-      !relu_in) {
-    const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * 16 * (16 + 4) * 2 : 0);
+  if (in_bits && (cout == 16 || cout == 32) && W == 16 && !fp8 && g_conv0_row && !add &&
+      !mask_src && !relu_in) {
+    const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * 16 * (cout + 4) * 2 : 0);
     if (sm0 > 160 * 1024) return (int)hipErrorInvalidValue;
     static const bool batch_rows = [] {  // A/B knob: MBK_CONV0_BATCH_ROWS=0 -> pairwise loads
       const char* e = getenv("MBK_CONV0_BATCH_ROWS");
       return !(e && e[0] == '0');
     }();
-    const auto kfn = H == 16 && batch_rows ? conv0_row_kernel<16> : conv0_row_kernel<0>;
+    const bool hb = H == 16 && batch_rows;
+    const auto kfn = cout == 16 ? (hb ? conv0_row_kernel<16, 16> : conv0_row_kernel<0, 16>)
+                                : (hb ? conv0_row_kernel<16, 32> : conv0_row_kernel<0, 32>);
     const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)kfn, sm0);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();

@@ -379,30 +379,32 @@ def test_pool_bwd_idx_shapes(cuda, H, W, C):
     torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("n,pool", [(203, True), (7, True), (9, False)])
-def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool):
+@pytest.mark.parametrize("n,pool,cout", [(203, True, 16), (7, True, 16), (9, False, 16),
+                                          (203, True, 32), (9, False, 32)])
+def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout):
     """The 16-wide stage-0 conv (register row window + DPP pixel shifts) runs the MFMA taps
-    in the generic kernel's order: outputs, pre-pool values and argmax bytes are identical."""
+    in the generic kernel's order: outputs, pre-pool values and argmax bytes are identical.
+    cout 32 is GridNet's first layer (two 16-channel blocks per expanded fragment)."""
     from microbeast_amd import _native as N
     from microbeast_amd.ops.encoder import HipEncoder
     torch.manual_seed(3)
-    enc = HipEncoder(16, 16, 27, (16, 32, 32), cuda)
+    enc = HipEncoder(16, 16, 27, (cout, 32, 32), cuda)
     ws = [torch.randn(L.cout, L.cin_real, 3, 3, device=cuda) * 0.2 for L in enc.layers]
     enc.pack(ws, with_bwd=False)
     L0 = enc.layers[0]
     obs = _random_obs_bits(n, 256, seed=n).to(cuda)
-    b0 = torch.randn(16, device=cuda) * 0.1
+    b0 = torch.randn(cout, device=cuda) * 0.1
     outs = []
     for on in (1, 0):
         N.kernels().mbk_conv0_row_set(on)
         try:
             if pool:
-                cfull = torch.full((n, 16, 16, 16), 7.0, dtype=torch.bfloat16, device=cuda)
-                pidx = torch.full((n, 8, 8, 16), 255, dtype=torch.uint8, device=cuda)
+                cfull = torch.full((n, 16, 16, cout), 7.0, dtype=torch.bfloat16, device=cuda)
+                pidx = torch.full((n, 8, 8, cout), 255, dtype=torch.uint8, device=cuda)
                 p = enc._fwd(L0, obs, b0, y_full=cfull, pool_idx=pidx)
                 outs.append((p, cfull, pidx))
             else:  # raw launch without the pool (the encoder always pools stage convs)
-                y = torch.empty(n, 16, 16, 16, dtype=torch.bfloat16, device=cuda)
+                y = torch.empty(n, 16, 16, cout, dtype=torch.bfloat16, device=cuda)
                 N.check(N.kernels().mbk_conv_fwd(
                     obs.data_ptr(), 1, L0.cin, L0.cout, enc.packed_fwd.data_ptr() + 2 * L0.w_off,
                     b0.data_ptr(), 0, 0, y.data_ptr(), 0, 0, n, 16, 16, 4, 0, 0,
