@@ -390,6 +390,10 @@ def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False, 
 
 
 _IMGCONV = os.environ.get("MBK_GRID_IMGCONV", "1") == "1"
+# first layer's weight gradient with the max-pool backward folded into its LDS staging
+# (no pre-pool gradient in HBM): measured 64.1 vs 55.4 ms per GridNet update (the plain-layout
+# unpool wgrad loses more than the 8.6 GB round trip saves), so off by default
+_E1_UNPOOL = os.environ.get("MBK_GRID_E1_UNPOOL", "0") == "1"
 
 
 def _imgconv_ok(L, dev) -> bool:
@@ -1009,6 +1013,10 @@ class _GridNetPBC(torch.autograd.Function):
                 # conv.hip first layer: g1 is its (relu-masked) NHWC pooled gradient
                 L0 = plan.enc0.layers[0]
                 p, pidx = pooled, idx
+                if _E1_UNPOOL:   # max-pool backward folded into the wgrad's LDS staging
+                    plan.enc0._wgrad(L0, ctx.saved["bits_pad"], None, pg(0), pg(1), dp=g1,
+                                     pidx=pidx)
+                    break
                 dc = torch.empty(n, L0.H, L0.W, L0.cout, dtype=_BF, device=dev)
                 k = _N().kernels()
                 _N().check(k.mbk_pool_bwd_idx(pidx.data_ptr(), g1.data_ptr(), n, L0.H, L0.W,
