@@ -478,8 +478,11 @@ __device__ __forceinline__ uint32_t dpp_shl1_b(uint32_t v) {  // lane x <- lane 
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x101, 0xF, 0xF, true);
 }
 
-struct Row3 {  // one input row's bit words for pixels x-1 (l), x (c), x+1 (h) of lane x
+struct Row3 {  // one input row's LUT offsets for pixels x-1 (l), x (c), x+1 (h) of lane x
   uint32_t l, c, h;
+};
+struct XRow3 {  // the same row expanded: kx = 0, 1, 2 B fragments
+  Frag8 f[3];
 };
 
 template <int HT, int COUT>
@@ -515,10 +518,25 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
     return r;
   };
   const char* lutb = (const char*)lut;
-  // one output row pair (y, y+1) from input rows y-1 .. y+2; each (row, kx) fragment is
-  // expanded once (one LDS read) and feeds both rows' MFMA chains (and, for 32 output
-  // channels, both channel blocks) in their tap order
-  auto row_pair = [&](const Row3 r[4], int y, int im, int img0) {
+  // an input row's three expanded (kx) fragments, kept in registers while the row is in the
+  // 4-row window: each row is expanded once (3 LUT reads) and serves two row pairs. (Time
+  // unchanged: 2.2 ms per 524K images before and after, and with the next group's rows
+  // prefetched; it scales with the MFMA count -- 4.4 ms at 32 channels.)
+  auto xrow = [&](uint32_t bits) {
+    const Row3 r = row(bits);
+    XRow3 x;
+    x.f[0].u = *(const uint4*)(lutb + r.l);
+    x.f[1].u = *(const uint4*)(lutb + r.c);
+    x.f[2].u = *(const uint4*)(lutb + r.h);
+    return x;
+  };
+  XRow3 xzero;
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx) xzero.f[kx].u = make_uint4(0, 0, 0, 0);
+  // one output row pair (y, y+1) from input rows y-1 .. y+2; each (row, kx) fragment feeds
+  // both rows' MFMA chains (and, for 32 output channels, both channel blocks) in their tap
+  // order
+  auto row_pair = [&](const XRow3 r[4], int y, int im, int img0) {
     f32x4 acc0[CB], acc1[CB];
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) acc0[cb] = acc1[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -526,8 +544,7 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        Frag8 f;
-        f.u = *(const uint4*)(lutb + (kx == 0 ? r[q].l : kx == 1 ? r[q].c : r[q].h));
+        const Frag8& f = r[q].f[kx];
 #pragma unroll
         for (int cb = 0; cb < CB; ++cb) {
           if (q < 3)
@@ -571,7 +588,6 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
 #pragma unroll
     for (int y = 0; y < NR; ++y) dst[y] = ok ? xb[y * W] : 0u;
   };
-  const Row3 zero3 = {0u, 0u, 0u};  // LUT entry 0 = all-zero planes
 
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * kRowImgs;
@@ -579,36 +595,36 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
     if (HT > 0) {
       load_rows(grp, rows);
       if (wave < nimg) {
-        Row3 r[4];
-        r[0] = zero3;
-        r[1] = row(rows[0]);
-        r[2] = NR > 1 ? row(rows[1 % NR]) : zero3;
-        r[3] = NR > 2 ? row(rows[2 % NR]) : zero3;
+        XRow3 r[4];
+        r[0] = xzero;
+        r[1] = xrow(rows[0]);
+        r[2] = NR > 1 ? xrow(rows[1 % NR]) : xzero;
+        r[3] = NR > 2 ? xrow(rows[2 % NR]) : xzero;
 #pragma unroll
         for (int y = 0; y < NR; y += 2) {
           row_pair(r, y, wave, img0);
           r[0] = r[2];
           r[1] = r[3];
-          r[2] = y + 3 < NR ? row(rows[(y + 3) % NR]) : zero3;
-          r[3] = y + 4 < NR ? row(rows[(y + 4) % NR]) : zero3;
+          r[2] = y + 3 < NR ? xrow(rows[(y + 3) % NR]) : xzero;
+          r[3] = y + 4 < NR ? xrow(rows[(y + 4) % NR]) : xzero;
         }
       }
     } else if (wave < nimg) {
       const int im = wave;
       const uint32_t* xb = (const uint32_t*)a.x + (size_t)(img0 + im) * HW + li;
-      Row3 r[4];  // expanded input rows y-1, y, y+1, y+2 (zero outside the image)
-      r[0] = zero3;
-      r[1] = row(xb[0]);
-      r[2] = H > 1 ? row(xb[W]) : zero3;
-      r[3] = H > 2 ? row(xb[2 * W]) : zero3;
+      XRow3 r[4];  // expanded input rows y-1, y, y+1, y+2 (zero outside the image)
+      r[0] = xzero;
+      r[1] = xrow(xb[0]);
+      r[2] = H > 1 ? xrow(xb[W]) : xzero;
+      r[3] = H > 2 ? xrow(xb[2 * W]) : xzero;
       for (int y = 0; y < H; y += 2) {
         const uint32_t n0 = y + 3 < H ? xb[(y + 3) * W] : 0u;  // next iteration's rows
         const uint32_t n1 = y + 4 < H ? xb[(y + 4) * W] : 0u;
         row_pair(r, y, im, img0);
         r[0] = r[2];
         r[1] = r[3];
-        r[2] = y + 3 < H ? row(n0) : zero3;
-        r[3] = y + 4 < H ? row(n1) : zero3;
+        r[2] = y + 3 < H ? xrow(n0) : xzero;
+        r[3] = y + 4 < H ? xrow(n1) : xzero;
       }
     }
     if (a.pool && wave < nimg) {
