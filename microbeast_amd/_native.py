@@ -59,6 +59,8 @@ _SIGS = {
     "mbk_pwgrad_all_parts": [c_int, c_int, c_int],
     "mbk_pwgrad_parts": [c_int, c_int, c_int, c_int],
     "mbk_reduce_map": [c_void_p, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p],
+    "mbk_reduce_inv": [c_void_p, c_int, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_int64,
+                       c_void_p],
     "mbk_ppool_fwd": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_ppool_bwd": [c_void_p, c_int64, c_int, c_void_p, c_int64, c_int, c_void_p, c_void_p,
                       c_int, c_int, c_int, c_int, c_void_p, c_void_p],

@@ -955,6 +955,28 @@ __global__ __launch_bounds__(kThreads) void reduce_map_kernel(const float* __res
   dst[j] = s;
 }
 
+// The same sum walked in partial order: thread m reads partial[p * stride + m] (consecutive
+// lanes, consecutive addresses: coalesced, where reduce_map's gather through a transposing
+// weight map touches one cache line per lane) and writes dst[inv[m]] (inv[m] < 0: unused).
+// Destinations no partial maps to are zeroed by the caller. Entries m >= nw (the bias sums
+// the weight-gradient kernels store after the weights) go to dst2[m - nw] in the same pass.
+__global__ __launch_bounds__(kThreads) void reduce_inv_kernel(const float* __restrict__ partial,
+                                                              int nparts, long long stride,
+                                                              const int* __restrict__ inv,
+                                                              long long nm, float* __restrict__ dst,
+                                                              float* __restrict__ dst2, long long nw) {
+  const long long m = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (m >= nm) return;
+  const int j = m < nw ? inv[m] : 0;
+  if (j < 0) return;
+  const float* src = partial + m;
+  float s = 0.f;
+#pragma unroll 8
+  for (int p = 0; p < nparts; ++p) s += src[(size_t)p * stride];
+  if (m < nw) dst[j] = s;
+  else dst2[m - nw] = s;
+}
+
 // ------------------------------------------------------------------ max pool 3x3 / 2 / pad 1
 // y [H*W][n][C] (relu'd) -> out [Ho*Wo][n][C], idx (uint8, ky*3+kx of the first maximum in
 // scan order). Thread = (pooled pixel, image, 8 channels).
@@ -1611,6 +1633,15 @@ extern "C" int mbk_reduce_map(const float* partial, int nparts, long long stride
   if (n <= 0) return 0;
   hipLaunchKernelGGL(reduce_map_kernel, dim3((unsigned)((n + kThreads - 1) / kThreads)),
                      dim3(kThreads), 0, st, partial, nparts, stride, map, n, dst);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_reduce_inv(const float* partial, int nparts, long long stride, const int* inv,
+                              long long nm, float* dst, float* dst2, long long nw, hipStream_t st) {
+  if (nm <= 0) return 0;
+  if (nm > nw && !dst2) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(reduce_inv_kernel, dim3((unsigned)((nm + kThreads - 1) / kThreads)),
+                     dim3(kThreads), 0, st, partial, nparts, stride, inv, nm, dst, dst2, nw);
   return (int)hipGetLastError();
 }
 

@@ -362,6 +362,46 @@ def imgconv(A, a_ps, a_bs, cin, B, N, M, C, c_ps, c_bs, H, bias=None, relu=False
 
 
 _BIAS_MAPS: dict = {}
+_INV_MAPS: dict = {}
+
+
+def _reduce_to(k, N_, partial, parts: int, stride: int, gmap: torch.Tensor, out: torch.Tensor,
+               nw: int | None = None, bias_out: torch.Tensor | None = None):
+    """out.flat[j] = sum_p partial[p, gmap[j]] (0 where gmap[j] < 0): walked in partial order
+    through the inverse map (``reduce_inv_kernel``: coalesced reads) when gmap is injective,
+    else the gather form (``reduce_map_kernel``). The inverse is built once per map. With
+    ``bias_out``, partial entries [nw, stride) are the bias sums: bias_out = their totals."""
+    nw = stride if nw is None else nw
+    if bias_out is not None:
+        assert bias_out.dtype == torch.float32 and bias_out.numel() == stride - nw
+    key = (gmap.data_ptr(), gmap.numel(), nw)
+    ent = _INV_MAPS.get(key)
+    if ent is None:
+        g = gmap.long()
+        valid = g >= 0
+        src = g[valid]
+        inv = None
+        if src.numel() == 0 or (int(src.max()) < nw and
+                                torch.unique(src).numel() == src.numel()):
+            inv = torch.full((nw,), -1, dtype=torch.int32, device=gmap.device)
+            inv[src] = torch.nonzero(valid).squeeze(1).to(torch.int32)
+        ent = _INV_MAPS[key] = (inv, bool(valid.all()), gmap)   # gmap kept alive with its key
+    inv, full, _ = ent
+    if inv is None:
+        N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
+                                  out.data_ptr(), N_.stream_ptr()), "reduce_map")
+        if bias_out is not None:
+            N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride,
+                                      _bias_map(stride - nw, nw, out.device).data_ptr(),
+                                      stride - nw, bias_out.data_ptr(), N_.stream_ptr()),
+                     "reduce_map bias")
+        return
+    if not full:
+        N_.check(k.mbk_memset(out.data_ptr(), 0, out.numel() * 4, N_.stream_ptr()), "memset")
+    nm = stride if bias_out is not None else nw
+    N_.check(k.mbk_reduce_inv(partial.data_ptr(), parts, stride, inv.data_ptr(), nm,
+                              out.data_ptr(), bias_out.data_ptr() if bias_out is not None else 0,
+                              nw, N_.stream_ptr()), "reduce_inv")
 
 
 def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False, bias_out=None):
@@ -379,13 +419,7 @@ def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False, 
     args = (ctypes.c_longlong * 15)(g.data_ptr(), g_ps, g_bs, O, x.data_ptr(), x_ps, x_bs, I,
                                     int(x_relu), 0, 0, 9, M, parts, partial.data_ptr())
     N_.check(k.mbk_imgwgrad(args, H, N_.stream_ptr()), "imgwgrad")
-    N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
-                              out.data_ptr(), N_.stream_ptr()), "reduce_map")
-    if bias_out is not None:
-        assert bias_out.numel() == O and bias_out.dtype == torch.float32
-        N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride,
-                                  _bias_map(O, 9 * O * I, out.device).data_ptr(), O,
-                                  bias_out.data_ptr(), N_.stream_ptr()), "reduce_map bias")
+    _reduce_to(k, N_, partial, parts, stride, gmap, out, 9 * O * I, bias_out)
     return out
 
 
@@ -448,8 +482,7 @@ def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False, 
                                     cells.bucket_cnt.data_ptr() if cells is not None else 0,
                                     cells.rowimg.data_ptr() if cells is not None else 0)
     N_.check(k.mbk_pwgrad(args, N_.stream_ptr()), "pwgrad")
-    N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
-                              out.data_ptr(), N_.stream_ptr()), "reduce_map")
+    _reduce_to(k, N_, partial, parts, stride, gmap, out)
     return out
 
 
@@ -500,13 +533,7 @@ def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_r
                                     int(x_relu), ftab.t.data_ptr(), ftab.shape[1], ftab.shape[0],
                                     ntap, M, parts, partial.data_ptr())
     N_.check(k.mbk_pwgrad_all(args, N_.stream_ptr()), "pwgrad_all")
-    N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride, gmap.data_ptr(), out.numel(),
-                              out.data_ptr(), N_.stream_ptr()), "reduce_map")
-    if bias_out is not None:
-        assert bias_out.numel() == O and bias_out.dtype == torch.float32
-        N_.check(k.mbk_reduce_map(partial.data_ptr(), parts, stride,
-                                  _bias_map(O, ntap * O * I, out.device).data_ptr(), O,
-                                  bias_out.data_ptr(), N_.stream_ptr()), "reduce_map bias")
+    _reduce_to(k, N_, partial, parts, stride, gmap, out, ntap * O * I, bias_out)
     return out
 
 
