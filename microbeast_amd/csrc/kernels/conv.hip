@@ -485,6 +485,72 @@ struct XRow3 {  // the same row expanded: kx = 0, 1, 2 B fragments
   Frag8 f[3];
 };
 
+// max_pool2d(3, 2, 1) + argmax of ONE 16 x 16 image's conv outputs in LDS by its own wave
+// (same values and argmax bytes as mbk::pool_tile): lane = (pooled column ox, 4-channel
+// group c4, row half); each lane walks its pooled rows top to bottom. Separable: a row's
+// 3-wide horizontal max (first maximising kx) is computed once and shared by the two windows
+// that contain the row; the vertical pass keeps the first maximising ky, so the index is the
+// first maximum in scan order. W = H = 16: only x = -1 / y = -1 fall outside the map.
+template <int COUT, int OSTR>
+__device__ __forceinline__ void pool_img16(const bf16* __restrict__ ot, size_t obase,
+                                           bf16* __restrict__ y, uint8_t* __restrict__ pool_idx,
+                                           int lane) {
+  constexpr int C4 = COUT / 4, ROWS = C4;  // pooled rows per lane: 8 rows x 8 x C4 / 64 lanes
+  static_assert(C4 == 4 || C4 == 8, "16 or 32 channels");
+  const int ox = lane & 7, c4 = (lane >> 3) % C4, oy0 = (lane >> 3) / C4 * ROWS;
+  struct HRow { float m[4]; int k[4]; };
+  auto hrow = [&](int yy) {  // horizontal max of input row yy over x = 2 ox - 1 .. 2 ox + 1
+    HRow h;
+    const bf16* b = ot + (yy * 16 + 2 * ox) * OSTR + 4 * c4;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      float v[4];
+      if (kx == 0 && ox == 0) {
+        v[0] = v[1] = v[2] = v[3] = -INFINITY;
+      } else {
+        const uint2 u = *(const uint2*)(b + (kx - 1) * OSTR);
+        v[0] = __uint_as_float(u.x << 16);
+        v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+        v[2] = __uint_as_float(u.y << 16);
+        v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (kx == 0 || v[j] > h.m[j]) { h.m[j] = v[j]; h.k[j] = kx; }
+      }
+    }
+    return h;
+  };
+  HRow top;
+  if (oy0 == 0) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { top.m[j] = -INFINITY; top.k[j] = 0; }
+  } else {
+    top = hrow(2 * oy0 - 1);
+  }
+#pragma unroll
+  for (int r = 0; r < ROWS; ++r) {
+    const int oy = oy0 + r;
+    const HRow mid = hrow(2 * oy), bot = hrow(2 * oy + 1);
+    float m[4];
+    uint32_t am = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int ix = top.k[j];          // ky = 0 (a -inf row never wins: mid is inside the map)
+      m[j] = top.m[j];
+      if (mid.m[j] > m[j]) { m[j] = mid.m[j]; ix = 3 + mid.k[j]; }
+      if (bot.m[j] > m[j]) { m[j] = bot.m[j]; ix = 6 + bot.k[j]; }
+      am |= (uint32_t)ix << (8 * j);
+    }
+    const size_t oi = obase + (size_t)(oy * 8 + ox) * COUT + 4 * c4;
+    // the maxima are loaded bf16 values: their float bits carry the bf16 exactly
+    *(uint2*)(y + oi) = make_uint2((__float_as_uint(m[0]) >> 16) | (__float_as_uint(m[1]) & 0xFFFF0000u),
+                                   (__float_as_uint(m[2]) >> 16) | (__float_as_uint(m[3]) & 0xFFFF0000u));
+    if (pool_idx) *(uint32_t*)(pool_idx + oi) = am;
+    top = bot;
+  }
+}
+
 template <int HT, int COUT>
 __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -634,8 +700,12 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int Ho = (H + 1) >> 1, Wo = W >> 1;
-      mbk::pool_tile<COUT, OSTR, 64>(otile + (size_t)wave * HW * OSTR, H, W, 1,
-                                     (size_t)(img0 + wave) * Ho * Wo * COUT, a.y, a.pool_idx, lane);
+      if (HT == 16)
+        pool_img16<COUT, OSTR>(otile + (size_t)wave * HW * OSTR,
+                               (size_t)(img0 + wave) * Ho * Wo * COUT, a.y, a.pool_idx, lane);
+      else
+        mbk::pool_tile<COUT, OSTR, 64>(otile + (size_t)wave * HW * OSTR, H, W, 1,
+                                       (size_t)(img0 + wave) * Ho * Wo * COUT, a.y, a.pool_idx, lane);
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();   // reads done before the next group's rows overwrite
     }
