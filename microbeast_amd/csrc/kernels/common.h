@@ -168,64 +168,83 @@ __device__ __forceinline__ float wave_sum(float v) {
 // ------------------------------------------------------------------ pooled epilogue
 // max_pool2d(3, 2, 1) of the workgroup's conv outputs staged in LDS (otile [(im*H+y)*W+x]
 // [OSTR] bf16) -> pooled y + per-channel argmax (ky*3+kx, first maximum in scan order as
-// ATen). Branch-free: the centre tap (always inside the map) seeds the max, the later taps
-// replace it only when strictly greater and the earlier ones (visited last to first) also
-// when equal, which leaves the smallest maximising tap; out-of-map taps read as -inf.
+// ATen). A thread owns one (image, pooled column, 4 channels) and walks its pooled rows top to
+// bottom, separably: an input row's 3-wide horizontal max (first maximising kx, strict >) is
+// computed once and shared by the two windows containing the row, and the vertical pass keeps
+// the first maximising ky -- so the index is the smallest maximising tap, 6 tap reads per
+// output instead of 9. Out-of-map taps read as -inf; the centre (2 oy, 2 ox) is always inside.
 // Index maths by float reciprocals (exact: pixel counts are tiny, see conv.hip index_math_ok).
 // Shared by conv.hip (conv_fwd / conv0_row epilogues) and resblock.hip (fused stage conv).
+template <int COUT, int OSTR>
+struct PoolHRow {
+  float m[4];
+  int k[4];
+};
+
 template <int COUT, int OSTR, int NT>
 __device__ __forceinline__ void pool_tile(const __hip_bfloat16* __restrict__ otile, int H, int W, int nimg,
                                           size_t obase, __hip_bfloat16* __restrict__ y,
                                           uint8_t* __restrict__ pool_idx, int tid) {
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1, HoWo = Ho * Wo;
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
   constexpr int C4 = COUT / 4;
-  const int tot = nimg * HoWo * C4;
-  const float inv_howo = 1.f / (float)HoWo, inv_wo = 1.f / (float)Wo;
+  const int tot = nimg * Wo * C4;
+  const float inv_wo = 1.f / (float)Wo;
+  using HRow = PoolHRow<COUT, OSTR>;
   for (int e = tid; e < tot; e += NT) {
-    const int c4 = e % C4, p = e / C4;
-    const int im = (int)(((float)p + 0.5f) * inv_howo), r = p - im * HoWo;
-    const int oy = (int)(((float)r + 0.5f) * inv_wo), ox = r - oy * Wo;
-    const int cy = 2 * oy, cx = 2 * ox;
-    const __hip_bfloat16* base = otile + ((im * H + cy) * W + cx) * OSTR + 4 * c4;
-    auto tap = [&](int dy, int dx, float v[4]) {
-      const bool ok = cy + dy >= 0 && cy + dy < H && cx + dx >= 0 && cx + dx < W;
-      const uint2 u2 = *(const uint2*)(base + (ok ? (dy * W + dx) * OSTR : 0));
-      v[0] = __uint_as_float(u2.x << 16);
-      v[1] = __uint_as_float(u2.x & 0xFFFF0000u);
-      v[2] = __uint_as_float(u2.y << 16);
-      v[3] = __uint_as_float(u2.y & 0xFFFF0000u);
-      if (!ok) v[0] = v[1] = v[2] = v[3] = -INFINITY;
+    const int c4 = e % C4, col = e / C4;
+    const int im = (int)(((float)col + 0.5f) * inv_wo), ox = col - im * Wo;
+    const __hip_bfloat16* base = otile + ((size_t)im * H * W + 2 * ox) * OSTR + 4 * c4;
+    const bool lo_ok = ox > 0, hi_ok = 2 * ox + 1 < W;
+    auto hrow = [&](int yy) {  // input row yy, x = 2 ox - 1 .. 2 ox + 1
+      HRow h;
+      const __hip_bfloat16* b = base + yy * W * OSTR;
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const bool ok = kx == 1 || (kx == 0 ? lo_ok : hi_ok);
+        const uint2 u = *(const uint2*)(b + (ok ? (kx - 1) * OSTR : 0));
+        float v[4];
+        v[0] = __uint_as_float(u.x << 16);
+        v[1] = __uint_as_float(u.x & 0xFFFF0000u);
+        v[2] = __uint_as_float(u.y << 16);
+        v[3] = __uint_as_float(u.y & 0xFFFF0000u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (!ok) v[j] = -INFINITY;
+          if (kx == 0 || v[j] > h.m[j]) { h.m[j] = v[j]; h.k[j] = kx; }
+        }
+      }
+      return h;
     };
-    float mx[4];
-    int am[4];
-    tap(0, 0, mx);
+    HRow top;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) am[j] = 4;
+    for (int j = 0; j < 4; ++j) { top.m[j] = -INFINITY; top.k[j] = 0; }
+    for (int oy = 0; oy < Ho; ++oy) {
+      const HRow mid = hrow(2 * oy);
+      HRow bot;
+      if (2 * oy + 1 < H) {
+        bot = hrow(2 * oy + 1);
+      } else {
 #pragma unroll
-    for (int t = 5; t < 9; ++t) {  // after the centre in scan order: strictly greater
-      float v[4];
-      tap(t / 3 - 1, t % 3 - 1, v);
+        for (int j = 0; j < 4; ++j) { bot.m[j] = -INFINITY; bot.k[j] = 0; }
+      }
+      float mx[4];
+      uint32_t am = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (v[j] > mx[j]) { mx[j] = v[j]; am[j] = t; }
+      for (int j = 0; j < 4; ++j) {
+        int ix = top.k[j];   // ky = 0; an out-of-map top row never wins (mid is inside)
+        mx[j] = top.m[j];
+        if (mid.m[j] > mx[j]) { mx[j] = mid.m[j]; ix = 3 + mid.k[j]; }
+        if (bot.m[j] > mx[j]) { mx[j] = bot.m[j]; ix = 6 + bot.k[j]; }
+        am |= (uint32_t)ix << (8 * j);
+      }
+      const size_t oi = obase + ((size_t)(im * Ho + oy) * Wo + ox) * COUT + 4 * c4;
+      // the maxima are loaded bf16 values: their float bits carry the bf16 exactly
+      *(uint2*)(y + oi) =
+          make_uint2((__float_as_uint(mx[0]) >> 16) | (__float_as_uint(mx[1]) & 0xFFFF0000u),
+                     (__float_as_uint(mx[2]) >> 16) | (__float_as_uint(mx[3]) & 0xFFFF0000u));
+      if (pool_idx) *(uint32_t*)(pool_idx + oi) = am;
+      top = bot;
     }
-#pragma unroll
-    for (int t = 3; t >= 0; --t) {  // before the centre, last to first: greater or equal
-      float v[4];
-      tap(t / 3 - 1, t % 3 - 1, v);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (v[j] >= mx[j]) { mx[j] = v[j]; am[j] = t; }
-    }
-    const size_t oi = obase + (size_t)p * COUT + 4 * c4;
-    const uint32_t o0 = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(mx[0])) |
-                        ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(mx[1])) << 16);
-    const uint32_t o1 = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(mx[2])) |
-                        ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(mx[3])) << 16);
-    *(uint2*)(y + oi) = make_uint2(o0, o1);
-    if (pool_idx)
-      *(uint32_t*)(pool_idx + oi) =
-          (uint32_t)am[0] | ((uint32_t)am[1] << 8) | ((uint32_t)am[2] << 16) | ((uint32_t)am[3] << 24);
   }
 }
 
