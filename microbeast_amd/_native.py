@@ -82,6 +82,8 @@ _SIGS = {
                               c_int, c_int, c_void_p],
     "mbk_conv_pack_fp8": [c_void_p, c_int, c_void_p],
     "mbk_pool_bwd_idx": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_pool_bwd_idx_blk": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mbk_pool_bwd_idx_out": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],

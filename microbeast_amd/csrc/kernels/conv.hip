@@ -1211,6 +1211,63 @@ __global__ __launch_bounds__(256) void pool_bwd_idx_kernel(const uint8_t* __rest
   }
 }
 
+// Same result in output order: thread e writes 16-byte chunk e of dc, so every store
+// instruction covers 1 KB of contiguous memory (the 2x2-block form above writes 16 bytes
+// at a 2-pixel stride per instruction, half of every 64-byte segment). Each thread gathers
+// its (<= 4) windows' argmax bytes and gradients, which neighbouring lanes share through
+// L1/L2; the HBM traffic stays one read of dp/pidx plus one write of dc. Windows are summed
+// in the 2x2-block kernel's (dj, dk) order from 0.f, so both give identical bits.
+template <int C>
+__global__ __launch_bounds__(256) void pool_bwd_out_kernel(const uint8_t* __restrict__ pidx,
+                                                           const bf16* __restrict__ dp, int N,
+                                                           int H, int W,
+                                                           bf16* __restrict__ dc) {
+  constexpr int C8 = C / 8;
+  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+  const uint32_t tot = (uint32_t)N * H * W * C8;
+  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+    const int c8 = e % C8;
+    const uint32_t p = e / C8;
+    const int x = p % W;
+    const uint32_t q = p / W;
+    const int y = q % H;
+    const uint32_t n = q / H;
+    // pixel row y sits in window j = y >> 1 at ky = (y & 1) + 1, and for odd y also in
+    // window j + 1 at ky = 0 (same for columns)
+    const int j = y >> 1, k = x >> 1;
+    const bool y2 = (y & 1) && j + 1 < Ho, x2 = (x & 1) && k + 1 < Wo;
+    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int dj = 0; dj < 2; ++dj)
+#pragma unroll
+      for (int dk = 0; dk < 2; ++dk) {
+        if ((dj && !y2) || (dk && !x2)) continue;
+        const uint32_t ky = dj ? 0u : (uint32_t)(y & 1) + 1u;
+        const uint32_t kx = dk ? 0u : (uint32_t)(x & 1) + 1u;
+        const uint32_t me = ky * 3u + kx;
+        const uint32_t o = ((n * Ho + j + dj) * Wo + k + dk) * C + c8 * 8;
+        const uint2 iv = *(const uint2*)(pidx + o);
+        const uint4 d = *(const uint4*)(dp + o);
+        const uint32_t ids[2] = {iv.x, iv.y};
+        const uint32_t dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const uint32_t id = (ids[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+          const uint32_t hb = (dv[t >> 1] >> (16 * (t & 1))) & 0xFFFFu;
+          if (id == me) g[t] += __uint_as_float(hb << 16);
+        }
+      }
+    uint32_t o[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint32_t lo = __bfloat16_as_ushort(f2bf(g[2 * t]));
+      const uint32_t hi = __bfloat16_as_ushort(f2bf(g[2 * t + 1]));
+      o[t] = lo | (hi << 16);
+    }
+    ((uint4*)dc)[e] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // ------------------------------------------------------------------ weight packing
 struct PackJob {
   const float* w;   // [cout][cin_real][3][3]
@@ -1577,8 +1634,8 @@ extern "C" int mbk_pool_bwd(const void* cfull, const void* dp, int N, int H, int
   return (int)hipGetLastError();
 }
 
-extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, int W, int C,
-                                void* dc, hipStream_t stream) {
+static int pool_bwd_idx_launch(const void* pidx, const void* dp, int N, int H, int W, int C,
+                               void* dc, hipStream_t stream, bool out_order) {
   if (C != 16 && C != 32) return (int)hipErrorInvalidValue;
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
   const size_t per_img_in = (size_t)H * W * C, per_img_out = (size_t)Ho * Wo * C;
@@ -1586,13 +1643,20 @@ extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, 
   const int chunk = (int)std::max<size_t>(1, ((size_t)1 << 31) / per_img_in - 1);
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
-    const size_t tot = (size_t)n * Ho * Wo * (C / 8);
+    const size_t tot = (size_t)n * (out_order ? (size_t)H * W : (size_t)Ho * Wo) * (C / 8);
     size_t blocks = (tot + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     const uint8_t* pi = (const uint8_t*)pidx + n0 * per_img_out;
     const bf16* d = (const bf16*)dp + n0 * per_img_out;
     bf16* o = (bf16*)dc + n0 * per_img_in;
-    if (C == 16)
+    if (out_order) {
+      if (C == 16)
+        hipLaunchKernelGGL(pool_bwd_out_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                           pi, d, n, H, W, o);
+      else
+        hipLaunchKernelGGL(pool_bwd_out_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, stream,
+                           pi, d, n, H, W, o);
+    } else if (C == 16)
       hipLaunchKernelGGL(pool_bwd_idx_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, stream, pi,
                          d, n, H, W, o);
     else
@@ -1600,6 +1664,26 @@ extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, 
                          d, n, H, W, o);
   }
   return (int)hipGetLastError();
+}
+
+// MBK_POOL_BWD_OUT=1 selects the output-order kernel, 0 the 2x2-block form
+extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, int W, int C,
+                                void* dc, hipStream_t stream) {
+  static const bool out = [] {
+    const char* s = getenv("MBK_POOL_BWD_OUT");
+    return s && s[0] == '1';
+  }();
+  return pool_bwd_idx_launch(pidx, dp, N, H, W, C, dc, stream, out);
+}
+
+extern "C" int mbk_pool_bwd_idx_out(const void* pidx, const void* dp, int N, int H, int W, int C,
+                                    void* dc, hipStream_t stream) {
+  return pool_bwd_idx_launch(pidx, dp, N, H, W, C, dc, stream, true);
+}
+
+extern "C" int mbk_pool_bwd_idx_blk(const void* pidx, const void* dp, int N, int H, int W, int C,
+                                    void* dc, hipStream_t stream) {
+  return pool_bwd_idx_launch(pidx, dp, N, H, W, C, dc, stream, false);
 }
 
 extern "C" int mbk_conv_pack_fp8(const MbkPackJob8* jobs, int n, hipStream_t stream) {

@@ -374,6 +374,16 @@ def test_pool_bwd_idx_shapes(cuda, H, W, C):
     dc = torch.empty(n, H, W, C, dtype=torch.bfloat16, device=cuda)
     N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dpg.data_ptr(), n, H, W, C,
                                          dc.data_ptr(), N.stream_ptr()), "pool_bwd_idx")
+    # the output-order kernel and the 2x2-block kernel give the same bits
+    dco = torch.full_like(dc, float("nan"))
+    dcb = torch.full_like(dc, float("nan"))
+    N.check(N.kernels().mbk_pool_bwd_idx_out(pidx.data_ptr(), dpg.data_ptr(), n, H, W, C,
+                                             dco.data_ptr(), N.stream_ptr()), "pool_bwd_idx_out")
+    N.check(N.kernels().mbk_pool_bwd_idx_blk(pidx.data_ptr(), dpg.data_ptr(), n, H, W, C,
+                                             dcb.data_ptr(), N.stream_ptr()), "pool_bwd_idx_blk")
+    torch.cuda.synchronize()
+    assert torch.equal(dco.view(torch.int16), dcb.view(torch.int16))
+    assert torch.equal(dc.view(torch.int16), dcb.view(torch.int16))
     ct = c.clone().requires_grad_(True)
     F.max_pool2d(ct, 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
     torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
