@@ -9,4 +9,5 @@ tail -1 gpurun_out/${tag}_pooltests.log
 bash tools/lt_ab.sh ${tag} "MBK_POOL_BWD_OUT=0" "MBK_POOL_BWD_OUT=1" || exit 1
 MBK_POOL_BWD_OUT=1 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/${tag}_bench_out.log 2>&1 || exit $?
 tail -1 gpurun_out/${tag}_bench_out.log | cut -c1-300
+[ "${2:-full}" = quick ] && exit 0
 bash tools/gpu_all.sh ${tag}
