@@ -26,7 +26,11 @@ def main(argv=None) -> int:
     if flags.test:
         from .evaluate import evaluate
 
-        evaluate(flags)
+        try:
+            evaluate(flags)
+        except FileNotFoundError as e:  # no checkpoint: fail, do not score random weights
+            print(f"microbeast: {e}", file=sys.stderr)
+            return 2
     else:
         from .train import train
 

@@ -35,7 +35,10 @@ class Flags:
     n_envs: int = 6
     env_size: int = 8
     unroll_length: int = 64
-    batch_size: int = 2
+    batch_size: int = 0           # rollout slots per update; 0 = auto: 2 on the mono runtime
+                                  # (the reference's B = 2, microbeast.py:117), 1 on the gpu
+                                  # runtime (one 8192-env x 64-step slot = 524,288 frames: the
+                                  # benched update, and --lr_base_batch, so the lr stays 2.5e-4)
     n_buffers: int = 0            # 0 -> max(2 * n_actors, batch_size)
     total_steps: int = 100_000_000
     max_episode_steps: int = 2000
@@ -91,6 +94,8 @@ class Flags:
     resume: bool = False
     checkpoint: str = ""          # path for --test / --resume (default <savedir>/<exp>.ckpt)
     eval_episodes: int = 10
+    allow_random_init: bool = False  # --test without a checkpoint: evaluate random weights
+                                     # instead of failing
     batch_timeout: float = 600.0
     actor_restarts: int = 3       # watchdog: respawn a dead actor at most this often
     fault_inject_every: int = 0   # kill an actor every N updates (tests the watchdog)
@@ -98,8 +103,14 @@ class Flags:
     quiet: bool = False
     max_updates: int = 0          # stop after N updates (0 = until total_steps)
 
+    def resolved_batch_size(self, runtime: str) -> int:
+        """--batch_size 0 (the default) picks the per-runtime value (see the field)."""
+        if self.batch_size > 0:
+            return self.batch_size
+        return 1 if runtime == "gpu" else 2
+
     def resolved_n_buffers(self) -> int:
-        return self.n_buffers or max(2 * self.n_actors, self.batch_size)
+        return self.n_buffers or max(2 * self.n_actors, self.resolved_batch_size("mono"))
 
     def opponent_list(self) -> list[str]:
         return [s.strip() for s in self.opponents.split(",") if s.strip()]

@@ -21,8 +21,12 @@ def evaluate(flags: Flags, checkpoint: str | None = None, greedy: bool = False) 
         ck = load_checkpoint(path)
         model.load_state_dict(ck["model_state_dict"])
         src = path
-    else:
-        src = "random-init (no checkpoint found)"
+    elif flags.allow_random_init:
+        src = "random-init (no checkpoint found, --allow_random_init)"
+    else:  # an evaluation of untrained weights must not pass for a checkpoint's result
+        raise FileNotFoundError(
+            f"--test: no checkpoint at {path!r}; train first, pass --checkpoint PATH, or "
+            f"--allow_random_init to evaluate random-init weights")
     model.eval()
     n = flags.n_envs
     env = create_env(flags.env_size, n, flags.max_episode_steps, seed=flags.seed + 777,

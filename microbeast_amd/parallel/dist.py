@@ -91,7 +91,11 @@ def init_distributed(use_cuda: bool, timeout_s: float = 600.0,
             from .launch import free_port
             kw.update(init_method=f"tcp://127.0.0.1:{free_port()}", rank=rank, world_size=world)
         dist.init_process_group(**kw)
-    host = dist.new_group(backend="gloo") if backend != "gloo" else None
+    # the host group's timeout also bounds how long healthy ranks wait in agree() while a
+    # peer rebuilds its actor engine (graph capture, HBM slots: seconds, up to --actor_restarts
+    # times): give it room beyond the RCCL group's
+    host = (dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=max(timeout_s, 1800)))
+            if backend != "gloo" else None)
     return DistInfo(rank, world, local, backend, pg=True, host_group=host)
 
 
@@ -226,6 +230,22 @@ def all_ok(ok: bool, info: DistInfo) -> bool:
     t = torch.tensor([1 if ok else 0], dtype=torch.int32)
     dist.all_reduce(t, op=dist.ReduceOp.MIN, group=info.host_group)
     return bool(t.item())
+
+
+# per-update rank states for agree(): the MIN over ranks decides what every rank does
+FAILED, RESTARTING, OK = 0, 1, 2
+
+
+def agree(state: int, info: DistInfo) -> int:
+    """MIN of every rank's update state (FAILED < RESTARTING < OK) over the gloo host group.
+    A rank whose engine failed but may restart reports RESTARTING: every rank then skips the
+    update together (healthy ranks keep the batch they fetched) and meets again in the next
+    round, so no rank sits in a gradient collective while a peer rebuilds its actors."""
+    if not info.enabled:
+        return int(state)
+    t = torch.tensor([int(state)], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=info.host_group)
+    return int(t.item())
 
 
 def barrier(info: DistInfo) -> None:

@@ -228,7 +228,7 @@ class MonoRuntime:
             self.server.check()
         if self.prefetcher is not None:
             return self.prefetcher.get_batch(timeout)
-        return get_batch(self.flags.batch_size, self.free, self.full, self.buffers,
+        return get_batch(self.flags.resolved_batch_size("mono"), self.free, self.full, self.buffers,
                          timeout=timeout, on_wait=self.watchdog)
 
     def drain_episodes(self):

@@ -30,7 +30,7 @@ class PinnedPrefetcher:
     def __init__(self, runtime, device, depth: int = 2, timeout: float = 600.0):
         self.rt = runtime
         self.device = torch.device(device)
-        self.B = runtime.flags.batch_size
+        self.B = runtime.flags.resolved_batch_size("mono")
         self.timeout = timeout
         self.copy_stream = torch.cuda.Stream(self.device)
         self.q: queue.Queue = queue.Queue(maxsize=max(1, depth))

@@ -15,6 +15,7 @@ checkpoints and shuts its actors down.
 """
 from __future__ import annotations
 
+import dataclasses
 import gc
 import os
 import time
@@ -41,6 +42,13 @@ def scaled_lr(flags: Flags, frames_per_update: int) -> float:
     r = max(1.0, frames_per_update / max(1, flags.lr_base_batch))
     k = {"none": 0.0, "sqrt": 0.5, "linear": 1.0}[flags.lr_scaling]
     return flags.lr * (r ** k)
+
+
+def update_frames(flags: Flags, runtime: str, world_size: int = 1) -> int:
+    """Env frames consumed per learner update over all ranks: batch slots x envs per slot x T x
+    world (gpu runtime: a slot is one env group's unroll; mono: one actor's n_envs)."""
+    per_slot = flags.envs_per_group if runtime == "gpu" else flags.n_envs
+    return flags.resolved_batch_size(runtime) * per_slot * flags.unroll_length * world_size
 
 
 def _hparams(flags: Flags, lr: float | None = None) -> LearnerHParams:
@@ -145,8 +153,15 @@ def train(flags: Flags) -> dict:
     info = D.init_distributed(use_cuda=want_cuda, high_priority=flags.rccl_high_priority)
     dev = torch.device("cuda", info.local_rank) if want_cuda else torch.device("cpu")
     runtime = flags.runtime if flags.runtime != "auto" else ("gpu" if want_cuda else "mono")
+    if runtime == "gpu" and flags.dtype == "fp32":
+        # the engine's policy step and the learner are the bf16 MFMA kernels: refuse rather
+        # than run bf16 under an fp32 flag
+        raise ValueError("--dtype fp32 is not available on the gpu runtime (bf16 / fp8 MFMA "
+                         "kernels); use --dtype bf16, or --runtime mono for fp32 PyTorch ops")
     if runtime == "gpu" and not want_cuda:
         raise RuntimeError("--runtime gpu needs a GPU")
+    if flags.batch_size <= 0:  # auto: 2 slots on mono (reference B), 1 on gpu (524,288 frames)
+        flags = dataclasses.replace(flags, batch_size=flags.resolved_batch_size(runtime))
     actor_threads = flags.actor_threads
     if runtime == "gpu":
         from .parallel.launch import pin_rank, rank_cpu_budget
@@ -163,8 +178,7 @@ def train(flags: Flags) -> dict:
         f"world={info.world_size} map={flags.env_size}x{flags.env_size} arch={flags.arch}")
 
     model = make_model(flags, dev)
-    per_rank = (flags.envs_per_group if runtime == "gpu" else flags.n_envs)
-    lr = scaled_lr(flags, flags.batch_size * per_rank * flags.unroll_length * info.world_size)
+    lr = scaled_lr(flags, update_frames(flags, runtime, info.world_size))
     if lr != flags.lr:
         log(f"[microbeast_amd] lr {flags.lr:g} -> {lr:g} (--lr_scaling {flags.lr_scaling})")
     learner = Learner(model, _hparams(flags, lr), dev, info)
@@ -207,7 +221,8 @@ def train(flags: Flags) -> dict:
             league = League(capacity=flags.league_size, snapshot_every=flags.league_update_every,
                             pfsp_power=flags.pfsp_power, eps=flags.league_eps,
                             seed=flags.seed + info.rank)
-            shard = load_league_shard(ck_path, info.rank) if ck is not None else None
+            shard = (load_league_shard(ck_path, info.rank, ck.get("n_update"))
+                     if ck is not None else None)
             if shard is not None:  # this rank's own league (DP runs save one per rank)
                 league.load_state_dict(shard, dev)
             elif ck is not None and ck.get("league"):
@@ -220,7 +235,6 @@ def train(flags: Flags) -> dict:
         if league is not None and ck is not None and ck.get("league"):
             # resumed: play the restored snapshot instead of the learner copy
             rt.set_opponent(league.snapshot(league.current), league.current)
-        frames_per_update = flags.batch_size * flags.envs_per_group * flags.unroll_length
     else:
         from .runtime.mono import MonoRuntime
 
@@ -230,8 +244,7 @@ def train(flags: Flags) -> dict:
         rt.start()
         if want_cuda:  # pinned DMA of full slots into HBM, one batch ahead of the learner
             rt.enable_prefetch(dev)
-        frames_per_update = flags.batch_size * flags.n_envs * flags.unroll_length
-    frames_per_update *= info.world_size
+    frames_per_update = update_frames(flags, runtime, info.world_size)
 
     def save_all(step_, n_update_):
         """Rank 0 writes the checkpoint; every rank with a league writes its own league shard
@@ -239,8 +252,8 @@ def train(flags: Flags) -> dict:
         if info.is_main:
             save_checkpoint(ck_path, learner.model, learner.opt, step_, n_update_, flags,
                             extra=_league_extra(league))
-        if league is not None and info.enabled:
-            save_league_shard(ck_path, info.rank, league.state_dict())
+        if league is not None:  # every run with a league, so a shard is never stale
+            save_league_shard(ck_path, info.rank, league.state_dict(), n_update_)
 
     engine_restarts = 0
     prof = None  # --profile_updates: torch.profiler timeline of a few steady-state updates
@@ -260,6 +273,7 @@ def train(flags: Flags) -> dict:
                 f"v {lv[1]:.4f} ent {lv[2]:.3f} fps {m['fps']:,.0f} lag {m['lag']}"
                 + (f" league {m['league']}" if m.get("league") else ""))
 
+    held = None  # gpu runtime: a batch kept over a round in which a DP peer restarted
     pending_eps = []  # finished episodes since the last rank-0 gather (DP: batched exchange)
 
     def sync_episodes(force=False):
@@ -276,28 +290,38 @@ def train(flags: Flags) -> dict:
             t0 = time.perf_counter()
             failure = None
             if runtime == "gpu":
-                try:
-                    batch, slots = rt.get_batch(timeout=flags.batch_timeout)
-                except EngineFailure as ex:
-                    failure = str(ex)  # (the exception's frames hold the old runtime: drop it)
-                if failure is not None and engine_restarts < flags.actor_restarts:
-                    # a dead env worker stops the native engine; rebuild the
-                    # actor side and keep training (bounded by --actor_restarts). The old
-                    # runtime (HBM slots, pinned staging, graphs) is freed BEFORE the new one
-                    # is allocated, so a restart never needs two runtimes' memory
-                    engine_restarts += 1
-                    log(f"[microbeast_amd] {failure}; restarting the actor engine "
-                        f"({engine_restarts}/{flags.actor_restarts})")
-                    batch = slots = None  # (views of the old runtime's rollout slots)
-                    rt = restart_runtime(rt, lambda: make_gpu_runtime(engine_restarts),
-                                         learner.flat, n_update, league)
-                    continue
-            # every rank agrees to go on before the update's gradient collectives, so one
-            # that cannot (restarts exhausted) stops all of them now, not at the PG timeout
-            if not D.all_ok(failure is None, info):
+                if held is not None:  # fetched in a round a peer spent restarting
+                    (batch, slots), held = held, None
+                else:
+                    try:
+                        batch, slots = rt.get_batch(timeout=flags.batch_timeout)
+                    except EngineFailure as ex:
+                        failure = str(ex)  # (the exception's frames hold the old runtime: drop it)
+            state = (D.OK if failure is None
+                     else D.RESTARTING if engine_restarts < flags.actor_restarts else D.FAILED)
+            # every rank agrees on the update before its gradient collectives: one that cannot
+            # go on (restarts exhausted) stops all of them now, not at the PG timeout, and one
+            # that restarts its engine makes all of them skip the round together
+            agreed = D.agree(state, info)
+            if agreed == D.FAILED:
                 if failure is not None:
                     raise EngineFailure(failure)
                 raise RuntimeError("another data-parallel rank stopped (engine failure)")
+            if agreed == D.RESTARTING:
+                if failure is None:
+                    held = (batch, slots)
+                    continue
+                # a dead env worker stops the native engine; rebuild the
+                # actor side and keep training (bounded by --actor_restarts). The old
+                # runtime (HBM slots, pinned staging, graphs) is freed BEFORE the new one
+                # is allocated, so a restart never needs two runtimes' memory
+                engine_restarts += 1
+                log(f"[microbeast_amd] {failure}; restarting the actor engine "
+                    f"({engine_restarts}/{flags.actor_restarts})")
+                batch = slots = None  # (views of the old runtime's rollout slots)
+                rt = restart_runtime(rt, lambda: make_gpu_runtime(engine_restarts),
+                                     learner.flat, n_update, league)
+                continue
             if runtime == "gpu":
                 lag = rt.policy_lag(slots, n_update)
             else:

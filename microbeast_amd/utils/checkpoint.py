@@ -70,7 +70,7 @@ def league_shard_path(path: str, rank: int) -> str:
     return f"{path}.league{rank}"
 
 
-def save_league_shard(path: str, rank: int, league_state: dict) -> str:
+def save_league_shard(path: str, rank: int, league_state: dict, n_update: int = -1) -> str:
     p = league_shard_path(path, rank)
     d = os.path.dirname(os.path.abspath(p))
     os.makedirs(d, exist_ok=True)
@@ -79,13 +79,20 @@ def save_league_shard(path: str, rank: int, league_state: dict) -> str:
     if isinstance(st.get("snaps"), dict):
         st["snaps"] = {k: v.detach().cpu().clone() for k, v in st["snaps"].items()}
     tmp = p + ".tmp"
-    torch.save({"format": FORMAT, "rank": int(rank), "league": st}, tmp)
+    torch.save({"format": FORMAT, "rank": int(rank), "n_update": int(n_update), "league": st},
+               tmp)
     os.replace(tmp, p)
     return p
 
 
-def load_league_shard(path: str, rank: int) -> dict | None:
+def load_league_shard(path: str, rank: int, n_update: int | None = None) -> dict | None:
+    """The rank's league shard, or None when there is none or (``n_update`` given) when it
+    was written at a different update than the main checkpoint: a shard left by an earlier DP
+    run must not override the newer league a later single-rank checkpoint holds."""
     p = league_shard_path(path, rank)
     if not os.path.exists(p):
         return None
-    return torch.load(p, map_location="cpu", weights_only=True).get("league")
+    d = torch.load(p, map_location="cpu", weights_only=True)
+    if n_update is not None and int(d.get("n_update", -1)) != int(n_update):
+        return None
+    return d.get("league")

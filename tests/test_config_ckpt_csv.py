@@ -20,10 +20,24 @@ def test_cli_reference_flags():
     f = parse_flags(["--env_size", "16", "--lr", "1e-3", "--self_play"], interactive=False)
     assert f.env_size == 16 and f.lr == 1e-3 and f.self_play is True
     d = parse_flags([], interactive=False)
-    assert (d.n_actors, d.n_envs, d.env_size, d.unroll_length, d.batch_size) == (10, 6, 8, 64, 2)
+    assert (d.n_actors, d.n_envs, d.env_size, d.unroll_length) == (10, 6, 8, 64)
+    assert d.resolved_batch_size("mono") == 2 and d.resolved_batch_size("gpu") == 1
+    assert parse_flags(["--batch_size", "3"], interactive=False).resolved_batch_size("gpu") == 3
     assert d.resolved_n_buffers() == 20 and d.gamma == 0.99 and d.adam_eps == 1e-5
     with pytest.raises(Exception):
         strtobool("maybe")
+
+
+def test_default_lr_is_reference_on_one_rank():
+    """the default flags on one GPU must train at the reference lr 2.5e-4
+    (microbeast.py:200); only a larger (DP / --batch_size) update scales it."""
+    from microbeast_amd.train import scaled_lr, update_frames
+
+    d = parse_flags([], interactive=False)
+    assert update_frames(d, "gpu", 1) == 524288
+    assert scaled_lr(d, update_frames(d, "gpu", 1)) == pytest.approx(2.5e-4)
+    assert scaled_lr(d, update_frames(d, "mono", 1)) == pytest.approx(2.5e-4)
+    assert scaled_lr(d, update_frames(d, "gpu", 4)) == pytest.approx(5e-4)  # sqrt(4)
 
 
 def test_checkpoint_roundtrip(tmp_path):
@@ -87,3 +101,16 @@ def test_lr_scaling_only_scales_batches_above_the_base():
     assert abs(scaled_lr(f, 4 * base) - 4 * f.lr) < 1e-12
     f.lr_scaling = "none"
     assert scaled_lr(f, 8 * base) == f.lr
+
+
+def test_stale_league_shard_is_ignored(tmp_path):
+    """a shard from an earlier DP run must not override a newer checkpoint's
+    league: shards carry their update number and load only when it matches."""
+    from microbeast_amd.utils.checkpoint import load_league_shard, save_league_shard
+
+    ck = str(tmp_path / "x.ckpt")
+    save_league_shard(ck, 0, {"results": {1: [2, 3]}, "next_id": 4}, n_update=5)
+    assert load_league_shard(ck, 0, 5)["next_id"] == 4
+    assert load_league_shard(ck, 0, 7) is None
+    assert load_league_shard(ck, 0) is not None  # no update given: no check
+    assert load_league_shard(ck, 1, 5) is None

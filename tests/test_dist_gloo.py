@@ -79,11 +79,15 @@ def test_dp_allreduce_equals_single_process(tmp_path, comm):
 def _worker_ok_league(rank, world, port, outdir):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from microbeast_amd.parallel import dist as D
     from microbeast_amd.parallel.dist import all_ok, barrier, destroy, init_distributed
     from microbeast_amd.runtime.league import League
     from microbeast_amd.utils.checkpoint import load_league_shard, save_league_shard
     info = init_distributed(use_cuda=False)
     res = [all_ok(True, info), all_ok(rank != 1, info), all_ok(True, info)]
+    # tri-state per-update agreement: a restarting rank makes every rank skip the round
+    res += [D.agree(D.OK, info), D.agree(D.RESTARTING if rank == 1 else D.OK, info),
+            D.agree(D.FAILED if rank == 0 else D.RESTARTING, info)]
     # every rank checkpoints its own league (snapshots + PFSP results) next to the main file
     lg = League(capacity=4, snapshot_every=1, seed=rank)
     for k in range(3):
@@ -107,6 +111,6 @@ def test_fail_fast_flag_and_per_rank_league_shards(tmp_path):
                        join=True, start_method="spawn")
     for r in range(world):
         d = torch.load(tmp_path / f"ok{r}.pt")
-        assert d["ok"] == [True, False, True]
+        assert d["ok"] == [True, False, True, 2, 1, 0]
         assert torch.equal(d["snap2"], torch.full((8,), float(10 * r + 2)))
         assert d["games"][1] == (2.0 if r == 0 else 1.0)
