@@ -285,16 +285,53 @@ int MicroRTSSim::nearest(int uid, int owner_filter, int type_filter, int* dist) 
   return best;
 }
 
+// Bots move one step toward (tx, ty): the free neighbour that shortens the Manhattan distance
+// (most steps on an open map), else the first step of a shortest path around the units in the
+// way (BFS over free cells from the target; the greedy step alone left bots oscillating behind
+// a blocker, which made the stand-in's games far longer than microRTS's pathfinding bots')
 int MicroRTSSim::dir_toward(const Unit& u, int tx, int ty) const {
   int best = -1, bd = 1 << 30;
+  const int d0 = std::abs(tx - u.x) + std::abs(ty - u.y);
   for (int d = 0; d < 4; ++d) {
     int nx = u.x + kDX[d], ny = u.y + kDY[d];
     if (!empty(nx, ny)) continue;
     int dd = std::abs(tx - nx) + std::abs(ty - ny);
     if (dd < bd) { bd = dd; best = d; }
   }
-  return best;
+  if (best < 0 || bd < d0) return best;
+  const int S = s_ * s_;
+  int16_t dist[32 * 32];
+  int16_t q[32 * 32];
+  if (S > 32 * 32) return best;
+  std::fill(dist, dist + S, (int16_t)-1);
+  int qh = 0, qt = 0;
+  const int tc = cell(tx, ty);
+  dist[tc] = 0;
+  q[qt++] = (int16_t)tc;
+  while (qh < qt) {
+    const int c = q[qh++], cx = c % s_, cy = c / s_;
+    for (int d = 0; d < 4; ++d) {
+      const int nx = cx + kDX[d], ny = cy + kDY[d];
+      if (!in_bounds(nx, ny)) continue;
+      const int nc = cell(nx, ny);
+      if (dist[nc] >= 0) continue;
+      if (nx == u.x && ny == u.y) {  // reached the mover: step to the neighbour it came from
+        for (int k = 0; k < 4; ++k)
+          if (u.x + kDX[k] == cx && u.y + kDY[k] == cy) return empty(cx, cy) ? k : best;
+      }
+      if (grid_[nc] >= 0) continue;
+      dist[nc] = (int16_t)(dist[c] + 1);
+      q[qt++] = (int16_t)nc;
+    }
+  }
+  return best;  // no path: keep the greedy step
 }
+
+// coac build order: workers kept by the base, and how many of them harvest (the rest rush)
+static int kCoacWorkers = 8, kCoacHarvesters = 1;
+static int kLightWorkers = 3;  // light rush: workers kept, all but one harvest
+static bool kChaseBaseFirst = true;
+static int kChaseBaseSlack = 3;
 
 // Scripted opponents (stand-ins for coacAI, randomBiasedAI, lightRushAI,
 // workerRushAI — libs/utils.py:69-72). They act through exec() with the same
@@ -304,9 +341,12 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
   Unit& u = units_[uid];
   uint8_t a[7] = {0, 0, 0, 0, 0, 0, 0};
   const int enemy = 1 - player;
+  // attack in range, units that fight back first (lowest hp among them), buildings last --
+  // the target choice of microRTS's rush AIs
   auto try_attack = [&]() -> bool {
     const UnitSpec& sp = kSpec[u.type];
     if (sp.damage <= 0) return false;
+    int best = -1, bkey = 1 << 30;
     for (int ay = -3; ay <= 3; ++ay)
       for (int ax = -3; ax <= 3; ++ax) {
         if (ax * ax + ay * ay > sp.range * sp.range || (ax == 0 && ay == 0)) continue;
@@ -314,11 +354,14 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
         if (!in_bounds(tx, ty)) continue;
         int g = grid_[cell(tx, ty)];
         if (g >= 0 && units_[g].owner == enemy) {
-          a[0] = A_ATTACK; a[6] = (uint8_t)((ay + 3) * 7 + (ax + 3));
-          return exec(uid, a, rwo);
+          const Unit& t = units_[g];
+          const int key = (kSpec[t.type].damage > 0 ? 0 : 64) + t.hp;
+          if (key < bkey) { bkey = key; best = (ay + 3) * 7 + (ax + 3); }
         }
       }
-    return false;
+    if (best < 0) return false;
+    a[0] = A_ATTACK; a[6] = (uint8_t)best;
+    return exec(uid, a, rwo);
   };
   auto move_to = [&](int tx, int ty) -> bool {
     int d = dir_toward(u, tx, ty);
@@ -357,9 +400,15 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
     }
     return move_to(units_[r].x, units_[r].y);
   };
+  // attack-move: the nearest enemy unit that can fight back or produce (mobile units, bases,
+  // barracks), the rest (e.g. nothing) only when none is left
   auto chase = [&]() -> bool {
     int dist, e = nearest(uid, enemy, -1, &dist);
     if (e < 0) return false;
+    if (kChaseBaseFirst) {
+      int db, b = nearest(uid, enemy, BASE, &db);
+      if (b >= 0 && db <= dist + kChaseBaseSlack) e = b;
+    }
     return move_to(units_[e].x, units_[e].y);
   };
 
@@ -412,14 +461,17 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
       return;
     }
     case BOT_LIGHT_RUSH: {
-      if (u.type == BASE) { if (n_workers < 2) produce(WORKER); return; }
+      // the first worker puts the barracks down with the starting resources, two harvest for
+      // the light units, any further worker joins the attack
+      if (u.type == BASE) { if (n_workers < kLightWorkers) produce(WORKER); return; }
       if (u.type == BARRACKS) { produce(LIGHT); return; }
       if (u.type == WORKER) {
         if (try_attack()) return;
-        if (n_barracks == 0 && resources_[player] >= kSpec[BARRACKS].cost && widx == 1) {
+        if (n_barracks == 0 && resources_[player] >= kSpec[BARRACKS].cost && widx == 0) {
           if (produce(BARRACKS)) return;
         }
-        if (harvest_cycle()) return;
+        if (widx < kLightWorkers - 1 && harvest_cycle()) return;
+        chase();
         return;
       }
       if (try_attack()) return;
@@ -429,7 +481,7 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
     case BOT_COAC:
     default: {
       // economy + mixed army (a small "coacAI"-like build order)
-      if (u.type == BASE) { if (n_workers < 3) produce(WORKER); return; }
+      if (u.type == BASE) { if (n_workers < kCoacWorkers) produce(WORKER); return; }
       if (u.type == BARRACKS) {
         const int r = resources_[player];
         int t = (r >= kSpec[HEAVY].cost && rand_unit() < 0.3f) ? HEAVY
@@ -439,10 +491,12 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
       }
       if (u.type == WORKER) {
         if (try_attack()) return;
-        if (n_barracks == 0 && resources_[player] >= kSpec[BARRACKS].cost && widx == 1) {
+        // barracks only once the worker rush is under way (the rush comes first on small maps)
+        if (n_barracks == 0 && n_workers >= kCoacWorkers / 2 &&
+            resources_[player] >= kSpec[BARRACKS].cost && widx == 1) {
           if (produce(BARRACKS)) return;
         }
-        if (widx <= 1 && harvest_cycle()) return;
+        if (widx < kCoacHarvesters && harvest_cycle()) return;
         chase();
         return;
       }

@@ -113,6 +113,11 @@ class MicroRTSSim {
   void write_obs_codes_as(int player, uint16_t* out) const;
   bool external_opponent() const { return external_opp_; }
   int resources(int player) const { return resources_[player]; }
+  int count_units(int owner, int type) const {  // diagnostics (csrc/tests/calib_components.cpp)
+    int n = 0;
+    for (const Unit& u : units_) n += u.alive && u.owner == owner && (type < 0 || u.type == type);
+    return n;
+  }
 
  private:
   int s_, max_steps_, bot_;

@@ -15,11 +15,16 @@ def test_uniform_policy_episode_statistics():
     from calibrate_env import run
     out = run(size=8, envs=48, steps=1500, seed=5, max_steps=2000)
     print(out)
-    assert out["episodes"] >= 80
-    # reference logs: ~300-step episodes (stand-in with microRTS unit timings: ~450)
-    assert 250 <= out["mean_len"] <= 650
-    # reference: <= 3.5 % of episodes reach return 10 (a win is +10); engine wins are rarer
+    assert out["episodes"] >= 100
+    # reference logs: ~300-step episodes, 221..512 (stand-in: ~340, median ~270)
+    assert 250 <= out["mean_len"] <= 400
+    # reference: mean return -2.26 .. -1.85 (a loss is -10 plus ~8 of shaping rewards)
+    assert -3.0 <= out["mean_return"] <= 0.0
+    # reference: 3.4-4.2 % of episodes reach return 10. The stand-in's random_biased and
+    # light_rush bots kill the uniform agent later than the Java bots (the logged episodes all
+    # end by step 512; random_biased games here average ~785), so its share is ~11 %:
+    # docs/DESIGN.md section 9a, csrc/tests/calib_components.cpp
+    assert out["win_share_return_ge_10"] <= 0.14
     assert out["win_share_engine"] <= 0.06
     # the sparse head's work: ~1 % of cells hold an idle own unit
     assert 0.004 <= out["active_cell_fraction"] <= 0.03
-    assert -8.0 <= out["mean_return"] <= 8.0
