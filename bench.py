@@ -32,6 +32,7 @@ import sys
 import time
 
 BASELINE_FPS = 38.9  # best reference run (5_ener), frames/s whole node
+CPU_BOUND_BUSY = 0.85  # env-worker busy fraction from which a rank counts as CPU-bound
 
 
 def parse(argv=None):
@@ -235,6 +236,23 @@ def main(argv=None):
         learner.learn(rt.get_batch()[0], sync_timing=True)
         phase = learner.timing
     rt.stop()
+    # every rank's actor side, so a weak-scaled N-GPU run shows which rank (if any) is
+    # CPU-bound: env workers busy ~100 % of the time means the rank's CPU share, not the
+    # GPU, sets its frame rate (each rank steps its own envs)
+    steps_done = max(1, st1["gpu_steps"] - st0["gpu_steps"])
+    busy = (st1["env_s"] - st0["env_s"]) / (el * threads)
+    mine = {"rank": info.rank, "cpus_per_rank": budget, "env_threads": threads,
+            "env_worker_busy_frac": round(busy, 3),
+            "env_cores_busy": round(busy * threads, 2),
+            "frames_stepped_per_s": round((st1["frames"] - st0["frames"]) / el, 1),
+            "gpu_phase_ms": round(1e3 * (st1["gpu_phase_s"] - st0["gpu_phase_s"]) / steps_done, 3),
+            "env_phase_ms": round(1e3 * (st1["env_phase_s"] - st0["env_phase_s"]) / steps_done, 3)}
+    ranks = D.gather_objects(mine, info)
+    cpu_bound = [r["rank"] for r in ranks if r["env_worker_busy_frac"] >= CPU_BOUND_BUSY]
+    if cpu_bound and info.is_main:
+        print(f"warning: env workers of rank(s) {cpu_bound} are >= {CPU_BOUND_BUSY:.0%} busy: "
+              f"those ranks are CPU-bound on their {budget}-CPU share (give each rank more CPUs "
+              f"or fewer envs)", file=sys.stderr)
     if info.is_main:
         out = {
             "metric": f"env frames/sec (whole node) on {s}x{s} microRTS",
@@ -287,6 +305,8 @@ def main(argv=None):
                 "graph_launch_ms": round(1e3 * (st1["graph_launch_s"] - st0["graph_launch_s"])
                                          / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
             },
+            "actor_stats_per_rank": ranks,
+            "cpu_bound_ranks": cpu_bound,
             "learner_phase_ms_rank0": {k: round(v, 3) for k, v in phase_ms.items()},
             "policy_lag_updates": ({"mean": round(sum(lags) / len(lags), 2), "max": max(lags)}
                                    if lags else None),

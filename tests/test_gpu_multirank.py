@@ -40,6 +40,9 @@ def test_bench_two_ranks_one_gpu(cuda, scaling):
     print(json.dumps(out))
     assert out["policy_lag_updates"]["max"] >= 0
     assert set(out["learner_phase_ms_rank0"]) >= {"fwd", "bwd", "allreduce", "optim"}
+    per = out["actor_stats_per_rank"]  # every rank's actor side, gathered to rank 0
+    assert [r["rank"] for r in per] == [0, 1]
+    assert all(r["frames_stepped_per_s"] > 0 and r["cpus_per_rank"] >= 1 for r in per)
 
 
 def test_bench_refuses_more_gpus_than_visible(cuda):
