@@ -71,7 +71,7 @@ struct TG {
 // zero the halo ring of a halo'd tile [nimg][(H+2)][(W+2)] of PIXB-byte pixels (index math
 // by float reciprocals: exact for these tiny ranges, no runtime integer division); 16-byte
 // stores, or 8-byte ones for the fp8 tiles (PIXB = C + 8)
-template <int PIXB>
+template <int PIXB, bool WV = false>  // WV: the calling wave alone (its own images)
 __device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W) {
   const int Hp = H + 2, Wp = W + 2;
   const int per = 2 * Wp + 2 * H;  // halo pixels per image
@@ -79,7 +79,7 @@ __device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W) {
   constexpr int qn = PIXB / U;
   const int tot = nimg * per * qn;
   const float inv_per = 1.f / (float)per;
-  for (int e = threadIdx.x; e < tot; e += kThreads) {
+  for (int e = WV ? (int)(threadIdx.x & 63) : (int)threadIdx.x; e < tot; e += WV ? 64 : kThreads) {
     const int r = e / qn, q = e - r * qn;  // qn is a compile-time constant
     const int im = (int)(((float)r + 0.5f) * inv_per), k = r - im * per;
     int py, px;
@@ -184,7 +184,11 @@ __device__ __forceinline__ void wfetch8(const uint8_t* gw, int cin, int cout, lo
 //   MODE OUT_TILE_RELU writes fp8(relu(bf16(v))) into an fp8 tile (out, stride COUT + 8);
 //   MODE OUT_TILE_ADD writes the bf16 residual stream (out) and, for cp = 1 / 2, its fp8 copy
 //   relu'd / as is into the fp8 tile at out8 (the next conv's input).
-template <int CIN, int COUT, bool RELU, int MODE, bool WLDS, bool F8 = false>
+// WV (wave-owned tiles, act_trunk_w_kernel): 0 = the workgroup's waves share the tile's pixel
+// blocks (wave w takes blocks w, w + NW, ...); 1 = the calling wave alone runs every block of
+// its own images, two blocks per iteration; 2 = the same one block at a time (maps whose pixel
+// count is one block: no idle partner chain)
+template <int CIN, int COUT, bool RELU, int MODE, bool WLDS, bool F8 = false, int WV = 0>
 // in / out: byte offsets of halo'd tiles in trunk_smem (out of a MODE == OUT_STAGE call: a
 // dense bf16 staging [nimg][H][W][COUT]); weights: LDS offset (WLDS, rows of wstride bytes)
 // or this lane's fragments prefetched into registers by wfetch (wreg)
@@ -275,11 +279,14 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
       }
     }
   };
-  for (int pb0 = wave; pb0 < nblk; pb0 += 2 * NW) {
+  constexpr int NJ = WV == 2 ? 1 : 2;  // independent block chains per iteration
+  const int pstart = WV ? 0 : wave;
+  constexpr int pstep = WV ? NJ : 2 * NW, poff = WV ? 1 : NW;
+  for (int pb0 = pstart; pb0 < nblk; pb0 += pstep) {
     int base[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = (pb0 + j * NW) * 16 + li;
+    for (int j = 0; j < NJ; ++j) {
+      const int m = (pb0 + j * poff) * 16 + li;
       const int mm = m < M ? m : 0;  // rows past M compute garbage that is never stored
       const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
@@ -287,7 +294,7 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
     }
     f32x4 acc[2][NB];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[j][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -300,17 +307,17 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
       if constexpr (F8) {
         long a8[2];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) a8[j] = *(const long*)(trunk_smem + base[j] + toff);
+        for (int j = 0; j < NJ; ++j) a8[j] = *(const long*)(trunk_smem + base[j] + toff);
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(bw8[c][nb], a8[j], acc[j][nb], 0, 0, 0);
         continue;
       }
       Frag8 a[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         a[j].u = *(const uint4*)(trunk_smem + base[j] + toff);
         if constexpr (RELU)
           a[j].u = make_uint4(relu2(a[j].u.x), relu2(a[j].u.y), relu2(a[j].u.z), relu2(a[j].u.w));
@@ -320,24 +327,24 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, a[j].v, acc[j][nb], 0, 0, 0);
     }
     epilogue(pb0, acc[0]);
-    epilogue(pb0 + NW, acc[1]);
+    if constexpr (NJ == 2) epilogue(pb0 + poff, acc[1]);
   }
 }
 
 // max_pool2d(3, 2, 1) of staging [nimg][H][W][C] into the interior of a halo'd tile (F8: and
 // fp8(relu(.)) into the fp8 tile out8, the next residual block's conv input)
-template <int C, bool F8 = false>
+template <int C, bool F8 = false, bool WV = false>
 __device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg, char* out,
                                          char* out8 = nullptr) {
   constexpr int PO = TG<C>::PIXB, C4 = C / 4;
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1, HWo = Ho * Wo;
   const int tot = nimg * HWo * C4;
   const float inv_hwo = 1.f / (float)HWo, inv_wo = 1.f / (float)Wo;
-  for (int e = threadIdx.x; e < tot; e += kThreads) {
+  for (int e = WV ? (int)(threadIdx.x & 63) : (int)threadIdx.x; e < tot; e += WV ? 64 : kThreads) {
     const int c4 = e % C4, p = e / C4;  // C4: compile-time power of two
     const int im = (int)(((float)p + 0.5f) * inv_hwo), r = p - im * HWo;
     const int oy = (int)(((float)r + 0.5f) * inv_wo), ox = r - oy * Wo;
@@ -713,6 +720,7 @@ struct ActTrunkArgs {
   int* bucket_cnt;  // this step's half of the [2][S] counters
   int* bucket_cnt_prev;  // the previous step's half: zeroed by workgroup 0
   int* bucket;
+  uint64_t* cellx;  // launch B's per-env granule rows; the wave-owned kernel spills lists there
   const float* reward_src;
   const uint8_t* done_src;
   float* reward_dst;
@@ -815,7 +823,7 @@ __device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* 
       a.stamps[(size_t)blockIdx.x * 64 * kActStamps + (k) * 64 + threadIdx.x] =           \
           __builtin_amdgcn_s_memrealtime();                                              \
   } while (0)
-constexpr int kActStamps = 8;
+constexpr int kActStamps = 9;
 
 __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
   char* smem = trunk_smem;
@@ -1048,8 +1056,338 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
     ACT_STAMP(6);
     trunk_fc(R1, H2, W2, nimg, img0, t, (float*)R2);  // ends with a barrier
     ACT_STAMP(7);
+    ACT_STAMP(8);
   }
 #undef ACT_PHASE
+}
+
+// ------------------------------------------------------------------ launch A, wave-owned tiles
+// act_trunk_kernel's work with the tile split by WAVE instead of by phase: wave w owns envs
+// 2w, 2w+1 of the 16-env tile from their sparse rows to their critic value -- codes, decode,
+// stage-0 conv + pool, the 14 convs (conv_lds WV = 1 / 2 over its own images), the pools, the
+// halo zeroing and network.5 + critic -- in its own slices of the two regions, so the trunk
+// needs no workgroup barrier at all (LDS is in order within a wave). act_trunk_kernel ran ~25
+// workgroup-wide phases per tile with 2 waves per SIMD: every phase waited for its slowest wave,
+// the 2x2 stage had 4 pixel blocks for 8 waves, and no tile's prologue overlapped another's
+// convs (profiles/33: 52 % of wave cycles waiting, MFMA 9.7 %). Here one wave's decode, pools
+// and LDS latency run while the other waves' MFMAs do.
+//
+// Only the bucket reservation stays tile-wide (one global atomic per (tile, cell), as before):
+// decode appends each active pair to the tile's LDS list (LDS atomics for the list index and
+// the pair's slot among the tile's pairs of that cell) and the list is turned into bucket
+// entries after the trunk, behind two barriers. List, counters and count are double-buffered
+// by tile parity, so the next tile's decode never waits for the bucket writes; a tile with
+// more than kWList pairs spills the rest into its envs' cellx rows (launch B writes those
+// rows only later).
+//
+// network.5 + critic per wave: the FC's MFMA B operand is the wave's 2 images (16-column
+// blocks, 14 columns idle: 48 more MFMAs per wave and tile, no barrier or cross-wave value
+// reduction), with fc_fwd_kernel<256>'s K order and critic summation order (the four
+// 64-hidden partials summed in wave order), so f and v are bit-identical to it.
+constexpr int kWEnv = 2;                                     // envs (images) per wave
+constexpr int kWImgB = 10 * 10 * TG<16>::PIXB;               // largest per-image footprint (X0)
+constexpr int kWSlice = kWEnv * kWImgB;                      // a wave's slice of R1 / R2
+constexpr int kWRegion = (kThreads / 64) * kWSlice;          // R1 = R2 = 76800 bytes
+constexpr int kWLut = 2 * kWRegion;                          // byte -> 8 bf16 table, 4 KB
+constexpr int kWCnt = kWLut + 256 * 16;                      // [2][256] pair counts per cell
+constexpr int kWNp = kWCnt + 2 * kActS * 4;                  // [2] list lengths (+ pad)
+constexpr int kWList = 508;                                  // list entries per parity in LDS
+constexpr int kWLst = kWNp + 16;                             // [2][kWList] packed pairs
+constexpr int kWSmem = kWLst + 2 * kWList * 4;
+static_assert(kWSmem <= 160 * 1024, "wave-owned acting tile exceeds the LDS");
+static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage footprints");
+// a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run)
+constexpr int kWCodes = 0, kWBits = kWEnv * kActS * 2;
+static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
+
+// one wave: relu -> network.5 -> relu -> critic for its nimg <= 2 images (X2 halo'd at x2)
+__device__ __forceinline__ void wave_fc(int x2, int nimg, int img0, const TrunkArgs& a) {
+  constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2, I = NKS * 32;
+  const int lane = threadIdx.x & 63, G = lane >> 4, li = lane & 15;
+  const bool valid = li < nimg;
+  Frag8 b[NKS];  // this lane's image column (li) of relu(X2), one 32-channel pixel per K step
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int py = ks / W2, px = ks - py * W2;
+    b[ks].u = valid ? relu8(*(const uint4*)(trunk_smem + x2 +
+                                            ((li * (H2 + 2) + py + 1) * (W2 + 2) + px + 1) * PX +
+                                            G * 16))
+                    : make_uint4(0, 0, 0, 0);
+  }
+  float vq[4];  // fc_fwd's per-wave partials: hidden blocks 4 wq .. 4 wq + 3
+#pragma unroll 1
+  for (int wq = 0; wq < 4; ++wq) {
+    float vpart = 0.f;
+#pragma unroll 1
+    for (int j = 0; j < 4; ++j) {
+      const int hb = wq * 4 + j;
+      const uint4* wrow = (const uint4*)(a.w5 + (size_t)(hb * 16 + li) * I) + G;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        Frag8 w;
+        w.u = wrow[ks * 4];
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.v, b[ks].v, acc, 0, 0, 0);
+      }
+      const int h0 = hb * 16 + 4 * G;
+      float hv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
+        vpart += hv[i] * a.wc[h0 + i];
+      }
+      uint32_t o[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
+               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
+      if (valid) *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
+    }
+    vpart += __shfl_xor(vpart, 16, 64);
+    vpart += __shfl_xor(vpart, 32, 64);
+    vq[wq] = vpart;
+  }
+  if (G == 0 && valid) a.v_out[img0 + li] = vq[0] + vq[1] + vq[2] + vq[3] + a.bc[0];
+}
+
+__global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
+  const TrunkArgs& t = a.t;
+  constexpr int S = kActS, H0 = 8, W0 = 8, H1 = 4, W1 = 4, H2 = 2, W2 = 2;
+  constexpr int NW = kThreads / 64, TNI = NW * kWEnv;
+  const int E = t.N;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int oR1 = wave * kWSlice, oR2 = kWRegion + wave * kWSlice;  // this wave's slices
+  char* R1 = trunk_smem + oR1;
+  char* R2 = trunk_smem + oR2;
+  const char* lut = trunk_smem + kWLut;
+  uint16_t* lcodes = (uint16_t*)(R2 + kWCodes);
+  uint32_t* lbits = (uint32_t*)(R2 + kWBits);
+  const int ngroups = (E + TNI - 1) / TNI;
+  // once per launch: the LUT, both parities' tile counters, the previous step's bucket half
+  if (tid < 256) ((uint4*)(trunk_smem + kWLut))[tid] = mbk::bits8_bf16((uint32_t)tid);
+  for (int c = tid; c < 2 * S; c += kThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
+  if (tid < 2) ((int*)(trunk_smem + kWNp))[tid] = 0;
+  if (blockIdx.x == 0)  // the previous step's launch B is done with these
+    for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
+  mbk::lds_barrier();
+  uint32_t pre0 = 0u, pre1 = 0u;  // this wave's next-tile row words (lane < kActSpec)
+  // a layer's weight fragments are fetched at its start (no register prefetch one layer ahead
+  // as in act_trunk_kernel: that doubled the 72 fragment VGPRs and spilled; here the other
+  // waves' work covers one wave's L2 wait)
+#define ACT_WPHASE(l, CI, CO, RELU, MODE, WV_, IN, H_, W_, OUT)                           \
+  do {                                                                                   \
+    uint4 wc[kWFrag];                                                                    \
+    wfetch(t.w[l], CI, CO, wc);                                                          \
+    conv_lds<CI, CO, RELU, MODE, false, false, WV_>(IN, H_, W_, nw, 0, wc, TG<CI>::NCH * 64, \
+                                                    t.b[l], OUT);                       \
+    __builtin_amdgcn_wave_barrier();                                                     \
+  } while (0)
+  int k = 0;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x, ++k) {
+    const int par = k & 1;
+    int* lcnt = (int*)(trunk_smem + kWCnt) + par * S;
+    int* np = (int*)(trunk_smem + kWNp) + par;
+    uint32_t* lst = (uint32_t*)(trunk_smem + kWLst) + par * kWList;
+    const int img0 = grp * TNI, nimg = min(TNI, E - img0);
+    const int e0 = wave * kWEnv;                 // this wave's first env within the tile
+    const int nw = max(0, min(kWEnv, nimg - e0));  // ... and how many it has
+    uint32_t* ovf = (uint32_t*)(a.cellx + (size_t)img0 * S);  // list spill (this tile's rows)
+    bool spilled = false;
+    if (nw > 0) {
+      // stage-0 conv weights / bias first: their L2 latency hides behind the rows and decode
+      Frag8 bw0[9];
+      {
+        const uint4* wp = (const uint4*)(a.w0 + (size_t)li * 9 * 32 + g * 8);
+#pragma unroll
+        for (int c = 0; c < 9; ++c) bw0[c].u = wp[c * 4];
+      }
+      float bias0[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bias0[i] = a.b0[4 * g + i];
+      ACT_STAMP(0);
+      // ---- codes of the wave's envs -> its LDS code rows; resources in registers
+      int res0 = 0, res1 = 0;  // (kWEnv = 2: named, so a rolled loop keeps them in registers)
+#pragma unroll 1
+      for (int j = 0; j < nw; ++j) {
+        const int el = e0 + j;
+        uint16_t* cs = lcodes + j * S;
+        if (a.code_list) {
+          for (int c = lane * 4; c < S; c += 256) *(uint2*)(cs + c) = make_uint2(0u, 0u);
+          const uint32_t* row = a.code_list + (size_t)(img0 + el) * a.list_stride;
+          const uint32_t w = k == 0 ? (lane < kActSpec && lane <= S ? row[lane] : 0u)
+                                    : (j ? pre1 : pre0);
+          const uint32_t w0 = (uint32_t)__shfl((int)w, 0, 64);
+          const int n = min((int)(w0 & 0xFFFFu), S);
+          (j ? res1 : res0) = (int)(w0 >> 16);
+          __builtin_amdgcn_wave_barrier();
+          if (lane >= 1 && lane < kActSpec && lane <= n && (w & 0xFFFFu) < (uint32_t)S)
+            cs[w & 0xFFFFu] = (uint16_t)(w >> 16);
+          for (int q = kActSpec + lane; q <= n; q += 64) {
+            const uint32_t x = row[q];
+            if ((x & 0xFFFFu) < (uint32_t)S) cs[x & 0xFFFFu] = (uint16_t)(x >> 16);
+          }
+        } else {
+          ((uint4*)cs)[lane & 31] = ((const uint4*)(a.codes + (size_t)(img0 + el) * S))[lane & 31];
+          (j ? res1 : res0) = a.res[img0 + el];
+        }
+        if (lane == 0) {
+          if (a.reward_dst) a.reward_dst[img0 + el] = a.reward_src[img0 + el];
+          if (a.done_dst) a.done_dst[img0 + el] = a.done_src[img0 + el];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      ACT_STAMP(1);
+      // ---- decode (act_trunk_kernel P2, per env of this wave)
+#pragma unroll 1
+      for (int j = 0; j < nw; ++j) {
+        const int el = e0 + j, e = img0 + el;
+        const uint16_t* cs = lcodes + j * S;
+        const int r = j ? res1 : res0;
+        const int c0 = lane * 4;
+        uint32_t ob[4], mk[12];
+        int nact = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = c0 + q;
+          uint32_t w3[3];
+          mbk::cell_mask(cs, c, 16, 16, r, w3);
+          ob[q] = mbr::code_bits(cs[c]);
+          mk[3 * q] = w3[0];
+          mk[3 * q + 1] = w3[1];
+          mk[3 * q + 2] = w3[2];
+          nact += (w3[0] | w3[1] | w3[2]) != 0u;
+        }
+        int kx = nact;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(kx, o, 64);
+          if (lane >= o) kx += y;
+        }
+        const int n = __shfl(kx, 63, 64);
+        kx -= nact;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (mk[3 * q] | mk[3 * q + 1] | mk[3 * q + 2]) {
+            const int c = c0 + q;
+            const int i = atomicAdd(np, 1);
+            const uint32_t en = (uint32_t)c | ((uint32_t)atomicAdd(&lcnt[c], 1) << 8) |
+                                ((uint32_t)el << 12) | ((uint32_t)kx << 16);
+            if (i < kWList) {
+              lst[i] = en;
+            } else {
+              ovf[i - kWList] = en;
+              spilled = true;
+            }
+            ++kx;
+          }
+        }
+        const uint4 o4 = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+        const uint4 m0 = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+        const uint4 m1 = make_uint4(mk[4], mk[5], mk[6], mk[7]);
+        const uint4 m2 = make_uint4(mk[8], mk[9], mk[10], mk[11]);
+        *(uint4*)(lbits + j * S + c0) = o4;
+        const size_t eo = (size_t)e * S + c0;
+        *(uint4*)(a.obs + eo) = o4;
+        uint4* mp = (uint4*)(a.mask + eo * 3);
+        mp[0] = m0;
+        mp[1] = m1;
+        mp[2] = m2;
+        if (a.obs2) {
+          *(uint4*)(a.obs2 + eo) = o4;
+          uint4* mp2 = (uint4*)(a.mask2 + eo * 3);
+          mp2[0] = m0;
+          mp2[1] = m1;
+          mp2[2] = m2;
+        }
+        const uint4 z4 = make_uint4(0, 0, 0, 0);
+        uint4* act4 = (uint4*)(a.action + (size_t)e * S * 7);
+        for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = z4;
+        if (lane == 0) {
+          a.pending[e] = n;
+          a.pending[E + e] = n;
+          if (n == 0) a.logp[e] = 0.f;
+        }
+        if (a.act_list) {
+          if (n == 0 && lane == 0) a.act_list[(size_t)e * a.list_stride] = 0u;
+        } else {
+          *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      ACT_STAMP(2);
+      // ---- stage-0 conv + pool of the wave's images into its X0 slice
+      zero_halo<TG<16>::PIXB, true>(R1, nw, H0, W0);
+      for (int j = 0; j < nw; ++j) act_conv0(lbits + j * S, lut, bw0, bias0, R1, j);
+      if (a.code_list) {  // the wave's next-tile rows, in flight during this tile's trunk
+        const int img0n = img0 + gridDim.x * TNI;
+        const bool pl = lane < kActSpec && lane <= S;
+        pre0 = (img0n + e0 < E && pl) ? a.code_list[(size_t)(img0n + e0) * a.list_stride + lane] : 0u;
+        pre1 = (img0n + e0 + 1 < E && pl)
+                   ? a.code_list[(size_t)(img0n + e0 + 1) * a.list_stride + lane] : 0u;
+      }
+      __builtin_amdgcn_wave_barrier();
+      zero_halo<TG<16>::PIXB, true>(R2, nw, H0, W0);  // U0 layout (decode scratch is dead)
+      __builtin_amdgcn_wave_barrier();
+      ACT_STAMP(3);
+      // ---- stage 0 residual blocks, stages 1 and 2 on the wave's own images
+#pragma unroll 1
+      for (int rb = 0; rb < 2; ++rb) {
+        ACT_WPHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, 1, oR1, H0, W0, oR2);
+        ACT_WPHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, 1, oR2, H0, W0, oR1);
+      }
+      ACT_STAMP(4);
+      ACT_WPHASE(4, 16, 32, false, OUT_STAGE, 1, oR1, H0, W0, oR2);
+      pool_lds<32, false, true>((const bf16*)R2, H0, W0, nw, R1);
+      zero_halo<TG<32>::PIXB, true>(R1, nw, H1, W1);
+      zero_halo<TG<32>::PIXB, true>(R2, nw, H1, W1);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+      for (int rb = 0; rb < 2; ++rb) {
+        ACT_WPHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 1, oR1, H1, W1, oR2);
+        ACT_WPHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 1, oR2, H1, W1, oR1);
+      }
+      ACT_STAMP(5);
+      ACT_WPHASE(9, 32, 32, false, OUT_STAGE, 1, oR1, H1, W1, oR2);
+      pool_lds<32, false, true>((const bf16*)R2, H1, W1, nw, R1);
+      zero_halo<TG<32>::PIXB, true>(R1, nw, H2, W2);
+      zero_halo<TG<32>::PIXB, true>(R2, nw, H2, W2);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+      for (int rb = 0; rb < 2; ++rb) {
+        ACT_WPHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 2, oR1, H2, W2, oR2);
+        ACT_WPHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 2, oR2, H2, W2, oR1);
+      }
+      ACT_STAMP(6);
+      wave_fc(oR1, nw, img0 + e0, t);
+      ACT_STAMP(7);
+    }
+    // ---- the tile's bucket reservation (one global atomic per active cell) and entries
+    if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // spill rows in L2 first
+    mbk::lds_barrier();
+    for (int c = tid; c < S; c += kThreads) {
+      const int n = lcnt[c];
+      if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
+    }
+    {  // the other parity (the previous tile's, consumed before this barrier) for the next tile
+      int* lc2 = (int*)(trunk_smem + kWCnt) + (par ^ 1) * S;
+      for (int c = tid; c < S; c += kThreads) lc2[c] = 0;
+      if (tid == 0) ((int*)(trunk_smem + kWNp))[par ^ 1] = 0;
+    }
+    mbk::lds_barrier();
+    const int npr = *np;
+    for (int i = tid; i < npr; i += kThreads) {
+      const uint32_t en = i < kWList ? lst[i]
+                                     : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+      const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
+      const int el = (int)((en >> 12) & 0xFu), rank = (int)(en >> 16);
+      a.bucket[(size_t)c * E + lcnt[c] + slot] = (img0 + el) | (rank << 16);
+    }
+    if (tid == 0 && a.stamps && k == 0)  // the reservation's end (stamp 8, wave 0's clock)
+      a.stamps[(size_t)blockIdx.x * 64 * kActStamps + 8 * 64] = __builtin_amdgcn_s_memrealtime();
+  }
+#undef ACT_WPHASE
 }
 
 size_t region_bytes(int H0, int W0, int TNI) {
@@ -1231,6 +1569,15 @@ extern "C" int mbk_act_set_stamps(void* stamps) {
   return kActStamps;
 }
 
+static int act_wave() {  // MBK_ACT_WAVE=0: the phase-split kernel (A/B)
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("MBK_ACT_WAVE");
+    v = e ? std::atoi(e) : 1;
+  }
+  return v;
+}
+
 extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
   if (!m || !s || m->E <= 0 || m->H != 16 || m->W != 16) return (int)hipErrorInvalidValue;
   if (!m->w0 || !m->b0 || !m->w5 || !m->b5 || !m->wc || !m->bc || !m->feat || !m->cellx ||
@@ -1266,13 +1613,15 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   t.N = m->E;
   t.H0 = 8;
   t.W0 = 8;
-  const int tni = act_tni();
+  const bool wave_owned = act_wave() != 0;
+  const int tni = wave_owned ? (kThreads / 64) * kWEnv : act_tni();
   t.tni = tni;
   const size_t r =
       (std::max(region_bytes(8, 8, tni), (size_t)act_layout(tni).end) + 15) & ~(size_t)15;
   t.r1_bytes = t.r2_bytes = (int)r;
-  const size_t sm = 2 * r;
+  const size_t sm = wave_owned ? (size_t)kWSmem : 2 * r;
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
+  if (wave_owned && m->E > 65535) return (int)hipErrorInvalidValue;  // bucket entry: env | rank
   a.w0 = (const bf16*)m->w0;
   a.b0 = m->b0;
   a.codes = s->codes;
@@ -1292,6 +1641,7 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.bucket_cnt = m->bucket_cnt + (s->step & 1) * S;
   a.bucket_cnt_prev = m->bucket_cnt + ((s->step + 1) & 1) * S;
   a.bucket = m->bucket;
+  a.cellx = m->cellx;
   a.reward_src = s->reward_src;
   a.done_src = s->done_src;
   a.reward_dst = s->reward_dst;
@@ -1304,18 +1654,24 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
+  const void* kfn = wave_owned ? (const void*)act_trunk_w_kernel : (const void*)act_trunk_kernel;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)act_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                         160 * 1024);
+    hipFuncSetAttribute((const void*)act_trunk_w_kernel,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)act_trunk_kernel, kThreads,
-                                                   sm) != hipSuccess || per < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess ||
+      per < 1)
     per = 1;
   const int ngroups = (m->E + tni - 1) / tni;
   const int grid = std::min(ngroups, cus * per);
-  hipLaunchKernelGGL(act_trunk_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
+  if (wave_owned)
+    hipLaunchKernelGGL(act_trunk_w_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
+  else
+    hipLaunchKernelGGL(act_trunk_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

@@ -19,8 +19,10 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-PHASES = ["P1 codes->LDS", "P2 decode", "P3 buckets+conv0", "stage 0 res", "stage 1",
-          "stage 2", "fc + critic"]
+# stamp intervals of wave 0's first tile (MBK_ACT_WAVE=1: its own 2 envs, then the tile's
+# bucket phase; MBK_ACT_WAVE=0: the phase-split kernel's workgroup-wide phases, last one empty)
+PHASES = ["P1 codes->LDS", "P2 decode", "P3 (buckets+) conv0", "stage 0 res", "stage 1",
+          "stage 2", "fc + critic", "tile buckets"]
 
 
 def main():
@@ -99,7 +101,7 @@ def main():
     print(f"launch A (decode + trunk + critic) {1e3 * ta / n:.1f} us, launch B (head + finale) "
           f"{1e3 * tb / n:.1f} us, rows in {'HBM' if a.device_rows else 'pinned host memory'}")
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    stamps = torch.zeros(ncu * 4 * 8 * 64, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(ncu * 4 * 9 * 64, dtype=torch.int64, device=dev)
     nst = k.mbk_act_set_stamps(stamps.data_ptr())
     st.step = a.steps + 3
     N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk (stamped)")
