@@ -276,7 +276,7 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(const bf16* __restrict__ x,
     for (int i = 0; i < 4; ++i) {
       // the critic consumes the bf16-rounded activations (what the head sees)
       hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + b5[h0 + i], 0.f)));
-      vpart += hv[i] * wc[h0 + i];
+      vpart = __builtin_fmaf(hv[i], wc[h0 + i], vpart);  // explicit: same in every FC kernel
     }
     uint32_t o[2];
 #pragma unroll
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + bb[j][i], 0.f)));
-        vpart += hv[i] * ww[j][i];
+        vpart = __builtin_fmaf(hv[i], ww[j][i], vpart);
       }
       uint32_t o[2];
 #pragma unroll

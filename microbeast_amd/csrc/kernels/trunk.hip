@@ -442,7 +442,7 @@ __device__ __forceinline__ void trunk_fc(const char* x2, int H2, int W2, int nim
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
-        vpart += hv[i] * a.wc[h0 + i];
+        vpart = __builtin_fmaf(hv[i], a.wc[h0 + i], vpart);
       }
       uint32_t o[2];
 #pragma unroll
@@ -1134,7 +1134,7 @@ __device__ __forceinline__ void wave_fc(int x2, int nimg, int img0, const TrunkA
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
-        vpart += hv[i] * a.wc[h0 + i];
+        vpart = __builtin_fmaf(hv[i], a.wc[h0 + i], vpart);
       }
       uint32_t o[2];
 #pragma unroll
