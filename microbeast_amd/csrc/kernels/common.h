@@ -158,6 +158,29 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// ------------------------------------------------------------------ critic order
+// The critic value v = wc . f + bc from the MFMA C layout of network.5 (lane (G, li) holds
+// hidden units 4G .. 4G+3 of a 16-unit block for row li): every FC kernel (fc.hip fc_fwd /
+// fc_fwd_rb, trunk.hip trunk_fc and the acting tile's FC) sums in THIS order, so the graph,
+// fused-acting and learner values agree bit for bit: per block, the lane's 4 products as an
+// explicit fma chain from 0 (llvm.fmuladd fuses differently per kernel), then the xor-16 /
+// xor-32 butterfly over the lane groups (crit_block); then the blocks in hidden order, then
+// the bias (crit_sum over the blocks' partials).
+__device__ __forceinline__ float crit_block(const float hv[4], const float w[4]) {
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q = __builtin_fmaf(hv[i], w[i], q);
+  q += __shfl_xor(q, 16, 64);
+  q += __shfl_xor(q, 32, 64);
+  return q;
+}
+// part[hb * stride] for hb = 0 .. nb-1, in order, then + bc
+__device__ __forceinline__ float crit_sum(const float* part, int nb, int stride, float bc) {
+  float v = part[0];
+  for (int hb = 1; hb < nb; ++hb) v += part[hb * stride];
+  return v + bc;
+}
+
 // ------------------------------------------------------------------ reductions
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(const bf16* __restrict__ x,
                                                      bf16* __restrict__ f_out,
                                                      float* __restrict__ v_out) {
   constexpr int NBW = O / 64;  // 16-wide hidden blocks per wave
-  __shared__ float vred[4][16];
+  __shared__ float vred[O / 16][16];  // per hidden block: the critic partial of each row
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
   const int r0 = blockIdx.x * 16;
@@ -267,17 +267,18 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(const bf16* __restrict__ x,
       acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc[j], 0, 0, 0);
     }
   }
-  float vpart = 0.f;
 #pragma unroll
   for (int j = 0; j < NBW; ++j) {
     const int h0 = (wave * NBW + j) * 16 + 4 * G;  // lane: hidden units h0..h0+3 of `row`
-    float hv[4];
+    float hv[4], w4[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       // the critic consumes the bf16-rounded activations (what the head sees)
       hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + b5[h0 + i], 0.f)));
-      vpart = __builtin_fmaf(hv[i], wc[h0 + i], vpart);  // explicit: same in every FC kernel
+      w4[i] = wc[h0 + i];
     }
+    const float q = mbk::crit_block(hv, w4);
+    if (G == 0) vred[wave * NBW + j][li] = q;
     uint32_t o[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -285,13 +286,10 @@ __global__ __launch_bounds__(256) void fc_fwd_kernel(const bf16* __restrict__ x,
              ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
     if (valid) *(uint2*)(f_out + (size_t)row * O + h0) = make_uint2(o[0], o[1]);
   }
-  vpart += __shfl_xor(vpart, 16, 64);
-  vpart += __shfl_xor(vpart, 32, 64);
-  if (G == 0) vred[wave][li] = vpart;
   __syncthreads();
   if (threadIdx.x < 16 && r0 + (int)threadIdx.x < F) {
     const int t = threadIdx.x;
-    v_out[r0 + t] = vred[0][t] + vred[1][t] + vred[2][t] + vred[3][t] + bc[0];
+    v_out[r0 + t] = mbk::crit_sum(&vred[0][t], O / 16, 16, bc[0]);
   }
 }
 
@@ -311,7 +309,7 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
                                                         bf16* __restrict__ f_out,
                                                         float* __restrict__ v_out) {
   constexpr int NBW = O / 64, I = NKS * 32;
-  __shared__ float vred[2][4][16];
+  __shared__ float vred[2][O / 16][16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
   const int nrb = (F + 15) / 16;
@@ -361,16 +359,15 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
       for (int j = 0; j < NBW; ++j)
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][ks].v, b.v, acc[j], 0, 0, 0);
     }
-    float vpart = 0.f;
 #pragma unroll
     for (int j = 0; j < NBW; ++j) {
       const int h0 = (wave * NBW + j) * 16 + 4 * G;
       float hv[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < 4; ++i)
         hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + bb[j][i], 0.f)));
-        vpart = __builtin_fmaf(hv[i], ww[j][i], vpart);
-      }
+      const float q = mbk::crit_block(hv, ww[j]);
+      if (G == 0) vred[buf][wave * NBW + j][li] = q;
       uint32_t o[2];
 #pragma unroll
       for (int k = 0; k < 2; ++k)
@@ -378,13 +375,10 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
                ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
       if (valid) *(uint2*)(f_out + (size_t)row * O + h0) = make_uint2(o[0], o[1]);
     }
-    vpart += __shfl_xor(vpart, 16, 64);
-    vpart += __shfl_xor(vpart, 32, 64);
-    if (G == 0) vred[buf][wave][li] = vpart;
     __syncthreads();  // (double-buffered: the next block's writes go to the other half)
     if (threadIdx.x < 16 && rb * 16 + (int)threadIdx.x < F) {
       const int t = threadIdx.x;
-      v_out[rb * 16 + t] = vred[buf][0][t] + vred[buf][1][t] + vred[buf][2][t] + vred[buf][3][t] + bcv;
+      v_out[rb * 16 + t] = mbk::crit_sum(&vred[buf][0][t], O / 16, 16, bcv);
     }
   }
 }

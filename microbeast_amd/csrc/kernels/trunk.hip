@@ -421,7 +421,6 @@ __device__ __forceinline__ void trunk_fc(const char* x2, int H2, int W2, int nim
     const bool valid = im < nimg;
     // one hidden block at a time (4 accumulators live, not 16): the head runs at the end of
     // a 256-VGPR kernel; x fragments are re-read from LDS per block instead
-    float vpart = 0.f;
 #pragma unroll 1
     for (int j = 0; j < NBW; ++j) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -438,12 +437,14 @@ __device__ __forceinline__ void trunk_fc(const char* x2, int H2, int W2, int nim
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.v, b.v, acc, 0, 0, 0);
       }
       const int h0 = (wq * NBW + j) * 16 + 4 * G;
-      float hv[4];
+      float hv[4], w4[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
-        vpart = __builtin_fmaf(hv[i], a.wc[h0 + i], vpart);
+        w4[i] = a.wc[h0 + i];
       }
+      const float q = mbk::crit_block(hv, w4);  // the critic order of every FC kernel
+      if (G == 0) vred[(half * 16 + wq * NBW + j) * 16 + li] = q;
       uint32_t o[2];
 #pragma unroll
       for (int k = 0; k < 2; ++k)
@@ -451,14 +452,10 @@ __device__ __forceinline__ void trunk_fc(const char* x2, int H2, int W2, int nim
                ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
       if (valid) *(uint2*)(a.f_out + (size_t)(img0 + im) * O + h0) = make_uint2(o[0], o[1]);
     }
-    vpart += __shfl_xor(vpart, 16, 64);
-    vpart += __shfl_xor(vpart, 32, 64);
-    if (G == 0) vred[(half * 4 + wq) * 16 + li] = vpart;
     __syncthreads();
     if (threadIdx.x < 32) {
       const int hh = threadIdx.x >> 4, t = threadIdx.x & 15, r = c0 + hh * 16 + t;
-      const float* vr = vred + hh * 64;
-      if (r < nimg) a.v_out[img0 + r] = vr[t] + vr[16 + t] + vr[32 + t] + vr[48 + t] + a.bc[0];
+      if (r < nimg) a.v_out[img0 + r] = mbk::crit_sum(vred + hh * 256 + t, 16, 16, a.bc[0]);
     }
     __syncthreads();
   }
@@ -823,7 +820,7 @@ __device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* 
       a.stamps[(size_t)blockIdx.x * 64 * kActStamps + (k) * 64 + threadIdx.x] =           \
           __builtin_amdgcn_s_memrealtime();                                              \
   } while (0)
-constexpr int kActStamps = 9;
+constexpr int kActStamps = 21;  // the wave-owned kernel uses all; act_trunk_kernel 0-8
 
 __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
   char* smem = trunk_smem;
@@ -1063,27 +1060,27 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
 
 // ------------------------------------------------------------------ launch A, wave-owned tiles
 // act_trunk_kernel's work with the tile split by WAVE instead of by phase: wave w owns envs
-// 2w, 2w+1 of the 16-env tile from their sparse rows to their critic value -- codes, decode,
-// stage-0 conv + pool, the 14 convs (conv_lds WV = 1 / 2 over its own images), the pools, the
-// halo zeroing and network.5 + critic -- in its own slices of the two regions, so the trunk
-// needs no workgroup barrier at all (LDS is in order within a wave). act_trunk_kernel ran ~25
-// workgroup-wide phases per tile with 2 waves per SIMD: every phase waited for its slowest wave,
-// the 2x2 stage had 4 pixel blocks for 8 waves, and no tile's prologue overlapped another's
-// convs (profiles/33: 52 % of wave cycles waiting, MFMA 9.7 %). Here one wave's decode, pools
-// and LDS latency run while the other waves' MFMAs do.
+// 2w, 2w+1 of the 16-env tile from their sparse rows to their trunk output -- codes, decode,
+// stage-0 conv + pool, the 14 convs (conv_lds WV = 1 / 2 over its own images), the pools and
+// the halo zeroing -- in its own slices of the two regions, so the trunk needs no workgroup
+// barrier at all (LDS is in order within a wave). act_trunk_kernel ran ~25 workgroup-wide
+// phases per tile with 2 waves per SIMD: every phase waited for its slowest wave, the 2x2 stage
+// had 4 pixel blocks for 8 waves, and no tile's prologue overlapped another's convs
+// (profiles/33: 52 % of wave cycles waiting, MFMA 9.7 %).
 //
-// Only the bucket reservation stays tile-wide (one global atomic per (tile, cell), as before):
-// decode appends each active pair to the tile's LDS list (LDS atomics for the list index and
-// the pair's slot among the tile's pairs of that cell) and the list is turned into bucket
-// entries after the trunk, behind two barriers. List, counters and count are double-buffered
-// by tile parity, so the next tile's decode never waits for the bucket writes; a tile with
-// more than kWList pairs spills the rest into its envs' cellx rows (launch B writes those
-// rows only later).
+// Tile-wide, behind two barriers at the tile's end: the bucket reservation (one global atomic
+// per (tile, cell), as before) and network.5 + critic. Decode appends each active pair to the
+// tile's LDS list (LDS atomics for its index and its slot among the tile's pairs of that
+// cell); list, counters and count are double-buffered by tile parity, so the next tile's decode
+// never waits for the bucket writes; a tile with more than kWList pairs spills the rest into
+// its envs' cellx rows (launch B writes those rows only later). The FC gives each wave two
+// hidden blocks of all 16 images (its W5 fragments are loaded before the first barrier), the
+// critic partials meet in LDS (mbk::crit_block / crit_sum: every FC kernel's order).
 //
-// network.5 + critic per wave: the FC's MFMA B operand is the wave's 2 images (16-column
-// blocks, 14 columns idle: 48 more MFMAs per wave and tile, no barrier or cross-wave value
-// reduction), with fc_fwd_kernel<256>'s K order and critic summation order (the four
-// 64-hidden partials summed in wave order), so f and v are bit-identical to it.
+// Memory order per wave and tile (vmcnt counts loads and stores in issue order): the stage-0
+// weights, this tile's rows (first tile only), reward / done, then the NEXT tile's rows from
+// pinned host memory right away, so their PCIe latency has the decode and stage-0 conv to
+// hide behind before the first weight wait that orders after them.
 constexpr int kWEnv = 2;                                     // envs (images) per wave
 constexpr int kWImgB = 10 * 10 * TG<16>::PIXB;               // largest per-image footprint (X0)
 constexpr int kWSlice = kWEnv * kWImgB;                      // a wave's slice of R1 / R2
@@ -1091,8 +1088,9 @@ constexpr int kWRegion = (kThreads / 64) * kWSlice;          // R1 = R2 = 76800 
 constexpr int kWLut = 2 * kWRegion;                          // byte -> 8 bf16 table, 4 KB
 constexpr int kWCnt = kWLut + 256 * 16;                      // [2][256] pair counts per cell
 constexpr int kWNp = kWCnt + 2 * kActS * 4;                  // [2] list lengths (+ pad)
-constexpr int kWList = 508;                                  // list entries per parity in LDS
-constexpr int kWLst = kWNp + 16;                             // [2][kWList] packed pairs
+constexpr int kWVred = kWNp + 16;                            // [16 blocks][16 images] critic
+constexpr int kWList = 380;                                  // list entries per parity in LDS
+constexpr int kWLst = kWVred + 16 * 16 * 4;                  // [2][kWList] packed pairs
 constexpr int kWSmem = kWLst + 2 * kWList * 4;
 static_assert(kWSmem <= 160 * 1024, "wave-owned acting tile exceeds the LDS");
 static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage footprints");
@@ -1100,54 +1098,50 @@ static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage
 constexpr int kWCodes = 0, kWBits = kWEnv * kActS * 2;
 static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
 
-// one wave: relu -> network.5 -> relu -> critic for its nimg <= 2 images (X2 halo'd at x2)
-__device__ __forceinline__ void wave_fc(int x2, int nimg, int img0, const TrunkArgs& a) {
-  constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2, I = NKS * 32;
-  const int lane = threadIdx.x & 63, G = lane >> 4, li = lane & 15;
+// network.5 + critic of the tile: wave w computes hidden blocks 2w, 2w+1 (wf: their W5
+// fragments, loaded before the barrier) for the tile's 16 images, whose X2 tiles sit in the
+// waves' R1 slices (image i: wave i / 2's slice, its image i % 2); critic partials -> vred
+__device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
+                                        const uint4 wf[2][4], float* vred) {
+  constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int G = lane >> 4, li = lane & 15;
   const bool valid = li < nimg;
-  Frag8 b[NKS];  // this lane's image column (li) of relu(X2), one 32-channel pixel per K step
+  const int x2 = (li >> 1) * kWSlice + (li & 1) * (H2 + 2) * (W2 + 2) * PX;
+  Frag8 b[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
     const int py = ks / W2, px = ks - py * W2;
-    b[ks].u = valid ? relu8(*(const uint4*)(trunk_smem + x2 +
-                                            ((li * (H2 + 2) + py + 1) * (W2 + 2) + px + 1) * PX +
+    b[ks].u = valid ? relu8(*(const uint4*)(trunk_smem + x2 + ((py + 1) * (W2 + 2) + px + 1) * PX +
                                             G * 16))
                     : make_uint4(0, 0, 0, 0);
   }
-  float vq[4];  // fc_fwd's per-wave partials: hidden blocks 4 wq .. 4 wq + 3
-#pragma unroll 1
-  for (int wq = 0; wq < 4; ++wq) {
-    float vpart = 0.f;
-#pragma unroll 1
-    for (int j = 0; j < 4; ++j) {
-      const int hb = wq * 4 + j;
-      const uint4* wrow = (const uint4*)(a.w5 + (size_t)(hb * 16 + li) * I) + G;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        Frag8 w;
-        w.u = wrow[ks * 4];
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.v, b[ks].v, acc, 0, 0, 0);
-      }
-      const int h0 = hb * 16 + 4 * G;
-      float hv[4];
+  for (int jj = 0; jj < 2; ++jj) {
+    const int hb = 2 * wave + jj;
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
-        vpart = __builtin_fmaf(hv[i], a.wc[h0 + i], vpart);
-      }
-      uint32_t o[2];
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-        o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
-               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
-      if (valid) *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
+    for (int ks = 0; ks < NKS; ++ks) {
+      Frag8 w;
+      w.u = wf[jj][ks];
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w.v, b[ks].v, acc, 0, 0, 0);
     }
-    vpart += __shfl_xor(vpart, 16, 64);
-    vpart += __shfl_xor(vpart, 32, 64);
-    vq[wq] = vpart;
+    const int h0 = hb * 16 + 4 * G;
+    float hv[4], w4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[i] + a.b5[h0 + i], 0.f)));
+      w4[i] = a.wc[h0 + i];
+    }
+    const float q = mbk::crit_block(hv, w4);
+    if (G == 0) vred[hb * 16 + li] = q;
+    uint32_t o[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
+             ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
+    if (valid) *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
   }
-  if (G == 0 && valid) a.v_out[img0 + li] = vq[0] + vq[1] + vq[2] + vq[3] + a.bc[0];
 }
 
 __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
@@ -1163,7 +1157,9 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   const char* lut = trunk_smem + kWLut;
   uint16_t* lcodes = (uint16_t*)(R2 + kWCodes);
   uint32_t* lbits = (uint32_t*)(R2 + kWBits);
+  float* vred = (float*)(trunk_smem + kWVred);
   const int ngroups = (E + TNI - 1) / TNI;
+  const bool pl = lane < kActSpec && lane <= S;  // lanes that read a row's first words
   // once per launch: the LUT, both parities' tile counters, the previous step's bucket half
   if (tid < 256) ((uint4*)(trunk_smem + kWLut))[tid] = mbk::bits8_bf16((uint32_t)tid);
   for (int c = tid; c < 2 * S; c += kThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
@@ -1171,10 +1167,15 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   if (blockIdx.x == 0)  // the previous step's launch B is done with these
     for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
   mbk::lds_barrier();
-  uint32_t pre0 = 0u, pre1 = 0u;  // this wave's next-tile row words (lane < kActSpec)
-  // a layer's weight fragments are fetched at its start (no register prefetch one layer ahead
-  // as in act_trunk_kernel: that doubled the 72 fragment VGPRs and spilled; here the other
-  // waves' work covers one wave's L2 wait)
+  uint32_t pre0 = 0u, pre1 = 0u;  // this wave's rows (first words) for the current tile
+  if (a.code_list && (int)blockIdx.x < ngroups) {
+    const int en = blockIdx.x * TNI + wave * kWEnv;
+    pre0 = (en < E && pl) ? a.code_list[(size_t)en * a.list_stride + lane] : 0u;
+    pre1 = (en + 1 < E && pl) ? a.code_list[(size_t)(en + 1) * a.list_stride + lane] : 0u;
+  }
+  // conv layer l: its weight fragments are loaded at its start (a one-layer-ahead register
+  // prefetch as in act_trunk_kernel needs 72 more VGPRs and spills here); each MFMA waits only
+  // for its own fragment, so the loads stream behind the first pixel blocks' MFMAs
 #define ACT_WPHASE(l, CI, CO, RELU, MODE, WV_, IN, H_, W_, OUT)                           \
   do {                                                                                   \
     uint4 wc[kWFrag];                                                                    \
@@ -1182,6 +1183,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
     conv_lds<CI, CO, RELU, MODE, false, false, WV_>(IN, H_, W_, nw, 0, wc, TG<CI>::NCH * 64, \
                                                     t.b[l], OUT);                       \
     __builtin_amdgcn_wave_barrier();                                                     \
+    ACT_STAMP(4 + (l));                                                                  \
   } while (0)
   int k = 0;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x, ++k) {
@@ -1190,10 +1192,11 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
     int* np = (int*)(trunk_smem + kWNp) + par;
     uint32_t* lst = (uint32_t*)(trunk_smem + kWLst) + par * kWList;
     const int img0 = grp * TNI, nimg = min(TNI, E - img0);
-    const int e0 = wave * kWEnv;                 // this wave's first env within the tile
+    const int e0 = wave * kWEnv;                   // this wave's first env within the tile
     const int nw = max(0, min(kWEnv, nimg - e0));  // ... and how many it has
     uint32_t* ovf = (uint32_t*)(a.cellx + (size_t)img0 * S);  // list spill (this tile's rows)
     bool spilled = false;
+    uint4 wf[2][4];  // this wave's two W5 hidden blocks for the tile's FC
     if (nw > 0) {
       // stage-0 conv weights / bias first: their L2 latency hides behind the rows and decode
       Frag8 bw0[9];
@@ -1206,7 +1209,20 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) bias0[i] = a.b0[4 * g + i];
       ACT_STAMP(0);
-      // ---- codes of the wave's envs -> its LDS code rows; resources in registers
+      // ---- loads first: reward / done of the last env step (lane j: env j), the next tile's
+      // rows; then this tile's codes into the wave's LDS code rows
+      float rwv = 0.f;
+      uint8_t dnv = 0;
+      if (lane < nw) {
+        if (a.reward_dst) rwv = a.reward_src[img0 + e0 + lane];
+        if (a.done_dst) dnv = a.done_src[img0 + e0 + lane];
+      }
+      const uint32_t cur0 = pre0, cur1 = pre1;
+      if (a.code_list) {
+        const int en = img0 + gridDim.x * TNI + e0;
+        pre0 = (en < E && pl) ? a.code_list[(size_t)en * a.list_stride + lane] : 0u;
+        pre1 = (en + 1 < E && pl) ? a.code_list[(size_t)(en + 1) * a.list_stride + lane] : 0u;
+      }
       int res0 = 0, res1 = 0;  // (kWEnv = 2: named, so a rolled loop keeps them in registers)
 #pragma unroll 1
       for (int j = 0; j < nw; ++j) {
@@ -1215,8 +1231,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         if (a.code_list) {
           for (int c = lane * 4; c < S; c += 256) *(uint2*)(cs + c) = make_uint2(0u, 0u);
           const uint32_t* row = a.code_list + (size_t)(img0 + el) * a.list_stride;
-          const uint32_t w = k == 0 ? (lane < kActSpec && lane <= S ? row[lane] : 0u)
-                                    : (j ? pre1 : pre0);
+          const uint32_t w = j ? cur1 : cur0;
           const uint32_t w0 = (uint32_t)__shfl((int)w, 0, 64);
           const int n = min((int)(w0 & 0xFFFFu), S);
           (j ? res1 : res0) = (int)(w0 >> 16);
@@ -1230,10 +1245,6 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         } else {
           ((uint4*)cs)[lane & 31] = ((const uint4*)(a.codes + (size_t)(img0 + el) * S))[lane & 31];
           (j ? res1 : res0) = a.res[img0 + el];
-        }
-        if (lane == 0) {
-          if (a.reward_dst) a.reward_dst[img0 + el] = a.reward_src[img0 + el];
-          if (a.done_dst) a.done_dst[img0 + el] = a.done_src[img0 + el];
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -1314,18 +1325,15 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
           *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
         }
       }
+      if (lane < nw) {
+        if (a.reward_dst) a.reward_dst[img0 + e0 + lane] = rwv;
+        if (a.done_dst) a.done_dst[img0 + e0 + lane] = dnv;
+      }
       __builtin_amdgcn_wave_barrier();
       ACT_STAMP(2);
       // ---- stage-0 conv + pool of the wave's images into its X0 slice
       zero_halo<TG<16>::PIXB, true>(R1, nw, H0, W0);
       for (int j = 0; j < nw; ++j) act_conv0(lbits + j * S, lut, bw0, bias0, R1, j);
-      if (a.code_list) {  // the wave's next-tile rows, in flight during this tile's trunk
-        const int img0n = img0 + gridDim.x * TNI;
-        const bool pl = lane < kActSpec && lane <= S;
-        pre0 = (img0n + e0 < E && pl) ? a.code_list[(size_t)(img0n + e0) * a.list_stride + lane] : 0u;
-        pre1 = (img0n + e0 + 1 < E && pl)
-                   ? a.code_list[(size_t)(img0n + e0 + 1) * a.list_stride + lane] : 0u;
-      }
       __builtin_amdgcn_wave_barrier();
       zero_halo<TG<16>::PIXB, true>(R2, nw, H0, W0);  // U0 layout (decode scratch is dead)
       __builtin_amdgcn_wave_barrier();
@@ -1336,7 +1344,6 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         ACT_WPHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, 1, oR1, H0, W0, oR2);
         ACT_WPHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, 1, oR2, H0, W0, oR1);
       }
-      ACT_STAMP(4);
       ACT_WPHASE(4, 16, 32, false, OUT_STAGE, 1, oR1, H0, W0, oR2);
       pool_lds<32, false, true>((const bf16*)R2, H0, W0, nw, R1);
       zero_halo<TG<32>::PIXB, true>(R1, nw, H1, W1);
@@ -1347,7 +1354,6 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         ACT_WPHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 1, oR1, H1, W1, oR2);
         ACT_WPHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 1, oR2, H1, W1, oR1);
       }
-      ACT_STAMP(5);
       ACT_WPHASE(9, 32, 32, false, OUT_STAGE, 1, oR1, H1, W1, oR2);
       pool_lds<32, false, true>((const bf16*)R2, H1, W1, nw, R1);
       zero_halo<TG<32>::PIXB, true>(R1, nw, H2, W2);
@@ -1358,13 +1364,18 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         ACT_WPHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 2, oR1, H2, W2, oR2);
         ACT_WPHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 2, oR2, H2, W2, oR1);
       }
-      ACT_STAMP(6);
-      wave_fc(oR1, nw, img0 + e0, t);
-      ACT_STAMP(7);
+      ACT_STAMP(18);
     }
-    // ---- the tile's bucket reservation (one global atomic per active cell) and entries
+    // ---- tile end: W5 fragments in flight across the barrier
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const uint4* wrow = (const uint4*)(t.w5 + (size_t)((2 * wave + jj) * 16 + li) * (H2 * W2 * 32)) + g;
+#pragma unroll
+      for (int ks = 0; ks < H2 * W2; ++ks) wf[jj][ks] = wrow[ks * 4];
+    }
     if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // spill rows in L2 first
     mbk::lds_barrier();
+    ACT_STAMP(19);
     for (int c = tid; c < S; c += kThreads) {
       const int n = lcnt[c];
       if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
@@ -1374,7 +1385,9 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
       for (int c = tid; c < S; c += kThreads) lc2[c] = 0;
       if (tid == 0) ((int*)(trunk_smem + kWNp))[par ^ 1] = 0;
     }
+    tile_fc(nimg, img0, t, wf, vred);
     mbk::lds_barrier();
+    if (tid < nimg) a.t.v_out[img0 + tid] = mbk::crit_sum(vred + tid, 16, 16, t.bc[0]);
     const int npr = *np;
     for (int i = tid; i < npr; i += kThreads) {
       const uint32_t en = i < kWList ? lst[i]
@@ -1384,8 +1397,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
       const int el = (int)((en >> 12) & 0xFu), rank = (int)(en >> 16);
       a.bucket[(size_t)c * E + lcnt[c] + slot] = (img0 + el) | (rank << 16);
     }
-    if (tid == 0 && a.stamps && k == 0)  // the reservation's end (stamp 8, wave 0's clock)
-      a.stamps[(size_t)blockIdx.x * 64 * kActStamps + 8 * 64] = __builtin_amdgcn_s_memrealtime();
+    ACT_STAMP(20);
   }
 #undef ACT_WPHASE
 }

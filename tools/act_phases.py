@@ -19,10 +19,14 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# stamp intervals of wave 0's first tile (MBK_ACT_WAVE=1: its own 2 envs, then the tile's
-# bucket phase; MBK_ACT_WAVE=0: the phase-split kernel's workgroup-wide phases, last one empty)
-PHASES = ["P1 codes->LDS", "P2 decode", "P3 (buckets+) conv0", "stage 0 res", "stage 1",
-          "stage 2", "fc + critic", "tile buckets"]
+# stamp intervals of wave 0's first tile. MBK_ACT_WAVE=1 (default, act_trunk_w_kernel): its own
+# 2 envs through the trunk, then the tile-wide end (bucket reservation, FC + critic, entries);
+# MBK_ACT_WAVE=0 (act_trunk_kernel): the workgroup-wide phases (stamps 0-8)
+PHASES_PHASE = ["P1 codes->LDS", "P2 decode", "P3 buckets+conv0", "stage 0 res", "stage 1",
+                "stage 2", "fc + critic", "-"]
+PHASES_WAVE = (["rows + codes", "decode", "conv0 + pool + halos"]
+               + [f"conv {l}" + (" (+pool)" if l in (4, 9) else "") for l in range(14)]
+               + ["(trunk end)", "barrier 1 wait", "reserve + FC + barrier 2 + entries"])
 
 
 def main():
@@ -101,18 +105,20 @@ def main():
     print(f"launch A (decode + trunk + critic) {1e3 * ta / n:.1f} us, launch B (head + finale) "
           f"{1e3 * tb / n:.1f} us, rows in {'HBM' if a.device_rows else 'pinned host memory'}")
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    stamps = torch.zeros(ncu * 4 * 9 * 64, dtype=torch.int64, device=dev)
+    stamps = torch.zeros(ncu * 4 * 32 * 64, dtype=torch.int64, device=dev)
     nst = k.mbk_act_set_stamps(stamps.data_ptr())
     st.step = a.steps + 3
     N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk (stamped)")
     torch.cuda.synchronize()
     k.mbk_act_set_stamps(None)
+    wave = os.environ.get("MBK_ACT_WAVE", "1") != "0"
+    names = PHASES_WAVE if wave else PHASES_PHASE
     t = stamps.view(-1, nst, 64)[:, :, 0].cpu().double()
-    t = t[t[:, 0] > 0]
+    t = t[t[:, 0] > 0][:, :len(names) + 1]
     d = (t[:, 1:] - t[:, :-1]) * 10.0 / 1e3  # 100 MHz ticks -> us
     tot = float(d.sum(1).mean())
     print(f"first tile of {len(t)} workgroups: {tot:.1f} us")
-    for i, name in enumerate(PHASES):
+    for i, name in enumerate(names):
         print(f"  {name:18s} {float(d[:, i].mean()):7.2f} us  {float(d[:, i].mean()) / tot:6.1%}")
 
 

@@ -4,7 +4,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 tag=${1:-aw}
-timeout -k 10 300 python -u -m pytest tests/test_gpu_act.py -x -q --timeout 120 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_act.py tests/test_gpu_fc.py tests/test_gpu_engine.py -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/${tag}_act_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_act_tests.log; exit 1; }
 tail -2 gpurun_out/${tag}_act_tests.log
 for w in 1 0; do
