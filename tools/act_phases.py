@@ -113,7 +113,8 @@ def main():
     k.mbk_act_set_stamps(None)
     wave = os.environ.get("MBK_ACT_WAVE", "1") != "0"
     names = PHASES_WAVE if wave else PHASES_PHASE
-    t = stamps.view(-1, nst, 64)[:, :, 0].cpu().double()
+    nb = stamps.numel() // (nst * 64)
+    t = stamps[:nb * nst * 64].view(nb, nst, 64)[:, :, 0].cpu().double()
     t = t[t[:, 0] > 0][:, :len(names) + 1]
     d = (t[:, 1:] - t[:, :-1]) * 10.0 / 1e3  # 100 MHz ticks -> us
     tot = float(d.sum(1).mean())

@@ -122,6 +122,24 @@ def main():
             continue
         y0, u1, g = (ops[s_][k] for s_, k in zip(src, ("y0", "u1", "g")))
         print(f"  y0={src[0]:5s} u1={src[1]:5s} g={src[2]:5s}  rel {rel(dw(y0, u1, g, w1), want):.4f}")
+    # the mask flips: where, how big are u1 there, how much du do they gate?
+    du_ref = torch.nn.grad.conv2d_input(ops["ref"]["u1"].shape, w1, ops["ref"]["g"], padding=1)
+    ur = ops["ref"]["u1"]
+    for path in ("bf16", "hip"):
+        uo = ops[path]["u1"]
+        flip = (uo > 0) != (ur > 0)
+        nf = int(flip.sum())
+        imp = float(du_ref[flip].abs().sum() / du_ref.abs().sum())
+        print(f"{path}: {nf} mask flips of {flip.numel()}; share of |du| they gate {imp:.4f}")
+        if nf:
+            print(f"  |u1_ref| at flips: median {float(ur[flip].abs().median()):.3e} max "
+                  f"{float(ur[flip].abs().max()):.3e}; |u1_{path}| median "
+                  f"{float(uo[flip].abs().median()):.3e}; zeros in u1_{path} at flips "
+                  f"{int((uo[flip] == 0).sum())}; zeros overall {int((uo == 0).sum())} "
+                  f"(ref {int((ur == 0).sum())})")
+            print(f"  flips per channel {flip.sum((0, 2, 3)).tolist()}")
+            print(f"  flips per pixel {flip.sum((0, 1)).flatten().tolist()}")
+            print(f"  u1_ref > 0 at flips: {int((ur[flip] > 0).sum())}")
     # where in g: per pixel, and concentrated in few frames?
     dg = (ops["hip"]["g"] - ops["ref"]["g"]).flatten(1).norm(dim=1)
     gn = ops["ref"]["g"].flatten(1).norm(dim=1)
