@@ -723,6 +723,13 @@ struct ActTrunkArgs {
   float* reward_dst;
   uint8_t* done_dst;
   uint64_t* stamps;  // diagnostic phase stamps (null: off)
+  // fused head (act_trunk_w_kernel, fused != 0): the tile's sparse head at its end, so the
+  // policy step is ONE launch (no buckets, pending counters or granule rows in HBM)
+  const bf16* Wp;    // [S][80][256] bf16 packed head rows
+  const float* bp;   // [S][80]
+  uint64_t* rng;     // Philox (seed, step): rng[1] <- step + 1 (the graph path's counter)
+  uint64_t step;
+  int fused;
 };
 
 constexpr int kActS = 256;  // 16x16 maps: one map row = one 16-pixel MFMA block
@@ -1089,9 +1096,21 @@ constexpr int kWLut = 2 * kWRegion;                          // byte -> 8 bf16 t
 constexpr int kWCnt = kWLut + 256 * 16;                      // [2][256] pair counts per cell
 constexpr int kWNp = kWCnt + 2 * kActS * 4;                  // [2] list lengths (+ pad)
 constexpr int kWVred = kWNp + 16;                            // [16 blocks][16 images] critic
-constexpr int kWList = 380;                                  // list entries per parity in LDS
-constexpr int kWLst = kWVred + 16 * 16 * 4;                  // [2][kWList] packed pairs
+constexpr int kWCellU = kWVred + 16 * 16 * 4;                // fused head: cell -> unit [256] u16
+constexpr int kWCellL = kWCellU + kActS * 2;                 // unit -> cell [256] u8
+constexpr int kWMisc = kWCellL + kActS;                      // unit count, then [16] env n
+constexpr int kWList = 270;                                  // list entries per parity in LDS
+constexpr int kWLst = kWMisc + 80;                           // [2][kWList] packed pairs
 constexpr int kWSmem = kWLst + 2 * kWList * 4;
+// the fused head's tile-end scratch, in regions whose trunk data is dead by then: f rows,
+// unit rows and the per-wave logit tiles in R2, the per-env granules in R1 (after the FC)
+constexpr int kHNP = 80, kHKD = 256;                         // head.hip NP / KD
+constexpr int kWHf = kWRegion;                               // [16][256] bf16 features
+constexpr int kWHrows = kWHf + 16 * kHKD * 2;                // [<=256 units][16] u16 rows
+constexpr int kWHz = kWHrows + kActS * 16 * 2;               // [8 waves][16][81] f32
+constexpr int kWHgran = 0;                                   // [16 envs][256] u64 granules
+static_assert(kWHz + 8 * 16 * (kHNP + 1) * 4 <= 2 * kWRegion, "fused head scratch (R2)");
+static_assert(16 * kActS * 8 <= kWRegion, "fused head granules (R1)");
 static_assert(kWSmem <= 160 * 1024, "wave-owned acting tile exceeds the LDS");
 static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage footprints");
 // a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run)
@@ -1102,7 +1121,7 @@ static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
 // fragments, loaded before the barrier) for the tile's 16 images, whose X2 tiles sit in the
 // waves' R1 slices (image i: wave i / 2's slice, its image i % 2); critic partials -> vred
 __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
-                                        const uint4 wf[2][4], float* vred) {
+                                        const uint4 wf[2][4], float* vred, bool fused) {
   constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
@@ -1140,7 +1159,46 @@ __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
     for (int k = 0; k < 2; ++k)
       o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
              ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
-    if (valid) *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
+    if (valid) {
+      if (fused)  // the tile's head reads f from LDS
+        *(uint2*)(trunk_smem + kWHf + (li * kHKD + h0) * 2) = make_uint2(o[0], o[1]);
+      else
+        *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
+    }
+  }
+}
+
+// Z[16 pairs][80] of one fused-head unit (the tile's pairs of cell c, <= 16: one per env) into
+// the wave's LDS tile z: head.hip unit_z's MFMA operands and K order (bit-identical logits), with
+// the X rows read from the tile's LDS features
+__device__ __forceinline__ void tile_unit_z(const uint16_t* rows, int cnt, int c,
+                                            const bf16* __restrict__ Wp,
+                                            const float* __restrict__ bp, float (*z)[kHNP + 1]) {
+  const int lane = threadIdx.x & 63, G = lane >> 4, li = lane & 15;
+  const bool valid = li < cnt;
+  const int el = valid ? (rows[li] & 15) : 0;
+  const char* xrow = trunk_smem + kWHf + el * kHKD * 2 + G * 16;
+  const bf16* wc = Wp + (size_t)c * kHNP * kHKD;
+  f32x4 acc[5];
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < kHKD / 32; ++ks) {
+    Frag8 x;
+    x.u = valid ? *(const uint4*)(xrow + ks * 64) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      Frag8 w;
+      w.u = *((const uint4*)(wc + (size_t)(nb * 16 + li) * kHKD + ks * 32) + G);
+      acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.v, w.v, acc[nb], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int nb = 0; nb < 5; ++nb) {
+    const int col = nb * 16 + li;
+    const float bias = bp[c * kHNP + col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) z[4 * G + i][col] = acc[nb][i] + bias;
   }
 }
 
@@ -1164,8 +1222,17 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   if (tid < 256) ((uint4*)(trunk_smem + kWLut))[tid] = mbk::bits8_bf16((uint32_t)tid);
   for (int c = tid; c < 2 * S; c += kThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
   if (tid < 2) ((int*)(trunk_smem + kWNp))[tid] = 0;
-  if (blockIdx.x == 0)  // the previous step's launch B is done with these
+  const bool fused = a.fused != 0;
+  int* ncells = (int*)(trunk_smem + kWMisc);  // fused: distinct active cells of the tile
+  int* env_n = ncells + 1;                    // fused: active cells per env of the tile
+  uint16_t* cellunit = (uint16_t*)(trunk_smem + kWCellU);
+  uint8_t* celllist = (uint8_t*)(trunk_smem + kWCellL);
+  if (tid == 0) *ncells = 0;
+  if (fused) {
+    if (blockIdx.x == 0 && tid == 0) a.rng[1] = a.step + 1;  // the graph path's counter
+  } else if (blockIdx.x == 0) {  // the previous step's launch B is done with these
     for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
+  }
   mbk::lds_barrier();
   uint32_t pre0 = 0u, pre1 = 0u;  // this wave's rows (first words) for the current tile
   if (a.code_list && (int)blockIdx.x < ngroups) {
@@ -1282,8 +1349,14 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
           if (mk[3 * q] | mk[3 * q + 1] | mk[3 * q + 2]) {
             const int c = c0 + q;
             const int i = atomicAdd(np, 1);
-            const uint32_t en = (uint32_t)c | ((uint32_t)atomicAdd(&lcnt[c], 1) << 8) |
-                                ((uint32_t)el << 12) | ((uint32_t)kx << 16);
+            const int slot = atomicAdd(&lcnt[c], 1);
+            if (fused && slot == 0) {  // the tile's first pair of cell c opens its unit
+              const int ui = atomicAdd(ncells, 1);
+              cellunit[c] = (uint16_t)ui;
+              celllist[ui] = (uint8_t)c;
+            }
+            const uint32_t en = (uint32_t)c | ((uint32_t)slot << 8) | ((uint32_t)el << 12) |
+                                ((uint32_t)kx << 16);
             if (i < kWList) {
               lst[i] = en;
             } else {
@@ -1315,8 +1388,12 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         uint4* act4 = (uint4*)(a.action + (size_t)e * S * 7);
         for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = z4;
         if (lane == 0) {
-          a.pending[e] = n;
-          a.pending[E + e] = n;
+          if (fused) {
+            env_n[el] = n;
+          } else {
+            a.pending[e] = n;
+            a.pending[E + e] = n;
+          }
           if (n == 0) a.logp[e] = 0.f;
         }
         if (a.act_list) {
@@ -1373,31 +1450,131 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
 #pragma unroll
       for (int ks = 0; ks < H2 * W2; ++ks) wf[jj][ks] = wrow[ks * 4];
     }
-    if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // spill rows in L2 first
+    // spill rows in L2 first; fused: also this wave's mask rows (the head re-reads the active
+    // cells' masks from HBM, written by other waves of the tile)
+    if (spilled || (fused && nw > 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mbk::lds_barrier();
     ACT_STAMP(19);
-    for (int c = tid; c < S; c += kThreads) {
-      const int n = lcnt[c];
-      if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
+    if (!fused) {
+      for (int c = tid; c < S; c += kThreads) {
+        const int n = lcnt[c];
+        if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
+      }
     }
     {  // the other parity (the previous tile's, consumed before this barrier) for the next tile
       int* lc2 = (int*)(trunk_smem + kWCnt) + (par ^ 1) * S;
       for (int c = tid; c < S; c += kThreads) lc2[c] = 0;
       if (tid == 0) ((int*)(trunk_smem + kWNp))[par ^ 1] = 0;
     }
-    tile_fc(nimg, img0, t, wf, vred);
+    const int npr = *np;
+    uint16_t* urows = (uint16_t*)(trunk_smem + kWHrows);
+    if (fused) {  // each pair's (env, rank) into its unit's row slot
+      for (int i = tid; i < npr; i += kThreads) {
+        const uint32_t en = i < kWList ? lst[i]
+                                       : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+        const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
+        urows[cellunit[c] * 16 + slot] = (uint16_t)(((en >> 12) & 0xFu) | ((en >> 16) << 4));
+      }
+    }
+    tile_fc(nimg, img0, t, wf, vred, fused);
     mbk::lds_barrier();
     if (tid < nimg) a.t.v_out[img0 + tid] = mbk::crit_sum(vred + tid, 16, 16, t.bc[0]);
-    const int npr = *np;
-    for (int i = tid; i < npr; i += kThreads) {
-      const uint32_t en = i < kWList ? lst[i]
-                                     : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-      const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
-      const int el = (int)((en >> 12) & 0xFu), rank = (int)(en >> 16);
-      a.bucket[(size_t)c * E + lcnt[c] + slot] = (img0 + el) | (rank << 16);
+    if (!fused) {
+      for (int i = tid; i < npr; i += kThreads) {
+        const uint32_t en = i < kWList ? lst[i]
+                                       : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+        const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
+        const int el = (int)((en >> 12) & 0xFu), rank = (int)(en >> 16);
+        a.bucket[(size_t)c * E + lcnt[c] + slot] = (img0 + el) | (rank << 16);
+      }
+      ACT_STAMP(20);
+      continue;
     }
+    // ---- fused head: wave w samples units w, w + 8, ... (a unit = the tile's pairs of one
+    // cell, one per env), head_act_kernel's maths: unit_z logits, Philox draws keyed by
+    // (env * S + cell, step), cell_forward; each pair's {log-prob, cell | packed action << 16}
+    // granule goes to its env's rank slot in LDS
+    {
+      const int nu = *ncells;
+      float (*z)[kHNP + 1] = (float (*)[kHNP + 1])(trunk_smem + kWHz + wave * 16 * (kHNP + 1) * 4);
+      uint64_t* gran = (uint64_t*)(trunk_smem + kWHgran);
+      const uint64_t seed = a.rng[0], step = a.step;
+      for (int ui = wave; ui < nu; ui += NW) {
+        const int c = celllist[ui], cnt = lcnt[c];
+        const uint16_t* rows = urows + ui * 16;
+        tile_unit_z(rows, cnt, c, a.Wp, a.bp, z);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's logit tile is in LDS
+        __builtin_amdgcn_wave_barrier();
+        if (lane < cnt) {
+          const int el = rows[lane] & 15, rank = rows[lane] >> 4;
+          const size_t fc = (size_t)(img0 + el) * S + c;
+          uint32_t m[3];
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+            m[q] = __hip_atomic_load(a.mask + fc * 3 + q, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          uint8_t act[mbk::kComps];
+          float uu[mbk::kComps];
+          mbk::u32x4 ctr = {(uint32_t)fc, (uint32_t)(fc >> 32), (uint32_t)step,
+                            (uint32_t)(step >> 32)};
+          mbk::u32x4 q0 = mbk::philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+          ctr.y ^= 0x80000000u;
+          mbk::u32x4 q1 = mbk::philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
+          uu[0] = mbk::u01(q0.x); uu[1] = mbk::u01(q0.y); uu[2] = mbk::u01(q0.z);
+          uu[3] = mbk::u01(q0.w); uu[4] = mbk::u01(q1.x); uu[5] = mbk::u01(q1.y);
+          uu[6] = mbk::u01(q1.z);
+          float lp, ent;
+          mbk::cell_forward(&z[lane][0], m, act, true, uu, &lp, &ent);
+#pragma unroll
+          for (int q = 0; q < mbk::kComps; ++q) a.action[fc * mbk::kComps + q] = act[q];
+          gran[el * S + rank] =
+              (uint64_t)__float_as_uint(lp) |
+              ((uint64_t)((uint32_t)c | ((uint32_t)mbr::pack_env_action(act) << 16)) << 32);
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    mbk::lds_barrier();
+    // ---- per env of this wave: log-prob (row_sum_pack's lane-strided order) and its actions
+#pragma unroll 1
+    for (int j = 0; j < nw; ++j) {
+      const int el = e0 + j, fe = img0 + el, n = env_n[el];
+      if (n == 0) continue;  // decode wrote logp 0 and the empty action row
+      const uint64_t* row = (const uint64_t*)(trunk_smem + kWHgran) + el * S;
+      float sl = 0.f;
+      int nz = 0;
+      uint32_t* lrow = a.act_list ? a.act_list + (size_t)fe * a.list_stride : nullptr;
+      for (int k0 = 0; k0 < n; k0 += 64) {
+        const int kk = k0 + lane;
+        const uint64_t x = kk < n ? row[kk] : 0ull;
+        const uint32_t hi = (uint32_t)(x >> 32);
+        const int kn = min(64, n - k0);
+        for (int q = 0; q < kn; ++q) {
+          const uint32_t lo_q = (uint32_t)__shfl((int)(uint32_t)x, q, 64);
+          const uint32_t hi_q = (uint32_t)__shfl((int)hi, q, 64);
+          if ((int)(hi_q & 63u) == lane) sl += __uint_as_float(lo_q);
+        }
+        const uint32_t code = hi >> 16;
+        if (lrow) {
+          const uint64_t bal = __ballot(kk < n && code != 0u);
+          const int pos = nz + __popcll(bal & ((1ull << lane) - 1ull));
+          if (kk < n && code != 0u) lrow[1 + pos] = (hi & 0xFFFFu) | (code << 16);
+          nz += __popcll(bal);
+        } else if (kk < n) {
+          a.act16[(size_t)fe * S + (hi & 0xFFFFu)] = (uint16_t)code;
+        }
+      }
+      sl = mbk::wave_sum(sl);
+      if (lane == 0) {
+        a.logp[fe] = sl;
+        if (lrow) lrow[0] = (uint32_t)nz;
+      }
+    }
+    if (tid == 0) *ncells = 0;
     ACT_STAMP(20);
+    mbk::lds_barrier();  // the next tile's decode / conv0 reuse R1 / R2
   }
 #undef ACT_WPHASE
 }
@@ -1590,6 +1767,18 @@ static int act_wave() {  // MBK_ACT_WAVE=0: the phase-split kernel (A/B)
   return v;
 }
 
+// The policy step in ONE launch: the wave-owned kernel samples the sparse head at each tile's
+// end (MBK_ACT_FUSED=0: launch A stops at the trunk + buckets and head.hip launch B samples).
+// head.hip's mbk_act_head asks this and launches nothing when A did the head.
+extern "C" int mbk_act_fused() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("MBK_ACT_FUSED");
+    v = (e ? std::atoi(e) : 1) != 0 && act_wave() != 0;
+  }
+  return v;
+}
+
 extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
   if (!m || !s || m->E <= 0 || m->H != 16 || m->W != 16) return (int)hipErrorInvalidValue;
   if (!m->w0 || !m->b0 || !m->w5 || !m->b5 || !m->wc || !m->bc || !m->feat || !m->cellx ||
@@ -1659,6 +1848,14 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.reward_dst = s->reward_dst;
   a.done_dst = s->done_dst;
   a.stamps = g_act_stamps;
+  a.fused = wave_owned && mbk_act_fused();
+  if (a.fused) {
+    if (!m->Wp || !m->bp || !m->rng) return (int)hipErrorInvalidValue;
+    a.Wp = (const bf16*)m->Wp;
+    a.bp = m->bp;
+    a.rng = m->rng;
+    a.step = s->step;
+  }
   static int cus = 0;
   if (!cus) {
     int dev = 0;
