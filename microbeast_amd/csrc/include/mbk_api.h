@@ -100,6 +100,11 @@ int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
 // the two launches separately (mbk_act_step = A then B)
 int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
 int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
+// launch-A form (tests / A/B): wave-owned kernel (1) or phase-split (0), head fused into A (1)
+// or left to launch B (0); -1 = the MBK_ACT_WAVE / MBK_ACT_FUSED environment default.
+// Returns wave * 2 + fused; mbk_act_fused() says whether mbk_act_head launches nothing.
+int mbk_act_set_mode(int wave, int fused);
+int mbk_act_fused(void);
 
 #ifdef __cplusplus
 }

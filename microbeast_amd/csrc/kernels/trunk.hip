@@ -1758,25 +1758,32 @@ extern "C" int mbk_act_set_stamps(void* stamps) {
   return kActStamps;
 }
 
-static int act_wave() {  // MBK_ACT_WAVE=0: the phase-split kernel (A/B)
-  static int v = -1;
-  if (v < 0) {
+// launch-A form: MBK_ACT_WAVE=0 the phase-split act_trunk_kernel (A/B), else the wave-owned
+// kernel; MBK_ACT_FUSED=0 stops that one at the trunk + buckets and leaves the head to launch
+// B. mbk_act_set_mode overrides both (tests run every form in one process; -1 = environment).
+static int g_act_wave = -1, g_act_fused = -1;
+static int act_wave() {
+  if (g_act_wave < 0) {
     const char* e = std::getenv("MBK_ACT_WAVE");
-    v = e ? std::atoi(e) : 1;
+    g_act_wave = (e ? std::atoi(e) : 1) != 0;
   }
-  return v;
+  return g_act_wave;
 }
 
 // The policy step in ONE launch: the wave-owned kernel samples the sparse head at each tile's
-// end (MBK_ACT_FUSED=0: launch A stops at the trunk + buckets and head.hip launch B samples).
-// head.hip's mbk_act_head asks this and launches nothing when A did the head.
+// end. head.hip's mbk_act_head asks this and launches nothing when A did the head.
 extern "C" int mbk_act_fused() {
-  static int v = -1;
-  if (v < 0) {
+  if (g_act_fused < 0) {
     const char* e = std::getenv("MBK_ACT_FUSED");
-    v = (e ? std::atoi(e) : 1) != 0 && act_wave() != 0;
+    g_act_fused = (e ? std::atoi(e) : 1) != 0;
   }
-  return v;
+  return g_act_fused && act_wave();
+}
+
+extern "C" int mbk_act_set_mode(int wave, int fused) {
+  g_act_wave = wave < 0 ? -1 : wave != 0;
+  g_act_fused = fused < 0 ? -1 : fused != 0;
+  return act_wave() * 2 + mbk_act_fused();
 }
 
 extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {

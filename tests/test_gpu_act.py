@@ -49,10 +49,25 @@ def _model(cuda, seed):
     return m
 
 
+# launch-A forms (mbk_act_set_mode): wave-owned kernel with the head fused in (the default,
+# ONE launch per step), wave-owned + head launch B, phase-split kernel + head launch B
+MODES = {"fused": (1, 1), "wave+B": (1, 0), "phase+B": (0, 0)}
+
+
+@pytest.fixture(params=list(MODES))
+def act_mode(request, cuda):
+    k = N.kernels()
+    got = k.mbk_act_set_mode(*MODES[request.param])
+    assert got == MODES[request.param][0] * 2 + MODES[request.param][1]
+    yield request.param
+    k.mbk_act_set_mode(-1, -1)
+
+
 @pytest.mark.parametrize("E,sparse", [(96, False), (520, False), (200, True)])
-def test_fused_act_step_bit_identical(cuda, E, sparse):
+def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
     """sparse: the PCIe-light form the engine uses (occupied-cell code rows in, non-noop action
-    rows out) must give the same step as the dense codes / dense packed actions."""
+    rows out) must give the same step as the dense codes / dense packed actions. Every launch-A
+    form (act_mode) gives the same bits."""
     from microbeast_amd.ops.act import ActWorkspace, code_lists, dense_actions
     from microbeast_amd.runtime.gpu_actors import graph_policy_step, make_io
 
@@ -110,7 +125,8 @@ def test_fused_act_step_bit_identical(cuda, E, sparse):
         assert torch.equal(rdst, reward) and torch.equal(ddst, done)
         # between steps the previous step's bucket counters are back at zero (double buffer)
         par = (7 + i) % 2  # this step's Philox step is 7 + i
-        assert int(ws.bucket_cnt[par * 256:(par + 1) * 256].abs().sum()) > 0
+        fused = act_mode == "fused"  # (one launch: no bucket counters at all)
+        assert (int(ws.bucket_cnt[par * 256:(par + 1) * 256].abs().sum()) > 0) != fused
         if i > 0:
             assert int(ws.bucket_cnt[(1 - par) * 256:(2 - par) * 256].abs().sum()) == 0
         assert int(ws.pending[:E].abs().sum()) == 0

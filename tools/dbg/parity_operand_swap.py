@@ -140,6 +140,25 @@ def main():
             print(f"  flips per channel {flip.sum((0, 2, 3)).tolist()}")
             print(f"  flips per pixel {flip.sum((0, 1)).flatten().tolist()}")
             print(f"  u1_ref > 0 at flips: {int((ur[flip] > 0).sum())}")
+    # is u1_hip the conv of ITS OWN input? emulate conv0(relu(y0_hip)) in fp64 with the
+    # bf16-rounded weights and fp32 bias, then round to bf16 like the kernel's epilogue
+    c0 = ref.network[2].res_block1.conv0
+    w0b = c0.weight.detach().bfloat16().double()
+    emu = F.conv2d(F.relu(ops["hip"]["y0"]), w0b, c0.bias.detach().double(), padding=1)
+    emu_b = emu.float().bfloat16().double()
+    print(f"u1_hip vs fp64 emulation on its own input: rel {rel(ops['hip']['u1'], emu):.2e}, "
+          f"bf16-rounded emu equal {float((emu_b == ops['hip']['u1']).double().mean()):.5f}, "
+          f"sign flips vs emu {int(((emu > 0) != (ops['hip']['u1'] > 0)).sum())}")
+    for path in ("bf16", "hip"):
+        d = ops[path]["u1"] - ur
+        print(f"{path}: per-channel mean(u1 - u1_ref) x1e5 "
+              f"{[round(float(v) * 1e5, 2) for v in d.mean((0, 2, 3))]}")
+        print(f"{path}: per-channel std(u1 - u1_ref) x1e5 "
+              f"{[round(float(v) * 1e5, 2) for v in d.std((0, 2, 3))]}")
+    print(f"|du_ref| per channel (mean x1e6): "
+          f"{[round(float(v) * 1e6, 2) for v in du_ref.abs().mean((0, 2, 3))]}")
+    print(f"|u1_ref| per channel (median x1e3): "
+          f"{[round(float(v) * 1e3, 3) for v in ur.abs().median(3)[0].median(2)[0].median(0)[0]]}")
     # where in g: per pixel, and concentrated in few frames?
     dg = (ops["hip"]["g"] - ops["ref"]["g"]).flatten(1).norm(dim=1)
     gn = ops["ref"]["g"].flatten(1).norm(dim=1)
