@@ -79,7 +79,9 @@ __device__ __forceinline__ void zero_halo(char* t, int nimg, int H, int W) {
   constexpr int qn = PIXB / U;
   const int tot = nimg * per * qn;
   const float inv_per = 1.f / (float)per;
-  for (int e = WV ? (int)(threadIdx.x & 63) : (int)threadIdx.x; e < tot; e += WV ? 64 : kThreads) {
+  int e0 = WV ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  if (WV) asm volatile("" : "+v"(e0));  // opaque: not hoisted out of the acting tile loop
+  for (int e = e0; e < tot; e += WV ? 64 : kThreads) {
     const int r = e / qn, q = e - r * qn;  // qn is a compile-time constant
     const int im = (int)(((float)r + 0.5f) * inv_per), k = r - im * per;
     int py, px;
@@ -335,6 +337,107 @@ __device__ __forceinline__ void conv_lds(int in, int H, int W, int nimg, int lw_
   }
 }
 
+// One wave's conv over all of its own pixel blocks at once (the wave-owned acting tile): the
+// K-chunk loop is outside and the NBLK blocks (all the wave's pixels: NBLK * 16 >= M) inside,
+// so every chunk's weight fragment feeds NBLK independent accumulator chains and its LDS reads
+// issue together -- conv_lds WV = 1 ran two chains per iteration and paid the LDS latency, the
+// MFMA dependency and the epilogue once per block pair. Same taps, K order and epilogue maths
+// per output pixel as conv_lds (bit-identical). Pixel rows m >= M compute on pixel 0 and are not
+// stored.
+template <int CIN, int COUT, bool RELU, int MODE, int NBLK, int NPASS = 1>
+__device__ __forceinline__ void conv_w(int in, int H, int W, int M, const uint4* wreg,
+                                       const float* __restrict__ bias, int out) {
+  // NPASS passes of NBLK blocks (pass p: blocks p * NBLK ..): bounds the live accumulators
+#pragma unroll 1
+  for (int pass = 0; pass < NPASS; ++pass) {
+  const int jb = pass * NBLK;
+  constexpr int NCH = TG<CIN>::NCH, NB = COUT / 16;
+  constexpr int PI = TG<CIN>::PIXB, PO = TG<COUT>::PIXB;
+  // an opaque lane index: every address below derives from it, so none of them is hoisted out
+  // of the tile loop (LICM kept all phases' pixel offsets live across the whole tile: spills)
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int g = lane >> 4, li = lane & 15;
+  const int Hp = H + 2, Wp = W + 2, HW = H * W;
+  const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
+  Frag8 bw[NCH][NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) bw[c][nb].u = wreg[c * 2 + nb];
+  typedef const __attribute__((address_space(1))) f32x4* GF4;
+  float bv[NB][4];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const f32x4 b4 = ((GF4)bias)[(nb * 16 + 4 * g) / 4];
+    bv[nb][0] = b4[0]; bv[nb][1] = b4[1]; bv[nb][2] = b4[2]; bv[nb][3] = b4[3];
+  }
+  int base[NBLK];
+#pragma unroll
+  for (int j = 0; j < NBLK; ++j) {
+    const int m = (jb + j) * 16 + li;
+    const int mm = m < M ? m : 0;
+    const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+    base[j] = in + ((im * Hp + y) * Wp + x) * PI;
+  }
+  f32x4 acc[NBLK][NB];
+#pragma unroll
+  for (int j = 0; j < NBLK; ++j)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[j][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    int tap, ch0;
+    if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
+    else { tap = c; ch0 = 8 * g; }
+    const int tapc = tap < 9 ? tap : 8;
+    const int toff = ((tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2;
+#pragma unroll
+    for (int j = 0; j < NBLK; ++j) {
+      Frag8 a;
+      a.u = *(const uint4*)(trunk_smem + base[j] + toff);
+      if constexpr (RELU)
+        a.u = make_uint4(relu2(a.u.x), relu2(a.u.y), relu2(a.u.z), relu2(a.u.w));
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        acc[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, a.v, acc[j][nb], 0, 0, 0);
+    }
+    // keep the scheduler from hoisting every chunk's fragment reads up front (NBLK x NCH
+    // uint4 live: spills); one chunk's reads in flight ahead of its MFMAs is enough ILP
+    __builtin_amdgcn_sched_barrier(0);
+  }
+#pragma unroll
+  for (int j = 0; j < NBLK; ++j) {
+    const int m = (jb + j) * 16 + li;
+    if (m >= M) continue;
+    const int im = (int)(((float)m + 0.5f) * inv_hw), r = m - im * HW;
+    const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
+    const int pix = (im * Hp + y + 1) * Wp + x + 1;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co0 = nb * 16 + 4 * g;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = acc[j][nb][i] + bv[nb][i];
+      if constexpr (MODE == OUT_STAGE) {
+        *(uint2*)(trunk_smem + out + (m * COUT + co0) * 2) =
+            make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+      } else {
+        char* p = trunk_smem + out + (pix * PO + co0 * 2);
+        if constexpr (MODE == OUT_TILE_ADD) {
+          const uint2 ad = *(const uint2*)p;
+          v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
+        }
+        uint2 o = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if constexpr (MODE == OUT_TILE_RELU) o = make_uint2(relu2(o.x), relu2(o.y));
+        *(uint2*)p = o;
+      }
+    }
+  }
+  }
+}
+
 // max_pool2d(3, 2, 1) of staging [nimg][H][W][C] into the interior of a halo'd tile (F8: and
 // fp8(relu(.)) into the fp8 tile out8, the next residual block's conv input)
 template <int C, bool F8 = false, bool WV = false>
@@ -344,7 +447,9 @@ __device__ __forceinline__ void pool_lds(const bf16* stg, int H, int W, int nimg
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1, HWo = Ho * Wo;
   const int tot = nimg * HWo * C4;
   const float inv_hwo = 1.f / (float)HWo, inv_wo = 1.f / (float)Wo;
-  for (int e = WV ? (int)(threadIdx.x & 63) : (int)threadIdx.x; e < tot; e += WV ? 64 : kThreads) {
+  int e0 = WV ? (int)(threadIdx.x & 63) : (int)threadIdx.x;
+  if (WV) asm volatile("" : "+v"(e0));  // opaque: not hoisted out of the acting tile loop
+  for (int e = e0; e < tot; e += WV ? 64 : kThreads) {
     const int c4 = e % C4, p = e / C4;  // C4: compile-time power of two
     const int im = (int)(((float)p + 0.5f) * inv_hwo), r = p - im * HWo;
     const int oy = (int)(((float)r + 0.5f) * inv_wo), ox = r - oy * Wo;
@@ -763,7 +868,9 @@ __device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* 
                                           const Frag8 bw[9], const float bias[4], char* x0,
                                           int im) {
   constexpr int H0 = 8, W0 = 8, PX = TG<16>::PIXB;
-  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // opaque: no address hoisted out of the caller's tile loop
+  const int g = lane >> 4, li = lane & 15;
   const int sh = 8 * g;
   struct R3 {
     uint32_t l, c, h;
@@ -1123,7 +1230,9 @@ static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
 __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
                                         const uint4 wf[2][4], float* vred, bool fused) {
   constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // opaque: no address hoisted out of the tile loop
+  const int wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
   const bool valid = li < nimg;
   const int x2 = (li >> 1) * kWSlice + (li & 1) * (H2 + 2) * (W2 + 2) * PX;
@@ -1174,7 +1283,9 @@ __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
 __device__ __forceinline__ void tile_unit_z(const uint16_t* rows, int cnt, int c,
                                             const bf16* __restrict__ Wp,
                                             const float* __restrict__ bp, float (*z)[kHNP + 1]) {
-  const int lane = threadIdx.x & 63, G = lane >> 4, li = lane & 15;
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));  // opaque: no address hoisted out of the tile loop
+  const int G = lane >> 4, li = lane & 15;
   const bool valid = li < cnt;
   const int el = valid ? (rows[li] & 15) : 0;
   const char* xrow = trunk_smem + kWHf + el * kHKD * 2 + G * 16;
@@ -1243,12 +1354,12 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   // conv layer l: its weight fragments are loaded at its start (a one-layer-ahead register
   // prefetch as in act_trunk_kernel needs 72 more VGPRs and spills here); each MFMA waits only
   // for its own fragment, so the loads stream behind the first pixel blocks' MFMAs
-#define ACT_WPHASE(l, CI, CO, RELU, MODE, WV_, IN, H_, W_, OUT)                           \
+#define ACT_WPHASE(l, CI, CO, RELU, MODE, NBLK, IN, H_, W_, OUT)                          \
   do {                                                                                   \
     uint4 wc[kWFrag];                                                                    \
     wfetch(t.w[l], CI, CO, wc);                                                          \
-    conv_lds<CI, CO, RELU, MODE, false, false, WV_>(IN, H_, W_, nw, 0, wc, TG<CI>::NCH * 64, \
-                                                    t.b[l], OUT);                       \
+    conv_w<CI, CO, RELU, MODE, (NBLK) < 4 ? (NBLK) : 4, (NBLK) < 4 ? 1 : (NBLK) / 4>(     \
+        IN, H_, W_, nw * (H_) * (W_), wc, t.b[l], OUT);                                  \
     __builtin_amdgcn_wave_barrier();                                                     \
     ACT_STAMP(4 + (l));                                                                  \
   } while (0)
@@ -1418,28 +1529,28 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
       // ---- stage 0 residual blocks, stages 1 and 2 on the wave's own images
 #pragma unroll 1
       for (int rb = 0; rb < 2; ++rb) {
-        ACT_WPHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, 1, oR1, H0, W0, oR2);
-        ACT_WPHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, 1, oR2, H0, W0, oR1);
+        ACT_WPHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, 8, oR1, H0, W0, oR2);
+        ACT_WPHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, 8, oR2, H0, W0, oR1);
       }
-      ACT_WPHASE(4, 16, 32, false, OUT_STAGE, 1, oR1, H0, W0, oR2);
+      ACT_WPHASE(4, 16, 32, false, OUT_STAGE, 8, oR1, H0, W0, oR2);
       pool_lds<32, false, true>((const bf16*)R2, H0, W0, nw, R1);
       zero_halo<TG<32>::PIXB, true>(R1, nw, H1, W1);
       zero_halo<TG<32>::PIXB, true>(R2, nw, H1, W1);
       __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
       for (int rb = 0; rb < 2; ++rb) {
-        ACT_WPHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 1, oR1, H1, W1, oR2);
-        ACT_WPHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 1, oR2, H1, W1, oR1);
+        ACT_WPHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 2, oR1, H1, W1, oR2);
+        ACT_WPHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 2, oR2, H1, W1, oR1);
       }
-      ACT_WPHASE(9, 32, 32, false, OUT_STAGE, 1, oR1, H1, W1, oR2);
+      ACT_WPHASE(9, 32, 32, false, OUT_STAGE, 2, oR1, H1, W1, oR2);
       pool_lds<32, false, true>((const bf16*)R2, H1, W1, nw, R1);
       zero_halo<TG<32>::PIXB, true>(R1, nw, H2, W2);
       zero_halo<TG<32>::PIXB, true>(R2, nw, H2, W2);
       __builtin_amdgcn_wave_barrier();
 #pragma unroll 1
       for (int rb = 0; rb < 2; ++rb) {
-        ACT_WPHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 2, oR1, H2, W2, oR2);
-        ACT_WPHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 2, oR2, H2, W2, oR1);
+        ACT_WPHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, 1, oR1, H2, W2, oR2);
+        ACT_WPHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, 1, oR2, H2, W2, oR1);
       }
       ACT_STAMP(18);
     }

@@ -146,6 +146,16 @@ def main():
     w0b = c0.weight.detach().bfloat16().double()
     emu = F.conv2d(F.relu(ops["hip"]["y0"]), w0b, c0.bias.detach().double(), padding=1)
     emu_b = emu.float().bfloat16().double()
+    emu_r = F.conv2d(F.relu(ops["ref"]["y0"]), w0b, c0.bias.detach().double(), padding=1)
+    emu_b16 = F.conv2d(F.relu(ops["bf16"]["y0"]), w0b, c0.bias.detach().double(), padding=1)
+    print(f"sanity: u1_ref vs emulation on y0_ref {rel(ur, emu_r):.2e}; u1_bf16 vs emulation on "
+          f"y0_bf16 {rel(ops['bf16']['u1'], emu_b16):.2e}; emulation(y0_hip) vs u1_ref "
+          f"{rel(emu, ur):.2e}")
+    # per frame: is the mismatch in a few frames (e.g. rows from another frame)?
+    fe = (ops["hip"]["u1"] - emu).flatten(1).norm(dim=1) / (emu.flatten(1).norm(dim=1) + 1e-30)
+    top = torch.argsort(fe, descending=True)[:8]
+    print("frames with the largest u1_hip vs own-input error:",
+          [(int(f), round(float(fe[f]), 4)) for f in top], "median", float(fe.median()))
     print(f"u1_hip vs fp64 emulation on its own input: rel {rel(ops['hip']['u1'], emu):.2e}, "
           f"bf16-rounded emu equal {float((emu_b == ops['hip']['u1']).double().mean()):.5f}, "
           f"sign flips vs emu {int(((emu > 0) != (ops['hip']['u1'] > 0)).sum())}")
