@@ -9,10 +9,14 @@ weights on the same rollout batch (real GPU-engine rollouts, off-policy by one u
 Compared: the 5 losses, every parameter's gradient, and the post-Adam parameters.
 The gradient tolerance is the bf16 noise floor measured on the same update: the PyTorch
 path run on the GPU under bf16 autocast (MIOpen / hipBLASLt, a different implementation)
-against the same fp32 oracle; the HIP path must stay within 3x of that floor (or 3 %).
+against the same fp32 oracle, and for the residual blocks' conv0 layers the spread that
+rounding-level flips of their relu gate cause (their weight gradients are sums with heavy
+cancellation: tests/test_relu_flip_conditioning.py); the HIP path must stay within 3x of that
+floor (or 3 %). No layer has an escape clause.
 (Reference update: libs/utils.py:234-335 with SURVEY §8 D1-D4 fixed.)"""
 import copy
 
+import numpy as np
 import pytest
 import torch
 
@@ -20,9 +24,51 @@ from helpers import engine_batches
 
 pytestmark = pytest.mark.gpu
 
-# the one layer whose gradient may pass on direction + norm instead of the noise-floor bound
-# (bf16 vs fp32 sign flips of its relu gate on 2x2 maps, see the comment in the test)
-_TIE_LAYER = "network.2.res_block1.conv0."
+
+
+def _gate_hooks(model):
+    """Capture every residual block's conv0 operands in the fp32 oracle: block input x, conv0
+    output u (the relu gate of its gradient), block-output gradient g, conv1's pre-update
+    weight."""
+    caps = {}
+    for si in range(len(model.channels)):
+        for bi in (0, 1):
+            blk = getattr(model.network[si], f"res_block{bi}")
+            c = caps.setdefault(f"network.{si}.res_block{bi}.conv0.", {})
+            c["w1"] = blk.conv1.weight.detach().double().clone()
+            blk.register_forward_pre_hook(lambda m, i, c=c: c.__setitem__("x", i[0].detach()))
+            blk.conv0.register_forward_hook(lambda m, i, o, c=c: c.__setitem__("u", o.detach()))
+            def out_hook(m, i, o, c=c):  # (a forward hook's return value replaces the output)
+                o.register_hook(lambda g, c=c: c.__setitem__("g", g.detach()))
+            blk.register_forward_hook(out_hook)
+    return caps
+
+
+def _gate_flip_floor(c, w0, u_bf, draws=8):
+    """rel change of conv0's (weight, bias) gradient when its relu gate [u > 0] is recomputed
+    from u plus noise of the size an independent bf16 implementation's u actually deviates
+    from fp32 on this update (per channel: std of torch-bf16's u - u_ref, u_bf). A flip of a few
+    near-zero gates moves the 2x2-stage gradients by percents
+    (tests/test_relu_flip_conditioning.py), which one torch-bf16 sample need not show."""
+    import torch.nn.functional as F
+    x, u, g = (c[k].double() for k in ("x", "u", "g"))
+    w1 = c["w1"]
+    rx = F.relu(x)
+    du0 = torch.nn.grad.conv2d_input(u.shape, w1, g, padding=1)
+
+    def grads(uu):
+        du = du0 * (uu > 0)
+        return (torch.nn.grad.conv2d_weight(rx, tuple(w0.shape), du, padding=1),
+                du.sum((0, 2, 3)))
+    ref_w, ref_b = grads(u)
+    sig = (u_bf.double()[:u.shape[0]] - u).std(dim=(0, 2, 3), keepdim=True).expand_as(u)
+    gen = torch.Generator().manual_seed(1)
+    rw, rb = [], []
+    for _ in range(draws):
+        gw, gb = grads(u + torch.randn(u.shape, generator=gen, dtype=torch.float64) * sig)
+        rw.append(float((gw - ref_w).norm() / (ref_w.norm() + 1e-30)))
+        rb.append(float((gb - ref_b).norm() / (ref_b.norm() + 1e-30)))
+    return float(np.median(rw)), float(np.median(rb))
 
 
 @pytest.mark.parametrize("S", [8, 16])
@@ -49,6 +95,14 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
     bf_model = copy.deepcopy(base)
     bf_model.hip_kernels = False  # torch ops under bf16 autocast on the GPU
     hp = LearnerHParams()
+    caps = _gate_hooks(ref_model)
+    w0s = {n: p.detach().clone() for n, p in ref_model.named_parameters() if n.endswith("conv0.weight")}
+    u_bf = {}  # torch-bf16 conv0 outputs: the deviation size a bf16 implementation has
+    for si in range(len(bf_model.channels)):
+        for bi in (0, 1):
+            cv = getattr(bf_model.network[si], f"res_block{bi}").conv0
+            cv.register_forward_hook(lambda m, i, o, k=f"network.{si}.res_block{bi}.conv0.":
+                                     u_bf.__setitem__(k, o.detach().float().cpu()))
     Lh = Learner(hip_model, hp, cuda)
     Lr = Learner(ref_model, hp, torch.device("cpu"))
     Lb = Learner(bf_model, hp, cuda)
@@ -60,6 +114,10 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
     gb = Lb.flat.grad.cpu()
     print(f"losses hip {lh.tolist()}\nlosses ref {lr.tolist()}")
     gh, gr = Lh.flat.grad.cpu(), Lr.flat.grad
+    gate = {}  # residual conv0 layers: the relu-gate-flip floor of their gradient
+    for pre, c in caps.items():
+        fw, fb = _gate_flip_floor(c, w0s[pre + "weight"], u_bf[pre])
+        gate[pre + "weight"], gate[pre + "bias"] = fw, fb
     rows, bad = [], []
     for name, o, n, _ in Lr.flat.slices:
         a, b = gh[o:o + n], gr[o:o + n]
@@ -70,26 +128,18 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
                 bad.append(name)
             continue
         rel = float((a - b).norm()) / nb
-        floor = float((gb[o:o + n] - b).norm()) / nb
+        # the bf16 floor of this layer: an independent bf16 implementation (torch under
+        # autocast) on the same update, and for residual conv0 layers the spread a rounding-level
+        # flip of their relu gate causes (_gate_flip_floor); the HIP path stays within 3x of it
+        floor = max(float((gb[o:o + n] - b).norm()) / nb, gate.get(name, 0.0))
         cos = float(torch.dot(a, b)) / (float(a.norm()) * nb + 1e-30)
         rows.append((name, rel, floor, cos))
-        # cos bound consistent with the rel bound (rel ~ sqrt(2 (1 - cos)) for small errors).
-        # Second way to pass, for the named layer ONLY (_TIE_LAYER): direction within cos 0.995
-        # of fp32 and norm within 5 %. Needed by the stage-2 block-1
-        # conv0 on 2x2 maps: its du is gated by [u1 > 0] and 0.24 % of u1's signs differ
-        # between bf16 and fp32 (u1 rel 0.4 %, trunk-output grad rel 3.3 %), which puts its
-        # rel at 0.08-0.09 vs a bf16-torch floor of 0.0125 while cos stays 0.996 (probe:
-        # tools/dbg/stage2_grad_probe.py; the dgrad + mask kernel itself matches fp32 to 1.7e-3
-        # on the same operands, tools/dbg/dgrad_2x2_check.py). With the microRTS unit timings
-        # (round 3 env rules) the S = 16 batch of this test puts that layer at cos 0.9947 / rel
-        # 0.103, deterministically (same rollouts every run), hence the 0.99 bound.
-        ok = rel < max(3.0 * floor, 3e-2) and cos > 1.0 - 0.5 * max(3.0 * floor, 3e-2) ** 2
-        ratio = float(a.norm()) / nb
-        tie_ok = name.startswith(_TIE_LAYER) and cos > 0.99 and abs(ratio - 1.0) < 0.05
-        if not (ok or tie_ok):
+        tol = max(3.0 * floor, 3e-2)
+        ok = rel < tol and cos > 1.0 - 0.5 * tol ** 2  # (rel ~ sqrt(2 (1 - cos)))
+        if not ok:
             bad.append(name)
     for r in rows:  # full table on failure (pytest -s shows it always)
-        print(f"{r[0]:40s} rel {r[1]:.3e}  torch-bf16 floor {r[2]:.3e}  cos {r[3]:.5f}")
+        print(f"{r[0]:40s} rel {r[1]:.3e}  bf16 floor {r[2]:.3e}  cos {r[3]:.5f}")
     # losses: pg, value, entropy, total, mean rho
     torch.testing.assert_close(lh, lr, rtol=2e-2, atol=2e-3)
     assert not bad, f"gradients outside the bf16 noise floor: {bad}"
