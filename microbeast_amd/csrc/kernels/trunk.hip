@@ -386,25 +386,37 @@ __device__ __forceinline__ void conv_w(int in, int H, int W, int M, const uint4*
   for (int j = 0; j < NBLK; ++j)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[j][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
+  // chunk c's LDS byte offset (tap, 8-channel group of this lane)
+  auto toff = [&](int c) {
     int tap, ch0;
     if (CIN == 16) { tap = 2 * c + (g >> 1); ch0 = 8 * (g & 1); }
     else { tap = c; ch0 = 8 * g; }
     const int tapc = tap < 9 ? tap : 8;
-    const int toff = ((tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2;
+    return ((tapc / 3) * Wp + (tapc % 3)) * PI + ch0 * 2;
+  };
+  // software pipeline: chunk c+1's NBLK fragment reads are issued before chunk c's MFMAs, so the
+  // LDS latency hides behind NBLK x NB MFMAs instead of stalling every block
+  Frag8 fr[2][NBLK];
+#pragma unroll
+  for (int j = 0; j < NBLK; ++j) fr[0][j].u = *(const uint4*)(trunk_smem + base[j] + toff(0));
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    if (c + 1 < NCH) {
+      const int to = toff(c + 1);
+#pragma unroll
+      for (int j = 0; j < NBLK; ++j)
+        fr[(c + 1) & 1][j].u = *(const uint4*)(trunk_smem + base[j] + to);
+    }
 #pragma unroll
     for (int j = 0; j < NBLK; ++j) {
-      Frag8 a;
-      a.u = *(const uint4*)(trunk_smem + base[j] + toff);
+      Frag8 a = fr[c & 1][j];
       if constexpr (RELU)
         a.u = make_uint4(relu2(a.u.x), relu2(a.u.y), relu2(a.u.z), relu2(a.u.w));
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
         acc[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[c][nb].v, a.v, acc[j][nb], 0, 0, 0);
     }
-    // keep the scheduler from hoisting every chunk's fragment reads up front (NBLK x NCH
-    // uint4 live: spills); one chunk's reads in flight ahead of its MFMAs is enough ILP
+    // (no reads hoisted further: two chunks' fragments in flight at most)
     __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
