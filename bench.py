@@ -247,6 +247,12 @@ def main(argv=None):
             "frames_stepped_per_s": round((st1["frames"] - st0["frames"]) / el, 1),
             "gpu_phase_ms": round(1e3 * (st1["gpu_phase_s"] - st0["gpu_phase_s"]) / steps_done, 3),
             "env_phase_ms": round(1e3 * (st1["env_phase_s"] - st0["env_phase_s"]) / steps_done, 3)}
+    nf = st1.get("act_fused_steps", 0) - st0.get("act_fused_steps", 0)
+    nb = st1.get("act_b_steps", 0) - st0.get("act_b_steps", 0)
+    if nf + nb:  # the fused acting step's per-step head form (engine: active-cell threshold)
+        mine["act_head_in_A_frac"] = round(nf / (nf + nb), 3)
+        mine["active_cells_per_env"] = round(
+            (st1["act_active_cells"] - st0["act_active_cells"]) / ((nf + nb) * rt.E), 3)
     ranks = D.gather_objects(mine, info)
     cpu_bound = [r["rank"] for r in ranks if r["env_worker_busy_frac"] >= CPU_BOUND_BUSY]
     if cpu_bound and info.is_main:

@@ -94,6 +94,8 @@ typedef struct {
   float* reward_dst;
   uint8_t* done_dst;
   uint64_t step;           // Philox step of this policy step (the lane's step count)
+  int head_form;           // 0 = the process default (mbk_act_set_mode / MBK_ACT_FUSED),
+                           // 1 = head sampled inside launch A, 2 = head in launch B
 } MbkActStep;
 
 int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
@@ -105,6 +107,8 @@ int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
 // Returns wave * 2 + fused; mbk_act_fused() says whether mbk_act_head launches nothing.
 int mbk_act_set_mode(int wave, int fused);
 int mbk_act_fused(void);
+// the form this step runs (head_form resolved against the default; 0 = launch B samples)
+int mbk_act_step_fused(const MbkActStep* s);
 
 #ifdef __cplusplus
 }

@@ -1328,11 +1328,11 @@ extern "C" int mbk_head_pack(const float* W, const float* b, int S, void* Wp, fl
 }
 
 // ------------------------------------------------------------------ fused acting step, launch B
-extern "C" int mbk_act_fused();  // trunk.hip: launch A sampled the head itself
+extern "C" int mbk_act_step_fused(const MbkActStep* s);  // trunk.hip: A sampled the head
 
 extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
   if (!m || !s || m->E <= 0) return (int)hipErrorInvalidValue;
-  if (mbk_act_fused()) return 0;
+  if (mbk_act_step_fused(s)) return 0;
   const int S = m->H * m->W;
   if (S < 1 || S > kMaxUnitCells - 1 || (S & 3)) return (int)hipErrorInvalidValue;
   if (!m->feat || !m->Wp || !m->bp || !m->rng || !m->bucket || !m->bucket_cnt || !m->cellx ||

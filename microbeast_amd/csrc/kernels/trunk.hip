@@ -1351,9 +1351,10 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   uint16_t* cellunit = (uint16_t*)(trunk_smem + kWCellU);
   uint8_t* celllist = (uint8_t*)(trunk_smem + kWCellL);
   if (tid == 0) *ncells = 0;
-  if (fused) {
-    if (blockIdx.x == 0 && tid == 0) a.rng[1] = a.step + 1;  // the graph path's counter
-  } else if (blockIdx.x == 0) {  // the previous step's launch B is done with these
+  if (blockIdx.x == 0) {
+    if (fused && tid == 0) a.rng[1] = a.step + 1;  // the graph path's counter
+    // the previous step's launch B is done with these (zeroed in both forms: the engine
+    // picks the form per step, and the next B-form step counts into this half)
     for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
   }
   mbk::lds_barrier();
@@ -1903,6 +1904,13 @@ extern "C" int mbk_act_fused() {
   return g_act_fused && act_wave();
 }
 
+// the form of one step: MbkActStep.head_form 1 = head in A, 2 = launch B, 0 = the default
+// above (the engine picks per step from the env workers' active-cell count)
+extern "C" int mbk_act_step_fused(const MbkActStep* s) {
+  if (!act_wave()) return 0;
+  return s->head_form == 1 ? 1 : s->head_form == 2 ? 0 : mbk_act_fused();
+}
+
 extern "C" int mbk_act_set_mode(int wave, int fused) {
   g_act_wave = wave < 0 ? -1 : wave != 0;
   g_act_fused = fused < 0 ? -1 : fused != 0;
@@ -1978,7 +1986,7 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.reward_dst = s->reward_dst;
   a.done_dst = s->done_dst;
   a.stamps = g_act_stamps;
-  a.fused = wave_owned && mbk_act_fused();
+  a.fused = mbk_act_step_fused(s);
   if (a.fused) {
     if (!m->Wp || !m->bp || !m->rng) return (int)hipErrorInvalidValue;
     a.Wp = (const bf16*)m->Wp;

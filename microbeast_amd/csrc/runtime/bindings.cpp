@@ -359,6 +359,9 @@ PYBIND11_MODULE(_mbrt, m) {
         d["env_phase_s"] = s.env_phase_s;
         d["enqueue_s"] = s.enqueue_s;
         d["graph_launch_s"] = s.graph_launch_s;
+        d["act_fused_steps"] = s.act_fused_steps;
+        d["act_b_steps"] = s.act_b_steps;
+        d["act_active_cells"] = s.act_active_cells;
         d["slot_wait_s"] = s.slot_wait_s;
         d["env_s"] = s.env_s;
         d["publishes"] = s.publishes;

@@ -258,6 +258,8 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
   // MBK_ACT_SPARSE=0: dense zero-copy codes / actions (4 + 4 MB of PCIe per 8192-env step
   // instead of ~0.5-1 MB)
   const char* sp = std::getenv("MBK_ACT_SPARSE");
+  const char* fm = std::getenv("MBK_ACT_FUSED_MAX");
+  act_fused_max_ = std::getenv("MBK_ACT_FUSED") ? -1.f : fm ? (float)std::atof(fm) : 0.014f;
   sparse_ = !models.empty() && !copy && !(sp && sp[0] == '0');
   if (sparse_ && !h_code_list_) {
     const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
@@ -316,6 +318,7 @@ void GpuEngine::dispatch_env(int g) {
     }
     G.timed = false;
   }
+  G.idle.store(0, std::memory_order_relaxed);
   G.phase.store(ENV_BUSY, std::memory_order_release);
   G.remaining.store(cfg_.envs_per_group, std::memory_order_release);
   G.next_env.store(0, std::memory_order_release);
@@ -373,8 +376,9 @@ void GpuEngine::worker_loop(int wid) {
           if (inject_fault_.exchange(0) != 0)
             throw std::runtime_error("injected env-worker fault (--fault_inject_every)");
           if (sparse_)
-            env_->step_range_lists(a0 + e, a0 + e1, h_act_list_, h_code_list_, list_stride_,
-                                   h_reward_, h_done_, &log_);
+            G.idle.fetch_add(env_->step_range_lists(a0 + e, a0 + e1, h_act_list_, h_code_list_,
+                                                    list_stride_, h_reward_, h_done_, &log_),
+                             std::memory_order_relaxed);
           else if (G.selfplay)
             env_->step_range_codes_sp(a0 + e, a0 + e1, h_act16_, h_act16_p1_, h_codes_, h_res_,
                                       h_codes_p1_, h_res_p1_, h_reward_, h_done_, &log_,
@@ -538,6 +542,15 @@ bool GpuEngine::enqueue_gpu(int g) {
       a.done_dst = (uint8_t*)u8_at(buf_.done, rs, ri);
     }
     a.step = L.act_step++;
+    if (sparse_ && act_fused_max_ >= 0.f) {
+      // the in-tile head samples a tile's cells one unit per wave: cheapest while few cells
+      // are active, launch B's bucketed head wins above ~1.4 % (tools/active_sweep.py)
+      const int idle = G.idle.load(std::memory_order_relaxed);
+      a.head_form = idle <= act_fused_max_ * (float)E * (float)S_ ? 1 : 2;
+      act_active_cells_.fetch_add(idle, std::memory_order_relaxed);
+    }
+    (mbk_act_step_fused(&a) ? act_fused_steps_ : act_b_steps_)
+        .fetch_add(1, std::memory_order_relaxed);
     if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
     {
       const auto t0 = std::chrono::steady_clock::now();
@@ -817,6 +830,9 @@ EngineStats GpuEngine::stats() const {
   s.publishes = publishes_.load();
   s.opp_publishes = opp_publishes_.load();
   s.opp_version = opp_version_pub_.load();
+  s.act_fused_steps = act_fused_steps_.load();
+  s.act_b_steps = act_b_steps_.load();
+  s.act_active_cells = act_active_cells_.load();
   std::lock_guard<std::mutex> l(stats_m_);
   s.driver_idle_s = driver_idle_s_;
   s.slot_wait_s = slot_wait_s_;

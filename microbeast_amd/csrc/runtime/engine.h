@@ -134,6 +134,9 @@ struct EngineStats {
   int64_t publishes = 0;
   int64_t opp_publishes = 0;
   int opp_version = -1;
+  // fused acting step (act models set): steps whose head ran inside launch A / in launch B,
+  // and the agent's idle units (active cells) summed over the steps the engine chose for
+  int64_t act_fused_steps = 0, act_b_steps = 0, act_active_cells = 0;
 };
 
 class GpuEngine {
@@ -210,6 +213,7 @@ class GpuEngine {
     std::atomic<int> phase{ENV_BUSY};
     std::atomic<int> next_env{0};
     std::atomic<int> remaining{0};
+    std::atomic<int> idle{0};  // sparse env workers: the agent's idle units after this step
     int cur = -1, prev = -1, t = 0;
     bool first = true;
     bool selfplay = false;
@@ -304,6 +308,11 @@ class GpuEngine {
   std::atomic<int64_t> gpu_phase_ns_{0}, env_phase_ns_{0}, enqueue_ns_{0}, launch_ns_{0};
   bool step_timing_ = false;
   std::atomic<int64_t> step_h2d_ns_{0}, step_graph_ns_{0}, step_out_ns_{0}, timed_steps_{0};
+  std::atomic<int64_t> act_fused_steps_{0}, act_b_steps_{0}, act_active_cells_{0};
+  // per-step head form of the fused acting step (sparse path): head inside launch A while the
+  // group's active cells <= act_fused_max_ * envs * cells, else launch B; off (process
+  // default for every step) when MBK_ACT_FUSED is set or MBK_ACT_FUSED_MAX < 0
+  float act_fused_max_ = 0.014f;
   double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
   mutable std::mutex stats_m_;
 

@@ -115,9 +115,10 @@ void VecEnv::write_code_lists(uint32_t* lists, int stride) const {
   }
 }
 
-void VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,
-                              int stride, float* reward, uint8_t* done, EpisodeLog* log) {
+int VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,
+                             int stride, float* reward, uint8_t* done, EpisodeLog* log) {
   const size_t S = (size_t)size_ * size_;
+  int idle = 0;
   thread_local std::vector<uint16_t> dense;  // the listed actions expanded to a cell row
   dense.assign(S, 0);
   for (int i = e0; i < e1; ++i) {
@@ -148,9 +149,10 @@ void VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_
     reward[i] = r;
     done[i] = d ? 1 : 0;
     uint32_t* crow = code_lists + (size_t)i * stride;
-    const int n = sims_[i]->write_obs_code_list(crow + 1);
+    const int n = sims_[i]->write_obs_code_list(crow + 1, &idle);
     crow[0] = (uint32_t)n | ((uint32_t)sims_[i]->resources(0) << 16);
   }
+  return idle;
 }
 
 void VecEnv::step_range_codes_sp(int e0, int e1, const uint16_t* actions,

@@ -70,8 +70,9 @@ class VecEnv {
   // word 0 = n | resources << 16, then n entries cell | value << 16. Codes out: the occupied
   // cells; actions in: the cells with a non-noop action (a cell not listed no-ops).
   void write_code_lists(uint32_t* lists, int stride) const;
-  void step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,
-                        int stride, float* reward, uint8_t* done, EpisodeLog* log);
+  // Returns the agent's idle units over the range (the cells the next policy step samples).
+  int step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,
+                       int stride, float* reward, uint8_t* done, EpisodeLog* log);
   // Self-play variant: envs with an external opponent also take its packed actions
   // (opp_actions, its mirrored frame) and emit its codes / resources; their finished
   // episodes are tagged with `opponent` (the league snapshot that was playing).

@@ -50,8 +50,11 @@ def _model(cuda, seed):
 
 
 # launch-A forms (mbk_act_set_mode): wave-owned kernel with the head fused in (the default,
-# ONE launch per step), wave-owned + head launch B, phase-split kernel + head launch B
-MODES = {"fused": (1, 1), "wave+B": (1, 0), "phase+B": (0, 0)}
+# ONE launch per step), wave-owned + head launch B, phase-split kernel + head launch B, and
+# the engine's per-step choice (MbkActStep.head_form, switching between fused and B: the
+# bucket counters' double buffer must stay consistent across switches)
+MODES = {"fused": (1, 1), "wave+B": (1, 0), "phase+B": (0, 0), "mixed": (1, 1)}
+MIXED = [1, 2, 2, 1, 1, 2]  # head_form per step, cycled
 
 
 @pytest.fixture(params=list(MODES))
@@ -91,6 +94,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
     rdst, ddst = torch.zeros_like(reward), torch.zeros_like(done)
     n_active = 0
     for i, (codes, res) in enumerate(_codes_stream(E, 24, seed=E)):
+        form = MIXED[i % len(MIXED)] if act_mode == "mixed" else 0
         io["in_codes"].copy_(codes)
         io["in_res"].copy_(res)
         graph_policy_step(io, m, rng_a, E, 16, cuda)
@@ -100,7 +104,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
             ws.step(None, None, obs, mask, action, logp, value, None,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
                     reward=reward, done=done, reward_dst=rdst, done_dst=ddst, code_list=cl,
-                    act_list=act_list)
+                    act_list=act_list, head_form=form)
             torch.cuda.synchronize()
             act16 = dense_actions(act_list, S).to(cuda)
             al = act_list.cpu().to(torch.int64) & 0xFFFFFFFF
@@ -109,7 +113,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
         else:
             ws.step(io["in_codes"], io["in_res"], obs, mask, action, logp, value, act16,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
-                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst)
+                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst, head_form=form)
         torch.cuda.synchronize()
         assert torch.equal(obs, io["in_obs"]), f"obs planes differ at step {i}"
         assert torch.equal(mask, io["in_mask"]), f"masks differ at step {i}"
@@ -125,7 +129,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
         assert torch.equal(rdst, reward) and torch.equal(ddst, done)
         # between steps the previous step's bucket counters are back at zero (double buffer)
         par = (7 + i) % 2  # this step's Philox step is 7 + i
-        fused = act_mode == "fused"  # (one launch: no bucket counters at all)
+        fused = act_mode == "fused" or form == 1  # (one launch: no bucket counters at all)
         assert (int(ws.bucket_cnt[par * 256:(par + 1) * 256].abs().sum()) > 0) != fused
         if i > 0:
             assert int(ws.bucket_cnt[(1 - par) * 256:(2 - par) * 256].abs().sum()) == 0
@@ -178,5 +182,8 @@ def test_engine_fused_act_learns(cuda, monkeypatch):
             assert torch.isfinite(losses).all()
         st = rt.stats()
         assert st["frames"] > 0 and st["gpu_steps"] > 0 and st["publishes"] >= 1
+        # the per-step head form (sparse rows: engine-picked from the env workers' counts)
+        assert st["act_fused_steps"] + st["act_b_steps"] > 0
+        assert st["act_active_cells"] > 0
     finally:
         rt.stop()
