@@ -104,20 +104,20 @@ _SIGS = {
     "mbk_conv_pack": [c_void_p, c_int, c_void_p],
     "mbk_head_compact": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_head_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                      c_void_p, c_void_p, c_int, c_void_p],
-    "mbk_head_pair_rowsum": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                             c_void_p],
+    "mbk_head_pair_rowsum": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                             c_void_p, c_void_p],
     "mbk_head_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p],
-    "mbk_head_dx_gather": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "mbk_head_dx_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "mbk_head_dx_value_parts": [c_int],
-    "mbk_head_dx_value": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
-                          c_void_p, c_void_p, c_int, c_void_p],
+    "mbk_head_dx_value": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                          c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p],
     "mbk_head_pack": [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_decode_obs_mask": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_decode_obs_mask_bucket": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,

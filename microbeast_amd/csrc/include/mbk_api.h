@@ -96,6 +96,9 @@ typedef struct {
   uint64_t step;           // Philox step of this policy step (the lane's step count)
   int head_form;           // 0 = the process default (mbk_act_set_mode / MBK_ACT_FUSED),
                            // 1 = head sampled inside launch A, 2 = head in launch B
+  uint32_t* code_list_dev; // optional HBM scratch [E][list_stride]: a small row-staging
+                           // launch copies each code_list row's n + 1 words here first and
+                           // launch A reads them from HBM instead of over PCIe
 } MbkActStep;
 
 int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);

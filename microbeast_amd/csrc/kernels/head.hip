@@ -13,8 +13,12 @@
 //
 //   head_count / head_scan / head_scatter : deterministic, stable counting sort
 //       of active pairs by cell (frames ascending inside a cell group), a tile
-//       list of 16-pair units, and pidx[f][c] (pair slot or -1). Inactive cells
-//       get action 0 / log-prob 0 / entropy 0 written here.
+//       list of 16-pair units, and pidx[f][c] (the pair slot, written for active
+//       cells only). head_count reads the masks once (F x S x 12 B, the only pass
+//       over them) and leaves a per-frame active-cell bitmap abits[f][S/32]: the
+//       scatter and every per-frame consumer (row sums, dX gathers) walk that
+//       instead of the masks / a dense pidx. Sampling: inactive cells get action 0
+//       / log-prob 0 / entropy 0 written here.
 //   head_fwd   : one wave per 16-pair unit: Z[16x80] = X[f rows] . W_c^T + b_c on
 //                v_mfma_f32_16x16x32_bf16 (W_c = that cell's 78 rows, padded to 80),
 //                then sample (Philox, inverse CDF) or score per row.
@@ -61,18 +65,33 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
 __device__ __forceinline__ bool active3(const uint32_t* m) { return (m[0] | m[1] | m[2]) != 0u; }
 
 // ------------------------------------------------------------------ compaction
-// cnt[c * nfb + b] = active pairs of cell c among frames [b*FB, (b+1)*FB)
+// cnt[c * nfb + b] = active pairs of cell c among frames [b*FB, (b+1)*FB), and the frames'
+// active-cell bitmap abits[f][(S + 31) / 32] (bit c & 31 of word c >> 5): a wave ballots its
+// 64 cells per frame
+__device__ __forceinline__ int abits_words(int S) { return (S + 31) >> 5; }
+
 __global__ __launch_bounds__(256) void head_count_kernel(const uint32_t* __restrict__ mask,
                                                          int F, int S, int FB,
-                                                         int* __restrict__ cnt) {
+                                                         int* __restrict__ cnt,
+                                                         uint32_t* __restrict__ abits) {
   const int b = blockIdx.x, nfb = gridDim.x;
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  if (c >= S) return;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.y * 256 + threadIdx.x, c0 = c - lane;
+  if (c0 >= S) return;  // whole waves only: the ballot needs every lane
+  const bool in = c < S;
+  const int SW = abits_words(S), w0 = c0 >> 5;
+  const bool two = c0 + 32 < S;
   const int f0 = b * FB, f1 = min(F, f0 + FB);
   int n = 0;
 #pragma unroll 8
-  for (int f = f0; f < f1; ++f) n += active3(mask + ((size_t)f * S + c) * 3);
-  cnt[c * nfb + b] = n;
+  for (int f = f0; f < f1; ++f) {
+    const bool a = in && active3(mask + ((size_t)f * S + c) * 3);
+    n += a;
+    const uint64_t bal = __ballot(a);
+    if (lane == 0) abits[(size_t)f * SW + w0] = (uint32_t)bal;
+    if (lane == 1 && two) abits[(size_t)f * SW + w0 + 1] = (uint32_t)(bal >> 32);
+  }
+  if (in) cnt[c * nfb + b] = n;
 }
 
 // exclusive scan in (c, b) order + per-cell groups + 16-pair unit list
@@ -168,9 +187,11 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
   }
 }
 
-// pairs[] (frame ids, grouped by cell), pidx[f][c]; zero outputs of inactive cells
+// pairs[] (frame ids, grouped by cell) and pidx[f][c] of the active cells from head_count's
+// bitmap (32 B per frame at 16x16 instead of the 3 KB of masks); sampling also zeroes the
+// outputs of inactive cells
 __global__ __launch_bounds__(256) void head_scatter_kernel(
-    const uint32_t* __restrict__ mask, int F, int S, int FB, const int* __restrict__ off,
+    const uint32_t* __restrict__ abits, int F, int S, int FB, const int* __restrict__ off,
     const int* __restrict__ grp_start,
     int* __restrict__ pairs, int* __restrict__ pidx, uint8_t* __restrict__ action_zero,
     float* __restrict__ cell_lp, float* __restrict__ cell_ent) {
@@ -178,15 +199,17 @@ __global__ __launch_bounds__(256) void head_scatter_kernel(
   const int c = blockIdx.y * 256 + threadIdx.x;
   if (c >= S) return;
   const int f0 = b * FB, f1 = min(F, f0 + FB);
+  const int SW = abits_words(S), w = c >> 5, bit = c & 31;
+  const bool dense = action_zero || cell_lp || cell_ent;
   int pos = grp_start[c] + off[c * nfb + b];
+#pragma unroll 4
   for (int f = f0; f < f1; ++f) {
     const size_t fc = (size_t)f * S + c;
-    if (active3(mask + fc * 3)) {
+    if ((abits[(size_t)f * SW + w] >> bit) & 1u) {
       pairs[pos] = f;
       pidx[fc] = pos;
       ++pos;
-    } else {
-      pidx[fc] = -1;
+    } else if (dense) {
       if (action_zero) {
 #pragma unroll
         for (int k = 0; k < kComps; ++k) action_zero[fc * kComps + k] = 0;
@@ -511,9 +534,11 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
 }
 
 // logp[f] = sum over f's active cells of the pair log-probs (ent likewise): one wave per
-// frame walking pidx[f][:] (4 B per cell instead of reading dense per-cell outputs that
-// head_scatter had to zero), fixed-order butterfly reduction (deterministic)
-__global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __restrict__ pidx, int F,
+// frame walking its bitmap row and reading pidx at the active cells only, fixed-order
+// butterfly reduction (deterministic)
+__global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __restrict__ pidx,
+                                                               const uint32_t* __restrict__ abits,
+                                                               int F,
                                                                int S, const float* __restrict__ plp,
                                                                const float* __restrict__ pent,
                                                                float* __restrict__ logp,
@@ -523,22 +548,22 @@ __global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __rest
   if (f >= F) return;
   float a = 0.f, b = 0.f;
   const int* pr = pidx + (size_t)f * S;
+  const uint32_t* ab = abits + (size_t)f * abits_words(S);
   auto add = [&](int p) {
-    if (p >= 0) {
-      a += plp[p];
-      if (pent) b += pent[p];
-    }
+    a += plp[p];
+    if (pent) b += pent[p];
   };
-  if ((S & 3) == 0) {  // 16-byte loads: 4 cells per lane per pass
+  if ((S & 3) == 0) {  // 4 cells per lane per pass (a nibble of one bitmap word)
     for (int c = 4 * lane; c < S; c += 256) {
-      const int4 q = *(const int4*)(pr + c);
-      add(q.x);
-      add(q.y);
-      add(q.z);
-      add(q.w);
+      const uint32_t nib = (ab[c >> 5] >> (c & 31)) & 15u;
+      if (nib == 0u) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((nib >> j) & 1u) add(pr[c + j]);
     }
   } else {
-    for (int c = lane; c < S; c += 64) add(pr[c]);
+    for (int c = lane; c < S; c += 64)
+      if ((ab[c >> 5] >> (c & 31)) & 1u) add(pr[c]);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -1026,19 +1051,27 @@ __global__ __launch_bounds__(256) void head_dw_reduce_kernel(const float* __rest
   }
 }
 
+// the active bit of cell c in frame row ab (head_count's bitmap)
+__device__ __forceinline__ bool abit(const uint32_t* ab, int c, int S) {
+  return c < S && ((ab[c >> 5] >> (c & 31)) & 1u);
+}
+
 // dX[f][:] = sum over active cells c of dXp[pidx[f][c]][:]; one wave per frame
 __global__ __launch_bounds__(256) void head_dx_gather_kernel(const bf16* __restrict__ dXp,
-                                                             const int* __restrict__ pidx, int F,
-                                                             int S, float* __restrict__ dX) {
-  // one wave per frame: 64 cells' pair indices per coalesced load, ballot the active
-  // ones (~1% of cells) and sum only their dXp rows
+                                                             const int* __restrict__ pidx,
+                                                             const uint32_t* __restrict__ abits,
+                                                             int F, int S,
+                                                             float* __restrict__ dX) {
+  // one wave per frame: the active cells (~1 %) of 64 from the bitmap, their pair indices,
+  // and only their dXp rows
   const int lane = threadIdx.x & 63;
   const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (f >= F) return;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   const int* pr = pidx + (size_t)f * S;
+  const uint32_t* ab = abits + (size_t)f * abits_words(S);
   for (int c0 = 0; c0 < S; c0 += 64) {
-    const int p = c0 + lane < S ? pr[c0 + lane] : -1;
+    const int p = abit(ab, c0 + lane, S) ? pr[c0 + lane] : -1;
     uint64_t m = __ballot(p >= 0);
     while (m) {
       const int b = __builtin_ctzll(m);
@@ -1060,7 +1093,9 @@ __global__ __launch_bounds__(256) void head_dx_gather_kernel(const bf16* __restr
 // frame written, then re-read with h by value_bwd) never exists. One wave per frame row,
 // a lane owns hidden units 4 lane .. 4 lane + 3 (the gather's float4 layout).
 __global__ __launch_bounds__(256) void head_dx_value_kernel(const bf16* __restrict__ dXp,
-                                                            const int* __restrict__ pidx, int F,
+                                                            const int* __restrict__ pidx,
+                                                            const uint32_t* __restrict__ abits,
+                                                            int F,
                                                             int S, const float* __restrict__ dv,
                                                             const bf16* __restrict__ h,
                                                             const float* __restrict__ wc, int R,
@@ -1075,26 +1110,42 @@ __global__ __launch_bounds__(256) void head_dx_value_kernel(const bf16* __restri
   constexpr int kMaxCh = MAX_S / 64;
   const int nch = (S + 63) / 64;
   const int stride = gridDim.x * 4;
+  // The bitmap words run one frame further ahead: a frame's pair indices are loaded (active
+  // lanes only) from bits that already arrived, so no iteration waits on two dependent trips.
   float dn = 0.f;
   uint2 hn = make_uint2(0, 0);
   int pn[kMaxCh];
-  auto fetch = [&](int r) {
+  uint32_t wn[kMaxCh];  // bitmap word of cell q * 64 + lane, frame r + stride
+  auto fetch_bits = [&](int r) {
+    const uint32_t* ab = abits + (size_t)r * abits_words(S);
+#pragma unroll
+    for (int q = 0; q < kMaxCh; ++q)
+      wn[q] = (r < F && q < nch && q * 64 + lane < S) ? ab[(q * 64 + lane) >> 5] : 0u;
+  };
+  auto fetch = [&](int r) {  // uses wn = r's bitmap words
     dn = dv[r];
     hn = ((const uint2*)(h + (size_t)r * KD))[lane];
     const int* pr = pidx + (size_t)r * S;
 #pragma unroll
     for (int q = 0; q < kMaxCh; ++q)
-      pn[q] = (r < F && q < nch && q * 64 + lane < S) ? pr[q * 64 + lane] : -1;
+      pn[q] = ((wn[q] >> (lane & 31)) & 1u) ? pr[q * 64 + lane] : -1;
   };
   const int rfirst = blockIdx.x * 4 + wave;
-  if (rfirst < R) fetch(rfirst);
+  if (rfirst < R) {
+    fetch_bits(rfirst);
+    fetch(rfirst);
+    if (rfirst + stride < R) fetch_bits(rfirst + stride);
+  }
   for (int r = rfirst; r < R; r += stride) {
     const float d = dn;
     const uint2 hv = hn;
     int pc[kMaxCh];
 #pragma unroll
     for (int q = 0; q < kMaxCh; ++q) pc[q] = pn[q];
-    if (r + stride < R) fetch(r + stride);
+    if (r + stride < R) {
+      fetch(r + stride);
+      if (r + 2 * stride < R) fetch_bits(r + 2 * stride);
+    }
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int q = 0; q < kMaxCh; ++q) {
@@ -1169,22 +1220,25 @@ extern "C" int mbk_head_fb(int F) {
   return fb;
 }
 
+// abits [F][(S + 31) / 32] uint32: the active-cell bitmap the consumers of pidx read
 extern "C" int mbk_head_compact(const uint32_t* mask, int F, int S, int* cnt, int* off,
                                 int* grp_start, int* grp_count, int* unit_cell, int* unit_row,
                                 int* chunk_cell, int* chunk_row, int* chunk_start,
-                                int* totals, int* pairs, int* pidx, uint8_t* action_zero,
-                                float* cell_lp, float* cell_ent, hipStream_t stream) {
+                                int* totals, int* pairs, int* pidx, uint32_t* abits,
+                                uint8_t* action_zero, float* cell_lp, float* cell_ent,
+                                hipStream_t stream) {
   if (S > MAX_S) return (int)hipErrorInvalidValue;
   const int FB = mbk_head_fb(F);
   const int nfb = (F + FB - 1) / FB;
   dim3 g1(nfb, (S + 255) / 256);
-  hipLaunchKernelGGL(head_count_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, cnt);
+  if (!abits) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_count_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, cnt, abits);
   // per-cell totals go to grp_count (overwritten with the same values by the scan)
   hipLaunchKernelGGL(head_cell_scan_kernel, dim3(S), dim3(256), 0, stream, cnt, nfb, off,
                      grp_count);
   hipLaunchKernelGGL(head_scan_kernel, dim3(1), dim3(1024), 0, stream, grp_count, S, grp_start,
                      grp_count, unit_cell, unit_row, chunk_cell, chunk_row, chunk_start, totals);
-  hipLaunchKernelGGL(head_scatter_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, off,
+  hipLaunchKernelGGL(head_scatter_kernel, g1, dim3(256), 0, stream, abits, F, S, FB, off,
                      grp_start, pairs, pidx, action_zero, cell_lp, cell_ent);
   return (int)hipGetLastError();
 }
@@ -1224,12 +1278,12 @@ extern "C" int mbk_head_fwd_counts(const void* X, const void* Wp, const float* b
   return (int)hipGetLastError();
 }
 
-extern "C" int mbk_head_pair_rowsum(const int* pidx, int F, int S, const float* plp,
-                                    const float* pent, float* logp, float* ent,
+extern "C" int mbk_head_pair_rowsum(const int* pidx, const uint32_t* abits, int F, int S,
+                                    const float* plp, const float* pent, float* logp, float* ent,
                                     hipStream_t stream) {
   if (F <= 0) return 0;
-  hipLaunchKernelGGL(head_pair_rowsum_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, pidx, F, S,
-                     plp, pent, logp, ent);
+  hipLaunchKernelGGL(head_pair_rowsum_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, pidx,
+                     abits, F, S, plp, pent, logp, ent);
   return (int)hipGetLastError();
 }
 
@@ -1285,10 +1339,10 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
   return (int)hipGetLastError();
 }
 
-extern "C" int mbk_head_dx_gather(const void* dXp, const int* pidx, int F, int S, float* dX,
-                                  hipStream_t stream) {
+extern "C" int mbk_head_dx_gather(const void* dXp, const int* pidx, const uint32_t* abits, int F,
+                                  int S, float* dX, hipStream_t stream) {
   hipLaunchKernelGGL(head_dx_gather_kernel, dim3((F + 3) / 4), dim3(256), 0, stream,
-                     (const bf16*)dXp, pidx, F, S, dX);
+                     (const bf16*)dXp, pidx, abits, F, S, dX);
   return (int)hipGetLastError();
 }
 
@@ -1307,13 +1361,13 @@ extern "C" int mbk_head_dx_value_parts(int R) {
 
 // dh [R][256] bf16 = (dv wc + gathered head dX) * (h > 0); partial [parts][257] fp32 rows of
 // (dWc, dbc); rows >= F take the value term only. parts = mbk_head_dx_value_parts(R).
-extern "C" int mbk_head_dx_value(const void* dXp, const int* pidx, int F, int S, const float* dv,
-                                 const void* h, const float* wc, int R, void* dh, float* partial,
-                                 int parts, hipStream_t stream) {
+extern "C" int mbk_head_dx_value(const void* dXp, const int* pidx, const uint32_t* abits, int F,
+                                 int S, const float* dv, const void* h, const float* wc, int R,
+                                 void* dh, float* partial, int parts, hipStream_t stream) {
   if (R <= 0) return 0;
   if (F > R || parts < 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(head_dx_value_kernel, dim3(parts), dim3(256), 0, stream, (const bf16*)dXp,
-                     pidx, F, S, dv, (const bf16*)h, wc, R, (bf16*)dh, partial);
+                     pidx, abits, F, S, dv, (const bf16*)h, wc, R, (bf16*)dh, partial);
   return (int)hipGetLastError();
 }
 

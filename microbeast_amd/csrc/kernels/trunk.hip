@@ -1895,13 +1895,46 @@ static int act_wave() {
 }
 
 // The policy step in ONE launch: the wave-owned kernel samples the sparse head at each tile's
-// end. head.hip's mbk_act_head asks this and launches nothing when A did the head.
+// end (MBK_ACT_FUSED=1; the default 0 leaves it to launch B, which measured level or ahead
+// under the learner, profiles/34). head.hip's mbk_act_head asks this and launches nothing
+// when A did the head.
 extern "C" int mbk_act_fused() {
   if (g_act_fused < 0) {
     const char* e = std::getenv("MBK_ACT_FUSED");
-    g_act_fused = (e ? std::atoi(e) : 1) != 0;
+    g_act_fused = (e ? std::atoi(e) : 0) != 0;
   }
   return g_act_fused && act_wave();
+}
+
+// Sparse input rows, pinned host -> HBM, ahead of launch A: read inside A, the first tile's
+// rows cost ~19 us of PCIe wait in every workgroup (act_phases: 214 -> 184 us per 8192 envs
+// with the rows already in HBM). Here a few workgroups stream them (two envs per wave
+// instruction, 32 lanes each, kRowU env pairs in flight per wave) while the rest of the GPU
+// runs other work; only a row's n + 1 words move.
+constexpr int kRowU = 4;
+__global__ __launch_bounds__(256) void act_rows_kernel(const uint32_t* __restrict__ src,
+                                                       uint32_t* __restrict__ dst, int E,
+                                                       int stride, int S) {
+  const int lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
+  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nwaves = (int)(gridDim.x * blockDim.x >> 6);
+  for (int base = wave * 2 * kRowU; base < E; base += nwaves * 2 * kRowU) {
+    uint32_t w[kRowU];
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const int e = base + 2 * u + half;
+      w[u] = e < E ? src[(size_t)e * stride + l] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kRowU; ++u) {
+      const int e = base + 2 * u + half;
+      const int n = min((int)((uint32_t)__shfl((int)w[u], half * 32, 64) & 0xFFFFu), S);
+      if (e >= E) continue;
+      const size_t r = (size_t)e * stride;
+      if (l <= n) dst[r + l] = w[u];
+      for (int q = 32 + l; q <= n; q += 32) dst[r + q] = src[r + q];
+    }
+  }
 }
 
 // the form of one step: MbkActStep.head_form 1 = head in A, 2 = launch B, 0 = the default
@@ -1966,6 +1999,12 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.codes = s->codes;
   a.res = s->res;
   a.code_list = s->code_list;
+  if (s->code_list && s->code_list_dev) {
+    if (!al16(s->code_list_dev)) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(act_rows_kernel, dim3(64), dim3(256), 0, stream, s->code_list,
+                       s->code_list_dev, m->E, s->list_stride, m->H * m->W);
+    a.code_list = s->code_list_dev;
+  }
   a.act_list = s->act_list;
   a.list_stride = s->list_stride;
   a.obs = s->obs;

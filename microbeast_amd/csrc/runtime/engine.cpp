@@ -183,6 +183,7 @@ GpuEngine::~GpuEngine() {
   if (h_act_list_) hipHostFree(h_act_list_);
   if (gate_) hipFree(gate_);
   for (Lane& L : lanes_) {
+    if (L.d_rows) hipFree(L.d_rows);
     for (int p = 0; p < 2; ++p) {
       if (L.ev_h2d[p]) hipEventDestroy(L.ev_h2d[p]);
       if (L.ev_done[p]) hipEventDestroy(L.ev_done[p]);
@@ -259,7 +260,7 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
   // instead of ~0.5-1 MB)
   const char* sp = std::getenv("MBK_ACT_SPARSE");
   const char* fm = std::getenv("MBK_ACT_FUSED_MAX");
-  act_fused_max_ = std::getenv("MBK_ACT_FUSED") ? -1.f : fm ? (float)std::atof(fm) : 0.014f;
+  act_fused_max_ = std::getenv("MBK_ACT_FUSED") ? -1.f : fm ? (float)std::atof(fm) : -1.f;
   sparse_ = !models.empty() && !copy && !(sp && sp[0] == '0');
   if (sparse_ && !h_code_list_) {
     const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
@@ -270,6 +271,14 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
       throw std::runtime_error("set_act_models: hipHostMalloc of the sparse staging failed");
     std::memset(h_act_list_, 0, bytes);
     env_->write_code_lists(h_code_list_, list_stride_);  // the reset state, as lists
+  }
+  // MBK_ACT_ROWS_DEV=0: launch A reads the rows over PCIe itself (no staging launch)
+  const char* rd = std::getenv("MBK_ACT_ROWS_DEV");
+  if (sparse_ && !(rd && rd[0] == '0')) {
+    const size_t bytes = (size_t)cfg_.envs_per_group * list_stride_ * 4;
+    for (Lane& L : lanes_)
+      if (!L.d_rows && hipMalloc((void**)&L.d_rows, bytes) != hipSuccess)
+        throw std::runtime_error("set_act_models: hipMalloc of the row staging failed");
   }
 }
 
@@ -519,6 +528,7 @@ bool GpuEngine::enqueue_gpu(int g) {
     MbkActStep a{};
     if (sparse_) {
       a.code_list = h_code_list_ + e0 * list_stride_;
+      a.code_list_dev = L.d_rows;
       a.act_list = h_act_list_ + e0 * list_stride_;
       a.list_stride = list_stride_;
     } else {

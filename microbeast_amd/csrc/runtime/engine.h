@@ -252,6 +252,7 @@ class GpuEngine {
     int opp_version = -1;     // driver thread only
     int policy_version = 0;   // learner update of the weights landed on this lane
     uint64_t act_step = 0;    // fused steps: Philox step of the lane's next policy step
+    uint32_t* d_rows = nullptr;  // sparse steps: the HBM copy of a group's input rows
   };
 
   EngineConfig cfg_;
@@ -309,10 +310,12 @@ class GpuEngine {
   bool step_timing_ = false;
   std::atomic<int64_t> step_h2d_ns_{0}, step_graph_ns_{0}, step_out_ns_{0}, timed_steps_{0};
   std::atomic<int64_t> act_fused_steps_{0}, act_b_steps_{0}, act_active_cells_{0};
-  // per-step head form of the fused acting step (sparse path): head inside launch A while the
-  // group's active cells <= act_fused_max_ * envs * cells, else launch B; off (process
-  // default for every step) when MBK_ACT_FUSED is set or MBK_ACT_FUSED_MAX < 0
-  float act_fused_max_ = 0.014f;
+  // per-step head form of the fused acting step (sparse path), MBK_ACT_FUSED_MAX=f: head
+  // inside launch A while the group's active cells <= f * envs * cells, else launch B. Off by
+  // default (every step takes the process default, launch B): under the learner the B form
+  // measured level with or ahead of the in-A head even at 0.5 % active cells (profiles/34),
+  // and far ahead at 2-5 %; the in-A head wins only for acting alone at <~1.4 %.
+  float act_fused_max_ = -1.f;
   double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
   mutable std::mutex stats_m_;
 

@@ -50,7 +50,8 @@ class SparseHead:
         self.chunk_cell = torch.zeros(F * S // 512 + S + 1, dtype=torch.int32, device=dev)
         self.chunk_row = torch.zeros_like(self.chunk_cell)
         self.pairs = torch.zeros(F * S, dtype=torch.int32, device=dev)
-        self.pidx = torch.zeros(F * S, dtype=torch.int32, device=dev)
+        self.pidx = torch.zeros(F * S, dtype=torch.int32, device=dev)  # active cells only
+        self.abits = torch.zeros(F * ((S + 31) // 32), dtype=torch.int32, device=dev)
         self.cell_lp = torch.zeros(F * S, dtype=torch.float32, device=dev)
         self.cell_ent = torch.zeros(F * S, dtype=torch.float32, device=dev)
         self._F = F
@@ -120,7 +121,7 @@ class SparseHead:
             self.grp_start.data_ptr(), self.grp_count.data_ptr(), self.unit_cell.data_ptr(),
             self.unit_row.data_ptr(), self.chunk_cell.data_ptr(), self.chunk_row.data_ptr(),
             self.chunk_start.data_ptr(), self.totals.data_ptr(), self.pairs.data_ptr(),
-            self.pidx.data_ptr(), N.ptr(action_zero),
+            self.pidx.data_ptr(), self.abits.data_ptr(), N.ptr(action_zero),
             self.cell_lp.data_ptr() if dense_out else None,
             self.cell_ent.data_ptr() if dense_out else None, N.stream_ptr()), "head_compact")
 
@@ -146,7 +147,8 @@ class SparseHead:
         if want_ent:
             ent = ent_out if ent_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
         if pair_out:
-            N.check(k.mbk_head_pair_rowsum(self.pidx.data_ptr(), F, self.S,
+            N.check(k.mbk_head_pair_rowsum(self.pidx.data_ptr(), self.abits.data_ptr(), F,
+                                           self.S,
                                            self.cell_lp.data_ptr(),
                                            self.cell_ent.data_ptr() if want_ent else None,
                                            logp.data_ptr(), N.ptr(ent), st), "head_pair_rowsum")
@@ -197,14 +199,15 @@ class SparseHead:
             R = h.shape[0]
             assert h.is_contiguous() and h.shape[1] == KD and dv.dtype == torch.float32
             dh = torch.empty(R, KD, dtype=torch.bfloat16, device=X.device)
-            N.check(k.mbk_head_dx_value(dXp.data_ptr(), self.pidx.data_ptr(), F, self.S,
+            N.check(k.mbk_head_dx_value(dXp.data_ptr(), self.pidx.data_ptr(),
+                                        self.abits.data_ptr(), F, self.S,
                                         dv.data_ptr(), h.data_ptr(), wc.data_ptr(), R,
                                         dh.data_ptr(), partial.data_ptr(), partial.shape[0], st),
                     "head_dx_value")
             return dh, dW, db
         dX = torch.empty(F, KD, dtype=torch.float32, device=X.device)
-        N.check(k.mbk_head_dx_gather(dXp.data_ptr(), self.pidx.data_ptr(), F, self.S,
-                                     dX.data_ptr(), st), "head_dx_gather")
+        N.check(k.mbk_head_dx_gather(dXp.data_ptr(), self.pidx.data_ptr(), self.abits.data_ptr(),
+                                     F, self.S, dX.data_ptr(), st), "head_dx_gather")
         return dX, dW, db
 
 

@@ -49,8 +49,8 @@ def _model(cuda, seed):
     return m
 
 
-# launch-A forms (mbk_act_set_mode): wave-owned kernel with the head fused in (the default,
-# ONE launch per step), wave-owned + head launch B, phase-split kernel + head launch B, and
+# launch-A forms (mbk_act_set_mode): wave-owned kernel with the head fused in (ONE launch per
+# step), wave-owned + head launch B (the default), phase-split kernel + head launch B, and
 # the engine's per-step choice (MbkActStep.head_form, switching between fused and B: the
 # bucket counters' double buffer must stay consistent across switches)
 MODES = {"fused": (1, 1), "wave+B": (1, 0), "phase+B": (0, 0), "mixed": (1, 1)}
@@ -93,6 +93,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
     done = (torch.rand(E, device=cuda) < 0.3).to(torch.uint8)
     rdst, ddst = torch.zeros_like(reward), torch.zeros_like(done)
     n_active = 0
+    rows_dev = torch.empty(E, S + 4, dtype=torch.int32, device=cuda)  # row staging scratch
     for i, (codes, res) in enumerate(_codes_stream(E, 24, seed=E)):
         form = MIXED[i % len(MIXED)] if act_mode == "mixed" else 0
         io["in_codes"].copy_(codes)
@@ -100,11 +101,16 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
         graph_policy_step(io, m, rng_a, E, 16, cuda)
         second = i % 3 == 0
         if sparse:
-            cl = code_lists(codes, res, stride).to(cuda)
+            # odd steps: rows in pinned host memory staged to HBM by the row launch (the
+            # engine's form); even steps: rows already in HBM
+            staged = i % 2 == 1
+            cl = code_lists(codes, res, stride)
+            cl = cl.pin_memory() if staged else cl.to(cuda)
             ws.step(None, None, obs, mask, action, logp, value, None,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
                     reward=reward, done=done, reward_dst=rdst, done_dst=ddst, code_list=cl,
-                    act_list=act_list, head_form=form)
+                    act_list=act_list, head_form=form,
+                    code_list_dev=rows_dev if staged else None)
             torch.cuda.synchronize()
             act16 = dense_actions(act_list, S).to(cuda)
             al = act_list.cpu().to(torch.int64) & 0xFFFFFFFF

@@ -36,6 +36,8 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warm", type=int, default=30, help="env steps before sampling codes")
     p.add_argument("--device_rows", action="store_true", help="sparse rows in HBM, not pinned")
+    p.add_argument("--staged", action="store_true",
+                   help="pinned rows staged into HBM by the row launch (the engine's form)")
     a = p.parse_args()
     from microbeast_amd import _native as N
     from microbeast_amd.models.agent import Agent
@@ -85,6 +87,9 @@ def main():
     al = torch.zeros(E, stride, dtype=torch.int32).pin_memory()
     st = MbkActStep()
     st.code_list, st.act_list, st.list_stride = rows.data_ptr(), al.data_ptr(), stride
+    if a.staged:
+        rows_dev = torch.empty_like(rows, device=dev)
+        st.code_list_dev = rows_dev.data_ptr()
     st.obs, st.mask, st.action, st.logp, st.value = (o.data_ptr(), mk.data_ptr(), act.data_ptr(),
                                                      lp.data_ptr(), v.data_ptr())
     k = N.kernels()
@@ -104,7 +109,9 @@ def main():
             tb += ev[1].elapsed_time(ev[2])
     n = a.steps
     print(f"launch A (decode + trunk + critic) {1e3 * ta / n:.1f} us, launch B (head + finale) "
-          f"{1e3 * tb / n:.1f} us, rows in {'HBM' if a.device_rows else 'pinned host memory'}")
+          f"{1e3 * tb / n:.1f} us, rows in "
+          f"{'HBM' if a.device_rows else 'pinned host memory'}"
+          f"{' (staged into HBM by the row launch, included in A)' if a.staged else ''}")
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     stamps = torch.zeros(ncu * 4 * 32 * 64, dtype=torch.int64, device=dev)
     nst = k.mbk_act_set_stamps(stamps.data_ptr())
