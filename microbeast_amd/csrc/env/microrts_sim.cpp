@@ -662,16 +662,18 @@ void MicroRTSSim::write_obs_codes_as(int player, uint16_t* out) const {
   }
 }
 
-int MicroRTSSim::write_obs_code_list(uint32_t* entries, int* idle_own) const {
+int MicroRTSSim::write_obs_code_list(uint32_t* entries, int* idle_own, int player) const {
   int n = 0, idle = 0;
   for (const Unit& u : units_) {
     if (!u.alive) continue;
-    const int own = u.owner < 0 ? 0 : (u.owner == 0 ? 1 : 2);
+    int px = u.x, py = u.y;
+    if (player != 0) map_xy(player, u.x, u.y, &px, &py);
+    const int own = u.owner < 0 ? 0 : (u.owner == player ? 1 : 2);
     idle += (own == 1 && u.act == A_NOOP);
     const uint16_t code = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
                                          std::min<int>(std::max<int>(u.res, 0), 4), own, u.type,
                                          u.act);
-    entries[n++] = (uint32_t)cell(u.x, u.y) | ((uint32_t)code << 16);
+    entries[n++] = (uint32_t)cell(px, py) | ((uint32_t)code << 16);
   }
   if (idle_own) *idle_own += idle;
   return n;

@@ -108,8 +108,9 @@ class MicroRTSSim {
   void write_obs_codes(uint16_t* out) const { write_obs_codes_as(0, out); }
   // sparse form of write_obs_codes for the fused acting step's PCIe-light input: the occupied
   // cells only, entry = cell | code << 16, into entries[0 .. n); returns n (<= cells).
-  // *idle_own (optional) += the agent's idle units: the cells the sparse head samples
-  int write_obs_code_list(uint32_t* entries, int* idle_own = nullptr) const;
+  // *idle_own (optional) += the agent's idle units: the cells the sparse head samples.
+  // player 1: its mirrored frame (write_obs_codes_as), for the self-play opponent's policy
+  int write_obs_code_list(uint32_t* entries, int* idle_own = nullptr, int player = 0) const;
   // codes from `player`'s perspective (player 1: mirrored frame, owner 1 = itself)
   void write_obs_codes_as(int player, uint16_t* out) const;
   bool external_opponent() const { return external_opp_; }

@@ -138,6 +138,21 @@ PYBIND11_MODULE(_mbrt, m) {
              py::gil_scoped_release g;
              e.env->step_range_codes(0, e.env->num_envs(), P<uint16_t>(act16), P<uint16_t>(codes),
                                      P<int32_t>(res), P<float>(rew), P<uint8_t>(done), &e.log);
+           })
+      // sparse rows (the engine's fused-step form): code_lists(player) and the self-play step
+      .def("code_lists",
+           [](PyVecEnv& e, uintptr_t lists, int stride, int player) {
+             e.env->write_code_lists(P<uint32_t>(lists), stride, player);
+           },
+           py::arg("lists"), py::arg("stride"), py::arg("player") = 0)
+      .def("step_lists_sp",
+           [](PyVecEnv& e, uintptr_t acts, uintptr_t opp_acts, uintptr_t lists,
+              uintptr_t lists_p1, int stride, uintptr_t rew, uintptr_t done, int opponent) {
+             py::gil_scoped_release g;
+             return e.env->step_range_lists_sp(0, e.env->num_envs(), P<uint32_t>(acts),
+                                               P<uint32_t>(opp_acts), P<uint32_t>(lists),
+                                               P<uint32_t>(lists_p1), stride, P<float>(rew),
+                                               P<uint8_t>(done), &e.log, opponent);
            });
 
   py::class_<IndexRing>(m, "IndexRing")
@@ -325,21 +340,27 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("set_group_graphs", &GpuEngine::set_group_graphs)
       // fused acting steps: one packed MbkActModel (mbk_api.h, built by ops/act.py) per lane
       .def("set_act_models",
-           [](GpuEngine& e, std::vector<py::bytes> blocks, bool copy) {
-             std::vector<MbkActModel> ms;
-             for (const py::bytes& b : blocks) {
-               const std::string raw = b;
-               if (raw.size() != sizeof(MbkActModel))
-                 throw std::runtime_error("set_act_models: block size " +
-                                          std::to_string(raw.size()) + " != sizeof(MbkActModel) " +
-                                          std::to_string(sizeof(MbkActModel)));
-               MbkActModel m;
-               std::memcpy(&m, raw.data(), sizeof(m));
-               ms.push_back(m);
-             }
-             e.set_act_models(ms, copy);
+           [](GpuEngine& e, std::vector<py::bytes> blocks, bool copy,
+              std::vector<py::bytes> opp_blocks) {
+             auto unpack = [](const std::vector<py::bytes>& bs) {
+               std::vector<MbkActModel> ms;
+               for (const py::bytes& b : bs) {
+                 const std::string raw = b;
+                 if (raw.size() != sizeof(MbkActModel))
+                   throw std::runtime_error("set_act_models: block size " +
+                                            std::to_string(raw.size()) +
+                                            " != sizeof(MbkActModel) " +
+                                            std::to_string(sizeof(MbkActModel)));
+                 MbkActModel m;
+                 std::memcpy(&m, raw.data(), sizeof(m));
+                 ms.push_back(m);
+               }
+               return ms;
+             };
+             e.set_act_models(unpack(blocks), copy, unpack(opp_blocks));
            },
-           py::arg("blocks"), py::arg("copy") = false)
+           py::arg("blocks"), py::arg("copy") = false,
+           py::arg("opp_blocks") = std::vector<py::bytes>{})
       .def("act_mode", &GpuEngine::act_mode)
       .def_static("act_model_size", [] { return (int)sizeof(MbkActModel); })
       .def("inject_fault", &GpuEngine::inject_fault)

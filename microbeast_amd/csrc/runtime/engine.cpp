@@ -181,9 +181,12 @@ GpuEngine::~GpuEngine() {
   if (h_done_) hipHostFree(h_done_);
   if (h_code_list_) hipHostFree(h_code_list_);
   if (h_act_list_) hipHostFree(h_act_list_);
+  if (h_code_list_p1_) hipHostFree(h_code_list_p1_);
+  if (h_act_list_p1_) hipHostFree(h_act_list_p1_);
   if (gate_) hipFree(gate_);
   for (Lane& L : lanes_) {
     if (L.d_rows) hipFree(L.d_rows);
+    if (L.opp_scratch) hipFree(L.opp_scratch);
     for (int p = 0; p < 2; ++p) {
       if (L.ev_h2d[p]) hipEventDestroy(L.ev_h2d[p]);
       if (L.ev_done[p]) hipEventDestroy(L.ev_done[p]);
@@ -244,17 +247,25 @@ void GpuEngine::set_group_graphs(const std::vector<uintptr_t>& graphs) {
   for (uintptr_t h : graphs) group_graph_.push_back((hipGraphExec_t)h);
 }
 
-void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy) {
+void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy,
+                               const std::vector<MbkActModel>& opp_models) {
   if (running_.load()) throw std::runtime_error("set_act_models: engine running");
   if (!models.empty() && (int)models.size() != cfg_.n_lanes)
     throw std::runtime_error("set_act_models: need one model per lane");
-  if (!models.empty() && (cfg_.selfplay_groups > 0 || buf_.ep_return || buf_.ep_step ||
-                          buf_.last_action0 || buf_.logits))
-    throw std::runtime_error("set_act_models: not with self-play or reference buffer keys");
-  for (const MbkActModel& m : models)
-    if (m.E != cfg_.envs_per_group || m.H != cfg_.size || m.W != cfg_.size)
-      throw std::runtime_error("set_act_models: model block shape mismatch");
+  if (!models.empty() && (buf_.ep_return || buf_.ep_step || buf_.last_action0 || buf_.logits))
+    throw std::runtime_error("set_act_models: not with reference buffer keys");
+  const bool sp_needed = !models.empty() && cfg_.selfplay_groups > 0;
+  if (sp_needed && ((int)opp_models.size() != cfg_.n_lanes || copy))
+    throw std::runtime_error("set_act_models: self-play needs one opponent block per lane and "
+                             "the sparse (zero-copy) rows");
+  if (!sp_needed && !opp_models.empty())
+    throw std::runtime_error("set_act_models: opponent blocks without self-play groups");
+  for (const std::vector<MbkActModel>* v : {&models, &opp_models})
+    for (const MbkActModel& m : *v)
+      if (m.E != cfg_.envs_per_group || m.H != cfg_.size || m.W != cfg_.size)
+        throw std::runtime_error("set_act_models: model block shape mismatch");
   act_models_ = models;
+  opp_act_models_ = opp_models;
   act_copy_ = copy;
   // MBK_ACT_SPARSE=0: dense zero-copy codes / actions (4 + 4 MB of PCIe per 8192-env step
   // instead of ~0.5-1 MB)
@@ -271,6 +282,23 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
       throw std::runtime_error("set_act_models: hipHostMalloc of the sparse staging failed");
     std::memset(h_act_list_, 0, bytes);
     env_->write_code_lists(h_code_list_, list_stride_);  // the reset state, as lists
+  }
+  if (sp_needed) {
+    if (!sparse_) throw std::runtime_error("set_act_models: self-play needs MBK_ACT_SPARSE=1");
+    const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
+    const size_t bytes = total * list_stride_ * 4;
+    if (!h_code_list_p1_ &&
+        (hipHostMalloc((void**)&h_code_list_p1_, bytes, hipHostMallocDefault) != hipSuccess ||
+         hipHostMalloc((void**)&h_act_list_p1_, bytes, hipHostMallocDefault) != hipSuccess))
+      throw std::runtime_error("set_act_models: hipHostMalloc of the opponent rows failed");
+    std::memset(h_act_list_p1_, 0, bytes);
+    std::memset(h_code_list_p1_, 0, bytes);
+    env_->write_code_lists(h_code_list_p1_, list_stride_, 1);
+    const size_t E = cfg_.envs_per_group, sc = E * S_ * (4 + 12 + 8) + 2 * E * 4 + 256 +
+                                                 E * list_stride_ * 4;
+    for (Lane& L : lanes_)
+      if (!L.opp_scratch && hipMalloc((void**)&L.opp_scratch, sc) != hipSuccess)
+        throw std::runtime_error("set_act_models: hipMalloc of the opponent scratch failed");
   }
   // MBK_ACT_ROWS_DEV=0: launch A reads the rows over PCIe itself (no staging launch)
   const char* rd = std::getenv("MBK_ACT_ROWS_DEV");
@@ -384,7 +412,13 @@ void GpuEngine::worker_loop(int wid) {
         try {
           if (inject_fault_.exchange(0) != 0)
             throw std::runtime_error("injected env-worker fault (--fault_inject_every)");
-          if (sparse_)
+          if (sparse_ && G.selfplay)
+            G.idle.fetch_add(env_->step_range_lists_sp(a0 + e, a0 + e1, h_act_list_,
+                                                       h_act_list_p1_, h_code_list_,
+                                                       h_code_list_p1_, list_stride_, h_reward_,
+                                                       h_done_, &log_, G.opp_version),
+                             std::memory_order_relaxed);
+          else if (sparse_)
             G.idle.fetch_add(env_->step_range_lists(a0 + e, a0 + e1, h_act_list_, h_code_list_,
                                                     list_stride_, h_reward_, h_done_, &log_),
                              std::memory_order_relaxed);
@@ -565,6 +599,24 @@ bool GpuEngine::enqueue_gpu(int g) {
     {
       const auto t0 = std::chrono::steady_clock::now();
       ENG_CHECK((hipError_t)mbk_act_step(&M, &a, st));
+      if (G.selfplay) {  // the opponent acts on its own (mirrored) rows with its own weights
+        const size_t ES = E * S_;
+        uint8_t* sc = L.opp_scratch;
+        MbkActStep o{};
+        o.code_list = h_code_list_p1_ + e0 * list_stride_;
+        o.act_list = h_act_list_p1_ + e0 * list_stride_;
+        o.list_stride = list_stride_;
+        o.obs = (uint32_t*)sc;
+        o.mask = (uint32_t*)(sc + ES * 4);
+        o.action = sc + ES * 16;
+        o.logp = (float*)(sc + ES * 24);
+        o.value = (float*)(sc + ES * 24 + E * 4);
+        o.code_list_dev = L.d_rows ? (uint32_t*)(sc + ES * 24 + 2 * E * 4 + 256) : nullptr;
+        o.head_form = a.head_form;
+        o.step = L.opp_act_step++;
+        ENG_CHECK((hipError_t)mbk_act_step(&opp_act_models_[G.lane], &o, st));
+        G.opp_version = L.opp_version;
+      }
       launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                std::chrono::steady_clock::now() - t0).count(),
                            std::memory_order_relaxed);

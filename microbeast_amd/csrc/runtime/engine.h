@@ -197,8 +197,12 @@ class GpuEngine {
   // fused acting steps (mbk_act_step: two kernel launches per step, writing the rollout row
   // directly -- no policy graph, no scatter copy): one model / workspace block per lane, set
   // before start(). copy: H2D / D2H the codes and actions through the lane's device buffers
-  // instead of reading / writing the pinned host staging from the kernels.
-  void set_act_models(const std::vector<MbkActModel>& models, bool copy);
+  // instead of reading / writing the pinned host staging from the kernels. opp_models: one
+  // block per lane of the self-play opponent's inference weights (required iff self-play
+  // groups exist; sparse rows only): its step reads the opponent's mirrored code rows and
+  // writes its action rows, its rollout-shaped outputs go to lane scratch.
+  void set_act_models(const std::vector<MbkActModel>& models, bool copy,
+                      const std::vector<MbkActModel>& opp_models = {});
   bool act_mode() const { return !act_models_.empty(); }
   const EngineConfig& config() const { return cfg_; }
   VecEnv& env() { return *env_; }
@@ -253,6 +257,10 @@ class GpuEngine {
     int policy_version = 0;   // learner update of the weights landed on this lane
     uint64_t act_step = 0;    // fused steps: Philox step of the lane's next policy step
     uint32_t* d_rows = nullptr;  // sparse steps: the HBM copy of a group's input rows
+    // self-play opponent steps: HBM rows + scratch for the outputs the rollout does not keep
+    // (obs [E][S] u32, mask [E][S][3] u32, action [E][S][7] u8, logp / value [E] f32)
+    uint8_t* opp_scratch = nullptr;
+    uint64_t opp_act_step = 0;
   };
 
   EngineConfig cfg_;
@@ -328,6 +336,7 @@ class GpuEngine {
   uint32_t* gate_ = nullptr;  // policy gate flag (device), see EngineConfig
   std::vector<hipGraphExec_t> group_graph_;  // zero-copy graphs per group (may be empty)
   std::vector<MbkActModel> act_models_;      // fused acting steps per lane (may be empty)
+  std::vector<MbkActModel> opp_act_models_;  // ... and the self-play opponent's
   bool act_copy_ = false;
   // sparse PCIe form of the fused zero-copy step (VecEnv::step_range_lists): pinned rows of
   // list_stride_ uint32 per env, occupied-cell codes in, non-noop actions out
@@ -335,6 +344,8 @@ class GpuEngine {
   int list_stride_ = 0;
   uint32_t* h_code_list_ = nullptr;
   uint32_t* h_act_list_ = nullptr;
+  uint32_t* h_code_list_p1_ = nullptr;  // self-play: the opponent's rows (its own frame)
+  uint32_t* h_act_list_p1_ = nullptr;
 };
 
 }  // namespace mb

@@ -107,12 +107,64 @@ void VecEnv::step_range_codes(int e0, int e1, const uint16_t* actions, uint16_t*
   }
 }
 
-void VecEnv::write_code_lists(uint32_t* lists, int stride) const {
+void VecEnv::write_code_lists(uint32_t* lists, int stride, int player) const {
   for (size_t i = 0; i < sims_.size(); ++i) {
+    if (player != 0 && !sims_[i]->external_opponent()) continue;
     uint32_t* row = lists + i * (size_t)stride;
-    const int n = sims_[i]->write_obs_code_list(row + 1);
-    row[0] = (uint32_t)n | ((uint32_t)sims_[i]->resources(0) << 16);
+    const int n = sims_[i]->write_obs_code_list(row + 1, nullptr, player);
+    row[0] = (uint32_t)n | ((uint32_t)sims_[i]->resources(player) << 16);
   }
+}
+
+int VecEnv::step_range_lists_sp(int e0, int e1, const uint32_t* act_lists,
+                                const uint32_t* opp_lists, uint32_t* code_lists,
+                                uint32_t* code_lists_p1, int stride, float* reward, uint8_t* done,
+                                EpisodeLog* log, int opponent) {
+  const size_t S = (size_t)size_ * size_;
+  thread_local std::vector<uint16_t> dense, dense_opp;  // listed actions as cell rows
+  dense.assign(S, 0);
+  dense_opp.assign(S, 0);
+  auto expand = [&](const uint32_t* row, std::vector<uint16_t>& out, uint16_t keep) {
+    const uint32_t na = std::min<uint32_t>(row[0] & 0xFFFFu, (uint32_t)S);
+    for (uint32_t k = 1; k <= na; ++k) {
+      const uint32_t c = row[k] & 0xFFFFu;
+      if (c < S) out[c] = keep ? (uint16_t)(row[k] >> 16) : 0;
+    }
+  };
+  int idle = 0;
+  for (int i = e0; i < e1; ++i) {
+    if (i + 1 < e1) sims_[i + 1]->prefetch();
+    MicroRTSSim& sim = *sims_[i];
+    const bool sp = sim.external_opponent();
+    const uint32_t* arow = act_lists + (size_t)i * stride;
+    const uint32_t* orow = opp_lists + (size_t)i * stride;
+    expand(arow, dense, 1);
+    if (sp) expand(orow, dense_opp, 1);
+    bool d = false;
+    const float r = sp ? sim.step_packed2(dense.data(), dense_opp.data(), &d)
+                       : sim.step_packed(dense.data(), &d);
+    expand(arow, dense, 0);  // back to all-noop for the next env
+    if (sp) expand(orow, dense_opp, 0);
+    ep_ret_[i] += r;
+    ep_len_[i] += 1;
+    if (d) {
+      if (log) log->push({ep_ret_[i], ep_len_[i], base_ + i, sim.winner(),
+                          sp ? opponent : -1 - sim.bot()});
+      ep_ret_[i] = 0.f;
+      ep_len_[i] = 0;
+    }
+    reward[i] = r;
+    done[i] = d ? 1 : 0;
+    uint32_t* crow = code_lists + (size_t)i * stride;
+    const int n = sim.write_obs_code_list(crow + 1, &idle);
+    crow[0] = (uint32_t)n | ((uint32_t)sim.resources(0) << 16);
+    if (sp) {
+      uint32_t* prow = code_lists_p1 + (size_t)i * stride;
+      const int n1 = sim.write_obs_code_list(prow + 1, nullptr, 1);
+      prow[0] = (uint32_t)n1 | ((uint32_t)sim.resources(1) << 16);
+    }
+  }
+  return idle;
 }
 
 int VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,

@@ -69,10 +69,17 @@ class VecEnv {
   // Sparse PCIe form (fused acting step, zero-copy): per env a row of `stride` uint32 words,
   // word 0 = n | resources << 16, then n entries cell | value << 16. Codes out: the occupied
   // cells; actions in: the cells with a non-noop action (a cell not listed no-ops).
-  void write_code_lists(uint32_t* lists, int stride) const;
+  // player 1: the self-play envs' opponent rows (mirrored frame; other envs untouched)
+  void write_code_lists(uint32_t* lists, int stride, int player = 0) const;
   // Returns the agent's idle units over the range (the cells the next policy step samples).
   int step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t* code_lists,
                        int stride, float* reward, uint8_t* done, EpisodeLog* log);
+  // Self-play form: envs with an external opponent also take its sparse action rows
+  // (opp_lists, its mirrored frame) and emit its code rows (code_lists_p1); their finished
+  // episodes are tagged with `opponent`.
+  int step_range_lists_sp(int e0, int e1, const uint32_t* act_lists, const uint32_t* opp_lists,
+                          uint32_t* code_lists, uint32_t* code_lists_p1, int stride,
+                          float* reward, uint8_t* done, EpisodeLog* log, int opponent);
   // Self-play variant: envs with an external opponent also take its packed actions
   // (opp_actions, its mirrored frame) and emit its codes / resources; their finished
   // episodes are tagged with `opponent` (the league snapshot that was playing).

@@ -263,19 +263,26 @@ class GpuActorRuntime:
         self.engine = rt.GpuEngine(cfg, bufs)
         # fused acting steps (ops/act.py): 2 launches per policy step that write the rollout
         # row in place, instead of the captured 6-launch graph + scatter copy. Headline agent
-        # shape only (16x16, bf16 trunk); MBK_FUSED_ACT=0 keeps the graph path, MBK_ACT_COPY=1
-        # moves codes / actions through device buffers with H2D / D2H copies
+        # shape (16x16, bf16 trunk), self-play groups included (the opponent's step runs the
+        # same launches on its mirrored rows with its own weights); MBK_FUSED_ACT=0 keeps the
+        # graph path, MBK_ACT_COPY=1 moves codes / actions through device buffers with H2D /
+        # D2H copies (not with self-play)
+        act_copy = os.environ.get("MBK_ACT_COPY", "0") == "1"
         self.fused_act = (os.environ.get("MBK_FUSED_ACT", "1") == "1"
-                          and self.selfplay_groups == 0 and not self.reference_keys
-                          and not self.copy_overlap
+                          and not self.reference_keys and not self.copy_overlap
+                          and not (self.selfplay_groups > 0 and act_copy)
                           and all(act_ops.supported(ln["model"], size, fp8_policy)
                                   for ln in self.lanes))
         if self.fused_act:
             for lane in self.lanes:
                 lane["act"] = act_ops.ActWorkspace(lane["model"], E, lane["rng"], dev)
+                if self.selfplay_groups > 0:  # (packed by its captured pack graph)
+                    lane["opp_act"] = act_ops.ActWorkspace(lane["opp_model"], E,
+                                                           lane["rng_p1"], dev)
             torch.cuda.synchronize()
-            self.engine.set_act_models([ln["act"].block() for ln in self.lanes],
-                                       os.environ.get("MBK_ACT_COPY", "0") == "1")
+            self.engine.set_act_models([ln["act"].block() for ln in self.lanes], act_copy,
+                                       [ln["opp_act"].block() for ln in self.lanes
+                                        if "opp_act" in ln])
         # zero-copy policy steps (engine.h set_group_graphs): one graph per group whose decode
         # reads the group's codes / resources from the engine's pinned host staging and whose
         # pack writes its actions there (MBK_ZERO_COPY=1; self-play keeps the copy path)

@@ -66,15 +66,18 @@ def test_engine_rollout_alignment_and_learn(cuda, variant, monkeypatch):
         assert d < 1e-2
 
 
-def test_selfplay_league_engine(cuda):
-    """Self-play groups: the opponent graph drives player 1 from league snapshots; its
-    episodes come back tagged with the snapshot id; bot groups keep scripted opponents."""
+@pytest.mark.parametrize("s", [8, 16])
+def test_selfplay_league_engine(cuda, s):
+    """Self-play groups: the opponent policy drives player 1 from league snapshots; its
+    episodes come back tagged with the snapshot id; bot groups keep scripted opponents.
+    16x16: both players on the fused acting step (sparse rows, the opponent's own weight
+    block); 8x8: the captured-graph path."""
     from microbeast_amd.learner import Learner, LearnerHParams
     from microbeast_amd.models.agent import Agent
     from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
     from microbeast_amd.runtime.league import League
 
-    s, T, E = 8, 8, 16
+    T, E = 8, 16
 
     def mk():
         return Agent((s, s, 27))
@@ -83,6 +86,7 @@ def test_selfplay_league_engine(cuda):
     learner = Learner(mk(), LearnerHParams(), cuda)
     rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=E, unroll=T, batch_slots=1,
                          device=cuda, n_threads=2, max_steps=12, selfplay_groups=1, n_lanes=2)
+    assert rt.fused_act == (s == 16)
     league = League(capacity=4, snapshot_every=2, eps=0.5, seed=3)
     sid0 = league.add_snapshot(learner.flat.data)
     rt.start(learner.flat, opponent_version=sid0)

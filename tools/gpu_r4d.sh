@@ -22,3 +22,6 @@ print(sys.argv[1], r["value"], r["ms_per_step"], r.get("learner_phase_ms_rank0")
       ("act_head_in_A_frac", "gpu_phase_ms", "env_phase_ms")})
 PY
 done; done
+# config 5 (self-play league group) on the fused acting path, bf16
+timeout -k 10 300 python bench.py --steps 15 --warmup 4 --selfplay_groups 1 > gpurun_out/${tag}_c5.log 2>&1 || exit 5
+echo "c5 bf16: $(tail -1 gpurun_out/${tag}_c5.log | cut -c1-200)"
