@@ -170,6 +170,8 @@ _SIGS = {
     "mbk_act_set_stamps": [c_void_p],
     "mbk_act_set_mode": [c_int, c_int],  # (wave-owned A, fused head): -1 = environment
     "mbk_act_fused": [],
+    "mbk_rows_to_codes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
+    "mbk_codes_to_rows": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_void_p, c_void_p],
 }

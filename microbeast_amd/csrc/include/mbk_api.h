@@ -102,6 +102,12 @@ typedef struct {
 } MbkActStep;
 
 int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
+// sparse-row I/O of the captured-graph policy step (copy.hip): pinned occupied-cell rows ->
+// dense device codes + resources, and dense packed actions -> pinned non-noop action rows
+int mbk_rows_to_codes(const uint32_t* rows, int stride, int E, int S, void* codes, int32_t* res,
+                      hipStream_t stream);
+int mbk_codes_to_rows(const void* act16, int E, int S, uint32_t* rows, int stride,
+                      hipStream_t stream);
 // the two launches separately (mbk_act_step = A then B)
 int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
 int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);

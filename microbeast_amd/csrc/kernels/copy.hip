@@ -52,7 +52,78 @@ __global__ __launch_bounds__(256) void row_gather_kernel(const V* __restrict__ s
   for (int j = blockIdx.x * 256 + threadIdx.x; j < nv; j += gridDim.x * 256) d[j] = s[j];
 }
 
+// Sparse-row I/O of the captured-graph policy step (the shapes the fused acting kernel does
+// not cover: other map sizes, the deep encoder, GridNet). The env workers write occupied-cell
+// rows (word 0 = n | resources << 16, then cell | code << 16) into pinned host memory; one
+// wave per env expands its row into the graph's dense device codes through LDS (zero, scatter,
+// one coalesced store), so only a row's n + 1 words cross PCIe instead of the whole
+// [S] code row of the H2D blit copy (1.15 KB per env at 24x24).
+constexpr int kRowEnvs = 4;  // envs (waves) per workgroup
+constexpr int kRowMaxS = 1024;
+__global__ __launch_bounds__(64 * kRowEnvs) void rows_to_codes_kernel(
+    const uint32_t* __restrict__ rows, int stride, int E, int S, uint16_t* __restrict__ codes,
+    int32_t* __restrict__ res) {
+  __shared__ uint16_t lc[kRowEnvs][kRowMaxS];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int e = blockIdx.x * kRowEnvs + w;
+  if (e >= E) return;
+  uint16_t* l = lc[w];
+  for (int c = lane; c < S; c += 64) l[c] = 0;
+  const uint32_t* row = rows + (size_t)e * stride;
+  const uint32_t w0 = row[0];
+  const int n = min((int)(w0 & 0xFFFFu), S);
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the zeroing is in LDS
+  __builtin_amdgcn_wave_barrier();
+  for (int q = 1 + lane; q <= n; q += 64) {
+    const uint32_t x = row[q];
+    if ((x & 0xFFFFu) < (uint32_t)S) l[x & 0xFFFFu] = (uint16_t)(x >> 16);
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __builtin_amdgcn_wave_barrier();
+  uint16_t* out = codes + (size_t)e * S;
+  for (int c = lane; c < S; c += 64) out[c] = l[c];
+  if (lane == 0) res[e] = (int32_t)(w0 >> 16);
+}
+
+// ... and back: the graph's dense packed actions [E][S] -> the env workers' pinned action rows
+// (word 0 = n, then cell | code << 16 for the non-noop cells, ascending), one wave per env.
+__global__ __launch_bounds__(64 * kRowEnvs) void codes_to_rows_kernel(
+    const uint16_t* __restrict__ act16, int E, int S, uint32_t* __restrict__ rows, int stride) {
+  const int lane = threadIdx.x & 63;
+  const int e = blockIdx.x * kRowEnvs + (threadIdx.x >> 6);
+  if (e >= E) return;
+  const uint16_t* a = act16 + (size_t)e * S;
+  uint32_t* row = rows + (size_t)e * stride;
+  int nz = 0;
+  for (int c0 = 0; c0 < S; c0 += 64) {
+    const int c = c0 + lane;
+    const uint32_t code = c < S ? a[c] : 0u;
+    const uint64_t bal = __ballot(code != 0u);
+    if (code != 0u) row[1 + nz + __popcll(bal & ((1ull << lane) - 1ull))] = (uint32_t)c | (code << 16);
+    nz += __popcll(bal);
+  }
+  if (lane == 0) row[0] = (uint32_t)nz;
+}
+
 }  // namespace
+
+extern "C" int mbk_rows_to_codes(const uint32_t* rows, int stride, int E, int S, void* codes,
+                                 int32_t* res, hipStream_t stream) {
+  if (E <= 0) return 0;
+  if (S > kRowMaxS || stride < S + 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rows_to_codes_kernel, dim3((E + kRowEnvs - 1) / kRowEnvs),
+                     dim3(64 * kRowEnvs), 0, stream, rows, stride, E, S, (uint16_t*)codes, res);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mbk_codes_to_rows(const void* act16, int E, int S, uint32_t* rows, int stride,
+                                 hipStream_t stream) {
+  if (E <= 0) return 0;
+  if (stride < S + 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(codes_to_rows_kernel, dim3((E + kRowEnvs - 1) / kRowEnvs),
+                     dim3(64 * kRowEnvs), 0, stream, (const uint16_t*)act16, E, S, rows, stride);
+  return (int)hipGetLastError();
+}
 
 // dst[i] = src[idx[i]] for i < k (idx: device int64), rows of row_bytes (% 4 == 0)
 extern "C" int mbk_row_gather(const void* src, void* dst, const int64_t* idx, int k,

@@ -362,6 +362,8 @@ PYBIND11_MODULE(_mbrt, m) {
            py::arg("blocks"), py::arg("copy") = false,
            py::arg("opp_blocks") = std::vector<py::bytes>{})
       .def("act_mode", &GpuEngine::act_mode)
+      .def("set_sparse_io", &GpuEngine::set_sparse_io)
+      .def("sparse_io", &GpuEngine::sparse_io)
       .def_static("act_model_size", [] { return (int)sizeof(MbkActModel); })
       .def("inject_fault", &GpuEngine::inject_fault)
       .def("error", &GpuEngine::error)

@@ -247,6 +247,40 @@ void GpuEngine::set_group_graphs(const std::vector<uintptr_t>& graphs) {
   for (uintptr_t h : graphs) group_graph_.push_back((hipGraphExec_t)h);
 }
 
+// pinned sparse rows for every env (both players' for self-play envs), filled with the reset
+// state; shared by the fused acting step and the graph path's sparse I/O
+void GpuEngine::alloc_rows() {
+  if (h_code_list_) return;
+  const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
+  list_stride_ = (S_ + 1 + 3) & ~3;  // word 0 + up to S entries, 16-byte rows
+  const size_t bytes = total * list_stride_ * 4;
+  if (hipHostMalloc((void**)&h_code_list_, bytes, hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc((void**)&h_act_list_, bytes, hipHostMallocDefault) != hipSuccess)
+    throw std::runtime_error("GpuEngine: hipHostMalloc of the sparse rows failed");
+  std::memset(h_act_list_, 0, bytes);
+  env_->write_code_lists(h_code_list_, list_stride_);  // the reset state, as lists
+  if (cfg_.selfplay_groups > 0) {
+    if (hipHostMalloc((void**)&h_code_list_p1_, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&h_act_list_p1_, bytes, hipHostMallocDefault) != hipSuccess)
+      throw std::runtime_error("GpuEngine: hipHostMalloc of the opponent rows failed");
+    std::memset(h_act_list_p1_, 0, bytes);
+    std::memset(h_code_list_p1_, 0, bytes);
+    env_->write_code_lists(h_code_list_p1_, list_stride_, 1);
+  }
+}
+
+void GpuEngine::set_sparse_io(bool on) {
+  if (running_.load()) throw std::runtime_error("set_sparse_io: engine running");
+  if (!on) { sparse_ = false; return; }
+  if (act_mode()) return;  // the fused step decides itself (set_act_models)
+  if (!group_graph_.empty() || buf_.ep_return || buf_.ep_step)
+    throw std::runtime_error("set_sparse_io: not with zero-copy graphs or reference keys");
+  for (const Lane& L : lanes_)
+    if (L.overlap) throw std::runtime_error("set_sparse_io: not with copy overlap");
+  alloc_rows();
+  sparse_ = true;
+}
+
 void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy,
                                const std::vector<MbkActModel>& opp_models) {
   if (running_.load()) throw std::runtime_error("set_act_models: engine running");
@@ -273,27 +307,9 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
   const char* fm = std::getenv("MBK_ACT_FUSED_MAX");
   act_fused_max_ = std::getenv("MBK_ACT_FUSED") ? -1.f : fm ? (float)std::atof(fm) : -1.f;
   sparse_ = !models.empty() && !copy && !(sp && sp[0] == '0');
-  if (sparse_ && !h_code_list_) {
-    const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
-    list_stride_ = (S_ + 1 + 3) & ~3;  // word 0 + up to S entries, 16-byte rows
-    const size_t bytes = total * list_stride_ * 4;
-    if (hipHostMalloc((void**)&h_code_list_, bytes, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&h_act_list_, bytes, hipHostMallocDefault) != hipSuccess)
-      throw std::runtime_error("set_act_models: hipHostMalloc of the sparse staging failed");
-    std::memset(h_act_list_, 0, bytes);
-    env_->write_code_lists(h_code_list_, list_stride_);  // the reset state, as lists
-  }
+  if (sparse_) alloc_rows();
   if (sp_needed) {
     if (!sparse_) throw std::runtime_error("set_act_models: self-play needs MBK_ACT_SPARSE=1");
-    const size_t total = (size_t)cfg_.n_groups * cfg_.envs_per_group;
-    const size_t bytes = total * list_stride_ * 4;
-    if (!h_code_list_p1_ &&
-        (hipHostMalloc((void**)&h_code_list_p1_, bytes, hipHostMallocDefault) != hipSuccess ||
-         hipHostMalloc((void**)&h_act_list_p1_, bytes, hipHostMallocDefault) != hipSuccess))
-      throw std::runtime_error("set_act_models: hipHostMalloc of the opponent rows failed");
-    std::memset(h_act_list_p1_, 0, bytes);
-    std::memset(h_code_list_p1_, 0, bytes);
-    env_->write_code_lists(h_code_list_p1_, list_stride_, 1);
     const size_t E = cfg_.envs_per_group, sc = E * S_ * (4 + 12 + 8) + 2 * E * 4 + 256 +
                                                  E * list_stride_ * 4;
     for (Lane& L : lanes_)
@@ -654,7 +670,11 @@ bool GpuEngine::enqueue_gpu(int g) {
       ENG_CHECK(hipStreamWaitEvent(s_in, L.ev_done[par], 0));
     }
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], s_in));
-    if (!zc) {
+    if (sparse_) {  // occupied-cell rows -> the graph's dense codes (no blit copy)
+      ENG_CHECK((hipError_t)mbk_rows_to_codes(h_code_list_ + e0 * list_stride_, list_stride_,
+                                              (int)E, S_, (void*)in_codes, (int32_t*)in_res,
+                                              s_in));
+    } else if (!zc) {
       ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
                                hipMemcpyHostToDevice, s_in));
       ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
@@ -675,10 +695,16 @@ bool GpuEngine::enqueue_gpu(int g) {
                            std::memory_order_relaxed);
     }
     if (G.selfplay) {  // the opponent acts on its own (mirrored) view with its own weights
-      ENG_CHECK(hipMemcpyAsync((void*)io.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
-                               hipMemcpyHostToDevice, st));
-      ENG_CHECK(hipMemcpyAsync((void*)io.in_res_p1, h_res_p1_ + e0, E * 4, hipMemcpyHostToDevice,
-                               st));
+      if (sparse_) {
+        ENG_CHECK((hipError_t)mbk_rows_to_codes(h_code_list_p1_ + e0 * list_stride_,
+                                                list_stride_, (int)E, S_, (void*)io.in_codes_p1,
+                                                (int32_t*)io.in_res_p1, st));
+      } else {
+        ENG_CHECK(hipMemcpyAsync((void*)io.in_codes_p1, h_codes_p1_ + e0 * S_, E * S_ * 2,
+                                 hipMemcpyHostToDevice, st));
+        ENG_CHECK(hipMemcpyAsync((void*)io.in_res_p1, h_res_p1_ + e0, E * 4,
+                                 hipMemcpyHostToDevice, st));
+      }
       ENG_CHECK(hipGraphLaunch(L.opp_graph, st));
       G.opp_version = L.opp_version;
     }
@@ -734,12 +760,22 @@ bool GpuEngine::enqueue_gpu(int g) {
       full_cv_.notify_all();
       G.prev = -1;
     }
-    if (!zc)
-      ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
-                               hipMemcpyDeviceToHost, s_out));
-    if (G.selfplay)
-      ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1, E * S_ * 2,
-                               hipMemcpyDeviceToHost, st));
+    if (sparse_) {  // packed actions -> the env workers' non-noop action rows
+      ENG_CHECK((hipError_t)mbk_codes_to_rows((const void*)out_act16, (int)E, S_,
+                                              h_act_list_ + e0 * list_stride_, list_stride_,
+                                              s_out));
+      if (G.selfplay)
+        ENG_CHECK((hipError_t)mbk_codes_to_rows((const void*)io.out_act16_p1, (int)E, S_,
+                                                h_act_list_p1_ + e0 * list_stride_,
+                                                list_stride_, st));
+    } else {
+      if (!zc)
+        ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
+                                 hipMemcpyDeviceToHost, s_out));
+      if (G.selfplay)
+        ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1,
+                                 E * S_ * 2, hipMemcpyDeviceToHost, st));
+    }
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], s_out));
     if (L.overlap) ENG_CHECK(hipEventRecord(L.ev_d2h[par], s_out));
     ENG_CHECK(hipEventRecord(G.ev, s_out));

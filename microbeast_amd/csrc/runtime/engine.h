@@ -204,6 +204,12 @@ class GpuEngine {
   void set_act_models(const std::vector<MbkActModel>& models, bool copy,
                       const std::vector<MbkActModel>& opp_models = {});
   bool act_mode() const { return !act_models_.empty(); }
+  // captured-graph steps with sparse-row I/O (before start(); not with zero-copy graphs,
+  // copy overlap or reference keys): env workers write occupied-cell rows, one small launch
+  // expands them into the graph's device codes and another compacts its packed actions into
+  // the workers' action rows -- no H2D / D2H blit copies of dense [S] code rows
+  void set_sparse_io(bool on);
+  bool sparse_io() const { return sparse_; }
   const EngineConfig& config() const { return cfg_; }
   VecEnv& env() { return *env_; }
   bool failed() const { return failed_.load(); }
@@ -332,6 +338,7 @@ class GpuEngine {
   bool enqueue_gpu(int g);
   void dispatch_env(int g);
   void fail(const std::string& msg);
+  void alloc_rows();
   int chunk_;
   uint32_t* gate_ = nullptr;  // policy gate flag (device), see EngineConfig
   std::vector<hipGraphExec_t> group_graph_;  // zero-copy graphs per group (may be empty)

@@ -303,6 +303,15 @@ class GpuActorRuntime:
                     self._capture(io_g, lane["model"], lane["rng"]))
                 gg.append(lane["group_graphs"][-1])
             self.engine.set_group_graphs([int(x.raw_cuda_graph_exec()) for x in gg])
+        # captured-graph steps (shapes the fused step does not cover, self-play with
+        # MBK_FUSED_ACT=0, GridNet): sparse occupied-cell rows in / non-noop action rows out
+        # through two small launches instead of H2D / D2H blit copies of dense code rows
+        # (MBK_GRAPH_SPARSE=0: the dense copies)
+        self.sparse_io = (not self.fused_act and not self.zero_copy and not self.copy_overlap
+                          and not self.reference_keys
+                          and os.environ.get("MBK_GRAPH_SPARSE", "1") == "1")
+        if self.sparse_io:
+            self.engine.set_sparse_io(True)
         self.started = False
         self.frames_per_slot = E * self.T
 

@@ -193,3 +193,42 @@ def test_engine_fused_act_learns(cuda, monkeypatch):
         assert st["act_active_cells"] > 0
     finally:
         rt.stop()
+
+
+@pytest.mark.parametrize("size", [8, 10, 24])
+def test_graph_sparse_row_io(cuda, size):
+    """The captured-graph step's sparse I/O (copy.hip): pinned occupied-cell rows -> dense
+    device codes + resources, and dense packed actions -> pinned non-noop action rows, equal to
+    the host-side helpers (ops/act.py code_lists / dense_actions) on real simulator codes."""
+    from microbeast_amd.ops.act import code_lists, dense_actions
+    k = N.kernels()
+    S, E = size * size, 37
+    stride = (S + 1 + 3) & ~3
+    rt = N.runtime()
+    env = rt.VecEnv(size, E, 300, 4, [0, 1, 2, 3])
+    env.reset(0, 0)
+    rows = torch.full((E, stride), -7, dtype=torch.int32).pin_memory()
+    env.code_lists(rows.data_ptr(), stride, 0)
+    codes = torch.empty(E, S, dtype=torch.int16, device=cuda)
+    res = torch.empty(E, dtype=torch.int32, device=cuda)
+    N.check(k.mbk_rows_to_codes(rows.data_ptr(), stride, E, S, codes.data_ptr(), res.data_ptr(),
+                                N.stream_ptr()), "rows_to_codes")
+    c_ref = torch.zeros(E, S, dtype=torch.int16)
+    r_ref = torch.zeros(E, dtype=torch.int32)
+    env.obs_codes(c_ref.data_ptr(), r_ref.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(codes.cpu(), c_ref) and torch.equal(res.cpu(), r_ref)
+    g = torch.Generator().manual_seed(size)
+    act16 = torch.randint(1, 30000, (E, S), generator=g, dtype=torch.int16)
+    act16[torch.rand(E, S, generator=g) < 0.97] = 0
+    act16[0] = 0  # an env with no action at all
+    out = torch.full((E, stride), -1, dtype=torch.int32).pin_memory()
+    N.check(k.mbk_codes_to_rows(act16.to(cuda).data_ptr(), E, S, out.data_ptr(), stride,
+                                N.stream_ptr()), "codes_to_rows")
+    torch.cuda.synchronize()
+    assert int(out[0, 0]) == 0
+    assert torch.equal(dense_actions(out, S), act16)
+    ref = code_lists(act16, torch.zeros(E, dtype=torch.int32), stride)
+    n = ref[:, 0]
+    for e in range(E):  # entries ascending by cell, exactly the non-noop cells
+        assert torch.equal(out[e, :1 + int(n[e])], ref[e, :1 + int(n[e])])

@@ -25,3 +25,8 @@ done; done
 # config 5 (self-play league group) on the fused acting path, bf16
 timeout -k 10 300 python bench.py --steps 15 --warmup 4 --selfplay_groups 1 > gpurun_out/${tag}_c5.log 2>&1 || exit 5
 echo "c5 bf16: $(tail -1 gpurun_out/${tag}_c5.log | cut -c1-200)"
+# config 4 (24x24 deep encoder) and config 2 through the engine: graph path, sparse row I/O
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --size 24 --arch impala_deep > gpurun_out/${tag}_c4.log 2>&1 || exit 6
+echo "c4: $(tail -1 gpurun_out/${tag}_c4.log | cut -c1-200)"
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --size 10 --arch gridnet > gpurun_out/${tag}_c2e.log 2>&1 || exit 7
+echo "c2 engine: $(tail -1 gpurun_out/${tag}_c2e.log | cut -c1-200)"
