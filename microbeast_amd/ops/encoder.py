@@ -135,10 +135,11 @@ class HipEncoder:
         # max-pool backward folded into the stage conv's wgrad / dgrad staging: saves the
         # pre-pool gradient's HBM round trip but measured 6 % slower per update on MI355X
         # (extra expand phase + a 1-wave/SIMD dgrad variant), so off by default
-        # MBK_FUSED_POOL_BWD: 0 (default) | 1 (every stage) | s0 (stage 0 only: wgrad only,
-        # the observation layer has no dgrad)
+        # MBK_FUSED_POOL_BWD: 0 (default) | 1 (every stage) | s<digits> (those stages, e.g. s0:
+        # stage 0 only, wgrad only -- the observation layer has no dgrad; s12: stages 1, 2)
         _fp = os.environ.get("MBK_FUSED_POOL_BWD", "0")
-        self.fused_pool_bwd_stages = ({0, 1, 2, 3} if _fp == "1" else {0} if _fp == "s0"
+        self.fused_pool_bwd_stages = ({0, 1, 2, 3} if _fp == "1"
+                                      else {int(c) for c in _fp[1:]} if _fp.startswith("s")
                                       else set())
         self.fused_pool_bwd = bool(self.fused_pool_bwd_stages)
         # 16-channel residual blocks (stage 0): one fused backward launch per block

@@ -232,3 +232,55 @@ def test_graph_sparse_row_io(cuda, size):
     n = ref[:, 0]
     for e in range(E):  # entries ascending by cell, exactly the non-noop cells
         assert torch.equal(out[e, :1 + int(n[e])], ref[e, :1 + int(n[e])])
+
+
+@pytest.mark.parametrize("sparse", ["1", "0"])
+def test_engine_fused_act_logp_tracks_published_weights(cuda, monkeypatch, sparse):
+    """After publishes, a rollout acted with the fused step under version v carries behaviour
+    log-probs equal to what the learner scores with the weights of version v (the step reads
+    packed weights through pointers captured once; a publish that missed a buffer would leave
+    the actors on stale weights), for sparse and dense zero-copy rows."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
+
+    s, T, E = 16, 8, 64
+    monkeypatch.setenv("MBK_FUSED_ACT", "1")
+    monkeypatch.setenv("MBK_ACT_SPARSE", sparse)
+
+    def mk():
+        return Agent((s, s, 27))
+
+    torch.manual_seed(0)
+    learner = Learner(mk(), LearnerHParams(), cuda)
+    with torch.no_grad():  # a non-uniform policy (params are views of the flat buffer)
+        learner.model.actor.weight.normal_(0, 0.05)
+    rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=E, unroll=T, batch_slots=1,
+                         device=cuda, n_threads=2)
+    assert rt.fused_act and rt.engine.act_mode()
+    rt.start(learner.flat)
+    version, batch = 0, None
+    try:
+        for _ in range(16):
+            b, slots = rt.get_batch()
+            vers = [rt.engine.slot_version(int(x)) for x in slots]
+            if version >= 2 and min(vers) == version:
+                torch.cuda.synchronize()
+                batch = {k: v.clone() for k, v in b.items()}
+                rt.release(slots)
+                break
+            learner.learn(b)
+            rt.release(slots)
+            version += 1
+            rt.publish(learner.flat, version=version)
+    finally:
+        rt.stop()
+    assert batch is not None, "no rollout acted under the latest published weights"
+    m = learner.model
+    obs = batch["obs"].reshape((T + 1) * E, -1)
+    mask = batch["mask"][:T].reshape(T * E, s * s, 3)
+    act = batch["action"][:T].reshape(T * E, s * s, 7)
+    with torch.no_grad():
+        lp, _, _ = m.evaluate(obs, mask, act, n_score=T * E)
+    assert (mask != 0).any(-1).sum().item() > 0
+    torch.testing.assert_close(lp, batch["logp"][:T].reshape(-1), rtol=2e-2, atol=5e-2)

@@ -30,3 +30,5 @@ timeout -k 10 300 python bench.py --steps 10 --warmup 3 --size 24 --arch impala_
 echo "c4: $(tail -1 gpurun_out/${tag}_c4.log | cut -c1-200)"
 timeout -k 10 300 python bench.py --steps 10 --warmup 3 --size 10 --arch gridnet > gpurun_out/${tag}_c2e.log 2>&1 || exit 7
 echo "c2 engine: $(tail -1 gpurun_out/${tag}_c2e.log | cut -c1-200)"
+# learner: pool backward folded into the stage conv's staging, per stage set
+bash tools/lt_ab.sh ${tag}pb "MBK_FUSED_POOL_BWD=0" "MBK_FUSED_POOL_BWD=s12" "MBK_FUSED_POOL_BWD=s1" || exit 8
