@@ -602,12 +602,13 @@ bool GpuEngine::enqueue_gpu(int g) {
       a.done_dst = (uint8_t*)u8_at(buf_.done, rs, ri);
     }
     a.step = L.act_step++;
-    if (sparse_ && act_fused_max_ >= 0.f) {
+    if (sparse_) {
+      const int idle = G.idle.load(std::memory_order_relaxed);
+      act_active_cells_.fetch_add(idle, std::memory_order_relaxed);
       // the in-tile head samples a tile's cells one unit per wave: cheapest while few cells
       // are active, launch B's bucketed head wins above ~1.4 % (tools/active_sweep.py)
-      const int idle = G.idle.load(std::memory_order_relaxed);
-      a.head_form = idle <= act_fused_max_ * (float)E * (float)S_ ? 1 : 2;
-      act_active_cells_.fetch_add(idle, std::memory_order_relaxed);
+      if (act_fused_max_ >= 0.f)
+        a.head_form = idle <= act_fused_max_ * (float)E * (float)S_ ? 1 : 2;
     }
     (mbk_act_step_fused(&a) ? act_fused_steps_ : act_b_steps_)
         .fetch_add(1, std::memory_order_relaxed);
