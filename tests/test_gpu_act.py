@@ -261,14 +261,17 @@ def test_engine_fused_act_logp_tracks_published_weights(cuda, monkeypatch, spars
     rt.start(learner.flat)
     version, batch = 0, None
     try:
-        for _ in range(16):
+        for _ in range(24):
             b, slots = rt.get_batch()
             vers = [rt.engine.slot_version(int(x)) for x in slots]
-            if version >= 2 and min(vers) == version:
-                torch.cuda.synchronize()
-                batch = {k: v.clone() for k, v in b.items()}
+            if version >= 2:  # weights frozen at the last publish: wait for its rollouts
+                if min(vers) == version:
+                    torch.cuda.synchronize()
+                    batch = {k: v.clone() for k, v in b.items()}
+                    rt.release(slots)
+                    break
                 rt.release(slots)
-                break
+                continue
             learner.learn(b)
             rt.release(slots)
             version += 1
