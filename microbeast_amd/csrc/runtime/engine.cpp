@@ -316,9 +316,11 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
       if (!L.opp_scratch && hipMalloc((void**)&L.opp_scratch, sc) != hipSuccess)
         throw std::runtime_error("set_act_models: hipMalloc of the opponent scratch failed");
   }
-  // MBK_ACT_ROWS_DEV=0: launch A reads the rows over PCIe itself (no staging launch)
+  // MBK_ACT_ROWS_DEV=1: stage the rows into HBM with a small launch before launch A (off by
+  // default: it moves the PCIe time out of A -- 191 -> 172 + 30 us per 8192 envs -- and
+  // measured level on the bench, profiles/34)
   const char* rd = std::getenv("MBK_ACT_ROWS_DEV");
-  if (sparse_ && !(rd && rd[0] == '0')) {
+  if (sparse_ && rd && rd[0] == '1') {
     const size_t bytes = (size_t)cfg_.envs_per_group * list_stride_ * 4;
     for (Lane& L : lanes_)
       if (!L.d_rows && hipMalloc((void**)&L.d_rows, bytes) != hipSuccess)

@@ -25,7 +25,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 PHASES_PHASE = ["P1 codes->LDS", "P2 decode", "P3 buckets+conv0", "stage 0 res", "stage 1",
                 "stage 2", "fc + critic", "-"]
 PHASES_WAVE = (["rows + codes", "decode", "conv0 + pool + halos"]
-               + [f"conv {l}" + (" (+pool)" if l in (4, 9) else "") for l in range(14)]
+               + [("pool + halos + " if l in (5, 10) else "") + f"conv {l}" for l in range(14)]
                + ["(trunk end)", "barrier 1 wait",
                   "FC + head units + finale (MBK_ACT_FUSED=0: bucket entries)"])
 
