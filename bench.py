@@ -115,6 +115,12 @@ def main(argv=None):
                   f"by {info.world_size} ranks", file=sys.stderr)
             return 2
         args.envs_per_group //= info.world_size
+        # the per-rank group shrinks with N (8192 -> 1024 at N = 8): a lone 1024-env policy
+        # step leaves most of the GPU idle (latency-bound), so strong scaling runs the groups'
+        # steps on concurrent policy lanes -- the GPU then sees ~groups x envs_per_group envs
+        # of acting work at a time, as at N = 1 (--lanes overrides)
+        if args.lanes == 1:
+            args.lanes = min(args.groups, info.world_size)
     if info.world_size != args.gpus and info.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {info.world_size}; reporting "
               f"{info.world_size}", file=sys.stderr)

@@ -37,6 +37,8 @@ def test_bench_two_ranks_one_gpu(cuda, scaling):
     else:
         assert out["config"]["global_batch"] == 128 * 16
         assert out["config"]["envs_per_gpu"] == 2 * 64
+        # the halved groups step on concurrent policy lanes (not one latency-bound lane)
+        assert out["config"]["policy_lanes"] == 2
     print(json.dumps(out))
     assert out["policy_lag_updates"]["max"] >= 0
     assert set(out["learner_phase_ms_rank0"]) >= {"fwd", "bwd", "allreduce", "optim"}
