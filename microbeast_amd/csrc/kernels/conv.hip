@@ -551,11 +551,17 @@ __device__ __forceinline__ void pool_img16(const bf16* __restrict__ ot, size_t o
   }
 }
 
-template <int HT, int COUT>
+// WIDE: maps 17..32 pixels wide (24x24: BASELINE config 4) in 16-column blocks; the DPP pixel
+// shifts cannot cross a block, so lane 0's left and lane 15's right neighbour words come from
+// the next column block's row word (loaded uniformly); the pre-pool LDS tile drops its row
+// padding (OSTR = COUT) so 8 images of 24 x 24 x 16 fit next to the LUT (151 KB).
+template <int HT, int COUT, bool WIDE = false>
 __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int OSTR = COUT + 4, W = 16, CB = COUT / 16;
+  constexpr int OSTR = WIDE ? COUT : COUT + 4, CB = COUT / 16;
+  const int W = WIDE ? a.W : 16;
   const int H = HT > 0 ? HT : a.H, HW = H * W;
+  const int NCB = WIDE ? (W + 15) >> 4 : 1;  // column blocks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   uint4* lut = (uint4*)smem;                 // [256] byte -> 8 bf16 planes
@@ -576,11 +582,18 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   const int ngroups = (a.N + kRowImgs - 1) / kRowImgs;
   __syncthreads();  // LUT ready
   const int sh = 8 * g;
-  auto row = [&](uint32_t bits) {  // bytes this lane's 8 planes (group g) take from the LUT
+  // bytes this lane's 8 planes (group g) take from the LUT; bl / bh: the words left of lane 0
+  // and right of lane 15 (0 = the conv's zero padding; only WIDE blocks pass others)
+  auto row = [&](uint32_t bits, uint32_t bl = 0u, uint32_t bh = 0u) {
     Row3 r;
+    uint32_t lw = dpp_shr1_b(bits), hw = dpp_shl1_b(bits);
+    if (WIDE) {
+      lw = li == 0 ? bl : lw;
+      hw = li == 15 ? bh : hw;
+    }
     r.c = ((bits >> sh) & 0xFFu) * 16u;
-    r.l = ((dpp_shr1_b(bits) >> sh) & 0xFFu) * 16u;
-    r.h = ((dpp_shl1_b(bits) >> sh) & 0xFFu) * 16u;
+    r.l = ((lw >> sh) & 0xFFu) * 16u;
+    r.h = ((hw >> sh) & 0xFFu) * 16u;
     return r;
   };
   const char* lutb = (const char*)lut;
@@ -588,8 +601,8 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   // 4-row window: each row is expanded once (3 LUT reads) and serves two row pairs. (Time
   // unchanged: 2.2 ms per 524K images before and after, and with the next group's rows
   // prefetched; it scales with the MFMA count -- 4.4 ms at 32 channels.)
-  auto xrow = [&](uint32_t bits) {
-    const Row3 r = row(bits);
+  auto xrow = [&](uint32_t bits, uint32_t bl = 0u, uint32_t bh = 0u) {
+    const Row3 r = row(bits, bl, bh);
     XRow3 x;
     x.f[0].u = *(const uint4*)(lutb + r.l);
     x.f[1].u = *(const uint4*)(lutb + r.c);
@@ -602,7 +615,7 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   // one output row pair (y, y+1) from input rows y-1 .. y+2; each (row, kx) fragment feeds
   // both rows' MFMA chains (and, for 32 output channels, both channel blocks) in their tap
   // order
-  auto row_pair = [&](const XRow3 r[4], int y, int im, int img0) {
+  auto row_pair = [&](const XRow3 r[4], int y, int im, int img0, int x0 = 0) {
     f32x4 acc0[CB], acc1[CB];
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) acc0[cb] = acc1[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -624,7 +637,8 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
     for (int h = 0; h < 2; ++h) {
       const int yy = y + h;
       if (yy >= H) break;
-      const int m = yy * W + li;
+      if (WIDE && x0 + li >= W) break;
+      const int m = yy * W + x0 + li;
 #pragma unroll
       for (int cb = 0; cb < CB; ++cb) {
         const f32x4& acc = h ? acc1[cb] : acc0[cb];
@@ -675,6 +689,31 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
           r[3] = y + 4 < NR ? xrow(rows[(y + 4) % NR]) : xzero;
         }
       }
+    } else if (WIDE && wave < nimg) {
+      const int im = wave;
+      const uint32_t* xi = (const uint32_t*)a.x + (size_t)(img0 + im) * HW;
+      for (int cbk = 0; cbk < NCB; ++cbk) {
+        const int x0 = 16 * cbk;
+        const bool in = x0 + li < W, has_r = x0 + 16 < W;
+        // row yy of this column block: the lane's word and the block's two edge neighbours
+        auto xrw = [&](int yy) {
+          if (yy < 0 || yy >= H) return xzero;
+          const uint32_t* rp = xi + (size_t)yy * W;
+          return xrow(in ? rp[x0 + li] : 0u, x0 > 0 ? rp[x0 - 1] : 0u, has_r ? rp[x0 + 16] : 0u);
+        };
+        XRow3 r[4];
+        r[0] = xzero;
+        r[1] = xrw(0);
+        r[2] = xrw(1);
+        r[3] = xrw(2);
+        for (int y = 0; y < H; y += 2) {
+          row_pair(r, y, im, img0, x0);
+          r[0] = r[2];
+          r[1] = r[3];
+          r[2] = xrw(y + 3);
+          r[3] = xrw(y + 4);
+        }
+      }
     } else if (wave < nimg) {
       const int im = wave;
       const uint32_t* xb = (const uint32_t*)a.x + (size_t)(img0 + im) * HW + li;
@@ -700,7 +739,7 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
       const int Ho = (H + 1) >> 1, Wo = W >> 1;
-      if (HT == 16)
+      if (HT == 16 && !WIDE)
         pool_img16<COUT, OSTR>(otile + (size_t)wave * HW * OSTR,
                                (size_t)(img0 + wave) * Ho * Wo * COUT, a.y, a.pool_idx, lane);
       else
@@ -1469,6 +1508,15 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
       hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     const int grid = fwd_grid(ngroups, (const void*)kfn, sm);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
+    return (int)hipGetLastError();
+  }
+  // 17..32 pixels wide (config 4's 24 x 24), 16 channels: the WIDE row kernel
+  if (in_bits && cout == 16 && W > 16 && W <= 32 && !fp8 && g_conv0_row && !add && !mask_src &&
+      !relu_in && kLutBytes + (size_t)kRowImgs * H * W * 16 * 2 <= 160 * 1024) {
+    const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * W * 16 * 2 : 0);
+    const auto kfn = conv0_row_kernel<0, 16, true>;
+    const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)kfn, sm0);
+    hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();
   }
   if (in_bits && (cout == 16 || cout == 32) && W == 16 && !fp8 && g_conv0_row && !add &&

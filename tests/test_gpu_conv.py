@@ -389,35 +389,40 @@ def test_pool_bwd_idx_shapes(cuda, H, W, C):
     torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("n,pool,cout", [(203, True, 16), (7, True, 16), (9, False, 16),
-                                          (203, True, 32), (9, False, 32)])
-def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout):
+@pytest.mark.parametrize("n,pool,cout,s", [(203, True, 16, 16), (7, True, 16, 16),
+                                            (9, False, 16, 16), (203, True, 32, 16),
+                                            (9, False, 32, 16), (41, True, 16, 24),
+                                            (9, False, 16, 24), (11, True, 16, 20)])
+def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout, s):
     """The 16-wide stage-0 conv (register row window + DPP pixel shifts) runs the MFMA taps
     in the generic kernel's order: outputs, pre-pool values and argmax bytes are identical.
-    cout 32 is GridNet's first layer (two 16-channel blocks per expanded fragment)."""
+    cout 32 is GridNet's first layer (two 16-channel blocks per expanded fragment); s 24 / 20:
+    the WIDE form (16-column blocks whose edge neighbours come from the next block's word,
+    BASELINE config 4's 24x24 maps)."""
     from microbeast_amd import _native as N
     from microbeast_amd.ops.encoder import HipEncoder
     torch.manual_seed(3)
-    enc = HipEncoder(16, 16, 27, (cout, 32, 32), cuda)
+    enc = HipEncoder(s, s, 27, (cout, 32, 32), cuda)
     ws = [torch.randn(L.cout, L.cin_real, 3, 3, device=cuda) * 0.2 for L in enc.layers]
     enc.pack(ws, with_bwd=False)
     L0 = enc.layers[0]
-    obs = _random_obs_bits(n, 256, seed=n).to(cuda)
+    obs = _random_obs_bits(n, s * s, seed=n).to(cuda)
+    so = (s + 1) // 2
     b0 = torch.randn(cout, device=cuda) * 0.1
     outs = []
     for on in (1, 0):
         N.kernels().mbk_conv0_row_set(on)
         try:
             if pool:
-                cfull = torch.full((n, 16, 16, cout), 7.0, dtype=torch.bfloat16, device=cuda)
-                pidx = torch.full((n, 8, 8, cout), 255, dtype=torch.uint8, device=cuda)
+                cfull = torch.full((n, s, s, cout), 7.0, dtype=torch.bfloat16, device=cuda)
+                pidx = torch.full((n, so, so, cout), 255, dtype=torch.uint8, device=cuda)
                 p = enc._fwd(L0, obs, b0, y_full=cfull, pool_idx=pidx)
                 outs.append((p, cfull, pidx))
             else:  # raw launch without the pool (the encoder always pools stage convs)
-                y = torch.empty(n, 16, 16, cout, dtype=torch.bfloat16, device=cuda)
+                y = torch.empty(n, s, s, cout, dtype=torch.bfloat16, device=cuda)
                 N.check(N.kernels().mbk_conv_fwd(
                     obs.data_ptr(), 1, L0.cin, L0.cout, enc.packed_fwd.data_ptr() + 2 * L0.w_off,
-                    b0.data_ptr(), 0, 0, y.data_ptr(), 0, 0, n, 16, 16, 4, 0, 0,
+                    b0.data_ptr(), 0, 0, y.data_ptr(), 0, 0, n, s, s, 4, 0, 0,
                     N.stream_ptr()), "conv_fwd")
                 outs.append((y,))
         finally:
@@ -427,7 +432,7 @@ def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout):
         assert torch.equal(a, b)
     if not pool:
         from microbeast_amd.ops.obs import bits_to_planes
-        cr = F.conv2d(bits_to_planes(obs.cpu(), 16, 16), ws[0].cpu().bfloat16().float(), b0.cpu(),
+        cr = F.conv2d(bits_to_planes(obs.cpu(), s, s), ws[0].cpu().bfloat16().float(), b0.cpu(),
                       padding=1)
         torch.testing.assert_close(outs[0][0].float().cpu().permute(0, 3, 1, 2), cr, rtol=2e-2,
                                    atol=2e-2)
