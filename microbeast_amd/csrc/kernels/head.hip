@@ -1419,7 +1419,13 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  hipLaunchKernelGGL(head_act_kernel, dim3(2 * cus), dim3(256), 0, stream, a);
+  // MBK_HEAD_ACT_GRID=<workgroups per 8 CUs> (default 16 = 2 per CU): fewer, longer-lived
+  // workgroups need fewer free CU slots while the learner holds the GPU
+  static const int per8 = [] {
+    const char* e = getenv("MBK_HEAD_ACT_GRID");
+    return e && std::atoi(e) > 0 ? std::atoi(e) : 16;
+  }();
+  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * per8 / 8)), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
