@@ -21,3 +21,13 @@ a = r.get("actor_stats_per_rank", [{}])[0]
 print("head_act grid per 8 CUs", sys.argv[1], r["value"], r["ms_per_step"], r.get("learner_phase_ms_rank0"), a.get("gpu_phase_ms"))
 PY
 done
+# learner launches over 65K-image ranges (+ the policy gate): the policy step's CU access
+for v in "MBK_LEARN_CHUNK=65536" "MBK_LEARN_CHUNK=65536 MBK_POLICY_GATE=1"; do
+  env $v timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/${tag}_bench_lc.log 2>&1 || exit 4
+  python - "$v" gpurun_out/${tag}_bench_lc.log <<'PY'
+import json, sys
+r = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+a = r.get("actor_stats_per_rank", [{}])[0]
+print(sys.argv[1], r["value"], r["ms_per_step"], r.get("learner_phase_ms_rank0"), a.get("gpu_phase_ms"))
+PY
+done
