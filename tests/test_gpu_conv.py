@@ -419,10 +419,12 @@ def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout, s):
                 p = enc._fwd(L0, obs, b0, y_full=cfull, pool_idx=pidx)
                 outs.append((p, cfull, pidx))
             else:  # raw launch without the pool (the encoder always pools stage convs)
+                from microbeast_amd.ops.encoder import _imgs_fwd
                 y = torch.empty(n, s, s, cout, dtype=torch.bfloat16, device=cuda)
+                imgs = _imgs_fwd(L0, L0.cin, L0.cout, True, False)  # the generic kernel's tile
                 N.check(N.kernels().mbk_conv_fwd(
                     obs.data_ptr(), 1, L0.cin, L0.cout, enc.packed_fwd.data_ptr() + 2 * L0.w_off,
-                    b0.data_ptr(), 0, 0, y.data_ptr(), 0, 0, n, s, s, 4, 0, 0,
+                    b0.data_ptr(), 0, 0, y.data_ptr(), 0, 0, n, s, s, imgs, 0, 0,
                     N.stream_ptr()), "conv_fwd")
                 outs.append((y,))
         finally:
