@@ -104,7 +104,7 @@ _SIGS = {
     "mbk_conv_pack": [c_void_p, c_int, c_void_p],
     "mbk_head_compact": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p],
+                         c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p],
     "mbk_head_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                      c_void_p, c_void_p, c_int, c_void_p],

@@ -99,6 +99,9 @@ typedef struct {
   uint32_t* code_list_dev; // optional HBM scratch [E][list_stride]: a small row-staging
                            // launch copies each code_list row's n + 1 words here first and
                            // launch A reads them from HBM instead of over PCIe
+  uint32_t* abits;         // optional [E][S/32] active-cell bitmap of the row (bit c & 31 of
+  uint32_t* abits2;        // word c >> 5: the cell's mask is non-zero), + the obs2 copy; the
+                           // learner's head compaction then never reads the masks in full
 } MbkActStep;
 
 int mbk_act_step(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);

@@ -187,6 +187,22 @@ __global__ __launch_bounds__(1024) void head_scan_kernel(const int* __restrict__
   }
 }
 
+// head_count from a bitmap the acting step already wrote (the rollout's abits rows): 32 B
+// per frame instead of the F x S x 12 B of masks
+__global__ __launch_bounds__(256) void head_count_bits_kernel(const uint32_t* __restrict__ abits,
+                                                              int F, int S, int FB,
+                                                              int* __restrict__ cnt) {
+  const int b = blockIdx.x, nfb = gridDim.x;
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  if (c >= S) return;
+  const int SW = abits_words(S), w = c >> 5, bit = c & 31;
+  const int f0 = b * FB, f1 = min(F, f0 + FB);
+  int n = 0;
+#pragma unroll 8
+  for (int f = f0; f < f1; ++f) n += (abits[(size_t)f * SW + w] >> bit) & 1u;
+  cnt[c * nfb + b] = n;
+}
+
 // pairs[] (frame ids, grouped by cell) and pidx[f][c] of the active cells from head_count's
 // bitmap (32 B per frame at 16x16 instead of the 3 KB of masks); sampling also zeroes the
 // outputs of inactive cells
@@ -1220,19 +1236,24 @@ extern "C" int mbk_head_fb(int F) {
   return fb;
 }
 
-// abits [F][(S + 31) / 32] uint32: the active-cell bitmap the consumers of pidx read
+// abits [F][(S + 31) / 32] uint32: the active-cell bitmap the consumers of pidx read, written
+// here from the masks (abits_given 0) or already written by the acting step (1: the masks are
+// not read at all)
 extern "C" int mbk_head_compact(const uint32_t* mask, int F, int S, int* cnt, int* off,
                                 int* grp_start, int* grp_count, int* unit_cell, int* unit_row,
                                 int* chunk_cell, int* chunk_row, int* chunk_start,
                                 int* totals, int* pairs, int* pidx, uint32_t* abits,
-                                uint8_t* action_zero, float* cell_lp, float* cell_ent,
-                                hipStream_t stream) {
+                                int abits_given, uint8_t* action_zero, float* cell_lp,
+                                float* cell_ent, hipStream_t stream) {
   if (S > MAX_S) return (int)hipErrorInvalidValue;
   const int FB = mbk_head_fb(F);
   const int nfb = (F + FB - 1) / FB;
   dim3 g1(nfb, (S + 255) / 256);
   if (!abits) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_count_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, cnt, abits);
+  if (abits_given)
+    hipLaunchKernelGGL(head_count_bits_kernel, g1, dim3(256), 0, stream, abits, F, S, FB, cnt);
+  else
+    hipLaunchKernelGGL(head_count_kernel, g1, dim3(256), 0, stream, mask, F, S, FB, cnt, abits);
   // per-cell totals go to grp_count (overwritten with the same values by the scan)
   hipLaunchKernelGGL(head_cell_scan_kernel, dim3(S), dim3(256), 0, stream, cnt, nfb, off,
                      grp_count);

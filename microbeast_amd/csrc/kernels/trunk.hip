@@ -821,6 +821,8 @@ struct ActTrunkArgs {
   const uint16_t* codes;
   const int32_t* res;
   const uint32_t* code_list;  // sparse input rows (mbk_api.h MbkActStep), or null
+  uint32_t* abits;             // optional active-cell bitmap rows [E][S / 32] (+ obs2 copy)
+  uint32_t* abits2;
   uint32_t* act_list;         // sparse action rows: A writes n = 0 for envs with nothing to act
   int list_stride;
   uint32_t* obs;
@@ -851,6 +853,29 @@ struct ActTrunkArgs {
 
 constexpr int kActS = 256;  // 16x16 maps: one map row = one 16-pixel MFMA block
 constexpr int kActPre = kMaxTNI / (kThreads / 64);  // envs per wave and tile (2)
+
+// The env's active-cell bitmap row from its decode (lane l holds cells 4l .. 4l + 3, mk: their
+// mask words): word w = cells 32 w .. 32 w + 31 = lanes 8 w .. 8 w + 7, bit 4 i + q = lane
+// 8 w + i's cell q. Four ballots, then lanes 0..7 spread their byte of each to every 4th bit.
+__device__ __forceinline__ uint32_t spread4(uint32_t x) {  // bit i -> bit 4 i (8 bits)
+  x &= 0xFFu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return (x | (x << 3)) & 0x11111111u;
+}
+__device__ __forceinline__ void write_abits(const uint32_t mk[12], int lane, uint32_t* row,
+                                            uint32_t* row2) {
+  uint32_t w = 0u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint64_t b = __ballot((mk[3 * q] | mk[3 * q + 1] | mk[3 * q + 2]) != 0u);
+    w |= spread4((uint32_t)(b >> (8 * (lane & 7)))) << q;
+  }
+  if (lane < 8) {
+    row[lane] = w;
+    if (row2) row2[lane] = w;
+  }
+}
 // words of a sparse input row read in the first access (count + 31 entries: most envs); the
 // rest only for envs with more occupied cells
 constexpr int kActSpec = 32;
@@ -1077,6 +1102,8 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       const uint4 m1 = make_uint4(mk[4], mk[5], mk[6], mk[7]);
       const uint4 m2 = make_uint4(mk[8], mk[9], mk[10], mk[11]);
       *(uint4*)(lbits + el * S + c0) = o4;
+      if (a.abits) write_abits(mk, lane, a.abits + (size_t)e * (S / 32),
+                               a.abits2 ? a.abits2 + (size_t)e * (S / 32) : nullptr);
       const size_t eo = (size_t)e * S + c0;
       *(uint4*)(a.obs + eo) = o4;
       uint4* mp = (uint4*)(a.mask + eo * 3);
@@ -1495,6 +1522,8 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         const uint4 m1 = make_uint4(mk[4], mk[5], mk[6], mk[7]);
         const uint4 m2 = make_uint4(mk[8], mk[9], mk[10], mk[11]);
         *(uint4*)(lbits + j * S + c0) = o4;
+        if (a.abits) write_abits(mk, lane, a.abits + (size_t)e * (S / 32),
+                                 a.abits2 ? a.abits2 + (size_t)e * (S / 32) : nullptr);
         const size_t eo = (size_t)e * S + c0;
         *(uint4*)(a.obs + eo) = o4;
         uint4* mp = (uint4*)(a.mask + eo * 3);
@@ -2011,6 +2040,9 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.mask = s->mask;
   a.obs2 = s->obs2;
   a.mask2 = s->mask2;
+  if ((s->abits2 && !s->abits) || (s->abits2 && !s->obs2)) return (int)hipErrorInvalidValue;
+  a.abits = s->abits;
+  a.abits2 = s->abits2;
   a.action = s->action;
   a.logp = s->logp;
   a.act16 = s->act16;

@@ -279,6 +279,7 @@ PYBIND11_MODULE(_mbrt, m) {
         buf.ep_step = opt("ep_step");
         buf.last_action0 = opt("last_action0");
         buf.logits = opt("policy_logits");
+        buf.abits = opt("abits");
         auto get = [](py::dict d, const char* k) {
           return d.contains(k) ? d[k].cast<uintptr_t>() : (uintptr_t)0;
         };

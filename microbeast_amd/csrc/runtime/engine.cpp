@@ -595,6 +595,14 @@ bool GpuEngine::enqueue_gpu(int g) {
       a.mask2 = (uint32_t*)mask_at(G.prev, T);
     }
     a.action = (uint8_t*)act_at(G.cur, t);
+    if (buf_.abits) {  // [slot][T+1][E][S/32]
+      const size_t sw = (size_t)(S_ + 31) / 32;
+      auto ab_at = [&](int slot, size_t i) {
+        return (uint32_t*)buf_.abits + (slot * slot_stride_scalar_ + i * E) * sw;
+      };
+      a.abits = ab_at(G.cur, t);
+      if (close_prev) a.abits2 = ab_at(G.prev, T);
+    }
     a.logp = (float*)f32_at(buf_.logp, G.cur, t);
     a.value = (float*)f32_at(buf_.value, G.cur, t);
     if (!G.first) {

@@ -110,6 +110,9 @@ struct EngineBuffers {
   uintptr_t ep_step = 0;       // i32 [.., E]   running episode length after the step
   uintptr_t last_action0 = 0;  // u8 [n_slots, E, S, 7]: the action before row 0 of a slot
   uintptr_t logits = 0;        // f32 [.., E, 78*S] dense policy logits
+  // optional active-cell bitmap [.., E, S/32] u32 (fused acting steps write it; the learner's
+  // head compaction reads it instead of the masks)
+  uintptr_t abits = 0;
   std::vector<LaneIO> lanes;  // one per policy lane
 };
 

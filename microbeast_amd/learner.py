@@ -78,7 +78,12 @@ class Learner:
         S = mask.shape[2]
         m = mask[:T].reshape(T * B, S, mask.shape[-1])
         a = action[:T].reshape(T * B, S, action.shape[-1])
-        logp, ent, value = self.model.evaluate(flat_obs, m, a, n_score=T * B)
+        kw = {}
+        ab = batch.get("abits")
+        if ab is not None and getattr(self.model, "accepts_abits", False):
+            # the acting step's active-cell bitmap: the head compaction skips the mask pass
+            kw["abits"] = ab[:T].reshape(T * B, ab.shape[-1])
+        logp, ent, value = self.model.evaluate(flat_obs, m, a, n_score=T * B, **kw)
         vt = vtrace(logp.view(T, B), batch["logp"][:T], value.view(T1, B), batch["reward"][:T],
                     batch["done"][:T], ent.view(T, B), gamma=self.hp.gamma, rho_bar=self.hp.rho_bar,
                     c_bar=self.hp.c_bar, pg_rho_bar=self.hp.pg_rho_bar,

@@ -93,6 +93,8 @@ class Agent(nn.Module):
     ([6,4,4,4,4,7,49] * h*w) or None to derive it from the map size.
     """
 
+    accepts_abits = True  # evaluate(..., abits=): the acting step's active-cell bitmap
+
     def __init__(self, obs_space_shape=(16, 16, 27), nvec=None, mapsize=None, device="cpu",
                  channels=(16, 32, 32), hidden=256, compute_dtype=torch.bfloat16,
                  hip_kernels: bool = True):
@@ -337,11 +339,12 @@ class Agent(nn.Module):
         action, logp = cell_head.sample(logits, mask_bits, rng_state, generator)
         return action, logp, value
 
-    def evaluate(self, obs, mask_bits, action, n_score: int | None = None):
+    def evaluate(self, obs, mask_bits, action, n_score: int | None = None, abits=None):
         """Log-prob/entropy of ``action`` (first ``n_score`` rows) and values (all rows).
 
         Used by the learner on a time-major (T+1)*B batch: values are needed on
-        all T+1 rows (bootstrap), the head only on the first T*B.
+        all T+1 rows (bootstrap), the head only on the first T*B. abits: the scored rows'
+        active-cell bitmap [n_score, S/32] from the acting step (HIP learner path only).
         """
         if self._use_hip(obs) and torch.is_grad_enabled():
             # learner: trunk, then ONE autograd node for network.5 + head + critic whose
@@ -357,7 +360,7 @@ class Agent(nn.Module):
                 self._tail_maps = TailMaps(*key, y.device)
             return impala_tail(y, fc, self.critic, self.actor, mask_bits.reshape(ns, -1, 3),
                                action.reshape(ns, -1, 7), ns, self._head(y.device),
-                               self._tail_maps)
+                               self._tail_maps, abits)
         f = self.features(obs)
         if self._use_hip(obs):
             value = linear(f, self.critic).float().view(-1)

@@ -112,28 +112,36 @@ class SparseHead:
                                           N.stream_ptr()), "head_pack")
 
     def compact(self, mask_bits: torch.Tensor, F: int, action_zero: torch.Tensor | None,
-                dense_out: bool = True):
+                dense_out: bool = True, abits: torch.Tensor | None = None):
         """dense_out: zero the per-cell log-prob / entropy of inactive cells (sampling);
-        scoring keeps pair-indexed outputs and sums them through pidx instead."""
+        scoring keeps pair-indexed outputs and sums them through pidx instead. abits: the
+        frames' active-cell bitmap [F, S/32] int32 the acting step already wrote (the masks
+        are then not read here); None: built from the masks."""
         self._ensure(F)
+        if abits is not None:
+            assert abits.is_contiguous() and abits.numel() == F * ((self.S + 31) // 32)
+        self._abits = abits if abits is not None else self.abits
         N.check(N.kernels().mbk_head_compact(
             mask_bits.data_ptr(), F, self.S, self.cnt.data_ptr(), self.off.data_ptr(),
             self.grp_start.data_ptr(), self.grp_count.data_ptr(), self.unit_cell.data_ptr(),
             self.unit_row.data_ptr(), self.chunk_cell.data_ptr(), self.chunk_row.data_ptr(),
             self.chunk_start.data_ptr(), self.totals.data_ptr(), self.pairs.data_ptr(),
-            self.pidx.data_ptr(), self.abits.data_ptr(), N.ptr(action_zero),
+            self.pidx.data_ptr(), self._abits.data_ptr(), int(abits is not None),
+            N.ptr(action_zero),
             self.cell_lp.data_ptr() if dense_out else None,
             self.cell_ent.data_ptr() if dense_out else None, N.stream_ptr()), "head_compact")
 
     def forward(self, X: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor,
                 sample: bool, rng: torch.Tensor | None, logp_out: torch.Tensor | None = None,
-                ent_out: torch.Tensor | None = None, want_ent: bool = True):
+                ent_out: torch.Tensor | None = None, want_ent: bool = True,
+                abits: torch.Tensor | None = None):
         """X bf16 [F,256] contiguous. sample=True writes ``action`` (uint8 [F,S,7])."""
         F = X.shape[0]
         k = N.kernels()
         st = N.stream_ptr()
         pair_out = not sample  # scoring: pair-indexed outputs, summed per frame through pidx
-        self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out)
+        self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out,
+                     abits=abits)
         N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
                                mask_bits.data_ptr(), action.data_ptr(), N.ptr(rng), int(sample),
                                self.pairs.data_ptr(), self.unit_cell.data_ptr(),
@@ -147,7 +155,7 @@ class SparseHead:
         if want_ent:
             ent = ent_out if ent_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
         if pair_out:
-            N.check(k.mbk_head_pair_rowsum(self.pidx.data_ptr(), self.abits.data_ptr(), F,
+            N.check(k.mbk_head_pair_rowsum(self.pidx.data_ptr(), self._abits.data_ptr(), F,
                                            self.S,
                                            self.cell_lp.data_ptr(),
                                            self.cell_ent.data_ptr() if want_ent else None,
@@ -200,13 +208,13 @@ class SparseHead:
             assert h.is_contiguous() and h.shape[1] == KD and dv.dtype == torch.float32
             dh = torch.empty(R, KD, dtype=torch.bfloat16, device=X.device)
             N.check(k.mbk_head_dx_value(dXp.data_ptr(), self.pidx.data_ptr(),
-                                        self.abits.data_ptr(), F, self.S,
+                                        self._abits.data_ptr(), F, self.S,
                                         dv.data_ptr(), h.data_ptr(), wc.data_ptr(), R,
                                         dh.data_ptr(), partial.data_ptr(), partial.shape[0], st),
                     "head_dx_value")
             return dh, dW, db
         dX = torch.empty(F, KD, dtype=torch.float32, device=X.device)
-        N.check(k.mbk_head_dx_gather(dXp.data_ptr(), self.pidx.data_ptr(), self.abits.data_ptr(),
+        N.check(k.mbk_head_dx_gather(dXp.data_ptr(), self.pidx.data_ptr(), self._abits.data_ptr(),
                                      F, self.S, dX.data_ptr(), st), "head_dx_gather")
         return dX, dW, db
 

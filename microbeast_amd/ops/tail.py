@@ -69,7 +69,7 @@ class TailMaps:
 
 class _ImpalaTail(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, w5, b5, wc, bc, wa, ba, mask, action, n_score, head, maps):
+    def forward(ctx, y, w5, b5, wc, bc, wa, ba, mask, action, n_score, head, maps, abits=None):
         ctx.set_materialize_grads(False)
         n = y.shape[0]
         y2 = y.reshape(n, -1)
@@ -83,7 +83,7 @@ class _ImpalaTail(torch.autograd.Function):
                                        v.data_ptr(), N.stream_ptr()), "fc_fwd")
         fh = f[:n_score]
         head.pack(wa.detach(), ba.detach(), with_t=True)
-        logp, ent = head.forward(fh, mask, action, sample=False, rng=None)
+        logp, ent = head.forward(fh, mask, action, sample=False, rng=None, abits=abits)
         ctx.save_for_backward(y2, f, wt, mask, action)
         ctx.meta = (head, maps, n_score, y.shape)
         ctx.params = (w5, b5, wc, bc, wa, ba)
@@ -133,10 +133,11 @@ class _ImpalaTail(torch.autograd.Function):
         map_gather([(dw5, gw5, maps.grad)])
         gb5 = grad_out(b5)
         colsum(dh, O, gb5)
-        return (dy.view(yshape), gw5, gb5, gwc, gbc, gwa, gba) + (None,) * 5
+        return (dy.view(yshape), gw5, gb5, gwc, gbc, gwa, gba) + (None,) * 6
 
 
-def impala_tail(y, fc, critic, actor, mask, action, n_score, head, maps):
-    """(logp [n_score], entropy [n_score], value [n]) of the trunk output y [n, ho, wo, c]."""
+def impala_tail(y, fc, critic, actor, mask, action, n_score, head, maps, abits=None):
+    """(logp [n_score], entropy [n_score], value [n]) of the trunk output y [n, ho, wo, c].
+    abits: the scored frames' active-cell bitmap rows from the acting step (optional)."""
     return _ImpalaTail.apply(y, fc.weight, fc.bias, critic.weight, critic.bias, actor.weight,
-                             actor.bias, mask, action, n_score, head, maps)
+                             actor.bias, mask, action, n_score, head, maps, abits)

@@ -170,6 +170,11 @@ class GpuActorRuntime:
             "reward": zeros(NS, T1, E, dtype=torch.float32, device=dev),
             "done": zeros(NS, T1, E, dtype=torch.uint8, device=dev),
         }
+        # active-cell bitmap rows (32 B per 16x16 frame), written by the fused acting step:
+        # the learner's head compaction reads them instead of the [S, 3] masks (dropped from
+        # the batch below when the graph path acts)
+        if S % 32 == 0:
+            self.rb["abits"] = zeros(NS, T1, E, S // 32, dtype=torch.int32, device=dev)
         self.reference_keys = reference_keys or policy_logits
         self.emit_logits = policy_logits
         if self.reference_keys:
@@ -312,6 +317,8 @@ class GpuActorRuntime:
                           and os.environ.get("MBK_GRAPH_SPARSE", "1") == "1")
         if self.sparse_io:
             self.engine.set_sparse_io(True)
+        if not self.fused_act and "abits" in self.rb:
+            self._abits_unwritten = self.rb.pop("abits")  # (the engine holds its address)
         self.started = False
         self.frames_per_slot = E * self.T
 

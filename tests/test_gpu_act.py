@@ -94,6 +94,8 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
     rdst, ddst = torch.zeros_like(reward), torch.zeros_like(done)
     n_active = 0
     rows_dev = torch.empty(E, S + 4, dtype=torch.int32, device=cuda)  # row staging scratch
+    abits = torch.full((E, S // 32), -1, dtype=torch.int32, device=cuda)
+    abits2 = torch.full_like(abits, -1)
     for i, (codes, res) in enumerate(_codes_stream(E, 24, seed=E)):
         form = MIXED[i % len(MIXED)] if act_mode == "mixed" else 0
         io["in_codes"].copy_(codes)
@@ -110,7 +112,8 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
                     reward=reward, done=done, reward_dst=rdst, done_dst=ddst, code_list=cl,
                     act_list=act_list, head_form=form,
-                    code_list_dev=rows_dev if staged else None)
+                    code_list_dev=rows_dev if staged else None, abits=abits,
+                    abits2=abits2 if second else None)
             torch.cuda.synchronize()
             act16 = dense_actions(act_list, S).to(cuda)
             al = act_list.cpu().to(torch.int64) & 0xFFFFFFFF
@@ -119,12 +122,18 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
         else:
             ws.step(io["in_codes"], io["in_res"], obs, mask, action, logp, value, act16,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
-                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst, head_form=form)
+                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst, head_form=form,
+                    abits=abits, abits2=abits2 if second else None)
         torch.cuda.synchronize()
         assert torch.equal(obs, io["in_obs"]), f"obs planes differ at step {i}"
         assert torch.equal(mask, io["in_mask"]), f"masks differ at step {i}"
         if second:
             assert torch.equal(obs2, obs) and torch.equal(mask2, mask)
+            assert torch.equal(abits2, abits)
+        # the active-cell bitmap row = the masks' non-zero cells, bit c & 31 of word c >> 5
+        live = (mask != 0).any(-1).view(E, S // 32, 32).to(torch.int64)
+        ref = (live << torch.arange(32, device=cuda)).sum(-1)
+        assert torch.equal(abits.to(torch.int64) & 0xFFFFFFFF, ref), f"abits differ at step {i}"
         assert torch.equal(action, io["out_action"]), f"actions differ at step {i}"
         assert torch.equal(act16, io["out_act16"]), f"packed actions differ at step {i}"
         assert torch.equal(logp.view(torch.int32), io["out_logp"].view(torch.int32)), \
@@ -287,3 +296,33 @@ def test_engine_fused_act_logp_tracks_published_weights(cuda, monkeypatch, spars
         lp, _, _ = m.evaluate(obs, mask, act, n_score=T * E)
     assert (mask != 0).any(-1).sum().item() > 0
     torch.testing.assert_close(lp, batch["logp"][:T].reshape(-1), rtol=2e-2, atol=5e-2)
+
+
+
+def test_learner_update_with_acting_bitmap_is_identical(cuda):
+    """A real engine rollout carries the fused step's active-cell bitmap rows; the learner's
+    head compaction then skips its pass over the masks. The update (losses and every updated
+    parameter) is bit-identical to the one that builds the bitmap from the masks itself."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from helpers import engine_batches
+
+    from microbeast_amd.learner import Learner, LearnerHParams
+    from microbeast_amd.models.agent import Agent
+    (batch,) = engine_batches(cuda, 16, 1, groups=2, envs=64, T=8, seed=3, learn=False)
+    assert "abits" in batch
+    mask = batch["mask"]
+    T1, B, S, _ = mask.shape
+    live = (mask != 0).any(-1).view(T1, B, S // 32, 32).to(torch.int64)
+    ref = (live << torch.arange(32, device=cuda)).sum(-1)
+    assert torch.equal(batch["abits"].to(torch.int64) & 0xFFFFFFFF, ref)
+    outs = []
+    for with_bits in (True, False):
+        torch.manual_seed(11)
+        learner = Learner(Agent((16, 16, 27)), LearnerHParams(), cuda)
+        b = dict(batch) if with_bits else {k: v for k, v in batch.items() if k != "abits"}
+        losses = learner.learn(b)
+        torch.cuda.synchronize()
+        outs.append((losses.clone(), learner.flat.data.clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])

@@ -31,3 +31,13 @@ a = r.get("actor_stats_per_rank", [{}])[0]
 print(sys.argv[1], r["value"], r["ms_per_step"], r.get("learner_phase_ms_rank0"), a.get("gpu_phase_ms"))
 PY
 done
+# pipeline shape on the new acting kernel: 2 policy lanes, 3 / 5 groups
+for v in "--lanes 2" "--groups 5" "--groups 3"; do
+  timeout -k 10 300 python bench.py --steps 20 --warmup 5 $v > gpurun_out/${tag}_bench_shape.log 2>&1 || exit 5
+  python - "$v" gpurun_out/${tag}_bench_shape.log <<'PY'
+import json, sys
+r = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+a = r.get("actor_stats_per_rank", [{}])[0]
+print(sys.argv[1], r["value"], r["ms_per_step"], a.get("gpu_phase_ms"), a.get("env_phase_ms"))
+PY
+done
