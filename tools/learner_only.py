@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--no_abits", action="store_true",
+                    help="no active-cell bitmap rows in the batch (the head counts from masks)")
     a = ap.parse_args()
     import torch
 
@@ -48,6 +50,10 @@ def main():
         "reward": torch.randn(T + 1, B, device=dev, generator=g),
         "done": torch.zeros(T + 1, B, dtype=torch.uint8, device=dev),
     }
+    if not a.no_abits and S % 32 == 0:  # what the fused acting step writes with the rollout
+        live = (mask != 0).any(-1).view(T + 1, B, S // 32, 32).to(torch.int64)
+        w = (live << torch.arange(32, device=dev)).sum(-1)
+        batch["abits"] = torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
     learner.learn(batch)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
