@@ -615,12 +615,15 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   // one output row pair (y, y+1) from input rows y-1 .. y+2; each (row, kx) fragment feeds
   // both rows' MFMA chains (and, for 32 output channels, both channel blocks) in their tap
   // order
-  auto row_pair = [&](const XRow3 r[4], int y, int im, int img0, int x0 = 0) {
+  // skip: the pair's four input rows are all zero (a padded map's rows, e.g. GridNet's 10x10
+  // maps padded to 16): the MFMA sums are exactly +0, so only the bias is written
+  auto row_pair = [&](const XRow3 r[4], int y, int im, int img0, int x0 = 0, bool skip = false) {
     f32x4 acc0[CB], acc1[CB];
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) acc0[cb] = acc1[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      if (skip) break;
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const Frag8& f = r[q].f[kx];
@@ -682,7 +685,10 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
         r[3] = NR > 2 ? xrow(rows[2 % NR]) : xzero;
 #pragma unroll
         for (int y = 0; y < NR; y += 2) {
-          row_pair(r, y, wave, img0);
+          const uint32_t any = (y >= 1 ? rows[(y + NR - 1) % NR] : 0u) | rows[y % NR] |
+                               (y + 1 < NR ? rows[(y + 1) % NR] : 0u) |
+                               (y + 2 < NR ? rows[(y + 2) % NR] : 0u);
+          row_pair(r, y, wave, img0, 0, __ballot(any != 0u) == 0ull);
           r[0] = r[2];
           r[1] = r[3];
           r[2] = y + 3 < NR ? xrow(rows[(y + 3) % NR]) : xzero;

@@ -392,13 +392,17 @@ def test_pool_bwd_idx_shapes(cuda, H, W, C):
 @pytest.mark.parametrize("n,pool,cout,s", [(203, True, 16, 16), (7, True, 16, 16),
                                             (9, False, 16, 16), (203, True, 32, 16),
                                             (9, False, 32, 16), (41, True, 16, 24),
-                                            (9, False, 16, 24), (11, True, 16, 20)])
+                                            (9, False, 16, 24), (11, True, 16, 20),
+                                            (37, True, 32, -16)])
 def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout, s):
     """The 16-wide stage-0 conv (register row window + DPP pixel shifts) runs the MFMA taps
     in the generic kernel's order: outputs, pre-pool values and argmax bytes are identical.
     cout 32 is GridNet's first layer (two 16-channel blocks per expanded fragment); s 24 / 20:
     the WIDE form (16-column blocks whose edge neighbours come from the next block's word,
-    BASELINE config 4's 24x24 maps)."""
+    BASELINE config 4's 24x24 maps); s -16: a 10x10 map zero-padded to 16x16 (GridNet's first
+    layer), whose all-zero row windows skip their MFMAs."""
+    padded = s < 0
+    s = abs(s)
     from microbeast_amd import _native as N
     from microbeast_amd.ops.encoder import HipEncoder
     torch.manual_seed(3)
@@ -407,6 +411,9 @@ def test_conv0_row_kernel_bit_identical_to_generic(cuda, n, pool, cout, s):
     enc.pack(ws, with_bwd=False)
     L0 = enc.layers[0]
     obs = _random_obs_bits(n, s * s, seed=n).to(cuda)
+    if padded:
+        obs.view(n, s, s)[:, 10:] = 0
+        obs.view(n, s, s)[:, :, 10:] = 0
     so = (s + 1) // 2
     b0 = torch.randn(cout, device=cuda) * 0.1
     outs = []
