@@ -543,7 +543,9 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
     }
     if constexpr (STAGE) {
       // ---- next stage's conv (16 -> 32) over y1 in Tx -> bf16 staging (Tu) -> pooled output
-      constexpr int NB = 2, OSTR = 2 * C + 4;
+      // (12-wide maps, BASELINE config 4's 24x24 stage 0: unpadded rows, so the staging still
+      // fits the relu(u) tile it aliases: 12 x 12 x 64 B <= 14 x 14 x 48 B)
+      constexpr int NB = 2, OSTR = WC == 12 ? 2 * C : 2 * C + 4;
       bf16* otile = (bf16*)Tu;
       Frag8 ws[NCH][NB];  // L2 reads per round (10 KB, every workgroup): keeps the persistent
       float bsv[NB][4];   // registers at the 4-layer set (occupancy 3 waves / SIMD)
@@ -1043,7 +1045,8 @@ static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const bool st = a.ws != nullptr;
   // the stage conv's pre-pool staging [imgs*H*W][36] bf16 lives in Tu
-  if (st && (size_t)imgs * H * W * (2 * C + 4) * 2 > sm / 2) return (int)hipErrorInvalidValue;
+  if (st && (size_t)imgs * H * W * (W == 12 ? 2 * C : 2 * C + 4) * 2 > sm / 2)
+    return (int)hipErrorInvalidValue;
   auto kfn = st ? (W == 8 ? res_fwd16_kernel<8, true> : W == 5 ? res_fwd16_kernel<5, true>
                    : W == 12 ? res_fwd16_kernel<12, true> : W == 4 ? res_fwd16_kernel<4, true>
                    : res_fwd16_kernel<0, true>)

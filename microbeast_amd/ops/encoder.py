@@ -476,8 +476,10 @@ class HipEncoder:
                 Ln = self.layers[li + 5] if li + 5 < len(self.layers) else None
                 if (self.fused_stage_fwd and Ln is not None and Ln.cin == 16 and Ln.cout == 32
                         and Ln.pool and not Ln.bits
-                        # its pre-pool staging aliases the relu(u) tile (8x8, 5x5: fits)
-                        and Ln.H * Ln.W * 72 <= (Ln.H + 2) * (Ln.W + 2) * 48):
+                        # its pre-pool staging aliases the relu(u) tile (8x8, 5x5: fits;
+                        # 12x12 with unpadded 64-byte staging rows)
+                        and Ln.H * Ln.W * (64 if Ln.W == 12 else 72)
+                        <= (Ln.H + 2) * (Ln.W + 2) * 48):
                     u0, y0, u1, y1, nxt = self._res_fwd16(li, p, [b.detach() for b in bs],
                                                           stage=save)
                 else:
