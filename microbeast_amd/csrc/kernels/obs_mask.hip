@@ -79,13 +79,17 @@ __global__ __launch_bounds__(512) void decode_obs_mask_kernel(const uint16_t* __
       const uint16_t* ce = codes + (size_t)e * S;
       if (vec4) *(uint2*)(cs + c0) = *(const uint2*)(ce + c0);
       else
-        for (int c = c0; c < c1; ++c) cs[c] = ce[c];
+        for (int c = lane; c < S; c += 64) cs[c] = ce[c];  // coalesced
     }
     __syncthreads();
     if (live) {
       const int r = res[e];
       uint32_t ob[4], mk[12];
-      for (int c = c0; c < c1; ++c) {
+      // 16x16: 4 consecutive cells per lane (one 16-byte store each); other sizes: cells
+      // lane, lane + 64, ... so a wave's obs / mask stores are coalesced (the contiguous split
+      // strided them Q cells apart: 9 at 24x24)
+      const int cstart = vec4 ? c0 : lane, cend = vec4 ? c1 : S, cstep = vec4 ? 1 : 64;
+      for (int c = cstart; c < cend; c += cstep) {
         uint32_t w[3];
         cell_mask(cs, c, H, W, r, w);
         const uint32_t bits = code_bits(cs[c]);
