@@ -18,7 +18,7 @@ def _legal(mask_bits, gen):
     return a
 
 
-@pytest.mark.parametrize("s", [8, 16])
+@pytest.mark.parametrize("s", [8, 10, 16, 24])
 def test_gpu_mask_matches_simulator(cuda, s):
     rt = N.runtime()
     n, S = 32, s * s
