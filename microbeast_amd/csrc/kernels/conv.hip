@@ -799,8 +799,12 @@ inline size_t wg_tile_bytes(int cin, int cout, int imgs, int H, int W, int wt) {
   const int rbd = wt * cout * 2 + (cout == 32 ? 32 : 128);
   return (size_t)imgs * (H + 2) * rbx + 64 + (size_t)imgs * H * rbd + 64;
 }
-// the band-layout instantiation for this shape (0: the plain layout)
-inline int wg_band_w(int H, int W) { return (W == 16 || W == 8) && H % 4 == 0 ? W : 0; }
+// the band-layout instantiation for this shape (0: the plain layout); 24 (config 4's 24x24
+// stage 0): three 8-column chunks per band, and 24 x XPB / DPB keep the 8 / 16-wide rows'
+// residues mod 256 bytes, so the tr reads stay conflict-free
+inline int wg_band_w(int H, int W) {
+  return (W == 16 || W == 8 || W == 24) && H % 4 == 0 ? W : 0;
+}
 
 // Persistent over image rounds (grid = occupancy-sized, one partial per workgroup).
 // Both GEMM operands come from NHWC LDS tiles through ds_read_b64_tr_b16 (band layout
@@ -1597,6 +1601,7 @@ template <int CI, int CO, bool B>
 const void* wgrad_kfn(int H, int W, bool unpool) {
   if (unpool) return (const void*)conv_wgrad_kernel<CI, CO, B, true>;
   switch (wg_band_w(H, W)) {
+    case 24: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 24>;
     case 16: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 16>;
     case 8: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 8>;
     default: return (const void*)conv_wgrad_kernel<CI, CO, B>;

@@ -90,8 +90,8 @@ def _imgs_wgrad(layer: ConvLayer) -> int:
     xepp = 1 if layer.bits else layer.cin // 8
     dch = layer.cout // 8
     imgs = max(1, min(_PF_WGRAD // (hw * xepp), _PF_WGRAD // (hw * dch)))
-    # LDS per image: conv.hip wg_tile_bytes (band layout on 8 / 16-wide maps pads the rows)
-    if layer.W in (8, 16) and layer.H % 4 == 0:
+    # LDS per image: conv.hip wg_tile_bytes (band layout on 8 / 16 / 24-wide maps pads the rows)
+    if layer.W in (8, 16, 24) and layer.H % 4 == 0:
         rbx = (layer.W + 2) * layer.cin * 2 + (32 if layer.cin == 32 else 64)
         rbd = layer.W * layer.cout * 2 + (32 if layer.cout == 32 else 128)
         per = (layer.H + 2) * rbx + layer.H * rbd

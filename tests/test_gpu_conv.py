@@ -82,7 +82,10 @@ def test_single_conv_layers_exact_structure(cuda):
     torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
 
 
-def test_pool_bwd_and_l0_wgrad(cuda):
+@pytest.mark.parametrize("s", [16, 24])
+def test_pool_bwd_and_l0_wgrad(cuda, s):
+    """pool backward vs autograd; the bit-plane layer's weight gradient (band layout on 16-
+    and 24-wide maps) vs F.conv2d's"""
     from microbeast_amd import _native as N
     from microbeast_amd.ops.encoder import HipEncoder
     from microbeast_amd.ops.obs import bits_to_planes
@@ -99,14 +102,14 @@ def test_pool_bwd_and_l0_wgrad(cuda):
     F.max_pool2d(ct, 3, 2, 1).backward(dp.float().permute(0, 3, 1, 2))
     torch.testing.assert_close(dc.float().cpu(), ct.grad.permute(0, 2, 3, 1), rtol=1e-2, atol=1e-2)
     # wgrad of the bit-plane input layer
-    enc = HipEncoder(16, 16, 27, (16, 32, 32), cuda)
+    enc = HipEncoder(s, s, 27, (16, 32, 32), cuda)
     L0 = enc.layers[0]
-    obs = _random_obs_bits(4, 256, seed=7)
-    dy = torch.randn(4, 16, 16, 16).bfloat16()
+    obs = _random_obs_bits(4, s * s, seed=7)
+    dy = torch.randn(4, s, s, 16).bfloat16()
     dw = torch.zeros(16, 27, 3, 3, device=cuda)
     db = torch.zeros(16, device=cuda)
     enc._wgrad(L0, obs.to(cuda), dy.to(cuda), dw, db)
-    planes = bits_to_planes(obs, 16, 16)
+    planes = bits_to_planes(obs, s, s)
     wt = torch.zeros(16, 27, 3, 3, requires_grad=True)
     bt = torch.zeros(16, requires_grad=True)
     F.conv2d(planes, wt, bt, padding=1).backward(dy.float().permute(0, 3, 1, 2))
