@@ -2080,12 +2080,12 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.done_dst = s->done_dst;
   a.stamps = g_act_stamps;
   a.fused = mbk_act_step_fused(s);
-  a.step = s->step;  // (Philox step of the in-A head; every form: the tile queue's parity)
   if (a.fused) {
     if (!m->Wp || !m->bp || !m->rng) return (int)hipErrorInvalidValue;
     a.Wp = (const bf16*)m->Wp;
     a.bp = m->bp;
     a.rng = m->rng;
+    a.step = s->step;
   }
   static int cus = 0;
   if (!cus) {
