@@ -66,8 +66,7 @@ typedef struct {
                            // the other half (step t-1's, read by its launch B)
   int* bucket;             // [S][E]
   uint64_t* cellx;         // [E][S] per active cell (rank k): {log-prob, cell | action << 16}
-  int* pending;            // [2E + 2]: active cells not yet sampled, then each env's total,
-                           // then launch A's tile queue counters (by step parity)
+  int* pending;            // [2E]: active cells not yet sampled, then each env's total
   int E, H, W;
 } MbkActModel;
 

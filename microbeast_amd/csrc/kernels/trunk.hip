@@ -1048,11 +1048,8 @@ __global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
       if (tid < nimg) lres[tid] = a.res[img0 + tid];
     }
     if (tid < 256) ((uint4*)lut)[tid] = mbk::bits8_bf16((uint32_t)tid);
-    if (blockIdx.x == 0 && grp == 0) {  // the previous step's launch B is done with these
+    if (blockIdx.x == 0 && grp == 0)  // the previous step's launch B is done with these
       for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
-      // the wave-owned kernel's tile queue of the next step (the forms may alternate)
-      if (tid == 0) a.pending[2 * E + (int)((a.step + 1) & 1)] = 0;
-    }
     for (int c = tid; c < S; c += kThreads) lcnt[c] = 0;
     if (tid == 0) *npairs = 0;
     if (tid < nimg) {
@@ -1376,19 +1373,6 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   for (int c = tid; c < 2 * S; c += kThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
   if (tid < 2) ((int*)(trunk_smem + kWNp))[tid] = 0;
   const bool fused = a.fused != 0;
-  // Tiles come from a per-step atomic queue (pending[2E + step parity]), not blockIdx: under
-  // the learner only some CUs have room for a 154 KB tile, and the workgroups that run take the
-  // tiles the unscheduled ones would have held; a late workgroup finds the queue empty and
-  // exits. Each workgroup holds its next tile one ahead (its rows are prefetched).
-  int* tctr = a.pending + 2 * E + (int)(a.step & 1);
-  int* tq0 = (int*)(trunk_smem + kWNp) + 2;  // [2] the first two tiles
-  int* tq = (int*)(trunk_smem + kWMisc) + 17;  // [2] next-next tile per tile parity (free ints
-                                               // after ncells + env_n[16])
-  int cur_t = 0, nxt_t = 0, nxt2 = 0;
-  if (tid == 0) {
-    tq0[0] = atomicAdd(tctr, 1);
-    tq0[1] = atomicAdd(tctr, 1);
-  }
   int* ncells = (int*)(trunk_smem + kWMisc);  // fused: distinct active cells of the tile
   int* env_n = ncells + 1;                    // fused: active cells per env of the tile
   uint16_t* cellunit = (uint16_t*)(trunk_smem + kWCellU);
@@ -1399,14 +1383,11 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
     // the previous step's launch B is done with these (zeroed in both forms: the engine
     // picks the form per step, and the next B-form step counts into this half)
     for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
-    if (tid == 0) a.pending[2 * E + (int)((a.step + 1) & 1)] = 0;  // the next step's queue
   }
   mbk::lds_barrier();
-  cur_t = tq0[0];
-  nxt_t = tq0[1];
   uint32_t pre0 = 0u, pre1 = 0u;  // this wave's rows (first words) for the current tile
-  if (a.code_list && cur_t < ngroups) {
-    const int en = cur_t * TNI + wave * kWEnv;
+  if (a.code_list && (int)blockIdx.x < ngroups) {
+    const int en = blockIdx.x * TNI + wave * kWEnv;
     pre0 = (en < E && pl) ? a.code_list[(size_t)en * a.list_stride + lane] : 0u;
     pre1 = (en + 1 < E && pl) ? a.code_list[(size_t)(en + 1) * a.list_stride + lane] : 0u;
   }
@@ -1423,10 +1404,8 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
     ACT_STAMP(4 + (l));                                                                  \
   } while (0)
   int k = 0;
-  for (; cur_t < ngroups; ++k, cur_t = nxt_t, nxt_t = nxt2) {
-    const int grp = cur_t;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x, ++k) {
     const int par = k & 1;
-    if (tid == 0) tq[par] = atomicAdd(tctr, 1);  // the tile after nxt_t (read after the barrier)
     int* lcnt = (int*)(trunk_smem + kWCnt) + par * S;
     int* np = (int*)(trunk_smem + kWNp) + par;
     uint32_t* lst = (uint32_t*)(trunk_smem + kWLst) + par * kWList;
@@ -1458,7 +1437,7 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
       }
       const uint32_t cur0 = pre0, cur1 = pre1;
       if (a.code_list) {
-        const int en = nxt_t * TNI + e0;  // (nxt_t >= ngroups: en >= E, nothing read)
+        const int en = img0 + gridDim.x * TNI + e0;
         pre0 = (en < E && pl) ? a.code_list[(size_t)en * a.list_stride + lane] : 0u;
         pre1 = (en + 1 < E && pl) ? a.code_list[(size_t)(en + 1) * a.list_stride + lane] : 0u;
       }
@@ -1641,7 +1620,6 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
       if (tid == 0) ((int*)(trunk_smem + kWNp))[par ^ 1] = 0;
     }
     const int npr = *np;
-    nxt2 = tq[par];  // written by thread 0 at this tile's start, before the barrier above
     uint16_t* urows = (uint16_t*)(trunk_smem + kWHrows);
     if (fused) {  // each pair's (env, rank) into its unit's row slot
       for (int i = tid; i < npr; i += kThreads) {

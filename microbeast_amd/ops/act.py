@@ -100,9 +100,7 @@ class ActWorkspace:
         self.head = head
         self.feat = torch.empty(E, 256, dtype=torch.bfloat16, device=device)
         self.cellx = torch.zeros(E * S, dtype=torch.int64, device=device)
-        # per-env pending counters + active totals, then the wave-owned launch A's two tile
-        # queue counters (step parity)
-        self.pending = torch.zeros(2 * E + 4, dtype=torch.int32, device=device)
+        self.pending = torch.zeros(2 * E, dtype=torch.int32, device=device)  # + active totals
         # per-cell bucket counters, double-buffered by step parity (mbk_api.h bucket_cnt)
         self.bucket_cnt = torch.zeros(2 * S, dtype=torch.int32, device=device)
         self.rng = rng
