@@ -108,6 +108,9 @@ _SIGS = {
     "mbk_head_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                      c_void_p, c_void_p, c_int, c_void_p],
+    "mbk_head_score": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                       c_void_p],
     "mbk_head_pair_rowsum": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "mbk_head_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

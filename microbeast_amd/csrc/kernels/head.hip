@@ -1045,6 +1045,167 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
   }
 }
 
+// ------------------------------------------------------------------ learner scoring
+// The learner's forward over the compacted pairs (pair-indexed log-prob / entropy of the given
+// actions; head_pair_rowsum sums them per frame). head_fwd_kernel's 16-pair units read all of
+// W_c (40 KB) from L2 per unit and ran the 78-logit epilogue on 16 lanes of 64 (560 us per
+// 524K-frame update). Here a workgroup takes a contiguous range of 256-row work items (half of
+// one 512-pair chunk of one cell), so W_c is staged in LDS once per cell run. Each wave MFMAs
+// its 64 rows as four 16-row blocks (A straight from X, B from LDS), parks the logits in its
+// LDS tile and reads them back one row per lane: the epilogue (cell_forward, the sampling
+// path's) then runs on all 64 lanes. (A C-layout epilogue -- a row's 16 lanes reducing each
+// segment by DPP -- issued ~8x the VALU instructions per row: 356 us, VALU-bound.)
+constexpr int HS_NW = 4, HS_TM = 64 * HS_NW, HS_IPC = CHUNK / HS_TM;  // items per chunk
+constexpr int HS_ZS = NP + 1;                        // Z tile row stride (floats): conflict-free
+constexpr int HS_LZ = 80 * HB_RW;                    // per-wave Z tiles [64][HS_ZS] f32
+constexpr int HS_LDS = HS_LZ + HS_NW * 64 * HS_ZS * 4;
+
+__global__ __launch_bounds__(64 * HS_NW, 1) void head_score_kernel(
+    const bf16* __restrict__ X, const bf16* __restrict__ Wp, const float* __restrict__ bp,
+    const uint32_t* __restrict__ mask, const uint8_t* __restrict__ action,
+    const int* __restrict__ pairs, const int* __restrict__ grp_start,
+    const int* __restrict__ grp_count, const int* __restrict__ chunk_cell,
+    const int* __restrict__ chunk_row, const int* __restrict__ totals, int S,
+    float* __restrict__ plp, float* __restrict__ pent) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wl = smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  float* zt = (float*)(smem + HS_LZ) + wave * 64 * HS_ZS;
+  // items: HS_IPC per chunk (rows 0, HS_TM, .. of it); workgroup b takes items [b q, b q + q)
+  const int nitems = HS_IPC * totals[2];
+  const int q = (nitems + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int i0 = (int)blockIdx.x * q, i1 = min(nitems, i0 + q);
+  const int sq = tid & 31, sr0 = tid >> 5;  // W staging: 16-byte chunk sq of rows sr0 + RS k
+  float bcol[5];
+  int wc = -1;
+  // item cursor: the next non-empty item from it on (it == i1: none), its cell, this wave's
+  // first row and row count, and the frame of row `lane` (loaded one item ahead)
+  struct Item {
+    int it, c, rb, nr, f;
+  };
+  auto item_at = [&](int it) {
+    Item u{i1, 0, 0, 0, -1};
+    for (; it < i1; ++it) {
+      const int ch = it / HS_IPC, t0 = (it % HS_IPC) * HS_TM;
+      const int c = chunk_cell[ch], g0 = chunk_row[ch];
+      const int n = min(CHUNK, grp_start[c] + grp_count[c] - g0);
+      if (t0 >= n) continue;  // workgroup-uniform
+      u.it = it;
+      u.c = c;
+      u.rb = g0 + t0 + 64 * wave;
+      u.nr = min(64, n - t0 - 64 * wave);
+      u.f = lane < u.nr ? pairs[u.rb + lane] : -1;
+      break;
+    }
+    return u;
+  };
+  Item nx = item_at(i0);
+  while (nx.it < i1) {
+    const Item cu = nx;
+    const int c = cu.c, rb = cu.rb, nr = cu.nr, f = cu.f;
+    // this lane's row: mask words and the words holding its 7 action bytes
+    uint32_t m[3] = {0u, 0u, 0u}, aw[3] = {0u, 0u, 0u};
+    int ab = 0;
+    if (f >= 0) {
+      const size_t fc = (size_t)f * S + c;
+      m[0] = mask[fc * 3]; m[1] = mask[fc * 3 + 1]; m[2] = mask[fc * 3 + 2];
+      const size_t ab0 = fc * kComps;
+      const uint32_t* aw4 = (const uint32_t*)(action + (ab0 & ~(size_t)3));
+      aw[0] = aw4[0]; aw[1] = aw4[1]; aw[2] = (ab0 & 3) >= 2 ? aw4[2] : 0u;
+      ab = (int)(ab0 & 3);
+    }
+    nx = item_at(cu.it + 1);  // the next item's frames: in flight through this one
+    if (c != wc) {  // stage W_c (rows 0..79) once per run of the cell's items
+      // (rare: a workgroup's items are contiguous, so this runs once or twice per workgroup)
+      constexpr int RS = 64 * HS_NW / 32;  // rows per pass
+      const uint4* src = (const uint4*)(Wp + (size_t)c * NP * KD) + sr0 * (KD / 8) + sq;
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) bcol[nb] = bp[(size_t)c * NP + nb * 16 + li];
+      lds_barrier();  // every wave is done with the previous W_c
+#pragma unroll
+      for (int k = 0; k < 80 / RS; ++k)
+        *(uint4*)(wl + hb_phi(sr0 + RS * k) * HB_RW + sq * 16) = src[RS * k * (KD / 8)];
+      wc = c;
+      lds_barrier();  // W_c staged
+    }
+    if (nr <= 0) continue;  // wave-uniform: a partial item's idle waves
+    // ---- Z = X W_c^T + b for the wave's 4 row blocks -> Z tile (C layout: lane (li, G) holds
+    // column nb*16+li of rows 16 mb + 4G+i); the next block's A fragments load during each GEMM
+    uint4 xa[2][KD / 32];
+    auto load_a = [&](int mb, uint4 (&d)[KD / 32]) {
+      const int fr = __shfl(f, 16 * mb + li, 64);
+      const uint4* xr = (const uint4*)(X + (size_t)max(fr, 0) * KD) + G;
+#pragma unroll
+      for (int ks = 0; ks < KD / 32; ++ks) d[ks] = fr >= 0 ? xr[ks * 4] : make_uint4(0, 0, 0, 0);
+    };
+    load_a(0, xa[0]);
+#pragma unroll
+    for (int mb = 0; mb < 4; ++mb) {
+      if (mb + 1 < 4 && 16 * (mb + 1) < nr) load_a(mb + 1, xa[(mb + 1) & 1]);
+      if (16 * mb >= nr) break;  // wave-uniform
+      f32x4 z[5];
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) z[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KD / 32; ++ks) {
+        Frag8 a;
+        a.u = xa[mb & 1][ks];
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) {
+          Frag8 b;
+          b.u = *(const uint4*)(wl + hb_phi(nb * 16 + li) * HB_RW + ks * 64 + 16 * G);
+          z[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, z[nb], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zt[(16 * mb + 4 * G + i) * HS_ZS + nb * 16 + li] = z[nb][i] + bcol[nb];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's Z tile writes are done
+    __builtin_amdgcn_wave_barrier();
+    // ---- one row per lane: the 78 logits into registers, then the masked cell epilogue
+    if (lane < nr) {
+      float zr[kCell];
+      const float* zrow = zt + lane * HS_ZS;
+#pragma unroll
+      for (int j = 0; j < kCell; ++j) zr[j] = zrow[j];
+      // cell_forward's scoring with the action's logit read from the tile (a register array
+      // indexed by the action would live in scratch)
+      float lp = 0.f, ent = 0.f;
+#pragma unroll
+      for (int k = 0; k < kComps; ++k) {
+        const int off = seg_off(k), n = seg_off(k + 1) - off;
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < n; ++j)
+          if (mask_bit(m, off + j)) mx = fmaxf(mx, zr[off + j]);
+        if (mx == -INFINITY) continue;  // fully masked segment: log-prob 0, entropy 0
+        float sm = 0.f, sz = 0.f;
+#pragma unroll
+        for (int j = 0; j < n; ++j) {
+          const float e = mask_bit(m, off + j) ? __expf(zr[off + j] - mx) : 0.f;
+          sm += e;
+          sz += e * zr[off + j];
+        }
+        const float lse = mx + __logf(sm);
+        ent += lse - sz * (1.f / sm);
+        const int bi = ab + k;
+        const uint32_t w = bi < 4 ? aw[0] : bi < 8 ? aw[1] : aw[2];
+        const int a = (int)((w >> (8 * (bi & 3))) & 0xFFu);
+        const uint32_t mj = (uint32_t)(off + a);
+        const uint32_t mwd = mj < 32 ? m[0] : mj < 64 ? m[1] : m[2];
+        const bool valid = a < n && ((mwd >> (mj & 31)) & 1u);
+        lp += (valid ? zrow[off + a] : -1e8f) - lse;
+      }
+      plp[rb + lane] = lp;
+      if (pent) pent[rb + lane] = ent;
+    }
+    __builtin_amdgcn_wave_barrier();  // the Z tile is rewritten by the next item
+  }
+}
+
 // dW[c*78+n][d] = sum over the cell's chunks (fixed order); zero for idle cells
 __global__ __launch_bounds__(256) void head_dw_reduce_kernel(const float* __restrict__ dWp,
                                                              const float* __restrict__ dbp,
@@ -1357,6 +1518,29 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
   dim3 g2((kCell * KD + kCell + 255) / 256, S);
   hipLaunchKernelGGL(head_dw_reduce_kernel, g2, dim3(256), 0, stream, dWp, dbp, chunk_start,
                      grp_count, S, dW, db);
+  return (int)hipGetLastError();
+}
+
+// Learner scoring of the compacted pairs (head_score_kernel): pair-indexed log-prob and
+// entropy (pent may be null) of the given actions over the backward's chunk list, one 127 KB
+// workgroup per CU (no host sync: the chunk count is read on the device).
+extern "C" int mbk_head_score(const void* X, const void* Wp, const float* bp,
+                              const uint32_t* mask, const uint8_t* action, const int* pairs,
+                              const int* grp_start, const int* grp_count, const int* chunk_cell,
+                              const int* chunk_row, const int* totals, int S, float* plp,
+                              float* pent, hipStream_t stream) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    hipFuncSetAttribute((const void*)head_score_kernel,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, HS_LDS);
+  }
+  hipLaunchKernelGGL(head_score_kernel, dim3(cus), dim3(64 * HS_NW), HS_LDS, stream,
+                     (const bf16*)X, (const bf16*)Wp, bp, mask, action, pairs, grp_start,
+                     grp_count, chunk_cell, chunk_row, totals, S, plp, pent);
   return (int)hipGetLastError();
 }
 

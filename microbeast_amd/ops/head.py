@@ -12,6 +12,8 @@ per-cell recompute + dZ + dX_pair + dW_c (one workgroup per cell) -> dX gather.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _native as N
@@ -36,6 +38,9 @@ class SparseHead:
         # acting: derive the 16-pair units from the decode's bucket counts inside head_fwd
         # (no head_units launch); False: the separate head_units kernel (reference path)
         self.count_units = True
+        # learner scoring on the backward's chunk tiles (mbk_head_score: W_c staged per cell
+        # run, one row per lane); MBK_HEAD_SCORE=0: head_fwd's 16-pair units (A/B reference)
+        self.score_tiles = os.environ.get("MBK_HEAD_SCORE", "1") != "0"
 
     def _ensure(self, F: int):
         if F <= self._F:
@@ -142,14 +147,24 @@ class SparseHead:
         pair_out = not sample  # scoring: pair-indexed outputs, summed per frame through pidx
         self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out,
                      abits=abits)
-        N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
-                               mask_bits.data_ptr(), action.data_ptr(), N.ptr(rng), int(sample),
-                               self.pairs.data_ptr(), self.unit_cell.data_ptr(),
-                               self.unit_row.data_ptr(), self.grp_start.data_ptr(),
-                               self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
-                               self.fwd_grid, self.cell_lp.data_ptr(),
-                               self.cell_ent.data_ptr() if want_ent else None, int(pair_out),
-                               st), "head_fwd")
+        if pair_out and self.score_tiles:
+            N.check(k.mbk_head_score(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
+                                     mask_bits.data_ptr(), action.data_ptr(),
+                                     self.pairs.data_ptr(), self.grp_start.data_ptr(),
+                                     self.grp_count.data_ptr(), self.chunk_cell.data_ptr(),
+                                     self.chunk_row.data_ptr(), self.totals.data_ptr(), self.S,
+                                     self.cell_lp.data_ptr(),
+                                     self.cell_ent.data_ptr() if want_ent else None, st),
+                    "head_score")
+        else:
+            N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
+                                   mask_bits.data_ptr(), action.data_ptr(), N.ptr(rng),
+                                   int(sample), self.pairs.data_ptr(), self.unit_cell.data_ptr(),
+                                   self.unit_row.data_ptr(), self.grp_start.data_ptr(),
+                                   self.grp_count.data_ptr(), self.totals.data_ptr(), self.S,
+                                   self.fwd_grid, self.cell_lp.data_ptr(),
+                                   self.cell_ent.data_ptr() if want_ent else None,
+                                   int(pair_out), st), "head_fwd")
         logp = logp_out if logp_out is not None else torch.empty(F, dtype=torch.float32, device=X.device)
         ent = None
         if want_ent:

@@ -59,6 +59,33 @@ def test_sparse_score_fwd_bwd(cuda, F, S, p):
     assert torch.equal(g1, Wg.grad)
 
 
+@pytest.mark.parametrize("F,S,p", [(1000, 256, 0.08), (40000, 16, 0.25)])
+def test_score_tiles_match_unit_scoring(cuda, F, S, p):
+    """The learner's tiled scoring (mbk_head_score: chunk tiles, one row per lane) gives the
+    per-frame log-prob / entropy of head_fwd's per-unit scoring and of the fp32 reference,
+    including actions on masked logits (log-prob -1e8 - lse) and fully masked segments."""
+    X, W, b, m, a = _problem(F, S, p_active=p, seed=5)
+    g = torch.Generator().manual_seed(9)
+    bad = (torch.rand(F, S, generator=g) < 0.05) & m.any(-1)
+    a[..., 6] = torch.where(bad, torch.full_like(a[..., 6], 48), a[..., 6])  # maybe masked
+    mk = pack_mask(m).to(cuda)
+    outs = []
+    for tiles in (True, False):
+        head = SparseHead(S, cuda)
+        head.score_tiles = tiles
+        with torch.no_grad():
+            lp, ent = sparse_score(X.to(cuda), W.to(cuda), b.to(cuda), mk, a.to(cuda), head)
+        outs.append((lp.cpu(), ent.cpu()))
+    logits = X.float() @ W.bfloat16().float().T + b
+    _, lpr, entr = cell_head.cell_head_torch(logits, m, a)
+    assert (lpr < -1e7).any()  # the masked-action path is exercised
+    for lp, ent in outs:
+        torch.testing.assert_close(lp, lpr, rtol=1e-4, atol=2e-3)
+        torch.testing.assert_close(ent, entr, rtol=1e-4, atol=2e-3)
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(outs[0][1], outs[1][1], rtol=1e-5, atol=1e-4)
+
+
 def test_sparse_sample(cuda):
     F, S = 500, 256
     X, W, b, m, _ = _problem(F, S, seed=3)
