@@ -110,13 +110,13 @@ _SIGS = {
                      c_void_p, c_void_p, c_int, c_void_p],
     "mbk_head_score": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
-                       c_void_p],
+                       c_void_p, c_void_p],
     "mbk_head_pair_rowsum": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p,
                              c_void_p, c_void_p],
     "mbk_head_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                      c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                     c_void_p, c_void_p],
+                     c_void_p, c_void_p, c_void_p],
     "mbk_head_dx_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p],
     "mbk_head_dx_value_parts": [c_int],
     "mbk_head_dx_value": [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p,

@@ -650,6 +650,10 @@ __device__ __forceinline__ void hb_sum16(float (&v)[N]) {
     }
 }
 
+// ST: the forward's per-pair softmax statistics (head_score_kernel's stats: lse and entropy of
+// each segment) are staged with the row metadata, and the epilogue is per logit: no segment
+// max / sum reductions (a row's 16 lanes reducing by DPP were ~40 % of the kernel, VALU-bound).
+template <bool ST>
 __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     const bf16* __restrict__ X, const bf16* __restrict__ Wp, const float* __restrict__ bp,
     const uint32_t* __restrict__ mask, const uint8_t* __restrict__ action,
@@ -658,7 +662,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     const int* __restrict__ chunk_row, const int* __restrict__ totals,
     const float* __restrict__ g_logp, const float* __restrict__ g_ent, int S,
     bf16* __restrict__ dXp, float* __restrict__ dWp, float* __restrict__ dbp,
-    uint64_t* __restrict__ stamps) {
+    uint64_t* __restrict__ stamps, const float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wl = smem + HB_LW;
   int nst = 0;  // diagnostic phase stamps (MBK_HB_STAMPS): thread 0, first 8 tiles
@@ -751,6 +755,26 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
       d[0] = mt[0]; d[1] = mt[1]; d[2] = mt[2];
     }
   };
+  // ST: a quarter (16 B) of one row's 64-byte statistics {lse[7], H[7], 0, 0} per thread,
+  // stored at bytes 228.. of the dZ tile row's padding (lse at 228 + 4k, H at 256 + 4k)
+  const int srow = tid >> 2, squ = tid & 3;
+  uint4 st4 = make_uint4(0u, 0u, 0u, 0u);
+  auto load_stats = [&](const Cur& u) {
+    if constexpr (ST) {
+      const int nr = u.ch < nchunks ? min(HB_TM, u.n - u.t0) : 0;
+      st4 = srow < nr ? ((const uint4*)(stats + (size_t)(u.g0 + u.t0 + srow) * 16))[squ]
+                      : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto store_stats = [&]() {
+    if constexpr (ST) {
+      uint32_t* d = (uint32_t*)(zl + hb_phi(srow) * HB_RZ + 228 + squ * 16);
+      d[0] = st4.x; d[1] = st4.y;
+      if (squ < 3) {
+        d[2] = st4.z; d[3] = st4.w;
+      }
+    }
+  };
   auto load_x = [&]() {  // the rows of fx into registers
 #pragma unroll
     for (int k = 0; k < 8; ++k)
@@ -774,6 +798,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
   load_fx(cur);
   load_x();           // tile 0's rows and metadata
   load_meta(cur.c);
+  load_stats(cur);
   load_fx(nx1);       // tile 1's frames
   f32x4 accw[5][2];
   float dbs[5], bcol[5];
@@ -784,6 +809,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     lds_barrier();  // previous tile's LDS reads done
     store_x();
     store_meta();
+    store_stats();
     if (new_chunk) {
       stage_w(c);
 #pragma unroll
@@ -848,8 +874,27 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
         okm |= (sk[nb] < kComps && ((mw[i][nb >> 1] >> bit) & 1u)) ? 1u << (nb * 4 + i) : 0u;
       }
     }
+    if constexpr (ST) {
+      // per logit: lp = z - lse_k, p = e^lp, dz = gl (1[j == a_k] - p) - ge p (lp + H_k)
 #pragma unroll
-    for (int k = 0; k < kComps; ++k) {
+      for (int i = 0; i < 4; ++i) {
+        const char* rowp = zl + hb_phi(16 * wave + 4 * G + i) * HB_RZ;
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb) {
+          const int k = min(sk[nb], kComps - 1);
+          const float lse = *(const float*)(rowp + 228 + 4 * k);
+          const float H = *(const float*)(rowp + 256 + 4 * k);
+          const int bi = ab[i] + k;
+          const uint32_t wsel = bi < 4 ? aw[i][0] : bi < 8 ? aw[i][1] : aw[i][2];
+          const int a = (int)((wsel >> (8 * (bi & 3))) & 0xFFu);
+          const float lp = zz[nb][i] - lse;
+          const float p = __expf(lp);
+          zz[nb][i] = gl[i] * ((so[nb] == a ? 1.f : 0.f) - p) - ge[i] * p * (lp + H);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < (ST ? 0 : kComps); ++k) {
       const int c0 = seg_off(k), c1 = seg_off(k + 1);
       const int nb0 = c0 / 16, nb1 = (c1 - 1) / 16;
       bool any = false;
@@ -931,6 +976,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     if (has_next) {
       load_x();
       load_meta(nx1.c);
+      load_stats(nx1);
     }
     // then the tile after next: its cursor (scalar loads when it starts a chunk) and frames
     // (fx / fr hold the next tile's frames until the two gathers above are issued)
@@ -1066,7 +1112,7 @@ __global__ __launch_bounds__(64 * HS_NW, 1) void head_score_kernel(
     const int* __restrict__ pairs, const int* __restrict__ grp_start,
     const int* __restrict__ grp_count, const int* __restrict__ chunk_cell,
     const int* __restrict__ chunk_row, const int* __restrict__ totals, int S,
-    float* __restrict__ plp, float* __restrict__ pent) {
+    float* __restrict__ plp, float* __restrict__ pent, float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* wl = smem;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1174,9 +1220,11 @@ __global__ __launch_bounds__(64 * HS_NW, 1) void head_score_kernel(
       // cell_forward's scoring with the action's logit read from the tile (a register array
       // indexed by the action would live in scratch)
       float lp = 0.f, ent = 0.f;
+      float sl[kComps], sh[kComps];  // per segment: lse and entropy (0: fully masked)
 #pragma unroll
       for (int k = 0; k < kComps; ++k) {
         const int off = seg_off(k), n = seg_off(k + 1) - off;
+        sl[k] = sh[k] = 0.f;
         float mx = -INFINITY;
 #pragma unroll
         for (int j = 0; j < n; ++j)
@@ -1190,7 +1238,10 @@ __global__ __launch_bounds__(64 * HS_NW, 1) void head_score_kernel(
           sz += e * zr[off + j];
         }
         const float lse = mx + __logf(sm);
-        ent += lse - sz * (1.f / sm);
+        const float h = lse - sz * (1.f / sm);
+        ent += h;
+        sl[k] = lse;
+        sh[k] = h;
         const int bi = ab + k;
         const uint32_t w = bi < 4 ? aw[0] : bi < 8 ? aw[1] : aw[2];
         const int a = (int)((w >> (8 * (bi & 3))) & 0xFFu);
@@ -1201,6 +1252,13 @@ __global__ __launch_bounds__(64 * HS_NW, 1) void head_score_kernel(
       }
       plp[rb + lane] = lp;
       if (pent) pent[rb + lane] = ent;
+      if (stats) {  // the backward's softmax statistics of this pair: {lse[7], H[7], 0, 0}
+        float4* st = (float4*)(stats + (size_t)(rb + lane) * 16);
+        st[0] = make_float4(sl[0], sl[1], sl[2], sl[3]);
+        st[1] = make_float4(sl[4], sl[5], sl[6], sh[0]);
+        st[2] = make_float4(sh[1], sh[2], sh[3], sh[4]);
+        st[3] = make_float4(sh[5], sh[6], 0.f, 0.f);
+      }
     }
     __builtin_amdgcn_wave_barrier();  // the Z tile is rewritten by the next item
   }
@@ -1474,7 +1532,8 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
                             const int* grp_start, const int* grp_count, const int* chunk_cell,
                             const int* chunk_row, const int* chunk_start, const int* totals,
                             const float* g_logp, const float* g_ent, int S, int grid, void* dXp,
-                            float* dWp, float* dbp, float* dW, float* db, hipStream_t stream) {
+                            float* dWp, float* dbp, float* dW, float* db, const float* stats,
+                            hipStream_t stream) {
   {
     static int cus = 0;
     static uint64_t* hb_stamps = nullptr;
@@ -1483,7 +1542,9 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
       hipGetDevice(&dev);
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (cus <= 0) cus = 256;
-      hipFuncSetAttribute((const void*)head_bwd2_kernel,
+      hipFuncSetAttribute((const void*)head_bwd2_kernel<false>,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, HB_LDS);
+      hipFuncSetAttribute((const void*)head_bwd2_kernel<true>,
                           hipFuncAttributeMaxDynamicSharedMemorySize, HB_LDS);
       if (getenv("MBK_HB_STAMPS")) {
         hipMalloc(&hb_stamps, (size_t)cus * 64 * 8);
@@ -1492,10 +1553,11 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
     }
     // one 158 KB workgroup per CU; the caller's grid (chunk count bound) caps it
     const int g2 = std::max(1, std::min(grid, cus));
-    hipLaunchKernelGGL(head_bwd2_kernel, dim3(g2), dim3(64 * HB_NW), HB_LDS, stream,
-                       (const bf16*)X, (const bf16*)Wp, bp, mask, action, pairs, grp_start,
-                       grp_count, chunk_cell, chunk_row, totals, g_logp, g_ent, S, (bf16*)dXp, dWp,
-                       dbp, hb_stamps);
+    // stats (mbk_head_score's, same batch and weights): the per-logit epilogue
+    hipLaunchKernelGGL(stats ? head_bwd2_kernel<true> : head_bwd2_kernel<false>, dim3(g2),
+                       dim3(64 * HB_NW), HB_LDS, stream, (const bf16*)X, (const bf16*)Wp, bp,
+                       mask, action, pairs, grp_start, grp_count, chunk_cell, chunk_row, totals,
+                       g_logp, g_ent, S, (bf16*)dXp, dWp, dbp, hb_stamps, stats);
     if (hb_stamps) {  // per-phase mean over workgroups and their tiles 1..7 (us)
       std::vector<uint64_t> h((size_t)g2 * 64);
       hipMemcpyAsync(h.data(), hb_stamps, h.size() * 8, hipMemcpyDeviceToHost, stream);
@@ -1523,12 +1585,13 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
 
 // Learner scoring of the compacted pairs (head_score_kernel): pair-indexed log-prob and
 // entropy (pent may be null) of the given actions over the backward's chunk list, one 127 KB
-// workgroup per CU (no host sync: the chunk count is read on the device).
+// workgroup per CU (no host sync: the chunk count is read on the device). stats (or null):
+// per pair 16 floats {lse[7], H[7], 0, 0} for mbk_head_bwd's epilogue.
 extern "C" int mbk_head_score(const void* X, const void* Wp, const float* bp,
                               const uint32_t* mask, const uint8_t* action, const int* pairs,
                               const int* grp_start, const int* grp_count, const int* chunk_cell,
                               const int* chunk_row, const int* totals, int S, float* plp,
-                              float* pent, hipStream_t stream) {
+                              float* pent, float* stats, hipStream_t stream) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1540,7 +1603,7 @@ extern "C" int mbk_head_score(const void* X, const void* Wp, const float* bp,
   }
   hipLaunchKernelGGL(head_score_kernel, dim3(cus), dim3(64 * HS_NW), HS_LDS, stream,
                      (const bf16*)X, (const bf16*)Wp, bp, mask, action, pairs, grp_start,
-                     grp_count, chunk_cell, chunk_row, totals, S, plp, pent);
+                     grp_count, chunk_cell, chunk_row, totals, S, plp, pent, stats);
   return (int)hipGetLastError();
 }
 

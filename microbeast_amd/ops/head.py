@@ -41,6 +41,12 @@ class SparseHead:
         # learner scoring on the backward's chunk tiles (mbk_head_score: W_c staged per cell
         # run, one row per lane); MBK_HEAD_SCORE=0: head_fwd's 16-pair units (A/B reference)
         self.score_tiles = os.environ.get("MBK_HEAD_SCORE", "1") != "0"
+        # the scoring forward also writes per-pair softmax statistics (lse / entropy of each
+        # segment) for the backward's per-logit epilogue; it then reads the pair / chunk totals
+        # (the one host sync of the head, otherwise taken by the backward). MBK_HEAD_STATS=0: off
+        self.score_stats = os.environ.get("MBK_HEAD_STATS", "1") != "0"
+        self.stats = None
+        self._fwd_totals = None  # (P, nch) of the batch the statistics belong to
 
     def _ensure(self, F: int):
         if F <= self._F:
@@ -147,15 +153,24 @@ class SparseHead:
         pair_out = not sample  # scoring: pair-indexed outputs, summed per frame through pidx
         self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out,
                      abits=abits)
+        self._fwd_totals = None
         if pair_out and self.score_tiles:
+            stats = None
+            if self.score_stats:
+                P, _, nch = (int(v) for v in self.totals.tolist())
+                if self.stats is None or self.stats.numel() < P * 16:
+                    self.stats = torch.empty(max(P * 5 // 4, 1024) * 16, dtype=torch.float32,
+                                             device=X.device)
+                stats = self.stats
+                self._fwd_totals = (P, nch)
             N.check(k.mbk_head_score(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
                                      mask_bits.data_ptr(), action.data_ptr(),
                                      self.pairs.data_ptr(), self.grp_start.data_ptr(),
                                      self.grp_count.data_ptr(), self.chunk_cell.data_ptr(),
                                      self.chunk_row.data_ptr(), self.totals.data_ptr(), self.S,
                                      self.cell_lp.data_ptr(),
-                                     self.cell_ent.data_ptr() if want_ent else None, st),
-                    "head_score")
+                                     self.cell_ent.data_ptr() if want_ent else None,
+                                     N.ptr(stats), st), "head_score")
         else:
             N.check(k.mbk_head_fwd(X.data_ptr(), self.Wp.data_ptr(), self.bp.data_ptr(),
                                    mask_bits.data_ptr(), action.data_ptr(), N.ptr(rng),
@@ -198,8 +213,13 @@ class SparseHead:
         F = X.shape[0]
         k = N.kernels()
         st = N.stream_ptr()
-        # one sync: sizes the pair-major dX and per-chunk dW buffers
-        P, _, nch = (int(v) for v in self.totals.tolist())
+        # sizes of the pair-major dX and per-chunk dW buffers: from the scoring forward when it
+        # wrote statistics for this batch, else one sync here
+        fwd = self._fwd_totals
+        if fwd is not None:
+            P, nch = fwd
+        else:
+            P, _, nch = (int(v) for v in self.totals.tolist())
         dXp = torch.empty(max(P, 1), KD, dtype=torch.bfloat16, device=X.device)  # pair rows
         dWp = torch.empty(max(nch, 1), 78, KD, dtype=torch.float32, device=X.device)
         dbp = torch.empty(max(nch, 1), 78, dtype=torch.float32, device=X.device)
@@ -216,7 +236,9 @@ class SparseHead:
                                self.chunk_row.data_ptr(), self.chunk_start.data_ptr(),
                                self.totals.data_ptr(), g_logp.data_ptr(), N.ptr(g_ent), self.S,
                                grid, dXp.data_ptr(), dWp.data_ptr(), dbp.data_ptr(),
-                               dW.data_ptr(), db.data_ptr(), st), "head_bwd")
+                               dW.data_ptr(), db.data_ptr(),
+                               self.stats.data_ptr() if fwd is not None else None, st),
+                "head_bwd")
         if value is not None:
             dv, h, wc, partial = value
             R = h.shape[0]

@@ -29,10 +29,14 @@ def _problem(F, S, p_active=0.08, seed=0):
 
 # (40000, 16, 0.25): ~10K pairs per cell, ~313 512-pair chunks: several 128-pair tiles per
 # chunk and several chunks per workgroup of head_bwd2 (its prefetch pipeline across both)
+# stats: the backward's per-logit epilogue on the scoring forward's softmax statistics (default)
+# or its own per-segment reductions
+@pytest.mark.parametrize("stats", [True, False])
 @pytest.mark.parametrize("F,S,p", [(300, 64, 0.08), (1000, 256, 0.08), (40000, 16, 0.25)])
-def test_sparse_score_fwd_bwd(cuda, F, S, p):
+def test_sparse_score_fwd_bwd(cuda, F, S, p, stats):
     X, W, b, m, a = _problem(F, S, p_active=p)
     head = SparseHead(S, cuda)
+    head.score_stats = stats
     Xg = X.to(cuda).requires_grad_(True)
     Wg = W.to(cuda).requires_grad_(True)
     bg = b.to(cuda).requires_grad_(True)
