@@ -549,9 +549,10 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
   }
 }
 
-// logp[f] = sum over f's active cells of the pair log-probs (ent likewise): one wave per
-// frame walking its bitmap row and reading pidx at the active cells only, fixed-order
-// butterfly reduction (deterministic)
+// logp[f] = sum over f's active cells of the pair log-probs (ent likewise), in cell order
+// (deterministic): one lane per frame walking its bitmap row's set bits (~2 of 256 cells), so
+// 64 frames share a wave. (One wave per frame -- 524K tiny waves, each paying the bitmap ->
+// pidx -> log-prob chain with 1 to 2 of its 64 lanes busy -- took 183 us per learner update.)
 __global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __restrict__ pidx,
                                                                const uint32_t* __restrict__ abits,
                                                                int F,
@@ -559,37 +560,24 @@ __global__ __launch_bounds__(256) void head_pair_rowsum_kernel(const int* __rest
                                                                const float* __restrict__ pent,
                                                                float* __restrict__ logp,
                                                                float* __restrict__ ent) {
-  const int lane = threadIdx.x & 63;
-  const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int f = blockIdx.x * 256 + threadIdx.x;
   if (f >= F) return;
-  float a = 0.f, b = 0.f;
+  const int SW = abits_words(S);
+  const uint32_t* ab = abits + (size_t)f * SW;
   const int* pr = pidx + (size_t)f * S;
-  const uint32_t* ab = abits + (size_t)f * abits_words(S);
-  auto add = [&](int p) {
-    a += plp[p];
-    if (pent) b += pent[p];
-  };
-  if ((S & 3) == 0) {  // 4 cells per lane per pass (a nibble of one bitmap word)
-    for (int c = 4 * lane; c < S; c += 256) {
-      const uint32_t nib = (ab[c >> 5] >> (c & 31)) & 15u;
-      if (nib == 0u) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if ((nib >> j) & 1u) add(pr[c + j]);
+  float a = 0.f, b = 0.f;
+  for (int w = 0; w < SW; ++w) {
+    uint32_t bits = ab[w];
+    if (32 * w + 32 > S) bits &= (1u << (S - 32 * w)) - 1u;  // (the last word's tail)
+    while (bits) {
+      const int p = pr[32 * w + __builtin_ctz(bits)];
+      bits &= bits - 1u;
+      a += plp[p];
+      if (pent) b += pent[p];
     }
-  } else {
-    for (int c = lane; c < S; c += 64)
-      if ((ab[c >> 5] >> (c & 31)) & 1u) add(pr[c]);
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    a += __shfl_xor(a, o, 64);
-    b += __shfl_xor(b, o, 64);
-  }
-  if (lane == 0) {
-    logp[f] = a;
-    if (ent) ent[f] = b;
-  }
+  logp[f] = a;
+  if (ent) ent[f] = b;
 }
 
 // ------------------------------------------------------------------ backward
@@ -1522,7 +1510,7 @@ extern "C" int mbk_head_pair_rowsum(const int* pidx, const uint32_t* abits, int 
                                     const float* plp, const float* pent, float* logp, float* ent,
                                     hipStream_t stream) {
   if (F <= 0) return 0;
-  hipLaunchKernelGGL(head_pair_rowsum_kernel, dim3((F + 3) / 4), dim3(256), 0, stream, pidx,
+  hipLaunchKernelGGL(head_pair_rowsum_kernel, dim3((F + 255) / 256), dim3(256), 0, stream, pidx,
                      abits, F, S, plp, pent, logp, ent);
   return (int)hipGetLastError();
 }

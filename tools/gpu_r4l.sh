@@ -3,7 +3,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 tag=${1:-r4l}
-timeout -k 10 300 python -u -m pytest tests/test_gpu_head.py -x -v --timeout 200 --timeout-method thread \
+timeout -k 10 300 python -u -m pytest tests/test_gpu_head.py tests/test_gpu_learner_parity.py tests/test_gpu_act.py -x -v --timeout 200 --timeout-method thread \
   > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
 tail -1 gpurun_out/${tag}_tests.log
 for v in 1 0; do
