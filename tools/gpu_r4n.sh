@@ -1,4 +1,4 @@
-# Max-pool backward folded into the stage convs' wgrad / dgrad staging (band-layout wgrad now):
+# Max-pool backward folded into the stage convs' wgrad / dgrad staging:
 # stage 0 only (MBK_FUSED_POOL_BWD=s0), every stage (1) vs separate (0).
 #   bash tools/gpu_r4n.sh <tag>
 set -o pipefail
