@@ -108,6 +108,9 @@ _SIGS = {
     "mbk_head_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                      c_void_p, c_void_p, c_int, c_void_p],
+    "mbk_fc_wgrad_wide_parts": [c_int, c_int, c_int],
+    "mbk_fc_wgrad_wide": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                          c_void_p, c_void_p, c_void_p],
     "mbk_head_score": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                        c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
                        c_void_p, c_void_p],

@@ -32,6 +32,7 @@ constexpr int XROW = IC * 2;    // x tile row bytes
 union Frag8 {
   bf16x8 v;
   s16x4 h[2];
+  uint4 u;
 };
 
 __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
@@ -196,9 +197,12 @@ __global__ __launch_bounds__(kThreads) void fc_wgrad_kernel(const bf16* __restri
 
 // out[e] (+)= sum_p partial[p][e] over parts [y*pps, (y+1)*pps); `stage` set: write the
 // split sums to stage[y][e] for a second pass. 64 columns x 4 part-lanes per block.
+// out_b (or null): columns >= split go to out_b[e - split] instead (a W + b partial row)
 __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ partial, int nparts,
                                                      int pps, long row, float* __restrict__ stage,
-                                                     float* __restrict__ out, int accumulate) {
+                                                     float* __restrict__ out, int accumulate,
+                                                     float* __restrict__ out_b = nullptr,
+                                                     long split = 0) {
   __shared__ float red[4][64];
   const int col = threadIdx.x & 63, pl = threadIdx.x >> 6;
   const long e = (long)blockIdx.x * 64 + col;
@@ -212,8 +216,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   __syncthreads();
   if (pl != 0 || e >= row) return;
   s = red[0][col] + red[1][col] + red[2][col] + red[3][col];
-  if (stage) stage[(size_t)blockIdx.y * row + e] = s;
-  else out[e] = accumulate ? out[e] + s : s;
+  if (stage) {
+    stage[(size_t)blockIdx.y * row + e] = s;
+    return;
+  }
+  float* o = out_b && e >= split ? out_b + (e - split) : out + e;
+  *o = accumulate ? *o + s : s;
 }
 
 // Acting-path trunk tail, one launch: f = relu(relu(x) . W5^T + b5) (bf16 out) and the
@@ -383,6 +391,118 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
   }
 }
 
+
+// ---- FC weight + bias gradient of the IMPALA tail, one pass: dW = g^T x, db = g^T 1 with
+// O = 256 outputs and I = 16 CB inputs (128 on 16x16 maps). fc_wgrad_kernel's 64 x 64 output
+// chunks re-read every g / x row per chunk (8 chunks) from 128-row stages holding 16 MFMAs per
+// wave between two barriers (297 us per 524K rows, 1.3 TB/s); colsum then re-read g for db
+// (76 us). Here a 512-thread workgroup (one per CU) owns all of W: wave w computes W rows
+// 32 w .. 32 w + 31 against all I columns (A = g^T and B = x through ds_read_b64_tr_b16, row
+// strides 32 mod 256 bytes with the 4-row block swap of head_bwd2: conflict-free), plus the
+// bias as one more MFMA per K block against an all-ones B fragment; every g / x row is read
+// from HBM once (the next stage's rows are in registers during this stage's MFMAs).
+constexpr int FW_NW = 8, FW_RS = 128, FW_GR = 544, FW_XR = 288;
+constexpr int FW_LDS = FW_RS * (FW_GR + FW_XR);
+
+__device__ __forceinline__ int fw_phi(int r) {
+  const int b = (r >> 2) & 3;
+  return (b == 1 || b == 2) ? r ^ 12 : r;
+}
+
+template <int CB>
+__global__ __launch_bounds__(64 * FW_NW, 1) void fc_wgrad_wide_kernel(
+    const bf16* __restrict__ g, const bf16* __restrict__ x, int N, int relu_x,
+    int stages_per_part, float* __restrict__ partial) {
+  constexpr int O = 256, I = 16 * CB, MB = 2;
+  constexpr int GQ = O / 8, XQ = I / 8;                    // uint4 per g / x row
+  constexpr int NG = FW_RS * GQ / (64 * FW_NW), NX = (FW_RS * XQ + 64 * FW_NW - 1) / (64 * FW_NW);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* gt = smem;
+  char* xt = smem + FW_RS * FW_GR;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = lane >> 4, li = lane & 15;
+  const int nst = (N + FW_RS - 1) / FW_RS;
+  const int s0 = blockIdx.x * stages_per_part, s1 = min(nst, s0 + stages_per_part);
+  f32x4 acc[MB][CB], accb[MB];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    accb[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cb = 0; cb < CB; ++cb) acc[mb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  Frag8 ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  uint4 pg[NG], px[NX];
+  auto load = [&](int st) {
+    const int n0 = st * FW_RS;
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int e = tid + k * 64 * FW_NW, row = e / GQ, q = e % GQ;
+      pg[k] = n0 + row < N ? ((const uint4*)(g + (size_t)(n0 + row) * O))[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const int e = tid + k * 64 * FW_NW, row = e / XQ, q = e % XQ;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < FW_RS * XQ && n0 + row < N) v = ((const uint4*)(x + (size_t)(n0 + row) * I))[q];
+      px[k] = relu_x ? relu8(v) : v;
+    }
+  };
+  if (s0 < s1) load(s0);
+  for (int st = s0; st < s1; ++st) {
+    __syncthreads();  // the previous stage's tile reads are done
+#pragma unroll
+    for (int k = 0; k < NG; ++k) {
+      const int e = tid + k * 64 * FW_NW, row = e / GQ, q = e % GQ;
+      *(uint4*)(gt + fw_phi(row) * FW_GR + q * 16) = pg[k];
+    }
+#pragma unroll
+    for (int k = 0; k < NX; ++k) {
+      const int e = tid + k * 64 * FW_NW, row = e / XQ, q = e % XQ;
+      if (e < FW_RS * XQ) *(uint4*)(xt + fw_phi(row) * FW_XR + q * 16) = px[k];
+    }
+    __syncthreads();
+    if (st + 1 < s1) load(st + 1);
+#pragma unroll
+    for (int kb = 0; kb < FW_RS / 32; ++kb) {
+      int pr[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) pr[h] = fw_phi(kb * 32 + 8 * G + 4 * h + (li >> 2));
+      Frag8 af[MB];
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          af[mb].h[h] = tr_read(gt + pr[h] * FW_GR + (32 * wave + mb * 16 + 4 * (li & 3)) * 2);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        accb[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, ones.v, accb[mb], 0, 0, 0);
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) {
+        Frag8 bfr;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          bfr.h[h] = tr_read(xt + pr[h] * FW_XR + (cb * 16 + 4 * (li & 3)) * 2);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          acc[mb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bfr.v, acc[mb][cb], 0, 0, 0);
+      }
+    }
+  }
+  // this part's row of partials: W [O][I] then b [O]; lane (li, G) holds column cb*16 + li of
+  // W rows 32 w + mb*16 + 4G + i
+  float* out = partial + (size_t)blockIdx.x * (O * I + O);
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = 32 * wave + mb * 16 + 4 * G + i;
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb) out[o * I + cb * 16 + li] = acc[mb][cb][i];
+      if (li == 0) out[O * I + o] = accb[mb][i];
+    }
+}
+
 }  // namespace
 
 extern "C" int mbk_fc_fwd(const void* x, int relu_in, const void* w5, const float* b5,
@@ -487,6 +607,65 @@ extern "C" int mbk_fc_wgrad(const void* g, const void* x, int N, int O, int I, f
   XShifts xs{};
   xs.ntap = 1;
   return fc_wgrad_impl(g, x, N, O, I, xs, partial, nparts, out, accumulate, stream);
+}
+
+// fc_wgrad_wide_kernel's part count for N rows (one workgroup per CU, >= 4 stages each);
+// 0: the shape (O = 256, I in {32, 64, 128}) is not covered
+extern "C" int mbk_fc_wgrad_wide_parts(int N, int O, int I) {
+  if (O != 256 || (I != 32 && I != 64 && I != 128) || N <= 0) return 0;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  const int nst = (N + FW_RS - 1) / FW_RS;
+  return std::max(1, std::min(cus, (nst + 3) / 4));
+}
+
+// dW = g^T relu?(x) and db = column sums of g in one pass (fc_wgrad_wide_kernel) for
+// O = 256, I in {32, 64, 128}: out = fp32 [O][I], out_b = fp32 [O]. partial: (nparts +
+// ceil(nparts / 32)) * (O * I + O) floats of scratch.
+extern "C" int mbk_fc_wgrad_wide(const void* g, const void* x, int N, int O, int I, int relu_x,
+                                 float* partial, int nparts, float* out, float* out_b,
+                                 hipStream_t stream) {
+  if (mbk_fc_wgrad_wide_parts(N, O, I) == 0 || nparts < 1) return (int)hipErrorInvalidValue;
+  const int nst = (N + FW_RS - 1) / FW_RS;
+  const int spp = (nst + nparts - 1) / nparts;
+  const void* kfn = I == 128 ? (const void*)fc_wgrad_wide_kernel<8>
+                    : I == 64 ? (const void*)fc_wgrad_wide_kernel<4>
+                              : (const void*)fc_wgrad_wide_kernel<2>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)fc_wgrad_wide_kernel<8>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, FW_LDS);
+    hipFuncSetAttribute((const void*)fc_wgrad_wide_kernel<4>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, FW_LDS);
+    hipFuncSetAttribute((const void*)fc_wgrad_wide_kernel<2>,
+                        hipFuncAttributeMaxDynamicSharedMemorySize, FW_LDS);
+    attr = true;
+  }
+  const bf16* gp = (const bf16*)g;
+  const bf16* xp = (const bf16*)x;
+  void* args[] = {&gp, &xp, &N, &relu_x, (void*)&spp, &partial};
+  hipLaunchKernel(kfn, dim3(nparts), dim3(64 * FW_NW), args, FW_LDS, stream);
+  const long row = (long)O * I + O;
+  const unsigned cols = (unsigned)((row + 63) / 64);
+  constexpr int kPps = 32;
+  if (nparts > 2 * kPps) {
+    const int splits = (nparts + kPps - 1) / kPps;
+    float* st = partial + (size_t)nparts * row;
+    hipLaunchKernelGGL(colsum_kernel, dim3(cols, splits), dim3(256), 0, stream,
+                       (const float*)partial, nparts, kPps, row, st, (float*)nullptr, 0);
+    hipLaunchKernelGGL(colsum_kernel, dim3(cols, 1), dim3(256), 0, stream, (const float*)st,
+                       splits, splits, row, (float*)nullptr, out, 0, out_b, (long)O * I);
+  } else {
+    hipLaunchKernelGGL(colsum_kernel, dim3(cols, 1), dim3(256), 0, stream,
+                       (const float*)partial, nparts, nparts, row, (float*)nullptr, out, 0, out_b,
+                       (long)O * I);
+  }
+  return (int)hipGetLastError();
 }
 
 // mbk_fc_wgrad with relu_x: dW = g^T relu(x) (the pre-relu trunk output is what is saved)

@@ -348,10 +348,12 @@ class Agent(nn.Module):
         """
         if self._use_hip(obs) and torch.is_grad_enabled():
             # learner: trunk, then ONE autograd node for network.5 + head + critic whose
-            # backward kernels write every gradient (ops/tail.py)
-            y = self._trunk(obs)
-            n = y.shape[0]
+            # backward kernels write every gradient (ops/tail.py). The head's compaction (and
+            # its one host sync) goes first: it reads only masks / bitmap rows.
+            n = obs.shape[0]
             ns = n if n_score is None else n_score
+            self._head(obs.device).prepare_scoring(mask_bits.reshape(ns, -1, 3), ns, abits)
+            y = self._trunk(obs)
             _, ho, wo, c = y.shape
             fc = self.network[len(self.channels) + 2]
             key = (fc.out_features, c, ho, wo)

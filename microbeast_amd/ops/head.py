@@ -47,6 +47,7 @@ class SparseHead:
         self.score_stats = os.environ.get("MBK_HEAD_STATS", "1") != "0"
         self.stats = None
         self._fwd_totals = None  # (P, nch) of the batch the statistics belong to
+        self._prep = None        # (mask ptr, F, abits ptr, totals) of prepare_scoring
 
     def _ensure(self, F: int):
         if F <= self._F:
@@ -142,6 +143,22 @@ class SparseHead:
             self.cell_lp.data_ptr() if dense_out else None,
             self.cell_ent.data_ptr() if dense_out else None, N.stream_ptr()), "head_compact")
 
+    def prepare_scoring(self, mask_bits: torch.Tensor, F: int, abits: torch.Tensor | None = None):
+        """The scoring forward's compaction, issued before the trunk, with an asynchronous
+        copy of the pair / chunk totals (which size the statistics buffer) to pinned memory:
+        by the time the scoring forward reads them the trunk's kernels are queued behind the
+        copy, so the head's host sync drains nothing. The next scoring ``forward`` of the same
+        (mask, F, abits) skips the compaction."""
+        self.compact(mask_bits, F, None, dense_out=False, abits=abits)
+        ev = None
+        if self.score_tiles and self.score_stats and self.totals.is_cuda:
+            if getattr(self, "_tot_host", None) is None:
+                self._tot_host = torch.empty(3, dtype=torch.int32, pin_memory=True)
+            self._tot_host.copy_(self.totals, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        self._prep = (mask_bits.data_ptr(), F, N.ptr(abits), ev)
+
     def forward(self, X: torch.Tensor, mask_bits: torch.Tensor, action: torch.Tensor,
                 sample: bool, rng: torch.Tensor | None, logp_out: torch.Tensor | None = None,
                 ent_out: torch.Tensor | None = None, want_ent: bool = True,
@@ -151,13 +168,25 @@ class SparseHead:
         k = N.kernels()
         st = N.stream_ptr()
         pair_out = not sample  # scoring: pair-indexed outputs, summed per frame through pidx
-        self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out,
-                     abits=abits)
+        prep, self._prep = self._prep, None
+        if pair_out and prep is not None and prep[:3] == (mask_bits.data_ptr(), F, N.ptr(abits)):
+            pre_tot = None  # compacted by prepare_scoring; the totals are on their way
+            if prep[3] is not None:
+                prep[3].synchronize()
+                P, _, nch = (int(v) for v in self._tot_host.tolist())
+                pre_tot = (P, nch)
+        else:
+            prep = None
+            self.compact(mask_bits, F, action if sample else None, dense_out=not pair_out,
+                         abits=abits)
         self._fwd_totals = None
         if pair_out and self.score_tiles:
             stats = None
             if self.score_stats:
-                P, _, nch = (int(v) for v in self.totals.tolist())
+                if prep is not None and pre_tot is not None:
+                    P, nch = pre_tot
+                else:
+                    P, _, nch = (int(v) for v in self.totals.tolist())
                 if self.stats is None or self.stats.numel() < P * 16:
                     self.stats = torch.empty(max(P * 5 // 4, 1024) * 16, dtype=torch.float32,
                                              device=X.device)

@@ -29,6 +29,8 @@ from .optim import grad_out
 _BF = torch.bfloat16
 # MBK_FUSED_DX_VALUE=0: separate head_dx_gather + value_bwd launches (A/B, tests)
 _FUSED_DX_VALUE = os.environ.get("MBK_FUSED_DX_VALUE", "1") == "1"
+# dW5 + db5 in one pass (fc_wgrad_wide_kernel); MBK_FC_WIDE=0: fc_wgrad chunks + colsum
+_FC_WIDE = os.environ.get("MBK_FC_WIDE", "1") == "1"
 
 
 def nhwc_linear_maps(k1: int, c: int, hh: int, ww: int):
@@ -123,16 +125,24 @@ class _ImpalaTail(torch.autograd.Function):
         O = dh.shape[1]
         N.check(k.mbk_gemm_nt_mask(dh.data_ptr(), wt.data_ptr(), dy.data_ptr(), None, n, I, O, O,
                                    O, I, 0, 1, y2.data_ptr(), st), "gemm_nt_mask")
-        nparts = k.mbk_fc_wgrad_parts(n, O, I)
-        scratch = torch.empty((nparts + (nparts + 31) // 32) * O * I, dtype=torch.float32,
-                              device=dev)
         dw5 = torch.empty(O, I, dtype=torch.float32, device=dev)
-        N.check(k.mbk_fc_wgrad_ex(dh.data_ptr(), y2.data_ptr(), n, O, I, scratch.data_ptr(),
-                                  nparts, dw5.data_ptr(), 0, 1, st), "fc_wgrad_ex")
+        gb5 = grad_out(b5)
+        wparts = k.mbk_fc_wgrad_wide_parts(n, O, I) if _FC_WIDE else 0
+        if wparts > 0:  # dW5 and db5 in one pass over dh / y2 (fc.hip fc_wgrad_wide_kernel)
+            scratch = torch.empty((wparts + (wparts + 31) // 32) * (O * I + O),
+                                  dtype=torch.float32, device=dev)
+            N.check(k.mbk_fc_wgrad_wide(dh.data_ptr(), y2.data_ptr(), n, O, I, 1,
+                                        scratch.data_ptr(), wparts, dw5.data_ptr(),
+                                        gb5.data_ptr(), st), "fc_wgrad_wide")
+        else:
+            nparts = k.mbk_fc_wgrad_parts(n, O, I)
+            scratch = torch.empty((nparts + (nparts + 31) // 32) * O * I, dtype=torch.float32,
+                                  device=dev)
+            N.check(k.mbk_fc_wgrad_ex(dh.data_ptr(), y2.data_ptr(), n, O, I, scratch.data_ptr(),
+                                      nparts, dw5.data_ptr(), 0, 1, st), "fc_wgrad_ex")
+            colsum(dh, O, gb5)
         gw5 = grad_out(w5)
         map_gather([(dw5, gw5, maps.grad)])
-        gb5 = grad_out(b5)
-        colsum(dh, O, gb5)
         return (dy.view(yshape), gw5, gb5, gwc, gbc, gwa, gba) + (None,) * 6
 
 

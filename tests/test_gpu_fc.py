@@ -37,3 +37,28 @@ def test_linear_autograd_matches_reference_layer(cuda):
     assert rel(gw, wr.grad) < 1e-3
     assert rel(gb, br.grad) < 1e-3
     assert rel(gy.float().permute(0, 3, 1, 2).reshape(9000, -1), yr.grad) < 1e-2
+
+
+@pytest.mark.parametrize("n,i", [(266240, 128), (5037, 128), (9000, 32), (70001, 64), (100, 128)])
+def test_fc_wgrad_wide_weight_and_bias(cuda, n, i):
+    """One-pass dW = g^T relu(x), db = g^T 1 (fc_wgrad_wide_kernel, the IMPALA tail's FC)
+    vs fp32 PyTorch, including partial last stages and fewer rows than workgroups."""
+    from microbeast_amd import _native as N
+    k = N.kernels()
+    o = 256
+    torch.manual_seed(n + i)
+    g = torch.randn(n, o, device=cuda).bfloat16()
+    x = torch.randn(n, i, device=cuda).bfloat16()
+    parts = k.mbk_fc_wgrad_wide_parts(n, o, i)
+    assert parts > 0
+    scratch = torch.empty((parts + (parts + 31) // 32) * (o * i + o), device=cuda)
+    dw = torch.empty(o, i, device=cuda)
+    db = torch.empty(o, device=cuda)
+    N.check(k.mbk_fc_wgrad_wide(g.data_ptr(), x.data_ptr(), n, o, i, 1, scratch.data_ptr(),
+                                parts, dw.data_ptr(), db.data_ptr(), N.stream_ptr()),
+            "fc_wgrad_wide")
+    ref_w = g.float().t() @ torch.relu(x.float())
+    ref_b = g.float().sum(0)
+    assert ((dw - ref_w).norm() / ref_w.norm()).item() < 1e-5
+    assert ((db - ref_b).norm() / ref_b.norm()).item() < 1e-5
+    assert k.mbk_fc_wgrad_wide_parts(n, o, 288) == 0  # uncovered shapes fall back
