@@ -497,6 +497,10 @@ bool GpuEngine::enqueue_gpu(int g) {
     for (int c = 0; c < 2; ++c) {
       PubChan& P = pub_[c];
       if (!P.pending[ln]) continue;
+      // not before the staging copy has executed: the learner's thread publishes as soon as
+      // it has queued an update, and a stream wait here would hold this lane's policy steps
+      // (every group on it) until that whole update is done; a later step applies it
+      if (ready_only_ && hipEventQuery(P.ready) == hipErrorNotReady) continue;
       ENG_CHECK(hipStreamWaitEvent(st, P.ready, 0));
       ENG_CHECK(hipMemcpyAsync((void*)P.dst[ln], P.staging, P.n, hipMemcpyDeviceToDevice,
                                st));
@@ -531,7 +535,21 @@ bool GpuEngine::enqueue_gpu(int g) {
     int slot = -1;
     {
       std::lock_guard<std::mutex> l(slot_m_);
-      if (!free_slots_.empty()) { slot = free_slots_.front(); free_slots_.pop_front(); }
+      // the first free slot whose release has executed on the GPU: a slot the learner
+      // released right after queueing its update would make this lane's stream wait for the
+      // whole update (the learner's thread no longer blocks mid-update); the group waits
+      // on the host instead while the lane's other groups keep acting
+      for (auto it = free_slots_.begin(); it != free_slots_.end(); ++it) {
+        const int s = *it;
+        if (ready_only_ && release_pending_[s]) {
+          const hipError_t q = hipEventQuery(release_ev_[s]);
+          if (q == hipErrorNotReady) continue;
+          if (q == hipSuccess) release_pending_[s] = false;
+        }
+        slot = s;
+        free_slots_.erase(it);
+        break;
+      }
     }
     if (slot < 0) {  // learner-bound: wait for a released slot
       if (!waiting()) slot_wait_q_.push_back(g);

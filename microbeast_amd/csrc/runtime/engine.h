@@ -35,6 +35,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -298,6 +299,12 @@ class GpuEngine {
   std::deque<int> free_slots_, full_slots_;
   std::vector<hipEvent_t> full_ev_, release_ev_;
   std::vector<bool> release_pending_;
+  // slots / weight publishes are taken only once their learner-stream events have executed
+  // (MBK_ENGINE_READY_ONLY=0: take them at once behind a stream wait, the old behaviour)
+  bool ready_only_ = [] {
+    const char* e = std::getenv("MBK_ENGINE_READY_ONLY");
+    return !(e && e[0] == '0');
+  }();
   std::vector<int> slot_version_;  // written when a group takes the slot (driver thread)
   std::deque<int> slot_wait_q_;  // driver thread only: groups waiting for a free slot
 

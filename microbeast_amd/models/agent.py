@@ -41,6 +41,9 @@ HIP_CHANNELS = (16, 32)  # conv widths the HIP trunk kernels are instantiated fo
 # separate fc.hip launch (default): measured 0.208 vs 0.200 ms per 8192-env policy step in
 # isolation and no gain under the learner (the fused variant spills 8 VGPRs)
 _TRUNK_HEAD = os.environ.get("MBK_TRUNK_HEAD", "0") == "1"
+# learner: the head's compaction (and the async read of its totals) before the trunk
+# (MBK_HEAD_PREP=0: inside the head's forward, after the trunk)
+_HEAD_PREP = os.environ.get("MBK_HEAD_PREP", "1") == "1"
 
 
 def layer_init(layer: nn.Module, std: float = math.sqrt(2), bias_const: float = 0.0) -> nn.Module:
@@ -352,7 +355,8 @@ class Agent(nn.Module):
             # its one host sync) goes first: it reads only masks / bitmap rows.
             n = obs.shape[0]
             ns = n if n_score is None else n_score
-            self._head(obs.device).prepare_scoring(mask_bits.reshape(ns, -1, 3), ns, abits)
+            if _HEAD_PREP:
+                self._head(obs.device).prepare_scoring(mask_bits.reshape(ns, -1, 3), ns, abits)
             y = self._trunk(obs)
             _, ho, wo, c = y.shape
             fc = self.network[len(self.channels) + 2]
