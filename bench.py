@@ -43,12 +43,13 @@ def parse(argv=None):
     p.add_argument("--size", type=int, default=16)
     p.add_argument("--arch", type=str, default="impala_flat",
                    help="impala_flat (headline) | gridnet (BASELINE config 2) | impala_deep")
-    p.add_argument("--groups", type=int, default=4,
-                   help="env groups pipelined through the policy stream (profile 21 same-box "
-                        "sweep: 4 x 8192 9.83-9.94M vs 3 x 8192 9.51-9.56M frames/s; the "
-                        "policy lane is ~72%% busy with 3, the group cycle's latency bound)")
-    p.add_argument("--lanes", type=int, default=1,
-                   help="concurrent policy streams, each with its own graph + I/O")
+    p.add_argument("--groups", type=int, default=3,
+                   help="env groups pipelined through the policy lanes (profile 36 same-box "
+                        "sweep, 2 lanes: 3 x 8192 15.9-16.0M frames/s at a mean policy lag of "
+                        "3.6 updates; 1 lane x 4 groups 14.6-14.9M at 4.1)")
+    p.add_argument("--lanes", type=int, default=0,
+                   help="concurrent policy streams, each with its own graph + I/O (0 = auto: "
+                        "2; strong scaling at N > 1: min(groups, N), at least 2)")
     p.add_argument("--envs_per_group", type=int, default=8192)
     p.add_argument("--unroll", type=int, default=64)
     p.add_argument("--batch_slots", type=int, default=1)
@@ -119,8 +120,10 @@ def main(argv=None):
         # step leaves most of the GPU idle (latency-bound), so strong scaling runs the groups'
         # steps on concurrent policy lanes -- the GPU then sees ~groups x envs_per_group envs
         # of acting work at a time, as at N = 1 (--lanes overrides)
-        if args.lanes == 1:
-            args.lanes = min(args.groups, info.world_size)
+        if args.lanes == 0:
+            args.lanes = max(2, min(args.groups, info.world_size))
+    if args.lanes == 0:
+        args.lanes = min(2, args.groups)
     if info.world_size != args.gpus and info.is_main:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {info.world_size}; reporting "
               f"{info.world_size}", file=sys.stderr)
