@@ -212,7 +212,7 @@ def train(flags: Flags) -> dict:
                                    bots=flags.opponent_list(), reward_weight=flags.reward_weights(),
                                    env_index_base=info.rank * envs_total, selfplay_groups=sp_groups,
                                    fp8_policy=flags.fp8_policy or flags.dtype == "fp8",
-                                   n_lanes=flags.policy_lanes)
+                                   n_lanes=max(1, min(flags.policy_lanes, flags.groups)))
 
         rt = make_gpu_runtime(0)
         if sp_groups:
