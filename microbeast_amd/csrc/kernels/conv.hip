@@ -702,22 +702,32 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
         const int x0 = 16 * cbk;
         const bool in = x0 + li < W, has_r = x0 + 16 < W;
         // row yy of this column block: the lane's word and the block's two edge neighbours
-        auto xrw = [&](int yy) {
-          if (yy < 0 || yy >= H) return xzero;
-          const uint32_t* rp = xi + (size_t)yy * W;
-          return xrow(in ? rp[x0 + li] : 0u, x0 > 0 ? rp[x0 - 1] : 0u, has_r ? rp[x0 + 16] : 0u);
+        // (rows outside the image: zero words, which expand to zero fragments)
+        auto ldw = [&](int yy) {
+          uint3 v = make_uint3(0u, 0u, 0u);
+          if (yy >= 0 && yy < H) {
+            const uint32_t* rp = xi + (size_t)yy * W;
+            v = make_uint3(in ? rp[x0 + li] : 0u, x0 > 0 ? rp[x0 - 1] : 0u,
+                           has_r ? rp[x0 + 16] : 0u);
+          }
+          return v;
         };
+        auto xrw = [&](uint3 v) { return xrow(v.x, v.y, v.z); };
         XRow3 r[4];
         r[0] = xzero;
-        r[1] = xrw(0);
-        r[2] = xrw(1);
-        r[3] = xrw(2);
+        r[1] = xrw(ldw(0));
+        r[2] = xrw(ldw(1));
+        r[3] = xrw(ldw(2));
         for (int y = 0; y < H; y += 2) {
+          // the next pair's input rows load during this pair's MFMAs (expanding them right
+          // after their loads exposed two global-load latencies per row pair: 9.0 ms per
+          // 524K 24x24 images)
+          const uint3 n0 = ldw(y + 3), n1 = ldw(y + 4);
           row_pair(r, y, im, img0, x0);
           r[0] = r[2];
           r[1] = r[3];
-          r[2] = xrw(y + 3);
-          r[3] = xrw(y + 4);
+          r[2] = xrw(n0);
+          r[3] = xrw(n1);
         }
       }
     } else if (wave < nimg) {
