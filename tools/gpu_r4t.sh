@@ -5,7 +5,7 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 tag=${1:-r4t}
 show() { tail -1 $1 | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"]/1e6,3), d["ms_per_step"], d.get("policy_lag_updates"))'; }
-for v in "" "--groups 4 --lanes 1"; do
+for v in ""; do
   n=$(echo "$v" | tr -d ' -')
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 $v > gpurun_out/${tag}_c3_$n.log 2>&1 || exit 1
   echo "headline [$v] $(show gpurun_out/${tag}_c3_$n.log)"
