@@ -19,7 +19,8 @@ ONE server in the learner process:
   each actor's response ring;
 * weights: the learner's ``publish`` copies its flat buffer into a device staging
   copy on the learner stream and records an event; the server applies it between
-  two batches (stream wait + D2D), so a batch never mixes weight versions.
+  two batches once that event has executed (D2D), so a batch never mixes weight versions
+  and the inference stream never waits for the learner's queued update.
 
 The server also runs on a CPU device (same protocol; used by the CPU test suite).
 """
@@ -149,6 +150,12 @@ class InferenceServer:
         with self._lock:
             ev, self._pending = self._pending, None
             if ev is None:
+                return
+            if not ev.query():
+                # the learner's thread publishes once it has queued an update: waiting on the
+                # staging copy here would hold the inference stream until that whole update
+                # ran; a later batch applies it (a newer publish supersedes it meanwhile)
+                self._pending = ev
                 return
             self.stream.wait_event(ev)
             with torch.cuda.stream(self.stream):
