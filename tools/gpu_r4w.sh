@@ -6,7 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 tag=${1:-r4w}
 i=0
 for rep in 1 2; do
-for v in "MBK_NOP=0|" "MBK_NOP=0|--learner_cu_reserve 32" "MBK_NOP=0|--learner_cu_reserve 16" "MBK_RES_BWD_PER_CU=1|"; do
+for v in "MBK_NOP=0|" "MBK_NOP=0|--groups 2" "MBK_NOP=0|--lanes 3" "MBK_NOP=0|--groups 4"; do
   i=$((i+1))
   e=${v%%|*}; a=${v#*|}
   env $e timeout -k 10 300 python bench.py --steps 30 --warmup 5 $a > gpurun_out/${tag}_b$i.log 2>&1 || exit 1
