@@ -81,6 +81,21 @@ def parse(argv=None):
                         "one slot per update (global batch grows with N); strong: the global "
                         "problem of 1 GPU (the same groups x envs_per_group envs, one update "
                         "of envs_per_group x unroll frames) is split over the N ranks")
+    p.add_argument("--settle", type=int, default=300,
+                   help="untimed training updates before the warm-up, so the timed window measures "
+                        "a training run's steady state: from random init the policy learns to "
+                        "produce units and the agent's idle units (active cells) per env rise "
+                        "from ~1.2 to 7-11 within ~130 updates, which slows acting, the sparse "
+                        "head and the env side (profile 38: 16.2 -> ~12.3 M frames/s). 0 = time "
+                        "the early-game transient")
+    p.add_argument("--preroll", type=int, default=0,
+                   help="before the first policy step every env plays r ~ U[0, preroll) steps of "
+                        "the uniform random-init policy on the CPU (untimed), so the timed window "
+                        "starts from envs spread over the game's phases, not all at reset "
+                        "(0 = off)")
+    p.add_argument("--report_every", type=int, default=0,
+                   help="diagnostics: every k timed steps print the window's frames/s and active "
+                        "cells per env to stderr (host clock; 0 = off)")
     p.add_argument("--policy_gate", type=int, default=-1,
                    help="1: learner launches wait while a policy step's kernels run (engine "
                         "policy gate); 0: off; -1: MBK_POLICY_GATE (default off)")
@@ -160,7 +175,8 @@ def main(argv=None):
                          env_index_base=info.rank * envs_total,
                          selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy,
                          n_lanes=args.lanes, policy_cu_every=args.cu_partition,
-                         policy_gate=None if args.policy_gate < 0 else bool(args.policy_gate))
+                         policy_gate=None if args.policy_gate < 0 else bool(args.policy_gate),
+                         preroll=args.preroll)
     league = None
     if args.selfplay_groups > 0:
         from microbeast_amd.runtime.league import League
@@ -212,7 +228,7 @@ def main(argv=None):
                 league.current = sid
         return losses
 
-    for _ in range(args.warmup):
+    for _ in range(args.settle + args.warmup):
         losses = step()
     # drop rollouts that piled up during warm-up (graph capture, first-call setup) so the
     # timed window measures the steady-state production rate, not a pre-filled backlog
@@ -226,8 +242,18 @@ def main(argv=None):
     st0 = rt.stats()
     lags.clear()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    win = (time.perf_counter(), st0)
+    for i in range(args.steps):
         losses = step()
+        if args.report_every > 0 and (i + 1) % args.report_every == 0 and info.is_main:
+            now, st = time.perf_counter(), rt.stats()
+            nst = max(1, (st["act_fused_steps"] + st["act_b_steps"])
+                      - (win[1]["act_fused_steps"] + win[1]["act_b_steps"]))
+            print(f"[window] steps {i + 1 - args.report_every}-{i + 1}: "
+                  f"{args.report_every * frames_per_step / (now - win[0]) / 1e6:.2f} M frames/s, "
+                  f"active cells/env {(st['act_active_cells'] - win[1]['act_active_cells']) / (nst * rt.E):.3f}",
+                  file=sys.stderr, flush=True)
+            win = (now, st)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     D.barrier(info)
@@ -273,6 +299,9 @@ def main(argv=None):
             "metric": f"env frames/sec (whole node) on {s}x{s} microRTS",
             "value": round(fps, 1),
             "unit": "frames/s",
+            # game phase the window measured: the agent's idle units (cells the sparse head
+            # samples) per env and policy step, rank 0; the head's and the env's work grow with it
+            "active_cells_per_env": mine.get("active_cells_per_env"),
             "n_gpus": info.world_size,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -302,6 +331,8 @@ def main(argv=None):
                 "policy_lanes": rt.n_lanes,
                 "allreduce": f"{args.allreduce_dtype} {args.bucket_mb:g}MB buckets",
                 "policy_gate": rt.policy_gate,
+                "settle_updates": args.settle,
+                "preroll": args.preroll,
             },
             "actor_stats": {
                 "env_frames_stepped_per_s_rank0": round((st1["frames"] - st0["frames"]) / el, 1),

@@ -81,6 +81,12 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("drain_episodes", [](PyVecEnv& e) { return records_to_list(e.log.drain()); })
       .def("set_bot", [](PyVecEnv& e, int i, int bot) { e.env->sim(i).set_bot(bot); })
       .def("bot", [](PyVecEnv& e, int i) { return e.env->sim(i).bot(); })
+      .def("preroll",
+           [](PyVecEnv& e, int max_pre, uint64_t seed, int n_threads) {
+             py::gil_scoped_release g;
+             return e.env->preroll(max_pre, seed, n_threads);
+           },
+           py::arg("max_pre"), py::arg("seed"), py::arg("n_threads") = 1)
       .def("set_external_opponent",
            [](PyVecEnv& e, bool on) {
              for (int i = 0; i < e.env->num_envs(); ++i) e.env->sim(i).set_external_opponent(on);
@@ -264,6 +270,7 @@ PYBIND11_MODULE(_mbrt, m) {
         if (c.contains("n_lanes")) cfg.n_lanes = c["n_lanes"].cast<int>();
         if (c.contains("policy_cu_every")) cfg.policy_cu_every = c["policy_cu_every"].cast<int>();
         if (c.contains("policy_gate")) cfg.policy_gate = c["policy_gate"].cast<bool>();
+        if (c.contains("preroll")) cfg.preroll = c["preroll"].cast<int>();
         EngineBuffers buf;
         buf.obs = b["obs"].cast<uintptr_t>();
         buf.mask = b["mask"].cast<uintptr_t>();
@@ -391,6 +398,7 @@ PYBIND11_MODULE(_mbrt, m) {
         d["publishes"] = s.publishes;
         d["opp_publishes"] = s.opp_publishes;
         d["opp_version"] = s.opp_version;
+        d["preroll_steps"] = s.preroll_steps;
         return d;
       });
 }

@@ -105,8 +105,17 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     std::memset(h_act16_p1_, 0, (size_t)total * S_ * 2);
     env_->set_external_opponent(sp0 * cfg_.envs_per_group, total, true);
   }
-  env_->set_validate(false);  // masks are derived on the GPU from the codes
-  env_->reset_codes(h_codes_, h_res_);
+  if (cfg_.preroll > 1) {
+    // desynchronised start (bench.py): each env first plays a random number of uniform-policy
+    // steps on the CPU (with CPU masks), then the GPU takes over from those states
+    env_->reset_codes(nullptr, nullptr);
+    preroll_steps_ = env_->preroll(cfg_.preroll, cfg_.seed, std::max(1, cfg_.n_threads));
+    env_->set_validate(false);  // masks are derived on the GPU from the codes
+    env_->write_codes(h_codes_, h_res_);
+  } else {
+    env_->set_validate(false);  // masks are derived on the GPU from the codes
+    env_->reset_codes(h_codes_, h_res_);
+  }
   if (cfg_.selfplay_groups > 0) env_->reset_codes_p1(h_codes_p1_, h_res_p1_);
   {
     const char* st = std::getenv("MBK_STEP_TIMING");
@@ -123,7 +132,7 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
   }
   full_ev_.resize(cfg_.n_slots);
   release_ev_.resize(cfg_.n_slots);
-  release_pending_.assign(cfg_.n_slots, false);
+  release_pending_.assign(cfg_.n_slots, 0);
   slot_version_.assign(cfg_.n_slots, 0);
   for (int s = 0; s < cfg_.n_slots; ++s) {
     CTOR_CHECK(hipEventCreateWithFlags(&full_ev_[s], hipEventDisableTiming));
@@ -533,6 +542,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       return false;
     }
     int slot = -1;
+    bool pending = false;  // read under slot_m_: release() updates the flags from another thread
     {
       std::lock_guard<std::mutex> l(slot_m_);
       // the first free slot whose release has executed on the GPU: a slot the learner
@@ -544,9 +554,10 @@ bool GpuEngine::enqueue_gpu(int g) {
         if (ready_only_ && release_pending_[s]) {
           const hipError_t q = hipEventQuery(release_ev_[s]);
           if (q == hipErrorNotReady) continue;
-          if (q == hipSuccess) release_pending_[s] = false;
+          if (q == hipSuccess) release_pending_[s] = 0;
         }
         slot = s;
+        pending = release_pending_[s] != 0;
         free_slots_.erase(it);
         break;
       }
@@ -556,7 +567,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       return false;
     }
     if (!slot_wait_q_.empty() && slot_wait_q_.front() == g) slot_wait_q_.pop_front();
-    if (release_pending_[slot]) ENG_CHECK(hipStreamWaitEvent(st, release_ev_[slot], 0));
+    if (pending) ENG_CHECK(hipStreamWaitEvent(st, release_ev_[slot], 0));
     G.cur = slot;
     slot_version_[slot] = L.policy_version;
   }
@@ -905,7 +916,7 @@ void GpuEngine::release(const std::vector<int>& slots, uintptr_t stream) {
   }
   std::lock_guard<std::mutex> l(slot_m_);
   for (int s : slots) {
-    release_pending_[s] = true;
+    release_pending_[s] = 1;
     free_slots_.push_back(s);
   }
 }
@@ -951,6 +962,7 @@ EngineStats GpuEngine::stats() const {
   s.step_graph_s = step_graph_ns_.load() * 1e-9;
   s.step_out_s = step_out_ns_.load() * 1e-9;
   s.timed_steps = timed_steps_.load();
+  s.preroll_steps = preroll_steps_;
   s.env_phase_s = env_phase_ns_.load() * 1e-9;
   s.enqueue_s = enqueue_ns_.load() * 1e-9;
   s.graph_launch_s = launch_ns_.load() * 1e-9;

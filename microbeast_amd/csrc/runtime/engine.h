@@ -71,6 +71,10 @@ struct EngineConfig {
   // for it to read 0 before each launch (mbk_stream_wait_zero), so a policy step never
   // queues behind more than the one learner kernel already running
   bool policy_gate = false;
+  // >1: before the first policy step every env plays r ~ U[0, preroll) uniform-policy steps on
+  // the CPU (VecEnv::preroll), so the envs start spread over the game's phases, not all at
+  // their first frame (bench.py: the timed window then measures the steady state)
+  int preroll = 0;
 };
 
 // Fixed-address I/O of one lane's captured policy graph (and opponent graph). The graph
@@ -141,6 +145,7 @@ struct EngineStats {
   // fused acting step (act models set): steps whose head ran inside launch A / in launch B,
   // and the agent's idle units (active cells) summed over the steps the engine chose for
   int64_t act_fused_steps = 0, act_b_steps = 0, act_active_cells = 0;
+  int64_t preroll_steps = 0;  // env steps played by EngineConfig::preroll before the start
 };
 
 class GpuEngine {
@@ -298,7 +303,8 @@ class GpuEngine {
   std::condition_variable full_cv_;
   std::deque<int> free_slots_, full_slots_;
   std::vector<hipEvent_t> full_ev_, release_ev_;
-  std::vector<bool> release_pending_;
+  int64_t preroll_steps_ = 0;
+  std::vector<uint8_t> release_pending_;  // per slot; guarded by slot_m_ (bytes, not bits)
   // slots / weight publishes are taken only once their learner-stream events have executed
   // (MBK_ENGINE_READY_ONLY=0: take them at once behind a stream wait, the old behaviour)
   bool ready_only_ = [] {

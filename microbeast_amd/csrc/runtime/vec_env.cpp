@@ -1,6 +1,9 @@
 #include "vec_env.h"
 
 #include <algorithm>
+#include <atomic>
+#include <random>
+#include <thread>
 
 namespace mb {
 
@@ -64,6 +67,75 @@ void VecEnv::reset_codes(uint16_t* codes, int32_t* res) {
     if (codes) sims_[i]->write_obs_codes(codes + i * S);
     if (res) res[i] = sims_[i]->resources(0);
   }
+}
+
+void VecEnv::write_codes(uint16_t* codes, int32_t* res) const {
+  const size_t S = (size_t)size_ * size_;
+  for (size_t i = 0; i < sims_.size(); ++i) {
+    sims_[i]->write_obs_codes(codes + i * S);
+    res[i] = sims_[i]->resources(0);
+  }
+}
+
+namespace {
+// one draw per action component, uniform over the legal choices of the cell's 78-bit mask
+void uniform_legal(const uint32_t* mask, int S, std::mt19937_64& rng, uint8_t* act) {
+  for (int c = 0; c < S; ++c) {
+    const uint32_t* m = mask + (size_t)c * kMaskWords;
+    uint8_t* a = act + (size_t)c * kActComps;
+    if ((m[0] | m[1] | m[2]) == 0) {  // no own idle unit here (almost every cell)
+      for (int k = 0; k < kActComps; ++k) a[k] = 0;
+      continue;
+    }
+    for (int k = 0; k < kActComps; ++k) {
+      int cand[49], n = 0;
+      for (int j = 0; j < kNvec[k]; ++j) {
+        const int b = kNvecOff[k] + j;
+        if ((m[b >> 5] >> (b & 31)) & 1u) cand[n++] = j;
+      }
+      a[k] = n ? (uint8_t)cand[rng() % (uint64_t)n] : 0;
+    }
+  }
+}
+}  // namespace
+
+int64_t VecEnv::preroll(int max_pre, uint64_t seed, int n_threads) {
+  if (max_pre <= 1 || sims_.empty()) return 0;
+  const int n = (int)sims_.size(), S = size_ * size_;
+  std::atomic<int> next{0};
+  std::atomic<int64_t> played{0};
+  auto work = [&]() {
+    std::vector<uint32_t> m(S * kMaskWords), m1(S * kMaskWords);
+    std::vector<uint8_t> a(S * kActComps), a1(S * kActComps);
+    for (int i; (i = next.fetch_add(1)) < n;) {
+      std::mt19937_64 rng(seed * 0x9E3779B97F4A7C15ull + (uint64_t)(base_ + i));
+      const int r = (int)(rng() % (uint64_t)max_pre);
+      MicroRTSSim& sim = *sims_[i];
+      for (int t = 0; t < r; ++t) {
+        sim.write_mask(m.data());
+        uniform_legal(m.data(), S, rng, a.data());
+        if (sim.external_opponent()) {
+          sim.write_mask_p1(m1.data());
+          uniform_legal(m1.data(), S, rng, a1.data());
+          sim.set_opponent_actions(a1.data());
+        }
+        bool d = false;
+        ep_ret_[i] += sim.step(a.data(), &d, nullptr);
+        ep_len_[i] += 1;
+        if (d) {
+          ep_ret_[i] = 0.f;
+          ep_len_[i] = 0;
+        }
+      }
+      played.fetch_add(r);
+    }
+  };
+  const int nt = std::max(1, std::min(n_threads, n));
+  std::vector<std::thread> th;
+  for (int k = 1; k < nt; ++k) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  return played.load();
 }
 
 void VecEnv::reset_codes_p1(uint16_t* codes_p1, int32_t* res_p1) const {

@@ -88,6 +88,15 @@ class VecEnv {
                            float* reward, uint8_t* done, EpisodeLog* log, int opponent,
                            float* ep_return = nullptr, int32_t* ep_step = nullptr);
   void set_external_opponent(int e0, int e1, bool on);
+  // Desynchronise the envs (bench.py / --preroll): env i plays r_i ~ U[0, max_pre) steps of
+  // the random-init agent's policy -- every action component uniform over its legal choices
+  // (actor gain 0, reference model.py:136) -- and of the same policy for a self-play opponent,
+  // with auto-reset, so a measurement starts from a spread of game phases instead of every env
+  // at its first frame. Needs the CPU masks (set_validate(true)); finished episodes are not
+  // logged, running returns / lengths carry over. Returns the env steps played.
+  int64_t preroll(int max_pre, uint64_t seed, int n_threads);
+  // current codes / resources of every env (no reset)
+  void write_codes(uint16_t* codes, int32_t* res) const;
   // Dense reference layout for parity tools: obs f32 (n,s,s,27), mask u8 (n,s*s*78)
   void dense_obs(float* out) const;
   void dense_mask(uint8_t* out) const;

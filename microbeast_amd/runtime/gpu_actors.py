@@ -148,8 +148,11 @@ class GpuActorRuntime:
                  env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False,
                  n_lanes: int | None = None, policy_cu_every: int = 0,
                  reference_keys: bool = False, policy_logits: bool = False,
-                 policy_gate: bool | None = None):
-        """reference_keys: also emit the reference buffer keys ep_return / ep_step /
+                 policy_gate: bool | None = None, preroll: int = 0):
+        """preroll > 1: every env first plays r ~ U[0, preroll) steps of the uniform
+        random-init policy on the CPU (engine.h EngineConfig::preroll), so the run starts from
+        envs spread over the game's phases rather than all at their first frame.
+        reference_keys: also emit the reference buffer keys ep_return / ep_step /
         last_action (libs/utils.py:34-46) into the slots; policy_logits: plus the dense
         78*h*w policy logits of every step (the sparse acting head never needs them, so
         this adds one dense head GEMM per policy step and 312*h*w bytes per frame)."""
@@ -251,7 +254,8 @@ class GpuActorRuntime:
                    reward_weight=list(reward_weight), env_index_base=env_index_base,
                    device=dev.index if dev.index is not None else torch.cuda.current_device(),
                    selfplay_groups=self.selfplay_groups, n_lanes=self.n_lanes,
-                   policy_cu_every=int(policy_cu_every), policy_gate=self.policy_gate)
+                   policy_cu_every=int(policy_cu_every), policy_gate=self.policy_gate,
+                   preroll=int(preroll))
         bufs = {k: v.data_ptr() for k, v in self.rb.items()}
         bufs["lanes"] = []
         for lane in self.lanes:

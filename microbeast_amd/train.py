@@ -148,11 +148,27 @@ def _league_extra(league):
     return {"league": league.state_dict()} if league is not None else None
 
 
+def resolve_runtime(flags: Flags, want_cuda: bool) -> str:
+    """The actor runtime a run uses. The GPU engine's env workers step the native stand-in
+    only (C++ MicroRTSSim, sparse code rows); the real gym-microrts adapter (envs/microrts.py,
+    reference libs/utils.py:59-76) runs in the mono runtime's CPU actor processes, so
+    ``--env microrts`` picks that runtime under ``--runtime auto`` and is refused on ``gpu``."""
+    if flags.env not in ("synthetic", "microrts"):
+        raise ValueError(f"--env {flags.env!r}: expected synthetic | microrts")
+    runtime = flags.runtime if flags.runtime != "auto" else (
+        "gpu" if want_cuda and flags.env == "synthetic" else "mono")
+    if runtime == "gpu" and flags.env != "synthetic":
+        raise ValueError(f"--env {flags.env} is not available on the gpu runtime (its env workers "
+                         "step the native microRTS stand-in only); use --runtime mono (CPU actor "
+                         "processes over the gym-microrts adapter) or --env synthetic")
+    return runtime
+
+
 def train(flags: Flags) -> dict:
     want_cuda = flags.device == "cuda" or (flags.device == "auto" and torch.cuda.is_available())
     info = D.init_distributed(use_cuda=want_cuda, high_priority=flags.rccl_high_priority)
     dev = torch.device("cuda", info.local_rank) if want_cuda else torch.device("cpu")
-    runtime = flags.runtime if flags.runtime != "auto" else ("gpu" if want_cuda else "mono")
+    runtime = resolve_runtime(flags, want_cuda)
     if runtime == "gpu" and flags.dtype == "fp32":
         # the engine's policy step and the learner are the bf16 MFMA kernels: refuse rather
         # than run bf16 under an fp32 flag
@@ -319,8 +335,15 @@ def train(flags: Flags) -> dict:
                 log(f"[microbeast_amd] {failure}; restarting the actor engine "
                     f"({engine_restarts}/{flags.actor_restarts})")
                 batch = slots = None  # (views of the old runtime's rollout slots)
-                rt = restart_runtime(rt, lambda: make_gpu_runtime(engine_restarts),
-                                     learner.flat, n_update, league)
+                try:
+                    rt = restart_runtime(rt, lambda: make_gpu_runtime(engine_restarts),
+                                         learner.flat, n_update, league)
+                except Exception:
+                    # the peers skipped this round and now wait in the next agree(): tell them
+                    # to stop instead of leaving them blocked until the host-group timeout
+                    # (ADVICE r4); the old runtime is already closed, stop() is a no-op
+                    D.agree(D.FAILED, info)
+                    raise
                 continue
             if runtime == "gpu":
                 lag = rt.policy_lag(slots, n_update)

@@ -39,3 +39,42 @@ def test_test_mode_without_checkpoint_fails(tmp_path):
     assert not (tmp_path / "nock_eval.csv").exists()
     assert main(base + ["--allow_random_init"]) == 0
     assert (tmp_path / "nock_eval.csv").exists()
+
+
+def test_gpu_runtime_refuses_real_env(tmp_path):
+    """the GPU engine steps the native stand-in only, so ``--env microrts``
+    on it must fail loudly instead of silently training on the stand-in."""
+    from microbeast_amd.train import train
+
+    f = parse_flags(["--runtime", "gpu", "--env", "microrts", "--savedir", str(tmp_path),
+                     "--exp_name", "x"], interactive=False)
+    with pytest.raises(ValueError, match="--env microrts is not available on the gpu runtime"):
+        train(f)
+
+
+def test_auto_runtime_routes_real_env_to_mono():
+    """``--runtime auto --env microrts`` picks the CPU actor runtime, whose actor processes
+    build the gym-microrts adapter (runtime/mono.py passes ``env=flags.env`` to create_env);
+    the adapter refuses loudly when gym-microrts is absent."""
+    from microbeast_amd.envs.synthetic import create_env
+    from microbeast_amd.train import resolve_runtime
+
+    real = parse_flags(["--env", "microrts"], interactive=False)
+    assert resolve_runtime(real, want_cuda=True) == "mono"
+    assert resolve_runtime(real, want_cuda=False) == "mono"
+    stand_in = parse_flags([], interactive=False)
+    assert resolve_runtime(stand_in, want_cuda=True) == "gpu"
+    from microbeast_amd.envs.microrts import gym_microrts_available
+
+    if not gym_microrts_available():
+        with pytest.raises(RuntimeError, match="gym-microrts"):
+            create_env(4, 2, 20, env="microrts")
+
+
+def test_unknown_env_raises(tmp_path):
+    from microbeast_amd.train import train
+
+    f = parse_flags(["--env", "atari", "--savedir", str(tmp_path), "--exp_name", "x"],
+                    interactive=False)
+    with pytest.raises(ValueError, match="--env"):
+        train(f)

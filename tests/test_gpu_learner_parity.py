@@ -12,7 +12,10 @@ path run on the GPU under bf16 autocast (MIOpen / hipBLASLt, a different impleme
 against the same fp32 oracle, and for the residual blocks' conv0 layers the spread that
 rounding-level flips of their relu gate cause (their weight gradients are sums with heavy
 cancellation: tests/test_relu_flip_conditioning.py); the HIP path must stay within 3x of that
-floor (or 3 %). No layer has an escape clause.
+floor (or 3 %). The residual conv0 layers are split operand-swap style: the HIP gradient
+against the oracle's operands gated by HIP's own u is held to that same 3x floor, and the gate's
+own effect to 3x the bf16-rounding gate-noise floor (tests/test_relu_flip_conditioning.py's
+noise model, capped at 25 %). No layer has an escape clause.
 (Reference update: libs/utils.py:234-335 with SURVEY §8 D1-D4 fixed.)"""
 import copy
 
@@ -44,35 +47,63 @@ def _gate_hooks(model):
     return caps
 
 
-def _gate_flip_floor(c, w0, u_bf, draws=8):
-    """rel change of conv0's (weight, bias) gradient when its relu gate [u > 0] is recomputed
-    from u plus noise of the size an independent bf16 implementation's u actually deviates
-    from fp32 on this update (per channel: std of torch-bf16's u - u_ref, u_bf). A flip of a few
-    near-zero gates moves the 2x2-stage gradients by percents
-    (tests/test_relu_flip_conditioning.py), which one torch-bf16 sample need not show."""
-    import torch.nn.functional as F
-    x, u, g = (c[k].double() for k in ("x", "u", "g"))
-    w1 = c["w1"]
-    rx = F.relu(x)
-    du0 = torch.nn.grad.conv2d_input(u.shape, w1, g, padding=1)
+# bf16 rounding-size noise on a pre-activation: the model tests/test_relu_flip_conditioning.py
+# validates (absolute + relative bf16 rounding)
+_GATE_ABS, _GATE_REL = 1.5e-4, 2.0 ** -9
 
-    def grads(uu):
-        du = du0 * (uu > 0)
-        return (torch.nn.grad.conv2d_weight(rx, tuple(w0.shape), du, padding=1),
-                du.sum((0, 2, 3)))
-    ref_w, ref_b = grads(u)
-    sig = (u_bf.double()[:u.shape[0]] - u).std(dim=(0, 2, 3), keepdim=True).expand_as(u)
+
+def _conv0_grads(c, w0, gate_u):
+    """fp64 (weight, bias) gradient of a residual block's conv0 from the fp32 oracle's own
+    operands (block input x, block-output gradient g, conv1 weight) with the relu gate
+    [gate_u > 0] of its choice."""
+    import torch.nn.functional as F
+    x, g = c["x"].double(), c["g"].double()
+    du = torch.nn.grad.conv2d_input(c["u"].shape, c["w1"], g, padding=1) * (gate_u > 0)
+    return (torch.nn.grad.conv2d_weight(F.relu(x), tuple(w0.shape), du, padding=1),
+            du.sum((0, 2, 3)))
+
+
+def _rel(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _gate_noise_floor(c, w0, draws=8):
+    """median rel change of conv0's (weight, bias) gradient when its relu gate is recomputed
+    from u plus bf16-rounding-size noise (_GATE_ABS + |u| _GATE_REL): how far a correct bf16
+    implementation's gate alone moves this layer's gradient (rounding-level flips of near-zero
+    pre-activations move these cancellation-heavy sums by percents)."""
+    u = c["u"].double()
+    ref_w, ref_b = _conv0_grads(c, w0, u)
     gen = torch.Generator().manual_seed(1)
     rw, rb = [], []
     for _ in range(draws):
-        gw, gb = grads(u + torch.randn(u.shape, generator=gen, dtype=torch.float64) * sig)
-        rw.append(float((gw - ref_w).norm() / (ref_w.norm() + 1e-30)))
-        rb.append(float((gb - ref_b).norm() / (ref_b.norm() + 1e-30)))
+        noise = torch.randn(u.shape, generator=gen, dtype=torch.float64)
+        gw, gb = _conv0_grads(c, w0, u + noise * (_GATE_ABS + u.abs() * _GATE_REL))
+        rw.append(_rel(gw, ref_w))
+        rb.append(_rel(gb, ref_b))
     return float(np.median(rw)), float(np.median(rb))
 
 
+def _hip_gates(monkeypatch):
+    """Capture the HIP path's own residual conv0 outputs (u0, u1 of every stage, NHWC bf16)
+    as its backward reads them."""
+    from microbeast_amd.ops import encoder as E
+    caps = {}
+    orig = E.HipEncoder.backward
+
+    def bwd(self, g, saved, params):
+        for s in range(len(saved) // 6):
+            _x, _pidx, _p, u0, _y0, u1 = saved[6 * s:6 * s + 6]
+            caps[f"network.{s}.res_block0.conv0."] = u0.detach().float().cpu()
+            caps[f"network.{s}.res_block1.conv0."] = u1.detach().float().cpu()
+        return orig(self, g, saved, params)
+
+    monkeypatch.setattr(E.HipEncoder, "backward", bwd)
+    return caps
+
+
 @pytest.mark.parametrize("S", [8, 16])
-def test_learn_hip_matches_fp32_torch(cuda, S):
+def test_learn_hip_matches_fp32_torch(cuda, S, monkeypatch):
     from microbeast_amd.learner import Learner, LearnerHParams
     from microbeast_amd.models.agent import Agent
 
@@ -97,12 +128,7 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
     hp = LearnerHParams()
     caps = _gate_hooks(ref_model)
     w0s = {n: p.detach().clone() for n, p in ref_model.named_parameters() if n.endswith("conv0.weight")}
-    u_bf = {}  # torch-bf16 conv0 outputs: the deviation size a bf16 implementation has
-    for si in range(len(bf_model.channels)):
-        for bi in (0, 1):
-            cv = getattr(bf_model.network[si], f"res_block{bi}").conv0
-            cv.register_forward_hook(lambda m, i, o, k=f"network.{si}.res_block{bi}.conv0.":
-                                     u_bf.__setitem__(k, o.detach().float().cpu()))
+    hip_u = _hip_gates(monkeypatch)
     Lh = Learner(hip_model, hp, cuda)
     Lr = Learner(ref_model, hp, torch.device("cpu"))
     Lb = Learner(bf_model, hp, cuda)
@@ -114,32 +140,49 @@ def test_learn_hip_matches_fp32_torch(cuda, S):
     gb = Lb.flat.grad.cpu()
     print(f"losses hip {lh.tolist()}\nlosses ref {lr.tolist()}")
     gh, gr = Lh.flat.grad.cpu(), Lr.flat.grad
-    gate = {}  # residual conv0 layers: the relu-gate-flip floor of their gradient
+    # residual conv0 layers, operand-swap split: the HIP gradient against the
+    # oracle's own operands gated by HIP's u (the rest: held to the ordinary bf16 floor), and that
+    # gate's effect against the bf16-rounding gate-noise floor (capped), separately
+    split = {}
     for pre, c in caps.items():
-        fw, fb = _gate_flip_floor(c, w0s[pre + "weight"], u_bf[pre])
-        gate[pre + "weight"], gate[pre + "bias"] = fw, fb
+        n = c["u"].shape[0]
+        u_h = hip_u[pre][:n].permute(0, 3, 1, 2).double()
+        w0 = w0s[pre + "weight"]
+        ref_w, ref_b = _conv0_grads(c, w0, c["u"].double())
+        hg_w, hg_b = _conv0_grads(c, w0, u_h)
+        fw, fb = _gate_noise_floor(c, w0)
+        split[pre + "weight"] = (hg_w.float().flatten(), _rel(hg_w, ref_w), fw)
+        split[pre + "bias"] = (hg_b.float(), _rel(hg_b, ref_b), fb)
     rows, bad = [], []
     for name, o, n, _ in Lr.flat.slices:
         a, b = gh[o:o + n], gr[o:o + n]
         nb = float(b.norm())
         if nb == 0.0:
-            rows.append((name, float(a.abs().max()), 0.0, 1.0))
+            rows.append((name, float(a.abs().max()), 0.0, 1.0, ""))
             if float(a.abs().max()) != 0.0:
                 bad.append(name)
             continue
         rel = float((a - b).norm()) / nb
         # the bf16 floor of this layer: an independent bf16 implementation (torch under
-        # autocast) on the same update, and for residual conv0 layers the spread a rounding-level
-        # flip of their relu gate causes (_gate_flip_floor); the HIP path stays within 3x of it
-        floor = max(float((gb[o:o + n] - b).norm()) / nb, gate.get(name, 0.0))
+        # autocast) on the same update against the same oracle; the HIP path stays within 3x
+        floor = float((gb[o:o + n] - b).norm()) / nb
         cos = float(torch.dot(a, b)) / (float(a.norm()) * nb + 1e-30)
-        rows.append((name, rel, floor, cos))
         tol = max(3.0 * floor, 3e-2)
-        ok = rel < tol and cos > 1.0 - 0.5 * tol ** 2  # (rel ~ sqrt(2 (1 - cos)))
+        note = ""
+        if name in split:  # residual conv0: the rest (HIP vs its own gate) and the gate part
+            ref_gate, gate_rel, gate_floor = split[name]
+            rest = float((a - ref_gate).norm()) / (float(ref_gate.norm()) + 1e-30)
+            gate_tol = min(max(3.0 * gate_floor, 3e-2), 0.25)
+            ok = rest < tol and gate_rel < gate_tol
+            note = (f"  rest {rest:.3e} (tol {tol:.2e})  gate {gate_rel:.3e} "
+                    f"(noise floor {gate_floor:.3e}, tol {gate_tol:.2e})")
+        else:
+            ok = rel < tol and cos > 1.0 - 0.5 * tol ** 2  # (rel ~ sqrt(2 (1 - cos)))
+        rows.append((name, rel, floor, cos, note))
         if not ok:
             bad.append(name)
-    for r in rows:  # full table on failure (pytest -s shows it always)
-        print(f"{r[0]:40s} rel {r[1]:.3e}  bf16 floor {r[2]:.3e}  cos {r[3]:.5f}")
+    for r in rows:  # full table (pytest -s shows it; the floors are printed and pinned here)
+        print(f"{r[0]:40s} rel {r[1]:.3e}  bf16 floor {r[2]:.3e}  cos {r[3]:.5f}{r[4]}")
     # losses: pg, value, entropy, total, mean rho
     torch.testing.assert_close(lh, lr, rtol=2e-2, atol=2e-3)
     assert not bad, f"gradients outside the bf16 noise floor: {bad}"

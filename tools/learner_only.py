@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--T", type=int, default=64)
     ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--active", type=float, default=0.007,
+                    help="fraction of (frame, cell) pairs with a legal action: 0.007 ~ the random-"
+                         "init policy's early game, 0.025 ~ a settled training run (6.5 / 256)")
     ap.add_argument("--no_abits", action="store_true",
                     help="no active-cell bitmap rows in the batch (the head counts from masks)")
     a = ap.parse_args()
@@ -37,9 +40,9 @@ def main():
     learner = Learner(make_model(flags, dev), LearnerHParams(), dev)
     S, T, B = a.size * a.size, a.T, a.batch
     g = torch.Generator(device=dev).manual_seed(1)
-    # ~0.7 % active cells like the engine's rollouts: sparse legal-action masks
+    # sparse legal-action masks with --active of the cells live, like the engine's rollouts
     mask = torch.zeros(T + 1, B, S, 3, dtype=torch.int32, device=dev)
-    act = torch.rand(T + 1, B, S, device=dev, generator=g) < 0.007
+    act = torch.rand(T + 1, B, S, device=dev, generator=g) < a.active
     mask[..., 0] = torch.where(act, torch.randint(1, 2 ** 31 - 1, (T + 1, B, S), device=dev,
                                                   generator=g, dtype=torch.int32), 0)
     batch = {

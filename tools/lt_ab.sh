@@ -1,6 +1,6 @@
 # Same-box A/B of learner-update timelines: for each "VAR=value ..." variant, one
 # rocprofv3 kernel trace of tools/learner_only.py and its per-dispatch table (layer_times.py).
-#   bash tools/lt_ab.sh <tag> "MBK_X=0" "MBK_X=1" ...
+#   [LT_ARGS="--active 0.025"] bash tools/lt_ab.sh <tag> "MBK_X=0" "MBK_X=1" ...
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 tag=$1; shift
@@ -11,7 +11,7 @@ for v in "$@"; do
   i=$((i+1))
   rm -rf /tmp/lt_$i
   (cd /tmp && env $v timeout -k 10 300 rocprofv3 --kernel-trace -d /tmp/lt_$i -o run --output-format csv \
-    -- python $R/tools/learner_only.py --steps 2) > $R/gpurun_out/${tag}_lt$i.log 2>&1 || { tail -5 $R/gpurun_out/${tag}_lt$i.log; exit 1; }
+    -- python $R/tools/learner_only.py --steps 2 $LT_ARGS) > $R/gpurun_out/${tag}_lt$i.log 2>&1 || { tail -5 $R/gpurun_out/${tag}_lt$i.log; exit 1; }
   python $R/tools/layer_times.py /tmp/lt_$i --out $R/gpurun_out/${tag}_lt$i.md > /dev/null || exit 1
   echo "[$v] $(tail -1 $R/gpurun_out/${tag}_lt$i.md)"
 done
