@@ -595,6 +595,205 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ wave-owned forward (8x8)
+// res_fwd16_kernel for IMPALA stage 0 at 16x16 (8x8 maps): every wave owns whole images, so
+// the kernel has no workgroup barrier. Profile r5a (PMC, learner_only): the generic kernel
+// issued ~13 VALU per MFMA -- per 16-pixel block and layer ~20 for the runtime pixel ->
+// (image, y, x) split, 20 v_pk_max for relu on every tap fragment of conv0 / conv2, ~15 in
+// the epilogue -- at 14.9 % MFMA, and its 5 barriers per round of 4 images left the waves
+// parked half of their cycles. Here:
+//  * a wave runs the 4 convs (+ the stage conv and pool) of one image at a time in its own
+//    LDS tiles: the taps another row pair needs were written by the same wave, whose LDS
+//    accesses complete in issue order, so nothing synchronises with the other waves;
+//  * a 16-pixel block is a map row pair, so block j's offsets are the lane's own offset plus
+//    j * 2 rows: instruction immediates, no per-block address math;
+//  * the residual stream is staged twice, raw (Tx: the residual adds, the stage conv) and
+//    relu'd (Tr: conv0 / conv2's taps), the relu applied once per pixel at staging and in
+//    conv1's epilogue instead of once per tap read;
+//  * block j + 1's tap fragments are read while block j's MFMA chain runs;
+//  * the next image's input is loaded into registers during the current image.
+// Same accumulation order and rounding as conv.hip conv_fwd: bit-identical outputs (test).
+namespace w88 {
+constexpr int H = 8, W = 8, HW = 64, PB = 32, RB = 512;
+constexpr int IMGB = ((H + 1) * RB + (W + 2) * PB + 15) & ~15;  // lay16(8, 8).imgb
+constexpr int REG = 3 * IMGB;  // a wave's LDS: Tx, Tr, Tu
+constexpr int TX = 0, TR = IMGB, TU = 2 * IMGB;
+}  // namespace w88
+
+__device__ __forceinline__ uint32_t cvt_pk2(float a, float b) {  // v_cvt_pk_bf16_f32 (RNE)
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, b16x2));
+}
+
+// compiler-only ordering point between a wave's LDS writes and its later reads of them (the
+// hardware completes one wave's LDS instructions in order)
+__device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
+
+template <bool STAGE>
+__global__ __launch_bounds__(kThreads) void res_fwd16_w88_kernel(ResFwdArgs a) {
+  using namespace w88;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  char* R = smem + wave * REG;  // this wave's tiles
+  for (int e = lane; e < REG / 16; e += 64) ((uint4*)R)[e] = make_uint4(0, 0, 0, 0);
+  Frag8 w[4][NCH];
+  float bv[4][4];
+#pragma unroll
+  for (int l = 0; l < 4; ++l) {
+    const uint4* wp = (const uint4*)(a.w[l] + (size_t)li * NCH * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) w[l][c].u = wp[c * 4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[l][i] = a.b[l][4 * g + i];
+  }
+  // STAGE: the next stage's conv weights stay in registers too (an L2 reload per image left
+  // that conv's first MFMAs waiting on it)
+  constexpr int NB = 2;
+  Frag8 ws[NCH][NB];
+  float bsv[NB][4];
+  if constexpr (STAGE) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const uint4* wp = (const uint4*)(a.ws + (size_t)(nb * 16 + li) * NCH * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) ws[c][nb].u = wp[c * 4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bsv[nb][i] = a.bs[nb * 16 + 4 * g + i];
+    }
+  }
+  // this lane's pixel of block 0 (row li / 8, column li % 8): tap (0, 0) offset per K chunk
+  const int lb = (li >> 3) * RB + (li & 7) * PB;
+  int aoff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int tap = 2 * c + (g >> 1), tapc = tap < 9 ? tap : 8;
+    aoff[c] = lb + (tapc / 3) * RB + (tapc % 3) * PB + 16 * (g & 1);
+  }
+  const int ob = lb + RB + PB + 8 * g;              // output pixel (interior), channels 4g..
+  const uint32_t goff = (uint32_t)(li * C + 4 * g) * 2;  // its bytes in a block's HBM rows
+  // staging: this lane's two 16-byte chunks of an image (pixel e / 2, channel half e % 2)
+  int so[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = lane + 64 * k, px = e >> 1;
+    so[k] = ((px >> 3) + 1) * RB + ((px & 7) + 1) * PB + (e & 1) * 16;
+  }
+  const int nw = gridDim.x * (kThreads / 64);
+  int img = blockIdx.x * (kThreads / 64) + wave;
+  uint4 pp[2];
+  auto fetch = [&](int im) {
+    const uint4* src = (const uint4*)(a.p + (size_t)im * HW * C);
+    pp[0] = src[lane];
+    pp[1] = src[lane + 64];
+  };
+  if (img < a.N) fetch(img);
+  for (; img < a.N; img += nw) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      *(uint4*)(R + TX + so[k]) = pp[k];
+      *(uint4*)(R + TR + so[k]) = relu8(pp[k]);
+    }
+    if (img + nw < a.N) fetch(img + nw);
+    wave_lds_order();
+    const size_t gpix = (size_t)img * HW;
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const bool inner = (l & 1) == 0;  // conv0 / conv2: Tr -> u;  conv1 / conv3: Tu, + Tx
+      const int src = inner ? TR : TU;
+      char* gw = (char*)((l == 0 ? a.u0 : l == 1 ? a.y0 : l == 2 ? a.u1 : a.y1) + gpix * C);
+      f32x4 acc[4];
+      Frag8 fr[2][NCH];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) fr[0][c].u = *(const uint4*)(R + src + aoff[c]);
+      // software pipeline in issue order: each MFMA of block j, then one tap read of block
+      // j + 1 (hipcc's scheduler otherwise reuses one fragment register and waits for every
+      // read); the scheduling barriers keep this order, the waitcnt pass then waits only for
+      // the oldest of the five reads in flight
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              w[l][c].v, fr[j & 1][c].v, c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[j], 0, 0, 0);
+          if (j + 1 < 4)
+            fr[(j + 1) & 1][c].u = *(const uint4*)(R + src + (j + 1) * 2 * RB + aoff[c]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = j * 2 * RB + ob;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[j][i] + bv[l][i];
+        if (!inner) {
+          const uint2 ad = *(const uint2*)(R + TX + o);
+          v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
+        }
+        const uint2 out = make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
+        *(uint2*)(gw + j * 16 * C * 2 + goff) = out;
+        const uint2 rl = make_uint2(relu2(out.x), relu2(out.y));
+        if (inner) {
+          *(uint2*)(R + TU + o) = rl;
+        } else if (l == 1) {  // y0: the residual of conv3 (raw) and conv2's input (relu'd)
+          *(uint2*)(R + TX + o) = out;
+          *(uint2*)(R + TR + o) = rl;
+        } else if (STAGE) {
+          *(uint2*)(R + TX + o) = out;  // y1: the stage conv's input (no relu)
+        }
+      }
+      wave_lds_order();
+    }
+    if constexpr (STAGE) {
+      // next stage's conv (16 -> 32) over y1 in Tx -> bf16 staging (aliases Tu) -> pooled output
+      constexpr int OSTR = 2 * C + 4;
+      static_assert(HW * OSTR * 2 <= IMGB, "pre-pool staging must fit the relu(u) tile");
+      bf16* otile = (bf16*)(R + TU);
+      Frag8 fr[2][NCH];
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) fr[0][c].u = *(const uint4*)(R + TX + aoff[c]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f32x4 ac2[NB];
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {  // (the conv layers' software pipeline)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+            ac2[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                ws[c][nb].v, fr[j & 1][c].v, c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : ac2[nb], 0,
+                0, 0);
+          if (j + 1 < 4)
+            fr[(j + 1) & 1][c].u = *(const uint4*)(R + TX + (j + 1) * 2 * RB + aoff[c]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        const int m = j * 16 + li;  // pixel of the image
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          *(uint2*)(otile + m * OSTR + nb * 16 + 4 * g) =
+              make_uint2(cvt_pk2(ac2[nb][0] + bsv[nb][0], ac2[nb][1] + bsv[nb][1]),
+                         cvt_pk2(ac2[nb][2] + bsv[nb][2], ac2[nb][3] + bsv[nb][3]));
+      }
+      wave_lds_order();
+      constexpr int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
+      mbk::pool_tile<2 * C, OSTR, 64>(otile, H, W, 1, (size_t)img * Ho * Wo * 2 * C, a.ps, a.pidx,
+                                      lane);
+      wave_lds_order();
+      // restore Tu's halo ring (conv1 / conv3 read it as zero padding): rows 0 and 9 (10
+      // pixels each) and columns 0 and 9 of rows 1-8, 32 B per pixel
+      if (lane < 36) {
+        const int q = lane;
+        const int off = q < 10 ? q * PB : q < 20 ? 9 * RB + (q - 10) * PB
+                      : q < 28 ? (q - 19) * RB : (q - 27) * RB + 9 * PB;
+        *(uint4*)(R + TU + off) = make_uint4(0, 0, 0, 0);
+        *(uint4*)(R + TU + off + 16) = make_uint4(0, 0, 0, 0);
+      }
+      wave_lds_order();
+    }
+  }
+}
+
 // One 32-channel residual block per launch (stages 1-2 of the IMPALA trunk):
 //   u = conv0(relu x); y = x + conv1(relu u)
 // x is staged once into a halo'd LDS tile (and serves as the residual), relu(u) stays in
@@ -1007,6 +1206,9 @@ size_t resf_smem(int imgs, int H, int W) {
   return 2 * (((size_t)imgs * lay16(H, W).imgb + 15) & ~(size_t)15);
 }
 
+// the wave-owned 8x8 forward (res_fwd16_w88_kernel): three tiles per wave
+constexpr size_t resf_w88_smem() { return (size_t)(kThreads / 64) * w88::REG; }
+
 }  // namespace
 
 static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream);
@@ -1047,14 +1249,17 @@ static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
   // the stage conv's pre-pool staging [imgs*H*W][36] bf16 lives in Tu
   if (st && (size_t)imgs * H * W * (W == 12 ? 2 * C : 2 * C + 4) * 2 > sm / 2)
     return (int)hipErrorInvalidValue;
-  auto kfn = st ? (W == 8 ? res_fwd16_kernel<8, true> : W == 5 ? res_fwd16_kernel<5, true>
+  const bool fast = H == 8 && W == 8;  // (imgs: the generic kernel's round size only)
+  const size_t smf = fast ? resf_w88_smem() : sm;
+  auto kfn = fast ? (st ? res_fwd16_w88_kernel<true> : res_fwd16_w88_kernel<false>)
+           : st ? (W == 8 ? res_fwd16_kernel<8, true> : W == 5 ? res_fwd16_kernel<5, true>
                    : W == 12 ? res_fwd16_kernel<12, true> : W == 4 ? res_fwd16_kernel<4, true>
                    : res_fwd16_kernel<0, true>)
                 : (W == 8 ? res_fwd16_kernel<8, false> : W == 5 ? res_fwd16_kernel<5, false>
                    : W == 12 ? res_fwd16_kernel<12, false> : W == 4 ? res_fwd16_kernel<4, false>
                    : res_fwd16_kernel<0, false>);
-  if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+  if (smf > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)smf);
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1064,16 +1269,17 @@ static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
   }
   const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, smf) !=
           hipSuccess || per < 1)
     per = 1;
-  const int nrounds = (N + imgs - 1) / imgs;
+  // work items: images per wave (wave-owned) or rounds of imgs images per workgroup
+  const int nrounds = fast ? (N + kThreads / 64 - 1) / (kThreads / 64) : (N + imgs - 1) / imgs;
   static const int mult = [] {  // see conv.hip fwd_grid
     const char* e = getenv("MBK_FWD_GRID_MULT");
     return e ? std::max(1, atoi(e)) : 1;
   }();
   hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)ncu * per * mult))),
-                     dim3(kThreads), sm, stream, a);
+                     dim3(kThreads), smf, stream, a);
   return (int)hipGetLastError();
 }
 
