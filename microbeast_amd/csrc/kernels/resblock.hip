@@ -71,6 +71,24 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
       (s16x4 __attribute__((address_space(3)))*)(uintptr_t)(lds_addr));
 }
 
+// 8x8-map tile geometry of the wave-owned kernels (res_fwd16_w88 / res_bwd16_w88): lay16(8, 8)
+namespace w88 {
+constexpr int H = 8, W = 8, HW = 64, PB = 32, RB = 512;
+constexpr int IMGB = ((H + 1) * RB + (W + 2) * PB + 15) & ~15;  // lay16(8, 8).imgb
+constexpr int REG = 3 * IMGB;  // a wave's LDS: Tx, Tr, Tu
+constexpr int TX = 0, TR = IMGB, TU = 2 * IMGB;
+}  // namespace w88
+
+__device__ __forceinline__ uint32_t cvt_pk2(float a, float b) {  // v_cvt_pk_bf16_f32 (RNE)
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, b16x2));
+}
+
+// compiler-only ordering point between a wave's LDS writes and its later reads of them (the
+// hardware completes one wave's LDS instructions in order)
+__device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
+
 struct ResBwdArgs {
   const bf16* x;     // block input (pre-relu)      [N][H][W][16]
   const bf16* u;     // conv0 output (pre-relu)     [N][H][W][16]
@@ -368,13 +386,239 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ wave-owned backward (8x8)
+// res_bwd16_kernel for IMPALA stage 0 at 16x16 (8x8 maps), with res_fwd16_w88_kernel's
+// structure: each wave owns whole images in its own LDS tiles (Tg = g, Tu = relu u, Tx = relu x,
+// Td = du), so the rounds need no workgroup barrier (the generic kernel had 3 per round of 4
+// images and sat at 19.9 % MFMA, profile r5a); block j of the dgrads is map row pair j and
+// K block kb of the weight gradients is rows 4 kb .. 4 kb + 3, so their offsets are
+// immediates; tap reads are software-pipelined against the MFMA chains. Per image:
+//   du = conv1^T(g) * [u > 0] -> Td; dW1 += relu(u) (x) g;
+//   dx = conv0^T(du) * [x > 0] + g -> HBM; dW0 += relu(x) (x) du.
+// Weight gradients stay in each wave's MFMA accumulators; the workgroup sums its 4 waves' in a
+// fixed order at the end (the generic kernel's reduction, same partial rows). du / dx are
+// bit-identical to the per-layer kernels; the weight gradients differ by fp32 summation order.
+namespace w88b {
+constexpr int RB = w88::RB, PB = w88::PB, IMGB = w88::IMGB;
+constexpr int REG = 4 * IMGB;  // a wave's LDS: Tg, Tu, Tx, Td
+constexpr int TG = 0, TU = IMGB, TX = 2 * IMGB, TD = 3 * IMGB;
+}  // namespace w88b
+
+__global__ __launch_bounds__(kThreads) void res_bwd16_w88_kernel(ResBwdArgs a) {
+  using namespace w88b;
+  constexpr int HW = 64;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  char* R = smem + wave * REG;
+  for (int e = lane; e < REG / 16; e += 64) ((uint4*)R)[e] = make_uint4(0, 0, 0, 0);
+  Frag8 w1[NCH], w0[NCH];  // dgrad weights (A fragments): lane holds w[co = li][chunk c][8g..]
+  {
+    const uint4* p1 = (const uint4*)(a.w1t + (size_t)li * NCH * 32 + g * 8);
+    const uint4* p0 = (const uint4*)(a.w0t + (size_t)li * NCH * 32 + g * 8);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      w1[c].u = p1[c * 4];
+      w0[c].u = p0[c * 4];
+    }
+  }
+  f32x4 acc1[9], acc0[9];  // wgrad accumulators, tap t: rows co = 4G + i, cols ci = li
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // dgrad: this lane's pixel of row pair 0, tap (0, 0) offset per K chunk
+  const int lb = (li >> 3) * RB + (li & 7) * PB;
+  int aoff[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int tap = 2 * c + (g >> 1), tapc = tap < 9 ? tap : 8;
+    aoff[c] = lb + (tapc / 3) * RB + (tapc % 3) * PB + 16 * (g & 1);
+  }
+  const int ob = lb + RB + PB + 8 * g;  // output pixel (interior), channels 4g..
+  const uint32_t goff = (uint32_t)(li * C + 4 * g) * 2;
+  // wgrad K block 0 (rows 0-3): half h's pixel of this lane group is row g, column
+  // 4 h + li / 4; the dY (A) read starts at channel 4 (li % 4), the X (B) taps at 8 (li % 4) B
+  int xo[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) xo[h] = g * RB + (4 * h + (li >> 2)) * PB;
+  const int ao = RB + PB + 8 * (li & 3), bo = 8 * (li & 3);
+  int so[2];  // staging: this lane's two 16-byte chunks of an image
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = lane + 64 * k, px = e >> 1;
+    so[k] = ((px >> 3) + 1) * RB + ((px & 7) + 1) * PB + (e & 1) * 16;
+  }
+  // bias gradients as one more MFMA per K block: dY (A) times an all-ones B fragment, so every
+  // column of accb* holds the row's pixel sum (no per-element VALU adds, no extra registers
+  // beyond the accumulator)
+  f32x4 accb1 = f32x4{0.f, 0.f, 0.f, 0.f}, accb0 = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag8 ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  const int nw = gridDim.x * (kThreads / 64);
+  int img = blockIdx.x * (kThreads / 64) + wave;
+  uint4 px[2], pu[2], pg[2];
+  auto fetch = [&](int im) {
+    const size_t o = (size_t)im * HW * 2;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      px[k] = ((const uint4*)a.x)[o + lane + 64 * k];
+      pu[k] = ((const uint4*)a.u)[o + lane + 64 * k];
+      pg[k] = ((const uint4*)a.g)[o + lane + 64 * k];
+    }
+  };
+  // one dgrad pass (4 row-pair blocks x 5 K chunks = 20 MFMAs, step st = 5 j + c) from tile S
+  // with weights W; each tap read is issued DD steps ahead of its MFMA (a ring of DD + 1
+  // fragments instead of two blocks' 10: the kernel stays within 2 waves per SIMD)
+  auto dgrad = [&](int S, const Frag8* W, f32x4* acc) {
+    constexpr int DD = 3;
+    Frag8 fr[20];
+    auto rd = [&](int st) {
+      fr[st].u = *(const uint4*)(R + S + (st / NCH) * 2 * RB + aoff[st % NCH]);
+    };
+#pragma unroll
+    for (int st = 0; st < DD; ++st) rd(st);
+#pragma unroll
+    for (int st = 0; st < 20; ++st) {
+      const int j = st / NCH, c = st % NCH;
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          W[c].v, fr[st].v, c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[j], 0, 0, 0);
+      if (st + DD < 20) rd(st + DD);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // one weight-gradient pass over the image's 2 K blocks (18 MFMAs: K block kb = s / 9, tap
+  // t = s % 9): dY from tile D (interior), X taps from tile X, the tap reads DW steps ahead of
+  // their MFMA (a ring of DW fragments in flight, not two K blocks' 18)
+  auto wgrad = [&](int D, int X, f32x4* acc, f32x4& accb) {
+    constexpr int DW = 4;
+    Frag8 af[2], bf[18];
+    auto rd_b = [&](int st) {
+      const int kb = st / 9, t = st % 9;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        bf[st].h[h] = tr_read(R + X + kb * 4 * RB + xo[h] + bo + (t / 3) * RB + (t % 3) * PB);
+    };
+#pragma unroll
+    for (int h = 0; h < 2; ++h) af[0].h[h] = tr_read(R + D + xo[h] + ao);
+#pragma unroll
+    for (int st = 0; st < DW; ++st) rd_b(st);
+#pragma unroll
+    for (int st = 0; st < 18; ++st) {
+      const int kb = st / 9, t = st % 9;
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kb].v, bf[st].v, acc[t], 0, 0, 0);
+      if (t == 8) accb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kb].v, ones.v, accb, 0, 0, 0);
+      if (st + DW < 18) rd_b(st + DW);
+      if (st == 4) {  // K block 1 = rows 4-7: its dY fragment
+#pragma unroll
+        for (int h = 0; h < 2; ++h) af[1].h[h] = tr_read(R + D + 4 * RB + xo[h] + ao);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  if (img < a.N) fetch(img);
+  for (; img < a.N; img += nw) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      *(uint4*)(R + TX + so[k]) = relu8(px[k]);
+      *(uint4*)(R + TU + so[k]) = relu8(pu[k]);
+      *(uint4*)(R + TG + so[k]) = pg[k];
+    }
+    if (img + nw < a.N) fetch(img + nw);
+    wave_lds_order();
+    // ---- du = conv1^T(g) * [u > 0] -> Td
+    f32x4 acc[4];
+    dgrad(TG, w1, acc);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = j * 2 * RB + ob;
+      const uint2 mu = *(const uint2*)(R + TU + o);
+      const uint32_t mw[2] = {mu.x, mu.y};
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[j][i] : 0.f;
+      }
+      const uint2 du = make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
+      *(uint2*)(R + TD + o) = du;
+    }
+    // ---- dW1 += relu(u) (x) g
+    wgrad(TG, TU, acc1, accb1);
+    wave_lds_order();
+    // ---- dx = conv0^T(du) * [x > 0] + g -> HBM
+    dgrad(TD, w0, acc);
+    char* gdx = (char*)(a.dx + (size_t)img * HW * C);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int o = j * 2 * RB + ob;
+      const uint2 mx = *(const uint2*)(R + TX + o), ad = *(const uint2*)(R + TG + o);
+      const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[j][i] : 0.f;
+        v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
+      }
+      *(uint2*)(gdx + j * 16 * C * 2 + goff) = make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
+    }
+    // ---- dW0 += relu(x) (x) du
+    wgrad(TD, TX, acc0, accb0);
+    wave_lds_order();
+  }
+  __syncthreads();  // every wave's tiles are dead: the reduction reuses the LDS
+  // ---- per-workgroup partial rows: the 4 waves' accumulators summed through LDS in a fixed
+  // order (deterministic), then the bias sums (res_bwd16_kernel's reduction)
+  float* red = (float*)smem;  // [C][KTOT]
+  for (int which = 0; which < 2; ++which) {
+    float* out = a.partial + which * a.lstride + (size_t)blockIdx.x * ROW;
+    for (int w = 0; w < kThreads / 64; ++w) {
+      if (wave == w) {
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int co = 4 * g + i, n = t * C + li;
+            float* p = red + co * KTOT + n;
+            const float v = which == 0 ? acc1[t][i] : acc0[t][i];
+            *p = (w == 0 ? 0.f : *p) + v;
+          }
+      }
+      __syncthreads();
+    }
+    for (int e = tid; e < C * KTOT / 4; e += kThreads) ((float4*)out)[e] = ((const float4*)red)[e];
+    __syncthreads();
+  }
+  // bias: column 0 of each wave's all-ones accumulator (rows co = 4g + i), waves summed in order
+  for (int which = 0; which < 2; ++which) {
+    if (li == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[wave * C + 4 * g + i] = which == 0 ? accb1[i] : accb0[i];
+    __syncthreads();
+    if (tid < C) {
+      float s = 0.f;
+      for (int w = 0; w < kThreads / 64; ++w) s += red[w * C + tid];
+      a.partial[which * a.lstride + (size_t)blockIdx.x * ROW + C * KTOT + tid] = s;
+    }
+    __syncthreads();
+  }
+}
+
+constexpr size_t res_w88b_smem() { return (size_t)(kThreads / 64) * w88b::REG; }
+
 size_t res_smem(int imgs, int H, int W) {
   const size_t tb = ((size_t)imgs * lay16(H, W).imgb + 15) & ~(size_t)15;
   return 4 * tb + 64;
 }
 
+// the wave-owned 8x8 backward runs whole images per wave: any imgs, 4 images per round
+bool res_bwd_w88(int H, int W) { return H == 8 && W == 8; }
+
 int res_grid(int N, int H, int W, int imgs) {
-  const size_t sm = res_smem(imgs, H, W);
+  if (res_bwd_w88(H, W)) imgs = kThreads / 64;
+  const size_t sm = res_bwd_w88(H, W) ? res_w88b_smem() : res_smem(imgs, H, W);
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -383,7 +627,8 @@ int res_grid(int N, int H, int W, int imgs) {
     if (cus <= 0) cus = 256;
   }
   const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
-  const void* kfn = (const void*)res_bwd16_kernel<0>;  // same resources for every width
+  const void* kfn = res_bwd_w88(H, W) ? (const void*)res_bwd16_w88_kernel
+                                       : (const void*)res_bwd16_kernel<0>;  // (every width)
   if (sm > 64 * 1024) (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
@@ -613,23 +858,6 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_kernel(ResFwdArgs a) {
 //  * block j + 1's tap fragments are read while block j's MFMA chain runs;
 //  * the next image's input is loaded into registers during the current image.
 // Same accumulation order and rounding as conv.hip conv_fwd: bit-identical outputs (test).
-namespace w88 {
-constexpr int H = 8, W = 8, HW = 64, PB = 32, RB = 512;
-constexpr int IMGB = ((H + 1) * RB + (W + 2) * PB + 15) & ~15;  // lay16(8, 8).imgb
-constexpr int REG = 3 * IMGB;  // a wave's LDS: Tx, Tr, Tu
-constexpr int TX = 0, TR = IMGB, TU = 2 * IMGB;
-}  // namespace w88
-
-__device__ __forceinline__ uint32_t cvt_pk2(float a, float b) {  // v_cvt_pk_bf16_f32 (RNE)
-  typedef float f32x2 __attribute__((ext_vector_type(2)));
-  typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, b16x2));
-}
-
-// compiler-only ordering point between a wave's LDS writes and its later reads of them (the
-// hardware completes one wave's LDS instructions in order)
-__device__ __forceinline__ void wave_lds_order() { asm volatile("" ::: "memory"); }
-
 template <bool STAGE>
 __global__ __launch_bounds__(kThreads) void res_fwd16_w88_kernel(ResFwdArgs a) {
   using namespace w88;
@@ -1298,11 +1526,12 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
                              int imgs, int accumulate, hipStream_t stream) {
   if (N <= 0) return 0;
   if (nparts < 1 || nparts != mbk_res_bwd16_parts(N, H, W, imgs)) return (int)hipErrorInvalidValue;
-  const size_t sm = res_smem(imgs, H, W);
+  const bool fast = res_bwd_w88(H, W);
+  const size_t sm = fast ? res_w88b_smem() : res_smem(imgs, H, W);
   const int64_t lstride = (int64_t)(nparts + (nparts + 31) / 32) * ROW;
   ResBwdArgs a{(const bf16*)x, (const bf16*)u, (const bf16*)g, (bf16*)dx,
                (const bf16*)w1t, (const bf16*)w0t, partial, lstride, N, H, W, imgs};
-  auto kfn = W == 8 ? res_bwd16_kernel<8> : W == 5 ? res_bwd16_kernel<5>
+  auto kfn = fast ? res_bwd16_w88_kernel : W == 5 ? res_bwd16_kernel<5>
            : W == 12 ? res_bwd16_kernel<12> : W == 4 ? res_bwd16_kernel<4> : res_bwd16_kernel<0>;
   if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
