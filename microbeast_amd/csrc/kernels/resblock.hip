@@ -386,49 +386,55 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ wave-owned backward (8x8)
-// res_bwd16_kernel for IMPALA stage 0 at 16x16 (8x8 maps), with res_fwd16_w88_kernel's
-// structure: each wave owns whole images in its own LDS tiles (Tg = g, Tu = relu u, Tx = relu x,
-// Td = du), so the rounds need no workgroup barrier (the generic kernel had 3 per round of 4
-// images and sat at 19.9 % MFMA, profile r5a); block j of the dgrads is map row pair j and
-// K block kb of the weight gradients is rows 4 kb .. 4 kb + 3, so their offsets are
-// immediates; tap reads are software-pipelined against the MFMA chains. Per image:
-//   du = conv1^T(g) * [u > 0] -> Td; dW1 += relu(u) (x) g;
-//   dx = conv0^T(du) * [x > 0] + g -> HBM; dW0 += relu(x) (x) du.
-// Weight gradients stay in each wave's MFMA accumulators; the workgroup sums its 4 waves' in a
-// fixed order at the end (the generic kernel's reduction, same partial rows). du / dx are
-// bit-identical to the per-layer kernels; the weight gradients differ by fp32 summation order.
+// ------------------------------------------------------------------ wave-pair backward (8x8)
+// res_bwd16_kernel for IMPALA stage 0 at 16x16 (8x8 maps). The generic kernel ran 3 workgroup
+// barriers per round of 4 images at 19.9 % MFMA (profile r5a); a wave-owned version (each wave
+// whole images, dgrads and weight gradients) needed 276 registers -- the two layers' 72
+// weight-gradient accumulators next to the dgrad weights -- so one wave per SIMD, every latency
+// exposed (1.28 ms, 21.7 % MFMA); splitting each image over a wave pair synchronised by
+// workgroup barriers (3 per 4 images) left the waves parked 58 % of their cycles (1.25 ms).
+// Here 8 waves form 4 independent producer / consumer pairs, each pair on one SIMD:
+//   D-wave p (waves 0-3): stages x, u, g; du = conv1^T(g) * [u > 0] -> Td; dx = conv0^T(du) *
+//     [x > 0] + g -> HBM (dgrad weights in VGPRs);
+//   W-wave p + 4 (waves 4-7): dW1 += relu(u) (x) g, dW0 += relu(x) (x) du (accumulators in AGPRs
+//     for the whole launch),
+// over two sets of the pair's LDS tiles (Tg = g, Tu = relu u, Tx = relu x, Td = du), image i in
+// set i % 2, synchronised by three per-pair LDS flags per set (staged / du written / consumed)
+// instead of workgroup barriers: a wave's LDS writes complete in issue order, so a flag written
+// after the data publishes it. Block j of the dgrads is map row pair j and K block kb of the
+// weight gradients rows 4 kb .. 4 kb + 3, so their offsets are immediates; tap reads are
+// software-pipelined against the MFMA chains. du / dx are bit-identical to the per-layer
+// kernels; the weight gradients differ by fp32 summation order (the W-waves' fixed-order sum).
 namespace w88b {
 constexpr int RB = w88::RB, PB = w88::PB, IMGB = w88::IMGB;
-constexpr int REG = 4 * IMGB;  // a wave's LDS: Tg, Tu, Tx, Td
+constexpr int SET = 4 * IMGB;  // one tile set: Tg, Tu, Tx, Td
+constexpr int REG = 2 * SET;   // a pair's LDS
 constexpr int TG = 0, TU = IMGB, TX = 2 * IMGB, TD = 3 * IMGB;
+constexpr int kPT = 512;        // 4 pairs
+constexpr int FLAGS = 4 * REG;  // per pair, per set: staged, du written, consumed (iteration #)
 }  // namespace w88b
 
-__global__ __launch_bounds__(kThreads) void res_bwd16_w88_kernel(ResBwdArgs a) {
+// spin until an LDS flag reaches v (written by the other wave of the pair)
+__device__ __forceinline__ void wait_flag(const int* f, int v) {
+  while (*(const volatile int*)f < v) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void set_flag(int* f, int v, int lane) {
+  if (lane == 0) *(volatile int*)f = v;
+}
+
+__global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) {
   using namespace w88b;
   constexpr int HW = 64;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
-  char* R = smem + wave * REG;
-  for (int e = lane; e < REG / 16; e += 64) ((uint4*)R)[e] = make_uint4(0, 0, 0, 0);
-  Frag8 w1[NCH], w0[NCH];  // dgrad weights (A fragments): lane holds w[co = li][chunk c][8g..]
-  {
-    const uint4* p1 = (const uint4*)(a.w1t + (size_t)li * NCH * 32 + g * 8);
-    const uint4* p0 = (const uint4*)(a.w0t + (size_t)li * NCH * 32 + g * 8);
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      w1[c].u = p1[c * 4];
-      w0[c].u = p0[c * 4];
-    }
-  }
-  f32x4 acc1[9], acc0[9];  // wgrad accumulators, tap t: rows co = 4G + i, cols ci = li
-#pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  // dgrad: this lane's pixel of row pair 0, tap (0, 0) offset per K chunk
+  const bool dw = wave < 4;  // D-wave (dgrads) or W-wave (weight gradients)
+  const int pair = wave & 3;
+  char* R = smem + pair * REG;
+  int* fl = (int*)(smem + FLAGS) + pair * 6;  // [set][staged, du, consumed]
+  for (int e = tid; e < FLAGS / 16; e += kPT) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
+  if (tid < 24) ((int*)(smem + FLAGS))[tid] = 0;
+  // dgrad (D-waves): this lane's pixel of row pair 0, tap (0, 0) offset per K chunk
   const int lb = (li >> 3) * RB + (li & 7) * PB;
   int aoff[NCH];
 #pragma unroll
@@ -438,11 +444,14 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_w88_kernel(ResBwdArgs a) {
   }
   const int ob = lb + RB + PB + 8 * g;  // output pixel (interior), channels 4g..
   const uint32_t goff = (uint32_t)(li * C + 4 * g) * 2;
-  // wgrad K block 0 (rows 0-3): half h's pixel of this lane group is row g, column
-  // 4 h + li / 4; the dY (A) read starts at channel 4 (li % 4), the X (B) taps at 8 (li % 4) B
+  // wgrad (W-waves) K block 0 (rows 0-3): any pixel order along K will do as long as dY (A)
+  // and X (B) agree, so half h's pixel of lane group g is row 2 (g / 2) + h, column
+  // 4 (g % 2) + li / 4: each 32-lane half of a transposed read then covers one whole map row,
+  // 256 contiguous bytes = all 64 banks (rows g and g + 1, 512 B apart, were 2-way conflicts);
+  // the dY read starts at channel 4 (li % 4), the X taps at 8 (li % 4) B
   int xo[2];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) xo[h] = g * RB + (4 * h + (li >> 2)) * PB;
+  for (int h = 0; h < 2; ++h) xo[h] = (2 * (g >> 1) + h) * RB + (4 * (g & 1) + (li >> 2)) * PB;
   const int ao = RB + PB + 8 * (li & 3), bo = 8 * (li & 3);
   int so[2];  // staging: this lane's two 16-byte chunks of an image
 #pragma unroll
@@ -450,58 +459,137 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_w88_kernel(ResBwdArgs a) {
     const int e = lane + 64 * k, px = e >> 1;
     so[k] = ((px >> 3) + 1) * RB + ((px & 7) + 1) * PB + (e & 1) * 16;
   }
+  const int step = gridDim.x * 4;
+  const int first = blockIdx.x * 4 + pair;  // the pair's images: first, first + step, ...
+  __syncthreads();  // zeroed tiles and flags
+  if (dw) {
+    Frag8 w1[NCH], w0[NCH];  // dgrad weights (A fragments): lane holds w[co = li][chunk c][8g..]
+    {
+      const uint4* p1 = (const uint4*)(a.w1t + (size_t)li * NCH * 32 + g * 8);
+      const uint4* p0 = (const uint4*)(a.w0t + (size_t)li * NCH * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        w1[c].u = p1[c * 4];
+        w0[c].u = p0[c * 4];
+      }
+    }
+    // one dgrad pass (4 row-pair blocks x 5 K chunks = 20 MFMAs, step st = 5 j + c) from tile
+    // S with weights W; each tap read issued DD steps ahead of its MFMA
+    auto dgrad = [&](const char* S, const Frag8* W, f32x4* acc) {
+      constexpr int DD = 8;
+      Frag8 fr[20];
+      auto rd = [&](int st) {
+        fr[st].u = *(const uint4*)(S + (st / NCH) * 2 * RB + aoff[st % NCH]);
+      };
+#pragma unroll
+      for (int st = 0; st < DD; ++st) rd(st);
+#pragma unroll
+      for (int st = 0; st < 20; ++st) {
+        const int j = st / NCH, c = st % NCH;
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            W[c].v, fr[st].v, c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[j], 0, 0, 0);
+        if (st + DD < 20) rd(st + DD);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    uint4 px[2], pu[2], pg[2];
+    auto fetch = [&](int im) {
+      const size_t o = (size_t)im * HW * 2;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        px[k] = ((const uint4*)a.x)[o + lane + 64 * k];
+        pu[k] = ((const uint4*)a.u)[o + lane + 64 * k];
+        pg[k] = ((const uint4*)a.g)[o + lane + 64 * k];
+      }
+    };
+    if (first < a.N) fetch(first);
+    int it = 1;
+    for (int img = first; img < a.N; img += step, ++it) {
+      const int b = it & 1;
+      char* T = R + b * SET;
+      int* f = fl + 3 * b;
+      if (it > 2) wait_flag(f + 2, it - 2);  // the W-wave is done with this set's last image
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        *(uint4*)(T + TX + so[k]) = relu8(px[k]);
+        *(uint4*)(T + TU + so[k]) = relu8(pu[k]);
+        *(uint4*)(T + TG + so[k]) = pg[k];
+      }
+      set_flag(f, it, lane);  // staged
+      if (img + step < a.N) fetch(img + step);
+      wave_lds_order();
+      f32x4 acc[4];
+      // du = conv1^T(g) * [u > 0] -> Td (the epilogue's mask words read ahead of the MFMAs)
+      uint2 mus[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mus[j] = *(const uint2*)(T + TU + j * 2 * RB + ob);
+      dgrad(T + TG, w1, acc);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = j * 2 * RB + ob;
+        const uint2 mu = mus[j];
+        const uint32_t mw[2] = {mu.x, mu.y};
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+          v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[j][i] : 0.f;
+        }
+        *(uint2*)(T + TD + o) = make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
+      }
+      set_flag(f + 1, it, lane);  // du written
+      wave_lds_order();
+      // dx = conv0^T(du) * [x > 0] + g -> HBM
+      uint2 mxs[4], ads[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mxs[j] = *(const uint2*)(T + TX + j * 2 * RB + ob);
+        ads[j] = *(const uint2*)(T + TG + j * 2 * RB + ob);
+      }
+      dgrad(T + TD, w0, acc);
+      char* gdx = (char*)(a.dx + (size_t)img * HW * C);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint2 mx = mxs[j], ad = ads[j];
+        const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+          v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[j][i] : 0.f;
+          v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
+        }
+        *(uint2*)(gdx + j * 16 * C * 2 + goff) =
+            make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
+      }
+      wave_lds_order();
+    }
+    __syncthreads();  // (the W-waves' matching barrier: every pair is done)
+  } else {  // ---------------- W-waves
+  f32x4 acc1[9], acc0[9];  // wgrad accumulators, tap t: rows co = 4G + i, cols ci = li
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc0[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   // bias gradients as one more MFMA per K block: dY (A) times an all-ones B fragment, so every
-  // column of accb* holds the row's pixel sum (no per-element VALU adds, no extra registers
-  // beyond the accumulator)
+  // column of accb* holds the row's pixel sum
   f32x4 accb1 = f32x4{0.f, 0.f, 0.f, 0.f}, accb0 = f32x4{0.f, 0.f, 0.f, 0.f};
   Frag8 ones;
   ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-  const int nw = gridDim.x * (kThreads / 64);
-  int img = blockIdx.x * (kThreads / 64) + wave;
-  uint4 px[2], pu[2], pg[2];
-  auto fetch = [&](int im) {
-    const size_t o = (size_t)im * HW * 2;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      px[k] = ((const uint4*)a.x)[o + lane + 64 * k];
-      pu[k] = ((const uint4*)a.u)[o + lane + 64 * k];
-      pg[k] = ((const uint4*)a.g)[o + lane + 64 * k];
-    }
-  };
-  // one dgrad pass (4 row-pair blocks x 5 K chunks = 20 MFMAs, step st = 5 j + c) from tile S
-  // with weights W; each tap read is issued DD steps ahead of its MFMA (a ring of DD + 1
-  // fragments instead of two blocks' 10: the kernel stays within 2 waves per SIMD)
-  auto dgrad = [&](int S, const Frag8* W, f32x4* acc) {
-    constexpr int DD = 3;
-    Frag8 fr[20];
-    auto rd = [&](int st) {
-      fr[st].u = *(const uint4*)(R + S + (st / NCH) * 2 * RB + aoff[st % NCH]);
-    };
-#pragma unroll
-    for (int st = 0; st < DD; ++st) rd(st);
-#pragma unroll
-    for (int st = 0; st < 20; ++st) {
-      const int j = st / NCH, c = st % NCH;
-      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-          W[c].v, fr[st].v, c == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[j], 0, 0, 0);
-      if (st + DD < 20) rd(st + DD);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
   // one weight-gradient pass over the image's 2 K blocks (18 MFMAs: K block kb = s / 9, tap
-  // t = s % 9): dY from tile D (interior), X taps from tile X, the tap reads DW steps ahead of
-  // their MFMA (a ring of DW fragments in flight, not two K blocks' 18)
-  auto wgrad = [&](int D, int X, f32x4* acc, f32x4& accb) {
-    constexpr int DW = 4;
+  // t = s % 9): dY from tile D (interior), X taps from tile X, each tap read DW steps ahead
+  auto wgrad = [&](const char* D, const char* X, f32x4* acc, f32x4& accb) {
+    constexpr int DW = 8;
     Frag8 af[2], bf[18];
     auto rd_b = [&](int st) {
       const int kb = st / 9, t = st % 9;
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        bf[st].h[h] = tr_read(R + X + kb * 4 * RB + xo[h] + bo + (t / 3) * RB + (t % 3) * PB);
+        bf[st].h[h] = tr_read(X + kb * 4 * RB + xo[h] + bo + (t / 3) * RB + (t % 3) * PB);
     };
 #pragma unroll
-    for (int h = 0; h < 2; ++h) af[0].h[h] = tr_read(R + D + xo[h] + ao);
+    for (int h = 0; h < 2; ++h) af[0].h[h] = tr_read(D + xo[h] + ao);
 #pragma unroll
     for (int st = 0; st < DW; ++st) rd_b(st);
 #pragma unroll
@@ -512,101 +600,61 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_w88_kernel(ResBwdArgs a) {
       if (st + DW < 18) rd_b(st + DW);
       if (st == 4) {  // K block 1 = rows 4-7: its dY fragment
 #pragma unroll
-        for (int h = 0; h < 2; ++h) af[1].h[h] = tr_read(R + D + 4 * RB + xo[h] + ao);
+        for (int h = 0; h < 2; ++h) af[1].h[h] = tr_read(D + 4 * RB + xo[h] + ao);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  if (img < a.N) fetch(img);
-  for (; img < a.N; img += nw) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      *(uint4*)(R + TX + so[k]) = relu8(px[k]);
-      *(uint4*)(R + TU + so[k]) = relu8(pu[k]);
-      *(uint4*)(R + TG + so[k]) = pg[k];
-    }
-    if (img + nw < a.N) fetch(img + nw);
+  int it = 1;
+  for (int img = first; img < a.N; img += step, ++it) {
+    const int b = it & 1;
+    const char* T = R + b * SET;
+    int* f = fl + 3 * b;
+    wait_flag(f, it);  // staged
+    wgrad(T + TG, T + TU, acc1, accb1);  // dW1 += relu(u) (x) g
+    wait_flag(f + 1, it);  // du written
+    wgrad(T + TD, T + TX, acc0, accb0);  // dW0 += relu(x) (x) du
     wave_lds_order();
-    // ---- du = conv1^T(g) * [u > 0] -> Td
-    f32x4 acc[4];
-    dgrad(TG, w1, acc);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int o = j * 2 * RB + ob;
-      const uint2 mu = *(const uint2*)(R + TU + o);
-      const uint32_t mw[2] = {mu.x, mu.y};
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[j][i] : 0.f;
-      }
-      const uint2 du = make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
-      *(uint2*)(R + TD + o) = du;
-    }
-    // ---- dW1 += relu(u) (x) g
-    wgrad(TG, TU, acc1, accb1);
-    wave_lds_order();
-    // ---- dx = conv0^T(du) * [x > 0] + g -> HBM
-    dgrad(TD, w0, acc);
-    char* gdx = (char*)(a.dx + (size_t)img * HW * C);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int o = j * 2 * RB + ob;
-      const uint2 mx = *(const uint2*)(R + TX + o), ad = *(const uint2*)(R + TG + o);
-      const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
-      float v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        v[i] = (__uint_as_float(hb << 16) > 0.f) ? acc[j][i] : 0.f;
-        v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
-      }
-      *(uint2*)(gdx + j * 16 * C * 2 + goff) = make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
-    }
-    // ---- dW0 += relu(x) (x) du
-    wgrad(TD, TX, acc0, accb0);
-    wave_lds_order();
+    set_flag(f + 2, it, lane);  // consumed
   }
-  __syncthreads();  // every wave's tiles are dead: the reduction reuses the LDS
-  // ---- per-workgroup partial rows: the 4 waves' accumulators summed through LDS in a fixed
-  // order (deterministic), then the bias sums (res_bwd16_kernel's reduction)
-  float* red = (float*)smem;  // [C][KTOT]
-  for (int which = 0; which < 2; ++which) {
-    float* out = a.partial + which * a.lstride + (size_t)blockIdx.x * ROW;
-    for (int w = 0; w < kThreads / 64; ++w) {
-      if (wave == w) {
+  __syncthreads();  // every pair is done: the tiles are dead
+  // every tile is dead after the last (3): each W-wave parks its accumulators in its own slot
+  float* red = (float*)smem;
 #pragma unroll
-        for (int t = 0; t < 9; ++t)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int co = 4 * g + i, n = t * C + li;
-            float* p = red + co * KTOT + n;
-            const float v = which == 0 ? acc1[t][i] : acc0[t][i];
-            *p = (w == 0 ? 0.f : *p) + v;
-          }
-      }
-      __syncthreads();
-    }
-    for (int e = tid; e < C * KTOT / 4; e += kThreads) ((float4*)out)[e] = ((const float4*)red)[e];
-    __syncthreads();
-  }
-  // bias: column 0 of each wave's all-ones accumulator (rows co = 4g + i), waves summed in order
   for (int which = 0; which < 2; ++which) {
+    float* sl = red + (which * 4 + pair) * (C * KTOT);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        sl[(4 * g + i) * KTOT + t * C + li] = which == 0 ? acc1[t][i] : acc0[t][i];
     if (li == 0)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[wave * C + 4 * g + i] = which == 0 ? accb1[i] : accb0[i];
-    __syncthreads();
+      for (int i = 0; i < 4; ++i)
+        red[8 * C * KTOT + (which * 4 + pair) * C + 4 * g + i] = which == 0 ? accb1[i] : accb0[i];
+  }
+  }
+  __syncthreads();
+  // ---- per-workgroup partial rows: the 4 W-waves' slots summed in a fixed order
+  // (deterministic); bias = column 0 of the all-ones accumulators
+  const float* red = (const float*)smem;
+  for (int which = 0; which < 2; ++which) {
+    float* out = a.partial + which * a.lstride + (size_t)blockIdx.x * ROW;
+    const float* sl = red + which * 4 * (C * KTOT);
+    for (int e = tid; e < C * KTOT; e += kPT)
+      out[e] = ((sl[e] + sl[C * KTOT + e]) + sl[2 * C * KTOT + e]) + sl[3 * C * KTOT + e];
     if (tid < C) {
-      float s = 0.f;
-      for (int w = 0; w < kThreads / 64; ++w) s += red[w * C + tid];
-      a.partial[which * a.lstride + (size_t)blockIdx.x * ROW + C * KTOT + tid] = s;
+      const float* b = red + 8 * C * KTOT + which * 4 * C;
+      out[C * KTOT + tid] = ((b[tid] + b[C + tid]) + b[2 * C + tid]) + b[3 * C + tid];
     }
-    __syncthreads();
   }
 }
 
-constexpr size_t res_w88b_smem() { return (size_t)(kThreads / 64) * w88b::REG; }
+// 4 pairs' two tile sets + their flags; the final reduction (8 slots of C x KTOT floats +
+// biases) reuses the tiles
+constexpr size_t res_w88b_smem() { return (size_t)w88b::FLAGS + 4 * 6 * 4; }
+static_assert((8 * C * KTOT + 8 * C) * 4 <= w88b::FLAGS, "reduction slots must fit the tiles");
+static_assert(res_w88b_smem() <= 160 * 1024, "LDS");
 
 size_t res_smem(int imgs, int H, int W) {
   const size_t tb = ((size_t)imgs * lay16(H, W).imgb + 15) & ~(size_t)15;
@@ -617,7 +665,7 @@ size_t res_smem(int imgs, int H, int W) {
 bool res_bwd_w88(int H, int W) { return H == 8 && W == 8; }
 
 int res_grid(int N, int H, int W, int imgs) {
-  if (res_bwd_w88(H, W)) imgs = kThreads / 64;
+  if (res_bwd_w88(H, W)) imgs = 4;  // 4 wave pairs, an image each
   const size_t sm = res_bwd_w88(H, W) ? res_w88b_smem() : res_smem(imgs, H, W);
   static int cus = 0;
   if (!cus) {
@@ -631,7 +679,8 @@ int res_grid(int N, int H, int W, int imgs) {
                                        : (const void*)res_bwd16_kernel<0>;  // (every width)
   if (sm > 64 * 1024) (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, res_bwd_w88(H, W) ? w88b::kPT : kThreads,
+                                                   sm) != hipSuccess || per < 1)
     per = 1;
   // workgroups per CU the grid is sized for: at 2 (its occupancy) the kernel fills every
   // CU's LDS and VGPRs, so nothing else (the acting policy step) can start until it ends
@@ -1535,7 +1584,7 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
            : W == 12 ? res_bwd16_kernel<12> : W == 4 ? res_bwd16_kernel<4> : res_bwd16_kernel<0>;
   if (sm > 64 * 1024) (void)hipFuncSetAttribute((const void*)kfn,
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-  hipLaunchKernelGGL(kfn, dim3(nparts), dim3(kThreads), sm, stream, a);
+  hipLaunchKernelGGL(kfn, dim3(nparts), dim3(fast ? w88b::kPT : kThreads), sm, stream, a);
   int rc = (int)hipGetLastError();
   if (rc) return rc;
   rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, accumulate, stream);
