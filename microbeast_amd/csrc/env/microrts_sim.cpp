@@ -327,11 +327,20 @@ int MicroRTSSim::dir_toward(const Unit& u, int tx, int ty) const {
   return best;  // no path: keep the greedy step
 }
 
+// Bot tuning (compile-time; docs/DESIGN.md 9a, csrc/tests/calib_components.cpp):
 // coac build order: workers kept by the base, and how many of them harvest (the rest rush)
-static int kCoacWorkers = 8, kCoacHarvesters = 1;
-static int kLightWorkers = 3;  // light rush: workers kept, all but one harvest
-static bool kChaseBaseFirst = true;
-static int kChaseBaseSlack = 3;
+static constexpr int kCoacWorkers = 8, kCoacHarvesters = 1;
+static constexpr int kLightWorkers = 3;  // light rush: workers kept, all but one harvest
+static constexpr bool kChaseBaseFirst = true;
+static constexpr int kChaseBaseSlack = 3;
+// random-biased: a move toward the nearest enemy unit weighs kRBToward (microRTS's
+// RandomBiasedAI moves uniformly; its games against the uniform agent end by step ~500 in the
+// reference's logs, the stand-in's random walk needed ~860), and once the enemy base is down
+// its mobile units hunt what is left (kHuntNoBase); the same hunt for the scripted rushes'
+// harvesters (kHuntAll) measured longer games and is off
+static constexpr int kRBToward = 8;
+static constexpr bool kHuntNoBase = true;
+static constexpr bool kHuntAll = false;
 
 // Scripted opponents (stand-ins for coacAI, randomBiasedAI, lightRushAI,
 // workerRushAI — libs/utils.py:69-72). They act through exec() with the same
@@ -414,16 +423,69 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
 
   switch (bot_) {
     case BOT_PASSIVE: return;
-    case BOT_RANDOM:
     case BOT_RANDOM_BIASED: {
+      // stand-in calibration: once the enemy base is down, mobile units hunt what is left
+      if (kHuntNoBase && u.type >= WORKER && count_units(enemy, BASE) == 0) {
+        if (try_attack()) return;
+        if (chase()) return;
+      }
+      // microRTS RandomBiasedAI: one of the unit's concrete actions (each move direction, each
+      // harvest / return direction, each produce direction x type, each attack target, and
+      // none) at random, attack / harvest / return weighted 5x the others
+      uint32_t w[3];
+      unit_mask(u, player, w);
+      struct Cand { uint8_t t, p0, p1; };
+      Cand cand[4 + 4 + 4 + 4 * 7 + 49 + 1];
+      int wt[sizeof(cand) / sizeof(cand[0])], n = 0, tot = 0;
+      auto add = [&](uint8_t t, uint8_t p0, uint8_t p1, int weight) {
+        cand[n] = {t, p0, p1};
+        wt[n++] = weight;
+        tot += weight;
+      };
+      add(A_NOOP, 0, 0, 1);
+      // stand-in calibration (docs/DESIGN.md 9a): a move that closes in on the nearest enemy
+      // unit weighs kRBToward (1 = microRTS's uniform moves)
+      int ed = -1, ex = 0, ey = 0;
+      if (kRBToward > 1 && u.type >= WORKER) {
+        const int e = nearest(uid, 1 - player, -1, &ed);
+        if (e >= 0) { ex = units_[e].x; ey = units_[e].y; } else { ed = -1; }
+      }
+      for (int d = 0; d < 4; ++d) {
+        if (getbit(w, kNvecOff[1] + d)) {
+          const int nd = std::abs(ex - (u.x + kDX[d])) + std::abs(ey - (u.y + kDY[d]));
+          add(A_MOVE, (uint8_t)d, 0, ed >= 0 && nd < ed ? kRBToward : 1);
+        }
+        if (getbit(w, kNvecOff[2] + d)) add(A_HARVEST, (uint8_t)d, 0, 5);
+        if (getbit(w, kNvecOff[3] + d)) add(A_RETURN, (uint8_t)d, 0, 5);
+        if (getbit(w, kNvecOff[4] + d))
+          for (int k = 0; k < 7; ++k)
+            if (getbit(w, kNvecOff[5] + k)) add(A_PRODUCE, (uint8_t)d, (uint8_t)k, 1);
+      }
+      if (getbit(w, kNvecOff[0] + A_ATTACK))
+        for (int j = 0; j < 49; ++j)
+          if (getbit(w, kNvecOff[6] + j)) add(A_ATTACK, (uint8_t)j, 0, 5);
+      int r = (int)(rand_u32() % (uint32_t)tot), k = 0;
+      while (r >= wt[k]) r -= wt[k++];
+      const Cand c = cand[k];
+      if (c.t == A_NOOP) return;
+      a[0] = c.t;
+      switch (c.t) {
+        case A_MOVE: a[1] = c.p0; break;
+        case A_HARVEST: a[2] = c.p0; break;
+        case A_RETURN: a[3] = c.p0; break;
+        case A_PRODUCE: a[4] = c.p0; a[5] = c.p1; break;
+        case A_ATTACK: a[6] = c.p0; break;
+        default: break;
+      }
+      exec(uid, a, rwo);
+      return;
+    }
+    case BOT_RANDOM: {
       uint32_t w[3];
       unit_mask(u, player, w);
       // biased: prefer attack > harvest/return > produce > move (randomBiasedAI)
-      int order[6] = {A_ATTACK, A_RETURN, A_HARVEST, A_PRODUCE, A_MOVE, A_NOOP};
       int at = A_NOOP;
-      if (bot_ == BOT_RANDOM_BIASED && rand_unit() < 0.8f) {
-        for (int k = 0; k < 6; ++k) if (getbit(w, order[k])) { at = order[k]; break; }
-      } else {
+      {
         int c[6], n = 0;
         for (int k = 0; k < 6; ++k) if (getbit(w, k)) c[n++] = k;
         at = n ? c[rand_u32() % n] : A_NOOP;
@@ -455,7 +517,7 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
       if (u.type == BASE) { produce(WORKER); return; }
       if (u.type == WORKER) {
         if (try_attack()) return;
-        if (widx == 0 && harvest_cycle()) return;
+        if (widx == 0 && !(kHuntAll && count_units(enemy, BASE) == 0) && harvest_cycle()) return;
         chase();
       }
       return;
@@ -496,7 +558,9 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
             resources_[player] >= kSpec[BARRACKS].cost && widx == 1) {
           if (produce(BARRACKS)) return;
         }
-        if (widx < kCoacHarvesters && harvest_cycle()) return;
+        if (widx < kCoacHarvesters && !(kHuntAll && count_units(enemy, BASE) == 0) &&
+            harvest_cycle())
+          return;
         chase();
         return;
       }

@@ -2,7 +2,7 @@
 // plays the reference's initial policy (every component uniform over its legal choices, as
 // tools/calibrate_env.py) and sums the six raw reward components per episode.
 //   g++ -O2 -std=c++17 -I.. calib_components.cpp ../env/microrts_sim.cpp -o /tmp/calib
-//   /tmp/calib [size=8] [episodes per bot=300]
+//   /tmp/calib [size=8] [episodes per bot=300] [max_steps=2000]
 #include <cstdio>
 #include <cstdlib>
 #include <random>
@@ -21,7 +21,7 @@ int main(int argc, char** argv) {
   const char* names[4] = {"coac", "random_biased", "light_rush", "worker_rush"};
   std::mt19937_64 rng(7);
   for (int bot = 0; bot < 4; ++bot) {
-    MicroRTSSim sim(s, 2000, bot, 1234 + bot, rw);
+    MicroRTSSim sim(s, argc > 3 ? std::atoi(argv[3]) : 2000, bot, 1234 + bot, rw);
     sim.reset();
     const int S = s * s;
     std::vector<uint32_t> mask(S * 3);
