@@ -81,13 +81,14 @@ def parse(argv=None):
                         "one slot per update (global batch grows with N); strong: the global "
                         "problem of 1 GPU (the same groups x envs_per_group envs, one update "
                         "of envs_per_group x unroll frames) is split over the N ranks")
-    p.add_argument("--settle", type=int, default=300,
+    p.add_argument("--settle", type=int, default=500,
                    help="untimed training updates before the warm-up, so the timed window measures "
                         "a training run's steady state: from random init the policy learns to "
-                        "produce units and the agent's idle units (active cells) per env rise "
-                        "from ~1.2 to 7-11 within ~130 updates, which slows acting, the sparse "
-                        "head and the env side (profile 38: 16.2 -> ~12.3 M frames/s). 0 = time "
-                        "the early-game transient")
+                        "produce units, the agent's idle units (active cells) per env rise from "
+                        "~1.1 to ~9 by update ~120 (the acting step, the sparse head and the env "
+                        "side slow down: ~13 M frames/s) and settle at 4-5 from update ~450 on "
+                        "(15.0-15.6 M, the rate a 3,200-update CLI run averages: profile 38). "
+                        "0 = time the early-game transient")
     p.add_argument("--preroll", type=int, default=0,
                    help="before the first policy step every env plays r ~ U[0, preroll) steps of "
                         "the uniform random-init policy on the CPU (untimed), so the timed window "

@@ -402,7 +402,9 @@ def train(flags: Flags) -> dict:
         logger.close()
     wall = time.perf_counter() - t_start
     out = dict(last, updates=n_update, steps=step, wall_s=wall, checkpoint=ck_path,
-               mean_fps=step / max(wall, 1e-9), engine_restarts=engine_restarts)
+               mean_fps=step / max(wall, 1e-9), engine_restarts=engine_restarts,
+               # gpu runtime: the policy step ran the fused two-launch kernels (ops/act.py)
+               fused_act=bool(getattr(rt, "fused_act", False)))
     log(f"[microbeast_amd] done: {out}")
     D.destroy(info)
     return out

@@ -160,3 +160,35 @@ def test_engine_restart_frees_the_old_runtime_first(cuda):
         rt.release(slots)
     finally:
         rt.stop()
+
+
+def test_gpu_fused_16x16_training_improves(cuda, tmp_path):
+    """the headline acting path learns -- 16x16 through the fused two-launch
+    policy step (wave-owned trunk launch A with bitmap rows, head launch B, 2 policy lanes) and
+    the learner's head_score / head_bwd2 epilogues, against the passive bot: the second half's
+    episodes must beat the first 15 % on return per step and on win rate."""
+    from microbeast_amd.config import parse_flags
+    from microbeast_amd.train import train
+    out = train(parse_flags(["--exp_name", "l16", "--runtime", "gpu", "--env_size", "16",
+                             "--opponents", "passive", "--groups", "2", "--envs_per_group",
+                             "1024", "--policy_lanes", "2", "--unroll_length", "32",
+                             "--batch_size", "1", "--max_updates", "700",
+                             "--max_episode_steps", "300", "--savedir", str(tmp_path),
+                             "--quiet", "--log_every", "50", "--checkpoint_every", "0"],
+                            interactive=False))
+    assert out["fused_act"], "the 16x16 run did not take the fused acting step"
+    eps = _rows(tmp_path / "l16.csv")
+    n = len(eps)
+    assert n > 2000
+    first, last = eps[:int(0.15 * n)], eps[n // 2:]
+
+    def stats(rows):
+        ret = sum(float(r["Return"]) for r in rows)
+        steps = sum(int(r["steps"]) for r in rows)
+        win = sum(r["winner"] == "0" for r in rows) / len(rows)
+        return ret / len(rows), ret / steps, win
+
+    (r0, q0, w0), (r1, q1, w1) = stats(first), stats(last)
+    print(f"16x16 fused: return {r0:.2f} -> {r1:.2f}, per step {q0:.4f} -> {q1:.4f}, win rate "
+          f"{w0:.3f} -> {w1:.3f} over {n} episodes, {out['mean_fps']:.0f} frames/s")
+    assert r1 > r0 and q1 > 1.1 * q0 and w1 >= w0
