@@ -56,15 +56,6 @@ def parse(argv=None):
     p.add_argument("--threads", type=int, default=0, help="env worker threads per rank (0=auto)")
     p.add_argument("--seed", type=int, default=1)
     p.add_argument("--verbose", action="store_true", help="per-step progress on stderr")
-    p.add_argument("--learner_cu_reserve", type=int, default=0,
-                   help="run the learner on a CU-masked stream leaving every k-th CU to the "
-                        "policy stream (0 = off)")
-    p.add_argument("--cu_partition", type=int, default=0,
-                   help="k > 0: policy streams on CUs i %% k == 0, the learner on the rest "
-                        "(disjoint CU sets, persistent grids sized for each side)")
-    p.add_argument("--learner_cu_budget", type=int, default=0,
-                   help="size the learner's persistent grids for this many CUs (no CU mask) so "
-                        "policy kernels always find free wave slots (0 = all CUs)")
     p.add_argument("--selfplay_groups", type=int, default=0,
                    help="BASELINE config 5: env groups playing a self-play league (opponent "
                         "policy graph + PFSP over HBM snapshots) instead of scripted bots")
@@ -76,6 +67,10 @@ def parse(argv=None):
                    help="rehearsal only: allow more ranks than GPUs (ranks share a GPU over gloo)")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", help="fp32 | bf16 payload")
     p.add_argument("--bucket_mb", type=float, default=8.0)
+    p.add_argument("--comm_rehearsal", action="store_true",
+                   help="1 GPU only: every gradient bucket fires a stand-in collective kernel "
+                        "on a 4th high-priority stream from the same hooks (the stream set of an "
+                        "N > 1 rank; parallel/dist.py). Diagnostics, not the headline")
     p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
                    help="weak: every rank runs --groups x --envs_per_group envs and consumes "
                         "one slot per update (global batch grows with N); strong: the global "
@@ -97,9 +92,6 @@ def parse(argv=None):
     p.add_argument("--report_every", type=int, default=0,
                    help="diagnostics: every k timed steps print the window's frames/s and active "
                         "cells per env to stderr (host clock; 0 = off)")
-    p.add_argument("--policy_gate", type=int, default=-1,
-                   help="1: learner launches wait while a policy step's kernels run (engine "
-                        "policy gate); 0: off; -1: MBK_POLICY_GATE (default off)")
     return p.parse_args(argv)
 
 
@@ -165,19 +157,14 @@ def main(argv=None):
     torch.manual_seed(args.seed)
     model = make_model()
     learner = Learner(model, LearnerHParams(bucket_mb=args.bucket_mb,
-                                            allreduce_dtype=args.allreduce_dtype), dev, info)
+                                            allreduce_dtype=args.allreduce_dtype,
+                                            comm_rehearsal=args.comm_rehearsal), dev, info)
     envs_total = args.groups * args.envs_per_group
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    if args.cu_partition > 0:  # policy graphs are captured with grids for the policy CUs
-        from microbeast_amd import _native as N
-        N.kernels().mbk_set_cu_budget((ncu + args.cu_partition - 1) // args.cu_partition)
     rt = GpuActorRuntime(make_model, s, args.groups, args.envs_per_group, args.unroll,
                          args.batch_slots, dev, n_threads=threads, seed=args.seed + 1000 * info.rank,
                          env_index_base=info.rank * envs_total,
                          selfplay_groups=args.selfplay_groups, fp8_policy=args.fp8_policy,
-                         n_lanes=args.lanes, policy_cu_every=args.cu_partition,
-                         policy_gate=None if args.policy_gate < 0 else bool(args.policy_gate),
-                         preroll=args.preroll)
+                         n_lanes=args.lanes, preroll=args.preroll)
     league = None
     if args.selfplay_groups > 0:
         from microbeast_amd.runtime.league import League
@@ -185,27 +172,6 @@ def main(argv=None):
         league.current = league.add_snapshot(learner.flat.data)
     rt.start(learner.flat, opponent_version=league.current if league is not None else -1)
     frames_per_step = args.batch_slots * args.envs_per_group * args.unroll
-    if args.cu_partition > 0:
-        from microbeast_amd import _native as N
-        k = args.cu_partition
-        N.kernels().mbk_set_cu_budget(ncu - (ncu + k - 1) // k)
-        h = N.runtime().create_cu_masked_stream(dev.index, k)
-        learner_stream = torch.cuda.ExternalStream(h, device=dev)
-        learner_stream.wait_stream(torch.cuda.current_stream())
-        torch.cuda.set_stream(learner_stream)
-    if args.learner_cu_budget > 0:
-        from microbeast_amd import _native as N
-        N.kernels().mbk_set_cu_budget(args.learner_cu_budget)
-    if args.learner_cu_reserve > 0:
-        from microbeast_amd import _native as N
-        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-        # persistent learner grids sized for the CUs the masked stream may use
-        N.kernels().mbk_set_cu_budget(ncu - (ncu + args.learner_cu_reserve - 1)
-                                      // args.learner_cu_reserve)
-        h = N.runtime().create_cu_masked_stream(dev.index, args.learner_cu_reserve)
-        learner_stream = torch.cuda.ExternalStream(h, device=dev)
-        learner_stream.wait_stream(torch.cuda.current_stream())
-        torch.cuda.set_stream(learner_stream)
 
     nstep = [0]
     lags = []
@@ -248,8 +214,7 @@ def main(argv=None):
         losses = step()
         if args.report_every > 0 and (i + 1) % args.report_every == 0 and info.is_main:
             now, st = time.perf_counter(), rt.stats()
-            nst = max(1, (st["act_fused_steps"] + st["act_b_steps"])
-                      - (win[1]["act_fused_steps"] + win[1]["act_b_steps"]))
+            nst = max(1, st["act_steps"] - win[1]["act_steps"])
             print(f"[window] steps {i + 1 - args.report_every}-{i + 1}: "
                   f"{args.report_every * frames_per_step / (now - win[0]) / 1e6:.2f} M frames/s, "
                   f"active cells/env {(st['act_active_cells'] - win[1]['act_active_cells']) / (nst * rt.E):.3f}",
@@ -283,12 +248,10 @@ def main(argv=None):
             "frames_stepped_per_s": round((st1["frames"] - st0["frames"]) / el, 1),
             "gpu_phase_ms": round(1e3 * (st1["gpu_phase_s"] - st0["gpu_phase_s"]) / steps_done, 3),
             "env_phase_ms": round(1e3 * (st1["env_phase_s"] - st0["env_phase_s"]) / steps_done, 3)}
-    nf = st1.get("act_fused_steps", 0) - st0.get("act_fused_steps", 0)
-    nb = st1.get("act_b_steps", 0) - st0.get("act_b_steps", 0)
-    if nf + nb:  # the fused acting step's per-step head form (engine: active-cell threshold)
-        mine["act_head_in_A_frac"] = round(nf / (nf + nb), 3)
+    na = st1.get("act_steps", 0) - st0.get("act_steps", 0)
+    if na:  # fused acting steps: the agent's idle units per env and step (the game phase)
         mine["active_cells_per_env"] = round(
-            (st1["act_active_cells"] - st0["act_active_cells"]) / ((nf + nb) * rt.E), 3)
+            (st1["act_active_cells"] - st0["act_active_cells"]) / (na * rt.E), 3)
     ranks = D.gather_objects(mine, info)
     cpu_bound = [r["rank"] for r in ranks if r["env_worker_busy_frac"] >= CPU_BOUND_BUSY]
     if cpu_bound and info.is_main:
@@ -331,8 +294,8 @@ def main(argv=None):
                 "cpu_affinity_per_rank": len(cpus),
                 "policy_lanes": rt.n_lanes,
                 "allreduce": f"{args.allreduce_dtype} {args.bucket_mb:g}MB buckets",
-                "policy_gate": rt.policy_gate,
                 "settle_updates": args.settle,
+                "comm_rehearsal": args.comm_rehearsal,
                 "preroll": args.preroll,
             },
             "actor_stats": {

@@ -30,7 +30,7 @@ c_void_p, c_int, c_int64, c_float = ctypes.c_void_p, ctypes.c_int, ctypes.c_int6
 
 _SIGS = {
     "mbk_multi_copy": [c_void_p, c_int, c_void_p],
-    "mbk_stream_wait_zero": [c_void_p, c_void_p],
+    "mbk_comm_standin": [c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p],
     "mbk_row_gather": [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p],
     "mbk_memset": [c_void_p, c_int, c_int64, c_void_p],
     "mbk_masked_cell_fwd": [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int, c_int64,
@@ -78,19 +78,13 @@ _SIGS = {
                      c_void_p],
     "mbk_conv_fwd_fp8": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                          c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
-    "mbk_conv_dgrad_unpool": [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, c_int,
-                              c_int, c_int, c_void_p],
     "mbk_conv_pack_fp8": [c_void_p, c_int, c_void_p],
     "mbk_pool_bwd_idx": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_pool_bwd_idx_blk": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_pool_bwd_idx_out": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
-                       c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
-    "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                       c_int, c_int, c_int, c_void_p],
+    "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
     "mbk_conv_set_grid_cap": [c_int],
     "mbk_conv0_row_set": [c_int],
-    "mbk_set_cu_budget": [c_int],
-    "mbk_get_cu_budget": [],
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],
     "mbk_fc_wgrad": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                      c_void_p],
@@ -174,8 +168,6 @@ _SIGS = {
     "mbk_act_trunk": [c_void_p, c_void_p, c_void_p],
     "mbk_act_head": [c_void_p, c_void_p, c_void_p],
     "mbk_act_set_stamps": [c_void_p],
-    "mbk_act_set_mode": [c_int, c_int],  # (wave-owned A, fused head): -1 = environment
-    "mbk_act_fused": [],
     "mbk_rows_to_codes": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p],
     "mbk_codes_to_rows": [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p],
     "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
@@ -211,48 +203,16 @@ def kernels():
     return _kern
 
 
-# Policy gate (runtime/engine.h EngineConfig::policy_gate): while a GPU actor runtime has
-# registered its gate flag (set_policy_gate, after every policy graph is captured), each
-# kernel launcher called from Python first makes its stream (the launchers' last argument)
-# wait for the flag to read 0, i.e. for the in-flight policy step's kernels to finish. The
-# policy steps themselves run from captured graphs in the engine and never pass through here.
-# (Process-wide, not per thread: custom autograd backward nodes run on torch's device thread.)
-_gate_ptr = [None]
-
-
-def set_policy_gate(ptr: int | None) -> None:
-    _gate_ptr[0] = ptr or None
-
-
-def _gate_launch(lib, fn):
-    wait = lib.mbk_stream_wait_zero
-
-    def call(*args):
-        g = _gate_ptr[0]
-        if g is not None:
-            check(wait(g, args[-1]), "stream_wait_zero (policy gate)")
-        return fn(*args)
-
-    return call
-
-
 class _Checked:
     """Only signature-declared launchers are reachable (ctypes' default int
     conversion would silently truncate 64-bit device pointers)."""
 
     def __init__(self, lib):
         self._lib = lib
-        # every launcher takes its hipStream_t last (c_void_p); the query / setter helpers
-        # (int-returning *_parts, cu budget) do not launch and are not gated
-        self._gated = {n: _gate_launch(lib, getattr(lib, n)) for n, a in _SIGS.items()
-                       if a and a[-1] is c_void_p
-                       and n not in ("mbk_stream_wait_zero", "mbk_act_set_stamps")}
 
     def __getattr__(self, name):
         if name not in _SIGS:
             raise AttributeError(f"{name}: no ctypes signature declared in _native._SIGS")
-        if _gate_ptr[0] is not None and name in self._gated:
-            return self._gated[name]
         return getattr(self._lib, name)
 
 

@@ -30,7 +30,7 @@ PKG = HERE.parent
 LIBDIR = PKG / "_lib"
 BUILD = PKG.parent / "build" / "native"
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
-ARCH = os.environ.get("MBK_OFFLOAD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X (CDNA4) only
 
 KERNEL_FLAGS = [
     f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",

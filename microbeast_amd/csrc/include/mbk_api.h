@@ -94,11 +94,6 @@ typedef struct {
   float* reward_dst;
   uint8_t* done_dst;
   uint64_t step;           // Philox step of this policy step (the lane's step count)
-  int head_form;           // 0 = the process default (mbk_act_set_mode / MBK_ACT_FUSED),
-                           // 1 = head sampled inside launch A, 2 = head in launch B
-  uint32_t* code_list_dev; // optional HBM scratch [E][list_stride]: a small row-staging
-                           // launch copies each code_list row's n + 1 words here first and
-                           // launch A reads them from HBM instead of over PCIe
   uint32_t* abits;         // optional [E][S/32] active-cell bitmap of the row (bit c & 31 of
   uint32_t* abits2;        // word c >> 5: the cell's mask is non-zero), + the obs2 copy; the
                            // learner's head compaction then never reads the masks in full
@@ -114,13 +109,6 @@ int mbk_codes_to_rows(const void* act16, int E, int S, uint32_t* rows, int strid
 // the two launches separately (mbk_act_step = A then B)
 int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
 int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream);
-// launch-A form (tests / A/B): wave-owned kernel (1) or phase-split (0), head fused into A (1)
-// or left to launch B (0); -1 = the MBK_ACT_WAVE / MBK_ACT_FUSED environment default.
-// Returns wave * 2 + fused; mbk_act_fused() says whether mbk_act_head launches nothing.
-int mbk_act_set_mode(int wave, int fused);
-int mbk_act_fused(void);
-// the form this step runs (head_form resolved against the default; 0 = launch B samples)
-int mbk_act_step_fused(const MbkActStep* s);
 
 #ifdef __cplusplus
 }

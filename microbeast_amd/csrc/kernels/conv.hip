@@ -78,9 +78,6 @@ struct ConvFwdArgs {
   uint8_t* pool_idx;  // pooled argmax (0..8 in the 3x3 window) for the backward
   int N, H, W, imgs, relu_in, pool;
   const float* wscale;  // fp8 path: per-output-channel dequant scale of the e4m3 weights
-  // pool-fused input (dgrad of a stage conv): x = max_pool2d backward of dp through pidx
-  const bf16* dp;       // [N][Ho][Wo][CIN]
-  const uint8_t* pidx;  // [N][Ho][Wo][CIN]
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -131,40 +128,6 @@ __device__ __forceinline__ uint2 bf16x8_to_fp8(uint4 v) {
   return make_uint2(cvt_fp8x4(f[0], f[1], f[2], f[3]), cvt_fp8x4(f[4], f[5], f[6], f[7]));
 }
 
-// max_pool2d(3, 2, 1) backward folded into the consumer's staging: 8 channels
-// [8q, 8q+8) of the pre-pool gradient at pixel (y, x) of image im = the sum of the pooled
-// gradients of the (<= 4) windows whose stored argmax (0..8 in the window) is (y, x).
-// P / I: that round's pooled grads (bf16) and argmax bytes, dense [img][Ho][Wo][C] in LDS.
-__device__ __forceinline__ uint4 unpool8(const char* P, const char* I, int im, int y, int x,
-                                         int q, int H, int W, int C) {
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-  float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int oy = max(0, y / 2 - 1); oy <= min(Ho - 1, (y + 1) / 2); ++oy) {
-    const int ky = y - (2 * oy - 1);
-    if (ky < 0 || ky > 2) continue;
-    for (int ox = max(0, x / 2 - 1); ox <= min(Wo - 1, (x + 1) / 2); ++ox) {
-      const int kx = x - (2 * ox - 1);
-      if (kx < 0 || kx > 2) continue;
-      const uint32_t me = (uint32_t)(ky * 3 + kx);
-      const int o = ((im * Ho + oy) * Wo + ox) * C + q * 8;
-      const uint2 ids = *(const uint2*)(I + o);
-      const uint4 dv = *(const uint4*)(P + o * 2);
-      const uint32_t iw[2] = {ids.x, ids.y};
-      const uint32_t dw[4] = {dv.x, dv.y, dv.z, dv.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (((iw[j >> 2] >> (8 * (j & 3))) & 0xFFu) == me)
-          g[j] += __uint_as_float(((dw[j >> 1] >> (16 * (j & 1))) & 0xFFFFu) << 16);
-    }
-  }
-  uint32_t o[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j)
-    o[j] = (uint32_t)__bfloat16_as_ushort(f2bf(g[2 * j])) |
-           ((uint32_t)__bfloat16_as_ushort(f2bf(g[2 * j + 1])) << 16);
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
 template <int CIN, bool BITS, bool F8>
 __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
   // interior staging element e -> byte offset of its slot in the halo'd LDS tile
@@ -185,7 +148,7 @@ __device__ __forceinline__ int fwd_lds_off(int e, int H, int W) {
 // read traffic), weights are e4m3 with a power-of-two per-output-channel scale, and the
 // MFMA is v_mfma_f32_16x16x32_fp8_fp8 (same lane map as the bf16 form). Inference only.
 
-template <int CIN, int COUT, bool BITS, bool F8, bool UNPOOL = false>
+template <int CIN, int COUT, bool BITS, bool F8>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NCH = Geo<CIN>::NCH;
@@ -204,12 +167,6 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
   bf16* otile = (bf16*)(smem + tile_bytes);
   const int ngroups = (a.N + a.imgs - 1) / a.imgs;
   const int per_grp = a.imgs * HW * EPP;
-  // pool-fused input: pooled grads + argmax of the group, dense, after the tile
-  constexpr bool unpool = UNPOOL && !BITS && !F8;  // compile-time: keeps other variants lean
-  const int Hq = (H + 1) >> 1, Wq = (W + 1) >> 1;
-  const int pper = a.imgs * Hq * Wq * EPP;
-  char* sP = smem + tile_bytes;  // (no pool staging in this mode)
-  char* sI = sP + (((a.imgs * Hq * Wq * CIN * 2) + 15) & ~15);
 
   for (int e = tid; e < tile_bytes / 16; e += kThreads) ((uint4*)tile)[e] = make_uint4(0, 0, 0, 0);
   int loff[kPF];
@@ -242,22 +199,10 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
       wsc[nb][i] = F8 ? a.wscale[nb * 16 + 4 * g + i] : 1.f;
     }
 
-  // ---- register prefetch of one group's interior pixels (pooled grads when unpool)
+  // ---- register prefetch of one group's interior pixels
   uint4 pv[kPF];
   uint32_t pw[kPF];
-  uint2 pi[kPF];
   auto prefetch = [&](int grp) {
-    if constexpr (unpool) {
-      const size_t base = (size_t)grp * pper;
-      const int lim = min(pper, (a.N - grp * a.imgs) * Hq * Wq * EPP);
-#pragma unroll
-      for (int k = 0; k < kPF; ++k) {
-        const int e = tid + k * kThreads;
-        pv[k] = e < lim ? ((const uint4*)a.dp)[base + e] : make_uint4(0, 0, 0, 0);
-        pi[k] = e < lim ? ((const uint2*)a.pidx)[base + e] : make_uint2(0, 0);
-      }
-      return;
-    }
     const size_t base = (size_t)grp * per_grp;
     const int lim = min(per_grp, (a.N - grp * a.imgs) * HW * EPP);
 #pragma unroll
@@ -301,40 +246,18 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvFwdArgs a) {
     const int img0 = grp * a.imgs;
     const int nimg = min(a.imgs, a.N - img0);
     const int lim = nimg * HW * EPP;
-    if constexpr (unpool) {
-      const int plim = nimg * Hq * Wq * EPP;
 #pragma unroll
-      for (int k = 0; k < kPF; ++k) {
-        const int e = tid + k * kThreads;
-        if (e < plim) {
-          *(uint4*)(sP + e * 16) = pv[k];
-          *(uint2*)(sI + e * 8) = pi[k];
-        }
+    for (int k = 0; k < kPF; ++k) {
+      const int e = tid + k * kThreads;
+      if (e < lim) {
+        if (BITS) put_bits(loff[k], pw[k]);
+        else put(loff[k], pv[k]);
       }
-      for (int e = tid + kPF * kThreads; e < plim; e += kThreads) {
-        *(uint4*)(sP + e * 16) = ((const uint4*)a.dp)[(size_t)grp * pper + e];
-        *(uint2*)(sI + e * 8) = ((const uint2*)a.pidx)[(size_t)grp * pper + e];
-      }
-      __syncthreads();
-      for (int e = tid; e < lim; e += kThreads) {  // expand into the tile interior
-        const int q = e % EPP, p = e / EPP;
-        const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
-        put(fwd_lds_off<CIN, BITS, F8>(e, H, W), unpool8(sP, sI, im, y, x, q, H, W, CIN));
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPF; ++k) {
-        const int e = tid + k * kThreads;
-        if (e < lim) {
-          if (BITS) put_bits(loff[k], pw[k]);
-          else put(loff[k], pv[k]);
-        }
-      }
-      for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
-        const size_t src = (size_t)grp * per_grp + e;
-        if (BITS) put_bits(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint32_t*)a.x)[src]);
-        else put(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint4*)a.x)[src]);
-      }
+    }
+    for (int e = tid + kPF * kThreads; e < lim; e += kThreads) {  // groups beyond the prefetch
+      const size_t src = (size_t)grp * per_grp + e;
+      if (BITS) put_bits(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint32_t*)a.x)[src]);
+      else put(fwd_lds_off<CIN, BITS, F8>(e, H, W), ((const uint4*)a.x)[src]);
     }
     __syncthreads();
     if (grp + (int)gridDim.x < ngroups) prefetch(grp + gridDim.x);
@@ -773,9 +696,6 @@ struct ConvWgradArgs {
   const bf16* dy;
   float* partial;  // [gridDim.x][COUT*9*CIN + COUT]
   int N, H, W, imgs, relu_in;
-  // pool-fused mode (dy == nullptr): dY is the max-pool backward of dp through pidx
-  const bf16* dp;         // [N][Ho][Wo][COUT] pooled gradient
-  const uint8_t* pidx;    // [N][Ho][Wo][COUT] argmax in the 3x3 window
 };
 
 __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
@@ -820,7 +740,7 @@ inline int wg_band_w(int H, int W) {
 // Both GEMM operands come from NHWC LDS tiles through ds_read_b64_tr_b16 (band layout
 // above when WT > 0); the next round's X interior and dY are prefetched into registers
 // during the MFMAs.
-template <int CIN, int COUT, bool BITS, bool UNPOOL = false, int WT = 0>
+template <int CIN, int COUT, bool BITS, int WT = 0>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int XPB = CIN * 2;       // X tile pixel stride (bytes), NHWC bf16
@@ -846,20 +766,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   const int dbytes = band ? a.imgs * IMGD : ((a.imgs * HW * DPB) + 15) & ~15;
   char* dzero = dt + dbytes;
   float* red = (float*)smem;  // [COUT][KTOT] after the loop
-  // pool-fused: the round's pooled grads (bf16) and argmax bytes, dense [img][Ho][Wo][C]
-  constexpr bool unpool = UNPOOL;  // compile-time: keeps the plain variants lean
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-  char* sP = dzero + 64;
-  char* sI = sP + (((a.imgs * Ho * Wo * COUT * 2) + 15) & ~15);
   // bit-plane staging: byte -> 8 bf16 lookup table (4 KB) after the tiles
-  uint4* lut = (uint4*)(unpool ? sI + (((a.imgs * Ho * Wo * COUT) + 15) & ~15) : dzero + 64);
+  uint4* lut = (uint4*)(dzero + 64);
 
   for (int e = tid; e < (xbytes + 64) / 16; e += kThreads) ((uint4*)xt)[e] = make_uint4(0, 0, 0, 0);
   for (int e = tid; e < 4; e += kThreads) ((uint4*)dzero)[e] = make_uint4(0, 0, 0, 0);
   if constexpr (BITS)
     for (int e = tid; e < 256; e += kThreads) lut[e] = expand_bits8((uint32_t)e);
   const int xper = a.imgs * HW * XEPP, dper = a.imgs * HW * DCH;
-  const int pper = a.imgs * Ho * Wo * DCH;  // pooled 8-channel chunks per round
   int xoff[kPFW];
 #pragma unroll
   for (int k = 0; k < kPFW; ++k) {
@@ -890,27 +804,21 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   // twice the bytes are in flight (the tile loads are HBM-latency bound at one round ahead)
   struct PF {
     uint4 px[kPFW], pd[kPFW];
-    uint2 pi[kPFW];
     uint32_t pb[kPFW];
   };
   PF pf0, pf1;
   auto prefetch = [&](int rd, PF& f) {
     uint4 (&px)[kPFW] = f.px; uint4 (&pd)[kPFW] = f.pd;
-    uint2 (&pi)[kPFW] = f.pi; uint32_t (&pb)[kPFW] = f.pb;
+    uint32_t (&pb)[kPFW] = f.pb;
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
-    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH, pl = nimg * Ho * Wo * DCH;
-    const size_t xb = (size_t)rd * xper, db = (size_t)rd * dper, pbase = (size_t)rd * pper;
+    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH;
+    const size_t xb = (size_t)rd * xper, db = (size_t)rd * dper;
 #pragma unroll
     for (int k = 0; k < kPFW; ++k) {
       const int e = tid + k * kThreads;
       if (BITS) pb[k] = e < xl ? ((const uint32_t*)a.x)[xb + e] : 0u;
       else px[k] = e < xl ? ((const uint4*)a.x)[xb + e] : make_uint4(0, 0, 0, 0);
-      if constexpr (unpool) {
-        pd[k] = e < pl ? ((const uint4*)a.dp)[pbase + e] : make_uint4(0, 0, 0, 0);
-        pi[k] = e < pl ? ((const uint2*)a.pidx)[pbase + e] : make_uint2(0, 0);
-      } else {
-        pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
-      }
+      pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
     }
   };
   auto put_x = [&](int off, uint4 v) {
@@ -951,9 +859,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   __syncthreads();  // zero halo / zero rows visible
   auto round = [&](int rd, PF& f) {
     uint4 (&px)[kPFW] = f.px; uint4 (&pd)[kPFW] = f.pd;
-    uint2 (&pi)[kPFW] = f.pi; uint32_t (&pb)[kPFW] = f.pb;
+    uint32_t (&pb)[kPFW] = f.pb;
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
-    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH, pl = nimg * Ho * Wo * DCH;
+    const int xl = nimg * HW * XEPP, dl = nimg * HW * DCH;
 #pragma unroll
     for (int k = 0; k < kPFW; ++k) {
       const int e = tid + k * kThreads;
@@ -961,35 +869,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         if (BITS) put_bits(xoff[k], pb[k]);
         else put_x(xoff[k], px[k]);
       }
-      if constexpr (unpool) {
-        if (e < pl) {
-          *(uint4*)(sP + e * 16) = pd[k];
-          *(uint2*)(sI + e * 8) = pi[k];
-        }
-      } else if (e < dl) {
-        put_d(e, pd[k]);
-      }
+      if (e < dl) put_d(e, pd[k]);
     }
     for (int e = tid + kPFW * kThreads; e < xl; e += kThreads) {
       if (BITS) put_bits(xoff_of(e), ((const uint32_t*)a.x)[(size_t)rd * xper + e]);
       else put_x(xoff_of(e), ((const uint4*)a.x)[(size_t)rd * xper + e]);
     }
-    if constexpr (unpool) {
-      for (int e = tid + kPFW * kThreads; e < pl; e += kThreads) {
-        *(uint4*)(sP + e * 16) = ((const uint4*)a.dp)[(size_t)rd * pper + e];
-        *(uint2*)(sI + e * 8) = ((const uint2*)a.pidx)[(size_t)rd * pper + e];
-      }
-      __syncthreads();
-      // expand: dY chunk e = (pixel, 8-channel group) from the pooled grads
-      for (int e = tid; e < dl; e += kThreads) {
-        const int q = e % DCH, p = e / DCH;
-        const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
-        put_d(e, unpool8(sP, sI, im, y, x, q, H, W, COUT));
-      }
-    } else {
-      for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
-        put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
-    }
+    for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
+      put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
     __syncthreads();
     if (rd + 2 * gstep < nrounds) prefetch(rd + 2 * gstep, f);
 
@@ -1270,63 +1157,6 @@ __global__ __launch_bounds__(256) void pool_bwd_idx_kernel(const uint8_t* __rest
   }
 }
 
-// Same result in output order: thread e writes 16-byte chunk e of dc, so every store
-// instruction covers 1 KB of contiguous memory (the 2x2-block form above writes 16 bytes
-// at a 2-pixel stride per instruction, half of every 64-byte segment). Each thread gathers
-// its (<= 4) windows' argmax bytes and gradients, which neighbouring lanes share through
-// L1/L2; the HBM traffic stays one read of dp/pidx plus one write of dc. Windows are summed
-// in the 2x2-block kernel's (dj, dk) order from 0.f, so both give identical bits.
-template <int C>
-__global__ __launch_bounds__(256) void pool_bwd_out_kernel(const uint8_t* __restrict__ pidx,
-                                                           const bf16* __restrict__ dp, int N,
-                                                           int H, int W,
-                                                           bf16* __restrict__ dc) {
-  constexpr int C8 = C / 8;
-  const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
-  const uint32_t tot = (uint32_t)N * H * W * C8;
-  for (uint32_t e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
-    const int c8 = e % C8;
-    const uint32_t p = e / C8;
-    const int x = p % W;
-    const uint32_t q = p / W;
-    const int y = q % H;
-    const uint32_t n = q / H;
-    // pixel row y sits in window j = y >> 1 at ky = (y & 1) + 1, and for odd y also in
-    // window j + 1 at ky = 0 (same for columns)
-    const int j = y >> 1, k = x >> 1;
-    const bool y2 = (y & 1) && j + 1 < Ho, x2 = (x & 1) && k + 1 < Wo;
-    float g[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int dj = 0; dj < 2; ++dj)
-#pragma unroll
-      for (int dk = 0; dk < 2; ++dk) {
-        if ((dj && !y2) || (dk && !x2)) continue;
-        const uint32_t ky = dj ? 0u : (uint32_t)(y & 1) + 1u;
-        const uint32_t kx = dk ? 0u : (uint32_t)(x & 1) + 1u;
-        const uint32_t me = ky * 3u + kx;
-        const uint32_t o = ((n * Ho + j + dj) * Wo + k + dk) * C + c8 * 8;
-        const uint2 iv = *(const uint2*)(pidx + o);
-        const uint4 d = *(const uint4*)(dp + o);
-        const uint32_t ids[2] = {iv.x, iv.y};
-        const uint32_t dv[4] = {d.x, d.y, d.z, d.w};
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const uint32_t id = (ids[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-          const uint32_t hb = (dv[t >> 1] >> (16 * (t & 1))) & 0xFFFFu;
-          if (id == me) g[t] += __uint_as_float(hb << 16);
-        }
-      }
-    uint32_t o[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint32_t lo = __bfloat16_as_ushort(f2bf(g[2 * t]));
-      const uint32_t hi = __bfloat16_as_ushort(f2bf(g[2 * t + 1]));
-      o[t] = lo | (hi << 16);
-    }
-    ((uint4*)dc)[e] = make_uint4(o[0], o[1], o[2], o[3]);
-  }
-}
-
 // ------------------------------------------------------------------ weight packing
 struct PackJob {
   const float* w;   // [cout][cin_real][3][3]
@@ -1423,24 +1253,16 @@ __global__ __launch_bounds__(256) void conv_pack_fp8_kernel(PackJobs8 jobs) {
 }
 
 inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, bool pool,
-                       bool fp8 = false, bool unpool = false) {
+                       bool fp8 = false) {
   (void)bits;  // bit planes are staged expanded (cin = 32)
   const int pixb = fp8 ? cin + 8 : cin * 2 + 16;
   size_t t = (((size_t)imgs * (H + 2) * (W + 2) * pixb) + 15) & ~(size_t)15;
   if (pool) t += (size_t)imgs * H * W * (cout + 4) * 2;
-  if (unpool) {
-    const size_t pp = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * cin;
-    t += ((pp * 2 + 15) & ~(size_t)15) + ((pp + 15) & ~(size_t)15);
-  }
   return t;
 }
 
-inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool = false) {
-  size_t t = wg_tile_bytes(cin, cout, imgs, H, W, unpool ? 0 : wg_band_w(H, W));
-  if (unpool) {
-    const size_t pp = (size_t)imgs * ((H + 1) / 2) * ((W + 1) / 2) * cout;
-    t += ((pp * 2 + 15) & ~(size_t)15) + ((pp + 15) & ~(size_t)15);
-  }
+inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W) {
+  size_t t = wg_tile_bytes(cin, cout, imgs, H, W, wg_band_w(H, W));
   t += 4096;  // bit-plane lookup table (allocated for every variant: keeps the sizing simple)
   size_t red = (size_t)cout * 9 * cin * 4;
   return t > red ? t : red;
@@ -1448,8 +1270,6 @@ inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool 
 
 int g_grid_cap = 0;    // tests force multi-group workgroups with a small cap
 int g_conv0_row = 1;   // stage-0 conv of 16-wide maps on conv0_row_kernel (0: generic kernel)
-int g_cu_budget = 0;   // CUs a persistent grid is sized for (0 = all); set when the learner
-                       // runs on a CU-masked stream so its grid fits the masked CUs exactly
 
 // resident workgroups the whole device holds for (kernel, dynamic LDS)
 int resident_blocks(const void* kfn, size_t sm) {
@@ -1464,22 +1284,16 @@ int resident_blocks(const void* kfn, size_t sm) {
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
     per = 1;
-  const int ncu = g_cu_budget > 0 ? std::min(g_cu_budget, cus) : cus;
-  int r = ncu * per;
+  int r = cus * per;
   if (g_grid_cap > 0 && r > g_grid_cap) r = g_grid_cap;
   return r;
 }
 
-// Forward / dgrad grids: resident_blocks x g_fwd_mult workgroups. mult = 1 is persistent
-// (each workgroup walks many image groups); larger values make workgroups retire while the
-// kernel runs, so a concurrently queued high-priority kernel (the acting policy step) gets
-// CU slots without waiting for the whole learner kernel. MBK_FWD_GRID_MULT overrides.
+// Forward / dgrad grids: persistent, one resident set of workgroups that walks the image
+// groups (2x / 4x grids that retire workgroups early for the acting step measured level or
+// slower on the bench: DESIGN.md §9 rejected variants)
 int fwd_grid(int ngroups, const void* kfn, size_t sm) {
-  static const int mult = [] {
-    const char* e = getenv("MBK_FWD_GRID_MULT");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
-  const long r = (long)resident_blocks(kfn, sm) * mult;
+  const long r = (long)resident_blocks(kfn, sm);
   return (int)std::max(1L, std::min((long)ngroups, r));
 }
 
@@ -1498,17 +1312,13 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
                            const float* wscale, const float* bias, const void* add,
                            const void* mask_src, void* y, void* y_full, void* pool_idx, int N,
                            int H, int W, int imgs, int relu_in, int pool, bool fp8,
-                           hipStream_t stream, const void* dp = nullptr,
-                           const void* pidx = nullptr) {
+                           hipStream_t stream) {
   if (N <= 0) return 0;
   if (fp8 && !wscale) return (int)hipErrorInvalidValue;
   if (!index_math_ok(imgs, H, W)) return (int)hipErrorInvalidValue;
-  const bool unpool = dp != nullptr;
-  if (unpool && (in_bits || fp8 || pool || !pidx)) return (int)hipErrorInvalidValue;
   ConvFwdArgs a{x, (const bf16*)w, bias, (const bf16*)add, (const bf16*)mask_src, (bf16*)y,
-                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool, wscale,
-                (const bf16*)dp, (const uint8_t*)pidx};
-  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0, fp8, unpool);
+                (bf16*)y_full, (uint8_t*)pool_idx, N, H, W, imgs, relu_in, pool, wscale};
+  const size_t sm = fwd_smem(cin, in_bits != 0, imgs, H, W, cout, pool != 0, fp8);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const int ngroups = (N + imgs - 1) / imgs;
 #define LAUNCH(CI, CO, B)                                                                   \
@@ -1519,17 +1329,6 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     const int grid = fwd_grid(ngroups, (const void*)kfn, sm);                               \
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);                     \
   } while (0)
-  if (unpool) {  // dgrad of a pooled stage conv (cin = that conv's cout)
-    auto kfn = cin == 32 && cout == 16   ? conv_fwd_kernel<32, 16, false, false, true>
-               : cin == 32 && cout == 32 ? conv_fwd_kernel<32, 32, false, false, true>
-                                         : nullptr;
-    if (!kfn) return (int)hipErrorInvalidValue;
-    if (sm > 64 * 1024)
-      hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    const int grid = fwd_grid(ngroups, (const void*)kfn, sm);
-    hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
-    return (int)hipGetLastError();
-  }
   // 17..32 pixels wide (config 4's 24 x 24), 16 channels: the WIDE row kernel
   if (in_bits && cout == 16 && W > 16 && W <= 32 && !fp8 && g_conv0_row && !add && !mask_src &&
       !relu_in && kLutBytes + (size_t)kRowImgs * H * W * 16 * 2 <= 160 * 1024) {
@@ -1543,11 +1342,7 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
       !mask_src && !relu_in) {
     const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * 16 * (cout + 4) * 2 : 0);
     if (sm0 > 160 * 1024) return (int)hipErrorInvalidValue;
-    static const bool batch_rows = [] {  // A/B knob: MBK_CONV0_BATCH_ROWS=0 -> pairwise loads
-      const char* e = getenv("MBK_CONV0_BATCH_ROWS");
-      return !(e && e[0] == '0');
-    }();
-    const bool hb = H == 16 && batch_rows;
+    const bool hb = H == 16;  // 16 x 16 maps: batched row loads
     const auto kfn = cout == 16 ? (hb ? conv0_row_kernel<16, 16> : conv0_row_kernel<0, 16>)
                                 : (hb ? conv0_row_kernel<16, 32> : conv0_row_kernel<0, 32>);
     const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)kfn, sm0);
@@ -1575,15 +1370,6 @@ extern "C" int mbk_conv_fwd(const void* x, int in_bits, int cin, int cout, const
                          pool_idx, N, H, W, imgs, relu_in, pool, false, stream);
 }
 
-// Data gradient of a pooled stage conv with the max-pool backward folded in: the input
-// (the pre-pool gradient, cin channels at H x W) is rebuilt per tile from dp / pidx.
-extern "C" int mbk_conv_dgrad_unpool(const void* dp, const void* pidx, int cin, int cout,
-                                     const void* w, void* y, int N, int H, int W, int imgs,
-                                     hipStream_t stream) {
-  return conv_fwd_launch(nullptr, 0, cin, cout, w, nullptr, nullptr, nullptr, nullptr, y,
-                         nullptr, nullptr, N, H, W, imgs, 0, 0, false, stream, dp, pidx);
-}
-
 // Inference conv on fp8 MFMA: w = e4m3 packed weights (mbk_conv_pack_fp8), wscale = their
 // per-output-channel dequant scale; activations in / out stay bf16 NHWC.
 extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, const void* w,
@@ -1605,50 +1391,43 @@ extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, c
   else if (cin == 32 && cout == 32) LAUNCH(32, 32, false);                                  \
   else return -(int)hipErrorInvalidValue;
 
-// the wgrad instantiation of (CI, CO, B) for this map width: band layout (WT = 8 / 16) or
-// the plain one (pool-fused mode always plain)
+// the wgrad instantiation of (CI, CO, B) for this map width: band layout (WT = 8 / 16 / 24)
+// or the plain one
 template <int CI, int CO, bool B>
-const void* wgrad_kfn(int H, int W, bool unpool) {
-  if (unpool) return (const void*)conv_wgrad_kernel<CI, CO, B, true>;
+const void* wgrad_kfn(int H, int W) {
   switch (wg_band_w(H, W)) {
-    case 24: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 24>;
-    case 16: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 16>;
-    case 8: return (const void*)conv_wgrad_kernel<CI, CO, B, false, 8>;
+    case 24: return (const void*)conv_wgrad_kernel<CI, CO, B, 24>;
+    case 16: return (const void*)conv_wgrad_kernel<CI, CO, B, 16>;
+    case 8: return (const void*)conv_wgrad_kernel<CI, CO, B, 8>;
     default: return (const void*)conv_wgrad_kernel<CI, CO, B>;
   }
 }
 
 // number of partial rows mbk_conv_wgrad will write for this shape (<= nrounds)
 extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
-                                    int imgs, int unpool) {
-  const size_t sm = wgrad_smem(cin, cout, imgs, H, W, unpool != 0);
+                                    int imgs) {
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
   if (sm > 160 * 1024 || !index_math_ok(imgs, H, W)) return -(int)hipErrorInvalidValue;
   const int nrounds = (N + imgs - 1) / imgs;
   int res = 1;
-#define Q(CI, CO, B) res = resident_blocks(wgrad_kfn<CI, CO, B>(H, W, unpool != 0), sm)
+#define Q(CI, CO, B) res = resident_blocks(wgrad_kfn<CI, CO, B>(H, W), sm)
   WGRAD_DISPATCH(Q)
 #undef Q
-  static const int mult = [] {  // see fwd_grid: more, shorter-lived workgroups (+ partials)
-    const char* e = getenv("MBK_WGRAD_GRID_MULT");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
-  return (int)std::max(1L, std::min((long)nrounds, (long)res * mult));
+  return (int)std::max(1L, std::min((long)nrounds, (long)res));
 }
 
-// dy == nullptr: pool-fused mode, dY = max_pool2d backward of dp through pidx
 extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, const void* dy,
-                              const void* dp, const void* pidx, float* partial, int nparts, int N,
-                              int H, int W, int imgs, int relu_in, hipStream_t stream) {
-  if (!dy && (!dp || !pidx)) return (int)hipErrorInvalidValue;
-  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in,
-                  dy ? nullptr : (const bf16*)dp, dy ? nullptr : (const uint8_t*)pidx};
-  const size_t sm = wgrad_smem(cin, cout, imgs, H, W, dy == nullptr);
+                              float* partial, int nparts, int N, int H, int W, int imgs,
+                              int relu_in, hipStream_t stream) {
+  if (!dy) return (int)hipErrorInvalidValue;
+  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in};
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
   if (sm > 160 * 1024 || nparts < 1 || !index_math_ok(imgs, H, W))
     return (int)hipErrorInvalidValue;
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
-    const void* kfn = wgrad_kfn<CI, CO, B>(H, W, dy == nullptr);                            \
+    const void* kfn = wgrad_kfn<CI, CO, B>(H, W);                            \
     if (sm > 64 * 1024)                                                                     \
       hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
     void* args[] = {&a};                                                                    \
@@ -1669,8 +1448,6 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
 
 extern "C" void mbk_conv_set_grid_cap(int cap) { g_grid_cap = cap; }
 extern "C" void mbk_conv0_row_set(int on) { g_conv0_row = on; }
-extern "C" void mbk_set_cu_budget(int n) { g_cu_budget = n; }
-extern "C" int mbk_get_cu_budget() { return g_cu_budget; }
 
 // partial holds nparts rows plus ceil(nparts / kReducePps) scratch rows after them
 extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,
@@ -1703,8 +1480,10 @@ extern "C" int mbk_pool_bwd(const void* cfull, const void* dp, int N, int H, int
   return (int)hipGetLastError();
 }
 
-static int pool_bwd_idx_launch(const void* pidx, const void* dp, int N, int H, int W, int C,
-                               void* dc, hipStream_t stream, bool out_order) {
+// dc = max_pool2d(3, 2, 1) backward of dp through the stored argmax bytes (2x2-block form:
+// the output-order form measured level, DESIGN.md §9 rejected variants)
+extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, int W, int C,
+                                void* dc, hipStream_t stream) {
   if (C != 16 && C != 32) return (int)hipErrorInvalidValue;
   const int Ho = (H + 1) >> 1, Wo = (W + 1) >> 1;
   const size_t per_img_in = (size_t)H * W * C, per_img_out = (size_t)Ho * Wo * C;
@@ -1712,20 +1491,13 @@ static int pool_bwd_idx_launch(const void* pidx, const void* dp, int N, int H, i
   const int chunk = (int)std::max<size_t>(1, ((size_t)1 << 31) / per_img_in - 1);
   for (int n0 = 0; n0 < N; n0 += chunk) {
     const int n = std::min(chunk, N - n0);
-    const size_t tot = (size_t)n * (out_order ? (size_t)H * W : (size_t)Ho * Wo) * (C / 8);
+    const size_t tot = (size_t)n * Ho * Wo * (C / 8);
     size_t blocks = (tot + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     const uint8_t* pi = (const uint8_t*)pidx + n0 * per_img_out;
     const bf16* d = (const bf16*)dp + n0 * per_img_out;
     bf16* o = (bf16*)dc + n0 * per_img_in;
-    if (out_order) {
-      if (C == 16)
-        hipLaunchKernelGGL(pool_bwd_out_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, stream,
-                           pi, d, n, H, W, o);
-      else
-        hipLaunchKernelGGL(pool_bwd_out_kernel<32>, dim3((unsigned)blocks), dim3(256), 0, stream,
-                           pi, d, n, H, W, o);
-    } else if (C == 16)
+    if (C == 16)
       hipLaunchKernelGGL(pool_bwd_idx_kernel<16>, dim3((unsigned)blocks), dim3(256), 0, stream, pi,
                          d, n, H, W, o);
     else
@@ -1733,26 +1505,6 @@ static int pool_bwd_idx_launch(const void* pidx, const void* dp, int N, int H, i
                          d, n, H, W, o);
   }
   return (int)hipGetLastError();
-}
-
-// MBK_POOL_BWD_OUT=1 selects the output-order kernel, 0 the 2x2-block form
-extern "C" int mbk_pool_bwd_idx(const void* pidx, const void* dp, int N, int H, int W, int C,
-                                void* dc, hipStream_t stream) {
-  static const bool out = [] {
-    const char* s = getenv("MBK_POOL_BWD_OUT");
-    return s && s[0] == '1';
-  }();
-  return pool_bwd_idx_launch(pidx, dp, N, H, W, C, dc, stream, out);
-}
-
-extern "C" int mbk_pool_bwd_idx_out(const void* pidx, const void* dp, int N, int H, int W, int C,
-                                    void* dc, hipStream_t stream) {
-  return pool_bwd_idx_launch(pidx, dp, N, H, W, C, dc, stream, true);
-}
-
-extern "C" int mbk_pool_bwd_idx_blk(const void* pidx, const void* dp, int N, int H, int W, int C,
-                                    void* dc, hipStream_t stream) {
-  return pool_bwd_idx_launch(pidx, dp, N, H, W, C, dc, stream, false);
 }
 
 extern "C" int mbk_conv_pack_fp8(const MbkPackJob8* jobs, int n, hipStream_t stream) {

@@ -167,10 +167,34 @@ extern "C" int mbk_multi_copy(const MbkCopySeg* segs, int n, hipStream_t stream)
   return (int)hipGetLastError();
 }
 
-// Learner-side half of the engine's policy gate (runtime/engine.h EngineConfig::policy_gate):
-// `stream` waits until the flag reads 0 (no policy step's kernels in flight) before its next
-// launch. A stream wait-value packet, polled by the command processor.
-extern "C" int mbk_stream_wait_zero(const void* flag, hipStream_t stream) {
-  return (int)hipStreamWaitValue32(stream, const_cast<void*>(flag), 0u, hipStreamWaitValueEq,
-                                   0xFFFFFFFFu);
+// Stand-in for one bucket's ring all-reduce at world size 1 (parallel/dist.py rehearsal):
+// `passes` sweeps of scratch += g over the bucket (a ring all-reduce over N ranks moves the
+// bucket 2 (N - 1) times through each GPU, half of them with a reduce add), on a small grid
+// like RCCL's channels (one workgroup per channel), so the learner / policy kernels see the
+// CU, HBM and queue footprint of the collective a multi-GPU run adds. g is only read.
+__global__ __launch_bounds__(256) void comm_standin_kernel(const float* __restrict__ g,
+                                                           float* __restrict__ s, int64_t n,
+                                                           int passes) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int p = 0; p < passes; ++p) {
+    for (int64_t i = t0; i < n4; i += stride) {
+      const float4 a = ((const float4*)g)[i];
+      float4 b = ((float4*)s)[i];
+      b.x += a.x; b.y += a.y; b.z += a.z; b.w += a.w;
+      ((float4*)s)[i] = b;
+    }
+    for (int64_t i = (n4 << 2) + t0; i < n; i += stride) s[i] += g[i];
+  }
+}
+
+extern "C" int mbk_comm_standin(const float* g, float* scratch, int64_t n, int passes,
+                                int channels, hipStream_t stream) {
+  if (n <= 0 || passes <= 0) return 0;
+  if (((uintptr_t)g & 15) || ((uintptr_t)scratch & 15) || channels < 1)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(comm_standin_kernel, dim3(channels), dim3(256), 0, stream, g, scratch, n,
+                     passes);
+  return (int)hipGetLastError();
 }

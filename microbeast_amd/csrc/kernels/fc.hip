@@ -511,11 +511,7 @@ extern "C" int mbk_fc_fwd(const void* x, int relu_in, const void* w5, const floa
   if (F <= 0) return 0;
   if (I % 32) return (int)hipErrorInvalidValue;
   const int blocks = (F + 15) / 16;
-  static const bool rb_on = [] {
-    const char* e = getenv("MBK_FC_RB");
-    return !(e && e[0] == '0');
-  }();
-  if (rb_on && (O == 256 || O == 128) && I <= 128) {
+  if ((O == 256 || O == 128) && I <= 128) {
     static int cus = 0;
     if (!cus) {
       int dev = 0;
@@ -569,12 +565,8 @@ int fc_wgrad_impl(const void* g, const void* x, int N, int O, int I, const XShif
   const int rpp = ((stages + nparts - 1) / nparts) * R;
   const int chunks = ((O + OC - 1) / OC) * ((xs.ntap * I + IC - 1) / IC);
   // dispatch order: chunk-fastest for the shifted (conv) form, whose chunks re-read the same
-  // rows; MBK_WGRAD_ORDER=chunk|part overrides (A/B knob)
-  static const int order = [] {
-    const char* e = getenv("MBK_WGRAD_ORDER");
-    return e ? (e[0] == 'c' ? 1 : 0) : -1;
-  }();
-  const int cf = order >= 0 ? order : (xs.ntap > 1 ? 1 : 0);
+  // rows
+  const int cf = xs.ntap > 1 ? 1 : 0;
   const dim3 grid = cf ? dim3(chunks, nparts) : dim3(nparts, chunks);
   if (O % 8 == 0)
     hipLaunchKernelGGL(fc_wgrad_kernel<true>, grid, dim3(kThreads), 0, stream, (const bf16*)g,

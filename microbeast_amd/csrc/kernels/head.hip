@@ -1638,11 +1638,8 @@ extern "C" int mbk_head_pack(const float* W, const float* b, int S, void* Wp, fl
 }
 
 // ------------------------------------------------------------------ fused acting step, launch B
-extern "C" int mbk_act_step_fused(const MbkActStep* s);  // trunk.hip: A sampled the head
-
 extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
   if (!m || !s || m->E <= 0) return (int)hipErrorInvalidValue;
-  if (mbk_act_step_fused(s)) return 0;
   const int S = m->H * m->W;
   if (S < 1 || S > kMaxUnitCells - 1 || (S & 3)) return (int)hipErrorInvalidValue;
   if (!m->feat || !m->Wp || !m->bp || !m->rng || !m->bucket || !m->bucket_cnt || !m->cellx ||
@@ -1675,13 +1672,8 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  // MBK_HEAD_ACT_GRID=<workgroups per 8 CUs> (default 16 = 2 per CU): fewer, longer-lived
-  // workgroups need fewer free CU slots while the learner holds the GPU
-  static const int per8 = [] {
-    const char* e = getenv("MBK_HEAD_ACT_GRID");
-    return e && std::atoi(e) > 0 ? std::atoi(e) : 16;
-  }();
-  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * per8 / 8)), dim3(256), 0, stream, a);
+  // two workgroups per CU (fewer, longer-lived ones measured level under the learner)
+  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * 2)), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 

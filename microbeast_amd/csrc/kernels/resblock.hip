@@ -24,7 +24,6 @@
 
 #include <algorithm>
 
-extern "C" int mbk_get_cu_budget();  // conv.hip: CUs the learner's persistent grids target
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
@@ -674,7 +673,7 @@ int res_grid(int N, int H, int W, int imgs) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
+  const int ncu = cus;
   const void* kfn = res_bwd_w88(H, W) ? (const void*)res_bwd16_w88_kernel
                                        : (const void*)res_bwd16_kernel<0>;  // (every width)
   if (sm > 64 * 1024) (void)hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
@@ -682,19 +681,8 @@ int res_grid(int N, int H, int W, int imgs) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, res_bwd_w88(H, W) ? w88b::kPT : kThreads,
                                                    sm) != hipSuccess || per < 1)
     per = 1;
-  // workgroups per CU the grid is sized for: at 2 (its occupancy) the kernel fills every
-  // CU's LDS and VGPRs, so nothing else (the acting policy step) can start until it ends
-  static const int cap = [] {
-    const char* e = getenv("MBK_RES_BWD_PER_CU");
-    return e ? std::max(1, atoi(e)) : 0;
-  }();
-  if (cap > 0) per = std::min(per, cap);
   const int nrounds = (N + imgs - 1) / imgs;
-  static const int mult = [] {  // see conv.hip fwd_grid / mbk_conv_wgrad_parts
-    const char* e = getenv("MBK_WGRAD_GRID_MULT");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
-  return (int)std::max(1L, std::min((long)nrounds, (long)ncu * per * mult));
+  return (int)std::max(1L, std::min((long)nrounds, (long)ncu * per));
 }
 
 }  // namespace
@@ -1544,18 +1532,14 @@ static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
+  const int ncu = cus;
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, smf) !=
           hipSuccess || per < 1)
     per = 1;
   // work items: images per wave (wave-owned) or rounds of imgs images per workgroup
   const int nrounds = fast ? (N + kThreads / 64 - 1) / (kThreads / 64) : (N + imgs - 1) / imgs;
-  static const int mult = [] {  // see conv.hip fwd_grid
-    const char* e = getenv("MBK_FWD_GRID_MULT");
-    return e ? std::max(1, atoi(e)) : 1;
-  }();
-  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)ncu * per * mult))),
+  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)ncu * per))),
                      dim3(kThreads), smf, stream, a);
   return (int)hipGetLastError();
 }
@@ -1605,7 +1589,7 @@ extern "C" int mbk_res_bwd32_parts(int N, int H, int W, int imgs) {
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
+  const int ncu = cus;
   const int nrounds = (N + imgs - 1) / imgs;
   return std::max(1, std::min(nrounds, ncu));
 }
@@ -1663,7 +1647,7 @@ extern "C" int mbk_res_blk32_fwd(const void* x, void* u, void* y, const void* co
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const int ncu = mbk_get_cu_budget() > 0 ? std::min(mbk_get_cu_budget(), cus) : cus;
+  const int ncu = cus;
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)kfn, kThreads, sm) !=
           hipSuccess || per < 1)

@@ -23,7 +23,6 @@
 #include "common.h"
 #include "decode.h"
 
-extern "C" int mbk_get_cu_budget();
 
 #include <algorithm>
 #include <cstdlib>
@@ -617,48 +616,34 @@ __device__ __forceinline__ void store_output(const TrunkArgs& a, int img0, int n
   }
 }
 
-// LDSW: weights staged in LDS (double-buffered) vs read through L2. FC: the fused trunk
-// head runs after the last conv; the next group's first weight fetch then waits until after
-// it (keeps the prefetch registers free across the head: no spills).
-template <bool LDSW, bool FC>
+// Weights read through L2 into registers one layer ahead (staging them in LDS, double-
+// buffered, measured slower than L2 + 16 images per tile). FC: the fused trunk head runs
+// after the last conv; the next group's first weight fetch then waits until after it (keeps
+// the prefetch registers free across the head: no spills).
+template <bool FC>
 __global__ __launch_bounds__(kThreads) void trunk_tail_kernel(TrunkArgs a) {
   char* smem = trunk_smem;
   const int oR1 = 0, oR2 = a.r1_bytes;  // region offsets for conv_lds
-  const int oWB[2] = {2 * a.r1_bytes, 2 * a.r1_bytes + kWBufBytes};
   char* R1 = smem + oR1;
   char* R2 = smem + oR2;
-  char* WB[2] = {smem + oWB[0], smem + oWB[1]};
   const int H0 = a.H0, W0 = a.W0, H1 = (H0 + 1) >> 1, W1 = (W0 + 1) >> 1;
   const int H2 = (H1 + 1) >> 1, W2 = (W1 + 1) >> 1;
   const int TNI = a.tni;
   const int ngroups = (a.N + TNI - 1) / TNI;
-  uint4 wr[kWRegs];
-  uint4 wnext[kWFrag];  // register prefetch of the next layer's weights (L2 variant)
-  if (!LDSW) wfetch(a.w[0], tail_cin(0), tail_cout(0), wnext);
-  if (LDSW) {  // layer 0's weights for the first iteration
-    wload(a.w[0], tail_n16(0), wr);
-    wstore(WB[0], tail_n16(0), TG<16>::NCH, wr);
-  }
-  // phase helper (LDSW): prefetch layer l+1 (wrapping to 0 for the next group) into
-  // registers, run conv l from WB[l & 1], park l+1 in the other buffer
+  uint4 wnext[kWFrag];  // register prefetch of the next layer's weights
+  wfetch(a.w[0], tail_cin(0), tail_cout(0), wnext);
+  // phase helper: take layer l's prefetched weights, prefetch layer l+1 (wrapping to 0 for
+  // the next group), run conv l
 #define TAIL_PHASE(l, CI, CO, RELU, MODE, IN, H_, W_, WBUF, OUT)                          \
   do {                                                                                      \
-    if (LDSW) {                                                                             \
+    uint4 wc[kWFrag];                                                                       \
+    _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];                    \
+    if (!(FC && (l) == 13)) {                                                               \
       const int ln = ((l) + 1) % 14;                                                        \
-      wload(a.w[ln], tail_n16(ln), wr);                                                     \
-      conv_lds<CI, CO, RELU, MODE, true>(IN, H_, W_, nimg, WBUF, nullptr, wrow_bytes<CI>(), \
-                                         a.b[l], OUT);                                      \
-      wstore(WB[ln & 1], tail_n16(ln), ln < 5 ? TG<16>::NCH : TG<32>::NCH, wr);             \
-    } else {                                                                                \
-      uint4 wc[kWFrag];                                                                     \
-      _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];                  \
-      if (!(FC && (l) == 13)) {                                                             \
-        const int ln = ((l) + 1) % 14;                                                      \
-        wfetch(a.w[ln], tail_cin(ln), tail_cout(ln), wnext);                                \
-      }                                                                                     \
-      conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, wc, TG<CI>::NCH * 64,        \
-                                          a.b[l], OUT);                                     \
+      wfetch(a.w[ln], tail_cin(ln), tail_cout(ln), wnext);                                  \
     }                                                                                       \
+    conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, wc, TG<CI>::NCH * 64, a.b[l],  \
+                                        OUT);                                               \
   } while (0)
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * TNI, nimg = min(TNI, a.N - img0);
@@ -842,17 +827,9 @@ struct ActTrunkArgs {
   float* reward_dst;
   uint8_t* done_dst;
   uint64_t* stamps;  // diagnostic phase stamps (null: off)
-  // fused head (act_trunk_w_kernel, fused != 0): the tile's sparse head at its end, so the
-  // policy step is ONE launch (no buckets, pending counters or granule rows in HBM)
-  const bf16* Wp;    // [S][80][256] bf16 packed head rows
-  const float* bp;   // [S][80]
-  uint64_t* rng;     // Philox (seed, step): rng[1] <- step + 1 (the graph path's counter)
-  uint64_t step;
-  int fused;
 };
 
 constexpr int kActS = 256;  // 16x16 maps: one map row = one 16-pixel MFMA block
-constexpr int kActPre = kMaxTNI / (kThreads / 64);  // envs per wave and tile (2)
 
 // The env's active-cell bitmap row from its decode (lane l holds cells 4l .. 4l + 3, mk: their
 // mask words): word w = cells 32 w .. 32 w + 31 = lanes 8 w .. 8 w + 7, bit 4 i + q = lane
@@ -879,22 +856,6 @@ __device__ __forceinline__ void write_abits(const uint32_t mk[12], int lane, uin
 // words of a sparse input row read in the first access (count + 31 entries: most envs); the
 // rest only for envs with more occupied cells
 constexpr int kActSpec = 32;
-struct ActLayout {          // byte offsets of the prologue scratch inside R2, tile of tni envs
-  int codes, bits, lut, cnt, np, res, pairs, end;
-};
-__host__ __device__ constexpr ActLayout act_layout(int tni) {
-  ActLayout L{};
-  L.codes = 0;
-  L.bits = L.codes + tni * kActS * 2;
-  L.lut = L.bits + tni * kActS * 4;
-  L.cnt = L.lut + 256 * 16;
-  L.np = L.cnt + kActS * 4;
-  L.res = L.np + 16;
-  L.pairs = L.res + ((tni * 4 + 15) & ~15);
-  L.end = L.pairs + tni * kActS * 8;
-  return L;
-}
-
 __device__ __forceinline__ float bf16_round(float v) { return lo_f(pack2(v, 0.f)); }
 
 // stage-0 conv of one 16x16 image (bit planes [256] u32 in LDS) + max_pool2d(3, 2, 1), into the
@@ -971,252 +932,14 @@ __device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* 
       a.stamps[(size_t)blockIdx.x * 64 * kActStamps + (k) * 64 + threadIdx.x] =           \
           __builtin_amdgcn_s_memrealtime();                                              \
   } while (0)
-constexpr int kActStamps = 21;  // the wave-owned kernel uses all; act_trunk_kernel 0-8
-
-__global__ __launch_bounds__(kThreads) void act_trunk_kernel(ActTrunkArgs a) {
-  char* smem = trunk_smem;
-  const TrunkArgs& t = a.t;
-  const int oR1 = 0, oR2 = t.r1_bytes;
-  char* R1 = smem + oR1;
-  char* R2 = smem + oR2;
-  constexpr int H = 16, W = 16, S = kActS, H0 = 8, W0 = 8, H1 = 4, W1 = 4, H2 = 2, W2 = 2;
-  constexpr int NW = kThreads / 64;
-  const int TNI = t.tni, E = t.N;
-  const ActLayout L = act_layout(TNI);
-  uint16_t* lcodes = (uint16_t*)(R2 + L.codes);
-  uint32_t* lbits = (uint32_t*)(R2 + L.bits);
-  const char* lut = R2 + L.lut;
-  int* lcnt = (int*)(R2 + L.cnt);
-  int* npairs = (int*)(R2 + L.np);
-  int* lres = (int*)(R2 + L.res);
-  int2* lpairs = (int2*)(R2 + L.pairs);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int ngroups = (E + TNI - 1) / TNI;
-  uint4 wnext[kWFrag];  // layer l+1's weight fragments, fetched during layer l
-  uint32_t pre[kActPre] = {0u, 0u};  // sparse input: this lane's word of the next tile's rows
-#define ACT_PHASE(l, CI, CO, RELU, MODE, IN, H_, W_, OUT)                                  \
-  do {                                                                                   \
-    uint4 wc[kWFrag];                                                                    \
-    _Pragma("unroll") for (int k = 0; k < kWFrag; ++k) wc[k] = wnext[k];                 \
-    if ((l) != 13) wfetch(t.w[(l) + 1], tail_cin((l) + 1), tail_cout((l) + 1), wnext);   \
-    conv_lds<CI, CO, RELU, MODE, false>(IN, H_, W_, nimg, 0, wc, TG<CI>::NCH * 64, t.b[l], \
-                                        OUT);                                            \
-  } while (0)
-  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int img0 = grp * TNI, nimg = min(TNI, E - img0);
-    // stage-0 conv weights (A = w[co = li][tap][8g .. 8g+7]) and bias: issued first, their L2
-    // latency hides behind the code loads and the decode
-    Frag8 bw0[9];
-    {
-      const uint4* wp = (const uint4*)(a.w0 + (size_t)li * 9 * 32 + g * 8);
-#pragma unroll
-      for (int c = 0; c < 9; ++c) bw0[c].u = wp[c * 4];
-    }
-    float bias0[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias0[i] = a.b0[4 * g + i];
-    ACT_STAMP(0);
-    // ---- P1: codes / resources -> LDS, byte LUT, counters; reward / done of the last env step
-    if (a.code_list) {
-      // sparse rows (occupied cells only, ~3-8x fewer PCIe bytes than the dense codes): one
-      // wave per env reads the count word and the first 63 entries in one access, scatters
-      // them into the zeroed LDS code row, and reads further entries only if there are more
-      for (int el = wave, j = 0; el < nimg; el += NW, ++j) {
-        uint16_t* cs = lcodes + el * S;
-        for (int c = lane * 4; c < S; c += 256) *(uint2*)(cs + c) = make_uint2(0u, 0u);
-        const uint32_t* row = a.code_list + (size_t)(img0 + el) * a.list_stride;
-        // the first 64 words of the row: prefetched during the previous tile's trunk
-        const uint32_t w = grp == (int)blockIdx.x ? (lane < kActSpec && lane <= S ? row[lane] : 0u)
-                         : pre[j & (kActPre - 1)];
-        const uint32_t w0 = (uint32_t)__shfl((int)w, 0, 64);
-        const int n = min((int)(w0 & 0xFFFFu), S);
-        if (lane == 0) lres[el] = (int)(w0 >> 16);
-        __builtin_amdgcn_wave_barrier();
-        if (lane >= 1 && lane < kActSpec && lane <= n && (w & 0xFFFFu) < (uint32_t)S)
-          cs[w & 0xFFFFu] = (uint16_t)(w >> 16);
-        for (int k = kActSpec + lane; k <= n; k += 64) {
-          const uint32_t x = row[k];
-          if ((x & 0xFFFFu) < (uint32_t)S) cs[x & 0xFFFFu] = (uint16_t)(x >> 16);
-        }
-      }
-    } else {
-      for (int i = tid; i < nimg * (S / 8); i += kThreads) {  // 16 B = 8 codes per thread
-        const int im = i / (S / 8), q = i - im * (S / 8);
-        ((uint4*)lcodes)[i] = ((const uint4*)(a.codes + (size_t)(img0 + im) * S))[q];
-      }
-      if (tid < nimg) lres[tid] = a.res[img0 + tid];
-    }
-    if (tid < 256) ((uint4*)lut)[tid] = mbk::bits8_bf16((uint32_t)tid);
-    if (blockIdx.x == 0 && grp == 0)  // the previous step's launch B is done with these
-      for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
-    for (int c = tid; c < S; c += kThreads) lcnt[c] = 0;
-    if (tid == 0) *npairs = 0;
-    if (tid < nimg) {
-      if (a.reward_dst) a.reward_dst[img0 + tid] = a.reward_src[img0 + tid];
-      if (a.done_dst) a.done_dst[img0 + tid] = a.done_src[img0 + tid];
-    }
-    mbk::lds_barrier();
-    ACT_STAMP(1);
-    // ---- P2: decode, one wave per env
-    for (int el = wave; el < nimg; el += NW) {
-      const int e = img0 + el;
-      const uint16_t* cs = lcodes + el * S;
-      const int r = lres[el];
-      const int c0 = lane * 4;
-      uint32_t ob[4], mk[12];
-      int nact = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = c0 + j;
-        uint32_t w3[3];
-        mbk::cell_mask(cs, c, H, W, r, w3);
-        ob[j] = mbr::code_bits(cs[c]);
-        mk[3 * j] = w3[0];
-        mk[3 * j + 1] = w3[1];
-        mk[3 * j + 2] = w3[2];
-        nact += (w3[0] | w3[1] | w3[2]) != 0u;
-      }
-      // each active cell's rank k among the env's active cells, in cell order (exclusive scan
-      // of the lanes' counts): the head stores the cell's result in the env's k-th granule, so
-      // the finisher reads n granules instead of a whole cell row
-      int kx = nact;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(kx, o, 64);
-        if (lane >= o) kx += y;
-      }
-      const int n = __shfl(kx, 63, 64);
-      kx -= nact;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (mk[3 * j] | mk[3 * j + 1] | mk[3 * j + 2]) {
-          const int c = c0 + j;
-          const int i = atomicAdd(npairs, 1);
-          lpairs[i] = make_int2((c << 19) | atomicAdd(&lcnt[c], 1), e | (kx << 16));
-          ++kx;
-        }
-      }
-      const uint4 o4 = make_uint4(ob[0], ob[1], ob[2], ob[3]);
-      const uint4 m0 = make_uint4(mk[0], mk[1], mk[2], mk[3]);
-      const uint4 m1 = make_uint4(mk[4], mk[5], mk[6], mk[7]);
-      const uint4 m2 = make_uint4(mk[8], mk[9], mk[10], mk[11]);
-      *(uint4*)(lbits + el * S + c0) = o4;
-      if (a.abits) write_abits(mk, lane, a.abits + (size_t)e * (S / 32),
-                               a.abits2 ? a.abits2 + (size_t)e * (S / 32) : nullptr);
-      const size_t eo = (size_t)e * S + c0;
-      *(uint4*)(a.obs + eo) = o4;
-      uint4* mp = (uint4*)(a.mask + eo * 3);
-      mp[0] = m0;
-      mp[1] = m1;
-      mp[2] = m2;
-      if (a.obs2) {  // the same row is the previous slot's bootstrap row T
-        *(uint4*)(a.obs2 + eo) = o4;
-        uint4* mp2 = (uint4*)(a.mask2 + eo * 3);
-        mp2[0] = m0;
-        mp2[1] = m1;
-        mp2[2] = m2;
-      }
-      // the env's action row starts at zero (the head overwrites the active cells); n is the
-      // head's completion counter for the env and the number of its granules
-      const uint4 z4 = make_uint4(0, 0, 0, 0);
-      uint4* act4 = (uint4*)(a.action + (size_t)e * S * 7);
-      for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = z4;
-      if (lane == 0) {
-        a.pending[e] = n;
-        a.pending[E + e] = n;
-        if (n == 0) a.logp[e] = 0.f;
-      }
-      if (a.act_list) {  // nothing to sample: an empty action row
-        if (n == 0 && lane == 0) a.act_list[(size_t)e * a.list_stride] = 0u;
-      } else {  // dense packed actions: all cells no-op until the head writes the active ones
-        *(uint2*)(a.act16 + eo) = make_uint2(0u, 0u);
-      }
-    }
-    mbk::lds_barrier();
-    ACT_STAMP(2);
-    // ---- P3: one global bucket reservation per active cell of the tile (lcnt -> its base) ...
-    for (int c = tid; c < S; c += kThreads) {
-      const int n = lcnt[c];
-      if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
-    }
-    // ... while the stage-0 conv + pool runs, wave w on images w, w + NW
-    for (int im = wave; im < nimg; im += NW) act_conv0(lbits + im * S, lut, bw0, bias0, R1, im);
-    // layer 1's weights: fetched once the prologue's registers are dead (earlier, they spill)
-    wfetch(t.w[0], tail_cin(0), tail_cout(0), wnext);
-    if (a.code_list) {  // the next tile's sparse rows, in flight during this tile's trunk
-      const int img0n = img0 + gridDim.x * TNI;
-#pragma unroll
-      for (int j = 0; j < kActPre; ++j) {
-        const int el = wave + j * NW;
-        pre[j] = (el < TNI && img0n + el < E && lane < kActSpec && lane <= S)
-                     ? a.code_list[(size_t)(img0n + el) * a.list_stride + lane] : 0u;
-      }
-    }
-    mbk::lds_barrier();
-    {
-      const int np = *npairs;
-      for (int i = tid; i < np; i += kThreads) {
-        const int2 pr = lpairs[i];
-        const int c = pr.x >> 19, slot = pr.x & 0x7FFFF;
-        a.bucket[(size_t)c * E + lcnt[c] + slot] = pr.y;
-      }
-    }
-    zero_halo<TG<16>::PIXB>(R1, nimg, H0, W0);
-    mbk::lds_barrier();  // the prologue scratch in R2 is dead from here
-    zero_halo<TG<16>::PIXB>(R2, nimg, H0, W0);
-    mbk::lds_barrier();
-    ACT_STAMP(3);
-    // ---- stage 0 residual blocks, stages 1 and 2, network.5 + critic (trunk_tail_kernel)
-#pragma unroll 1
-    for (int rb = 0; rb < 2; ++rb) {
-      ACT_PHASE(2 * rb, 16, 16, true, OUT_TILE_RELU, oR1, H0, W0, oR2);
-      mbk::lds_barrier();
-      ACT_PHASE(2 * rb + 1, 16, 16, false, OUT_TILE_ADD, oR2, H0, W0, oR1);
-      mbk::lds_barrier();
-    }
-    ACT_STAMP(4);
-    ACT_PHASE(4, 16, 32, false, OUT_STAGE, oR1, H0, W0, oR2);
-    mbk::lds_barrier();
-    pool_lds<32>((const bf16*)R2, H0, W0, nimg, R1);
-    zero_halo<TG<32>::PIXB>(R1, nimg, H1, W1);
-    mbk::lds_barrier();
-    zero_halo<TG<32>::PIXB>(R2, nimg, H1, W1);
-#pragma unroll 1
-    for (int rb = 0; rb < 2; ++rb) {
-      ACT_PHASE(5 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H1, W1, oR2);
-      mbk::lds_barrier();
-      ACT_PHASE(6 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H1, W1, oR1);
-      mbk::lds_barrier();
-    }
-    ACT_STAMP(5);
-    ACT_PHASE(9, 32, 32, false, OUT_STAGE, oR1, H1, W1, oR2);
-    mbk::lds_barrier();
-    pool_lds<32>((const bf16*)R2, H1, W1, nimg, R1);
-    zero_halo<TG<32>::PIXB>(R1, nimg, H2, W2);
-    mbk::lds_barrier();
-    zero_halo<TG<32>::PIXB>(R2, nimg, H2, W2);
-#pragma unroll 1
-    for (int rb = 0; rb < 2; ++rb) {
-      ACT_PHASE(10 + 2 * rb, 32, 32, true, OUT_TILE_RELU, oR1, H2, W2, oR2);
-      mbk::lds_barrier();
-      ACT_PHASE(11 + 2 * rb, 32, 32, false, OUT_TILE_ADD, oR2, H2, W2, oR1);
-      mbk::lds_barrier();
-    }
-    ACT_STAMP(6);
-    trunk_fc(R1, H2, W2, nimg, img0, t, (float*)R2);  // ends with a barrier
-    ACT_STAMP(7);
-    ACT_STAMP(8);
-  }
-#undef ACT_PHASE
-}
+constexpr int kActStamps = 21;
 
 // ------------------------------------------------------------------ launch A, wave-owned tiles
-// act_trunk_kernel's work with the tile split by WAVE instead of by phase: wave w owns envs
+// The acting trunk with the tile split by WAVE instead of by phase: wave w owns envs
 // 2w, 2w+1 of the 16-env tile from their sparse rows to their trunk output -- codes, decode,
 // stage-0 conv + pool, the 14 convs (conv_lds WV = 1 / 2 over its own images), the pools and
 // the halo zeroing -- in its own slices of the two regions, so the trunk needs no workgroup
-// barrier at all (LDS is in order within a wave). act_trunk_kernel ran ~25 workgroup-wide
+// barrier at all (LDS is in order within a wave). The phase-split form ran ~25 workgroup-wide
 // phases per tile with 2 waves per SIMD: every phase waited for its slowest wave, the 2x2 stage
 // had 4 pixel blocks for 8 waves, and no tile's prologue overlapped another's convs
 // (profiles/33: 52 % of wave cycles waiting, MFMA 9.7 %).
@@ -1242,21 +965,9 @@ constexpr int kWLut = 2 * kWRegion;                          // byte -> 8 bf16 t
 constexpr int kWCnt = kWLut + 256 * 16;                      // [2][256] pair counts per cell
 constexpr int kWNp = kWCnt + 2 * kActS * 4;                  // [2] list lengths (+ pad)
 constexpr int kWVred = kWNp + 16;                            // [16 blocks][16 images] critic
-constexpr int kWCellU = kWVred + 16 * 16 * 4;                // fused head: cell -> unit [256] u16
-constexpr int kWCellL = kWCellU + kActS * 2;                 // unit -> cell [256] u8
-constexpr int kWMisc = kWCellL + kActS;                      // unit count, then [16] env n
 constexpr int kWList = 270;                                  // list entries per parity in LDS
-constexpr int kWLst = kWMisc + 80;                           // [2][kWList] packed pairs
+constexpr int kWLst = kWVred + 16 * 16 * 4;                  // [2][kWList] packed pairs
 constexpr int kWSmem = kWLst + 2 * kWList * 4;
-// the fused head's tile-end scratch, in regions whose trunk data is dead by then: f rows,
-// unit rows and the per-wave logit tiles in R2, the per-env granules in R1 (after the FC)
-constexpr int kHNP = 80, kHKD = 256;                         // head.hip NP / KD
-constexpr int kWHf = kWRegion;                               // [16][256] bf16 features
-constexpr int kWHrows = kWHf + 16 * kHKD * 2;                // [<=256 units][16] u16 rows
-constexpr int kWHz = kWHrows + kActS * 16 * 2;               // [8 waves][16][81] f32
-constexpr int kWHgran = 0;                                   // [16 envs][256] u64 granules
-static_assert(kWHz + 8 * 16 * (kHNP + 1) * 4 <= 2 * kWRegion, "fused head scratch (R2)");
-static_assert(16 * kActS * 8 <= kWRegion, "fused head granules (R1)");
 static_assert(kWSmem <= 160 * 1024, "wave-owned acting tile exceeds the LDS");
 static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage footprints");
 // a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run)
@@ -1267,7 +978,7 @@ static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
 // fragments, loaded before the barrier) for the tile's 16 images, whose X2 tiles sit in the
 // waves' R1 slices (image i: wave i / 2's slice, its image i % 2); critic partials -> vred
 __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
-                                        const uint4 wf[2][4], float* vred, bool fused) {
+                                        const uint4 wf[2][4], float* vred) {
   constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2;
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));  // opaque: no address hoisted out of the tile loop
@@ -1307,48 +1018,7 @@ __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
     for (int k = 0; k < 2; ++k)
       o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
              ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
-    if (valid) {
-      if (fused)  // the tile's head reads f from LDS
-        *(uint2*)(trunk_smem + kWHf + (li * kHKD + h0) * 2) = make_uint2(o[0], o[1]);
-      else
-        *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
-    }
-  }
-}
-
-// Z[16 pairs][80] of one fused-head unit (the tile's pairs of cell c, <= 16: one per env) into
-// the wave's LDS tile z: head.hip unit_z's MFMA operands and K order (bit-identical logits), with
-// the X rows read from the tile's LDS features
-__device__ __forceinline__ void tile_unit_z(const uint16_t* rows, int cnt, int c,
-                                            const bf16* __restrict__ Wp,
-                                            const float* __restrict__ bp, float (*z)[kHNP + 1]) {
-  int lane = threadIdx.x & 63;
-  asm volatile("" : "+v"(lane));  // opaque: no address hoisted out of the tile loop
-  const int G = lane >> 4, li = lane & 15;
-  const bool valid = li < cnt;
-  const int el = valid ? (rows[li] & 15) : 0;
-  const char* xrow = trunk_smem + kWHf + el * kHKD * 2 + G * 16;
-  const bf16* wc = Wp + (size_t)c * kHNP * kHKD;
-  f32x4 acc[5];
-#pragma unroll
-  for (int nb = 0; nb < 5; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int ks = 0; ks < kHKD / 32; ++ks) {
-    Frag8 x;
-    x.u = valid ? *(const uint4*)(xrow + ks * 64) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-    for (int nb = 0; nb < 5; ++nb) {
-      Frag8 w;
-      w.u = *((const uint4*)(wc + (size_t)(nb * 16 + li) * kHKD + ks * 32) + G);
-      acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(x.v, w.v, acc[nb], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int nb = 0; nb < 5; ++nb) {
-    const int col = nb * 16 + li;
-    const float bias = bp[c * kHNP + col];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) z[4 * G + i][col] = acc[nb][i] + bias;
+    if (valid) *(uint2*)(a.f_out + (size_t)(img0 + li) * 256 + h0) = make_uint2(o[0], o[1]);
   }
 }
 
@@ -1372,16 +1042,8 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
   if (tid < 256) ((uint4*)(trunk_smem + kWLut))[tid] = mbk::bits8_bf16((uint32_t)tid);
   for (int c = tid; c < 2 * S; c += kThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
   if (tid < 2) ((int*)(trunk_smem + kWNp))[tid] = 0;
-  const bool fused = a.fused != 0;
-  int* ncells = (int*)(trunk_smem + kWMisc);  // fused: distinct active cells of the tile
-  int* env_n = ncells + 1;                    // fused: active cells per env of the tile
-  uint16_t* cellunit = (uint16_t*)(trunk_smem + kWCellU);
-  uint8_t* celllist = (uint8_t*)(trunk_smem + kWCellL);
-  if (tid == 0) *ncells = 0;
   if (blockIdx.x == 0) {
-    if (fused && tid == 0) a.rng[1] = a.step + 1;  // the graph path's counter
-    // the previous step's launch B is done with these (zeroed in both forms: the engine
-    // picks the form per step, and the next B-form step counts into this half)
+    // the previous step's launch B is done with these
     for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
   }
   mbk::lds_barrier();
@@ -1501,11 +1163,6 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
             const int c = c0 + q;
             const int i = atomicAdd(np, 1);
             const int slot = atomicAdd(&lcnt[c], 1);
-            if (fused && slot == 0) {  // the tile's first pair of cell c opens its unit
-              const int ui = atomicAdd(ncells, 1);
-              cellunit[c] = (uint16_t)ui;
-              celllist[ui] = (uint8_t)c;
-            }
             const uint32_t en = (uint32_t)c | ((uint32_t)slot << 8) | ((uint32_t)el << 12) |
                                 ((uint32_t)kx << 16);
             if (i < kWList) {
@@ -1541,12 +1198,8 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
         uint4* act4 = (uint4*)(a.action + (size_t)e * S * 7);
         for (int i = lane; i < S * 7 / 16; i += 64) act4[i] = z4;
         if (lane == 0) {
-          if (fused) {
-            env_n[el] = n;
-          } else {
-            a.pending[e] = n;
-            a.pending[E + e] = n;
-          }
+          a.pending[e] = n;
+          a.pending[E + e] = n;
           if (n == 0) a.logp[e] = 0.f;
         }
         if (a.act_list) {
@@ -1603,16 +1256,13 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
 #pragma unroll
       for (int ks = 0; ks < H2 * W2; ++ks) wf[jj][ks] = wrow[ks * 4];
     }
-    // spill rows in L2 first; fused: also this wave's mask rows (the head re-reads the active
-    // cells' masks from HBM, written by other waves of the tile)
-    if (spilled || (fused && nw > 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // spill rows in L2 first
+    if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mbk::lds_barrier();
     ACT_STAMP(19);
-    if (!fused) {
-      for (int c = tid; c < S; c += kThreads) {
-        const int n = lcnt[c];
-        if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
-      }
+    for (int c = tid; c < S; c += kThreads) {
+      const int n = lcnt[c];
+      if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
     }
     {  // the other parity (the previous tile's, consumed before this barrier) for the next tile
       int* lc2 = (int*)(trunk_smem + kWCnt) + (par ^ 1) * S;
@@ -1620,114 +1270,18 @@ __global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
       if (tid == 0) ((int*)(trunk_smem + kWNp))[par ^ 1] = 0;
     }
     const int npr = *np;
-    uint16_t* urows = (uint16_t*)(trunk_smem + kWHrows);
-    if (fused) {  // each pair's (env, rank) into its unit's row slot
-      for (int i = tid; i < npr; i += kThreads) {
-        const uint32_t en = i < kWList ? lst[i]
-                                       : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-        const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
-        urows[cellunit[c] * 16 + slot] = (uint16_t)(((en >> 12) & 0xFu) | ((en >> 16) << 4));
-      }
-    }
-    tile_fc(nimg, img0, t, wf, vred, fused);
+    tile_fc(nimg, img0, t, wf, vred);
     mbk::lds_barrier();
     if (tid < nimg) a.t.v_out[img0 + tid] = mbk::crit_sum(vred + tid, 16, 16, t.bc[0]);
-    if (!fused) {
-      for (int i = tid; i < npr; i += kThreads) {
-        const uint32_t en = i < kWList ? lst[i]
-                                       : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
-        const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
-        const int el = (int)((en >> 12) & 0xFu), rank = (int)(en >> 16);
-        a.bucket[(size_t)c * E + lcnt[c] + slot] = (img0 + el) | (rank << 16);
-      }
-      ACT_STAMP(20);
-      continue;
+    for (int i = tid; i < npr; i += kThreads) {
+      const uint32_t en = i < kWList ? lst[i]
+                                     : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+      const int c = (int)(en & 0xFFu), slot = (int)((en >> 8) & 0xFu);
+      const int el = (int)((en >> 12) & 0xFu), rank = (int)(en >> 16);
+      a.bucket[(size_t)c * E + lcnt[c] + slot] = (img0 + el) | (rank << 16);
     }
-    // ---- fused head: wave w samples units w, w + 8, ... (a unit = the tile's pairs of one
-    // cell, one per env), head_act_kernel's maths: unit_z logits, Philox draws keyed by
-    // (env * S + cell, step), cell_forward; each pair's {log-prob, cell | packed action << 16}
-    // granule goes to its env's rank slot in LDS
-    {
-      const int nu = *ncells;
-      float (*z)[kHNP + 1] = (float (*)[kHNP + 1])(trunk_smem + kWHz + wave * 16 * (kHNP + 1) * 4);
-      uint64_t* gran = (uint64_t*)(trunk_smem + kWHgran);
-      const uint64_t seed = a.rng[0], step = a.step;
-      for (int ui = wave; ui < nu; ui += NW) {
-        const int c = celllist[ui], cnt = lcnt[c];
-        const uint16_t* rows = urows + ui * 16;
-        tile_unit_z(rows, cnt, c, a.Wp, a.bp, z);
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's logit tile is in LDS
-        __builtin_amdgcn_wave_barrier();
-        if (lane < cnt) {
-          const int el = rows[lane] & 15, rank = rows[lane] >> 4;
-          const size_t fc = (size_t)(img0 + el) * S + c;
-          uint32_t m[3];
-#pragma unroll
-          for (int q = 0; q < 3; ++q)
-            m[q] = __hip_atomic_load(a.mask + fc * 3 + q, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-          uint8_t act[mbk::kComps];
-          float uu[mbk::kComps];
-          mbk::u32x4 ctr = {(uint32_t)fc, (uint32_t)(fc >> 32), (uint32_t)step,
-                            (uint32_t)(step >> 32)};
-          mbk::u32x4 q0 = mbk::philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-          ctr.y ^= 0x80000000u;
-          mbk::u32x4 q1 = mbk::philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
-          uu[0] = mbk::u01(q0.x); uu[1] = mbk::u01(q0.y); uu[2] = mbk::u01(q0.z);
-          uu[3] = mbk::u01(q0.w); uu[4] = mbk::u01(q1.x); uu[5] = mbk::u01(q1.y);
-          uu[6] = mbk::u01(q1.z);
-          float lp, ent;
-          mbk::cell_forward(&z[lane][0], m, act, true, uu, &lp, &ent);
-#pragma unroll
-          for (int q = 0; q < mbk::kComps; ++q) a.action[fc * mbk::kComps + q] = act[q];
-          gran[el * S + rank] =
-              (uint64_t)__float_as_uint(lp) |
-              ((uint64_t)((uint32_t)c | ((uint32_t)mbr::pack_env_action(act) << 16)) << 32);
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
-    mbk::lds_barrier();
-    // ---- per env of this wave: log-prob (row_sum_pack's lane-strided order) and its actions
-#pragma unroll 1
-    for (int j = 0; j < nw; ++j) {
-      const int el = e0 + j, fe = img0 + el, n = env_n[el];
-      if (n == 0) continue;  // decode wrote logp 0 and the empty action row
-      const uint64_t* row = (const uint64_t*)(trunk_smem + kWHgran) + el * S;
-      float sl = 0.f;
-      int nz = 0;
-      uint32_t* lrow = a.act_list ? a.act_list + (size_t)fe * a.list_stride : nullptr;
-      for (int k0 = 0; k0 < n; k0 += 64) {
-        const int kk = k0 + lane;
-        const uint64_t x = kk < n ? row[kk] : 0ull;
-        const uint32_t hi = (uint32_t)(x >> 32);
-        const int kn = min(64, n - k0);
-        for (int q = 0; q < kn; ++q) {
-          const uint32_t lo_q = (uint32_t)__shfl((int)(uint32_t)x, q, 64);
-          const uint32_t hi_q = (uint32_t)__shfl((int)hi, q, 64);
-          if ((int)(hi_q & 63u) == lane) sl += __uint_as_float(lo_q);
-        }
-        const uint32_t code = hi >> 16;
-        if (lrow) {
-          const uint64_t bal = __ballot(kk < n && code != 0u);
-          const int pos = nz + __popcll(bal & ((1ull << lane) - 1ull));
-          if (kk < n && code != 0u) lrow[1 + pos] = (hi & 0xFFFFu) | (code << 16);
-          nz += __popcll(bal);
-        } else if (kk < n) {
-          a.act16[(size_t)fe * S + (hi & 0xFFFFu)] = (uint16_t)code;
-        }
-      }
-      sl = mbk::wave_sum(sl);
-      if (lane == 0) {
-        a.logp[fe] = sl;
-        if (lrow) lrow[0] = (uint32_t)nz;
-      }
-    }
-    if (tid == 0) *ncells = 0;
     ACT_STAMP(20);
-    mbk::lds_barrier();  // the next tile's decode / conv0 reuse R1 / R2
   }
 #undef ACT_WPHASE
 }
@@ -1845,25 +1399,11 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
   }
   // images per iteration: as many as LDS allows (each conv phase pays one L2 round trip
   // for its weights, so more images amortise it) while keeping >= one group per CU
-  static int variant = -1, force_tni = 0;  // tuning knobs (A/B in tools/microbench.py)
-  if (variant < 0) {
-    const char* v = std::getenv("MBK_TRUNK_VARIANT");
-    variant = (v && std::string(v) == "lds") ? 1 : 0;  // measured: L2 + 16 images is faster
-    const char* t = std::getenv("MBK_TRUNK_TNI");
-    force_tni = t ? std::atoi(t) : 0;
-  }
   const bool f8 = a.w8[0] != nullptr;
-  // the fused head and the fp8 trunk use the L2 variant
-  const bool ldsw = variant == 1 && a.f_out == nullptr && !f8;
-  const size_t wb = ldsw ? 2 * kWBufBytes : 0;
   int tni = 1;
-  while (tni < kMaxTNI && trunk_smem_bytes(H0, W0, tni * 2, wb, f8) <= 160 * 1024 &&
+  while (tni < kMaxTNI && trunk_smem_bytes(H0, W0, tni * 2, 0, f8) <= 160 * 1024 &&
          (N + tni * 2 - 1) / (tni * 2) >= cus)
     tni *= 2;
-  if (force_tni > 0) {
-    tni = std::min(force_tni, kMaxTNI);
-    while (tni > 1 && trunk_smem_bytes(H0, W0, tni, wb, f8) > 160 * 1024) tni /= 2;
-  }
   a.tni = tni;
   // float-reciprocal pixel index math in the kernel is exact only for tni*H0*W0 < 2^16
   if (H0 * W0 > 1024 || (int64_t)tni * H0 * W0 >= (int64_t(1) << 16))
@@ -1871,13 +1411,11 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
   const size_t r = region_bytes(H0, W0, tni);
   a.r1_bytes = f8 ? (int)trunk8_region_a(H0, W0, tni) : (int)r;
   a.r2_bytes = f8 ? (int)trunk8_region_b(H0, W0, tni) : (int)r;
-  const size_t sm = trunk_smem_bytes(H0, W0, tni, wb, f8);
+  const size_t sm = trunk_smem_bytes(H0, W0, tni, 0, f8);
   if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
   const bool fc = a.f_out != nullptr;
   if (fc && f8) return (int)hipErrorInvalidValue;
-  auto kfn = f8 ? trunk_tail8_kernel
-             : fc ? trunk_tail_kernel<false, true>
-                  : ldsw ? trunk_tail_kernel<true, false> : trunk_tail_kernel<false, false>;
+  auto kfn = f8 ? trunk_tail8_kernel : fc ? trunk_tail_kernel<true> : trunk_tail_kernel<false>;
   if (sm > 64 * 1024)
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   int per = 0;
@@ -1885,23 +1423,13 @@ static int trunk_launch(TrunkArgs a, int N, int H0, int W0, hipStream_t stream) 
           hipSuccess || per < 1)
     per = 1;
   const int ngroups = (N + tni - 1) / tni;
-  // persistent grid over the whole device (the CU budget, mbk_set_cu_budget, sizes the
-  // LEARNER's persistent grids; this is the acting kernel)
+  // persistent grid over the whole device
   const int grid = std::min(ngroups, cus * per);
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }
 
 // ------------------------------------------------------------------ fused acting step, launch A
-static int act_tni() {
-  static int tni = 0;
-  if (!tni) {  // MBK_ACT_TNI=8: half-size tiles (77 KB of LDS, so a tile can share a CU)
-    const char* v = std::getenv("MBK_ACT_TNI");
-    tni = (v && std::atoi(v) == 8) ? 8 : kMaxTNI;
-  }
-  return tni;
-}
-
 static bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 static uint64_t* g_act_stamps = nullptr;  // diagnostic phase stamps (tools/act_phases.py)
@@ -1909,74 +1437,6 @@ static uint64_t* g_act_stamps = nullptr;  // diagnostic phase stamps (tools/act_
 extern "C" int mbk_act_set_stamps(void* stamps) {
   g_act_stamps = (uint64_t*)stamps;
   return kActStamps;
-}
-
-// launch-A form: MBK_ACT_WAVE=0 the phase-split act_trunk_kernel (A/B), else the wave-owned
-// kernel; MBK_ACT_FUSED=0 stops that one at the trunk + buckets and leaves the head to launch
-// B. mbk_act_set_mode overrides both (tests run every form in one process; -1 = environment).
-static int g_act_wave = -1, g_act_fused = -1;
-static int act_wave() {
-  if (g_act_wave < 0) {
-    const char* e = std::getenv("MBK_ACT_WAVE");
-    g_act_wave = (e ? std::atoi(e) : 1) != 0;
-  }
-  return g_act_wave;
-}
-
-// The policy step in ONE launch: the wave-owned kernel samples the sparse head at each tile's
-// end (MBK_ACT_FUSED=1; the default 0 leaves it to launch B, which measured level or ahead
-// under the learner, profiles/34). head.hip's mbk_act_head asks this and launches nothing
-// when A did the head.
-extern "C" int mbk_act_fused() {
-  if (g_act_fused < 0) {
-    const char* e = std::getenv("MBK_ACT_FUSED");
-    g_act_fused = (e ? std::atoi(e) : 0) != 0;
-  }
-  return g_act_fused && act_wave();
-}
-
-// Sparse input rows, pinned host -> HBM, ahead of launch A: read inside A, the first tile's
-// rows cost ~19 us of PCIe wait in every workgroup (act_phases: 214 -> 184 us per 8192 envs
-// with the rows already in HBM). Here a few workgroups stream them (two envs per wave
-// instruction, 32 lanes each, kRowU env pairs in flight per wave) while the rest of the GPU
-// runs other work; only a row's n + 1 words move.
-constexpr int kRowU = 4;
-__global__ __launch_bounds__(256) void act_rows_kernel(const uint32_t* __restrict__ src,
-                                                       uint32_t* __restrict__ dst, int E,
-                                                       int stride, int S) {
-  const int lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
-  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const int nwaves = (int)(gridDim.x * blockDim.x >> 6);
-  for (int base = wave * 2 * kRowU; base < E; base += nwaves * 2 * kRowU) {
-    uint32_t w[kRowU];
-#pragma unroll
-    for (int u = 0; u < kRowU; ++u) {
-      const int e = base + 2 * u + half;
-      w[u] = e < E ? src[(size_t)e * stride + l] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kRowU; ++u) {
-      const int e = base + 2 * u + half;
-      const int n = min((int)((uint32_t)__shfl((int)w[u], half * 32, 64) & 0xFFFFu), S);
-      if (e >= E) continue;
-      const size_t r = (size_t)e * stride;
-      if (l <= n) dst[r + l] = w[u];
-      for (int q = 32 + l; q <= n; q += 32) dst[r + q] = src[r + q];
-    }
-  }
-}
-
-// the form of one step: MbkActStep.head_form 1 = head in A, 2 = launch B, 0 = the default
-// above (the engine picks per step from the env workers' active-cell count)
-extern "C" int mbk_act_step_fused(const MbkActStep* s) {
-  if (!act_wave()) return 0;
-  return s->head_form == 1 ? 1 : s->head_form == 2 ? 0 : mbk_act_fused();
-}
-
-extern "C" int mbk_act_set_mode(int wave, int fused) {
-  g_act_wave = wave < 0 ? -1 : wave != 0;
-  g_act_fused = fused < 0 ? -1 : fused != 0;
-  return act_wave() * 2 + mbk_act_fused();
 }
 
 extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStream_t stream) {
@@ -2014,26 +1474,16 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   t.N = m->E;
   t.H0 = 8;
   t.W0 = 8;
-  const bool wave_owned = act_wave() != 0;
-  const int tni = wave_owned ? (kThreads / 64) * kWEnv : act_tni();
+  const int tni = (kThreads / 64) * kWEnv;
   t.tni = tni;
-  const size_t r =
-      (std::max(region_bytes(8, 8, tni), (size_t)act_layout(tni).end) + 15) & ~(size_t)15;
-  t.r1_bytes = t.r2_bytes = (int)r;
-  const size_t sm = wave_owned ? (size_t)kWSmem : 2 * r;
-  if (sm > 160 * 1024) return (int)hipErrorInvalidValue;
-  if (wave_owned && m->E > 65535) return (int)hipErrorInvalidValue;  // bucket entry: env | rank
+  t.r1_bytes = t.r2_bytes = kWRegion;
+  const size_t sm = (size_t)kWSmem;
+  if (m->E > 65535) return (int)hipErrorInvalidValue;  // bucket entry: env | rank
   a.w0 = (const bf16*)m->w0;
   a.b0 = m->b0;
   a.codes = s->codes;
   a.res = s->res;
   a.code_list = s->code_list;
-  if (s->code_list && s->code_list_dev) {
-    if (!al16(s->code_list_dev)) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(act_rows_kernel, dim3(64), dim3(256), 0, stream, s->code_list,
-                       s->code_list_dev, m->E, s->list_stride, m->H * m->W);
-    a.code_list = s->code_list_dev;
-  }
   a.act_list = s->act_list;
   a.list_stride = s->list_stride;
   a.obs = s->obs;
@@ -2057,14 +1507,6 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   a.reward_dst = s->reward_dst;
   a.done_dst = s->done_dst;
   a.stamps = g_act_stamps;
-  a.fused = mbk_act_step_fused(s);
-  if (a.fused) {
-    if (!m->Wp || !m->bp || !m->rng) return (int)hipErrorInvalidValue;
-    a.Wp = (const bf16*)m->Wp;
-    a.bp = m->bp;
-    a.rng = m->rng;
-    a.step = s->step;
-  }
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -2072,13 +1514,10 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  const void* kfn = wave_owned ? (const void*)act_trunk_w_kernel : (const void*)act_trunk_kernel;
+  const void* kfn = (const void*)act_trunk_w_kernel;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)act_trunk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                        160 * 1024);
-    hipFuncSetAttribute((const void*)act_trunk_w_kernel,
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   int per = 0;
@@ -2087,9 +1526,6 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
     per = 1;
   const int ngroups = (m->E + tni - 1) / tni;
   const int grid = std::min(ngroups, cus * per);
-  if (wave_owned)
-    hipLaunchKernelGGL(act_trunk_w_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
-  else
-    hipLaunchKernelGGL(act_trunk_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
+  hipLaunchKernelGGL(act_trunk_w_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

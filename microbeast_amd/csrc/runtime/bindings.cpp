@@ -233,24 +233,6 @@ PYBIND11_MODULE(_mbrt, m) {
                                  hipMemcpyDefault, (hipStream_t)stream);
   });
 
-  // A stream restricted to a subset of CUs (MI355X: 256 CUs in 8 XCDs). Used for the
-  // learner so that every `reserve_every`-th CU stays free for the latency-critical
-  // policy stream; CU ids are spread so every XCD / shader engine keeps some free.
-  m.def("create_cu_masked_stream", [](int device, int reserve_every) -> uintptr_t {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
-      throw std::runtime_error("hipGetDeviceProperties failed");
-    const int ncu = prop.multiProcessorCount;
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i)
-      if (reserve_every <= 0 || (i % reserve_every) != 0) mask[i / 32] |= 1u << (i % 32);
-    hipSetDevice(device);
-    hipStream_t st = nullptr;
-    if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess)
-      throw std::runtime_error("hipExtStreamCreateWithCUMask failed");
-    return (uintptr_t)st;
-  });
-
   py::class_<GpuEngine>(m, "GpuEngine")
       .def(py::init([](py::dict c, py::dict b) {
         EngineConfig cfg;
@@ -268,8 +250,6 @@ PYBIND11_MODULE(_mbrt, m) {
         cfg.device = c["device"].cast<int>();
         if (c.contains("selfplay_groups")) cfg.selfplay_groups = c["selfplay_groups"].cast<int>();
         if (c.contains("n_lanes")) cfg.n_lanes = c["n_lanes"].cast<int>();
-        if (c.contains("policy_cu_every")) cfg.policy_cu_every = c["policy_cu_every"].cast<int>();
-        if (c.contains("policy_gate")) cfg.policy_gate = c["policy_gate"].cast<bool>();
         if (c.contains("preroll")) cfg.preroll = c["preroll"].cast<int>();
         EngineBuffers buf;
         buf.obs = b["obs"].cast<uintptr_t>();
@@ -305,9 +285,6 @@ PYBIND11_MODULE(_mbrt, m) {
           io.in_res_p1 = get(d, "in_res_p1");
           io.out_act16_p1 = get(d, "out_act16_p1");
           io.out_logits = get(d, "out_logits");
-          io.in_codes_b = get(d, "in_codes_b");
-          io.in_res_b = get(d, "in_res_b");
-          io.out_act16_b = get(d, "out_act16_b");
           buf.lanes.push_back(io);
         }
         return new GpuEngine(cfg, buf);
@@ -317,9 +294,9 @@ PYBIND11_MODULE(_mbrt, m) {
            [](GpuEngine& e, std::vector<std::vector<uintptr_t>> graphs) {
              std::vector<LaneGraphs> lg;
              for (const auto& t : graphs) {
-               if (t.size() != 4 && t.size() != 5)
-                 throw std::runtime_error("start: need 4 (or 5) graph handles per lane");
-               lg.push_back(LaneGraphs{t[0], t[1], t[2], t[3], t.size() == 5 ? t[4] : 0});
+               if (t.size() != 4)
+                 throw std::runtime_error("start: need 4 graph handles per lane");
+               lg.push_back(LaneGraphs{t[0], t[1], t[2], t[3]});
              }
              e.start(lg);
            })
@@ -341,15 +318,12 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("drain_episodes", [](GpuEngine& e) { return records_to_list(e.drain_episodes()); })
       .def("stream", &GpuEngine::stream, py::arg("lane") = 0)
       .def("failed", &GpuEngine::failed)
-      .def("gate_ptr", &GpuEngine::gate_ptr)
       .def("host_codes", &GpuEngine::host_codes)
       .def("host_res", &GpuEngine::host_res)
       .def("host_act16", &GpuEngine::host_act16)
-      .def("set_group_graphs", &GpuEngine::set_group_graphs)
       // fused acting steps: one packed MbkActModel (mbk_api.h, built by ops/act.py) per lane
       .def("set_act_models",
-           [](GpuEngine& e, std::vector<py::bytes> blocks, bool copy,
-              std::vector<py::bytes> opp_blocks) {
+           [](GpuEngine& e, std::vector<py::bytes> blocks, std::vector<py::bytes> opp_blocks) {
              auto unpack = [](const std::vector<py::bytes>& bs) {
                std::vector<MbkActModel> ms;
                for (const py::bytes& b : bs) {
@@ -365,9 +339,9 @@ PYBIND11_MODULE(_mbrt, m) {
                }
                return ms;
              };
-             e.set_act_models(unpack(blocks), copy, unpack(opp_blocks));
+             e.set_act_models(unpack(blocks), unpack(opp_blocks));
            },
-           py::arg("blocks"), py::arg("copy") = false,
+           py::arg("blocks"),
            py::arg("opp_blocks") = std::vector<py::bytes>{})
       .def("act_mode", &GpuEngine::act_mode)
       .def("set_sparse_io", &GpuEngine::set_sparse_io)
@@ -390,8 +364,7 @@ PYBIND11_MODULE(_mbrt, m) {
         d["env_phase_s"] = s.env_phase_s;
         d["enqueue_s"] = s.enqueue_s;
         d["graph_launch_s"] = s.graph_launch_s;
-        d["act_fused_steps"] = s.act_fused_steps;
-        d["act_b_steps"] = s.act_b_steps;
+        d["act_steps"] = s.act_steps;
         d["act_active_cells"] = s.act_active_cells;
         d["slot_wait_s"] = s.slot_wait_s;
         d["env_s"] = s.env_s;

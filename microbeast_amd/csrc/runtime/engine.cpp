@@ -58,25 +58,7 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     L.io = buf_.lanes[l];
     if (!L.io.in_codes || !L.io.in_res || !L.io.out_act16)
       throw std::runtime_error("GpuEngine: in_codes / in_res / out_act16 buffers required");
-    if (cfg_.policy_cu_every > 0) {
-      int ncu = 0;
-      CTOR_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg_.device));
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; i += cfg_.policy_cu_every) mask[i / 32] |= 1u << (i % 32);
-      CTOR_CHECK(hipExtStreamCreateWithCUMask(&L.stream, (uint32_t)mask.size(), mask.data()));
-    } else {
-      CTOR_CHECK(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, prio_greatest));
-    }
-    L.overlap = L.io.in_codes_b && L.io.in_res_b && L.io.out_act16_b && cfg_.selfplay_groups == 0;
-    if (L.overlap) {
-      CTOR_CHECK(hipStreamCreateWithPriority(&L.s_in, hipStreamNonBlocking, prio_greatest));
-      CTOR_CHECK(hipStreamCreateWithPriority(&L.s_out, hipStreamNonBlocking, prio_greatest));
-      for (int p = 0; p < 2; ++p) {
-        CTOR_CHECK(hipEventCreateWithFlags(&L.ev_h2d[p], hipEventDisableTiming));
-        CTOR_CHECK(hipEventCreateWithFlags(&L.ev_done[p], hipEventDisableTiming));
-        CTOR_CHECK(hipEventCreateWithFlags(&L.ev_d2h[p], hipEventDisableTiming));
-      }
-    }
+    CTOR_CHECK(hipStreamCreateWithPriority(&L.stream, hipStreamNonBlocking, prio_greatest));
   }
   CTOR_CHECK(hipHostMalloc((void**)&h_codes_, (size_t)total * S_ * 2, hipHostMallocDefault));
   CTOR_CHECK(hipHostMalloc((void**)&h_res_, (size_t)total * 4, hipHostMallocDefault));
@@ -146,25 +128,15 @@ GpuEngine::GpuEngine(const EngineConfig& cfg, const EngineBuffers& buf) : cfg_(c
     c.consumed.assign(cfg_.n_lanes, nullptr);
     for (auto& ev : c.consumed) CTOR_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   }
-  // work chunk: enough chunks for every worker, at least 2 envs each
+  // work chunk: enough chunks for every worker, at least 2 envs each (16 envs per item
+  // measured level with 8, 24, 32 and faster than 8: profile 36)
   chunk_ = std::max(1, std::min(16, cfg_.envs_per_group / std::max(1, 2 * cfg_.n_threads)));
-  if (const char* c = std::getenv("MBK_ENV_CHUNK")) {  // envs per work item (A/B knob)
-    const int v = std::atoi(c);
-    if (v > 0) chunk_ = std::max(1, std::min(v, cfg_.envs_per_group));
-  }
-  if (cfg_.policy_gate && cfg_.n_lanes == 1) {
-    CTOR_CHECK(hipMalloc((void**)&gate_, sizeof(uint32_t)));
-    CTOR_CHECK(hipMemset(gate_, 0, sizeof(uint32_t)));
-  }
 }
 
 GpuEngine::~GpuEngine() {
   stop();
-  for (Lane& L : lanes_) {
+  for (Lane& L : lanes_)
     if (L.stream) hipStreamSynchronize(L.stream);
-    if (L.s_in) hipStreamSynchronize(L.s_in);
-    if (L.s_out) hipStreamSynchronize(L.s_out);
-  }
   for (auto& g : groups_) {
     if (g->ev) hipEventDestroy(g->ev);
     for (auto e : g->tev)
@@ -192,17 +164,8 @@ GpuEngine::~GpuEngine() {
   if (h_act_list_) hipHostFree(h_act_list_);
   if (h_code_list_p1_) hipHostFree(h_code_list_p1_);
   if (h_act_list_p1_) hipHostFree(h_act_list_p1_);
-  if (gate_) hipFree(gate_);
   for (Lane& L : lanes_) {
-    if (L.d_rows) hipFree(L.d_rows);
     if (L.opp_scratch) hipFree(L.opp_scratch);
-    for (int p = 0; p < 2; ++p) {
-      if (L.ev_h2d[p]) hipEventDestroy(L.ev_h2d[p]);
-      if (L.ev_done[p]) hipEventDestroy(L.ev_done[p]);
-      if (L.ev_d2h[p]) hipEventDestroy(L.ev_d2h[p]);
-    }
-    if (L.s_in) hipStreamDestroy(L.s_in);
-    if (L.s_out) hipStreamDestroy(L.s_out);
     if (L.stream) hipStreamDestroy(L.stream);
   }
 }
@@ -237,23 +200,10 @@ void GpuEngine::start(const std::vector<LaneGraphs>& graphs) {
     L.opp_graph = (hipGraphExec_t)g.opp;
     L.pack_graph[0] = (hipGraphExec_t)g.pack;
     L.pack_graph[1] = (hipGraphExec_t)g.opp_pack;
-    L.graph_b = (hipGraphExec_t)g.policy_b;
-    if (L.overlap && !L.graph_b)
-      throw std::runtime_error("GpuEngine::start: copy overlap needs the second policy graph");
   }
   running_.store(true);
   for (int w = 0; w < cfg_.n_threads; ++w) workers_.emplace_back(&GpuEngine::worker_loop, this, w);
   driver_ = std::thread(&GpuEngine::driver_loop, this);
-}
-
-void GpuEngine::set_group_graphs(const std::vector<uintptr_t>& graphs) {
-  if (running_.load()) throw std::runtime_error("set_group_graphs: engine running");
-  if (!graphs.empty() && (int)graphs.size() != cfg_.n_groups)
-    throw std::runtime_error("set_group_graphs: need one graph per group");
-  if (!graphs.empty() && cfg_.selfplay_groups > 0)
-    throw std::runtime_error("set_group_graphs: not with self-play groups");
-  group_graph_.clear();
-  for (uintptr_t h : graphs) group_graph_.push_back((hipGraphExec_t)h);
 }
 
 // pinned sparse rows for every env (both players' for self-play envs), filled with the reset
@@ -281,16 +231,14 @@ void GpuEngine::alloc_rows() {
 void GpuEngine::set_sparse_io(bool on) {
   if (running_.load()) throw std::runtime_error("set_sparse_io: engine running");
   if (!on) { sparse_ = false; return; }
-  if (act_mode()) return;  // the fused step decides itself (set_act_models)
-  if (!group_graph_.empty() || buf_.ep_return || buf_.ep_step)
-    throw std::runtime_error("set_sparse_io: not with zero-copy graphs or reference keys");
-  for (const Lane& L : lanes_)
-    if (L.overlap) throw std::runtime_error("set_sparse_io: not with copy overlap");
+  if (act_mode()) return;  // the fused step always runs on the sparse rows
+  if (buf_.ep_return || buf_.ep_step)
+    throw std::runtime_error("set_sparse_io: not with the reference buffer keys");
   alloc_rows();
   sparse_ = true;
 }
 
-void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy,
+void GpuEngine::set_act_models(const std::vector<MbkActModel>& models,
                                const std::vector<MbkActModel>& opp_models) {
   if (running_.load()) throw std::runtime_error("set_act_models: engine running");
   if (!models.empty() && (int)models.size() != cfg_.n_lanes)
@@ -298,9 +246,8 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
   if (!models.empty() && (buf_.ep_return || buf_.ep_step || buf_.last_action0 || buf_.logits))
     throw std::runtime_error("set_act_models: not with reference buffer keys");
   const bool sp_needed = !models.empty() && cfg_.selfplay_groups > 0;
-  if (sp_needed && ((int)opp_models.size() != cfg_.n_lanes || copy))
-    throw std::runtime_error("set_act_models: self-play needs one opponent block per lane and "
-                             "the sparse (zero-copy) rows");
+  if (sp_needed && (int)opp_models.size() != cfg_.n_lanes)
+    throw std::runtime_error("set_act_models: self-play needs one opponent block per lane");
   if (!sp_needed && !opp_models.empty())
     throw std::runtime_error("set_act_models: opponent blocks without self-play groups");
   for (const std::vector<MbkActModel>* v : {&models, &opp_models})
@@ -309,31 +256,15 @@ void GpuEngine::set_act_models(const std::vector<MbkActModel>& models, bool copy
         throw std::runtime_error("set_act_models: model block shape mismatch");
   act_models_ = models;
   opp_act_models_ = opp_models;
-  act_copy_ = copy;
-  // MBK_ACT_SPARSE=0: dense zero-copy codes / actions (4 + 4 MB of PCIe per 8192-env step
-  // instead of ~0.5-1 MB)
-  const char* sp = std::getenv("MBK_ACT_SPARSE");
-  const char* fm = std::getenv("MBK_ACT_FUSED_MAX");
-  act_fused_max_ = std::getenv("MBK_ACT_FUSED") ? -1.f : fm ? (float)std::atof(fm) : -1.f;
-  sparse_ = !models.empty() && !copy && !(sp && sp[0] == '0');
+  // sparse rows in / out of pinned host memory, read / written by the kernels themselves
+  // (dense codes / actions cost 4 + 4 MB of PCIe per 8192-env step instead of ~0.5-1 MB)
+  sparse_ = !models.empty();
   if (sparse_) alloc_rows();
   if (sp_needed) {
-    if (!sparse_) throw std::runtime_error("set_act_models: self-play needs MBK_ACT_SPARSE=1");
-    const size_t E = cfg_.envs_per_group, sc = E * S_ * (4 + 12 + 8) + 2 * E * 4 + 256 +
-                                                 E * list_stride_ * 4;
+    const size_t E = cfg_.envs_per_group, sc = E * S_ * (4 + 12 + 8) + 2 * E * 4 + 256;
     for (Lane& L : lanes_)
       if (!L.opp_scratch && hipMalloc((void**)&L.opp_scratch, sc) != hipSuccess)
         throw std::runtime_error("set_act_models: hipMalloc of the opponent scratch failed");
-  }
-  // MBK_ACT_ROWS_DEV=1: stage the rows into HBM with a small launch before launch A (off by
-  // default: it moves the PCIe time out of A -- 191 -> 172 + 30 us per 8192 envs -- and
-  // measured level on the bench, profiles/34)
-  const char* rd = std::getenv("MBK_ACT_ROWS_DEV");
-  if (sparse_ && rd && rd[0] == '1') {
-    const size_t bytes = (size_t)cfg_.envs_per_group * list_stride_ * 4;
-    for (Lane& L : lanes_)
-      if (!L.d_rows && hipMalloc((void**)&L.d_rows, bytes) != hipSuccess)
-        throw std::runtime_error("set_act_models: hipMalloc of the row staging failed");
   }
 }
 
@@ -344,22 +275,8 @@ void GpuEngine::stop() {
   if (driver_.joinable()) driver_.join();
   for (auto& t : workers_) if (t.joinable()) t.join();
   workers_.clear();
-  for (Lane& L : lanes_) {
+  for (Lane& L : lanes_)
     if (L.stream) hipStreamSynchronize(L.stream);
-    if (L.s_in) hipStreamSynchronize(L.s_in);
-    if (L.s_out) hipStreamSynchronize(L.s_out);
-  }
-  // an enqueue that failed between the gate's set and clear must not leave the learner's
-  // stream waiting forever. On a non-blocking stream: a plain hipMemset would queue on the
-  // null stream behind the very learner work that is waiting for the flag
-  if (gate_) {
-    hipStream_t s = nullptr;
-    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) == hipSuccess) {
-      (void)hipMemsetAsync(gate_, 0, sizeof(uint32_t), s);
-      (void)hipStreamSynchronize(s);
-      (void)hipStreamDestroy(s);
-    }
-  }
 }
 
 void GpuEngine::dispatch_env(int g) {
@@ -393,35 +310,7 @@ void GpuEngine::dispatch_env(int g) {
   work_cv_.notify_all();
 }
 
-// MBK_PIN_WORKERS=1: env worker w runs on the w-th CPU of the process's affinity set (the
-// rank's NUMA-local share, parallel/launch.py pin_rank), so the scheduler never migrates a
-// worker mid-group-step; the driver and Python keep the whole set
-static void pin_worker(int wid) {
-  static const bool on = [] {
-    const char* e = std::getenv("MBK_PIN_WORKERS");
-    return e && e[0] == '1';
-  }();
-  if (!on) return;
-  cpu_set_t all;
-  CPU_ZERO(&all);
-  if (sched_getaffinity(0, sizeof(all), &all) != 0) return;
-  const int n = CPU_COUNT(&all);
-  if (n < 2) return;
-  int k = wid % n;
-  for (int c = 0; c < CPU_SETSIZE; ++c) {
-    if (!CPU_ISSET(c, &all)) continue;
-    if (k-- == 0) {
-      cpu_set_t one;
-      CPU_ZERO(&one);
-      CPU_SET(c, &one);
-      (void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
-      return;
-    }
-  }
-}
-
 void GpuEngine::worker_loop(int wid) {
-  pin_worker(wid);
   const int E = cfg_.envs_per_group, NG = cfg_.n_groups;
   while (running_.load(std::memory_order_relaxed)) {
     const uint64_t epoch = work_epoch_.load();
@@ -509,7 +398,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       // not before the staging copy has executed: the learner's thread publishes as soon as
       // it has queued an update, and a stream wait here would hold this lane's policy steps
       // (every group on it) until that whole update is done; a later step applies it
-      if (ready_only_ && hipEventQuery(P.ready) == hipErrorNotReady) continue;
+      if (hipEventQuery(P.ready) == hipErrorNotReady) continue;
       ENG_CHECK(hipStreamWaitEvent(st, P.ready, 0));
       ENG_CHECK(hipMemcpyAsync((void*)P.dst[ln], P.staging, P.n, hipMemcpyDeviceToDevice,
                                st));
@@ -551,7 +440,7 @@ bool GpuEngine::enqueue_gpu(int g) {
       // on the host instead while the lane's other groups keep acting
       for (auto it = free_slots_.begin(); it != free_slots_.end(); ++it) {
         const int s = *it;
-        if (ready_only_ && release_pending_[s]) {
+        if (release_pending_[s]) {
           const hipError_t q = hipEventQuery(release_ev_[s]);
           if (q == hipErrorNotReady) continue;
           if (q == hipSuccess) release_pending_[s] = 0;
@@ -598,25 +487,12 @@ bool GpuEngine::enqueue_gpu(int g) {
     // fused acting step: 2 launches decode the codes, run the trunk, sample, and write the
     // rollout row (obs, mask, action, log-prob, value, previous reward / done) in place
     const MbkActModel& M = act_models_[G.lane];
-    const bool zc = !act_copy_;
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], st));
-    if (!zc) {
-      ENG_CHECK(hipMemcpyAsync((void*)io.in_codes, h_codes_ + e0 * S_, E * S_ * 2,
-                               hipMemcpyHostToDevice, st));
-      ENG_CHECK(hipMemcpyAsync((void*)io.in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, st));
-    }
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
     MbkActStep a{};
-    if (sparse_) {
-      a.code_list = h_code_list_ + e0 * list_stride_;
-      a.code_list_dev = L.d_rows;
-      a.act_list = h_act_list_ + e0 * list_stride_;
-      a.list_stride = list_stride_;
-    } else {
-      a.codes = zc ? h_codes_ + e0 * S_ : (const uint16_t*)io.in_codes;
-      a.res = zc ? h_res_ + e0 : (const int32_t*)io.in_res;
-      a.act16 = zc ? h_act16_ + e0 * S_ : (uint16_t*)io.out_act16;
-    }
+    a.code_list = h_code_list_ + e0 * list_stride_;
+    a.act_list = h_act_list_ + e0 * list_stride_;
+    a.list_stride = list_stride_;
     a.obs = (uint32_t*)obs_at(G.cur, t);
     a.mask = (uint32_t*)mask_at(G.cur, t);
     if (close_prev) {  // this row is also the previous slot's bootstrap row T
@@ -641,17 +517,8 @@ bool GpuEngine::enqueue_gpu(int g) {
       a.done_dst = (uint8_t*)u8_at(buf_.done, rs, ri);
     }
     a.step = L.act_step++;
-    if (sparse_) {
-      const int idle = G.idle.load(std::memory_order_relaxed);
-      act_active_cells_.fetch_add(idle, std::memory_order_relaxed);
-      // the in-tile head samples a tile's cells one unit per wave: cheapest while few cells
-      // are active, launch B's bucketed head wins above ~1.4 % (tools/active_sweep.py)
-      if (act_fused_max_ >= 0.f)
-        a.head_form = idle <= act_fused_max_ * (float)E * (float)S_ ? 1 : 2;
-    }
-    (mbk_act_step_fused(&a) ? act_fused_steps_ : act_b_steps_)
-        .fetch_add(1, std::memory_order_relaxed);
-    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
+    act_active_cells_.fetch_add(G.idle.load(std::memory_order_relaxed), std::memory_order_relaxed);
+    act_steps_.fetch_add(1, std::memory_order_relaxed);
     {
       const auto t0 = std::chrono::steady_clock::now();
       ENG_CHECK((hipError_t)mbk_act_step(&M, &a, st));
@@ -667,8 +534,6 @@ bool GpuEngine::enqueue_gpu(int g) {
         o.action = sc + ES * 16;
         o.logp = (float*)(sc + ES * 24);
         o.value = (float*)(sc + ES * 24 + E * 4);
-        o.code_list_dev = L.d_rows ? (uint32_t*)(sc + ES * 24 + 2 * E * 4 + 256) : nullptr;
-        o.head_form = a.head_form;
         o.step = L.opp_act_step++;
         ENG_CHECK((hipError_t)mbk_act_step(&opp_act_models_[G.lane], &o, st));
         G.opp_version = L.opp_version;
@@ -677,7 +542,6 @@ bool GpuEngine::enqueue_gpu(int g) {
                                std::chrono::steady_clock::now() - t0).count(),
                            std::memory_order_relaxed);
     }
-    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[2], st));
     if (close_prev) {
       ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
@@ -689,47 +553,25 @@ bool GpuEngine::enqueue_gpu(int g) {
       full_cv_.notify_all();
       G.prev = -1;
     }
-    if (!zc)
-      ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)io.out_act16, E * S_ * 2,
-                               hipMemcpyDeviceToHost, st));
     if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], st));
     ENG_CHECK(hipEventRecord(G.ev, st));
   } else {
-    // zero-copy step: the group's own graph reads its codes from / writes its actions to the
-    // pinned host staging (PCIe inside the decode / pack kernels: no SDMA commands, and no
-    // copy<->compute engine hand-offs on the lane)
-    hipGraphExec_t zc = group_graph_.empty() ? nullptr : group_graph_[g];
-    // copy overlap: this step's PCIe buffers (parity p) and the streams its copies run on
-    const int par = L.par;
-    const uintptr_t in_codes = (L.overlap && par) ? io.in_codes_b : io.in_codes;
-    const uintptr_t in_res = (L.overlap && par) ? io.in_res_b : io.in_res;
-    const uintptr_t out_act16 = (L.overlap && par) ? io.out_act16_b : io.out_act16;
-    hipStream_t s_in = L.overlap ? L.s_in : st;
-    if (L.overlap) {
-      // parity p's inputs were consumed by the step two back (its graph + scatter are done)
-      ENG_CHECK(hipStreamWaitEvent(s_in, L.ev_done[par], 0));
-    }
-    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], s_in));
+    // captured-graph step (other map sizes / agents, fp8 acting, the reference buffer keys)
+    const uintptr_t in_codes = io.in_codes, in_res = io.in_res, out_act16 = io.out_act16;
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[0], st));
     if (sparse_) {  // occupied-cell rows -> the graph's dense codes (no blit copy)
       ENG_CHECK((hipError_t)mbk_rows_to_codes(h_code_list_ + e0 * list_stride_, list_stride_,
                                               (int)E, S_, (void*)in_codes, (int32_t*)in_res,
-                                              s_in));
-    } else if (!zc) {
+                                              st));
+    } else {
       ENG_CHECK(hipMemcpyAsync((void*)in_codes, h_codes_ + e0 * S_, E * S_ * 2,
-                               hipMemcpyHostToDevice, s_in));
-      ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, s_in));
+                               hipMemcpyHostToDevice, st));
+      ENG_CHECK(hipMemcpyAsync((void*)in_res, h_res_ + e0, E * 4, hipMemcpyHostToDevice, st));
     }
-    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], s_in));
-    if (L.overlap) {
-      ENG_CHECK(hipEventRecord(L.ev_h2d[par], s_in));
-      ENG_CHECK(hipStreamWaitEvent(st, L.ev_h2d[par], 0));
-      ENG_CHECK(hipStreamWaitEvent(st, L.ev_d2h[par], 0));  // act16[p] copied out two steps back
-    }
-    // learner launches hold from here (the H2D above is SDMA: no CUs) to the scatter's end
-    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 1u, 0));
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[1], st));
     {
       const auto t0 = std::chrono::steady_clock::now();
-      ENG_CHECK(hipGraphLaunch(zc ? zc : (L.overlap && par) ? L.graph_b : L.graph, st));
+      ENG_CHECK(hipGraphLaunch(L.graph, st));
       launch_ns_.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
                                std::chrono::steady_clock::now() - t0).count(),
                            std::memory_order_relaxed);
@@ -782,14 +624,6 @@ bool GpuEngine::enqueue_gpu(int g) {
       seg[n++] = {(const void*)io.in_mask, mask_at(G.prev, T), E * S_ * 4 * kMaskWords};
     }
     ENG_CHECK((hipError_t)mbk_multi_copy(seg, n, st));
-    if (gate_) ENG_CHECK(hipStreamWriteValue32(st, gate_, 0u, 0));  // (the D2H is SDMA)
-    hipStream_t s_out = st;
-    if (L.overlap) {  // D2H on the copy-out stream once this step's graph + scatter are done
-      ENG_CHECK(hipEventRecord(L.ev_done[par], st));
-      s_out = L.s_out;
-      ENG_CHECK(hipStreamWaitEvent(s_out, L.ev_done[par], 0));
-      L.par ^= 1;
-    }
     if (close_prev) {
       ENG_CHECK(hipEventRecord(full_ev_[G.prev], st));
       {
@@ -803,22 +637,20 @@ bool GpuEngine::enqueue_gpu(int g) {
     if (sparse_) {  // packed actions -> the env workers' non-noop action rows
       ENG_CHECK((hipError_t)mbk_codes_to_rows((const void*)out_act16, (int)E, S_,
                                               h_act_list_ + e0 * list_stride_, list_stride_,
-                                              s_out));
+                                              st));
       if (G.selfplay)
         ENG_CHECK((hipError_t)mbk_codes_to_rows((const void*)io.out_act16_p1, (int)E, S_,
                                                 h_act_list_p1_ + e0 * list_stride_,
                                                 list_stride_, st));
     } else {
-      if (!zc)
-        ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
-                                 hipMemcpyDeviceToHost, s_out));
+      ENG_CHECK(hipMemcpyAsync(h_act16_ + e0 * S_, (const void*)out_act16, E * S_ * 2,
+                               hipMemcpyDeviceToHost, st));
       if (G.selfplay)
         ENG_CHECK(hipMemcpyAsync(h_act16_p1_ + e0 * S_, (const void*)io.out_act16_p1,
                                  E * S_ * 2, hipMemcpyDeviceToHost, st));
     }
-    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], s_out));
-    if (L.overlap) ENG_CHECK(hipEventRecord(L.ev_d2h[par], s_out));
-    ENG_CHECK(hipEventRecord(G.ev, s_out));
+    if (G.timed) ENG_CHECK(hipEventRecord(G.tev[3], st));
+    ENG_CHECK(hipEventRecord(G.ev, st));
   }
   gpu_steps_.fetch_add(1);
   G.t += 1;
@@ -969,8 +801,7 @@ EngineStats GpuEngine::stats() const {
   s.publishes = publishes_.load();
   s.opp_publishes = opp_publishes_.load();
   s.opp_version = opp_version_pub_.load();
-  s.act_fused_steps = act_fused_steps_.load();
-  s.act_b_steps = act_b_steps_.load();
+  s.act_steps = act_steps_.load();
   s.act_active_cells = act_active_cells_.load();
   std::lock_guard<std::mutex> l(stats_m_);
   s.driver_idle_s = driver_idle_s_;

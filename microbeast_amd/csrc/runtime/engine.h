@@ -62,15 +62,6 @@ struct EngineConfig {
   int device = 0;
   int selfplay_groups = 0;  // groups [n_groups - selfplay_groups, n_groups) are self-play
   int n_lanes = 1;          // concurrent policy streams (each with its own graph + I/O)
-  // >0: CU-partition the GPU: policy streams may only use CUs i with i % k == 0 (the
-  // learner takes the complement on its own masked stream), so persistent learner
-  // kernels and latency-critical policy kernels never compete for the same CUs
-  int policy_cu_every = 0;
-  // policy gate (one lane only): the lane stream sets a device flag to 1 for the span of
-  // each policy step's kernels (stream write-value packets) and the learner's stream waits
-  // for it to read 0 before each launch (mbk_stream_wait_zero), so a policy step never
-  // queues behind more than the one learner kernel already running
-  bool policy_gate = false;
   // >1: before the first policy step every env plays r ~ U[0, preroll) uniform-policy steps on
   // the CPU (VecEnv::preroll), so the envs start spread over the game's phases, not all at
   // their first frame (bench.py: the timed window then measures the steady state)
@@ -86,10 +77,6 @@ struct LaneIO {
   // opponent graph I/O (self-play groups only)
   uintptr_t in_codes_p1 = 0, in_res_p1 = 0, out_act16_p1 = 0;
   uintptr_t out_logits = 0;  // dense policy logits [E][78*S] f32 (reference keys only)
-  // copy overlap (no self-play): a second set of the PCIe-facing buffers, read / written by a
-  // second captured graph; steps alternate between the two sets so the H2D of the next step
-  // and the D2H of the last one run on copy streams while the lane computes
-  uintptr_t in_codes_b = 0, in_res_b = 0, out_act16_b = 0;
 };
 
 // Per-lane graphs (raw hipGraphExec_t). opp: opponent policy (self-play only); pack /
@@ -97,7 +84,6 @@ struct LaneIO {
 // derived inference weights so the policy graph itself never re-packs.
 struct LaneGraphs {
   uintptr_t policy = 0, opp = 0, pack = 0, opp_pack = 0;
-  uintptr_t policy_b = 0;  // copy overlap: the graph on the second buffer set (LaneIO *_b)
 };
 
 // Device buffers owned by Python (torch tensors); raw addresses.
@@ -142,9 +128,9 @@ struct EngineStats {
   int64_t publishes = 0;
   int64_t opp_publishes = 0;
   int opp_version = -1;
-  // fused acting step (act models set): steps whose head ran inside launch A / in launch B,
-  // and the agent's idle units (active cells) summed over the steps the engine chose for
-  int64_t act_fused_steps = 0, act_b_steps = 0, act_active_cells = 0;
+  // fused acting steps (act models set) and the agent's idle units (active cells: the cells
+  // the sparse head samples) summed over them
+  int64_t act_steps = 0, act_active_cells = 0;
   int64_t preroll_steps = 0;  // env steps played by EngineConfig::preroll before the start
 };
 
@@ -155,8 +141,6 @@ class GpuEngine {
   // one LaneGraphs per lane; the opponent graph is required iff selfplay_groups > 0
   void start(const std::vector<LaneGraphs>& graphs);
   void stop();
-  // device address of the policy gate flag (0: gating off)
-  uintptr_t gate_ptr() const { return (uintptr_t)gate_; }
   // Blocks until n full slots are available (or timeout). Returns slot ids.
   std::vector<int> get_full(int n, double timeout_s);
   void stream_wait_full(uintptr_t stream, int slot);
@@ -199,22 +183,17 @@ class GpuEngine {
   uintptr_t host_code_list() const { return (uintptr_t)h_code_list_; }
   uintptr_t host_act_list() const { return (uintptr_t)h_act_list_; }
   int list_stride() const { return list_stride_; }
-  // zero-copy policy steps: one captured graph per group that reads the group's codes /
-  // resources straight from pinned host memory and writes its packed actions there (no
-  // H2D / D2H copy commands on the lane); set before start(), 0 entries = copy path
-  void set_group_graphs(const std::vector<uintptr_t>& graphs);
   // fused acting steps (mbk_act_step: two kernel launches per step, writing the rollout row
-  // directly -- no policy graph, no scatter copy): one model / workspace block per lane, set
-  // before start(). copy: H2D / D2H the codes and actions through the lane's device buffers
-  // instead of reading / writing the pinned host staging from the kernels. opp_models: one
-  // block per lane of the self-play opponent's inference weights (required iff self-play
-  // groups exist; sparse rows only): its step reads the opponent's mirrored code rows and
-  // writes its action rows, its rollout-shaped outputs go to lane scratch.
-  void set_act_models(const std::vector<MbkActModel>& models, bool copy,
+  // directly -- no policy graph, no scatter copy -- from / to the env workers' pinned sparse
+  // rows): one model / workspace block per lane, set before start(). opp_models: one block per
+  // lane of the self-play opponent's inference weights (required iff self-play groups exist):
+  // its step reads the opponent's mirrored code rows and writes its action rows, its
+  // rollout-shaped outputs go to lane scratch.
+  void set_act_models(const std::vector<MbkActModel>& models,
                       const std::vector<MbkActModel>& opp_models = {});
   bool act_mode() const { return !act_models_.empty(); }
-  // captured-graph steps with sparse-row I/O (before start(); not with zero-copy graphs,
-  // copy overlap or reference keys): env workers write occupied-cell rows, one small launch
+  // captured-graph steps with sparse-row I/O (before start(); not with reference keys): env
+  // workers write occupied-cell rows, one small launch
   // expands them into the graph's device codes and another compacts its packed actions into
   // the workers' action rows -- no H2D / D2H blit copies of dense [S] code rows
   void set_sparse_io(bool on);
@@ -257,21 +236,11 @@ class GpuEngine {
   struct Lane {
     hipStream_t stream = nullptr;
     hipGraphExec_t graph = nullptr, opp_graph = nullptr;
-    // copy overlap (LaneIO *_b set): H2D / D2H copy streams, the parity of the next step and
-    // per parity: H2D landed, graph + scatter done (its inputs consumed, its act16 final),
-    // D2H done (its act16 buffer free again)
-    bool overlap = false;
-    hipGraphExec_t graph_b = nullptr;
-    hipStream_t s_in = nullptr, s_out = nullptr;
-    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
-    hipEvent_t ev_d2h[2] = {nullptr, nullptr};
-    int par = 0;
     hipGraphExec_t pack_graph[2] = {nullptr, nullptr};
     LaneIO io;
     int opp_version = -1;     // driver thread only
     int policy_version = 0;   // learner update of the weights landed on this lane
     uint64_t act_step = 0;    // fused steps: Philox step of the lane's next policy step
-    uint32_t* d_rows = nullptr;  // sparse steps: the HBM copy of a group's input rows
     // self-play opponent steps: HBM rows + scratch for the outputs the rollout does not keep
     // (obs [E][S] u32, mask [E][S][3] u32, action [E][S][7] u8, logp / value [E] f32)
     uint8_t* opp_scratch = nullptr;
@@ -305,12 +274,6 @@ class GpuEngine {
   std::vector<hipEvent_t> full_ev_, release_ev_;
   int64_t preroll_steps_ = 0;
   std::vector<uint8_t> release_pending_;  // per slot; guarded by slot_m_ (bytes, not bits)
-  // slots / weight publishes are taken only once their learner-stream events have executed
-  // (MBK_ENGINE_READY_ONLY=0: take them at once behind a stream wait, the old behaviour)
-  bool ready_only_ = [] {
-    const char* e = std::getenv("MBK_ENGINE_READY_ONLY");
-    return !(e && e[0] == '0');
-  }();
   std::vector<int> slot_version_;  // written when a group takes the slot (driver thread)
   std::deque<int> slot_wait_q_;  // driver thread only: groups waiting for a free slot
 
@@ -339,13 +302,7 @@ class GpuEngine {
   std::atomic<int64_t> gpu_phase_ns_{0}, env_phase_ns_{0}, enqueue_ns_{0}, launch_ns_{0};
   bool step_timing_ = false;
   std::atomic<int64_t> step_h2d_ns_{0}, step_graph_ns_{0}, step_out_ns_{0}, timed_steps_{0};
-  std::atomic<int64_t> act_fused_steps_{0}, act_b_steps_{0}, act_active_cells_{0};
-  // per-step head form of the fused acting step (sparse path), MBK_ACT_FUSED_MAX=f: head
-  // inside launch A while the group's active cells <= f * envs * cells, else launch B. Off by
-  // default (every step takes the process default, launch B): under the learner the B form
-  // measured level with or ahead of the in-A head even at 0.5 % active cells (profiles/34),
-  // and far ahead at 2-5 %; the in-A head wins only for acting alone at <~1.4 %.
-  float act_fused_max_ = -1.f;
+  std::atomic<int64_t> act_steps_{0}, act_active_cells_{0};
   double driver_idle_s_ = 0.0, slot_wait_s_ = 0.0;
   mutable std::mutex stats_m_;
 
@@ -356,13 +313,11 @@ class GpuEngine {
   void fail(const std::string& msg);
   void alloc_rows();
   int chunk_;
-  uint32_t* gate_ = nullptr;  // policy gate flag (device), see EngineConfig
-  std::vector<hipGraphExec_t> group_graph_;  // zero-copy graphs per group (may be empty)
   std::vector<MbkActModel> act_models_;      // fused acting steps per lane (may be empty)
   std::vector<MbkActModel> opp_act_models_;  // ... and the self-play opponent's
-  bool act_copy_ = false;
-  // sparse PCIe form of the fused zero-copy step (VecEnv::step_range_lists): pinned rows of
-  // list_stride_ uint32 per env, occupied-cell codes in, non-noop actions out
+  // sparse PCIe rows (VecEnv::step_range_lists): pinned rows of list_stride_ uint32 per env,
+  // occupied-cell codes in, non-noop actions out (the fused step and the graph path's
+  // set_sparse_io)
   bool sparse_ = false;
   int list_stride_ = 0;
   uint32_t* h_code_list_ = nullptr;

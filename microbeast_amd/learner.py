@@ -41,6 +41,7 @@ class LearnerHParams:
     max_grad_norm: float = 0.0  # reference: none
     bucket_mb: float = 8.0
     allreduce_dtype: str = "fp32"  # fp32 | bf16 (gradient all-reduce payload)
+    comm_rehearsal: bool = False   # world 1: stand-in collectives on a 4th stream (dist.py)
 
 
 class Learner:
@@ -55,7 +56,8 @@ class Learner:
         self.opt = FlatAdam(self.flat, lr=hp.lr, eps=hp.adam_eps, max_grad_norm=hp.max_grad_norm)
         self.reducer = GradAllReducer(
             self.flat, self.info, hp.bucket_mb,
-            torch.bfloat16 if hp.allreduce_dtype == "bf16" else torch.float32)
+            torch.bfloat16 if hp.allreduce_dtype == "bf16" else torch.float32,
+            rehearse=hp.comm_rehearsal)
         self.ws = VTraceWorkspace()
         self.n_updates = 0
         self.timing = {}

@@ -20,7 +20,6 @@ or the reference dense float (N, h, w, 27) layout.
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -37,13 +36,6 @@ from ..ops.tail import TailMaps, impala_tail
 HIP_CHANNELS = (16, 32)  # conv widths the HIP trunk kernels are instantiated for
 
 
-# network.5 + critic fused into the acting trunk kernel (trunk.hip, MBK_TRUNK_HEAD=1) vs the
-# separate fc.hip launch (default): measured 0.208 vs 0.200 ms per 8192-env policy step in
-# isolation and no gain under the learner (the fused variant spills 8 VGPRs)
-_TRUNK_HEAD = os.environ.get("MBK_TRUNK_HEAD", "0") == "1"
-# learner: the head's compaction (and the async read of its totals) before the trunk
-# (MBK_HEAD_PREP=0: inside the head's forward, after the trunk)
-_HEAD_PREP = os.environ.get("MBK_HEAD_PREP", "1") == "1"
 
 
 def layer_init(layer: nn.Module, std: float = math.sqrt(2), bias_const: float = 0.0) -> nn.Module:
@@ -186,12 +178,11 @@ class Agent(nn.Module):
         from .. import _native as N
         n = obs.shape[0] if obs.dim() == 2 else obs.numel() // (self.h * self.w)
         fc = self.network[len(self.channels) + 2]
-        head = None
-        if fc.out_features == 256 and not self._hip_enc.fp8 and _TRUNK_HEAD:  # in trunk_tail
-            head = (self._fc_cache["w5"], fc.bias, self.critic.weight, self.critic.bias)
+        # (network.5 + critic inside the trunk launch, mbk_trunk_tail_fc, measured 0.208 vs
+        # 0.200 ms per 8192-env step and no gain under the learner: the separate launch)
         y = encode(obs.reshape(n, self.h * self.w), self._hip_enc,
                    encoder_params(self.network, len(self.channels)), False, prepacked=True,
-                   head=head, value_out=value_out)
+                   value_out=value_out)
         if isinstance(y, tuple):
             return y
         I = y[0].numel()
@@ -355,8 +346,7 @@ class Agent(nn.Module):
             # its one host sync) goes first: it reads only masks / bitmap rows.
             n = obs.shape[0]
             ns = n if n_score is None else n_score
-            if _HEAD_PREP:
-                self._head(obs.device).prepare_scoring(mask_bits.reshape(ns, -1, 3), ns, abits)
+            self._head(obs.device).prepare_scoring(mask_bits.reshape(ns, -1, 3), ns, abits)
             y = self._trunk(obs)
             _, ho, wo, c = y.shape
             fc = self.network[len(self.channels) + 2]

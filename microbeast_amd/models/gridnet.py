@@ -12,7 +12,6 @@ times); logits of padding cells are dropped.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -49,7 +48,7 @@ class GridNetAgent(nn.Module):
         self.nvec = list(cell_head.NVEC) * (h * w)
         self.emulate = False      # run the grid path's torch emulation off-GPU (tests)
         # logits of the active cells only (compact rows) when acting / scoring; 0: dense
-        self.sparse_logits = os.environ.get("MBK_GRID_SPARSE", "1") == "1"
+        self.sparse_logits = True
         self._grid_plan = None
         for p in self.parameters():  # grid-path kernels write gradients into flat slots
             p._mbk_direct_grad = True

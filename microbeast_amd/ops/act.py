@@ -44,8 +44,8 @@ class MbkActStep(ctypes.Structure):
                 ("action", c_void_p), ("logp", c_void_p), ("value", c_void_p),
                 ("act16", c_void_p), ("act_list", c_void_p), ("list_stride", c_int),
                 ("reward_src", c_void_p), ("done_src", c_void_p), ("reward_dst", c_void_p),
-                ("done_dst", c_void_p), ("step", ctypes.c_uint64), ("head_form", c_int),
-                ("code_list_dev", c_void_p), ("abits", c_void_p), ("abits2", c_void_p)]
+                ("done_dst", c_void_p), ("step", ctypes.c_uint64), ("abits", c_void_p),
+                ("abits2", c_void_p)]
 
 
 def code_lists(codes: torch.Tensor, res: torch.Tensor, stride: int) -> torch.Tensor:
@@ -133,18 +133,14 @@ class ActWorkspace:
 
     def step(self, codes, res, obs, mask, action, logp, value, act16, obs2=None, mask2=None,
              reward=None, done=None, reward_dst=None, done_dst=None, code_list=None,
-             act_list=None, step: int | None = None, head_form: int = 0,
-             code_list_dev=None, abits=None, abits2=None) -> None:
+             act_list=None, step: int | None = None, abits=None, abits2=None) -> None:
         """One fused policy step on the current stream. codes int16 [E, S], res int32 [E]
         (or code_list int32 [E, stride] sparse rows, ``code_lists``); outputs obs int32 [E, S],
         mask int32 [E, S, 3], action uint8 [E, S, 7], logp / value fp32 [E], act16 int16
         [E, S] (or act_list int32 [E, stride] sparse rows); optional second obs / mask
         destination and the reward / done copy of the previous env step. step: the Philox
         step (default: the device counter rng[1], one host sync; the engine counts steps per
-        lane itself). head_form: 1 = head sampled inside launch A, 2 = launch B, 0 = the
-        process default (mbk_act_set_mode). code_list_dev: HBM scratch shaped like code_list
-        (pinned host rows are then staged into it by a small launch before launch A).
-        abits / abits2: int32 [E, S/32] active-cell bitmap rows to write (the learner's head
+        lane itself). abits / abits2: int32 [E, S/32] active-cell bitmap rows to write (the learner's head
         compaction input), abits2 with obs2."""
         s = MbkActStep()
         s.codes, s.res = N.ptr(codes), N.ptr(res)
@@ -158,8 +154,6 @@ class ActWorkspace:
         s.reward_src, s.done_src = N.ptr(reward), N.ptr(done)
         s.step = int(self.rng[1]) if step is None else int(step)
         s.reward_dst, s.done_dst = N.ptr(reward_dst), N.ptr(done_dst)
-        s.head_form = int(head_form)
-        s.code_list_dev = N.ptr(code_list_dev)
         s.abits, s.abits2 = N.ptr(abits), N.ptr(abits2)
         N.check(N.kernels().mbk_act_step(ctypes.addressof(self.struct), ctypes.addressof(s),
                                          N.stream_ptr()), "act_step")

@@ -14,7 +14,6 @@ inner conv output.
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 
 import torch
@@ -53,15 +52,15 @@ def _nch(c: int) -> int:
 
 _PF_FWD = 8 * 256    # conv_fwd register-prefetch capacity (elements per group)
 _PF_WGRAD = 4 * 256  # conv_wgrad prefetch capacity, X and dY each
-# conv_fwd workgroup sizing knobs (A/B via tools/microbench.py): LDS budget per workgroup
-# (48 KB = 3 workgroups per CU) and the target output pixels per image group
-_FWD_LDS = int(os.environ.get("MBK_CONV_LDS_KB", "48")) * 1024
-_FWD_PIX = int(os.environ.get("MBK_CONV_PIX", "512"))
+# conv_fwd workgroup sizing (tools/microbench.py sweeps): LDS budget per workgroup (48 KB =
+# 3 workgroups per CU) and the target output pixels per image group
+_FWD_LDS = 48 * 1024
+_FWD_PIX = 512
 # res_bwd32 round size: output pixels per round and the LDS budget (KB) of its four tiles
 # (maps of <= 2x2 pixels are mostly halo: their own budget)
-_RES32_PIX = int(os.environ.get("MBK_RES32_PIX", "256"))
-_RES32_LDS_KB = int(os.environ.get("MBK_RES32_LDS_KB", "100"))
-_RES32_LDS_KB_SMALL = int(os.environ.get("MBK_RES32_LDS_KB_SMALL", "150"))
+_RES32_PIX = 256
+_RES32_LDS_KB = 100
+_RES32_LDS_KB_SMALL = 150
 
 
 def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
@@ -78,11 +77,6 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
             break
         imgs //= 2
     return imgs
-
-
-def _at(t: torch.Tensor | None, i0: int) -> int | None:
-    """Device address of image i0 of an image-major tensor (None passes through)."""
-    return None if t is None else t[i0:].data_ptr()
 
 
 def _imgs_wgrad(layer: ConvLayer) -> int:
@@ -132,36 +126,26 @@ class HipEncoder:
         # reference (16, 32, 32) shape
         self.fused_tail = (tuple(channels) == (16, 32, 32) and self.layers[1].H <= 16
                            and self.layers[1].W <= 16)
-        # max-pool backward folded into the stage conv's wgrad / dgrad staging: saves the
-        # pre-pool gradient's HBM round trip but measured 6 % slower per update on MI355X
-        # (extra expand phase + a 1-wave/SIMD dgrad variant), so off by default
-        # MBK_FUSED_POOL_BWD: 0 (default) | 1 (every stage) | s<digits> (those stages, e.g. s0:
-        # stage 0 only, wgrad only -- the observation layer has no dgrad; s12: stages 1, 2)
-        _fp = os.environ.get("MBK_FUSED_POOL_BWD", "0")
-        self.fused_pool_bwd_stages = ({0, 1, 2, 3} if _fp == "1"
-                                      else {int(c) for c in _fp[1:]} if _fp.startswith("s")
-                                      else set())
-        self.fused_pool_bwd = bool(self.fused_pool_bwd_stages)
-        # 16-channel residual blocks (stage 0): one fused backward launch per block
-        # (resblock.hip) instead of wgrad1 / dgrad1 / wgrad0 / dgrad0 (MBK_FUSED_RES=0: off)
-        self.fused_res_bwd = os.environ.get("MBK_FUSED_RES", "1") == "1"
+        # Fused residual kernels (resblock.hip). Each flag selects the fused launch over the
+        # per-layer conv_fwd / conv_wgrad composition it is bit-identical to (forward) or
+        # checked against (backward); the per-layer path is what the parity tests compare
+        # with (tests/test_gpu_conv.py), not a tuning knob.
+        # 16-channel residual blocks (stage 0): one fused backward launch per block instead
+        # of wgrad1 / dgrad1 / wgrad0 / dgrad0
+        self.fused_res_bwd = True
         # 32-channel residual blocks (stages 1-2): one fused backward launch per block
-        self.fused_res_bwd32 = os.environ.get("MBK_FUSED_RES32", "1") == "1"
-        self.fused_res_fwd = os.environ.get("MBK_FUSED_RES_FWD", "1") == "1"
-        self.fused_res_fwd32 = os.environ.get("MBK_FUSED_RES_FWD32", "1") == "1"
-        # stage-0 residual kernel also runs stage 1's conv + pool (MBK_FUSED_STAGE_FWD=0: off)
-        self.fused_stage_fwd = os.environ.get("MBK_FUSED_STAGE_FWD", "1") == "1"
-        # learner launches over at most this many images each (0: one launch per layer): the
-        # persistent per-image kernels then hold the CUs for ~0.3 ms instead of 1-3 ms, so a
-        # policy step (high-priority stream, engine policy gate) waits less behind them
-        self.chunk = int(os.environ.get("MBK_LEARN_CHUNK", "0"))
+        self.fused_res_bwd32 = True
+        self.fused_res_fwd = True
+        self.fused_res_fwd32 = True
+        # the stage-0 residual kernel also runs stage 1's conv + pool
+        self.fused_stage_fwd = True
         self._partial_rb = None
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
         self.fp8 = fp8
-        # fp8 layers 1..14 in one fused launch (MBK_TRUNK8=0: the 14 per-layer fp8 launches)
-        self.fused_tail8 = os.environ.get("MBK_TRUNK8", "1") == "1"
+        # fp8 layers 1..14 in one fused launch (False: the 14 per-layer fp8 launches)
+        self.fused_tail8 = True
         self.packed_fwd8 = torch.zeros(off, dtype=torch.uint8, device=device)
         self.scale8 = torch.zeros(sum(L.cout for L in self.layers), dtype=torch.float32,
                                   device=device)
@@ -172,13 +156,6 @@ class HipEncoder:
             so += L.cout
 
     # ------------------------------------------------------------ helpers
-    def _spans(self, n: int) -> list[tuple[int, int]]:
-        """Image ranges of the launches a learner kernel over n images is split into."""
-        c = self.chunk
-        if c <= 0 or n <= c:
-            return [(0, n)]
-        return [(i, min(n, i + c)) for i in range(0, n, c)]
-
     def pack(self, weights: list[torch.Tensor], with_bwd: bool) -> None:
         k = N.kernels()
         for c0 in range(0, len(self.layers), 16):  # one launch packs up to 16 layers
@@ -230,16 +207,6 @@ class HipEncoder:
             x.data_ptr(), int(L.bits), L.cin, L.cout, self.packed_fwd8.data_ptr() + L.w_off,
             self.scale8.data_ptr() + 4 * self._s_off[i], N.ptr(bias), N.ptr(add), y.data_ptr(),
             n, L.H, L.W, imgs, int(L.relu_in), int(L.pool), N.stream_ptr()), "conv_fwd_fp8")
-        return y
-
-    def _dgrad_unpool(self, L: ConvLayer, dp: torch.Tensor, pidx: torch.Tensor) -> torch.Tensor:
-        """Input gradient of a pooled stage conv straight from the pooled gradient."""
-        n = dp.shape[0]
-        y = torch.empty(n, L.H, L.W, L.cin, dtype=torch.bfloat16, device=dp.device)
-        imgs = _imgs_fwd(L, L.cout, L.cin, False, False)
-        N.check(N.kernels().mbk_conv_dgrad_unpool(
-            dp.data_ptr(), pidx.data_ptr(), L.cout, L.cin, self.packed_bwd.data_ptr() + 2 * L.wb_off,
-            y.data_ptr(), n, L.H, L.W, imgs, N.stream_ptr()), "conv_dgrad_unpool")
         return y
 
     def _tail(self, p: torch.Tensor, bs: list[torch.Tensor], head=None, value_out=None):
@@ -299,23 +266,17 @@ class HipEncoder:
         Ho, Wo = ((H + 1) // 2, (W + 1) // 2) if pool else (H, W)
         y = torch.empty(n, Ho, Wo, cout, dtype=torch.bfloat16, device=x.device)
         imgs = _imgs_fwd(L, cin, cout, bits, pool)
-        k = N.kernels()
-        for i0, i1 in self._spans(n):
-            N.check(k.mbk_conv_fwd(
-                _at(x, i0), int(bits), cin, cout, w, N.ptr(bias), _at(add, i0),
-                _at(mask_src, i0), _at(y, i0), _at(y_full, i0), _at(pool_idx, i0), i1 - i0, H, W,
-                imgs, int(relu), int(pool), N.stream_ptr()),
-                "conv_fwd")
+        N.check(N.kernels().mbk_conv_fwd(
+            x.data_ptr(), int(bits), cin, cout, w, N.ptr(bias), N.ptr(add), N.ptr(mask_src),
+            y.data_ptr(), N.ptr(y_full), N.ptr(pool_idx), n, H, W, imgs, int(relu), int(pool),
+            N.stream_ptr()), "conv_fwd")
         return y
 
-    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor, dp=None, pidx=None):
-        """dy=None: pool-fused, dY is max_pool2d's backward of dp through the argmax pidx."""
+    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor):
         n = x.shape[0]
         imgs = _imgs_wgrad(L)
-        unpool = dy is None
         # persistent grid: as many workgroups as the device keeps resident (<= rounds)
-        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs,
-                                                  int(unpool))
+        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs)
         if nparts < 1:
             raise RuntimeError(f"conv_wgrad: unsupported shape {L}")
         row = L.cout * 9 * L.cin + L.cout
@@ -324,17 +285,11 @@ class HipEncoder:
             self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=x.device)
         k = N.kernels()
         st = N.stream_ptr()
-        for c, (i0, i1) in enumerate(self._spans(n)):
-            if c:
-                nparts = k.mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, i1 - i0, L.H, L.W,
-                                                imgs, int(unpool))
-            N.check(k.mbk_conv_wgrad(_at(x, i0), int(L.bits), L.cin, L.cout, _at(dy, i0),
-                                     _at(dp, i0), _at(pidx, i0), self._partial.data_ptr(), nparts,
-                                     i1 - i0, L.H, L.W, imgs, int(L.relu_in), st), "conv_wgrad")
-            # later chunks add their sums into the gradient (fp32)
-            N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real,
-                                       L.cout, dw.data_ptr(), db.data_ptr(), int(c > 0), st),
-                    "wgrad_reduce")
+        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, dy.data_ptr(),
+                                 self._partial.data_ptr(), nparts, n, L.H, L.W, imgs,
+                                 int(L.relu_in), st), "conv_wgrad")
+        N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
+                                   dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
 
     def _res_fwd16(self, li: int, p: torch.Tensor, bs: list[torch.Tensor], stage=None):
         """Both residual blocks of a 16-channel stage in one launch (resblock.hip): returns
@@ -348,24 +303,22 @@ class HipEncoder:
         bp = (ctypes.c_void_p * 4)(*[bs[li + 1 + j].data_ptr() for j in range(4)])
         k = N.kernels()
         if stage is None:
-            for i0, i1 in self._spans(n):
-                N.check(k.mbk_res_fwd16(_at(p, i0), *[_at(o, i0) for o in outs],
-                                        ctypes.cast(wp, ctypes.c_void_p),
-                                        ctypes.cast(bp, ctypes.c_void_p), i1 - i0, H, W, 4,
-                                        N.stream_ptr()), "res_fwd16")
+            N.check(k.mbk_res_fwd16(p.data_ptr(), *[o.data_ptr() for o in outs],
+                                    ctypes.cast(wp, ctypes.c_void_p),
+                                    ctypes.cast(bp, ctypes.c_void_p), n, H, W, 4,
+                                    N.stream_ptr()), "res_fwd16")
             return outs
         Ln = self.layers[li + 5]
         Ho, Wo = (H + 1) // 2, (W + 1) // 2
         pn = torch.empty(n, Ho, Wo, Ln.cout, dtype=torch.bfloat16, device=p.device)
         pidx = (torch.empty(n, Ho, Wo, Ln.cout, dtype=torch.uint8, device=p.device)
                 if stage else None)
-        for i0, i1 in self._spans(n):
-            N.check(k.mbk_res_fwd16_stage(_at(p, i0), *[_at(o, i0) for o in outs],
-                                          ctypes.cast(wp, ctypes.c_void_p),
-                                          ctypes.cast(bp, ctypes.c_void_p),
-                                          base + 2 * Ln.w_off, bs[li + 5].data_ptr(),
-                                          _at(pn, i0), _at(pidx, i0), i1 - i0, H, W, 4,
-                                          N.stream_ptr()), "res_fwd16_stage")
+        N.check(k.mbk_res_fwd16_stage(p.data_ptr(), *[o.data_ptr() for o in outs],
+                                      ctypes.cast(wp, ctypes.c_void_p),
+                                      ctypes.cast(bp, ctypes.c_void_p),
+                                      base + 2 * Ln.w_off, bs[li + 5].data_ptr(),
+                                      pn.data_ptr(), N.ptr(pidx), n, H, W, 4,
+                                      N.stream_ptr()), "res_fwd16_stage")
         return (*outs, (pn, pidx))
 
     def _res_blk32(self, l0: int, x: torch.Tensor, bs: list[torch.Tensor]):
@@ -377,11 +330,10 @@ class HipEncoder:
         wp = (ctypes.c_void_p * 2)(*[base + 2 * self.layers[l0 + j].w_off for j in range(2)])
         bp = (ctypes.c_void_p * 2)(*[bs[l0 + j].detach().data_ptr() for j in range(2)])
         imgs = max(1, min(16, (80 * 1024) // (2 * (H + 2) * (W + 2) * 80)))
-        for i0, i1 in self._spans(n):
-            N.check(N.kernels().mbk_res_blk32_fwd(_at(x, i0), _at(u, i0), _at(y, i0),
-                                                  ctypes.cast(wp, ctypes.c_void_p),
-                                                  ctypes.cast(bp, ctypes.c_void_p), i1 - i0, H, W,
-                                                  imgs, N.stream_ptr()), "res_blk32_fwd")
+        N.check(N.kernels().mbk_res_blk32_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(),
+                                              ctypes.cast(wp, ctypes.c_void_p),
+                                              ctypes.cast(bp, ctypes.c_void_p), n, H, W, imgs,
+                                              N.stream_ptr()), "res_blk32_fwd")
         return u, y
 
     def _res_bwd16(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
@@ -393,18 +345,17 @@ class HipEncoder:
         imgs = max(1, min(8, (80 * 1024) // (4 * (H + 2) * (W + 2) * 48)))
         dx = torch.empty_like(x)
         base = self.packed_bwd.data_ptr()
-        for c, (i0, i1) in enumerate(self._spans(n)):
-            nparts = k.mbk_res_bwd16_parts(i1 - i0, H, W, imgs)
-            if nparts < 1:
-                raise RuntimeError(f"res_bwd16: unsupported shape {H}x{W}")
-            need = k.mbk_res_bwd16_partial_floats(nparts)
-            if self._partial_rb is None or self._partial_rb.numel() < need:
-                self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
-            N.check(k.mbk_res_bwd16(_at(x, i0), _at(u, i0), _at(g, i0), _at(dx, i0),
-                                    base + 2 * L1.wb_off, base + 2 * L0.wb_off,
-                                    self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
-                                    db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), i1 - i0, H, W,
-                                    imgs, int(c > 0), N.stream_ptr()), "res_bwd16")
+        nparts = k.mbk_res_bwd16_parts(n, H, W, imgs)
+        if nparts < 1:
+            raise RuntimeError(f"res_bwd16: unsupported shape {H}x{W}")
+        need = k.mbk_res_bwd16_partial_floats(nparts)
+        if self._partial_rb is None or self._partial_rb.numel() < need:
+            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        N.check(k.mbk_res_bwd16(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
+                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
+                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs, 0,
+                                N.stream_ptr()), "res_bwd16")
         return dx
 
     def _res_bwd32(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
@@ -417,18 +368,17 @@ class HipEncoder:
         imgs = max(1, min(_RES32_PIX // (H * W), (lds_kb * 1024 - 128) // (4 * (H + 2) * (W + 2) * 80)))
         dx = torch.empty_like(x)
         base = self.packed_bwd.data_ptr()
-        for c, (i0, i1) in enumerate(self._spans(n)):
-            nparts = k.mbk_res_bwd32_parts(i1 - i0, H, W, imgs)
-            if nparts < 1:
-                raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")
-            need = k.mbk_res_bwd32_partial_floats(nparts)
-            if self._partial_rb is None or self._partial_rb.numel() < need:
-                self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
-            N.check(k.mbk_res_bwd32(_at(x, i0), _at(u, i0), _at(g, i0), _at(dx, i0),
-                                    base + 2 * L1.wb_off, base + 2 * L0.wb_off,
-                                    self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
-                                    db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), i1 - i0, H, W,
-                                    imgs, int(c > 0), N.stream_ptr()), "res_bwd32")
+        nparts = k.mbk_res_bwd32_parts(n, H, W, imgs)
+        if nparts < 1:
+            raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")
+        need = k.mbk_res_bwd32_partial_floats(nparts)
+        if self._partial_rb is None or self._partial_rb.numel() < need:
+            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        N.check(k.mbk_res_bwd32(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
+                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
+                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs, 0,
+                                N.stream_ptr()), "res_bwd32")
         return dx
 
     # ------------------------------------------------------------ passes
@@ -535,18 +485,11 @@ class HipEncoder:
                 dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
-            if self.fused_pool_bwd and s in self.fused_pool_bwd_stages:
-                # max_pool2d backward folded into both consumers' LDS staging: the
-                # pre-pool gradient is never materialised in HBM
-                self._wgrad(Ls, x, None, grads[2 * li], grads[2 * li + 1], dp=dp, pidx=pidx)
-                g = self._dgrad_unpool(Ls, dp, pidx) if s > 0 else None
-                continue
             dc = torch.empty(pidx.shape[0], Ls.H, Ls.W, Ls.cout, dtype=torch.bfloat16,
                              device=pidx.device)
-            for i0, i1 in self._spans(pidx.shape[0]):
-                N.check(N.kernels().mbk_pool_bwd_idx(_at(pidx, i0), _at(dp, i0), i1 - i0, Ls.H,
-                                                     Ls.W, Ls.cout, _at(dc, i0), N.stream_ptr()),
-                        "pool_bwd_idx")
+            N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dp.data_ptr(), pidx.shape[0],
+                                                 Ls.H, Ls.W, Ls.cout, dc.data_ptr(),
+                                                 N.stream_ptr()), "pool_bwd_idx")
             self._wgrad(Ls, x, dc, grads[2 * li], grads[2 * li + 1])
             g = self._fwd(Ls, dc, None, dgrad=True) if s > 0 else None
         return grads

@@ -12,7 +12,6 @@ per-cell recompute + dZ + dX_pair + dW_c (one workgroup per cell) -> dX gather.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -39,12 +38,12 @@ class SparseHead:
         # (no head_units launch); False: the separate head_units kernel (reference path)
         self.count_units = True
         # learner scoring on the backward's chunk tiles (mbk_head_score: W_c staged per cell
-        # run, one row per lane); MBK_HEAD_SCORE=0: head_fwd's 16-pair units (A/B reference)
-        self.score_tiles = os.environ.get("MBK_HEAD_SCORE", "1") != "0"
+        # run, one row per lane); False: head_fwd's 16-pair units (the tests' reference)
+        self.score_tiles = True
         # the scoring forward also writes per-pair softmax statistics (lse / entropy of each
         # segment) for the backward's per-logit epilogue; it then reads the pair / chunk totals
-        # (the one host sync of the head, otherwise taken by the backward). MBK_HEAD_STATS=0: off
-        self.score_stats = os.environ.get("MBK_HEAD_STATS", "1") != "0"
+        # (the one host sync of the head, otherwise taken by the backward). False: off (tests)
+        self.score_stats = True
         self.stats = None
         self._fwd_totals = None  # (P, nch) of the batch the statistics belong to
         self._prep = None        # (mask ptr, F, abits ptr, totals) of prepare_scoring

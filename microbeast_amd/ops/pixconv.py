@@ -34,7 +34,6 @@ the kernels against the emulation / fp32.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -423,16 +422,11 @@ def imgwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, M, gmap, out, H, x_relu=False, 
     return out
 
 
-_IMGCONV = os.environ.get("MBK_GRID_IMGCONV", "1") == "1"
-# first layer's weight gradient with the max-pool backward folded into its LDS staging
-# (no pre-pool gradient in HBM): measured 64.1 vs 55.4 ms per GridNet update (the plain-layout
-# unpool wgrad loses more than the 8.6 GB round trip saves), so off by default
-_E1_UNPOOL = os.environ.get("MBK_GRID_E1_UNPOOL", "0") == "1"
 
 
 def _imgconv_ok(L, dev) -> bool:
     """the image-tile kernel covers GridNet's 8x8 32 -> 64 conv (forward and input gradient)"""
-    return (_IMGCONV and dev.type == "cuda" and L.H == 8 and L.W == 8 and L.cin == 32
+    return (dev.type == "cuda" and L.H == 8 and L.W == 8 and L.cin == 32
             and L.cout == 64)
 
 
@@ -537,15 +531,12 @@ def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_r
     return out
 
 
-_WGRAD_ALL = os.environ.get("MBK_PWGRAD_ALL", "1") == "1"
-
-
 def _wgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L, ntap, M, out, x_relu=False, bias_out=None):
     """weight gradient of a dense layer: the all-taps form for the 3x3 convs (~7.6 pairs per
     output pixel share one staged g row; it also yields the bias gradient), the per-tap form
     for the transposed convs and the critic (1-4 pairs per output pixel: nothing to share,
     measured 2x slower all-taps). ``bias_out`` (with g as [pixels][M][O] rows): sum of g."""
-    if _WGRAD_ALL and ntap <= 9 and L.mean_pairs >= 4.0:
+    if ntap <= 9 and L.mean_pairs >= 4.0:
         return pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, L.tf, ntap, M, L.gmap, out,
                           x_relu=x_relu, bias_out=bias_out)
     if bias_out is not None:
@@ -845,8 +836,8 @@ class PixPlan:
         # band-layout wgrad) when it is the 32-channel layer those kernels implement
         self.enc0 = None
         c0 = convs[0]
-        if (self.device.type == "cuda" and c0.weight.shape[0] == 32 and c0.weight.shape[1] <= 32
-                and os.environ.get("MBK_GRID_E1_CONV", "1") == "1"):
+        if (self.device.type == "cuda" and c0.weight.shape[0] == 32
+                and c0.weight.shape[1] <= 32):
             from .encoder import HipEncoder
             self.enc0 = HipEncoder(ph, pw, c0.weight.shape[1], channels=(32,), device=dev)
 
@@ -1039,11 +1030,7 @@ class _GridNetPBC(torch.autograd.Function):
             if i == 0 and plan.enc0 is not None and ctx.acts[0] is None:
                 # conv.hip first layer: g1 is its (relu-masked) NHWC pooled gradient
                 L0 = plan.enc0.layers[0]
-                p, pidx = pooled, idx
-                if _E1_UNPOOL:   # max-pool backward folded into the wgrad's LDS staging
-                    plan.enc0._wgrad(L0, ctx.saved["bits_pad"], None, pg(0), pg(1), dp=g1,
-                                     pidx=pidx)
-                    break
+                pidx = idx
                 dc = torch.empty(n, L0.H, L0.W, L0.cout, dtype=_BF, device=dev)
                 k = _N().kernels()
                 _N().check(k.mbk_pool_bwd_idx(pidx.data_ptr(), g1.data_ptr(), n, L0.H, L0.W,

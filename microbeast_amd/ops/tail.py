@@ -18,7 +18,6 @@ first ``n_score`` rows of f. Backward:
 """
 from __future__ import annotations
 
-import os
 
 import torch
 
@@ -27,10 +26,9 @@ from .pixconv import colsum, map_gather, value_bwd
 from .optim import grad_out
 
 _BF = torch.bfloat16
-# MBK_FUSED_DX_VALUE=0: separate head_dx_gather + value_bwd launches (A/B, tests)
-_FUSED_DX_VALUE = os.environ.get("MBK_FUSED_DX_VALUE", "1") == "1"
-# dW5 + db5 in one pass (fc_wgrad_wide_kernel); MBK_FC_WIDE=0: fc_wgrad chunks + colsum
-_FC_WIDE = os.environ.get("MBK_FC_WIDE", "1") == "1"
+# head_dx_gather + value_bwd in one launch (False: the two separate launches, which the
+# parity test compares against)
+_FUSED_DX_VALUE = True
 
 
 def nhwc_linear_maps(k1: int, c: int, hh: int, ww: int):
@@ -127,7 +125,7 @@ class _ImpalaTail(torch.autograd.Function):
                                    O, I, 0, 1, y2.data_ptr(), st), "gemm_nt_mask")
         dw5 = torch.empty(O, I, dtype=torch.float32, device=dev)
         gb5 = grad_out(b5)
-        wparts = k.mbk_fc_wgrad_wide_parts(n, O, I) if _FC_WIDE else 0
+        wparts = k.mbk_fc_wgrad_wide_parts(n, O, I)
         if wparts > 0:  # dW5 and db5 in one pass over dh / y2 (fc.hip fc_wgrad_wide_kernel)
             scratch = torch.empty((wparts + (wparts + 31) // 32) * (O * I + O),
                                   dtype=torch.float32, device=dev)

@@ -104,14 +104,30 @@ def broadcast_flat(flat: FlatParams, info: DistInfo) -> None:
         dist.broadcast(flat.data, src=0)
 
 
+# world-1 rehearsal of the hook-fired collectives (bench.py --comm_rehearsal): per bucket a
+# stand-in kernel on a separate high-priority stream, RCCL-like grid (one workgroup per
+# channel) and roughly a ring all-reduce's HBM bytes (2 read-modify-write sweeps of the bucket)
+REHEARSAL_CHANNELS = 32
+REHEARSAL_PASSES = 2
+
+
 class GradAllReducer:
     """Bucketed, backward-overlapped gradient all-reduce over a FlatParams grad."""
 
     def __init__(self, flat: FlatParams, info: DistInfo, bucket_mb: float = 8.0,
-                 comm_dtype: torch.dtype = torch.float32):
+                 comm_dtype: torch.dtype = torch.float32, rehearse: bool = False):
         """comm_dtype=bfloat16 all-reduces a bf16 copy of each bucket (half the xGMI bytes);
-        the result is written back into the fp32 gradient buffer (fp32 master grads)."""
+        the result is written back into the fp32 gradient buffer (fp32 master grads).
+        rehearse (world size 1, no process group, GPU): the same buckets fire from the same
+        hooks, but each launches ``mbk_comm_standin`` on a 4th, high-priority stream in place
+        of RCCL's all-reduce, and ``finish`` makes the learner's stream wait for it as it
+        waits for RCCL -- so a 1-GPU kernel trace shows whether the policy lanes or the
+        learner serialize behind a collective's stream (docs/DESIGN.md §6). The gradient
+        itself is never written."""
         self.flat, self.info = flat, info
+        self.rehearse = bool(rehearse) and not info.enabled and flat.grad.is_cuda
+        self.side = None      # rehearsal stream
+        self.scratch = None   # rehearsal payload (the stand-in's accumulator)
         self.comm_dtype = comm_dtype
         self.grad_scale = 1.0 / max(1, info.world_size)  # applied inside Adam
         self.comm = None  # persistent low-precision payload (comm_dtype != fp32)
@@ -120,8 +136,11 @@ class GradAllReducer:
         self.works = []
         self.pending: list[int] = []
         self.fired: list[bool] = []
-        if not info.enabled:
+        if not info.enabled and not self.rehearse:
             return
+        if self.rehearse:
+            self.side = torch.cuda.Stream(flat.grad.device, priority=-1)
+            self.scratch = torch.zeros(flat.numel, dtype=torch.float32, device=flat.grad.device)
         limit = int(bucket_mb * 1e6 / 4)
         # walk parameters from last to first (backward order), cutting buckets
         cur_end, cur_start, members, groups = None, None, [], []
@@ -162,6 +181,14 @@ class GradAllReducer:
         s, e = self.buckets[b]
         self.fired[b] = True
         g = self.flat.grad[s:e]
+        if self.rehearse:
+            from .. import _native as N
+            self.side.wait_stream(torch.cuda.current_stream())
+            # (bucket starts are multiples of 4 floats: FlatParams pads every slice)
+            N.check(N.kernels().mbk_comm_standin(g.data_ptr(), self.scratch[s:e].data_ptr(),
+                                                 e - s, REHEARSAL_PASSES, REHEARSAL_CHANNELS,
+                                                 self.side.cuda_stream), "comm_standin")
+            return
         if self.comm is not None:
             c = self.comm[s:e]
             if g.is_cuda and c.dtype == torch.bfloat16:  # native narrowing copy (no ATen)
@@ -174,7 +201,7 @@ class GradAllReducer:
         self.works.append(dist.all_reduce(g, op=dist.ReduceOp.SUM, async_op=True))
 
     def start_step(self):
-        if self.info.enabled:
+        if self.info.enabled or self.rehearse:
             self.count = [0] * len(self.buckets)
             self.fired = [False] * len(self.buckets)
             self.works = []
@@ -183,11 +210,14 @@ class GradAllReducer:
         """Launch any bucket whose params got no gradient and make the current stream wait
         for all of them (no host sync). The gradient is left as the SUM over ranks: the
         optimizer applies ``grad_scale`` (1/world) in its own pass."""
-        if not self.info.enabled:
+        if not self.info.enabled and not self.rehearse:
             return
         for b in range(len(self.buckets)):
             if not self.fired[b]:
                 self._launch(b)
+        if self.rehearse:
+            torch.cuda.current_stream().wait_stream(self.side)
+            return
         for w in self.works:
             w.wait()
         self.works = []

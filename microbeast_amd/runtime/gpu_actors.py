@@ -59,17 +59,6 @@ class EngineFailure(RuntimeError):
     process is intact and may rebuild the actor side (train.py)."""
 
 
-class _HostView:
-    """A raw device-addressable host pointer where the policy step expects a tensor (only
-    ``data_ptr()`` is used): the engine's pinned staging for zero-copy graphs."""
-
-    def __init__(self, ptr: int):
-        self._ptr = int(ptr)
-
-    def data_ptr(self) -> int:
-        return self._ptr
-
-
 def graph_policy_step(io: dict, m, rng: torch.Tensor, E: int, size: int, device) -> None:
     """The captured graph's policy step (6 launches for the flat agent: decode + bucket, stage-0
     conv, trunk, network.5 + critic, head, finale) on fixed-address I/O ``io`` (``make_io``).
@@ -146,16 +135,18 @@ class GpuActorRuntime:
                  n_slots: int | None = None, max_steps: int = 2000, seed: int = 1,
                  bots=DEFAULT_BOTS, reward_weight=(10.0, 1.0, 1.0, 0.2, 1.0, 4.0),
                  env_index_base: int = 0, selfplay_groups: int = 0, fp8_policy: bool = False,
-                 n_lanes: int | None = None, policy_cu_every: int = 0,
+                 n_lanes: int | None = None,
                  reference_keys: bool = False, policy_logits: bool = False,
-                 policy_gate: bool | None = None, preroll: int = 0):
+                 preroll: int = 0, fused_act: bool | None = None):
         """preroll > 1: every env first plays r ~ U[0, preroll) steps of the uniform
         random-init policy on the CPU (engine.h EngineConfig::preroll), so the run starts from
         envs spread over the game's phases rather than all at their first frame.
         reference_keys: also emit the reference buffer keys ep_return / ep_step /
         last_action (libs/utils.py:34-46) into the slots; policy_logits: plus the dense
         78*h*w policy logits of every step (the sparse acting head never needs them, so
-        this adds one dense head GEMM per policy step and 312*h*w bytes per frame)."""
+        this adds one dense head GEMM per policy step and 312*h*w bytes per frame).
+        fused_act: None picks the fused acting step whenever ops/act.py supports the model
+        shape; False forces the captured-graph step (the tests compare the two)."""
         rt = N.runtime()
         self.device = device
         self.size, self.S = size, size * size
@@ -195,10 +186,6 @@ class GpuActorRuntime:
         self.n_lanes = max(1, min(n_groups, n_lanes if n_lanes is not None else 1))
         self.fp8_policy = fp8_policy
         self.selfplay_groups = int(selfplay_groups)
-        # double-buffered PCIe I/O with H2D / D2H on copy streams (MBK_COPY_OVERLAP=0: off;
-        # self-play lanes keep the single-stream step)
-        self.copy_overlap = (os.environ.get("MBK_COPY_OVERLAP", "0") == "1"
-                             and self.selfplay_groups == 0)
         self.lanes = []
         for ln in range(self.n_lanes):
             lane = {"io": self._make_io(),
@@ -211,15 +198,6 @@ class GpuActorRuntime:
             lane["flat"] = FlatParams(lane["model"], dev)
             lane["pack_graph"] = self._capture_pack(lane["model"])
             lane["graph"] = self._capture(lane["io"], lane["model"], lane["rng"])
-            if self.copy_overlap:
-                # second set of the PCIe-facing buffers + its own graph (engine.h LaneIO *_b):
-                # the engine alternates steps between the two so the next step's H2D and the
-                # last one's D2H run on copy streams while the lane computes
-                io_b = dict(lane["io"])
-                for k in ("in_codes", "in_res", "out_act16"):
-                    io_b[k] = torch.zeros_like(lane["io"][k])
-                lane["io_b"] = io_b
-                lane["graph_b"] = self._capture(io_b, lane["model"], lane["rng"])
             if self.selfplay_groups > 0:
                 lane["io_p1"] = self._make_io()
                 lane["rng_p1"] = torch.tensor(
@@ -240,11 +218,6 @@ class GpuActorRuntime:
         self.opp_graph = l0.get("opp_graph")
         if self.selfplay_groups > 0:
             self.opp_flat, self.opp_model = l0["opp_flat"], l0["opp_model"]
-        # policy gate (engine.h EngineConfig::policy_gate): learner launches wait while a
-        # policy step's kernels are in flight (one lane only; MBK_POLICY_GATE=0/1)
-        if policy_gate is None:
-            policy_gate = os.environ.get("MBK_POLICY_GATE", "0") == "1"
-        self.policy_gate = bool(policy_gate) and self.n_lanes == 1
         if n_threads is None:
             n_threads = max(1, min(32, available_cpus() - 1))
         self.n_threads = n_threads
@@ -254,15 +227,11 @@ class GpuActorRuntime:
                    reward_weight=list(reward_weight), env_index_base=env_index_base,
                    device=dev.index if dev.index is not None else torch.cuda.current_device(),
                    selfplay_groups=self.selfplay_groups, n_lanes=self.n_lanes,
-                   policy_cu_every=int(policy_cu_every), policy_gate=self.policy_gate,
                    preroll=int(preroll))
         bufs = {k: v.data_ptr() for k, v in self.rb.items()}
         bufs["lanes"] = []
         for lane in self.lanes:
             d = {k: v.data_ptr() for k, v in lane["io"].items()}
-            if self.copy_overlap:
-                d.update({k + "_b": lane["io_b"][k].data_ptr()
-                          for k in ("in_codes", "in_res", "out_act16")})
             if self.selfplay_groups > 0:
                 d.update({"in_codes_p1": lane["io_p1"]["in_codes"].data_ptr(),
                           "in_res_p1": lane["io_p1"]["in_res"].data_ptr(),
@@ -273,15 +242,14 @@ class GpuActorRuntime:
         # fused acting steps (ops/act.py): 2 launches per policy step that write the rollout
         # row in place, instead of the captured 6-launch graph + scatter copy. Headline agent
         # shape (16x16, bf16 trunk), self-play groups included (the opponent's step runs the
-        # same launches on its mirrored rows with its own weights); MBK_FUSED_ACT=0 keeps the
-        # graph path, MBK_ACT_COPY=1 moves codes / actions through device buffers with H2D /
-        # D2H copies (not with self-play)
-        act_copy = os.environ.get("MBK_ACT_COPY", "0") == "1"
-        self.fused_act = (os.environ.get("MBK_FUSED_ACT", "1") == "1"
-                          and not self.reference_keys and not self.copy_overlap
-                          and not (self.selfplay_groups > 0 and act_copy)
+        # same launches on its mirrored rows with its own weights). The kernels read the
+        # occupied-cell rows from / write the action rows to the engine's pinned host staging
+        self.fused_act = (fused_act is not False and not self.reference_keys
                           and all(act_ops.supported(ln["model"], size, fp8_policy)
                                   for ln in self.lanes))
+        if fused_act and not self.fused_act:
+            raise ValueError("fused_act=True: the fused acting step does not cover this model "
+                             "/ map size / dtype or the reference buffer keys")
         if self.fused_act:
             for lane in self.lanes:
                 lane["act"] = act_ops.ActWorkspace(lane["model"], E, lane["rng"], dev)
@@ -289,36 +257,14 @@ class GpuActorRuntime:
                     lane["opp_act"] = act_ops.ActWorkspace(lane["opp_model"], E,
                                                            lane["rng_p1"], dev)
             torch.cuda.synchronize()
-            self.engine.set_act_models([ln["act"].block() for ln in self.lanes], act_copy,
+            self.engine.set_act_models([ln["act"].block() for ln in self.lanes],
                                        [ln["opp_act"].block() for ln in self.lanes
                                         if "opp_act" in ln])
-        # zero-copy policy steps (engine.h set_group_graphs): one graph per group whose decode
-        # reads the group's codes / resources from the engine's pinned host staging and whose
-        # pack writes its actions there (MBK_ZERO_COPY=1; self-play keeps the copy path)
-        self.zero_copy = (os.environ.get("MBK_ZERO_COPY", "0") == "1"
-                          and self.selfplay_groups == 0 and not self.fused_act)
-        if self.zero_copy:
-            hc, hr, ha = (self.engine.host_codes(), self.engine.host_res(),
-                          self.engine.host_act16())
-            gg = []
-            for g in range(n_groups):
-                lane = self.lanes[g % self.n_lanes]
-                e0 = g * E
-                io_g = dict(lane["io"])
-                io_g["in_codes"] = _HostView(hc + e0 * self.S * 2)
-                io_g["in_res"] = _HostView(hr + e0 * 4)
-                io_g["out_act16"] = _HostView(ha + e0 * self.S * 2)
-                lane.setdefault("group_graphs", []).append(
-                    self._capture(io_g, lane["model"], lane["rng"]))
-                gg.append(lane["group_graphs"][-1])
-            self.engine.set_group_graphs([int(x.raw_cuda_graph_exec()) for x in gg])
-        # captured-graph steps (shapes the fused step does not cover, self-play with
-        # MBK_FUSED_ACT=0, GridNet): sparse occupied-cell rows in / non-noop action rows out
-        # through two small launches instead of H2D / D2H blit copies of dense code rows
-        # (MBK_GRAPH_SPARSE=0: the dense copies)
-        self.sparse_io = (not self.fused_act and not self.zero_copy and not self.copy_overlap
-                          and not self.reference_keys
-                          and os.environ.get("MBK_GRAPH_SPARSE", "1") == "1")
+        # captured-graph steps (shapes the fused step does not cover, fp8 acting, GridNet):
+        # sparse occupied-cell rows in / non-noop action rows out through two small launches
+        # instead of H2D / D2H blit copies of dense code rows (the reference buffer keys keep
+        # the dense copies: their last_action / logits rows are dense)
+        self.sparse_io = not self.fused_act and not self.reference_keys
         if self.sparse_io:
             self.engine.set_sparse_io(True)
         if not self.fused_act and "abits" in self.rb:
@@ -386,15 +332,12 @@ class GpuActorRuntime:
         torch.cuda.synchronize()
         ex = lambda g: int(g.raw_cuda_graph_exec()) if g is not None else 0  # noqa: E731
         self.engine.start([[ex(ln["graph"]), ex(ln.get("opp_graph")), ex(ln["pack_graph"]),
-                            ex(ln.get("opp_pack_graph")), ex(ln.get("graph_b"))]
+                            ex(ln.get("opp_pack_graph"))]
                            for ln in self.lanes])
         self.started = True
-        if self.policy_gate:  # every policy graph is captured: gate the learner's launches
-            N.set_policy_gate(self.engine.gate_ptr())
 
     def stop(self):
         if self.started:
-            N.set_policy_gate(None)
             self.engine.stop()
             self.started = False
 

@@ -49,28 +49,12 @@ def _model(cuda, seed):
     return m
 
 
-# launch-A forms (mbk_act_set_mode): wave-owned kernel with the head fused in (ONE launch per
-# step), wave-owned + head launch B (the default), phase-split kernel + head launch B, and
-# the engine's per-step choice (MbkActStep.head_form, switching between fused and B: the
-# bucket counters' double buffer must stay consistent across switches)
-MODES = {"fused": (1, 1), "wave+B": (1, 0), "phase+B": (0, 0), "mixed": (1, 1)}
-MIXED = [1, 2, 2, 1, 1, 2]  # head_form per step, cycled
-
-
-@pytest.fixture(params=list(MODES))
-def act_mode(request, cuda):
-    k = N.kernels()
-    got = k.mbk_act_set_mode(*MODES[request.param])
-    assert got == MODES[request.param][0] * 2 + MODES[request.param][1]
-    yield request.param
-    k.mbk_act_set_mode(-1, -1)
-
-
 @pytest.mark.parametrize("E,sparse", [(96, False), (520, False), (200, True)])
-def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
-    """sparse: the PCIe-light form the engine uses (occupied-cell code rows in, non-noop action
-    rows out) must give the same step as the dense codes / dense packed actions. Every launch-A
-    form (act_mode) gives the same bits."""
+def test_fused_act_step_bit_identical(cuda, E, sparse):
+    """The fused step (launch A: decode + trunk + critic, launch B: sparse head) is
+    bit-identical to the captured-graph step. sparse: the PCIe-light form the engine uses
+    (occupied-cell code rows in, non-noop action rows out) must give the same step as the
+    dense codes / dense packed actions."""
     from microbeast_amd.ops.act import ActWorkspace, code_lists, dense_actions
     from microbeast_amd.runtime.gpu_actors import graph_policy_step, make_io
 
@@ -93,27 +77,22 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
     done = (torch.rand(E, device=cuda) < 0.3).to(torch.uint8)
     rdst, ddst = torch.zeros_like(reward), torch.zeros_like(done)
     n_active = 0
-    rows_dev = torch.empty(E, S + 4, dtype=torch.int32, device=cuda)  # row staging scratch
     abits = torch.full((E, S // 32), -1, dtype=torch.int32, device=cuda)
     abits2 = torch.full_like(abits, -1)
     for i, (codes, res) in enumerate(_codes_stream(E, 24, seed=E)):
-        form = MIXED[i % len(MIXED)] if act_mode == "mixed" else 0
         io["in_codes"].copy_(codes)
         io["in_res"].copy_(res)
         graph_policy_step(io, m, rng_a, E, 16, cuda)
         second = i % 3 == 0
         if sparse:
-            # odd steps: rows in pinned host memory staged to HBM by the row launch (the
-            # engine's form); even steps: rows already in HBM
-            staged = i % 2 == 1
+            # odd steps: rows in pinned host memory, read by launch A over PCIe (the engine's
+            # form); even steps: rows already in HBM
             cl = code_lists(codes, res, stride)
-            cl = cl.pin_memory() if staged else cl.to(cuda)
+            cl = cl.pin_memory() if i % 2 == 1 else cl.to(cuda)
             ws.step(None, None, obs, mask, action, logp, value, None,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
                     reward=reward, done=done, reward_dst=rdst, done_dst=ddst, code_list=cl,
-                    act_list=act_list, head_form=form,
-                    code_list_dev=rows_dev if staged else None, abits=abits,
-                    abits2=abits2 if second else None)
+                    act_list=act_list, abits=abits, abits2=abits2 if second else None)
             torch.cuda.synchronize()
             act16 = dense_actions(act_list, S).to(cuda)
             al = act_list.cpu().to(torch.int64) & 0xFFFFFFFF
@@ -122,7 +101,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
         else:
             ws.step(io["in_codes"], io["in_res"], obs, mask, action, logp, value, act16,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
-                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst, head_form=form,
+                    reward=reward, done=done, reward_dst=rdst, done_dst=ddst,
                     abits=abits, abits2=abits2 if second else None)
         torch.cuda.synchronize()
         assert torch.equal(obs, io["in_obs"]), f"obs planes differ at step {i}"
@@ -144,8 +123,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
         assert torch.equal(rdst, reward) and torch.equal(ddst, done)
         # between steps the previous step's bucket counters are back at zero (double buffer)
         par = (7 + i) % 2  # this step's Philox step is 7 + i
-        fused = act_mode == "fused" or form == 1  # (one launch: no bucket counters at all)
-        assert (int(ws.bucket_cnt[par * 256:(par + 1) * 256].abs().sum()) > 0) != fused
+        assert int(ws.bucket_cnt[par * 256:(par + 1) * 256].abs().sum()) > 0
         if i > 0:
             assert int(ws.bucket_cnt[(1 - par) * 256:(2 - par) * 256].abs().sum()) == 0
         assert int(ws.pending[:E].abs().sum()) == 0
@@ -154,7 +132,7 @@ def test_fused_act_step_bit_identical(cuda, E, sparse, act_mode):
     assert int(rng_b[1]) == 7 + 24
 
 
-def test_engine_fused_act_learns(cuda, monkeypatch):
+def test_engine_fused_act_learns(cuda):
     """The engine's fused step form on a 16x16 map: rollout rows written in place are aligned
     (legal actions under the mask of the same row), learn / publish work, two lanes."""
     from microbeast_amd.learner import Learner, LearnerHParams
@@ -163,7 +141,6 @@ def test_engine_fused_act_learns(cuda, monkeypatch):
     from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
 
     s, T, E = 16, 8, 64
-    monkeypatch.setenv("MBK_FUSED_ACT", "1")
 
     def mk():
         return Agent((s, s, 27))
@@ -197,8 +174,7 @@ def test_engine_fused_act_learns(cuda, monkeypatch):
             assert torch.isfinite(losses).all()
         st = rt.stats()
         assert st["frames"] > 0 and st["gpu_steps"] > 0 and st["publishes"] >= 1
-        # the per-step head form (sparse rows: engine-picked from the env workers' counts)
-        assert st["act_fused_steps"] + st["act_b_steps"] > 0
+        assert st["act_steps"] > 0
         assert st["act_active_cells"] > 0
     finally:
         rt.stop()
@@ -243,19 +219,16 @@ def test_graph_sparse_row_io(cuda, size):
         assert torch.equal(out[e, :1 + int(n[e])], ref[e, :1 + int(n[e])])
 
 
-@pytest.mark.parametrize("sparse", ["1", "0"])
-def test_engine_fused_act_logp_tracks_published_weights(cuda, monkeypatch, sparse):
+def test_engine_fused_act_logp_tracks_published_weights(cuda):
     """After publishes, a rollout acted with the fused step under version v carries behaviour
     log-probs equal to what the learner scores with the weights of version v (the step reads
     packed weights through pointers captured once; a publish that missed a buffer would leave
-    the actors on stale weights), for sparse and dense zero-copy rows."""
+    the actors on stale weights)."""
     from microbeast_amd.learner import Learner, LearnerHParams
     from microbeast_amd.models.agent import Agent
     from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
 
     s, T, E = 16, 8, 64
-    monkeypatch.setenv("MBK_FUSED_ACT", "1")
-    monkeypatch.setenv("MBK_ACT_SPARSE", sparse)
 
     def mk():
         return Agent((s, s, 27))

@@ -93,3 +93,31 @@ def test_rccl_world1_bit_identical(cuda, batch, comm):
         assert _gather_episodes(recs, info) == recs  # gloo host group
     finally:
         D.destroy(info)
+
+
+def test_comm_rehearsal_fires_from_hooks_and_leaves_update_identical(cuda, batch):
+    """bench.py --comm_rehearsal (world 1, no process group): every bucket's stand-in
+    collective launches from a grad hook on the 4th (high-priority) stream while backward
+    runs, the learner's stream waits for it, and the update stays bit-identical (the stand-in
+    never writes the gradient)."""
+    from microbeast_amd.learner import Learner, LearnerHParams
+    ref = _run(cuda, batch)
+    torch.manual_seed(123)
+    L = Learner(_mk(), LearnerHParams(bucket_mb=0.25, comm_rehearsal=True), cuda)
+    red = L.reducer
+    assert red.rehearse and red.side is not None and len(red.buckets) >= 3
+    assert red.side.priority < torch.cuda.current_stream().priority
+    fired_before_finish = []
+    orig = red.finish
+
+    def finish():
+        fired_before_finish.append(list(red.fired))
+        orig()
+    red.finish = finish
+    for b in batch[:2]:
+        L.learn(b)
+    torch.cuda.synchronize()
+    assert all(all(f) for f in fired_before_finish)
+    assert float(red.scratch.abs().sum()) > 0  # the stand-in ran over the gradient
+    assert torch.equal(L.flat.data, ref.flat.data)
+    assert torch.equal(L.opt.m, ref.opt.m) and torch.equal(L.opt.v, ref.opt.v)

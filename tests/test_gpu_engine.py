@@ -7,18 +7,16 @@ from microbeast_amd.ops.cell_head import OFFS, unpack_mask
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("variant", ["lanes2", "zero_copy", "copy_overlap", "policy_gate"])
-def test_engine_rollout_alignment_and_learn(cuda, variant, monkeypatch):
-    """Slot alignment / action legality / learn / publish through every engine step form:
-    two lanes; zero-copy group graphs (codes and actions through pinned host memory); double-
-    buffered I/O on copy streams; the policy gate (learner launches wait on the step flag)."""
+@pytest.mark.parametrize("variant", ["lanes1", "lanes2", "reference_keys"])
+def test_engine_rollout_alignment_and_learn(cuda, variant):
+    """Slot alignment / action legality / learn / publish through the captured-graph step
+    forms: one and two lanes on the sparse row I/O; the reference buffer keys (dense code /
+    action copies: their last_action rows are dense)."""
     from microbeast_amd.learner import Learner, LearnerHParams
     from microbeast_amd.models.agent import Agent
     from microbeast_amd.runtime.gpu_actors import GpuActorRuntime
 
     s, T = 8, 8
-    monkeypatch.setenv("MBK_ZERO_COPY", "1" if variant == "zero_copy" else "0")
-    monkeypatch.setenv("MBK_COPY_OVERLAP", "1" if variant == "copy_overlap" else "0")
     lanes = 2 if variant == "lanes2" else 1
 
     def mk():
@@ -28,10 +26,9 @@ def test_engine_rollout_alignment_and_learn(cuda, variant, monkeypatch):
     learner = Learner(mk(), LearnerHParams(), cuda)
     rt = GpuActorRuntime(mk, s, n_groups=2, envs_per_group=16, unroll=T, batch_slots=1,
                          device=cuda, n_threads=2, n_lanes=lanes,
-                         policy_gate=variant == "policy_gate")
-    assert rt.zero_copy == (variant == "zero_copy")
-    assert rt.copy_overlap == (variant == "copy_overlap")
-    assert rt.policy_gate == (variant == "policy_gate")
+                         reference_keys=variant == "reference_keys")
+    assert not rt.fused_act  # 8x8: the captured-graph step
+    assert rt.sparse_io == (variant != "reference_keys")
     rt.start(learner.flat)
     try:
         prev_last_obs = {}

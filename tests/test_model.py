@@ -60,22 +60,3 @@ def test_gridnet_shapes():
     m10 = GridNetAgent((10, 10, 27), compute_dtype=torch.float32)
     logits, v = m10.policy_value(torch.randint(0, 2**26, (2, 100), dtype=torch.int32))
     assert logits.shape == (2, 100 * 78)
-
-
-def test_learn_chunk_spans_partition_the_batch():
-    """HipEncoder._spans (MBK_LEARN_CHUNK image ranges) covers [0, n) exactly, in order, with
-    only the last range short; _at addresses image i0 of an image-major tensor."""
-    from microbeast_amd.ops.encoder import HipEncoder, _at
-    enc = HipEncoder.__new__(HipEncoder)  # geometry-free: _spans only reads .chunk
-    for chunk, n in ((0, 37), (8, 37), (8, 32), (64, 37), (1, 5)):
-        enc.chunk = chunk
-        sp = enc._spans(n)
-        assert sp[0][0] == 0 and sp[-1][1] == n
-        assert all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
-        if chunk > 0:
-            assert all(i1 - i0 == chunk for i0, i1 in sp[:-1]) and 0 < sp[-1][1] - sp[-1][0] <= chunk
-        else:
-            assert sp == [(0, n)]
-    t = torch.zeros(10, 4, 4, 16, dtype=torch.bfloat16)
-    assert _at(t, 3) == t.data_ptr() + 3 * 4 * 4 * 16 * 2
-    assert _at(None, 3) is None

@@ -19,15 +19,11 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-# stamp intervals of wave 0's first tile. MBK_ACT_WAVE=1 (default, act_trunk_w_kernel): its own
-# 2 envs through the trunk, then the tile-wide end (bucket reservation, FC + critic, entries);
-# MBK_ACT_WAVE=0 (act_trunk_kernel): the workgroup-wide phases (stamps 0-8)
-PHASES_PHASE = ["P1 codes->LDS", "P2 decode", "P3 buckets+conv0", "stage 0 res", "stage 1",
-                "stage 2", "fc + critic", "-"]
+# stamp intervals of wave 0's first tile (act_trunk_w_kernel): its own 2 envs through the
+# trunk, then the tile-wide end (bucket reservation, FC + critic, bucket entries)
 PHASES_WAVE = (["rows + codes", "decode", "conv0 + pool + halos"]
                + [("pool + halos + " if l in (5, 10) else "") + f"conv {l}" for l in range(14)]
-               + ["(trunk end)", "barrier 1 wait",
-                  "FC + head units + finale (MBK_ACT_FUSED=0: bucket entries)"])
+               + ["(trunk end)", "barrier 1 wait", "FC + critic + bucket entries"])
 
 
 def main():
@@ -36,8 +32,6 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warm", type=int, default=30, help="env steps before sampling codes")
     p.add_argument("--device_rows", action="store_true", help="sparse rows in HBM, not pinned")
-    p.add_argument("--staged", action="store_true",
-                   help="pinned rows staged into HBM by the row launch (the engine's form)")
     a = p.parse_args()
     from microbeast_amd import _native as N
     from microbeast_amd.models.agent import Agent
@@ -87,9 +81,6 @@ def main():
     al = torch.zeros(E, stride, dtype=torch.int32).pin_memory()
     st = MbkActStep()
     st.code_list, st.act_list, st.list_stride = rows.data_ptr(), al.data_ptr(), stride
-    if a.staged:
-        rows_dev = torch.empty_like(rows, device=dev)
-        st.code_list_dev = rows_dev.data_ptr()
     st.obs, st.mask, st.action, st.logp, st.value = (o.data_ptr(), mk.data_ptr(), act.data_ptr(),
                                                      lp.data_ptr(), v.data_ptr())
     k = N.kernels()
@@ -110,8 +101,7 @@ def main():
     n = a.steps
     print(f"launch A (decode + trunk + critic) {1e3 * ta / n:.1f} us, launch B (head + finale) "
           f"{1e3 * tb / n:.1f} us, rows in "
-          f"{'HBM' if a.device_rows else 'pinned host memory'}"
-          f"{' (staged into HBM by the row launch, included in A)' if a.staged else ''}")
+          f"{'HBM' if a.device_rows else 'pinned host memory'}")
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     stamps = torch.zeros(ncu * 4 * 32 * 64, dtype=torch.int64, device=dev)
     nst = k.mbk_act_set_stamps(stamps.data_ptr())
@@ -119,8 +109,7 @@ def main():
     N.check(k.mbk_act_trunk(*args, N.stream_ptr()), "act_trunk (stamped)")
     torch.cuda.synchronize()
     k.mbk_act_set_stamps(None)
-    wave = os.environ.get("MBK_ACT_WAVE", "1") != "0"
-    names = PHASES_WAVE if wave else PHASES_PHASE
+    names = PHASES_WAVE
     nb = stamps.numel() // (nst * 64)
     t = stamps[:nb * nst * 64].view(nb, nst, 64)[:, :, 0].cpu().double()
     t = t[t[:, 0] > 0][:, :len(names) + 1]

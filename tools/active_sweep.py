@@ -6,7 +6,7 @@ The headline bench runs random-init weights, whose uniform policy keeps ~0.5 % o
 on 16x16; a trained policy builds more units (the r3b1L CLI run averaged 10.96 M frames/s
 against the bench's ~14 M). This tool prices both sides at 0.5 / 2 / 5 % active cells:
 
-* GPU: the policy step (ops/act.py, mbk_act_step, every launch form of mbk_act_set_mode) on
+* GPU: the policy step (ops/act.py, mbk_act_step, launch A + launch B) on
   E envs of real simulator codes with extra own idle workers dropped on empty cells until each
   env has the target number of active cells (the step's decode recomputes the masks from the
   codes, so the head samples exactly those cells);
@@ -96,24 +96,21 @@ def gpu_sweep(E: int, fracs, steps: int) -> list[dict]:
                                                          act.data_ptr(), lp.data_ptr(),
                                                          v.data_ptr())
         args = (ctypes.addressof(ws.struct), ctypes.addressof(st))
-        for mode, (wave, fused) in {"fused": (1, 1), "wave+B": (1, 0), "phase+B": (0, 0)}.items():
-            k.mbk_act_set_mode(wave, fused)
-            ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-            tot = 0.0
-            for i in range(steps + 3):
-                st.step = i
-                ev[0].record()
-                N.check(k.mbk_act_step(*args, N.stream_ptr()), "act_step")
-                ev[1].record()
-                torch.cuda.synchronize()
-                if i >= 3:
-                    tot += ev[0].elapsed_time(ev[1])
-            active = float((mk != 0).any(-1).float().mean())
-            out.append({"what": "policy_step", "mode": mode, "target_active": f,
-                        "active_frac": round(active, 4), "us_per_step": round(1e3 * tot / steps, 1),
-                        "E": E})
-            print(json.dumps(out[-1]), flush=True)
-    k.mbk_act_set_mode(-1, -1)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        tot = 0.0
+        for i in range(steps + 3):
+            st.step = i
+            ev[0].record()
+            N.check(k.mbk_act_step(*args, N.stream_ptr()), "act_step")
+            ev[1].record()
+            torch.cuda.synchronize()
+            if i >= 3:
+                tot += ev[0].elapsed_time(ev[1])
+        active = float((mk != 0).any(-1).float().mean())
+        out.append({"what": "policy_step", "target_active": f,
+                    "active_frac": round(active, 4), "us_per_step": round(1e3 * tot / steps, 1),
+                    "E": E})
+        print(json.dumps(out[-1]), flush=True)
     return out
 
 

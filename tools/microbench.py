@@ -27,9 +27,6 @@ def main():
                    help="also run the policy step eagerly (no graph) so rocprof sees its kernels")
     p.add_argument("--fp8", action="store_true", help="policy step on the fp8 acting trunk")
     p.add_argument("--no_learner", action="store_true", help="policy step timings only")
-    p.add_argument("--variants", type=str, default="",
-                   help="comma list of encoder toggles to A/B in the same process: "
-                        "fusedpool, nofusedpool")
     a = p.parse_args()
     import torch
 
@@ -96,10 +93,7 @@ def main():
                  "logp": torch.zeros(T + 1, B, device=dev), "reward": rew.to(dev),
                  "done": done.to(dev)}
         active = int((mask.view(-1, 3) != 0).any(-1).sum())
-        for variant in [""] + [v for v in a.variants.split(",") if v]:
-            enc = learner.model._hip_enc
-            if enc is not None and variant in ("fusedpool", "nofusedpool"):
-                enc.fused_pool_bwd = variant == "fusedpool"
+        for variant in [""]:
             for _ in range(3):
                 learner.learn(batch)
             torch.cuda.synchronize()
