@@ -5,7 +5,7 @@ usage: python tools/timeline.py <rocprof_out_dir> [window_frac]
 
 Splits the steady-state window (last ``window_frac`` of the span) by hardware queue: the
 policy queue is the one running ``trunk_tail`` / ``act_trunk`` kernels, everything else with kernels is
-"learner". A policy step starts at its ``decode_obs_mask`` (graph step), ``act_rows`` or ``act_trunk`` (fused step)
+"learner". A policy step starts at its ``decode_obs_mask`` (graph step) or ``act_trunk`` (fused step)
 kernel. Reports per-step stream
 time inside vs outside learner activity, per-queue busy and idle time, and the union.
 """
@@ -65,10 +65,7 @@ def main():
     lea_busy = sum(e - s for s, e in merge([(s, e) for s, e, _, _ in lea]))
     pol_busy = sum(e - s for s, e in merge([(s, e) for s, e, _, _ in pol]))
     all_busy = sum(e - s for s, e in merge([(s, e) for s, e, _, _ in rows]))
-    # (a fused step with staged rows starts at its act_rows launch, right before act_trunk)
-    starts = [i for i, r in enumerate(pol)
-              if "decode_obs_mask" in r[3] or "act_rows" in r[3]
-              or ("act_trunk" in r[3] and not (i > 0 and "act_rows" in pol[i - 1][3]))]
+    starts = [i for i, r in enumerate(pol) if "decode_obs_mask" in r[3] or "act_trunk" in r[3]]
     steps = []
     for a, b in zip(starts, starts[1:]):
         s = pol[a][0]
