@@ -80,9 +80,13 @@ _SIGS = {
                          c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "mbk_conv_pack_fp8": [c_void_p, c_int, c_void_p],
     "mbk_pool_bwd_idx": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
-    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
-                       c_int, c_int, c_int, c_void_p],
-    "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+    "mbk_conv_wgrad": [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                       c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mbk_conv_wgrad_parts": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+    "mbk_pool_conv_bwd_parts": [c_int, c_int, c_int, c_int, c_int],
+    "mbk_pool_conv_bwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                          c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mbk_pool_conv_bwd_partial_floats": [c_int],
     "mbk_conv_set_grid_cap": [c_int],
     "mbk_conv0_row_set": [c_int],
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],
@@ -173,7 +177,8 @@ _SIGS = {
     "mbk_gemm_nt_mask": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                          c_int, c_int, c_int, c_void_p, c_void_p],
 }
-_RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64, "mbk_res_bwd32_partial_floats": c_int64}
+_RESTYPE = {"mbk_res_bwd16_partial_floats": c_int64, "mbk_res_bwd32_partial_floats": c_int64,
+            "mbk_pool_conv_bwd_partial_floats": c_int64}
 
 
 def _ensure_built() -> None:

@@ -696,6 +696,9 @@ struct ConvWgradArgs {
   const bf16* dy;
   float* partial;  // [gridDim.x][COUT*9*CIN + COUT]
   int N, H, W, imgs, relu_in;
+  // UNPOOL: dY is the max-pool backward of dp through the stored argmax bytes pidx
+  const bf16* dp;       // [N][Ho][Wo][COUT]
+  const uint8_t* pidx;  // [N][Ho][Wo][COUT]
 };
 
 __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
@@ -740,7 +743,12 @@ inline int wg_band_w(int H, int W) {
 // Both GEMM operands come from NHWC LDS tiles through ds_read_b64_tr_b16 (band layout
 // above when WT > 0); the next round's X interior and dY are prefetched into registers
 // during the MFMAs.
-template <int CIN, int COUT, bool BITS, int WT = 0>
+// UNPOOL (the stage-0 layer of a 16-wide map: its dY is the pool backward of the next
+// layer's input gradient): each round stages the pooled gradient and argmax bytes (3 of the
+// 8 KB per image a materialised dY costs) and scatters them into the zeroed band-layout dY
+// tile (one wave per image, four window-parity phases), so the full-resolution dY never
+// touches HBM and no pool_bwd_idx launch runs.
+template <int CIN, int COUT, bool BITS, int WT = 0, bool UNPOOL = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int XPB = CIN * 2;       // X tile pixel stride (bytes), NHWC bf16
@@ -774,6 +782,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   if constexpr (BITS)
     for (int e = tid; e < 256; e += kThreads) lut[e] = expand_bits8((uint32_t)e);
   const int xper = a.imgs * HW * XEPP, dper = a.imgs * HW * DCH;
+  // UNPOOL scatter lanes (wave w = channels 4w .. 4w + 3, see the round): lane = (image of
+  // the round, window k of a parity phase, channel pair)
+  constexpr int WO2 = WT / 2;
+  const int s_im = lane >> 5, s_k = (lane >> 1) & 15, s_c0 = 4 * wave + 2 * (lane & 1);
   int xoff[kPFW];
 #pragma unroll
   for (int k = 0; k < kPFW; ++k) {
@@ -804,6 +816,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   // twice the bytes are in flight (the tile loads are HBM-latency bound at one round ahead)
   struct PF {
     uint4 px[kPFW], pd[kPFW];
+    uint32_t sd[UNPOOL ? 4 : 1], si[UNPOOL ? 4 : 1];  // UNPOOL: the lane's 4 phases' dp / argmax
     uint32_t pb[kPFW];
   };
   PF pf0, pf1;
@@ -818,7 +831,18 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
       const int e = tid + k * kThreads;
       if (BITS) pb[k] = e < xl ? ((const uint32_t*)a.x)[xb + e] : 0u;
       else px[k] = e < xl ? ((const uint4*)a.x)[xb + e] : make_uint4(0, 0, 0, 0);
-      pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
+      if constexpr (!UNPOOL) pd[k] = e < dl ? ((const uint4*)a.dy)[db + e] : make_uint4(0, 0, 0, 0);
+    }
+    if constexpr (UNPOOL) {
+      const bool ok = s_im < nimg;
+      const size_t img = (size_t)rd * a.imgs + (ok ? s_im : 0);
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int oy = 2 * (s_k >> 2) + (ph >> 1), ox = 2 * (s_k & 3) + (ph & 1);
+        const size_t o = (img * WO2 * WO2 + oy * WO2 + ox) * COUT + s_c0;
+        f.sd[ph] = ok ? *(const uint32_t*)(a.dp + o) : 0u;
+        f.si[ph] = ok ? *(const uint16_t*)(a.pidx + o) : 0u;
+      }
     }
   };
   auto put_x = [&](int off, uint4 v) {
@@ -869,14 +893,50 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         if (BITS) put_bits(xoff[k], pb[k]);
         else put_x(xoff[k], px[k]);
       }
-      if (e < dl) put_d(e, pd[k]);
+      if constexpr (!UNPOOL)
+        if (e < dl) put_d(e, pd[k]);
     }
     for (int e = tid + kPFW * kThreads; e < xl; e += kThreads) {
       if (BITS) put_bits(xoff_of(e), ((const uint32_t*)a.x)[(size_t)rd * xper + e]);
       else put_x(xoff_of(e), ((const uint4*)a.x)[(size_t)rd * xper + e]);
     }
-    for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
-      put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
+    if constexpr (UNPOOL) {
+      // scatter, wave w taking channels 4w .. 4w + 3 of every image of the round from its
+      // lanes' prefetched registers: no two waves touch one element and a wave's LDS ops
+      // complete in issue order, so neither the zeroing of its channel slice nor the 4 phases
+      // need a barrier. Phase ph = the 16 windows of parity (oy % 2, ox % 2) = (ph / 2, ph % 2),
+      // which never overlap; each element gets dY[pixel][c] += dp (bf16 storage, fp32 add: a
+      // pixel 2 windows chose sees one extra bf16 rounding against pool_bwd_idx's fp32 sum)
+      static_assert(!UNPOOL || (band && WT == 16 && COUT == 16 && kThreads == 256),
+                    "16-wide stage-0 layout, 4 waves x 4 channels");
+      for (int p = lane; p < nimg * HW; p += 64) {  // this wave's 8 bytes of every pixel
+        const int im = p / HW, r = p % HW;
+        *(uint2*)(dt + im * IMGD + (r / WT) * RBD + (r % WT) * DPB + 8 * wave) = make_uint2(0, 0);
+      }
+      asm volatile("" ::: "memory");
+      if (s_im < nimg) {
+        char* dimg = dt + s_im * IMGD;
+#pragma unroll
+        for (int ph = 0; ph < 4; ++ph) {
+          const int oy = 2 * (s_k >> 2) + (ph >> 1), ox = 2 * (s_k & 3) + (ph & 1);
+          const uint32_t d2 = f.sd[ph], i2 = f.si[ph];
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int t = (int)((i2 >> (8 * j)) & 0xFFu);
+            const int ky = (t * 11) >> 5, kx = t - 3 * ky;  // t / 3 for t < 9
+            const int py = 2 * oy - 1 + ky, px = 2 * ox - 1 + kx;
+            uint16_t* el = (uint16_t*)(dimg + py * RBD + px * DPB + (s_c0 + j) * 2);
+            const float add = __uint_as_float(j ? (d2 & 0xFFFF0000u) : (d2 << 16));
+            const float v = __uint_as_float((uint32_t)*el << 16) + add;
+            *el = __bfloat16_as_ushort(f2bf(v));
+          }
+          asm volatile("" ::: "memory");
+        }
+      }
+    } else {
+      for (int e = tid + kPFW * kThreads; e < dl; e += kThreads)
+        put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
+    }
     __syncthreads();
     if (rd + 2 * gstep < nrounds) prefetch(rd + 2 * gstep, f);
 
@@ -1261,7 +1321,8 @@ inline size_t fwd_smem(int cin, bool bits, int imgs, int H, int W, int cout, boo
   return t;
 }
 
-inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W) {
+inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool = false) {
+  (void)unpool;  // (the pool-fused form keeps its pooled operands in registers)
   size_t t = wg_tile_bytes(cin, cout, imgs, H, W, wg_band_w(H, W));
   t += 4096;  // bit-plane lookup table (allocated for every variant: keeps the sizing simple)
   size_t red = (size_t)cout * 9 * cin * 4;
@@ -1392,9 +1453,14 @@ extern "C" int mbk_conv_fwd_fp8(const void* x, int in_bits, int cin, int cout, c
   else return -(int)hipErrorInvalidValue;
 
 // the wgrad instantiation of (CI, CO, B) for this map width: band layout (WT = 8 / 16 / 24)
-// or the plain one
+// or the plain one; unpool: the stage-0 layer of a 16-wide map only (null otherwise)
 template <int CI, int CO, bool B>
-const void* wgrad_kfn(int H, int W) {
+const void* wgrad_kfn(int H, int W, bool unpool = false) {
+  if (unpool) {
+    if constexpr (CI == 32 && CO == 16 && B)
+      if (wg_band_w(H, W) == 16) return (const void*)conv_wgrad_kernel<32, 16, true, 16, true>;
+    return nullptr;
+  }
   switch (wg_band_w(H, W)) {
     case 24: return (const void*)conv_wgrad_kernel<CI, CO, B, 24>;
     case 16: return (const void*)conv_wgrad_kernel<CI, CO, B, 16>;
@@ -1405,29 +1471,36 @@ const void* wgrad_kfn(int H, int W) {
 
 // number of partial rows mbk_conv_wgrad will write for this shape (<= nrounds)
 extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
-                                    int imgs) {
-  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
+                                    int imgs, int unpool) {
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W, unpool != 0);
   if (sm > 160 * 1024 || !index_math_ok(imgs, H, W)) return -(int)hipErrorInvalidValue;
   const int nrounds = (N + imgs - 1) / imgs;
   int res = 1;
-#define Q(CI, CO, B) res = resident_blocks(wgrad_kfn<CI, CO, B>(H, W), sm)
+  const void* kq = nullptr;
+#define Q(CI, CO, B) kq = wgrad_kfn<CI, CO, B>(H, W, unpool != 0)
   WGRAD_DISPATCH(Q)
 #undef Q
+  if (!kq) return -(int)hipErrorInvalidValue;
+  res = resident_blocks(kq, sm);
   return (int)std::max(1L, std::min((long)nrounds, (long)res));
 }
 
+// dy == nullptr: the stage-0 pool-fused form, dY = max_pool2d backward of dp through pidx
 extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, const void* dy,
-                              float* partial, int nparts, int N, int H, int W, int imgs,
-                              int relu_in, hipStream_t stream) {
-  if (!dy) return (int)hipErrorInvalidValue;
-  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in};
-  const size_t sm = wgrad_smem(cin, cout, imgs, H, W);
+                              const void* dp, const void* pidx, float* partial, int nparts,
+                              int N, int H, int W, int imgs, int relu_in, hipStream_t stream) {
+  const bool unpool = dy == nullptr;
+  if (unpool && (!dp || !pidx || imgs > 2)) return (int)hipErrorInvalidValue;
+  ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in, (const bf16*)dp,
+                  (const uint8_t*)pidx};
+  const size_t sm = wgrad_smem(cin, cout, imgs, H, W, unpool);
   if (sm > 160 * 1024 || nparts < 1 || !index_math_ok(imgs, H, W))
     return (int)hipErrorInvalidValue;
   dim3 grid(nparts);
 #define LAUNCH(CI, CO, B)                                                                   \
   do {                                                                                      \
-    const void* kfn = wgrad_kfn<CI, CO, B>(H, W);                            \
+    const void* kfn = wgrad_kfn<CI, CO, B>(H, W, unpool);                    \
+    if (!kfn) return (int)hipErrorInvalidValue;                              \
     if (sm > 64 * 1024)                                                                     \
       hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);        \
     void* args[] = {&a};                                                                    \

@@ -79,7 +79,7 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
     return imgs
 
 
-def _imgs_wgrad(layer: ConvLayer) -> int:
+def _imgs_wgrad(layer: ConvLayer, unpool: bool = False) -> int:
     hw = layer.H * layer.W
     xepp = 1 if layer.bits else layer.cin // 8
     dch = layer.cout // 8
@@ -91,6 +91,8 @@ def _imgs_wgrad(layer: ConvLayer) -> int:
         per = (layer.H + 2) * rbx + layer.H * rbd
     else:
         per = (layer.H + 2) * (layer.W + 2) * layer.cin * 2 + hw * layer.cout * 2
+    if unpool:  # the pool-fused form scatters 2 images per round (one per 32-lane half)
+        imgs = min(imgs, 2)
     while imgs > 1:
         if imgs * per <= 64 * 1024:
             break
@@ -139,6 +141,13 @@ class HipEncoder:
         self.fused_res_fwd32 = True
         # the stage-0 residual kernel also runs stage 1's conv + pool
         self.fused_stage_fwd = True
+        # the observation layer's weight gradient expands the max-pool backward in its own
+        # LDS staging (16-wide maps; bit-identical): no pool_bwd_idx launch, no 4.3 GB
+        # full-resolution gradient in HBM per 524K-frame update
+        self.fused_pool_wgrad0 = True
+        # the 16 -> 32 stage conv on 8x8 maps: pool backward, weight gradient and input
+        # gradient in one launch (stagebwd.hip; no full-resolution gradient in HBM)
+        self.fused_pool_conv_bwd = True
         self._partial_rb = None
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
         self._partial = None
@@ -272,11 +281,15 @@ class HipEncoder:
             N.stream_ptr()), "conv_fwd")
         return y
 
-    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor):
+    def _wgrad(self, L: ConvLayer, x, dy, dw: torch.Tensor, db: torch.Tensor, dp=None,
+               pidx=None):
+        """dy=None: dY is max_pool2d's backward of dp through the argmax bytes pidx, expanded
+        in the kernel's staging (the stage-0 layer of a 16-wide map)."""
         n = x.shape[0]
-        imgs = _imgs_wgrad(L)
+        imgs = _imgs_wgrad(L, unpool=dy is None)
         # persistent grid: as many workgroups as the device keeps resident (<= rounds)
-        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs)
+        nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs,
+                                                  int(dy is None))
         if nparts < 1:
             raise RuntimeError(f"conv_wgrad: unsupported shape {L}")
         row = L.cout * 9 * L.cin + L.cout
@@ -285,9 +298,9 @@ class HipEncoder:
             self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=x.device)
         k = N.kernels()
         st = N.stream_ptr()
-        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, dy.data_ptr(),
-                                 self._partial.data_ptr(), nparts, n, L.H, L.W, imgs,
-                                 int(L.relu_in), st), "conv_wgrad")
+        N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, N.ptr(dy),
+                                 N.ptr(dp), N.ptr(pidx), self._partial.data_ptr(), nparts, n,
+                                 L.H, L.W, imgs, int(L.relu_in), st), "conv_wgrad")
         N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
                                    dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
 
@@ -356,6 +369,23 @@ class HipEncoder:
                                 self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
                                 db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs, 0,
                                 N.stream_ptr()), "res_bwd16")
+        return dx
+
+    def _pool_conv_bwd(self, L: ConvLayer, dp, pidx, x, dw, db):
+        """Backward of a pooled stage conv in one launch (stagebwd.hip): returns dx; writes the
+        layer's weight / bias gradients."""
+        n = x.shape[0]
+        k = N.kernels()
+        nparts = k.mbk_pool_conv_bwd_parts(n, L.cin, L.cout, L.H, L.W)
+        need = k.mbk_pool_conv_bwd_partial_floats(nparts)
+        if self._partial_rb is None or self._partial_rb.numel() < need:
+            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        dx = torch.empty_like(x)
+        N.check(k.mbk_pool_conv_bwd(dp.data_ptr(), pidx.data_ptr(), x.data_ptr(),
+                                    self.packed_bwd.data_ptr() + 2 * L.wb_off, dx.data_ptr(),
+                                    self._partial_rb.data_ptr(), nparts, dw.data_ptr(),
+                                    db.data_ptr(), n, L.cin, L.cout, L.H, L.W, 0,
+                                    N.stream_ptr()), "pool_conv_bwd")
         return dx
 
     def _res_bwd32(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
@@ -485,6 +515,15 @@ class HipEncoder:
                 dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
+            if s == 0 and Ls.bits and Ls.W == 16 and self.fused_pool_wgrad0:
+                self._wgrad(Ls, x, None, grads[2 * li], grads[2 * li + 1], dp=dp, pidx=pidx)
+                g = None
+                continue
+            if (s > 0 and self.fused_pool_conv_bwd and x.is_cuda
+                    and N.kernels().mbk_pool_conv_bwd_parts(x.shape[0], Ls.cin, Ls.cout, Ls.H,
+                                                            Ls.W) > 0):
+                g = self._pool_conv_bwd(Ls, dp, pidx, x, grads[2 * li], grads[2 * li + 1])
+                continue
             dc = torch.empty(pidx.shape[0], Ls.H, Ls.W, Ls.cout, dtype=torch.bfloat16,
                              device=pidx.device)
             N.check(N.kernels().mbk_pool_bwd_idx(pidx.data_ptr(), dp.data_ptr(), pidx.shape[0],

@@ -443,6 +443,74 @@ def test_fused_res_bwd16_matches_per_layer_kernels(cuda, s, n):
             torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("n", [1, 5, 37, 700])
+def test_pool_conv_bwd_stage1_matches_per_layer(cuda, n):
+    """stagebwd.hip (pool backward + weight gradient + input gradient of the 16 -> 32 stage
+    conv on 8x8 maps in one launch) against pool_bwd_idx + conv_wgrad + the conv_fwd dgrad:
+    the input gradient and everything upstream of it agree to bf16 rounding of the dc sums
+    (identical whenever the <= 4 windows of a pixel sum exactly in fp32), the stage conv's
+    weight / bias gradients to fp32 summation order."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(3)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(n, 256, seed=n + 1).to(cuda)
+    m.features(obs[:1])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    grads = {}
+    for fused in (False, True):
+        enc.fused_pool_conv_bwd = fused
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(9)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[fused] = [p.grad.detach().clone() for p in params]
+    enc.fused_pool_conv_bwd = True
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        assert torch.isfinite(b).all(), i
+        torch.testing.assert_close(b, a, rtol=2e-3, atol=1e-5, msg=f"param {i}")
+    # stage 2 and stage 1's residual blocks run before the fused launch: untouched
+    for i in range(12, 30):
+        assert torch.equal(grads[False][i], grads[True][i]), i
+
+
+@pytest.mark.parametrize("n", [1, 2, 37, 300])
+def test_pool_fused_stage0_wgrad_matches(cuda, n):
+    """The observation layer's weight gradient with the max-pool backward scattered into its
+    own LDS staging (conv.hip UNPOOL, 16-wide maps) against pool_bwd_idx + the band-layout
+    kernel: the same dY tile up to one bf16 rounding where two windows chose the same pixel,
+    the same MFMA chains and partial rows; the other layers' gradients are untouched."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(2)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(n, 256, seed=n).to(cuda)
+    m.features(obs[:1])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    grads = {}
+    for fused in (False, True):
+        enc.fused_pool_wgrad0 = fused
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(7)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[fused] = [p.grad.detach().clone() for p in params]
+    enc.fused_pool_wgrad0 = True
+    assert float(grads[True][0].abs().sum()) > 0
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        if i < 2:
+            rel = float((b - a).norm() / a.norm())
+            assert rel < 5e-3, (i, rel, float((b - a).abs().max()), float(a.abs().max()))
+        else:
+            assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("s,n", [(16, 37), (10, 21)])
 def test_fused_res_fwd16_bit_identical(cuda, s, n):
     """resblock.hip res_fwd16 (both 16-channel residual blocks in one launch) writes the

@@ -26,6 +26,9 @@ def main():
                          "init policy's early game, 0.025 ~ a settled training run (6.5 / 256)")
     ap.add_argument("--no_abits", action="store_true",
                     help="no active-cell bitmap rows in the batch (the head counts from masks)")
+    ap.add_argument("--set", action="append", default=[],
+                    help="enc.<attr>=<int> / head.<attr>=<int>: set a variant attribute of the "
+                         "HIP encoder / sparse head before the first update (A/B in one process)")
     a = ap.parse_args()
     import torch
 
@@ -58,6 +61,13 @@ def main():
         w = (live << torch.arange(32, device=dev)).sum(-1)
         batch["abits"] = torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
     learner.learn(batch)
+    for kv in a.set:
+        k, v = kv.split("=")
+        obj, attr = k.split(".")
+        m = learner.model
+        tgt = m._hip_enc if obj == "enc" else m._head(dev)
+        assert hasattr(tgt, attr), kv
+        setattr(tgt, attr, type(getattr(tgt, attr))(int(v)))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
