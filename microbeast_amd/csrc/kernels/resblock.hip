@@ -393,24 +393,31 @@ __global__ __launch_bounds__(kThreads) void res_bwd16_kernel(ResBwdArgs a) {
 // exposed (1.28 ms, 21.7 % MFMA); splitting each image over a wave pair synchronised by
 // workgroup barriers (3 per 4 images) left the waves parked 58 % of their cycles (1.25 ms).
 // Here 8 waves form 4 independent producer / consumer pairs, each pair on one SIMD:
-//   D-wave p (waves 0-3): stages x, u, g; du = conv1^T(g) * [u > 0] -> Td; dx = conv0^T(du) *
-//     [x > 0] + g -> HBM (dgrad weights in VGPRs);
-//   W-wave p + 4 (waves 4-7): dW1 += relu(u) (x) g, dW0 += relu(x) (x) du (accumulators in AGPRs
-//     for the whole launch),
+//   D-wave p (waves 0-3): du = conv1^T(g) * [u > 0] -> Td; dx = conv0^T(du) * [x > 0] + g ->
+//     HBM (dgrad weights in VGPRs);
+//   W-wave p + 4 (waves 4-7): stages x, u, g (HBM loads one image ahead); dW1 += relu(u) (x) g,
+//     dW0 += relu(x) (x) du (accumulators for the whole launch),
 // over two sets of the pair's LDS tiles (Tg = g, Tu = relu u, Tx = relu x, Td = du), image i in
-// set i % 2, synchronised by three per-pair LDS flags per set (staged / du written / consumed)
-// instead of workgroup barriers: a wave's LDS writes complete in issue order, so a flag written
-// after the data publishes it. Block j of the dgrads is map row pair j and K block kb of the
+// set i % 2, synchronised by three per-pair LDS flags per set (staged / du written / D done with
+// the set) instead of workgroup barriers: a wave's LDS writes complete in issue order, so a flag
+// written after the data publishes it. (The staging sat in the D-wave until round 5: with the
+// epilogues too, the D-wave was the pair's critical path and its W-wave spun on the flags --
+// 4.2 VALU per MFMA, 55 % of wave cycles waiting, profile r5n.) Block j of the dgrads is map row pair j and K block kb of the
 // weight gradients rows 4 kb .. 4 kb + 3, so their offsets are immediates; tap reads are
 // software-pipelined against the MFMA chains. du / dx are bit-identical to the per-layer
 // kernels; the weight gradients differ by fp32 summation order (the W-waves' fixed-order sum).
 namespace w88b {
 constexpr int RB = w88::RB, PB = w88::PB, IMGB = w88::IMGB;
 constexpr int SET = 4 * IMGB;  // one tile set: Tg, Tu, Tx, Td
-constexpr int REG = 2 * SET;   // a pair's LDS
+// tile sets per pair: 1 (single-buffered: 79 KB per workgroup, so 2 workgroups -- 4 waves --
+// share each SIMD and one pair's waits are the other's issue slots) or 2 (157 KB, 1 per CU)
+constexpr int NSET = 1;
+constexpr int REG = NSET * SET;  // a pair's LDS
 constexpr int TG = 0, TU = IMGB, TX = 2 * IMGB, TD = 3 * IMGB;
-constexpr int kPT = 512;        // 4 pairs
-constexpr int FLAGS = 4 * REG;  // per pair, per set: staged, du written, consumed (iteration #)
+constexpr int NP = 2;            // pairs per workgroup (3 workgroups of 2 pairs per CU at
+                                 // 162 VGPRs: 3 waves per SIMD)
+constexpr int kPT = 128 * NP;
+constexpr int FLAGS = NP * REG;  // per pair, per set: staged, du written, D done (iteration #)
 }  // namespace w88b
 
 // spin until an LDS flag reaches v (written by the other wave of the pair)
@@ -427,12 +434,12 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
-  const bool dw = wave < 4;  // D-wave (dgrads) or W-wave (weight gradients)
-  const int pair = wave & 3;
+  const bool dw = wave < NP;  // D-wave (dgrads) or W-wave (weight gradients)
+  const int pair = wave % NP;
   char* R = smem + pair * REG;
-  int* fl = (int*)(smem + FLAGS) + pair * 6;  // [set][staged, du, consumed]
+  int* fl = (int*)(smem + FLAGS) + pair * 6;  // [set][staged, du, D done]
   for (int e = tid; e < FLAGS / 16; e += kPT) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
-  if (tid < 24) ((int*)(smem + FLAGS))[tid] = 0;
+  if (tid < 6 * NP) ((int*)(smem + FLAGS))[tid] = 0;
   // dgrad (D-waves): this lane's pixel of row pair 0, tap (0, 0) offset per K chunk
   const int lb = (li >> 3) * RB + (li & 7) * PB;
   int aoff[NCH];
@@ -458,8 +465,8 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
     const int e = lane + 64 * k, px = e >> 1;
     so[k] = ((px >> 3) + 1) * RB + ((px & 7) + 1) * PB + (e & 1) * 16;
   }
-  const int step = gridDim.x * 4;
-  const int first = blockIdx.x * 4 + pair;  // the pair's images: first, first + step, ...
+  const int step = gridDim.x * NP;
+  const int first = blockIdx.x * NP + pair;  // the pair's images: first, first + step, ...
   __syncthreads();  // zeroed tiles and flags
   if (dw) {
     Frag8 w1[NCH], w0[NCH];  // dgrad weights (A fragments): lane holds w[co = li][chunk c][8g..]
@@ -491,31 +498,12 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
         __builtin_amdgcn_sched_barrier(0);
       }
     };
-    uint4 px[2], pu[2], pg[2];
-    auto fetch = [&](int im) {
-      const size_t o = (size_t)im * HW * 2;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        px[k] = ((const uint4*)a.x)[o + lane + 64 * k];
-        pu[k] = ((const uint4*)a.u)[o + lane + 64 * k];
-        pg[k] = ((const uint4*)a.g)[o + lane + 64 * k];
-      }
-    };
-    if (first < a.N) fetch(first);
     int it = 1;
     for (int img = first; img < a.N; img += step, ++it) {
-      const int b = it & 1;
+      const int b = it % NSET;
       char* T = R + b * SET;
       int* f = fl + 3 * b;
-      if (it > 2) wait_flag(f + 2, it - 2);  // the W-wave is done with this set's last image
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        *(uint4*)(T + TX + so[k]) = relu8(px[k]);
-        *(uint4*)(T + TU + so[k]) = relu8(pu[k]);
-        *(uint4*)(T + TG + so[k]) = pg[k];
-      }
-      set_flag(f, it, lane);  // staged
-      if (img + step < a.N) fetch(img + step);
+      wait_flag(f, it);  // staged (by the W-wave)
       wave_lds_order();
       f32x4 acc[4];
       // du = conv1^T(g) * [u > 0] -> Td (the epilogue's mask words read ahead of the MFMAs)
@@ -562,6 +550,7 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
             make_uint2(cvt_pk2(v[0], v[1]), cvt_pk2(v[2], v[3]));
       }
       wave_lds_order();
+      set_flag(f + 2, it, lane);  // done with the set (its reads completed in issue order)
     }
     __syncthreads();  // (the W-waves' matching barrier: every pair is done)
   } else {  // ---------------- W-waves
@@ -604,24 +593,44 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
       __builtin_amdgcn_sched_barrier(0);
     }
   };
+  uint4 px[2], pu[2], pg[2];
+  auto fetch = [&](int im) {
+    const size_t o = (size_t)im * HW * 2;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      px[k] = ((const uint4*)a.x)[o + lane + 64 * k];
+      pu[k] = ((const uint4*)a.u)[o + lane + 64 * k];
+      pg[k] = ((const uint4*)a.g)[o + lane + 64 * k];
+    }
+  };
+  if (first < a.N) fetch(first);
   int it = 1;
   for (int img = first; img < a.N; img += step, ++it) {
-    const int b = it & 1;
-    const char* T = R + b * SET;
+    const int b = it % NSET;
+    char* T = R + b * SET;
     int* f = fl + 3 * b;
-    wait_flag(f, it);  // staged
+    if (it > NSET) wait_flag(f + 2, it - NSET);  // the D-wave is done with this set's last image
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      *(uint4*)(T + TX + so[k]) = relu8(px[k]);
+      *(uint4*)(T + TU + so[k]) = relu8(pu[k]);
+      *(uint4*)(T + TG + so[k]) = pg[k];
+    }
+    set_flag(f, it, lane);  // staged
+    if (img + step < a.N) fetch(img + step);
+    wave_lds_order();
     wgrad(T + TG, T + TU, acc1, accb1);  // dW1 += relu(u) (x) g
     wait_flag(f + 1, it);  // du written
+    wave_lds_order();
     wgrad(T + TD, T + TX, acc0, accb0);  // dW0 += relu(x) (x) du
     wave_lds_order();
-    set_flag(f + 2, it, lane);  // consumed
   }
   __syncthreads();  // every pair is done: the tiles are dead
   // every tile is dead after the last (3): each W-wave parks its accumulators in its own slot
   float* red = (float*)smem;
 #pragma unroll
   for (int which = 0; which < 2; ++which) {
-    float* sl = red + (which * 4 + pair) * (C * KTOT);
+    float* sl = red + (which * NP + pair) * (C * KTOT);
 #pragma unroll
     for (int t = 0; t < 9; ++t)
 #pragma unroll
@@ -630,29 +639,38 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
     if (li == 0)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        red[8 * C * KTOT + (which * 4 + pair) * C + 4 * g + i] = which == 0 ? accb1[i] : accb0[i];
+        red[2 * NP * C * KTOT + (which * NP + pair) * C + 4 * g + i] =
+            which == 0 ? accb1[i] : accb0[i];
   }
   }
   __syncthreads();
-  // ---- per-workgroup partial rows: the 4 W-waves' slots summed in a fixed order
+  // ---- per-workgroup partial rows: the NP W-waves' slots summed in a fixed order
   // (deterministic); bias = column 0 of the all-ones accumulators
   const float* red = (const float*)smem;
   for (int which = 0; which < 2; ++which) {
     float* out = a.partial + which * a.lstride + (size_t)blockIdx.x * ROW;
-    const float* sl = red + which * 4 * (C * KTOT);
-    for (int e = tid; e < C * KTOT; e += kPT)
-      out[e] = ((sl[e] + sl[C * KTOT + e]) + sl[2 * C * KTOT + e]) + sl[3 * C * KTOT + e];
+    const float* sl = red + which * NP * (C * KTOT);
+    for (int e = tid; e < C * KTOT; e += kPT) {
+      float v = sl[e];
+#pragma unroll
+      for (int p = 1; p < NP; ++p) v += sl[p * C * KTOT + e];
+      out[e] = v;
+    }
     if (tid < C) {
-      const float* b = red + 8 * C * KTOT + which * 4 * C;
-      out[C * KTOT + tid] = ((b[tid] + b[C + tid]) + b[2 * C + tid]) + b[3 * C + tid];
+      const float* b = red + 2 * NP * C * KTOT + which * NP * C;
+      float v = b[tid];
+#pragma unroll
+      for (int p = 1; p < NP; ++p) v += b[p * C + tid];
+      out[C * KTOT + tid] = v;
     }
   }
 }
 
-// 4 pairs' two tile sets + their flags; the final reduction (8 slots of C x KTOT floats +
+// NP pairs' tile sets + their flags; the final reduction (2 NP slots of C x KTOT floats +
 // biases) reuses the tiles
-constexpr size_t res_w88b_smem() { return (size_t)w88b::FLAGS + 4 * 6 * 4; }
-static_assert((8 * C * KTOT + 8 * C) * 4 <= w88b::FLAGS, "reduction slots must fit the tiles");
+constexpr size_t res_w88b_smem() { return (size_t)w88b::FLAGS + w88b::NP * 6 * 4; }
+static_assert((2 * w88b::NP * C * KTOT + 2 * w88b::NP * C) * 4 <= w88b::FLAGS,
+              "reduction slots must fit the tiles");
 static_assert(res_w88b_smem() <= 160 * 1024, "LDS");
 
 size_t res_smem(int imgs, int H, int W) {
@@ -664,7 +682,7 @@ size_t res_smem(int imgs, int H, int W) {
 bool res_bwd_w88(int H, int W) { return H == 8 && W == 8; }
 
 int res_grid(int N, int H, int W, int imgs) {
-  if (res_bwd_w88(H, W)) imgs = 4;  // 4 wave pairs, an image each
+  if (res_bwd_w88(H, W)) imgs = w88b::NP;  // NP wave pairs, an image each
   const size_t sm = res_bwd_w88(H, W) ? res_w88b_smem() : res_smem(imgs, H, W);
   static int cus = 0;
   if (!cus) {
