@@ -1239,17 +1239,32 @@ struct ResBwd32Args {
   int N, H, W, imgs;
 };
 
+// Tile geometry: halo'd pixel (hy, hx) of image im at im * is + hy * rs + hx * pb. 4-wide maps
+// (IMPALA stage 1 at 16x16): unpadded 64-byte pixels in 400-byte rows, so the 4 pixels of a
+// transposed read's lane group span 4 x 64 B and the group two map rows down starts 800 = 32
+// (mod 256) bytes later: a half-wave's 8 x 32 B reads cover 256 distinct bytes (the 80-byte
+// pixels of the generic layout overlapped: 32.8 % bank conflicts, profile 40)
+struct Geo32 {
+  int pb, rs, is;
+};
+__host__ __device__ inline Geo32 geo32(int H, int W) {
+  if (W == 4) return {64, 400, ((H + 1) * 400 + (W + 2) * 64 + 15) & ~15};
+  return {PIXB32, (W + 2) * PIXB32, (H + 2) * (W + 2) * PIXB32};
+}
+
 template <int WC>
 __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W;
+  const Geo32 G3 = geo32(H, W);
+  const int PB = WC == 4 ? 64 : G3.pb, RS = WC == 4 ? 400 : G3.rs, IS = G3.is;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const bool lo = wave < 4;          // waves 0-3: dgrad1 (A) + wgrad0 (B)
   const int wq = wave & 3;           // rank inside the half
   const int cb = wq >> 1, cib = wq & 1;
-  const int tb = ((a.imgs * Hp * Wp * PIXB32) + 15) & ~15;
+  const int tb = ((a.imgs * IS) + 15) & ~15;
   char* Tg = smem;
   char* Tu = smem + tb;       // relu(u)
   char* Tx = smem + 2 * tb;   // relu(x)
@@ -1273,7 +1288,7 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
   for (int t = 0; t < 9; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
   int coff[NCH32];  // K chunk c = tap c, channels 8g.. of this lane
 #pragma unroll
-  for (int c = 0; c < NCH32; ++c) coff[c] = ((c / 3) * Wp + (c % 3)) * PIXB32 + 16 * g;
+  for (int c = 0; c < NCH32; ++c) coff[c] = (c / 3) * RS + (c % 3) * PB + 16 * g;
   float db1[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum g: channels 8 (tid & 3) .. +8 (staging)
   float db0[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // sum du: channels nb*16 + 4g + i (waves 0-3)
 
@@ -1297,7 +1312,7 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
     const int q = e & (EPP - 1), p = e / EPP;
     const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
     const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB32 + q * 16;
+    return im * IS + (y + 1) * RS + (x + 1) * PB + q * 16;
   };
   auto put = [&](int e, uint4 vx, uint4 vu, uint4 vg) {
     const int o = lds_off(e);
@@ -1322,18 +1337,18 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
       const int pp = ok ? p : 0;
       const int im = (int)(((float)pp + 0.5f) * inv_hw), r = pp - im * HW;
       const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-      xpos[h] = (im * Hp + y) * Wp + x;
-      dptr[h] = ok ? D + (xpos[h] + Wp + 1) * PIXB32 + cb * 32 : zero;
+      xpos[h] = im * IS + y * RS + x * PB;  // byte offset of the pixel's window top-left
+      dptr[h] = ok ? D + xpos[h] + RS + PB + cb * 32 : zero;
     }
     Frag8 af;
 #pragma unroll
     for (int h = 0; h < 2; ++h) af.h[h] = tr_read(dptr[h] + (4 * (li & 3)) * 2);
     // out-of-range pixels read pixel 0's (finite) X values against a zero dY column
-    const char* xb0 = X + xpos[0] * PIXB32 + cib * 32 + 8 * (li & 3);
-    const char* xb1 = X + xpos[1] * PIXB32 + cib * 32 + 8 * (li & 3);
+    const char* xb0 = X + xpos[0] + cib * 32 + 8 * (li & 3);
+    const char* xb1 = X + xpos[1] + cib * 32 + 8 * (li & 3);
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
-      const int off = ((t / 3) * Wp + (t % 3)) * PIXB32;
+      const int off = (t / 3) * RS + (t % 3) * PB;
       Frag8 bf;
       bf.h[0] = tr_read(xb0 + off);
       bf.h[1] = tr_read(xb1 + off);
@@ -1367,8 +1382,8 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
         const int mm = valid ? m : 0;
         const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        const int base = (im * Hp + y) * Wp + x;
-        const char* bp = Tg + base * PIXB32;
+        const int base = im * IS + y * RS + x * PB;
+        const char* bp = Tg + base;
         f32x4 ac[NB32];
 #pragma unroll
         for (int nb = 0; nb < NB32; ++nb) ac[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1381,7 +1396,7 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
             ac[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av.v, ac[nb], 0, 0, 0);
         }
         if (!valid) continue;
-        const int o = (base + Wp + 1) * PIXB32;
+        const int o = base + RS + PB;
 #pragma unroll
         for (int nb = 0; nb < NB32; ++nb) {
           const int co0 = nb * 16 + 4 * g;
@@ -1411,8 +1426,8 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
         const int mm = valid ? m : 0;
         const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        const int base = (im * Hp + y) * Wp + x;
-        const char* bp = Td + base * PIXB32;
+        const int base = im * IS + y * RS + x * PB;
+        const char* bp = Td + base;
         f32x4 ac[NB32];
 #pragma unroll
         for (int nb = 0; nb < NB32; ++nb) ac[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1425,7 +1440,7 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
             ac[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av.v, ac[nb], 0, 0, 0);
         }
         if (!valid) continue;
-        const int o = (base + Wp + 1) * PIXB32;
+        const int o = base + RS + PB;
 #pragma unroll
         for (int nb = 0; nb < NB32; ++nb) {
           const int co0 = nb * 16 + 4 * g;
@@ -1477,7 +1492,7 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
 }
 
 size_t res32b_smem(int imgs, int H, int W) {
-  const size_t tb = ((size_t)imgs * (H + 2) * (W + 2) * PIXB32 + 15) & ~(size_t)15;
+  const size_t tb = ((size_t)imgs * geo32(H, W).is + 15) & ~(size_t)15;
   return std::max(4 * tb + 128, (size_t)kT32 * 16 * 4);
 }
 
