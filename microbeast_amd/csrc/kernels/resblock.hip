@@ -1086,6 +1086,10 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_w88_kernel(ResFwdArgs a) {
 // order = conv.hip's conv_fwd<32, 32> chains, so outputs are bit-identical to it.
 constexpr int C32 = 32, PIXB32 = C32 * 2 + 16, NCH32 = 9, NB32 = 2;
 
+struct Geo32f {
+  int pb, rs, is;
+};
+
 struct ResBlk32Args {
   const bf16* x;     // [N][H][W][32] block input (pre-relu)
   bf16 *u, *y;       // outputs
@@ -1094,14 +1098,26 @@ struct ResBlk32Args {
   int N, H, W, imgs;
 };
 
+// Tile geometry (halo'd pixel (hy, hx) of image im at im * is + hy * rs + hx * pb). 4-wide maps
+// (stage 1 at 16x16): 64-byte pixels in 416-byte rows (= 32 mod 64): the 16 B tap reads of a
+// ds_read_b128 lane group -- 4 pixels of each of the image's 4 rows, two channel chunks --
+// start at 16 distinct 16-byte slots of the 256-byte bank window (the generic 80-byte pixels:
+// 32 % bank conflicts, profile 40)
+__host__ __device__ inline Geo32f geo32f(int H, int W) {
+  if (W == 4) return {64, 416, ((H + 1) * 416 + (W + 2) * 64 + 15) & ~15};
+  return {PIXB32, (W + 2) * PIXB32, (H + 2) * (W + 2) * PIXB32};
+}
+
 template <int WC>
 __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
+  const int H = a.H, W = WC > 0 ? WC : a.W, HW = H * W;
+  const Geo32f G3 = geo32f(H, W);
+  const int PB = WC == 4 ? 64 : G3.pb, RS = WC == 4 ? 416 : G3.rs, IS = G3.is;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int tb = ((a.imgs * Hp * Wp * PIXB32) + 15) & ~15;
+  const int tb = ((a.imgs * IS) + 15) & ~15;
   char* Tx = smem;       // x (raw): conv0's input (relu at read) and the residual
   char* Tu = smem + tb;  // relu(u): conv1's input
   for (int e = tid; e < 2 * tb / 16; e += kThreads) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
@@ -1119,7 +1135,7 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
     }
   int coff[NCH32];  // K chunk c = tap c, channels 8g.. of this lane
 #pragma unroll
-  for (int c = 0; c < NCH32; ++c) coff[c] = ((c / 3) * Wp + (c % 3)) * PIXB32 + 16 * g;
+  for (int c = 0; c < NCH32; ++c) coff[c] = (c / 3) * RS + (c % 3) * PB + 16 * g;
   constexpr int EPP = C32 / 8;  // uint4 per pixel
   const int per = a.imgs * HW * EPP;
   const int nrounds = (a.N + a.imgs - 1) / a.imgs;
@@ -1127,7 +1143,7 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
     const int q = e & (EPP - 1), p = e / EPP;
     const int im = (int)(((float)p + 0.5f) * inv_hw), r = p - im * HW;
     const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-    return ((im * Hp + y + 1) * Wp + x + 1) * PIXB32 + q * 16;
+    return im * IS + (y + 1) * RS + (x + 1) * PB + q * 16;
   };
   // The next round's x is fetched into registers while this round computes (when a round
   // is at most kPF uint4 per thread), so the global-load latency leaves the critical path.
@@ -1171,8 +1187,8 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
         const int mm = valid ? m : 0;
         const int im = (int)(((float)mm + 0.5f) * inv_hw), r = mm - im * HW;
         const int y = (int)(((float)r + 0.5f) * inv_w), x = r - y * W;
-        const int base = (im * Hp + y) * Wp + x;
-        const char* bp = src + base * PIXB32;
+        const int base = im * IS + y * RS + x * PB;
+        const char* bp = src + base;
         f32x4 acc[NB32];
 #pragma unroll
         for (int nb = 0; nb < NB32; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1186,7 +1202,7 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
             acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[l][c][nb].v, av.v, acc[nb], 0, 0, 0);
         }
         if (!valid) continue;
-        const int o = (base + Wp + 1) * PIXB32;
+        const int o = base + RS + PB;
 #pragma unroll
         for (int nb = 0; nb < NB32; ++nb) {
           const int co0 = nb * 16 + 4 * g;
@@ -1497,7 +1513,7 @@ size_t res32b_smem(int imgs, int H, int W) {
 }
 
 size_t resb32_smem(int imgs, int H, int W) {
-  return 2 * (((size_t)imgs * (H + 2) * (W + 2) * PIXB32 + 15) & ~(size_t)15);
+  return 2 * (((size_t)imgs * geo32f(H, W).is + 15) & ~(size_t)15);
 }
 
 size_t resf_smem(int imgs, int H, int W) {
