@@ -98,6 +98,7 @@ _SIGS = {
                     c_int, c_int, c_int, c_int, c_void_p],
     "mbk_wgrad_reduce": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_int,
                          c_void_p],
+    "mbk_wgrad_reduce_batch": [c_void_p, c_int, c_void_p],
     "mbk_pool_bwd": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mbk_conv_pack": [c_void_p, c_int, c_void_p],
     "mbk_head_compact": [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,

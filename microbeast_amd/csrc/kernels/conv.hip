@@ -1068,17 +1068,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
 // block = 64 output columns x 4 part-lanes over parts [y*pps, (y+1)*pps); with `stage`
 // set the split sums go to stage[y][row] for a second pass (two-level: the persistent
 // wgrad writes up to a few thousand partial rows). Fixed summation order (deterministic).
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial,
-                                                           int nparts, int pps,
-                                                           float* __restrict__ stage, int cin,
-                                                           int cin_real, int cout,
-                                                           float* __restrict__ dw,
-                                                           float* __restrict__ db, int accumulate) {
-  __shared__ float red[4][64];
+// One 64-column slice of a partial-row reduction: sums rows [split*pps, min(nparts, ..+pps))
+// of ``partial`` (4 row lanes x 64 columns, then the 4 lane sums in order) and writes the
+// split's row of ``stage`` or, with stage == nullptr, the fp32 weight / bias gradient.
+__device__ __forceinline__ void wgrad_reduce_cols(const float* __restrict__ partial, int nparts,
+                                                  int pps, int split, int colblk,
+                                                  float* __restrict__ stage, int cin,
+                                                  int cin_real, int cout, float* __restrict__ dw,
+                                                  float* __restrict__ db, int accumulate,
+                                                  float (*red)[64]) {
   const int ktot = 9 * cin, row = cout * ktot + cout;
   const int col = threadIdx.x & 63, pl = threadIdx.x >> 6;
-  const int e = blockIdx.x * 64 + col;
-  const int p0 = blockIdx.y * pps, p1 = min(nparts, p0 + pps);
+  const int e = colblk * 64 + col;
+  const int p0 = split * pps, p1 = min(nparts, p0 + pps);
   float s = 0.f;
   if (e < row) {
 #pragma unroll 4
@@ -1089,7 +1091,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   if (pl != 0 || e >= row) return;
   s = red[0][col] + red[1][col] + red[2][col] + red[3][col];
   if (stage) {
-    stage[(size_t)blockIdx.y * row + e] = s;
+    stage[(size_t)split * row + e] = s;
     return;
   }
   if (e < cout * ktot) {
@@ -1100,6 +1102,52 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   } else if (db) {
     const int co = e - cout * ktot;
     db[co] = accumulate ? db[co] + s : s;
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ partial,
+                                                           int nparts, int pps,
+                                                           float* __restrict__ stage, int cin,
+                                                           int cin_real, int cout,
+                                                           float* __restrict__ dw,
+                                                           float* __restrict__ db, int accumulate) {
+  __shared__ float red[4][64];
+  wgrad_reduce_cols(partial, nparts, pps, blockIdx.y, blockIdx.x, stage, cin, cin_real, cout, dw,
+                    db, accumulate, red);
+}
+
+// Many layers' reductions in one launch (blockIdx.z = job; the encoder defers every weight
+// gradient reduce of a backward pass to one mbk_wgrad_reduce_batch call). Level 0 runs a
+// job's split sums (two-level jobs) or its whole sum; level 1 the two-level jobs' second
+// stage: per element the same adds in the same order as mbk_wgrad_reduce -> bit-identical.
+struct MbkReduceJob {
+  const float* partial;
+  float* dw;
+  float* db;
+  int nparts, cin, cin_real, cout, accumulate;
+};
+constexpr int kReducePps = 32;
+constexpr int kMaxReduceJobs = 32;
+struct ReduceBatch {
+  MbkReduceJob j[kMaxReduceJobs];
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(ReduceBatch b, int level) {
+  __shared__ float red[4][64];
+  const MbkReduceJob J = b.j[blockIdx.z];
+  const int row = J.cout * 9 * J.cin + J.cout;
+  if ((int)blockIdx.x * 64 >= row) return;  // whole workgroup: before any barrier
+  const bool two = J.nparts > 2 * kReducePps;
+  const int splits = two ? (J.nparts + kReducePps - 1) / kReducePps : 1;
+  float* stage = two ? (float*)J.partial + (size_t)J.nparts * row : nullptr;
+  if (level == 0) {
+    if ((int)blockIdx.y >= splits) return;
+    wgrad_reduce_cols(J.partial, J.nparts, two ? kReducePps : J.nparts, blockIdx.y, blockIdx.x,
+                      stage, J.cin, J.cin_real, J.cout, J.dw, J.db, J.accumulate, red);
+  } else {
+    if (!two || blockIdx.y != 0) return;
+    wgrad_reduce_cols(stage, splits, splits, 0, blockIdx.x, nullptr, J.cin, J.cin_real, J.cout,
+                      J.dw, J.db, J.accumulate, red);
   }
 }
 
@@ -1525,7 +1573,6 @@ extern "C" void mbk_conv0_row_set(int on) { g_conv0_row = on; }
 // partial holds nparts rows plus ceil(nparts / kReducePps) scratch rows after them
 extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int cin_real, int cout,
                                 float* dw, float* db, int accumulate, hipStream_t stream) {
-  constexpr int kReducePps = 32;
   const int row = cout * 9 * cin + cout;
   const dim3 cols((row + 63) / 64);
   if (nparts > 2 * kReducePps) {
@@ -1541,6 +1588,35 @@ extern "C" int mbk_wgrad_reduce(const float* partial, int nparts, int cin, int c
                        nparts, nparts, (float*)nullptr, cin, cin_real, cout, dw, db, accumulate);
   }
   return (int)hipGetLastError();
+}
+
+// jobs[0..n): each as one mbk_wgrad_reduce call, in <= 2 launches per 32 jobs.
+extern "C" int mbk_wgrad_reduce_batch(const MbkReduceJob* jobs, int n, hipStream_t stream) {
+  for (int j0 = 0; j0 < n; j0 += kMaxReduceJobs) {
+    const int nj = std::min(kMaxReduceJobs, n - j0);
+    ReduceBatch b{};
+    int cols = 1, splits = 1;
+    bool two = false;
+    for (int i = 0; i < nj; ++i) {
+      const MbkReduceJob& J = jobs[j0 + i];
+      if (!J.partial || !J.dw || J.nparts < 1 || J.cin < 1 || J.cout < 1 || J.cin_real > J.cin)
+        return (int)hipErrorInvalidValue;
+      b.j[i] = J;
+      const int row = J.cout * 9 * J.cin + J.cout;
+      cols = std::max(cols, (row + 63) / 64);
+      if (J.nparts > 2 * kReducePps) {
+        two = true;
+        splits = std::max(splits, (J.nparts + kReducePps - 1) / kReducePps);
+      }
+    }
+    hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(cols, splits, nj), dim3(256), 0, stream,
+                       b, 0);
+    if (two)
+      hipLaunchKernelGGL(wgrad_reduce_batch_kernel, dim3(cols, 1, nj), dim3(256), 0, stream, b, 1);
+    const int rc = (int)hipGetLastError();
+    if (rc) return rc;
+  }
+  return 0;
 }
 
 extern "C" int mbk_pool_bwd(const void* cfull, const void* dp, int N, int H, int W, int C,

@@ -1601,7 +1601,9 @@ extern "C" int64_t mbk_res_bwd16_partial_floats(int nparts) {
 
 // dx = conv0^T(conv1^T(g) * [u>0]) * [x>0] + g and both layers' weight / bias gradients.
 // partial: mbk_res_bwd16_partial_floats(nparts) floats. dw1/db1/dw0/db0: fp32 parameter
-// gradients [16][16][3][3] / [16] (overwritten).
+// gradients [16][16][3][3] / [16] (overwritten); dw1 == nullptr: only the partial rows are
+// written (layer 1's at partial, layer 0's at partial + partial_floats / 2) and the caller
+// reduces them later.
 extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* dx,
                              const void* w1t, const void* w0t, float* partial, int nparts,
                              float* dw1, float* db1, float* dw0, float* db0, int N, int H, int W,
@@ -1619,7 +1621,7 @@ extern "C" int mbk_res_bwd16(const void* x, const void* u, const void* g, void* 
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   hipLaunchKernelGGL(kfn, dim3(nparts), dim3(fast ? w88b::kPT : kThreads), sm, stream, a);
   int rc = (int)hipGetLastError();
-  if (rc) return rc;
+  if (rc || !dw1) return rc;  // dw1 == nullptr: the caller reduces (mbk_wgrad_reduce_batch)
   rc = mbk_wgrad_reduce(partial, nparts, C, C, C, dw1, db1, accumulate, stream);
   if (rc) return rc;
   return mbk_wgrad_reduce(partial + lstride, nparts, C, C, C, dw0, db0, accumulate, stream);
@@ -1648,7 +1650,8 @@ extern "C" int64_t mbk_res_bwd32_partial_floats(int nparts) {
 }
 
 // 32-channel block backward (see res_bwd32_kernel): dx and both layers' weight / bias
-// gradients dw1/db1/dw0/db0 (fp32 [32][32][3][3] / [32], overwritten).
+// gradients dw1/db1/dw0/db0 (fp32 [32][32][3][3] / [32], overwritten; dw1 == nullptr: partial
+// rows only, as mbk_res_bwd16).
 extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* dx,
                              const void* w1t, const void* w0t, float* partial, int nparts,
                              float* dw1, float* db1, float* dw0, float* db0, int N, int H, int W,
@@ -1666,7 +1669,7 @@ extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* 
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
   hipLaunchKernelGGL(kfn, dim3(nparts), dim3(kT32), sm, stream, a);
   int rc = (int)hipGetLastError();
-  if (rc) return rc;
+  if (rc || !dw1) return rc;  // dw1 == nullptr: the caller reduces (mbk_wgrad_reduce_batch)
   rc = mbk_wgrad_reduce(partial, nparts, C32, C32, C32, dw1, db1, accumulate, stream);
   if (rc) return rc;
   return mbk_wgrad_reduce(partial + lstride, nparts, C32, C32, C32, dw0, db0, accumulate, stream);

@@ -289,7 +289,7 @@ extern "C" int mbk_pool_conv_bwd(const void* dp, const void* pidx, const void* x
                     (bf16*)dx, partial, N};
   hipLaunchKernelGGL(pool_conv_bwd_s1_kernel, dim3(nparts), dim3(s1::kPT), s1::SMEM, stream, a);
   const int rc = (int)hipGetLastError();
-  if (rc) return rc;
+  if (rc || !dw) return rc;  // dw == nullptr: the caller reduces (mbk_wgrad_reduce_batch)
   return mbk_wgrad_reduce(partial, nparts, cin, cin, cout, dw, db, accumulate, stream);
 }
 

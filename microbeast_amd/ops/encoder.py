@@ -41,6 +41,12 @@ class _Job(ctypes.Structure):
                 ("cin", ctypes.c_int), ("cin_real", ctypes.c_int), ("cout", ctypes.c_int)]
 
 
+class _RJob(ctypes.Structure):  # conv.hip MbkReduceJob
+    _fields_ = [("partial", ctypes.c_void_p), ("dw", ctypes.c_void_p), ("db", ctypes.c_void_p),
+                ("nparts", ctypes.c_int), ("cin", ctypes.c_int), ("cin_real", ctypes.c_int),
+                ("cout", ctypes.c_int), ("accumulate", ctypes.c_int)]
+
+
 class _Job8(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("q", ctypes.c_void_p), ("scale", ctypes.c_void_p),
                 ("cin", ctypes.c_int), ("cin_real", ctypes.c_int), ("cout", ctypes.c_int)]
@@ -148,9 +154,13 @@ class HipEncoder:
         # the 16 -> 32 stage conv on 8x8 maps: pool backward, weight gradient and input
         # gradient in one launch (stagebwd.hip; no full-resolution gradient in HBM)
         self.fused_pool_conv_bwd = True
-        self._partial_rb = None
+        # one batched weight-gradient reduce per backward pass instead of one per layer
+        self.defer_reduce = True
+        # partial-row buffers of the weight gradients, one per layer (a backward pass defers
+        # every reduce to one batched launch at its end: mbk_wgrad_reduce_batch)
+        self._pbufs = {}
+        self._rjobs = None  # list while a backward pass defers its reduces
         self.packed_bwd = torch.zeros(max(boff, 1), dtype=torch.bfloat16, device=device)
-        self._partial = None
         # fp8 inference path (BASELINE config 5): e4m3 weights + per-channel scales
         self.fp8 = fp8
         # fp8 layers 1..14 in one fused launch (False: the 14 per-layer fp8 launches)
@@ -294,15 +304,40 @@ class HipEncoder:
             raise RuntimeError(f"conv_wgrad: unsupported shape {L}")
         row = L.cout * 9 * L.cin + L.cout
         need = (nparts + (nparts + 31) // 32) * row  # + the two-level reduce's scratch rows
-        if self._partial is None or self._partial.numel() < need or self._partial.device != x.device:
-            self._partial = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=x.device)
+        part = self._partials(L, need, x.device)
         k = N.kernels()
         st = N.stream_ptr()
         N.check(k.mbk_conv_wgrad(x.data_ptr(), int(L.bits), L.cin, L.cout, N.ptr(dy),
-                                 N.ptr(dp), N.ptr(pidx), self._partial.data_ptr(), nparts, n,
+                                 N.ptr(dp), N.ptr(pidx), part.data_ptr(), nparts, n,
                                  L.H, L.W, imgs, int(L.relu_in), st), "conv_wgrad")
-        N.check(k.mbk_wgrad_reduce(self._partial.data_ptr(), nparts, L.cin, L.cin_real, L.cout,
-                                   dw.data_ptr(), db.data_ptr(), 0, st), "wgrad_reduce")
+        self._reduce(part.data_ptr(), nparts, L, dw, db)
+
+    def _partials(self, L: ConvLayer, need: int, device) -> torch.Tensor:
+        """Layer L's partial-row buffer (one shared buffer when reduces are not deferred)."""
+        key = id(L) if self._rjobs is not None else None
+        b = self._pbufs.get(key)
+        if b is None or b.numel() < need or b.device != device:
+            b = torch.empty(max(need, 1 << 20), dtype=torch.float32, device=device)
+            self._pbufs[key] = b
+        return b
+
+    def _reduce(self, partial: int, nparts: int, L: ConvLayer, dw, db) -> None:
+        """Sum nparts partial rows at ``partial`` into L's fp32 dw / db: now, or queued for the
+        backward pass's one batched launch (bit-identical either way, conv.hip)."""
+        job = _RJob(partial, dw.data_ptr(), db.data_ptr(), nparts, L.cin, L.cin_real, L.cout, 0)
+        if self._rjobs is not None:
+            self._rjobs.append(job)
+            return
+        N.check(N.kernels().mbk_wgrad_reduce_batch(ctypes.byref(job), 1, N.stream_ptr()),
+                "wgrad_reduce_batch")
+
+    def _flush_reduces(self) -> None:
+        jobs, self._rjobs = self._rjobs, None
+        if jobs:
+            arr = (_RJob * len(jobs))(*jobs)
+            N.check(N.kernels().mbk_wgrad_reduce_batch(ctypes.cast(arr, ctypes.c_void_p),
+                                                      len(jobs), N.stream_ptr()),
+                    "wgrad_reduce_batch")
 
     def _res_fwd16(self, li: int, p: torch.Tensor, bs: list[torch.Tensor], stage=None):
         """Both residual blocks of a 16-channel stage in one launch (resblock.hip): returns
@@ -362,13 +397,13 @@ class HipEncoder:
         if nparts < 1:
             raise RuntimeError(f"res_bwd16: unsupported shape {H}x{W}")
         need = k.mbk_res_bwd16_partial_floats(nparts)
-        if self._partial_rb is None or self._partial_rb.numel() < need:
-            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        part = self._partials(L0, need, x.device)
         N.check(k.mbk_res_bwd16(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
-                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
-                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
-                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs, 0,
+                                base + 2 * L1.wb_off, base + 2 * L0.wb_off, part.data_ptr(),
+                                nparts, None, None, None, None, n, H, W, imgs, 0,
                                 N.stream_ptr()), "res_bwd16")
+        self._reduce(part.data_ptr(), nparts, L1, dw1, db1)
+        self._reduce(part.data_ptr() + 4 * (need // 2), nparts, L0, dw0, db0)
         return dx
 
     def _pool_conv_bwd(self, L: ConvLayer, dp, pidx, x, dw, db):
@@ -378,14 +413,13 @@ class HipEncoder:
         k = N.kernels()
         nparts = k.mbk_pool_conv_bwd_parts(n, L.cin, L.cout, L.H, L.W)
         need = k.mbk_pool_conv_bwd_partial_floats(nparts)
-        if self._partial_rb is None or self._partial_rb.numel() < need:
-            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        part = self._partials(L, need, x.device)
         dx = torch.empty_like(x)
         N.check(k.mbk_pool_conv_bwd(dp.data_ptr(), pidx.data_ptr(), x.data_ptr(),
                                     self.packed_bwd.data_ptr() + 2 * L.wb_off, dx.data_ptr(),
-                                    self._partial_rb.data_ptr(), nparts, dw.data_ptr(),
-                                    db.data_ptr(), n, L.cin, L.cout, L.H, L.W, 0,
-                                    N.stream_ptr()), "pool_conv_bwd")
+                                    part.data_ptr(), nparts, None, None, n, L.cin, L.cout, L.H,
+                                    L.W, 0, N.stream_ptr()), "pool_conv_bwd")
+        self._reduce(part.data_ptr(), nparts, L, dw, db)
         return dx
 
     def _res_bwd32(self, L0: ConvLayer, L1: ConvLayer, x, u, g, dw1, db1, dw0, db0):
@@ -402,13 +436,13 @@ class HipEncoder:
         if nparts < 1:
             raise RuntimeError(f"res_bwd32: unsupported shape {H}x{W}")
         need = k.mbk_res_bwd32_partial_floats(nparts)
-        if self._partial_rb is None or self._partial_rb.numel() < need:
-            self._partial_rb = torch.empty(need, dtype=torch.float32, device=x.device)
+        part = self._partials(L0, need, x.device)
         N.check(k.mbk_res_bwd32(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
-                                base + 2 * L1.wb_off, base + 2 * L0.wb_off,
-                                self._partial_rb.data_ptr(), nparts, dw1.data_ptr(),
-                                db1.data_ptr(), dw0.data_ptr(), db0.data_ptr(), n, H, W, imgs, 0,
+                                base + 2 * L1.wb_off, base + 2 * L0.wb_off, part.data_ptr(),
+                                nparts, None, None, None, None, n, H, W, imgs, 0,
                                 N.stream_ptr()), "res_bwd32")
+        self._reduce(part.data_ptr(), nparts, L1, dw1, db1)
+        self._reduce(part.data_ptr() + 4 * (need // 2), nparts, L0, dw0, db0)
         return dx
 
     # ------------------------------------------------------------ passes
@@ -483,6 +517,9 @@ class HipEncoder:
         grads = [grad_out(p) for p in params]
         nst = len(self.layers) // 5
         g = g.contiguous()
+        # the layers' partial-row reduces run as one batched launch at the end (30 small
+        # launches off the backward's critical path; bit-identical sums)
+        self._rjobs = [] if self.defer_reduce and g.is_cuda else None
         for s in range(nst - 1, -1, -1):
             li = 5 * s
             x, pidx, p, u0, y0, u1 = saved[6 * s:6 * s + 6]
@@ -531,6 +568,7 @@ class HipEncoder:
                                                  N.stream_ptr()), "pool_bwd_idx")
             self._wgrad(Ls, x, dc, grads[2 * li], grads[2 * li + 1])
             g = self._fwd(Ls, dc, None, dgrad=True) if s > 0 else None
+        self._flush_reduces()
         return grads
 
 

@@ -511,6 +511,37 @@ def test_pool_fused_stage0_wgrad_matches(cuda, n):
             assert torch.equal(a, b), i
 
 
+@pytest.mark.parametrize("n,fused", [(5, True), (700, True), (37, False)])
+def test_batched_deferred_reduce_bit_identical(cuda, n, fused):
+    """One mbk_wgrad_reduce_batch launch pair at the end of the backward pass (conv.hip) against
+    a reduce per layer right after its kernel: the same adds in the same order -> every
+    parameter gradient bit-identical (n=700: two-level reduces; fused=False: the per-layer
+    conv_wgrad path)."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(4)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(n, 256, seed=n + 3).to(cuda)
+    m.features(obs[:1])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    enc.fused_res_bwd = enc.fused_res_bwd32 = fused
+    grads = {}
+    for defer in (False, True):
+        enc.defer_reduce = defer
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(11)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[defer] = [p.grad.detach().clone() for p in params]
+    enc.fused_res_bwd = enc.fused_res_bwd32 = enc.defer_reduce = True
+    assert float(grads[True][0].abs().sum()) > 0
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("s,n", [(16, 37), (10, 21)])
 def test_fused_res_fwd16_bit_identical(cuda, s, n):
     """resblock.hip res_fwd16 (both 16-channel residual blocks in one launch) writes the
