@@ -28,7 +28,8 @@ def main():
                     help="no active-cell bitmap rows in the batch (the head counts from masks)")
     ap.add_argument("--set", action="append", default=[],
                     help="enc.<attr>=<int> / head.<attr>=<int>: set a variant attribute of the "
-                         "HIP encoder / sparse head before the first update (A/B in one process)")
+                         "HIP encoder / sparse head before the first update (A/B in one process); "
+                         "native.<setter>=<int>: call a kernel-library setter")
     a = ap.parse_args()
     import torch
 
@@ -64,6 +65,10 @@ def main():
     for kv in a.set:
         k, v = kv.split("=")
         obj, attr = k.split(".")
+        if obj == "native":  # a kernel-library setter: native.mbk_x_set=<int>
+            from microbeast_amd import _native as N
+            getattr(N.kernels(), attr)(int(v))
+            continue
         m = learner.model
         tgt = m._hip_enc if obj == "enc" else m._head(dev)
         assert hasattr(tgt, attr), kv
