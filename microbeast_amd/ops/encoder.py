@@ -147,6 +147,8 @@ class HipEncoder:
         self.fused_res_fwd32 = True
         # the stage-0 residual kernel also runs stage 1's conv + pool
         self.fused_stage_fwd = True
+        # the 32 -> 32 stage conv + pool on 4x4 maps: wave-owned images, no workgroup barriers
+        self.fused_pool_fwd4 = True
         # the observation layer's weight gradient expands the max-pool backward in its own
         # LDS staging (16-wide maps; bit-identical): no pool_bwd_idx launch, no 4.3 GB
         # full-resolution gradient in HBM per 524K-frame update
@@ -369,6 +371,16 @@ class HipEncoder:
                                       N.stream_ptr()), "res_fwd16_stage")
         return (*outs, (pn, pidx))
 
+    def _pool_conv_fwd4(self, L: ConvLayer, x, bias, pidx):
+        """Pooled stage conv 32 -> 32 on 4x4 maps with wave-owned images (stage2.hip):
+        bit-identical to the pooled conv_fwd launch."""
+        n = x.shape[0]
+        y = torch.empty(n, 2, 2, L.cout, dtype=torch.bfloat16, device=x.device)
+        N.check(N.kernels().mbk_pool_conv_fwd4(x.data_ptr(), self.packed_fwd.data_ptr() + 2 * L.w_off,
+                                               bias.data_ptr(), y.data_ptr(), N.ptr(pidx), n,
+                                               N.stream_ptr()), "pool_conv_fwd4")
+        return y
+
     def _res_blk32(self, l0: int, x: torch.Tensor, bs: list[torch.Tensor]):
         """One 32-channel residual block (layers l0, l0+1) in one launch (resblock.hip):
         returns (u, y), bit-identical to two conv_fwd launches."""
@@ -484,6 +496,9 @@ class HipEncoder:
             if nxt is not None:  # computed by the previous stage's fused residual kernel
                 p, pidx = nxt
                 nxt = None
+            elif (self.fused_pool_fwd4 and x.is_cuda and L.cin == 32 and L.cout == 32
+                  and L.pool and not L.bits and L.H == 4 and L.W == 4):
+                p = self._pool_conv_fwd4(L, x, bs[li].detach(), pidx)
             else:
                 p = self._fwd(L, x, bs[li].detach(), pool_idx=pidx)
             if self.fused_res_fwd and L.cout == 16 and p.is_cuda:

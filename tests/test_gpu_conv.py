@@ -590,6 +590,31 @@ def test_fused_stage_conv_in_res_fwd16_bit_identical(cuda, s, n):
         assert torch.equal(a, b), i
 
 
+@pytest.mark.parametrize("s,n", [(16, 37), (14, 21), (16, 1), (16, 1001)])
+def test_pool_conv_fwd4_bit_identical(cuda, s, n):
+    """stage2.hip (the 32 -> 32 stage conv + max-pool on 4x4 maps, wave-owned images) writes
+    the same pooled output and argmax bytes as the pooled conv_fwd launch; every other saved
+    activation and the trunk output follow (odd n: a pair's lone last image)."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encoder_params
+    torch.manual_seed(8)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(n, s * s, seed=5).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = [p.detach() for p in encoder_params(m.network, 3)]
+    outs = {}
+    for fused in (False, True):
+        enc.fused_pool_fwd4 = fused
+        y, saved = enc.forward(obs, params, save=True)
+        torch.cuda.synchronize()
+        outs[fused] = [t.clone() for t in saved if torch.is_tensor(t)] + [y.clone()]
+    enc.fused_pool_fwd4 = True
+    assert len(outs[False]) == len(outs[True])
+    for i, (a, b) in enumerate(zip(outs[False], outs[True])):
+        assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 9)])
 def test_fused_res_blk32_bit_identical(cuda, s, n):
     """resblock.hip res_blk32 (one 32-channel residual block per launch, weights of both
