@@ -593,15 +593,16 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  uint4 px[2], pu[2], pg[2];
+  // (named registers: the indexed [2] arrays of the first form went to scratch)
+  uint4 px0, px1, pu0, pu1, pg0, pg1;
   auto fetch = [&](int im) {
-    const size_t o = (size_t)im * HW * 2;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      px[k] = ((const uint4*)a.x)[o + lane + 64 * k];
-      pu[k] = ((const uint4*)a.u)[o + lane + 64 * k];
-      pg[k] = ((const uint4*)a.g)[o + lane + 64 * k];
-    }
+    const size_t o = (size_t)im * HW * 2 + lane;
+    px0 = ((const uint4*)a.x)[o];
+    px1 = ((const uint4*)a.x)[o + 64];
+    pu0 = ((const uint4*)a.u)[o];
+    pu1 = ((const uint4*)a.u)[o + 64];
+    pg0 = ((const uint4*)a.g)[o];
+    pg1 = ((const uint4*)a.g)[o + 64];
   };
   if (first < a.N) fetch(first);
   int it = 1;
@@ -610,12 +611,12 @@ __global__ __launch_bounds__(w88b::kPT) void res_bwd16_w88_kernel(ResBwdArgs a) 
     char* T = R + b * SET;
     int* f = fl + 3 * b;
     if (it > NSET) wait_flag(f + 2, it - NSET);  // the D-wave is done with this set's last image
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      *(uint4*)(T + TX + so[k]) = relu8(px[k]);
-      *(uint4*)(T + TU + so[k]) = relu8(pu[k]);
-      *(uint4*)(T + TG + so[k]) = pg[k];
-    }
+    *(uint4*)(T + TX + so[0]) = relu8(px0);
+    *(uint4*)(T + TU + so[0]) = relu8(pu0);
+    *(uint4*)(T + TG + so[0]) = pg0;
+    *(uint4*)(T + TX + so[1]) = relu8(px1);
+    *(uint4*)(T + TU + so[1]) = relu8(pu1);
+    *(uint4*)(T + TG + so[1]) = pg1;
     set_flag(f, it, lane);  // staged
     if (img + step < a.N) fetch(img + step);
     wave_lds_order();

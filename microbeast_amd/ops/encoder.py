@@ -424,7 +424,7 @@ class HipEncoder:
         n = x.shape[0]
         k = N.kernels()
         nparts = k.mbk_pool_conv_bwd_parts(n, L.cin, L.cout, L.H, L.W)
-        need = k.mbk_pool_conv_bwd_partial_floats(nparts)
+        need = k.mbk_pool_conv_bwd_partial_floats(nparts, L.cin, L.cout)
         part = self._partials(L, need, x.device)
         dx = torch.empty_like(x)
         N.check(k.mbk_pool_conv_bwd(dp.data_ptr(), pidx.data_ptr(), x.data_ptr(),
