@@ -1375,13 +1375,30 @@ __global__ __launch_bounds__(256) void head_dx_value_kernel(const bf16* __restri
       if (q >= nch) break;
       const int p = pc[q];
       uint64_t m = __ballot(p >= 0);
+      // up to 4 pair rows in flight per trip (one dependent HBM latency per 4 pairs instead
+      // of per pair), added in the same order
       while (m) {
-        const int b = __builtin_ctzll(m);
-        m &= m - 1;
-        const int pp = __shfl(p, b);
-        const uint2 v = ((const uint2*)(dXp + (size_t)pp * KD))[lane];  // 4 bf16
-        acc.x += __uint_as_float(v.x << 16); acc.y += __uint_as_float(v.x & 0xFFFF0000u);
-        acc.z += __uint_as_float(v.y << 16); acc.w += __uint_as_float(v.y & 0xFFFF0000u);
+        int pp[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pp[j] = -1;
+          if (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            pp[j] = __shfl(p, b);
+          }
+        }
+        uint2 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = pp[j] >= 0 ? ((const uint2*)(dXp + (size_t)pp[j] * KD))[lane]  // 4 bf16
+                            : make_uint2(0u, 0u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (pp[j] < 0) break;
+          acc.x += __uint_as_float(v[j].x << 16); acc.y += __uint_as_float(v[j].x & 0xFFFF0000u);
+          acc.z += __uint_as_float(v[j].y << 16); acc.w += __uint_as_float(v[j].y & 0xFFFF0000u);
+        }
       }
     }
     const float hj[4] = {__uint_as_float(hv.x << 16), __uint_as_float(hv.x & 0xFFFF0000u),

@@ -1226,6 +1226,101 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
 
 #undef MBK_RB32_FETCH
 
+// The same block on 2x2 maps (IMPALA stage 2 at 16x16) with wave-owned image quads: one
+// 16-pixel MFMA block is 4 whole images, so a wave stages its quad (1 KB: one uint4 per
+// lane, prefetched a quad ahead), runs conv0 -> relu(u) in its own LDS tile -> conv1 + the
+// residual, and never meets a workgroup barrier (the round form spent ~2.8 us per 16-image
+// round in three barriers and its staging for 36 MFMAs per wave). Both layers' weights stay in
+// VGPRs for the launch; chains and epilogues are res_blk32_kernel's, so bit-identical to it.
+namespace w2 {
+constexpr int NW = 4, kPT = 64 * NW;
+// halo'd 4x4 tile per image, 64-byte pixels in 288-byte rows, images 1152 bytes apart: the
+// 16 pixels of a tap read's lane groups land on distinct bank slots (tools/lds_banks.py
+// model: 1.0 cycles per group vs 4.0 for 256 / 1024)
+constexpr int PB = 64, RS = 288, IS = 4 * RS;
+constexpr int TB = 4 * IS;                         // a quad's tile
+constexpr int SLICE = 2 * TB;                      // x, relu(u)
+constexpr int SMEM = NW * SLICE;
+}  // namespace w2
+
+__global__ __launch_bounds__(w2::kPT) void res_blk32_w2_kernel(ResBlk32Args a) {
+  using namespace w2;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  char* Tx = smem + wave * SLICE;
+  char* Tu = Tx + TB;
+  for (int e = lane; e < SLICE / 16; e += 64) ((uint4*)Tx)[e] = make_uint4(0, 0, 0, 0);
+  Frag8 w[2][NCH32][NB32];
+  float bv[2][NB32][4];
+#pragma unroll
+  for (int l = 0; l < 2; ++l)
+#pragma unroll
+    for (int nb = 0; nb < NB32; ++nb) {
+      const uint4* wp = (const uint4*)(a.w[l] + (size_t)(nb * 16 + li) * NCH32 * 32 + g * 8);
+#pragma unroll
+      for (int c = 0; c < NCH32; ++c) w[l][c][nb].u = wp[c * 4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[l][nb][i] = a.b[l][nb * 16 + 4 * g + i];
+    }
+  // MFMA lanes: pixel li = image li / 4, (y, x) = ((li / 2) % 2, li % 2); K chunk 8g..
+  const int pim = li >> 2, py = (li >> 1) & 1, pxx = li & 1;
+  const int pbase = pim * IS + py * RS + pxx * PB;  // tap (0, 0) of the halo'd tile
+  const int pout = pbase + RS + PB;                 // the pixel itself
+  // staging lanes: uint4 #lane of the quad = image lane / 16, pixel (lane / 4) % 4, chunk lane % 4
+  const int sp = (lane >> 2) & 3;
+  const int sofs = (lane >> 4) * IS + ((sp >> 1) + 1) * RS + ((sp & 1) + 1) * PB + 16 * (lane & 3);
+  const int nq = (a.N + 3) >> 2;
+  const int step = gridDim.x * NW;
+  const int first = blockIdx.x * NW + wave;
+  uint4 pf;
+  auto fetch = [&](int q) {
+    const int e = q * 64 + lane;  // uint4 index (4 per pixel, 16 per image)
+    pf = e < a.N * 16 ? ((const uint4*)a.x)[e] : make_uint4(0, 0, 0, 0);
+  };
+  wave_lds_order();
+  if (first < nq) fetch(first);
+  for (int q = first; q < nq; q += step) {
+    *(uint4*)(Tx + sofs) = pf;
+    if (q + step < nq) fetch(q + step);
+    wave_lds_order();
+    const size_t m = (size_t)q * 16 + li;  // global pixel of this lane
+    const bool valid = m < (size_t)a.N * 4;
+#pragma unroll
+    for (int l = 0; l < 2; ++l) {
+      const char* src = (l == 0 ? Tx : Tu) + pbase;
+      f32x4 acc[NB32];
+#pragma unroll
+      for (int nb = 0; nb < NB32; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NCH32; ++c) {
+        Frag8 av;
+        av.u = *(const uint4*)(src + (c / 3) * RS + (c % 3) * PB + 16 * g);
+        if (l == 0) av.u = relu8(av.u);  // Tu already holds relu(u)
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb)
+          acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[l][c][nb].v, av.v, acc[nb], 0, 0, 0);
+      }
+      bf16* gout = l == 0 ? a.u : a.y;
+#pragma unroll
+      for (int nb = 0; nb < NB32; ++nb) {
+        const int co0 = nb * 16 + 4 * g;
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = acc[nb][i] + bv[l][nb][i];
+        if (l == 1) {
+          const uint2 ad = *(const uint2*)(Tx + pout + co0 * 2);
+          v[0] += lo_f(ad.x); v[1] += hi_f(ad.x); v[2] += lo_f(ad.y); v[3] += hi_f(ad.y);
+        }
+        const uint2 out = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if (valid) *(uint2*)(gout + m * C32 + co0) = out;
+        if (l == 0) *(uint2*)(Tu + pout + co0 * 2) = make_uint2(relu2(out.x), relu2(out.y));
+      }
+      wave_lds_order();
+    }
+  }
+}
+
 // ------------------------------------------------------------------ fused backward, 32 ch
 // Backward of one 32-channel residual block (stages 1-2), the res_bwd16 dataflow
 // (x, u, g staged once; du kept in LDS; dx written once) with the 32-channel operands split
@@ -1678,6 +1773,31 @@ extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* 
 
 // One 32-channel residual block's forward (see res_blk32_kernel): u = conv0(relu x),
 // y = x + conv1(relu u), bit-identical to two conv_fwd<32, 32> launches.
+// One 32-channel residual block on 2x2 maps with wave-owned image quads (res_blk32_w2_kernel):
+// bit-identical to mbk_res_blk32_fwd.
+extern "C" int mbk_res_blk32_fwd_w2(const void* x, void* u, void* y, const void* const* w,
+                                    const float* const* b, int N, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if ((((uintptr_t)x | (uintptr_t)w[0] | (uintptr_t)w[1]) & 15) || (((uintptr_t)u | (uintptr_t)y) & 7))
+    return (int)hipErrorInvalidValue;
+  static int cus = 0, per = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)res_blk32_w2_kernel,
+                                                     w2::kPT, w2::SMEM) != hipSuccess || per < 1)
+      per = 1;
+  }
+  ResBlk32Args a{(const bf16*)x, (bf16*)u, (bf16*)y, {(const bf16*)w[0], (const bf16*)w[1]},
+                 {b[0], b[1]}, N, 2, 2, 4};
+  const int nq = (N + 3) / 4, groups = (nq + w2::NW - 1) / w2::NW;
+  hipLaunchKernelGGL(res_blk32_w2_kernel, dim3(std::max(1, std::min(groups, cus * per))),
+                     dim3(w2::kPT), w2::SMEM, stream, a);
+  return (int)hipGetLastError();
+}
+
 extern "C" int mbk_res_blk32_fwd(const void* x, void* u, void* y, const void* const* w,
                                  const float* const* b, int N, int H, int W, int imgs,
                                  hipStream_t stream) {
