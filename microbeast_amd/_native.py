@@ -154,7 +154,8 @@ _SIGS = {
     "mbk_res_blk32_fwd": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                           c_void_p],
     "mbk_pool_conv_fwd4": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
-    "mbk_res_blk32_fwd_w2": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
+    "mbk_res_blk32_fwd_wave": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                               c_int, c_void_p],
     "mbk_res_bwd16_partial_floats": [c_int],
     "mbk_res_bwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

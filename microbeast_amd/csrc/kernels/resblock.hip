@@ -1226,31 +1226,35 @@ __global__ __launch_bounds__(kThreads) void res_blk32_kernel(ResBlk32Args a) {
 
 #undef MBK_RB32_FETCH
 
-// The same block on 2x2 maps (IMPALA stage 2 at 16x16) with wave-owned image quads: one
-// 16-pixel MFMA block is 4 whole images, so a wave stages its quad (1 KB: one uint4 per
-// lane, prefetched a quad ahead), runs conv0 -> relu(u) in its own LDS tile -> conv1 + the
-// residual, and never meets a workgroup barrier (the round form spent ~2.8 us per 16-image
-// round in three barriers and its staging for 36 MFMAs per wave). Both layers' weights stay in
-// VGPRs for the launch; chains and epilogues are res_blk32_kernel's, so bit-identical to it.
-namespace w2 {
+// The same block on 4x4 and 2x2 maps (IMPALA stages 1 / 2 at 16x16) with wave-owned 16-pixel
+// blocks: one MFMA block is one 4x4 image or four 2x2 images, so a wave stages its block
+// (1 KB: one uint4 per lane, prefetched a block ahead), runs conv0 -> relu(u) in its own LDS
+// tile -> conv1 + the residual, and never meets a workgroup barrier (the round form spent most
+// of its time in three barriers per round and its staging: ~2.8 us per 16-image round on 2x2
+// maps for 36 MFMAs per wave). Both layers' weights stay in VGPRs for the launch; chains and
+// epilogues are res_blk32_kernel's, so bit-identical to it.
+namespace rbw {
 constexpr int NW = 4, kPT = 64 * NW;
-// halo'd 4x4 tile per image, 64-byte pixels in 288-byte rows, images 1152 bytes apart: the
-// 16 pixels of a tap read's lane groups land on distinct bank slots (tools/lds_banks.py
-// model: 1.0 cycles per group vs 4.0 for 256 / 1024)
-constexpr int PB = 64, RS = 288, IS = 4 * RS;
-constexpr int TB = 4 * IS;                         // a quad's tile
-constexpr int SLICE = 2 * TB;                      // x, relu(u)
-constexpr int SMEM = NW * SLICE;
-}  // namespace w2
+constexpr int PB = 64;  // 64-byte pixels
+// MW = 4: one halo'd 6x6 image, 416-byte rows; MW = 2: four halo'd 4x4 images, 288-byte rows,
+// 1152 bytes apart. Both put the 16 pixels of a tap read's lane groups on distinct bank slots
+// (tools/lds_banks.py model: 1.0 cycles per group; 4.0 for 256-byte rows / 1024-byte images).
+template <int MW> struct Geo;
+template <> struct Geo<4> { static constexpr int RS = 416, IS = 0, TB = (5 * 416 + 6 * 64 + 15) & ~15; };
+template <> struct Geo<2> { static constexpr int RS = 288, IS = 4 * 288, TB = 4 * 4 * 288; };
+template <int MW> constexpr int smem() { return NW * 2 * Geo<MW>::TB; }
+}  // namespace rbw
 
-__global__ __launch_bounds__(w2::kPT) void res_blk32_w2_kernel(ResBlk32Args a) {
-  using namespace w2;
+template <int MW>
+__global__ __launch_bounds__(rbw::kPT) void res_blk32_wave_kernel(ResBlk32Args a) {
+  using namespace rbw;
+  constexpr int RS = Geo<MW>::RS, IS = Geo<MW>::IS, TB = Geo<MW>::TB;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
-  char* Tx = smem + wave * SLICE;
+  char* Tx = smem + wave * 2 * TB;
   char* Tu = Tx + TB;
-  for (int e = lane; e < SLICE / 16; e += 64) ((uint4*)Tx)[e] = make_uint4(0, 0, 0, 0);
+  for (int e = lane; e < 2 * TB / 16; e += 64) ((uint4*)Tx)[e] = make_uint4(0, 0, 0, 0);
   Frag8 w[2][NCH32][NB32];
   float bv[2][NB32][4];
 #pragma unroll
@@ -1263,20 +1267,23 @@ __global__ __launch_bounds__(w2::kPT) void res_blk32_w2_kernel(ResBlk32Args a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) bv[l][nb][i] = a.b[l][nb * 16 + 4 * g + i];
     }
-  // MFMA lanes: pixel li = image li / 4, (y, x) = ((li / 2) % 2, li % 2); K chunk 8g..
-  const int pim = li >> 2, py = (li >> 1) & 1, pxx = li & 1;
-  const int pbase = pim * IS + py * RS + pxx * PB;  // tap (0, 0) of the halo'd tile
-  const int pout = pbase + RS + PB;                 // the pixel itself
-  // staging lanes: uint4 #lane of the quad = image lane / 16, pixel (lane / 4) % 4, chunk lane % 4
-  const int sp = (lane >> 2) & 3;
-  const int sofs = (lane >> 4) * IS + ((sp >> 1) + 1) * RS + ((sp & 1) + 1) * PB + 16 * (lane & 3);
-  const int nq = (a.N + 3) >> 2;
+  // pixel p (0..15) of the block: image, row, column inside the halo'd tile set
+  auto pix = [](int p) {
+    return MW == 4 ? (p >> 2) * RS + (p & 3) * PB
+                   : (p >> 2) * IS + ((p >> 1) & 1) * RS + (p & 1) * PB;
+  };
+  const int pbase = pix(li);        // MFMA lanes: pixel li, tap (0, 0) of its window
+  const int pout = pbase + RS + PB;  // the pixel itself
+  // staging lanes: uint4 #lane of the block = pixel lane / 4, 16-byte chunk lane % 4
+  const int sofs = pix(lane >> 2) + RS + PB + 16 * (lane & 3);
+  const int64_t npix = (int64_t)a.N * MW * MW;
+  const int nq = (int)((npix + 15) >> 4);
   const int step = gridDim.x * NW;
   const int first = blockIdx.x * NW + wave;
   uint4 pf;
   auto fetch = [&](int q) {
-    const int e = q * 64 + lane;  // uint4 index (4 per pixel, 16 per image)
-    pf = e < a.N * 16 ? ((const uint4*)a.x)[e] : make_uint4(0, 0, 0, 0);
+    const int64_t e = (int64_t)q * 64 + lane;  // uint4 index (4 per pixel)
+    pf = e < npix * 4 ? ((const uint4*)a.x)[e] : make_uint4(0, 0, 0, 0);
   };
   wave_lds_order();
   if (first < nq) fetch(first);
@@ -1284,8 +1291,8 @@ __global__ __launch_bounds__(w2::kPT) void res_blk32_w2_kernel(ResBlk32Args a) {
     *(uint4*)(Tx + sofs) = pf;
     if (q + step < nq) fetch(q + step);
     wave_lds_order();
-    const size_t m = (size_t)q * 16 + li;  // global pixel of this lane
-    const bool valid = m < (size_t)a.N * 4;
+    const int64_t m = (int64_t)q * 16 + li;  // global pixel of this lane
+    const bool valid = m < npix;
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
       const char* src = (l == 0 ? Tx : Tu) + pbase;
@@ -1773,28 +1780,37 @@ extern "C" int mbk_res_bwd32(const void* x, const void* u, const void* g, void* 
 
 // One 32-channel residual block's forward (see res_blk32_kernel): u = conv0(relu x),
 // y = x + conv1(relu u), bit-identical to two conv_fwd<32, 32> launches.
-// One 32-channel residual block on 2x2 maps with wave-owned image quads (res_blk32_w2_kernel):
-// bit-identical to mbk_res_blk32_fwd.
-extern "C" int mbk_res_blk32_fwd_w2(const void* x, void* u, void* y, const void* const* w,
-                                    const float* const* b, int N, hipStream_t stream) {
+// One 32-channel residual block on 4x4 or 2x2 maps with wave-owned 16-pixel blocks
+// (res_blk32_wave_kernel): bit-identical to mbk_res_blk32_fwd.
+extern "C" int mbk_res_blk32_fwd_wave(const void* x, void* u, void* y, const void* const* w,
+                                      const float* const* b, int N, int H, int W,
+                                      hipStream_t stream) {
   if (N <= 0) return 0;
+  if (H != W || (W != 4 && W != 2)) return (int)hipErrorInvalidValue;
   if ((((uintptr_t)x | (uintptr_t)w[0] | (uintptr_t)w[1]) & 15) || (((uintptr_t)u | (uintptr_t)y) & 7))
     return (int)hipErrorInvalidValue;
-  static int cus = 0, per = 0;
+  const void* kfn = W == 4 ? (const void*)res_blk32_wave_kernel<4> : (const void*)res_blk32_wave_kernel<2>;
+  const int sm = W == 4 ? rbw::smem<4>() : rbw::smem<2>();
+  static int cus = 0, per4 = 0, per2 = 0;
   if (!cus) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)res_blk32_w2_kernel,
-                                                     w2::kPT, w2::SMEM) != hipSuccess || per < 1)
-      per = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, (const void*)res_blk32_wave_kernel<4>,
+                                                     rbw::kPT, rbw::smem<4>()) != hipSuccess || per4 < 1)
+      per4 = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, (const void*)res_blk32_wave_kernel<2>,
+                                                     rbw::kPT, rbw::smem<2>()) != hipSuccess || per2 < 1)
+      per2 = 1;
   }
   ResBlk32Args a{(const bf16*)x, (bf16*)u, (bf16*)y, {(const bf16*)w[0], (const bf16*)w[1]},
-                 {b[0], b[1]}, N, 2, 2, 4};
-  const int nq = (N + 3) / 4, groups = (nq + w2::NW - 1) / w2::NW;
-  hipLaunchKernelGGL(res_blk32_w2_kernel, dim3(std::max(1, std::min(groups, cus * per))),
-                     dim3(w2::kPT), w2::SMEM, stream, a);
+                 {b[0], b[1]}, N, H, W, 1};
+  const int64_t nq = ((int64_t)N * H * W + 15) / 16;
+  const int64_t groups = (nq + rbw::NW - 1) / rbw::NW;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, (int64_t)cus * (W == 4 ? per4 : per2)));
+  void* args[] = {(void*)&a};
+  (void)hipLaunchKernel(kfn, dim3(grid), dim3(rbw::kPT), args, sm, stream);
   return (int)hipGetLastError();
 }
 

@@ -149,8 +149,8 @@ class HipEncoder:
         self.fused_stage_fwd = True
         # the 32 -> 32 stage conv + pool on 4x4 maps: wave-owned images, no workgroup barriers
         self.fused_pool_fwd4 = True
-        # 32-channel residual blocks on 2x2 maps with wave-owned image quads
-        self.fused_res_blk32_w2 = True
+        # 32-channel residual blocks on 4x4 / 2x2 maps with wave-owned 16-pixel blocks
+        self.fused_res_blk32_wave = True
         # the observation layer's weight gradient expands the max-pool backward in its own
         # LDS staging (16-wide maps; bit-identical): no pool_bwd_idx launch, no 4.3 GB
         # full-resolution gradient in HBM per 524K-frame update
@@ -391,11 +391,11 @@ class HipEncoder:
         base = self.packed_fwd.data_ptr()
         wp = (ctypes.c_void_p * 2)(*[base + 2 * self.layers[l0 + j].w_off for j in range(2)])
         bp = (ctypes.c_void_p * 2)(*[bs[l0 + j].detach().data_ptr() for j in range(2)])
-        if self.fused_res_blk32_w2 and H == 2 and W == 2:
-            N.check(N.kernels().mbk_res_blk32_fwd_w2(x.data_ptr(), u.data_ptr(), y.data_ptr(),
-                                                     ctypes.cast(wp, ctypes.c_void_p),
-                                                     ctypes.cast(bp, ctypes.c_void_p), n,
-                                                     N.stream_ptr()), "res_blk32_fwd_w2")
+        if self.fused_res_blk32_wave and H == W and W in (2, 4):
+            N.check(N.kernels().mbk_res_blk32_fwd_wave(x.data_ptr(), u.data_ptr(), y.data_ptr(),
+                                                       ctypes.cast(wp, ctypes.c_void_p),
+                                                       ctypes.cast(bp, ctypes.c_void_p), n, H, W,
+                                                       N.stream_ptr()), "res_blk32_fwd_wave")
             return u, y
         imgs = max(1, min(16, (80 * 1024) // (2 * (H + 2) * (W + 2) * 80)))
         N.check(N.kernels().mbk_res_blk32_fwd(x.data_ptr(), u.data_ptr(), y.data_ptr(),

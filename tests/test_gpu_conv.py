@@ -617,25 +617,26 @@ def test_pool_conv_fwd4_bit_identical(cuda, s, n):
         assert torch.equal(a, b), i
 
 
-@pytest.mark.parametrize("n", [1, 3, 37, 1002])
-def test_res_blk32_w2_bit_identical(cuda, n):
-    """The wave-owned 2x2-map residual block (image quads, no workgroup barriers) writes the
-    same u and y as the round-based res_blk32 kernel (n % 4 != 0: a partial last quad)."""
+@pytest.mark.parametrize("s,n", [(16, 1), (16, 3), (16, 37), (16, 1002), (14, 21)])
+def test_res_blk32_wave_bit_identical(cuda, s, n):
+    """The wave-owned 32-channel residual blocks (4x4 maps: one image per 16-pixel block; 2x2
+    maps: image quads; no workgroup barriers) write the same u and y as the round-based
+    res_blk32 kernel (n % 4 != 0: a partial last quad; 14x14: 4x4 and 2x2 stage maps)."""
     from microbeast_amd.models.agent import Agent
     from microbeast_amd.ops.encoder import encoder_params
     torch.manual_seed(9)
-    m = Agent((16, 16, 27)).to(cuda)
-    obs = _random_obs_bits(n, 256, seed=7).to(cuda)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(n, s * s, seed=7).to(cuda)
     m.features(obs)
     enc = m._hip_enc
     params = [p.detach() for p in encoder_params(m.network, 3)]
     outs = {}
     for fused in (False, True):
-        enc.fused_res_blk32_w2 = fused
+        enc.fused_res_blk32_wave = fused
         y, saved = enc.forward(obs, params, save=True)
         torch.cuda.synchronize()
         outs[fused] = [t.clone() for t in saved if torch.is_tensor(t)] + [y.clone()]
-    enc.fused_res_blk32_w2 = True
+    enc.fused_res_blk32_wave = True
     for i, (a, b) in enumerate(zip(outs[False], outs[True])):
         assert torch.equal(a, b), i
 
