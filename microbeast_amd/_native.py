@@ -156,6 +156,9 @@ _SIGS = {
     "mbk_pool_conv_fwd4": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p],
     "mbk_res_blk32_fwd_wave": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
                                c_int, c_void_p],
+    "mbk_res_bwd32_team_parts": [c_int, c_int, c_int],
+    "mbk_res_bwd32_team": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                           c_int, c_int, c_int, c_int, c_void_p],
     "mbk_res_bwd16_partial_floats": [c_int],
     "mbk_res_bwd16": [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                       c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,

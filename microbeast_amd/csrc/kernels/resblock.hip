@@ -1610,6 +1610,241 @@ __global__ __launch_bounds__(kT32) void res_bwd32_kernel(ResBwd32Args a) {
   }
 }
 
+// ------------------------------------------------------------------ team backward, 32 ch
+// The 32-channel block backward on 4x4 / 2x2 maps (IMPALA stages 1 / 2 at 16x16) without
+// workgroup barriers. res_bwd32_kernel ran rounds of 14-29 images with two barriers each (on
+// 2x2 maps ~5 us per round for ~36 MFMAs per wave). One wave per role cannot hold a layer's
+// 36 weight-gradient tiles next to the dgrad weights, so a TEAM of four waves shares a stream
+// of 32-pixel items (two 16-pixel groups: two 4x4 images or eight 2x2 images), each role with
+// its own operands in VGPRs for the whole launch:
+//   W1 (stager): stages relu(x), relu(u), g of the item (prefetched an item ahead); dW1 +=
+//       relu(u) (x) g over the item's 32 pixels (36 tiles + the bias column by an all-ones MFMA)
+//   D1: du = conv1^T(g) * [u > 0] -> the item's du tiles (conv1 dgrad weights)
+//   D0: dx = conv0^T(du) * [x > 0] + g -> HBM (conv0 dgrad weights)
+//   W0: dW0 += relu(x) (x) du (36 tiles + bias)
+// over NSET tile sets per team, synchronised by per-team LDS flags holding iteration numbers
+// (staged / du written / D0 done / W0 done): a wave's LDS writes complete in issue order, so a
+// flag written after the data publishes it, and W1 re-stages a set only once D0 and W0 are done
+// with it (D1 finished reading it before it wrote du). Every role walks the same item sequence
+// and each wait is on a flag another role sets in that same iteration, so every wave reaches
+// the end. du / dx: res_bwd32's chains and epilogues (bit-identical); weight gradients: one
+// partial row per team (fp32 order differs from the round kernel's).
+namespace rbt {
+constexpr int NT = 2, kPT = 64 * 4 * NT;  // teams per workgroup, threads
+constexpr int NSET = 2;
+constexpr int PB = 64;
+template <int MW> constexpr int TB() { return rbw::Geo<MW>::TB; }  // one 16-pixel group's tile
+// a set: g, relu(u), relu(x), du tiles of the item's two groups
+template <int MW> constexpr int SETB() { return 4 * 2 * TB<MW>(); }
+template <int MW> constexpr int TEAMB() { return NSET * SETB<MW>(); }
+constexpr int FLAGS_PER_TEAM = 4 * NSET;
+template <int MW> constexpr int smem() { return NT * TEAMB<MW>() + NT * FLAGS_PER_TEAM * 4; }
+static_assert(smem<2>() <= 160 * 1024 && smem<4>() <= 160 * 1024, "LDS");
+}  // namespace rbt
+
+template <int MW>
+__global__ __launch_bounds__(rbt::kPT) void res_bwd32_team_kernel(ResBwd32Args a) {
+  using namespace rbt;
+  constexpr int RS = rbw::Geo<MW>::RS, IS = rbw::Geo<MW>::IS, T = TB<MW>();
+  constexpr int OG = 0, OU = 2 * T, OX = 4 * T, OD = 6 * T;  // tensor offsets in a set
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int team = wave >> 2, role = wave & 3;  // 0 W1, 1 D1, 2 D0, 3 W0
+  char* base = smem + team * TEAMB<MW>();
+  int* fl = (int*)(smem + NT * TEAMB<MW>()) + team * FLAGS_PER_TEAM;  // [kind][set]
+  int* f_staged = fl;
+  int* f_du = fl + NSET;
+  int* f_d0 = fl + 2 * NSET;
+  int* f_w0 = fl + 3 * NSET;
+  for (int e = tid; e < NT * TEAMB<MW>() / 16; e += kPT) ((uint4*)smem)[e] = make_uint4(0, 0, 0, 0);
+  if (tid < NT * FLAGS_PER_TEAM) ((int*)(smem + NT * TEAMB<MW>()))[tid] = 0;
+  __syncthreads();  // zeroed tiles (halos) and flags
+  auto pix = [](int p) {  // pixel p (0..15) of a group: window top-left inside its tile
+    return MW == 4 ? (p >> 2) * RS + (p & 3) * PB
+                   : (p >> 2) * IS + ((p >> 1) & 1) * RS + (p & 1) * PB;
+  };
+  const int64_t npix = (int64_t)a.N * MW * MW;
+  const int nitems = (int)((npix + 31) >> 5);
+  const int step = gridDim.x * NT;
+  const int first = blockIdx.x * NT + team;
+  const int pbase = pix(li), pin = pbase + RS + PB;  // dgrad lanes: pixel li of a group
+
+  if (role == 1 || role == 2) {
+    // ---- D1 / D0: dgrad weights (lane: rows nb * 16 + li, chunk c, elements 8g..)
+    Frag8 w[NCH32][NB32];
+    {
+      const bf16* wt = role == 1 ? a.w1t : a.w0t;
+#pragma unroll
+      for (int nb = 0; nb < NB32; ++nb) {
+        const uint4* wp = (const uint4*)(wt + (size_t)(nb * 16 + li) * NCH32 * 32 + g * 8);
+#pragma unroll
+        for (int c = 0; c < NCH32; ++c) w[c][nb].u = wp[c * 4];
+      }
+    }
+    int it = 0;
+    for (int item = first; item < nitems; item += step, ++it) {
+      const int b = it % NSET;
+      char* S = base + b * SETB<MW>();
+      wait_flag(role == 1 ? f_staged + b : f_du + b, it + 1);
+      wave_lds_order();
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const char* src = S + (role == 1 ? OG : OD) + j * T + pbase;
+        f32x4 ac[NB32];
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) ac[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < NCH32; ++c) {
+          Frag8 av;
+          av.u = *(const uint4*)(src + (c / 3) * RS + (c % 3) * PB + 16 * g);
+#pragma unroll
+          for (int nb = 0; nb < NB32; ++nb)
+            ac[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av.v, ac[nb], 0, 0, 0);
+        }
+        const int o = j * T + pin;
+        const int64_t m = (int64_t)item * 32 + 16 * j + li;
+#pragma unroll
+        for (int nb = 0; nb < NB32; ++nb) {
+          const int co0 = nb * 16 + 4 * g;
+          if (role == 1) {  // du = conv1^T(g) * [u > 0]
+            const uint2 mu = *(const uint2*)(S + OU + o + co0 * 2);
+            const uint32_t mw[2] = {mu.x, mu.y};
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+              v[i] = (__uint_as_float(hb << 16) > 0.f) ? ac[nb][i] : 0.f;
+            }
+            *(uint2*)(S + OD + o + co0 * 2) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          } else {  // dx = conv0^T(du) * [x > 0] + g
+            const uint2 mx = *(const uint2*)(S + OX + o + co0 * 2);
+            const uint2 ad = *(const uint2*)(S + OG + o + co0 * 2);
+            const uint32_t mw[2] = {mx.x, mx.y}, aw[2] = {ad.x, ad.y};
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint32_t hb = (mw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+              v[i] = (__uint_as_float(hb << 16) > 0.f) ? ac[nb][i] : 0.f;
+              v[i] += __uint_as_float(((aw[i >> 1] >> (16 * (i & 1))) & 0xFFFFu) << 16);
+            }
+            if (m < npix)
+              *(uint2*)(a.dx + m * C32 + co0) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+          }
+        }
+      }
+      wave_lds_order();
+      set_flag(role == 1 ? f_du + b : f_d0 + b, it + 1, lane);
+    }
+    return;
+  }
+
+  // ---- W1 (stager) / W0: weight gradients over the item's 32 pixels (K index
+  // k = 8g + 4hh + q: group g / 2, pixel 8 (g % 2) + 4 hh + q of it; q = li / 4)
+  f32x4 acc[2][2][9], accb[2];  // [co block][ci block][tap]
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    accb[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[mb][nb][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  Frag8 ones;
+  ones.u = make_uint4(0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+  int kp[2];  // this lane's K-row pixel (window top-left) for hh = 0, 1
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) kp[hh] = (g >> 1) * T + pix(8 * (g & 1) + 4 * hh + (li >> 2));
+  const int c8 = 8 * (li & 3);
+  const bool w1 = role == 0;
+  // staging (W1): uint4 e = lane + 64 k of a tensor's item (group k, pixel lane / 4, chunk)
+  const int sofs = pix(lane >> 2) + RS + PB + 16 * (lane & 3);
+  uint4 px0, px1, pu0, pu1, pg0, pg1;  // (named registers: indexed arrays go to scratch)
+  auto fetch = [&](int item) {
+    // (branches, not selects: a select between a global element and a local zero became a
+    // flat load through a scratch copy)
+    const int64_t e = (int64_t)item * 128 + lane;
+    const int64_t lim = npix * 4;
+    px0 = pu0 = pg0 = px1 = pu1 = pg1 = make_uint4(0, 0, 0, 0);
+    if (e < lim) {
+      px0 = ((const uint4*)a.x)[e];
+      pu0 = ((const uint4*)a.u)[e];
+      pg0 = ((const uint4*)a.g)[e];
+    }
+    if (e + 64 < lim) {
+      px1 = ((const uint4*)a.x)[e + 64];
+      pu1 = ((const uint4*)a.u)[e + 64];
+      pg1 = ((const uint4*)a.g)[e + 64];
+    }
+  };
+  if (w1 && first < nitems) fetch(first);
+  int it = 0;
+  for (int item = first; item < nitems; item += step, ++it) {
+    const int b = it % NSET;
+    char* S = base + b * SETB<MW>();
+    if (w1) {
+      if (it >= NSET) {  // D0 and W0 are done with this set's last item
+        wait_flag(f_d0 + b, it + 1 - NSET);
+        wait_flag(f_w0 + b, it + 1 - NSET);
+      }
+      wave_lds_order();
+      *(uint4*)(S + OX + sofs) = relu8(px0);
+      *(uint4*)(S + OU + sofs) = relu8(pu0);
+      *(uint4*)(S + OG + sofs) = pg0;
+      *(uint4*)(S + OX + T + sofs) = relu8(px1);
+      *(uint4*)(S + OU + T + sofs) = relu8(pu1);
+      *(uint4*)(S + OG + T + sofs) = pg1;
+      wave_lds_order();
+      set_flag(f_staged + b, it + 1, lane);
+      if (item + step < nitems) fetch(item + step);
+    } else {
+      wait_flag(f_du + b, it + 1);
+      wave_lds_order();
+    }
+    // W1: dW1 += relu(u) (x) g (A = g, B = relu(u) taps); W0: dW0 += relu(x) (x) du
+    const char* D = S + (w1 ? OG : OD) + RS + PB + c8;
+    const char* X = S + (w1 ? OU : OX) + c8;
+    Frag8 af[2];
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) af[mb].h[hh] = tr_read(D + kp[hh] + mb * 32);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int off = (t / 3) * RS + (t % 3) * PB;
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        Frag8 bf;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) bf.h[hh] = tr_read(X + kp[hh] + off + nb * 32);
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb)
+          acc[mb][nb][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, bf.v, acc[mb][nb][t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+      accb[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mb].v, ones.v, accb[mb], 0, 0, 0);
+    wave_lds_order();
+    if (!w1) set_flag(f_w0 + b, it + 1, lane);
+  }
+  // ---- this team's partial row of its layer (conv1 rows at partial, conv0 rows at + lstride)
+  float* out = a.partial + (w1 ? 0 : a.lstride) + (size_t)(blockIdx.x * NT + team) * ROW32;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          out[(mb * 16 + 4 * g + i) * KTOT32 + t * C32 + nb * 16 + li] = acc[mb][nb][t][i];
+    if (li == 0)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) out[C32 * KTOT32 + mb * 16 + 4 * g + i] = accb[mb][i];
+  }
+}
+
 size_t res32b_smem(int imgs, int H, int W) {
   const size_t tb = ((size_t)imgs * geo32(H, W).is + 15) & ~(size_t)15;
   return std::max(4 * tb + 128, (size_t)kT32 * 16 * 4);
@@ -1746,6 +1981,52 @@ extern "C" int mbk_res_bwd32_parts(int N, int H, int W, int imgs) {
   const int ncu = cus;
   const int nrounds = (N + imgs - 1) / imgs;
   return std::max(1, std::min(nrounds, ncu));
+}
+
+// Partial-row PAIRS mbk_res_bwd32_team writes (teams of its grid); <= 0: unsupported shape.
+extern "C" int mbk_res_bwd32_team_parts(int N, int H, int W) {
+  if (N <= 0 || H != W || (W != 4 && W != 2)) return -1;
+  static int cus = 0, per4 = 0, per2 = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+    (void)hipFuncSetAttribute((const void*)res_bwd32_team_kernel<4>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, rbt::smem<4>());
+    (void)hipFuncSetAttribute((const void*)res_bwd32_team_kernel<2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, rbt::smem<2>());
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per4, (const void*)res_bwd32_team_kernel<4>,
+                                                     rbt::kPT, rbt::smem<4>()) != hipSuccess || per4 < 1)
+      per4 = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per2, (const void*)res_bwd32_team_kernel<2>,
+                                                     rbt::kPT, rbt::smem<2>()) != hipSuccess || per2 < 1)
+      per2 = 1;
+  }
+  const int64_t nitems = ((int64_t)N * H * W + 31) / 32;
+  const int64_t wgs = (nitems + rbt::NT - 1) / rbt::NT;
+  return (int)(rbt::NT * std::max<int64_t>(1, std::min<int64_t>(wgs, (int64_t)cus * (W == 4 ? per4 : per2))));
+}
+
+// The 32-channel block backward on 4x4 / 2x2 maps by wave teams (res_bwd32_team_kernel):
+// dx (bit-identical to mbk_res_bwd32) and the two layers' partial rows (conv1 at partial,
+// conv0 at partial + partial_floats / 2); the caller reduces them (mbk_wgrad_reduce_batch).
+extern "C" int mbk_res_bwd32_team(const void* x, const void* u, const void* g, void* dx,
+                                  const void* w1t, const void* w0t, float* partial, int nparts,
+                                  int N, int H, int W, hipStream_t stream) {
+  if (N <= 0) return 0;
+  if (nparts < 1 || nparts != mbk_res_bwd32_team_parts(N, H, W)) return (int)hipErrorInvalidValue;
+  if ((((uintptr_t)x | (uintptr_t)u | (uintptr_t)g | (uintptr_t)w1t | (uintptr_t)w0t) & 15) ||
+      ((uintptr_t)dx & 7))
+    return (int)hipErrorInvalidValue;
+  const int64_t lstride = (int64_t)(nparts + (nparts + 31) / 32) * ROW32;
+  ResBwd32Args a{(const bf16*)x, (const bf16*)u, (const bf16*)g, (bf16*)dx,
+                 (const bf16*)w1t, (const bf16*)w0t, partial, lstride, N, H, W, 1};
+  const void* kfn = W == 4 ? (const void*)res_bwd32_team_kernel<4> : (const void*)res_bwd32_team_kernel<2>;
+  const int sm = W == 4 ? rbt::smem<4>() : rbt::smem<2>();
+  void* args[] = {(void*)&a};
+  (void)hipLaunchKernel(kfn, dim3(nparts / rbt::NT), dim3(rbt::kPT), args, sm, stream);
+  return (int)hipGetLastError();
 }
 
 extern "C" int64_t mbk_res_bwd32_partial_floats(int nparts) {

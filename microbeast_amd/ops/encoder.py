@@ -151,6 +151,9 @@ class HipEncoder:
         self.fused_pool_fwd4 = True
         # 32-channel residual blocks on 4x4 / 2x2 maps with wave-owned 16-pixel blocks
         self.fused_res_blk32_wave = True
+        # their backward on 4x4 / 2x2 maps by wave teams (stager + dW1, du, dx, dW0) synchronised
+        # by LDS flags instead of workgroup rounds
+        self.fused_res_bwd32_team = True
         # the observation layer's weight gradient expands the max-pool backward in its own
         # LDS staging (16-wide maps; bit-identical): no pool_bwd_idx launch, no 4.3 GB
         # full-resolution gradient in HBM per 524K-frame update
@@ -448,6 +451,20 @@ class HipEncoder:
         n = x.shape[0]
         H, W = L0.H, L0.W
         k = N.kernels()
+        if self.fused_res_bwd32_team and H == W and W in (2, 4):
+            # wave teams on 32-pixel items, no workgroup barriers (resblock.hip)
+            dx = torch.empty_like(x)
+            base = self.packed_bwd.data_ptr()
+            nparts = k.mbk_res_bwd32_team_parts(n, H, W)
+            need = k.mbk_res_bwd32_partial_floats(nparts)
+            part = self._partials(L0, need, x.device)
+            N.check(k.mbk_res_bwd32_team(x.data_ptr(), u.data_ptr(), g.data_ptr(), dx.data_ptr(),
+                                         base + 2 * L1.wb_off, base + 2 * L0.wb_off,
+                                         part.data_ptr(), nparts, n, H, W, N.stream_ptr()),
+                    "res_bwd32_team")
+            self._reduce(part.data_ptr(), nparts, L1, dw1, db1)
+            self._reduce(part.data_ptr() + 4 * (need // 2), nparts, L0, dw0, db0)
+            return dx
         lds_kb = _RES32_LDS_KB if H * W > 4 else _RES32_LDS_KB_SMALL
         imgs = max(1, min(_RES32_PIX // (H * W), (lds_kb * 1024 - 128) // (4 * (H + 2) * (W + 2) * 80)))
         dx = torch.empty_like(x)

@@ -665,6 +665,41 @@ def test_fused_res_blk32_bit_identical(cuda, s, n):
         assert torch.equal(a, b), i
 
 
+@pytest.mark.parametrize("s,n", [(16, 1), (16, 3), (16, 37), (16, 1001), (14, 21)])
+def test_res_bwd32_team_matches_round_kernel(cuda, s, n):
+    """The wave-team backward of the 32-channel blocks on 4x4 / 2x2 maps (stager + dW1, du, dx,
+    dW0 waves on 32-pixel items, LDS flags) against the round-based res_bwd32 kernel: every
+    input gradient flowing on is bit-identical (same dgrad chains), so every other layer's
+    gradients are too; the teams' residual weight gradients differ by fp32 summation order
+    (n = 1, 3: a partial last item)."""
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(5)
+    m = Agent((s, s, 27)).to(cuda)
+    obs = _random_obs_bits(n, s * s, seed=n).to(cuda)
+    m.features(obs)
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    grads = {}
+    for team in (False, True):
+        enc.fused_res_bwd32_team = team
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(8)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[team] = [p.grad.detach().clone() for p in params]
+    enc.fused_res_bwd32_team = True
+    for i, (a, b) in enumerate(zip(grads[False], grads[True])):
+        layer = i // 2
+        assert torch.isfinite(b).all(), i
+        if layer >= 5 and layer % 5 != 0:  # 32-channel residual conv
+            torch.testing.assert_close(b, a, rtol=1e-4, atol=1e-6, msg=f"param {i}")
+        else:
+            assert torch.equal(a, b), i
+
+
 @pytest.mark.parametrize("s,n", [(16, 37), (10, 21), (24, 9)])
 def test_fused_res_bwd32_matches_per_layer_kernels(cuda, s, n):
     """resblock.hip res_bwd32 (one 8-wave launch per 32-channel residual block backward)
