@@ -1688,20 +1688,28 @@ __global__ __launch_bounds__(rbt::kPT) void res_bwd32_team_kernel(ResBwd32Args a
       char* S = base + b * SETB<MW>();
       wait_flag(role == 1 ? f_staged + b : f_du + b, it + 1);
       wave_lds_order();
+      // both groups' chains interleaved: 4 independent accumulators behind each tap read pair
+      const char* src = S + (role == 1 ? OG : OD) + pbase;
+      f32x4 acj[2][NB32];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const char* src = S + (role == 1 ? OG : OD) + j * T + pbase;
-        f32x4 ac[NB32];
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int nb = 0; nb < NB32; ++nb) ac[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nb = 0; nb < NB32; ++nb) acj[j][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < NCH32; ++c) {
-          Frag8 av;
-          av.u = *(const uint4*)(src + (c / 3) * RS + (c % 3) * PB + 16 * g);
+      for (int c = 0; c < NCH32; ++c) {
+        Frag8 av[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          av[j].u = *(const uint4*)(src + j * T + (c / 3) * RS + (c % 3) * PB + 16 * g);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
           for (int nb = 0; nb < NB32; ++nb)
-            ac[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av.v, ac[nb], 0, 0, 0);
-        }
+            acj[j][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w[c][nb].v, av[j].v, acj[j][nb], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f32x4* ac = acj[j];
         const int o = j * T + pin;
         const int64_t m = (int64_t)item * 32 + 16 * j + li;
 #pragma unroll
