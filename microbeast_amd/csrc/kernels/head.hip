@@ -665,7 +665,12 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = lane >> 4, li = lane & 15;
   const int nchunks = totals[2];
-  if ((int)blockIdx.x >= nchunks) return;
+  // a contiguous range of chunks per workgroup (chunks are in cell order): consecutive chunks
+  // of one cell keep W_c staged and accumulate dW / db in registers, and only the last chunk
+  // of each such run writes a partial (head_dw_reduce reads exactly those: hb_run_end)
+  const int qn = (nchunks + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int ch_begin = (int)blockIdx.x * qn, ch_end = min(nchunks, ch_begin + qn);
+  if (ch_begin >= nchunks) return;
   // W rows 80..95 stay zero (the dX GEMM's K runs to 96)
   for (int e = tid; e < 16 * HB_RW / 16; e += 64 * HB_NW)
     ((uint4*)(wl + 80 * HB_RW))[e] = make_uint4(0, 0, 0, 0);
@@ -690,6 +695,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     int ch, t0, c, g0, n;
   };
   auto chunk_cur = [&](int ch) {
+    if (ch >= ch_end) ch = nchunks;  // past this workgroup's range: the end
     Cur u{ch, 0, 0, 0, 0};
     if (ch < nchunks) {
       u.c = chunk_cell[ch];
@@ -701,7 +707,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
   auto advance = [&](const Cur& u) {
     if (u.ch >= nchunks) return u;
     if (u.t0 + HB_TM < u.n) return Cur{u.ch, u.t0 + HB_TM, u.c, u.g0, u.n};
-    return chunk_cur(u.ch + (int)gridDim.x);
+    return chunk_cur(u.ch + 1);
   };
   // Per-row metadata (mask words, the aligned action words, g_logp, g_ent, frame) goes through
   // the dZ tile's row padding (bytes 192..227 of each 288-byte row): threads 0..383 each load
@@ -781,7 +787,7 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     for (int k = 0; k < 5; ++k) *(uint4*)(wl + hb_phi(sr0 + 16 * k) * HB_RW + sq * 16) = v[k];
   };
 
-  Cur cur = chunk_cur(blockIdx.x);
+  Cur cur = chunk_cur(ch_begin);
   Cur nx1 = advance(cur);
   load_fx(cur);
   load_x();           // tile 0's rows and metadata
@@ -814,6 +820,8 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
     lds_barrier();
     HB_STAMP(1);
     const bool last = nx1.ch != ch, has_next = nx1.ch < nchunks;
+    // the last tile of a run of this cell's chunks (the next tile is another cell's, or none)
+    const bool run_end = last && !(has_next && nx1.c == c);
     // ---- Z = X W_c^T + b (this wave's 16 rows x 80)
     f32x4 z[5];
 #pragma unroll
@@ -1043,8 +1051,9 @@ __global__ __launch_bounds__(64 * HB_NW, 1) void head_bwd2_kernel(
       if (r < nr) *(uint4*)(dXp + (size_t)(g + r) * KD + (lane & 31) * 8) = v;
     }
     HB_STAMP(6);
-    if (last) {
-      // ---- this chunk's partial dW / db (reduced per cell by head_dw_reduce)
+    if (run_end) {
+      // ---- this run's partial dW / db, in the slot of its last chunk (reduced per cell by
+      // head_dw_reduce)
       // one base per lane, compile-time offsets (no per-row 64-bit pointers kept live)
       float* dwb = dWp + ((size_t)ch * kCell + 4 * G) * KD + 32 * wave + li;
 #pragma unroll
@@ -1253,23 +1262,36 @@ __global__ __launch_bounds__(64 * HS_NW, 1) void head_score_kernel(
 }
 
 // dW[c*78+n][d] = sum over the cell's chunks (fixed order); zero for idle cells
+// head_bwd2 (grid bwd_grid) wrote a partial only at the last chunk of each run of one cell's
+// chunks inside a workgroup's contiguous range: chunk ch of a cell whose chunks end at c_end
+__device__ __forceinline__ bool hb_run_end(int ch, int c_end, int nchunks, int bwd_grid) {
+  const int qn = (nchunks + bwd_grid - 1) / bwd_grid;
+  return ch + 1 == c_end || (ch + 1) % qn == 0;
+}
+
 __global__ __launch_bounds__(256) void head_dw_reduce_kernel(const float* __restrict__ dWp,
                                                              const float* __restrict__ dbp,
                                                              const int* __restrict__ chunk_start,
                                                              const int* __restrict__ grp_count,
-                                                             int S, float* __restrict__ dW,
+                                                             const int* __restrict__ totals,
+                                                             int bwd_grid, int S,
+                                                             float* __restrict__ dW,
                                                              float* __restrict__ db) {
   const int c = blockIdx.y;
   const int e = blockIdx.x * 256 + threadIdx.x;  // within [78][256] (+78 bias entries)
   const int nch = (grp_count[c] + CHUNK - 1) / CHUNK, c0 = chunk_start[c];
+  const int nchunks = totals[2];
   if (e < kCell * KD) {
     float s = 0.f;
-    for (int q = 0; q < nch; ++q) s += dWp[(size_t)(c0 + q) * kCell * KD + e];
+    for (int q = 0; q < nch; ++q)
+      if (hb_run_end(c0 + q, c0 + nch, nchunks, bwd_grid))
+        s += dWp[(size_t)(c0 + q) * kCell * KD + e];
     dW[(size_t)c * kCell * KD + e] = s;
   } else if (e < kCell * KD + kCell) {
     const int n = e - kCell * KD;
     float s = 0.f;
-    for (int q = 0; q < nch; ++q) s += dbp[(size_t)(c0 + q) * kCell + n];
+    for (int q = 0; q < nch; ++q)
+      if (hb_run_end(c0 + q, c0 + nch, nchunks, bwd_grid)) s += dbp[(size_t)(c0 + q) * kCell + n];
     db[c * kCell + n] = s;
   }
 }
@@ -1539,6 +1561,7 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
                             const float* g_logp, const float* g_ent, int S, int grid, void* dXp,
                             float* dWp, float* dbp, float* dW, float* db, const float* stats,
                             hipStream_t stream) {
+  int bwd_grid = 1;
   {
     static int cus = 0;
     static uint64_t* hb_stamps = nullptr;
@@ -1558,6 +1581,7 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
     }
     // one 158 KB workgroup per CU; the caller's grid (chunk count bound) caps it
     const int g2 = std::max(1, std::min(grid, cus));
+    bwd_grid = g2;
     // stats (mbk_head_score's, same batch and weights): the per-logit epilogue
     hipLaunchKernelGGL(stats ? head_bwd2_kernel<true> : head_bwd2_kernel<false>, dim3(g2),
                        dim3(64 * HB_NW), HB_LDS, stream, (const bf16*)X, (const bf16*)Wp, bp,
@@ -1584,7 +1608,7 @@ extern "C" int mbk_head_bwd(const void* X, const void* Wp, const void* WpT, cons
   }
   dim3 g2((kCell * KD + kCell + 255) / 256, S);
   hipLaunchKernelGGL(head_dw_reduce_kernel, g2, dim3(256), 0, stream, dWp, dbp, chunk_start,
-                     grp_count, S, dW, db);
+                     grp_count, totals, bwd_grid, S, dW, db);
   return (int)hipGetLastError();
 }
 
