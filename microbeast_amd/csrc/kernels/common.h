@@ -22,6 +22,12 @@ __device__ __forceinline__ bool mask_bit(const uint32_t m[3], int j) {
   const uint32_t w = j < 32 ? m[0] : (j < 64 ? m[1] : m[2]);
   return (w >> (j & 31)) & 1u;
 }
+// the same on three named words (the compiler folded the array form's selects back into a
+// runtime index -- a scratch store + load per call -- inside cell_forward's segment loops)
+__device__ __forceinline__ bool mask_bit3(uint32_t m0, uint32_t m1, uint32_t m2, int j) {
+  const uint32_t w = j < 32 ? m0 : (j < 64 ? m1 : m2);
+  return (w >> (j & 31)) & 1u;
+}
 
 // ------------------------------------------------------------------ Philox4x32-10
 struct u32x4 { uint32_t x, y, z, w; };
@@ -60,20 +66,22 @@ template <typename ZPtr>
 __device__ __forceinline__ void cell_forward(const ZPtr z, const uint32_t m[3], uint8_t* act,
                                              bool sample, const float u[kComps], float* logp_out,
                                              float* ent_out) {
+  uint32_t m0 = m[0], m1 = m[1], m2 = m[2];
+  asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));  // opaque: no array to re-index
   float lp = 0.f, ent = 0.f;
 #pragma unroll
   for (int k = 0; k < kComps; ++k) {
     const int off = seg_off(k), n = seg_off(k + 1) - off;
     float mx = -INFINITY;
     for (int j = 0; j < n; ++j)
-      if (mask_bit(m, off + j)) mx = fmaxf(mx, (float)z[off + j]);
+      if (mask_bit3(m0, m1, m2, off + j)) mx = fmaxf(mx, (float)z[off + j]);
     if (mx == -INFINITY) {  // fully masked segment
       if (sample) act[k] = 0;
       continue;
     }
     float s = 0.f, sz = 0.f;
     for (int j = 0; j < n; ++j)
-      if (mask_bit(m, off + j)) {
+      if (mask_bit3(m0, m1, m2, off + j)) {
         const float zj = (float)z[off + j];
         const float e = __expf(zj - mx);
         s += e;
@@ -89,7 +97,7 @@ __device__ __forceinline__ void cell_forward(const ZPtr z, const uint32_t m[3], 
       a = -1;
       int last = 0;
       for (int j = 0; j < n; ++j)
-        if (mask_bit(m, off + j)) {
+        if (mask_bit3(m0, m1, m2, off + j)) {
           last = j;
           c += __expf((float)z[off + j] - mx);
           if (a < 0 && c >= target) a = j;
@@ -99,7 +107,7 @@ __device__ __forceinline__ void cell_forward(const ZPtr z, const uint32_t m[3], 
     } else {
       a = act[k];
     }
-    const bool valid = a < n && mask_bit(m, off + a);
+    const bool valid = a < n && mask_bit3(m0, m1, m2, off + a);
     lp += (valid ? (float)z[off + a] : -1e8f) - lse;
   }
   *logp_out = lp;
