@@ -51,6 +51,28 @@ def _N():
     return N
 
 
+
+# ---- CPU emulation hook -----------------------------------------------------------------
+# The pixel-major kernels run on the GPU only. Their plain-torch emulation on CPU tensors (the
+# same bf16 maths, per-pixel loops: an oracle, not a product path) lives in the test suite
+# (tests/pixconv_emulation.py) and is registered by it; GridNetAgent.emulate routes a CPU model
+# through it.
+_EMULATION = None
+
+
+def set_emulation(module) -> None:
+    """Register the CPU emulation of this module's kernels (tests/pixconv_emulation.py)."""
+    global _EMULATION
+    _EMULATION = module
+
+
+def _emulation():
+    if _EMULATION is None:
+        raise RuntimeError("pixel-major GridNet kernels need a GPU: their CPU emulation is test "
+                           "code (tests/pixconv_emulation.py, pixconv.set_emulation)")
+    return _EMULATION
+
+
 def _view(t: torch.Tensor, ps: int, bs: int, rows: int, cols: int, P: int) -> torch.Tensor:
     """rows x cols strided view at pixel P of a (pixel stride, image stride) operand"""
     return torch.as_strided(t.reshape(-1), (rows, cols), (bs, 1), P * ps)
@@ -176,32 +198,8 @@ def pconv(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias=None, relu=False
         _fits(C, tab.dst_max, c_ps, M, c_bs, N, "pconv C")
     if mask is not None:
         _fits(mask, tab.dst_max, c_ps, M, c_bs, N, "pconv mask")
-    if not C.is_cuda:
-        if cells is not None or gather is not None:
-            return _pconv_sparse_ref(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias, relu,
-                                     a_relu, mask, cells, gather)
-        tabc = tab.t.cpu()
-        for z in range(tabc.shape[0]):
-            P, cnt = int(tabc[z, 0]), int(tabc[z, 1])
-            acc = torch.zeros(M, N, dtype=torch.float32)
-            for j in range(cnt):
-                e = int(tabc[z, 2 + j])
-                q, t = e >> 8, e & 255
-                a = _view(A, a_ps, a_bs, M, cin, q).float()
-                if a_relu:
-                    a = a.clamp_min(0)
-                b = B.reshape(-1)[t * N * cin:(t + 1) * N * cin].view(N, cin).float()
-                acc += a @ b.t()
-            if bias is not None:
-                acc += bias.float()
-            if relu:
-                acc = acc.clamp_min(0)
-            out = acc.to(C.dtype)
-            if mask is not None:
-                m = _view(mask, c_ps, c_bs, M, N, P).float() > 0
-                out = torch.where(m, out, torch.zeros_like(out))
-            _view(C, c_ps, c_bs, M, N, P).copy_(out)
-        return C
+    if not C.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().pconv(**locals())
     N_ = _N()
     for t in (A, B, C, mask):
         assert t is None or (t.dtype == _BF and t.is_contiguous())
@@ -220,44 +218,6 @@ def pconv(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias=None, relu=False
     N_.check(N_.kernels().mbk_pconv(args, N_.stream_ptr()), "pconv")
     return C
 
-
-def _pconv_sparse_ref(A, a_ps, a_bs, cin, B, tab, N, M, C, c_ps, c_bs, bias, relu, a_relu, mask,
-                      cells, gather):
-    tabc = tab.t.cpu()
-    for z in range(tabc.shape[0]):
-        P, cnt = int(tabc[z, 0]), int(tabc[z, 1])
-        if cells is not None:
-            o, nr = int(cells.bucket_off[z]), int(cells.bucket_cnt[z])
-            imgs = cells.rowimg[o:o + nr].long()
-        else:
-            nr = M
-        acc = torch.zeros(nr, N, dtype=torch.float32)
-        for j in range(cnt):
-            e = int(tabc[z, 2 + j])
-            q, t = e >> 8, e & 255
-            if cells is not None:
-                a = _view(A, a_ps, a_bs, M, cin, q)[imgs].float()
-            else:
-                rows = gather.cellrow[q * M:(q + 1) * M].long()
-                src = torch.as_strided(A.reshape(-1), (gather.cap, cin), (a_bs, 1), 0)
-                a = torch.where((rows >= 0)[:, None], src[rows.clamp(min=0)].float(), 0.0)
-            if a_relu:
-                a = a.clamp_min(0)
-            b = B.reshape(-1)[t * N * cin:(t + 1) * N * cin].view(N, cin).float()
-            acc += a @ b.t()
-        if bias is not None:
-            acc += bias.float()
-        if relu:
-            acc = acc.clamp_min(0)
-        out = acc.to(C.dtype)
-        if cells is not None:
-            torch.as_strided(C.reshape(-1), (nr, N), (c_bs, 1), o * c_bs).copy_(out)
-        else:
-            if mask is not None:
-                m = _view(mask, c_ps, c_bs, M, N, P).float() > 0
-                out = torch.where(m, out, torch.zeros_like(out))
-            _view(C, c_ps, c_bs, M, N, P).copy_(out)
-    return C
 
 
 class Cells:
@@ -316,10 +276,8 @@ class Cells:
 
     def rows_colsum(self, Z: torch.Tensor, ld: int, C: int, out: torch.Tensor):
         """out[:C] = column sums of the compact rows of Z [cap][ld] (fp32, fixed order)"""
-        if not Z.is_cuda:
-            nact = int(self.totals[0])
-            out.view(-1).copy_(Z.view(-1, ld)[:nact, :C].float().sum(0))
-            return
+        if not Z.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+            return _emulation().rows_colsum(**locals())
         N_ = _N()
         k = N_.kernels()
         nblk = 256
@@ -441,26 +399,8 @@ def pwgrad(g, g_ps, g_bs, O, x, x_ps, x_bs, I, tab, M, gmap, out, x_relu=False, 
     else:
         assert cells.cap * g_bs <= g.numel() and tab.dst_max < cells.S and M == cells.n
     _fits(x, tab.src_max, x_ps, M, x_bs, I, "pwgrad x")
-    if not out.is_cuda:
-        tabc = tab.t.cpu()
-        dw = torch.zeros(ntap, O, I, dtype=torch.float32)
-        for t in range(ntap):
-            for j in range(int(tabc[t, 0])):
-                e = int(tabc[t, 1 + j])
-                P, q = e >> 16, e & 0xFFFF
-                if cells is not None:
-                    o, nr = int(cells.bucket_off[P]), int(cells.bucket_cnt[P])
-                    gv = torch.as_strided(g.reshape(-1), (nr, O), (g_bs, 1), o * g_bs).float()
-                    xv = _view(x, x_ps, x_bs, M, I, q)[cells.rowimg[o:o + nr].long()].float()
-                else:
-                    gv = _view(g, g_ps, g_bs, M, O, P).float()
-                    xv = _view(x, x_ps, x_bs, M, I, q).float()
-                if x_relu:
-                    xv = xv.clamp_min(0)
-                dw[t] += gv.t() @ xv
-        m = gmap.long()
-        out.view(-1).copy_(torch.where(m >= 0, dw.reshape(-1)[m.clamp(min=0)], 0.0))
-        return out
+    if not out.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().pwgrad(**locals())
     N_ = _N()
     k = N_.kernels()
     assert g.dtype == _BF and x.dtype == _BF and g.is_contiguous() and x.is_contiguous()
@@ -496,26 +436,8 @@ def pwgrad_all(g, g_ps, g_bs, O, x, x_ps, x_bs, I, ftab, ntap, M, gmap, out, x_r
     assert ntap <= 9 and ftab.tap_max < ntap
     _fits(g, ftab.dst_max, g_ps, M, g_bs, O, "pwgrad_all g")
     _fits(x, ftab.src_max, x_ps, M, x_bs, I, "pwgrad_all x")
-    if not out.is_cuda:
-        tabc = ftab.t.cpu()
-        dw = torch.zeros(ntap, O, I, dtype=torch.float32)
-        if bias_out is not None:
-            bias_out.zero_()
-        for z in range(tabc.shape[0]):
-            P = int(tabc[z, 0])
-            gv = _view(g, g_ps, g_bs, M, O, P).float()
-            for j in range(int(tabc[z, 1])):
-                e = int(tabc[z, 2 + j])
-                q, t = e >> 8, e & 255
-                xv = _view(x, x_ps, x_bs, M, I, q).float()
-                if x_relu:
-                    xv = xv.clamp_min(0)
-                dw[t] += gv.t() @ xv
-            if bias_out is not None:
-                bias_out += gv.float().sum(0)
-        m = gmap.long()
-        out.view(-1).copy_(torch.where(m >= 0, dw.reshape(-1)[m.clamp(min=0)], 0.0))
-        return out
+    if not out.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().pwgrad_all(**locals())
     N_ = _N()
     k = N_.kernels()
     assert g.dtype == _BF and x.dtype == _BF and g.is_contiguous() and x.is_contiguous()
@@ -550,27 +472,8 @@ def ppool_fwd(y, H: int, W: int, n: int, C: int):
     Ho, Wo = (H + 1) // 2, (W + 1) // 2
     out = torch.empty(Ho * Wo, n, C, dtype=_BF, device=y.device)
     idx = torch.empty(Ho * Wo, n, C, dtype=torch.uint8, device=y.device)
-    if not y.is_cuda:
-        yv = y.view(H, W, n, C).float()
-        best = torch.full((Ho, Wo, n, C), float("-inf"))
-        bi = torch.zeros(Ho, Wo, n, C, dtype=torch.uint8)
-        for ky in range(3):
-            for kx in range(3):
-                for Y in range(Ho):
-                    yy = 2 * Y - 1 + ky
-                    if not 0 <= yy < H:
-                        continue
-                    for X in range(Wo):
-                        xx = 2 * X - 1 + kx
-                        if not 0 <= xx < W:
-                            continue
-                        v = yv[yy, xx]
-                        upd = v > best[Y, X]
-                        best[Y, X] = torch.where(upd, v, best[Y, X])
-                        bi[Y, X] = torch.where(upd, ky * 3 + kx, bi[Y, X].int()).to(torch.uint8)
-        out.copy_(best.view(Ho * Wo, n, C))
-        idx.copy_(bi.view(Ho * Wo, n, C))
-        return out, idx
+    if not y.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().ppool_fwd(**locals())
     N_ = _N()
     assert y.is_contiguous() and y.dtype == _BF and C % 8 == 0
     N_.check(N_.kernels().mbk_ppool_fwd(y.data_ptr(), H, W, n, C, out.data_ptr(), idx.data_ptr(),
@@ -582,22 +485,8 @@ def ppool_bwd(g1, n1: int, g2, n2: int, pooled, idx, H: int, W: int, n: int, C: 
     """gradient of relu(max_pool(conv)) w.r.t. conv [H*W][n][C]: g1 [Po][n1][C] (+ g2
     [Po][n2][C]) routed to the argmax where pooled > 0."""
     Ho, Wo = (H + 1) // 2, (W + 1) // 2
-    if not pooled.is_cuda:
-        g = torch.zeros(Ho * Wo, n, C)
-        g[:, :n1] += g1.float().view(Ho * Wo, n1, C)
-        if g2 is not None:
-            g[:, :n2] += g2.float().view(Ho * Wo, n2, C)
-        g = g * (pooled.float() > 0)
-        dy = torch.zeros(H, W, n, C)
-        gv, iv = g.view(Ho, Wo, n, C), idx.view(Ho, Wo, n, C)
-        for Y in range(Ho):
-            for X in range(Wo):
-                for ky in range(3):
-                    for kx in range(3):
-                        yy, xx = 2 * Y - 1 + ky, 2 * X - 1 + kx
-                        if 0 <= yy < H and 0 <= xx < W:
-                            dy[yy, xx] += gv[Y, X] * (iv[Y, X] == ky * 3 + kx)
-        return dy.view(H * W, n, C).to(_BF)
+    if not pooled.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().ppool_bwd(**locals())
     N_ = _N()
     for t in (g1, g2, pooled):
         assert t is None or (t.is_contiguous() and t.dtype == _BF)
@@ -613,12 +502,8 @@ def colsum(x: torch.Tensor, C: int, out: torch.Tensor, c0: int | None = None,
     """Column sums of the first C columns of 2-D x into out[:c0] and out1[:C-c0] (fp32,
     deterministic)."""
     c0 = C if c0 is None else c0
-    if not x.is_cuda:
-        s = x[:, :C].float().sum(0)
-        out.view(-1).copy_(s[:c0])
-        if out1 is not None:
-            out1.view(-1).copy_(s[c0:])
-        return
+    if not x.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().colsum(**locals())
     N_ = _N()
     k = N_.kernels()
     assert x.stride(1) == 1 and out.is_contiguous() and out.dtype == torch.float32
@@ -633,11 +518,8 @@ def map_gather(segs):
     """segs: [(src fp32 tensor, dst tensor, map int32)]: dst.flat[i] = src.flat[map[i]] or 0."""
     if not segs:
         return
-    if not segs[0][1].is_cuda:
-        for src, dst, m in segs:
-            v = src.reshape(-1)[m.long().clamp(min=0)] * (m >= 0)
-            dst.view(-1).copy_(v.reshape(-1))
-        return
+    if not segs[0][1].is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().map_gather(**locals())
     N_ = _N()
     n = len(segs)
     for src, dst, m in segs:
@@ -655,11 +537,8 @@ def map_gather(segs):
 def gemm_nt(a, b, bias=None, out_dtype=None):
     """a . b^T + bias on gemm.hip: a [M, K], b [N, K] bf16, K % 8 == 0."""
     out_dtype = out_dtype or _BF
-    if not a.is_cuda:
-        y = a.float() @ b.float().t()
-        if bias is not None:
-            y = y + bias
-        return y.to(out_dtype)
+    if not a.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().gemm_nt(**locals())
     N_ = _N()
     assert a.is_contiguous() and b.is_contiguous() and a.dtype == _BF and b.dtype == _BF
     out = torch.empty(a.shape[0], b.shape[0], dtype=out_dtype, device=a.device)
@@ -676,14 +555,8 @@ def value_bwd(dv: torch.Tensor, h: torch.Tensor, w2: torch.Tensor, gw2: torch.Te
     applied) and writes dW2 / db2 (fp32) into gw2 / gb2. gadd: another gradient of the first
     gadd.shape[0] rows of h (fp32 / bf16), added before the relu mask."""
     R, K = h.shape
-    if not h.is_cuda:
-        dvf = dv.float().reshape(R, 1)
-        gw2.view(-1).copy_((dvf * h.float()).sum(0))
-        gb2.view(-1).copy_(dvf.sum())
-        d = dvf * w2.reshape(1, K)
-        if gadd is not None:
-            d[:gadd.shape[0]] += gadd.float()
-        return (d * (h > 0)).to(_BF)
+    if not h.is_cuda:  # CPU: the test suite's emulation (set_emulation)
+        return _emulation().value_bwd(**locals())
     N_ = _N()
     k = N_.kernels()
     assert dv.dtype == torch.float32 and dv.is_contiguous() and h.is_contiguous()

@@ -11,6 +11,11 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: multi-process / long CPU tests")
+    # the pixel-major GridNet ops' CPU emulation is test code (tests/pixconv_emulation.py)
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import pixconv_emulation
+    from microbeast_amd.ops import pixconv
+    pixconv.set_emulation(pixconv_emulation)
 
 
 @pytest.fixture(scope="session")
