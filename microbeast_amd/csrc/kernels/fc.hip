@@ -316,11 +316,13 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
                                                         const float* __restrict__ bc, int F,
                                                         bf16* __restrict__ f_out,
                                                         float* __restrict__ v_out) {
-  constexpr int NBW = O / 64, I = NKS * 32;
-  __shared__ float vred[2][O / 16][16];
+  // two 16-row blocks per iteration (one barrier per 32 rows: the per-block barrier and
+  // critic reduction bounded the one-block form, 190 us per 524K rows)
+  constexpr int NBW = O / 64, I = NKS * 32, RB = 2;
+  __shared__ float vred[2][RB][O / 16][16];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
-  const int nrb = (F + 15) / 16;
+  const int nrb = (F + 16 * RB - 1) / (16 * RB);  // 32-row groups
   Frag8 wf[NBW][NKS];
   float bb[NBW][4], ww[NBW][4];
 #pragma unroll
@@ -339,54 +341,66 @@ __global__ __launch_bounds__(256) void fc_fwd_rb_kernel(const bf16* __restrict__
     }
   }
   const float bcv = bc[0];
-  auto load_x = [&](int rb, uint4* xv) {
-    const int row = rb * 16 + li;
-    const uint4* xr = (const uint4*)(x + (size_t)(row < F ? row : 0) * I) + G;
+  // named registers per block (indexed arrays filled in a lambda can land in scratch)
+  uint4 xn0[NKS], xn1[NKS];
+  auto load_x = [&](int rg) {
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) xv[ks] = xr[ks * 4];
+    for (int r = 0; r < RB; ++r) {
+      const int row = (rg * RB + r) * 16 + li;
+      const uint4* xr = (const uint4*)(x + (size_t)(row < F ? row : 0) * I) + G;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) (r ? xn1 : xn0)[ks] = xr[ks * 4];
+    }
   };
-  uint4 xn[NKS];
-  if ((int)blockIdx.x < nrb) load_x(blockIdx.x, xn);
+  if ((int)blockIdx.x < nrb) load_x(blockIdx.x);
   int buf = 0;
-  for (int rb = blockIdx.x; rb < nrb; rb += gridDim.x, buf ^= 1) {
-    const int row = rb * 16 + li;
-    const bool valid = row < F;
-    uint4 xv[NKS];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) xv[ks] = valid ? xn[ks] : make_uint4(0, 0, 0, 0);
-    if (rb + (int)gridDim.x < nrb) load_x(rb + gridDim.x, xn);
-    f32x4 acc[NBW];
-#pragma unroll
-    for (int j = 0; j < NBW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int rg = blockIdx.x; rg < nrb; rg += gridDim.x, buf ^= 1) {
+    uint4 xv0[NKS], xv1[NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      uint4 v = relu_in ? relu8(xv[ks]) : xv[ks];
-      Frag8 b;
-      __builtin_memcpy(&b, &v, 16);
-#pragma unroll
-      for (int j = 0; j < NBW; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][ks].v, b.v, acc[j], 0, 0, 0);
+      xv0[ks] = xn0[ks];
+      xv1[ks] = xn1[ks];
     }
+    if (rg + (int)gridDim.x < nrb) load_x(rg + gridDim.x);
 #pragma unroll
-    for (int j = 0; j < NBW; ++j) {
-      const int h0 = (wave * NBW + j) * 16 + 4 * G;
-      float hv[4];
+    for (int r = 0; r < RB; ++r) {
+      const int row = (rg * RB + r) * 16 + li;
+      const bool valid = row < F;
+      f32x4 acc[NBW];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + bb[j][i], 0.f)));
-      const float q = mbk::crit_block(hv, ww[j]);
-      if (G == 0) vred[buf][wave * NBW + j][li] = q;
-      uint32_t o[2];
+      for (int j = 0; j < NBW; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
-               ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
-      if (valid) *(uint2*)(f_out + (size_t)row * O + h0) = make_uint2(o[0], o[1]);
+      for (int ks = 0; ks < NKS; ++ks) {
+        uint4 v = valid ? (r ? xv1[ks] : xv0[ks]) : make_uint4(0, 0, 0, 0);
+        if (relu_in) v = relu8(v);
+        Frag8 b;
+        __builtin_memcpy(&b, &v, 16);
+#pragma unroll
+        for (int j = 0; j < NBW; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j][ks].v, b.v, acc[j], 0, 0, 0);
+      }
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        const int h0 = (wave * NBW + j) * 16 + 4 * G;
+        float hv[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          hv[i] = __bfloat162float(__float2bfloat16(fmaxf(acc[j][i] + bb[j][i], 0.f)));
+        const float q = mbk::crit_block(hv, ww[j]);
+        if (G == 0) vred[buf][r][wave * NBW + j][li] = q;
+        uint32_t o[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          o[k] = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k])) |
+                 ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(hv[2 * k + 1])) << 16);
+        if (valid) *(uint2*)(f_out + (size_t)row * O + h0) = make_uint2(o[0], o[1]);
+      }
     }
-    __syncthreads();  // (double-buffered: the next block's writes go to the other half)
-    if (threadIdx.x < 16 && rb * 16 + (int)threadIdx.x < F) {
-      const int t = threadIdx.x;
-      v_out[rb * 16 + t] = mbk::crit_sum(&vred[buf][0][t], O / 16, 16, bcv);
+    __syncthreads();  // (double-buffered: the next group's writes go to the other half)
+    if (threadIdx.x < 16 * RB) {
+      const int r = threadIdx.x >> 4, t = threadIdx.x & 15;
+      const int row = (rg * RB + r) * 16 + t;
+      if (row < F) v_out[row] = mbk::crit_sum(&vred[buf][r][0][t], O / 16, 16, bcv);
     }
   }
 }
@@ -519,7 +533,7 @@ extern "C" int mbk_fc_fwd(const void* x, int relu_in, const void* w5, const floa
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
       if (cus <= 0) cus = 256;
     }
-    const int grid = std::min(blocks, cus * 2);  // 2 workgroups per CU (146 VGPRs)
+    const int grid = std::min((blocks + 1) / 2, cus * 2);  // 32-row groups; 2 workgroups per CU
 #define FC_RB(OO, KS)                                                                        \
   hipLaunchKernelGGL((fc_fwd_rb_kernel<OO, KS>), dim3(grid), dim3(256), 0, stream,          \
                      (const bf16*)x, relu_in, (const bf16*)w5, b5, wc, bc, F, (bf16*)f_out, \
