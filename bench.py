@@ -43,10 +43,11 @@ def parse(argv=None):
     p.add_argument("--size", type=int, default=16)
     p.add_argument("--arch", type=str, default="impala_flat",
                    help="impala_flat (headline) | gridnet (BASELINE config 2) | impala_deep")
-    p.add_argument("--groups", type=int, default=3,
-                   help="env groups pipelined through the policy lanes (profile 36 same-box "
-                        "sweep, 2 lanes: 3 x 8192 15.9-16.0M frames/s at a mean policy lag of "
-                        "3.6 updates; 1 lane x 4 groups 14.6-14.9M at 4.1)")
+    p.add_argument("--groups", type=int, default=4,
+                   help="env groups pipelined through the policy lanes (profile 42 same-box "
+                        "A/Bs at the round-5 learner speed, 2 lanes: 4 x 8192 16.4-17.8M vs "
+                        "3 x 8192 14.5-15.3M frames/s at a mean policy lag of ~4.5 vs ~3.6 "
+                        "updates; profile 36 measured them level with the round-4 learner)")
     p.add_argument("--lanes", type=int, default=0,
                    help="concurrent policy streams, each with its own graph + I/O (0 = auto: "
                         "2; strong scaling at N > 1: min(groups, N), at least 2)")

@@ -72,8 +72,8 @@ class Flags:
     # --- runtime
     runtime: str = "auto"         # auto | gpu (native engine) | mono (CPU actor processes)
     device: str = "auto"          # auto | cpu | cuda
-    groups: int = 3               # gpu runtime: env groups pipelined through the GPU
-    envs_per_group: int = 8192    # (3 x 8192 on 2 lanes = the benched headline config, bench.py)
+    groups: int = 4               # gpu runtime: env groups pipelined through the GPU
+    envs_per_group: int = 8192    # (4 x 8192 on 2 lanes = the benched headline config, bench.py)
     actor_threads: int = 0        # gpu runtime: native env worker threads (0 = auto)
     policy_lanes: int = 2         # gpu runtime: concurrent policy streams (own graph + I/O each)
     actor_inference: str = "auto"  # mono runtime: server (batched policy in the learner
