@@ -83,8 +83,9 @@ def parse(argv=None):
                         "produce units, the agent's idle units (active cells) per env rise from "
                         "~1.1 to ~9 by update ~120 (the acting step, the sparse head and the env "
                         "side slow down: ~13 M frames/s) and settle at 4-5 from update ~450 on "
-                        "(15.0-15.6 M, the rate a 3,200-update CLI run averages: profile 38). "
-                        "0 = time the early-game transient")
+                        "(profile 38; the 4-group training run r5d1L logs 17.0-18.8 M from "
+                        "update 650 on, 17.2 M whole-run). 0 = time the early-game transient "
+                        "(and drop the warm-up's queued rollouts before the window)")
     p.add_argument("--preroll", type=int, default=0,
                    help="before the first policy step every env plays r ~ U[0, preroll) steps of "
                         "the uniform random-init policy on the CPU (untimed), so the timed window "
@@ -198,10 +199,14 @@ def main(argv=None):
 
     for _ in range(args.settle + args.warmup):
         losses = step()
-    # drop rollouts that piled up during warm-up (graph capture, first-call setup) so the
-    # timed window measures the steady-state production rate, not a pre-filled backlog
+    # --settle 0 (early-game transient): drop rollouts that piled up during the short warm-up
+    # (graph capture, first-call setup) so the window does not consume a pre-filled backlog.
+    # After a settle the queue of full rollouts is at its steady-state depth, which the window
+    # also leaves behind at its end; draining it there would open the window on an empty
+    # pipeline (the learner idles ~one step while acting refills it) and, at 20 steps, read
+    # ~5 % below the same config's 150-step window (profile 42, r8h)
     torch.cuda.synchronize()
-    while True:
+    while args.settle == 0:
         slots = rt.engine.get_full(1, 0.0)
         if not slots:
             break
@@ -304,6 +309,10 @@ def main(argv=None):
                 "env_worker_busy_frac": round((st1["env_s"] - st0["env_s"]) / (el * threads), 3),
                 "gpu_policy_steps_per_s": round((st1["gpu_steps"] - st0["gpu_steps"]) / el, 1),
                 "publishes": st1["publishes"] - st0["publishes"],
+                # rollouts queued for the learner when the window opened / closed: the window
+                # starts and ends in the same pipeline state (no pre-filled backlog consumed)
+                "full_slots_waiting": {"start": st0.get("full_depth"),
+                                       "end": st1.get("full_depth")},
                 "slot_wait_s": round(st1["slot_wait_s"] - st0["slot_wait_s"], 3),
                 "driver_idle_s": round(st1["driver_idle_s"] - st0["driver_idle_s"], 3),
                 # per group step: GPU latency (enqueue -> done seen) and CPU env phase

@@ -355,6 +355,7 @@ PYBIND11_MODULE(_mbrt, m) {
         d["frames"] = s.frames;
         d["gpu_steps"] = s.gpu_steps;
         d["slots_full"] = s.slots_full;
+        d["full_depth"] = s.full_depth;
         d["driver_idle_s"] = s.driver_idle_s;
         d["gpu_phase_s"] = s.gpu_phase_s;
         d["step_h2d_s"] = s.step_h2d_s;

@@ -803,6 +803,10 @@ EngineStats GpuEngine::stats() const {
   s.opp_version = opp_version_pub_.load();
   s.act_steps = act_steps_.load();
   s.act_active_cells = act_active_cells_.load();
+  {
+    std::lock_guard<std::mutex> q(slot_m_);
+    s.full_depth = (int)full_slots_.size();
+  }
   std::lock_guard<std::mutex> l(stats_m_);
   s.driver_idle_s = driver_idle_s_;
   s.slot_wait_s = slot_wait_s_;

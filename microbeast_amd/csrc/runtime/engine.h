@@ -110,7 +110,8 @@ struct EngineBuffers {
 struct EngineStats {
   int64_t frames = 0;          // env steps taken (all envs)
   int64_t gpu_steps = 0;       // inference graph launches
-  int64_t slots_full = 0;
+  int64_t slots_full = 0;      // rollout slots filled so far
+  int full_depth = 0;          // full slots waiting for the learner right now
   double driver_idle_s = 0.0;  // driver found nothing to do
   double slot_wait_s = 0.0;    // groups stalled for a free slot (learner-bound)
   double env_s = 0.0;          // summed worker time inside env step
@@ -268,7 +269,7 @@ class GpuEngine {
   int32_t* h_ep_step_ = nullptr;
 
   // slots
-  std::mutex slot_m_;
+  mutable std::mutex slot_m_;
   std::condition_variable full_cv_;
   std::deque<int> free_slots_, full_slots_;
   std::vector<hipEvent_t> full_ev_, release_ev_;
