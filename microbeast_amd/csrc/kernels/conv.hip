@@ -478,10 +478,16 @@ __device__ __forceinline__ void pool_img16(const bf16* __restrict__ ot, size_t o
 // shifts cannot cross a block, so lane 0's left and lane 15's right neighbour words come from
 // the next column block's row word (loaded uniformly); the pre-pool LDS tile drops its row
 // padding (OSTR = COUT) so 8 images of 24 x 24 x 16 fit next to the LUT (151 KB).
+// Pre-pool tile row stride (bf16): 24 for 16 channels puts pool_img16's b64 reads on disjoint
+// banks in each half-wave (2-way at 20; the epilogue's b64 writes go 1 -> 2-way, but the pool
+// reads outnumber them, tools/lds_banks.py rules): 2.40 -> 2.27-2.31 ms per 524K images with
+// the v_bfe LUT addresses below (profile 43).
+constexpr int conv0_ostr(int cout, bool wide) { return wide ? cout : cout == 16 ? 24 : cout + 4; }
+
 template <int HT, int COUT, bool WIDE = false>
 __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int OSTR = WIDE ? COUT : COUT + 4, CB = COUT / 16;
+  constexpr int OSTR = conv0_ostr(COUT, WIDE), CB = COUT / 16;
   const int W = WIDE ? a.W : 16;
   const int H = HT > 0 ? HT : a.H, HW = H * W;
   const int NCB = WIDE ? (W + 15) >> 4 : 1;  // column blocks
@@ -514,9 +520,10 @@ __global__ __launch_bounds__(kThreads) void conv0_row_kernel(ConvFwdArgs a) {
       lw = li == 0 ? bl : lw;
       hw = li == 15 ? bh : hw;
     }
-    r.c = ((bits >> sh) & 0xFFu) * 16u;
-    r.l = ((lw >> sh) & 0xFFu) * 16u;
-    r.h = ((hw >> sh) & 0xFFu) * 16u;
+    // one v_bfe_u32 per byte (shift + and of the plain form: 96 fewer VALU per 16x16 image)
+    r.c = __builtin_amdgcn_ubfe(bits, (uint32_t)sh, 8u) * 16u;
+    r.l = __builtin_amdgcn_ubfe(lw, (uint32_t)sh, 8u) * 16u;
+    r.h = __builtin_amdgcn_ubfe(hw, (uint32_t)sh, 8u) * 16u;
     return r;
   };
   const char* lutb = (const char*)lut;
@@ -1449,7 +1456,8 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
   }
   if (in_bits && (cout == 16 || cout == 32) && W == 16 && !fp8 && g_conv0_row && !add &&
       !mask_src && !relu_in) {
-    const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * 16 * (cout + 4) * 2 : 0);
+    const size_t sm0 =
+        kLutBytes + (pool ? (size_t)kRowImgs * H * 16 * conv0_ostr(cout, false) * 2 : 0);
     if (sm0 > 160 * 1024) return (int)hipErrorInvalidValue;
     const bool hb = H == 16;  // 16 x 16 maps: batched row loads
     const auto kfn = cout == 16 ? (hb ? conv0_row_kernel<16, 16> : conv0_row_kernel<0, 16>)

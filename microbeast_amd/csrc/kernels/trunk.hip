@@ -874,10 +874,10 @@ __device__ __forceinline__ void act_conv0(const uint32_t* bits_img, const char* 
     uint32_t l, c, h;
   };
   auto row = [&](uint32_t b) {  // LUT offsets of pixels x-1, x, x+1 (this lane's plane byte)
-    R3 r;
-    r.c = ((b >> sh) & 0xFFu) * 16u;
-    r.l = ((mbk::dpp_shr1_zero(b) >> sh) & 0xFFu) * 16u;
-    r.h = ((mbk::dpp_shl1_zero(b) >> sh) & 0xFFu) * 16u;
+    R3 r;  // one v_bfe_u32 per byte, as conv0_row_kernel
+    r.c = __builtin_amdgcn_ubfe(b, (uint32_t)sh, 8u) * 16u;
+    r.l = __builtin_amdgcn_ubfe(mbk::dpp_shr1_zero(b), (uint32_t)sh, 8u) * 16u;
+    r.h = __builtin_amdgcn_ubfe(mbk::dpp_shl1_zero(b), (uint32_t)sh, 8u) * 16u;
     return r;
   };
   uint32_t rows[16];
