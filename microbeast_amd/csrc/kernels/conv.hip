@@ -770,7 +770,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int RBX = wg_rbx<XPB, WT>(), RBD = wg_rbd<DPB, WT>();
   const int H = a.H, W = band ? WT : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index in an SGPR: the K-block loop's (image, band, chunk) split of the wave-uniform
+  // block index then runs on the scalar unit instead of as VALU divisions
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = (lane >> 4), li = lane & 15;
   const int IMGX = Hp * RBX, IMGD = H * RBD;  // band layout image strides
   // LDS carve: [X tile | zero row (64B) | dY tile | zero row]; reused for the final reduce
@@ -916,9 +918,11 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
       // pixel 2 windows chose sees one extra bf16 rounding against pool_bwd_idx's fp32 sum)
       static_assert(!UNPOOL || (band && WT == 16 && COUT == 16 && kThreads == 256),
                     "16-wide stage-0 layout, 4 waves x 4 channels");
-      for (int p = lane; p < nimg * HW; p += 64) {  // this wave's 8 bytes of every pixel
-        const int im = p / HW, r = p % HW;
-        *(uint2*)(dt + im * IMGD + (r / WT) * RBD + (r % WT) * DPB + 8 * wave) = make_uint2(0, 0);
+      {  // this wave's 8 bytes of every pixel: lane = (row y % 4, column), rows 4 apart (one
+         // pointer add per store instead of the pixel -> (image, row, column) split per store)
+        char* zp = dt + (lane >> 4) * RBD + (lane & 15) * DPB + 8 * wave;
+        for (int im = 0; im < nimg; ++im, zp += IMGD - H * RBD)
+          for (int y4 = 0; y4 < H; y4 += 4, zp += 4 * RBD) *(uint2*)zp = make_uint2(0, 0);
       }
       asm volatile("" ::: "memory");
       if (s_im < nimg) {
