@@ -1347,7 +1347,7 @@ __global__ __launch_bounds__(256) void head_dx_value_kernel(const bf16* __restri
                                                             bf16* __restrict__ dh,
                                                             float* __restrict__ partial) {
   __shared__ float red[4][KD + 4];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float4 w = ((const float4*)wc)[lane];
   float sw[4] = {0.f, 0.f, 0.f, 0.f}, sb = 0.f;
   // the next frame's dv, h and pair-index row are loaded before this frame's gathers (one
