@@ -449,7 +449,7 @@ struct HeadActArgs {
   int S, E;
 };
 
-__global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
+__device__ __forceinline__ void head_act_kernel_body(const HeadActArgs& a) {
   __shared__ float zs[4][16][NP + 1];
   __shared__ int upre[kMaxUnitCells + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -547,6 +547,10 @@ __global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
   }
+}
+// thin wrapper: the body takes the arguments by const reference (conv0_row_kernel, profile 43)
+__global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
+  head_act_kernel_body(a);
 }
 
 // logp[f] = sum over f's active cells of the pair log-probs (ent likewise), in cell order
