@@ -12,8 +12,10 @@ learners / wall time. Weak scaling (default): per-GPU work fixed, the global bat
 with N. ``--scaling strong``: the 1-GPU problem (envs and frames per update) split over N.
 
 Synthetic environment (native microRTS stand-in; gym-microrts/Java is not
-available offline) and random-init weights of the reference architecture
-(IMPALA-CNN 16/32/32 + 256 FC + flat 78*16*16 head, 5.27 M params).
+available offline) and the reference architecture (IMPALA-CNN 16/32/32 + 256 FC +
+flat 78*16*16 head, 5.27 M params), random-init and then trained for ``--settle``
+untimed updates (default 500) so the timed window measures a training run's steady
+state; the JSON ``data`` field names the settle count.
 
     python bench.py --gpus N --steps K --warmup W
 
@@ -282,7 +284,9 @@ def main(argv=None):
             "vs_baseline": (round(fps / BASELINE_FPS, 1)
                             if args.arch == "impala_flat" and s == 16 else None),
             "dtype": "bf16" + (" (fp8 e4m3 acting trunk)" if args.fp8_policy else ""),
-            "data": "synthetic (native microRTS stand-in env, random-init weights)",
+            "data": ("synthetic (native microRTS stand-in env, "
+                     + (f"random-init weights after {args.settle} untimed training updates)"
+                        if args.settle else "random-init weights)")),
             "config": {
                 "model": (f"impala_flat IMPALA-CNN 16/32/32 + FC256 + flat 78x{s}x{s} head "
                           f"({num_params(model) / 1e6:.2f}M params)" if args.arch == "impala_flat"

@@ -80,7 +80,7 @@ def _compile(cc: str, src: Path, flags: list[str], verbose: bool) -> Path:
 
 
 def _link(cc: str, objs: list[Path], out: Path, extra: list[str], verbose: bool) -> None:
-    LIBDIR.mkdir(parents=True, exist_ok=True)
+    out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_suffix(out.suffix + ".tmp")
     cmd = [cc, "-shared", "-o", str(tmp), *map(str, objs), *extra]
     if verbose:
@@ -103,8 +103,14 @@ def ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
-def build(verbose: bool = False, jobs: int | None = None) -> dict:
+def build(verbose: bool = False, jobs: int | None = None, defines: list[str] | None = None,
+          libdir: Path | None = None) -> dict:
+    """Compile and link both libraries into ``libdir`` (default: the package's ``_lib``).
+    ``defines`` (``-DNAME=V`` flags for the kernel sources) build an A/B variant of the kernel
+    library, e.g. ``tools/variant.py``; the package itself always loads ``_lib``."""
     hipcc = _hipcc()
+    libdir = Path(libdir) if libdir is not None else LIBDIR
+    kflags = KERNEL_FLAGS + list(defines or [])
     cxx = os.environ.get("CXX", "g++")
     import pybind11  # noqa: WPS433 (build-time only)
 
@@ -113,15 +119,15 @@ def build(verbose: bool = False, jobs: int | None = None) -> dict:
     jobs = jobs or min(16, os.cpu_count() or 4)
     ks, rs = kernel_sources(), runtime_sources()
     with cf.ThreadPoolExecutor(jobs) as ex:
-        kfut = [ex.submit(_compile, hipcc, s, KERNEL_FLAGS, verbose) for s in ks]
+        kfut = [ex.submit(_compile, hipcc, s, kflags, verbose) for s in ks]
         rfut = [ex.submit(_compile, cxx, s, host_flags, verbose) for s in rs]
         kobj = [f.result() for f in kfut]
         robj = [f.result() for f in rfut]
-    klib = LIBDIR / "libmbk_kernels.so"
+    klib = libdir / "libmbk_kernels.so"
     _link(hipcc, kobj, klib, [f"--offload-arch={ARCH}", "-fPIC"], verbose)
-    rt = LIBDIR / f"_mbrt{ext_suffix()}"
+    rt = libdir / f"_mbrt{ext_suffix()}"
     _link(cxx, robj, rt,
-          [f"-L{LIBDIR}", "-lmbk_kernels", f"-L{ROCM / 'lib'}", "-lamdhip64", "-pthread",
+          [f"-L{libdir}", "-lmbk_kernels", f"-L{ROCM / 'lib'}", "-lamdhip64", "-pthread",
            "-Wl,-rpath,$ORIGIN"], verbose)
     return {"kernels": str(klib), "runtime": str(rt)}
 

@@ -35,6 +35,10 @@
 #include "../include/microrts_rules.h"
 #include "common.h"
 
+#ifndef MBK_HA_MB
+#define MBK_HA_MB 4
+#endif
+
 using namespace mbk;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -416,20 +420,31 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
 }
 
 // ------------------------------------------------------------------ acting step, launch B
-// head_fwd_kernel's count-mode sampling (same units, GEMM, Philox stream and cell epilogue) with
-// the policy step's finale folded in, so a step is two launches (trunk.hip act_trunk_kernel +
-// this one) instead of head + row_sum_pack:
+// head_fwd_kernel's count-mode sampling (same GEMM chain per logit, same Philox stream, same
+// cell epilogue, so the two are bit-identical) with the policy step's finale folded in, so a step
+// is two launches (trunk.hip act_trunk_w_kernel + this one) instead of head + row_sum_pack:
+//   * work item = a JOB of up to 64 pairs of one cell (4 of head_fwd's 16-pair units): the wave
+//     loads each W_c fragment once per job and feeds it to the 4 row blocks' MFMA chains (the
+//     16-pair units of round 5 re-read the cell's whole 40 KB W_c from L2 per 16 pairs: ~150 MB
+//     per 8192-env step, the kernel's dominant cost under the learner's HBM traffic);
+//   * jobs are dealt to the XCDs in contiguous ranges of the cell-sorted job list (blockIdx % 8
+//     labels the blocks of one XCD): an XCD's L2 then holds only ~1/8 of the 10.5 MB of packed
+//     head weights instead of all of it;
+//   * the 64 rows' logits go to the wave's LDS tile and the masked-cell epilogue (Philox, the
+//     inverse-CDF sample, cell_forward) runs ONE PAIR PER LANE on all 64 lanes (head_fwd's unit
+//     runs it on 16 lanes of 64);
 //   * each sampled pair stores {log-prob, packed env action} as ONE 8-byte write-through (sc1)
 //     granule in its env's per-cell row, drains it (vmcnt(0)), then decrements its env's
 //     pending-cell counter (agent-scope atomic, set by launch A);
-//   * the lane whose decrement empties the counter hands the env to its wave, which reads the
-//     env's row with sc1 loads only (no fence: MI355X_MICROARCH.md "Valid forms" -- every byte
-//     stored sc1 and drained before the signal, every load of it sc1) and writes the env's
-//     log-prob (row_sum_pack's lane-strided sum + wave_sum: bit-identical) and its 16-bit
-//     action codes (one coalesced 128-byte store per 64 cells, also to pinned host memory);
+//   * the lane whose decrement empties the counter runs the env's finale itself (lane-parallel
+//     over the wave's finishing envs): it reads the env's row with sc1 loads only (no fence:
+//     MI355X_MICROARCH.md "Valid forms" -- every byte stored sc1 and drained before the signal,
+//     every load of it sc1) and writes the env's log-prob (its cells' log-probs summed in cell
+//     order, as row_sum_pack sums them: bit-identical) and its action codes / sparse action row
+//     (also to pinned host memory);
 //   * the bucket counters are double-buffered by step parity (launch A of the next step zeroes
 //     this step's half) and the Philox step comes from the host, so no workgroup waits for or
-//     counts the others (a 512-way arrival ticket cost ~6 us).
+//     counts the others.
 struct HeadActArgs {
   const bf16* X;
   const bf16* Wp;
@@ -449,39 +464,118 @@ struct HeadActArgs {
   int S, E;
 };
 
+constexpr int HA_NW = 2;            // waves per workgroup (LDS: ~3 workgroups per CU)
+constexpr int HA_MB = MBK_HA_MB;     // 16-row blocks per job
+constexpr int HA_JOB = 16 * HA_MB;  // pairs per job
+constexpr int HA_ZS = NP + 1;       // logit tile row stride (floats): one row per lane
+
+// exclusive prefix of ceil(cnt / HA_JOB) over the S <= kMaxUnitCells cells into jpre (wave 0,
+// 16 cells per lane; jpre[kMaxUnitCells] = the job total). Caller barriers before reading it.
+__device__ __forceinline__ void job_prefix(const int* __restrict__ cnt, int S, int* jpre) {
+  const int lane = threadIdx.x & 63;
+  if ((threadIdx.x >> 6) != 0) return;
+  int loc[16], run = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = lane * 16 + k;
+    loc[k] = run;
+    run += c < S ? (cnt[c] + HA_JOB - 1) / HA_JOB : 0;
+  }
+  int x = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  const int base = x - run;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = lane * 16 + k;
+    if (c <= S) jpre[c] = base + loc[k];
+  }
+  if (lane == 63) jpre[kMaxUnitCells] = x;
+}
+
 __device__ __forceinline__ void head_act_kernel_body(const HeadActArgs& a) {
-  __shared__ float zs[4][16][NP + 1];
-  __shared__ int upre[kMaxUnitCells + 1];
+  __shared__ float zs[HA_NW][HA_JOB * HA_ZS];
+  __shared__ int jpre[kMaxUnitCells + 1];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int li = lane & 15;
+  const int G = lane >> 4, li = lane & 15;
   const int S = a.S, E = a.E;
-  unit_prefix(a.cnt, S, upre);
+  job_prefix(a.cnt, S, jpre);
   __syncthreads();
-  const int nunits = upre[kMaxUnitCells];
+  const int njobs = jpre[kMaxUnitCells];
   const uint64_t seed = a.rng[0], step = a.step;
   // the device copy of the step counter follows the graph path's (nobody reads it in here)
   if (blockIdx.x == 0 && threadIdx.x == 0) a.rng[1] = step + 1;
-  float (*z)[NP + 1] = zs[wave];
-  for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
-    int lo = 0, hi = S - 1;  // last cell whose prefix <= u
+  // XCD-contiguous job ranges: the blocks b with b % ng == x (one XCD under the round-robin
+  // placement; speed only) take jobs [x J / ng, (x + 1) J / ng)
+  const int ng = min(8, (int)gridDim.x), xg = (int)blockIdx.x % ng;
+  const int nbx = ((int)gridDim.x - xg + ng - 1) / ng, bx = (int)blockIdx.x / ng;
+  const int j0 = (int)((long long)njobs * xg / ng), j1 = (int)((long long)njobs * (xg + 1) / ng);
+  float* zt = zs[wave];
+  for (int j = j0 + bx * HA_NW + wave; j < j1; j += nbx * HA_NW) {
+    int lo = 0, hi = S - 1;  // last cell whose job prefix <= j
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (upre[mid] <= u) lo = mid; else hi = mid - 1;
+      if (jpre[mid] <= j) lo = mid; else hi = mid - 1;
     }
     const int c = lo;
-    const int r0 = c * E + 16 * (u - upre[c]);
-    const int gend = c * E + a.cnt[c];
-    const int r = r0 + li;
-    const bool valid = r < gend;
-    const int ent = valid ? a.bucket[r] : a.bucket[r0];
+    const int rb = c * E + HA_JOB * (j - jpre[c]);
+    const int nr = min(HA_JOB, c * E + a.cnt[c] - rb);  // rows of this job (1 .. 64)
+    // this lane's pair (the epilogue's row = lane) and the MFMA rows' frames (block mb, row li)
+    const bool mine = lane < nr;
+    const int ent = mine ? a.bucket[rb + lane] : 0;
     const int f = ent & 0xFFFF, rank = ent >> 16;  // env, rank among its active cells
-    unit_z(a.X, a.Wp, a.bp, f, valid, c, z);
+    const size_t fc = (size_t)f * S + c;
+    uint32_t m[3] = {0u, 0u, 0u};
+    if (mine) { m[0] = a.mask[fc * 3]; m[1] = a.mask[fc * 3 + 1]; m[2] = a.mask[fc * 3 + 2]; }
+    f32x4 acc[HA_MB][5];
+#pragma unroll
+    for (int mb = 0; mb < HA_MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const uint4* xr[HA_MB];
+    bool xv[HA_MB];
+#pragma unroll
+    for (int mb = 0; mb < HA_MB; ++mb) {
+      const int fr = __shfl(f, 16 * mb + li, 64);
+      xv[mb] = 16 * mb + li < nr;
+      xr[mb] = (const uint4*)(a.X + (size_t)fr * KD) + G;  // 8 bf16 per uint4
+    }
+    const bf16* wc = a.Wp + (size_t)c * NP * KD;
+    // Z = X W_c^T + b: per logit the MFMA chain of unit_z (ks ascending from 0, then + bias).
+    // Straight-line code over all 4 row blocks (a partial job's empty blocks multiply zero
+    // rows): a wave-uniform skip inside the ks loop kept the compiler from hoisting the next
+    // k-step's loads above it, one L2 round trip per k-step
+#pragma unroll
+    for (int ks = 0; ks < KD / 32; ++ks) {
+      Frag8 bw[5];
+#pragma unroll
+      for (int nb = 0; nb < 5; ++nb)
+        bw[nb].u = *((const uint4*)(wc + (size_t)(nb * 16 + li) * KD + ks * 32) + G);
+#pragma unroll
+      for (int mb = 0; mb < HA_MB; ++mb) {
+        Frag8 xa;
+        xa.u = xv[mb] ? xr[mb][ks * 4] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int nb = 0; nb < 5; ++nb)
+          acc[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xa.v, bw[nb].v, acc[mb][nb], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int nb = 0; nb < 5; ++nb) {
+      const int col = nb * 16 + li;
+      const float bias = a.bp[c * NP + col];
+#pragma unroll
+      for (int mb = 0; mb < HA_MB; ++mb) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) zt[(16 * mb + 4 * G + i) * HA_ZS + col] = acc[mb][nb][i] + bias;
+      }
+    }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes of this wave visible
     __builtin_amdgcn_wave_barrier();
-    const bool mine = lane < 16 && valid;
     if (mine) {
-      const size_t fc = (size_t)f * S + c;
-      uint32_t m[3] = {a.mask[fc * 3], a.mask[fc * 3 + 1], a.mask[fc * 3 + 2]};
       uint8_t act[kComps];
       float uu[kComps];
       u32x4 ctr = {(uint32_t)fc, (uint32_t)(fc >> 32), (uint32_t)step, (uint32_t)(step >> 32)};
@@ -490,8 +584,8 @@ __device__ __forceinline__ void head_act_kernel_body(const HeadActArgs& a) {
       u32x4 q1 = philox(ctr, (uint32_t)seed, (uint32_t)(seed >> 32));
       uu[0] = u01(q0.x); uu[1] = u01(q0.y); uu[2] = u01(q0.z); uu[3] = u01(q0.w);
       uu[4] = u01(q1.x); uu[5] = u01(q1.y); uu[6] = u01(q1.z);
-      float lp, ent;
-      cell_forward(&z[lane][0], m, act, true, uu, &lp, &ent);
+      float lp, en;
+      cell_forward(zt + lane * HA_ZS, m, act, true, uu, &lp, &en);
 #pragma unroll
       for (int k = 0; k < kComps; ++k) a.action[fc * kComps + k] = act[k];
       const uint64_t x = (uint64_t)__float_as_uint(lp) |
@@ -505,51 +599,40 @@ __device__ __forceinline__ void head_act_kernel_body(const HeadActArgs& a) {
     if (mine)
       fin = __hip_atomic_fetch_add(a.pending + f, -1, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT) == 1;
-    uint64_t bm = __ballot(fin);
-    while (bm) {  // envs whose last active cell this wave sampled
-      const int l = __builtin_ctzll(bm);
-      bm &= bm - 1;
-      const int fe = __shfl(f, l, 64);
-      // the env's n granules (rank k = k-th active cell in cell order), sc1 loads only
-      const uint64_t* row = a.cellx + (size_t)fe * S;
-      const int n = a.pending[E + fe];
-      float s = 0.f;
-      int nz = 0;  // sparse rows: entries written so far
-      uint32_t* lrow = a.act_list ? a.act_list + (size_t)fe * a.list_stride : nullptr;
-      for (int k0 = 0; k0 < n; k0 += 64) {
-        const int k = k0 + lane;
-        const uint64_t x = k < n ? __hip_atomic_load(row + k, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-        const uint32_t hi = (uint32_t)(x >> 32);
-        // row_sum_pack's lane-strided sum (lane l adds cells l, l + 64, ... in order) without
-        // its +0.0 terms: walk the granules in cell order, each lane keeps its own cells
-        const int kn = min(64, n - k0);
-        for (int q = 0; q < kn; ++q) {
-          const uint32_t lo_q = (uint32_t)__shfl((int)(uint32_t)x, q, 64);
-          const uint32_t hi_q = (uint32_t)__shfl((int)hi, q, 64);
-          if ((int)(hi_q & 63u) == lane) s += __uint_as_float(lo_q);
-        }
-        const uint32_t code = hi >> 16;
-        if (lrow) {  // only the non-noop cells travel back to the env
-          const uint64_t bal = __ballot(k < n && code != 0u);
-          const int pos = nz + __popcll(bal & ((1ull << lane) - 1ull));
-          if (k < n && code != 0u) lrow[1 + pos] = (hi & 0xFFFFu) | (code << 16);
-          nz += __popcll(bal);
-        } else if (k < n) {
-          a.act16[(size_t)fe * S + (hi & 0xFFFFu)] = (uint16_t)code;
+    if (fin) {  // this lane sampled its env's last active cell: the env's finale, lane-parallel
+      // (round 5 ran one env at a time on the whole wave: with 64 pairs per job a wave can finish
+      // dozens of envs, each a dependent sc1 round trip)
+      const uint64_t* row = a.cellx + (size_t)f * S;
+      const int n = a.pending[E + f];  // the env's active cells (granules, rank = cell order)
+      uint32_t* lrow = a.act_list ? a.act_list + (size_t)f * a.list_stride : nullptr;
+      float s = 0.f;  // the env's log-prob: its cells' log-probs in cell order (row_sum_pack's)
+      int nz = 0;     // sparse rows: entries written so far
+      for (int k0 = 0; k0 < n; k0 += 8) {
+        uint64_t xs[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)  // sc1 loads only (see above), 8 in flight
+          xs[i] = k0 + i < n ? __hip_atomic_load(row + k0 + i, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          if (k0 + i >= n) break;
+          const uint32_t hi = (uint32_t)(xs[i] >> 32), code = hi >> 16;
+          s += __uint_as_float((uint32_t)xs[i]);
+          if (lrow) {  // only the non-noop cells travel back to the env
+            if (code != 0u) lrow[1 + nz++] = (hi & 0xFFFFu) | (code << 16);
+          } else {
+            a.act16[(size_t)f * S + (hi & 0xFFFFu)] = (uint16_t)code;
+          }
         }
       }
-      s = wave_sum(s);
-      if (lane == 0) {
-        a.logp[fe] = s;
-        if (lrow) lrow[0] = (uint32_t)nz;
-      }
+      a.logp[f] = s;
+      if (lrow) lrow[0] = (uint32_t)nz;
     }
-    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_wave_barrier();  // the logit tile is rewritten by the next job
   }
 }
 // thin wrapper: the body takes the arguments by const reference (conv0_row_kernel, profile 43)
-__global__ __launch_bounds__(256) void head_act_kernel(HeadActArgs a) {
+__global__ __launch_bounds__(64 * HA_NW, 2) void head_act_kernel(HeadActArgs a) {
   head_act_kernel_body(a);
 }
 
@@ -1717,8 +1800,9 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus <= 0) cus = 256;
   }
-  // two workgroups per CU (fewer, longer-lived ones measured level under the learner)
-  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * 2)), dim3(256), 0, stream, a);
+  // three 2-wave workgroups per CU (the LDS logit tiles allow three): ~1500 waves for the
+  // ~800 64-pair jobs of a settled 8192-env step
+  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * 3)), dim3(64 * HA_NW), 0, stream, a);
   return (int)hipGetLastError();
 }
 

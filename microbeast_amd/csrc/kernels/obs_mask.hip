@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void pack_env_actions_kernel(const uint8_t* __
 }
 
 // Policy-step finale in one launch (one wave per env): the env's log-prob = sum of its
-// cells' log-probs (masked_cell.hip row_sum's lane-strided sum + wave_sum, bit-identical),
+// cells' log-probs in cell order (the fused step's finale order, bit-identical),
 // its cells' 7 action bytes packed into the 16-bit codes the env reads, and the sampler's
 // step counter advanced (block 0) -- row_sum_rng + pack_env_actions without the second
 // launch (each dependent launch of the policy graph waits for CUs behind the learner).
@@ -208,9 +208,15 @@ __global__ __launch_bounds__(256) void row_sum_pack_kernel(const float* __restri
     for (int c = threadIdx.x; c < ncnt; c += blockDim.x) cnt[c] = 0;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   if (r >= rows) return;
+  // the cells' log-probs summed in cell order (inactive cells add an exact +0): the order the
+  // fused step's finale (head.hip head_act_kernel) sums an env's active cells in, lane-serially
   float s = 0.f;
-  for (int c = lane; c < cols; c += 64) s += cell_lp[r * cols + c];
-  s = mbk::wave_sum(s);
+  for (int c0 = 0; c0 < cols; c0 += 64) {
+    const float v = c0 + lane < cols ? cell_lp[r * cols + c0 + lane] : 0.f;
+    const int kn = min(64, cols - c0);
+    for (int q = 0; q < kn; ++q)
+      s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), q));
+  }
   if (lane == 0) logp[r] = s;
   for (int c = lane; c < cols; c += 64) {
     const int64_t i = r * cols + c;

@@ -420,11 +420,19 @@ constexpr int kPT = 128 * NP;
 constexpr int FLAGS = NP * REG;  // per pair, per set: staged, du written, D done (iteration #)
 }  // namespace w88b
 
+// LDS flags between the two waves of a pair. The hardware runs one wave's LDS instructions in
+// issue order, so a flag store issued after a tile's stores is seen after them; what must not
+// move is the ISSUE order, i.e. the compiler may not sink an ordinary LDS store below the
+// volatile flag store (or hoist a tile load above the flag poll). Both helpers therefore carry
+// the compiler fence themselves (wave_lds_order: asm memory clobber, no instruction), so no call
+// site can forget it (two set_flag sites relied on the fence being written beside them).
 // spin until an LDS flag reaches v (written by the other wave of the pair)
 __device__ __forceinline__ void wait_flag(const int* f, int v) {
   while (*(const volatile int*)f < v) __builtin_amdgcn_s_sleep(1);
+  wave_lds_order();  // acquire side: no tile load above the poll
 }
 __device__ __forceinline__ void set_flag(int* f, int v, int lane) {
+  wave_lds_order();  // release side: every tile store issued before the flag
   if (lane == 0) *(volatile int*)f = v;
 }
 

@@ -120,13 +120,12 @@ int64_t VecEnv::preroll(int max_pre, uint64_t seed, int n_threads) {
           sim.set_opponent_actions(a1.data());
         }
         bool d = false;
-        ep_ret_[i] += sim.step(a.data(), &d, nullptr);
-        ep_len_[i] += 1;
-        if (d) {
-          ep_ret_[i] = 0.f;
-          ep_len_[i] = 0;
-        }
+        sim.step(a.data(), &d, nullptr);
       }
+      // the preroll's uniform-policy play is not the policy's: the first logged episode of a
+      // prerolled env counts reward and steps from the hand-off on only
+      ep_ret_[i] = 0.f;
+      ep_len_[i] = 0;
       played.fetch_add(r);
     }
   };

@@ -592,7 +592,12 @@ class HipEncoder:
                 dp = self._fwd(L[li + 1], du0, None, mask_src=p, add=dy0, dgrad=True)
             # maxpool + stage conv
             Ls = L[li]
-            if s == 0 and Ls.bits and Ls.W == 16 and self.fused_pool_wgrad0:
+            # the fused pool + weight-gradient kernel exists for the 16-wide stage-0 band
+            # layout only: ask the library, else fall through to pool_bwd_idx
+            if (s == 0 and Ls.bits and Ls.W == 16 and self.fused_pool_wgrad0 and x.is_cuda
+                    and N.kernels().mbk_conv_wgrad_parts(
+                        int(Ls.bits), Ls.cin, Ls.cout, x.shape[0], Ls.H, Ls.W,
+                        _imgs_wgrad(Ls, True), 1) > 0):
                 self._wgrad(Ls, x, None, grads[2 * li], grads[2 * li + 1], dp=dp, pidx=pidx)
                 g = None
                 continue

@@ -32,7 +32,14 @@ def main():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warm", type=int, default=30, help="env steps before sampling codes")
     p.add_argument("--device_rows", action="store_true", help="sparse rows in HBM, not pinned")
+    p.add_argument("--spread", action="store_true",
+                   help="roll every env's map by its own random (dy, dx): the active cells then "
+                        "spread over the whole map as in a settled run (~100 pairs per cell) "
+                        "instead of sitting on the same few cells of every env")
+    p.add_argument("--lib", default=None, help="variant library dir (tools/variant.py)")
     a = p.parse_args()
+    from tools.variant import use_lib
+    use_lib(a.lib)
     from microbeast_amd import _native as N
     from microbeast_amd.models.agent import Agent
     from microbeast_amd.ops.act import ActWorkspace, MbkActStep
@@ -53,6 +60,12 @@ def main():
     codes = torch.zeros(E, S, dtype=torch.int16)
     res = torch.zeros(E, dtype=torch.int32)
     env.obs_codes(codes.data_ptr(), res.data_ptr())
+    if a.spread:
+        g = torch.Generator().manual_seed(5)
+        sh = torch.randint(0, 16, (E, 2), generator=g)
+        yy = (torch.arange(16)[None, :, None] - sh[:, 0, None, None]) % 16
+        xx = (torch.arange(16)[None, None, :] - sh[:, 1, None, None]) % 16
+        codes = torch.gather(codes.view(E, S), 1, (yy * 16 + xx).view(E, S))
     c = codes.to(torch.int64) & 0xFFFF
     nz = c != 0
     cnt = nz.sum(1)
