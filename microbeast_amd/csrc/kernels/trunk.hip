@@ -970,9 +970,13 @@ constexpr int kWLst = kWVred + 16 * 16 * 4;                  // [2][kWList] pack
 constexpr int kWSmem = kWLst + 2 * kWList * 4;
 static_assert(kWSmem <= 160 * 1024, "wave-owned acting tile exceeds the LDS");
 static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage footprints");
-// a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run)
+// a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run), and the
+// compacted decode's mask rows + own-idle-unit list inside its R1 slice (dead once the stage-0
+// conv writes X0 there)
 constexpr int kWCodes = 0, kWBits = kWEnv * kActS * 2;
 static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
+constexpr int kWMask = 0, kWList16 = kWEnv * kActS * 12;
+static_assert(kWList16 + kWEnv * kActS * 2 <= kWSlice, "decode mask scratch");
 
 // network.5 + critic of the tile: wave w computes hidden blocks 2w, 2w+1 (wf: their W5
 // fragments, loaded before the barrier) for the tile's 16 images, whose X2 tiles sit in the
@@ -1129,37 +1133,83 @@ __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
       }
       __builtin_amdgcn_wave_barrier();
       ACT_STAMP(1);
-      // ---- decode (act_trunk_kernel P2, per env of this wave)
-#pragma unroll 1
-      for (int j = 0; j < nw; ++j) {
-        const int el = e0 + j, e = img0 + el;
+      // ---- decode (act_trunk_kernel P2), compacted: only an own idle unit's cell has a non-zero
+      // mask (cell_mask returns zero words for every other cell, and an own idle unit always
+      // gets its NOOP bit), so pass 1 lists the wave's own idle units (both envs) and pass 2
+      // runs the mask rules once per listed cell, one cell per lane, into the LDS mask rows.
+      // (Round 5 ran cell_mask on all 4 cells of every lane per env: the wave executed the rule
+      // path for every q slot in which any lane had an idle unit -- ~3 of 4 per env.)
+      const int c0 = lane * 4;
+      uint32_t* lmk = (uint32_t*)(R1 + kWMask);       // [kWEnv][S][3] mask words (R1: free
+      uint16_t* llist = (uint16_t*)(R1 + kWList16);   // until the stage-0 conv) + the list
+      uint32_t actq = 0u;  // bit 4 j + q: cell c0 + q of env j holds an own idle unit
+      int kxj[kWEnv], nj[kWEnv];
+#pragma unroll
+      for (int j = 0; j < kWEnv; ++j) {
+        kxj[j] = nj[j] = 0;
+        if (j >= nw) break;
         const uint16_t* cs = lcodes + j * S;
-        const int r = j ? res1 : res0;
-        const int c0 = lane * 4;
-        uint32_t ob[4], mk[12];
         int nact = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int c = c0 + q;
-          uint32_t w3[3];
-          mbk::cell_mask(cs, c, 16, 16, r, w3);
-          ob[q] = mbr::code_bits(cs[c]);
-          mk[3 * q] = w3[0];
-          mk[3 * q + 1] = w3[1];
-          mk[3 * q + 2] = w3[2];
-          nact += (w3[0] | w3[1] | w3[2]) != 0u;
+          const uint16_t code = cs[c0 + q];
+          const int t = mbr::code_type(code);
+          const bool idle = mbr::code_owner(code) == 1 && mbr::code_act(code) == mbr::A_NOOP &&
+                            t != mbr::RESOURCE && t != mbr::NONE;
+          actq |= (uint32_t)idle << (4 * j + q);
+          nact += idle;
         }
+        uint4* mz = (uint4*)(lmk + (j * S + c0) * 3);
+        mz[0] = mz[1] = mz[2] = make_uint4(0u, 0u, 0u, 0u);
         int kx = nact;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
           const int y = __shfl_up(kx, o, 64);
           if (lane >= o) kx += y;
         }
-        const int n = __shfl(kx, 63, 64);
-        kx -= nact;
+        nj[j] = __shfl(kx, 63, 64);
+        kxj[j] = kx - nact;
+      }
+      {  // the list: env 0's cells, then env 1's, each in cell order
+        int pos = kxj[0];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if ((actq >> q) & 1u) llist[pos++] = (uint16_t)(c0 + q);
+        pos = nj[0] + kxj[1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if ((actq >> (4 + q)) & 1u) llist[pos++] = (uint16_t)(S | (c0 + q));
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < nj[0] + nj[1]; i += 64) {  // pass 2: the rules, one cell per lane
+        const int en = llist[i], j = en >> 8, c = en & (S - 1);
+        uint32_t w3[3];
+        mbk::cell_mask(lcodes + j * S, c, 16, 16, j ? res1 : res0, w3);
+        uint32_t* d = lmk + (j * S + c) * 3;
+        d[0] = w3[0];
+        d[1] = w3[1];
+        d[2] = w3[2];
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll 1
+      for (int j = 0; j < nw; ++j) {
+        const int el = e0 + j, e = img0 + el;
+        const uint16_t* cs = lcodes + j * S;
+        uint32_t ob[4], mk[12];
+        {
+          const uint4* ms = (const uint4*)(lmk + (j * S + c0) * 3);
+          const uint4 u0 = ms[0], u1 = ms[1], u2 = ms[2];
+          mk[0] = u0.x; mk[1] = u0.y; mk[2] = u0.z; mk[3] = u0.w;
+          mk[4] = u1.x; mk[5] = u1.y; mk[6] = u1.z; mk[7] = u1.w;
+          mk[8] = u2.x; mk[9] = u2.y; mk[10] = u2.z; mk[11] = u2.w;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ob[q] = mbr::code_bits(cs[c0 + q]);
+        const int n = j ? nj[1] : nj[0];
+        int kx = j ? kxj[1] : kxj[0];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          if (mk[3 * q] | mk[3 * q + 1] | mk[3 * q + 2]) {
+          if ((actq >> (4 * j + q)) & 1u) {
             const int c = c0 + q;
             const int i = atomicAdd(np, 1);
             const int slot = atomicAdd(&lcnt[c], 1);
