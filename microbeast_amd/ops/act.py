@@ -50,15 +50,20 @@ class MbkActStep(ctypes.Structure):
 
 def code_lists(codes: torch.Tensor, res: torch.Tensor, stride: int) -> torch.Tensor:
     """Dense 16-bit codes [E, S] + resources [E] -> the sparse input rows of the fused step
-    (word 0 = n | res << 16, then cell | code << 16 per occupied cell; the engine's env
-    workers write this form directly, VecEnv::step_range_lists)."""
+    (word 0 = n | res << 16, then cell | code << 16 per occupied cell in cell order; the
+    engine's env workers write this form directly, VecEnv::step_range_lists)."""
     E, S = codes.shape
-    out = torch.zeros(E, stride, dtype=torch.int64)
     c = codes.cpu().to(torch.int64) & 0xFFFF
-    for e in range(E):
-        nz = torch.nonzero(c[e]).view(-1)
-        out[e, 0] = len(nz) | (int(res[e]) << 16)
-        out[e, 1:1 + len(nz)] = nz | (c[e, nz] << 16)
+    nz = c != 0
+    cnt = nz.sum(1)
+    order = torch.argsort((~nz).to(torch.int8), dim=1, stable=True)  # occupied cells first
+    cells = torch.arange(S).expand(E, S)
+    ent = torch.gather(cells, 1, order) | (torch.gather(c, 1, order) << 16)
+    keep = torch.arange(S)[None, :] < cnt[:, None]
+    out = torch.zeros(E, stride, dtype=torch.int64)
+    out[:, 0] = cnt | (res.cpu().to(torch.int64) << 16)
+    out[:, 1:1 + S] = torch.where(keep, ent, 0)
+    out = torch.where(out >= 2 ** 31, out - 2 ** 32, out)  # the uint32 words as int32
     return out.to(torch.int32)
 
 
@@ -66,12 +71,13 @@ def dense_actions(act_list: torch.Tensor, S: int) -> torch.Tensor:
     """Sparse action rows (word 0 = n, then cell | code << 16) -> dense int16 [E, S] codes."""
     a = act_list.cpu().to(torch.int64) & 0xFFFFFFFF
     E = a.shape[0]
-    out = torch.zeros(E, S, dtype=torch.int64)
-    for e in range(E):
-        n = int(a[e, 0])
-        ent = a[e, 1:1 + n]
-        out[e, ent & 0xFFFF] = ent >> 16
-    return out.to(torch.int16)
+    n = a[:, :1]
+    listed = torch.arange(a.shape[1] - 1)[None, :] < n
+    ent = a[:, 1:]
+    cell = torch.where(listed, ent & 0xFFFF, S)  # unlisted entries land in a dropped column
+    out = torch.zeros(E, S + 1, dtype=torch.int64)
+    out.scatter_(1, cell, torch.where(listed, ent >> 16, 0))
+    return out[:, :S].to(torch.int16)
 
 
 def supported(model, size: int, fp8: bool = False) -> bool:

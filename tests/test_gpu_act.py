@@ -38,6 +38,18 @@ def _codes_stream(E, steps, seed):
     return out
 
 
+def _pad_rows(cl, codes, k):
+    """cl with k extra (empty cell, code 0) entries appended to every other env's row."""
+    cl = cl.clone()
+    E, S = codes.shape
+    for e in range(0, E, 2):
+        n = int(cl[e, 0]) & 0xFFFF
+        empty = torch.nonzero(codes[e] == 0).view(-1)[:k]
+        cl[e, 1 + n:1 + n + len(empty)] = empty.to(torch.int32)
+        cl[e, 0] = (int(cl[e, 0]) & ~0xFFFF) | (n + len(empty))
+    return cl
+
+
 def _model(cuda, seed):
     from microbeast_amd.models.agent import Agent
     torch.manual_seed(seed)
@@ -49,12 +61,13 @@ def _model(cuda, seed):
     return m
 
 
-@pytest.mark.parametrize("E,sparse", [(96, False), (520, False), (200, True)])
+@pytest.mark.parametrize("E,sparse", [(96, False), (520, False), (200, True), (200, "pad")])
 def test_fused_act_step_bit_identical(cuda, E, sparse):
     """The fused step (launch A: decode + trunk + critic, launch B: sparse head) is
     bit-identical to the captured-graph step. sparse: the PCIe-light form the engine uses
     (occupied-cell code rows in, non-noop action rows out) must give the same step as the
-    dense codes / dense packed actions."""
+    dense codes / dense packed actions; "pad": every other env's row longer than launch A's
+    first 32-word access (the rest of the row is read in a second pass)."""
     from microbeast_amd.ops.act import ActWorkspace, code_lists, dense_actions
     from microbeast_amd.runtime.gpu_actors import graph_policy_step, make_io
 
@@ -88,6 +101,9 @@ def test_fused_act_step_bit_identical(cuda, E, sparse):
             # odd steps: rows in pinned host memory, read by launch A over PCIe (the engine's
             # form); even steps: rows already in HBM
             cl = code_lists(codes, res, stride)
+            if sparse == "pad":  # rows longer than launch A's first access (32 words)
+                cl = _pad_rows(cl, codes, 40)
+                assert int((cl[:, 0] & 0xFFFF).max()) >= 32
             cl = cl.pin_memory() if i % 2 == 1 else cl.to(cuda)
             ws.step(None, None, obs, mask, action, logp, value, None,
                     obs2=obs2 if second else None, mask2=mask2 if second else None,
@@ -130,6 +146,72 @@ def test_fused_act_step_bit_identical(cuda, E, sparse):
         n_active += int((mask != 0).any(-1).sum())
     assert n_active > 50 * 24  # the head actually sampled
     assert int(rng_b[1]) == 7 + 24
+
+
+def _fast_codes_stream(E, steps, seed):
+    """Codes of E simulator envs over `steps` steps of random packed actions (the engine's
+    step_codes path with validation off: infeasible actions are dropped by the simulator)."""
+    rt = N.runtime()
+    S = 256
+    env = rt.VecEnv(16, E, 300, seed, [0, 1, 2, 3, 5])
+    env.set_validate(False)
+    env.reset(0, 0)
+    codes = torch.zeros(E, S, dtype=torch.int16)
+    res = torch.zeros(E, dtype=torch.int32)
+    rew, done = torch.zeros(E), torch.zeros(E, dtype=torch.uint8)
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for t in range(steps):
+        a16 = torch.randint(0, 1 << 14, (E, S), generator=g, dtype=torch.int32).to(torch.int16)
+        env.step_codes(a16.data_ptr(), codes.data_ptr(), res.data_ptr(), rew.data_ptr(),
+                       done.data_ptr())
+        if t >= steps - 4:
+            out.append((codes.clone(), res.clone()))
+    return out
+
+
+def test_fused_act_step_bit_identical_full_grid(cuda):
+    """The headline's 8192-env group: launch A runs 2 tiles per workgroup (the next tile's rows
+    prefetched during the current one, the tile lists / counters double-buffered by parity)
+    and launch B deals ~hundreds of 64-pair jobs -- paths a small E never reaches. The fused
+    step must still equal the captured-graph step bit for bit, with the rows read over PCIe
+    from pinned memory and every other env's row longer than launch A's first access."""
+    from microbeast_amd.ops.act import ActWorkspace, code_lists, dense_actions
+    from microbeast_amd.runtime.gpu_actors import graph_policy_step, make_io
+
+    E, S = 8192, 256
+    m = _model(cuda, 5)
+    rng_a = torch.tensor([777, 3], dtype=torch.int64, device=cuda)
+    rng_b = rng_a.clone()
+    io = make_io(E, S, cuda)
+    ws = ActWorkspace(m, E, rng_b, cuda)
+    obs = torch.empty(E, S, dtype=torch.int32, device=cuda)
+    mask = torch.empty(E, S, 3, dtype=torch.int32, device=cuda)
+    action = torch.full((E, S, 7), 0xAB, dtype=torch.uint8, device=cuda)
+    logp = torch.full((E,), float("nan"), device=cuda)
+    value = torch.full((E,), float("nan"), device=cuda)
+    stride = S + 4
+    act_list = torch.full((E, stride), -1, dtype=torch.int32).pin_memory()
+    for i, (codes, res) in enumerate(_fast_codes_stream(E, 40, seed=11)):
+        io["in_codes"].copy_(codes)
+        io["in_res"].copy_(res)
+        graph_policy_step(io, m, rng_a, E, 16, cuda)
+        cl = _pad_rows(code_lists(codes, res, stride), codes, 40).pin_memory()
+        ws.step(None, None, obs, mask, action, logp, value, None, code_list=cl,
+                act_list=act_list)
+        torch.cuda.synchronize()
+        assert torch.equal(obs, io["in_obs"]), f"obs planes differ at step {i}"
+        assert torch.equal(mask, io["in_mask"]), f"masks differ at step {i}"
+        assert torch.equal(action, io["out_action"]), f"actions differ at step {i}"
+        assert torch.equal(dense_actions(act_list, S).to(cuda), io["out_act16"]), \
+            f"packed actions differ at step {i}"
+        assert torch.equal(logp.view(torch.int32), io["out_logp"].view(torch.int32)), \
+            f"log-probs differ at step {i}"
+        assert torch.equal(value.view(torch.int32), io["out_value"].view(torch.int32)), \
+            f"values differ at step {i}"
+        assert torch.equal(rng_a, rng_b)
+        assert int(ws.pending[:E].abs().sum()) == 0
+    assert int((mask != 0).any(-1).sum()) > E  # the head sampled
 
 
 def test_engine_fused_act_learns(cuda):
