@@ -3,6 +3,8 @@
 per-layer path on the whole training loop; diagnostics, not the headline).
 
     python tools/bench_variant.py fused_pool_wgrad0=0 fused_pool_conv_bwd=0 -- --steps 20
+    python tools/bench_variant.py rt.fused_act=0 fused_tail=0 -- --steps 20   (graph step,
+        per-stage inference kernels)
 """
 import os
 import sys
@@ -14,6 +16,17 @@ def main():
     argv = sys.argv[1:]
     cut = argv.index("--") if "--" in argv else len(argv)
     sets = dict(kv.split("=") for kv in argv[:cut])
+    rt_sets = {k[3:]: v for k, v in sets.items() if k.startswith("rt.")}
+    sets = {k: v for k, v in sets.items() if not k.startswith("rt.")}
+    if rt_sets:  # GpuActorRuntime keyword overrides, e.g. rt.fused_act=0 (the graph step)
+        from microbeast_amd.runtime import gpu_actors as G
+        rinit = G.GpuActorRuntime.__init__
+
+        def rpatched(self, *a, **k):
+            for key, v in rt_sets.items():
+                k[key] = bool(int(v))
+            rinit(self, *a, **k)
+        G.GpuActorRuntime.__init__ = rpatched
     from microbeast_amd.ops import encoder as E
     init = E.HipEncoder.__init__
 
