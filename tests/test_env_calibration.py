@@ -20,11 +20,15 @@ def test_uniform_policy_episode_statistics():
     assert 250 <= out["mean_len"] <= 400
     # reference: mean return -2.26 .. -1.85 (a loss is -10 plus ~8 of shaping rewards)
     assert -3.0 <= out["mean_return"] <= 0.0
-    # reference: 3.4-4.2 % of episodes reach return 10. The stand-in's share is ~11 % (long
-    # runs, tools/calibrate_env.py): the uniform agent wins ~20 % of its random-biased games and
-    # collects ~15 of shaping reward in the ~510-step light-rush games -- the residual env-parity
-    # gap of docs/DESIGN.md section 9a (csrc/tests/calib_components.cpp splits it per bot)
-    assert out["win_share_return_ge_10"] <= 0.14
+    # reference: 3.4-4.2 % of episodes reach return 10. The stand-in's share is 10.8 % over
+    # 973 episodes (tools/calibrate_env.py, 120 envs x 3000 steps) and 10.3 % in this seed-5
+    # run (deterministic). Per bot and reward component (csrc/tests/calib_components.cpp, 300
+    # episodes each, docs/DESIGN.md section 9a): coac 4.7 %, worker rush 8.0 %, random-biased
+    # 26.7 % (the uniform agent WINS 21 % of those games) and light rush 30.0 % (a 520-step
+    # loss collects 5.2 harvest + 4.6 worker + 5.3 attack = ~15 of shaping reward, because the
+    # rush's first light unit needs the 200-tick barracks and arrives ~step 370: microRTS's own
+    # unit timings). Band = the measured value + 1 point
+    assert out["win_share_return_ge_10"] <= 0.118
     # the logged episodes all end by step 512: no bot family may average longer than that
     # (random_biased averaged ~785-860 steps before its moves leaned toward the enemy)
     for bot, st in out["per_bot"].items():
