@@ -99,6 +99,24 @@ def parse(argv=None):
     return p.parse_args(argv)
 
 
+def _occupancy(rt):
+    """Occupied cells per env in the engine's sparse code rows (None without them)."""
+    import ctypes
+
+    import numpy as np
+    try:
+        ptr, stride = rt.engine.code_rows()
+    except AttributeError:
+        return None
+    if not ptr or not stride:
+        return None
+    n_envs = rt.E * rt.G
+    buf = (ctypes.c_uint32 * (n_envs * stride)).from_address(ptr)
+    n = np.frombuffer(buf, dtype=np.uint32).reshape(n_envs, stride)[:, 0] & 0xFFFF
+    return {"mean": round(float(n.mean()), 2), "p90": int(np.percentile(n, 90)),
+            "max": int(n.max()), "frac_over_31": round(float((n > 31).mean()), 4)}
+
+
 def main(argv=None):
     args = parse(argv)
     from microbeast_amd.parallel import launch
@@ -240,6 +258,7 @@ def main(argv=None):
     fps = total_frames / el
     loss_vals = [float(x) for x in losses.tolist()]
     phase_ms = learner.phases.read()  # HIP-event split of the last timed update (no sync)
+    occ = _occupancy(rt)
     phase = None
     if args.profile_phases:
         learner.learn(rt.get_batch()[0], sync_timing=True)
@@ -329,6 +348,9 @@ def main(argv=None):
                 "graph_launch_ms": round(1e3 * (st1["graph_launch_s"] - st0["graph_launch_s"])
                                          / max(1, st1["gpu_steps"] - st0["gpu_steps"]), 3),
             },
+            # occupied cells per env in the rows launch A read at the window's end (its first
+            # access reads 32 words: rows of more than 31 cells cost a second PCIe round trip)
+            "occupied_cells_per_env": occ,
             "actor_stats_per_rank": ranks,
             "cpu_bound_ranks": cpu_bound,
             "learner_phase_ms_rank0": {k: round(v, 3) for k, v in phase_ms.items()},

@@ -936,7 +936,8 @@ constexpr int kActStamps = 21;
 
 // ------------------------------------------------------------------ launch A, wave-owned tiles
 // The acting trunk with the tile split by WAVE instead of by phase: wave w owns envs
-// 2w, 2w+1 of the 16-env tile from their sparse rows to their trunk output -- codes, decode,
+// 2w, 2w+1 of the 8-env tile (4 waves, 80 KB of LDS: two workgroups per CU, round 6) from
+// their sparse rows to their trunk output -- codes, decode,
 // stage-0 conv + pool, the 14 convs (conv_lds WV = 1 / 2 over its own images), the pools and
 // the halo zeroing -- in its own slices of the two regions, so the trunk needs no workgroup
 // barrier at all (LDS is in order within a wave). The phase-split form ran ~25 workgroup-wide
@@ -949,47 +950,61 @@ constexpr int kActStamps = 21;
 // tile's LDS list (LDS atomics for its index and its slot among the tile's pairs of that
 // cell); list, counters and count are double-buffered by tile parity, so the next tile's decode
 // never waits for the bucket writes; a tile with more than kWList pairs spills the rest into
-// its envs' cellx rows (launch B writes those rows only later). The FC gives each wave two
-// hidden blocks of all 16 images (its W5 fragments are loaded before the first barrier), the
+// its envs' cellx rows (launch B writes those rows only later). The FC gives each wave four
+// hidden blocks of all 8 images (its W5 fragments are loaded before the first barrier), the
 // critic partials meet in LDS (mbk::crit_block / crit_sum: every FC kernel's order).
+// Round 6 halved the tile (16 envs / 8 waves / 157 KB -> 8 envs / 4 waves / 80 KB): a
+// workgroup's tile-end barrier now waits for 4 waves, not 8, while the CU's other workgroup
+// keeps issuing, and under the learner a workgroup fits beside a learner workgroup of up to
+// 80 KB. Isolated 170 -> 177 us per 8192-env step (twice the per-tile FC and bucket work), but
+// 4 of 4 seed-paired bench runs faster (16.35 -> 16.91 M frames/s mean on one box).
 //
 // Memory order per wave and tile (vmcnt counts loads and stores in issue order): the stage-0
 // weights, this tile's rows (first tile only), reward / done, then the NEXT tile's rows from
 // pinned host memory right away, so their PCIe latency has the decode and stage-0 conv to
 // hide behind before the first weight wait that orders after them.
+constexpr int kWNW = 4;                                      // waves per workgroup
+constexpr int kWThreads = 64 * kWNW;
 constexpr int kWEnv = 2;                                     // envs (images) per wave
+constexpr int kWTni = kWNW * kWEnv;                          // envs per tile
 constexpr int kWImgB = 10 * 10 * TG<16>::PIXB;               // largest per-image footprint (X0)
 constexpr int kWSlice = kWEnv * kWImgB;                      // a wave's slice of R1 / R2
-constexpr int kWRegion = (kThreads / 64) * kWSlice;          // R1 = R2 = 76800 bytes
-constexpr int kWLut = 2 * kWRegion;                          // byte -> 8 bf16 table, 4 KB
-constexpr int kWCnt = kWLut + 256 * 16;                      // [2][256] pair counts per cell
+constexpr int kWRegion = kWNW * kWSlice;                     // R1 = R2 = 38400 bytes
+constexpr int kWCnt = 2 * kWRegion;                          // [2][256] pair counts per cell
 constexpr int kWNp = kWCnt + 2 * kActS * 4;                  // [2] list lengths (+ pad)
-constexpr int kWVred = kWNp + 16;                            // [16 blocks][16 images] critic
-constexpr int kWList = 270;                                  // list entries per parity in LDS
-constexpr int kWLst = kWVred + 16 * 16 * 4;                  // [2][kWList] packed pairs
+constexpr int kWVred = kWNp + 16;                            // [16 blocks][8 images] critic
+constexpr int kWList = 136;                                  // list entries per parity in LDS
+constexpr int kWLst = kWVred + 16 * kWTni * 4;               // [2][kWList] packed pairs
 constexpr int kWSmem = kWLst + 2 * kWList * 4;
-static_assert(kWSmem <= 160 * 1024, "wave-owned acting tile exceeds the LDS");
+// two workgroups per CU (160 KB): one workgroup's tile-end barrier wait and FC run beside the
+// other's convs, and a learner workgroup of up to 80 KB can share the CU with one of them
+// (round 5's 16-env workgroups took 157 KB: a whole CU)
+static_assert(2 * kWSmem <= 160 * 1024, "two wave-owned acting workgroups per CU");
 static_assert(8 * 8 * 32 * 2 <= kWImgB && 6 * 6 * TG<32>::PIXB <= kWImgB, "stage footprints");
-// a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run), and the
-// compacted decode's mask rows + own-idle-unit list inside its R1 slice (dead once the stage-0
-// conv writes X0 there)
+// a wave's decode scratch inside its R2 slice (dead once its stage-0 conv has run) with the
+// wave's own copy of the stage-0 byte -> 8 bf16 table behind it (written before each tile's
+// stage-0 conv: 4 LDS stores per lane, instead of a workgroup-wide 4 KB that no longer fits),
+// and the compacted decode's mask rows + own-idle-unit list inside its R1 slice (dead once the
+// stage-0 conv writes X0 there)
 constexpr int kWCodes = 0, kWBits = kWEnv * kActS * 2;
-static_assert(kWBits + kWEnv * kActS * 4 <= kWSlice, "decode scratch");
+constexpr int kWLut = kWBits + kWEnv * kActS * 4;
+static_assert(kWLut + 256 * 16 <= kWSlice, "decode scratch + LUT");
 constexpr int kWMask = 0, kWList16 = kWEnv * kActS * 12;
 static_assert(kWList16 + kWEnv * kActS * 2 <= kWSlice, "decode mask scratch");
 
-// network.5 + critic of the tile: wave w computes hidden blocks 2w, 2w+1 (wf: their W5
-// fragments, loaded before the barrier) for the tile's 16 images, whose X2 tiles sit in the
+// network.5 + critic of the tile: wave w computes hidden blocks 4w .. 4w+3 (wf: their W5
+// fragments, loaded before the barrier) for the tile's 8 images, whose X2 tiles sit in the
 // waves' R1 slices (image i: wave i / 2's slice, its image i % 2); critic partials -> vred
+// [hidden block][image] (mbk::crit_sum then adds the blocks in hidden order, as every FC)
 __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
-                                        const uint4 wf[2][4], float* vred) {
+                                        const uint4 wf[4][4], float* vred) {
   constexpr int H2 = 2, W2 = 2, PX = TG<32>::PIXB, NKS = H2 * W2;
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));  // opaque: no address hoisted out of the tile loop
   const int wave = threadIdx.x >> 6;
   const int G = lane >> 4, li = lane & 15;
   const bool valid = li < nimg;
-  const int x2 = (li >> 1) * kWSlice + (li & 1) * (H2 + 2) * (W2 + 2) * PX;
+  const int x2 = ((li >> 1) & (kWNW - 1)) * kWSlice + (li & 1) * (H2 + 2) * (W2 + 2) * PX;
   Frag8 b[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
@@ -999,8 +1014,8 @@ __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
                     : make_uint4(0, 0, 0, 0);
   }
 #pragma unroll
-  for (int jj = 0; jj < 2; ++jj) {
-    const int hb = 2 * wave + jj;
+  for (int jj = 0; jj < 4; ++jj) {
+    const int hb = 4 * wave + jj;
     f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
@@ -1016,7 +1031,7 @@ __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
       w4[i] = a.wc[h0 + i];
     }
     const float q = mbk::crit_block(hv, w4);
-    if (G == 0) vred[hb * 16 + li] = q;
+    if (G == 0 && li < kWTni) vred[hb * kWTni + li] = q;
     uint32_t o[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -1029,26 +1044,25 @@ __device__ __forceinline__ void tile_fc(int nimg, int img0, const TrunkArgs& a,
 __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
   const TrunkArgs& t = a.t;
   constexpr int S = kActS, H0 = 8, W0 = 8, H1 = 4, W1 = 4, H2 = 2, W2 = 2;
-  constexpr int NW = kThreads / 64, TNI = NW * kWEnv;
+  constexpr int NW = kWNW, TNI = kWTni;
   const int E = t.N;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   const int oR1 = wave * kWSlice, oR2 = kWRegion + wave * kWSlice;  // this wave's slices
   char* R1 = trunk_smem + oR1;
   char* R2 = trunk_smem + oR2;
-  const char* lut = trunk_smem + kWLut;
+  const char* lut = R2 + kWLut;  // this wave's copy (rewritten before each stage-0 conv)
   uint16_t* lcodes = (uint16_t*)(R2 + kWCodes);
   uint32_t* lbits = (uint32_t*)(R2 + kWBits);
   float* vred = (float*)(trunk_smem + kWVred);
   const int ngroups = (E + TNI - 1) / TNI;
   const bool pl = lane < kActSpec && lane <= S;  // lanes that read a row's first words
-  // once per launch: the LUT, both parities' tile counters, the previous step's bucket half
-  if (tid < 256) ((uint4*)(trunk_smem + kWLut))[tid] = mbk::bits8_bf16((uint32_t)tid);
-  for (int c = tid; c < 2 * S; c += kThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
+  // once per launch: both parities' tile counters, the previous step's bucket half
+  for (int c = tid; c < 2 * S; c += kWThreads) ((int*)(trunk_smem + kWCnt))[c] = 0;
   if (tid < 2) ((int*)(trunk_smem + kWNp))[tid] = 0;
   if (blockIdx.x == 0) {
     // the previous step's launch B is done with these
-    for (int c = tid; c < S; c += kThreads) a.bucket_cnt_prev[c] = 0;
+    for (int c = tid; c < S; c += kWThreads) a.bucket_cnt_prev[c] = 0;
   }
   mbk::lds_barrier();
   uint32_t pre0 = 0u, pre1 = 0u;  // this wave's rows (first words) for the current tile
@@ -1080,7 +1094,7 @@ __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
     const int nw = max(0, min(kWEnv, nimg - e0));  // ... and how many it has
     uint32_t* ovf = (uint32_t*)(a.cellx + (size_t)img0 * S);  // list spill (this tile's rows)
     bool spilled = false;
-    uint4 wf[2][4];  // this wave's two W5 hidden blocks for the tile's FC
+    uint4 wf[4][4];  // this wave's four W5 hidden blocks for the tile's FC
     if (nw > 0) {
       // stage-0 conv weights / bias first: their L2 latency hides behind the rows and decode
       Frag8 bw0[9];
@@ -1265,6 +1279,8 @@ __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
       __builtin_amdgcn_wave_barrier();
       ACT_STAMP(2);
       // ---- stage-0 conv + pool of the wave's images into its X0 slice
+      for (int i = lane; i < 256; i += 64)  // this wave's byte -> 8 bf16 table
+        ((uint4*)(R2 + kWLut))[i] = mbk::bits8_bf16((uint32_t)i);
       zero_halo<TG<16>::PIXB, true>(R1, nw, H0, W0);
       for (int j = 0; j < nw; ++j) act_conv0(lbits + j * S, lut, bw0, bias0, R1, j);
       __builtin_amdgcn_wave_barrier();
@@ -1301,8 +1317,8 @@ __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
     }
     // ---- tile end: W5 fragments in flight across the barrier
 #pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const uint4* wrow = (const uint4*)(t.w5 + (size_t)((2 * wave + jj) * 16 + li) * (H2 * W2 * 32)) + g;
+    for (int jj = 0; jj < 4; ++jj) {
+      const uint4* wrow = (const uint4*)(t.w5 + (size_t)((4 * wave + jj) * 16 + li) * (H2 * W2 * 32)) + g;
 #pragma unroll
       for (int ks = 0; ks < H2 * W2; ++ks) wf[jj][ks] = wrow[ks * 4];
     }
@@ -1310,20 +1326,20 @@ __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
     if (spilled) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     mbk::lds_barrier();
     ACT_STAMP(19);
-    for (int c = tid; c < S; c += kThreads) {
+    for (int c = tid; c < S; c += kWThreads) {
       const int n = lcnt[c];
       if (n > 0) lcnt[c] = atomicAdd(&a.bucket_cnt[c], n);
     }
     {  // the other parity (the previous tile's, consumed before this barrier) for the next tile
       int* lc2 = (int*)(trunk_smem + kWCnt) + (par ^ 1) * S;
-      for (int c = tid; c < S; c += kThreads) lc2[c] = 0;
+      for (int c = tid; c < S; c += kWThreads) lc2[c] = 0;
       if (tid == 0) ((int*)(trunk_smem + kWNp))[par ^ 1] = 0;
     }
     const int npr = *np;
     tile_fc(nimg, img0, t, wf, vred);
     mbk::lds_barrier();
-    if (tid < nimg) a.t.v_out[img0 + tid] = mbk::crit_sum(vred + tid, 16, 16, t.bc[0]);
-    for (int i = tid; i < npr; i += kThreads) {
+    if (tid < nimg) a.t.v_out[img0 + tid] = mbk::crit_sum(vred + tid, 16, kWTni, t.bc[0]);
+    for (int i = tid; i < npr; i += kWThreads) {
       const uint32_t en = i < kWList ? lst[i]
                                      : __hip_atomic_load(ovf + (i - kWList), __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT);
@@ -1336,7 +1352,7 @@ __device__ __forceinline__ void act_trunk_w_kernel_body(const ActTrunkArgs& a) {
 #undef ACT_WPHASE
 }
 // thin wrapper: the body takes the arguments by const reference (conv0_row_kernel, profile 43)
-__global__ __launch_bounds__(kThreads) void act_trunk_w_kernel(ActTrunkArgs a) {
+__global__ __launch_bounds__(kWThreads, 2) void act_trunk_w_kernel(ActTrunkArgs a) {
   act_trunk_w_kernel_body(a);
 }
 
@@ -1528,7 +1544,7 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
   t.N = m->E;
   t.H0 = 8;
   t.W0 = 8;
-  const int tni = (kThreads / 64) * kWEnv;
+  const int tni = kWTni;
   t.tni = tni;
   t.r1_bytes = t.r2_bytes = kWRegion;
   const size_t sm = (size_t)kWSmem;
@@ -1575,11 +1591,11 @@ extern "C" int mbk_act_trunk(const MbkActModel* m, const MbkActStep* s, hipStrea
     attr = true;
   }
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess ||
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kWThreads, sm) != hipSuccess ||
       per < 1)
     per = 1;
   const int ngroups = (m->E + tni - 1) / tni;
   const int grid = std::min(ngroups, cus * per);
-  hipLaunchKernelGGL(act_trunk_w_kernel, dim3(grid), dim3(kThreads), sm, stream, a);
+  hipLaunchKernelGGL(act_trunk_w_kernel, dim3(grid), dim3(kWThreads), sm, stream, a);
   return (int)hipGetLastError();
 }

@@ -348,6 +348,10 @@ PYBIND11_MODULE(_mbrt, m) {
       .def("sparse_io", &GpuEngine::sparse_io)
       .def_static("act_model_size", [] { return (int)sizeof(MbkActModel); })
       .def("inject_fault", &GpuEngine::inject_fault)
+      // the pinned sparse code rows (word 0 = occupied cells | resources << 16): diagnostics
+      .def("code_rows", [](GpuEngine& e) {
+        return py::make_tuple((uintptr_t)e.host_code_list(), e.list_stride());
+      })
       .def("error", &GpuEngine::error)
       .def("stats", [](GpuEngine& e) {
         EngineStats s = e.stats();

@@ -37,6 +37,11 @@ def main():
                         "spread over the whole map as in a settled run (~100 pairs per cell) "
                         "instead of sitting on the same few cells of every env")
     p.add_argument("--lib", default=None, help="variant library dir (tools/variant.py)")
+    p.add_argument("--settled_rows", action="store_true",
+                   help="pad every row with (empty cell, code 0) entries -- a no-op for the "
+                        "decode -- to the settled bench's occupancy (mean ~21 cells per env, "
+                        "p90 30, ~7 %% over 31: bench.py occupied_cells_per_env), so launch A's "
+                        "row reads cost what they cost in the bench")
     a = p.parse_args()
     from tools.variant import use_lib
     use_lib(a.lib)
@@ -75,6 +80,18 @@ def main():
     ent = (torch.gather(cells, 1, order) | (torch.gather(c, 1, order) << 16))
     keep = torch.arange(S)[None, :] < cnt[:, None]
     rows[:, 1:1 + S] = torch.where(keep, ent, 0).to(torch.int32)
+    if a.settled_rows:
+        g = torch.Generator().manual_seed(9)
+        want = (torch.randn(E, generator=g) * 7.0 + 20.5).clamp(11, 40).round().to(torch.int64)
+        for e in range(E):
+            n = int(cnt[e])
+            k = max(0, int(want[e]) - n)
+            empty = torch.nonzero(c[e] == 0).view(-1)[:k]
+            rows[e, 1 + n:1 + n + len(empty)] = empty.to(torch.int32)
+            rows[e, 0] = (int(rows[e, 0]) & ~0xFFFF) | (n + len(empty))
+        occ = rows[:, 0] & 0xFFFF
+        print(f"settled rows: occupied mean {occ.float().mean():.1f}, "
+              f"over 31: {float((occ > 31).float().mean()):.3f}")
     rows = rows.to(dev) if a.device_rows else rows.pin_memory()
     print(f"occupied cells per env: mean {cnt.float().mean():.1f} max {int(cnt.max())}; "
           f"active (idle own units) {float((mask != 0).any(-1).float().sum(1).mean()):.2f}")

@@ -16,6 +16,11 @@ def main():
     argv = sys.argv[1:]
     cut = argv.index("--") if "--" in argv else len(argv)
     sets = dict(kv.split("=") for kv in argv[:cut])
+    lib = sets.pop("lib", None)  # lib=variants/<name>: a tools/variant.py build of the kernels
+    if lib:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from variant import use_lib
+        use_lib(lib)
     rt_sets = {k[3:]: v for k, v in sets.items() if k.startswith("rt.")}
     sets = {k: v for k, v in sets.items() if not k.startswith("rt.")}
     if rt_sets:  # GpuActorRuntime keyword overrides, e.g. rt.fused_act=0 (the graph step)
