@@ -15,10 +15,22 @@ cancellation: tests/test_relu_flip_conditioning.py); the HIP path must stay with
 floor (or 3 %). The residual conv0 layers are split operand-swap style: the HIP
 gradient against the oracle's operands gated by HIP's own u is held to that same 3x floor, and
 the gate itself must be no noisier than torch-bf16's (relative error of u) and flip signs only
-at rounding-level |u| (within 4x torch-bf16's 99th-percentile deviation); the gate's effect on
-dW, which is chance in these ill-conditioned sums (tools/dbg/gate_flips.py: HIP's u is 2-3x
-closer to fp32 than torch-bf16's, yet its 232 rounding-level flips in stage 0 moved dW by 7.7 %
-where torch's 167 moved it 0.3 %), is capped at 25 %. No layer has an escape clause.
+at rounding-level |u| (within 4x torch-bf16's 99th-percentile deviation).
+
+The gate's effect on dW. Per-flip attribution (_flip_attribution, printed
+with -s): a flip at (n, co, y, x) adds or removes the rank-1 term du * relu(x)-patch to dW[co],
+so a gate's effect is bounded by the sum of |du| |patch| over its flips. On this test's
+deterministic update (12 residual conv0 layers over S = 8 and 16):
+  * the input patch norms at the flips equal the layer's mean for HIP and torch-bf16 alike
+    (the flips are not where activity is high);
+  * |du| is heavy-tailed, and a gate's dW effect is set by the few flips that land on its
+    tail: mean |du| at the flips ranges 0.25-5x the layer mean for HIP and 0.1-2.8x for torch;
+  * torch-bf16's own gate moves dW by up to 8.0 % (network.1.res_block0), HIP's by up to
+    11.2 % (network.1.res_block0 / network.2.res_block1); averaged over the 12 layers 3.3 % vs
+    2.3 %, with HIP's u 2-3x closer to fp32 and fewer flips in most layers.
+The round-5 "7.7 % vs 0.3 %" was one layer of each taken from that tail. The gate part is
+therefore capped at 15 % per layer (measured max 11.2 %) and, across the layers, at 2x the
+independent bf16 implementation's mean effect (measured 1.4x). No layer has an escape clause.
 (Reference update: libs/utils.py:234-335 with SURVEY §8 D1-D4 fixed.)"""
 import copy
 
@@ -63,6 +75,31 @@ def _conv0_grads(c, w0, gate_u):
 
 def _rel(a, b):
     return float((a - b).norm() / (b.norm() + 1e-30))
+
+
+def _flip_attribution(c, u_r, u_gate, ref_w):
+    """Per-flip attribution of a gate's effect on a residual conv0's weight gradient: a flip at
+    (n, co, y, x) adds or removes the rank-1 term du[n, co, y, x] * relu(x)[n, :, y-1..y+1,
+    x-1..x+1] to dW[co]; its size is |du| times the norm of that input patch. Returns the flips'
+    summed term norms and their largest one (both relative to |dW_ref|), the mean |du| at the
+    flips against the mean |du| over the layer, and the gate's measured effect on dW."""
+    import torch.nn.functional as F
+    x, g = c["x"].double(), c["g"].double()
+    du = torch.nn.grad.conv2d_input(c["u"].shape, c["w1"], g, padding=1)  # ungated
+    xr = F.relu(x)
+    pn = F.avg_pool2d((xr * xr).sum(1, keepdim=True), 3, 1, 1, count_include_pad=True) * 9.0
+    pn = pn.sqrt()  # |patch| at every output position [N, 1, H, W]
+    flips = (u_gate > 0) != (u_r > 0)
+    term = (du.abs() * pn)[flips]
+    nw = float(ref_w.norm()) + 1e-30
+    w_gate, _ = _conv0_grads(c, c["w0"], u_gate)
+    pfl = pn.expand_as(du)[flips]
+    return {"flips": int(flips.sum()), "sum_term": float(term.sum()) / nw,
+            "patch_at_flip": float(pfl.mean()) if pfl.numel() else 0.0,
+            "patch_mean": float(pn.mean()),
+            "max_term": (float(term.max()) / nw) if term.numel() else 0.0,
+            "du_at_flip": float(du.abs()[flips].mean()) if term.numel() else 0.0,
+            "du_mean": float(du.abs().mean()), "dW_rel": _rel(w_gate, ref_w)}
 
 
 def _hip_gates(monkeypatch):
@@ -135,6 +172,7 @@ def test_learn_hip_matches_fp32_torch(cuda, S, monkeypatch):
         n = c["u"].shape[0]
         u_h = hip_u[pre][:n].permute(0, 3, 1, 2).double()
         w0 = w0s[pre + "weight"]
+        c["w0"] = w0
         ref_w, ref_b = _conv0_grads(c, w0, c["u"].double())
         hg_w, hg_b = _conv0_grads(c, w0, u_h)
         # the gate itself: HIP's u must be no noisier than an independent bf16 implementation's
@@ -149,10 +187,13 @@ def test_learn_hip_matches_fp32_torch(cuda, S, monkeypatch):
         flips = (u_h > 0) != (u_r > 0)
         gate = {"u_rel": _rel(u_h, u_r), "u_rel_bf": _rel(u_b, u_r), "flips": int(flips.sum()),
                 "max_u_at_flip": float(u_r[flips].abs().max()) if bool(flips.any()) else 0.0,
-                "dev99": dev99}
+                "dev99": dev99,
+                "attr_hip": _flip_attribution(c, u_r, u_h, ref_w),
+                "attr_bf": _flip_attribution(c, u_r, u_b, ref_w)}
         split[pre + "weight"] = (hg_w.float().flatten(), _rel(hg_w, ref_w), gate)
         split[pre + "bias"] = (hg_b.float(), _rel(hg_b, ref_b), gate)
     rows, bad = [], []
+    gate_effects = []  # (HIP, torch-bf16) gate effect on each residual conv0's dW
     for name, o, n, _ in Lr.flat.slices:
         a, b = gh[o:o + n], gr[o:o + n]
         nb = float(b.norm())
@@ -172,11 +213,21 @@ def test_learn_hip_matches_fp32_torch(cuda, S, monkeypatch):
             ref_gate, gate_rel, gt = split[name]
             rest = float((a - ref_gate).norm()) / (float(ref_gate.norm()) + 1e-30)
             gate_ok = (gt["u_rel"] <= 1.5 * gt["u_rel_bf"] + 1e-6
-                       and gt["max_u_at_flip"] <= 4.0 * gt["dev99"] and gate_rel < 0.25)
+                       and gt["max_u_at_flip"] <= 4.0 * gt["dev99"] and gate_rel < 0.15)
+            gate_effects.append((gt["attr_hip"]["dW_rel"], gt["attr_bf"]["dW_rel"]))
             ok = rest < tol and gate_ok
+            ah, ab = gt["attr_hip"], gt["attr_bf"]
             note = (f"  rest {rest:.3e} (tol {tol:.2e})  gate: dW {gate_rel:.3e}, u rel "
                     f"{gt['u_rel']:.2e} (bf16 {gt['u_rel_bf']:.2e}), {gt['flips']} flips at "
-                    f"|u| <= {gt['max_u_at_flip']:.2e} (4 x bf16 dev99 {4 * gt['dev99']:.2e})")
+                    f"|u| <= {gt['max_u_at_flip']:.2e} (4 x bf16 dev99 {4 * gt['dev99']:.2e})"
+                    f"\n      flip attribution hip: {ah['flips']} flips, sum |du||patch| "
+                    f"{ah['sum_term']:.3e}, max {ah['max_term']:.3e}, |du| at flips "
+                    f"{ah['du_at_flip']:.2e} vs mean {ah['du_mean']:.2e}, |patch| at flips "
+                    f"{ah['patch_at_flip']:.2e} vs mean {ah['patch_mean']:.2e}, dW {ah['dW_rel']:.3e}"
+                    f"\n      flip attribution bf16: {ab['flips']} flips, sum |du||patch| "
+                    f"{ab['sum_term']:.3e}, max {ab['max_term']:.3e}, |du| at flips "
+                    f"{ab['du_at_flip']:.2e} vs mean {ab['du_mean']:.2e}, |patch| at flips "
+                    f"{ab['patch_at_flip']:.2e} vs mean {ab['patch_mean']:.2e}, dW {ab['dW_rel']:.3e}")
         else:
             ok = rel < tol and cos > 1.0 - 0.5 * tol ** 2  # (rel ~ sqrt(2 (1 - cos)))
         rows.append((name, rel, floor, cos, note))
@@ -187,6 +238,12 @@ def test_learn_hip_matches_fp32_torch(cuda, S, monkeypatch):
     # losses: pg, value, entropy, total, mean rho
     torch.testing.assert_close(lh, lr, rtol=2e-2, atol=2e-3)
     assert not bad, f"gradients outside the bf16 noise floor: {bad}"
+    # the HIP gate is not systematically worse than an independent bf16 implementation's
+    gh_mean = float(np.mean([h for h, _ in gate_effects]))
+    gb_mean = float(np.mean([b for _, b in gate_effects]))
+    print(f"gate effect on residual conv0 dW, mean over layers: hip {gh_mean:.3e} "
+          f"torch-bf16 {gb_mean:.3e}")
+    assert gh_mean <= 2.0 * gb_mean + 1e-4, (gh_mean, gb_mean)
     # Adam's first step is ~lr * sign(g): equal except where a tiny gradient flips sign
     d = (Lh.flat.data.cpu() - Lr.flat.data).abs()
     assert float(d.max()) <= 2.0 * hp.lr + 1e-6
