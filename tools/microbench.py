@@ -18,7 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--size", type=int, default=16)
-    p.add_argument("--arch", default="impala_flat", help="impala_flat | gridnet")
+    p.add_argument("--arch", default="impala_flat", help="impala_flat | gridnet | impala_deep")
     p.add_argument("--E", type=str, default="256,1024")
     p.add_argument("--learn_T", type=int, default=64)
     p.add_argument("--learn_B", type=str, default="512,1024")
@@ -39,6 +39,8 @@ def main():
     if a.arch == "gridnet":
         from microbeast_amd.models.gridnet import GridNetAgent
         mk = lambda: GridNetAgent((s, s, 27))  # noqa: E731
+    elif a.arch == "impala_deep":
+        mk = lambda: Agent((s, s, 27), channels=(16, 32, 32, 32))  # noqa: E731
     else:
         mk = lambda: Agent((s, s, 27))  # noqa: E731
     for E in [int(x) for x in a.E.split(",") if x]:
