@@ -208,14 +208,19 @@ __global__ __launch_bounds__(256) void row_sum_pack_kernel(const float* __restri
     for (int c = threadIdx.x; c < ncnt; c += blockDim.x) cnt[c] = 0;
   const int64_t r = (int64_t)blockIdx.x * 4 + wave;
   if (r >= rows) return;
-  // the cells' log-probs summed in cell order (inactive cells add an exact +0): the order the
-  // fused step's finale (head.hip head_act_kernel) sums an env's active cells in, lane-serially
+  // the cells' log-probs summed in cell order: the order the fused step's finale (head.hip
+  // head_act_kernel) sums an env's active cells in. Zero entries (inactive cells) are skipped:
+  // adding +-0 to the running sum is exact, so only the few non-zero cells are added serially
+  // (adding all 576 cells of a 24x24 row one by one took 52 us per 8192-env step)
   float s = 0.f;
   for (int c0 = 0; c0 < cols; c0 += 64) {
     const float v = c0 + lane < cols ? cell_lp[r * cols + c0 + lane] : 0.f;
-    const int kn = min(64, cols - c0);
-    for (int q = 0; q < kn; ++q)
+    uint64_t nz = __ballot(v != 0.f);
+    while (nz) {
+      const int q = __builtin_ctzll(nz);
+      nz &= nz - 1;
       s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), q));
+    }
   }
   if (lane == 0) logp[r] = s;
   for (int c = lane; c < cols; c += 64) {
