@@ -225,6 +225,13 @@ def main(argv=None):
     # also leaves behind at its end; draining it there would open the window on an empty
     # pipeline (the learner idles ~one step while acting refills it) and, at 20 steps, read
     # ~5 % below the same config's 150-step window (profile 42, r8h)
+    # after a settle, open the window in the pipeline's median steady state -- exactly one full
+    # rollout queued (starts with 0 or 2 moved a 20-step window by about -/+5 %; the window's
+    # start and end depths are reported) -- running at most 8 more untimed updates to get there
+    for _ in range(8 if args.settle > 0 else 0):
+        if rt.stats().get("full_depth") == 1:
+            break
+        step()
     torch.cuda.synchronize()
     while args.settle == 0:
         slots = rt.engine.get_full(1, 0.0)
