@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cstring>
 #include <cstdlib>
+#include <stdexcept>
 
 namespace mb {
 
@@ -27,6 +28,9 @@ static inline bool getbit(const uint32_t* w, int j) { return (w[j >> 5] >> (j & 
 
 MicroRTSSim::MicroRTSSim(int size, int max_steps, int bot, uint64_t seed, const float* rw)
     : s_(size), max_steps_(max_steps), bot_(bot) {
+  // maps up to 32x32: step()'s idle list and dir_toward's BFS live on the stack, and a cell
+  // index fits the 16-bit fields of the sparse rows
+  if (size < 1 || size > 32) throw std::invalid_argument("MicroRTSSim: map size must be 1..32");
   static const float def[kNumRewards] = {10.f, 1.f, 1.f, 0.2f, 1.f, 4.f};
   for (int i = 0; i < kNumRewards; ++i) rw_[i] = rw ? rw[i] : def[i];
   // splitmix64 seeding so neighbouring seeds give unrelated streams
@@ -59,6 +63,7 @@ int MicroRTSSim::add_unit(int type, int owner, int x, int y, int res) {
   if (uid < 0) { uid = (int)units_.size(); units_.push_back(u); }
   else units_[uid] = u;
   grid_[cell(x, y)] = (int16_t)uid;
+  if (owner >= 0) ++cnt_[owner][type];
   return uid;
 }
 
@@ -67,6 +72,7 @@ void MicroRTSSim::kill(int uid) {
   if (!u.alive) return;
   grid_[cell(u.x, u.y)] = -1;
   u.alive = 0;
+  if (u.owner >= 0) --cnt_[u.owner][u.type];
 }
 
 // "maps/{s}x{s}/basesWorkers{s}x{s}.xml" stand-in (libs/utils.py:73): each
@@ -74,6 +80,7 @@ void MicroRTSSim::kill(int uid) {
 void MicroRTSSim::reset() {
   units_.clear();
   units_.reserve((size_t)s_ * s_ + 4);  // units never outnumber cells: no reallocation
+  std::memset(cnt_, 0, sizeof(cnt_));
   std::fill(grid_.begin(), grid_.end(), (int16_t)-1);
   tick_ = 0;
   resources_[0] = resources_[1] = 5;
@@ -138,9 +145,9 @@ void MicroRTSSim::unit_mask(const Unit& u, int player, uint32_t* w) const {
     }
   }
   if (sp.damage > 0) {
-    const int R = sp.range;
-    for (int ay = -3; ay <= 3; ++ay)
-      for (int ax = -3; ax <= 3; ++ax) {
+    const int R = sp.range, Rs = std::min(R, 3);
+    for (int ay = -Rs; ay <= Rs; ++ay)
+      for (int ax = -Rs; ax <= Rs; ++ax) {
         if (ax * ax + ay * ay > R * R || (ax == 0 && ay == 0)) continue;
         int tx = u.x + ax, ty = u.y + ay;
         if (!in_bounds(tx, ty)) continue;
@@ -356,8 +363,9 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
     const UnitSpec& sp = kSpec[u.type];
     if (sp.damage <= 0) return false;
     int best = -1, bkey = 1 << 30;
-    for (int ay = -3; ay <= 3; ++ay)
-      for (int ax = -3; ax <= 3; ++ax) {
+    const int Rs = std::min<int>(sp.range, 3);  // the cells in range, in the same order
+    for (int ay = -Rs; ay <= Rs; ++ay)
+      for (int ax = -Rs; ax <= Rs; ++ax) {
         if (ax * ax + ay * ay > sp.range * sp.range || (ax == 0 && ay == 0)) continue;
         int tx = u.x + ax, ty = u.y + ay;
         if (!in_bounds(tx, ty)) continue;
@@ -412,12 +420,17 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
   // attack-move: the nearest enemy unit that can fight back or produce (mobile units, bases,
   // barracks), the rest (e.g. nothing) only when none is left
   auto chase = [&]() -> bool {
-    int dist, e = nearest(uid, enemy, -1, &dist);
-    if (e < 0) return false;
-    if (kChaseBaseFirst) {
-      int db, b = nearest(uid, enemy, BASE, &db);
-      if (b >= 0 && db <= dist + kChaseBaseSlack) e = b;
+    // nearest(uid, enemy, -1) and nearest(uid, enemy, BASE) in one pass (same tie order)
+    int e = -1, dist = 1 << 30, b = -1, db = 1 << 30;
+    for (size_t i = 0; i < units_.size(); ++i) {
+      const Unit& t = units_[i];
+      if (!t.alive || t.owner != enemy) continue;
+      const int d = std::abs(t.x - u.x) + std::abs(t.y - u.y);
+      if (d < dist) { dist = d; e = (int)i; }
+      if (t.type == BASE && d < db) { db = d; b = (int)i; }
     }
+    if (e < 0) return false;
+    if (kChaseBaseFirst && b >= 0 && db <= dist + kChaseBaseSlack) e = b;
     return move_to(units_[e].x, units_[e].y);
   };
 
@@ -574,12 +587,7 @@ void MicroRTSSim::bot_unit(int uid, int player, float* rwo, int n_workers, int n
 void MicroRTSSim::bot_act(int player, float* rwo) {
   // own worker / barracks counts for the build orders (taken once per tick), and each
   // worker's index among own workers in unit order (the first ones harvest)
-  int n_workers = 0, n_barracks = 0;
-  for (const Unit& t : units_)
-    if (t.alive && t.owner == player) {
-      n_workers += t.type == WORKER;
-      n_barracks += t.type == BARRACKS;
-    }
+  const int n_workers = cnt_[player][WORKER], n_barracks = cnt_[player][BARRACKS];
   const size_t n = units_.size();
   int widx = 0;
   for (size_t i = 0; i < n; ++i) {
@@ -603,14 +611,21 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
   // own units cannot be removed by own actions, so the set is fixed at this point and
   // exec() re-checks idleness. Same semantics as the scan, a fraction of the memory traffic.
   const int nc = s_ * s_;
-  idle_.clear();
-  for (size_t i = 0; i < units_.size(); ++i) {
+  uint32_t idle[32 * 32 + 4];  // units never outnumber cells (maps up to 32x32)
+  int n_idle = 0;
+  for (size_t i = 0; i < units_.size(); ++i) {  // branch-free collection, then sort by cell
     const Unit& u = units_[i];
-    if (u.alive && u.owner == 0 && u.busy == 0)
-      idle_.push_back(((uint32_t)cell(u.x, u.y) << 16) | (uint32_t)i);
+    idle[n_idle] = ((uint32_t)cell(u.x, u.y) << 16) | (uint32_t)i;
+    n_idle += (u.alive != 0) & (u.owner == 0) & (u.busy == 0);
   }
-  std::sort(idle_.begin(), idle_.end());
-  for (const uint32_t key : idle_) {
+  for (int q = 1; q < n_idle; ++q) {
+    const uint32_t key = idle[q];
+    int j = q;
+    for (; j > 0 && idle[j - 1] > key; --j) idle[j] = idle[j - 1];
+    idle[j] = key;
+  }
+  for (int q = 0; q < n_idle; ++q) {
+    const uint32_t key = idle[q];
     const int c = (int)(key >> 16), g = (int)(key & 0xFFFFu);
     uint8_t tmp[kActComps];
     const uint8_t* a = actions + (size_t)c * kActComps;
@@ -664,15 +679,18 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
     bot_act(1, nullptr);
   }
   // 3) advance time
-  for (Unit& u : units_)
-    if (u.alive && u.busy > 0) {
-      if (--u.busy == 0) u.act = A_NOOP;
-    }
+  for (Unit& u : units_) {  // branch-free: busy flips are data-dependent
+    const int16_t b = u.busy, nb = (int16_t)(b - (u.alive && b > 0));
+    u.act = (b > 0 && nb == 0 && u.alive) ? (int8_t)A_NOOP : u.act;
+    u.busy = nb;
+  }
   ++tick_;
   // 4) terminal check
   int alive[2] = {0, 0};
-  for (const Unit& u : units_)
-    if (u.alive && u.owner >= 0) alive[u.owner]++;
+  for (int t = 0; t < 8; ++t) {
+    alive[0] += cnt_[0][t];
+    alive[1] += cnt_[1][t];
+  }
   bool d = false;
   if (alive[1] == 0 || alive[0] == 0) {
     d = true;
@@ -727,17 +745,23 @@ void MicroRTSSim::write_obs_codes_as(int player, uint16_t* out) const {
 }
 
 int MicroRTSSim::write_obs_code_list(uint32_t* entries, int* idle_own, int player) const {
+  // branch-free over the unit list (dead slots sit between live ones): every unit's entry is
+  // written at n, and n advances past the live ones only (a write past the S cells' entries,
+  // only possible on a full board, goes to a scratch word)
+  const int S = s_ * s_;
+  uint32_t spill;
   int n = 0, idle = 0;
   for (const Unit& u : units_) {
-    if (!u.alive) continue;
     int px = u.x, py = u.y;
     if (player != 0) map_xy(player, u.x, u.y, &px, &py);
     const int own = u.owner < 0 ? 0 : (u.owner == player ? 1 : 2);
-    idle += (own == 1 && u.act == A_NOOP);
-    const uint16_t code = mbr::cell_code(std::min<int>(std::max<int>(u.hp, 0), 4),
-                                         std::min<int>(std::max<int>(u.res, 0), 4), own, u.type,
-                                         u.act);
-    entries[n++] = (uint32_t)cell(px, py) | ((uint32_t)code << 16);
+    const int live = u.alive != 0;
+    idle += live & (own == 1) & (u.act == A_NOOP);
+    const int hp = u.hp < 0 ? 0 : (u.hp > 4 ? 4 : u.hp);
+    const int res = u.res < 0 ? 0 : (u.res > 4 ? 4 : u.res);
+    const uint16_t code = mbr::cell_code(hp, res, own, u.type, u.act);
+    *(n < S ? entries + n : &spill) = (uint32_t)cell(px, py) | ((uint32_t)code << 16);
+    n += live;
   }
   if (idle_own) *idle_own += idle;
   return n;

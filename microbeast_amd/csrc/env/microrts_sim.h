@@ -115,9 +115,15 @@ class MicroRTSSim {
   void write_obs_codes_as(int player, uint16_t* out) const;
   bool external_opponent() const { return external_opp_; }
   int resources(int player) const { return resources_[player]; }
-  int count_units(int owner, int type) const {  // diagnostics (csrc/tests/calib_components.cpp)
+  int count_units(int owner, int type) const {  // alive units of owner (0/1), type (< 0: all)
+    if (owner < 0 || owner > 1) {
+      int n = 0;
+      for (const Unit& u : units_) n += u.alive && u.owner == owner && (type < 0 || u.type == type);
+      return n;
+    }
+    if (type >= 0) return cnt_[owner][type];
     int n = 0;
-    for (const Unit& u : units_) n += u.alive && u.owner == owner && (type < 0 || u.type == type);
+    for (int t = 0; t < 8; ++t) n += cnt_[owner][t];
     return n;
   }
 
@@ -136,7 +142,7 @@ class MicroRTSSim {
   std::vector<uint32_t> mask_;    // cached agent mask (s*s*3)
   std::vector<uint32_t> mask_p1_; // cached opponent mask (for self-play / validation)
   std::vector<uint8_t> opp_actions_;
-  std::vector<uint32_t> idle_;    // step scratch: (cell << 16 | unit) of idle agent units
+  int cnt_[2][8] = {};            // alive units per owner (0 / 1) and type, kept by add / kill
   const uint16_t* p16_ = nullptr;    // step_packed: agent actions decoded lazily per cell
   const uint16_t* opp16_ = nullptr;  // step_packed2: opponent's packed actions
 
