@@ -464,7 +464,10 @@ struct HeadActArgs {
   int S, E;
 };
 
-constexpr int HA_NW = 2;            // waves per workgroup (LDS: ~3 workgroups per CU)
+#ifndef MBK_HA_NW
+#define MBK_HA_NW 2
+#endif
+constexpr int HA_NW = MBK_HA_NW;    // waves per workgroup (LDS: ~3 workgroups per CU)
 constexpr int HA_MB = MBK_HA_MB;     // 16-row blocks per job
 constexpr int HA_JOB = 16 * HA_MB;  // pairs per job
 constexpr int HA_ZS = NP + 1;       // logit tile row stride (floats): one row per lane
@@ -1802,7 +1805,8 @@ extern "C" int mbk_act_head(const MbkActModel* m, const MbkActStep* s, hipStream
   }
   // three 2-wave workgroups per CU (the LDS logit tiles allow three): ~1500 waves for the
   // ~800 64-pair jobs of a settled 8192-env step
-  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * 3)), dim3(64 * HA_NW), 0, stream, a);
+  hipLaunchKernelGGL(head_act_kernel, dim3(std::max(1, cus * 6 / HA_NW)), dim3(64 * HA_NW), 0,
+                     stream, a);
   return (int)hipGetLastError();
 }
 
