@@ -70,6 +70,9 @@ def parse(argv=None):
                    help="rehearsal only: allow more ranks than GPUs (ranks share a GPU over gloo)")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", help="fp32 | bf16 payload")
     p.add_argument("--bucket_mb", type=float, default=8.0)
+    p.add_argument("--learner_bwd_occupancy", type=int, default=1,
+                   help="learner backward workgroups per CU (0 = as many as fit; 1 leaves the "
+                        "acting kernels a slot beside them: +4 %% over 8 seed pairs, profile 45)")
     p.add_argument("--comm_rehearsal", action="store_true",
                    help="1 GPU only: every gradient bucket fires a stand-in collective kernel "
                         "on a 4th high-priority stream from the same hooks (the stream set of an "
@@ -177,6 +180,9 @@ def main(argv=None):
         return Agent((s, s, 27))
 
     torch.manual_seed(args.seed)
+    from microbeast_amd import _native  # before the learner sizes its partial buffers
+    _native.check(_native.kernels().mbk_set_learner_occupancy(0, args.learner_bwd_occupancy),
+                  "set_learner_occupancy")
     model = make_model()
     learner = Learner(model, LearnerHParams(bucket_mb=args.bucket_mb,
                                             allreduce_dtype=args.allreduce_dtype,

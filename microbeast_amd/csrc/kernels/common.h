@@ -6,6 +6,17 @@
 
 #define MBK_WAVE 64
 
+// Learner persistent grids: resident workgroups per CU capped at mbk_occ_cap(0) (forward
+// kernels) / mbk_occ_cap(1) (backward kernels), 0 = no cap. The acting kernels (215-256
+// VGPRs) cannot co-reside with two learner workgroups per CU (2 waves x ~224 VGPRs per SIMD)
+// and wait for the learner kernel's end; one backward workgroup per CU leaves them a slot
+// (profile 45). Default: no caps; the GPU actor runtime sets the backward cap to 1
+// (mbk_set_learner_occupancy, conv.hip: before the first learner allocation only, since the
+// partial-buffer sizes -- the *_parts queries -- follow it).
+int mbk_occ_cap(int bwd);
+inline int mbk_occ_f(int per) { const int c = mbk_occ_cap(0); return c > 0 && per > c ? c : per; }
+inline int mbk_occ_b(int per) { const int c = mbk_occ_cap(1); return c > 0 && per > c ? c : per; }
+
 namespace mbk {
 
 // microRTS GridMode per-cell action components (reference model.py:168,

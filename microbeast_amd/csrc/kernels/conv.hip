@@ -1406,7 +1406,8 @@ int g_grid_cap = 0;    // tests force multi-group workgroups with a small cap
 int g_conv0_row = 1;   // stage-0 conv of 16-wide maps on conv0_row_kernel (0: generic kernel)
 
 // resident workgroups the whole device holds for (kernel, dynamic LDS)
-int resident_blocks(const void* kfn, size_t sm) {
+// (occ: mbk_occ_f / mbk_occ_b, the forward / backward per-CU caps of common.h)
+int resident_blocks(const void* kfn, size_t sm, int (*occ)(int) = nullptr) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1418,7 +1419,7 @@ int resident_blocks(const void* kfn, size_t sm) {
   int per = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kfn, kThreads, sm) != hipSuccess || per < 1)
     per = 1;
-  int r = cus * per;
+  int r = cus * (occ ? occ(per) : per);
   if (g_grid_cap > 0 && r > g_grid_cap) r = g_grid_cap;
   return r;
 }
@@ -1427,7 +1428,7 @@ int resident_blocks(const void* kfn, size_t sm) {
 // groups (2x / 4x grids that retire workgroups early for the acting step measured level or
 // slower on the bench: DESIGN.md §9 rejected variants)
 int fwd_grid(int ngroups, const void* kfn, size_t sm) {
-  const long r = (long)resident_blocks(kfn, sm);
+  const long r = (long)resident_blocks(kfn, sm, mbk_occ_f);
   return (int)std::max(1L, std::min((long)ngroups, r));
 }
 
@@ -1555,7 +1556,7 @@ extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H
   WGRAD_DISPATCH(Q)
 #undef Q
   if (!kq) return -(int)hipErrorInvalidValue;
-  res = resident_blocks(kq, sm);
+  res = resident_blocks(kq, sm, mbk_occ_b);
   return (int)std::max(1L, std::min((long)nrounds, (long)res));
 }
 
@@ -1716,4 +1717,20 @@ extern "C" int mbk_conv_pack(const MbkPackJob* jobs, int n, hipStream_t stream) 
   p.n = n;
   hipLaunchKernelGGL(conv_pack_kernel, dim3(16, n), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
+}
+
+static int g_occ_cap[2] = {0, 0};  // learner forward / backward workgroups per CU (0: no cap)
+static bool g_occ_read = false;    // a grid was sized with the caps: they are fixed from now on
+int mbk_occ_cap(int bwd) {
+  g_occ_read = true;
+  return g_occ_cap[bwd ? 1 : 0];
+}
+// 0, or hipErrorInvalidValue when a grid / partial buffer was already sized with other caps
+extern "C" int mbk_set_learner_occupancy(int fwd, int bwd) {
+  fwd = fwd < 0 ? 0 : fwd;
+  bwd = bwd < 0 ? 0 : bwd;
+  if (g_occ_read && (fwd != g_occ_cap[0] || bwd != g_occ_cap[1])) return (int)hipErrorInvalidValue;
+  g_occ_cap[0] = fwd;
+  g_occ_cap[1] = bwd;
+  return 0;
 }

@@ -709,7 +709,7 @@ int res_grid(int N, int H, int W, int imgs) {
                                                    sm) != hipSuccess || per < 1)
     per = 1;
   const int nrounds = (N + imgs - 1) / imgs;
-  return (int)std::max(1L, std::min((long)nrounds, (long)ncu * per));
+  return (int)std::max(1L, std::min((long)nrounds, (long)ncu * mbk_occ_b(per)));
 }
 
 }  // namespace
@@ -1942,7 +1942,7 @@ static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
     per = 1;
   // work items: images per wave (wave-owned) or rounds of imgs images per workgroup
   const int nrounds = fast ? (N + kThreads / 64 - 1) / (kThreads / 64) : (N + imgs - 1) / imgs;
-  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)ncu * per))),
+  hipLaunchKernelGGL(kfn, dim3(std::max(1L, std::min((long)nrounds, (long)ncu * mbk_occ_f(per)))),
                      dim3(kThreads), smf, stream, a);
   return (int)hipGetLastError();
 }
@@ -2021,7 +2021,7 @@ extern "C" int mbk_res_bwd32_team_parts(int N, int H, int W) {
   }
   const int64_t nitems = ((int64_t)N * H * W + 31) / 32;
   const int64_t wgs = (nitems + rbt::NT - 1) / rbt::NT;
-  return (int)(rbt::NT * std::max<int64_t>(1, std::min<int64_t>(wgs, (int64_t)cus * (W == 4 ? per4 : per2))));
+  return (int)(rbt::NT * std::max<int64_t>(1, std::min<int64_t>(wgs, (int64_t)cus * mbk_occ_b(W == 4 ? per4 : per2))));
 }
 
 // The 32-channel block backward on 4x4 / 2x2 maps by wave teams (res_bwd32_team_kernel):
@@ -2105,7 +2105,7 @@ extern "C" int mbk_res_blk32_fwd_wave(const void* x, void* u, void* y, const voi
                  {b[0], b[1]}, N, H, W, 1};
   const int64_t nq = ((int64_t)N * H * W + 15) / 16;
   const int64_t groups = (nq + rbw::NW - 1) / rbw::NW;
-  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, (int64_t)cus * (W == 4 ? per4 : per2)));
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, (int64_t)cus * mbk_occ_f(W == 4 ? per4 : per2)));
   void* args[] = {(void*)&a};
   (void)hipLaunchKernel(kfn, dim3(grid), dim3(rbw::kPT), args, sm, stream);
   return (int)hipGetLastError();
@@ -2139,7 +2139,7 @@ extern "C" int mbk_res_blk32_fwd(const void* x, void* u, void* y, const void* co
           hipSuccess || per < 1)
     per = 1;
   const int nrounds = (N + imgs - 1) / imgs;
-  hipLaunchKernelGGL(kfn, dim3(std::max(1, std::min(nrounds, ncu * per))), dim3(kThreads), sm,
+  hipLaunchKernelGGL(kfn, dim3(std::max(1, std::min(nrounds, ncu * mbk_occ_f(per)))), dim3(kThreads), sm,
                      stream, a);
   return (int)hipGetLastError();
 }

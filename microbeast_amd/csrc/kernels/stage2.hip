@@ -190,7 +190,7 @@ extern "C" int mbk_pool_conv_fwd4(const void* x, const void* w, const float* bia
   const int npairs = (N + s2::NI - 1) / s2::NI;
   const int groups = (npairs + s2::NW - 1) / s2::NW;
   PoolConvFwd4Args a{(const bf16*)x, (const bf16*)w, bias, (bf16*)y, (uint8_t*)pidx, N};
-  hipLaunchKernelGGL(pool_conv_fwd4_kernel, dim3(std::max(1, std::min(groups, cus * per))),
+  hipLaunchKernelGGL(pool_conv_fwd4_kernel, dim3(std::max(1, std::min(groups, cus * mbk_occ_f(per)))),
                      dim3(s2::kPT), s2::SMEM, stream, a);
   return (int)hipGetLastError();
 }

@@ -472,7 +472,7 @@ extern "C" int mbk_pool_conv_bwd_parts(int N, int cin, int cout, int H, int W) {
   }
   const int rounds = one ? (N + s1::NW - 1) / s1::NW
                          : ((N + s2::NI - 1) / s2::NI + s2::NW / 2 - 1) / (s2::NW / 2);
-  return std::max(1, std::min(rounds, cus * (one ? per1 : per2)));
+  return std::max(1, std::min(rounds, cus * mbk_occ_b(one ? per1 : per2)));
 }
 
 // dx = conv^T(pool_bwd(dp, pidx)) and the conv's weight / bias gradients (dw [cout][cin][3][3],

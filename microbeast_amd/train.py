@@ -19,6 +19,7 @@ import dataclasses
 import gc
 import os
 import time
+import warnings
 
 import torch
 
@@ -193,6 +194,13 @@ def train(flags: Flags) -> dict:
     log(f"[microbeast_amd] exp={flags.exp_name} runtime={runtime} device={dev} "
         f"world={info.world_size} map={flags.env_size}x{flags.env_size} arch={flags.arch}")
 
+    if runtime == "gpu":  # before the learner sizes its partial buffers
+        from . import _native
+        if _native.kernels().mbk_set_learner_occupancy(0, flags.learner_bwd_occupancy) != 0:
+            # a learner of this process already sized its grids (tests run several trainings
+            # in one process): the caps stay as they were
+            warnings.warn("--learner_bwd_occupancy ignored: learner grids already sized in "
+                          "this process")
     model = make_model(flags, dev)
     lr = scaled_lr(flags, update_frames(flags, runtime, info.world_size))
     if lr != flags.lr:
