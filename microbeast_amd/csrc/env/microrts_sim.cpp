@@ -64,6 +64,7 @@ int MicroRTSSim::add_unit(int type, int owner, int x, int y, int res) {
   else units_[uid] = u;
   grid_[cell(x, y)] = (int16_t)uid;
   if (owner >= 0) ++cnt_[owner][type];
+  last_add_ = uid;
   return uid;
 }
 
@@ -588,14 +589,32 @@ void MicroRTSSim::bot_act(int player, float* rwo) {
   // own worker / barracks counts for the build orders (taken once per tick), and each
   // worker's index among own workers in unit order (the first ones harvest)
   const int n_workers = cnt_[player][WORKER], n_barracks = cnt_[player][BARRACKS];
-  const size_t n = units_.size();
-  int widx = 0;
-  for (size_t i = 0; i < n; ++i) {
+  // the idle own units in unit order, each with its index among the own workers before it
+  // (branch-free: owners and idleness are mixed along the list). Equivalent to one loop that
+  // acts as it goes: a bot's action never kills or busies another own unit, and a unit it
+  // creates is busy; the one thing the sequential loop sees is a produced WORKER landing in a
+  // dead slot k between the producer and the list's end, which moves the worker index of the
+  // units after k (added[] below)
+  const int n = (int)units_.size();
+  uint16_t cand[32 * 32 + 4], cw[32 * 32 + 4], added[32 * 32 + 4];
+  int nc = 0, w = 0, na = 0;
+  for (int i = 0; i < n; ++i) {
     const Unit& u = units_[i];
-    if (!u.alive || u.owner != player) continue;
-    const bool worker = u.type == WORKER;
-    if (u.busy == 0) bot_unit((int)i, player, rwo, n_workers, n_barracks, widx);
-    widx += worker;
+    const int own = (u.alive != 0) & (u.owner == player);
+    cand[nc] = (uint16_t)i;
+    cw[nc] = (uint16_t)w;
+    nc += own & (u.busy == 0);
+    w += own & (u.type == WORKER);
+  }
+  for (int q = 0; q < nc; ++q) {
+    const int i = cand[q];
+    int widx = cw[q];
+    for (int t = 0; t < na; ++t) widx += added[t] < i;
+    last_add_ = -1;
+    bot_unit(i, player, rwo, n_workers, n_barracks, widx);
+    const int k = last_add_;
+    if (k > i && k < n && units_[k].type == WORKER && units_[k].owner == player)
+      added[na++] = (uint16_t)k;
   }
 }
 
@@ -678,14 +697,8 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
   } else {
     bot_act(1, nullptr);
   }
-  // 3) advance time
-  for (Unit& u : units_) {  // branch-free: busy flips are data-dependent
-    const int16_t b = u.busy, nb = (int16_t)(b - (u.alive && b > 0));
-    u.act = (b > 0 && nb == 0 && u.alive) ? (int8_t)A_NOOP : u.act;
-    u.busy = nb;
-  }
+  // 3) terminal check (advancing time below changes nobody's life: it can come first)
   ++tick_;
-  // 4) terminal check
   int alive[2] = {0, 0};
   for (int t = 0; t < 8; ++t) {
     alive[0] += cnt_[0][t];
@@ -700,16 +713,61 @@ float MicroRTSSim::step(const uint8_t* actions, bool* done, float* raw) {
     d = true;
     last_winner_ = -1;
   }
+  // 4) advance time (skipped on a terminal step: reset() follows), branch-free since the busy
+  // flips are data-dependent; step_packed_list writes the sparse row in the same pass
+  int rows_n = 0, rows_idle = 0;
+  if (!d && rows_out_) {
+    uint32_t spill;
+    for (Unit& u : units_) {
+      const int16_t b = u.busy, nb = (int16_t)(b - (u.alive && b > 0));
+      u.act = (b > 0 && nb == 0 && u.alive) ? (int8_t)A_NOOP : u.act;
+      u.busy = nb;
+      const int live = u.alive != 0;
+      rows_idle += live & (u.owner == 0) & (u.act == A_NOOP);
+      *(rows_n < nc ? rows_out_ + rows_n : &spill) = row_entry(u, 0);
+      rows_n += live;
+    }
+  } else if (!d) {
+    for (Unit& u : units_) {
+      const int16_t b = u.busy, nb = (int16_t)(b - (u.alive && b > 0));
+      u.act = (b > 0 && nb == 0 && u.alive) ? (int8_t)A_NOOP : u.act;
+      u.busy = nb;
+    }
+  }
   float r = 0.f;
   for (int i = 0; i < kNumRewards; ++i) r += rw_[i] * rw[i];
   if (raw) for (int i = 0; i < kNumRewards; ++i) raw[i] = rw[i];
   *done = d;
   if (d) {
     reset();
-  } else {
+    if (rows_out_) rows_n = write_obs_code_list(rows_out_, &rows_idle);
+  }
+  rows_n_ = rows_n;
+  rows_idle_ = rows_idle;
+  if (!d) {
     if (validate_) compute_mask(0, mask_);
     if (external_opp_ && validate_) compute_mask(1, mask_p1_);
   }
+  return r;
+}
+
+float MicroRTSSim::step_packed_list(const uint16_t* env_actions, bool* done, uint32_t* entries,
+                                    int* n, int* idle_own) {
+  rows_out_ = entries;
+  const float r = step_packed(env_actions, done);
+  rows_out_ = nullptr;
+  *n = rows_n_;
+  if (idle_own) *idle_own += rows_idle_;
+  return r;
+}
+
+float MicroRTSSim::step_packed2_list(const uint16_t* env_actions, const uint16_t* opp_actions,
+                                     bool* done, uint32_t* entries, int* n, int* idle_own) {
+  rows_out_ = entries;
+  const float r = step_packed2(env_actions, opp_actions, done);
+  rows_out_ = nullptr;
+  *n = rows_n_;
+  if (idle_own) *idle_own += rows_idle_;
   return r;
 }
 
@@ -752,15 +810,9 @@ int MicroRTSSim::write_obs_code_list(uint32_t* entries, int* idle_own, int playe
   uint32_t spill;
   int n = 0, idle = 0;
   for (const Unit& u : units_) {
-    int px = u.x, py = u.y;
-    if (player != 0) map_xy(player, u.x, u.y, &px, &py);
-    const int own = u.owner < 0 ? 0 : (u.owner == player ? 1 : 2);
     const int live = u.alive != 0;
-    idle += live & (own == 1) & (u.act == A_NOOP);
-    const int hp = u.hp < 0 ? 0 : (u.hp > 4 ? 4 : u.hp);
-    const int res = u.res < 0 ? 0 : (u.res > 4 ? 4 : u.res);
-    const uint16_t code = mbr::cell_code(hp, res, own, u.type, u.act);
-    *(n < S ? entries + n : &spill) = (uint32_t)cell(px, py) | ((uint32_t)code << 16);
+    idle += live & (u.owner == player) & (u.act == A_NOOP);
+    *(n < S ? entries + n : &spill) = row_entry(u, player);
     n += live;
   }
   if (idle_own) *idle_own += idle;

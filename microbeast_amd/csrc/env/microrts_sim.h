@@ -103,6 +103,12 @@ class MicroRTSSim {
     }
   }
   float step_packed(const uint16_t* env_actions, bool* done);
+  // step_packed + write_obs_code_list(entries, idle_own) (player 0) in the step's last pass over
+  // the units; *n = the entries written
+  float step_packed_list(const uint16_t* env_actions, bool* done, uint32_t* entries, int* n,
+                         int* idle_own);
+  float step_packed2_list(const uint16_t* env_actions, const uint16_t* opp_actions, bool* done,
+                          uint32_t* entries, int* n, int* idle_own);
   // self-play fast path: both players' packed actions, each in its own frame
   float step_packed2(const uint16_t* env_actions, const uint16_t* opp_actions, bool* done);
   void write_obs_codes(uint16_t* out) const { write_obs_codes_as(0, out); }
@@ -145,10 +151,23 @@ class MicroRTSSim {
   int cnt_[2][8] = {};            // alive units per owner (0 / 1) and type, kept by add / kill
   const uint16_t* p16_ = nullptr;    // step_packed: agent actions decoded lazily per cell
   const uint16_t* opp16_ = nullptr;  // step_packed2: opponent's packed actions
+  uint32_t* rows_out_ = nullptr;     // step_packed_list: the sparse row's entries
+  int rows_n_ = 0, rows_idle_ = 0;   // ... and its length / the agent's idle units
+  int last_add_ = -1;                // slot of the last add_unit (bot_act's worker index)
 
   uint32_t rand_u32();
   float rand_unit();
   int cell(int x, int y) const { return y * s_ + x; }
+  // sparse-row entry of a unit from `player`'s side: cell | code << 16 (player 1: mirrored;
+  // the code is include/microrts_rules.h cell_code)
+  uint32_t row_entry(const Unit& u, int player) const {
+    const int px = player ? s_ - 1 - u.x : u.x, py = player ? s_ - 1 - u.y : u.y;
+    const int own = u.owner < 0 ? 0 : (u.owner == player ? 1 : 2);
+    const int hp = u.hp < 0 ? 0 : (u.hp > 4 ? 4 : u.hp);
+    const int res = u.res < 0 ? 0 : (u.res > 4 ? 4 : u.res);
+    return (uint32_t)cell(px, py) |
+           ((uint32_t)(hp | (res << 3) | (own << 6) | (u.type << 8) | (u.act << 11)) << 16);
+  }
   bool in_bounds(int x, int y) const { return x >= 0 && y >= 0 && x < s_ && y < s_; }
   bool empty(int x, int y) const { return in_bounds(x, y) && grid_[cell(x, y)] < 0; }
   int add_unit(int type, int owner, int x, int y, int res = 0);

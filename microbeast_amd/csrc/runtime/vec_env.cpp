@@ -212,8 +212,10 @@ int VecEnv::step_range_lists_sp(int e0, int e1, const uint32_t* act_lists,
     expand(arow, dense, 1);
     if (sp) expand(orow, dense_opp, 1);
     bool d = false;
-    const float r = sp ? sim.step_packed2(dense.data(), dense_opp.data(), &d)
-                       : sim.step_packed(dense.data(), &d);
+    uint32_t* crow = code_lists + (size_t)i * stride;
+    int n = 0;
+    const float r = sp ? sim.step_packed2_list(dense.data(), dense_opp.data(), &d, crow + 1, &n, &idle)
+                       : sim.step_packed_list(dense.data(), &d, crow + 1, &n, &idle);
     expand(arow, dense, 0);  // back to all-noop for the next env
     if (sp) expand(orow, dense_opp, 0);
     ep_ret_[i] += r;
@@ -226,8 +228,6 @@ int VecEnv::step_range_lists_sp(int e0, int e1, const uint32_t* act_lists,
     }
     reward[i] = r;
     done[i] = d ? 1 : 0;
-    uint32_t* crow = code_lists + (size_t)i * stride;
-    const int n = sim.write_obs_code_list(crow + 1, &idle);
     crow[0] = (uint32_t)n | ((uint32_t)sim.resources(0) << 16);
     if (sp) {
       uint32_t* prow = code_lists_p1 + (size_t)i * stride;
@@ -257,7 +257,9 @@ int VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t
       if (c < S) dense[c] = (uint16_t)(arow[k] >> 16);
     }
     bool d = false;
-    const float r = sims_[i]->step_packed(dense.data(), &d);
+    uint32_t* crow = code_lists + (size_t)i * stride;
+    int n = 0;
+    const float r = sims_[i]->step_packed_list(dense.data(), &d, crow + 1, &n, &idle);
     for (uint32_t k = 1; k <= na; ++k) {  // back to all-noop for the next env
       const uint32_t c = arow[k] & 0xFFFFu;
       if (c < S) dense[c] = 0;
@@ -271,8 +273,6 @@ int VecEnv::step_range_lists(int e0, int e1, const uint32_t* act_lists, uint32_t
     }
     reward[i] = r;
     done[i] = d ? 1 : 0;
-    uint32_t* crow = code_lists + (size_t)i * stride;
-    const int n = sims_[i]->write_obs_code_list(crow + 1, &idle);
     crow[0] = (uint32_t)n | ((uint32_t)sims_[i]->resources(0) << 16);
   }
   return idle;

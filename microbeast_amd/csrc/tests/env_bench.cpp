@@ -83,10 +83,11 @@ int main(int argc, char** argv) {
       if (i + 2 < E) __builtin_prefetch(sims[i + 2]);
       if (i + 1 < E) sims[i + 1]->prefetch();
       bool d = false;
-      rew[i] = sims[i]->step_packed(&act[(size_t)i * S], &d);
-      dn[i] = d;
       uint32_t* row = &rows[(size_t)i * (S + 1)];
-      row[0] = (uint32_t)sims[i]->write_obs_code_list(row + 1, &id);
+      int n = 0;
+      rew[i] = sims[i]->step_packed_list(&act[(size_t)i * S], &d, row + 1, &n, &id);
+      dn[i] = d;
+      row[0] = (uint32_t)n;
     }
     const auto t1 = std::chrono::steady_clock::now();
     for (int i = 0; i < E; ++i) {
