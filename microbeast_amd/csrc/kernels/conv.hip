@@ -751,7 +751,8 @@ inline size_t wg_tile_bytes(int cin, int cout, int imgs, int H, int W, int wt) {
            ((((size_t)imgs * H * W * cout * 2) + 15) & ~(size_t)15) + 64;
   const int rbx = (wt + 2) * cin * 2 + (cin == 32 ? 32 : 64);
   const int rbd = wt * cout * 2 + (cout == 32 ? 32 : 128);
-  return (size_t)imgs * (H + 2) * rbx + 64 + (size_t)imgs * H * rbd + 64;
+  // (cin > cout: the tap-shifted dY tile carries a zero halo, see conv_wgrad_kernel TSH)
+  return (size_t)imgs * (H + 2) * rbx + 64 + (size_t)imgs * (H + (cin > cout ? 2 : 0)) * rbd + 64;
 }
 // the band-layout instantiation for this shape (0: the plain layout); 24 (config 4's 24x24
 // stage 0): three 8-column chunks per band, and 24 x XPB / DPB keep the 8 / 16-wide rows'
@@ -782,13 +783,22 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   constexpr int DCH = COUT / 8;             // dY uint4 per pixel
   constexpr bool band = WT > 0;
   constexpr int RBX = wg_rbx<XPB, WT>(), RBD = wg_rbd<DPB, WT>();
+  // TSH (band layout, CIN > COUT: the stage-0 layer, 32 bit planes -> 16 channels): the tap
+  // shift moves from X to dY. dW[t] = sum_p dY[p] X[p + off_t] = sum_q dY[q - off_t] X[q], so a
+  // K block reads its CB X fragments once and one shifted dY fragment per tap: 2 + 18 tr reads
+  // per 19 MFMAs instead of 2 + 36 (the LDS array, not the MFMA, bounded the kernel). The dY
+  // tile then carries a zero halo ((H + 2) rows, pixel x at column x + 1: the 128-byte row pad
+  // already holds the two halo pixels, so the row stride and its bank residue are unchanged).
+  constexpr bool TSH = band && CIN > COUT;
+  static_assert(!TSH || (WT + 2) * DPB <= RBD, "dY halo fits the padded row");
   const int H = a.H, W = band ? WT : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;
   // wave index in an SGPR: the K-block loop's (image, band, chunk) split of the wave-uniform
   // block index then runs on the scalar unit instead of as VALU divisions
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = (lane >> 4), li = lane & 15;
-  const int IMGX = Hp * RBX, IMGD = H * RBD;  // band layout image strides
+  const int IMGX = Hp * RBX, IMGD = (TSH ? Hp : H) * RBD;  // band layout image strides
+  constexpr int DIN = TSH ? RBD + DPB : 0;  // dY tile offset of interior pixel (0, 0)
   // LDS carve: [X tile | zero row (64B) | dY tile | zero row]; reused for the final reduce
   const int xbytes = band ? a.imgs * IMGX : ((a.imgs * Hp * Wp * XPB) + 15) & ~15;
   char* xt = smem;
@@ -800,7 +810,9 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   // bit-plane staging: byte -> 8 bf16 lookup table (4 KB) after the tiles
   uint4* lut = (uint4*)(dzero + 64);
 
-  for (int e = tid; e < (xbytes + 64) / 16; e += kThreads) ((uint4*)xt)[e] = make_uint4(0, 0, 0, 0);
+  // (TSH: the dY tile too, once: its halo is never written)
+  for (int e = tid; e < (xbytes + 64 + (TSH ? dbytes : 0)) / 16; e += kThreads)
+    ((uint4*)xt)[e] = make_uint4(0, 0, 0, 0);
   for (int e = tid; e < 4; e += kThreads) ((uint4*)dzero)[e] = make_uint4(0, 0, 0, 0);
   if constexpr (BITS)
     for (int e = tid; e < 256; e += kThreads) lut[e] = expand_bits8((uint32_t)e);
@@ -889,7 +901,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
     if constexpr (!band) return e * 16;
     const int q = e % DCH, p = e / DCH;
     const int im = p / HW, r = p - im * HW, y = r / W, x = r - y * W;
-    return im * IMGD + y * RBD + x * DPB + q * 16;
+    return im * IMGD + DIN + y * RBD + x * DPB + q * 16;
   };
   auto put_d = [&](int e, uint4 v) { *(uint4*)(dt + doff_of(e)) = v; };
   auto xoff_of = [&](int e) {
@@ -934,13 +946,13 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
                     "16-wide stage-0 layout, 4 waves x 4 channels");
       {  // this wave's 8 bytes of every pixel: lane = (row y % 4, column), rows 4 apart (one
          // pointer add per store instead of the pixel -> (image, row, column) split per store)
-        char* zp = dt + (lane >> 4) * RBD + (lane & 15) * DPB + 8 * wave;
+        char* zp = dt + DIN + (lane >> 4) * RBD + (lane & 15) * DPB + 8 * wave;
         for (int im = 0; im < nimg; ++im, zp += IMGD - H * RBD)
           for (int y4 = 0; y4 < H; y4 += 4, zp += 4 * RBD) *(uint2*)zp = make_uint2(0, 0);
       }
       asm volatile("" ::: "memory");
       if (s_im < nimg) {
-        char* dimg = dt + s_im * IMGD;
+        char* dimg = dt + s_im * IMGD + DIN;
 #pragma unroll
         for (int ph = 0; ph < 4; ++ph) {
           const int oy = 2 * (s_k >> 2) + (ph >> 1), ox = 2 * (s_k & 3) + (ph & 1);
@@ -976,6 +988,36 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         const int y = (rem / CPR) * 4 + G, x0 = (rem % CPR) * 8 + (li >> 2);
         const char* db = dt + im * IMGD + y * RBD + x0 * DPB + 8 * (li & 3);
         const char* xb = xt + im * IMGX + y * RBX + x0 * XPB + 8 * (li & 3);
+        if constexpr (TSH) {
+          // K = the block's 32 X pixels q (B: the centre tap of the halo'd X tile); tap t's A
+          // is dY at q - off_t = halo'd dY (y + 2 - t / 3, x + 2 - t % 3); the centre one
+          // (t = 4, the unshifted dY) also feeds the bias MFMA
+          Frag8 bx[CB];
+#pragma unroll
+          for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) bx[cb].h[h] = tr_read(xb + RBX + (1 + 4 * h) * XPB + cb * 32);
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            Frag8 at[MB];
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                at[mb].h[h] = tr_read(db + (2 - t / 3) * RBD + (2 - t % 3 + 4 * h) * DPB + mb * 32);
+            if (t == 4)
+#pragma unroll
+              for (int mb = 0; mb < MB; ++mb)
+                accb[mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[mb].v, ones.v, accb[mb], 0, 0, 0);
+#pragma unroll
+            for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+              for (int mb = 0; mb < MB; ++mb)
+                acc[mb][t * CB + cb] =
+                    __builtin_amdgcn_mfma_f32_16x16x32_bf16(at[mb].v, bx[cb].v, acc[mb][t * CB + cb], 0, 0, 0);
+          }
+          continue;
+        }
         Frag8 af[MB];
 #pragma unroll
         for (int mb = 0; mb < MB; ++mb)

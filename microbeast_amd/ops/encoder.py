@@ -94,13 +94,17 @@ def _imgs_wgrad(layer: ConvLayer, unpool: bool = False) -> int:
     if layer.W in (8, 16, 24) and layer.H % 4 == 0:
         rbx = (layer.W + 2) * layer.cin * 2 + (32 if layer.cin == 32 else 64)
         rbd = layer.W * layer.cout * 2 + (32 if layer.cout == 32 else 128)
-        per = (layer.H + 2) * rbx + layer.H * rbd
+        # (cin > cout: the tap-shifted dY tile has a zero halo: H + 2 rows)
+        per = (layer.H + 2) * rbx + (layer.H + (2 if layer.cin > layer.cout else 0)) * rbd
     else:
         per = (layer.H + 2) * (layer.W + 2) * layer.cin * 2 + hw * layer.cout * 2
     if unpool:  # the pool-fused form scatters 2 images per round (one per 32-lane half)
         imgs = min(imgs, 2)
+    # (the halo'd dY tile is ~4 % larger: the stage-0 form keeps its 2 images per round, two
+    # workgroups per CU still fit)
+    lim = (72 if layer.cin > layer.cout else 64) * 1024
     while imgs > 1:
-        if imgs * per <= 64 * 1024:
+        if imgs * per <= lim:
             break
         imgs //= 2
     return imgs
