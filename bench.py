@@ -73,6 +73,8 @@ def parse(argv=None):
     p.add_argument("--learner_bwd_occupancy", type=int, default=1,
                    help="learner backward workgroups per CU (0 = as many as fit; 1 leaves the "
                         "acting kernels a slot beside them: +4 %% over 8 seed pairs, profile 45)")
+    p.add_argument("--learner_fwd_occupancy", type=int, default=0,
+                   help="learner forward workgroups per CU (0 = as many as fit)")
     p.add_argument("--comm_rehearsal", action="store_true",
                    help="1 GPU only: every gradient bucket fires a stand-in collective kernel "
                         "on a 4th high-priority stream from the same hooks (the stream set of an "
@@ -181,7 +183,8 @@ def main(argv=None):
 
     torch.manual_seed(args.seed)
     from microbeast_amd import _native  # before the learner sizes its partial buffers
-    _native.check(_native.kernels().mbk_set_learner_occupancy(0, args.learner_bwd_occupancy),
+    _native.check(_native.kernels().mbk_set_learner_occupancy(args.learner_fwd_occupancy,
+                                                                     args.learner_bwd_occupancy),
                   "set_learner_occupancy")
     model = make_model()
     learner = Learner(model, LearnerHParams(bucket_mb=args.bucket_mb,

@@ -86,6 +86,7 @@ class Flags:
     rccl_high_priority: bool = True  # RCCL collectives on a high-priority stream
     learner_bwd_occupancy: int = 1  # gpu runtime: learner backward workgroups per CU (0 = as
                                     # many as fit; 1 leaves the acting kernels a slot, profile 45)
+    learner_fwd_occupancy: int = 0  # gpu runtime: learner forward workgroups per CU (0 = as many as fit)
     lr_scaling: str = "sqrt"      # none | sqrt | linear: lr *= max(1, frames per update / lr_base_batch)^k
     lr_base_batch: int = 524288   # frames per update the base lr is tuned for (1 GPU, 4 x 8192 x 64 / 4)
     episode_sync_every: int = 10  # DP: gather finished episodes to rank 0 every N updates

@@ -196,10 +196,11 @@ def train(flags: Flags) -> dict:
 
     if runtime == "gpu":  # before the learner sizes its partial buffers
         from . import _native
-        if _native.kernels().mbk_set_learner_occupancy(0, flags.learner_bwd_occupancy) != 0:
+        if _native.kernels().mbk_set_learner_occupancy(flags.learner_fwd_occupancy,
+                                                     flags.learner_bwd_occupancy) != 0:
             # a learner of this process already sized its grids (tests run several trainings
             # in one process): the caps stay as they were
-            warnings.warn("--learner_bwd_occupancy ignored: learner grids already sized in "
+            warnings.warn("--learner_fwd/bwd_occupancy ignored: learner grids already sized in "
                           "this process")
     model = make_model(flags, dev)
     lr = scaled_lr(flags, update_frames(flags, runtime, info.world_size))

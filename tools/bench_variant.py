@@ -29,7 +29,7 @@ def main():
 
         def rpatched(self, *a, **k):
             for key, v in rt_sets.items():
-                k[key] = bool(int(v))
+                k[key] = int(v)
             rinit(self, *a, **k)
         G.GpuActorRuntime.__init__ = rpatched
     from microbeast_amd.ops import encoder as E

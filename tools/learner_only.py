@@ -33,14 +33,15 @@ def main():
     ap.add_argument("--lib", default=None, help="variant library dir (tools/variant.py)")
     ap.add_argument("--bwd_occ", type=int, default=0,
                     help="backward workgroups per CU (the GPU actor runtime's cap is 1; 0: none)")
+    ap.add_argument("--fwd_occ", type=int, default=0, help="forward workgroups per CU (as --bwd_occ)")
     a = ap.parse_args()
     import torch
 
     from tools.variant import use_lib
     use_lib(a.lib)
-    if a.bwd_occ:
+    if a.bwd_occ or a.fwd_occ:
         from microbeast_amd import _native as N
-        N.check(N.kernels().mbk_set_learner_occupancy(0, a.bwd_occ), "set_learner_occupancy")
+        N.check(N.kernels().mbk_set_learner_occupancy(a.fwd_occ, a.bwd_occ), "set_learner_occupancy")
 
     from microbeast_amd.config import parse_flags
     from microbeast_amd.learner import Learner, LearnerHParams
