@@ -89,6 +89,7 @@ _SIGS = {
     "mbk_pool_conv_bwd_partial_floats": [c_int, c_int, c_int],
     "mbk_conv_set_grid_cap": [c_int],
     "mbk_set_learner_occupancy": [c_int, c_int],
+    "mbk_set_work_queues": [c_int],
     "mbk_conv0_row_set": [c_int],
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],
     "mbk_fc_wgrad": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,

@@ -17,7 +17,47 @@ int mbk_occ_cap(int bwd);
 inline int mbk_occ_f(int per) { const int c = mbk_occ_cap(0); return c > 0 && per > c ? c : per; }
 inline int mbk_occ_b(int per) { const int c = mbk_occ_cap(1); return c > 0 && per > c ? c : per; }
 
+// Dynamic work queues for the learner's persistent kernels (round 6). A persistent grid walking
+// its items by a static stride (blockIdx.x, + gridDim.x, ...) lasts as long as its latest-
+// starting workgroup: under the GPU actor runtime an acting launch holds a CU's slots for
+// 0.2-1 ms, so some of the grid's workgroups start that much later and still own a full share.
+// With a queue, each wave takes its next item (an image) from a counter, so early waves take
+// more and the kernel ends when the work does. The counter pair {next item, waves done} lives
+// per (stream, call site) and resets itself: the last wave to finish zeroes it for the next
+// launch on that stream (launches on one stream are ordered). Kernels whose items only write
+// their own outputs use it (forward kernels): results are bit-identical in any order.
+// mbk_work_queue: nullptr (static striding) while queues are off, or the stream is capturing a
+// graph before its counters exist.
+int* mbk_work_queue(hipStream_t stream, int site);
+constexpr int kQueueConv0 = 0, kQueueResFwd16 = 1, kQueueSites = 8;
+
 namespace mbk {
+
+// the wave's next item: lane 0 takes a ticket (a vector atomic: the branch is per lane)
+__device__ __forceinline__ int wave_ticket(int* q) {
+  int t = 0;
+  if ((threadIdx.x & 63) == 0)
+    t = __hip_atomic_fetch_add(q, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __shfl(t, 0, 64);
+}
+// Tickets hand out chunks of kQueueChunk items (one atomic per image on one address serialised
+// in L2: 26 vs 17 ms per learner update): the wave's next item after `it` inside its chunk
+// [.., cend), else the first of a new chunk (>= n: no work left; cend is updated)
+constexpr int kQueueChunk = 16;
+__device__ __forceinline__ int wave_next_item(int* q, int it, int& cend, int n) {
+  if (it + 1 < cend) return it + 1;
+  const int t = wave_ticket(q) * kQueueChunk;
+  cend = min(n, t + kQueueChunk);
+  return t;
+}
+// after the wave's last ticket (one past the work): the grid's last such wave resets the queue
+__device__ __forceinline__ void wave_queue_done(int* q, int total_waves) {
+  if ((threadIdx.x & 63) == 0 &&
+      __hip_atomic_fetch_add(q + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total_waves - 1) {
+    __hip_atomic_store(q, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 // microRTS GridMode per-cell action components (reference model.py:168,
 // libs/utils.py:40-44): nvec = [6,4,4,4,4,7,49], 78 logits per cell.

@@ -30,6 +30,8 @@
 #include "common.h"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
 
 using namespace mbk;
 
@@ -78,6 +80,7 @@ struct ConvFwdArgs {
   uint8_t* pool_idx;  // pooled argmax (0..8 in the 3x3 window) for the backward
   int N, H, W, imgs, relu_in, pool;
   const float* wscale;  // fp8 path: per-output-channel dequant scale of the e4m3 weights
+  int* queue = nullptr;  // HT > 0 row kernels: per-wave image queue (common.h), null: static
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -602,6 +605,52 @@ __device__ __forceinline__ void conv0_row_body(const ConvFwdArgs& a) {
     for (int y = 0; y < NR; ++y) dst[y] = ok ? xb[y * W] : 0u;
   };
 
+  if constexpr (HT > 0) {
+    if (a.queue) {  // per-wave image queue: the wave's LDS slot stays `wave`, its image varies
+      int cend = 0;
+      int img = mbk::wave_next_item(a.queue, -1, cend, a.N);
+      while (img < a.N) {
+        const uint32_t* xb = (const uint32_t*)a.x + (size_t)img * HW + li;
+#pragma unroll
+        for (int y = 0; y < NR; ++y) rows[y] = xb[y * W];
+        const int nxt = mbk::wave_next_item(a.queue, img, cend, a.N);  // (a new chunk's ticket
+                                                                       // is in flight meanwhile)
+        const int img0 = img - wave;                // (img0 + wave = img)
+        XRow3 r[4];
+        r[0] = xzero;
+        r[1] = xrow(rows[0]);
+        r[2] = NR > 1 ? xrow(rows[1 % NR]) : xzero;
+        r[3] = NR > 2 ? xrow(rows[2 % NR]) : xzero;
+#pragma unroll
+        for (int y = 0; y < NR; y += 2) {
+          const uint32_t any = (y >= 1 ? rows[(y + NR - 1) % NR] : 0u) | rows[y % NR] |
+                               (y + 1 < NR ? rows[(y + 1) % NR] : 0u) |
+                               (y + 2 < NR ? rows[(y + 2) % NR] : 0u);
+          row_pair(r, y, wave, img0, 0, __ballot(any != 0u) == 0ull);
+          r[0] = r[2];
+          r[1] = r[3];
+          r[2] = y + 3 < NR ? xrow(rows[(y + 3) % NR]) : xzero;
+          r[3] = y + 4 < NR ? xrow(rows[(y + 4) % NR]) : xzero;
+        }
+        if (a.pool) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          const int Ho = (H + 1) >> 1, Wo = W >> 1;
+          if (HT == 16)
+            pool_img16<COUT, OSTR>(otile + (size_t)wave * HW * OSTR, (size_t)img * Ho * Wo * COUT,
+                                   a.y, a.pool_idx, lane);
+          else
+            mbk::pool_tile<COUT, OSTR, 64>(otile + (size_t)wave * HW * OSTR, H, W, 1,
+                                           (size_t)img * Ho * Wo * COUT, a.y, a.pool_idx, lane);
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+        img = nxt;
+      }
+      mbk::wave_queue_done(a.queue, (int)gridDim.x * (kThreads / 64));
+      return;
+    }
+  }
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * kRowImgs;
     const int nimg = min(kRowImgs, a.N - img0);
@@ -1524,6 +1573,7 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     const auto kfn = cout == 16 ? (hb ? conv0_row16_kernel : conv0_row_kernel<0, 16>)
                                 : (hb ? conv0_row_kernel<16, 32> : conv0_row_kernel<0, 32>);
     const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)kfn, sm0);
+    if (hb) a.queue = mbk_work_queue(stream, kQueueConv0);
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();
   }
@@ -1774,5 +1824,32 @@ extern "C" int mbk_set_learner_occupancy(int fwd, int bwd) {
   if (g_occ_read && (fwd != g_occ_cap[0] || bwd != g_occ_cap[1])) return (int)hipErrorInvalidValue;
   g_occ_cap[0] = fwd;
   g_occ_cap[1] = bwd;
+  return 0;
+}
+
+// ------------------------------------------------------------------ learner work queues
+static int g_work_queues = 1;  // mbk_set_work_queues (A/B)
+int* mbk_work_queue(hipStream_t stream, int site) {
+  if (!g_work_queues || site < 0 || site >= kQueueSites) return nullptr;
+  static std::mutex mu;
+  static std::map<hipStream_t, int*> queues;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = queues.find(stream);
+  if (it == queues.end()) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
+      return nullptr;
+    int* p = nullptr;
+    if (hipMalloc(&p, kQueueSites * 2 * sizeof(int)) != hipSuccess ||
+        hipMemsetAsync(p, 0, kQueueSites * 2 * sizeof(int), stream) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    it = queues.emplace(stream, p).first;
+  }
+  return it->second + 2 * site;
+}
+extern "C" int mbk_set_work_queues(int on) {
+  g_work_queues = on ? 1 : 0;
   return 0;
 }

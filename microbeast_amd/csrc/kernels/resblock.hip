@@ -745,6 +745,7 @@ struct ResFwdArgs {
   const float* bs;
   bf16* ps;
   uint8_t* pidx;
+  int* queue = nullptr;          // wave-owned 8x8 form: per-wave image queue (common.h)
 };
 
 // STAGE: + the next ConvSequence's conv and pool (conv.hip conv_fwd<16, 32> with its pooled
@@ -973,7 +974,12 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_w88_kernel(ResFwdArgs a) {
     so[k] = ((px >> 3) + 1) * RB + ((px & 7) + 1) * PB + (e & 1) * 16;
   }
   const int nw = gridDim.x * (kThreads / 64);
-  int img = blockIdx.x * (kThreads / 64) + wave;
+  // images: a static stride, or (a.queue) the next tickets of the per-wave queue; the next
+  // image's ticket and rows are in flight during the current one
+  int* const q = a.queue;
+  int cend = 0;
+  int img = q ? mbk::wave_next_item(q, -1, cend, a.N) : (int)blockIdx.x * (kThreads / 64) + wave;
+  int nxt = q ? (img < a.N ? mbk::wave_next_item(q, img, cend, a.N) : a.N) : img + nw, nn = a.N;
   uint4 pp[2];
   auto fetch = [&](int im) {
     const uint4* src = (const uint4*)(a.p + (size_t)im * HW * C);
@@ -981,13 +987,14 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_w88_kernel(ResFwdArgs a) {
     pp[1] = src[lane + 64];
   };
   if (img < a.N) fetch(img);
-  for (; img < a.N; img += nw) {
+  for (; img < a.N; img = nxt, nxt = nn) {
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       *(uint4*)(R + TX + so[k]) = pp[k];
       *(uint4*)(R + TR + so[k]) = relu8(pp[k]);
     }
-    if (img + nw < a.N) fetch(img + nw);
+    if (nxt < a.N) fetch(nxt);
+    nn = q ? (nxt < a.N ? mbk::wave_next_item(q, nxt, cend, a.N) : a.N) : nxt + nw;
     wave_lds_order();
     const size_t gpix = (size_t)img * HW;
 #pragma unroll
@@ -1084,6 +1091,7 @@ __global__ __launch_bounds__(kThreads) void res_fwd16_w88_kernel(ResFwdArgs a) {
       wave_lds_order();
     }
   }
+  if (q) mbk::wave_queue_done(q, nw);
 }
 
 // One 32-channel residual block per launch (stages 1-2 of the IMPALA trunk):
@@ -1919,6 +1927,7 @@ static int res_fwd16_launch(ResFwdArgs a, hipStream_t stream) {
     return (int)hipErrorInvalidValue;
   const bool fast = H == 8 && W == 8;  // (imgs: the generic kernel's round size only)
   const size_t smf = fast ? resf_w88_smem() : sm;
+  if (fast) a.queue = mbk_work_queue(stream, kQueueResFwd16);
   auto kfn = fast ? (st ? res_fwd16_w88_kernel<true> : res_fwd16_w88_kernel<false>)
            : st ? (W == 8 ? res_fwd16_kernel<8, true> : W == 5 ? res_fwd16_kernel<5, true>
                    : W == 12 ? res_fwd16_kernel<12, true> : W == 4 ? res_fwd16_kernel<4, true>
