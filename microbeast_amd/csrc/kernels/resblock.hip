@@ -1113,6 +1113,7 @@ struct ResBlk32Args {
   const bf16* w[2];  // packed fwd weights [32][9][32] of conv0, conv1
   const float* b[2];
   int N, H, W, imgs;
+  int* queue = nullptr;  // res_blk32_wave_kernel: per-wave queue of 16-pixel blocks (common.h)
 };
 
 // Tile geometry (halo'd pixel (hy, hx) of image im at im * is + hy * rs + hx * pb). 4-wide maps
@@ -1295,7 +1296,12 @@ __global__ __launch_bounds__(rbw::kPT) void res_blk32_wave_kernel(ResBlk32Args a
   const int64_t npix = (int64_t)a.N * MW * MW;
   const int nq = (int)((npix + 15) >> 4);
   const int step = gridDim.x * NW;
-  const int first = blockIdx.x * NW + wave;
+  // blocks: a static stride, or (a.queue) the per-wave queue's chunks (next block in flight)
+  int* const wq = a.queue;
+  int cend = 0;
+  const int first = wq ? mbk::wave_next_item(wq, -1, cend, nq) : (int)blockIdx.x * NW + wave;
+  int nxt = wq ? (first < nq ? mbk::wave_next_item(wq, first, cend, nq) : nq) : first + step;
+  int nn = nq;
   uint4 pf;
   auto fetch = [&](int q) {
     const int64_t e = (int64_t)q * 64 + lane;  // uint4 index (4 per pixel)
@@ -1303,9 +1309,10 @@ __global__ __launch_bounds__(rbw::kPT) void res_blk32_wave_kernel(ResBlk32Args a
   };
   wave_lds_order();
   if (first < nq) fetch(first);
-  for (int q = first; q < nq; q += step) {
+  for (int q = first; q < nq; q = nxt, nxt = nn) {
     *(uint4*)(Tx + sofs) = pf;
-    if (q + step < nq) fetch(q + step);
+    if (nxt < nq) fetch(nxt);
+    nn = wq ? (nxt < nq ? mbk::wave_next_item(wq, nxt, cend, nq) : nq) : nxt + step;
     wave_lds_order();
     const int64_t m = (int64_t)q * 16 + li;  // global pixel of this lane
     const bool valid = m < npix;
@@ -1342,6 +1349,7 @@ __global__ __launch_bounds__(rbw::kPT) void res_blk32_wave_kernel(ResBlk32Args a
       wave_lds_order();
     }
   }
+  if (wq) mbk::wave_queue_done(wq, step);
 }
 
 // ------------------------------------------------------------------ fused backward, 32 ch
@@ -2112,6 +2120,7 @@ extern "C" int mbk_res_blk32_fwd_wave(const void* x, void* u, void* y, const voi
   }
   ResBlk32Args a{(const bf16*)x, (bf16*)u, (bf16*)y, {(const bf16*)w[0], (const bf16*)w[1]},
                  {b[0], b[1]}, N, H, W, 1};
+  a.queue = mbk_work_queue(stream, kQueueBlk32);
   const int64_t nq = ((int64_t)N * H * W + 15) / 16;
   const int64_t groups = (nq + rbw::NW - 1) / rbw::NW;
   const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(groups, (int64_t)cus * mbk_occ_f(W == 4 ? per4 : per2)));

@@ -57,6 +57,7 @@ struct PoolConvFwd4Args {
   bf16* y;            // [N][2][2][32] pooled
   uint8_t* pidx;      // [N][2][2][32] argmax taps (nullable)
   int N;
+  int* queue = nullptr;  // per-wave queue of image pairs (common.h), null: static stride
 };
 
 __global__ __launch_bounds__(s2::kPT) void pool_conv_fwd4_kernel(PoolConvFwd4Args a) {
@@ -86,7 +87,12 @@ __global__ __launch_bounds__(s2::kPT) void pool_conv_fwd4_kernel(PoolConvFwd4Arg
   const int oy = opx >> 1, ox = opx & 1;
   const int npairs = (a.N + NI - 1) / NI;
   const int step = gridDim.x * NW;
-  const int first = blockIdx.x * NW + wave;
+  int* const wq = a.queue;
+  int cend = 0;
+  const int first = wq ? mbk::wave_next_item(wq, -1, cend, npairs) : (int)blockIdx.x * NW + wave;
+  int nxt = wq ? (first < npairs ? mbk::wave_next_item(wq, first, cend, npairs) : npairs)
+               : first + step;
+  int nn = npairs;
   static_assert(NI == 2, "named prefetch registers");
   uint4 pf0, pf1;  // (named: an indexed register array went to scratch)
   auto fetch = [&](int pr) {
@@ -96,10 +102,11 @@ __global__ __launch_bounds__(s2::kPT) void pool_conv_fwd4_kernel(PoolConvFwd4Arg
   };
   wave_lds_order();
   if (first < npairs) fetch(first);
-  for (int pr = first; pr < npairs; pr += step) {
+  for (int pr = first; pr < npairs; pr = nxt, nxt = nn) {
     *(uint4*)(R + sofs) = pf0;
     *(uint4*)(R + XB + sofs) = pf1;
-    if (pr + step < npairs) fetch(pr + step);
+    if (nxt < npairs) fetch(nxt);
+    nn = wq ? (nxt < npairs ? mbk::wave_next_item(wq, nxt, cend, npairs) : npairs) : nxt + step;
     wave_lds_order();
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -165,6 +172,7 @@ __global__ __launch_bounds__(s2::kPT) void pool_conv_fwd4_kernel(PoolConvFwd4Arg
     }
     wave_lds_order();  // the next pair's staging overwrites the tiles
   }
+  if (wq) mbk::wave_queue_done(wq, step);
 }
 
 }  // namespace
@@ -190,6 +198,7 @@ extern "C" int mbk_pool_conv_fwd4(const void* x, const void* w, const float* bia
   const int npairs = (N + s2::NI - 1) / s2::NI;
   const int groups = (npairs + s2::NW - 1) / s2::NW;
   PoolConvFwd4Args a{(const bf16*)x, (const bf16*)w, bias, (bf16*)y, (uint8_t*)pidx, N};
+  a.queue = mbk_work_queue(stream, kQueuePoolConv4);
   hipLaunchKernelGGL(pool_conv_fwd4_kernel, dim3(std::max(1, std::min(groups, cus * mbk_occ_f(per)))),
                      dim3(s2::kPT), s2::SMEM, stream, a);
   return (int)hipGetLastError();
