@@ -70,9 +70,11 @@ def parse(argv=None):
                    help="rehearsal only: allow more ranks than GPUs (ranks share a GPU over gloo)")
     p.add_argument("--allreduce_dtype", type=str, default="fp32", help="fp32 | bf16 payload")
     p.add_argument("--bucket_mb", type=float, default=8.0)
-    p.add_argument("--learner_bwd_occupancy", type=int, default=1,
+    p.add_argument("--learner_bwd_occupancy", type=int, default=-1,
                    help="learner backward workgroups per CU (0 = as many as fit; 1 leaves the "
-                        "acting kernels a slot beside them: +4 %% over 8 seed pairs, profile 45)")
+                        "acting kernels a slot beside them: +4-7 %% on the headline, profile 45; "
+                        "-1 = auto: 1 for impala_flat, 0 for the learner-heavy gridnet / "
+                        "impala_deep, where the cap measured -2 / -7 %%)")
     p.add_argument("--learner_fwd_occupancy", type=int, default=0,
                    help="learner forward workgroups per CU (0 = as many as fit)")
     p.add_argument("--comm_rehearsal", action="store_true",
@@ -183,9 +185,10 @@ def main(argv=None):
 
     torch.manual_seed(args.seed)
     from microbeast_amd import _native  # before the learner sizes its partial buffers
-    _native.check(_native.kernels().mbk_set_learner_occupancy(args.learner_fwd_occupancy,
-                                                                     args.learner_bwd_occupancy),
-                  "set_learner_occupancy")
+    from microbeast_amd.config import bwd_occupancy
+    _native.check(_native.kernels().mbk_set_learner_occupancy(
+        args.learner_fwd_occupancy, bwd_occupancy(args.learner_bwd_occupancy, args.arch)),
+        "set_learner_occupancy")
     model = make_model()
     learner = Learner(model, LearnerHParams(bucket_mb=args.bucket_mb,
                                             allreduce_dtype=args.allreduce_dtype,

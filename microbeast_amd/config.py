@@ -84,7 +84,7 @@ class Flags:
     bucket_mb: float = 8.0
     allreduce_dtype: str = "fp32"  # fp32 | bf16 gradient all-reduce payload (fp32 master grads)
     rccl_high_priority: bool = True  # RCCL collectives on a high-priority stream
-    learner_bwd_occupancy: int = 1  # gpu runtime: learner backward workgroups per CU (0 = as
+    learner_bwd_occupancy: int = -1  # gpu runtime: learner backward workgroups per CU (-1 = auto; 0 = as
                                     # many as fit; 1 leaves the acting kernels a slot, profile 45)
     learner_fwd_occupancy: int = 0  # gpu runtime: learner forward workgroups per CU (0 = as many as fit)
     lr_scaling: str = "sqrt"      # none | sqrt | linear: lr *= max(1, frames per update / lr_base_batch)^k
@@ -163,3 +163,13 @@ def parse_flags(argv=None, interactive: bool | None = None) -> Flags:
 
 
 __all__ = ["Flags", "build_parser", "parse_flags", "strtobool", "field"]
+
+
+def bwd_occupancy(requested: int, arch: str) -> int:
+    """The learner's backward workgroups per CU under the GPU actor runtime (-1 = auto): one
+    for the headline IMPALA-flat model, whose acting kernels need a slot beside the learner
+    (+4-7 %), none for the learner-heavy GridNet / deep IMPALA configs (the cap measured -7 /
+    -2 % there, profile 45)."""
+    if requested >= 0:
+        return requested
+    return 1 if arch == "impala_flat" else 0

@@ -777,6 +777,9 @@ __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
 }
 
 constexpr int kPFW = 4;  // wgrad prefetch slots per thread for X and for dY
+#ifndef MBK_WGRAD_TSH
+#define MBK_WGRAD_TSH 1  // build knob (tools/variant.py): 0 = the tap shift on X (A/B only)
+#endif
 
 // Band layout of the weight-gradient tiles (WT > 0: compile-time map width 8 or 16, H % 4
 // == 0). A tr read gives lanes 0-31 32 bytes of 4 consecutive pixels each for the lane
@@ -838,7 +841,7 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
   // per 19 MFMAs instead of 2 + 36 (the LDS array, not the MFMA, bounded the kernel). The dY
   // tile then carries a zero halo ((H + 2) rows, pixel x at column x + 1: the 128-byte row pad
   // already holds the two halo pixels, so the row stride and its bank residue are unchanged).
-  constexpr bool TSH = band && CIN > COUT;
+  constexpr bool TSH = MBK_WGRAD_TSH && band && CIN > COUT;
   static_assert(!TSH || (WT + 2) * DPB <= RBD, "dY halo fits the padded row");
   const int H = a.H, W = band ? WT : a.W, HW = H * W, Hp = H + 2, Wp = W + 2;
   const float inv_hw = 1.f / (float)HW, inv_w = 1.f / (float)W;

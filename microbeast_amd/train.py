@@ -23,7 +23,7 @@ import warnings
 
 import torch
 
-from .config import Flags
+from .config import Flags, bwd_occupancy
 from .learner import Learner, LearnerHParams
 from .models.factory import make_model
 from .parallel import dist as D
@@ -197,7 +197,8 @@ def train(flags: Flags) -> dict:
     if runtime == "gpu":  # before the learner sizes its partial buffers
         from . import _native
         if _native.kernels().mbk_set_learner_occupancy(flags.learner_fwd_occupancy,
-                                                     flags.learner_bwd_occupancy) != 0:
+                                                     bwd_occupancy(flags.learner_bwd_occupancy,
+                                                                   flags.arch)) != 0:
             # a learner of this process already sized its grids (tests run several trainings
             # in one process): the caps stay as they were
             warnings.warn("--learner_fwd/bwd_occupancy ignored: learner grids already sized in "
