@@ -90,6 +90,7 @@ _SIGS = {
     "mbk_conv_set_grid_cap": [c_int],
     "mbk_set_learner_occupancy": [c_int, c_int],
     "mbk_set_work_queues": [c_int],
+    "mbk_set_work_queue_site": [c_int, c_int],
     "mbk_conv0_row_set": [c_int],
     "mbk_fc_wgrad_parts": [c_int, c_int, c_int],
     "mbk_fc_wgrad": [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,

@@ -30,7 +30,7 @@ inline int mbk_occ_b(int per) { const int c = mbk_occ_cap(1); return c > 0 && pe
 // graph before its counters exist.
 int* mbk_work_queue(hipStream_t stream, int site);
 constexpr int kQueueConv0 = 0, kQueueResFwd16 = 1, kQueueBlk32 = 2, kQueuePoolConv4 = 3,
-              kQueueSites = 8;
+              kQueueWgrad = 4, kQueueSites = 8;
 
 namespace mbk {
 

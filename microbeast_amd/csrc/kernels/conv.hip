@@ -769,6 +769,11 @@ struct ConvWgradArgs {
   // UNPOOL: dY is the max-pool backward of dp through the stored argmax bytes pidx
   const bf16* dp;       // [N][Ho][Wo][COUT]
   const uint8_t* pidx;  // [N][Ho][Wo][COUT]
+  // work queue of rounds (common.h; thread 0 takes 16-round chunks, the next rounds reach the
+  // workgroup through an LDS ring behind the LUT): a late-starting workgroup takes fewer
+  // rounds. Its partial row still sums its own rounds in its order, so the weight gradient is
+  // deterministic up to fp32 summation order only (null: static stride, bit-reproducible)
+  int* queue = nullptr;
 };
 
 __device__ __forceinline__ s16x4 tr_read(const char* lds_addr) {
@@ -965,10 +970,34 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
 
   const int nrounds = (a.N + a.imgs - 1) / a.imgs;
   const int gstep = gridDim.x;
-  if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x, pf0);
-  if ((int)blockIdx.x + gstep < nrounds) prefetch(blockIdx.x + gstep, pf1);
+  int* const wq = a.queue;
+  int* const ring = (int*)(dzero + 64 + 4096);  // rounds k .. k + 3 (queue mode)
+  int t_last = -1, t_cend = 0;                  // thread 0's queue cursor
+  auto gen = [&]() {  // thread 0: the workgroup's next round (>= nrounds: none left)
+    if (t_last >= nrounds) return t_last;
+    if (t_last + 1 < t_cend) return ++t_last;
+    const int t = __hip_atomic_fetch_add(wq, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) *
+                  mbk::kQueueChunk;
+    t_cend = min(nrounds, t + mbk::kQueueChunk);
+    return t_last = t;
+  };
+  if (wq) {
+    if (tid == 0) {
+      ring[0] = gen();
+      ring[1] = gen();
+      ring[2] = gen();
+    }
+    __syncthreads();
+    if (ring[0] < nrounds) prefetch(ring[0], pf0);
+    if (ring[1] < nrounds) prefetch(ring[1], pf1);
+  } else {
+    if ((int)blockIdx.x < nrounds) prefetch(blockIdx.x, pf0);
+    if ((int)blockIdx.x + gstep < nrounds) prefetch(blockIdx.x + gstep, pf1);
+  }
   __syncthreads();  // zero halo / zero rows visible
-  auto round = [&](int rd, PF& f) {
+  // rd2: the round this one prefetches for (two rounds ahead in this workgroup's sequence),
+  // read after the round's first barrier (queue mode: from the ring)
+  auto round = [&](int rd, PF& f, int k) {
     uint4 (&px)[kPFW] = f.px; uint4 (&pd)[kPFW] = f.pd;
     uint32_t (&pb)[kPFW] = f.pb;
     const int nimg = min(a.imgs, a.N - rd * a.imgs);
@@ -1027,7 +1056,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
         put_d(e, ((const uint4*)a.dy)[(size_t)rd * dper + e]);
     }
     __syncthreads();
-    if (rd + 2 * gstep < nrounds) prefetch(rd + 2 * gstep, f);
+    const int rd2 = wq ? ring[(k + 2) & 3] : rd + 2 * gstep;
+    if (rd2 < nrounds) prefetch(rd2, f);
 
     if constexpr (band) {
       // K block kb = (image, 4-row band, 8-column chunk); lane group G takes row G of the
@@ -1143,9 +1173,29 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(ConvWgradArgs a) {
     }
     __syncthreads();  // tile reads done before the next round is staged
   };
-  for (int rd = blockIdx.x; rd < nrounds; rd += 2 * gstep) {
-    round(rd, pf0);
-    if (rd + gstep < nrounds) round(rd + gstep, pf1);
+  if (wq) {
+    // round k: thread 0 queues round k + 3 into the ring before the round's first barrier;
+    // slot k & 3 was written three rounds (>= 2 barriers) earlier
+    for (int k = 0;; k += 2) {
+      if (tid == 0) ring[(k + 3) & 3] = gen();
+      const int r0 = ring[k & 3];
+      if (r0 >= nrounds) break;
+      round(r0, pf0, k);
+      if (tid == 0) ring[(k + 4) & 3] = gen();
+      const int r1 = ring[(k + 1) & 3];
+      if (r1 >= nrounds) break;
+      round(r1, pf1, k + 1);
+    }
+    if (tid == 0 && __hip_atomic_fetch_add(wq + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (int)gridDim.x - 1) {
+      __hip_atomic_store(wq, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(wq + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {
+    for (int rd = blockIdx.x; rd < nrounds; rd += 2 * gstep) {
+      round(rd, pf0, 0);
+      if (rd + gstep < nrounds) round(rd + gstep, pf1, 0);
+    }
   }
   // ---- reduce the 4 waves through LDS (sequential adds, no atomics)
   for (int w = 0; w < kThreads / 64; ++w) {
@@ -1492,6 +1542,7 @@ inline size_t wgrad_smem(int cin, int cout, int imgs, int H, int W, bool unpool 
   (void)unpool;  // (the pool-fused form keeps its pooled operands in registers)
   size_t t = wg_tile_bytes(cin, cout, imgs, H, W, wg_band_w(H, W));
   t += 4096;  // bit-plane lookup table (allocated for every variant: keeps the sizing simple)
+  t += 64;    // the work queue's round ring
   size_t red = (size_t)cout * 9 * cin * 4;
   return t > red ? t : red;
 }
@@ -1663,6 +1714,10 @@ extern "C" int mbk_conv_wgrad(const void* x, int in_bits, int cin, int cout, con
   if (unpool && (!dp || !pidx || imgs > 2)) return (int)hipErrorInvalidValue;
   ConvWgradArgs a{x, (const bf16*)dy, partial, N, H, W, imgs, relu_in, (const bf16*)dp,
                   (const uint8_t*)pidx};
+#ifndef MBK_WGRAD_QUEUE
+#define MBK_WGRAD_QUEUE 1  // build knob (tools/variant.py): 0 = static stride (A/B)
+#endif
+  if (MBK_WGRAD_QUEUE) a.queue = mbk_work_queue(stream, kQueueWgrad);
   const size_t sm = wgrad_smem(cin, cout, imgs, H, W, unpool);
   if (sm > 160 * 1024 || nparts < 1 || !index_math_ok(imgs, H, W))
     return (int)hipErrorInvalidValue;
@@ -1831,9 +1886,11 @@ extern "C" int mbk_set_learner_occupancy(int fwd, int bwd) {
 }
 
 // ------------------------------------------------------------------ learner work queues
-static int g_work_queues = 1;  // mbk_set_work_queues (A/B)
+static int g_work_queues = 1;                 // mbk_set_work_queues (A/B)
+static unsigned g_queue_sites = ~0u;          // mbk_set_work_queue_site: per call site
 int* mbk_work_queue(hipStream_t stream, int site) {
-  if (!g_work_queues || site < 0 || site >= kQueueSites) return nullptr;
+  if (!g_work_queues || site < 0 || site >= kQueueSites || !((g_queue_sites >> site) & 1u))
+    return nullptr;
   static std::mutex mu;
   static std::map<hipStream_t, int*> queues;
   std::lock_guard<std::mutex> lk(mu);
@@ -1854,5 +1911,12 @@ int* mbk_work_queue(hipStream_t stream, int site) {
 }
 extern "C" int mbk_set_work_queues(int on) {
   g_work_queues = on ? 1 : 0;
+  return 0;
+}
+// one call site's queue on / off (site: common.h kQueue*; 4 = the weight gradient, whose
+// partial rows then sum their rounds in a run-dependent order: bit-identity tests turn it off)
+extern "C" int mbk_set_work_queue_site(int site, int on) {
+  if (site < 0 || site >= kQueueSites) return (int)hipErrorInvalidValue;
+  g_queue_sites = on ? (g_queue_sites | (1u << site)) : (g_queue_sites & ~(1u << site));
   return 0;
 }

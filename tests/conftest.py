@@ -18,6 +18,9 @@ def pytest_configure(config):
     pixconv.set_emulation(pixconv_emulation)
 
 
+WGRAD_QUEUE_SITE = 4  # common.h kQueueWgrad
+
+
 @pytest.fixture(scope="session")
 def rt():
     from microbeast_amd import _native as N
@@ -31,4 +34,9 @@ def cuda():
         pytest.skip("no GPU")
     from microbeast_amd import _native as N
     N.kernels()  # fail loudly if the HIP library is missing
+    # the suite pins kernels and whole updates bit for bit across separate runs; the weight
+    # gradient's work queue (conv.hip, on in training and the bench) sums each workgroup's
+    # rounds in a run-dependent order, so the suite runs it with the static stride except
+    # where a test turns it on (test_gpu_conv.py::test_wgrad_queue_matches_static)
+    N.check(N.kernels().mbk_set_work_queue_site(WGRAD_QUEUE_SITE, 0), "queue site")
     return torch.device("cuda", 0)

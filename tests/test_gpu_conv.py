@@ -7,6 +7,43 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+_WGRAD_QUEUE = 4  # common.h kQueueWgrad (off for the suite: conftest.py)
+
+
+@pytest.mark.parametrize("n", [3, 700])
+def test_wgrad_queue_matches_static(cuda, n):
+    """The weight-gradient kernel on its work queue (16-round chunks taken by thread 0, the
+    next rounds through an LDS ring) against the static stride: every round summed exactly
+    once, so every parameter gradient equals the static one up to fp32 summation order."""
+    from microbeast_amd import _native as N
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encode, encoder_params
+    torch.manual_seed(5)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(n, 256, seed=n + 9).to(cuda)
+    m.features(obs[:1])
+    enc = m._hip_enc
+    params = encoder_params(m.network, 3)
+    grads = {}
+    for q in (0, 1):
+        N.check(N.kernels().mbk_set_work_queue_site(_WGRAD_QUEUE, q), "queue site")
+        for p in params:
+            p.grad = None
+        y = encode(obs, enc, params, True).float()
+        r = torch.randn(y.shape, generator=torch.Generator().manual_seed(13)).to(cuda)
+        (y * r).sum().backward()
+        torch.cuda.synchronize()
+        grads[q] = [p.grad.detach().clone() for p in params]
+    N.check(N.kernels().mbk_set_work_queue_site(_WGRAD_QUEUE, 0), "queue site")
+    assert float(grads[1][0].abs().sum()) > 0
+    for i, (a, b) in enumerate(zip(grads[0], grads[1])):
+        assert torch.isfinite(b).all(), i
+        assert _rel_safe(b, a) < 1e-5, (i, _rel_safe(b, a))
+
+
+def _rel_safe(a, b):
+    return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
+
 
 def _random_obs_bits(n, S, seed=0):
     g = torch.Generator().manual_seed(seed)
