@@ -24,10 +24,10 @@ def main():
     rt_sets = {k[3:]: v for k, v in sets.items() if k.startswith("rt.")}
     nat_sets = {k[7:]: v for k, v in sets.items() if k.startswith("native.")}
     sets = {k: v for k, v in sets.items() if not k.startswith(("rt.", "native."))}
-    if nat_sets:  # kernel-library setters, e.g. native.mbk_set_work_queues=0
-        from microbeast_amd import _native as N
+    if nat_sets:  # kernel-library setters, e.g. native.mbk_set_work_queues=0 or
+        from microbeast_amd import _native as N  # native.mbk_set_work_queue_site=5:0
         for key, v in nat_sets.items():
-            N.check(getattr(N.kernels(), key)(int(v)), key)
+            N.check(getattr(N.kernels(), key)(*[int(x) for x in v.split(":")]), key)
     if rt_sets:  # GpuActorRuntime keyword overrides, e.g. rt.fused_act=0 (the graph step)
         from microbeast_amd.runtime import gpu_actors as G
         rinit = G.GpuActorRuntime.__init__

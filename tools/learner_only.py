@@ -77,7 +77,7 @@ def main():
         obj, attr = k.split(".")
         if obj == "native":  # a kernel-library setter: native.mbk_x_set=<int>
             from microbeast_amd import _native as N
-            getattr(N.kernels(), attr)(int(v))
+            getattr(N.kernels(), attr)(*[int(x) for x in v.split(":")])  # a:b -> two ints
             continue
         m = learner.model
         tgt = m._hip_enc if obj == "enc" else m._head(dev)
