@@ -80,7 +80,7 @@ struct ConvFwdArgs {
   uint8_t* pool_idx;  // pooled argmax (0..8 in the 3x3 window) for the backward
   int N, H, W, imgs, relu_in, pool;
   const float* wscale;  // fp8 path: per-output-channel dequant scale of the e4m3 weights
-  int* queue = nullptr;  // HT > 0 row kernels: per-wave image queue (common.h), null: static
+  int* queue = nullptr;  // conv0_row kernels: per-wave image queue (common.h), null: static
 };
 
 // ------------------------------------------------------------------ forward / dgrad
@@ -596,85 +596,36 @@ __device__ __forceinline__ void conv0_row_body(const ConvFwdArgs& a) {
     }
   };
   constexpr int NR = HT > 0 ? HT : 1;
-  uint32_t rows[NR];  // HT: this wave's image, all rows (lane: column li)
-  auto load_rows = [&](int grp, uint32_t* dst) {
-    const int img = grp * kRowImgs + wave;
-    const bool ok = grp < ngroups && img < a.N;
-    const uint32_t* xb = (const uint32_t*)a.x + (size_t)(ok ? img : 0) * HW + li;
-#pragma unroll
-    for (int y = 0; y < NR; ++y) dst[y] = ok ? xb[y * W] : 0u;
-  };
 
-  if constexpr (HT > 0) {
-    if (a.queue) {  // per-wave image queue: the wave's LDS slot stays `wave`, its image varies
-      int cend = 0;
-      int img = mbk::wave_next_item(a.queue, -1, cend, a.N);
-      while (img < a.N) {
-        const uint32_t* xb = (const uint32_t*)a.x + (size_t)img * HW + li;
+  // this wave's image img0 + wave: conv rows, then its pool (each wave pools its own image's LDS
+  // rows: no workgroup barrier, so one wave's pool (VALU / LDS) overlaps the other waves' MFMA
+  // rows. LDS ops of a wave complete in order; the fences only keep the compiler from moving
+  // them across)
+  auto one = [&](int img0) {
+    if constexpr (HT > 0) {
+      uint32_t rows[NR];  // this wave's image, all rows (lane: column li)
+      {
+        const uint32_t* xb = (const uint32_t*)a.x + (size_t)(img0 + wave) * HW + li;
 #pragma unroll
         for (int y = 0; y < NR; ++y) rows[y] = xb[y * W];
-        const int nxt = mbk::wave_next_item(a.queue, img, cend, a.N);  // (a new chunk's ticket
-                                                                       // is in flight meanwhile)
-        const int img0 = img - wave;                // (img0 + wave = img)
-        XRow3 r[4];
-        r[0] = xzero;
-        r[1] = xrow(rows[0]);
-        r[2] = NR > 1 ? xrow(rows[1 % NR]) : xzero;
-        r[3] = NR > 2 ? xrow(rows[2 % NR]) : xzero;
-#pragma unroll
-        for (int y = 0; y < NR; y += 2) {
-          const uint32_t any = (y >= 1 ? rows[(y + NR - 1) % NR] : 0u) | rows[y % NR] |
-                               (y + 1 < NR ? rows[(y + 1) % NR] : 0u) |
-                               (y + 2 < NR ? rows[(y + 2) % NR] : 0u);
-          row_pair(r, y, wave, img0, 0, __ballot(any != 0u) == 0ull);
-          r[0] = r[2];
-          r[1] = r[3];
-          r[2] = y + 3 < NR ? xrow(rows[(y + 3) % NR]) : xzero;
-          r[3] = y + 4 < NR ? xrow(rows[(y + 4) % NR]) : xzero;
-        }
-        if (a.pool) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          const int Ho = (H + 1) >> 1, Wo = W >> 1;
-          if (HT == 16)
-            pool_img16<COUT, OSTR>(otile + (size_t)wave * HW * OSTR, (size_t)img * Ho * Wo * COUT,
-                                   a.y, a.pool_idx, lane);
-          else
-            mbk::pool_tile<COUT, OSTR, 64>(otile + (size_t)wave * HW * OSTR, H, W, 1,
-                                           (size_t)img * Ho * Wo * COUT, a.y, a.pool_idx, lane);
-          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-        }
-        img = nxt;
       }
-      mbk::wave_queue_done(a.queue, (int)gridDim.x * (kThreads / 64));
-      return;
-    }
-  }
-  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int img0 = grp * kRowImgs;
-    const int nimg = min(kRowImgs, a.N - img0);
-    if (HT > 0) {
-      load_rows(grp, rows);
-      if (wave < nimg) {
-        XRow3 r[4];
-        r[0] = xzero;
-        r[1] = xrow(rows[0]);
-        r[2] = NR > 1 ? xrow(rows[1 % NR]) : xzero;
-        r[3] = NR > 2 ? xrow(rows[2 % NR]) : xzero;
+      XRow3 r[4];
+      r[0] = xzero;
+      r[1] = xrow(rows[0]);
+      r[2] = NR > 1 ? xrow(rows[1 % NR]) : xzero;
+      r[3] = NR > 2 ? xrow(rows[2 % NR]) : xzero;
 #pragma unroll
-        for (int y = 0; y < NR; y += 2) {
-          const uint32_t any = (y >= 1 ? rows[(y + NR - 1) % NR] : 0u) | rows[y % NR] |
-                               (y + 1 < NR ? rows[(y + 1) % NR] : 0u) |
-                               (y + 2 < NR ? rows[(y + 2) % NR] : 0u);
-          row_pair(r, y, wave, img0, 0, __ballot(any != 0u) == 0ull);
-          r[0] = r[2];
-          r[1] = r[3];
-          r[2] = y + 3 < NR ? xrow(rows[(y + 3) % NR]) : xzero;
-          r[3] = y + 4 < NR ? xrow(rows[(y + 4) % NR]) : xzero;
-        }
+      for (int y = 0; y < NR; y += 2) {
+        const uint32_t any = (y >= 1 ? rows[(y + NR - 1) % NR] : 0u) | rows[y % NR] |
+                             (y + 1 < NR ? rows[(y + 1) % NR] : 0u) |
+                             (y + 2 < NR ? rows[(y + 2) % NR] : 0u);
+        row_pair(r, y, wave, img0, 0, __ballot(any != 0u) == 0ull);
+        r[0] = r[2];
+        r[1] = r[3];
+        r[2] = y + 3 < NR ? xrow(rows[(y + 3) % NR]) : xzero;
+        r[3] = y + 4 < NR ? xrow(rows[(y + 4) % NR]) : xzero;
       }
-    } else if (WIDE && wave < nimg) {
+    } else if constexpr (WIDE) {
       const int im = wave;
       const uint32_t* xi = (const uint32_t*)a.x + (size_t)(img0 + im) * HW;
       for (int cbk = 0; cbk < NCB; ++cbk) {
@@ -709,7 +660,7 @@ __device__ __forceinline__ void conv0_row_body(const ConvFwdArgs& a) {
           r[3] = xrw(n1);
         }
       }
-    } else if (wave < nimg) {
+    } else {
       const int im = wave;
       const uint32_t* xb = (const uint32_t*)a.x + (size_t)(img0 + im) * HW + li;
       XRow3 r[4];  // expanded input rows y-1, y, y+1, y+2 (zero outside the image)
@@ -727,7 +678,7 @@ __device__ __forceinline__ void conv0_row_body(const ConvFwdArgs& a) {
         r[3] = y + 4 < H ? xrow(n1) : xzero;
       }
     }
-    if (a.pool && wave < nimg) {
+    if (a.pool) {
       // each wave pools its own image's LDS rows: no workgroup barrier, so one wave's pool
       // (VALU / LDS) overlaps the other waves' MFMA rows. LDS ops of a wave complete in
       // order; the fences only keep the compiler from moving them across.
@@ -743,6 +694,18 @@ __device__ __forceinline__ void conv0_row_body(const ConvFwdArgs& a) {
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();   // reads done before the next group's rows overwrite
     }
+  };
+  if (a.queue) {  // per-wave image queue (16-image chunks): the wave's LDS slot stays `wave`
+    int cend = 0;
+    for (int img = mbk::wave_next_item(a.queue, -1, cend, a.N); img < a.N;
+         img = mbk::wave_next_item(a.queue, img, cend, a.N))
+      one(img - wave);
+    mbk::wave_queue_done(a.queue, (int)gridDim.x * (kThreads / 64));
+    return;
+  }
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * kRowImgs;
+    if (wave < min(kRowImgs, a.N - img0)) one(img0);
   }
 }
 
@@ -1615,6 +1578,8 @@ static int conv_fwd_launch(const void* x, int in_bits, int cin, int cout, const 
     const size_t sm0 = kLutBytes + (pool ? (size_t)kRowImgs * H * W * 16 * 2 : 0);
     const auto kfn = conv0_row_kernel<0, 16, true>;
     const int grid = fwd_grid((N + kRowImgs - 1) / kRowImgs, (const void*)kfn, sm0);
+    // (no work queue: on config 4 it measured 5.45 vs 5.85 M frames/s -- a faster learner
+    // forward there leaves the acting-bound step slower, tools/gpu_r6_c0q.sh)
     hipLaunchKernelGGL(kfn, dim3(grid), dim3(kThreads), sm0, stream, a);
     return (int)hipGetLastError();
   }

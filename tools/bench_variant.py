@@ -47,7 +47,7 @@ def main():
             setattr(self, key, bool(int(v)))
     E.HipEncoder.__init__ = patched
     import bench
-    return bench.main(argv[cut + 1:])
+    return bench.main([x for x in argv[cut + 1:] if x != "--"])  # (a second "--" from wrappers)
 
 
 if __name__ == "__main__":
