@@ -10,7 +10,8 @@
 // kernels) / mbk_occ_cap(1) (backward kernels), 0 = no cap. The acting kernels (215-256
 // VGPRs) cannot co-reside with two learner workgroups per CU (2 waves x ~224 VGPRs per SIMD)
 // and wait for the learner kernel's end; one backward workgroup per CU leaves them a slot
-// (profile 45). Default: no caps; the GPU actor runtime sets the backward cap to 1
+// (profile 45). Default: no caps; the GPU actor runtime sets the backward cap to 1 for the
+// IMPALA-flat model (config.bwd_occupancy; the learner-heavy GridNet / deep configs keep none)
 // (mbk_set_learner_occupancy, conv.hip: before the first learner allocation only, since the
 // partial-buffer sizes -- the *_parts queries -- follow it).
 int mbk_occ_cap(int bwd);
@@ -21,11 +22,14 @@ inline int mbk_occ_b(int per) { const int c = mbk_occ_cap(1); return c > 0 && pe
 // its items by a static stride (blockIdx.x, + gridDim.x, ...) lasts as long as its latest-
 // starting workgroup: under the GPU actor runtime an acting launch holds a CU's slots for
 // 0.2-1 ms, so some of the grid's workgroups start that much later and still own a full share.
-// With a queue, each wave takes its next item (an image) from a counter, so early waves take
-// more and the kernel ends when the work does. The counter pair {next item, waves done} lives
-// per (stream, call site) and resets itself: the last wave to finish zeroes it for the next
-// launch on that stream (launches on one stream are ordered). Kernels whose items only write
-// their own outputs use it (forward kernels): results are bit-identical in any order.
+// With a queue, each wave takes its next items (16-item chunks) from a counter, so early waves
+// take more and the kernel ends when the work does. The counter pair {next ticket, waves done}
+// lives per (stream, call site) and resets itself: the last wave to finish zeroes it for the
+// next launch on that stream (launches on one stream are ordered). The forward kernels' items
+// only write their own outputs: bit-identical in any order. The stage-0 weight gradient
+// (kQueueWgrad, workgroup-level: conv.hip) sums a run-dependent set of rounds per partial row:
+// reproducible up to fp32 summation order (its site can be switched off:
+// mbk_set_work_queue_site).
 // mbk_work_queue: nullptr (static striding) while queues are off, or the stream is capturing a
 // graph before its counters exist.
 int* mbk_work_queue(hipStream_t stream, int site);
