@@ -41,6 +41,41 @@ def test_wgrad_queue_matches_static(cuda, n):
         assert _rel_safe(b, a) < 1e-5, (i, _rel_safe(b, a))
 
 
+def test_forward_work_queues_bit_identical_per_stream(cuda):
+    """The learner forward's per-wave work queues (conv0_row16, res_fwd16_w88, res_blk32_wave,
+    pool_conv_fwd4; common.h) against the static stride: every saved activation and the trunk
+    output bit-identical, on the default stream twice (the counters reset themselves after each
+    launch) and on a second stream (its own counters)."""
+    from microbeast_amd import _native as N
+    from microbeast_amd.models.agent import Agent
+    from microbeast_amd.ops.encoder import encoder_params
+    torch.manual_seed(8)
+    m = Agent((16, 16, 27)).to(cuda)
+    obs = _random_obs_bits(1100, 256, seed=21).to(cuda)
+    m.features(obs[:1])
+    enc = m._hip_enc
+    params = [p.detach() for p in encoder_params(m.network, 3)]
+
+    def run():
+        y, saved = enc.forward(obs, params, save=True)
+        torch.cuda.current_stream().synchronize()
+        return [t.clone() for t in saved if isinstance(t, torch.Tensor)] + [y.clone()]
+    N.check(N.kernels().mbk_set_work_queues(0), "queues")
+    try:
+        ref = run()
+    finally:
+        N.check(N.kernels().mbk_set_work_queues(1), "queues")
+    outs = [run(), run()]
+    side = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(side):
+        outs.append(run())
+    torch.cuda.synchronize()
+    for o in outs:
+        assert len(o) == len(ref)
+        for a, b in zip(ref, o):
+            assert torch.equal(a, b)
+
+
 def _rel_safe(a, b):
     return ((a.float() - b.float()).norm() / (b.float().norm() + 1e-12)).item()
 
