@@ -1655,6 +1655,10 @@ const void* wgrad_kfn(int H, int W, bool unpool = false) {
   }
 }
 
+static int occ_b2(int per) {  // twice the backward cap
+  const int c = mbk_occ_cap(1);
+  return c > 0 && per > 2 * c ? 2 * c : per;
+}
 // number of partial rows mbk_conv_wgrad will write for this shape (<= nrounds)
 extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H, int W,
                                     int imgs, int unpool) {
@@ -1667,7 +1671,9 @@ extern "C" int mbk_conv_wgrad_parts(int in_bits, int cin, int cout, int N, int H
   WGRAD_DISPATCH(Q)
 #undef Q
   if (!kq) return -(int)hipErrorInvalidValue;
-  res = resident_blocks(kq, sm, mbk_occ_b);
+  // the backward cap leaves room for one acting workgroup (80 KB of LDS) beside the learner's:
+  // a pool-fused stage-0 form small enough for two of its workgroups beside it may take two
+  res = resident_blocks(kq, sm, unpool != 0 && 2 * sm + 80 * 1024 <= 160 * 1024 ? occ_b2 : mbk_occ_b);
   return (int)std::max(1L, std::min((long)nrounds, (long)res));
 }
 

@@ -85,7 +85,7 @@ def _imgs_fwd(layer: ConvLayer, cin: int, cout: int, bits: bool, pool: bool,
     return imgs
 
 
-def _imgs_wgrad(layer: ConvLayer, unpool: bool = False) -> int:
+def _imgs_wgrad(layer: ConvLayer, unpool: bool = False, unpool_imgs: int = 2) -> int:
     hw = layer.H * layer.W
     xepp = 1 if layer.bits else layer.cin // 8
     dch = layer.cout // 8
@@ -99,7 +99,7 @@ def _imgs_wgrad(layer: ConvLayer, unpool: bool = False) -> int:
     else:
         per = (layer.H + 2) * (layer.W + 2) * layer.cin * 2 + hw * layer.cout * 2
     if unpool:  # the pool-fused form scatters 2 images per round (one per 32-lane half)
-        imgs = min(imgs, 2)
+        imgs = min(imgs, unpool_imgs)
     # (the halo'd dY tile is ~4 % larger: the stage-0 form keeps its 2 images per round, two
     # workgroups per CU still fit)
     lim = (72 if layer.cin > layer.cout else 64) * 1024
@@ -162,6 +162,11 @@ class HipEncoder:
         # LDS staging (16-wide maps; bit-identical): no pool_bwd_idx launch, no 4.3 GB
         # full-resolution gradient in HBM per 524K-frame update
         self.fused_pool_wgrad0 = True
+        # images per round of the pool-fused stage-0 weight gradient: 1 (36 KB of LDS, so two
+        # of its workgroups fit beside an acting one under the backward cap: learner 17.63 ->
+        # 16.94 ms at cap 1, bwd inside the bench 16.3 -> 15.4 ms over 3 seed pairs, profile
+        # 45); 2 fills both 32-lane halves of its scatter but needs 70 KB
+        self.wgrad0_imgs = 1
         # the 16 -> 32 stage conv on 8x8 maps: pool backward, weight gradient and input
         # gradient in one launch (stagebwd.hip; no full-resolution gradient in HBM)
         self.fused_pool_conv_bwd = True
@@ -307,7 +312,7 @@ class HipEncoder:
         """dy=None: dY is max_pool2d's backward of dp through the argmax bytes pidx, expanded
         in the kernel's staging (the stage-0 layer of a 16-wide map)."""
         n = x.shape[0]
-        imgs = _imgs_wgrad(L, unpool=dy is None)
+        imgs = _imgs_wgrad(L, unpool=dy is None, unpool_imgs=self.wgrad0_imgs)
         # persistent grid: as many workgroups as the device keeps resident (<= rounds)
         nparts = N.kernels().mbk_conv_wgrad_parts(int(L.bits), L.cin, L.cout, n, L.H, L.W, imgs,
                                                   int(dy is None))
@@ -601,7 +606,7 @@ class HipEncoder:
             if (s == 0 and Ls.bits and Ls.W == 16 and self.fused_pool_wgrad0 and x.is_cuda
                     and N.kernels().mbk_conv_wgrad_parts(
                         int(Ls.bits), Ls.cin, Ls.cout, x.shape[0], Ls.H, Ls.W,
-                        _imgs_wgrad(Ls, True), 1) > 0):
+                        _imgs_wgrad(Ls, True, self.wgrad0_imgs), 1) > 0):
                 self._wgrad(Ls, x, None, grads[2 * li], grads[2 * li + 1], dp=dp, pidx=pidx)
                 g = None
                 continue
