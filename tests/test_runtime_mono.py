@@ -1,6 +1,7 @@
 """Reference-shaped CPU runtime end to end: BASELINE config 1 plumbing (4x4, 2 CPU actors,
 CPU learner), CSV logs, checkpoint + resume, watchdog under fault injection, --test eval."""
 import os
+import time
 
 import pytest
 import torch
@@ -102,6 +103,11 @@ def test_inference_server_batches_and_publishes():
         for t in th:
             t.join(30)
         assert all(g is not None for g in got)
+        # (the server books a batch's statistics after replying: under a loaded CPU the
+        # clients can return first)
+        deadline = time.time() + 5.0
+        while srv.stats()["mean_batch_actors"] == 0.0 and time.time() < deadline:
+            time.sleep(0.01)
         assert srv.stats()["mean_batch_actors"] > 1.0  # dynamic batching happened
         for i, (a, lp, v) in enumerate(got):
             _, _, v_ref = ref.act(clients[i].obs, clients[i].mask,
